@@ -1,0 +1,203 @@
+"""Headline benchmark: edges aggregated/s of the GCN CSR aggregation (+ Sinkhorn iters/s).
+
+Workload (BASELINE.json configs[3] graph, the largest single-GPU configuration): the synthetic
+2 x 1M-entity / 2 x 10M-triple KG pair of SURVEY.md §8d (41,999,552 nnz incl. self loops),
+D = 300 fp32 features resident in HBM.  A step = one GCN aggregation pass Y = relu(A · H) over
+the whole graph (layers/layers.py:35-38) — on N > 1 GPUs the rows are sharded per KG group and
+the step includes the RCCL halo all-gather of H inside the group (gnnea/dist.py).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+Prints ONE JSON line on rank 0.  `roofline` prices the SpMM kernel with the gather model
+4(N+1) + 8E + 4ED + 4ND bytes per launch over its HIP-event duration on the
+launching stream; `cpu_baseline` times the reference op (torch.spmm on the uncoalesced COO,
+oracle/cpu_baseline.py) on a bounded row sample on the host cores (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gnn-mtl_amd"))
+
+from gnnea import _lib, ops, synth  # noqa: E402
+from gnnea.dist import KGShard  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+D = 300
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def gather_model_bytes(n_rows, nnz, d, elem=4):
+    return 4 * (n_rows + 1) + 8 * nnz + elem * nnz * d + elem * n_rows * d
+
+
+def sinkhorn_rate(device, B=3000, reg=0.01):
+    """Marginal iters/s of utils/ot_loss.sinkhorn and SinkhornOT sinkhorn_iteration at B x B."""
+    from gnnea.sinkhorn import solve
+    g = torch.Generator(device="cpu").manual_seed(0)
+    X = 0.05 * torch.randn(B, 300, generator=g)
+    Y = 0.05 * torch.randn(B, 300, generator=g)
+    M = torch.cdist(X, Y)
+    M = (M / M.max()).to(device)
+    la = torch.zeros(B, dtype=torch.float64, device=device)
+    out = {}
+    for name, mode, lb_val, n0, n1 in (("ot_loss.sinkhorn", _lib.GNNEA_SK_KNOPP, 0.0, 100, 1100),
+                                       ("sinkhorn_iteration", _lib.GNNEA_SK_STAB,
+                                        -np.log(B), 100, 1100)):
+        la_m = la if mode == _lib.GNNEA_SK_KNOPP else la - np.log(B)
+        lb = torch.full((B,), lb_val, dtype=torch.float64, device=device)
+        C = M if mode == _lib.GNNEA_SK_KNOPP else M.double()
+        ts = []
+        for n_it in (n0, n1):
+            solve(mode, C, la_m, lb, reg, 0.0, n_it, want_plan=False, batch=100)  # warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            solve(mode, C, la_m, lb, reg, 0.0, n_it, want_plan=False, batch=100)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        out[name] = round((n1 - n0) / (ts[1] - ts[0]), 1)
+    return {"iters_per_s": out, "B": B, "reg": reg, "dtype": "f64 (C fp32/fp64)",
+            "method": "marginal (T(1100)-T(100))/1000, stopThr/tol = 0"}
+
+
+def cpu_baseline(shard, H, budget_s=12.0):
+    """Reference op on the host: torch.spmm on the uncoalesced COO rows of a bounded sample."""
+    from oracle.cpu_baseline import time_reference_spmm
+    threads = torch.get_num_threads()
+    n = shard.n
+    tr = synth.kg_pair_triples(n, shard_t(n), synth.CONFIGS["cfg4"]["n_rel"])
+    r, c, v = synth.adjacency_coo(tr, 2 * n, reference_order=True)
+    Hc = H.detach().cpu()
+    N = 2 * n
+    rate, nnz, dt = time_reference_spmm(r, c, v, N, N, Hc, sample_rows=N // 50)
+    want_rows = int(min(N, max(N // 50, rate * budget_s / max(nnz / (N // 50), 1))))
+    rate, nnz, dt = time_reference_spmm(r, c, v, N, N, Hc, sample_rows=want_rows)
+    return {"value": round(rate, 1), "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": "torch.spmm(uncoalesced int64 COO, H fp32) over the first %d of %d rows "
+                      "(%d edges, %.1f s) of the same cfg-4 graph, reference entry order" %
+                      (want_rows, N, nnz, dt)}
+
+
+def shard_t(n):
+    return synth.CONFIGS["cfg4"]["t"] if n == synth.CONFIGS["cfg4"]["n"] else 10 * n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=synth.CONFIGS["cfg4"]["n"], help="entities per KG")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sinkhorn", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    t0 = time.time()
+    n = args.n
+    shard = KGShard(n, shard_t(n), synth.CONFIGS["cfg4"]["n_rel"], rank, world, device)
+    log("rank %d: shard rows %d nnz %d built in %.1fs" % (rank, shard.n_rows, shard.nnz,
+                                                         time.time() - t0))
+    gen = torch.Generator(device=device).manual_seed(1 + rank)
+    h_local = torch.randn(shard.n_rows if world > 1 else shard.n_cols, D, device=device,
+                          generator=gen)
+    h_local /= h_local.norm(dim=1, keepdim=True)
+    h_full = torch.empty(shard.n_cols, D, device=device) if shard.g > 1 else None
+    y = torch.empty(shard.n_rows, D, device=device)
+    stream = torch.cuda.current_stream(device)
+
+    def step(ev=None):
+        hf = shard.gather_halo(h_local, h_full)
+        if ev is not None:
+            ev[0].record(stream)
+        ops.spmm(shard.csr, hf, _lib.GNNEA_ACT_RELU, out=y)
+        if ev is not None:
+            ev[1].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    stats = torch.tensor([elapsed, float(shard.nnz), kernel_ms], dtype=torch.float64,
+                         device=device)
+    if world > 1:
+        allst = [torch.zeros_like(stats) for _ in range(world)]
+        dist.all_gather(allst, stats)
+        allst = torch.stack(allst).cpu()
+        elapsed = float(allst[:, 0].max())
+        total_nnz = float(allst[:, 1].sum())
+    else:
+        total_nnz = float(shard.nnz)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_nnz / (elapsed / args.steps)
+
+    if rank == 0:
+        traffic = gather_model_bytes(shard.n_rows, shard.nnz, D)
+        achieved = traffic / (kernel_ms * 1e-3) / 1e9
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": "GCN aggregation relu(A.H) (layers/layers.py:35-38) on the "
+                                   "cfg-4 synthetic 2x%d-entity / 2x%d-triple KG pair, D=%d"
+                                   % (n, shard_t(n), D),
+                       "nnz": int(total_nnz), "nodes": 2 * n, "D": D,
+                       "parallelism": "single GPU" if world == 1 else
+                       "row-sharded, %d KG groups of %d GPUs, RCCL halo all-gather" % (
+                           2, shard.g)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "kernel": "gnnea::k_spmm_v4<relu,act,2>",
+                         "kernel_ms": round(kernel_ms, 4),
+                         "bytes_per_launch": int(traffic),
+                         "model": "gather: 4(N+1)+8E+4ED+4ND (rank 0 shard)"},
+        }
+        if world == 1 and not args.no_sinkhorn:
+            try:
+                line["sinkhorn"] = sinkhorn_rate(device)
+            except Exception as e:  # report, never hide
+                line["sinkhorn"] = {"error": repr(e)}
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(shard, h_local)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

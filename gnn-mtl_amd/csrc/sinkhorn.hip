@@ -1,0 +1,562 @@
+// a9-a12. Fused log-domain Sinkhorn (fp64 arithmetic, fp32 or fp64 cost storage).
+//
+// Reference semantics restated in potentials:
+//   KNOPP (utils/ot_loss.py:5-76), f = log u, g = log v:
+//       g_j = log b_j - LSE_i(f_i - M_ij/reg)      (v = b / K^T u,   :53-54)
+//       f_i = log a_i - LSE_j(g_j - M_ij/reg)      (u = 1 / (K/a) v, :55)
+//     K_ij = exp(-M_ij/reg) underflows to 0 below -745.13 in fp64: such terms are dropped,
+//     K^T u == 0 (column LSE below ln(DBL_TRUE_MIN)) or inf/NaN u, v break the loop with the
+//     previous iterate (:57-62); err = ||v (K^T u) - b||_2 every 10th iteration (:64-66).
+//   STAB / GEN / RELAX (SinkhornOT/sinkhorn_loss.py:159-356), potentials in units of eps,
+//   ua / va = absorbed potentials u/eps, v/eps, f / g = full potentials (u + eps log a)/eps:
+//       log s_i = LSE_j( min(ua_i + va_j - C_ij/eps, ln 1e30) + g_j - va_j )   (K b, clamped K)
+//       f_i = ua_i + min(p_row (log mu_i - log s_i), ln 1e30)                  (a = clamp((mu/s)^p))
+//     and symmetrically for g; absorption (ii%10==0, max(a|b) > 1e20, last iteration) sets
+//     ua = f, va = g and evaluates transport = sum K.C for the relative-tolerance break.
+// One iteration = row pass (one wave per row, coalesced 64-wide column sweep, online LSE with
+// one exp per element) + column pass (workgroup per 64-column strip x row split, partial
+// (max, sum) pairs) + single-workgroup combine (column LSE, update, err / flags).  A device
+// status block gates every kernel so iterations after the stop condition are no-ops.
+#include "common.h"
+
+namespace gnnea {
+
+constexpr double kLn1e20 = 46.051701859880914;   // log(1e20)  (sinkhorn_loss.py:11 big)
+constexpr double kLn1e30 = 69.07755278982137;    // log(1e30)  (sinkhorn_loss.py:12 huge)
+constexpr double kExpUnderflow = -745.1332191019412;  // exp(x) == 0 in fp64 for x below
+constexpr double kLnTrueMin = -744.4400719213812;     // log(DBL_TRUE_MIN)
+constexpr double kExpOverflow = 709.782712893384;     // exp(x) == inf above
+
+struct SkWs {
+  int64_t f, g, ua, va, part_m, part_s, rowbuf, total;
+  int ns;
+};
+
+static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+static int sk_nsplit(int I, int J) {
+  const int strips = (J + 63) / 64;
+  int ns = (1024 + strips - 1) / strips;
+  const int max_by_rows = (I + 15) / 16;
+  if (ns > max_by_rows) ns = max_by_rows;
+  if (ns > 64) ns = 64;
+  if (ns < 1) ns = 1;
+  return ns;
+}
+
+static SkWs sk_plan(int I, int J) {
+  SkWs w;
+  w.ns = sk_nsplit(I, J);
+  int64_t o = GNNEA_SK_STATUS_BYTES;
+  w.f = o; o = al256(o + 2 * 8ll * I);
+  w.g = o; o = al256(o + 2 * 8ll * J);
+  w.ua = o; o = al256(o + 8ll * I);
+  w.va = o; o = al256(o + 8ll * J);
+  w.part_m = o; o = al256(o + 8ll * w.ns * J);
+  w.part_s = o; o = al256(o + 8ll * w.ns * J);
+  w.rowbuf = o; o = al256(o + 8ll * I);
+  w.total = o;
+  return w;
+}
+
+struct SkDev {
+  int64_t* st;   // status ints
+  double* sd;    // status doubles (sd[8] ...)
+  double *f, *g, *ua, *va, *pm, *ps, *rowbuf;
+  int ns;
+};
+
+static SkDev sk_dev(const gnnea_sinkhorn* p) {
+  SkWs w = sk_plan(p->I, p->J);
+  char* b = (char*)p->ws;
+  SkDev d;
+  d.st = (int64_t*)b;
+  d.sd = (double*)b;
+  d.f = (double*)(b + w.f);
+  d.g = (double*)(b + w.g);
+  d.ua = (double*)(b + w.ua);
+  d.va = (double*)(b + w.va);
+  d.pm = (double*)(b + w.part_m);
+  d.ps = (double*)(b + w.part_s);
+  d.rowbuf = (double*)(b + w.rowbuf);
+  d.ns = w.ns;
+  return d;
+}
+
+enum { ST_DONE = 0, ST_ITERS = 1, ST_REASON = 2, ST_SLOT = 3, ST_BIG = 4, ST_FAIL = 5 };
+enum { SD_ERR = 8, SD_TPREV = 9, SD_LOSS = 10, SD_TNEW = 8 };
+
+template <typename T>
+__device__ __forceinline__ double ld_c(const T* C, int64_t idx) {
+  return (double)C[idx];
+}
+
+// online log-sum-exp with one exp per element
+struct Lse {
+  double m, s;
+  __device__ __forceinline__ void init() { m = -INFINITY; s = 0.0; }
+  __device__ __forceinline__ void add(double x) {
+    if (x == -INFINITY) return;
+    if (x > m) {
+      s = s * exp(m - x) + 1.0;
+      m = x;
+    } else {
+      s += exp(x - m);
+    }
+  }
+  __device__ __forceinline__ void merge(double m2, double s2) {
+    if (m2 == -INFINITY) return;
+    if (m == -INFINITY) { m = m2; s = s2; return; }
+    if (m2 > m) { s = s * exp(m - m2) + s2; m = m2; }
+    else s += s2 * exp(m2 - m);
+  }
+  __device__ __forceinline__ double value() const { return m == -INFINITY ? -INFINITY : m + log(s); }
+};
+
+__device__ __forceinline__ Lse wave_lse(Lse l) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double m2 = __shfl_xor(l.m, o, 64);
+    const double s2 = __shfl_xor(l.s, o, 64);
+    l.merge(m2, s2);
+  }
+  return l;
+}
+
+struct SkArgs {
+  int mode, I, J;
+  int64_t ldc;
+  double inv_eps, p_row, p_col, kclamp;  // kclamp: ln 1e30 for STAB modes, +inf for KNOPP
+  const double *la, *lb;
+};
+
+__device__ __forceinline__ void mark_done(int64_t* st, int64_t iters, int64_t reason,
+                                          int64_t slot) {
+  if (atomicCAS((unsigned long long*)&st[ST_DONE], 0ull, 1ull) == 0ull) {
+    st[ST_ITERS] = iters;
+    st[ST_REASON] = reason;
+    st[ST_SLOT] = slot;
+  }
+}
+
+// Row pass: f_out_i from g_in (one wave per row).
+template <typename T>
+__global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                int it, int slot_in, int slot_out) {
+  if (d.st[ST_DONE]) return;
+  const int i = blockIdx.x * 4 + wave_id();
+  if (i >= a.I) return;
+  const int lane = lane_id();
+  const double* g = d.g + (int64_t)slot_in * a.J;
+  const double uai = d.ua[i];
+  const T* Ci = C + (int64_t)i * a.ldc;
+  Lse l;
+  l.init();
+  for (int j = lane; j < a.J; j += 64) {
+    const double k = uai + d.va[j] - ld_c(Ci, j) * a.inv_eps;
+    if (k < kExpUnderflow) continue;  // K_ij == 0 in the reference's fp64 exp
+    l.add(fmin(k, a.kclamp) + g[j] - d.va[j]);
+  }
+  l = wave_lse(l);
+  if (lane != 0) return;
+  const double ls = l.value();
+  double la = a.p_row * (a.la[i] - ls);
+  if (a.mode == GNNEA_SK_KNOPP) {
+    const double f = la;  // u = 1/(Kp v)
+    d.f[(int64_t)slot_out * a.I + i] = f;
+    if (!(f <= kExpOverflow)) mark_done(d.st, it, 2, (it + 1) & 1);  // u inf / NaN
+  } else {
+    if (la > kLn1e30) la = kLn1e30;  // a = clamp(., 0, 1e30)
+    if (la > kLn1e20) atomicOr((unsigned long long*)&d.st[ST_BIG], 1ull);
+    d.f[(int64_t)slot_out * a.I + i] = uai + la;  // F = u + eps log a
+  }
+}
+
+// Column pass: partial (max, sumexp) of x_ij over a row split, for a 64-column strip.
+template <typename T>
+__global__ __launch_bounds__(256) void k_sk_col(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                int slot_f, int rows_per_split) {
+  if (d.st[ST_DONE]) return;
+  __shared__ double sm[4][64], ss[4][64];
+  const int lane = lane_id(), w = wave_id();
+  const int j = blockIdx.x * 64 + lane;
+  const int split = blockIdx.y;
+  const int r0 = split * rows_per_split;
+  const int r1 = min(a.I, r0 + rows_per_split);
+  const double* f = d.f + (int64_t)slot_f * a.I;
+  Lse l;
+  l.init();
+  if (j < a.J) {
+    const double vaj = d.va[j];
+    for (int i = r0 + w; i < r1; i += 4) {
+      const double k = d.ua[i] + vaj - ld_c(C, (int64_t)i * a.ldc + j) * a.inv_eps;
+      if (k < kExpUnderflow) continue;
+      l.add(fmin(k, a.kclamp) + f[i] - d.ua[i]);
+    }
+  }
+  sm[w][lane] = l.m;
+  ss[w][lane] = l.s;
+  __syncthreads();
+  if (w == 0 && j < a.J) {
+    for (int q = 1; q < 4; ++q) l.merge(sm[q][lane], ss[q][lane]);
+    d.pm[(int64_t)split * a.J + j] = l.m;
+    d.ps[(int64_t)split * a.J + j] = l.s;
+  }
+}
+
+// Column combine (single workgroup of 1024): column LSE -> g, KNOPP err / break checks,
+// STAB big-b flag.
+__global__ __launch_bounds__(1024) void k_sk_combine(SkArgs a, SkDev d, int it, int slot_g_prev,
+                                                     int slot_g_out) {
+  if (d.st[ST_DONE]) return;
+  __shared__ double red[1024];
+  __shared__ int fail_s;
+  if (threadIdx.x == 0) fail_s = 0;
+  __syncthreads();
+  const double* gp = d.g + (int64_t)slot_g_prev * a.J;
+  double* go = d.g + (int64_t)slot_g_out * a.J;
+  double errp = 0.0;
+  int fail = 0, big = 0;
+  for (int j = threadIdx.x; j < a.J; j += 1024) {
+    Lse l;
+    l.init();
+    for (int s = 0; s < d.ns; ++s) l.merge(d.pm[(int64_t)s * a.J + j], d.ps[(int64_t)s * a.J + j]);
+    const double ls = l.value();
+    if (a.mode == GNNEA_SK_KNOPP) {
+      // err of the previous iteration: v_{k-1} * (K^T u_{k-1}) - b
+      const double t = exp(gp[j] + ls) - exp(a.lb[j]);
+      errp += t * t;
+      if (!(ls >= kLnTrueMin)) fail = 1;  // K^T u == 0 (or NaN)
+      const double gj = a.lb[j] - ls;
+      if (!(gj <= kExpOverflow)) fail = 1;  // v inf / NaN
+      go[j] = gj;
+    } else {
+      double lb = a.p_col * (a.lb[j] - ls);
+      if (lb > kLn1e30) lb = kLn1e30;
+      if (lb > kLn1e20) big = 1;
+      go[j] = d.va[j] + lb;
+    }
+  }
+  if (a.mode == GNNEA_SK_KNOPP) {
+    red[threadIdx.x] = errp;
+    if (fail) atomicOr(&fail_s, 1);
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      const int prev = it - 1;  // reference cpt of the iterate (f, g)[prev]
+      if (prev >= 0 && prev % 10 == 0) {
+        const double err = sqrt(red[0]);
+        d.sd[SD_ERR] = err;
+        if (!(err > d.sd[11])) {  // sd[11] = stopThr; loop runs while err > stopThr
+          mark_done(d.st, prev + 1, 1, prev & 1);
+          return;
+        }
+      }
+      if (fail_s) mark_done(d.st, it, 2, (it + 1) & 1);
+    }
+  } else if (big) {
+    atomicOr((unsigned long long*)&d.st[ST_BIG], 2ull);
+  }
+}
+
+// STAB absorption, part A (one wave per row): decide, set ua = f, row sums of K.C.
+template <typename T>
+__global__ __launch_bounds__(256) void k_sk_absorb_rows(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                        int it, int slot, int max_iter,
+                                                        int init) {
+  if (d.st[ST_DONE]) return;
+  const bool absorb = init || (it % 10 == 0) || d.st[ST_BIG] || it == max_iter - 1;
+  if (!absorb) return;
+  const int i = blockIdx.x * 4 + wave_id();
+  if (i >= a.I) return;
+  const int lane = lane_id();
+  const double fi = init ? 0.0 : d.f[(int64_t)slot * a.I + i];
+  const double* g = d.g + (int64_t)slot * a.J;
+  const T* Ci = C + (int64_t)i * a.ldc;
+  double acc = 0.0;
+  for (int j = lane; j < a.J; j += 64) {
+    const double c = ld_c(Ci, j);
+    const double k = fmin(fi + (init ? 0.0 : g[j]) - c * a.inv_eps, a.kclamp);
+    acc += exp(k) * c;
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    d.rowbuf[i] = acc;
+    d.ua[i] = fi;
+  }
+}
+
+// STAB absorption, part B (single workgroup): va = g, transport, tolerance break, bookkeeping.
+__global__ __launch_bounds__(1024) void k_sk_absorb_final(SkArgs a, SkDev d, int it, int slot,
+                                                          int max_iter, int init, double tol) {
+  if (d.st[ST_DONE]) return;
+  const bool absorb = init || (it % 10 == 0) || d.st[ST_BIG] || it == max_iter - 1;
+  __syncthreads();
+  if (!absorb) return;
+  __shared__ double red[1024];
+  const double* g = d.g + (int64_t)slot * a.J;
+  for (int j = threadIdx.x; j < a.J; j += 1024) d.va[j] = init ? 0.0 : g[j];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < a.I; i += 1024) s += d.rowbuf[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const double tnew = red[0];
+  d.st[ST_BIG] = 0;
+  if (init) {
+    d.sd[SD_TPREV] = tnew;
+    d.sd[SD_TNEW] = tnew;
+    return;
+  }
+  const double tprev = d.sd[SD_TPREV];
+  d.sd[SD_TNEW] = tnew;
+  if (fabs(tnew - tprev) / fabs(tprev) < tol) {
+    mark_done(d.st, it, 1, slot);  // break: ii stays, `transport` keeps the previous value
+    return;
+  }
+  d.sd[SD_TPREV] = tnew;
+  if (it == max_iter - 1) mark_done(d.st, max_iter, 0, slot);
+}
+
+__global__ void k_sk_init(SkArgs a, SkDev d, double tol) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < 32) {
+    if (t < 8) d.st[t] = 0;
+    else d.sd[t] = 0.0;
+    if (t == 11) d.sd[11] = tol;
+  }
+  const bool knopp = a.mode == GNNEA_SK_KNOPP;
+  // KNOPP: u = 1/I, v = 1/J stored in slot 1 (the "previous" slot of iteration 0)
+  for (int i = t; i < a.I; i += gridDim.x * blockDim.x) {
+    d.ua[i] = 0.0;
+    d.f[i] = 0.0;
+    d.f[a.I + i] = knopp ? -log((double)a.I) : 0.0;
+  }
+  for (int j = t; j < a.J; j += gridDim.x * blockDim.x) {
+    d.va[j] = 0.0;
+    d.g[j] = 0.0;
+    d.g[a.J + j] = knopp ? -log((double)a.J) : 0.0;
+  }
+}
+
+// Final plan, one wave per row; also its row sums.
+// final ping-pong slot: the break / tolerance slot, else the last iteration run (1 = initial)
+__device__ __forceinline__ int sk_final_slot(const SkDev& d, int iters_run) {
+  if (d.st[ST_DONE]) return (int)(d.st[ST_SLOT] & 1);
+  return iters_run > 0 ? ((iters_run - 1) & 1) : 1;
+}
+
+template <typename T, typename P>
+__global__ __launch_bounds__(256) void k_sk_plan(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                 int iters_run, P* __restrict__ plan, int64_t ldp,
+                                                 double* __restrict__ row_sum) {
+  const int slot = sk_final_slot(d, iters_run);
+  const int i = blockIdx.x * 4 + wave_id();
+  if (i >= a.I) return;
+  const int lane = lane_id();
+  const bool knopp = a.mode == GNNEA_SK_KNOPP;
+  const double fi = knopp ? d.f[(int64_t)slot * a.I + i] : d.ua[i];
+  const double* g = knopp ? d.g + (int64_t)slot * a.J : d.va;
+  const T* Ci = C + (int64_t)i * a.ldc;
+  double rs = 0.0, loss = 0.0;
+  for (int j = lane; j < a.J; j += 64) {
+    const double c = ld_c(Ci, j);
+    double v;
+    if (knopp) {
+      // P = u * K * v with K = exp(-M/reg) underflowing to 0 below -745.13
+      const double k = -c * a.inv_eps;
+      v = k < kExpUnderflow ? 0.0 : exp(fi + g[j] + k);
+    } else {
+      v = exp(fmin(fi + g[j] - c * a.inv_eps, a.kclamp));
+    }
+    if (plan) plan[(int64_t)i * ldp + j] = (P)v;
+    rs += v;
+    loss += v * c;
+  }
+  rs = wave_sum(rs);
+  loss = wave_sum(loss);
+  if (lane == 0) {
+    if (row_sum) row_sum[i] = rs;
+    d.rowbuf[i] = loss;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_sk_colsum(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                   int iters_run, double* __restrict__ col_sum) {
+  const int slot = sk_final_slot(d, iters_run);
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.J) return;
+  const bool knopp = a.mode == GNNEA_SK_KNOPP;
+  const double gj = knopp ? d.g[(int64_t)slot * a.J + j] : d.va[j];
+  const double* f = knopp ? d.f + (int64_t)slot * a.I : d.ua;
+  double s = 0.0;
+  for (int i = 0; i < a.I; ++i) {
+    const double c = ld_c(C, (int64_t)i * a.ldc + j);
+    if (knopp) {
+      const double k = -c * a.inv_eps;
+      s += k < kExpUnderflow ? 0.0 : exp(f[i] + gj + k);
+    } else {
+      s += exp(fmin(f[i] + gj - c * a.inv_eps, a.kclamp));
+    }
+  }
+  col_sum[j] = s;
+}
+
+__global__ __launch_bounds__(1024) void k_sk_loss(SkArgs a, SkDev d, int iters_run) {
+  __shared__ double red[1024];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < a.I; i += 1024) s += d.rowbuf[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    d.sd[SD_LOSS] = red[0];
+    if (!d.st[ST_DONE]) {
+      d.st[ST_ITERS] = iters_run;
+      d.st[ST_SLOT] = sk_final_slot(d, iters_run);
+    }
+  }
+}
+
+static bool sk_valid(const gnnea_sinkhorn* p) {
+  if (!p || !p->C || !p->ws || !p->log_a || !p->log_b) return false;
+  if (p->I < 1 || p->J < 1 || p->ldc < p->J) return false;
+  if (p->c_dtype != GNNEA_F32 && p->c_dtype != GNNEA_F64) return false;
+  if (p->mode < GNNEA_SK_KNOPP || p->mode > GNNEA_SK_RELAX) return false;
+  if (!(p->eps > 0.0)) return false;
+  return true;
+}
+
+static SkArgs sk_args(const gnnea_sinkhorn* p) {
+  SkArgs a;
+  a.mode = p->mode;
+  a.I = p->I;
+  a.J = p->J;
+  a.ldc = p->ldc;
+  a.inv_eps = 1.0 / p->eps;
+  const bool gen = p->mode == GNNEA_SK_GEN, relax = p->mode == GNNEA_SK_RELAX;
+  a.p_row = gen ? p->p : 1.0;
+  a.p_col = (gen || relax) ? p->p : 1.0;
+  a.kclamp = p->mode == GNNEA_SK_KNOPP ? INFINITY : kLn1e30;
+  a.la = p->log_a;
+  a.lb = p->log_b;
+  return a;
+}
+
+template <typename T>
+static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t s) {
+  SkArgs a = sk_args(p);
+  SkDev d = sk_dev(p);
+  const int rows_per_split = (p->I + d.ns - 1) / d.ns;
+  const dim3 grow(div_up(p->I, 4)), gcol(div_up(p->J, 64), d.ns);
+  const T* C = (const T*)p->C;
+  for (int it = first; it < first + count; ++it) {
+    const int cur = it & 1, prev = (it + 1) & 1;
+    if (p->mode == GNNEA_SK_KNOPP) {
+      hipLaunchKernelGGL(k_sk_col<T>, gcol, dim3(256), 0, s, C, a, d, prev, rows_per_split);
+      hipLaunchKernelGGL(k_sk_combine, dim3(1), dim3(1024), 0, s, a, d, it, prev, cur);
+      hipLaunchKernelGGL(k_sk_row<T>, grow, dim3(256), 0, s, C, a, d, it, cur, cur);
+    } else {
+      hipLaunchKernelGGL(k_sk_row<T>, grow, dim3(256), 0, s, C, a, d, it, prev, cur);
+      hipLaunchKernelGGL(k_sk_col<T>, gcol, dim3(256), 0, s, C, a, d, cur, rows_per_split);
+      hipLaunchKernelGGL(k_sk_combine, dim3(1), dim3(1024), 0, s, a, d, it, prev, cur);
+      hipLaunchKernelGGL(k_sk_absorb_rows<T>, grow, dim3(256), 0, s, C, a, d, it, cur,
+                         p->max_iter, 0);
+      hipLaunchKernelGGL(k_sk_absorb_final, dim3(1), dim3(1024), 0, s, a, d, it, cur,
+                         p->max_iter, 0, p->tol);
+    }
+    GNNEA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+}  // namespace gnnea
+
+using namespace gnnea;
+
+extern "C" int64_t gnnea_sinkhorn_ws_bytes(int I, int J) {
+  if (I < 1 || J < 1) return GNNEA_EINVAL;
+  return sk_plan(I, J).total;
+}
+
+extern "C" int gnnea_sinkhorn_init(const gnnea_sinkhorn* p, void* stream) {
+  if (!sk_valid(p)) return GNNEA_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  SkArgs a = sk_args(p);
+  SkDev d = sk_dev(p);
+  const int n = p->I > p->J ? p->I : p->J;
+  hipLaunchKernelGGL(k_sk_init, dim3(div_up(n > 32 ? n : 32, 256)), dim3(256), 0, s, a, d,
+                     p->tol);
+  GNNEA_LAUNCH_CHECK();
+  if (p->mode != GNNEA_SK_KNOPP) {  // initial transport = sum K0 . C   (sinkhorn_loss.py:195)
+    const dim3 grow(div_up(p->I, 4));
+    if (p->c_dtype == GNNEA_F32)
+      hipLaunchKernelGGL(k_sk_absorb_rows<float>, grow, dim3(256), 0, s, (const float*)p->C, a,
+                         d, 0, 0, p->max_iter, 1);
+    else
+      hipLaunchKernelGGL(k_sk_absorb_rows<double>, grow, dim3(256), 0, s, (const double*)p->C,
+                         a, d, 0, 0, p->max_iter, 1);
+    hipLaunchKernelGGL(k_sk_absorb_final, dim3(1), dim3(1024), 0, s, a, d, 0, 0, p->max_iter, 1,
+                       p->tol);
+    GNNEA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+extern "C" int gnnea_sinkhorn_iterate(const gnnea_sinkhorn* p, int first, int count,
+                                      void* stream) {
+  if (!sk_valid(p) || first < 0 || count < 1) return GNNEA_EINVAL;
+  if (p->c_dtype == GNNEA_F32) return sk_iter_t<float>(p, first, count, (hipStream_t)stream);
+  return sk_iter_t<double>(p, first, count, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_sinkhorn_finish(const gnnea_sinkhorn* p, void* plan, int plan_dtype,
+                                     int64_t ldp, double* row_sum, double* col_sum,
+                                     void* stream) {
+  if (!sk_valid(p)) return GNNEA_EINVAL;
+  if (plan && plan_dtype != GNNEA_F32 && plan_dtype != GNNEA_F64) return GNNEA_EINVAL;
+  if (plan && ldp < p->J) return GNNEA_EINVAL;
+  // final potentials: the status block's slot after a break, else those of iteration
+  // iters_run-1 (iters_run == 0: the initial u = 1/I, v = 1/J)
+  hipStream_t s = (hipStream_t)stream;
+  SkArgs a = sk_args(p);
+  SkDev d = sk_dev(p);
+  const int slot = p->iters_run;
+  const dim3 grow(div_up(p->I, 4));
+#define GNNEA_PLAN(T, PT)                                                                   \
+  hipLaunchKernelGGL((k_sk_plan<T, PT>), grow, dim3(256), 0, s, (const T*)p->C, a, d, slot, \
+                     (PT*)plan, ldp, row_sum)
+  if (p->c_dtype == GNNEA_F32) {
+    if (plan_dtype == GNNEA_F32) GNNEA_PLAN(float, float);
+    else GNNEA_PLAN(float, double);
+  } else {
+    if (plan_dtype == GNNEA_F32) GNNEA_PLAN(double, float);
+    else GNNEA_PLAN(double, double);
+  }
+#undef GNNEA_PLAN
+  GNNEA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sk_loss, dim3(1), dim3(1024), 0, s, a, d, p->iters_run);
+  GNNEA_LAUNCH_CHECK();
+  if (col_sum) {
+    const dim3 gcs(div_up(p->J, 256));
+    if (p->c_dtype == GNNEA_F32)
+      hipLaunchKernelGGL(k_sk_colsum<float>, gcs, dim3(256), 0, s, (const float*)p->C, a, d,
+                         slot, col_sum);
+    else
+      hipLaunchKernelGGL(k_sk_colsum<double>, gcs, dim3(256), 0, s, (const double*)p->C, a, d,
+                         slot, col_sum);
+    GNNEA_LAUNCH_CHECK();
+  }
+  return 0;
+}

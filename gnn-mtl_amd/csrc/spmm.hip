@@ -1,0 +1,337 @@
+// a2-a4. CSR neighbour aggregation  Y = epilogue(A · X)
+// (replaces torch.spmm(adj, hidden) at layers/layers.py:35 and :64, the act at :38/:67 and the
+//  HighWay blend at :69-76).
+//
+// Gather model: per SpMM the kernel must move
+//     4(N+1) + 8E + 4·E·D + 4·N·D bytes,
+// dominated by the E·D neighbour-row gathers.  Layout of the work:
+//   * one wave (64 lanes) per destination row, 4 rows per 256-thread workgroup;
+//   * lane l owns float4 chunks l, l+64, ... of the feature row (16 B per lane per load:
+//     a wave-instruction moves up to 1 KiB of one neighbour row, fully coalesced);
+//   * the row's (col, val) pairs are loaded 64 at a time, one per lane, and broadcast to the
+//     wave with v_readlane (wave-uniform, no LDS);
+//   * neighbours are unrolled by 4 so every lane keeps 4 x NCH independent 16-B loads in flight;
+//   * workgroups are remapped XCD-contiguously so consecutive rows (ring neighbours, self loops)
+//     hit the same XCD's L2.
+// No atomics, no LDS; results are deterministic (fixed CSR order, fixed fma chain per lane).
+#include "common.h"
+
+namespace gnnea {
+
+enum { EPI_ACT = 0, EPI_HIGHWAY = 1 };
+
+struct HighwayArgs {
+  const float4* gate_pre;
+  int64_t ldg4;
+  const float4* bias4;
+  const float4* resid;
+  int64_t ldr4;
+  float4* save_s;
+  float4* save_g;
+  int64_t lds4;
+};
+
+template <int ACT>
+__device__ __forceinline__ float4 act4(float4 v) {
+  return make_float4(act_fwd<ACT>(v.x), act_fwd<ACT>(v.y), act_fwd<ACT>(v.z), act_fwd<ACT>(v.w));
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+template <int ACT, int EPI, int NCH>
+__global__ __launch_bounds__(256) void k_spmm_v4(const int32_t* __restrict__ rowptr,
+                                                 const int32_t* __restrict__ col,
+                                                 const float* __restrict__ val, int n_rows, int D4,
+                                                 const float4* __restrict__ X, int64_t ldx4,
+                                                 float4* __restrict__ Y, int64_t ldy4,
+                                                 HighwayArgs hw) {
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = blk * 4 + wave_id();
+  if (row >= n_rows) return;
+  const int lane = lane_id();
+  const int beg = rowptr[row], end = rowptr[row + 1];
+
+  float4 acc[NCH];
+  bool own[NCH];
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    own[q] = lane + 64 * q < D4;
+  }
+
+  for (int base = beg; base < end; base += 64) {
+    const int cnt = min(64, end - base);
+    const int mc = lane < cnt ? col[base + lane] : 0;
+    const float mv = lane < cnt ? val[base + lane] : 0.f;
+    int k = 0;
+    for (; k + 4 <= cnt; k += 4) {
+      const int j0 = readlane_i(mc, k), j1 = readlane_i(mc, k + 1);
+      const int j2 = readlane_i(mc, k + 2), j3 = readlane_i(mc, k + 3);
+      const float v0 = readlane_f(mv, k), v1 = readlane_f(mv, k + 1);
+      const float v2 = readlane_f(mv, k + 2), v3 = readlane_f(mv, k + 3);
+      const float4* x0 = X + (int64_t)j0 * ldx4 + lane;
+      const float4* x1 = X + (int64_t)j1 * ldx4 + lane;
+      const float4* x2 = X + (int64_t)j2 * ldx4 + lane;
+      const float4* x3 = X + (int64_t)j3 * ldx4 + lane;
+      float4 r0[NCH], r1[NCH], r2[NCH], r3[NCH];
+#pragma unroll
+      for (int q = 0; q < NCH; ++q) {
+        if (own[q]) {
+          r0[q] = x0[64 * q];
+          r1[q] = x1[64 * q];
+          r2[q] = x2[64 * q];
+          r3[q] = x3[64 * q];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < NCH; ++q) {
+        if (own[q]) {
+          acc[q] = f4_fma(v0, r0[q], acc[q]);
+          acc[q] = f4_fma(v1, r1[q], acc[q]);
+          acc[q] = f4_fma(v2, r2[q], acc[q]);
+          acc[q] = f4_fma(v3, r3[q], acc[q]);
+        }
+      }
+    }
+    for (; k < cnt; ++k) {
+      const int j = readlane_i(mc, k);
+      const float v = readlane_f(mv, k);
+      const float4* xr = X + (int64_t)j * ldx4 + lane;
+#pragma unroll
+      for (int q = 0; q < NCH; ++q)
+        if (own[q]) acc[q] = f4_fma(v, xr[64 * q], acc[q]);
+    }
+  }
+
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    if (!own[q]) continue;
+    const int c = lane + 64 * q;
+    float4 s = act4<ACT>(acc[q]);
+    if constexpr (EPI == EPI_ACT) {
+      Y[(int64_t)row * ldy4 + c] = s;
+    } else {
+      float4 gp = hw.gate_pre[(int64_t)row * hw.ldg4 + c];
+      if (hw.bias4) {
+        const float4 b = hw.bias4[c];
+        gp.x += b.x; gp.y += b.y; gp.z += b.z; gp.w += b.w;
+      }
+      const float4 g = make_float4(sigm(gp.x), sigm(gp.y), sigm(gp.z), sigm(gp.w));
+      const float4 r = hw.resid[(int64_t)row * hw.ldr4 + c];
+      // reference order: transform_gate * support + carry_gate * residual, carry = 1 - g
+      float4 o;
+      o.x = g.x * s.x + (1.f - g.x) * r.x;
+      o.y = g.y * s.y + (1.f - g.y) * r.y;
+      o.z = g.z * s.z + (1.f - g.z) * r.z;
+      o.w = g.w * s.w + (1.f - g.w) * r.w;
+      Y[(int64_t)row * ldy4 + c] = o;
+      if (hw.save_s) hw.save_s[(int64_t)row * hw.lds4 + c] = s;
+      if (hw.save_g) hw.save_g[(int64_t)row * hw.lds4 + c] = g;
+    }
+  }
+}
+
+// Scalar fallback for any D / alignment: lane owns columns lane, lane+64, ...
+template <int ACT, int EPI>
+__global__ __launch_bounds__(256) void k_spmm_scalar(const int32_t* __restrict__ rowptr,
+                                                     const int32_t* __restrict__ col,
+                                                     const float* __restrict__ val, int n_rows,
+                                                     int D, const float* __restrict__ X,
+                                                     int64_t ldx, float* __restrict__ Y,
+                                                     int64_t ldy, const float* gate_pre,
+                                                     int64_t ldg, const float* bias,
+                                                     const float* resid, int64_t ldr,
+                                                     float* save_s, float* save_g, int64_t lds) {
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = blk * 4 + wave_id();
+  if (row >= n_rows) return;
+  const int lane = lane_id();
+  const int beg = rowptr[row], end = rowptr[row + 1];
+  for (int c0 = 0; c0 < D; c0 += 64) {
+    const int c = c0 + lane;
+    float acc = 0.f;
+    for (int e = beg; e < end; ++e) {
+      const int j = col[e];
+      if (c < D) acc = fmaf(val[e], X[(int64_t)j * ldx + c], acc);
+    }
+    if (c >= D) continue;
+    const float s = act_fwd<ACT>(acc);
+    if constexpr (EPI == EPI_ACT) {
+      Y[(int64_t)row * ldy + c] = s;
+    } else {
+      float gp = gate_pre[(int64_t)row * ldg + c] + (bias ? bias[c] : 0.f);
+      const float g = sigm(gp);
+      const float r = resid[(int64_t)row * ldr + c];
+      Y[(int64_t)row * ldy + c] = g * s + (1.f - g) * r;
+      if (save_s) save_s[(int64_t)row * lds + c] = s;
+      if (save_g) save_g[(int64_t)row * lds + c] = g;
+    }
+  }
+}
+
+static inline bool al16(const void* p) { return p == nullptr || (((uintptr_t)p) & 15) == 0; }
+
+template <int ACT, int EPI>
+static int launch_spmm(const int32_t* rowptr, const int32_t* col, const float* val, int n_rows,
+                       int D, const float* X, int64_t ldx, float* Y, int64_t ldy,
+                       const float* gate_pre, int64_t ldg, const float* bias, const float* resid,
+                       int64_t ldr, float* save_s, float* save_g, int64_t lds,
+                       hipStream_t stream) {
+  const int nb = div_up(n_rows, 4);
+  bool vec = (D % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) && al16(X) && al16(Y);
+  if (EPI == EPI_HIGHWAY)
+    vec = vec && (ldg % 4 == 0) && (ldr % 4 == 0) && (lds % 4 == 0) && al16(gate_pre) &&
+          al16(bias) && al16(resid) && al16(save_s) && al16(save_g);
+  const int D4 = D / 4;
+  if (vec && D4 <= 256) {
+    HighwayArgs hw{(const float4*)gate_pre, ldg / 4, (const float4*)bias, (const float4*)resid,
+                   ldr / 4, (float4*)save_s, (float4*)save_g, lds / 4};
+    const int nch = (D4 + 63) / 64;
+#define GNNEA_SPMM_CASE(N)                                                                     \
+  case N:                                                                                      \
+    hipLaunchKernelGGL((k_spmm_v4<ACT, EPI, N>), dim3(nb), dim3(256), 0, stream, rowptr, col, \
+                       val, n_rows, D4, (const float4*)X, ldx / 4, (float4*)Y, ldy / 4, hw);    \
+    break;
+    switch (nch) {
+      GNNEA_SPMM_CASE(1)
+      GNNEA_SPMM_CASE(2)
+      GNNEA_SPMM_CASE(3)
+      GNNEA_SPMM_CASE(4)
+      default: break;
+    }
+#undef GNNEA_SPMM_CASE
+  } else {
+    hipLaunchKernelGGL((k_spmm_scalar<ACT, EPI>), dim3(nb), dim3(256), 0, stream, rowptr, col,
+                       val, n_rows, D, X, ldx, Y, ldy, gate_pre, ldg, bias, resid, ldr, save_s,
+                       save_g, lds);
+  }
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int EPI>
+static int dispatch_act(int act, const int32_t* rowptr, const int32_t* col, const float* val,
+                        int n_rows, int D, const float* X, int64_t ldx, float* Y, int64_t ldy,
+                        const float* gate_pre, int64_t ldg, const float* bias,
+                        const float* resid, int64_t ldr, float* save_s, float* save_g,
+                        int64_t lds, hipStream_t s) {
+#define GNNEA_ACT_CASE(A)                                                                     \
+  case A:                                                                                     \
+    return launch_spmm<A, EPI>(rowptr, col, val, n_rows, D, X, ldx, Y, ldy, gate_pre, ldg,    \
+                               bias, resid, ldr, save_s, save_g, lds, s);
+  switch (act) {
+    GNNEA_ACT_CASE(GNNEA_ACT_IDENTITY)
+    GNNEA_ACT_CASE(GNNEA_ACT_RELU)
+    GNNEA_ACT_CASE(GNNEA_ACT_ELU)
+    GNNEA_ACT_CASE(GNNEA_ACT_LEAKY_RELU)
+    GNNEA_ACT_CASE(GNNEA_ACT_SIGMOID)
+    GNNEA_ACT_CASE(GNNEA_ACT_TANH)
+    default: return GNNEA_EINVAL;
+  }
+#undef GNNEA_ACT_CASE
+}
+
+// ---- elementwise backward helpers ----------------------------------------------------------
+
+template <int ACT>
+__global__ void k_act_bwd(const float* __restrict__ dY, const float* __restrict__ Y,
+                          float* __restrict__ G, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) G[i] = dY[i] * act_grad_from_out<ACT>(Y[i]);
+}
+
+template <int ACT>
+__global__ void k_highway_bwd(const float* __restrict__ dY, const float* __restrict__ S,
+                              const float* __restrict__ Gt, const float* __restrict__ R,
+                              int64_t ld, int64_t n_rows, int D, float* __restrict__ dS_pre,
+                              float* __restrict__ dgate, float* __restrict__ dresid) {
+  const int64_t n = n_rows * (int64_t)D;
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; t < n; t += stride) {
+    const int64_t r = t / D, c = t - r * D;
+    const int64_t i = r * ld + c;
+    const float dy = dY[i], s = S[i], g = Gt[i], x = R[i];
+    dS_pre[i] = dy * g * act_grad_from_out<ACT>(s);
+    dgate[i] = dy * (s - x) * g * (1.f - g);
+    if (dresid) dresid[i] = dy * (1.f - g);
+  }
+}
+
+}  // namespace gnnea
+
+using namespace gnnea;
+
+extern "C" int gnnea_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                                  int32_t n_rows, int32_t D, const float* X, int64_t ldx,
+                                  float* Y, int64_t ldy, int act, void* stream) {
+  if (n_rows < 0 || D < 0) return GNNEA_EINVAL;
+  if (n_rows == 0 || D == 0) return 0;
+  if (!rowptr || !col || !val || !X || !Y || ldx < D || ldy < D) return GNNEA_EINVAL;
+  return dispatch_act<EPI_ACT>(act, rowptr, col, val, n_rows, D, X, ldx, Y, ldy, nullptr, 0,
+                               nullptr, nullptr, 0, nullptr, nullptr, 0, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_spmm_highway_f32(const int32_t* rowptr, const int32_t* col,
+                                      const float* val, int32_t n_rows, int32_t D,
+                                      const float* X, int64_t ldx, const float* gate_pre,
+                                      int64_t ldg, const float* bias_gate, const float* resid,
+                                      int64_t ldr, float* Y, int64_t ldy, float* save_s,
+                                      float* save_g, int64_t lds, int act, void* stream) {
+  if (n_rows < 0 || D < 0) return GNNEA_EINVAL;
+  if (n_rows == 0 || D == 0) return 0;
+  if (!rowptr || !col || !val || !X || !Y || !gate_pre || !resid) return GNNEA_EINVAL;
+  if (ldx < D || ldy < D || ldg < D || ldr < D || ((save_s || save_g) && lds < D))
+    return GNNEA_EINVAL;
+  return dispatch_act<EPI_HIGHWAY>(act, rowptr, col, val, n_rows, D, X, ldx, Y, ldy, gate_pre,
+                                   ldg, bias_gate, resid, ldr, save_s, save_g, lds,
+                                   (hipStream_t)stream);
+}
+
+extern "C" int gnnea_act_bwd_f32(const float* dY, const float* Y, float* G, int64_t n, int act,
+                                 void* stream) {
+  if (n < 0) return GNNEA_EINVAL;
+  if (n == 0) return 0;
+  if (!dY || !Y || !G) return GNNEA_EINVAL;
+  const int nb = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
+  hipStream_t s = (hipStream_t)stream;
+  switch (act) {
+    case GNNEA_ACT_IDENTITY: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_IDENTITY>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
+    case GNNEA_ACT_RELU: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_RELU>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
+    case GNNEA_ACT_ELU: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_ELU>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
+    case GNNEA_ACT_LEAKY_RELU: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_LEAKY_RELU>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
+    case GNNEA_ACT_SIGMOID: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_SIGMOID>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
+    case GNNEA_ACT_TANH: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_TANH>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
+    default: return GNNEA_EINVAL;
+  }
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int gnnea_highway_bwd_f32(const float* dY, const float* S, const float* G,
+                                     const float* resid, int64_t ld, int64_t n_rows, int32_t D,
+                                     float* dS_pre, float* dgate, float* dresid, int act,
+                                     void* stream) {
+  if (n_rows < 0 || D < 0 || ld < D) return GNNEA_EINVAL;
+  if (n_rows == 0 || D == 0) return 0;
+  if (!dY || !S || !G || !resid || !dS_pre || !dgate) return GNNEA_EINVAL;
+  const int64_t n = n_rows * (int64_t)D;
+  const int nb = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
+  hipStream_t s = (hipStream_t)stream;
+#define GNNEA_HWB(A)                                                                        \
+  hipLaunchKernelGGL(k_highway_bwd<A>, dim3(nb), dim3(256), 0, s, dY, S, G, resid, ld, n_rows, \
+                     D, dS_pre, dgate, dresid)
+  switch (act) {
+    case GNNEA_ACT_IDENTITY: GNNEA_HWB(GNNEA_ACT_IDENTITY); break;
+    case GNNEA_ACT_RELU: GNNEA_HWB(GNNEA_ACT_RELU); break;
+    case GNNEA_ACT_ELU: GNNEA_HWB(GNNEA_ACT_ELU); break;
+    case GNNEA_ACT_LEAKY_RELU: GNNEA_HWB(GNNEA_ACT_LEAKY_RELU); break;
+    case GNNEA_ACT_SIGMOID: GNNEA_HWB(GNNEA_ACT_SIGMOID); break;
+    case GNNEA_ACT_TANH: GNNEA_HWB(GNNEA_ACT_TANH); break;
+    default: return GNNEA_EINVAL;
+  }
+#undef GNNEA_HWB
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,141 @@
+"""ctypes binding of libgnnea.so (the C-ABI declared in include/gnnea.h).
+
+The library is loaded after ``import torch`` so that it binds to the HIP runtime torch already
+loaded (same soname, ``libamdhip64.so.7``): device pointers and streams are shared.  There is no
+fallback: if the library is missing every product op raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported before the HIP library is dlopen'ed)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgnnea.so")
+
+GNNEA_ACT_IDENTITY = 0
+GNNEA_ACT_RELU = 1
+GNNEA_ACT_ELU = 2
+GNNEA_ACT_LEAKY_RELU = 3
+GNNEA_ACT_SIGMOID = 4
+GNNEA_ACT_TANH = 5
+
+GNNEA_F32 = 0
+GNNEA_F64 = 1
+
+GNNEA_SK_KNOPP = 0
+GNNEA_SK_STAB = 1
+GNNEA_SK_GEN = 2
+GNNEA_SK_RELAX = 3
+GNNEA_SK_STATUS_BYTES = 256
+
+_p = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_f64 = ctypes.c_double
+
+
+class SinkhornProblem(ctypes.Structure):
+    """Mirror of ``gnnea_sinkhorn`` (include/gnnea.h)."""
+
+    _fields_ = [
+        ("mode", ctypes.c_int),
+        ("c_dtype", ctypes.c_int),
+        ("I", ctypes.c_int),
+        ("J", ctypes.c_int),
+        ("ldc", _i64),
+        ("C", _p),
+        ("log_a", _p),
+        ("log_b", _p),
+        ("eps", _f64),
+        ("p", _f64),
+        ("tol", _f64),
+        ("max_iter", ctypes.c_int),
+        ("iters_run", ctypes.c_int),
+        ("ws", _p),
+    ]
+
+
+# name -> (restype, argtypes): every symbol include/gnnea.h declares
+SIGNATURES = {
+    "gnnea_abi_version": (ctypes.c_int, []),
+    "gnnea_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "gnnea_coo_to_csr_ws_bytes": (_i64, [_i64, _i64, _i64]),
+    "gnnea_coo_to_csr": (ctypes.c_int, [_p, _p, ctypes.c_int, _p, _i64, _i64, _i64, _p, _p, _p,
+                                        _p, _p, _p, _i64, _p]),
+    "gnnea_csr_expand_rows": (ctypes.c_int, [_p, _i32, _i64, _p, _p]),
+    "gnnea_spmm_csr_f32": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64,
+                                          ctypes.c_int, _p]),
+    "gnnea_spmm_highway_f32": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64, _p, _p,
+                                              _i64, _p, _i64, _p, _p, _i64, ctypes.c_int, _p]),
+    "gnnea_act_bwd_f32": (ctypes.c_int, [_p, _p, _p, _i64, ctypes.c_int, _p]),
+    "gnnea_highway_bwd_f32": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p,
+                                             ctypes.c_int, _p]),
+    "gnnea_gat_scores_f32": (ctypes.c_int, [_p, _i64, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,
+                                            _p]),
+    "gnnea_gat_fwd_f32": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int, ctypes.c_int, _p, _p,
+                                         _f32, _p, ctypes.c_int, _p, _i64, _p, _p, _p]),
+    "gnnea_gat_bwd_edge_f32": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int, ctypes.c_int,
+                                              _p, _p, _f32, _p, _p, _p, _p, _p, _i64, _p, _p, _p]),
+    "gnnea_gat_bwd_node_f32": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _p,
+                                              _f32, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _i64, _p,
+                                              _p]),
+    "gnnea_gemm_ws_bytes": (_i64, [_i64, _i64, _i64]),
+    "gnnea_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
+                                      _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
+    "gnnea_sinkhorn_ws_bytes": (_i64, [ctypes.c_int, ctypes.c_int]),
+    "gnnea_sinkhorn_init": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p]),
+    "gnnea_sinkhorn_iterate": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), ctypes.c_int,
+                                              ctypes.c_int, _p]),
+    "gnnea_sinkhorn_finish": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p, ctypes.c_int,
+                                             _i64, _p, _p, _p]),
+}
+
+_LIB = None
+
+
+class GnneaError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the native library; raise loudly when it is absent."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise GnneaError(
+                "gnnea: native library %s is not built (run __graft_entry__.build() or "
+                "`make -C gnn-mtl_amd/csrc`); there is no CPU fallback" % LIB_PATH)
+        handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = handle
+    return _LIB
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().gnnea_error_string(int(rc))
+        raise GnneaError("gnnea call failed (%d): %s" % (rc, msg.decode() if msg else "?"))
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(*tensors):
+    """The product path is HIP-only: refuse host tensors instead of silently computing on CPU."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise GnneaError(
+                "gnnea: tensors must live on a HIP device (got %s); the MI355X engine has no "
+                "CPU path" % t.device)

@@ -1,0 +1,323 @@
+"""Functional HIP ops and their autograd wrappers (the only callers of the C-ABI).
+
+Every function here launches libgnnea kernels on the tensor's current stream; none has a CPU
+path (``_lib.require_device``).  Reference call sites each op replaces are cited per function.
+"""
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from ._lib import check, ptr, stream_of
+from .graph import DeviceCSR, csr_of
+
+ACT_CODES = {}
+
+
+def _register_acts():
+    ACT_CODES[F.relu] = _lib.GNNEA_ACT_RELU
+    ACT_CODES[torch.relu] = _lib.GNNEA_ACT_RELU
+    ACT_CODES[F.elu] = _lib.GNNEA_ACT_ELU
+    ACT_CODES[F.leaky_relu] = _lib.GNNEA_ACT_LEAKY_RELU
+    ACT_CODES[torch.sigmoid] = _lib.GNNEA_ACT_SIGMOID
+    ACT_CODES[F.sigmoid] = _lib.GNNEA_ACT_SIGMOID
+    ACT_CODES[torch.tanh] = _lib.GNNEA_ACT_TANH
+    ACT_CODES[F.tanh] = _lib.GNNEA_ACT_TANH
+
+
+_register_acts()
+
+
+def act_code(act):
+    """Fusable activation code for a reference ``act`` callable, or None (apply in torch)."""
+    try:
+        return ACT_CODES.get(act)
+    except TypeError:
+        return None
+
+
+def _f32c(t):
+    if t.dtype != torch.float32:
+        raise TypeError("gnnea: fp32 tensors required (got %s)" % t.dtype)
+    return t if t.is_contiguous() else t.contiguous()
+
+
+# ------------------------------------------------------------------------------------------ #
+# dense projection (MFMA)                                                                     #
+# ------------------------------------------------------------------------------------------ #
+_WS = {}
+
+
+def _gemm_ws(device, nbytes):
+    key = (device, )
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0):
+    """out = op(a) @ op(b) (+ bias) (+ beta*out) on MFMA f32 (gnnea_gemm_f32)."""
+    _lib.require_device(a, b)
+    a = _f32c(a)
+    b = _f32c(b)
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    Kb = b.shape[1] if trans_b else b.shape[0]
+    N = b.shape[0] if trans_b else b.shape[1]
+    if K != Kb:
+        raise ValueError("gnnea.gemm: inner dimensions differ (%d vs %d)" % (K, Kb))
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+        beta = 0.0
+    if bias is not None:
+        bias = _f32c(bias)
+    L = _lib.lib()
+    ws_bytes = int(L.gnnea_gemm_ws_bytes(M, N, K))
+    ws = _gemm_ws(a.device, ws_bytes) if ws_bytes > 0 else None
+    with torch.cuda.device(a.device):
+        check(L.gnnea_gemm_f32(int(trans_a), int(trans_b), M, N, K, ptr(a), a.stride(0), ptr(b),
+                               b.stride(0), ptr(bias), float(beta), ptr(out), out.stride(0),
+                               ptr(ws), ws_bytes if ws is not None else 0,
+                               stream_of(a.device)))
+    return out
+
+
+class LinearFn(torch.autograd.Function):
+    """y = x W^T + b  (nn.Linear.forward at layers/layers.py:32,61,93) on MFMA."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return gemm(x, weight, trans_b=True, bias=bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dy = _f32c(dy)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(dy, weight)  # [N,out]·[out,in]
+        if ctx.needs_input_grad[1]:
+            dw = gemm(dy, x, trans_a=True)  # [out,N]·[N,in]
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            ones = torch.ones((1, dy.shape[0]), dtype=torch.float32, device=dy.device)
+            db = gemm(ones, dy).view(-1)
+        return dx, dw, db
+
+
+class MatmulFn(torch.autograd.Function):
+    """y = x W  (torch.mm(input, self.W) at layers/att_layers.py:33, torch.spmm(x, kernel_gate)
+    at layers/layers.py:69) on MFMA."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return gemm(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = _f32c(dy)
+        dx = gemm(dy, w, trans_b=True) if ctx.needs_input_grad[0] else None
+        dw = gemm(x, dy, trans_a=True) if ctx.needs_input_grad[1] else None
+        return dx, dw
+
+
+def linear(x, weight, bias=None):
+    return LinearFn.apply(x, weight, bias)
+
+
+def matmul(x, w):
+    return MatmulFn.apply(x, w)
+
+
+# ------------------------------------------------------------------------------------------ #
+# CSR aggregation                                                                              #
+# ------------------------------------------------------------------------------------------ #
+def spmm(csr, x, act=_lib.GNNEA_ACT_IDENTITY, out=None):
+    """out = act(A @ x) with the gather-model CSR kernel (gnnea_spmm_csr_f32)."""
+    _lib.require_device(x)
+    x = _f32c(x)
+    if x.dim() != 2 or x.shape[0] != csr.n_cols:
+        raise ValueError("gnnea.spmm: x must be [%d, D]" % csr.n_cols)
+    if out is None:
+        out = torch.empty((csr.n_rows, x.shape[1]), dtype=torch.float32, device=x.device)
+    with torch.cuda.device(x.device):
+        check(_lib.lib().gnnea_spmm_csr_f32(
+            ptr(csr.rowptr), ptr(csr.col), ptr(csr.val), csr.n_rows, x.shape[1], ptr(x),
+            x.stride(0), ptr(out), out.stride(0), int(act), stream_of(x.device)))
+    return out
+
+
+def act_bwd(dy, y, act):
+    dy = _f32c(dy)
+    y = _f32c(y)
+    g = torch.empty_like(y)
+    with torch.cuda.device(y.device):
+        check(_lib.lib().gnnea_act_bwd_f32(ptr(dy), ptr(y), ptr(g), y.numel(), int(act),
+                                           stream_of(y.device)))
+    return g
+
+
+class AggregateFn(torch.autograd.Function):
+    """support = act(A · hidden) (layers/layers.py:34-38); backward A^T · (dY ⊙ act'(Y))."""
+
+    @staticmethod
+    def forward(ctx, hidden, csr, act):
+        out = spmm(csr, hidden, act)
+        ctx.csr = csr
+        ctx.act = act
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        (out,) = ctx.saved_tensors
+        g = dy if ctx.act == _lib.GNNEA_ACT_IDENTITY else act_bwd(dy, out, ctx.act)
+        dh = spmm(ctx.csr.transpose(), _f32c(g))
+        return dh, None, None
+
+
+def aggregate(adj, hidden, act_fn=None):
+    """Drop-in for ``act(torch.spmm(adj, hidden))``: fused when ``act_fn`` is known."""
+    csr = csr_of(adj)
+    code = act_code(act_fn) if act_fn is not None else _lib.GNNEA_ACT_IDENTITY
+    if code is None:
+        return act_fn(AggregateFn.apply(hidden, csr, _lib.GNNEA_ACT_IDENTITY))
+    return AggregateFn.apply(hidden, csr, code)
+
+
+class HighwayFn(torch.autograd.Function):
+    """HighWay GCN tail (layers/layers.py:64-76) in one kernel:
+    S = act(A·hidden); g = sigmoid(gate_pre + bias_gate); out = g*S + (1-g)*resid."""
+
+    @staticmethod
+    def forward(ctx, hidden, gate_pre, resid, bias_gate, csr, act):
+        hidden = _f32c(hidden)
+        gate_pre = _f32c(gate_pre)
+        resid = _f32c(resid)
+        N, D = csr.n_rows, hidden.shape[1]
+        out = torch.empty((N, D), dtype=torch.float32, device=hidden.device)
+        S = torch.empty_like(out)
+        G = torch.empty_like(out)
+        bias = _f32c(bias_gate) if bias_gate is not None else None
+        with torch.cuda.device(hidden.device):
+            check(_lib.lib().gnnea_spmm_highway_f32(
+                ptr(csr.rowptr), ptr(csr.col), ptr(csr.val), N, D, ptr(hidden), hidden.stride(0),
+                ptr(gate_pre), gate_pre.stride(0), ptr(bias), ptr(resid), resid.stride(0),
+                ptr(out), out.stride(0), ptr(S), ptr(G), S.stride(0), int(act),
+                stream_of(hidden.device)))
+        ctx.csr = csr
+        ctx.act = act
+        ctx.save_for_backward(S, G, resid)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        S, G, resid = ctx.saved_tensors
+        dy = _f32c(dy)
+        dS = torch.empty_like(S)
+        dgate = torch.empty_like(S)
+        dres = torch.empty_like(S) if ctx.needs_input_grad[2] else None
+        with torch.cuda.device(S.device):
+            check(_lib.lib().gnnea_highway_bwd_f32(
+                ptr(dy), ptr(S), ptr(G), ptr(resid), S.stride(0), S.shape[0], S.shape[1],
+                ptr(dS), ptr(dgate), ptr(dres), int(ctx.act), stream_of(S.device)))
+        dh = spmm(ctx.csr.transpose(), dS)
+        return dh, dgate, dres, None, None, None
+
+
+def highway(adj, hidden, gate_pre, resid, bias_gate, act_fn):
+    csr = csr_of(adj)
+    code = act_code(act_fn)
+    if code is None:
+        # non-fusable activation: aggregate in HIP, finish the blend in torch
+        s = act_fn(AggregateFn.apply(hidden, csr, _lib.GNNEA_ACT_IDENTITY))
+        g = torch.sigmoid(gate_pre + bias_gate) if bias_gate is not None else torch.sigmoid(gate_pre)
+        return g * s + (1.0 - g) * resid
+    return HighwayFn.apply(hidden, gate_pre, resid, bias_gate, csr, code)
+
+
+# ------------------------------------------------------------------------------------------ #
+# GAT (all heads, one edge pass)                                                              #
+# ------------------------------------------------------------------------------------------ #
+def gat_scores(H, a_all, heads, d_head):
+    N = H.shape[0]
+    s1 = torch.empty((N, heads), dtype=torch.float32, device=H.device)
+    s2 = torch.empty_like(s1)
+    with torch.cuda.device(H.device):
+        check(_lib.lib().gnnea_gat_scores_f32(ptr(H), H.stride(0), N, heads, d_head, ptr(a_all),
+                                              ptr(s1), ptr(s2), stream_of(H.device)))
+    return s1, s2
+
+
+class GATFn(torch.autograd.Function):
+    """h'_i = sum_j softmax_j(-LeakyReLU(a·[h_i||h_j])) h_j for all heads at once
+    (layers/att_layers.py:29-61 per head, concatenated at :86)."""
+
+    @staticmethod
+    def forward(ctx, H, a_all, csr, heads, d_head, alpha, act, edge_mask):
+        H = _f32c(H)
+        a_all = _f32c(a_all)
+        N = csr.n_rows
+        s1, s2 = gat_scores(H, a_all, heads, d_head)
+        Y = torch.empty((N, heads * d_head), dtype=torch.float32, device=H.device)
+        m = torch.empty((N, heads), dtype=torch.float32, device=H.device)
+        den = torch.empty_like(m)
+        em = _f32c(edge_mask) if edge_mask is not None else None
+        with torch.cuda.device(H.device):
+            check(_lib.lib().gnnea_gat_fwd_f32(
+                ptr(csr.rowptr), ptr(csr.col), N, ptr(H), H.stride(0), heads, d_head, ptr(s1),
+                ptr(s2), float(alpha), ptr(em), int(act), ptr(Y), Y.stride(0), ptr(m), ptr(den),
+                stream_of(H.device)))
+        ctx.csr = csr
+        ctx.meta = (heads, d_head, float(alpha), int(act))
+        ctx.save_for_backward(H, a_all, s1, s2, m, den, Y, em if em is not None else torch.empty(0))
+        ctx.has_mask = em is not None
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        H, a_all, s1, s2, m, den, Y, em = ctx.saved_tensors
+        heads, d_head, alpha, act = ctx.meta
+        em = em if ctx.has_mask else None
+        csr = ctx.csr
+        csrT = csr.transpose()
+        dY = _f32c(dY)
+        # G = dL/dh' ; P = h' (relu / identity: Y itself is a valid stand-in for c = G·h')
+        G = dY if act == _lib.GNNEA_ACT_IDENTITY else act_bwd(dY, Y, act)
+        N = csr.n_rows
+        dz = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=H.device)
+        ds1 = torch.empty((N, heads), dtype=torch.float32, device=H.device)
+        ds2 = torch.empty_like(ds1)
+        dH = torch.empty_like(H)
+        L = _lib.lib()
+        st = stream_of(H.device)
+        with torch.cuda.device(H.device):
+            check(L.gnnea_gat_bwd_edge_f32(
+                ptr(csr.rowptr), ptr(csr.col), N, ptr(H), H.stride(0), heads, d_head, ptr(s1),
+                ptr(s2), alpha, ptr(em), ptr(m), ptr(den), ptr(G), ptr(Y), G.stride(0), ptr(dz),
+                ptr(ds1), st))
+            check(L.gnnea_gat_bwd_node_f32(
+                ptr(csrT.rowptr), ptr(csrT.col), ptr(csrT.perm), N, heads, d_head, ptr(s1),
+                ptr(s2), alpha, ptr(em), ptr(m), ptr(den), ptr(G), G.stride(0), ptr(dz),
+                ptr(ds1), ptr(a_all), ptr(dH), dH.stride(0), ptr(ds2), st))
+        da = None
+        if ctx.needs_input_grad[1]:
+            # da1[h] = sum_i ds1[i,h] H_i,h ; da2[h] = sum_j ds2[j,h] H_j,h   (MFMA, split-K)
+            p1 = gemm(ds1, H, trans_a=True).view(heads, heads, d_head)
+            p2 = gemm(ds2, H, trans_a=True).view(heads, heads, d_head)
+            idx = torch.arange(heads, device=H.device)
+            da = torch.cat([p1[idx, idx], p2[idx, idx]], dim=1)
+        return dH, da, None, None, None, None, None, None
+
+
+def gat(adj, H, a_all, heads, d_head, alpha, act_fn, edge_mask=None):
+    csr = csr_of(adj)
+    code = act_code(act_fn) if act_fn is not None else _lib.GNNEA_ACT_IDENTITY
+    if code not in (_lib.GNNEA_ACT_IDENTITY, _lib.GNNEA_ACT_RELU):
+        y = GATFn.apply(H, a_all, csr, heads, d_head, alpha, _lib.GNNEA_ACT_IDENTITY, edge_mask)
+        return act_fn(y)
+    return GATFn.apply(H, a_all, csr, heads, d_head, alpha, code, edge_mask)

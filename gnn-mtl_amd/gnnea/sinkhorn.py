@@ -1,0 +1,98 @@
+"""Host driver of the fused log-domain Sinkhorn kernels (gnnea_sinkhorn_*).
+
+The loop has data-dependent exits (tolerance, numerical-error break), so the host enqueues
+iterations in batches and reads the device status block between batches; kernels of iterations
+past the stop condition are no-ops on the device.  All arithmetic is fp64 in the kernels.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import SinkhornProblem, check, ptr, stream_of
+
+ST_DONE, ST_ITERS, ST_REASON, ST_SLOT = 0, 1, 2, 3
+SD_ERR, SD_TPREV, SD_LOSS = 8, 9, 10
+
+
+class SinkhornResult:
+    def __init__(self, plan, row_sum, col_sum, iters, reason, err, transport_new, transport_prev,
+                 loss):
+        self.plan = plan
+        self.row_sum = row_sum
+        self.col_sum = col_sum
+        self.iters = iters
+        self.reason = reason  # 0 max-iter, 1 tolerance, 2 numerical-error break
+        self.err = err
+        self.transport_new = transport_new
+        self.transport_prev = transport_prev
+        self.loss = loss
+
+
+def _status(ws):
+    raw = ws[:_lib.GNNEA_SK_STATUS_BYTES].cpu()  # sync point between batches
+    ints = raw.view(torch.int64)
+    dbl = raw.view(torch.float64)
+    return ints, dbl
+
+
+def solve(mode, C, log_a, log_b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
+          want_plan=True, batch=10):
+    """Run one Sinkhorn solve; C is [I, J] fp32 / fp64 on a HIP device."""
+    _lib.require_device(C, log_a, log_b)
+    if C.dim() != 2:
+        raise ValueError("gnnea.sinkhorn: C must be 2-D")
+    if C.dtype not in (torch.float32, torch.float64):
+        C = C.double()
+    if C.stride(1) != 1:
+        C = C.contiguous()
+    I, J = C.shape
+    dev = C.device
+    la = log_a.reshape(-1).to(torch.float64).contiguous()
+    lb = log_b.reshape(-1).to(torch.float64).contiguous()
+    L = _lib.lib()
+    ws_bytes = int(L.gnnea_sinkhorn_ws_bytes(I, J))
+    if ws_bytes < 0:
+        check(ws_bytes)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    prob = SinkhornProblem(
+        mode=mode, c_dtype=_lib.GNNEA_F32 if C.dtype == torch.float32 else _lib.GNNEA_F64,
+        I=I, J=J, ldc=C.stride(0), C=C.data_ptr(), log_a=la.data_ptr(), log_b=lb.data_ptr(),
+        eps=float(eps), p=float(p), tol=float(tol), max_iter=int(max_iter), iters_run=0,
+        ws=ws.data_ptr())
+    pp = ctypes.byref(prob)
+    st = stream_of(dev)
+    with torch.cuda.device(dev):
+        check(L.gnnea_sinkhorn_init(pp, st))
+        run = 0
+        if mode == _lib.GNNEA_SK_KNOPP:
+            # utils/ot_loss.py:50  while err > stopThr and cpt < numItermax  (err starts at 1)
+            if 1.0 > tol and max_iter > 0:
+                # iteration k's err is evaluated by iteration k+1's combine: batch ends at k+1
+                bounds = [0, 2] + list(range(12, max_iter + 10, 10))
+                for lo, hi in zip(bounds[:-1], bounds[1:]):
+                    hi = min(hi, max_iter)
+                    if hi <= lo:
+                        break
+                    check(L.gnnea_sinkhorn_iterate(pp, lo, hi - lo, st))
+                    run = hi
+                    if _status(ws)[0][ST_DONE].item():
+                        break
+        else:
+            while run < max_iter:
+                n = min(batch, max_iter - run)
+                check(L.gnnea_sinkhorn_iterate(pp, run, n, st))
+                run += n
+                if _status(ws)[0][ST_DONE].item():
+                    break
+        prob.iters_run = run
+        plan = torch.empty((I, J), dtype=plan_dtype, device=dev) if want_plan else None
+        row_sum = torch.empty(I, dtype=torch.float64, device=dev)
+        col_sum = torch.empty(J, dtype=torch.float64, device=dev)
+        check(L.gnnea_sinkhorn_finish(
+            pp, ptr(plan), _lib.GNNEA_F32 if plan_dtype == torch.float32 else _lib.GNNEA_F64,
+            J, ptr(row_sum), ptr(col_sum), st))
+        ints, dbl = _status(ws)
+    return SinkhornResult(plan, row_sum, col_sum, int(ints[ST_ITERS]), int(ints[ST_REASON]),
+                          float(dbl[SD_ERR]), float(dbl[8]), float(dbl[SD_TPREV]),
+                          float(dbl[SD_LOSS]))

@@ -1,0 +1,54 @@
+"""Adjacency / feature input contract (reference utils/data_utils.py:51-57, 296-358).
+
+Only the functions that produce what the hot path consumes are mirrored here, vectorised with
+numpy instead of the reference's per-triple dict loops (which take minutes at 20M triples):
+``get_matrix``, ``get_sparse_tensor``, ``get_sparse_tensor_for_one_graph``,
+``sparse_mx_to_torch_sparse_tensor``.  Entry order and fp32 values are bit-identical to the
+reference (tests/test_adjacency.py); the dataset file loaders are out of scope.
+"""
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from gnnea import synth
+
+
+def sparse_mx_to_torch_sparse_tensor(sparse_mx):
+    """scipy sparse -> uncoalesced torch sparse COO (int64 indices, fp32 values), order kept."""
+    sparse_mx = sparse_mx.tocoo()
+    indices = torch.from_numpy(np.vstack((sparse_mx.row, sparse_mx.col)).astype(np.int64))
+    values = torch.from_numpy(np.asarray(sparse_mx.data).astype(np.float32))
+    return torch.sparse_coo_tensor(indices, values, torch.Size(sparse_mx.shape))
+
+
+def get_matrix(e, KG):
+    """(M, degree) dicts as the reference builds them (:296-321)."""
+    tr = np.asarray(KG, dtype=np.int64).reshape(-1, 3)
+    row, col, _ = synth.adjacency_coo(tr, int(max(e, tr[:, [0, 2]].max() + 1 if len(tr) else 0)))
+    M = {(int(r), int(c)): 1 for r, c in zip(row.tolist(), col.tolist())}
+    h, t = tr[:, 0], tr[:, 2]
+    ns = h != t
+    ents, first = np.unique(np.stack([h, t], 1).reshape(-1), return_index=True)
+    ents = ents[np.argsort(first, kind="stable")]
+    cnt = np.bincount(np.concatenate([h[ns], t[ns]]), minlength=int(ents.max()) + 1 if len(ents) else 0)
+    degree = {int(i): 1 + int(cnt[i]) for i in ents.tolist()}
+    return M, degree
+
+
+def get_sparse_tensor(e, KG):
+    """Normalised adjacency as a scipy COO matrix (:325-336), vectorised."""
+    tr = np.asarray(KG, dtype=np.int64).reshape(-1, 3)
+    row, col, val = synth.adjacency_coo(tr, e)
+    return sp.coo_matrix((val.astype(np.float64), (row, col)), shape=(e, e))
+
+
+def get_sparse_tensor_for_one_graph(e, KG, index_R):
+    """Single-KG adjacency with ids remapped by index_R (:339-350)."""
+    tr = np.asarray(KG, dtype=np.int64).reshape(-1, 3)
+    n_raw = int(tr[:, [0, 2]].max()) + 1 if len(tr) else 0
+    row, col, val = synth.adjacency_coo(tr, n_raw)
+    lut = np.full(n_raw, -1, dtype=np.int64)
+    for k, v in index_R.items():
+        if k < n_raw:
+            lut[k] = v
+    return sp.coo_matrix((val.astype(np.float64), (lut[row], lut[col])), shape=(e, e))

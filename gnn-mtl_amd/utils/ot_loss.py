@@ -1,0 +1,32 @@
+"""Entropic OT (reference utils/ot_loss.py) on the fused log-domain HIP Sinkhorn.
+
+``sinkhorn(a, b, M, reg, numItermax, stopThr, verbose) -> (P, loss)`` keeps the reference's
+semantics (fp64 arithmetic, u = 1/I and v = 1/J start, err = ||v (K^T u) - b||_2 checked every
+10th iteration, revert-and-break on K^T u == 0 / inf / NaN) while never materialising K.
+"""
+import torch
+
+from gnnea import _lib
+from gnnea.sinkhorn import solve
+
+
+def sinkhorn(a, b, M, reg, numItermax=1000, stopThr=1e-9, verbose=False):
+    assert a.device == b.device and b.device == M.device, "a, b, M must be on the same device"
+    _lib.require_device(M)
+    I, J = M.shape
+    a = a.double()
+    b = b.double()
+    if len(a) == 0:
+        a = torch.ones(I, dtype=torch.float64, device=M.device) / I
+    if len(b) == 0:
+        b = torch.ones(J, dtype=torch.float64, device=M.device) / J
+    assert len(a) == I and len(b) == J, "the dimension of weights and distance matrix don't match"
+    # fp32 M is widened exactly inside the kernels (the reference casts M to fp64, :27)
+    res = solve(_lib.GNNEA_SK_KNOPP, M, torch.log(a), torch.log(b), reg, stopThr, numItermax)
+    if res.reason == 2:
+        print("Warning: numerical errors at iteration ", res.iters)
+    if verbose:
+        print("{:5s}|{:5s}".format('It.', 'Err') + '\n' + '-' * 19)
+        print("{:5d}|{:.6e}".format(res.iters, res.err))
+    loss = torch.tensor(res.loss, dtype=torch.float64, device=M.device)
+    return res.plan, loss

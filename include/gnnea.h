@@ -1,0 +1,200 @@
+/*
+ * gnnea.h — C-ABI of libgnnea.so, the MI355X (gfx950) hot path of the GNN entity-alignment
+ * engine.  This is the drop-in boundary: the reference (HestiaSky/GNN-MTL) has no FFI of its own;
+ * its hot path is a handful of PyTorch calls inside its nn.Modules.  Each entry point below states
+ * the reference call site it replaces (paths relative to the reference repository root).
+ *
+ * Rules for every entry point:
+ *   - plain pointers + sizes only; all buffers are device-resident, caller-owned (torch-allocated);
+ *   - work is enqueued on the caller's HIP stream (`stream` is a hipStream_t, NULL = default);
+ *   - no allocation, no host synchronisation, no global state: calls are reentrant and
+ *     graph-capturable (gnnea_csr_* query sizes on the host only);
+ *   - return 0 on success, a negative GNNEA_E* code for bad arguments, or a positive hipError_t.
+ */
+#ifndef GNNEA_H
+#define GNNEA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNNEA_ABI_VERSION 1
+
+/* status codes (negative); positive values are hipError_t */
+#define GNNEA_OK 0
+#define GNNEA_EINVAL (-1)      /* bad argument (null pointer, negative size, unsupported combo) */
+#define GNNEA_EWORKSPACE (-2)  /* workspace smaller than the matching *_ws_bytes query */
+#define GNNEA_EALIGN (-3)      /* pointer / leading-dimension alignment the kernel needs */
+
+/* activation codes fused into epilogues (layers/layers.py:26 `self.act`; config 'act') */
+#define GNNEA_ACT_IDENTITY 0
+#define GNNEA_ACT_RELU 1
+#define GNNEA_ACT_ELU 2
+#define GNNEA_ACT_LEAKY_RELU 3 /* negative slope 0.01, F.leaky_relu default */
+#define GNNEA_ACT_SIGMOID 4
+#define GNNEA_ACT_TANH 5
+
+/* element types */
+#define GNNEA_F32 0
+#define GNNEA_F64 1
+#define GNNEA_BF16 2
+
+int gnnea_abi_version(void);
+const char* gnnea_error_string(int code);
+
+/* ------------------------------------------------------------------------------------------ *
+ * a1. Adjacency contract: COO -> CSR.
+ * Replaces the implicit coalesce inside torch.spmm(adj, hidden) (layers/layers.py:35,64) and
+ * adj.coalesce().indices() (layers/att_layers.py:31).  Input is the reference's torch sparse COO
+ * (utils/data_utils.py:51-57, 325-336): uncoalesced, int64 (or int32) indices, fp32 values.
+ * Output: int32 CSR sorted by (row, col), duplicates summed in input order (explicit zeros kept,
+ * as coalesce() keeps them), plus perm[k] = input position of the first duplicate of entry k.
+ * The transpose of a CSR is built by calling it again on (col, row) of that CSR.
+ * *nnz_out is written on the device (int64); rowptr has n_rows+1 entries.
+ * ------------------------------------------------------------------------------------------ */
+int64_t gnnea_coo_to_csr_ws_bytes(int64_t nnz, int64_t n_rows, int64_t n_cols);
+int gnnea_coo_to_csr(const void* row_idx, const void* col_idx, int index_bytes /*4 or 8*/,
+                     const float* val /*nullable: pattern only*/, int64_t nnz, int64_t n_rows,
+                     int64_t n_cols, int32_t* rowptr, int32_t* col_out, float* val_out /*nullable*/,
+                     int64_t* perm_out /*nullable*/, int64_t* nnz_out, void* ws, int64_t ws_bytes,
+                     void* stream);
+/* row id of every CSR entry: row_out[e] = r for rowptr[r] <= e < rowptr[r+1] */
+int gnnea_csr_expand_rows(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t* row_out,
+                          void* stream);
+
+/* ------------------------------------------------------------------------------------------ *
+ * a2/a3. CSR SpMM  Y = act(A · X)   (layers/layers.py:35 torch.spmm(adj, hidden) + :38 act)
+ * Gather model: one wave per destination row, 16-B lanes over the feature row, neighbour
+ * (col,val) broadcast by readlane.  X row stride ldx and Y row stride ldy in elements.
+ * Fast path needs D % 4 == 0, ldx % 4 == 0, ldy % 4 == 0 and 16-B aligned X, Y.
+ * ------------------------------------------------------------------------------------------ */
+int gnnea_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                       int32_t n_rows, int32_t D, const float* X, int64_t ldx, float* Y,
+                       int64_t ldy, int act, void* stream);
+
+/* a4. HighWay epilogue (layers/layers.py:64-76):
+ *   S = act(A·X);  g = sigmoid(gate_pre + bias_gate);  Y = g*S + (1-g)*resid
+ * gate_pre = x·kernel_gate (N x D), bias_gate (D, nullable = 0), resid = x (N x D).
+ * save_s / save_g (nullable) receive S and g for the backward pass. */
+int gnnea_spmm_highway_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                           int32_t n_rows, int32_t D, const float* X, int64_t ldx,
+                           const float* gate_pre, int64_t ldg, const float* bias_gate,
+                           const float* resid, int64_t ldr, float* Y, int64_t ldy,
+                           float* save_s, float* save_g, int64_t lds, int act, void* stream);
+
+/* Elementwise activation backward through the output:  G = dY * act'(Y)  (n elements). */
+int gnnea_act_bwd_f32(const float* dY, const float* Y, float* G, int64_t n, int act, void* stream);
+
+/* HighWay backward, elementwise part (autograd of layers/layers.py:67-76):
+ *   dS_pre  = dY * g * act'(S)            (-> SpMM^T gives d hidden)
+ *   dgate   = dY * (S - resid) * g*(1-g)  (-> d gate_pre; x-grad via kernel_gate^T)
+ *   dresid  = dY * (1 - g)                                                           */
+int gnnea_highway_bwd_f32(const float* dY, const float* S, const float* G, const float* resid,
+                          int64_t ld, int64_t n_rows, int32_t D, float* dS_pre, float* dgate,
+                          float* dresid, int act, void* stream);
+
+/* ------------------------------------------------------------------------------------------ *
+ * a5-a7. Sparse GAT, all heads per edge pass (layers/att_layers.py:29-61, 82-91).
+ * H is the head-concatenated projection X·[W_0|...|W_{h-1}] (N x heads*d_head, row stride ldh);
+ * s1[i,h] = a_h[:d]·H_i,h ; s2[j,h] = a_h[d:]·H_j,h  (att_layers.py:38-41 factorised per node).
+ * score_ij,h = -LeakyReLU_alpha(s1[i,h] + s2[j,h]); the row softmax is computed with the row max
+ * subtracted (mathematically identical to the reference's exp without shift, overflow-safe).
+ * edge_mask (nullable, nnz x heads) multiplies the numerator only (dropout after the row sum,
+ * att_layers.py:51).  Outputs Y = act(h') (ldy), row max m and denominator den (N x heads).
+ * Rows without edges produce 0 (the reference raises on them).
+ * ------------------------------------------------------------------------------------------ */
+int gnnea_gat_scores_f32(const float* H, int64_t ldh, int32_t n_rows, int heads, int d_head,
+                         const float* a /*heads x 2*d_head*/, float* s1, float* s2, void* stream);
+int gnnea_gat_fwd_f32(const int32_t* rowptr, const int32_t* col, int32_t n_rows, const float* H,
+                      int64_t ldh, int heads, int d_head, const float* s1, const float* s2,
+                      float alpha, const float* edge_mask, int act, float* Y, int64_t ldy,
+                      float* m_out, float* den_out, void* stream);
+/* Backward pass 1, row sweep (SDDMM + softmax backward):
+ *   for edge (i,j): da = G_i·H_j (per head), dscore = alpha_ij*(mask*da - G_i·P_i),
+ *   dz = -LeakyReLU'(z)*dscore  -> dz (nnz x heads);  ds1_i = sum_j dz.
+ * G = dL/dh' (pre-activation gradient), P = h' (pre-activation output), both ld = ldg. */
+int gnnea_gat_bwd_edge_f32(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
+                           const float* H, int64_t ldh, int heads, int d_head, const float* s1,
+                           const float* s2, float alpha, const float* edge_mask, const float* m,
+                           const float* den, const float* G, const float* P, int64_t ldg,
+                           float* dz, float* ds1, void* stream);
+/* Backward pass 2, transpose sweep over A^T (rowptrT/colT/permT from gnnea_coo_to_csr):
+ *   dH_j = sum_i alpha_ij*mask*G_i  +  ds1_j (x) a1 + ds2_j (x) a2 ;  ds2_j = sum_i dz(i,j). */
+int gnnea_gat_bwd_node_f32(const int32_t* rowptrT, const int32_t* colT, const int64_t* permT,
+                           int32_t n_rows, int heads, int d_head, const float* s1,
+                           const float* s2, float alpha, const float* edge_mask, const float* m,
+                           const float* den, const float* G, int64_t ldg, const float* dz,
+                           const float* ds1, const float* a, float* dH, int64_t lddh, float* ds2,
+                           void* stream);
+
+/* ------------------------------------------------------------------------------------------ *
+ * Dense projection (nn.Linear at layers/layers.py:32,61,93; torch.mm at att_layers.py:33;
+ * torch.spmm(x, kernel_gate) at layers.py:69).  f32-in / f32-accumulate MFMA
+ * (v_mfma_f32_32x32x2_f32): bit-for-bit an fmaf chain in k order.
+ *   C[M,N] = op(A)[M,K] · op(B)[K,N] (+ bias[N]) (+ beta*C) ; op = transpose when trans_* != 0.
+ * Row-major, leading dimensions in elements.  Products whose output tiles cannot fill the chip
+ * but have a long K (weight gradients: K = number of nodes) split K over workgroups into fp32
+ * slabs in `ws` (gnnea_gemm_ws_bytes) reduced in fixed order — deterministic; ws may be NULL.
+ * ------------------------------------------------------------------------------------------ */
+int64_t gnnea_gemm_ws_bytes(int64_t M, int64_t N, int64_t K);
+int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                   int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
+                   float* C, int64_t ldc, void* ws, int64_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------ *
+ * a9-a12. Fused log-domain Sinkhorn.
+ *   GNNEA_SK_KNOPP : utils/ot_loss.py:5-76 sinkhorn(a, b, M, reg, numItermax, stopThr)
+ *   GNNEA_SK_STAB  : SinkhornOT/sinkhorn_loss.py:159-220 sinkhorn_iteration
+ *   GNNEA_SK_GEN   : SinkhornOT/sinkhorn_loss.py:223-288 gsinkhorn_iteration
+ *   GNNEA_SK_RELAX : SinkhornOT/sinkhorn_loss.py:291-356 forward_relax_sinkhorn_iteration
+ * All arithmetic is fp64; the cost may be stored fp32 (exact fp32->fp64 widening, as the
+ * reference's .type(torch.DoubleTensor)) or fp64.  The solver state lives in `ws`; the host
+ * drives the data-dependent loop with gnnea_sinkhorn_iterate() batches and reads the status
+ * block (first GNNEA_SK_STATUS_BYTES of ws) between batches.  Kernels of an iteration after
+ * the stop condition are no-ops, so over-enqueueing is harmless.
+ * ------------------------------------------------------------------------------------------ */
+#define GNNEA_SK_KNOPP 0
+#define GNNEA_SK_STAB 1
+#define GNNEA_SK_GEN 2
+#define GNNEA_SK_RELAX 3
+
+/* status block (int64 words at the start of ws) */
+#define GNNEA_SK_ST_DONE 0       /* 1 once the loop has stopped */
+#define GNNEA_SK_ST_ITERS 1      /* reference's final iteration counter (cpt / ii) */
+#define GNNEA_SK_ST_REASON 2     /* 0 running/max-iter, 1 tolerance, 2 numerical-error break */
+#define GNNEA_SK_ST_SLOT 3       /* ping-pong slot holding the final potentials */
+#define GNNEA_SK_STATUS_BYTES 256
+/* double words after the int block: [8]=err/transport, [9]=transport_prev, [10]=loss */
+
+typedef struct gnnea_sinkhorn {
+  int mode;         /* GNNEA_SK_* */
+  int c_dtype;      /* GNNEA_F32 or GNNEA_F64 */
+  int I, J;         /* cost is I x J */
+  int64_t ldc;      /* row stride of C in elements */
+  const void* C;    /* cost matrix (M for KNOPP) */
+  const double* log_a; /* I: log of the source weights (a / mu) */
+  const double* log_b; /* J: log of the target weights (b / nu) */
+  double eps;       /* reg (KNOPP) or epsilon */
+  double p;         /* lambda/(lambda+eps) for GEN / RELAX; ignored otherwise */
+  double tol;       /* stopThr (KNOPP) or tol */
+  int max_iter;     /* numItermax / numIterMax */
+  int iters_run;    /* iterations enqueued so far (read by gnnea_sinkhorn_finish) */
+  void* ws;         /* device workspace of gnnea_sinkhorn_ws_bytes(I, J) bytes */
+} gnnea_sinkhorn;
+
+int64_t gnnea_sinkhorn_ws_bytes(int I, int J);
+int gnnea_sinkhorn_init(const gnnea_sinkhorn* prob, void* stream);
+/* enqueue iterations [first, first+count) (count >= 1) */
+int gnnea_sinkhorn_iterate(const gnnea_sinkhorn* prob, int first, int count, void* stream);
+/* plan (I x J, plan_dtype, row stride ldp, nullable): KNOPP: P = diag(u) K diag(v);
+ * others: K = clamp(exp(u+v-C/eps), 0, 1e30).  Also writes row sums (I) and column sums (J) of
+ * the plan into row_sum/col_sum (nullable, fp64) and the scalars into the status block. */
+int gnnea_sinkhorn_finish(const gnnea_sinkhorn* prob, void* plan, int plan_dtype, int64_t ldp,
+                          double* row_sum, double* col_sum, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNNEA_H */

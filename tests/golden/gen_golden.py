@@ -1,0 +1,205 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE implementation.
+
+Run in the build container only (it needs /root/reference, which never travels to the GPU box):
+
+    python tests/golden/gen_golden.py
+
+The reference is imported as-is from /root/reference.  Two third-party modules it imports at
+module top but never uses on the paths exercised here are absent from the image and replaced by
+empty placeholder modules before the import:
+  * ``ot`` (POT)      — imported by SinkhornOT/sinkhorn_loss.py:9, used only in __main__/tests;
+  * ``torchtext``     — imported by utils/data_utils.py:13, used only by load_data_nctext.
+Everything written here is data (inputs and expected outputs), no reference source.
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+
+
+def _placeholders():
+    sys.modules.setdefault("ot", types.ModuleType("ot"))
+    tt = types.ModuleType("torchtext")
+    ttd = types.ModuleType("torchtext.data")
+    for name in ("Dataset", "BucketIterator", "Field", "Example"):
+        setattr(ttd, name, object)
+    tt.data = ttd
+    sys.modules.setdefault("torchtext", tt)
+    sys.modules.setdefault("torchtext.data", ttd)
+
+
+def _synth():
+    # the synthetic generator lives in the product package (host logic, not reference code)
+    sys.path.insert(0, os.path.join(REPO, "gnn-mtl_amd"))
+    from gnnea import synth  # noqa: E402
+    sys.path.pop(0)
+    for k in [m for m in sys.modules if m == "gnnea" or m.startswith("gnnea.")]:
+        del sys.modules[k]
+    return synth
+
+
+def _digest(t):
+    import hashlib
+    a = t.detach().contiguous().numpy()
+    return "%s|%s|%s" % (a.dtype.str, "x".join(map(str, a.shape)), hashlib.sha256(a.tobytes()).hexdigest())
+
+
+def main():
+    synth = _synth()
+    _placeholders()
+    sys.path.insert(0, REF)
+    import layers.layers as RL
+    import layers.att_layers as RA
+    import models.encoders as RE
+    import models.decoders as RD
+    import utils.data_utils as RDU
+    import utils.ot_loss as ROT
+    import SinkhornOT.sinkhorn_loss as RSK
+    torch.set_num_threads(8)
+
+    # ---------------- graph (cfg-1: 2 x 1k entities, 2 x 2.5k triples) ----------------
+    n, t = 1000, 2500
+    N = 2 * n
+    triples = synth.kg_pair_triples(n, t, 1000, seed=0)
+    KG = [tuple(x) for x in triples.tolist()]
+    adj = RDU.sparse_mx_to_torch_sparse_tensor(RDU.get_sparse_tensor(N, KG))
+    X = synth.features(N, 300, seed=1)
+    idx = adj._indices().numpy()
+    np.savez_compressed(os.path.join(HERE, "graph_cfg1.npz"), triples=triples, row=idx[0],
+                        col=idx[1], val=adj._values().numpy(), X=X, N=np.int64(N))
+
+    # tiny edge-case graph: self-loop triple, multi-edges, isolated entity
+    tr_small = np.array([[0, 0, 0], [1, 5, 2], [1, 6, 2], [2, 1, 1], [3, 0, 3], [4, 2, 0],
+                         [5, 1, 6]], dtype=np.int64)
+    adj_s = RDU.sparse_mx_to_torch_sparse_tensor(
+        RDU.get_sparse_tensor(8, [tuple(x) for x in tr_small.tolist()]))
+    np.savez_compressed(os.path.join(HERE, "graph_small.npz"), triples=tr_small,
+                        row=adj_s._indices().numpy()[0], col=adj_s._indices().numpy()[1],
+                        val=adj_s._values().numpy(), N=np.int64(8))
+
+    x = torch.from_numpy(X)
+    torch.manual_seed(7)
+    R = torch.randn(N, 300)
+
+    def run_layer(layer, split_out):
+        xx = x.clone().requires_grad_(True)
+        out = layer((xx, adj))[0] if split_out else layer(xx, adj)
+        (out * R[:, :out.shape[1]]).sum().backward()
+        return out.detach().numpy(), xx.grad.numpy()
+
+    data = {}
+    # GraphConvolution(300, 300, dropout 0, relu, bias)  (layers/layers.py:19-42)
+    torch.manual_seed(10086)
+    gc = RL.GraphConvolution(300, 300, 0.0, F.relu, True)
+    gc.train()
+    out, dx = run_layer(gc, True)
+    data.update(gcn_W=gc.linear.weight.detach().numpy(), gcn_b=gc.linear.bias.detach().numpy(),
+                gcn_out=out, gcn_dx=dx, gcn_dW=gc.linear.weight.grad.numpy(),
+                gcn_db=gc.linear.bias.grad.numpy())
+    # HighWayGraphConvolution (layers/layers.py:45-80)
+    torch.manual_seed(10087)
+    hw = RL.HighWayGraphConvolution(300, 300, 0.0, F.relu, True, -1, "cpu")
+    hw.train()
+    out, dx = run_layer(hw, True)
+    data.update(hw_W=hw.linear.weight.detach().numpy(), hw_b=hw.linear.bias.detach().numpy(),
+                hw_Kg=hw.kernel_gate.numpy(), hw_out=out, hw_dx=dx,
+                hw_dW=hw.linear.weight.grad.numpy(), hw_db=hw.linear.bias.grad.numpy())
+    # GraphAttentionLayer, 4 heads x 75, concat (layers/att_layers.py:67-91)
+    torch.manual_seed(10088)
+    ga = RA.GraphAttentionLayer(300, 75, 0.0, F.relu, 0.2, 4, True)
+    ga.train()
+    out, dx = run_layer(ga, True)
+    data.update(gat_W=np.stack([h.W.detach().numpy() for h in ga.attentions]),
+                gat_a=np.stack([h.a.detach().numpy() for h in ga.attentions]),
+                gat_out=out, gat_dx=dx,
+                gat_dW=np.stack([h.W.grad.numpy() for h in ga.attentions]),
+                gat_da=np.stack([h.a.grad.numpy() for h in ga.attentions]))
+    np.savez_compressed(os.path.join(HERE, "layers_cfg1.npz"), **data)
+
+    # ---------------- full encoder + decoder forward, reference init under seed 10086 ----------
+    class Args:
+        pass
+
+    enc = {}
+    for model in ("GCN", "GAT", "HGCN"):
+        a = Args()
+        a.model, a.num_layers, a.dim, a.act, a.dropout, a.bias = model, 3, 300, "relu", 0.0, 1
+        a.n_heads, a.alpha, a.feat_dim, a.n_classes, a.cuda, a.device = 4, 0.2, 300, 300, -1, "cpu"
+        torch.manual_seed(10086)
+        e = RE.model2encoder[model](a)
+        d = RD.model2decoder[model](a)
+        e.eval()
+        d.eval()
+        xs = torch.from_numpy(X).to_sparse()
+        with torch.no_grad():
+            h = e.encode(xs, adj)
+            o = d.decode(h, adj)
+        enc[model + "_out"] = o.numpy()
+        # weights are regenerated by the drop-in constructors under the same seed; the fixture
+        # pins them bit-for-bit by digest (key order = state_dict order)
+        for part, mod in (("enc", e), ("dec", d)):
+            for k, v in mod.state_dict().items():
+                enc["%s_%s.%s" % (model, part, k)] = np.array(_digest(v))
+        if model == "HGCN":
+            for i, layer in enumerate(e.layers):
+                enc["HGCN_enc_kernel_gate.%d" % i] = np.array(_digest(layer.kernel_gate))
+            enc["HGCN_dec_kernel_gate"] = np.array(_digest(d.cls.kernel_gate))
+    np.savez_compressed(os.path.join(HERE, "encoders_cfg1.npz"), **enc)
+
+    # ---------------- Sinkhorn family ----------------
+    sk = {}
+    rng = np.random.default_rng(5)
+    for tag, (I, J) in {"s": (100, 120), "m": (300, 300)}.items():
+        Xs = 0.05 * rng.standard_normal((I, 300))
+        Ys = 0.05 * rng.standard_normal((J, 300))
+        M = torch.cdist(torch.from_numpy(Xs).float(), torch.from_numpy(Ys).float(), p=2)
+        M = M / M.max()
+        sk["%s_M" % tag] = M.numpy()
+        for reg in (0.05, 0.01):
+            key = "%s_r%g" % (tag, reg)
+            P, loss = ROT.sinkhorn(torch.ones(I), torch.ones(J), M, reg=reg)
+            sk[key + "_knopp_P"] = P.numpy()
+            sk[key + "_knopp_loss"] = loss.numpy()
+            C = M.double().view(1, I, J)
+            mu = torch.full((1, I, 1), 1.0 / I, dtype=torch.float64)
+            nu = torch.full((1, 1, J), 1.0 / J, dtype=torch.float64)
+            for name, fn in (("stab", lambda: RSK.sinkhorn_iteration(C, mu, nu, reg)),
+                             ("gen", lambda: RSK.gsinkhorn_iteration(C, mu, nu, 1.0, reg)),
+                             ("relax", lambda: RSK.forward_relax_sinkhorn_iteration(
+                                 C, mu, nu, 1.0, reg))):
+                tr_, m1, m2, K = fn()
+                sk["%s_%s_transport" % (key, name)] = tr_.numpy()
+                sk["%s_%s_m1" % (key, name)] = m1.numpy()
+                sk["%s_%s_m2" % (key, name)] = m2.numpy()
+                if tag == "s" or name == "stab":
+                    sk["%s_%s_K" % (key, name)] = K.numpy()
+    # underflow case: EA-like un-normalised distances, reg 0.01 -> K^T u == 0 break at it. 0
+    Xu = rng.standard_normal((64, 300)) * 0.6
+    Yu = rng.standard_normal((80, 300)) * 0.6
+    Mu = torch.cdist(torch.from_numpy(Xu).float(), torch.from_numpy(Yu).float(), p=2)
+    P, loss = ROT.sinkhorn(torch.ones(64), torch.ones(80), Mu, reg=0.01)
+    sk.update(under_M=Mu.numpy(), under_P=P.numpy(), under_loss=loss.numpy())
+    # the reference test's own configuration (SinkhornOT/test_Sinkhorn_OT.py:9-49): cosine
+    # costs of uniform vectors, eps 1e-4, fp64, seeded here (the test leaves the seed unset)
+    from SinkhornOT.cderivation import cos_dist_mat, get_inter_sim
+    Va = torch.from_numpy(rng.uniform(size=(100, 100)))
+    Vb = torch.from_numpy(rng.uniform(size=(100, 100)))
+    Mt = get_inter_sim(Va, Vb, cos_dist_mat).double()
+    at = torch.full((1, 100, 1), 0.01, dtype=torch.float64)
+    bt = torch.full((1, 1, 100), 0.01, dtype=torch.float64)
+    tr_, m1, m2, K = RSK.sinkhorn_iteration(Mt.view(1, 100, 100), at, bt, 1e-4)
+    sk.update(test_M=Mt.numpy(), test_transport=tr_.numpy(), test_m1=m1.numpy(),
+              test_m2=m2.numpy(), test_K=K.numpy())
+    np.savez_compressed(os.path.join(HERE, "sinkhorn.npz"), **sk)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,54 @@
+"""The C-ABI library loads and exports every symbol include/gnnea.h declares (no GPU needed)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "gnnea.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z0-9_]+\*?\s+\*?(gnnea_[a-z0-9_]+)\s*\(", src, re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_the_hot_path():
+    names = declared_functions()
+    for must in ("gnnea_coo_to_csr", "gnnea_spmm_csr_f32", "gnnea_spmm_highway_f32",
+                 "gnnea_gat_fwd_f32", "gnnea_gat_bwd_edge_f32", "gnnea_gat_bwd_node_f32",
+                 "gnnea_gemm_f32", "gnnea_sinkhorn_iterate", "gnnea_sinkhorn_finish"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from gnnea import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libgnnea.so not built")
+    L = _lib.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+        assert name in _lib.SIGNATURES, "ctypes signature missing for " + name
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True).stdout
+    exported = set(re.findall(r" T (gnnea_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_host_only_entry_points():
+    from gnnea import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libgnnea.so not built")
+    L = _lib.lib()
+    assert L.gnnea_abi_version() == 1
+    assert b"workspace" in L.gnnea_error_string(-2)
+    assert L.gnnea_sinkhorn_ws_bytes(3000, 3000) > 3000 * 8 * 4
+    assert L.gnnea_gemm_ws_bytes(300, 300, 2_000_000) > 0
+    # argument validation never touches the device
+    assert L.gnnea_spmm_csr_f32(None, None, None, -1, 300, None, 300, None, 300, 1, None) == -1
+    assert L.gnnea_gemm_f32(0, 0, 4, 4, 4, None, 4, None, 4, None, 0.0, None, 4, None, 0,
+                            None) == -1

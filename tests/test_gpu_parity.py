@@ -1,0 +1,307 @@
+"""HIP path vs the reference fixtures and the CPU oracle (run on an MI355X: pytest -m gpu).
+
+Tolerance: norm-relative ||y - y_ref||_inf / ||y_ref||_inf <= 1e-4 for fp32
+outputs (measured fp32-vs-fp64 error of the reference itself: 1.8e-7 .. 4.1e-7); fp64 Sinkhorn
+(log domain vs the reference's scaling form): 1e-9 relative on plans and scalars.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+TOL32 = 1e-4
+TOL64 = 1e-9
+
+
+def _adj(g, dev, n=None):
+    n = int(g["N"]) if n is None else n
+    idx = torch.from_numpy(np.stack([g["row"], g["col"]]).astype(np.int64))
+    return torch.sparse_coo_tensor(idx, torch.from_numpy(g["val"]), (n, n)).to(dev)
+
+
+def _R(dev):
+    torch.manual_seed(7)
+    return torch.randn(2000, 300).to(dev)
+
+
+# ------------------------------------------------------------------------------------------ #
+# a1: COO -> CSR                                                                              #
+# ------------------------------------------------------------------------------------------ #
+def test_csr_matches_scipy(golden, device):
+    import scipy.sparse as sp
+    from gnnea.graph import DeviceCSR
+    g = golden("graph_cfg1")
+    rng = np.random.default_rng(0)
+    # append duplicates and an explicit zero to exercise coalescing
+    dup = rng.integers(0, g["row"].size, 500)
+    row = np.concatenate([g["row"], g["row"][dup], [5]])
+    col = np.concatenate([g["col"], g["col"][dup], [1999]])
+    val = np.concatenate([g["val"], g["val"][dup] * 0.5, [0.0]]).astype(np.float32)
+    csr = DeviceCSR.from_coo(torch.from_numpy(row).to(device), torch.from_numpy(col).to(device),
+                             torch.from_numpy(val).to(device), 2000, 2000)
+    ref = sp.coo_matrix((val.astype(np.float64), (row, col)), shape=(2000, 2000)).tocsr()
+    ref.sort_indices()
+    assert np.array_equal(csr.rowptr.cpu().numpy(), ref.indptr)
+    assert np.array_equal(csr.col.cpu().numpy(), ref.indices)
+    assert np.allclose(csr.val.cpu().numpy(), ref.data, rtol=1e-6, atol=0)
+    assert (5, 1999) in set(zip(np.repeat(np.arange(2000), np.diff(ref.indptr)).tolist(),
+                                ref.indices.tolist()))
+    t = csr.transpose()
+    refT = ref.T.tocsr()
+    refT.sort_indices()
+    assert np.array_equal(t.rowptr.cpu().numpy(), refT.indptr)
+    assert np.array_equal(t.col.cpu().numpy(), refT.indices)
+    perm = t.perm.cpu().numpy()
+    assert np.array_equal(csr.val.cpu().numpy()[perm], t.val.cpu().numpy())
+
+
+def test_csr_rejects_out_of_range(device):
+    from gnnea.graph import DeviceCSR
+    r = torch.tensor([0, 1, 7], device=device)
+    c = torch.tensor([0, 1, 2], device=device)
+    with pytest.raises(ValueError):
+        DeviceCSR.from_coo(r, c, torch.ones(3, device=device), 4, 4)
+
+
+# ------------------------------------------------------------------------------------------ #
+# a2-a4: GCN / HighWay layers vs the reference fixtures                                       #
+# ------------------------------------------------------------------------------------------ #
+def _layer_case(layer, x, adj, R):
+    xx = x.clone().requires_grad_(True)
+    out = layer((xx, adj))[0]
+    (out * R[:, :out.shape[1]]).sum().backward()
+    return out.detach().cpu().numpy(), xx.grad.cpu().numpy()
+
+
+def test_gcn_layer_vs_reference(golden, device):
+    from layers.layers import GraphConvolution
+    g, L = golden("graph_cfg1"), golden("layers_cfg1")
+    gc = GraphConvolution(300, 300, 0.0, F.relu, True).to(device)
+    with torch.no_grad():
+        gc.linear.weight.copy_(torch.from_numpy(L["gcn_W"]))
+        gc.linear.bias.copy_(torch.from_numpy(L["gcn_b"]))
+    gc.train()
+    out, dx = _layer_case(gc, torch.from_numpy(g["X"]).to(device), _adj(g, device), _R(device))
+    assert rel_err(out, L["gcn_out"]) < TOL32
+    assert rel_err(dx, L["gcn_dx"]) < TOL32
+    assert rel_err(gc.linear.weight.grad.cpu(), L["gcn_dW"]) < TOL32
+    assert rel_err(gc.linear.bias.grad.cpu(), L["gcn_db"]) < TOL32
+
+
+def test_highway_layer_vs_reference(golden, device):
+    from layers.layers import HighWayGraphConvolution
+    g, L = golden("graph_cfg1"), golden("layers_cfg1")
+    hw = HighWayGraphConvolution(300, 300, 0.0, F.relu, True, 0, device).to(device)
+    with torch.no_grad():
+        hw.linear.weight.copy_(torch.from_numpy(L["hw_W"]))
+        hw.linear.bias.copy_(torch.from_numpy(L["hw_b"]))
+    hw.kernel_gate = torch.from_numpy(L["hw_Kg"]).to(device)
+    out, dx = _layer_case(hw, torch.from_numpy(g["X"]).to(device), _adj(g, device), _R(device))
+    assert rel_err(out, L["hw_out"]) < TOL32
+    assert rel_err(dx, L["hw_dx"]) < TOL32
+    assert rel_err(hw.linear.weight.grad.cpu(), L["hw_dW"]) < TOL32
+    assert rel_err(hw.linear.bias.grad.cpu(), L["hw_db"]) < TOL32
+
+
+def test_gat_layer_vs_reference(golden, device):
+    from layers.att_layers import GraphAttentionLayer
+    g, L = golden("graph_cfg1"), golden("layers_cfg1")
+    ga = GraphAttentionLayer(300, 75, 0.0, F.relu, 0.2, 4, True).to(device)
+    with torch.no_grad():
+        for h, att in enumerate(ga.attentions):
+            att.W.copy_(torch.from_numpy(L["gat_W"][h]))
+            att.a.copy_(torch.from_numpy(L["gat_a"][h]))
+    out, dx = _layer_case(ga, torch.from_numpy(g["X"]).to(device), _adj(g, device), _R(device))
+    assert rel_err(out, L["gat_out"]) < TOL32
+    assert rel_err(dx, L["gat_dx"]) < TOL32
+    dW = np.stack([a.W.grad.cpu().numpy() for a in ga.attentions])
+    da = np.stack([a.a.grad.cpu().numpy() for a in ga.attentions])
+    assert rel_err(dW, L["gat_dW"]) < TOL32
+    assert rel_err(da, L["gat_da"]) < TOL32
+
+
+@pytest.mark.parametrize("model", ["GCN", "GAT", "HGCN"])
+def test_encoder_decoder_vs_reference(golden, device, model):
+    from models.decoders import model2decoder
+    from models.encoders import model2encoder
+    from test_dropin_cpu import make_args
+    g, E = golden("graph_cfg1"), golden("encoders_cfg1")
+    a = make_args(model)
+    a.cuda, a.device = 0, device
+    torch.manual_seed(10086)  # reference init order reproduces the fixture's weights
+    enc = model2encoder[model](a).to(device).eval()
+    dec = model2decoder[model](a).to(device).eval()
+    adj = _adj(g, device)
+    xs = torch.from_numpy(g["X"]).to_sparse().to(device)  # sparse-COO features, as the ref
+    with torch.no_grad():
+        out = dec.decode(enc.encode(xs, adj), adj)
+    assert rel_err(out.cpu(), E[model + "_out"]) < TOL32
+
+
+# ------------------------------------------------------------------------------------------ #
+# kernels vs the oracle on edge cases                                                         #
+# ------------------------------------------------------------------------------------------ #
+def _random_coo(rng, n_rows, n_cols, nnz, dup=True):
+    r = rng.integers(0, n_rows, nnz)
+    c = rng.integers(0, n_cols, nnz)
+    if dup:
+        r = np.concatenate([r, r[: nnz // 10]])
+        c = np.concatenate([c, c[: nnz // 10]])
+    v = rng.standard_normal(r.size).astype(np.float32)
+    return r, c, v
+
+
+@pytest.mark.parametrize("D", [1, 3, 4, 64, 75, 128, 252, 300, 512, 1024])
+def test_spmm_shapes_vs_oracle(device, D):
+    from gnnea import ops
+    from gnnea.graph import DeviceCSR
+    from oracle.gnn import coo_aggregate
+    rng = np.random.default_rng(D)
+    n = 700
+    r, c, v = _random_coo(rng, n, n, 6000)
+    # one very long row (>64 and >128 neighbours) and empty rows at both ends
+    r = np.concatenate([r[(r > 3) & (r < n - 3)], np.full(200, 17)])
+    c = np.concatenate([c[: r.size - 200], rng.integers(0, n, 200)])
+    v = rng.standard_normal(r.size).astype(np.float32)
+    x = rng.standard_normal((n, D)).astype(np.float32)
+    csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                             torch.from_numpy(v).to(device), n, n)
+    for act, fn in ((0, lambda t: t), (1, torch.relu), (4, torch.sigmoid), (5, torch.tanh)):
+        y = ops.spmm(csr, torch.from_numpy(x).to(device), act).cpu()
+        ref = fn(coo_aggregate(r, c, v, n, torch.from_numpy(x).double()))
+        assert rel_err(y, ref) < TOL32, (D, act)
+    assert torch.all(ops.spmm(csr, torch.from_numpy(x).to(device))[:3].cpu() == 0)
+
+
+def test_spmm_strided_input(device):
+    from gnnea import ops
+    from gnnea.graph import DeviceCSR
+    from oracle.gnn import coo_aggregate
+    rng = np.random.default_rng(1)
+    r, c, v = _random_coo(rng, 300, 300, 3000)
+    big = torch.from_numpy(rng.standard_normal((300, 320)).astype(np.float32)).to(device)
+    x = big[:, :300]  # ld = 320
+    csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                             torch.from_numpy(v).to(device), 300, 300)
+    y = ops.spmm(csr, x).cpu()
+    assert rel_err(y, coo_aggregate(r, c, v, 300, x.cpu().double())) < TOL32
+
+
+@pytest.mark.parametrize("heads,d", [(1, 300), (4, 75), (2, 7), (8, 16)])
+def test_gat_fwd_bwd_vs_oracle(device, heads, d):
+    from gnnea import ops
+    from oracle.gnn import gat_layer
+    rng = np.random.default_rng(heads * 100 + d)
+    n, fin = 400, 48
+    r, c, _ = _random_coo(rng, n, n, 3000, dup=False)
+    r = np.concatenate([r, np.arange(n)])  # every node has a self loop (reference needs >=1)
+    c = np.concatenate([c, np.arange(n)])
+    v = np.ones(r.size, dtype=np.float32)
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([r, c])), torch.from_numpy(v),
+                                  (n, n)).to(device)
+    x = rng.standard_normal((n, fin)).astype(np.float32)
+    W = (rng.standard_normal((heads, fin, d)) * 0.3).astype(np.float32)
+    A = (rng.standard_normal((heads, 1, 2 * d)) * 0.3).astype(np.float32)
+    Rr = rng.standard_normal((n, heads * d)).astype(np.float32)
+    xt = torch.from_numpy(x).to(device).requires_grad_(True)
+    Wt = torch.from_numpy(W).to(device).requires_grad_(True)
+    At = torch.from_numpy(A).to(device).requires_grad_(True)
+    H = ops.matmul(xt, torch.cat(list(Wt), dim=1))
+    y = ops.gat(adj, H, At.view(heads, 2 * d), heads, d, 0.2, F.relu)
+    (y * torch.from_numpy(Rr).to(device)).sum().backward()
+    xo = torch.from_numpy(x).double().requires_grad_(True)
+    Wo = torch.from_numpy(W).double().requires_grad_(True)
+    Ao = torch.from_numpy(A).double().requires_grad_(True)
+    yo = gat_layer(xo, Wo, Ao, r, c, 0.2)
+    (yo * torch.from_numpy(Rr).double()).sum().backward()
+    assert rel_err(y.detach().cpu(), yo.detach()) < TOL32
+    assert rel_err(xt.grad.cpu(), xo.grad) < TOL32
+    assert rel_err(Wt.grad.cpu(), Wo.grad) < TOL32
+    assert rel_err(At.grad.cpu(), Ao.grad) < 3e-4
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (37, 300, 300), (300, 75, 300), (513, 600, 300),
+                                   (300, 300, 20000), (5, 300, 7)])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_vs_fp64(device, shape, ta, tb):
+    from gnnea import ops
+    M, N, K = shape
+    rng = np.random.default_rng(M + N + K)
+    a = rng.standard_normal((K, M) if ta else (M, K)).astype(np.float32)
+    b = rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    y = ops.gemm(torch.from_numpy(a).to(device), torch.from_numpy(b).to(device), bool(ta),
+                 bool(tb), bias=torch.from_numpy(bias).to(device)).cpu()
+    ref = (a.T if ta else a).astype(np.float64) @ (b.T if tb else b).astype(np.float64) + bias
+    assert rel_err(y, ref) < 1e-5
+
+
+# ------------------------------------------------------------------------------------------ #
+# a9-a12: Sinkhorn family vs the reference fixtures                                           #
+# ------------------------------------------------------------------------------------------ #
+@pytest.mark.parametrize("tag", ["s", "m"])
+@pytest.mark.parametrize("reg", [0.05, 0.01])
+def test_sinkhorn_family_vs_reference(golden, device, tag, reg):
+    import SinkhornOT.sinkhorn_loss as SK
+    from utils.ot_loss import sinkhorn
+    S = golden("sinkhorn")
+    M = torch.from_numpy(S["%s_M" % tag]).to(device)
+    I, J = M.shape
+    key = "%s_r%g" % (tag, reg)
+    P, loss = sinkhorn(torch.ones(I, device=device), torch.ones(J, device=device), M, reg=reg)
+    assert P.dtype == torch.float64
+    assert rel_err(P.cpu(), S[key + "_knopp_P"]) < TOL64
+    assert abs(loss.item() - float(S[key + "_knopp_loss"])) <= TOL64 * abs(loss.item())
+    C = M.double().view(1, I, J)
+    mu = torch.full((1, I, 1), 1.0 / I, dtype=torch.float64, device=device)
+    nu = torch.full((1, 1, J), 1.0 / J, dtype=torch.float64, device=device)
+    for name, fn in (("stab", lambda: SK.sinkhorn_iteration(C, mu, nu, reg)),
+                     ("gen", lambda: SK.gsinkhorn_iteration(C, mu, nu, 1.0, reg)),
+                     ("relax", lambda: SK.forward_relax_sinkhorn_iteration(C, mu, nu, 1.0, reg))):
+        t, m1, m2, K = fn()
+        assert K.shape == (1, I, J) and K.dtype == torch.float64
+        for v, ref in ((t, "transport"), (m1, "m1"), (m2, "m2")):
+            r = float(S["%s_%s_%s" % (key, name, ref)])
+            assert abs(v.item() - r) <= 1e-8 * max(abs(r), 1e-12), (name, ref, v.item(), r)
+        kk = "%s_%s_K" % (key, name)
+        if kk in S:
+            assert rel_err(K[0].cpu(), S[kk]) < TOL64, name
+
+
+def test_sinkhorn_underflow_break(golden, device):
+    from utils.ot_loss import sinkhorn
+    S = golden("sinkhorn")
+    M = torch.from_numpy(S["under_M"]).to(device)
+    P, loss = sinkhorn(torch.ones(M.shape[0], device=device),
+                       torch.ones(M.shape[1], device=device), M, reg=0.01)
+    assert rel_err(P.cpu(), S["under_P"]) < TOL64
+
+
+def test_sinkhorn_reference_test_config(golden, device):
+    import SinkhornOT.sinkhorn_loss as SK
+    S = golden("sinkhorn")
+    M = torch.from_numpy(S["test_M"]).to(device).view(1, 100, 100)
+    a = torch.full((1, 100, 1), 0.01, dtype=torch.float64, device=device)
+    b = torch.full((1, 1, 100), 0.01, dtype=torch.float64, device=device)
+    t, m1, m2, K = SK.sinkhorn_iteration(M, a, b, 1e-4)
+    assert abs(t.item() - float(S["test_transport"])) <= 1e-8 * abs(float(S["test_transport"]))
+    assert rel_err(K[0].cpu(), S["test_K"]) < 1e-8
+
+
+def test_sinkhorn_vs_oracle_random(device):
+    from oracle import sinkhorn as osk
+    from utils.ot_loss import sinkhorn
+    rng = np.random.default_rng(11)
+    for I, J, reg in ((50, 70, 0.1), (257, 129, 0.02), (1000, 1000, 0.01)):
+        M = rng.uniform(0, 1, (I, J))
+        a = rng.uniform(0.5, 1.5, I)
+        b = rng.uniform(0.5, 1.5, J)
+        b *= a.sum() / b.sum()
+        P, loss = sinkhorn(torch.from_numpy(a).to(device), torch.from_numpy(b).to(device),
+                           torch.from_numpy(M).to(device), reg=reg, numItermax=300)
+        Po, lo, _, _ = osk.knopp(a, b, M, reg, 300)
+        assert rel_err(P.cpu(), Po) < TOL64, (I, J)
+        assert abs(loss.item() - lo) <= TOL64 * abs(lo)
