@@ -139,32 +139,69 @@ __device__ __forceinline__ void mark_done(int64_t* st, int64_t iters, int64_t re
   }
 }
 
-// Row pass: f_out_i from g_in (one wave per row).
-template <typename T>
+// Chunked, branch-free online LSE: per chunk of CH values one rescale exp + one exp per value
+// (a per-element "if (x > m)" diverges across lanes and costs two exps per element).
+template <int CH>
+__device__ __forceinline__ void lse_chunk(Lse& l, const double (&x)[CH]) {
+  double cm = x[0];
+#pragma unroll
+  for (int k = 1; k < CH; ++k) cm = fmax(cm, x[k]);
+  if (cm == -INFINITY) return;  // whole chunk masked (K == 0)
+  const double nm = fmax(l.m, cm);
+  double acc = l.m == -INFINITY ? 0.0 : l.s * exp(l.m - nm);
+#pragma unroll
+  for (int k = 0; k < CH; ++k) acc += exp(x[k] - nm);  // exp(-inf) == 0
+  l.m = nm;
+  l.s = acc;
+}
+
+// logit of the reference's K_ij * scaling: -inf where K_ij underflows to 0 in fp64
+template <bool KNOPP>
+__device__ __forceinline__ double sk_term(double ua, double va, double c, double inv_eps,
+                                          double kclamp, double pot_minus_abs) {
+  const double k = KNOPP ? -c * inv_eps : ua + va - c * inv_eps;
+  if (k < kExpUnderflow) return -INFINITY;
+  return (KNOPP ? k : fmin(k, kclamp)) + pot_minus_abs;
+}
+
+// Row pass: f_out_i from g_in (one wave per row, 64-wide coalesced column sweep).
+template <typename T, bool KNOPP>
 __global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs a, SkDev d,
                                                 int it, int slot_in, int slot_out) {
   if (d.st[ST_DONE]) return;
   const int i = blockIdx.x * 4 + wave_id();
   if (i >= a.I) return;
   const int lane = lane_id();
-  const double* g = d.g + (int64_t)slot_in * a.J;
-  const double uai = d.ua[i];
-  const T* Ci = C + (int64_t)i * a.ldc;
+  const double* __restrict__ g = d.g + (int64_t)slot_in * a.J;
+  const double* __restrict__ va = d.va;
+  const double uai = KNOPP ? 0.0 : d.ua[i];
+  const T* __restrict__ Ci = C + (int64_t)i * a.ldc;
+  constexpr int CH = 4;
   Lse l;
   l.init();
-  for (int j = lane; j < a.J; j += 64) {
-    const double k = uai + d.va[j] - ld_c(Ci, j) * a.inv_eps;
-    if (k < kExpUnderflow) continue;  // K_ij == 0 in the reference's fp64 exp
-    l.add(fmin(k, a.kclamp) + g[j] - d.va[j]);
+  int j0 = 0;
+  for (; j0 + 64 * CH <= a.J; j0 += 64 * CH) {
+    double x[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int j = j0 + 64 * k + lane;
+      const double vj = KNOPP ? 0.0 : va[j];
+      x[k] = sk_term<KNOPP>(uai, vj, (double)Ci[j], a.inv_eps, a.kclamp, g[j] - vj);
+    }
+    lse_chunk<CH>(l, x);
+  }
+  for (int j = j0 + lane; j < a.J; j += 64) {
+    const double vj = KNOPP ? 0.0 : va[j];
+    const double x1[1] = {sk_term<KNOPP>(uai, vj, (double)Ci[j], a.inv_eps, a.kclamp, g[j] - vj)};
+    lse_chunk<1>(l, x1);
   }
   l = wave_lse(l);
   if (lane != 0) return;
   const double ls = l.value();
   double la = a.p_row * (a.la[i] - ls);
-  if (a.mode == GNNEA_SK_KNOPP) {
-    const double f = la;  // u = 1/(Kp v)
-    d.f[(int64_t)slot_out * a.I + i] = f;
-    if (!(f <= kExpOverflow)) mark_done(d.st, it, 2, (it + 1) & 1);  // u inf / NaN
+  if (KNOPP) {
+    d.f[(int64_t)slot_out * a.I + i] = la;  // u = 1/(Kp v)
+    if (!(la <= kExpOverflow)) mark_done(d.st, it, 2, (it + 1) & 1);  // u inf / NaN
   } else {
     if (la > kLn1e30) la = kLn1e30;  // a = clamp(., 0, 1e30)
     if (la > kLn1e20) atomicOr((unsigned long long*)&d.st[ST_BIG], 1ull);
@@ -172,8 +209,9 @@ __global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs 
   }
 }
 
-// Column pass: partial (max, sumexp) of x_ij over a row split, for a 64-column strip.
-template <typename T>
+// Column pass: partial (max, sumexp) over a row split, for a 64-column strip; the 4 waves of
+// the workgroup interleave rows and merge through LDS.
+template <typename T, bool KNOPP>
 __global__ __launch_bounds__(256) void k_sk_col(const T* __restrict__ C, SkArgs a, SkDev d,
                                                 int slot_f, int rows_per_split) {
   if (d.st[ST_DONE]) return;
@@ -183,15 +221,30 @@ __global__ __launch_bounds__(256) void k_sk_col(const T* __restrict__ C, SkArgs 
   const int split = blockIdx.y;
   const int r0 = split * rows_per_split;
   const int r1 = min(a.I, r0 + rows_per_split);
-  const double* f = d.f + (int64_t)slot_f * a.I;
+  const double* __restrict__ f = d.f + (int64_t)slot_f * a.I;
+  const double* __restrict__ ua = d.ua;
+  constexpr int CH = 4;
   Lse l;
   l.init();
   if (j < a.J) {
-    const double vaj = d.va[j];
-    for (int i = r0 + w; i < r1; i += 4) {
-      const double k = d.ua[i] + vaj - ld_c(C, (int64_t)i * a.ldc + j) * a.inv_eps;
-      if (k < kExpUnderflow) continue;
-      l.add(fmin(k, a.kclamp) + f[i] - d.ua[i]);
+    const double vaj = KNOPP ? 0.0 : d.va[j];
+    int i0 = r0 + w;
+    for (; i0 + 4 * (CH - 1) < r1; i0 += 4 * CH) {
+      double x[CH];
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int i = i0 + 4 * k;
+        const double ui = KNOPP ? 0.0 : ua[i];
+        x[k] = sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps, a.kclamp,
+                              f[i] - ui);
+      }
+      lse_chunk<CH>(l, x);
+    }
+    for (int i = i0; i < r1; i += 4) {
+      const double ui = KNOPP ? 0.0 : ua[i];
+      const double x1[1] = {sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps,
+                                           a.kclamp, f[i] - ui)};
+      lse_chunk<1>(l, x1);
     }
   }
   sm[w][lane] = l.m;
@@ -464,12 +517,14 @@ static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t 
   for (int it = first; it < first + count; ++it) {
     const int cur = it & 1, prev = (it + 1) & 1;
     if (p->mode == GNNEA_SK_KNOPP) {
-      hipLaunchKernelGGL(k_sk_col<T>, gcol, dim3(256), 0, s, C, a, d, prev, rows_per_split);
+      hipLaunchKernelGGL((k_sk_col<T, true>), gcol, dim3(256), 0, s, C, a, d, prev,
+                         rows_per_split);
       hipLaunchKernelGGL(k_sk_combine, dim3(1), dim3(1024), 0, s, a, d, it, prev, cur);
-      hipLaunchKernelGGL(k_sk_row<T>, grow, dim3(256), 0, s, C, a, d, it, cur, cur);
+      hipLaunchKernelGGL((k_sk_row<T, true>), grow, dim3(256), 0, s, C, a, d, it, cur, cur);
     } else {
-      hipLaunchKernelGGL(k_sk_row<T>, grow, dim3(256), 0, s, C, a, d, it, prev, cur);
-      hipLaunchKernelGGL(k_sk_col<T>, gcol, dim3(256), 0, s, C, a, d, cur, rows_per_split);
+      hipLaunchKernelGGL((k_sk_row<T, false>), grow, dim3(256), 0, s, C, a, d, it, prev, cur);
+      hipLaunchKernelGGL((k_sk_col<T, false>), gcol, dim3(256), 0, s, C, a, d, cur,
+                         rows_per_split);
       hipLaunchKernelGGL(k_sk_combine, dim3(1), dim3(1024), 0, s, a, d, it, prev, cur);
       hipLaunchKernelGGL(k_sk_absorb_rows<T>, grow, dim3(256), 0, s, C, a, d, it, cur,
                          p->max_iter, 0);

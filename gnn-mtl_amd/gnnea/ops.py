@@ -253,17 +253,31 @@ def gat_scores(H, a_all, heads, d_head):
     return s1, s2
 
 
+def _pad4(t, D):
+    """[N, roundup4(D)] 16-B aligned row-major tensor whose first D columns are t (the GAT
+    kernels move 16 B per lane); t itself when it already qualifies."""
+    Dp = (D + 3) // 4 * 4
+    if (t.dtype == torch.float32 and t.stride(1) == 1 and t.stride(0) == Dp
+            and t.data_ptr() % 16 == 0
+            and (t.storage_offset() + t.shape[0] * Dp) * 4 <= t.untyped_storage().nbytes()):
+        return t
+    out = torch.zeros((t.shape[0], Dp), dtype=torch.float32, device=t.device)
+    out[:, :D] = t
+    return out
+
+
 class GATFn(torch.autograd.Function):
     """h'_i = sum_j softmax_j(-LeakyReLU(a·[h_i||h_j])) h_j for all heads at once
     (layers/att_layers.py:29-61 per head, concatenated at :86)."""
 
     @staticmethod
     def forward(ctx, H, a_all, csr, heads, d_head, alpha, act, edge_mask):
-        H = _f32c(H)
+        D = heads * d_head
+        H = _pad4(H, D)
         a_all = _f32c(a_all)
         N = csr.n_rows
         s1, s2 = gat_scores(H, a_all, heads, d_head)
-        Y = torch.empty((N, heads * d_head), dtype=torch.float32, device=H.device)
+        Y = torch.empty((N, (D + 3) // 4 * 4), dtype=torch.float32, device=H.device)
         m = torch.empty((N, heads), dtype=torch.float32, device=H.device)
         den = torch.empty_like(m)
         em = _f32c(edge_mask) if edge_mask is not None else None
@@ -276,7 +290,7 @@ class GATFn(torch.autograd.Function):
         ctx.meta = (heads, d_head, float(alpha), int(act))
         ctx.save_for_backward(H, a_all, s1, s2, m, den, Y, em if em is not None else torch.empty(0))
         ctx.has_mask = em is not None
-        return Y
+        return Y if Y.shape[1] == D else Y[:, :D]
 
     @staticmethod
     def backward(ctx, dY):
@@ -285,9 +299,12 @@ class GATFn(torch.autograd.Function):
         em = em if ctx.has_mask else None
         csr = ctx.csr
         csrT = csr.transpose()
-        dY = _f32c(dY)
+        D = heads * d_head
+        dY = _pad4(dY.float(), D)
+        if dY.shape[1] != Y.shape[1]:
+            dY = _pad4(dY[:, :D].contiguous(), D)
         # G = dL/dh' ; P = h' (relu / identity: Y itself is a valid stand-in for c = G·h')
-        G = dY if act == _lib.GNNEA_ACT_IDENTITY else act_bwd(dY, Y, act)
+        G = dY if act == _lib.GNNEA_ACT_IDENTITY else act_bwd(dY.contiguous(), Y, act)
         N = csr.n_rows
         dz = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=H.device)
         ds1 = torch.empty((N, heads), dtype=torch.float32, device=H.device)
@@ -307,11 +324,11 @@ class GATFn(torch.autograd.Function):
         da = None
         if ctx.needs_input_grad[1]:
             # da1[h] = sum_i ds1[i,h] H_i,h ; da2[h] = sum_j ds2[j,h] H_j,h   (MFMA, split-K)
-            p1 = gemm(ds1, H, trans_a=True).view(heads, heads, d_head)
-            p2 = gemm(ds2, H, trans_a=True).view(heads, heads, d_head)
+            p1 = gemm(ds1, H[:, :D], trans_a=True).view(heads, heads, d_head)
+            p2 = gemm(ds2, H[:, :D], trans_a=True).view(heads, heads, d_head)
             idx = torch.arange(heads, device=H.device)
             da = torch.cat([p1[idx, idx], p2[idx, idx]], dim=1)
-        return dH, da, None, None, None, None, None, None
+        return (dH if dH.shape[1] == D else dH[:, :D]), da, None, None, None, None, None, None
 
 
 def gat(adj, H, a_all, heads, d_head, alpha, act_fn, edge_mask=None):

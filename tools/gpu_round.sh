@@ -25,6 +25,7 @@ for s in $steps; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) run bench 600 python bench.py ;;
+    micro) run microbench 600 python tools/microbench.py ;;
     prof)
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
           --output-format csv -- python "$ROOT/bench.py" --steps 10 --warmup 2 \

@@ -1,0 +1,152 @@
+"""Per-kernel timings of the hot path at the cfg-4 scale (HIP events, median of reps).
+
+    python tools/microbench.py [--n 1000000] [--reps 10] [--out gpurun_out/microbench.json]
+
+Reports ms and the roofline-relevant rate of: CSR SpMM (gather model GB/s), HighWay SpMM
+epilogue, MFMA f32 projection GEMM (TFLOP/s), GAT forward / backward (4 heads x 75), a GCN layer
+forward+backward through the drop-in module, and Sinkhorn per-iteration time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gnn-mtl_amd"))
+sys.path.insert(0, ROOT)
+
+from gnnea import _lib, ops, synth  # noqa: E402
+from gnnea.graph import DeviceCSR  # noqa: E402
+
+
+def timeit(fn, reps, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1000000)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "microbench.json"))
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    n = args.n
+    t = 10 * n
+    t0 = time.time()
+    tr = synth.kg_pair_triples(n, t, 3000)
+    r, c, v = synth.adjacency_coo(tr, 2 * n, reference_order=False)
+    N = 2 * n
+    csr = DeviceCSR.from_coo(torch.from_numpy(r.astype(np.int32)).to(dev),
+                             torch.from_numpy(c.astype(np.int32)).to(dev),
+                             torch.from_numpy(v).to(dev), N, N)
+    E = csr.nnz
+    csr.transpose()
+    print("graph N=%d E=%d built in %.1fs" % (N, E, time.time() - t0), file=sys.stderr)
+    D = 300
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(N, D, device=dev, generator=g)
+    X /= X.norm(dim=1, keepdim=True)
+    res = {"N": N, "E": E, "D": D}
+    only = set(args.only.split(",")) if args.only else None
+
+    def want(k):
+        return only is None or k in only
+
+    gather = 4 * (N + 1) + 8 * E + 4 * E * D + 4 * N * D
+    if want("spmm"):
+        Y = torch.empty_like(X)
+        ms = timeit(lambda: ops.spmm(csr, X, _lib.GNNEA_ACT_RELU, out=Y), args.reps)
+        res["spmm_relu"] = {"ms": ms, "GBps_gather_model": gather / ms / 1e6,
+                            "edges_per_s": E / ms * 1e3}
+    if want("highway"):
+        G = torch.randn(N, D, device=dev, generator=g)
+        Wg = torch.zeros(D, device=dev)
+        csr_obj = csr
+
+        def hw():
+            return ops.HighwayFn.apply(X, G, X, Wg, csr_obj, _lib.GNNEA_ACT_RELU)
+        ms = timeit(hw, args.reps)
+        b = gather + 2 * 4 * N * D + 2 * 4 * N * D  # + gate, resid reads, S/g saves
+        res["highway_fwd"] = {"ms": ms, "GBps_model": b / ms / 1e6}
+    if want("gemm"):
+        W = torch.randn(D, D, device=dev, generator=g) * 0.05
+        bvec = torch.zeros(D, device=dev)
+        ms = timeit(lambda: ops.gemm(X, W, trans_b=True, bias=bvec), args.reps)
+        res["gemm_xWt"] = {"ms": ms, "TFLOPs": 2.0 * N * D * D / ms / 1e9}
+        dY = torch.randn(N, D, device=dev, generator=g)
+        ms = timeit(lambda: ops.gemm(dY, X, trans_a=True), args.reps)
+        res["gemm_dW_splitK"] = {"ms": ms, "TFLOPs": 2.0 * N * D * D / ms / 1e9}
+        ms = timeit(lambda: torch.mm(X, W.t()), args.reps)
+        res["torch_mm_xWt_hipblaslt"] = {"ms": ms, "TFLOPs": 2.0 * N * D * D / ms / 1e9}
+    if want("gat"):
+        heads, dh = 4, 75
+        a_all = torch.randn(heads, 2 * dh, device=dev, generator=g) * 0.1
+        H = X.clone().requires_grad_(True)
+        a_all.requires_grad_(True)
+        adj_csr = csr
+
+        def fwd():
+            return ops.GATFn.apply(H, a_all, adj_csr, heads, dh, 0.2, _lib.GNNEA_ACT_RELU, None)
+        ms = timeit(fwd, args.reps)
+        b = 4 * (N + 1) + E * (4 + 4 * D + 4 * heads) + N * (4 * D + 8 * heads)
+        res["gat_fwd"] = {"ms": ms, "GBps_model": b / ms / 1e6, "head_edges_per_s":
+                          heads * E / ms * 1e3}
+        y = fwd()
+        dy = torch.randn_like(y)
+        ms = timeit(lambda: torch.autograd.grad(y, (H, a_all), dy, retain_graph=True),
+                    max(3, args.reps // 2), warm=1)
+        res["gat_bwd"] = {"ms": ms}
+    if want("gcn_layer"):
+        from layers.layers import GraphConvolution
+        idx = torch.stack([torch.from_numpy(r), torch.from_numpy(c)]).to(dev)
+        adj = torch.sparse_coo_tensor(idx, torch.from_numpy(v).to(dev), (N, N))
+        torch.manual_seed(0)
+        layer = GraphConvolution(D, D, 0.0, F.relu, True).to(dev)
+        xg = X.clone().requires_grad_(True)
+
+        def fb():
+            out, _ = layer((xg, adj))
+            out.backward(torch.ones_like(out))
+        ms = timeit(fb, max(3, args.reps // 2), warm=1)
+        res["gcn_layer_fwd_bwd"] = {"ms": ms}
+    if want("sinkhorn"):
+        from gnnea.sinkhorn import solve
+        B = 3000
+        M = torch.rand(B, B, device=dev, generator=g)
+        la = torch.zeros(B, dtype=torch.float64, device=dev)
+        for name, mode, C in (("knopp_f32C", _lib.GNNEA_SK_KNOPP, M),
+                              ("stab_f64C", _lib.GNNEA_SK_STAB, M.double())):
+            ts = []
+            for it in (50, 550):
+                solve(mode, C, la, la, 0.01, -1.0, it, want_plan=False, batch=100)
+                torch.cuda.synchronize()
+                s = time.perf_counter()
+                solve(mode, C, la, la, 0.01, -1.0, it, want_plan=False, batch=100)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - s)
+            res["sinkhorn_" + name] = {"us_per_iter": (ts[1] - ts[0]) / 500 * 1e6}
+    print(json.dumps(res, indent=1))
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    json.dump(res, open(args.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
