@@ -28,8 +28,8 @@ constexpr double kLnTrueMin = -744.4400719213812;     // log(DBL_TRUE_MIN)
 constexpr double kExpOverflow = 709.782712893384;     // exp(x) == inf above
 
 struct SkWs {
-  int64_t f, g, ua, va, part_m, part_s, rowbuf, total;
-  int ns;
+  int64_t f, g, ua, va, part_m, part_s, rowbuf, errpart, total;
+  int ns, ncb;
 };
 
 static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
@@ -55,6 +55,8 @@ static SkWs sk_plan(int I, int J) {
   w.part_m = o; o = al256(o + 8ll * w.ns * J);
   w.part_s = o; o = al256(o + 8ll * w.ns * J);
   w.rowbuf = o; o = al256(o + 8ll * I);
+  w.ncb = (J + 255) / 256;
+  w.errpart = o; o = al256(o + 8ll * w.ncb);
   w.total = o;
   return w;
 }
@@ -62,8 +64,8 @@ static SkWs sk_plan(int I, int J) {
 struct SkDev {
   int64_t* st;   // status ints
   double* sd;    // status doubles (sd[8] ...)
-  double *f, *g, *ua, *va, *pm, *ps, *rowbuf;
-  int ns;
+  double *f, *g, *ua, *va, *pm, *ps, *rowbuf, *errpart;
+  int ns, ncb;
 };
 
 static SkDev sk_dev(const gnnea_sinkhorn* p) {
@@ -79,7 +81,9 @@ static SkDev sk_dev(const gnnea_sinkhorn* p) {
   d.pm = (double*)(b + w.part_m);
   d.ps = (double*)(b + w.part_s);
   d.rowbuf = (double*)(b + w.rowbuf);
+  d.errpart = (double*)(b + w.errpart);
   d.ns = w.ns;
+  d.ncb = w.ncb;
   return d;
 }
 
@@ -169,6 +173,27 @@ template <typename T, bool KNOPP>
 __global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs a, SkDev d,
                                                 int it, int slot_in, int slot_out) {
   if (d.st[ST_DONE]) return;
+  if (KNOPP) {
+    // decisions of the reference loop, in its order (utils/ot_loss.py:50-72): the err test of
+    // iterate it-1 (when (it-1)%10 == 0), then the K^T u == 0 / inf / NaN break of iteration it
+    // flagged by this iteration's column combine.  Every workgroup takes the same decision.
+    const int prev = it - 1;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    if (prev >= 0 && prev % 10 == 0) {
+      double e = 0.0;
+      for (int b = 0; b < d.ncb; ++b) e += d.errpart[b];
+      const double err = sqrt(e);
+      if (lead) d.sd[SD_ERR] = err;
+      if (!(err > d.sd[11])) {  // sd[11] = stopThr: the loop runs while err > stopThr
+        if (lead) mark_done(d.st, prev + 1, 1, prev & 1);
+        return;
+      }
+    }
+    if (d.st[ST_FAIL]) {
+      if (lead) mark_done(d.st, it, 2, (it + 1) & 1);
+      return;
+    }
+  }
   const int i = blockIdx.x * 4 + wave_id();
   if (i >= a.I) return;
   const int lane = lane_id();
@@ -257,60 +282,44 @@ __global__ __launch_bounds__(256) void k_sk_col(const T* __restrict__ C, SkArgs 
   }
 }
 
-// Column combine (single workgroup of 1024): column LSE -> g, KNOPP err / break checks,
-// STAB big-b flag.
-__global__ __launch_bounds__(1024) void k_sk_combine(SkArgs a, SkDev d, int it, int slot_g_prev,
-                                                     int slot_g_out) {
+// Column combine: one thread per column merges the row-split partials into the column LSE and
+// updates g; KNOPP also produces per-workgroup partial sums of err^2 and the break flag (decided
+// by the next row pass), STAB modes the max(b) > 1e20 absorption flag.
+template <bool KNOPP>
+__global__ __launch_bounds__(256) void k_sk_combine(SkArgs a, SkDev d, int it, int slot_g_prev,
+                                                    int slot_g_out) {
   if (d.st[ST_DONE]) return;
-  __shared__ double red[1024];
-  __shared__ int fail_s;
-  if (threadIdx.x == 0) fail_s = 0;
-  __syncthreads();
-  const double* gp = d.g + (int64_t)slot_g_prev * a.J;
-  double* go = d.g + (int64_t)slot_g_out * a.J;
+  __shared__ double red[4];
+  const int j = blockIdx.x * 256 + threadIdx.x;
   double errp = 0.0;
-  int fail = 0, big = 0;
-  for (int j = threadIdx.x; j < a.J; j += 1024) {
+  bool fail = false, big = false;
+  if (j < a.J) {
     Lse l;
     l.init();
     for (int s = 0; s < d.ns; ++s) l.merge(d.pm[(int64_t)s * a.J + j], d.ps[(int64_t)s * a.J + j]);
     const double ls = l.value();
-    if (a.mode == GNNEA_SK_KNOPP) {
-      // err of the previous iteration: v_{k-1} * (K^T u_{k-1}) - b
-      const double t = exp(gp[j] + ls) - exp(a.lb[j]);
-      errp += t * t;
-      if (!(ls >= kLnTrueMin)) fail = 1;  // K^T u == 0 (or NaN)
+    if (KNOPP) {
+      // err of the previous iterate: v_{k-1} * (K^T u_{k-1}) - b    (utils/ot_loss.py:65-66)
+      const double t = exp(d.g[(int64_t)slot_g_prev * a.J + j] + ls) - exp(a.lb[j]);
+      errp = t * t;
+      fail = !(ls >= kLnTrueMin);  // K^T u == 0 (or NaN)     (:57)
       const double gj = a.lb[j] - ls;
-      if (!(gj <= kExpOverflow)) fail = 1;  // v inf / NaN
-      go[j] = gj;
+      fail = fail || !(gj <= kExpOverflow);  // v inf / NaN   (:58-59)
+      d.g[(int64_t)slot_g_out * a.J + j] = gj;
     } else {
       double lb = a.p_col * (a.lb[j] - ls);
       if (lb > kLn1e30) lb = kLn1e30;
-      if (lb > kLn1e20) big = 1;
-      go[j] = d.va[j] + lb;
+      big = lb > kLn1e20;
+      d.g[(int64_t)slot_g_out * a.J + j] = d.va[j] + lb;
     }
   }
-  if (a.mode == GNNEA_SK_KNOPP) {
-    red[threadIdx.x] = errp;
-    if (fail) atomicOr(&fail_s, 1);
+  if (KNOPP) {
+    errp = wave_sum(errp);
+    if (lane_id() == 0) red[wave_id()] = errp;
+    if (__any(fail) && lane_id() == 0) atomicOr((unsigned long long*)&d.st[ST_FAIL], 1ull);
     __syncthreads();
-    for (int o = 512; o > 0; o >>= 1) {
-      if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      const int prev = it - 1;  // reference cpt of the iterate (f, g)[prev]
-      if (prev >= 0 && prev % 10 == 0) {
-        const double err = sqrt(red[0]);
-        d.sd[SD_ERR] = err;
-        if (!(err > d.sd[11])) {  // sd[11] = stopThr; loop runs while err > stopThr
-          mark_done(d.st, prev + 1, 1, prev & 1);
-          return;
-        }
-      }
-      if (fail_s) mark_done(d.st, it, 2, (it + 1) & 1);
-    }
-  } else if (big) {
+    if (threadIdx.x == 0) d.errpart[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  } else if (__any(big) && lane_id() == 0) {
     atomicOr((unsigned long long*)&d.st[ST_BIG], 2ull);
   }
 }
@@ -512,20 +521,20 @@ static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t 
   SkArgs a = sk_args(p);
   SkDev d = sk_dev(p);
   const int rows_per_split = (p->I + d.ns - 1) / d.ns;
-  const dim3 grow(div_up(p->I, 4)), gcol(div_up(p->J, 64), d.ns);
+  const dim3 grow(div_up(p->I, 4)), gcol(div_up(p->J, 64), d.ns), gcomb(d.ncb);
   const T* C = (const T*)p->C;
   for (int it = first; it < first + count; ++it) {
     const int cur = it & 1, prev = (it + 1) & 1;
     if (p->mode == GNNEA_SK_KNOPP) {
       hipLaunchKernelGGL((k_sk_col<T, true>), gcol, dim3(256), 0, s, C, a, d, prev,
                          rows_per_split);
-      hipLaunchKernelGGL(k_sk_combine, dim3(1), dim3(1024), 0, s, a, d, it, prev, cur);
+      hipLaunchKernelGGL(k_sk_combine<true>, gcomb, dim3(256), 0, s, a, d, it, prev, cur);
       hipLaunchKernelGGL((k_sk_row<T, true>), grow, dim3(256), 0, s, C, a, d, it, cur, cur);
     } else {
       hipLaunchKernelGGL((k_sk_row<T, false>), grow, dim3(256), 0, s, C, a, d, it, prev, cur);
       hipLaunchKernelGGL((k_sk_col<T, false>), gcol, dim3(256), 0, s, C, a, d, cur,
                          rows_per_split);
-      hipLaunchKernelGGL(k_sk_combine, dim3(1), dim3(1024), 0, s, a, d, it, prev, cur);
+      hipLaunchKernelGGL(k_sk_combine<false>, gcomb, dim3(256), 0, s, a, d, it, prev, cur);
       hipLaunchKernelGGL(k_sk_absorb_rows<T>, grow, dim3(256), 0, s, C, a, d, it, cur,
                          p->max_iter, 0);
       hipLaunchKernelGGL(k_sk_absorb_final, dim3(1), dim3(1024), 0, s, a, d, it, cur,

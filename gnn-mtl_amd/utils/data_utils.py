@@ -4,8 +4,14 @@ Only the functions that produce what the hot path consumes are mirrored here, ve
 numpy instead of the reference's per-triple dict loops (which take minutes at 20M triples):
 ``get_matrix``, ``get_sparse_tensor``, ``get_sparse_tensor_for_one_graph``,
 ``sparse_mx_to_torch_sparse_tensor``.  Entry order and fp32 values are bit-identical to the
-reference (tests/test_adjacency.py); the dataset file loaders are out of scope.
+reference (tests/test_adjacency.py).  When the reference's own ``utils/data_utils.py`` is
+importable further down ``sys.path`` its loaders (``load_data``, ``load_data_ea``, ...) are
+re-exported with these builders patched in, so ``run/train_ea.py`` gets the vectorised path.
 """
+import importlib.util
+import os
+import sys
+
 import numpy as np
 import scipy.sparse as sp
 import torch
@@ -52,3 +58,28 @@ def get_sparse_tensor_for_one_graph(e, KG, index_R):
         if k < n_raw:
             lut[k] = v
     return sp.coo_matrix((val.astype(np.float64), (lut[row], lut[col])), shape=(e, e))
+
+
+def _merge_upstream():
+    here = os.path.dirname(os.path.abspath(__file__))
+    for base in sys.path:
+        cand = os.path.join(os.path.abspath(base or "."), "utils", "data_utils.py")
+        if os.path.dirname(cand) == here or not os.path.exists(cand):
+            continue
+        try:
+            spec = importlib.util.spec_from_file_location("utils._upstream_data_utils", cand)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+        except Exception:  # upstream loaders need absent deps (torchtext): keep ours only
+            return
+        ours = {k: globals()[k] for k in ("sparse_mx_to_torch_sparse_tensor", "get_matrix",
+                                           "get_sparse_tensor", "get_sparse_tensor_for_one_graph")}
+        for k, v in vars(mod).items():
+            if not k.startswith("__") and k not in ours:
+                globals().setdefault(k, v)
+        for k, v in ours.items():
+            setattr(mod, k, v)
+        return
+
+
+_merge_upstream()
