@@ -39,6 +39,19 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(world):
+    """Per-launch HBM bytes of the SpMM from the committed rocprofv3 PMC summary (same workload,
+    N = 1; collected by tools/gpu_round.sh pmc + tools/pmc_summary.py)."""
+    if world != 1:
+        return None, None
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_spmm_pmc.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d["traffic_bytes"], os.path.relpath(files[-1], ROOT)
+
+
 def gather_model_bytes(n_rows, nnz, d, elem=4):
     return 4 * (n_rows + 1) + 8 * nnz + elem * nnz * d + elem * n_rows * d
 
@@ -170,6 +183,7 @@ def main():
     if rank == 0:
         traffic = gather_model_bytes(shard.n_rows, shard.nnz, D)
         achieved = traffic / (kernel_ms * 1e-3) / 1e9
+        pmc_bytes, pmc_src = pmc_traffic(world)
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -184,7 +198,8 @@ def main():
                            2, shard.g)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "kernel": "gnnea::k_spmm_v4<relu,act,2>",
+                         "traffic": pmc_bytes, "traffic_source": pmc_src,
+                         "kernel": "gnnea::k_spmm_v4<relu,act,2>",
                          "kernel_ms": round(kernel_ms, 4),
                          "bytes_per_launch": int(traffic),
                          "model": "gather: 4(N+1)+8E+4ED+4ND (rank 0 shard)"},
