@@ -3,11 +3,14 @@
 // torch.spmm(x, kernel_gate) (layers/layers.py:69), forward and backward.
 //
 // v_mfma_f32_32x32x2_f32 (gfx950: exact f32, bit-for-bit a k-ordered fmaf chain; 64 FLOP per
-// clock per SIMD).  Geometry: 256-thread workgroup = 4 waves in 2x2, block tile 128x128,
-// BK = 32, each wave 64x64 = 2x2 MFMA tiles of 32x32 (64 accumulator VGPRs).  Operand tiles
-// are staged k-major in LDS ([BK][128+1] floats: column reads by 32 consecutive lanes are
-// conflict-free, the +1 pad breaks the transposing writes' bank collisions); the next K-tile
-// is prefetched into registers while the current one feeds the MFMAs (async-stage split).
+// clock per SIMD).  The feature projections here are tall and thin (M = 2M nodes, N = K = 300),
+// so the block tile spans the whole output width: BM = 64 rows x BN = 64*WT columns (WT = 5 ->
+// 320 >= 300, one column tile, X streamed from HBM exactly once), BK = 16.  4 waves in 2x2, each
+// wave 32 x 32*WT = WT accumulator tiles.  Operand tiles are staged in double-buffered LDS in the
+// layout their global rows already have (no transposes): an operand that is contiguous along K
+// is kept [row][BK+1] (the +1 makes the 32 lanes' column reads hit 32 banks), one contiguous along
+// M/N is kept [k][64*WT+4] and written with 16-B stores.  Next tile's global loads are issued into
+// registers before the MFMAs of the current one (one barrier per K step).
 // Large-K / small-output products (weight gradients, K = N_nodes) split K over workgroups into
 // fp32 slabs reduced in fixed order by a second kernel: deterministic, no atomics.
 #include "common.h"
@@ -16,120 +19,155 @@ namespace gnnea {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 128, BN = 128, BK = 32, LDT = 129;
+constexpr int GBM = 64, GBK = 16;
 
-template <int TA, int TB>
-__global__ __launch_bounds__(256, 2) void k_gemm_f32(int M, int N, int K, const float* __restrict__ A,
-                                                     int64_t lda, const float* __restrict__ B,
-                                                     int64_t ldb, const float* __restrict__ bias,
-                                                     float beta, float* __restrict__ C, int64_t ldc,
-                                                     int k_per_split, float* __restrict__ slab,
-                                                     int tiles_n) {
-  __shared__ float As[BK * LDT];
-  __shared__ float Bs[BK * LDT];
-  const int tiles = gridDim.x;
-  const int t_id = xcd_remap(blockIdx.x, tiles);
+// LDS geometry of one operand tile: ROWS x GBK with K contiguous ("rk") or K-major ("kr").
+template <bool K_CONTIG, int ROWS>
+struct Tile {
+  static constexpr int LD = K_CONTIG ? GBK + 1 : ROWS + 4;
+  static constexpr int SIZE = K_CONTIG ? ROWS * LD : GBK * LD;
+  __device__ static int at(int row, int k) { return K_CONTIG ? row * LD + k : k * LD + row; }
+};
+
+// Load a ROWS x GBK tile of op(X) into registers. op(X)[row][k] = X[row][k] (K_CONTIG) or
+// X[k][row]; rows >= nrows or k >= kend read as 0.  VEC: 16-B loads (ld % 4 == 0, aligned).
+template <bool K_CONTIG, int ROWS, bool VEC>
+struct Loader {
+  static constexpr int NV = ROWS * GBK / 4 / 256;  // float4 per thread (ROWS multiple of 64)
+  float4 r[NV];
+  __device__ void load(const float* __restrict__ X, int64_t ld, int row0, int nrows, int k0,
+                       int kend, int tid) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int idx = tid + 256 * q;
+      int row, k;
+      if (K_CONTIG) { row = idx / (GBK / 4); k = (idx % (GBK / 4)) * 4; }
+      else { k = idx / (ROWS / 4); row = (idx % (ROWS / 4)) * 4; }
+      const int gr = row0 + row, gk = k0 + k;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (VEC) {
+        if (K_CONTIG) {
+          if (gr < nrows && gk < kend) v = *(const float4*)(X + (int64_t)gr * ld + gk);
+        } else {
+          if (gk < kend && gr < nrows) v = *(const float4*)(X + (int64_t)gk * ld + gr);
+        }
+      } else {
+        float t[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = K_CONTIG ? gr : gr + e, kk = K_CONTIG ? gk + e : gk;
+          t[e] = (rr < nrows && kk < kend)
+                     ? (K_CONTIG ? X[(int64_t)rr * ld + kk] : X[(int64_t)kk * ld + rr])
+                     : 0.f;
+        }
+        v = make_float4(t[0], t[1], t[2], t[3]);
+      }
+      r[q] = v;
+    }
+  }
+  __device__ void store(float* __restrict__ S, int tid) const {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int idx = tid + 256 * q;
+      if (K_CONTIG) {
+        const int row = idx / (GBK / 4), k = (idx % (GBK / 4)) * 4;
+        float* p = S + Tile<true, ROWS>::at(row, k);
+        p[0] = r[q].x; p[1] = r[q].y; p[2] = r[q].z; p[3] = r[q].w;
+      } else {
+        const int k = idx / (ROWS / 4), row = (idx % (ROWS / 4)) * 4;
+        *(float4*)(S + Tile<false, ROWS>::at(row, k)) = r[q];
+      }
+    }
+  }
+};
+
+template <int TA, int TB, int WT, bool VEC>
+__global__ __launch_bounds__(256) void k_gemm_wide(int M, int N, int K, const float* __restrict__ A,
+                                                   int64_t lda, const float* __restrict__ B,
+                                                   int64_t ldb, const float* __restrict__ bias,
+                                                   float beta, float* __restrict__ C,
+                                                   int64_t ldc, int k_per_split,
+                                                   float* __restrict__ slab, int tiles_n) {
+  constexpr int BN = 64 * WT;
+  constexpr bool AK = TA == 0, BK_ = TB == 1;  // operand contiguous along K?
+  using TA_ = Tile<AK, GBM>;
+  using TB_ = Tile<BK_, BN>;
+  __shared__ float smem[2 * (TA_::SIZE + TB_::SIZE)];
+  // buffer b of A at smem + b*SIZE_A, of B at smem + 2*SIZE_A + b*SIZE_B
+  auto As = [&](int b) { return smem + b * TA_::SIZE; };
+  auto Bs = [&](int b) { return smem + 2 * TA_::SIZE + b * TB_::SIZE; };
+
+  const int t_id = xcd_remap(blockIdx.x, gridDim.x);
   const int bn = t_id % tiles_n, bm = t_id / tiles_n;
-  const int m0 = bm * BM, n0 = bn * BN;
+  const int m0 = bm * GBM, n0 = bn * BN;
   const int split = blockIdx.y;
   const int kb = split * k_per_split;
   const int ke = min(K, kb + k_per_split);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
-
-  float ra[16], rb[16];
-  // load op(A)[m0:m0+128, k0:k0+32] and op(B)[k0:k0+32, n0:n0+128] into registers
-  auto load_tile = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      int m, k;
-      if (TA == 0) { k = tid & 31; m = (tid >> 5) + 8 * q; }
-      else { m = tid & 127; k = (tid >> 7) + 2 * q; }
-      const int gm = m0 + m, gk = k0 + k;
-      float v = 0.f;
-      if (gm < M && gk < ke) v = TA == 0 ? A[(int64_t)gm * lda + gk] : A[(int64_t)gk * lda + gm];
-      ra[q] = v;
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      int n, k;
-      if (TB == 0) { n = tid & 127; k = (tid >> 7) + 2 * q; }
-      else { k = tid & 31; n = (tid >> 5) + 8 * q; }
-      const int gn = n0 + n, gk = k0 + k;
-      float v = 0.f;
-      if (gn < N && gk < ke) v = TB == 0 ? B[(int64_t)gk * ldb + gn] : B[(int64_t)gn * ldb + gk];
-      rb[q] = v;
-    }
-  };
-  auto store_tile = [&]() {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      int m, k;
-      if (TA == 0) { k = tid & 31; m = (tid >> 5) + 8 * q; }
-      else { m = tid & 127; k = (tid >> 7) + 2 * q; }
-      As[k * LDT + m] = ra[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      int n, k;
-      if (TB == 0) { n = tid & 127; k = (tid >> 7) + 2 * q; }
-      else { k = tid & 31; n = (tid >> 5) + 8 * q; }
-      Bs[k * LDT + n] = rb[q];
-    }
-  };
-
   const int kh = lane >> 5, li = lane & 31;
-  if (kb < ke) {
-    load_tile(kb);
-    for (int k0 = kb; k0 < ke; k0 += BK) {
-      __syncthreads();  // previous tile fully consumed
-      store_tile();
-      __syncthreads();
-      if (k0 + BK < ke) load_tile(k0 + BK);  // in flight under the MFMAs
+
+  f32x16 acc[WT];
 #pragma unroll
-      for (int kk = 0; kk < BK; kk += 2) {
-        const float a0 = As[(kk + kh) * LDT + wm * 64 + li];
-        const float a1 = As[(kk + kh) * LDT + wm * 64 + 32 + li];
-        const float b0 = Bs[(kk + kh) * LDT + wn * 64 + li];
-        const float b1 = Bs[(kk + kh) * LDT + wn * 64 + 32 + li];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+  for (int t = 0; t < WT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  Loader<AK, GBM, VEC> la;
+  Loader<BK_, BN, VEC> lb;
+  const int nsteps = ke > kb ? (ke - kb + GBK - 1) / GBK : 0;
+  if (nsteps > 0) {
+    la.load(A, lda, m0, M, kb, ke, tid);
+    lb.load(B, ldb, n0, N, kb, ke, tid);
+    la.store(As(0), tid);
+    lb.store(Bs(0), tid);
+    __syncthreads();
+  }
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (more) {  // in flight under the MFMAs below
+      la.load(A, lda, m0, M, kb + (s + 1) * GBK, ke, tid);
+      lb.load(B, ldb, n0, N, kb + (s + 1) * GBK, ke, tid);
+    }
+    const float* a_s = As(cur);
+    const float* b_s = Bs(cur);
+#pragma unroll
+    for (int kk = 0; kk < GBK; kk += 2) {
+      const float a = a_s[TA_::at(wm * 32 + li, kk + kh)];
+#pragma unroll
+      for (int t = 0; t < WT; ++t) {
+        const float b = b_s[TB_::at(wn * 32 * WT + t * 32 + li, kk + kh)];
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
       }
     }
+    if (more) {
+      la.store(As(cur ^ 1), tid);
+      lb.store(Bs(cur ^ 1), tid);
+    }
+    __syncthreads();
   }
 
   // epilogue: 32x32 C/D map  col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < WT; ++t) {
+    const int col = n0 + wn * 32 * WT + t * 32 + li;
+    if (col >= N) continue;
+    const float bv = (bias && !slab) ? bias[col] : 0.f;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int col = n0 + wn * 64 + u * 32 + li;
-      if (col >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 64 + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        if (row >= M) continue;
-        const float v = acc[t][u][r];
-        if (slab) {
-          slab[((int64_t)split * M + row) * N + col] = v;
-        } else {
-          float o = v;
-          if (bias) o += bias[col];
-          if (beta != 0.f) o += beta * C[(int64_t)row * ldc + col];
-          C[(int64_t)row * ldc + col] = o;
-        }
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      if (row >= M) continue;
+      const float v = acc[t][r];
+      if (slab) {
+        slab[((int64_t)split * M + row) * N + col] = v;
+      } else {
+        float o = v + bv;
+        if (beta != 0.f) o += beta * C[(int64_t)row * ldc + col];
+        C[(int64_t)row * ldc + col] = o;
       }
     }
+  }
 }
 
 __global__ void k_gemm_reduce(int M, int N, int splits, const float* __restrict__ slab,
@@ -148,16 +186,49 @@ __global__ void k_gemm_reduce(int M, int N, int splits, const float* __restrict_
   }
 }
 
+static int pick_wt(int64_t N) {
+  const int64_t wt = (N + 63) / 64;
+  return (int)(wt < 1 ? 1 : (wt > 5 ? 5 : wt));
+}
+
 // split-K only when the output grid cannot fill the chip and K is long
 static int pick_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
-  const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  if (tiles >= 512 || K < 4 * BK) return 1;
-  int64_t s = (1024 + tiles - 1) / tiles;
-  const int64_t by_k = K / (4 * BK);
+  const int64_t bn = 64 * pick_wt(N);
+  const int64_t tiles = ((M + GBM - 1) / GBM) * ((N + bn - 1) / bn);
+  if (tiles >= 512 || K < 8 * GBK) return 1;
+  int64_t s = (768 + tiles - 1) / tiles;
+  const int64_t by_k = K / (8 * GBK);
   if (s > by_k) s = by_k;
   if (s > 256) s = 256;
   while (s > 1 && s * M * N * 4 > ws_bytes) --s;
   return (int)(s < 1 ? 1 : s);
+}
+
+static bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+
+template <int TA, int TB, int WT>
+static void launch_wt(dim3 grid, hipStream_t s, bool vec, int M, int N, int K, const float* A,
+                      int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
+                      float* C, int64_t ldc, int kps, float* slab, int tiles_n) {
+  if (vec)
+    hipLaunchKernelGGL((k_gemm_wide<TA, TB, WT, true>), grid, dim3(256), 0, s, M, N, K, A, lda, B,
+                       ldb, bias, beta, C, ldc, kps, slab, tiles_n);
+  else
+    hipLaunchKernelGGL((k_gemm_wide<TA, TB, WT, false>), grid, dim3(256), 0, s, M, N, K, A, lda,
+                       B, ldb, bias, beta, C, ldc, kps, slab, tiles_n);
+}
+
+template <int TA, int TB>
+static void launch_t(int wt, dim3 grid, hipStream_t s, bool vec, int M, int N, int K,
+                     const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
+                     float beta, float* C, int64_t ldc, int kps, float* slab, int tiles_n) {
+  switch (wt) {
+    case 1: launch_wt<TA, TB, 1>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n); break;
+    case 2: launch_wt<TA, TB, 2>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n); break;
+    case 3: launch_wt<TA, TB, 3>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n); break;
+    case 4: launch_wt<TA, TB, 4>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n); break;
+    default: launch_wt<TA, TB, 5>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n); break;
+  }
 }
 
 }  // namespace gnnea
@@ -181,20 +252,24 @@ extern "C" int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, in
     if ((trans_a ? lda < M : lda < K) || (trans_b ? ldb < K : ldb < N)) return GNNEA_EINVAL;
   }
   hipStream_t s = (hipStream_t)stream;
-  const int tiles_n = (int)((N + BN - 1) / BN);
-  const int tiles = (int)(((M + BM - 1) / BM) * tiles_n);
+  const int wt = pick_wt(N);
+  const int64_t bn = 64 * wt;
+  const int tiles_n = (int)((N + bn - 1) / bn);
+  const int tiles = (int)(((M + GBM - 1) / GBM) * tiles_n);
   const int splits = ws ? pick_splits(M, N, K, ws_bytes) : 1;
-  const int kps = (int)(((K + splits - 1) / splits + BK - 1) / BK * BK);
+  const int kps = (int)(((K + splits - 1) / splits + GBK - 1) / GBK * GBK);
   float* slab = splits > 1 ? (float*)ws : nullptr;
+  // 16-B loads need every float4 fully inside or fully outside the operand along its
+  // contiguous dimension and 16-B aligned rows
+  const int64_t a_contig = trans_a ? M : K, b_contig = trans_b ? K : N;
+  const bool vec = K > 0 && lda % 4 == 0 && ldb % 4 == 0 && a_contig % 4 == 0 &&
+                   b_contig % 4 == 0 && al16(A) && al16(B);
   const dim3 grid(tiles, splits);
-#define GNNEA_GEMM(TA, TB)                                                                      \
-  hipLaunchKernelGGL((k_gemm_f32<TA, TB>), grid, dim3(256), 0, s, (int)M, (int)N, (int)K, A, lda, \
-                     B, ldb, bias, beta, C, ldc, kps > 0 ? kps : BK, slab, tiles_n)
-  if (!trans_a && !trans_b) GNNEA_GEMM(0, 0);
-  else if (!trans_a && trans_b) GNNEA_GEMM(0, 1);
-  else if (trans_a && !trans_b) GNNEA_GEMM(1, 0);
-  else GNNEA_GEMM(1, 1);
-#undef GNNEA_GEMM
+  const int kk = kps > 0 ? kps : GBK;
+  if (!trans_a && !trans_b) launch_t<0, 0>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
+  else if (!trans_a && trans_b) launch_t<0, 1>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
+  else if (trans_a && !trans_b) launch_t<1, 0>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
+  else launch_t<1, 1>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
   GNNEA_LAUNCH_CHECK();
   if (splits > 1) {
     const int64_t n = M * N;
