@@ -118,6 +118,8 @@ def main():
     ap.add_argument("--n", type=int, default=synth.CONFIGS["cfg4"]["n"], help="entities per KG")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sinkhorn", action="store_true")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="multi-rank logic on ONE device with gloo (halo staged through host)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -125,10 +127,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    if args.rehearse:
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     t0 = time.time()
     n = args.n
@@ -141,21 +148,14 @@ def main():
     h_local /= h_local.norm(dim=1, keepdim=True)
     h_full = torch.empty(shard.n_cols, D, device=device) if shard.g > 1 else None
     y = torch.empty(shard.n_rows, D, device=device)
-    stream = torch.cuda.current_stream(device)
 
     def step(ev=None):
-        hf = shard.gather_halo(h_local, h_full)
-        if ev is not None:
-            ev[0].record(stream)
-        ops.spmm(shard.csr, hf, _lib.GNNEA_ACT_RELU, out=y)
-        if ev is not None:
-            ev[1].record(stream)
+        shard.aggregate(h_local, h_full, y, _lib.GNNEA_ACT_RELU, ev)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -166,9 +166,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if shard.g == 1:
+        kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    else:  # own-block + remote-block SpMM launches (the wait for the halo excluded)
+        kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3])
+                                   for e in evs]))
     stats = torch.tensor([elapsed, float(shard.nnz), kernel_ms], dtype=torch.float64,
-                         device=device)
+                         device="cpu" if args.rehearse else device)
     if world > 1:
         allst = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(allst, stats)

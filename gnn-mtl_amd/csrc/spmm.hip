@@ -29,6 +29,7 @@ struct HighwayArgs {
   float4* save_s;
   float4* save_g;
   int64_t lds4;
+  float beta;  // EPI_ACT: Y = act(A.X + beta*Y)  (partial aggregations, dist halo overlap)
 };
 
 template <int ACT>
@@ -107,6 +108,15 @@ __global__ __launch_bounds__(256) void k_spmm_v4(const int32_t* __restrict__ row
   for (int q = 0; q < NCH; ++q) {
     if (!own[q]) continue;
     const int c = lane + 64 * q;
+    if constexpr (EPI == EPI_ACT) {
+      if (hw.beta != 0.f) {
+        const float4 y = Y[(int64_t)row * ldy4 + c];
+        acc[q].x = fmaf(hw.beta, y.x, acc[q].x);
+        acc[q].y = fmaf(hw.beta, y.y, acc[q].y);
+        acc[q].z = fmaf(hw.beta, y.z, acc[q].z);
+        acc[q].w = fmaf(hw.beta, y.w, acc[q].w);
+      }
+    }
     float4 s = act4<ACT>(acc[q]);
     if constexpr (EPI == EPI_ACT) {
       Y[(int64_t)row * ldy4 + c] = s;
@@ -141,7 +151,8 @@ __global__ __launch_bounds__(256) void k_spmm_scalar(const int32_t* __restrict__
                                                      int64_t ldy, const float* gate_pre,
                                                      int64_t ldg, const float* bias,
                                                      const float* resid, int64_t ldr,
-                                                     float* save_s, float* save_g, int64_t lds) {
+                                                     float* save_s, float* save_g, int64_t lds,
+                                                     float beta) {
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const int row = blk * 4 + wave_id();
   if (row >= n_rows) return;
@@ -155,6 +166,7 @@ __global__ __launch_bounds__(256) void k_spmm_scalar(const int32_t* __restrict__
       if (c < D) acc = fmaf(val[e], X[(int64_t)j * ldx + c], acc);
     }
     if (c >= D) continue;
+    if (EPI == EPI_ACT && beta != 0.f) acc = fmaf(beta, Y[(int64_t)row * ldy + c], acc);
     const float s = act_fwd<ACT>(acc);
     if constexpr (EPI == EPI_ACT) {
       Y[(int64_t)row * ldy + c] = s;
@@ -175,7 +187,7 @@ template <int ACT, int EPI>
 static int launch_spmm(const int32_t* rowptr, const int32_t* col, const float* val, int n_rows,
                        int D, const float* X, int64_t ldx, float* Y, int64_t ldy,
                        const float* gate_pre, int64_t ldg, const float* bias, const float* resid,
-                       int64_t ldr, float* save_s, float* save_g, int64_t lds,
+                       int64_t ldr, float* save_s, float* save_g, int64_t lds, float beta,
                        hipStream_t stream) {
   const int nb = div_up(n_rows, 4);
   bool vec = (D % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) && al16(X) && al16(Y);
@@ -185,7 +197,7 @@ static int launch_spmm(const int32_t* rowptr, const int32_t* col, const float* v
   const int D4 = D / 4;
   if (vec && D4 <= 256) {
     HighwayArgs hw{(const float4*)gate_pre, ldg / 4, (const float4*)bias, (const float4*)resid,
-                   ldr / 4, (float4*)save_s, (float4*)save_g, lds / 4};
+                   ldr / 4, (float4*)save_s, (float4*)save_g, lds / 4, beta};
     const int nch = (D4 + 63) / 64;
 #define GNNEA_SPMM_CASE(N)                                                                     \
   case N:                                                                                      \
@@ -203,7 +215,7 @@ static int launch_spmm(const int32_t* rowptr, const int32_t* col, const float* v
   } else {
     hipLaunchKernelGGL((k_spmm_scalar<ACT, EPI>), dim3(nb), dim3(256), 0, stream, rowptr, col,
                        val, n_rows, D, X, ldx, Y, ldy, gate_pre, ldg, bias, resid, ldr, save_s,
-                       save_g, lds);
+                       save_g, lds, beta);
   }
   GNNEA_LAUNCH_CHECK();
   return 0;
@@ -214,11 +226,11 @@ static int dispatch_act(int act, const int32_t* rowptr, const int32_t* col, cons
                         int n_rows, int D, const float* X, int64_t ldx, float* Y, int64_t ldy,
                         const float* gate_pre, int64_t ldg, const float* bias,
                         const float* resid, int64_t ldr, float* save_s, float* save_g,
-                        int64_t lds, hipStream_t s) {
+                        int64_t lds, float beta, hipStream_t s) {
 #define GNNEA_ACT_CASE(A)                                                                     \
   case A:                                                                                     \
     return launch_spmm<A, EPI>(rowptr, col, val, n_rows, D, X, ldx, Y, ldy, gate_pre, ldg,    \
-                               bias, resid, ldr, save_s, save_g, lds, s);
+                               bias, resid, ldr, save_s, save_g, lds, beta, s);
   switch (act) {
     GNNEA_ACT_CASE(GNNEA_ACT_IDENTITY)
     GNNEA_ACT_CASE(GNNEA_ACT_RELU)
@@ -270,7 +282,19 @@ extern "C" int gnnea_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, con
   if (n_rows == 0 || D == 0) return 0;
   if (!rowptr || !col || !val || !X || !Y || ldx < D || ldy < D) return GNNEA_EINVAL;
   return dispatch_act<EPI_ACT>(act, rowptr, col, val, n_rows, D, X, ldx, Y, ldy, nullptr, 0,
-                               nullptr, nullptr, 0, nullptr, nullptr, 0, (hipStream_t)stream);
+                               nullptr, nullptr, 0, nullptr, nullptr, 0, 0.f, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_spmm_csr_beta_f32(const int32_t* rowptr, const int32_t* col,
+                                       const float* val, int32_t n_rows, int32_t D,
+                                       const float* X, int64_t ldx, float beta, float* Y,
+                                       int64_t ldy, int act, void* stream) {
+  if (n_rows < 0 || D < 0) return GNNEA_EINVAL;
+  if (n_rows == 0 || D == 0) return 0;
+  if (!rowptr || !col || !val || !X || !Y || ldx < D || ldy < D) return GNNEA_EINVAL;
+  return dispatch_act<EPI_ACT>(act, rowptr, col, val, n_rows, D, X, ldx, Y, ldy, nullptr, 0,
+                               nullptr, nullptr, 0, nullptr, nullptr, 0, beta,
+                               (hipStream_t)stream);
 }
 
 extern "C" int gnnea_spmm_highway_f32(const int32_t* rowptr, const int32_t* col,
@@ -285,7 +309,7 @@ extern "C" int gnnea_spmm_highway_f32(const int32_t* rowptr, const int32_t* col,
   if (ldx < D || ldy < D || ldg < D || ldr < D || ((save_s || save_g) && lds < D))
     return GNNEA_EINVAL;
   return dispatch_act<EPI_HIGHWAY>(act, rowptr, col, val, n_rows, D, X, ldx, Y, ldy, gate_pre,
-                                   ldg, bias_gate, resid, ldr, save_s, save_g, lds,
+                                   ldg, bias_gate, resid, ldr, save_s, save_g, lds, 0.f,
                                    (hipStream_t)stream);
 }
 

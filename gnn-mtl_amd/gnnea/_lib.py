@@ -66,6 +66,8 @@ SIGNATURES = {
     "gnnea_csr_expand_rows": (ctypes.c_int, [_p, _i32, _i64, _p, _p]),
     "gnnea_spmm_csr_f32": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64,
                                           ctypes.c_int, _p]),
+    "gnnea_spmm_csr_beta_f32": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _f32, _p, _i64,
+                                               ctypes.c_int, _p]),
     "gnnea_spmm_highway_f32": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64, _p, _p,
                                               _i64, _p, _i64, _p, _p, _i64, ctypes.c_int, _p]),
     "gnnea_act_bwd_f32": (ctypes.c_int, [_p, _p, _p, _i64, ctypes.c_int, _p]),

@@ -62,6 +62,13 @@ def shard_coo(triples, n, t, part):
     return r[keep] - part.row0, c[keep], v[keep]
 
 
+def split_own_remote(r, c, v, part):
+    """Entries whose source row is owned locally (columns re-based to the local rows) and the
+    rest (KG-local columns, read from the all-gathered halo)."""
+    own = (c >= part.row0) & (c < part.row1)
+    return (r[own], c[own] - part.row0, v[own]), (r[~own], c[~own], v[~own])
+
+
 def make_groups(part):
     """Both KG groups (every rank must create every group, in the same order)."""
     if part.world == 1:
@@ -70,16 +77,21 @@ def make_groups(part):
     return groups[part.kg]
 
 
-def halo_gather(h_local, h_full, group, group_size):
-    """All-gather the group's projected rows into h_full [group_size * rows, D]."""
+def halo_gather(h_local, h_full, group, group_size, async_op=False):
+    """All-gather the group's projected rows into h_full [group_size * rows, D].
+
+    RCCL: one all_gather_into_tensor (async_op=True returns the work so the caller can overlap
+    the locally owned part of the aggregation).  gloo (CPU rehearsal of the multi-rank logic):
+    synchronous, staged through host memory when the tensors live on a device."""
     if group_size == 1:
-        return h_local
-    if dist.get_backend(group) == "gloo":  # CPU rehearsal path
-        parts = list(h_full.chunk(group_size, dim=0))
-        dist.all_gather(parts, h_local.contiguous(), group=group)
-        return h_full
-    dist.all_gather_into_tensor(h_full, h_local, group=group)
-    return h_full
+        return None
+    if dist.get_backend(group) == "gloo":
+        hl = h_local.detach().cpu().contiguous()
+        parts = [torch.empty_like(hl) for _ in range(group_size)]
+        dist.all_gather(parts, hl, group=group)
+        h_full.copy_(torch.cat(parts))
+        return None
+    return dist.all_gather_into_tensor(h_full, h_local, group=group, async_op=async_op)
 
 
 class KGShard:
@@ -91,11 +103,20 @@ class KGShard:
         self.n, self.device = n, device
         triples = synth.kg_pair_triples(n, t, n_rel, seed=seed)
         r, c, v = shard_coo(triples, n, t, self.part)
-        self.csr = DeviceCSR.from_coo(torch.from_numpy(r.astype(np.int32)).to(device),
-                                      torch.from_numpy(c.astype(np.int32)).to(device),
-                                      torch.from_numpy(v).to(device), self.part.n_rows,
-                                      self.part.n_cols)
-        self.nnz = self.csr.nnz
+        self.nnz = int(r.size)
+
+        def up(rr, cc, vv, ncols):
+            return DeviceCSR.from_coo(torch.from_numpy(rr.astype(np.int32)).to(device),
+                                      torch.from_numpy(cc.astype(np.int32)).to(device),
+                                      torch.from_numpy(vv).to(device), self.part.n_rows, ncols)
+        if self.part.g == 1:
+            self.csr = up(r, c, v, self.part.n_cols)
+            self.csr_own = self.csr_remote = None
+        else:
+            (ro, co, vo), (rr, cr, vr) = split_own_remote(r, c, v, self.part)
+            self.csr = None
+            self.csr_own = up(ro, co, vo, self.part.n_rows)
+            self.csr_remote = up(rr, cr, vr, self.part.n_cols)
         self.group = make_groups(self.part)
 
     @property
@@ -110,5 +131,24 @@ class KGShard:
     def n_cols(self):
         return self.part.n_cols
 
-    def gather_halo(self, h_local, h_full):
-        return halo_gather(h_local, h_full, self.group, self.part.g)
+    def aggregate(self, h_local, h_full, out, act, events=None):
+        """out = act(A_shard · H) for this rank's rows; H's remote rows arrive by the halo
+        all-gather, overlapped with the aggregation over the locally owned rows."""
+        from . import ops
+        from ._lib import GNNEA_ACT_IDENTITY
+        rec = (lambda k: events[k].record()) if events is not None else (lambda k: None)
+        if self.part.g == 1:
+            rec(0)
+            ops.spmm(self.csr, h_local, act, out=out)
+            rec(1)
+            return out
+        work = halo_gather(h_local, h_full, self.group, self.part.g, async_op=True)
+        rec(0)
+        ops.spmm(self.csr_own, h_local, GNNEA_ACT_IDENTITY, out=out)
+        rec(1)
+        if work is not None:
+            work.wait()
+        rec(2)
+        ops.spmm(self.csr_remote, h_full, act, out=out, beta=1.0)
+        rec(3)
+        return out

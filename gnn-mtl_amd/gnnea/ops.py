@@ -136,18 +136,26 @@ def matmul(x, w):
 # ------------------------------------------------------------------------------------------ #
 # CSR aggregation                                                                              #
 # ------------------------------------------------------------------------------------------ #
-def spmm(csr, x, act=_lib.GNNEA_ACT_IDENTITY, out=None):
-    """out = act(A @ x) with the gather-model CSR kernel (gnnea_spmm_csr_f32)."""
+def spmm(csr, x, act=_lib.GNNEA_ACT_IDENTITY, out=None, beta=0.0):
+    """out = act(A @ x + beta*out) with the gather-model CSR kernel (gnnea_spmm_csr_*_f32)."""
     _lib.require_device(x)
-    x = _f32c(x)
-    if x.dim() != 2 or x.shape[0] != csr.n_cols:
+    if x.dtype != torch.float32 or x.stride(1) != 1:
+        x = x.float().contiguous()
+    if x.dim() != 2 or x.shape[0] < csr.n_cols:
         raise ValueError("gnnea.spmm: x must be [%d, D]" % csr.n_cols)
     if out is None:
         out = torch.empty((csr.n_rows, x.shape[1]), dtype=torch.float32, device=x.device)
+        beta = 0.0
     with torch.cuda.device(x.device):
-        check(_lib.lib().gnnea_spmm_csr_f32(
-            ptr(csr.rowptr), ptr(csr.col), ptr(csr.val), csr.n_rows, x.shape[1], ptr(x),
-            x.stride(0), ptr(out), out.stride(0), int(act), stream_of(x.device)))
+        if beta == 0.0:
+            check(_lib.lib().gnnea_spmm_csr_f32(
+                ptr(csr.rowptr), ptr(csr.col), ptr(csr.val), csr.n_rows, x.shape[1], ptr(x),
+                x.stride(0), ptr(out), out.stride(0), int(act), stream_of(x.device)))
+        else:
+            check(_lib.lib().gnnea_spmm_csr_beta_f32(
+                ptr(csr.rowptr), ptr(csr.col), ptr(csr.val), csr.n_rows, x.shape[1], ptr(x),
+                x.stride(0), float(beta), ptr(out), out.stride(0), int(act),
+                stream_of(x.device)))
     return out
 
 

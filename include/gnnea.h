@@ -73,6 +73,11 @@ int gnnea_csr_expand_rows(const int32_t* rowptr, int32_t n_rows, int64_t nnz, in
 int gnnea_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                        int32_t n_rows, int32_t D, const float* X, int64_t ldx, float* Y,
                        int64_t ldy, int act, void* stream);
+/* Y = act(A · X + beta · Y): partial aggregations over column blocks (the multi-GPU halo
+ * overlap sums the locally owned block while the remote rows are in flight). */
+int gnnea_spmm_csr_beta_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                            int32_t n_rows, int32_t D, const float* X, int64_t ldx, float beta,
+                            float* Y, int64_t ldy, int act, void* stream);
 
 /* a4. HighWay epilogue (layers/layers.py:64-76):
  *   S = act(A·X);  g = sigmoid(gate_pre + bias_gate);  Y = g*S + (1-g)*resid

@@ -28,7 +28,7 @@ def _worker(rank, world, port, n, t, q):
     sys.path.insert(0, os.path.join(root, "gnn-mtl_amd"))
     sys.path.insert(0, root)
     from gnnea import synth
-    from gnnea.dist import Partition, halo_gather, make_groups, shard_coo
+    from gnnea.dist import Partition, halo_gather, make_groups, shard_coo, split_own_remote
     from oracle.gnn import coo_aggregate
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -44,8 +44,14 @@ def _worker(rank, world, port, n, t, q):
         else:
             h_local = H[part.global_row0:part.global_row0 + part.n_rows]
         h_full = torch.empty(part.n_cols, 16, dtype=torch.float64)
-        hf = halo_gather(h_local, h_full, group, part.g)
-        y = coo_aggregate(r, c, v, part.n_rows, hf)
+        if part.g == 1:
+            y = coo_aggregate(r, c, v, part.n_rows, h_local)
+        else:
+            # the product's overlap split: owned block from h_local, the rest from the halo
+            (ro, co, vo), (rr, cr, vr) = split_own_remote(r, c, v, part)
+            y = coo_aggregate(ro, co, vo, part.n_rows, h_local)
+            halo_gather(h_local, h_full, group, part.g)
+            y = y + coo_aggregate(rr, cr, vr, part.n_rows, h_full)
         outs = [torch.empty_like(y) for _ in range(world)]
         dist.all_gather(outs, y)
         if rank == 0:

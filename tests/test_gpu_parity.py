@@ -305,3 +305,49 @@ def test_sinkhorn_vs_oracle_random(device):
         Po, lo, _, _ = osk.knopp(a, b, M, reg, 300)
         assert rel_err(P.cpu(), Po) < TOL64, (I, J)
         assert abs(loss.item() - lo) <= TOL64 * abs(lo)
+
+
+def test_spmm_beta_accumulate(device):
+    from gnnea import ops
+    from gnnea.graph import DeviceCSR
+    from oracle.gnn import coo_aggregate
+    rng = np.random.default_rng(5)
+    r, c, v = _random_coo(rng, 500, 500, 4000)
+    x = rng.standard_normal((500, 300)).astype(np.float32)
+    y0 = rng.standard_normal((500, 300)).astype(np.float32)
+    csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                             torch.from_numpy(v).to(device), 500, 500)
+    out = torch.from_numpy(y0).to(device)
+    ops.spmm(csr, torch.from_numpy(x).to(device), 1, out=out, beta=1.0)
+    ref = torch.relu(coo_aggregate(r, c, v, 500, torch.from_numpy(x).double()) +
+                     torch.from_numpy(y0).double())
+    assert rel_err(out.cpu(), ref) < TOL32
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_shard_own_remote_split_on_device(device, world):
+    """The multi-GPU aggregation (owned block from the local rows, the rest from the halo,
+    accumulated with beta = 1) reproduces the single-GPU rows, per rank, on one device."""
+    from gnnea import ops, synth
+    from gnnea.dist import Partition, shard_coo, split_own_remote
+    from gnnea.graph import DeviceCSR
+    n, t = 800, 3000
+    tr = synth.kg_pair_triples(n, t, 50)
+    H = torch.from_numpy(synth.features(2 * n, 300, seed=2)).to(device)
+    R, C, V = synth.adjacency_coo(tr, 2 * n, reference_order=False)
+    full = DeviceCSR.from_coo(torch.from_numpy(R).to(device), torch.from_numpy(C).to(device),
+                              torch.from_numpy(V).to(device), 2 * n, 2 * n)
+    ref = ops.spmm(full, H, 1).cpu()
+    for rank in range(world):
+        p = Partition(n, rank, world)
+        r, c, v = shard_coo(tr, n, t, p)
+        (ro, co, vo), (rr, cr, vr) = split_own_remote(r, c, v, p)
+        up = lambda a, b, w, nc: DeviceCSR.from_coo(  # noqa: E731
+            torch.from_numpy(a).to(device), torch.from_numpy(b).to(device),
+            torch.from_numpy(w).to(device), p.n_rows, nc)
+        h_kg = H[p.kg * n:(p.kg + 1) * n]
+        h_local = h_kg[p.row0:p.row1]
+        y = ops.spmm(up(ro, co, vo, p.n_rows), h_local, 0)
+        ops.spmm(up(rr, cr, vr, n), h_kg, 1, out=y, beta=1.0)
+        g0 = p.global_row0
+        assert rel_err(y.cpu(), ref[g0:g0 + p.n_rows]) < TOL32
