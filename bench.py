@@ -115,7 +115,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=synth.CONFIGS["cfg4"]["n"], help="entities per KG")
+    ap.add_argument("--entities", type=int, default=synth.CONFIGS["cfg4"]["n"],
+                    help="entities per KG (default: cfg-4, 1M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sinkhorn", action="store_true")
     ap.add_argument("--rehearse", action="store_true",
@@ -138,7 +139,7 @@ def main():
             dist.init_process_group("nccl", device_id=device)
 
     t0 = time.time()
-    n = args.n
+    n = args.entities
     shard = KGShard(n, shard_t(n), synth.CONFIGS["cfg4"]["n_rel"], rank, world, device)
     log("rank %d: shard rows %d nnz %d built in %.1fs" % (rank, shard.n_rows, shard.nnz,
                                                          time.time() - t0))
