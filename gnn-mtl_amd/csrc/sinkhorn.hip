@@ -4,7 +4,7 @@
 //   KNOPP (utils/ot_loss.py:5-76), f = log u, g = log v:
 //       g_j = log b_j - LSE_i(f_i - M_ij/reg)      (v = b / K^T u,   :53-54)
 //       f_i = log a_i - LSE_j(g_j - M_ij/reg)      (u = 1 / (K/a) v, :55)
-//     K_ij = exp(-M_ij/reg) underflows to 0 below -745.13 in fp64: such terms are dropped,
+//     K_ij = exp_f64(-M_ij/reg) underflows to 0 below -745.13 in fp64: such terms are dropped,
 //     K^T u == 0 (column LSE below ln(DBL_TRUE_MIN)) or inf/NaN u, v break the loop with the
 //     previous iterate (:57-62); err = ||v (K^T u) - b||_2 every 10th iteration (:64-66).
 //   STAB / GEN / RELAX (SinkhornOT/sinkhorn_loss.py:159-356), potentials in units of eps,
@@ -23,9 +23,9 @@ namespace gnnea {
 
 constexpr double kLn1e20 = 46.051701859880914;   // log(1e20)  (sinkhorn_loss.py:11 big)
 constexpr double kLn1e30 = 69.07755278982137;    // log(1e30)  (sinkhorn_loss.py:12 huge)
-constexpr double kExpUnderflow = -745.1332191019412;  // exp(x) == 0 in fp64 for x below
+constexpr double kExpUnderflow = -745.1332191019412;  // exp_f64(x) == 0 in fp64 for x below
 constexpr double kLnTrueMin = -744.4400719213812;     // log(DBL_TRUE_MIN)
-constexpr double kExpOverflow = 709.782712893384;     // exp(x) == inf above
+constexpr double kExpOverflow = 709.782712893384;     // exp_f64(x) == inf above
 
 struct SkWs {
   int64_t f, g, ua, va, part_m, part_s, rowbuf, errpart, total;
@@ -102,17 +102,17 @@ struct Lse {
   __device__ __forceinline__ void add(double x) {
     if (x == -INFINITY) return;
     if (x > m) {
-      s = s * exp(m - x) + 1.0;
+      s = s * exp_f64(m - x) + 1.0;
       m = x;
     } else {
-      s += exp(x - m);
+      s += exp_f64(x - m);
     }
   }
   __device__ __forceinline__ void merge(double m2, double s2) {
     if (m2 == -INFINITY) return;
     if (m == -INFINITY) { m = m2; s = s2; return; }
-    if (m2 > m) { s = s * exp(m - m2) + s2; m = m2; }
-    else s += s2 * exp(m2 - m);
+    if (m2 > m) { s = s * exp_f64(m - m2) + s2; m = m2; }
+    else s += s2 * exp_f64(m2 - m);
   }
   __device__ __forceinline__ double value() const { return m == -INFINITY ? -INFINITY : m + log(s); }
 };
@@ -152,9 +152,9 @@ __device__ __forceinline__ void lse_chunk(Lse& l, const double (&x)[CH]) {
   for (int k = 1; k < CH; ++k) cm = fmax(cm, x[k]);
   if (cm == -INFINITY) return;  // whole chunk masked (K == 0)
   const double nm = fmax(l.m, cm);
-  double acc = l.m == -INFINITY ? 0.0 : l.s * exp(l.m - nm);
+  double acc = l.m == -INFINITY ? 0.0 : l.s * exp_f64(l.m - nm);
 #pragma unroll
-  for (int k = 0; k < CH; ++k) acc += exp(x[k] - nm);  // exp(-inf) == 0
+  for (int k = 0; k < CH; ++k) acc += exp_f64(x[k] - nm);  // exp_f64(-inf) == 0
   l.m = nm;
   l.s = acc;
 }
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256) void k_sk_combine(SkArgs a, SkDev d, int it, i
     const double ls = l.value();
     if (KNOPP) {
       // err of the previous iterate: v_{k-1} * (K^T u_{k-1}) - b    (utils/ot_loss.py:65-66)
-      const double t = exp(d.g[(int64_t)slot_g_prev * a.J + j] + ls) - exp(a.lb[j]);
+      const double t = exp_f64(d.g[(int64_t)slot_g_prev * a.J + j] + ls) - exp_f64(a.lb[j]);
       errp = t * t;
       fail = !(ls >= kLnTrueMin);  // K^T u == 0 (or NaN)     (:57)
       const double gj = a.lb[j] - ls;
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void k_sk_absorb_rows(const T* __restrict__ C,
   for (int j = lane; j < a.J; j += 64) {
     const double c = ld_c(Ci, j);
     const double k = fmin(fi + (init ? 0.0 : g[j]) - c * a.inv_eps, a.kclamp);
-    acc += exp(k) * c;
+    acc += exp_f64(k) * c;
   }
   acc = wave_sum(acc);
   if (lane == 0) {
@@ -432,11 +432,11 @@ __global__ __launch_bounds__(256) void k_sk_plan(const T* __restrict__ C, SkArgs
     const double c = ld_c(Ci, j);
     double v;
     if (knopp) {
-      // P = u * K * v with K = exp(-M/reg) underflowing to 0 below -745.13
+      // P = u * K * v with K = exp_f64(-M/reg) underflowing to 0 below -745.13
       const double k = -c * a.inv_eps;
-      v = k < kExpUnderflow ? 0.0 : exp(fi + g[j] + k);
+      v = k < kExpUnderflow ? 0.0 : exp_f64(fi + g[j] + k);
     } else {
-      v = exp(fmin(fi + g[j] - c * a.inv_eps, a.kclamp));
+      v = exp_f64(fmin(fi + g[j] - c * a.inv_eps, a.kclamp));
     }
     if (plan) plan[(int64_t)i * ldp + j] = (P)v;
     rs += v;
@@ -464,9 +464,9 @@ __global__ __launch_bounds__(256) void k_sk_colsum(const T* __restrict__ C, SkAr
     const double c = ld_c(C, (int64_t)i * a.ldc + j);
     if (knopp) {
       const double k = -c * a.inv_eps;
-      s += k < kExpUnderflow ? 0.0 : exp(f[i] + gj + k);
+      s += k < kExpUnderflow ? 0.0 : exp_f64(f[i] + gj + k);
     } else {
-      s += exp(fmin(f[i] + gj - c * a.inv_eps, a.kclamp));
+      s += exp_f64(fmin(f[i] + gj - c * a.inv_eps, a.kclamp));
     }
   }
   col_sum[j] = s;
