@@ -13,10 +13,11 @@
 //       f_i = ua_i + min(p_row (log mu_i - log s_i), ln 1e30)                  (a = clamp((mu/s)^p))
 //     and symmetrically for g; absorption (ii%10==0, max(a|b) > 1e20, last iteration) sets
 //     ua = f, va = g and evaluates transport = sum K.C for the relative-tolerance break.
-// One iteration = row pass (one wave per row, coalesced 64-wide column sweep, online LSE with
-// one exp per element) + column pass (workgroup per 64-column strip x row split, partial
-// (max, sum) pairs) + single-workgroup combine (column LSE, update, err / flags).  A device
-// status block gates every kernel so iterations after the stop condition are no-ops.
+// One iteration = row pass (one wave per row, coalesced 64-wide column sweep, chunked online
+// LSE with 16 loads in flight per lane) + column pass fused with the column update (16 columns
+// x 64 row groups per 1024-thread workgroup, merged through LDS).  Both passes are latency- and
+// fp64-exp-bound at B = 3000 (C is L2 / Infinity-Cache resident).  A device status block gates
+// every kernel so iterations after the stop condition are no-ops.
 #include "common.h"
 
 namespace gnnea {
@@ -28,34 +29,23 @@ constexpr double kLnTrueMin = -744.4400719213812;     // log(DBL_TRUE_MIN)
 constexpr double kExpOverflow = 709.782712893384;     // exp_f64(x) == inf above
 
 struct SkWs {
-  int64_t f, g, ua, va, part_m, part_s, rowbuf, errpart, total;
-  int ns, ncb;
+  int64_t f, g, ua, va, rowbuf, errpart, total;
+  int ncb;
 };
 
 static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
-static int sk_nsplit(int I, int J) {
-  const int strips = (J + 63) / 64;
-  int ns = (1024 + strips - 1) / strips;
-  const int max_by_rows = (I + 15) / 16;
-  if (ns > max_by_rows) ns = max_by_rows;
-  if (ns > 64) ns = 64;
-  if (ns < 1) ns = 1;
-  return ns;
-}
+constexpr int kColsPerBlock = 16;  // column pass: 16 columns x 64 row groups per workgroup
 
 static SkWs sk_plan(int I, int J) {
   SkWs w;
-  w.ns = sk_nsplit(I, J);
   int64_t o = GNNEA_SK_STATUS_BYTES;
   w.f = o; o = al256(o + 2 * 8ll * I);
   w.g = o; o = al256(o + 2 * 8ll * J);
   w.ua = o; o = al256(o + 8ll * I);
   w.va = o; o = al256(o + 8ll * J);
-  w.part_m = o; o = al256(o + 8ll * w.ns * J);
-  w.part_s = o; o = al256(o + 8ll * w.ns * J);
   w.rowbuf = o; o = al256(o + 8ll * I);
-  w.ncb = (J + 255) / 256;
+  w.ncb = (J + kColsPerBlock - 1) / kColsPerBlock;
   w.errpart = o; o = al256(o + 8ll * w.ncb);
   w.total = o;
   return w;
@@ -64,8 +54,8 @@ static SkWs sk_plan(int I, int J) {
 struct SkDev {
   int64_t* st;   // status ints
   double* sd;    // status doubles (sd[8] ...)
-  double *f, *g, *ua, *va, *pm, *ps, *rowbuf, *errpart;
-  int ns, ncb;
+  double *f, *g, *ua, *va, *rowbuf, *errpart;
+  int ncb;
 };
 
 static SkDev sk_dev(const gnnea_sinkhorn* p) {
@@ -78,11 +68,8 @@ static SkDev sk_dev(const gnnea_sinkhorn* p) {
   d.g = (double*)(b + w.g);
   d.ua = (double*)(b + w.ua);
   d.va = (double*)(b + w.va);
-  d.pm = (double*)(b + w.part_m);
-  d.ps = (double*)(b + w.part_s);
   d.rowbuf = (double*)(b + w.rowbuf);
   d.errpart = (double*)(b + w.errpart);
-  d.ns = w.ns;
   d.ncb = w.ncb;
   return d;
 }
@@ -201,7 +188,7 @@ __global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs 
   const double* __restrict__ va = d.va;
   const double uai = KNOPP ? 0.0 : d.ua[i];
   const T* __restrict__ Ci = C + (int64_t)i * a.ldc;
-  constexpr int CH = 4;
+  constexpr int CH = 16;  // 16 independent loads per lane in flight (latency-bound otherwise)
   Lse l;
   l.init();
   int j0 = 0;
@@ -234,69 +221,60 @@ __global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs 
   }
 }
 
-// Column pass: partial (max, sumexp) over a row split, for a 64-column strip; the 4 waves of
-// the workgroup interleave rows and merge through LDS.
+// Column pass, fused with the update: a 1024-thread workgroup owns 16 columns; thread
+// (c = tid % 16, rg = tid / 16) runs an online LSE over rows rg, rg+64, ... of column c with 16
+// independent loads in flight, the 64 row groups merge through LDS, and the first 16 threads
+// finish the column: g update, KNOPP err^2 partial (per workgroup) and break flags, STAB
+// max(b) > 1e20 absorption flag.
 template <typename T, bool KNOPP>
-__global__ __launch_bounds__(256) void k_sk_col(const T* __restrict__ C, SkArgs a, SkDev d,
-                                                int slot_f, int rows_per_split) {
+__global__ __launch_bounds__(1024) void k_sk_col(const T* __restrict__ C, SkArgs a, SkDev d, int it,
+                                                 int slot_f, int slot_g_prev, int slot_g_out) {
   if (d.st[ST_DONE]) return;
-  __shared__ double sm[4][64], ss[4][64];
-  const int lane = lane_id(), w = wave_id();
-  const int j = blockIdx.x * 64 + lane;
-  const int split = blockIdx.y;
-  const int r0 = split * rows_per_split;
-  const int r1 = min(a.I, r0 + rows_per_split);
+  __shared__ double sm[64][kColsPerBlock], ss[64][kColsPerBlock];
+  const int c = threadIdx.x % kColsPerBlock, rg = threadIdx.x / kColsPerBlock;
+  const int j = blockIdx.x * kColsPerBlock + c;
   const double* __restrict__ f = d.f + (int64_t)slot_f * a.I;
   const double* __restrict__ ua = d.ua;
-  constexpr int CH = 4;
+  constexpr int CH = 16;
   Lse l;
   l.init();
   if (j < a.J) {
     const double vaj = KNOPP ? 0.0 : d.va[j];
-    int i0 = r0 + w;
-    for (; i0 + 4 * (CH - 1) < r1; i0 += 4 * CH) {
+    int i0 = rg;
+    for (; i0 + 64 * (CH - 1) < a.I; i0 += 64 * CH) {
       double x[CH];
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
-        const int i = i0 + 4 * k;
+        const int i = i0 + 64 * k;
         const double ui = KNOPP ? 0.0 : ua[i];
         x[k] = sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps, a.kclamp,
                               f[i] - ui);
       }
       lse_chunk<CH>(l, x);
     }
-    for (int i = i0; i < r1; i += 4) {
+    for (int i = i0; i < a.I; i += 64) {
       const double ui = KNOPP ? 0.0 : ua[i];
       const double x1[1] = {sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps,
                                            a.kclamp, f[i] - ui)};
       lse_chunk<1>(l, x1);
     }
   }
-  sm[w][lane] = l.m;
-  ss[w][lane] = l.s;
+  sm[rg][c] = l.m;
+  ss[rg][c] = l.s;
   __syncthreads();
-  if (w == 0 && j < a.J) {
-    for (int q = 1; q < 4; ++q) l.merge(sm[q][lane], ss[q][lane]);
-    d.pm[(int64_t)split * a.J + j] = l.m;
-    d.ps[(int64_t)split * a.J + j] = l.s;
+#pragma unroll
+  for (int h = 32; h > 0; h >>= 1) {
+    if (rg < h) {
+      l.merge(sm[rg + h][c], ss[rg + h][c]);
+      sm[rg][c] = l.m;
+      ss[rg][c] = l.s;
+    }
+    __syncthreads();
   }
-}
-
-// Column combine: one thread per column merges the row-split partials into the column LSE and
-// updates g; KNOPP also produces per-workgroup partial sums of err^2 and the break flag (decided
-// by the next row pass), STAB modes the max(b) > 1e20 absorption flag.
-template <bool KNOPP>
-__global__ __launch_bounds__(256) void k_sk_combine(SkArgs a, SkDev d, int it, int slot_g_prev,
-                                                    int slot_g_out) {
-  if (d.st[ST_DONE]) return;
-  __shared__ double red[4];
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (rg != 0) return;  // threads 0..15: lanes 0..15 of wave 0
   double errp = 0.0;
   bool fail = false, big = false;
   if (j < a.J) {
-    Lse l;
-    l.init();
-    for (int s = 0; s < d.ns; ++s) l.merge(d.pm[(int64_t)s * a.J + j], d.ps[(int64_t)s * a.J + j]);
     const double ls = l.value();
     if (KNOPP) {
       // err of the previous iterate: v_{k-1} * (K^T u_{k-1}) - b    (utils/ot_loss.py:65-66)
@@ -313,14 +291,17 @@ __global__ __launch_bounds__(256) void k_sk_combine(SkArgs a, SkDev d, int it, i
       d.g[(int64_t)slot_g_out * a.J + j] = d.va[j] + lb;
     }
   }
-  if (KNOPP) {
-    errp = wave_sum(errp);
-    if (lane_id() == 0) red[wave_id()] = errp;
-    if (__any(fail) && lane_id() == 0) atomicOr((unsigned long long*)&d.st[ST_FAIL], 1ull);
-    __syncthreads();
-    if (threadIdx.x == 0) d.errpart[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-  } else if (__any(big) && lane_id() == 0) {
-    atomicOr((unsigned long long*)&d.st[ST_BIG], 2ull);
+  // reduce the 16 finishing lanes (xor offsets < 16 stay inside them)
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) errp += __shfl_xor(errp, o, 64);
+  const unsigned long long anyfail = __ballot(fail) & 0xffffull, anybig = __ballot(big) & 0xffffull;
+  if (threadIdx.x == 0) {
+    if (KNOPP) {
+      d.errpart[blockIdx.x] = errp;
+      if (anyfail) atomicOr((unsigned long long*)&d.st[ST_FAIL], 1ull);
+    } else if (anybig) {
+      atomicOr((unsigned long long*)&d.st[ST_BIG], 2ull);
+    }
   }
 }
 
@@ -520,21 +501,18 @@ template <typename T>
 static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t s) {
   SkArgs a = sk_args(p);
   SkDev d = sk_dev(p);
-  const int rows_per_split = (p->I + d.ns - 1) / d.ns;
-  const dim3 grow(div_up(p->I, 4)), gcol(div_up(p->J, 64), d.ns), gcomb(d.ncb);
+  const dim3 grow(div_up(p->I, 4)), gcol(d.ncb);
   const T* C = (const T*)p->C;
   for (int it = first; it < first + count; ++it) {
     const int cur = it & 1, prev = (it + 1) & 1;
     if (p->mode == GNNEA_SK_KNOPP) {
-      hipLaunchKernelGGL((k_sk_col<T, true>), gcol, dim3(256), 0, s, C, a, d, prev,
-                         rows_per_split);
-      hipLaunchKernelGGL(k_sk_combine<true>, gcomb, dim3(256), 0, s, a, d, it, prev, cur);
+      hipLaunchKernelGGL((k_sk_col<T, true>), gcol, dim3(1024), 0, s, C, a, d, it, prev, prev,
+                         cur);
       hipLaunchKernelGGL((k_sk_row<T, true>), grow, dim3(256), 0, s, C, a, d, it, cur, cur);
     } else {
       hipLaunchKernelGGL((k_sk_row<T, false>), grow, dim3(256), 0, s, C, a, d, it, prev, cur);
-      hipLaunchKernelGGL((k_sk_col<T, false>), gcol, dim3(256), 0, s, C, a, d, cur,
-                         rows_per_split);
-      hipLaunchKernelGGL(k_sk_combine<false>, gcomb, dim3(256), 0, s, a, d, it, prev, cur);
+      hipLaunchKernelGGL((k_sk_col<T, false>), gcol, dim3(1024), 0, s, C, a, d, it, cur, prev,
+                         cur);
       hipLaunchKernelGGL(k_sk_absorb_rows<T>, grow, dim3(256), 0, s, C, a, d, it, cur,
                          p->max_iter, 0);
       hipLaunchKernelGGL(k_sk_absorb_final, dim3(1), dim3(1024), 0, s, a, d, it, cur,
