@@ -200,3 +200,21 @@ extern "C" int gnnea_csr_expand_rows(const int32_t* rowptr, int32_t n_rows, int6
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
+
+namespace gnnea {
+__global__ void k_perm_invert(const int64_t* __restrict__ perm, int64_t n,
+                              int64_t* __restrict__ inv) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) inv[perm[k]] = k;
+}
+}  // namespace gnnea
+
+extern "C" int gnnea_perm_invert(const int64_t* perm, int64_t n, int64_t* inv, void* stream) {
+  if (n < 0) return GNNEA_EINVAL;
+  if (n == 0) return 0;
+  if (!perm || !inv) return GNNEA_EINVAL;
+  hipLaunchKernelGGL(gnnea::k_perm_invert, dim3(gnnea::div_up(n, 256)), dim3(256), 0,
+                     (hipStream_t)stream, perm, n, inv);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}

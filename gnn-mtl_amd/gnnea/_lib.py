@@ -64,6 +64,7 @@ SIGNATURES = {
     "gnnea_coo_to_csr": (ctypes.c_int, [_p, _p, ctypes.c_int, _p, _i64, _i64, _i64, _p, _p, _p,
                                         _p, _p, _p, _i64, _p]),
     "gnnea_csr_expand_rows": (ctypes.c_int, [_p, _i32, _i64, _p, _p]),
+    "gnnea_perm_invert": (ctypes.c_int, [_p, _i64, _p, _p]),
     "gnnea_spmm_csr_f32": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64,
                                           ctypes.c_int, _p]),
     "gnnea_spmm_csr_beta_f32": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _f32, _p, _i64,
@@ -77,11 +78,12 @@ SIGNATURES = {
                                             _p]),
     "gnnea_gat_fwd_f32": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int, ctypes.c_int, _p, _p,
                                          _f32, _p, ctypes.c_int, _p, _i64, _p, _p, _p]),
-    "gnnea_gat_bwd_edge_f32": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int, ctypes.c_int,
-                                              _p, _p, _f32, _p, _p, _p, _p, _p, _i64, _p, _p, _p]),
-    "gnnea_gat_bwd_node_f32": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _p,
-                                              _f32, _p, _p, _p, _p, _i64, _p, _p, _p, _p, _i64, _p,
-                                              _p]),
+    "gnnea_gat_bwd_prep_f32": (ctypes.c_int, [_i32, ctypes.c_int, ctypes.c_int, _p, _p, _i64, _p,
+                                              _p, _p, ctypes.c_int, _p, _p, _p]),
+    "gnnea_gat_bwd_src_f32": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _i64,
+                                             _p, _f32, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
+    "gnnea_gat_bwd_dst_f32": (ctypes.c_int, [_p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,
+                                             _i64, _p, _p]),
     "gnnea_gemm_ws_bytes": (_i64, [_i64, _i64, _i64]),
     "gnnea_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
                                       _i64, _p, _f32, _p, _i64, _p, _i64, _p]),

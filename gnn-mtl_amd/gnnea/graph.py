@@ -81,6 +81,18 @@ class DeviceCSR:
                                          want_perm=True)
         return self._t
 
+    def tpos(self):
+        """Position in transpose() of every entry of this CSR (inverse of transpose().perm)."""
+        if getattr(self, "_tpos", None) is None:
+            t = self.transpose()
+            inv = torch.empty(max(self.nnz, 1), dtype=torch.int64, device=self.device)
+            with torch.cuda.device(self.device):
+                _lib.check(_lib.lib().gnnea_perm_invert(_lib.ptr(t.perm), self.nnz,
+                                                        _lib.ptr(inv),
+                                                        _lib.stream_of(self.device)))
+            self._tpos = inv[:self.nnz]
+        return self._tpos
+
     def degrees(self):
         return (self.rowptr[1:] - self.rowptr[:-1])
 

@@ -311,24 +311,29 @@ class GATFn(torch.autograd.Function):
         dY = _pad4(dY.float(), D)
         if dY.shape[1] != Y.shape[1]:
             dY = _pad4(dY[:, :D].contiguous(), D)
-        # G = dL/dh' ; P = h' (relu / identity: Y itself is a valid stand-in for c = G·h')
-        G = dY if act == _lib.GNNEA_ACT_IDENTITY else act_bwd(dY.contiguous(), Y, act)
         N = csr.n_rows
-        dz = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=H.device)
-        ds1 = torch.empty((N, heads), dtype=torch.float32, device=H.device)
-        ds2 = torch.empty_like(ds1)
-        dH = torch.empty_like(H)
+        dev = H.device
         L = _lib.lib()
-        st = stream_of(H.device)
-        with torch.cuda.device(H.device):
-            check(L.gnnea_gat_bwd_edge_f32(
-                ptr(csr.rowptr), ptr(csr.col), N, ptr(H), H.stride(0), heads, d_head, ptr(s1),
-                ptr(s2), alpha, ptr(em), ptr(m), ptr(den), ptr(G), ptr(Y), G.stride(0), ptr(dz),
-                ptr(ds1), st))
-            check(L.gnnea_gat_bwd_node_f32(
-                ptr(csrT.rowptr), ptr(csrT.col), ptr(csrT.perm), N, heads, d_head, ptr(s1),
-                ptr(s2), alpha, ptr(em), ptr(m), ptr(den), ptr(G), G.stride(0), ptr(dz),
-                ptr(ds1), ptr(a_all), ptr(dH), dH.stride(0), ptr(ds2), st))
+        st = stream_of(dev)
+        G = torch.empty_like(Y)
+        rec = torch.empty((N, heads, 4), dtype=torch.float32, device=dev)
+        dH = torch.empty_like(H)
+        dzT = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=dev)
+        ds1 = torch.empty((N, heads), dtype=torch.float32, device=dev)
+        ds2 = torch.empty_like(ds1)
+        tpos = csr.tpos()
+        with torch.cuda.device(dev):
+            # G = dL/dh' and the per-node record {s1, m, 1/den, G.h'} (relu / identity: Y = h')
+            check(L.gnnea_gat_bwd_prep_f32(N, heads, d_head, ptr(dY), ptr(Y), Y.stride(0),
+                                           ptr(s1), ptr(m), ptr(den), int(act), ptr(G),
+                                           ptr(rec), st))
+            check(L.gnnea_gat_bwd_src_f32(
+                ptr(csrT.rowptr), ptr(csrT.col), ptr(csrT.perm), N, heads, d_head, ptr(H),
+                H.stride(0), ptr(s2), alpha, ptr(em), ptr(rec), ptr(G), G.stride(0), ptr(a_all),
+                ptr(dH), dH.stride(0), ptr(dzT), ptr(ds2), st))
+            check(L.gnnea_gat_bwd_dst_f32(ptr(csr.rowptr), ptr(tpos), N, heads, d_head,
+                                          ptr(dzT), ptr(a_all), ptr(dH), dH.stride(0), ptr(ds1),
+                                          st))
         da = None
         if ctx.needs_input_grad[1]:
             # da1[h] = sum_i ds1[i,h] H_i,h ; da2[h] = sum_j ds2[j,h] H_j,h   (MFMA, split-K)

@@ -63,6 +63,8 @@ int gnnea_coo_to_csr(const void* row_idx, const void* col_idx, int index_bytes /
 /* row id of every CSR entry: row_out[e] = r for rowptr[r] <= e < rowptr[r+1] */
 int gnnea_csr_expand_rows(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t* row_out,
                           void* stream);
+/* inverse permutation: inv[perm[k]] = k (forward CSR position -> transposed position) */
+int gnnea_perm_invert(const int64_t* perm, int64_t n, int64_t* inv, void* stream);
 
 /* ------------------------------------------------------------------------------------------ *
  * a2/a3. CSR SpMM  Y = act(A · X)   (layers/layers.py:35 torch.spmm(adj, hidden) + :38 act)
@@ -116,23 +118,25 @@ int gnnea_gat_fwd_f32(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
                       int64_t ldh, int heads, int d_head, const float* s1, const float* s2,
                       float alpha, const float* edge_mask, int act, float* Y, int64_t ldy,
                       float* m_out, float* den_out, void* stream);
-/* Backward pass 1, row sweep (SDDMM + softmax backward):
- *   for edge (i,j): da = G_i·H_j (per head), dscore = alpha_ij*(mask*da - G_i·P_i),
- *   dz = -LeakyReLU'(z)*dscore  -> dz (nnz x heads);  ds1_i = sum_j dz.
- * G = dL/dh' (pre-activation gradient), P = h' (pre-activation output), both ld = ldg. */
-int gnnea_gat_bwd_edge_f32(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
-                           const float* H, int64_t ldh, int heads, int d_head, const float* s1,
-                           const float* s2, float alpha, const float* edge_mask, const float* m,
-                           const float* den, const float* G, const float* P, int64_t ldg,
-                           float* dz, float* ds1, void* stream);
-/* Backward pass 2, transpose sweep over A^T (rowptrT/colT/permT from gnnea_coo_to_csr):
- *   dH_j = sum_i alpha_ij*mask*G_i  +  ds1_j (x) a1 + ds2_j (x) a2 ;  ds2_j = sum_i dz(i,j). */
-int gnnea_gat_bwd_node_f32(const int32_t* rowptrT, const int32_t* colT, const int64_t* permT,
-                           int32_t n_rows, int heads, int d_head, const float* s1,
-                           const float* s2, float alpha, const float* edge_mask, const float* m,
-                           const float* den, const float* G, int64_t ldg, const float* dz,
-                           const float* ds1, const float* a, float* dH, int64_t lddh, float* ds2,
-                           void* stream);
+/* Backward in one gather sweep over A^T (autograd of att_layers.py:38-58):
+ *  prep (rows i):   G_i = dY_i * act'(Y_i) (act: identity / relu, Y = h' there) and the per-node
+ *                   record rec[i,h] = {s1, m, 1/den, c = G_i,h . h'_i,h}  (float4 per head);
+ *  src  (rows j of A^T; rowptrT/colT/permT from gnnea_coo_to_csr on the transpose):
+ *                   dH_j = sum_i alpha_ij*mask*G_i + ds2_j (x) a2,  dz_ij = -LReLU'(z) *
+ *                   alpha_ij*(mask*G_i.H_j - c_i) per head, written in A^T order to dzT;
+ *  dst  (rows i of A; tpos = inverse of permT): ds1_i = sum_j dz_ij,  dH_i += ds1_i (x) a1.
+ * a is [heads][2*d_head] (a_h = [a1 | a2]). */
+int gnnea_gat_bwd_prep_f32(int32_t n_rows, int heads, int d_head, const float* dY,
+                           const float* Y, int64_t ld, const float* s1, const float* m,
+                           const float* den, int act, float* G, float* rec, void* stream);
+int gnnea_gat_bwd_src_f32(const int32_t* rowptrT, const int32_t* colT, const int64_t* permT,
+                          int32_t n_rows, int heads, int d_head, const float* H, int64_t ldh,
+                          const float* s2, float alpha, const float* edge_mask, const float* rec,
+                          const float* G, int64_t ldg, const float* a, float* dH, int64_t lddh,
+                          float* dzT, float* ds2, void* stream);
+int gnnea_gat_bwd_dst_f32(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows, int heads,
+                          int d_head, const float* dzT, const float* a, float* dH, int64_t lddh,
+                          float* ds1, void* stream);
 
 /* ------------------------------------------------------------------------------------------ *
  * Dense projection (nn.Linear at layers/layers.py:32,61,93; torch.mm at att_layers.py:33;
