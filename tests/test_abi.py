@@ -20,7 +20,8 @@ def declared_functions():
 def test_header_declares_the_hot_path():
     names = declared_functions()
     for must in ("gnnea_coo_to_csr", "gnnea_spmm_csr_f32", "gnnea_spmm_highway_f32",
-                 "gnnea_gat_fwd_f32", "gnnea_gat_bwd_edge_f32", "gnnea_gat_bwd_node_f32",
+                 "gnnea_gat_fwd_f32", "gnnea_gat_bwd_prep_f32", "gnnea_gat_bwd_src_f32",
+                 "gnnea_gat_bwd_dst_f32", "gnnea_spmm_csr_beta_f32", "gnnea_perm_invert",
                  "gnnea_gemm_f32", "gnnea_sinkhorn_iterate", "gnnea_sinkhorn_finish"):
         assert must in names
 
