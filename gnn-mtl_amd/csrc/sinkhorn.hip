@@ -35,7 +35,7 @@ struct SkWs {
 
 static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
-constexpr int kColsPerBlock = 16;  // column pass: 16 columns x 64 row groups per workgroup
+constexpr int kColsPerBlock = 8;  // column pass: 8 columns x 128 row groups per workgroup
 
 static SkWs sk_plan(int I, int J) {
   SkWs w;
@@ -155,60 +155,84 @@ __device__ __forceinline__ double sk_term(double ua, double va, double c, double
   return (KNOPP ? k : fmin(k, kclamp)) + pot_minus_abs;
 }
 
-// Row pass: f_out_i from g_in (one wave per row, 64-wide coalesced column sweep).
+// Row pass: f_out_i from g_in.  One 256-thread workgroup per row (4 waves split the columns,
+// CH = 12 independent loads per lane in one round for J <= 3072: the pass is latency-bound at
+// one wave per row), wave LSEs merged through LDS.
 template <typename T, bool KNOPP>
 __global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs a, SkDev d,
                                                 int it, int slot_in, int slot_out) {
   if (d.st[ST_DONE]) return;
+  __shared__ double wm[4], ws[4];
+  __shared__ int stop;
+  const int lane = lane_id(), w = wave_id();
   if (KNOPP) {
     // decisions of the reference loop, in its order (utils/ot_loss.py:50-72): the err test of
     // iterate it-1 (when (it-1)%10 == 0), then the K^T u == 0 / inf / NaN break of iteration it
-    // flagged by this iteration's column combine.  Every workgroup takes the same decision.
+    // flagged by this iteration's column pass.  Every workgroup takes the same decision.
     const int prev = it - 1;
-    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
-    if (prev >= 0 && prev % 10 == 0) {
-      double e = 0.0;
-      for (int b = 0; b < d.ncb; ++b) e += d.errpart[b];
-      const double err = sqrt(e);
-      if (lead) d.sd[SD_ERR] = err;
-      if (!(err > d.sd[11])) {  // sd[11] = stopThr: the loop runs while err > stopThr
-        if (lead) mark_done(d.st, prev + 1, 1, prev & 1);
-        return;
+    if (w == 0) {
+      int st = 0;
+      if (prev >= 0 && prev % 10 == 0) {
+        double e = 0.0;
+        for (int b = lane; b < d.ncb; b += 64) e += d.errpart[b];
+        const double err = sqrt(wave_sum(e));
+        if (!(err > d.sd[11])) st = 1;  // sd[11] = stopThr: loop runs while err > stopThr
+        if (blockIdx.x == 0 && lane == 0) {
+          d.sd[SD_ERR] = err;
+          if (st) mark_done(d.st, prev + 1, 1, prev & 1);
+        }
       }
+      if (!st && d.st[ST_FAIL]) {
+        st = 1;
+        if (blockIdx.x == 0 && lane == 0) mark_done(d.st, it, 2, (it + 1) & 1);
+      }
+      if (lane == 0) stop = st;
     }
-    if (d.st[ST_FAIL]) {
-      if (lead) mark_done(d.st, it, 2, (it + 1) & 1);
-      return;
-    }
+    __syncthreads();
+    if (stop) return;
   }
-  const int i = blockIdx.x * 4 + wave_id();
+  const int i = blockIdx.x;
   if (i >= a.I) return;
-  const int lane = lane_id();
   const double* __restrict__ g = d.g + (int64_t)slot_in * a.J;
   const double* __restrict__ va = d.va;
   const double uai = KNOPP ? 0.0 : d.ua[i];
   const T* __restrict__ Ci = C + (int64_t)i * a.ldc;
-  constexpr int CH = 16;  // 16 independent loads per lane in flight (latency-bound otherwise)
+  constexpr int CH = 12;
+  const int t = threadIdx.x;
   Lse l;
   l.init();
   int j0 = 0;
-  for (; j0 + 64 * CH <= a.J; j0 += 64 * CH) {
+  for (; j0 + 256 * CH <= a.J; j0 += 256 * CH) {
     double x[CH];
 #pragma unroll
     for (int k = 0; k < CH; ++k) {
-      const int j = j0 + 64 * k + lane;
+      const int j = j0 + 256 * k + t;
       const double vj = KNOPP ? 0.0 : va[j];
       x[k] = sk_term<KNOPP>(uai, vj, (double)Ci[j], a.inv_eps, a.kclamp, g[j] - vj);
     }
     lse_chunk<CH>(l, x);
   }
-  for (int j = j0 + lane; j < a.J; j += 64) {
-    const double vj = KNOPP ? 0.0 : va[j];
-    const double x1[1] = {sk_term<KNOPP>(uai, vj, (double)Ci[j], a.inv_eps, a.kclamp, g[j] - vj)};
-    lse_chunk<1>(l, x1);
+  if (j0 < a.J) {  // ragged tail: masked lanes contribute -inf
+    double x[CH];
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      const int j = j0 + 256 * k + t;
+      x[k] = -INFINITY;
+      if (j < a.J) {
+        const double vj = KNOPP ? 0.0 : va[j];
+        x[k] = sk_term<KNOPP>(uai, vj, (double)Ci[j], a.inv_eps, a.kclamp, g[j] - vj);
+      }
+    }
+    lse_chunk<CH>(l, x);
   }
   l = wave_lse(l);
-  if (lane != 0) return;
+  if (lane == 0) {
+    wm[w] = l.m;
+    ws[w] = l.s;
+  }
+  __syncthreads();
+  if (t != 0) return;
+  for (int q = 1; q < 4; ++q) l.merge(wm[q], ws[q]);
   const double ls = l.value();
   double la = a.p_row * (a.la[i] - ls);
   if (KNOPP) {
@@ -230,29 +254,30 @@ template <typename T, bool KNOPP>
 __global__ __launch_bounds__(1024) void k_sk_col(const T* __restrict__ C, SkArgs a, SkDev d, int it,
                                                  int slot_f, int slot_g_prev, int slot_g_out) {
   if (d.st[ST_DONE]) return;
-  __shared__ double sm[64][kColsPerBlock], ss[64][kColsPerBlock];
+  constexpr int RG = 1024 / kColsPerBlock;
+  __shared__ double sm[RG][kColsPerBlock], ss[RG][kColsPerBlock];
   const int c = threadIdx.x % kColsPerBlock, rg = threadIdx.x / kColsPerBlock;
   const int j = blockIdx.x * kColsPerBlock + c;
   const double* __restrict__ f = d.f + (int64_t)slot_f * a.I;
   const double* __restrict__ ua = d.ua;
-  constexpr int CH = 16;
+  constexpr int CH = 12;
   Lse l;
   l.init();
   if (j < a.J) {
     const double vaj = KNOPP ? 0.0 : d.va[j];
     int i0 = rg;
-    for (; i0 + 64 * (CH - 1) < a.I; i0 += 64 * CH) {
+    for (; i0 + RG * (CH - 1) < a.I; i0 += RG * CH) {
       double x[CH];
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
-        const int i = i0 + 64 * k;
+        const int i = i0 + RG * k;
         const double ui = KNOPP ? 0.0 : ua[i];
         x[k] = sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps, a.kclamp,
                               f[i] - ui);
       }
       lse_chunk<CH>(l, x);
     }
-    for (int i = i0; i < a.I; i += 64) {
+    for (int i = i0; i < a.I; i += RG) {
       const double ui = KNOPP ? 0.0 : ua[i];
       const double x1[1] = {sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps,
                                            a.kclamp, f[i] - ui)};
@@ -263,7 +288,7 @@ __global__ __launch_bounds__(1024) void k_sk_col(const T* __restrict__ C, SkArgs
   ss[rg][c] = l.s;
   __syncthreads();
 #pragma unroll
-  for (int h = 32; h > 0; h >>= 1) {
+  for (int h = RG / 2; h > 0; h >>= 1) {
     if (rg < h) {
       l.merge(sm[rg + h][c], ss[rg + h][c]);
       sm[rg][c] = l.m;
@@ -271,7 +296,7 @@ __global__ __launch_bounds__(1024) void k_sk_col(const T* __restrict__ C, SkArgs
     }
     __syncthreads();
   }
-  if (rg != 0) return;  // threads 0..15: lanes 0..15 of wave 0
+  if (rg != 0) return;  // threads 0..kColsPerBlock-1: the first lanes of wave 0
   double errp = 0.0;
   bool fail = false, big = false;
   if (j < a.J) {
@@ -291,10 +316,11 @@ __global__ __launch_bounds__(1024) void k_sk_col(const T* __restrict__ C, SkArgs
       d.g[(int64_t)slot_g_out * a.J + j] = d.va[j] + lb;
     }
   }
-  // reduce the 16 finishing lanes (xor offsets < 16 stay inside them)
+  // reduce the finishing lanes (xor offsets < kColsPerBlock stay inside them)
 #pragma unroll
-  for (int o = 8; o > 0; o >>= 1) errp += __shfl_xor(errp, o, 64);
-  const unsigned long long anyfail = __ballot(fail) & 0xffffull, anybig = __ballot(big) & 0xffffull;
+  for (int o = kColsPerBlock / 2; o > 0; o >>= 1) errp += __shfl_xor(errp, o, 64);
+  const unsigned long long lanes = (1ull << kColsPerBlock) - 1;
+  const unsigned long long anyfail = __ballot(fail) & lanes, anybig = __ballot(big) & lanes;
   if (threadIdx.x == 0) {
     if (KNOPP) {
       d.errpart[blockIdx.x] = errp;
@@ -501,7 +527,7 @@ template <typename T>
 static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t s) {
   SkArgs a = sk_args(p);
   SkDev d = sk_dev(p);
-  const dim3 grow(div_up(p->I, 4)), gcol(d.ncb);
+  const dim3 grow(p->I), gcol(d.ncb), gabs(div_up(p->I, 4));
   const T* C = (const T*)p->C;
   for (int it = first; it < first + count; ++it) {
     const int cur = it & 1, prev = (it + 1) & 1;
@@ -513,7 +539,7 @@ static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t 
       hipLaunchKernelGGL((k_sk_row<T, false>), grow, dim3(256), 0, s, C, a, d, it, prev, cur);
       hipLaunchKernelGGL((k_sk_col<T, false>), gcol, dim3(1024), 0, s, C, a, d, it, cur, prev,
                          cur);
-      hipLaunchKernelGGL(k_sk_absorb_rows<T>, grow, dim3(256), 0, s, C, a, d, it, cur,
+      hipLaunchKernelGGL(k_sk_absorb_rows<T>, gabs, dim3(256), 0, s, C, a, d, it, cur,
                          p->max_iter, 0);
       hipLaunchKernelGGL(k_sk_absorb_final, dim3(1), dim3(1024), 0, s, a, d, it, cur,
                          p->max_iter, 0, p->tol);
