@@ -29,13 +29,13 @@ constexpr double kLnTrueMin = -744.4400719213812;     // log(DBL_TRUE_MIN)
 constexpr double kExpOverflow = 709.782712893384;     // exp_f64(x) == inf above
 
 struct SkWs {
-  int64_t f, g, ua, va, rowbuf, errpart, total;
+  int64_t f, g, ua, va, rowbuf, errpart, part_m, part_s, total;
   int ncb;
 };
 
 static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
-constexpr int kColsPerBlock = 8;  // column pass: 8 columns x 128 row groups per workgroup
+constexpr int kMaxSplits = 16;  // row splits of the partial column pass
 
 static SkWs sk_plan(int I, int J) {
   SkWs w;
@@ -45,8 +45,10 @@ static SkWs sk_plan(int I, int J) {
   w.ua = o; o = al256(o + 8ll * I);
   w.va = o; o = al256(o + 8ll * J);
   w.rowbuf = o; o = al256(o + 8ll * I);
-  w.ncb = (J + kColsPerBlock - 1) / kColsPerBlock;
+  w.ncb = (J + 7) / 8;  // errpart slots: enough for the narrowest column workgroup (8 cols)
   w.errpart = o; o = al256(o + 8ll * w.ncb);
+  w.part_m = o; o = al256(o + 8ll * kMaxSplits * J);
+  w.part_s = o; o = al256(o + 8ll * kMaxSplits * J);
   w.total = o;
   return w;
 }
@@ -54,8 +56,8 @@ static SkWs sk_plan(int I, int J) {
 struct SkDev {
   int64_t* st;   // status ints
   double* sd;    // status doubles (sd[8] ...)
-  double *f, *g, *ua, *va, *rowbuf, *errpart;
-  int ncb;
+  double *f, *g, *ua, *va, *rowbuf, *errpart, *pm, *ps;
+  int ncb;  // errpart slots written by the column pass of the active variant
 };
 
 static SkDev sk_dev(const gnnea_sinkhorn* p) {
@@ -70,6 +72,8 @@ static SkDev sk_dev(const gnnea_sinkhorn* p) {
   d.va = (double*)(b + w.va);
   d.rowbuf = (double*)(b + w.rowbuf);
   d.errpart = (double*)(b + w.errpart);
+  d.pm = (double*)(b + w.part_m);
+  d.ps = (double*)(b + w.part_s);
   d.ncb = w.ncb;
   return d;
 }
@@ -155,87 +159,41 @@ __device__ __forceinline__ double sk_term(double ua, double va, double c, double
   return (KNOPP ? k : fmin(k, kclamp)) + pot_minus_abs;
 }
 
-// Row pass: f_out_i from g_in.  One 256-thread workgroup per row (4 waves split the columns,
-// CH = 12 independent loads per lane in one round for J <= 3072: the pass is latency-bound at
-// one wave per row), wave LSEs merged through LDS.
-template <typename T, bool KNOPP>
-__global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs a, SkDev d,
-                                                int it, int slot_in, int slot_out) {
-  if (d.st[ST_DONE]) return;
-  __shared__ double wm[4], ws[4];
+// KNOPP loop decisions, in the reference's order (utils/ot_loss.py:50-72): the err test of
+// iterate it-1 (when (it-1)%10 == 0), then the K^T u == 0 / inf / NaN break of iteration it
+// flagged by this iteration's column pass.  Evaluated by wave 0 of every row workgroup (all
+// take the same decision); returns true when the workgroup must stop.
+__device__ __forceinline__ bool knopp_stop(SkDev& d, int it) {
   __shared__ int stop;
-  const int lane = lane_id(), w = wave_id();
-  if (KNOPP) {
-    // decisions of the reference loop, in its order (utils/ot_loss.py:50-72): the err test of
-    // iterate it-1 (when (it-1)%10 == 0), then the K^T u == 0 / inf / NaN break of iteration it
-    // flagged by this iteration's column pass.  Every workgroup takes the same decision.
+  const int lane = lane_id();
+  if (wave_id() == 0) {
     const int prev = it - 1;
-    if (w == 0) {
-      int st = 0;
-      if (prev >= 0 && prev % 10 == 0) {
-        double e = 0.0;
-        for (int b = lane; b < d.ncb; b += 64) e += d.errpart[b];
-        const double err = sqrt(wave_sum(e));
-        if (!(err > d.sd[11])) st = 1;  // sd[11] = stopThr: loop runs while err > stopThr
-        if (blockIdx.x == 0 && lane == 0) {
-          d.sd[SD_ERR] = err;
-          if (st) mark_done(d.st, prev + 1, 1, prev & 1);
-        }
-      }
-      if (!st && d.st[ST_FAIL]) {
-        st = 1;
-        if (blockIdx.x == 0 && lane == 0) mark_done(d.st, it, 2, (it + 1) & 1);
-      }
-      if (lane == 0) stop = st;
-    }
-    __syncthreads();
-    if (stop) return;
-  }
-  const int i = blockIdx.x;
-  if (i >= a.I) return;
-  const double* __restrict__ g = d.g + (int64_t)slot_in * a.J;
-  const double* __restrict__ va = d.va;
-  const double uai = KNOPP ? 0.0 : d.ua[i];
-  const T* __restrict__ Ci = C + (int64_t)i * a.ldc;
-  constexpr int CH = 12;
-  const int t = threadIdx.x;
-  Lse l;
-  l.init();
-  int j0 = 0;
-  for (; j0 + 256 * CH <= a.J; j0 += 256 * CH) {
-    double x[CH];
-#pragma unroll
-    for (int k = 0; k < CH; ++k) {
-      const int j = j0 + 256 * k + t;
-      const double vj = KNOPP ? 0.0 : va[j];
-      x[k] = sk_term<KNOPP>(uai, vj, (double)Ci[j], a.inv_eps, a.kclamp, g[j] - vj);
-    }
-    lse_chunk<CH>(l, x);
-  }
-  if (j0 < a.J) {  // ragged tail: masked lanes contribute -inf
-    double x[CH];
-#pragma unroll
-    for (int k = 0; k < CH; ++k) {
-      const int j = j0 + 256 * k + t;
-      x[k] = -INFINITY;
-      if (j < a.J) {
-        const double vj = KNOPP ? 0.0 : va[j];
-        x[k] = sk_term<KNOPP>(uai, vj, (double)Ci[j], a.inv_eps, a.kclamp, g[j] - vj);
+    int st = 0;
+    if (prev >= 0 && prev % 10 == 0) {
+      double e = 0.0;
+      for (int b = lane; b < d.ncb; b += 64) e += d.errpart[b];
+      const double err = sqrt(wave_sum(e));
+      if (!(err > d.sd[11])) st = 1;  // sd[11] = stopThr: the loop runs while err > stopThr
+      if (blockIdx.x == 0 && lane == 0) {
+        d.sd[SD_ERR] = err;
+        if (st) mark_done(d.st, prev + 1, 1, prev & 1);
       }
     }
-    lse_chunk<CH>(l, x);
-  }
-  l = wave_lse(l);
-  if (lane == 0) {
-    wm[w] = l.m;
-    ws[w] = l.s;
+    if (!st && d.st[ST_FAIL]) {
+      st = 1;
+      if (blockIdx.x == 0 && lane == 0) mark_done(d.st, it, 2, (it + 1) & 1);
+    }
+    if (lane == 0) stop = st;
   }
   __syncthreads();
-  if (t != 0) return;
-  for (int q = 1; q < 4; ++q) l.merge(wm[q], ws[q]);
+  return stop != 0;
+}
+
+__device__ __forceinline__ void finish_row(const SkArgs& a, SkDev& d, int i, Lse l, int it,
+                                           int slot_out, double uai, bool knopp) {
   const double ls = l.value();
   double la = a.p_row * (a.la[i] - ls);
-  if (KNOPP) {
+  if (knopp) {
     d.f[(int64_t)slot_out * a.I + i] = la;  // u = 1/(Kp v)
     if (!(la <= kExpOverflow)) mark_done(d.st, it, 2, (it + 1) & 1);  // u inf / NaN
   } else {
@@ -245,43 +203,105 @@ __global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs 
   }
 }
 
-// Column pass, fused with the update: a 1024-thread workgroup owns 16 columns; thread
-// (c = tid % 16, rg = tid / 16) runs an online LSE over rows rg, rg+64, ... of column c with 16
-// independent loads in flight, the 64 row groups merge through LDS, and the first 16 threads
-// finish the column: g update, KNOPP err^2 partial (per workgroup) and break flags, STAB
-// max(b) > 1e20 absorption flag.
-template <typename T, bool KNOPP>
-__global__ __launch_bounds__(1024) void k_sk_col(const T* __restrict__ C, SkArgs a, SkDev d, int it,
-                                                 int slot_f, int slot_g_prev, int slot_g_out) {
+// Row pass: f_out_i from g_in.  WPR waves per row (4/WPR rows per 256-thread workgroup); each
+// lane keeps CH independent loads in flight per round; partial LSEs merged by shuffles + LDS.
+template <typename T, bool KNOPP, int CH, int WPR>
+__global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                int it, int slot_in, int slot_out) {
   if (d.st[ST_DONE]) return;
-  constexpr int RG = 1024 / kColsPerBlock;
-  __shared__ double sm[RG][kColsPerBlock], ss[RG][kColsPerBlock];
-  const int c = threadIdx.x % kColsPerBlock, rg = threadIdx.x / kColsPerBlock;
-  const int j = blockIdx.x * kColsPerBlock + c;
+  if (KNOPP && knopp_stop(d, it)) return;
+  __shared__ double wm[4], ws[4];
+  const int w = wave_id(), lane = lane_id();
+  const int i = blockIdx.x * (4 / WPR) + w / WPR;
+  const int t = (w % WPR) * 64 + lane;  // thread index inside the row's team
+  constexpr int NT = 64 * WPR;
+  Lse l;
+  l.init();
+  if (i < a.I) {
+    const double* __restrict__ g = d.g + (int64_t)slot_in * a.J;
+    const double* __restrict__ va = d.va;
+    const double uai = KNOPP ? 0.0 : d.ua[i];
+    const T* __restrict__ Ci = C + (int64_t)i * a.ldc;
+    for (int j0 = 0; j0 < a.J; j0 += NT * CH) {
+      double x[CH];
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int j = j0 + NT * k + t;
+        x[k] = -INFINITY;
+        if (j < a.J) {
+          const double vj = KNOPP ? 0.0 : va[j];
+          x[k] = sk_term<KNOPP>(uai, vj, (double)Ci[j], a.inv_eps, a.kclamp, g[j] - vj);
+        }
+      }
+      lse_chunk<CH>(l, x);
+    }
+  }
+  l = wave_lse(l);
+  if (WPR > 1) {
+    if (lane == 0) {
+      wm[w] = l.m;
+      ws[w] = l.s;
+    }
+    __syncthreads();
+    if (i >= a.I || (w % WPR) != 0 || lane != 0) return;
+    for (int q = 1; q < WPR; ++q) l.merge(wm[w + q], ws[w + q]);
+  } else if (i >= a.I || lane != 0) {
+    return;
+  }
+  finish_row(a, d, i, l, it, slot_out, KNOPP ? 0.0 : d.ua[i], KNOPP);
+}
+
+// Finish column j from its LSE: g update, KNOPP err^2 term and break flags, STAB big flag.
+__device__ __forceinline__ void finish_col(const SkArgs& a, SkDev& d, int j, double ls,
+                                           int slot_g_prev, int slot_g_out, bool knopp,
+                                           double& errp, bool& fail, bool& big) {
+  if (knopp) {
+    // err of the previous iterate: v_{k-1} * (K^T u_{k-1}) - b    (utils/ot_loss.py:65-66)
+    const double t = exp_f64(d.g[(int64_t)slot_g_prev * a.J + j] + ls) - exp_f64(a.lb[j]);
+    errp = t * t;
+    fail = !(ls >= kLnTrueMin);  // K^T u == 0 (or NaN)     (:57)
+    const double gj = a.lb[j] - ls;
+    fail = fail || !(gj <= kExpOverflow);  // v inf / NaN   (:58-59)
+    d.g[(int64_t)slot_g_out * a.J + j] = gj;
+  } else {
+    double lb = a.p_col * (a.lb[j] - ls);
+    if (lb > kLn1e30) lb = kLn1e30;
+    big = lb > kLn1e20;
+    d.g[(int64_t)slot_g_out * a.J + j] = d.va[j] + lb;
+  }
+}
+
+// Column pass, fused with the update: a 1024-thread workgroup owns COLS columns; thread
+// (c = tid % COLS, rg = tid / COLS) runs an online LSE over rows rg, rg + RG, ... of column c
+// with CH loads in flight, row groups merge through LDS, the first COLS threads finish.
+template <typename T, bool KNOPP, int COLS, int CH>
+__global__ __launch_bounds__(1024) void k_sk_col_fused(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                       int it, int slot_f, int slot_g_prev,
+                                                       int slot_g_out) {
+  if (d.st[ST_DONE]) return;
+  constexpr int RG = 1024 / COLS;
+  __shared__ double sm[RG][COLS], ss[RG][COLS];
+  const int c = threadIdx.x % COLS, rg = threadIdx.x / COLS;
+  const int j = blockIdx.x * COLS + c;
   const double* __restrict__ f = d.f + (int64_t)slot_f * a.I;
   const double* __restrict__ ua = d.ua;
-  constexpr int CH = 12;
   Lse l;
   l.init();
   if (j < a.J) {
     const double vaj = KNOPP ? 0.0 : d.va[j];
-    int i0 = rg;
-    for (; i0 + RG * (CH - 1) < a.I; i0 += RG * CH) {
+    for (int i0 = rg; i0 < a.I; i0 += RG * CH) {
       double x[CH];
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
         const int i = i0 + RG * k;
-        const double ui = KNOPP ? 0.0 : ua[i];
-        x[k] = sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps, a.kclamp,
-                              f[i] - ui);
+        x[k] = -INFINITY;
+        if (i < a.I) {
+          const double ui = KNOPP ? 0.0 : ua[i];
+          x[k] = sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps, a.kclamp,
+                                f[i] - ui);
+        }
       }
       lse_chunk<CH>(l, x);
-    }
-    for (int i = i0; i < a.I; i += RG) {
-      const double ui = KNOPP ? 0.0 : ua[i];
-      const double x1[1] = {sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps,
-                                           a.kclamp, f[i] - ui)};
-      lse_chunk<1>(l, x1);
     }
   }
   sm[rg][c] = l.m;
@@ -296,30 +316,13 @@ __global__ __launch_bounds__(1024) void k_sk_col(const T* __restrict__ C, SkArgs
     }
     __syncthreads();
   }
-  if (rg != 0) return;  // threads 0..kColsPerBlock-1: the first lanes of wave 0
+  if (rg != 0) return;  // threads 0..COLS-1 (first lanes of wave 0)
   double errp = 0.0;
   bool fail = false, big = false;
-  if (j < a.J) {
-    const double ls = l.value();
-    if (KNOPP) {
-      // err of the previous iterate: v_{k-1} * (K^T u_{k-1}) - b    (utils/ot_loss.py:65-66)
-      const double t = exp_f64(d.g[(int64_t)slot_g_prev * a.J + j] + ls) - exp_f64(a.lb[j]);
-      errp = t * t;
-      fail = !(ls >= kLnTrueMin);  // K^T u == 0 (or NaN)     (:57)
-      const double gj = a.lb[j] - ls;
-      fail = fail || !(gj <= kExpOverflow);  // v inf / NaN   (:58-59)
-      d.g[(int64_t)slot_g_out * a.J + j] = gj;
-    } else {
-      double lb = a.p_col * (a.lb[j] - ls);
-      if (lb > kLn1e30) lb = kLn1e30;
-      big = lb > kLn1e20;
-      d.g[(int64_t)slot_g_out * a.J + j] = d.va[j] + lb;
-    }
-  }
-  // reduce the finishing lanes (xor offsets < kColsPerBlock stay inside them)
+  if (j < a.J) finish_col(a, d, j, l.value(), slot_g_prev, slot_g_out, KNOPP, errp, fail, big);
 #pragma unroll
-  for (int o = kColsPerBlock / 2; o > 0; o >>= 1) errp += __shfl_xor(errp, o, 64);
-  const unsigned long long lanes = (1ull << kColsPerBlock) - 1;
+  for (int o = COLS / 2; o > 0; o >>= 1) errp += __shfl_xor(errp, o, 64);
+  const unsigned long long lanes = COLS >= 64 ? ~0ull : (1ull << COLS) - 1;
   const unsigned long long anyfail = __ballot(fail) & lanes, anybig = __ballot(big) & lanes;
   if (threadIdx.x == 0) {
     if (KNOPP) {
@@ -328,6 +331,78 @@ __global__ __launch_bounds__(1024) void k_sk_col(const T* __restrict__ C, SkArgs
     } else if (anybig) {
       atomicOr((unsigned long long*)&d.st[ST_BIG], 2ull);
     }
+  }
+}
+
+// Column pass, split: workgroup = 16 waves x 64 consecutive columns (full 256-B / 512-B rows)
+// over one of NS row splits; partial (max, sum) pairs merged by k_sk_col_combine.
+template <typename T, bool KNOPP, int CH>
+__global__ __launch_bounds__(1024) void k_sk_col_part(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                      int slot_f, int rows_per_split) {
+  if (d.st[ST_DONE]) return;
+  __shared__ double sm[16][64], ss[16][64];
+  const int lane = lane_id(), w = wave_id();
+  const int j = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * rows_per_split, r1 = min(a.I, r0 + rows_per_split);
+  const double* __restrict__ f = d.f + (int64_t)slot_f * a.I;
+  const double* __restrict__ ua = d.ua;
+  Lse l;
+  l.init();
+  if (j < a.J) {
+    const double vaj = KNOPP ? 0.0 : d.va[j];
+    for (int i0 = r0 + w; i0 < r1; i0 += 16 * CH) {
+      double x[CH];
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int i = i0 + 16 * k;
+        x[k] = -INFINITY;
+        if (i < r1) {
+          const double ui = KNOPP ? 0.0 : ua[i];
+          x[k] = sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps, a.kclamp,
+                                f[i] - ui);
+        }
+      }
+      lse_chunk<CH>(l, x);
+    }
+  }
+  sm[w][lane] = l.m;
+  ss[w][lane] = l.s;
+  __syncthreads();
+  if (w != 0 || j >= a.J) return;
+  for (int q = 1; q < 16; ++q) l.merge(sm[q][lane], ss[q][lane]);
+  d.pm[(int64_t)blockIdx.y * a.J + j] = l.m;
+  d.ps[(int64_t)blockIdx.y * a.J + j] = l.s;
+}
+
+template <bool KNOPP>
+__global__ __launch_bounds__(256) void k_sk_col_combine(SkArgs a, SkDev d, int ns, int slot_g_prev,
+                                                        int slot_g_out) {
+  if (d.st[ST_DONE]) return;
+  __shared__ double red[4];
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  double errp = 0.0;
+  bool fail = false, big = false;
+  if (j < a.J) {
+    double m[kMaxSplits], sv[kMaxSplits];
+#pragma unroll
+    for (int q = 0; q < kMaxSplits; ++q) {  // all loads first, then the merges
+      m[q] = q < ns ? d.pm[(int64_t)q * a.J + j] : -INFINITY;
+      sv[q] = q < ns ? d.ps[(int64_t)q * a.J + j] : 0.0;
+    }
+    Lse l;
+    l.init();
+#pragma unroll
+    for (int q = 0; q < kMaxSplits; ++q) l.merge(m[q], sv[q]);
+    finish_col(a, d, j, l.value(), slot_g_prev, slot_g_out, KNOPP, errp, fail, big);
+  }
+  if (KNOPP) {
+    errp = wave_sum(errp);
+    if (lane_id() == 0) red[wave_id()] = errp;
+    if (__any(fail) && lane_id() == 0) atomicOr((unsigned long long*)&d.st[ST_FAIL], 1ull);
+    __syncthreads();
+    if (threadIdx.x == 0) d.errpart[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  } else if (__any(big) && lane_id() == 0) {
+    atomicOr((unsigned long long*)&d.st[ST_BIG], 2ull);
   }
 }
 
@@ -523,22 +598,73 @@ static SkArgs sk_args(const gnnea_sinkhorn* p) {
   return a;
 }
 
+// Launch configuration of the two passes.  variant = 10*row + col (0 = default); the others
+// exist for in-process A/B timing (tools/microbench.py) and are all exercised by the tests.
+//   row: 0 wave/row CH 8 | 1 wave/row CH 4 | 2 wave/row CH 16 | 3 4 waves/row CH 12 | 4 2 waves/row CH 8
+//   col: 0 split 64-col CH 8 + combine | 1 fused 16 cols CH 16 | 2 fused 8 cols CH 12 | 3 split CH 4
+template <typename T, bool KNOPP>
+static void launch_row(int rv, const T* C, const SkArgs& a, const SkDev& d, int it, int si,
+                       int so, hipStream_t s) {
+  const int I = a.I;
+  switch (rv) {
+    case 1: hipLaunchKernelGGL((k_sk_row<T, KNOPP, 4, 1>), dim3(div_up(I, 4)), dim3(256), 0, s, C, a, d, it, si, so); break;
+    case 2: hipLaunchKernelGGL((k_sk_row<T, KNOPP, 16, 1>), dim3(div_up(I, 4)), dim3(256), 0, s, C, a, d, it, si, so); break;
+    case 3: hipLaunchKernelGGL((k_sk_row<T, KNOPP, 12, 4>), dim3(I), dim3(256), 0, s, C, a, d, it, si, so); break;
+    case 4: hipLaunchKernelGGL((k_sk_row<T, KNOPP, 8, 2>), dim3(div_up(I, 2)), dim3(256), 0, s, C, a, d, it, si, so); break;
+    default: hipLaunchKernelGGL((k_sk_row<T, KNOPP, 8, 1>), dim3(div_up(I, 4)), dim3(256), 0, s, C, a, d, it, si, so); break;
+  }
+}
+
+static int col_splits(int I, int J) {
+  const int strips = (J + 63) / 64;
+  int ns = (512 + strips - 1) / strips;
+  const int by_rows = (I + 63) / 64;
+  ns = ns > by_rows ? by_rows : ns;
+  ns = ns > kMaxSplits ? kMaxSplits : ns;
+  return ns < 1 ? 1 : ns;
+}
+
+template <typename T, bool KNOPP>
+static void launch_col(int cv, const T* C, const SkArgs& a, SkDev& d, int it, int sf, int sgp,
+                       int sgo, hipStream_t s) {
+  const int J = a.J;
+  switch (cv) {
+    case 1:
+      d.ncb = div_up(J, 16);
+      hipLaunchKernelGGL((k_sk_col_fused<T, KNOPP, 16, 16>), dim3(d.ncb), dim3(1024), 0, s, C, a, d, it, sf, sgp, sgo);
+      break;
+    case 2:
+      d.ncb = div_up(J, 8);
+      hipLaunchKernelGGL((k_sk_col_fused<T, KNOPP, 8, 12>), dim3(d.ncb), dim3(1024), 0, s, C, a, d, it, sf, sgp, sgo);
+      break;
+    default: {
+      const int ns = col_splits(a.I, J);
+      const int rps = (a.I + ns - 1) / ns;
+      d.ncb = div_up(J, 256);
+      if (cv == 3)
+        hipLaunchKernelGGL((k_sk_col_part<T, KNOPP, 4>), dim3(div_up(J, 64), ns), dim3(1024), 0, s, C, a, d, sf, rps);
+      else
+        hipLaunchKernelGGL((k_sk_col_part<T, KNOPP, 8>), dim3(div_up(J, 64), ns), dim3(1024), 0, s, C, a, d, sf, rps);
+      hipLaunchKernelGGL(k_sk_col_combine<KNOPP>, dim3(d.ncb), dim3(256), 0, s, a, d, ns, sgp, sgo);
+    }
+  }
+}
+
 template <typename T>
 static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t s) {
   SkArgs a = sk_args(p);
   SkDev d = sk_dev(p);
-  const dim3 grow(p->I), gcol(d.ncb), gabs(div_up(p->I, 4));
+  const int rv = (p->variant / 10) % 10, cv = p->variant % 10;
+  const dim3 gabs(div_up(p->I, 4));
   const T* C = (const T*)p->C;
   for (int it = first; it < first + count; ++it) {
     const int cur = it & 1, prev = (it + 1) & 1;
     if (p->mode == GNNEA_SK_KNOPP) {
-      hipLaunchKernelGGL((k_sk_col<T, true>), gcol, dim3(1024), 0, s, C, a, d, it, prev, prev,
-                         cur);
-      hipLaunchKernelGGL((k_sk_row<T, true>), grow, dim3(256), 0, s, C, a, d, it, cur, cur);
+      launch_col<T, true>(cv, C, a, d, it, prev, prev, cur, s);  // sets d.ncb for the row pass
+      launch_row<T, true>(rv, C, a, d, it, cur, cur, s);
     } else {
-      hipLaunchKernelGGL((k_sk_row<T, false>), grow, dim3(256), 0, s, C, a, d, it, prev, cur);
-      hipLaunchKernelGGL((k_sk_col<T, false>), gcol, dim3(1024), 0, s, C, a, d, it, cur, prev,
-                         cur);
+      launch_row<T, false>(rv, C, a, d, it, prev, cur, s);
+      launch_col<T, false>(cv, C, a, d, it, cur, prev, cur, s);
       hipLaunchKernelGGL(k_sk_absorb_rows<T>, gabs, dim3(256), 0, s, C, a, d, it, cur,
                          p->max_iter, 0);
       hipLaunchKernelGGL(k_sk_absorb_final, dim3(1), dim3(1024), 0, s, a, d, it, cur,

@@ -52,6 +52,8 @@ class SinkhornProblem(ctypes.Structure):
         ("tol", _f64),
         ("max_iter", ctypes.c_int),
         ("iters_run", ctypes.c_int),
+        ("variant", ctypes.c_int),
+        ("reserved", ctypes.c_int),
         ("ws", _p),
     ]
 

@@ -37,7 +37,7 @@ def _status(ws):
 
 
 def solve(mode, C, log_a, log_b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
-          want_plan=True, batch=10):
+          want_plan=True, batch=10, variant=0):
     """Run one Sinkhorn solve; C is [I, J] fp32 / fp64 on a HIP device."""
     _lib.require_device(C, log_a, log_b)
     if C.dim() != 2:
@@ -59,7 +59,7 @@ def solve(mode, C, log_a, log_b, eps, tol, max_iter, p=1.0, plan_dtype=torch.flo
         mode=mode, c_dtype=_lib.GNNEA_F32 if C.dtype == torch.float32 else _lib.GNNEA_F64,
         I=I, J=J, ldc=C.stride(0), C=C.data_ptr(), log_a=la.data_ptr(), log_b=lb.data_ptr(),
         eps=float(eps), p=float(p), tol=float(tol), max_iter=int(max_iter), iters_run=0,
-        ws=ws.data_ptr())
+        variant=int(variant), reserved=0, ws=ws.data_ptr())
     pp = ctypes.byref(prob)
     st = stream_of(dev)
     with torch.cuda.device(dev):

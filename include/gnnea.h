@@ -190,6 +190,8 @@ typedef struct gnnea_sinkhorn {
   double tol;       /* stopThr (KNOPP) or tol */
   int max_iter;     /* numItermax / numIterMax */
   int iters_run;    /* iterations enqueued so far (read by gnnea_sinkhorn_finish) */
+  int variant;      /* pass launch configuration, 0 = default (others: tuning A/B) */
+  int reserved;
   void* ws;         /* device workspace of gnnea_sinkhorn_ws_bytes(I, J) bytes */
 } gnnea_sinkhorn;
 

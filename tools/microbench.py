@@ -132,17 +132,23 @@ def main():
         B = 3000
         M = torch.rand(B, B, device=dev, generator=g)
         la = torch.zeros(B, dtype=torch.float64, device=dev)
+        variants = [int(v) for v in os.environ.get("SK_VARIANTS", "0").split(",")]
         for name, mode, C in (("knopp_f32C", _lib.GNNEA_SK_KNOPP, M),
                               ("stab_f64C", _lib.GNNEA_SK_STAB, M.double())):
-            ts = []
-            for it in (50, 550):
-                solve(mode, C, la, la, 0.01, -1.0, it, want_plan=False, batch=100)
-                torch.cuda.synchronize()
-                s = time.perf_counter()
-                solve(mode, C, la, la, 0.01, -1.0, it, want_plan=False, batch=100)
-                torch.cuda.synchronize()
-                ts.append(time.perf_counter() - s)
-            res["sinkhorn_" + name] = {"us_per_iter": (ts[1] - ts[0]) / 500 * 1e6}
+            for var in variants:
+                best = []
+                for rnd in range(3):  # interleaved rounds, median
+                    ts = []
+                    for it in (50, 550):
+                        torch.cuda.synchronize()
+                        s = time.perf_counter()
+                        solve(mode, C, la, la, 0.01, -1.0, it, want_plan=False, batch=100,
+                              variant=var)
+                        torch.cuda.synchronize()
+                        ts.append(time.perf_counter() - s)
+                    best.append((ts[1] - ts[0]) / 500 * 1e6)
+                key = "sinkhorn_" + name + ("" if var == 0 else "_v%d" % var)
+                res[key] = {"us_per_iter": float(np.median(best))}
     print(json.dumps(res, indent=1))
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
