@@ -601,7 +601,8 @@ static SkArgs sk_args(const gnnea_sinkhorn* p) {
 // Launch configuration of the two passes.  variant = 10*row + col (0 = default); the others
 // exist for in-process A/B timing (tools/microbench.py) and are all exercised by the tests.
 //   row: 0 wave/row CH 8 | 1 wave/row CH 4 | 2 wave/row CH 16 | 3 4 waves/row CH 12 | 4 2 waves/row CH 8
-//   col: 0 split 64-col CH 8 + combine | 1 fused 16 cols CH 16 | 2 fused 8 cols CH 12 | 3 split CH 4
+//   col: 0 fused 16 cols CH 16 | 1 split 64-col CH 8 + combine | 2 fused 8 cols CH 12 | 3 split CH 4
+// Default (0) = fastest measured at B = 3000 (profiles/r01_microbench_sk_variants.json).
 template <typename T, bool KNOPP>
 static void launch_row(int rv, const T* C, const SkArgs& a, const SkDev& d, int it, int si,
                        int so, hipStream_t s) {
@@ -629,7 +630,7 @@ static void launch_col(int cv, const T* C, const SkArgs& a, SkDev& d, int it, in
                        int sgo, hipStream_t s) {
   const int J = a.J;
   switch (cv) {
-    case 1:
+    case 0:
       d.ncb = div_up(J, 16);
       hipLaunchKernelGGL((k_sk_col_fused<T, KNOPP, 16, 16>), dim3(d.ncb), dim3(1024), 0, s, C, a, d, it, sf, sgp, sgo);
       break;
@@ -637,7 +638,7 @@ static void launch_col(int cv, const T* C, const SkArgs& a, SkDev& d, int it, in
       d.ncb = div_up(J, 8);
       hipLaunchKernelGGL((k_sk_col_fused<T, KNOPP, 8, 12>), dim3(d.ncb), dim3(1024), 0, s, C, a, d, it, sf, sgp, sgo);
       break;
-    default: {
+    default: {  // 1, 3: split + combine
       const int ns = col_splits(a.I, J);
       const int rps = (a.I + ns - 1) / ns;
       d.ncb = div_up(J, 256);
