@@ -119,6 +119,9 @@ def main():
                     help="entities per KG (default: cfg-4, 1M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sinkhorn", action="store_true")
+    ap.add_argument("--partition", choices=("features", "rows"), default="features",
+                    help="inside a KG group: feature-column slices (no exchange) or row blocks "
+                         "with the RCCL halo all-gather")
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank logic on ONE device with gloo (halo staged through host)")
     args = ap.parse_args()
@@ -140,15 +143,19 @@ def main():
 
     t0 = time.time()
     n = args.entities
-    shard = KGShard(n, shard_t(n), synth.CONFIGS["cfg4"]["n_rel"], rank, world, device)
+    shard = KGShard(n, shard_t(n), synth.CONFIGS["cfg4"]["n_rel"], rank, world, device,
+                    kind=args.partition, D=D)
+    part = shard.part
+    Dl = part.col1 - part.col0  # feature columns this rank aggregates
     log("rank %d: shard rows %d nnz %d built in %.1fs" % (rank, shard.n_rows, shard.nnz,
                                                          time.time() - t0))
     gen = torch.Generator(device=device).manual_seed(1 + rank)
-    h_local = torch.randn(shard.n_rows if world > 1 else shard.n_cols, D, device=device,
+    h_local = torch.randn(shard.n_rows if world > 1 else shard.n_cols, Dl, device=device,
                           generator=gen)
     h_local /= h_local.norm(dim=1, keepdim=True)
-    h_full = torch.empty(shard.n_cols, D, device=device) if shard.g > 1 else None
-    y = torch.empty(shard.n_rows, D, device=device)
+    h_full = (torch.empty(shard.n_cols, Dl, device=device)
+              if shard.g > 1 and part.kind == "rows" else None)
+    y = torch.empty(shard.n_rows, Dl, device=device)
 
     def step(ev=None):
         shard.aggregate(h_local, h_full, y, _lib.GNNEA_ACT_RELU, ev)
@@ -167,7 +174,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    if shard.g == 1:
+    if shard.g == 1 or part.kind == "features":
         kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     else:  # own-block + remote-block SpMM launches (the wait for the halo excluded)
         kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3])
@@ -186,7 +193,7 @@ def main():
     value = total_nnz / (elapsed / args.steps)
 
     if rank == 0:
-        traffic = gather_model_bytes(shard.n_rows, shard.nnz, D)
+        traffic = gather_model_bytes(shard.n_rows, shard.nnz, Dl)
         achieved = traffic / (kernel_ms * 1e-3) / 1e9
         pmc_bytes, pmc_src = pmc_traffic(world)
         line = {
@@ -199,15 +206,16 @@ def main():
                                    % (n, shard_t(n), D),
                        "nnz": int(total_nnz), "nodes": 2 * n, "D": D,
                        "parallelism": "single GPU" if world == 1 else
-                       "row-sharded, %d KG groups of %d GPUs, RCCL halo all-gather" % (
-                           2, shard.g)},
+                       ("2 KG groups of %d GPUs, feature-column slices (no exchange)" % shard.g
+                        if part.kind == "features" else
+                        "2 KG groups of %d GPUs, row blocks + RCCL halo all-gather" % shard.g)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_bytes, "traffic_source": pmc_src,
                          "kernel": "gnnea::k_spmm_v4<relu,act,2>",
                          "kernel_ms": round(kernel_ms, 4),
                          "bytes_per_launch": int(traffic),
-                         "model": "gather: 4(N+1)+8E+4ED+4ND (rank 0 shard)"},
+                         "model": "gather: 4(N+1)+8E+4ED+4ND (rank 0 shard, D = its slice)"},
         }
         if world == 1 and not args.no_sinkhorn:
             try:

@@ -1,13 +1,17 @@
-"""Node sharding of the two-KG graph across the GPUs of one node.
+"""Sharding of the two-KG graph across the GPUs of one node.
 
 Layout (one process per GPU, torch.distributed; backend "nccl" is RCCL over xGMI):
   * the adjacency is block-diagonal over the two KGs (no cross-KG entries), so ranks
-    [0, W/2) serve KG1 and [W/2, W) serve KG2 — no traffic between the two groups;
-  * inside a KG group of g = W/2 ranks each rank owns a contiguous block of n/g destination
-    rows; its CSR keeps KG-local column ids;
-  * per aggregation the group all-gathers the projected rows (the halo: on uniform random graphs
-    nearly every remote row is referenced) with RCCL, then every rank runs the CSR SpMM on its
-    rows.  W = 1 keeps the whole graph on one GPU; W = 2 is one KG per GPU with no exchange.
+    [0, W/2) serve KG1 and [W/2, W) serve KG2 — no traffic between the two groups
+    (W = 1 keeps the whole graph on one GPU; W = 2 is one KG per GPU, nothing to exchange);
+  * inside a KG group of g = W/2 ranks, two partitions are implemented:
+    - "features" (default): every rank holds the whole KG adjacency and a 16-B-aligned slice
+      of the feature columns (300 = 76+76+76+72 at g = 4).  relu(A·H) is column-separable,
+      so the aggregation needs NO exchange; in a full layer the group exchange moves to the
+      projection input (all-gather of the previous layer's column slices, same volume);
+    - "rows": each rank owns n/g destination rows (KG-local column ids) and all-gathers the
+      group's projected rows (the halo: on uniform random graphs nearly every remote row is
+      referenced) with RCCL, overlapped with the aggregation over its own rows.
 The partition / exchange logic is device-independent (numpy + torch.distributed) and is
 exercised with gloo on CPU in tests/test_dist_gloo.py; the GPU path adds only the CSR upload.
 """
@@ -18,11 +22,19 @@ import torch.distributed as dist
 from . import synth
 
 
+def feature_slices(D, g):
+    """g contiguous slices of D columns, each a multiple of 4 wide (16-B rows) but the last."""
+    base = (D // g + 3) // 4 * 4
+    cuts = [min(D, k * base) for k in range(g)] + [D]
+    return [(cuts[k], cuts[k + 1]) for k in range(g)]
+
+
 class Partition:
     """Which rows / columns of the two-KG adjacency rank `rank` of `world` owns."""
 
-    def __init__(self, n, rank, world):
-        self.n, self.rank, self.world = n, rank, world
+    def __init__(self, n, rank, world, kind="rows", D=300):
+        self.n, self.rank, self.world, self.kind = n, rank, world, kind
+        self.col0, self.col1 = 0, D
         if world == 1:
             self.kg, self.g, self.li = None, 1, 0
             self.n_cols = 2 * n
@@ -32,18 +44,27 @@ class Partition:
             if world % 2:
                 raise ValueError("gnnea.dist: world size must be 1 or even (two KG groups)")
             self.g = world // 2
-            if n % self.g:
+            if kind == "rows" and n % self.g:
                 raise ValueError("gnnea.dist: entities per KG must divide by the group size")
+            if kind not in ("rows", "features"):
+                raise ValueError("gnnea.dist: partition must be 'rows' or 'features'")
             self.kg = rank // self.g
             self.li = rank % self.g
             self.n_cols = n
-            rows = n // self.g
-            self.row0, self.row1 = self.li * rows, (self.li + 1) * rows
+            if kind == "features":
+                self.row0, self.row1 = 0, n
+                self.col0, self.col1 = feature_slices(D, self.g)[self.li]
+            else:
+                rows = n // self.g
+                self.row0, self.row1 = self.li * rows, (self.li + 1) * rows
             self.global_row0 = self.kg * n + self.row0
 
     @property
     def n_rows(self):
         return self.row1 - self.row0
+
+    def col0_col1(self):
+        return self.col0, self.col1
 
     def group_ranks(self, kg):
         return list(range(kg * self.g, (kg + 1) * self.g))
@@ -97,9 +118,9 @@ def halo_gather(h_local, h_full, group, group_size, async_op=False):
 class KGShard:
     """A rank's device-resident CSR shard of the synthetic cfg graph."""
 
-    def __init__(self, n, t, n_rel, rank, world, device, seed=0):
+    def __init__(self, n, t, n_rel, rank, world, device, seed=0, kind="rows", D=300):
         from .graph import DeviceCSR
-        self.part = Partition(n, rank, world)
+        self.part = Partition(n, rank, world, kind, D)
         self.n, self.device = n, device
         triples = synth.kg_pair_triples(n, t, n_rel, seed=seed)
         r, c, v = shard_coo(triples, n, t, self.part)
@@ -109,7 +130,7 @@ class KGShard:
             return DeviceCSR.from_coo(torch.from_numpy(rr.astype(np.int32)).to(device),
                                       torch.from_numpy(cc.astype(np.int32)).to(device),
                                       torch.from_numpy(vv).to(device), self.part.n_rows, ncols)
-        if self.part.g == 1:
+        if self.part.g == 1 or kind == "features":
             self.csr = up(r, c, v, self.part.n_cols)
             self.csr_own = self.csr_remote = None
         else:
@@ -117,7 +138,7 @@ class KGShard:
             self.csr = None
             self.csr_own = up(ro, co, vo, self.part.n_rows)
             self.csr_remote = up(rr, cr, vr, self.part.n_cols)
-        self.group = make_groups(self.part)
+        self.group = make_groups(self.part) if kind == "rows" else None
 
     @property
     def g(self):
@@ -137,7 +158,7 @@ class KGShard:
         from . import ops
         from ._lib import GNNEA_ACT_IDENTITY
         rec = (lambda k: events[k].record()) if events is not None else (lambda k: None)
-        if self.part.g == 1:
+        if self.part.g == 1 or self.part.kind == "features":  # no exchange in the aggregation
             rec(0)
             ops.spmm(self.csr, h_local, act, out=out)
             rec(1)

@@ -22,7 +22,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, n, t, q):
+def _worker(rank, world, port, n, t, q, kind="rows"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "gnn-mtl_amd"))
@@ -34,7 +34,7 @@ def _worker(rank, world, port, n, t, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        part = Partition(n, rank, world)
+        part = Partition(n, rank, world, kind, 16)
         group = make_groups(part)
         triples = synth.kg_pair_triples(n, t, 50)
         r, c, v = shard_coo(triples, n, t, part)
@@ -44,7 +44,16 @@ def _worker(rank, world, port, n, t, q):
         else:
             h_local = H[part.global_row0:part.global_row0 + part.n_rows]
         h_full = torch.empty(part.n_cols, 16, dtype=torch.float64)
-        if part.g == 1:
+        if kind == "features" and part.g > 1:
+            # column slice of the whole KG: no exchange; gather slices for the check below
+            hk = H[part.kg * n:(part.kg + 1) * n, part.col0:part.col1]
+            ys = coo_aggregate(r, c, v, part.n_rows, hk)
+            sl = [torch.empty(n, b - a, dtype=torch.float64)
+                  for a, b in (Partition(n, k, world, kind, 16).col0_col1()
+                               for k in part.group_ranks(part.kg))]
+            dist.all_gather(sl, ys, group=group)
+            y = torch.cat(sl, dim=1)
+        elif part.g == 1:
             y = coo_aggregate(r, c, v, part.n_rows, h_local)
         else:
             # the product's overlap split: owned block from h_local, the rest from the halo
@@ -55,6 +64,8 @@ def _worker(rank, world, port, n, t, q):
         outs = [torch.empty_like(y) for _ in range(world)]
         dist.all_gather(outs, y)
         if rank == 0:
+            if kind == "features" and part.g > 1:  # every group member holds the whole KG
+                outs = [outs[0], outs[part.g]]
             full = torch.cat(outs)  # ranks are ordered KG1 rows then KG2 rows
             R, Cc, V = synth.adjacency_coo(triples, 2 * n, reference_order=False)
             ref = coo_aggregate(R, Cc, V, 2 * n, H)
@@ -63,18 +74,29 @@ def _worker(rank, world, port, n, t, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_aggregation_matches_single_process(world):
+@pytest.mark.parametrize("world,kind", [(2, "rows"), (4, "rows"), (4, "features"),
+                                        (8, "features")])
+def test_sharded_aggregation_matches_single_process(world, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 200, 700, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 200, 700, q, kind))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) < 1e-12
+
+
+def test_feature_slices_aligned():
+    from gnnea.dist import feature_slices
+    for D, g in ((300, 2), (300, 4), (16, 4), (301, 3)):
+        sl = feature_slices(D, g)
+        assert sl[0][0] == 0 and sl[-1][1] == D
+        assert all(a % 4 == 0 for a, _ in sl)
+        assert all(sl[k][1] == sl[k + 1][0] for k in range(g - 1))
 
 
 def test_partition_covers_every_row_once():

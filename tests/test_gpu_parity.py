@@ -154,7 +154,7 @@ def _random_coo(rng, n_rows, n_cols, nnz, dup=True):
     return r, c, v
 
 
-@pytest.mark.parametrize("D", [1, 3, 4, 64, 75, 128, 252, 300, 512, 1024])
+@pytest.mark.parametrize("D", [1, 3, 4, 64, 72, 75, 76, 128, 148, 152, 252, 300, 512, 1024])
 def test_spmm_shapes_vs_oracle(device, D):
     from gnnea import ops
     from gnnea.graph import DeviceCSR
@@ -375,3 +375,27 @@ def test_sinkhorn_pass_variants(device, variant):
     t, m1, m2, K = osk.stabilized(M, a / I, b / I, reg, 100, 1e-9)
     assert rel_err(res.plan.cpu(), K) < TOL64
     assert abs(res.transport_new - t) <= 1e-9 * abs(t)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_feature_partition_on_device(device, world):
+    """Feature-column sharding: each rank's slice of relu(A.H) over its whole KG equals the
+    matching columns of the single-GPU result."""
+    from gnnea import ops, synth
+    from gnnea.dist import Partition, shard_coo
+    from gnnea.graph import DeviceCSR
+    n, t = 800, 3000
+    tr = synth.kg_pair_triples(n, t, 50)
+    H = torch.from_numpy(synth.features(2 * n, 300, seed=2)).to(device)
+    R, C, V = synth.adjacency_coo(tr, 2 * n, reference_order=False)
+    full = DeviceCSR.from_coo(torch.from_numpy(R).to(device), torch.from_numpy(C).to(device),
+                              torch.from_numpy(V).to(device), 2 * n, 2 * n)
+    ref = ops.spmm(full, H, 1).cpu()
+    for rank in range(world):
+        p = Partition(n, rank, world, "features", 300)
+        r, c, v = shard_coo(tr, n, t, p)
+        csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                                 torch.from_numpy(v).to(device), n, n)
+        h = H[p.kg * n:(p.kg + 1) * n, p.col0:p.col1].contiguous()
+        y = ops.spmm(csr, h, 1).cpu()
+        assert rel_err(y, ref[p.kg * n:(p.kg + 1) * n, p.col0:p.col1]) < TOL32
