@@ -95,6 +95,11 @@ SIGNATURES = {
                                               ctypes.c_int, _p]),
     "gnnea_sinkhorn_finish": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p, ctypes.c_int,
                                              _i64, _p, _p, _p]),
+    "gnnea_l1_keys_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _i64, _p]),
+    "gnnea_l1_pairs_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i32, _i32, _p, _p]),
+    "gnnea_l1_rank_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "gnnea_topk_rows_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _i64, _p, _i64, _i32,
+                                           _i32, _p, _p, _i32, _p, _p]),
 }
 
 _LIB = None

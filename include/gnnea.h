@@ -205,6 +205,32 @@ int gnnea_sinkhorn_iterate(const gnnea_sinkhorn* prob, int first, int count, voi
 int gnnea_sinkhorn_finish(const gnnea_sinkhorn* prob, void* plan, int plan_dtype, int64_t ldp,
                           double* row_sum, double* col_sum, void* stream);
 
+/* ------------------------------------------------------------------------------------------ *
+ * §8f #1. L1 (cityblock) distance search.  scipy.spatial.distance.cdist(.., 'cityblock') as
+ * used by BaseModel.get_neg (models/models_ea.py:19-30), get_hits (utils/eval_utils.py:71-98)
+ * and UEAModel.generate_pairs (models/models_ea.py:143-167).  fp32 rows, fp64 sums of
+ * |q_d - x_d| in d order: bit-identical to scipy's fp64 distances.  Row-major, ld in elements.
+ * ------------------------------------------------------------------------------------------ */
+/* keys[q*ldk + x] = (float) L1(Q[q], X[x])   (nq x nx; monotone rounding of the exact value) */
+int gnnea_l1_keys_f32(const float* Q, int64_t ldq, int32_t nq, const float* X, int64_t ldx,
+                      int32_t nx, int32_t D, float* keys, int64_t ldk, void* stream);
+/* out[i] = L1(A[i], B[i]) in fp64 (the diagonal of cdist(A, B)) */
+int gnnea_l1_pairs_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int32_t n,
+                       int32_t D, double* out, void* stream);
+/* rank[q] = #{x : L1(Q[q],X[x]) < diag[q]} + #{x < q : L1(Q[q],X[x]) == diag[q]}: the position of
+ * x = q in a stable argsort of row q (get_hits' rank_index).  rank is zeroed by the call. */
+int gnnea_l1_rank_f32(const float* Q, int64_t ldq, int32_t nq, const float* X, int64_t ldx,
+                      int32_t nx, int32_t D, const double* diag, int32_t* rank, void* stream);
+/* Per row q of keys (from gnnea_l1_keys_f32 of the same Q, X): the K smallest exact distances
+ * ordered by (distance, index), entries [skip, K) written to out_idx / out_dist (nullable) rows
+ * of stride ldo.  get_neg: K = k+1, skip = 1.  K <= 512.  *overflow (nullable) counts rows where
+ * more than 1024 - K candidates shared the K-th fp32 key (selection then keeps the lowest
+ * indices of that key). */
+int gnnea_topk_rows_f32(const float* keys, int64_t ldk, int32_t nq, int32_t nx, int32_t K,
+                        const float* Q, int64_t ldq, const float* X, int64_t ldx, int32_t D,
+                        int32_t skip, int64_t* out_idx, double* out_dist, int32_t ldo,
+                        int32_t* overflow, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -201,5 +201,51 @@ def main():
     print("golden fixtures written to", HERE)
 
 
+def gen_l1():
+    """§8f #1 fixtures: get_neg / get_hits / eval_at_1 / generate_pairs of the reference."""
+    _synth()
+    _placeholders()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import models.models_ea as RM
+    import utils.eval_utils as REV
+    rng = np.random.default_rng(11)
+    n, D = 1000, 300
+    left = (0.1 * rng.standard_normal((n, D))).astype(np.float32)
+    # right entity = left + noise: mixed hit ranks (Hits@1 well below 100)
+    right = (left + 0.3 * rng.standard_normal((n, D))).astype(np.float32)
+    vec = np.concatenate([left, right])
+    perm = rng.permutation(n)
+    train = np.stack([perm[:150], perm[:150] + n], 1).astype(np.int64)
+    test = np.stack([perm[150:550], perm[150:550] + n], 1).astype(np.int64)
+    out = {"vec": vec, "train": train, "test": test}
+    tv = torch.from_numpy(vec)
+    out["neg_right"] = RM.BaseModel.get_neg(None, train[:, 0], tv, 25)
+    out["neg2_left"] = RM.BaseModel.get_neg(None, train[:, 1], tv, 25)
+    for split, pairs in (("train", train), ("test", test)):
+        m = REV.get_hits(tv, pairs)
+        out["hits_%s_keys" % split] = np.array(list(m.keys()))
+        out["hits_%s_vals" % split] = np.array(list(m.values()), dtype=np.float64)
+    out["eval_at_1"] = np.array(float(REV.eval_at_1(tv, {"test": test})))
+    holder = types.SimpleNamespace(ILL=None)
+    e1 = 700
+    index1 = {i: int(x) for i, x in enumerate(rng.permutation(n)[:e1])}
+    index2 = {i: int(x) + n for i, x in enumerate(rng.permutation(n)[:e1])}
+    RM.UEAModel.generate_pairs(holder, tv, {"e1": e1, "e2": e1, "index1": index1,
+                                            "index2": index2}, 200)
+    out["gp_index1"] = np.array([index1[i] for i in range(e1)])
+    out["gp_index2"] = np.array([index2[i] for i in range(e1)])
+    out["gp_ILL"] = np.asarray(holder.ILL, dtype=np.int64)
+    RM.UEAModel.generate_pairs(holder, tv, {"e1": e1, "e2": e1, "index1": index1,
+                                            "index2": index2}, 30)
+    out["gp_ILL30"] = np.asarray(holder.ILL, dtype=np.int64)
+    np.savez_compressed(os.path.join(HERE, "l1_search.npz"), **out)
+    print("l1 fixtures written to", HERE)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["l1"]:
+        gen_l1()
+    else:
+        main()
+        gen_l1()

@@ -1,0 +1,121 @@
+"""§8f #1 parity: device L1 searches (gnnea_l1_*, gnnea_topk_rows_f32) vs the reference's
+scipy-based get_neg / get_hits / eval_at_1 / generate_pairs (golden fixtures) and vs the oracle.
+
+Distances are compared bit-exactly (fp64 sums of exact terms); index outputs bit-exactly.
+"""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import l1 as ol1
+
+pytestmark = pytest.mark.gpu
+
+
+def _fixture(golden, device):
+    f = golden("l1_search")
+    return f, torch.from_numpy(f["vec"]).to(device)
+
+
+def test_get_neg_vs_reference(golden, device):
+    from models.models_ea import BaseModel
+    f, vec = _fixture(golden, device)
+    tr = f["train"]
+    assert (BaseModel.get_neg(None, tr[:, 0], vec, 25) == f["neg_right"]).all()
+    assert (BaseModel.get_neg(None, tr[:, 1], vec, 25) == f["neg2_left"]).all()
+    # the reference passes host tensors: same result after the upload
+    assert (BaseModel.get_neg(None, tr[:, 0], vec.cpu(), 25) == f["neg_right"]).all()
+
+
+def test_get_hits_vs_reference(golden, device):
+    from utils.eval_utils import eval_at_1, get_hits
+    f, vec = _fixture(golden, device)
+    for split in ("train", "test"):
+        m = get_hits(vec, f[split])
+        assert list(m) == list(f["hits_%s_keys" % split])
+        assert list(m.values()) == list(f["hits_%s_vals" % split])
+    m = get_hits(vec.cpu(), f["test"], top_k=[1])
+    assert m == {"Hits@1_l": f["hits_test_vals"][0], "Hits@1_r": f["hits_test_vals"][4]}
+    assert abs(float(eval_at_1(vec, {"test": f["test"]})) - float(f["eval_at_1"])) < 1e-4
+
+
+def test_generate_pairs_vs_reference(golden, device):
+    from models.models_ea import UEAModel
+    f, vec = _fixture(golden, device)
+    e1 = len(f["gp_index1"])
+    data = {"e1": e1, "e2": e1, "index1": dict(enumerate(f["gp_index1"].tolist())),
+            "index2": dict(enumerate(f["gp_index2"].tolist()))}
+    for key, bsz in (("gp_ILL", 200), ("gp_ILL30", 30)):
+        holder = types.SimpleNamespace(ILL=None)
+        UEAModel.generate_pairs(holder, vec, data, bsz)
+        assert (holder.ILL == f[key]).all()
+
+
+def test_distances_bit_exact(device):
+    from gnnea import l1
+    rng = np.random.default_rng(3)
+    for nq, nx, D in ((1, 1, 1), (5, 70, 3), (130, 257, 300), (64, 64, 33), (77, 1000, 100)):
+        A = rng.standard_normal((nq, D)).astype(np.float32) * rng.uniform(0.01, 3)
+        B = rng.standard_normal((nx, D)).astype(np.float32)
+        ref = ol1.cityblock(A, B)
+        k = l1.keys(torch.from_numpy(A).to(device), torch.from_numpy(B).to(device)).cpu().numpy()
+        assert (k == ref.astype(np.float32)).all()
+        n = min(nq, nx)
+        d = l1.pairs(torch.from_numpy(A[:n]).to(device), torch.from_numpy(B[:n]).to(device))
+        assert (d.cpu().numpy() == np.diag(ref[:n, :n])).all()
+
+
+@pytest.mark.parametrize("nq,nx,D,K,skip", [(40, 3000, 300, 26, 1), (7, 513, 64, 1, 0),
+                                            (300, 2000, 100, 512, 0), (3, 600, 5, 600 // 2, 2)])
+def test_topk_vs_oracle(device, nq, nx, D, K, skip):
+    from gnnea import l1
+    rng = np.random.default_rng(nq + nx)
+    X = (0.1 * rng.standard_normal((nx, D))).astype(np.float32)
+    Q = X[rng.integers(0, nx, nq)] + (0.05 * rng.standard_normal((nq, D))).astype(np.float32)
+    S = ol1.cityblock(Q, X)
+    order = np.argsort(S, axis=1, kind="stable")[:, skip:K]
+    idx, dist = l1.topk(torch.from_numpy(Q).to(device), torch.from_numpy(X).to(device), K,
+                        skip, want_dist=True)
+    assert (idx.cpu().numpy() == order).all()
+    assert (dist.cpu().numpy() == np.take_along_axis(S, order, 1)).all()
+    assert int(l1.topk.last_overflow.item()) == 0
+
+
+def test_topk_ties_and_duplicates(device):
+    """Exact duplicate rows and an all-equal (collapsed) embedding: lowest indices first."""
+    from gnnea import l1
+    rng = np.random.default_rng(9)
+    X = (0.1 * rng.standard_normal((500, 16))).astype(np.float32)
+    X[100:140] = X[7]  # 41 copies of row 7
+    Q = X[[7, 100, 3]]
+    S = ol1.cityblock(Q, X)
+    order = np.argsort(S, axis=1, kind="stable")[:, :60]
+    idx = l1.topk(torch.from_numpy(Q).to(device), torch.from_numpy(X).to(device), 60)
+    assert (idx.cpu().numpy() == order).all()
+    Z = np.zeros((3000, 8), np.float32)  # every distance 0: ties beyond the candidate cap
+    idx = l1.topk(torch.from_numpy(Z[:4]).to(device), torch.from_numpy(Z).to(device), 11, 1)
+    assert (idx.cpu().numpy() == np.arange(1, 11)[None, :]).all()
+    assert int(l1.topk.last_overflow.item()) == 4
+
+
+def test_hits_ranks_with_ties(device):
+    from gnnea import l1
+    rng = np.random.default_rng(4)
+    L = np.round(rng.standard_normal((300, 4)), 1).astype(np.float32)  # many equal distances
+    R = np.round(L + 0.3 * rng.standard_normal((300, 4)), 1).astype(np.float32)
+    vec = np.concatenate([L, R])
+    pairs = np.stack([np.arange(300), np.arange(300) + 300], 1)
+    lr_ref, rl_ref = ol1.hit_ranks(vec, pairs)
+    lr, rl = l1.hits_ranks(torch.from_numpy(L).to(device), torch.from_numpy(R).to(device))
+    assert (lr.cpu().numpy() == lr_ref).all() and (rl.cpu().numpy() == rl_ref).all()
+
+
+def test_l1_rejects_bad_shapes(device):
+    from gnnea import _lib, l1
+    X = torch.zeros(10, 4, device=device)
+    with pytest.raises(ValueError):
+        l1.topk(X, X, 11)
+    with pytest.raises(_lib.GnneaError):
+        l1.topk(torch.zeros(2, 4, device=device), torch.zeros(2000, 4, device=device), 600)

@@ -102,3 +102,19 @@ def test_sinkhorn_reference_test_config(golden):
     t, m1, m2, K = osk.stabilized(M, np.full(100, 0.01), np.full(100, 0.01), 1e-4)
     assert abs(t - float(S["test_transport"])) <= 1e-10 * abs(t)
     assert rel_err(K, S["test_K"]) < 1e-10
+
+
+def test_l1_search_oracle(golden):
+    """oracle/l1.py vs the reference's get_neg / get_hits / eval_at_1 / generate_pairs."""
+    from oracle import l1 as ol1
+    f = golden("l1_search")
+    vec, tr, te = f["vec"], f["train"], f["test"]
+    assert (ol1.get_neg(tr[:, 0], vec, 25) == f["neg_right"]).all()
+    assert (ol1.get_neg(tr[:, 1], vec, 25) == f["neg2_left"]).all()
+    for split, pairs in (("train", tr), ("test", te)):
+        m = ol1.get_hits(vec, pairs)
+        assert list(m) == list(f["hits_%s_keys" % split])
+        assert list(m.values()) == list(f["hits_%s_vals" % split])
+    assert abs(ol1.eval_at_1(vec, te) - float(f["eval_at_1"])) < 1e-4  # reference: fp32 mean
+    for key, bsz in (("gp_ILL", 200), ("gp_ILL30", 30)):
+        assert (ol1.mutual_pairs(vec, f["gp_index1"], f["gp_index2"], bsz) == f[key]).all()

@@ -149,6 +149,19 @@ def main():
                     best.append((ts[1] - ts[0]) / 500 * 1e6)
                 key = "sinkhorn_" + name + ("" if var == 0 else "_v%d" % var)
                 res[key] = {"us_per_iter": float(np.median(best))}
+    if want("l1"):
+        # DBP15K-sized searches: get_neg of 4500 train entities over 30k, get_hits of 10.5k pairs
+        from gnnea import l1
+        V = torch.randn(30000, D, device=dev, generator=g) * 0.1
+        Qn = V[:4500].contiguous()
+        ms = timeit(lambda: l1.keys(Qn, V), args.reps)
+        pd = 4500 * 30000 * D
+        res["l1_keys_4500x30000"] = {"ms": ms, "Gpairdims_per_s": pd / ms / 1e6}
+        ms = timeit(lambda: l1.topk(Qn, V, 126, 1), args.reps)
+        res["get_neg_4500x30000_k125"] = {"ms": ms}
+        Lh, Rh = V[:10500].contiguous(), V[10500:21000].contiguous()
+        ms = timeit(lambda: l1.hits_ranks(Lh, Rh), args.reps)
+        res["get_hits_10500"] = {"ms": ms, "Gpairdims_per_s": 2 * 10500 ** 2 * D / ms / 1e6}
     print(json.dumps(res, indent=1))
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
