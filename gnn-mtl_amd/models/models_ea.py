@@ -11,29 +11,28 @@ import random
 import numpy as np
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
-from gnnea import l1
+from gnnea import l1, margin
 from models.decoders import model2decoder
 from models.encoders import model2encoder
 from utils.eval_utils import get_hits
 from utils.ot_loss import sinkhorn
 
 
-def _index(idx, device):
-    """Device int64 copy of a host index array, cached per array object (the negatives are
+def _index(idx, device, n_rows):
+    """Checked device int64 copy of a host index array, cached per array object (negatives are
     regenerated every 50 epochs; the loss reads them every epoch)."""
     if torch.is_tensor(idx):
-        return idx.to(device=device, dtype=torch.int64)
+        return margin._idx(idx, device, n_rows)
     cache = _index.cache
     key = id(idx)
     hit = cache.get(key)
-    if hit is not None and hit[0] is idx and hit[1].device == device:
+    if hit is not None and hit[0] is idx and hit[1].device == device and hit[2] == n_rows:
         return hit[1]
-    t = torch.as_tensor(np.asarray(idx).astype(np.int64), device=device)
+    t = margin._idx(idx, device, n_rows)
     if len(cache) > 16:
         cache.clear()
-    cache[key] = (idx, t)
+    cache[key] = (idx, t, n_rows)
     return t
 
 
@@ -41,18 +40,12 @@ _index.cache = {}
 
 
 def margin_loss(outputs, left, right, neg_left, neg_right, neg2_left, neg2_right, t, k):
-    """models/models_ea.py:105-124: mean of relu(|l - r|_1 + 1 - |nl - nr|_1) over the t*k
-    negatives of both sides."""
-    dev = outputs.device
-    left, right = _index(left, dev), _index(right, dev)
-    A = torch.sum(torch.abs(outputs[left] - outputs[right]), 1)
-    D = torch.reshape(A + 1.0, [t, 1])
-    B1 = torch.sum(torch.abs(outputs[_index(neg_left, dev)] - outputs[_index(neg_right, dev)]), 1)
-    L1 = F.relu(D - torch.reshape(B1, [t, k]))
-    B2 = torch.sum(torch.abs(outputs[_index(neg2_left, dev)] - outputs[_index(neg2_right, dev)]),
-                   1)
-    L2 = F.relu(D - torch.reshape(B2, [t, k]))
-    return (torch.sum(L1) + torch.sum(L2)) / (2.0 * t * k)
+    """models/models_ea.py:105-124 (fused gather-L1-hinge kernels, gnnea.margin)."""
+    if neg_right is None or neg2_left is None:
+        raise ValueError("get_loss: negatives are not set (get_neg runs every 50 epochs)")
+    n, dev = outputs.shape[0], outputs.device
+    idx = [_index(a, dev, n) for a in (left, right, neg_left, neg_right, neg2_left, neg2_right)]
+    return margin.margin_loss(outputs, *idx, t, k, checked=True)
 
 
 class BaseModel(nn.Module):
@@ -69,7 +62,7 @@ class BaseModel(nn.Module):
         out = output.detach()
         if not out.is_cuda and torch.cuda.is_available():
             out = out.to("cuda")
-        rows = _index(np.asarray(ILL), out.device)
+        rows = _index(np.asarray(ILL), out.device, out.shape[0])
         neg = l1.topk(out[rows], out, k + 1, skip=1)
         return neg.reshape(-1).cpu().numpy()
 

@@ -231,6 +231,24 @@ int gnnea_topk_rows_f32(const float* keys, int64_t ldk, int32_t nq, int32_t nx, 
                         int32_t skip, int64_t* out_idx, double* out_dist, int32_t ldo,
                         int32_t* overflow, void* stream);
 
+/* ------------------------------------------------------------------------------------------ *
+ * §8f #2. Entity-alignment margin loss (EAModel.get_loss, models/models_ea.py:103-123; the same
+ * body in UEAModel.get_loss :169-183).  out [N, D] fp32 rows of stride ld; left/right [t] pair
+ * rows; neg_* [t*k] negative-pair rows (int64).  Forward writes A[t] = |out[left]-out[right]|_1
+ * and h[2*t*k] = relu(A_i + 1 - |out[neg_l] - out[neg_r]|_1) (side 1 then side 2); the loss is
+ * sum(h) / (2 t k).  Backward adds scale * grad_loss[0] * d(sum h)/d(out) into grad (N x ldg,
+ * caller-zeroed) with fp32 atomics; scale = 1 / (2 t k).  D <= 1024.
+ * ------------------------------------------------------------------------------------------ */
+int gnnea_margin_fwd_f32(const float* out, int64_t ld, int32_t D, int32_t t, int32_t k,
+                         const int64_t* left, const int64_t* right, const int64_t* neg_left,
+                         const int64_t* neg_right, const int64_t* neg2_left,
+                         const int64_t* neg2_right, float* A, float* h, void* stream);
+int gnnea_margin_bwd_f32(const float* out, int64_t ld, int32_t D, int32_t t, int32_t k,
+                         const int64_t* left, const int64_t* right, const int64_t* neg_left,
+                         const int64_t* neg_right, const int64_t* neg2_left,
+                         const int64_t* neg2_right, const float* h, const float* grad_loss,
+                         float scale, float* grad, int64_t ldg, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -239,6 +239,17 @@ def gen_l1():
     RM.UEAModel.generate_pairs(holder, tv, {"e1": e1, "e2": e1, "index1": index1,
                                             "index2": index2}, 30)
     out["gp_ILL30"] = np.asarray(holder.ILL, dtype=np.int64)
+    # §8f #2 margin loss with those negatives (EAModel.get_loss), value and d loss / d outputs
+    k = 25
+    holder = types.SimpleNamespace(neg_num=k, neg_right=out["neg_right"],
+                                   neg2_left=out["neg2_left"])
+    holder.neg_left = (np.ones((len(train), k)) * train[:, 0:1]).reshape(-1)
+    holder.neg2_right = (np.ones((len(train), k)) * train[:, 1:2]).reshape(-1)
+    tg = tv.clone().requires_grad_(True)
+    loss = RM.EAModel.get_loss(holder, tg, {"train": train}, "train")
+    loss.backward()
+    out["margin_loss"] = np.array(float(loss))
+    out["margin_grad"] = tg.grad.numpy()
     np.savez_compressed(os.path.join(HERE, "l1_search.npz"), **out)
     print("l1 fixtures written to", HERE)
 

@@ -119,3 +119,57 @@ def test_l1_rejects_bad_shapes(device):
         l1.topk(X, X, 11)
     with pytest.raises(_lib.GnneaError):
         l1.topk(torch.zeros(2, 4, device=device), torch.zeros(2000, 4, device=device), 600)
+
+
+# ---------------- §8f #2 margin loss ----------------
+def test_margin_loss_vs_reference(golden, device):
+    """EAModel.get_loss through the fused kernels vs the reference (fp32; tolerance 1e-5
+    norm-relative: the reference's fp32 sums are reduced in another order)."""
+    from conftest import rel_err
+    from models.models_ea import EAModel
+    f, vec = _fixture(golden, device)
+    tr, k = f["train"], 25
+    holder = types.SimpleNamespace(neg_num=k, neg_right=f["neg_right"], neg2_left=f["neg2_left"])
+    holder.neg_left = (np.ones((len(tr), k)) * tr[:, 0:1]).reshape(-1)
+    holder.neg2_right = (np.ones((len(tr), k)) * tr[:, 1:2]).reshape(-1)
+    x = vec.clone().requires_grad_(True)
+    loss = EAModel.get_loss(holder, x, {"train": tr}, "train")
+    loss.backward()
+    assert abs(float(loss.detach()) - float(f["margin_loss"])) <= 1e-5 * float(f["margin_loss"])
+    assert rel_err(x.grad.cpu().numpy(), f["margin_grad"]) < 1e-5
+
+
+@pytest.mark.parametrize("N,D,t,k,anchored", [(500, 300, 60, 7, True), (300, 37, 40, 5, False),
+                                              (2000, 1024, 16, 33, True), (50, 8, 30, 9, False)])
+def test_margin_vs_oracle(device, N, D, t, k, anchored):
+    """Active and inactive hinge terms, repeated rows, non-anchored negatives, scalar and float4
+    paths; fp32 kernel vs fp64 oracle."""
+    from conftest import rel_err
+    from gnnea.margin import margin_loss
+    from oracle import margin as om
+    rng = np.random.default_rng(D + k)
+    vec = (rng.standard_normal((N, D)) / np.sqrt(D)).astype(np.float32)
+    left = rng.integers(0, N, t)
+    right = rng.integers(0, N, t)
+    vec[right[: t // 2]] = vec[left[: t // 2]] + 0.01 * rng.standard_normal((t // 2, D))
+    if anchored:
+        nl1, nr2 = np.repeat(left, k), np.repeat(right, k)
+    else:
+        nl1, nr2 = rng.integers(0, N, t * k), rng.integers(0, N, t * k)
+    nr1, nl2 = rng.integers(0, N, t * k), rng.integers(0, N, t * k)
+    x = torch.from_numpy(vec).to(device).requires_grad_(True)
+    loss = margin_loss(x, left, right, nl1, nr1, nl2, nr2, t, k)
+    loss.backward()
+    ref_loss, ref_grad = om.margin_loss_and_grad(vec, left, right, nl1, nr1, nl2, nr2, t, k)
+    assert 0 < ref_loss
+    assert abs(float(loss) - ref_loss) <= 1e-5 * ref_loss
+    assert rel_err(x.grad.cpu().numpy(), ref_grad) < 1e-5
+
+
+def test_margin_rejects_bad_indices(device):
+    from gnnea.margin import margin_loss
+    x = torch.zeros(10, 4, device=device)
+    with pytest.raises(IndexError):
+        margin_loss(x, [0], [10], [0], [1], [2], [3], 1, 1)
+    with pytest.raises(ValueError):
+        margin_loss(x, [0], [1], [0], None, [2], [3], 1, 1)

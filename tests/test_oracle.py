@@ -118,3 +118,17 @@ def test_l1_search_oracle(golden):
     assert abs(ol1.eval_at_1(vec, te) - float(f["eval_at_1"])) < 1e-4  # reference: fp32 mean
     for key, bsz in (("gp_ILL", 200), ("gp_ILL30", 30)):
         assert (ol1.mutual_pairs(vec, f["gp_index1"], f["gp_index2"], bsz) == f[key]).all()
+
+
+def test_margin_oracle(golden):
+    """oracle/margin.py vs the reference's EAModel.get_loss (value and d loss / d outputs)."""
+    from oracle import margin as om
+    f = golden("l1_search")
+    tr, k = f["train"], 25
+    t = len(tr)
+    nl = np.repeat(tr[:, 0], k)
+    nr2 = np.repeat(tr[:, 1], k)
+    loss, grad = om.margin_loss_and_grad(f["vec"], tr[:, 0], tr[:, 1], nl, f["neg_right"],
+                                         f["neg2_left"], nr2, t, k)
+    assert abs(loss - float(f["margin_loss"])) <= 1e-5 * abs(loss)
+    assert rel_err(grad, f["margin_grad"]) < 1e-5

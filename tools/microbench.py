@@ -162,6 +162,30 @@ def main():
         Lh, Rh = V[:10500].contiguous(), V[10500:21000].contiguous()
         ms = timeit(lambda: l1.hits_ranks(Lh, Rh), args.reps)
         res["get_hits_10500"] = {"ms": ms, "Gpairdims_per_s": 2 * 10500 ** 2 * D / ms / 1e6}
+    if want("margin"):
+        # DBP15K-sized margin loss: t = 4500 train pairs, k = 125 negatives, 30k x 300 outputs
+        from gnnea.margin import margin_loss
+        Nm, tm, km = 30000, 4500, 125
+        V = (torch.randn(Nm, D, device=dev, generator=g) * 0.05).requires_grad_(True)
+        li = torch.randint(0, Nm, (tm,), device=dev, generator=g)
+        ri = torch.randint(0, Nm, (tm,), device=dev, generator=g)
+        n1 = torch.randint(0, Nm, (tm * km,), device=dev, generator=g)
+        n2 = torch.randint(0, Nm, (tm * km,), device=dev, generator=g)
+        nl, nr = li.repeat_interleave(km), ri.repeat_interleave(km)
+        args_m = (li, ri, nl, n1, n2, nr, tm, km)
+
+        def fused():
+            loss = margin_loss(V, *args_m, checked=True)
+            loss.backward()
+
+        def torch_ops():  # the reference's op sequence on the device
+            A = torch.sum(torch.abs(V[li] - V[ri]), 1).reshape(tm, 1) + 1.0
+            B1 = torch.sum(torch.abs(V[nl] - V[n1]), 1).reshape(tm, km)
+            B2 = torch.sum(torch.abs(V[n2] - V[nr]), 1).reshape(tm, km)
+            loss = (F.relu(A - B1).sum() + F.relu(A - B2).sum()) / (2.0 * tm * km)
+            loss.backward()
+        res["margin_fwd_bwd_fused"] = {"ms": timeit(fused, args.reps)}
+        res["margin_fwd_bwd_torch_ops"] = {"ms": timeit(torch_ops, args.reps)}
     print(json.dumps(res, indent=1))
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
