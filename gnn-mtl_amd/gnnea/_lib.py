@@ -101,9 +101,9 @@ SIGNATURES = {
     "gnnea_topk_rows_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _i64, _p, _i64, _i32,
                                            _i32, _p, _p, _i32, _p, _p]),
     "gnnea_margin_fwd_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
-                                            _p, _p, _p]),
+                                            _p, _p, _p, _p]),
     "gnnea_margin_bwd_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
-                                            _p, _p, _f32, _p, _i64, _p]),
+                                            _p, _p, _p, _i32, _p, _f32, _p, _i64, _p]),
 }
 
 _LIB = None

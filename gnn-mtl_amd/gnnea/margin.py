@@ -3,13 +3,17 @@
 Drop-in body of EAModel.get_loss / UEAModel.get_loss (models/models_ea.py:103-123, 169-183):
   loss = (sum relu(A + 1 - B1) + sum relu(A + 1 - B2)) / (2 t k)
 with A, B the L1 distances of the gathered pair / negative-pair rows.  The forward never
-materialises the (t*k) x D gathers; the backward scatters sign vectors into d(outputs).
+materialises the (t*k) x D gathers; the backward gathers, per output row, the integer-weighted
+sign vectors of the terms that touch it (no atomics: deterministic).
 """
+import weakref
+
 import numpy as np
 import torch
 
 from . import _lib
 from ._lib import check, ptr, stream_of
+from .graph import DeviceCSR
 
 
 def _idx(a, device, n_rows):
@@ -28,6 +32,28 @@ def _idx(a, device, n_rows):
     return torch.from_numpy(arr).to(device)
 
 
+_INCIDENCE = {}
+
+
+def incidence(idx, n_rows):
+    """Row -> term-end incidence CSR of the six index tensors (include/gnnea.h, §8f #2), cached
+    per tuple of tensor objects: the negatives change every 50 epochs, the loss runs every one."""
+    key = tuple(id(a) for a in idx) + (n_rows,)
+    hit = _INCIDENCE.get(key)
+    if hit is not None and all(r() is a for r, a in zip(hit[0], idx)):
+        return hit[1]
+    left, right, nl1, nr1, nl2, nr2 = idx
+    rows = torch.cat([nl1, nl2, left, nr1, nr2, right])
+    if rows.numel() >= 2 ** 31:
+        raise ValueError("gnnea.margin: too many terms for an int32 incidence")
+    cols = torch.arange(rows.numel(), dtype=torch.int64, device=rows.device)
+    csr = DeviceCSR.from_coo(rows, cols, None, n_rows, max(1, rows.numel()))
+    if len(_INCIDENCE) > 8:
+        _INCIDENCE.clear()
+    _INCIDENCE[key] = (tuple(weakref.ref(a) for a in idx), csr)
+    return csr
+
+
 class MarginLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, outputs, left, right, nl1, nr1, nl2, nr2, t, k):
@@ -39,26 +65,28 @@ class MarginLossFn(torch.autograd.Function):
         dev = out.device
         A = torch.empty(t, dtype=torch.float32, device=dev)
         h = torch.empty(2 * t * k, dtype=torch.float32, device=dev)
+        m = torch.empty(2 * t * k + t, dtype=torch.float32, device=dev)
         with torch.cuda.device(dev):
             check(_lib.lib().gnnea_margin_fwd_f32(
                 ptr(out), out.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1),
-                ptr(nl2), ptr(nr2), ptr(A), ptr(h), stream_of(dev)))
-        ctx.save_for_backward(out, left, right, nl1, nr1, nl2, nr2, h)
+                ptr(nl2), ptr(nr2), ptr(A), ptr(h), ptr(m), stream_of(dev)))
+        ctx.save_for_backward(out, left, right, nl1, nr1, nl2, nr2, m)
         ctx.tk = (t, k)
         return torch.sum(h) / (2.0 * t * k)
 
     @staticmethod
     def backward(ctx, g):
-        out, left, right, nl1, nr1, nl2, nr2, h = ctx.saved_tensors
+        out, left, right, nl1, nr1, nl2, nr2, m = ctx.saved_tensors
         t, k = ctx.tk
         N, D = out.shape
-        grad = torch.zeros((N, D), dtype=torch.float32, device=out.device)
+        inc = incidence((left, right, nl1, nr1, nl2, nr2), N)
+        grad = torch.empty((N, D), dtype=torch.float32, device=out.device)
         g = g.reshape(1).to(torch.float32).contiguous()
         with torch.cuda.device(out.device):
             check(_lib.lib().gnnea_margin_bwd_f32(
                 ptr(out), out.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1),
-                ptr(nl2), ptr(nr2), ptr(h), ptr(g), 1.0 / (2.0 * t * k), ptr(grad), D,
-                stream_of(out.device)))
+                ptr(nl2), ptr(nr2), ptr(m), ptr(inc.rowptr), ptr(inc.col), N, ptr(g),
+                1.0 / (2.0 * t * k), ptr(grad), D, stream_of(out.device)))
         return grad, None, None, None, None, None, None, None, None
 
 
@@ -68,6 +96,8 @@ def margin_loss(outputs, left, right, neg_left, neg_right, neg2_left, neg2_right
     checked=True passes already range-checked int64 device tensors through untouched."""
     if neg_right is None or neg2_left is None:
         raise ValueError("gnnea.margin: negatives are not set (call get_neg first)")
+    if t <= 0 or k <= 0:
+        raise ValueError("gnnea.margin: need t > 0 pairs and k > 0 negatives")
     arrays = (left, right, neg_left, neg_right, neg2_left, neg2_right)
     if checked:
         idx = list(arrays)

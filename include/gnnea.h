@@ -234,19 +234,27 @@ int gnnea_topk_rows_f32(const float* keys, int64_t ldk, int32_t nq, int32_t nx, 
 /* ------------------------------------------------------------------------------------------ *
  * §8f #2. Entity-alignment margin loss (EAModel.get_loss, models/models_ea.py:103-123; the same
  * body in UEAModel.get_loss :169-183).  out [N, D] fp32 rows of stride ld; left/right [t] pair
- * rows; neg_* [t*k] negative-pair rows (int64).  Forward writes A[t] = |out[left]-out[right]|_1
- * and h[2*t*k] = relu(A_i + 1 - |out[neg_l] - out[neg_r]|_1) (side 1 then side 2); the loss is
- * sum(h) / (2 t k).  Backward adds scale * grad_loss[0] * d(sum h)/d(out) into grad (N x ldg,
- * caller-zeroed) with fp32 atomics; scale = 1 / (2 t k).  D <= 1024.
+ * rows; neg_* [t*k] negative-pair rows (int64).  Terms j in [0, M), M = 2tk + t: side-1
+ * negatives, side-2 negatives, then the pairs.
+ * Forward: A[t] = |out[left]-out[right]|_1, h[2tk] = relu(A_i + 1 - |out[neg_l]-out[neg_r]|_1)
+ * (loss = sum(h) / (2tk), summed by the caller) and the integer multipliers m[M] the backward
+ * needs (-[h>0] per negative, number of active terms per pair).
+ * Backward: grad (n_rows x ldg, every row written) = scale * grad_loss[0] *
+ *   sum over the incidence of each row r of m_j * sgn(out[r] - out[other end of term j]).
+ * The incidence CSR (inc_rowptr[n_rows+1], inc_ent) is gnnea_coo_to_csr of
+ *   rows = [nl1 | nl2 | left | nr1 | nr2 | right]  (2M entries),  cols = 0 .. 2M-1
+ * (entry p < M: row is term p's first end; p >= M: term p-M's second end); it depends on the
+ * index arrays only, so it is built once per negative set.  scale = 1 / (2tk).  D <= 1024.
  * ------------------------------------------------------------------------------------------ */
 int gnnea_margin_fwd_f32(const float* out, int64_t ld, int32_t D, int32_t t, int32_t k,
                          const int64_t* left, const int64_t* right, const int64_t* neg_left,
                          const int64_t* neg_right, const int64_t* neg2_left,
-                         const int64_t* neg2_right, float* A, float* h, void* stream);
+                         const int64_t* neg2_right, float* A, float* h, float* m, void* stream);
 int gnnea_margin_bwd_f32(const float* out, int64_t ld, int32_t D, int32_t t, int32_t k,
                          const int64_t* left, const int64_t* right, const int64_t* neg_left,
                          const int64_t* neg_right, const int64_t* neg2_left,
-                         const int64_t* neg2_right, const float* h, const float* grad_loss,
+                         const int64_t* neg2_right, const float* m, const int32_t* inc_rowptr,
+                         const int32_t* inc_ent, int32_t n_rows, const float* grad_loss,
                          float scale, float* grad, int64_t ldg, void* stream);
 
 #ifdef __cplusplus

@@ -19,4 +19,4 @@ def margin_loss_and_grad(vec, left, right, nl1, nr1, nl2, nr2, t, k):
     B2 = torch.sum(torch.abs(x[ix(nl2)] - x[ix(nr2)]), 1).reshape(t, k)
     loss = (torch.relu(A - B1).sum() + torch.relu(A - B2).sum()) / (2.0 * t * k)
     loss.backward()
-    return float(loss), x.grad.numpy()
+    return float(loss.detach()), x.grad.numpy()

@@ -173,3 +173,19 @@ def test_margin_rejects_bad_indices(device):
         margin_loss(x, [0], [10], [0], [1], [2], [3], 1, 1)
     with pytest.raises(ValueError):
         margin_loss(x, [0], [1], [0], None, [2], [3], 1, 1)
+
+
+def test_margin_backward_deterministic(device):
+    """The incidence-gather backward has no atomics: gradients are bit-identical run to run."""
+    from gnnea.margin import margin_loss
+    rng = np.random.default_rng(1)
+    N, D, t, k = 3000, 300, 200, 40
+    vec = torch.from_numpy((0.05 * rng.standard_normal((N, D))).astype(np.float32)).to(device)
+    idx = [rng.integers(0, 50, t), rng.integers(0, N, t)] + \
+        [rng.integers(0, 50 if i % 2 == 0 else N, t * k) for i in range(4)]  # hub rows
+    grads = []
+    for _ in range(3):
+        x = vec.clone().requires_grad_(True)
+        margin_loss(x, *idx, t, k).backward()
+        grads.append(x.grad.cpu().numpy())
+    assert (grads[0] == grads[1]).all() and (grads[0] == grads[2]).all()
