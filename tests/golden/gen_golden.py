@@ -254,9 +254,74 @@ def gen_l1():
     print("l1 fixtures written to", HERE)
 
 
+def gen_train_trace():
+    """run/train_ea.py:53-67 loop (3 epochs) of the reference EAModel on the cfg-1 graph."""
+    _synth()
+    _placeholders()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import models.models_ea as RM
+    import utils.eval_utils as REV
+    torch.set_num_threads(8)
+    g = dict(np.load(os.path.join(HERE, "graph_cfg1.npz")))
+    N = int(g["N"])
+    adj = torch.sparse_coo_tensor(np.stack([g["row"], g["col"]]), g["val"], (N, N))
+    x = torch.from_numpy(g["X"]).to_sparse()
+    rng = np.random.default_rng(21)
+    perm = rng.permutation(N // 2)
+    train = np.stack([perm[:300], perm[:300] + N // 2], 1).astype(np.int64)
+    test = np.stack([perm[300:800], perm[300:800] + N // 2], 1).astype(np.int64)
+    out = {"train": train, "test": test}
+
+    class Args:
+        pass
+
+    for model in ("GCN", "GAT", "HGCN"):
+        a = Args()
+        a.model, a.num_layers, a.dim, a.act, a.dropout, a.bias = model, 3, 300, "relu", 0.0, 1
+        a.n_heads, a.alpha, a.feat_dim, a.n_classes, a.cuda, a.device = 4, 0.2, 300, 300, -1, "cpu"
+        a.n_nodes, a.neg_num, a.data = N, 10, {"train": train, "test": test}
+        torch.manual_seed(10086)
+        m = RM.EAModel(a)
+        # plain SGD: Adam's first steps are +-lr for every weight whatever the gradient's size,
+        # so rounding-level gradient differences would turn into lr-sized weight differences
+        opt = torch.optim.SGD(params=m.parameters(), lr=2.0)
+        sched = torch.optim.lr_scheduler.StepLR(opt, step_size=2000, gamma=0.5)
+        losses = []
+        for epoch in range(3):
+            m.train()
+            opt.zero_grad()
+            outputs = m.decode(m.encode(x, adj), adj)
+            if epoch % 50 == 0:
+                m.neg_right = m.get_neg(train[:, 0], outputs, a.neg_num)
+                m.neg2_left = m.get_neg(train[:, 1], outputs, a.neg_num)
+                out[model + "_neg_right"] = m.neg_right
+                out[model + "_neg2_left"] = m.neg2_left
+            loss = m.get_loss(outputs, a.data, "train")
+            loss.backward()
+            if epoch == 0:  # parameter gradients of the first step (before Adam moves anything)
+                for name, p in m.named_parameters():
+                    out["%s_grad0.%s" % (model, name)] = p.grad.numpy().copy()
+            opt.step()
+            sched.step()
+            losses.append(float(loss))
+        m.eval()
+        with torch.no_grad():
+            outputs = m.decode(m.encode(x, adj), adj)
+        met = REV.get_hits(outputs, test)
+        out[model + "_losses"] = np.array(losses)
+        out[model + "_hits"] = np.array(list(met.values()))
+        out[model + "_final_out"] = outputs.numpy()
+    np.savez_compressed(os.path.join(HERE, "train_trace_cfg1.npz"), **out)
+    print("train trace written to", HERE)
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["l1"]:
-        gen_l1()
+    sections = {"l1": gen_l1, "train": gen_train_trace}
+    if sys.argv[1:]:
+        for name in sys.argv[1:]:
+            sections[name]()
     else:
         main()
         gen_l1()
+        gen_train_trace()

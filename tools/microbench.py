@@ -186,6 +186,50 @@ def main():
             loss.backward()
         res["margin_fwd_bwd_fused"] = {"ms": timeit(fused, args.reps)}
         res["margin_fwd_bwd_torch_ops"] = {"ms": timeit(torch_ops, args.reps)}
+    if want("epoch"):
+        # one run/train_ea.py epoch at DBP15K scale (2 x 15k entities, 2 x 50k triples, 4500
+        # train pairs, 125 negatives): encode + decode + get_loss + backward + Adam, plus the
+        # every-50-epochs get_neg and the eval get_hits (10.5k test pairs)
+        from models.models_ea import EAModel
+        from utils.eval_utils import get_hits
+
+        class A:
+            pass
+        n15 = 15000
+        tr15 = synth.kg_pair_triples(n15, 50000, 1000)
+        r5, c5, v5 = synth.adjacency_coo(tr15, 2 * n15, reference_order=False)
+        adj15 = torch.sparse_coo_tensor(torch.from_numpy(np.stack([r5, c5])),
+                                        torch.from_numpy(v5), (2 * n15, 2 * n15)).to(dev)
+        x15 = torch.from_numpy(synth.features(2 * n15, D)).to_sparse().to(dev)
+        perm = np.random.default_rng(0).permutation(n15)
+        train = np.stack([perm[:4500], perm[:4500] + n15], 1)
+        test = np.stack([perm[4500:], perm[4500:] + n15], 1)
+        for model in ("GCN", "HGCN", "GAT"):
+            a = A()
+            a.model, a.num_layers, a.dim, a.act, a.dropout, a.bias = model, 3, D, "relu", 0.0, 1
+            a.n_heads, a.alpha, a.feat_dim, a.n_classes = 4, 0.2, D, D
+            a.cuda, a.device, a.n_nodes, a.neg_num = 0, dev, 2 * n15, 125
+            a.data = {"train": train, "test": test}
+            torch.manual_seed(10086)
+            mdl = EAModel(a).to(dev)
+            opt = torch.optim.Adam(params=mdl.parameters(), lr=0.001)
+            with torch.no_grad():
+                o0 = mdl.decode(mdl.encode(x15, adj15), adj15)
+            mdl.neg_right = mdl.get_neg(train[:, 0], o0, 125)
+            mdl.neg2_left = mdl.get_neg(train[:, 1], o0, 125)
+
+            def epoch():
+                opt.zero_grad()
+                o = mdl.decode(mdl.encode(x15, adj15), adj15)
+                loss = mdl.get_loss(o, a.data, "train")
+                loss.backward()
+                opt.step()
+            ms = timeit(epoch, args.reps)
+            ms_neg = timeit(lambda: (mdl.get_neg(train[:, 0], o0, 125),
+                                     mdl.get_neg(train[:, 1], o0, 125)), 3, warm=1)
+            ms_hits = timeit(lambda: get_hits(o0, test), 3, warm=1)
+            res["epoch_dbp15k_" + model] = {"ms_train_step": ms, "ms_get_neg_x2": ms_neg,
+                                            "ms_get_hits": ms_hits}
     print(json.dumps(res, indent=1))
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
