@@ -64,18 +64,17 @@ def sinkhorn_rate(device, B=3000, reg=0.01):
     Y = 0.05 * torch.randn(B, 300, generator=g)
     M = torch.cdist(X, Y)
     M = (M / M.max()).to(device)
-    la = torch.zeros(B, dtype=torch.float64, device=device)
     out = {}
-    for name, mode, lb_val, n0, n1 in (("ot_loss.sinkhorn", _lib.GNNEA_SK_KNOPP, 0.0, 100, 1100),
-                                       ("sinkhorn_iteration", _lib.GNNEA_SK_STAB,
-                                        -np.log(B), 100, 1100)):
-        la_m = la if mode == _lib.GNNEA_SK_KNOPP else la - np.log(B)
-        lb = torch.full((B,), lb_val, dtype=torch.float64, device=device)
+    # ot_loss.sinkhorn as models_ea.py:217 calls it (a = b = ones); sinkhorn_iteration with the
+    # uniform marginals mu = nu = 1/B
+    for name, mode, w, n0, n1 in (("ot_loss.sinkhorn", _lib.GNNEA_SK_KNOPP, 1.0, 100, 1100),
+                                  ("sinkhorn_iteration", _lib.GNNEA_SK_STAB, 1.0 / B, 100, 1100)):
+        la_m = torch.full((B,), w, dtype=torch.float64, device=device)
+        lb = la_m
         C = M if mode == _lib.GNNEA_SK_KNOPP else M.double()
         ts = []
         for n_it in (n0, n1):
-            # tol = -1: never converges, so exactly n_it iterations run (the log-domain fixed
-            # point reaches err == 0 exactly, which a 0 threshold would treat as converged)
+            # tol = -1: never converges, so exactly n_it iterations run
             solve(mode, C, la_m, lb, reg, -1.0, n_it, want_plan=False, batch=100)  # warm
             torch.cuda.synchronize()
             t0 = time.perf_counter()

@@ -2,9 +2,9 @@
 
 ``sinkhorn_iteration`` / ``gsinkhorn_iteration`` / ``forward_relax_sinkhorn_iteration`` keep
 the reference signatures and return ``(transport, margin1, margin2, K)``.  The scaling-with-
-absorption loop is executed in the log domain (identical in exact arithmetic, including the
-absorption schedule that decides when the relative-tolerance test runs, the 1e30 clamps and
-the 1e20 absorption trigger).  The batch dimension is solved one problem at a time.
+absorption loop runs on the device in the reference's own form (fp64 K resident in HBM,
+absorption schedule, 1e30 clamps, 1e20 trigger, relative-tolerance break).  The batch dimension
+is solved one problem at a time.
 """
 import torch
 
@@ -45,8 +45,8 @@ def _run(mode, C, mu, nu, epsilon, numIterMax, tol, lambdda, debug, out_dtype, p
         c = Cb[k]
         if c.dtype not in (torch.float32, torch.float64):
             c = c.to(out_dtype)
-        res = solve(mode, c, torch.log(mub[k % mub.shape[0]].double()),
-                    torch.log(nub[k % nub.shape[0]].double()), epsilon, tol, numIterMax, p=p,
+        res = solve(mode, c, mub[k % mub.shape[0]].double(),
+                    nub[k % nub.shape[0]].double(), epsilon, tol, numIterMax, p=p,
                     plan_dtype=torch.float64)
         K = res.plan
         if debug:

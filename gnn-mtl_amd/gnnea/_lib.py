@@ -45,8 +45,8 @@ class SinkhornProblem(ctypes.Structure):
         ("J", ctypes.c_int),
         ("ldc", _i64),
         ("C", _p),
-        ("log_a", _p),
-        ("log_b", _p),
+        ("a", _p),
+        ("b", _p),
         ("eps", _f64),
         ("p", _f64),
         ("tol", _f64),

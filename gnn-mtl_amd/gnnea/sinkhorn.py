@@ -1,4 +1,4 @@
-"""Host driver of the fused log-domain Sinkhorn kernels (gnnea_sinkhorn_*).
+"""Host driver of the Sinkhorn kernels (gnnea_sinkhorn_*, scaling form with a resident fp64 K).
 
 The loop has data-dependent exits (tolerance, numerical-error break), so the host enqueues
 iterations in batches and reads the device status block between batches; kernels of iterations
@@ -36,10 +36,10 @@ def _status(ws):
     return ints, dbl
 
 
-def solve(mode, C, log_a, log_b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
+def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
           want_plan=True, batch=10, variant=0):
-    """Run one Sinkhorn solve; C is [I, J] fp32 / fp64 on a HIP device."""
-    _lib.require_device(C, log_a, log_b)
+    """Run one Sinkhorn solve; C is [I, J] fp32 / fp64 on a HIP device, a / b the weights."""
+    _lib.require_device(C, a, b)
     if C.dim() != 2:
         raise ValueError("gnnea.sinkhorn: C must be 2-D")
     if C.dtype not in (torch.float32, torch.float64):
@@ -48,8 +48,10 @@ def solve(mode, C, log_a, log_b, eps, tol, max_iter, p=1.0, plan_dtype=torch.flo
         C = C.contiguous()
     I, J = C.shape
     dev = C.device
-    la = log_a.reshape(-1).to(torch.float64).contiguous()
-    lb = log_b.reshape(-1).to(torch.float64).contiguous()
+    wa = a.reshape(-1).to(torch.float64).contiguous()
+    wb = b.reshape(-1).to(torch.float64).contiguous()
+    if wa.numel() != I or wb.numel() != J:
+        raise ValueError("gnnea.sinkhorn: weights must have I and J entries")
     L = _lib.lib()
     ws_bytes = int(L.gnnea_sinkhorn_ws_bytes(I, J))
     if ws_bytes < 0:
@@ -57,7 +59,7 @@ def solve(mode, C, log_a, log_b, eps, tol, max_iter, p=1.0, plan_dtype=torch.flo
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     prob = SinkhornProblem(
         mode=mode, c_dtype=_lib.GNNEA_F32 if C.dtype == torch.float32 else _lib.GNNEA_F64,
-        I=I, J=J, ldc=C.stride(0), C=C.data_ptr(), log_a=la.data_ptr(), log_b=lb.data_ptr(),
+        I=I, J=J, ldc=C.stride(0), C=C.data_ptr(), a=wa.data_ptr(), b=wb.data_ptr(),
         eps=float(eps), p=float(p), tol=float(tol), max_iter=int(max_iter), iters_run=0,
         variant=int(variant), reserved=0, ws=ws.data_ptr())
     pp = ctypes.byref(prob)

@@ -1,8 +1,9 @@
-"""Entropic OT (reference utils/ot_loss.py) on the fused log-domain HIP Sinkhorn.
+"""Entropic OT (reference utils/ot_loss.py) on the HIP Sinkhorn (gnnea_sinkhorn_*, KNOPP).
 
 ``sinkhorn(a, b, M, reg, numItermax, stopThr, verbose) -> (P, loss)`` keeps the reference's
-semantics (fp64 arithmetic, u = 1/I and v = 1/J start, err = ||v (K^T u) - b||_2 checked every
-10th iteration, revert-and-break on K^T u == 0 / inf / NaN) while never materialising K.
+semantics and arithmetic (fp64, K = exp(M / -reg) built once on the device, u = 1/I and v = 1/J
+start, err = ||v (K^T u) - b||_2 checked every 10th iteration, revert-and-break on K^T u == 0 /
+inf / NaN); the loop runs on the device, the host only reads the stop flag between batches.
 """
 import torch
 
@@ -22,7 +23,7 @@ def sinkhorn(a, b, M, reg, numItermax=1000, stopThr=1e-9, verbose=False):
         b = torch.ones(J, dtype=torch.float64, device=M.device) / J
     assert len(a) == I and len(b) == J, "the dimension of weights and distance matrix don't match"
     # fp32 M is widened exactly inside the kernels (the reference casts M to fp64, :27)
-    res = solve(_lib.GNNEA_SK_KNOPP, M, torch.log(a), torch.log(b), reg, stopThr, numItermax)
+    res = solve(_lib.GNNEA_SK_KNOPP, M, a, b, reg, stopThr, numItermax)
     if res.reason == 2:
         print("Warning: numerical errors at iteration ", res.iters)
     if verbose:

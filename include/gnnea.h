@@ -153,16 +153,17 @@ int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
                    float* C, int64_t ldc, void* ws, int64_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------ *
- * a9-a12. Fused log-domain Sinkhorn.
+ * a9-a12. Sinkhorn solvers in the reference's scaling form, fp64 arithmetic.
  *   GNNEA_SK_KNOPP : utils/ot_loss.py:5-76 sinkhorn(a, b, M, reg, numItermax, stopThr)
  *   GNNEA_SK_STAB  : SinkhornOT/sinkhorn_loss.py:159-220 sinkhorn_iteration
  *   GNNEA_SK_GEN   : SinkhornOT/sinkhorn_loss.py:223-288 gsinkhorn_iteration
  *   GNNEA_SK_RELAX : SinkhornOT/sinkhorn_loss.py:291-356 forward_relax_sinkhorn_iteration
- * All arithmetic is fp64; the cost may be stored fp32 (exact fp32->fp64 widening, as the
- * reference's .type(torch.DoubleTensor)) or fp64.  The solver state lives in `ws`; the host
- * drives the data-dependent loop with gnnea_sinkhorn_iterate() batches and reads the status
- * block (first GNNEA_SK_STATUS_BYTES of ws) between batches.  Kernels of an iteration after
- * the stop condition are no-ops, so over-enqueueing is harmless.
+ * The cost may be stored fp32 (widened exactly, as the reference's .type(torch.DoubleTensor)) or
+ * fp64; the fp64 kernel matrix K (I*J*8 bytes) lives in `ws`, built once (KNOPP) or at every
+ * absorption (STAB family).  The host drives the data-dependent loop with
+ * gnnea_sinkhorn_iterate() batches and reads the status block (first GNNEA_SK_STATUS_BYTES of ws)
+ * between batches.  Kernels of an iteration after the stop condition are no-ops, so
+ * over-enqueueing is harmless.
  * ------------------------------------------------------------------------------------------ */
 #define GNNEA_SK_KNOPP 0
 #define GNNEA_SK_STAB 1
@@ -173,9 +174,10 @@ int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
 #define GNNEA_SK_ST_DONE 0       /* 1 once the loop has stopped */
 #define GNNEA_SK_ST_ITERS 1      /* reference's final iteration counter (cpt / ii) */
 #define GNNEA_SK_ST_REASON 2     /* 0 running/max-iter, 1 tolerance, 2 numerical-error break */
-#define GNNEA_SK_ST_SLOT 3       /* ping-pong slot holding the final potentials */
+#define GNNEA_SK_ST_SLOT 3       /* ping-pong slot holding the final scalings */
 #define GNNEA_SK_STATUS_BYTES 256
-/* double words after the int block: [8]=err/transport, [9]=transport_prev, [10]=loss */
+/* double words after the int block: [8]=err (KNOPP) / transport_new, [9]=transport_prev,
+ * [10]=loss (KNOPP: sum P M) */
 
 typedef struct gnnea_sinkhorn {
   int mode;         /* GNNEA_SK_* */
@@ -183,14 +185,14 @@ typedef struct gnnea_sinkhorn {
   int I, J;         /* cost is I x J */
   int64_t ldc;      /* row stride of C in elements */
   const void* C;    /* cost matrix (M for KNOPP) */
-  const double* log_a; /* I: log of the source weights (a / mu) */
-  const double* log_b; /* J: log of the target weights (b / nu) */
+  const double* a;  /* I: source weights (a / mu) */
+  const double* b;  /* J: target weights (b / nu) */
   double eps;       /* reg (KNOPP) or epsilon */
   double p;         /* lambda/(lambda+eps) for GEN / RELAX; ignored otherwise */
   double tol;       /* stopThr (KNOPP) or tol */
   int max_iter;     /* numItermax / numIterMax */
   int iters_run;    /* iterations enqueued so far (read by gnnea_sinkhorn_finish) */
-  int variant;      /* pass launch configuration, 0 = default (others: tuning A/B) */
+  int variant;      /* reserved for launch-configuration variants, 0 */
   int reserved;
   void* ws;         /* device workspace of gnnea_sinkhorn_ws_bytes(I, J) bytes */
 } gnnea_sinkhorn;
@@ -200,8 +202,9 @@ int gnnea_sinkhorn_init(const gnnea_sinkhorn* prob, void* stream);
 /* enqueue iterations [first, first+count) (count >= 1) */
 int gnnea_sinkhorn_iterate(const gnnea_sinkhorn* prob, int first, int count, void* stream);
 /* plan (I x J, plan_dtype, row stride ldp, nullable): KNOPP: P = diag(u) K diag(v);
- * others: K = clamp(exp(u+v-C/eps), 0, 1e30).  Also writes row sums (I) and column sums (J) of
- * the plan into row_sum/col_sum (nullable, fp64) and the scalars into the status block. */
+ * others: the last K = clamp(exp((u+v-C)/eps), 0, 1e30).  Also writes row sums (I) and column
+ * sums (J) of the plan into row_sum/col_sum (nullable, fp64) and the scalars into the status
+ * block. */
 int gnnea_sinkhorn_finish(const gnnea_sinkhorn* prob, void* plan, int plan_dtype, int64_t ldp,
                           double* row_sum, double* col_sum, void* stream);
 

@@ -353,9 +353,9 @@ def test_shard_own_remote_split_on_device(device, world):
         assert rel_err(y.cpu(), ref[g0:g0 + p.n_rows]) < TOL32
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 10, 20, 30, 40, 12, 33])
-def test_sinkhorn_pass_variants(device, variant):
-    """Every launch configuration of the row / column passes gives the oracle's answer."""
+@pytest.mark.parametrize("variant", [0, 1])
+def test_sinkhorn_rectangular_vs_oracle(device, variant):
+    """Rectangular problems (I != J, b != a) agree with the oracle for both solver families."""
     from gnnea import _lib
     from gnnea.sinkhorn import solve
     from oracle import sinkhorn as osk
@@ -365,13 +365,13 @@ def test_sinkhorn_pass_variants(device, variant):
     a = np.ones(I)
     b = np.ones(J) * I / J
     res = solve(_lib.GNNEA_SK_KNOPP, torch.from_numpy(M).to(device),
-                torch.from_numpy(np.log(a)).to(device), torch.from_numpy(np.log(b)).to(device),
+                torch.from_numpy(a).to(device), torch.from_numpy(b).to(device),
                 reg, 1e-9, 200, variant=variant)
     Po, _, _, _ = osk.knopp(a, b, M, reg, 200)
     assert rel_err(res.plan.cpu(), Po) < TOL64
     res = solve(_lib.GNNEA_SK_STAB, torch.from_numpy(M).to(device),
-                torch.from_numpy(np.log(a / I)).to(device),
-                torch.from_numpy(np.log(b / I)).to(device), reg, 1e-9, 100, variant=variant)
+                torch.from_numpy(a / I).to(device),
+                torch.from_numpy(b / I).to(device), reg, 1e-9, 100, variant=variant)
     t, m1, m2, K = osk.stabilized(M, a / I, b / I, reg, 100, 1e-9)
     assert rel_err(res.plan.cpu(), K) < TOL64
     assert abs(res.transport_new - t) <= 1e-9 * abs(t)

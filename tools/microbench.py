@@ -131,7 +131,7 @@ def main():
         from gnnea.sinkhorn import solve
         B = 3000
         M = torch.rand(B, B, device=dev, generator=g)
-        la = torch.zeros(B, dtype=torch.float64, device=dev)
+        la = torch.ones(B, dtype=torch.float64, device=dev)
         variants = [int(v) for v in os.environ.get("SK_VARIANTS", "0").split(",")]
         for name, mode, C in (("knopp_f32C", _lib.GNNEA_SK_KNOPP, M),
                               ("stab_f64C", _lib.GNNEA_SK_STAB, M.double())):
