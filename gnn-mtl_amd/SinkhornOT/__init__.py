@@ -1,15 +1,13 @@
-# Drop-in package: sinkhorn_loss.py here runs the solvers on HIP; the reference's GW / FGW outer
-# loops (SinkhornOT/iterative_projection.py, cderivation.py) are found further down sys.path when
-# the reference is installed, and then call these solvers through their relative imports.
+# Drop-in package: sinkhorn_loss.py runs the solvers on HIP, cderivation.py /
+# iterative_projection.py are the GW / FGW outer loops on device GEMMs around them.  Modules not
+# rebuilt here (fgw.py, which needs the un-vendored UMH package) are found further down sys.path
+# when the reference is installed.
 from pkgutil import extend_path
 
 __path__ = extend_path(__path__, __name__)
 
 from .sinkhorn_loss import (forward_relax_sinkhorn_iteration, gsinkhorn_iteration,  # noqa: E402,F401
                             kl_div, sinkhorn_iteration)
-
-try:  # optional upstream GW / FGW outer loops (SURVEY.md §8f #3 — not rebuilt yet)
-    from .cderivation import cos_dist_mat, get_inter_sim, get_intra_sim  # noqa: F401
-    from .iterative_projection import gw_iterative_1, rgw_iterative_1  # noqa: F401
-except ImportError:
-    pass
+from .cderivation import cos_dist_mat, get_inter_sim, get_intra_sim  # noqa: E402,F401
+from .iterative_projection import (fgw_iterative_1, gw_iterative_1,  # noqa: E402,F401
+                                   rfgw_iterative_1, rgw_iterative_1)

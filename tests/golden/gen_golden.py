@@ -316,8 +316,37 @@ def gen_train_trace():
     print("train trace written to", HERE)
 
 
+def gen_gw():
+    """§8f #3: the reference's GW / relaxed GW / FGW outer loops on small fp64 problems."""
+    _synth()
+    _placeholders()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import SinkhornOT.iterative_projection as RIP
+    from SinkhornOT.cderivation import cos_dist_mat
+    torch.set_num_threads(8)
+    rng = np.random.default_rng(13)
+    out = {}
+    for tag, (I, J) in {"a": (60, 60), "b": (90, 70)}.items():
+        X = torch.from_numpy(rng.uniform(size=(I, 16)))
+        Y = torch.from_numpy(rng.uniform(size=(J, 16)))
+        C1, C2 = cos_dist_mat(X, X), cos_dist_mat(Y, Y)
+        M = cos_dist_mat(X, Y)
+        mu = torch.full((I,), 1.0 / I, dtype=torch.float64)
+        nu = torch.full((J,), 1.0 / J, dtype=torch.float64)
+        out.update({tag + "_C1": C1.numpy(), tag + "_C2": C2.numpy(), tag + "_M": M.numpy()})
+        T, d = RIP.gw_iterative_1(C1, C2, mu, nu, epsilon=0.01, max_iter=8)
+        out.update({tag + "_gw_T": T.numpy(), tag + "_gw_d": np.array(float(d))})
+        T, d = RIP.rgw_iterative_1(C1, C2, mu, nu, max_iter=8, lambdda=1.0, epsilon=0.01)
+        out.update({tag + "_rgw_T": T.numpy(), tag + "_rgw_d": np.array(float(d))})
+        T, d = RIP.fgw_iterative_1(M, C1, C2, mu, nu, alpha=0.5, p=2, max_iter=8, epsilon=0.01)
+        out.update({tag + "_fgw_T": T.numpy(), tag + "_fgw_d": np.array(float(d))})
+    np.savez_compressed(os.path.join(HERE, "gw.npz"), **out)
+    print("gw fixtures written to", HERE)
+
+
 if __name__ == "__main__":
-    sections = {"l1": gen_l1, "train": gen_train_trace}
+    sections = {"l1": gen_l1, "train": gen_train_trace, "gw": gen_gw}
     if sys.argv[1:]:
         for name in sys.argv[1:]:
             sections[name]()
@@ -325,3 +354,4 @@ if __name__ == "__main__":
         main()
         gen_l1()
         gen_train_trace()
+        gen_gw()

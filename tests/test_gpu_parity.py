@@ -461,3 +461,30 @@ def test_train_ea_trace_vs_reference(golden, device, model):
     hits = np.array(list(get_hits(outputs, test).values()))
     # the reference itself moves up to 3 of 500 ranks run to run (CPU thread order): near ties
     assert np.abs(hits - T[model + "_hits"]).max() <= 1.0
+
+
+# ------------------------------------------------------------------------------------------ #
+# §8f #3: GW / relaxed GW / FGW outer loops (device GEMMs + device Sinkhorn) vs the reference  #
+# ------------------------------------------------------------------------------------------ #
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_gw_outer_loops_vs_reference(golden, device, tag):
+    from SinkhornOT.iterative_projection import (fgw_iterative_1, gw_iterative_1,
+                                                 rgw_iterative_1)
+    f = golden("gw")
+    C1 = torch.from_numpy(f[tag + "_C1"]).to(device)
+    C2 = torch.from_numpy(f[tag + "_C2"]).to(device)
+    M = torch.from_numpy(f[tag + "_M"]).to(device)
+    I, J = C1.shape[0], C2.shape[0]
+    mu = torch.full((I,), 1.0 / I, dtype=torch.float64, device=device)
+    nu = torch.full((J,), 1.0 / J, dtype=torch.float64, device=device)
+    runs = {"gw": lambda: gw_iterative_1(C1, C2, mu, nu, epsilon=0.01, max_iter=8),
+            "rgw": lambda: rgw_iterative_1(C1, C2, mu, nu, max_iter=8, lambdda=1.0,
+                                           epsilon=0.01),
+            "fgw": lambda: fgw_iterative_1(M, C1, C2, mu, nu, alpha=0.5, p=2, max_iter=8,
+                                           epsilon=0.01)}
+    for name, run in runs.items():
+        T, d = run()
+        assert T.shape == f["%s_%s_T" % (tag, name)].shape
+        assert rel_err(T.cpu(), f["%s_%s_T" % (tag, name)]) < 1e-8, name
+        ref_d = float(f["%s_%s_d" % (tag, name)])
+        assert abs(float(d) - ref_d) <= 1e-8 * abs(ref_d), name
