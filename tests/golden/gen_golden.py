@@ -345,8 +345,35 @@ def gen_gw():
     print("gw fixtures written to", HERE)
 
 
+def gen_ingest():
+    """§8f #4: the reference's load_data_ea / load_seperate_data_ea on a small DBP15K-format
+    dataset written by tests/data/make_dbp15k_like.py."""
+    import tempfile
+    import types as _t
+    _synth()
+    _placeholders()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    sys.path.insert(0, os.path.join(REPO, "tests", "data"))
+    import make_dbp15k_like
+    import utils.data_utils as RDU
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as root:
+        lang = make_dbp15k_like.write(root)
+        os.chdir(root)
+        try:
+            np.random.seed(7)
+            data = RDU.load_data_ea(_t.SimpleNamespace(dataset=lang, model="GCN"))
+            np.random.seed(8)
+            sep = RDU.load_seperate_data_ea(_t.SimpleNamespace(dataset=lang))
+        finally:
+            os.chdir(cwd)
+    np.savez_compressed(os.path.join(HERE, "ingest.npz"), **make_dbp15k_like.flatten(data, sep))
+    print("ingest fixtures written to", HERE)
+
+
 if __name__ == "__main__":
-    sections = {"l1": gen_l1, "train": gen_train_trace, "gw": gen_gw}
+    sections = {"l1": gen_l1, "train": gen_train_trace, "gw": gen_gw, "ingest": gen_ingest}
     if sys.argv[1:]:
         for name in sys.argv[1:]:
             sections[name]()
@@ -355,3 +382,4 @@ if __name__ == "__main__":
         gen_l1()
         gen_train_trace()
         gen_gw()
+        gen_ingest()

@@ -8,10 +8,11 @@ import pytest
 from conftest import ROOT
 
 HEADER = os.path.join(ROOT, "include", "gnnea.h")
+HOST_HEADER = os.path.join(ROOT, "include", "gnnea_host.h")
 
 
-def declared_functions():
-    src = open(HEADER).read()
+def declared_functions(header=HEADER):
+    src = open(header).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     names = re.findall(r"^\s*(?:const\s+)?[a-z0-9_]+\*?\s+\*?(gnnea_[a-z0-9_]+)\s*\(", src, re.M)
     return sorted(set(names))
@@ -22,8 +23,24 @@ def test_header_declares_the_hot_path():
     for must in ("gnnea_coo_to_csr", "gnnea_spmm_csr_f32", "gnnea_spmm_highway_f32",
                  "gnnea_gat_fwd_f32", "gnnea_gat_bwd_prep_f32", "gnnea_gat_bwd_src_f32",
                  "gnnea_gat_bwd_dst_f32", "gnnea_spmm_csr_beta_f32", "gnnea_perm_invert",
-                 "gnnea_gemm_f32", "gnnea_sinkhorn_iterate", "gnnea_sinkhorn_finish"):
+                 "gnnea_gemm_f32", "gnnea_sinkhorn_iterate", "gnnea_sinkhorn_finish",
+                 "gnnea_l1_keys_f32", "gnnea_topk_rows_f32", "gnnea_l1_rank_f32",
+                 "gnnea_l1_pairs_f32", "gnnea_margin_fwd_f32", "gnnea_margin_bwd_f32"):
         assert must in names
+
+
+def test_host_library_exports_every_declared_symbol():
+    from gnnea import ingest
+    if not os.path.exists(ingest.LIB_PATH):
+        pytest.skip("libgnnea_host.so not built")
+    names = declared_functions(HOST_HEADER)
+    assert {"gnnea_h_loadfile", "gnnea_h_adjacency", "gnnea_h_relation_groups"} <= set(names)
+    L = ingest.lib()
+    for name in names:
+        assert hasattr(L, name) and name in ingest.SIGNATURES, name
+    out = subprocess.run(["nm", "-D", "--defined-only", ingest.LIB_PATH], capture_output=True,
+                         text=True).stdout
+    assert set(names) <= set(re.findall(r" T (gnnea_\w+)", out))
 
 
 def test_library_exports_every_declared_symbol():
