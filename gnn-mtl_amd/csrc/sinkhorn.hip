@@ -564,16 +564,32 @@ static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t 
   return 0;
 }
 
+// the memory-lean log-domain path (sinkhorn_log.hip)
+namespace sklog {
+int64_t ws_bytes(int I, int J);
+int init(const gnnea_sinkhorn* p, void* stream);
+int iterate(const gnnea_sinkhorn* p, int first, int count, void* stream);
+int finish(const gnnea_sinkhorn* p, void* plan, int plan_dtype, int64_t ldp, double* row_sum,
+           double* col_sum, void* stream);
+}  // namespace sklog
+
+// variant 1, or J beyond the sweep's register tiles: log-domain passes, no I x J workspace
+static bool use_log(const gnnea_sinkhorn* p) { return p->variant == 1 || p->J > kMaxJ; }
+
 }  // namespace gnnea
 
 using namespace gnnea;
 
 extern "C" int64_t gnnea_sinkhorn_ws_bytes(int I, int J) {
-  if (I < 1 || J < 1 || J > kMaxJ) return GNNEA_EINVAL;
-  return sk_plan(I, J).total;
+  if (I < 1 || J < 1) return GNNEA_EINVAL;
+  const int64_t lg = sklog::ws_bytes(I, J);
+  if (J > kMaxJ) return lg;
+  const int64_t sc = sk_plan(I, J).total;
+  return sc > lg ? sc : lg;
 }
 
 extern "C" int gnnea_sinkhorn_init(const gnnea_sinkhorn* p, void* stream) {
+  if (p && use_log(p)) return sklog::init(p, stream);
   if (!sk_valid(p)) return GNNEA_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const SkArgs a = sk_args(p);
@@ -607,6 +623,7 @@ extern "C" int gnnea_sinkhorn_init(const gnnea_sinkhorn* p, void* stream) {
 
 extern "C" int gnnea_sinkhorn_iterate(const gnnea_sinkhorn* p, int first, int count,
                                       void* stream) {
+  if (p && use_log(p)) return sklog::iterate(p, first, count, stream);
   if (!sk_valid(p) || first < 0 || count < 1) return GNNEA_EINVAL;
   if (p->c_dtype == GNNEA_F32) return sk_iter_t<float>(p, first, count, (hipStream_t)stream);
   return sk_iter_t<double>(p, first, count, (hipStream_t)stream);
@@ -615,6 +632,7 @@ extern "C" int gnnea_sinkhorn_iterate(const gnnea_sinkhorn* p, int first, int co
 extern "C" int gnnea_sinkhorn_finish(const gnnea_sinkhorn* p, void* plan, int plan_dtype,
                                      int64_t ldp, double* row_sum, double* col_sum,
                                      void* stream) {
+  if (p && use_log(p)) return sklog::finish(p, plan, plan_dtype, ldp, row_sum, col_sum, stream);
   if (!sk_valid(p)) return GNNEA_EINVAL;
   if (plan && plan_dtype != GNNEA_F32 && plan_dtype != GNNEA_F64) return GNNEA_EINVAL;
   if (plan && ldp < p->J) return GNNEA_EINVAL;

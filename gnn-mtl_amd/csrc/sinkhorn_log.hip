@@ -1,0 +1,771 @@
+// a9-a12. Fused log-domain Sinkhorn (fp64 arithmetic, fp32 or fp64 cost storage): the
+// memory-lean path of gnnea_sinkhorn_* (variant 1, and any J beyond the sweep's register tiles),
+// keeping no I x J state -- every pass recomputes its terms from C with fp64 exp.  Dispatched from
+// sinkhorn.hip; the status block is shared with the scaling-form path.
+//
+// Reference semantics restated in potentials:
+//   KNOPP (utils/ot_loss.py:5-76), f = log u, g = log v:
+//       g_j = log b_j - LSE_i(f_i - M_ij/reg)      (v = b / K^T u,   :53-54)
+//       f_i = log a_i - LSE_j(g_j - M_ij/reg)      (u = 1 / (K/a) v, :55)
+//     K_ij = exp_f64(-M_ij/reg) underflows to 0 below -745.13 in fp64: such terms are dropped,
+//     K^T u == 0 (column LSE below ln(DBL_TRUE_MIN)) or inf/NaN u, v break the loop with the
+//     previous iterate (:57-62); err = ||v (K^T u) - b||_2 every 10th iteration (:64-66).
+//   STAB / GEN / RELAX (SinkhornOT/sinkhorn_loss.py:159-356), potentials in units of eps,
+//   ua / va = absorbed potentials u/eps, v/eps, f / g = full potentials (u + eps log a)/eps:
+//       log s_i = LSE_j( min(ua_i + va_j - C_ij/eps, ln 1e30) + g_j - va_j )   (K b, clamped K)
+//       f_i = ua_i + min(p_row (log mu_i - log s_i), ln 1e30)                  (a = clamp((mu/s)^p))
+//     and symmetrically for g; absorption (ii%10==0, max(a|b) > 1e20, last iteration) sets
+//     ua = f, va = g and evaluates transport = sum K.C for the relative-tolerance break.
+// One iteration = row pass (one wave per row, coalesced 64-wide column sweep, chunked online
+// LSE with 16 loads in flight per lane) + column pass fused with the column update (16 columns
+// x 64 row groups per 1024-thread workgroup, merged through LDS).  Both passes are latency- and
+// fp64-exp-bound at B = 3000 (C is L2 / Infinity-Cache resident).  A device status block gates
+// every kernel so iterations after the stop condition are no-ops.
+#include "common.h"
+
+namespace gnnea {
+namespace sklog {
+
+constexpr double kLn1e20 = 46.051701859880914;   // log(1e20)  (sinkhorn_loss.py:11 big)
+constexpr double kLn1e30 = 69.07755278982137;    // log(1e30)  (sinkhorn_loss.py:12 huge)
+constexpr double kExpUnderflow = -745.1332191019412;  // exp_f64(x) == 0 in fp64 for x below
+constexpr double kLnTrueMin = -744.4400719213812;     // log(DBL_TRUE_MIN)
+constexpr double kExpOverflow = 709.782712893384;     // exp_f64(x) == inf above
+
+struct SkWs {
+  int64_t f, g, ua, va, rowbuf, errpart, part_m, part_s, la, lb, total;
+  int ncb;
+};
+
+static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
+constexpr int kMaxSplits = 16;  // row splits of the partial column pass
+
+static SkWs sk_plan(int I, int J) {
+  SkWs w;
+  int64_t o = GNNEA_SK_STATUS_BYTES;
+  w.f = o; o = al256(o + 2 * 8ll * I);
+  w.g = o; o = al256(o + 2 * 8ll * J);
+  w.ua = o; o = al256(o + 8ll * I);
+  w.va = o; o = al256(o + 8ll * J);
+  w.rowbuf = o; o = al256(o + 8ll * I);
+  w.ncb = (J + 7) / 8;  // errpart slots: enough for the narrowest column workgroup (8 cols)
+  w.errpart = o; o = al256(o + 8ll * w.ncb);
+  w.part_m = o; o = al256(o + 8ll * kMaxSplits * J);
+  w.part_s = o; o = al256(o + 8ll * kMaxSplits * J);
+  w.la = o; o = al256(o + 8ll * I);
+  w.lb = o; o = al256(o + 8ll * J);
+  w.total = o;
+  return w;
+}
+
+struct SkDev {
+  int64_t* st;   // status ints
+  double* sd;    // status doubles (sd[8] ...)
+  double *f, *g, *ua, *va, *rowbuf, *errpart, *pm, *ps;
+  int ncb;  // errpart slots written by the column pass of the active variant
+};
+
+static SkDev sk_dev(const gnnea_sinkhorn* p) {
+  SkWs w = sk_plan(p->I, p->J);
+  char* b = (char*)p->ws;
+  SkDev d;
+  d.st = (int64_t*)b;
+  d.sd = (double*)b;
+  d.f = (double*)(b + w.f);
+  d.g = (double*)(b + w.g);
+  d.ua = (double*)(b + w.ua);
+  d.va = (double*)(b + w.va);
+  d.rowbuf = (double*)(b + w.rowbuf);
+  d.errpart = (double*)(b + w.errpart);
+  d.pm = (double*)(b + w.part_m);
+  d.ps = (double*)(b + w.part_s);
+  d.ncb = w.ncb;
+  return d;
+}
+
+enum { ST_DONE = 0, ST_ITERS = 1, ST_REASON = 2, ST_SLOT = 3, ST_BIG = 4, ST_FAIL = 5 };
+enum { SD_ERR = 8, SD_TPREV = 9, SD_LOSS = 10, SD_TNEW = 8 };
+
+template <typename T>
+__device__ __forceinline__ double ld_c(const T* C, int64_t idx) {
+  return (double)C[idx];
+}
+
+// online log-sum-exp with one exp per element
+struct Lse {
+  double m, s;
+  __device__ __forceinline__ void init() { m = -INFINITY; s = 0.0; }
+  __device__ __forceinline__ void add(double x) {
+    if (x == -INFINITY) return;
+    if (x > m) {
+      s = s * exp_f64(m - x) + 1.0;
+      m = x;
+    } else {
+      s += exp_f64(x - m);
+    }
+  }
+  __device__ __forceinline__ void merge(double m2, double s2) {
+    if (m2 == -INFINITY) return;
+    if (m == -INFINITY) { m = m2; s = s2; return; }
+    if (m2 > m) { s = s * exp_f64(m - m2) + s2; m = m2; }
+    else s += s2 * exp_f64(m2 - m);
+  }
+  __device__ __forceinline__ double value() const { return m == -INFINITY ? -INFINITY : m + log(s); }
+};
+
+__device__ __forceinline__ Lse wave_lse(Lse l) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double m2 = __shfl_xor(l.m, o, 64);
+    const double s2 = __shfl_xor(l.s, o, 64);
+    l.merge(m2, s2);
+  }
+  return l;
+}
+
+struct SkArgs {
+  int mode, I, J;
+  int64_t ldc;
+  double inv_eps, p_row, p_col, kclamp;  // kclamp: ln 1e30 for STAB modes, +inf for KNOPP
+  const double *la, *lb;
+};
+
+__device__ __forceinline__ void mark_done(int64_t* st, int64_t iters, int64_t reason,
+                                          int64_t slot) {
+  if (atomicCAS((unsigned long long*)&st[ST_DONE], 0ull, 1ull) == 0ull) {
+    st[ST_ITERS] = iters;
+    st[ST_REASON] = reason;
+    st[ST_SLOT] = slot;
+  }
+}
+
+// Chunked, branch-free online LSE: per chunk of CH values one rescale exp + one exp per value
+// (a per-element "if (x > m)" diverges across lanes and costs two exps per element).
+template <int CH>
+__device__ __forceinline__ void lse_chunk(Lse& l, const double (&x)[CH]) {
+  double cm = x[0];
+#pragma unroll
+  for (int k = 1; k < CH; ++k) cm = fmax(cm, x[k]);
+  if (cm == -INFINITY) return;  // whole chunk masked (K == 0)
+  const double nm = fmax(l.m, cm);
+  double acc = l.m == -INFINITY ? 0.0 : l.s * exp_f64(l.m - nm);
+#pragma unroll
+  for (int k = 0; k < CH; ++k) acc += exp_f64(x[k] - nm);  // exp_f64(-inf) == 0
+  l.m = nm;
+  l.s = acc;
+}
+
+// logit of the reference's K_ij * scaling: -inf where K_ij underflows to 0 in fp64
+template <bool KNOPP>
+__device__ __forceinline__ double sk_term(double ua, double va, double c, double inv_eps,
+                                          double kclamp, double pot_minus_abs) {
+  const double k = KNOPP ? -c * inv_eps : ua + va - c * inv_eps;
+  if (k < kExpUnderflow) return -INFINITY;
+  return (KNOPP ? k : fmin(k, kclamp)) + pot_minus_abs;
+}
+
+// KNOPP loop decisions, in the reference's order (utils/ot_loss.py:50-72): the err test of
+// iterate it-1 (when (it-1)%10 == 0), then the K^T u == 0 / inf / NaN break of iteration it
+// flagged by this iteration's column pass.  Evaluated by wave 0 of every row workgroup (all
+// take the same decision); returns true when the workgroup must stop.
+__device__ __forceinline__ bool knopp_stop(SkDev& d, int it) {
+  __shared__ int stop;
+  const int lane = lane_id();
+  if (wave_id() == 0) {
+    const int prev = it - 1;
+    int st = 0;
+    if (prev >= 0 && prev % 10 == 0) {
+      double e = 0.0;
+      for (int b = lane; b < d.ncb; b += 64) e += d.errpart[b];
+      const double err = sqrt(wave_sum(e));
+      if (!(err > d.sd[11])) st = 1;  // sd[11] = stopThr: the loop runs while err > stopThr
+      if (blockIdx.x == 0 && lane == 0) {
+        d.sd[SD_ERR] = err;
+        if (st) mark_done(d.st, prev + 1, 1, prev & 1);
+      }
+    }
+    if (!st && d.st[ST_FAIL]) {
+      st = 1;
+      if (blockIdx.x == 0 && lane == 0) mark_done(d.st, it, 2, (it + 1) & 1);
+    }
+    if (lane == 0) stop = st;
+  }
+  __syncthreads();
+  return stop != 0;
+}
+
+__device__ __forceinline__ void finish_row(const SkArgs& a, SkDev& d, int i, Lse l, int it,
+                                           int slot_out, double uai, bool knopp) {
+  const double ls = l.value();
+  double la = a.p_row * (a.la[i] - ls);
+  if (knopp) {
+    d.f[(int64_t)slot_out * a.I + i] = la;  // u = 1/(Kp v)
+    if (!(la <= kExpOverflow)) mark_done(d.st, it, 2, (it + 1) & 1);  // u inf / NaN
+  } else {
+    if (la > kLn1e30) la = kLn1e30;  // a = clamp(., 0, 1e30)
+    if (la > kLn1e20) atomicOr((unsigned long long*)&d.st[ST_BIG], 1ull);
+    d.f[(int64_t)slot_out * a.I + i] = uai + la;  // F = u + eps log a
+  }
+}
+
+// Row pass: f_out_i from g_in.  WPR waves per row (4/WPR rows per 256-thread workgroup); each
+// lane keeps CH independent loads in flight per round; partial LSEs merged by shuffles + LDS.
+template <typename T, bool KNOPP, int CH, int WPR>
+__global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                int it, int slot_in, int slot_out) {
+  if (d.st[ST_DONE]) return;
+  if (KNOPP && knopp_stop(d, it)) return;
+  __shared__ double wm[4], ws[4];
+  const int w = wave_id(), lane = lane_id();
+  const int i = blockIdx.x * (4 / WPR) + w / WPR;
+  const int t = (w % WPR) * 64 + lane;  // thread index inside the row's team
+  constexpr int NT = 64 * WPR;
+  Lse l;
+  l.init();
+  if (i < a.I) {
+    const double* __restrict__ g = d.g + (int64_t)slot_in * a.J;
+    const double* __restrict__ va = d.va;
+    const double uai = KNOPP ? 0.0 : d.ua[i];
+    const T* __restrict__ Ci = C + (int64_t)i * a.ldc;
+    for (int j0 = 0; j0 < a.J; j0 += NT * CH) {
+      double x[CH];
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int j = j0 + NT * k + t;
+        x[k] = -INFINITY;
+        if (j < a.J) {
+          const double vj = KNOPP ? 0.0 : va[j];
+          x[k] = sk_term<KNOPP>(uai, vj, (double)Ci[j], a.inv_eps, a.kclamp, g[j] - vj);
+        }
+      }
+      lse_chunk<CH>(l, x);
+    }
+  }
+  l = wave_lse(l);
+  if (WPR > 1) {
+    if (lane == 0) {
+      wm[w] = l.m;
+      ws[w] = l.s;
+    }
+    __syncthreads();
+    if (i >= a.I || (w % WPR) != 0 || lane != 0) return;
+    for (int q = 1; q < WPR; ++q) l.merge(wm[w + q], ws[w + q]);
+  } else if (i >= a.I || lane != 0) {
+    return;
+  }
+  finish_row(a, d, i, l, it, slot_out, KNOPP ? 0.0 : d.ua[i], KNOPP);
+}
+
+// Finish column j from its LSE: g update, KNOPP err^2 term and break flags, STAB big flag.
+__device__ __forceinline__ void finish_col(const SkArgs& a, SkDev& d, int j, double ls,
+                                           int slot_g_prev, int slot_g_out, bool knopp,
+                                           double& errp, bool& fail, bool& big) {
+  if (knopp) {
+    // err of the previous iterate: v_{k-1} * (K^T u_{k-1}) - b    (utils/ot_loss.py:65-66)
+    const double t = exp_f64(d.g[(int64_t)slot_g_prev * a.J + j] + ls) - exp_f64(a.lb[j]);
+    errp = t * t;
+    fail = !(ls >= kLnTrueMin);  // K^T u == 0 (or NaN)     (:57)
+    const double gj = a.lb[j] - ls;
+    fail = fail || !(gj <= kExpOverflow);  // v inf / NaN   (:58-59)
+    d.g[(int64_t)slot_g_out * a.J + j] = gj;
+  } else {
+    double lb = a.p_col * (a.lb[j] - ls);
+    if (lb > kLn1e30) lb = kLn1e30;
+    big = lb > kLn1e20;
+    d.g[(int64_t)slot_g_out * a.J + j] = d.va[j] + lb;
+  }
+}
+
+// Column pass, fused with the update: a 1024-thread workgroup owns COLS columns; thread
+// (c = tid % COLS, rg = tid / COLS) runs an online LSE over rows rg, rg + RG, ... of column c
+// with CH loads in flight, row groups merge through LDS, the first COLS threads finish.
+template <typename T, bool KNOPP, int COLS, int CH>
+__global__ __launch_bounds__(1024) void k_sk_col_fused(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                       int it, int slot_f, int slot_g_prev,
+                                                       int slot_g_out) {
+  if (d.st[ST_DONE]) return;
+  constexpr int RG = 1024 / COLS;
+  __shared__ double sm[RG][COLS], ss[RG][COLS];
+  const int c = threadIdx.x % COLS, rg = threadIdx.x / COLS;
+  const int j = blockIdx.x * COLS + c;
+  const double* __restrict__ f = d.f + (int64_t)slot_f * a.I;
+  const double* __restrict__ ua = d.ua;
+  Lse l;
+  l.init();
+  if (j < a.J) {
+    const double vaj = KNOPP ? 0.0 : d.va[j];
+    for (int i0 = rg; i0 < a.I; i0 += RG * CH) {
+      double x[CH];
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int i = i0 + RG * k;
+        x[k] = -INFINITY;
+        if (i < a.I) {
+          const double ui = KNOPP ? 0.0 : ua[i];
+          x[k] = sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps, a.kclamp,
+                                f[i] - ui);
+        }
+      }
+      lse_chunk<CH>(l, x);
+    }
+  }
+  sm[rg][c] = l.m;
+  ss[rg][c] = l.s;
+  __syncthreads();
+#pragma unroll
+  for (int h = RG / 2; h > 0; h >>= 1) {
+    if (rg < h) {
+      l.merge(sm[rg + h][c], ss[rg + h][c]);
+      sm[rg][c] = l.m;
+      ss[rg][c] = l.s;
+    }
+    __syncthreads();
+  }
+  if (rg != 0) return;  // threads 0..COLS-1 (first lanes of wave 0)
+  double errp = 0.0;
+  bool fail = false, big = false;
+  if (j < a.J) finish_col(a, d, j, l.value(), slot_g_prev, slot_g_out, KNOPP, errp, fail, big);
+#pragma unroll
+  for (int o = COLS / 2; o > 0; o >>= 1) errp += __shfl_xor(errp, o, 64);
+  const unsigned long long lanes = COLS >= 64 ? ~0ull : (1ull << COLS) - 1;
+  const unsigned long long anyfail = __ballot(fail) & lanes, anybig = __ballot(big) & lanes;
+  if (threadIdx.x == 0) {
+    if (KNOPP) {
+      d.errpart[blockIdx.x] = errp;
+      if (anyfail) atomicOr((unsigned long long*)&d.st[ST_FAIL], 1ull);
+    } else if (anybig) {
+      atomicOr((unsigned long long*)&d.st[ST_BIG], 2ull);
+    }
+  }
+}
+
+// Column pass, split: workgroup = 16 waves x 64 consecutive columns (full 256-B / 512-B rows)
+// over one of NS row splits; partial (max, sum) pairs merged by k_sk_col_combine.
+template <typename T, bool KNOPP, int CH>
+__global__ __launch_bounds__(1024) void k_sk_col_part(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                      int slot_f, int rows_per_split) {
+  if (d.st[ST_DONE]) return;
+  __shared__ double sm[16][64], ss[16][64];
+  const int lane = lane_id(), w = wave_id();
+  const int j = blockIdx.x * 64 + lane;
+  const int r0 = blockIdx.y * rows_per_split, r1 = min(a.I, r0 + rows_per_split);
+  const double* __restrict__ f = d.f + (int64_t)slot_f * a.I;
+  const double* __restrict__ ua = d.ua;
+  Lse l;
+  l.init();
+  if (j < a.J) {
+    const double vaj = KNOPP ? 0.0 : d.va[j];
+    for (int i0 = r0 + w; i0 < r1; i0 += 16 * CH) {
+      double x[CH];
+#pragma unroll
+      for (int k = 0; k < CH; ++k) {
+        const int i = i0 + 16 * k;
+        x[k] = -INFINITY;
+        if (i < r1) {
+          const double ui = KNOPP ? 0.0 : ua[i];
+          x[k] = sk_term<KNOPP>(ui, vaj, (double)C[(int64_t)i * a.ldc + j], a.inv_eps, a.kclamp,
+                                f[i] - ui);
+        }
+      }
+      lse_chunk<CH>(l, x);
+    }
+  }
+  sm[w][lane] = l.m;
+  ss[w][lane] = l.s;
+  __syncthreads();
+  if (w != 0 || j >= a.J) return;
+  for (int q = 1; q < 16; ++q) l.merge(sm[q][lane], ss[q][lane]);
+  d.pm[(int64_t)blockIdx.y * a.J + j] = l.m;
+  d.ps[(int64_t)blockIdx.y * a.J + j] = l.s;
+}
+
+template <bool KNOPP>
+__global__ __launch_bounds__(256) void k_sk_col_combine(SkArgs a, SkDev d, int ns, int slot_g_prev,
+                                                        int slot_g_out) {
+  if (d.st[ST_DONE]) return;
+  __shared__ double red[4];
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  double errp = 0.0;
+  bool fail = false, big = false;
+  if (j < a.J) {
+    double m[kMaxSplits], sv[kMaxSplits];
+#pragma unroll
+    for (int q = 0; q < kMaxSplits; ++q) {  // all loads first, then the merges
+      m[q] = q < ns ? d.pm[(int64_t)q * a.J + j] : -INFINITY;
+      sv[q] = q < ns ? d.ps[(int64_t)q * a.J + j] : 0.0;
+    }
+    Lse l;
+    l.init();
+#pragma unroll
+    for (int q = 0; q < kMaxSplits; ++q) l.merge(m[q], sv[q]);
+    finish_col(a, d, j, l.value(), slot_g_prev, slot_g_out, KNOPP, errp, fail, big);
+  }
+  if (KNOPP) {
+    errp = wave_sum(errp);
+    if (lane_id() == 0) red[wave_id()] = errp;
+    if (__any(fail) && lane_id() == 0) atomicOr((unsigned long long*)&d.st[ST_FAIL], 1ull);
+    __syncthreads();
+    if (threadIdx.x == 0) d.errpart[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  } else if (__any(big) && lane_id() == 0) {
+    atomicOr((unsigned long long*)&d.st[ST_BIG], 2ull);
+  }
+}
+
+// STAB absorption, part A (one wave per row): decide, set ua = f, row sums of K.C.
+template <typename T>
+__global__ __launch_bounds__(256) void k_sk_absorb_rows(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                        int it, int slot, int max_iter,
+                                                        int init) {
+  if (d.st[ST_DONE]) return;
+  const bool absorb = init || (it % 10 == 0) || d.st[ST_BIG] || it == max_iter - 1;
+  if (!absorb) return;
+  const int i = blockIdx.x * 4 + wave_id();
+  if (i >= a.I) return;
+  const int lane = lane_id();
+  const double fi = init ? 0.0 : d.f[(int64_t)slot * a.I + i];
+  const double* g = d.g + (int64_t)slot * a.J;
+  const T* Ci = C + (int64_t)i * a.ldc;
+  double acc = 0.0;
+  for (int j = lane; j < a.J; j += 64) {
+    const double c = ld_c(Ci, j);
+    const double k = fmin(fi + (init ? 0.0 : g[j]) - c * a.inv_eps, a.kclamp);
+    acc += exp_f64(k) * c;
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    d.rowbuf[i] = acc;
+    d.ua[i] = fi;
+  }
+}
+
+// STAB absorption, part B (single workgroup): va = g, transport, tolerance break, bookkeeping.
+__global__ __launch_bounds__(1024) void k_sk_absorb_final(SkArgs a, SkDev d, int it, int slot,
+                                                          int max_iter, int init, double tol) {
+  if (d.st[ST_DONE]) return;
+  const bool absorb = init || (it % 10 == 0) || d.st[ST_BIG] || it == max_iter - 1;
+  __syncthreads();
+  if (!absorb) return;
+  __shared__ double red[1024];
+  const double* g = d.g + (int64_t)slot * a.J;
+  for (int j = threadIdx.x; j < a.J; j += 1024) d.va[j] = init ? 0.0 : g[j];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < a.I; i += 1024) s += d.rowbuf[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const double tnew = red[0];
+  d.st[ST_BIG] = 0;
+  if (init) {
+    d.sd[SD_TPREV] = tnew;
+    d.sd[SD_TNEW] = tnew;
+    return;
+  }
+  const double tprev = d.sd[SD_TPREV];
+  d.sd[SD_TNEW] = tnew;
+  if (fabs(tnew - tprev) / fabs(tprev) < tol) {
+    mark_done(d.st, it, 1, slot);  // break: ii stays, `transport` keeps the previous value
+    return;
+  }
+  d.sd[SD_TPREV] = tnew;
+  if (it == max_iter - 1) mark_done(d.st, max_iter, 0, slot);
+}
+
+__global__ void k_sk_logw(const double* __restrict__ wa, const double* __restrict__ wb, int I,
+                          int J, double* __restrict__ la, double* __restrict__ lb) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < I) la[t] = log(wa[t]);
+  if (t < J) lb[t] = log(wb[t]);
+}
+
+__global__ void k_sk_init(SkArgs a, SkDev d, double tol) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < 32) {
+    if (t < 8) d.st[t] = 0;
+    else d.sd[t] = 0.0;
+    if (t == 11) d.sd[11] = tol;
+  }
+  const bool knopp = a.mode == GNNEA_SK_KNOPP;
+  // KNOPP: u = 1/I, v = 1/J stored in slot 1 (the "previous" slot of iteration 0)
+  for (int i = t; i < a.I; i += gridDim.x * blockDim.x) {
+    d.ua[i] = 0.0;
+    d.f[i] = 0.0;
+    d.f[a.I + i] = knopp ? -log((double)a.I) : 0.0;
+  }
+  for (int j = t; j < a.J; j += gridDim.x * blockDim.x) {
+    d.va[j] = 0.0;
+    d.g[j] = 0.0;
+    d.g[a.J + j] = knopp ? -log((double)a.J) : 0.0;
+  }
+}
+
+// Final plan, one wave per row; also its row sums.
+// final ping-pong slot: the break / tolerance slot, else the last iteration run (1 = initial)
+__device__ __forceinline__ int sk_final_slot(const SkDev& d, int iters_run) {
+  if (d.st[ST_DONE]) return (int)(d.st[ST_SLOT] & 1);
+  return iters_run > 0 ? ((iters_run - 1) & 1) : 1;
+}
+
+template <typename T, typename P>
+__global__ __launch_bounds__(256) void k_sk_plan(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                 int iters_run, P* __restrict__ plan, int64_t ldp,
+                                                 double* __restrict__ row_sum) {
+  const int slot = sk_final_slot(d, iters_run);
+  const int i = blockIdx.x * 4 + wave_id();
+  if (i >= a.I) return;
+  const int lane = lane_id();
+  const bool knopp = a.mode == GNNEA_SK_KNOPP;
+  const double fi = knopp ? d.f[(int64_t)slot * a.I + i] : d.ua[i];
+  const double* g = knopp ? d.g + (int64_t)slot * a.J : d.va;
+  const T* Ci = C + (int64_t)i * a.ldc;
+  double rs = 0.0, loss = 0.0;
+  for (int j = lane; j < a.J; j += 64) {
+    const double c = ld_c(Ci, j);
+    double v;
+    if (knopp) {
+      // P = u * K * v with K = exp_f64(-M/reg) underflowing to 0 below -745.13
+      const double k = -c * a.inv_eps;
+      v = k < kExpUnderflow ? 0.0 : exp_f64(fi + g[j] + k);
+    } else {
+      v = exp_f64(fmin(fi + g[j] - c * a.inv_eps, a.kclamp));
+    }
+    if (plan) plan[(int64_t)i * ldp + j] = (P)v;
+    rs += v;
+    loss += v * c;
+  }
+  rs = wave_sum(rs);
+  loss = wave_sum(loss);
+  if (lane == 0) {
+    if (row_sum) row_sum[i] = rs;
+    d.rowbuf[i] = loss;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_sk_colsum(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                   int iters_run, double* __restrict__ col_sum) {
+  const int slot = sk_final_slot(d, iters_run);
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.J) return;
+  const bool knopp = a.mode == GNNEA_SK_KNOPP;
+  const double gj = knopp ? d.g[(int64_t)slot * a.J + j] : d.va[j];
+  const double* f = knopp ? d.f + (int64_t)slot * a.I : d.ua;
+  double s = 0.0;
+  for (int i = 0; i < a.I; ++i) {
+    const double c = ld_c(C, (int64_t)i * a.ldc + j);
+    if (knopp) {
+      const double k = -c * a.inv_eps;
+      s += k < kExpUnderflow ? 0.0 : exp_f64(f[i] + gj + k);
+    } else {
+      s += exp_f64(fmin(f[i] + gj - c * a.inv_eps, a.kclamp));
+    }
+  }
+  col_sum[j] = s;
+}
+
+__global__ __launch_bounds__(1024) void k_sk_loss(SkArgs a, SkDev d, int iters_run) {
+  __shared__ double red[1024];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < a.I; i += 1024) s += d.rowbuf[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    d.sd[SD_LOSS] = red[0];
+    if (!d.st[ST_DONE]) {
+      d.st[ST_ITERS] = iters_run;
+      d.st[ST_SLOT] = sk_final_slot(d, iters_run);
+    }
+  }
+}
+
+static bool sk_valid(const gnnea_sinkhorn* p) {
+  if (!p || !p->C || !p->ws || !p->a || !p->b) return false;
+  if (p->I < 1 || p->J < 1 || p->ldc < p->J) return false;
+  if (p->c_dtype != GNNEA_F32 && p->c_dtype != GNNEA_F64) return false;
+  if (p->mode < GNNEA_SK_KNOPP || p->mode > GNNEA_SK_RELAX) return false;
+  if (!(p->eps > 0.0)) return false;
+  return true;
+}
+
+static SkArgs sk_args(const gnnea_sinkhorn* p) {
+  SkArgs a;
+  a.mode = p->mode;
+  a.I = p->I;
+  a.J = p->J;
+  a.ldc = p->ldc;
+  a.inv_eps = 1.0 / p->eps;
+  const bool gen = p->mode == GNNEA_SK_GEN, relax = p->mode == GNNEA_SK_RELAX;
+  a.p_row = gen ? p->p : 1.0;
+  a.p_col = (gen || relax) ? p->p : 1.0;
+  a.kclamp = p->mode == GNNEA_SK_KNOPP ? INFINITY : kLn1e30;
+  const SkWs w = sk_plan(p->I, p->J);
+  a.la = (const double*)((const char*)p->ws + w.la);  // log a, log b: filled by init
+  a.lb = (const double*)((const char*)p->ws + w.lb);
+  return a;
+}
+
+// Launch configurations of the two passes (10*row + col); the path runs configuration 0, the
+// others are kept from the round-1 A/B timing (profiles/r01_microbench_sk_variants.json).
+//   row: 0 wave/row CH 8 | 1 wave/row CH 4 | 2 wave/row CH 16 | 3 4 waves/row CH 12 | 4 2 waves/row CH 8
+//   col: 0 fused 16 cols CH 16 | 1 split 64-col CH 8 + combine | 2 fused 8 cols CH 12 | 3 split CH 4
+// Default (0) = fastest measured at B = 3000 (profiles/r01_microbench_sk_variants.json).
+template <typename T, bool KNOPP>
+static void launch_row(int rv, const T* C, const SkArgs& a, const SkDev& d, int it, int si,
+                       int so, hipStream_t s) {
+  const int I = a.I;
+  switch (rv) {
+    case 1: hipLaunchKernelGGL((k_sk_row<T, KNOPP, 4, 1>), dim3(div_up(I, 4)), dim3(256), 0, s, C, a, d, it, si, so); break;
+    case 2: hipLaunchKernelGGL((k_sk_row<T, KNOPP, 16, 1>), dim3(div_up(I, 4)), dim3(256), 0, s, C, a, d, it, si, so); break;
+    case 3: hipLaunchKernelGGL((k_sk_row<T, KNOPP, 12, 4>), dim3(I), dim3(256), 0, s, C, a, d, it, si, so); break;
+    case 4: hipLaunchKernelGGL((k_sk_row<T, KNOPP, 8, 2>), dim3(div_up(I, 2)), dim3(256), 0, s, C, a, d, it, si, so); break;
+    default: hipLaunchKernelGGL((k_sk_row<T, KNOPP, 8, 1>), dim3(div_up(I, 4)), dim3(256), 0, s, C, a, d, it, si, so); break;
+  }
+}
+
+static int col_splits(int I, int J) {
+  const int strips = (J + 63) / 64;
+  int ns = (512 + strips - 1) / strips;
+  const int by_rows = (I + 63) / 64;
+  ns = ns > by_rows ? by_rows : ns;
+  ns = ns > kMaxSplits ? kMaxSplits : ns;
+  return ns < 1 ? 1 : ns;
+}
+
+template <typename T, bool KNOPP>
+static void launch_col(int cv, const T* C, const SkArgs& a, SkDev& d, int it, int sf, int sgp,
+                       int sgo, hipStream_t s) {
+  const int J = a.J;
+  switch (cv) {
+    case 0:
+      d.ncb = div_up(J, 16);
+      hipLaunchKernelGGL((k_sk_col_fused<T, KNOPP, 16, 16>), dim3(d.ncb), dim3(1024), 0, s, C, a, d, it, sf, sgp, sgo);
+      break;
+    case 2:
+      d.ncb = div_up(J, 8);
+      hipLaunchKernelGGL((k_sk_col_fused<T, KNOPP, 8, 12>), dim3(d.ncb), dim3(1024), 0, s, C, a, d, it, sf, sgp, sgo);
+      break;
+    default: {  // 1, 3: split + combine
+      const int ns = col_splits(a.I, J);
+      const int rps = (a.I + ns - 1) / ns;
+      d.ncb = div_up(J, 256);
+      if (cv == 3)
+        hipLaunchKernelGGL((k_sk_col_part<T, KNOPP, 4>), dim3(div_up(J, 64), ns), dim3(1024), 0, s, C, a, d, sf, rps);
+      else
+        hipLaunchKernelGGL((k_sk_col_part<T, KNOPP, 8>), dim3(div_up(J, 64), ns), dim3(1024), 0, s, C, a, d, sf, rps);
+      hipLaunchKernelGGL(k_sk_col_combine<KNOPP>, dim3(d.ncb), dim3(256), 0, s, a, d, ns, sgp, sgo);
+    }
+  }
+}
+
+template <typename T>
+static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t s) {
+  SkArgs a = sk_args(p);
+  SkDev d = sk_dev(p);
+  const int rv = 0, cv = 0;  // default pass configuration (variant field selects the path)
+  const dim3 gabs(div_up(p->I, 4));
+  const T* C = (const T*)p->C;
+  for (int it = first; it < first + count; ++it) {
+    const int cur = it & 1, prev = (it + 1) & 1;
+    if (p->mode == GNNEA_SK_KNOPP) {
+      launch_col<T, true>(cv, C, a, d, it, prev, prev, cur, s);  // sets d.ncb for the row pass
+      launch_row<T, true>(rv, C, a, d, it, cur, cur, s);
+    } else {
+      launch_row<T, false>(rv, C, a, d, it, prev, cur, s);
+      launch_col<T, false>(cv, C, a, d, it, cur, prev, cur, s);
+      hipLaunchKernelGGL(k_sk_absorb_rows<T>, gabs, dim3(256), 0, s, C, a, d, it, cur,
+                         p->max_iter, 0);
+      hipLaunchKernelGGL(k_sk_absorb_final, dim3(1), dim3(1024), 0, s, a, d, it, cur,
+                         p->max_iter, 0, p->tol);
+    }
+    GNNEA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+
+int64_t ws_bytes(int I, int J) {
+  if (I < 1 || J < 1) return GNNEA_EINVAL;
+  return sk_plan(I, J).total;
+}
+
+int init(const gnnea_sinkhorn* p, void* stream) {
+  if (!sk_valid(p)) return GNNEA_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  SkArgs a = sk_args(p);
+  SkDev d = sk_dev(p);
+  const int n = p->I > p->J ? p->I : p->J;
+  hipLaunchKernelGGL(k_sk_logw, dim3(div_up(n, 256)), dim3(256), 0, s, p->a, p->b, p->I, p->J,
+                     (double*)a.la, (double*)a.lb);
+  hipLaunchKernelGGL(k_sk_init, dim3(div_up(n > 32 ? n : 32, 256)), dim3(256), 0, s, a, d,
+                     p->tol);
+  GNNEA_LAUNCH_CHECK();
+  if (p->mode != GNNEA_SK_KNOPP) {  // initial transport = sum K0 . C   (sinkhorn_loss.py:195)
+    const dim3 grow(div_up(p->I, 4));
+    if (p->c_dtype == GNNEA_F32)
+      hipLaunchKernelGGL(k_sk_absorb_rows<float>, grow, dim3(256), 0, s, (const float*)p->C, a,
+                         d, 0, 0, p->max_iter, 1);
+    else
+      hipLaunchKernelGGL(k_sk_absorb_rows<double>, grow, dim3(256), 0, s, (const double*)p->C,
+                         a, d, 0, 0, p->max_iter, 1);
+    hipLaunchKernelGGL(k_sk_absorb_final, dim3(1), dim3(1024), 0, s, a, d, 0, 0, p->max_iter, 1,
+                       p->tol);
+    GNNEA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+int iterate(const gnnea_sinkhorn* p, int first, int count, void* stream) {
+  if (!sk_valid(p) || first < 0 || count < 1) return GNNEA_EINVAL;
+  if (p->c_dtype == GNNEA_F32) return sk_iter_t<float>(p, first, count, (hipStream_t)stream);
+  return sk_iter_t<double>(p, first, count, (hipStream_t)stream);
+}
+
+int finish(const gnnea_sinkhorn* p, void* plan, int plan_dtype, int64_t ldp, double* row_sum,
+           double* col_sum, void* stream) {
+  if (!sk_valid(p)) return GNNEA_EINVAL;
+  if (plan && plan_dtype != GNNEA_F32 && plan_dtype != GNNEA_F64) return GNNEA_EINVAL;
+  if (plan && ldp < p->J) return GNNEA_EINVAL;
+  // final potentials: the status block's slot after a break, else those of iteration
+  // iters_run-1 (iters_run == 0: the initial u = 1/I, v = 1/J)
+  hipStream_t s = (hipStream_t)stream;
+  SkArgs a = sk_args(p);
+  SkDev d = sk_dev(p);
+  const int slot = p->iters_run;
+  const dim3 grow(div_up(p->I, 4));
+#define GNNEA_PLAN(T, PT)                                                                   \
+  hipLaunchKernelGGL((k_sk_plan<T, PT>), grow, dim3(256), 0, s, (const T*)p->C, a, d, slot, \
+                     (PT*)plan, ldp, row_sum)
+  if (p->c_dtype == GNNEA_F32) {
+    if (plan_dtype == GNNEA_F32) GNNEA_PLAN(float, float);
+    else GNNEA_PLAN(float, double);
+  } else {
+    if (plan_dtype == GNNEA_F32) GNNEA_PLAN(double, float);
+    else GNNEA_PLAN(double, double);
+  }
+#undef GNNEA_PLAN
+  GNNEA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_sk_loss, dim3(1), dim3(1024), 0, s, a, d, p->iters_run);
+  GNNEA_LAUNCH_CHECK();
+  if (col_sum) {
+    const dim3 gcs(div_up(p->J, 256));
+    if (p->c_dtype == GNNEA_F32)
+      hipLaunchKernelGGL(k_sk_colsum<float>, gcs, dim3(256), 0, s, (const float*)p->C, a, d,
+                         slot, col_sum);
+    else
+      hipLaunchKernelGGL(k_sk_colsum<double>, gcs, dim3(256), 0, s, (const double*)p->C, a, d,
+                         slot, col_sum);
+    GNNEA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+}  // namespace sklog
+}  // namespace gnnea

@@ -12,6 +12,9 @@ from . import _lib
 from ._lib import SinkhornProblem, check, ptr, stream_of
 
 ST_DONE, ST_ITERS, ST_REASON, ST_SLOT = 0, 1, 2, 3
+# path of solve() calls that do not choose one: 0 = scaling form with the resident fp64 K
+# (falls back to 1 above J = 16384), 1 = fused log-domain passes (no I x J workspace)
+DEFAULT_VARIANT = 0
 SD_ERR, SD_TPREV, SD_LOSS = 8, 9, 10
 
 
@@ -37,9 +40,11 @@ def _status(ws):
 
 
 def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
-          want_plan=True, batch=10, variant=0):
+          want_plan=True, batch=10, variant=None):
     """Run one Sinkhorn solve; C is [I, J] fp32 / fp64 on a HIP device, a / b the weights."""
     _lib.require_device(C, a, b)
+    if variant is None:
+        variant = DEFAULT_VARIANT
     if C.dim() != 2:
         raise ValueError("gnnea.sinkhorn: C must be 2-D")
     if C.dtype not in (torch.float32, torch.float64):

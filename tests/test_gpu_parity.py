@@ -2,7 +2,7 @@
 
 Tolerance: norm-relative ||y - y_ref||_inf / ||y_ref||_inf <= 1e-4 for fp32
 outputs (measured fp32-vs-fp64 error of the reference itself: 1.8e-7 .. 4.1e-7); fp64 Sinkhorn
-(log domain vs the reference's scaling form): 1e-9 relative on plans and scalars.
+(both device paths, resident-K scaling form and log domain): 1e-9 relative on plans and scalars.
 """
 import numpy as np
 import pytest
@@ -242,9 +242,17 @@ def test_gemm_vs_fp64(device, shape, ta, tb):
 # ------------------------------------------------------------------------------------------ #
 # a9-a12: Sinkhorn family vs the reference fixtures                                           #
 # ------------------------------------------------------------------------------------------ #
+@pytest.fixture(params=[0, 1], ids=["scaling", "logdomain"])
+def sk_path(request, monkeypatch):
+    """Run a Sinkhorn test through both device paths (resident-K scaling form, log domain)."""
+    import gnnea.sinkhorn
+    monkeypatch.setattr(gnnea.sinkhorn, "DEFAULT_VARIANT", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("tag", ["s", "m"])
 @pytest.mark.parametrize("reg", [0.05, 0.01])
-def test_sinkhorn_family_vs_reference(golden, device, tag, reg):
+def test_sinkhorn_family_vs_reference(golden, device, tag, reg, sk_path):
     import SinkhornOT.sinkhorn_loss as SK
     from utils.ot_loss import sinkhorn
     S = golden("sinkhorn")
@@ -271,7 +279,7 @@ def test_sinkhorn_family_vs_reference(golden, device, tag, reg):
             assert rel_err(K[0].cpu(), S[kk]) < TOL64, name
 
 
-def test_sinkhorn_underflow_break(golden, device):
+def test_sinkhorn_underflow_break(golden, device, sk_path):
     from utils.ot_loss import sinkhorn
     S = golden("sinkhorn")
     M = torch.from_numpy(S["under_M"]).to(device)
@@ -280,7 +288,7 @@ def test_sinkhorn_underflow_break(golden, device):
     assert rel_err(P.cpu(), S["under_P"]) < TOL64
 
 
-def test_sinkhorn_reference_test_config(golden, device):
+def test_sinkhorn_reference_test_config(golden, device, sk_path):
     import SinkhornOT.sinkhorn_loss as SK
     S = golden("sinkhorn")
     M = torch.from_numpy(S["test_M"]).to(device).view(1, 100, 100)
