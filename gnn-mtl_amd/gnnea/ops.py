@@ -3,6 +3,8 @@
 Every function here launches libgnnea kernels on the tensor's current stream; none has a CPU
 path (``_lib.require_device``).  Reference call sites each op replaces are cited per function.
 """
+import ctypes
+
 import torch
 import torch.nn.functional as F
 
@@ -136,6 +138,24 @@ def matmul(x, w):
 # ------------------------------------------------------------------------------------------ #
 # CSR aggregation                                                                              #
 # ------------------------------------------------------------------------------------------ #
+INFINITY_CACHE_BYTES = 256 << 20
+
+
+def _off(t, r0):
+    """Device pointer of row r0 of a row-major fp32 tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr() + 4 * r0 * t.stride(0))
+
+
+def _blocks(csr, x):
+    """Row blocks to launch one after another: the diagonal blocks when the gathered matrix is
+    larger than the Infinity Cache (a single launch keeps all blocks' gathers in flight)."""
+    if x.shape[0] * x.shape[1] * 4 <= INFINITY_CACHE_BYTES:
+        return [(0, csr.n_rows)]
+    return csr.row_blocks()
+
+
 def spmm(csr, x, act=_lib.GNNEA_ACT_IDENTITY, out=None, beta=0.0):
     """out = act(A @ x + beta*out) with the gather-model CSR kernel (gnnea_spmm_csr_*_f32)."""
     _lib.require_device(x)
@@ -146,16 +166,19 @@ def spmm(csr, x, act=_lib.GNNEA_ACT_IDENTITY, out=None, beta=0.0):
     if out is None:
         out = torch.empty((csr.n_rows, x.shape[1]), dtype=torch.float32, device=x.device)
         beta = 0.0
+    L = _lib.lib()
+    st = stream_of(x.device)
     with torch.cuda.device(x.device):
-        if beta == 0.0:
-            check(_lib.lib().gnnea_spmm_csr_f32(
-                ptr(csr.rowptr), ptr(csr.col), ptr(csr.val), csr.n_rows, x.shape[1], ptr(x),
-                x.stride(0), ptr(out), out.stride(0), int(act), stream_of(x.device)))
-        else:
-            check(_lib.lib().gnnea_spmm_csr_beta_f32(
-                ptr(csr.rowptr), ptr(csr.col), ptr(csr.val), csr.n_rows, x.shape[1], ptr(x),
-                x.stride(0), float(beta), ptr(out), out.stride(0), int(act),
-                stream_of(x.device)))
+        for r0, r1 in _blocks(csr, x):
+            rp = ctypes.c_void_p(csr.rowptr.data_ptr() + 4 * r0)
+            if beta == 0.0:
+                check(L.gnnea_spmm_csr_f32(rp, ptr(csr.col), ptr(csr.val), r1 - r0, x.shape[1],
+                                           ptr(x), x.stride(0), _off(out, r0), out.stride(0),
+                                           int(act), st))
+            else:
+                check(L.gnnea_spmm_csr_beta_f32(rp, ptr(csr.col), ptr(csr.val), r1 - r0,
+                                                x.shape[1], ptr(x), x.stride(0), float(beta),
+                                                _off(out, r0), out.stride(0), int(act), st))
     return out
 
 
@@ -212,11 +235,13 @@ class HighwayFn(torch.autograd.Function):
         G = torch.empty_like(out)
         bias = _f32c(bias_gate) if bias_gate is not None else None
         with torch.cuda.device(hidden.device):
-            check(_lib.lib().gnnea_spmm_highway_f32(
-                ptr(csr.rowptr), ptr(csr.col), ptr(csr.val), N, D, ptr(hidden), hidden.stride(0),
-                ptr(gate_pre), gate_pre.stride(0), ptr(bias), ptr(resid), resid.stride(0),
-                ptr(out), out.stride(0), ptr(S), ptr(G), S.stride(0), int(act),
-                stream_of(hidden.device)))
+            for r0, r1 in _blocks(csr, hidden):
+                check(_lib.lib().gnnea_spmm_highway_f32(
+                    ctypes.c_void_p(csr.rowptr.data_ptr() + 4 * r0), ptr(csr.col), ptr(csr.val),
+                    r1 - r0, D, ptr(hidden), hidden.stride(0), _off(gate_pre, r0),
+                    gate_pre.stride(0), ptr(bias), _off(resid, r0), resid.stride(0),
+                    _off(out, r0), out.stride(0), _off(S, r0), _off(G, r0), S.stride(0),
+                    int(act), stream_of(hidden.device)))
         ctx.csr = csr
         ctx.act = act
         ctx.save_for_backward(S, G, resid)

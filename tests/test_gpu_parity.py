@@ -496,3 +496,30 @@ def test_gw_outer_loops_vs_reference(golden, device, tag):
         assert rel_err(T.cpu(), f["%s_%s_T" % (tag, name)]) < 1e-8, name
         ref_d = float(f["%s_%s_d" % (tag, name)])
         assert abs(float(d) - ref_d) <= 1e-8 * abs(ref_d), name
+
+
+def test_spmm_block_diagonal_launches(device, monkeypatch):
+    """The two-KG adjacency is launched per diagonal block when X exceeds the Infinity Cache;
+    per-row results are bit-identical to the single launch (same rows, same order)."""
+    from gnnea import ops, synth
+    from gnnea.graph import DeviceCSR
+    n = 300000
+    tr = synth.kg_pair_triples(n, 3 * n, 500, seed=4)
+    r, c, v = synth.adjacency_coo(tr, 2 * n, reference_order=False)
+    csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                             torch.from_numpy(v).to(device), 2 * n, 2 * n)
+    assert csr.row_blocks() == [(0, n), (n, 2 * n)]
+    x = torch.randn(2 * n, 128, device=device)
+    assert len(ops._blocks(csr, x)) == 2
+    y_blocks = ops.spmm(csr, x, 1)
+    monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 1 << 40)
+    assert len(ops._blocks(csr, x)) == 1
+    y_one = ops.spmm(csr, x, 1)
+    assert torch.equal(y_blocks, y_one)
+    # a graph with an edge across the KGs has no split
+    r2 = np.concatenate([r, [5]])
+    c2 = np.concatenate([c, [2 * n - 1]])
+    v2 = np.concatenate([v, [0.5]]).astype(np.float32)
+    csr2 = DeviceCSR.from_coo(torch.from_numpy(r2).to(device), torch.from_numpy(c2).to(device),
+                              torch.from_numpy(v2).to(device), 2 * n, 2 * n)
+    assert csr2.row_blocks() == [(0, 2 * n)]

@@ -76,6 +76,35 @@ def main():
         ms = timeit(lambda: ops.spmm(csr, X, _lib.GNNEA_ACT_RELU, out=Y), args.reps)
         res["spmm_relu"] = {"ms": ms, "GBps_gather_model": gather / ms / 1e6,
                             "edges_per_s": E / ms * 1e3}
+    if want("spmm_split"):
+        # the same SpMM as two launches, one per KG block of rows (block-diagonal adjacency)
+        Y = torch.empty_like(X)
+        L = _lib.lib()
+        st = _lib.stream_of(dev)
+
+        def two():
+            for k in range(2):
+                _lib.check(L.gnnea_spmm_csr_f32(
+                    _lib.ctypes.c_void_p(csr.rowptr.data_ptr() + 4 * k * n), _lib.ptr(csr.col),
+                    _lib.ptr(csr.val), n, D, _lib.ptr(X), D,
+                    _lib.ctypes.c_void_p(Y.data_ptr() + 4 * k * n * D), D, 1, st))
+        ms = timeit(two, args.reps)
+        res["spmm_relu_two_launches"] = {"ms": ms, "GBps_gather_model": gather / ms / 1e6,
+                                         "edges_per_s": E / ms * 1e3}
+    if want("spmm_slices"):
+        # per-rank work of the multi-GPU feature partition: one KG's rows (n of 2n), a column
+        # slice of width Dl (world 2: 300, world 4: 152 / 148, world 8: 76 / 72)
+        m = r < n
+        csr1 = DeviceCSR.from_coo(torch.from_numpy(r[m].astype(np.int32)).to(dev),
+                                  torch.from_numpy(c[m].astype(np.int32)).to(dev),
+                                  torch.from_numpy(v[m]).to(dev), n, n)
+        for Dl in (300, 152, 148, 76, 72):
+            Xs = X[:n, :Dl].contiguous()
+            Ys = torch.empty_like(Xs)
+            ms = timeit(lambda: ops.spmm(csr1, Xs, _lib.GNNEA_ACT_RELU, out=Ys), args.reps)
+            gb = 4 * (n + 1) + 8 * csr1.nnz + 4 * csr1.nnz * Dl + 4 * n * Dl
+            res["spmm_kg_D%d" % Dl] = {"ms": ms, "GBps_gather_model": gb / ms / 1e6,
+                                      "edges_per_s": csr1.nnz / ms * 1e3}
     if want("highway"):
         G = torch.randn(N, D, device=dev, generator=g)
         Wg = torch.zeros(D, device=dev)
