@@ -148,6 +148,11 @@ def _off(t, r0):
     return ctypes.c_void_p(t.data_ptr() + 4 * r0 * t.stride(0))
 
 
+def _off32(t, r0):
+    """Device pointer of element r0 of a 1-D 4-byte tensor (CSR rowptr)."""
+    return ctypes.c_void_p(t.data_ptr() + 4 * r0)
+
+
 def _blocks(csr, x):
     """Row blocks to launch one after another: the diagonal blocks when the gathered matrix is
     larger than the Infinity Cache (a single launch keeps all blocks' gathers in flight)."""
@@ -315,10 +320,11 @@ class GATFn(torch.autograd.Function):
         den = torch.empty_like(m)
         em = _f32c(edge_mask) if edge_mask is not None else None
         with torch.cuda.device(H.device):
-            check(_lib.lib().gnnea_gat_fwd_f32(
-                ptr(csr.rowptr), ptr(csr.col), N, ptr(H), H.stride(0), heads, d_head, ptr(s1),
-                ptr(s2), float(alpha), ptr(em), int(act), ptr(Y), Y.stride(0), ptr(m), ptr(den),
-                stream_of(H.device)))
+            for r0, r1 in _blocks(csr, H):  # per KG block when H exceeds the Infinity Cache
+                check(_lib.lib().gnnea_gat_fwd_f32(
+                    _off32(csr.rowptr, r0), ptr(csr.col), r1 - r0, ptr(H), H.stride(0), heads,
+                    d_head, _off(s1, r0), ptr(s2), float(alpha), ptr(em), int(act), _off(Y, r0),
+                    Y.stride(0), _off(m, r0), _off(den, r0), stream_of(H.device)))
         ctx.csr = csr
         ctx.meta = (heads, d_head, float(alpha), int(act))
         ctx.save_for_backward(H, a_all, s1, s2, m, den, Y, em if em is not None else torch.empty(0))
@@ -352,10 +358,12 @@ class GATFn(torch.autograd.Function):
             check(L.gnnea_gat_bwd_prep_f32(N, heads, d_head, ptr(dY), ptr(Y), Y.stride(0),
                                            ptr(s1), ptr(m), ptr(den), int(act), ptr(G),
                                            ptr(rec), st))
-            check(L.gnnea_gat_bwd_src_f32(
-                ptr(csrT.rowptr), ptr(csrT.col), ptr(csrT.perm), N, heads, d_head, ptr(H),
-                H.stride(0), ptr(s2), alpha, ptr(em), ptr(rec), ptr(G), G.stride(0), ptr(a_all),
-                ptr(dH), dH.stride(0), ptr(dzT), ptr(ds2), st))
+            for j0, j1 in _blocks(csrT, G):  # source rows j of A^T, per KG block
+                check(L.gnnea_gat_bwd_src_f32(
+                    _off32(csrT.rowptr, j0), ptr(csrT.col), ptr(csrT.perm), j1 - j0, heads,
+                    d_head, _off(H, j0), H.stride(0), _off(s2, j0), alpha, ptr(em), ptr(rec),
+                    ptr(G), G.stride(0), ptr(a_all), _off(dH, j0), dH.stride(0), ptr(dzT),
+                    _off(ds2, j0), st))
             check(L.gnnea_gat_bwd_dst_f32(ptr(csr.rowptr), ptr(tpos), N, heads, d_head,
                                           ptr(dzT), ptr(a_all), ptr(dH), dH.stride(0), ptr(ds1),
                                           st))

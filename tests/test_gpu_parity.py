@@ -512,10 +512,23 @@ def test_spmm_block_diagonal_launches(device, monkeypatch):
     x = torch.randn(2 * n, 128, device=device)
     assert len(ops._blocks(csr, x)) == 2
     y_blocks = ops.spmm(csr, x, 1)
+    heads, dh = 4, 75
+    H = (torch.randn(2 * n, heads * dh, device=device) * 0.1).requires_grad_(True)
+    a_all = (torch.randn(heads, 2 * dh, device=device) * 0.1).requires_grad_(True)
+    dy = torch.randn(2 * n, heads * dh, device=device)
+
+    def gat_run():
+        y = ops.GATFn.apply(H, a_all, csr, heads, dh, 0.2, 1, None)
+        gH, ga = torch.autograd.grad(y, (H, a_all), dy)
+        return y.detach(), gH, ga
+    assert len(ops._blocks(csr, H)) == 2
+    g_blocks = gat_run()
     monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 1 << 40)
     assert len(ops._blocks(csr, x)) == 1
     y_one = ops.spmm(csr, x, 1)
     assert torch.equal(y_blocks, y_one)
+    for u, w in zip(g_blocks, gat_run()):
+        assert torch.equal(u, w)
     # a graph with an edge across the KGs has no split
     r2 = np.concatenate([r, [5]])
     c2 = np.concatenate([c, [2 * n - 1]])
