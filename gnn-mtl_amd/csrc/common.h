@@ -64,6 +64,34 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
+// fp64 sum over the 64 lanes without the LDS path: DPP quad / half-row / row mirrors inside each
+// 16-lane row, then the gfx950 row swaps (v_permlane16_swap, v_permlane32_swap) across rows.
+// Every lane ends with the same value (pairs are only ever commuted).
+template <int CTRL>
+__device__ __forceinline__ double mov_dpp_f64(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)(unsigned)lo) | ((long long)hi << 32));
+}
+__device__ __forceinline__ double f64_of(unsigned lo, unsigned hi) {
+  return __builtin_bit_cast(double, ((long long)lo) | ((long long)hi << 32));
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  v += mov_dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += mov_dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += mov_dpp_f64<0x141>(v);  // row_half_mirror
+  v += mov_dpp_f64<0x140>(v);  // row_mirror
+  long long b = __builtin_bit_cast(long long, v);
+  auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+  auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  v = f64_of(lo[0], hi[0]) + f64_of(lo[1], hi[1]);
+  b = __builtin_bit_cast(long long, v);
+  lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  return f64_of(lo[0], hi[0]) + f64_of(lo[1], hi[1]);
+}
+
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5, "XCD swizzle must be
 // bijective"): consecutive logical blocks land on the same XCD so that rows that share
 // neighbours (ring edges, self loops) share one L2.  Speed only, never correctness.

@@ -217,10 +217,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d
                                                                const double* __restrict__ yin,
                                                                int gate) {
   constexpr int G = NCM <= 8 ? 32 / NCM : (NCM <= 16 ? 2 : 1);  // rows per group
-  if (gate && d.st[ST_DONE]) return;
-  if (PH1 && KNOPP && knopp_stop<KNOPP>(a, d, it)) return;
   __shared__ double red[2][kSweepWaves][G];
-  __shared__ double ys[2][G];
   const int w = wave_id(), lane = lane_id();
   const int wg = blockIdx.x;
   const int r0 = wg * a.rpw, r1 = min(a.I, r0 + a.rpw);
@@ -253,6 +250,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d
   };
   auto process = [&](const double (&kv)[G][NCM], int g0, int par) {
     const int nr = min(G, r1 - g0);
+    double yv[G];
     if (PH1) {
 #pragma unroll
       for (int r = 0; r < G; ++r) {
@@ -262,42 +260,50 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d
 #pragma unroll
           for (int k = 0; k < NCM; ++k) p = fma(KNOPP ? inva * kv[r][k] : kv[r][k], xs[k], p);
         }
-        p = wave_sum(p);
+        p = wave_sum_f64(p);
         if (lane == 0) red[par][w][r] = p;
       }
-      __syncthreads();
-      if (w == 0 && lane < nr) {
-        const int row = g0 + lane;
+      __syncthreads();  // the only barrier of the group: red[par] is double-buffered
+      // every wave reduces the 8 wave partials of each row itself (same order -> same y)
+#pragma unroll
+      for (int r = 0; r < G; ++r) {
         double sum = 0.0;
 #pragma unroll
-        for (int q = 0; q < kSweepWaves; ++q) sum += red[par][q][lane];
-        double y;
-        if (KNOPP) {
-          y = 1.0 / sum;  // u = 1 / (Kp v)
-          if (y != y || isinf(y)) mark_done(d.st, it, 2, (it + 1) & 1);
-        } else {
-          y = myclamp(powp(a.a[row] / sum, a.p_row));  // a = clamp((mu / K b)^p)
-          if (y > kBig) atomicOr((unsigned long long*)&d.st[ST_BIG], 1ull);
+        for (int q = 0; q < kSweepWaves; ++q) sum += red[par][q][r];
+        double y = 0.0;
+        if (r < nr) {
+          if (KNOPP) {
+            y = 1.0 / sum;  // u = 1 / (Kp v)
+          } else {
+            y = myclamp(powp(a.a[g0 + r] / sum, a.p_row));  // a = clamp((mu / K b)^p)
+          }
+          if (w == 0 && lane == r) {
+            d.u[(int64_t)slot_out * a.I + g0 + r] = y;
+            if (KNOPP && (y != y || isinf(y))) mark_done(d.st, it, 2, (it + 1) & 1);
+            if (!KNOPP && y > kBig) atomicOr((unsigned long long*)&d.st[ST_BIG], 1ull);
+          }
         }
-        d.u[(int64_t)slot_out * a.I + row] = y;
-        ys[par][lane] = y;
+        yv[r] = y;
       }
-    } else if (w == 0 && lane < nr) {
-      ys[par][lane] = yin[g0 + lane];
+    } else {
+#pragma unroll
+      for (int r = 0; r < G; ++r) yv[r] = r < nr ? yin[g0 + r] : 0.0;
     }
-    __syncthreads();  // ys[par] ready; red / ys of the other parity free for the next group
 #pragma unroll
     for (int r = 0; r < G; ++r) {
       if (r < nr) {
-        const double yr = ys[par][r];
 #pragma unroll
-        for (int k = 0; k < NCM; ++k) acc[k] = fma(yr, kv[r][k], acc[k]);
+        for (int k = 0; k < NCM; ++k) acc[k] = fma(yv[r], kv[r][k], acc[k]);
       }
     }
   };
   double kA[G][NCM], kB[G][NCM];
   int g0 = r0;
+  // the first group's loads go out before the stop decisions (two dependent round trips on the
+  // status block); loading K is harmless when the iteration turns out to be a no-op
   if (g0 < r1) load(kA, g0);
+  if (gate && d.st[ST_DONE]) return;
+  if (PH1 && KNOPP && knopp_stop<KNOPP>(a, d, it)) return;
   while (g0 < r1) {
     const int g1 = g0 + G;
     if (g1 < r1) load(kB, g1);
