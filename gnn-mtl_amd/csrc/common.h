@@ -49,7 +49,7 @@ __device__ __forceinline__ double readlane_d(double v, int k) {
 }
 
 template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
+__device__ __forceinline__ T wave_sum_shfl(T v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
@@ -64,9 +64,9 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
-// fp64 sum over the 64 lanes without the LDS path: DPP quad / half-row / row mirrors inside each
-// 16-lane row, then the gfx950 row swaps (v_permlane16_swap, v_permlane32_swap) across rows.
-// Every lane ends with the same value (pairs are only ever commuted).
+// Sums over the 64 lanes without the LDS path: DPP quad / half-row / row mirrors leave every lane
+// of a 16-lane row with that row's sum, then the four row sums are read as scalars and added in
+// row order.  Every lane ends with the same value.
 template <int CTRL>
 __device__ __forceinline__ double mov_dpp_f64(double v) {
   const long long b = __builtin_bit_cast(long long, v);
@@ -74,23 +74,33 @@ __device__ __forceinline__ double mov_dpp_f64(double v) {
   const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, false);
   return __builtin_bit_cast(double, ((long long)(unsigned)lo) | ((long long)hi << 32));
 }
-__device__ __forceinline__ double f64_of(unsigned lo, unsigned hi) {
-  return __builtin_bit_cast(double, ((long long)lo) | ((long long)hi << 32));
+template <int CTRL>
+__device__ __forceinline__ float mov_dpp_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
+                                                            0xf, 0xf, false));
 }
 __device__ __forceinline__ double wave_sum_f64(double v) {
   v += mov_dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
   v += mov_dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
   v += mov_dpp_f64<0x141>(v);  // row_half_mirror
   v += mov_dpp_f64<0x140>(v);  // row_mirror
-  long long b = __builtin_bit_cast(long long, v);
-  auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
-  auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-  v = f64_of(lo[0], hi[0]) + f64_of(lo[1], hi[1]);
-  b = __builtin_bit_cast(long long, v);
-  lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
-  hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
-  return f64_of(lo[0], hi[0]) + f64_of(lo[1], hi[1]);
+  return ((readlane_d(v, 0) + readlane_d(v, 16)) + readlane_d(v, 32)) + readlane_d(v, 48);
 }
+__device__ __forceinline__ float wave_sum_f32(float v) {
+  v += mov_dpp_f32<0xB1>(v);
+  v += mov_dpp_f32<0x4E>(v);
+  v += mov_dpp_f32<0x141>(v);
+  v += mov_dpp_f32<0x140>(v);
+  return ((readlane_f(v, 0) + readlane_f(v, 16)) + readlane_f(v, 32)) + readlane_f(v, 48);
+}
+
+// sum over the wave, every lane gets the result: VALU-only (DPP / permlane) for f32 and f64
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) { return wave_sum_shfl(v); }
+template <>
+__device__ __forceinline__ float wave_sum<float>(float v) { return wave_sum_f32(v); }
+template <>
+__device__ __forceinline__ double wave_sum<double>(double v) { return wave_sum_f64(v); }
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5, "XCD swizzle must be
 // bijective"): consecutive logical blocks land on the same XCD so that rows that share
