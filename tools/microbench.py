@@ -158,7 +158,7 @@ def main():
         res["gcn_layer_fwd_bwd"] = {"ms": ms}
     if want("sinkhorn"):
         from gnnea.sinkhorn import solve
-        B = 3000
+        B = int(os.environ.get("SK_B", "3000"))
         M = torch.rand(B, B, device=dev, generator=g)
         la = torch.ones(B, dtype=torch.float64, device=dev)
         variants = [int(v) for v in os.environ.get("SK_VARIANTS", "0").split(",")]
@@ -176,7 +176,8 @@ def main():
                         torch.cuda.synchronize()
                         ts.append(time.perf_counter() - s)
                     best.append((ts[1] - ts[0]) / 500 * 1e6)
-                key = "sinkhorn_" + name + ("" if var == 0 else "_v%d" % var)
+                key = "sinkhorn_" + name + ("" if var == 0 else "_v%d" % var) + \
+                    ("" if B == 3000 else "_B%d" % B)
                 res[key] = {"us_per_iter": float(np.median(best))}
     if want("l1"):
         # DBP15K-sized searches: get_neg of 4500 train entities over 30k, get_hits of 10.5k pairs
