@@ -170,10 +170,40 @@ __global__ __launch_bounds__(256) void k_gemm_wide(int M, int N, int K, const fl
   }
 }
 
+// slab reduction in fixed split order (deterministic); 4 outputs per thread when the rows allow
 __global__ void k_gemm_reduce(int M, int N, int splits, const float* __restrict__ slab,
                               const float* __restrict__ bias, float beta, float* __restrict__ C,
                               int64_t ldc) {
   const int64_t n = (int64_t)M * N;
+  const bool v4 = (N % 4 == 0) && (ldc % 4 == 0) && ((((uintptr_t)C) & 15) == 0);
+  if (v4) {
+    const int64_t n4 = n / 4;
+    const float4* sl = (const float4*)slab;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n4;
+         t += (int64_t)gridDim.x * blockDim.x) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      int q = 0;
+      for (; q + 2 <= splits; q += 2) {  // two slabs in flight
+        const float4 x = sl[(int64_t)q * n4 + t], y = sl[(int64_t)(q + 1) * n4 + t];
+        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+        b.x += y.x; b.y += y.y; b.z += y.z; b.w += y.w;
+      }
+      if (q < splits) {
+        const float4 x = sl[(int64_t)q * n4 + t];
+        a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+      }
+      float o[4] = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+      const int64_t e = 4 * t, row = e / N, col = e - row * N;
+      float* c = C + row * ldc + col;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (bias) o[k] += bias[col + k];
+        if (beta != 0.f) o[k] += beta * c[k];
+      }
+      *(float4*)c = make_float4(o[0], o[1], o[2], o[3]);
+    }
+    return;
+  }
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
        t += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
@@ -196,7 +226,7 @@ static int pick_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
   const int64_t bn = 64 * pick_wt(N);
   const int64_t tiles = ((M + GBM - 1) / GBM) * ((N + bn - 1) / bn);
   if (tiles >= 512 || K < 8 * GBK) return 1;
-  int64_t s = (768 + tiles - 1) / tiles;
+  int64_t s = (384 + tiles - 1) / tiles;  // ~384 workgroups: the slabs stay small
   const int64_t by_k = K / (8 * GBK);
   if (s > by_k) s = by_k;
   if (s > 256) s = 256;

@@ -99,7 +99,12 @@ __global__ __launch_bounds__(256) void k_margin_fwd(const float* __restrict__ ou
   if (threadIdx.x == 0) m[2 * tk + i] = (float)nact;
 }
 
-// one wave per output row; lanes over columns (float4 when VEC == 4)
+// Backward work item = one chunk of <= kMarginChunk incidence entries of one output row:
+// {row, beg, end, slot}.  slot < 0: the row has a single chunk and the wave writes grad[row];
+// otherwise the chunk's partial (integer-valued, exact in fp32) goes to scratch[slot] and
+// k_margin_combine adds a long row's chunks in slot order.  Long rows (hub entities that are the
+// hard negative of many pairs) are thus spread over many waves; the result stays deterministic.
+// Active entries are compacted per 64-entry batch and gathered four at a time.
 template <int VEC, int NC>
 __global__ __launch_bounds__(256) void k_margin_bwd(const float* __restrict__ out, int64_t ld,
                                                     int D, int t, int k,
@@ -110,21 +115,31 @@ __global__ __launch_bounds__(256) void k_margin_bwd(const float* __restrict__ ou
                                                     const int64_t* __restrict__ nl2,
                                                     const int64_t* __restrict__ nr2,
                                                     const float* __restrict__ m,
-                                                    const int32_t* __restrict__ inc_rowptr,
-                                                    const int32_t* __restrict__ inc_ent, int n_rows,
+                                                    const int32_t* __restrict__ inc_ent,
+                                                    const int4* __restrict__ items, int n_items,
                                                     const float* __restrict__ gout, float inv,
-                                                    float* __restrict__ grad, int64_t ldg) {
-  const int row = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
-  if (row >= n_rows) return;
+                                                    float* __restrict__ grad, int64_t ldg,
+                                                    float* __restrict__ scratch) {
+  const int it = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
+  if (it >= n_items) return;
+  const int4 item = items[it];
+  const int row = item.x, beg = item.y, end = item.z, slot = item.w;
   const int lane = lane_id();
   const int64_t tk = (int64_t)t * k, M = 2 * tk + t;
   RowFrag<VEC, NC> self, acc;
-  load_row<VEC, NC>(out + row * ld, D, self);
+  load_row<VEC, NC>(out + (int64_t)row * ld, D, self);
 #pragma unroll
   for (int c = 0; c < NC; ++c)
 #pragma unroll
     for (int e = 0; e < VEC; ++e) acc.v[c][e] = 0.f;
-  const int beg = inc_rowptr[row], end = inc_rowptr[row + 1];
+  auto add = [&](float mq, int64_t o) {
+    RowFrag<VEC, NC> x;
+    load_row<VEC, NC>(out + o * ld, D, x);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) acc.v[c][e] += mq * sgn(self.v[c][e] - x.v[c][e]);
+  };
   for (int base = beg; base < end; base += 64) {
     const int cnt = min(64, end - base);
     // lane-parallel decode of up to 64 incident entries: multiplier and the other row
@@ -141,31 +156,71 @@ __global__ __launch_bounds__(256) void k_margin_bwd(const float* __restrict__ ou
         else other = role_b ? left[j - 2 * tk] : right[j - 2 * tk];
       }
     }
-    for (int q = 0; q < cnt; ++q) {
-      const float mq = readlane_f(mj, q);
-      if (mq == 0.f) continue;  // inactive hinge term (wave-uniform)
-      const int64_t o = ((int64_t)readlane_i((int)(other >> 32), q) << 32) |
-                        (uint32_t)readlane_i((int)(other & 0xffffffff), q);
-      RowFrag<VEC, NC> x;
-      load_row<VEC, NC>(out + o * ld, D, x);
+    // active entries in lane order, four gathers in flight
+    unsigned long long act = __ballot(mj != 0.f);
+    auto pop = [&](float& mq, int64_t& o) {
+      const int q = __builtin_ctzll(act);
+      act &= act - 1;
+      mq = readlane_f(mj, q);
+      o = ((int64_t)readlane_i((int)(other >> 32), q) << 32) |
+          (uint32_t)readlane_i((int)(other & 0xffffffff), q);
+    };
+    while (__popcll(act) >= 4) {
+      float m0, m1, m2, m3;
+      int64_t o0, o1, o2, o3;
+      pop(m0, o0);
+      pop(m1, o1);
+      pop(m2, o2);
+      pop(m3, o3);
+      RowFrag<VEC, NC> x0, x1, x2, x3;
+      load_row<VEC, NC>(out + o0 * ld, D, x0);
+      load_row<VEC, NC>(out + o1 * ld, D, x1);
+      load_row<VEC, NC>(out + o2 * ld, D, x2);
+      load_row<VEC, NC>(out + o3 * ld, D, x3);
 #pragma unroll
       for (int c = 0; c < NC; ++c)
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) acc.v[c][e] += mq * sgn(self.v[c][e] - x.v[c][e]);
+        for (int e = 0; e < VEC; ++e) {
+          const float sv = self.v[c][e];
+          acc.v[c][e] += m0 * sgn(sv - x0.v[c][e]);
+          acc.v[c][e] += m1 * sgn(sv - x1.v[c][e]);
+          acc.v[c][e] += m2 * sgn(sv - x2.v[c][e]);
+          acc.v[c][e] += m3 * sgn(sv - x3.v[c][e]);
+        }
+    }
+    while (act) {
+      float mq;
+      int64_t o;
+      pop(mq, o);
+      add(mq, o);
     }
   }
-  const float c0 = gout[0] * inv;
+  const float c0 = slot < 0 ? gout[0] * inv : 1.0f;
+  float* dst = slot < 0 ? grad + (int64_t)row * ldg : scratch + (int64_t)slot * D;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int d = (c * 64 + lane) * VEC;
     if (d >= D) continue;
-    float* g = grad + row * ldg + d;
-    if constexpr (VEC == 4) {
-      *(float4*)g = make_float4(c0 * acc.v[c][0], c0 * acc.v[c][1], c0 * acc.v[c][2],
-                                c0 * acc.v[c][3]);
-    } else {
-      g[0] = c0 * acc.v[c][0];
-    }
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) dst[d + e] = c0 * acc.v[c][e];
+  }
+}
+
+// long rows: grad[row] = c * sum of the row's chunk partials, in slot order (one wave per row)
+__global__ __launch_bounds__(256) void k_margin_combine(const int32_t* __restrict__ long_rows,
+                                                        const int32_t* __restrict__ long_ptr,
+                                                        int n_long, int D,
+                                                        const float* __restrict__ scratch,
+                                                        const float* __restrict__ gout, float inv,
+                                                        float* __restrict__ grad, int64_t ldg) {
+  const int w = blockIdx.x * 4 + wave_id();
+  if (w >= n_long) return;
+  const int row = long_rows[w], s0 = long_ptr[w], s1 = long_ptr[w + 1];
+  const float c0 = gout[0] * inv;
+  for (int d = lane_id(); d < D; d += 64) {
+    float sum = 0.f;
+    for (int sl = s0; sl < s1; ++sl) sum += scratch[(int64_t)sl * D + d];
+    grad[(int64_t)row * ldg + d] = c0 * sum;
   }
 }
 
@@ -182,12 +237,12 @@ static void launch_fwd(const MarginArgs& a, float* A, float* h, float* m, hipStr
                      a.k, a.left, a.right, a.nl1, a.nr1, a.nl2, a.nr2, A, h, m);
 }
 template <int VEC, int NC>
-static void launch_bwd(const MarginArgs& a, const float* m, const int32_t* inc_rowptr,
-                       const int32_t* inc_ent, int n_rows, const float* gout, float inv,
-                       float* grad, int64_t ldg, hipStream_t s) {
-  hipLaunchKernelGGL((k_margin_bwd<VEC, NC>), dim3(div_up(n_rows, 4)), dim3(256), 0, s, a.out,
-                     a.ld, a.D, a.t, a.k, a.left, a.right, a.nl1, a.nr1, a.nl2, a.nr2, m,
-                     inc_rowptr, inc_ent, n_rows, gout, inv, grad, ldg);
+static void launch_bwd(const MarginArgs& a, const float* m, const int32_t* inc_ent,
+                       const int4* items, int n_items, const float* gout, float inv, float* grad,
+                       int64_t ldg, float* scratch, hipStream_t s) {
+  hipLaunchKernelGGL((k_margin_bwd<VEC, NC>), dim3(div_up(n_items, 4)), dim3(256), 0, s, a.out,
+                     a.ld, a.D, a.t, a.k, a.left, a.right, a.nl1, a.nr1, a.nl2, a.nr2, m, inc_ent,
+                     items, n_items, gout, inv, grad, ldg, scratch);
 }
 
 // NC = columns per lane chunk count; float4 path when rows are 16-B aligned
@@ -249,19 +304,24 @@ extern "C" int gnnea_margin_bwd_f32(const float* out, int64_t ld, int32_t D, int
                                     const int64_t* left, const int64_t* right,
                                     const int64_t* neg_left, const int64_t* neg_right,
                                     const int64_t* neg2_left, const int64_t* neg2_right,
-                                    const float* m, const int32_t* inc_rowptr,
-                                    const int32_t* inc_ent, int32_t n_rows,
-                                    const float* grad_loss, float scale, float* grad, int64_t ldg,
-                                    void* stream) {
+                                    const float* m, const int32_t* inc_ent,
+                                    const int32_t* items, int32_t n_items,
+                                    const int32_t* long_rows, const int32_t* long_ptr,
+                                    int32_t n_long, float* scratch, const float* grad_loss,
+                                    float scale, float* grad, int64_t ldg, void* stream) {
   const MarginArgs a{out, ld, D, t, k, left, right, neg_left, neg_right, neg2_left, neg2_right};
-  if (n_rows < 0) return GNNEA_EINVAL;
+  if (n_items < 0 || n_long < 0) return GNNEA_EINVAL;
   if (const int rc = margin_check(a)) return rc;
-  if (n_rows == 0) return 0;
-  if (!inc_rowptr || !grad_loss || !grad || ldg < D || (a.t > 0 && (!m || !inc_ent)))
-    return GNNEA_EINVAL;
-  const bool aligned_out = (ldg % 4 == 0) && (((uintptr_t)grad & 15) == 0);
-  GNNEA_MARGIN_DISPATCH(launch_bwd, a, m, inc_rowptr, inc_ent, n_rows, grad_loss, scale, grad, ldg,
-                        (hipStream_t)stream);
+  if (n_items == 0) return 0;
+  if (!m || !inc_ent || !items || !grad_loss || !grad || ldg < D) return GNNEA_EINVAL;
+  if (n_long > 0 && (!long_rows || !long_ptr || !scratch)) return GNNEA_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const bool aligned_out = true;
+  GNNEA_MARGIN_DISPATCH(launch_bwd, a, m, inc_ent, (const int4*)items, n_items, grad_loss, scale,
+                        grad, ldg, scratch, s);
+  if (n_long > 0)
+    hipLaunchKernelGGL(k_margin_combine, dim3(div_up(n_long, 4)), dim3(256), 0, s, long_rows,
+                       long_ptr, n_long, D, scratch, grad_loss, scale, grad, ldg);
   GNNEA_LAUNCH_CHECK();
   return 0;
 }

@@ -103,7 +103,8 @@ SIGNATURES = {
     "gnnea_margin_fwd_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
                                             _p, _p, _p, _p]),
     "gnnea_margin_bwd_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,
-                                            _p, _p, _p, _i32, _p, _f32, _p, _i64, _p]),
+                                            _p, _p, _p, _i32, _p, _p, _i32, _p, _p, _f32, _p,
+                                            _i64, _p]),
 }
 
 _LIB = None

@@ -35,23 +35,53 @@ def _idx(a, device, n_rows):
 _INCIDENCE = {}
 
 
+CHUNK = 256  # incidence entries per backward work item
+
+
+class Incidence:
+    """Row -> term-end incidence of the six index tensors and the backward work items."""
+
+    def __init__(self, idx, n_rows):
+        left, right, nl1, nr1, nl2, nr2 = idx
+        rows = torch.cat([nl1, nl2, left, nr1, nr2, right])
+        if rows.numel() >= 2 ** 31:
+            raise ValueError("gnnea.margin: too many terms for an int32 incidence")
+        dev = rows.device
+        cols = torch.arange(rows.numel(), dtype=torch.int64, device=dev)
+        self.csr = DeviceCSR.from_coo(rows, cols, None, n_rows, max(1, rows.numel()))
+        rp = self.csr.rowptr.long()
+        deg = rp[1:] - rp[:-1]
+        nch = (deg + CHUNK - 1) // CHUNK
+        r = torch.repeat_interleave(torch.arange(n_rows, device=dev), nch)
+        first = torch.cumsum(nch, 0) - nch
+        c = torch.arange(r.numel(), device=dev) - first[r]
+        beg = rp[r] + c * CHUNK
+        end = torch.minimum(rp[r + 1], beg + CHUNK)
+        multi = nch[r] > 1
+        slot = torch.where(multi, torch.cumsum(multi.long(), 0) - 1, torch.full_like(r, -1))
+        self.items = torch.stack([r, beg, end, slot], 1).to(torch.int32).contiguous()
+        lr = torch.nonzero(nch > 1).flatten()
+        self.long_rows = lr.to(torch.int32).contiguous()
+        self.long_ptr = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev),
+                                   torch.cumsum(nch[lr], 0)]).to(torch.int32).contiguous()
+        self.n_slots = int(multi.sum())  # one setup sync per negative set
+
+
+_INCIDENCE = {}
+
+
 def incidence(idx, n_rows):
-    """Row -> term-end incidence CSR of the six index tensors (include/gnnea.h, §8f #2), cached
-    per tuple of tensor objects: the negatives change every 50 epochs, the loss runs every one."""
+    """Incidence + work items of the six index tensors, cached per tuple of tensor objects: the
+    negatives change every 50 epochs, the loss runs every one."""
     key = tuple(id(a) for a in idx) + (n_rows,)
     hit = _INCIDENCE.get(key)
     if hit is not None and all(r() is a for r, a in zip(hit[0], idx)):
         return hit[1]
-    left, right, nl1, nr1, nl2, nr2 = idx
-    rows = torch.cat([nl1, nl2, left, nr1, nr2, right])
-    if rows.numel() >= 2 ** 31:
-        raise ValueError("gnnea.margin: too many terms for an int32 incidence")
-    cols = torch.arange(rows.numel(), dtype=torch.int64, device=rows.device)
-    csr = DeviceCSR.from_coo(rows, cols, None, n_rows, max(1, rows.numel()))
+    inc = Incidence(idx, n_rows)
     if len(_INCIDENCE) > 8:
         _INCIDENCE.clear()
-    _INCIDENCE[key] = (tuple(weakref.ref(a) for a in idx), csr)
-    return csr
+    _INCIDENCE[key] = (tuple(weakref.ref(a) for a in idx), inc)
+    return inc
 
 
 class MarginLossFn(torch.autograd.Function):
@@ -80,13 +110,16 @@ class MarginLossFn(torch.autograd.Function):
         t, k = ctx.tk
         N, D = out.shape
         inc = incidence((left, right, nl1, nr1, nl2, nr2), N)
-        grad = torch.empty((N, D), dtype=torch.float32, device=out.device)
+        grad = torch.zeros((N, D), dtype=torch.float32, device=out.device)
+        scratch = torch.empty((max(inc.n_slots, 1), D), dtype=torch.float32, device=out.device)
         g = g.reshape(1).to(torch.float32).contiguous()
         with torch.cuda.device(out.device):
             check(_lib.lib().gnnea_margin_bwd_f32(
                 ptr(out), out.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1),
-                ptr(nl2), ptr(nr2), ptr(m), ptr(inc.rowptr), ptr(inc.col), N, ptr(g),
-                1.0 / (2.0 * t * k), ptr(grad), D, stream_of(out.device)))
+                ptr(nl2), ptr(nr2), ptr(m), ptr(inc.csr.col), ptr(inc.items),
+                inc.items.shape[0], ptr(inc.long_rows), ptr(inc.long_ptr),
+                inc.long_rows.numel(), ptr(scratch), ptr(g), 1.0 / (2.0 * t * k), ptr(grad), D,
+                stream_of(out.device)))
         return grad, None, None, None, None, None, None, None, None
 
 

@@ -245,12 +245,16 @@ int gnnea_topk_rows_f32(const float* keys, int64_t ldk, int32_t nq, int32_t nx, 
  * Forward: A[t] = |out[left]-out[right]|_1, h[2tk] = relu(A_i + 1 - |out[neg_l]-out[neg_r]|_1)
  * (loss = sum(h) / (2tk), summed by the caller) and the integer multipliers m[M] the backward
  * needs (-[h>0] per negative, number of active terms per pair).
- * Backward: grad (n_rows x ldg, every row written) = scale * grad_loss[0] *
+ * Backward: grad (N x ldg, caller-zeroed) += scale * grad_loss[0] *
  *   sum over the incidence of each row r of m_j * sgn(out[r] - out[other end of term j]).
- * The incidence CSR (inc_rowptr[n_rows+1], inc_ent) is gnnea_coo_to_csr of
+ * The incidence CSR (inc_rowptr, inc_ent) is gnnea_coo_to_csr of
  *   rows = [nl1 | nl2 | left | nr1 | nr2 | right]  (2M entries),  cols = 0 .. 2M-1
- * (entry p < M: row is term p's first end; p >= M: term p-M's second end); it depends on the
- * index arrays only, so it is built once per negative set.  scale = 1 / (2tk).  D <= 1024.
+ * (entry p < M: row is term p's first end; p >= M: term p-M's second end).  Its rows are cut
+ * into work items {row, beg, end, slot} (int32 x 4, entries [beg, end) of inc_ent, at most a
+ * few hundred each): slot = -1 for a row with one item (written to grad directly), else a
+ * distinct scratch slot (scratch: n_slots x D floats); long rows are listed in long_rows with
+ * their slots long_ptr[w] .. long_ptr[w+1]-1 in order, and summed by a second kernel.  All of it
+ * depends on the index arrays only (built once per negative set).  scale = 1 / (2tk).  D <= 1024.
  * ------------------------------------------------------------------------------------------ */
 int gnnea_margin_fwd_f32(const float* out, int64_t ld, int32_t D, int32_t t, int32_t k,
                          const int64_t* left, const int64_t* right, const int64_t* neg_left,
@@ -259,9 +263,11 @@ int gnnea_margin_fwd_f32(const float* out, int64_t ld, int32_t D, int32_t t, int
 int gnnea_margin_bwd_f32(const float* out, int64_t ld, int32_t D, int32_t t, int32_t k,
                          const int64_t* left, const int64_t* right, const int64_t* neg_left,
                          const int64_t* neg_right, const int64_t* neg2_left,
-                         const int64_t* neg2_right, const float* m, const int32_t* inc_rowptr,
-                         const int32_t* inc_ent, int32_t n_rows, const float* grad_loss,
-                         float scale, float* grad, int64_t ldg, void* stream);
+                         const int64_t* neg2_right, const float* m, const int32_t* inc_ent,
+                         const int32_t* items, int32_t n_items, const int32_t* long_rows,
+                         const int32_t* long_ptr, int32_t n_long, float* scratch,
+                         const float* grad_loss, float scale, float* grad, int64_t ldg,
+                         void* stream);
 
 #ifdef __cplusplus
 }

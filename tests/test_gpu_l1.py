@@ -140,7 +140,8 @@ def test_margin_loss_vs_reference(golden, device):
 
 
 @pytest.mark.parametrize("N,D,t,k,anchored", [(500, 300, 60, 7, True), (300, 37, 40, 5, False),
-                                              (2000, 1024, 16, 33, True), (50, 8, 30, 9, False)])
+                                              (2000, 1024, 16, 33, True), (50, 8, 30, 9, False),
+                                              (40, 64, 300, 30, False)])  # hub rows: chunks
 def test_margin_vs_oracle(device, N, D, t, k, anchored):
     """Active and inactive hinge terms, repeated rows, non-anchored negatives, scalar and float4
     paths; fp32 kernel vs fp64 oracle."""
