@@ -178,16 +178,20 @@ def main():
     else:  # own-block + remote-block SpMM launches (the wait for the halo excluded)
         kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3])
                                    for e in evs]))
-    stats = torch.tensor([elapsed, float(shard.nnz), kernel_ms], dtype=torch.float64,
+    # units = edge aggregations over the full feature width: a rank that aggregates its KG's
+    # edges over Dl of the D columns contributes nnz * Dl / D of them (the slices of a KG group
+    # add up to each edge exactly once); row shards contribute their own rows' edges
+    units = float(shard.nnz) * Dl / D
+    stats = torch.tensor([elapsed, units, kernel_ms], dtype=torch.float64,
                          device="cpu" if args.rehearse else device)
     if world > 1:
         allst = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(allst, stats)
         allst = torch.stack(allst).cpu()
         elapsed = float(allst[:, 0].max())
-        total_nnz = float(allst[:, 1].sum())
+        total_nnz = float(allst[:, 1].sum())  # = nnz of the whole graph
     else:
-        total_nnz = float(shard.nnz)
+        total_nnz = units
     ms_per_step = elapsed / args.steps * 1e3
     value = total_nnz / (elapsed / args.steps)
 
@@ -209,7 +213,7 @@ def main():
             "config": {"workload": "GCN aggregation relu(A.H) (layers/layers.py:35-38) on the "
                                    "cfg-4 synthetic 2x%d-entity / 2x%d-triple KG pair, D=%d"
                                    % (n, shard_t(n), D),
-                       "nnz": int(total_nnz), "nodes": 2 * n, "D": D,
+                       "nnz": int(round(total_nnz)), "nodes": 2 * n, "D": D,
                        "parallelism": "single GPU" if world == 1 else
                        ("2 KG groups of %d GPUs, feature-column slices (no exchange)" % shard.g
                         if part.kind == "features" else
