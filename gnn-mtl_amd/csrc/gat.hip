@@ -24,45 +24,109 @@ __device__ __forceinline__ float hsel(const float (&w)[H], int h) {
 
 __device__ __forceinline__ float lrelu(float z, float alpha) { return z > 0.f ? z : alpha * z; }
 
+// ---------------------------------------------------------------------------------------- //
+// Head-grouped lane layout (scores and backward src pass).  With HP = H rounded up to a power of
+// two, each head owns LPH = 64 / HP consecutive lanes and lane s of a head owns the EPL
+// consecutive elements d = s*EPL + t of that head (d < d_head).  Every lane then works for ONE
+// head: per-head dot products are sums over a lane group (DPP steps inside 16-lane rows, one
+// bpermute per extra row), and no per-element head selection is needed.
+// ---------------------------------------------------------------------------------------- //
+template <int H> struct Pow2 { static constexpr int v = H <= 1 ? 1 : H <= 2 ? 2 : H <= 4 ? 4 : 8; };
+
+template <int H, int EPL>
+struct HeadLanes {
+  static constexpr int HP = Pow2<H>::v, LPH = 64 / HP;
+  int h, d0;           // the lane's head and first element within the head
+  bool ok[EPL];        // element exists
+  int c[EPL];          // column in the head-concatenated row (clamped in range when !ok)
+  __device__ __forceinline__ HeadLanes(int lane, int dh) {
+    h = lane / LPH;
+    d0 = (lane % LPH) * EPL;
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) {
+      ok[t] = h < H && d0 + t < dh;
+      c[t] = ok[t] ? h * dh + d0 + t : 0;
+    }
+  }
+};
+
+// Sums of NV values over each head's LPH lanes at once, by reduce-scatter: DPP steps on lane bits
+// 3 (row_mirror, only when a head spans whole rows), 2 (row_half_mirror), 1 (quad reverse), 0
+// (quad swap) each pair a lane with a partner that agrees on the bits split before, halving the
+// live values; heads wider than a row add xor-16 / xor-32 steps on the one remaining value.
+// Afterwards lane h*LPH + grp_lane<NV, LPH>(v) holds head h's full sum of value v.
+template <int CTRL, int CNT, int NV>
+__device__ __forceinline__ void rs_step(float (&p)[NV], bool up) {
+  if constexpr (CNT > 1) {
+    constexpr int half = CNT / 2;
+#pragma unroll
+    for (int t = 0; t < half; ++t) {
+      const float keep = up ? p[t + half] : p[t];
+      const float send = up ? p[t] : p[t + half];
+      p[t] = keep + mov_dpp_f32<CTRL>(send);
+    }
+  } else {
+    p[0] += mov_dpp_f32<CTRL>(p[0]);
+  }
+}
+template <int NV, int LPH>
+__device__ __forceinline__ float grp_sum(float (&p)[NV], int lane) {
+  static_assert(LPH >= 8 && (NV & (NV - 1)) == 0 && NV <= (LPH >= 16 ? 16 : 8), "grp_sum shape");
+  if constexpr (LPH >= 16) {
+    rs_step<0x140, NV, NV>(p, lane & 8);      // row_mirror: lane ^ 15
+    rs_step<0x141, NV / 2, NV>(p, lane & 4);  // row_half_mirror: lane ^ 7
+    rs_step<0x1B, NV / 4, NV>(p, lane & 2);   // quad_perm [3,2,1,0]: lane ^ 3
+    rs_step<0xB1, NV / 8, NV>(p, lane & 1);   // quad_perm [1,0,3,2]: lane ^ 1
+  } else {
+    rs_step<0x141, NV, NV>(p, lane & 4);
+    rs_step<0x1B, NV / 2, NV>(p, lane & 2);
+    rs_step<0xB1, NV / 4, NV>(p, lane & 1);
+  }
+  float v = p[0];
+  if constexpr (LPH >= 32) v += __shfl_xor(v, 16, 64);
+  if constexpr (LPH >= 64) v += __shfl_xor(v, 32, 64);
+  return v;
+}
+template <int NV, int LPH>
+__device__ __forceinline__ constexpr int grp_lane(int v) { return v * ((LPH >= 16 ? 16 : 8) / NV); }
+
 // s1[i,h] = sum_d H[i, h*dh+d] * a[h, d];  s2[i,h] = sum_d H[i, h*dh+d] * a[h, dh+d]
-template <int H, int NCH>
-__global__ __launch_bounds__(256) void k_gat_scores(const float4* __restrict__ Hm, int64_t ldh4,
-                                                    int n_rows, int D, int dh,
+// A wave walks rows (grid-stride) with the lane's slice of a preloaded.
+template <int H, int EPL>
+__global__ __launch_bounds__(256) void k_gat_scores(const float* __restrict__ Hm, int64_t ldh,
+                                                    int n_rows, int dh,
                                                     const float* __restrict__ a,
                                                     float* __restrict__ s1,
                                                     float* __restrict__ s2) {
-  const int row = blockIdx.x * 4 + wave_id();
-  if (row >= n_rows) return;
+  using L = HeadLanes<H, EPL>;
   const int lane = lane_id();
-  float p1[H], p2[H];
+  const L hl(lane, dh);
+  float a1[EPL], a2[EPL];
 #pragma unroll
-  for (int h = 0; h < H; ++h) p1[h] = p2[h] = 0.f;
-#pragma unroll
-  for (int q = 0; q < NCH; ++q) {
-    const int c4 = lane + 64 * q;
-    if (4 * c4 >= D) continue;
-    const float4 x = Hm[(int64_t)row * ldh4 + c4];
-    const float xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int c = 4 * c4 + t;
-      if (c >= D) continue;
-      const int h = c / dh, d = c - h * dh;
-      const float v1 = xs[t] * a[h * 2 * dh + d];
-      const float v2 = xs[t] * a[h * 2 * dh + dh + d];
-#pragma unroll
-      for (int k = 0; k < H; ++k) {
-        p1[k] += (h == k) ? v1 : 0.f;
-        p2[k] += (h == k) ? v2 : 0.f;
-      }
-    }
+  for (int t = 0; t < EPL; ++t) {
+    const int d = hl.ok[t] ? hl.d0 + t : 0;
+    const int hh = hl.ok[t] ? hl.h : 0;
+    a1[t] = hl.ok[t] ? a[hh * 2 * dh + d] : 0.f;
+    a2[t] = hl.ok[t] ? a[hh * 2 * dh + dh + d] : 0.f;
   }
+  const int nw = gridDim.x * 4;
+  for (int row = blockIdx.x * 4 + wave_id(); row < n_rows; row += nw) {
+    const float* x = Hm + (int64_t)row * ldh;
+    float xv[EPL];
 #pragma unroll
-  for (int h = 0; h < H; ++h) {
-    const float r1 = wave_sum(p1[h]), r2 = wave_sum(p2[h]);
-    if (lane == 0) {
-      s1[(int64_t)row * H + h] = r1;
-      s2[(int64_t)row * H + h] = r2;
+    for (int t = 0; t < EPL; ++t) xv[t] = x[hl.c[t]];
+    float p[2] = {0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) {
+      const float v = hl.ok[t] ? xv[t] : 0.f;
+      p[0] = fmaf(v, a1[t], p[0]);
+      p[1] = fmaf(v, a2[t], p[1]);
+    }
+    const float r = grp_sum<2, L::LPH>(p, lane);
+    const int o = lane % L::LPH;
+    if (hl.h < H) {
+      if (o == grp_lane<2, L::LPH>(0)) s1[(int64_t)row * H + hl.h] = r;
+      if (o == grp_lane<2, L::LPH>(1)) s2[(int64_t)row * H + hl.h] = r;
     }
   }
 }
@@ -77,6 +141,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd(const int32_t* __restrict__ row
                                                  float4* __restrict__ Y, int64_t ldy4,
                                                  float* __restrict__ m_out,
                                                  float* __restrict__ den_out) {
+  constexpr int kFE = 2;  // edges per chunk (measured: 2 beats 1 and 4)
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const int row = blk * 4 + wave_id();
   if (row >= n_rows) return;
@@ -135,52 +200,33 @@ __global__ __launch_bounds__(256) void k_gat_fwd(const int32_t* __restrict__ row
         wl[h] = emask ? w * emask[(int64_t)(base + lane) * H + h] : w;
       }
     }
-    int k = 0;
-    for (; k + 2 <= cnt; k += 2) {
-      const int j0 = readlane_i(mj, k), j1 = readlane_i(mj, k + 1);
-      float w0[H], w1[H];
+    // kFE edges at a time: their neighbour rows are gathered together (kFE * NCH loads in
+    // flight), then accumulated in edge order
+    for (int k = 0; k < cnt; k += kFE) {
+      float4 r[kFE][NCH];
+      float w[kFE][H];
 #pragma unroll
-      for (int h = 0; h < H; ++h) {
-        w0[h] = readlane_f(wl[h], k);
-        w1[h] = readlane_f(wl[h], k + 1);
+      for (int e = 0; e < kFE; ++e) {
+        const int ke = min(k + e, cnt - 1);  // past the chunk: a valid row, not accumulated
+        const float4* x = Hm + (int64_t)readlane_i(mj, ke) * ldh4 + lane;
+#pragma unroll
+        for (int h = 0; h < H; ++h) w[e][h] = readlane_f(wl[h], ke);
+#pragma unroll
+        for (int q = 0; q < NCH; ++q)
+          if (own[q]) r[e][q] = x[64 * q];
       }
-      const float4* x0 = Hm + (int64_t)j0 * ldh4 + lane;
-      const float4* x1 = Hm + (int64_t)j1 * ldh4 + lane;
-      float4 r0[NCH], r1[NCH];
 #pragma unroll
-      for (int q = 0; q < NCH; ++q)
-        if (own[q]) {
-          r0[q] = x0[64 * q];
-          r1[q] = x1[64 * q];
-        }
+      for (int e = 0; e < kFE; ++e) {
+        if (k + e >= cnt) break;  // uniform
 #pragma unroll
-      for (int q = 0; q < NCH; ++q)
-        if (own[q]) {
-          acc[q].x = fmaf(hsel<H>(w0, hd[q][0]), r0[q].x, acc[q].x);
-          acc[q].y = fmaf(hsel<H>(w0, hd[q][1]), r0[q].y, acc[q].y);
-          acc[q].z = fmaf(hsel<H>(w0, hd[q][2]), r0[q].z, acc[q].z);
-          acc[q].w = fmaf(hsel<H>(w0, hd[q][3]), r0[q].w, acc[q].w);
-          acc[q].x = fmaf(hsel<H>(w1, hd[q][0]), r1[q].x, acc[q].x);
-          acc[q].y = fmaf(hsel<H>(w1, hd[q][1]), r1[q].y, acc[q].y);
-          acc[q].z = fmaf(hsel<H>(w1, hd[q][2]), r1[q].z, acc[q].z);
-          acc[q].w = fmaf(hsel<H>(w1, hd[q][3]), r1[q].w, acc[q].w);
-        }
-    }
-    for (; k < cnt; ++k) {
-      const int j0 = readlane_i(mj, k);
-      float w0[H];
-#pragma unroll
-      for (int h = 0; h < H; ++h) w0[h] = readlane_f(wl[h], k);
-      const float4* x0 = Hm + (int64_t)j0 * ldh4 + lane;
-#pragma unroll
-      for (int q = 0; q < NCH; ++q)
-        if (own[q]) {
-          const float4 r = x0[64 * q];
-          acc[q].x = fmaf(hsel<H>(w0, hd[q][0]), r.x, acc[q].x);
-          acc[q].y = fmaf(hsel<H>(w0, hd[q][1]), r.y, acc[q].y);
-          acc[q].z = fmaf(hsel<H>(w0, hd[q][2]), r.z, acc[q].z);
-          acc[q].w = fmaf(hsel<H>(w0, hd[q][3]), r.w, acc[q].w);
-        }
+        for (int q = 0; q < NCH; ++q)
+          if (own[q]) {
+            acc[q].x = fmaf(hsel<H>(w[e], hd[q][0]), r[e][q].x, acc[q].x);
+            acc[q].y = fmaf(hsel<H>(w[e], hd[q][1]), r[e][q].y, acc[q].y);
+            acc[q].z = fmaf(hsel<H>(w[e], hd[q][2]), r[e][q].z, acc[q].z);
+            acc[q].w = fmaf(hsel<H>(w[e], hd[q][3]), r[e][q].w, acc[q].w);
+          }
+      }
     }
   }
   float rinv[H];
@@ -214,48 +260,6 @@ __global__ __launch_bounds__(256) void k_gat_fwd(const int32_t* __restrict__ row
 //   dst  (rows i of A): ds1_i = sum_j dz_ij (read through the inverse permutation),
 //        dH_i += ds1_i (x) a1
 // ---------------------------------------------------------------------------------------- //
-
-// Sum of p[h] over the 64 lanes for every head at once, by reduce-scatter: stage s halves the
-// number of live values per lane by exchanging across lane bit (5 - s); afterwards each lane
-// holds the full sum for one head, hp_of_lane(lane).  HP (power of two) shuffles+log2 instead
-// of 6*HP.  Returns the value; head_lane(h) gives a lane holding head h.
-template <int HP>
-__device__ __forceinline__ float rs_sum(float (&p)[HP], int lane) {
-  int cnt = HP, bit = 32;
-#pragma unroll
-  for (int st = 0; st < 6; ++st) {
-    if (cnt > 1) {
-      const bool up = lane & bit;
-      const int half = cnt / 2;
-#pragma unroll
-      for (int t = 0; t < HP / 2; ++t) {
-        if (t < half) {
-          const float keep = up ? p[t + half] : p[t];
-          const float send = up ? p[t] : p[t + half];
-          p[t] = keep + __shfl_xor(send, bit, 64);
-        }
-      }
-      cnt = half;
-    } else {
-      p[0] += __shfl_xor(p[0], bit, 64);
-    }
-    bit >>= 1;
-  }
-  return p[0];
-}
-template <int HP>
-__device__ __forceinline__ int head_lane(int h) {
-  // stage s keeps the upper half on lanes with bit (5 - s) set
-  int lane = 0, cnt = HP, bit = 32;
-  while (cnt > 1) {
-    const int half = cnt / 2;
-    if (h >= half) { lane |= bit; h -= half; }
-    cnt = half;
-    bit >>= 1;
-  }
-  return lane;
-}
-template <int H> struct Pow2 { static constexpr int v = H <= 1 ? 1 : H <= 2 ? 2 : H <= 4 ? 4 : 8; };
 
 template <int ACT, int H, int NCH>
 __global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
@@ -299,35 +303,37 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
   }
 }
 
-template <int H, int NCH>
+// Head-grouped layout: per in-edge (i, j) the lane accumulates alpha*mask*G_i into its own
+// elements and the product G_i . H_j over them; kEB edges' G rows are gathered together (the next
+// chunk's in flight meanwhile) and their per-head dot products reduced by one grp_sum (lane h*LPH + grp_lane(e) gets edge e, head h).
+template <int H, int EPL>
 __global__ __launch_bounds__(256) void k_gat_bwd_src(
     const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT,
-    const int64_t* __restrict__ permT, int n_rows, int D, int dh, const float4* __restrict__ Hm,
-    int64_t ldh4, const float* __restrict__ s2, float alpha, const float* __restrict__ emask,
-    const float4* __restrict__ rec, const float4* __restrict__ G, int64_t ldg4,
-    const float* __restrict__ a, float4* __restrict__ dH, int64_t lddh4, float* __restrict__ dzT,
+    const int64_t* __restrict__ permT, int n_rows, int dh, const float* __restrict__ Hm,
+    int64_t ldh, const float* __restrict__ s2, float alpha, const float* __restrict__ emask,
+    const float4* __restrict__ rec, const float* __restrict__ G, int64_t ldg,
+    const float* __restrict__ a, float* __restrict__ dH, int64_t lddh, float* __restrict__ dzT,
     float* __restrict__ ds2) {
-  constexpr int HP = Pow2<H>::v;
+  using L = HeadLanes<H, EPL>;
+  constexpr int LPH = L::LPH;
+  constexpr int kEB = 2;  // edges per chunk (measured: 2 beats 4 and 8 once double-buffered)
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const int row = blk * 4 + wave_id();  // source node j
   if (row >= n_rows) return;
   const int lane = lane_id();
   const int beg = rowptrT[row], end = rowptrT[row + 1];
+  const L hl(lane, dh);
+  const int hme = hl.h < H ? hl.h : 0;
 
-  int hd[NCH][4];
-  bool own[NCH];
-  float4 hj[NCH], acc[NCH];
+  float hj[EPL], acc[EPL];
+  {
+    const float* x = Hm + (int64_t)row * ldh;
 #pragma unroll
-  for (int q = 0; q < NCH; ++q) {
-    const int c4 = lane + 64 * q;
-    own[q] = 4 * c4 < D;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int c = 4 * c4 + t;
-      hd[q][t] = c < D ? c / dh : H;
+    for (int t = 0; t < EPL; ++t) {
+      const float v = x[hl.c[t]];
+      hj[t] = hl.ok[t] ? v : 0.f;
+      acc[t] = 0.f;
     }
-    hj[q] = own[q] ? Hm[(int64_t)row * ldh4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
-    acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float sj[H], ds2p[H];
 #pragma unroll
@@ -336,60 +342,85 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(
     ds2p[h] = 0.f;
   }
 
+  // chunk loads depend only on the in-neighbour ids: chunk c + 1 is in flight while chunk c is
+  // reduced (register double buffer), and chunk 0 goes out before the attention records arrive
+  float gA[kEB][EPL], gB[kEB][EPL];
+  auto load = [&](float (&g)[kEB][EPL], int mi, int k, int cnt) {
+#pragma unroll
+    for (int e = 0; e < kEB; ++e) {
+      const float* gr = G + (int64_t)readlane_i(mi, min(k + e, cnt - 1)) * ldg;
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) g[e][t] = gr[hl.c[t]];
+    }
+  };
   for (int base = beg; base < end; base += 64) {
     const int cnt = min(64, end - base);
     int mi = 0;
-    float al[H], zl[H], ml[H], cl[H], wl[H], dzl[H];
-#pragma unroll
-    for (int h = 0; h < H; ++h) al[h] = zl[h] = cl[h] = wl[h] = dzl[h] = 0.f, ml[h] = 1.f;
+    int64_t pe = 0;
     if (lane < cnt) {
       mi = colT[base + lane];  // destination row i of the forward edge (i, j)
-      const int64_t e = permT[base + lane];
-#pragma unroll
-      for (int h = 0; h < H; ++h) {
-        const float4 r = rec[(int64_t)mi * H + h];  // {s1_i, m_i, 1/den_i, c_i}
-        const float z = r.x + sj[h];
-        zl[h] = z;
-        al[h] = __expf(-lrelu(z, alpha) - r.y) * r.z;
-        cl[h] = r.w;
-        ml[h] = emask ? emask[e * H + h] : 1.f;
-        wl[h] = al[h] * ml[h];
-      }
+      pe = permT[base + lane];
     }
-    for (int k = 0; k < cnt; ++k) {
-      const int i = readlane_i(mi, k);
-      float w[H];
+    float4 rr[H];
 #pragma unroll
-      for (int h = 0; h < H; ++h) w[h] = readlane_f(wl[h], k);
-      const float4* gr = G + (int64_t)i * ldg4 + lane;
-      float pd[HP];
+    for (int h = 0; h < H; ++h) rr[h] = rec[(int64_t)mi * H + h];  // {s1_i, m_i, 1/den_i, c_i}
+    load(gA, mi, 0, cnt);
+    float al[H], zl[H], ml[H], cl[H], wl[H], dzl[H];
 #pragma unroll
-      for (int h = 0; h < HP; ++h) pd[h] = 0.f;
+    for (int h = 0; h < H; ++h) {
+      const float z = rr[h].x + sj[h];
+      zl[h] = z;
+      al[h] = lane < cnt ? __expf(-lrelu(z, alpha) - rr[h].y) * rr[h].z : 0.f;
+      cl[h] = rr[h].w;
+      ml[h] = (emask && lane < cnt) ? emask[pe * H + h] : 1.f;
+      wl[h] = al[h] * ml[h];
+      dzl[h] = 0.f;
+    }
+    auto process = [&](const float (&g)[kEB][EPL], int k) {
+      float w[kEB];
 #pragma unroll
-      for (int q = 0; q < NCH; ++q)
-        if (own[q]) {
-          const float4 g = gr[64 * q];
-          const float gs[4] = {g.x, g.y, g.z, g.w};
-          const float hs[4] = {hj[q].x, hj[q].y, hj[q].z, hj[q].w};
-          float o[4] = {acc[q].x, acc[q].y, acc[q].z, acc[q].w};
+      for (int e = 0; e < kEB; ++e) {
+        const int ke = min(k + e, cnt - 1);
+        float we = 0.f;
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            o[t] = fmaf(hsel<H>(w, hd[q][t]), gs[t], o[t]);
-            const float gh = gs[t] * hs[t];
-#pragma unroll
-            for (int h = 0; h < H; ++h) pd[h] += (hd[q][t] == h) ? gh : 0.f;
-          }
-          acc[q] = make_float4(o[0], o[1], o[2], o[3]);
+        for (int h = 0; h < H; ++h) {
+          const float v = readlane_f(wl[h], ke);
+          we = hme == h ? v : we;
         }
-      const float v = rs_sum<HP>(pd, lane);
-      float da[H];
-#pragma unroll
-      for (int h = 0; h < H; ++h) da[h] = readlane_f(v, head_lane<HP>(h));
-      if (lane == k) {
-#pragma unroll
-        for (int h = 0; h < H; ++h)
-          dzl[h] = -(al[h] * (ml[h] * da[h] - cl[h])) * (zl[h] > 0.f ? 1.f : alpha);
+        w[e] = we;
       }
+      float pd[kEB];
+#pragma unroll
+      for (int e = 0; e < kEB; ++e) {
+        float q = 0.f;
+#pragma unroll
+        for (int t = 0; t < EPL; ++t) {
+          const float gv = hl.ok[t] ? g[e][t] : 0.f;
+          if (k + e < cnt) acc[t] = fmaf(w[e], gv, acc[t]);  // uniform branch
+          q = fmaf(gv, hj[t], q);
+        }
+        pd[e] = q;
+      }
+      const float v = grp_sum<kEB, LPH>(pd, lane);
+#pragma unroll
+      for (int e = 0; e < kEB; ++e) {
+        if (k + e >= cnt) break;  // uniform
+        float da[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) da[h] = readlane_f(v, h * LPH + grp_lane<kEB, LPH>(e));
+        if (lane == k + e) {
+#pragma unroll
+          for (int h = 0; h < H; ++h)
+            dzl[h] = -(al[h] * (ml[h] * da[h] - cl[h])) * (zl[h] > 0.f ? 1.f : alpha);
+        }
+      }
+    };
+    for (int k = 0; k < cnt; k += 2 * kEB) {
+      if (k + kEB < cnt) load(gB, mi, k + kEB, cnt);
+      process(gA, k);
+      if (k + kEB >= cnt) break;
+      if (k + 2 * kEB < cnt) load(gA, mi, k + 2 * kEB, cnt);
+      process(gB, k + kEB);
     }
     if (lane < cnt) {
 #pragma unroll
@@ -399,22 +430,17 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(
       }
     }
   }
-  float d2[H];
+  float d2me = 0.f;
 #pragma unroll
-  for (int h = 0; h < H; ++h) d2[h] = wave_sum(ds2p[h]);
-#pragma unroll
-  for (int q = 0; q < NCH; ++q) {
-    if (!own[q]) continue;
-    float o[4] = {acc[q].x, acc[q].y, acc[q].z, acc[q].w};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int c = 4 * (lane + 64 * q) + t;
-      const int h = hd[q][t];
-      o[t] = h < H ? o[t] + hsel<H>(d2, h) * a[h * 2 * dh + dh + (c - h * dh)] : 0.f;
-    }
-    dH[(int64_t)row * lddh4 + lane + 64 * q] = make_float4(o[0], o[1], o[2], o[3]);
+  for (int h = 0; h < H; ++h) {
+    const float d2 = wave_sum(ds2p[h]);
+    d2me = hme == h ? d2 : d2me;
+    if (lane == 0) ds2[(int64_t)row * H + h] = d2;
   }
-  if (lane < H) ds2[(int64_t)row * H + lane] = hsel<H>(d2, lane);
+  float* out = dH + (int64_t)row * lddh;
+#pragma unroll
+  for (int t = 0; t < EPL; ++t)
+    if (hl.ok[t]) out[hl.c[t]] = acc[t] + d2me * a[hme * 2 * dh + dh + hl.d0 + t];
 }
 
 template <int H, int NCH>
@@ -480,6 +506,31 @@ using namespace gnnea;
     }                                                              \
   } while (0)
 
+// heads x EPL dispatch of the head-grouped kernels: EPL = ceil(d_head / LPH) rounded up to one of
+// {1,2,3,4,5,6,8,12,16} (d_head <= 16 * 64 / heads_pow2)
+static int epl_of(int heads, int dh) {
+  const int hp = heads <= 1 ? 1 : heads <= 2 ? 2 : heads <= 4 ? 4 : 8;
+  const int e = (dh + 64 / hp - 1) / (64 / hp);
+  static const int opts[] = {1, 2, 3, 4, 5, 6, 8, 12, 16};
+  for (int o : opts)
+    if (e <= o) return o;
+  return -1;
+}
+#define GNNEA_GAT_HL_DISPATCH(CALL)                                        \
+  do {                                                                     \
+    const int epl = epl_of(heads, d_head);                                 \
+    if (epl < 0 || heads > 8 || heads == 5 || heads == 7) return GNNEA_EINVAL; \
+    switch (heads * 32 + epl) {                                            \
+      CALL(1, 1) CALL(1, 2) CALL(1, 3) CALL(1, 4) CALL(1, 5) CALL(1, 6) CALL(1, 8) CALL(1, 12) CALL(1, 16) \
+      CALL(2, 1) CALL(2, 2) CALL(2, 3) CALL(2, 4) CALL(2, 5) CALL(2, 6) CALL(2, 8) CALL(2, 12) CALL(2, 16) \
+      CALL(3, 1) CALL(3, 2) CALL(3, 3) CALL(3, 4) CALL(3, 5) CALL(3, 6) CALL(3, 8) CALL(3, 12) CALL(3, 16) \
+      CALL(4, 1) CALL(4, 2) CALL(4, 3) CALL(4, 4) CALL(4, 5) CALL(4, 6) CALL(4, 8) CALL(4, 12) CALL(4, 16) \
+      CALL(6, 1) CALL(6, 2) CALL(6, 3) CALL(6, 4) CALL(6, 5) CALL(6, 6) CALL(6, 8) CALL(6, 12) CALL(6, 16) \
+      CALL(8, 1) CALL(8, 2) CALL(8, 3) CALL(8, 4) CALL(8, 5) CALL(8, 6) CALL(8, 8) CALL(8, 12) CALL(8, 16) \
+      default: return GNNEA_EINVAL;                                        \
+    }                                                                      \
+  } while (0)
+
 extern "C" int gnnea_gat_scores_f32(const float* Hm, int64_t ldh, int32_t n_rows, int heads,
                                     int d_head, const float* a, float* s1, float* s2,
                                     void* stream) {
@@ -488,14 +539,14 @@ extern "C" int gnnea_gat_scores_f32(const float* Hm, int64_t ldh, int32_t n_rows
   const int D = heads * d_head, D4 = (D + 3) / 4;
   if (!Hm || !a || !s1 || !s2) return GNNEA_EINVAL;
   if (!ok_ld(ldh, D) || !al16(Hm)) return GNNEA_EALIGN;
-  const int nb = div_up(n_rows, 4);
+  const int nb = div_up(n_rows, 4) < 2048 ? div_up(n_rows, 4) : 2048;  // waves walk rows
   hipStream_t s = (hipStream_t)stream;
-#define CALL(HH, NN)                                                                         \
-  case HH * 8 + NN:                                                                          \
-    hipLaunchKernelGGL((k_gat_scores<HH, NN>), dim3(nb), dim3(256), 0, s, (const float4*)Hm, \
-                       ldh / 4, n_rows, D, d_head, a, s1, s2);                               \
+#define CALL(HH, EE)                                                                          \
+  case HH * 32 + EE:                                                                          \
+    hipLaunchKernelGGL((k_gat_scores<HH, EE>), dim3(nb), dim3(256), 0, s, Hm, ldh, n_rows,    \
+                       d_head, a, s1, s2);                                                    \
     break;
-  GNNEA_GAT_DISPATCH(CALL);
+  GNNEA_GAT_HL_DISPATCH(CALL);
 #undef CALL
   GNNEA_LAUNCH_CHECK();
   return 0;
@@ -577,14 +628,13 @@ extern "C" int gnnea_gat_bwd_src_f32(const int32_t* rowptrT, const int32_t* colT
     return GNNEA_EALIGN;
   const int nb = div_up(n_rows, 4);
   hipStream_t s = (hipStream_t)stream;
-#define CALL(HH, NN)                                                                          \
-  case HH * 8 + NN:                                                                           \
-    hipLaunchKernelGGL((k_gat_bwd_src<HH, NN>), dim3(nb), dim3(256), 0, s, rowptrT, colT,     \
-                       permT, n_rows, D, d_head, (const float4*)H, ldh / 4, s2, alpha,        \
-                       edge_mask, (const float4*)rec, (const float4*)G, ldg / 4, a,           \
-                       (float4*)dH, lddh / 4, dzT, ds2);                                      \
+#define CALL(HH, EE)                                                                          \
+  case HH * 32 + EE:                                                                          \
+    hipLaunchKernelGGL((k_gat_bwd_src<HH, EE>), dim3(nb), dim3(256), 0, s, rowptrT, colT,     \
+                       permT, n_rows, d_head, H, ldh, s2, alpha, edge_mask,                   \
+                       (const float4*)rec, G, ldg, a, dH, lddh, dzT, ds2);                    \
     break;
-  GNNEA_GAT_DISPATCH(CALL);
+  GNNEA_GAT_HL_DISPATCH(CALL);
 #undef CALL
   GNNEA_LAUNCH_CHECK();
   return 0;

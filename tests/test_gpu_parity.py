@@ -190,13 +190,21 @@ def test_spmm_strided_input(device):
     assert rel_err(y, coo_aggregate(r, c, v, 300, x.cpu().double())) < TOL32
 
 
-@pytest.mark.parametrize("heads,d", [(1, 300), (4, 75), (2, 7), (8, 16)])
-def test_gat_fwd_bwd_vs_oracle(device, heads, d):
+@pytest.mark.parametrize("heads,d,hub", [(1, 300, False), (4, 75, False), (2, 7, False),
+                                         (8, 16, False), (3, 20, False), (6, 10, False),
+                                         (2, 300, False), (8, 128, False), (4, 64, False),
+                                         (4, 75, True), (1, 300, True)])
+def test_gat_fwd_bwd_vs_oracle(device, heads, d, hub):
     from gnnea import ops
     from oracle.gnn import gat_layer
     rng = np.random.default_rng(heads * 100 + d)
     n, fin = 400, 48
     r, c, _ = _random_coo(rng, n, n, 3000, dup=False)
+    if hub:
+        keep = c != 0
+        r, c = r[keep], c[keep]  # node 0 is a neighbour of every node: one source row with n in-edges (> 64)
+        r = np.concatenate([r, np.arange(1, n)])
+        c = np.concatenate([c, np.zeros(n - 1, dtype=c.dtype)])
     r = np.concatenate([r, np.arange(n)])  # every node has a self loop (reference needs >=1)
     c = np.concatenate([c, np.arange(n)])
     v = np.ones(r.size, dtype=np.float32)
