@@ -87,6 +87,30 @@ def sinkhorn_rate(device, B=3000, reg=0.01):
             "method": "marginal (T(1100)-T(100))/1000 incl. host batch syncs"}
 
 
+def bf16_rate(shard, H, steps):
+    """The same aggregation with bf16 feature storage (cfg-5's dtype, fp32 arithmetic)."""
+    Hb = H.to(torch.bfloat16)
+    Yb = torch.empty((shard.n_rows, H.shape[1]), dtype=torch.bfloat16, device=H.device)
+    for _ in range(3):
+        ops.spmm(shard.csr, Hb, _lib.GNNEA_ACT_RELU, out=Yb)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(steps):
+        ops.spmm(shard.csr, Hb, _lib.GNNEA_ACT_RELU, out=Yb)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / steps
+    traffic = gather_model_bytes(shard.n_rows, shard.nnz, H.shape[1], elem=2)
+    achieved = traffic / (ms * 1e-3) / 1e9
+    return {"value": round(shard.nnz / ms * 1e3, 1), "unit": "edges/s", "ms_per_step": round(ms, 4),
+            "dtype": "bf16 storage, f32 accumulate", "steps": steps,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "kernel": "gnnea::k_spmm_v4<relu,act,2,bf16,bf16>",
+                         "model": "gather: 4(N+1)+8E+2ED+2ND"}}
+
+
 def cpu_baseline(shard, H, budget_s=12.0):
     """Reference op on the host: torch.spmm on the uncoalesced COO rows of a bounded sample."""
     from oracle.cpu_baseline import time_reference_spmm
@@ -233,6 +257,11 @@ def main():
                 line["sinkhorn"] = sinkhorn_rate(device)
             except Exception as e:  # report, never hide
                 line["sinkhorn"] = {"error": repr(e)}
+        if world == 1:
+            try:
+                line["bf16"] = bf16_rate(shard, h_local, args.steps)
+            except Exception as e:  # report, never hide
+                line["bf16"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(shard, h_local)
         print(json.dumps(line), flush=True)

@@ -143,6 +143,47 @@ __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 acc) {
   return acc;
 }
 
+// bf16 storage (cfg-5): 16-bit brain floats carried as uint16_t, arithmetic in fp32.
+// f32 -> bf16 rounds to nearest even with NaN -> 0x7fc0, bit-identical to c10::BFloat16.
+typedef uint16_t bf16_t;
+__device__ __forceinline__ float bf16_to_f32(bf16_t b) {
+  return __builtin_bit_cast(float, (uint32_t)b << 16);
+}
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, f);
+  if (f != f) return (bf16_t)0x7fc0;
+  return (bf16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+// Four consecutive elements of a feature row: one 16-B (fp32) or 8-B (bf16) load per lane.
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+  typedef float4 raw;
+  static __device__ __forceinline__ float4 get(const raw& r) { return r; }
+  static __device__ __forceinline__ raw put(float4 v) { return v; }
+};
+template <> struct Vec4<bf16_t> {
+  typedef uint2 raw;
+  static __device__ __forceinline__ float4 get(const raw& r) {
+    return make_float4(__builtin_bit_cast(float, r.x << 16),
+                       __builtin_bit_cast(float, r.x & 0xffff0000u),
+                       __builtin_bit_cast(float, r.y << 16),
+                       __builtin_bit_cast(float, r.y & 0xffff0000u));
+  }
+  static __device__ __forceinline__ raw put(float4 v) {
+    raw r;
+    r.x = (uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16);
+    r.y = (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16);
+    return r;
+  }
+};
+template <typename T> __device__ __forceinline__ float to_f32(T v);
+template <> __device__ __forceinline__ float to_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f32<bf16_t>(bf16_t v) { return bf16_to_f32(v); }
+template <typename T> __device__ __forceinline__ T from_f32(float v);
+template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float v) { return f32_to_bf16(v); }
+
 inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // fp64 exp for the log-sum-exp inner loops (arguments are shifted logits, x <= ~0):

@@ -536,7 +536,7 @@ extern "C" int gnnea_gat_scores_f32(const float* Hm, int64_t ldh, int32_t n_rows
                                     void* stream) {
   if (n_rows < 0 || heads < 1 || d_head < 1) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
-  const int D = heads * d_head, D4 = (D + 3) / 4;
+  const int D = heads * d_head;
   if (!Hm || !a || !s1 || !s2) return GNNEA_EINVAL;
   if (!ok_ld(ldh, D) || !al16(Hm)) return GNNEA_EALIGN;
   const int nb = div_up(n_rows, 4) < 2048 ? div_up(n_rows, 4) : 2048;  // waves walk rows
@@ -620,7 +620,7 @@ extern "C" int gnnea_gat_bwd_src_f32(const int32_t* rowptrT, const int32_t* colT
                                      float* dzT, float* ds2, void* stream) {
   if (n_rows < 0 || heads < 1 || d_head < 1) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
-  const int D = heads * d_head, D4 = (D + 3) / 4;
+  const int D = heads * d_head;
   if (!rowptrT || !colT || !permT || !H || !s2 || !rec || !G || !a || !dH || !dzT || !ds2)
     return GNNEA_EINVAL;
   if (!ok_ld(ldh, D) || !ok_ld(ldg, D) || !ok_ld(lddh, D) || !al16(H) || !al16(G) || !al16(dH) ||

@@ -20,14 +20,17 @@ namespace gnnea {
 
 enum { EPI_ACT = 0, EPI_HIGHWAY = 1 };
 
+// TX: storage of the gathered rows X and of gate_pre / resid; TY: storage of Y and the saved
+// S / g (float or bf16_t; arithmetic is fp32 either way).
+template <typename TX, typename TY>
 struct HighwayArgs {
-  const float4* gate_pre;
+  const typename Vec4<TX>::raw* gate_pre;
   int64_t ldg4;
-  const float4* bias4;
-  const float4* resid;
+  const float4* bias4;  // fp32 bias_gate (nullable)
+  const typename Vec4<TX>::raw* resid;
   int64_t ldr4;
-  float4* save_s;
-  float4* save_g;
+  typename Vec4<TY>::raw* save_s;
+  typename Vec4<TY>::raw* save_g;
   int64_t lds4;
   float beta;  // EPI_ACT: Y = act(A.X + beta*Y)  (partial aggregations, dist halo overlap)
 };
@@ -39,13 +42,15 @@ __device__ __forceinline__ float4 act4(float4 v) {
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
-template <int ACT, int EPI, int NCH>
+template <int ACT, int EPI, int NCH, typename TX, typename TY>
 __global__ __launch_bounds__(256) void k_spmm_v4(const int32_t* __restrict__ rowptr,
                                                  const int32_t* __restrict__ col,
                                                  const float* __restrict__ val, int n_rows, int D4,
-                                                 const float4* __restrict__ X, int64_t ldx4,
-                                                 float4* __restrict__ Y, int64_t ldy4,
-                                                 HighwayArgs hw) {
+                                                 const typename Vec4<TX>::raw* __restrict__ X,
+                                                 int64_t ldx4,
+                                                 typename Vec4<TY>::raw* __restrict__ Y,
+                                                 int64_t ldy4, HighwayArgs<TX, TY> hw) {
+  typedef typename Vec4<TX>::raw RX;
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const int row = blk * 4 + wave_id();
   if (row >= n_rows) return;
@@ -70,11 +75,11 @@ __global__ __launch_bounds__(256) void k_spmm_v4(const int32_t* __restrict__ row
       const int j2 = readlane_i(mc, k + 2), j3 = readlane_i(mc, k + 3);
       const float v0 = readlane_f(mv, k), v1 = readlane_f(mv, k + 1);
       const float v2 = readlane_f(mv, k + 2), v3 = readlane_f(mv, k + 3);
-      const float4* x0 = X + (int64_t)j0 * ldx4 + lane;
-      const float4* x1 = X + (int64_t)j1 * ldx4 + lane;
-      const float4* x2 = X + (int64_t)j2 * ldx4 + lane;
-      const float4* x3 = X + (int64_t)j3 * ldx4 + lane;
-      float4 r0[NCH], r1[NCH], r2[NCH], r3[NCH];
+      const RX* x0 = X + (int64_t)j0 * ldx4 + lane;
+      const RX* x1 = X + (int64_t)j1 * ldx4 + lane;
+      const RX* x2 = X + (int64_t)j2 * ldx4 + lane;
+      const RX* x3 = X + (int64_t)j3 * ldx4 + lane;
+      RX r0[NCH], r1[NCH], r2[NCH], r3[NCH];
 #pragma unroll
       for (int q = 0; q < NCH; ++q) {
         if (own[q]) {
@@ -87,20 +92,20 @@ __global__ __launch_bounds__(256) void k_spmm_v4(const int32_t* __restrict__ row
 #pragma unroll
       for (int q = 0; q < NCH; ++q) {
         if (own[q]) {
-          acc[q] = f4_fma(v0, r0[q], acc[q]);
-          acc[q] = f4_fma(v1, r1[q], acc[q]);
-          acc[q] = f4_fma(v2, r2[q], acc[q]);
-          acc[q] = f4_fma(v3, r3[q], acc[q]);
+          acc[q] = f4_fma(v0, Vec4<TX>::get(r0[q]), acc[q]);
+          acc[q] = f4_fma(v1, Vec4<TX>::get(r1[q]), acc[q]);
+          acc[q] = f4_fma(v2, Vec4<TX>::get(r2[q]), acc[q]);
+          acc[q] = f4_fma(v3, Vec4<TX>::get(r3[q]), acc[q]);
         }
       }
     }
     for (; k < cnt; ++k) {
       const int j = readlane_i(mc, k);
       const float v = readlane_f(mv, k);
-      const float4* xr = X + (int64_t)j * ldx4 + lane;
+      const RX* xr = X + (int64_t)j * ldx4 + lane;
 #pragma unroll
       for (int q = 0; q < NCH; ++q)
-        if (own[q]) acc[q] = f4_fma(v, xr[64 * q], acc[q]);
+        if (own[q]) acc[q] = f4_fma(v, Vec4<TX>::get(xr[64 * q]), acc[q]);
     }
   }
 
@@ -110,7 +115,7 @@ __global__ __launch_bounds__(256) void k_spmm_v4(const int32_t* __restrict__ row
     const int c = lane + 64 * q;
     if constexpr (EPI == EPI_ACT) {
       if (hw.beta != 0.f) {
-        const float4 y = Y[(int64_t)row * ldy4 + c];
+        const float4 y = Vec4<TY>::get(Y[(int64_t)row * ldy4 + c]);
         acc[q].x = fmaf(hw.beta, y.x, acc[q].x);
         acc[q].y = fmaf(hw.beta, y.y, acc[q].y);
         acc[q].z = fmaf(hw.beta, y.z, acc[q].z);
@@ -119,39 +124,39 @@ __global__ __launch_bounds__(256) void k_spmm_v4(const int32_t* __restrict__ row
     }
     float4 s = act4<ACT>(acc[q]);
     if constexpr (EPI == EPI_ACT) {
-      Y[(int64_t)row * ldy4 + c] = s;
+      Y[(int64_t)row * ldy4 + c] = Vec4<TY>::put(s);
     } else {
-      float4 gp = hw.gate_pre[(int64_t)row * hw.ldg4 + c];
+      float4 gp = Vec4<TX>::get(hw.gate_pre[(int64_t)row * hw.ldg4 + c]);
       if (hw.bias4) {
         const float4 b = hw.bias4[c];
         gp.x += b.x; gp.y += b.y; gp.z += b.z; gp.w += b.w;
       }
       const float4 g = make_float4(sigm(gp.x), sigm(gp.y), sigm(gp.z), sigm(gp.w));
-      const float4 r = hw.resid[(int64_t)row * hw.ldr4 + c];
+      const float4 r = Vec4<TX>::get(hw.resid[(int64_t)row * hw.ldr4 + c]);
       // reference order: transform_gate * support + carry_gate * residual, carry = 1 - g
       float4 o;
       o.x = g.x * s.x + (1.f - g.x) * r.x;
       o.y = g.y * s.y + (1.f - g.y) * r.y;
       o.z = g.z * s.z + (1.f - g.z) * r.z;
       o.w = g.w * s.w + (1.f - g.w) * r.w;
-      Y[(int64_t)row * ldy4 + c] = o;
-      if (hw.save_s) hw.save_s[(int64_t)row * hw.lds4 + c] = s;
-      if (hw.save_g) hw.save_g[(int64_t)row * hw.lds4 + c] = g;
+      Y[(int64_t)row * ldy4 + c] = Vec4<TY>::put(o);
+      if (hw.save_s) hw.save_s[(int64_t)row * hw.lds4 + c] = Vec4<TY>::put(s);
+      if (hw.save_g) hw.save_g[(int64_t)row * hw.lds4 + c] = Vec4<TY>::put(g);
     }
   }
 }
 
-// Scalar fallback for any D / alignment: lane owns columns lane, lane+64, ...
-template <int ACT, int EPI>
+// Scalar path for any D / alignment: lane owns columns lane, lane+64, ...
+template <int ACT, int EPI, typename TX, typename TY>
 __global__ __launch_bounds__(256) void k_spmm_scalar(const int32_t* __restrict__ rowptr,
                                                      const int32_t* __restrict__ col,
                                                      const float* __restrict__ val, int n_rows,
-                                                     int D, const float* __restrict__ X,
-                                                     int64_t ldx, float* __restrict__ Y,
-                                                     int64_t ldy, const float* gate_pre,
+                                                     int D, const TX* __restrict__ X,
+                                                     int64_t ldx, TY* __restrict__ Y,
+                                                     int64_t ldy, const TX* gate_pre,
                                                      int64_t ldg, const float* bias,
-                                                     const float* resid, int64_t ldr,
-                                                     float* save_s, float* save_g, int64_t lds,
+                                                     const TX* resid, int64_t ldr,
+                                                     TY* save_s, TY* save_g, int64_t lds,
                                                      float beta) {
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const int row = blk * 4 + wave_id();
@@ -163,46 +168,52 @@ __global__ __launch_bounds__(256) void k_spmm_scalar(const int32_t* __restrict__
     float acc = 0.f;
     for (int e = beg; e < end; ++e) {
       const int j = col[e];
-      if (c < D) acc = fmaf(val[e], X[(int64_t)j * ldx + c], acc);
+      if (c < D) acc = fmaf(val[e], to_f32<TX>(X[(int64_t)j * ldx + c]), acc);
     }
     if (c >= D) continue;
-    if (EPI == EPI_ACT && beta != 0.f) acc = fmaf(beta, Y[(int64_t)row * ldy + c], acc);
+    if (EPI == EPI_ACT && beta != 0.f) acc = fmaf(beta, to_f32<TY>(Y[(int64_t)row * ldy + c]), acc);
     const float s = act_fwd<ACT>(acc);
     if constexpr (EPI == EPI_ACT) {
-      Y[(int64_t)row * ldy + c] = s;
+      Y[(int64_t)row * ldy + c] = from_f32<TY>(s);
     } else {
-      float gp = gate_pre[(int64_t)row * ldg + c] + (bias ? bias[c] : 0.f);
+      float gp = to_f32<TX>(gate_pre[(int64_t)row * ldg + c]) + (bias ? bias[c] : 0.f);
       const float g = sigm(gp);
-      const float r = resid[(int64_t)row * ldr + c];
-      Y[(int64_t)row * ldy + c] = g * s + (1.f - g) * r;
-      if (save_s) save_s[(int64_t)row * lds + c] = s;
-      if (save_g) save_g[(int64_t)row * lds + c] = g;
+      const float r = to_f32<TX>(resid[(int64_t)row * ldr + c]);
+      Y[(int64_t)row * ldy + c] = from_f32<TY>(g * s + (1.f - g) * r);
+      if (save_s) save_s[(int64_t)row * lds + c] = from_f32<TY>(s);
+      if (save_g) save_g[(int64_t)row * lds + c] = from_f32<TY>(g);
     }
   }
 }
 
-static inline bool al16(const void* p) { return p == nullptr || (((uintptr_t)p) & 15) == 0; }
+template <typename T>
+static inline bool alv(const void* p) {  // aligned for one Vec4<T> load
+  return p == nullptr || (((uintptr_t)p) & (sizeof(typename Vec4<T>::raw) - 1)) == 0;
+}
 
-template <int ACT, int EPI>
+template <int ACT, int EPI, typename TX, typename TY>
 static int launch_spmm(const int32_t* rowptr, const int32_t* col, const float* val, int n_rows,
-                       int D, const float* X, int64_t ldx, float* Y, int64_t ldy,
-                       const float* gate_pre, int64_t ldg, const float* bias, const float* resid,
-                       int64_t ldr, float* save_s, float* save_g, int64_t lds, float beta,
+                       int D, const TX* X, int64_t ldx, TY* Y, int64_t ldy,
+                       const TX* gate_pre, int64_t ldg, const float* bias, const TX* resid,
+                       int64_t ldr, TY* save_s, TY* save_g, int64_t lds, float beta,
                        hipStream_t stream) {
   const int nb = div_up(n_rows, 4);
-  bool vec = (D % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) && al16(X) && al16(Y);
+  bool vec = (D % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) && alv<TX>(X) && alv<TY>(Y);
   if (EPI == EPI_HIGHWAY)
-    vec = vec && (ldg % 4 == 0) && (ldr % 4 == 0) && (lds % 4 == 0) && al16(gate_pre) &&
-          al16(bias) && al16(resid) && al16(save_s) && al16(save_g);
+    vec = vec && (ldg % 4 == 0) && (ldr % 4 == 0) && (lds % 4 == 0) && alv<TX>(gate_pre) &&
+          alv<float>(bias) && alv<TX>(resid) && alv<TY>(save_s) && alv<TY>(save_g);
   const int D4 = D / 4;
   if (vec && D4 <= 256) {
-    HighwayArgs hw{(const float4*)gate_pre, ldg / 4, (const float4*)bias, (const float4*)resid,
-                   ldr / 4, (float4*)save_s, (float4*)save_g, lds / 4, beta};
+    typedef typename Vec4<TX>::raw RX;
+    typedef typename Vec4<TY>::raw RY;
+    HighwayArgs<TX, TY> hw{(const RX*)gate_pre, ldg / 4, (const float4*)bias, (const RX*)resid,
+                           ldr / 4, (RY*)save_s, (RY*)save_g, lds / 4, beta};
     const int nch = (D4 + 63) / 64;
-#define GNNEA_SPMM_CASE(N)                                                                     \
-  case N:                                                                                      \
-    hipLaunchKernelGGL((k_spmm_v4<ACT, EPI, N>), dim3(nb), dim3(256), 0, stream, rowptr, col, \
-                       val, n_rows, D4, (const float4*)X, ldx / 4, (float4*)Y, ldy / 4, hw);    \
+#define GNNEA_SPMM_CASE(N)                                                                    \
+  case N:                                                                                     \
+    hipLaunchKernelGGL((k_spmm_v4<ACT, EPI, N, TX, TY>), dim3(nb), dim3(256), 0, stream,      \
+                       rowptr, col, val, n_rows, D4, (const RX*)X, ldx / 4, (RY*)Y, ldy / 4,  \
+                       hw);                                                                   \
     break;
     switch (nch) {
       GNNEA_SPMM_CASE(1)
@@ -213,24 +224,24 @@ static int launch_spmm(const int32_t* rowptr, const int32_t* col, const float* v
     }
 #undef GNNEA_SPMM_CASE
   } else {
-    hipLaunchKernelGGL((k_spmm_scalar<ACT, EPI>), dim3(nb), dim3(256), 0, stream, rowptr, col,
-                       val, n_rows, D, X, ldx, Y, ldy, gate_pre, ldg, bias, resid, ldr, save_s,
-                       save_g, lds, beta);
+    hipLaunchKernelGGL((k_spmm_scalar<ACT, EPI, TX, TY>), dim3(nb), dim3(256), 0, stream, rowptr,
+                       col, val, n_rows, D, X, ldx, Y, ldy, gate_pre, ldg, bias, resid, ldr,
+                       save_s, save_g, lds, beta);
   }
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
 
-template <int EPI>
+template <int EPI, typename TX, typename TY>
 static int dispatch_act(int act, const int32_t* rowptr, const int32_t* col, const float* val,
-                        int n_rows, int D, const float* X, int64_t ldx, float* Y, int64_t ldy,
-                        const float* gate_pre, int64_t ldg, const float* bias,
-                        const float* resid, int64_t ldr, float* save_s, float* save_g,
-                        int64_t lds, float beta, hipStream_t s) {
+                        int n_rows, int D, const TX* X, int64_t ldx, TY* Y, int64_t ldy,
+                        const TX* gate_pre, int64_t ldg, const float* bias, const TX* resid,
+                        int64_t ldr, TY* save_s, TY* save_g, int64_t lds, float beta,
+                        hipStream_t s) {
 #define GNNEA_ACT_CASE(A)                                                                     \
   case A:                                                                                     \
-    return launch_spmm<A, EPI>(rowptr, col, val, n_rows, D, X, ldx, Y, ldy, gate_pre, ldg,    \
-                               bias, resid, ldr, save_s, save_g, lds, beta, s);
+    return launch_spmm<A, EPI, TX, TY>(rowptr, col, val, n_rows, D, X, ldx, Y, ldy, gate_pre, \
+                                       ldg, bias, resid, ldr, save_s, save_g, lds, beta, s);
   switch (act) {
     GNNEA_ACT_CASE(GNNEA_ACT_IDENTITY)
     GNNEA_ACT_CASE(GNNEA_ACT_RELU)
@@ -245,30 +256,79 @@ static int dispatch_act(int act, const int32_t* rowptr, const int32_t* col, cons
 
 // ---- elementwise backward helpers ----------------------------------------------------------
 
-template <int ACT>
-__global__ void k_act_bwd(const float* __restrict__ dY, const float* __restrict__ Y,
-                          float* __restrict__ G, int64_t n) {
+template <int ACT, typename T>
+__global__ void k_act_bwd(const T* __restrict__ dY, const T* __restrict__ Y, T* __restrict__ G,
+                          int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (; i < n; i += stride) G[i] = dY[i] * act_grad_from_out<ACT>(Y[i]);
+  for (; i < n; i += stride)
+    G[i] = from_f32<T>(to_f32<T>(dY[i]) * act_grad_from_out<ACT>(to_f32<T>(Y[i])));
 }
 
-template <int ACT>
-__global__ void k_highway_bwd(const float* __restrict__ dY, const float* __restrict__ S,
-                              const float* __restrict__ Gt, const float* __restrict__ R,
-                              int64_t ld, int64_t n_rows, int D, float* __restrict__ dS_pre,
-                              float* __restrict__ dgate, float* __restrict__ dresid) {
+template <int ACT, typename T>
+__global__ void k_highway_bwd(const T* __restrict__ dY, const T* __restrict__ S,
+                              const T* __restrict__ Gt, const T* __restrict__ R, int64_t ld,
+                              int64_t n_rows, int D, T* __restrict__ dS_pre,
+                              T* __restrict__ dgate, T* __restrict__ dresid) {
   const int64_t n = n_rows * (int64_t)D;
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (; t < n; t += stride) {
     const int64_t r = t / D, c = t - r * D;
     const int64_t i = r * ld + c;
-    const float dy = dY[i], s = S[i], g = Gt[i], x = R[i];
-    dS_pre[i] = dy * g * act_grad_from_out<ACT>(s);
-    dgate[i] = dy * (s - x) * g * (1.f - g);
-    if (dresid) dresid[i] = dy * (1.f - g);
+    const float dy = to_f32<T>(dY[i]), s = to_f32<T>(S[i]), g = to_f32<T>(Gt[i]);
+    const float x = to_f32<T>(R[i]);
+    dS_pre[i] = from_f32<T>(dy * g * act_grad_from_out<ACT>(s));
+    dgate[i] = from_f32<T>(dy * (s - x) * g * (1.f - g));
+    if (dresid) dresid[i] = from_f32<T>(dy * (1.f - g));
   }
+}
+
+template <typename T>
+static int act_bwd_t(const T* dY, const T* Y, T* G, int64_t n, int act, hipStream_t s) {
+  if (n < 0) return GNNEA_EINVAL;
+  if (n == 0) return 0;
+  if (!dY || !Y || !G) return GNNEA_EINVAL;
+  const int nb = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
+#define GNNEA_AB(A) hipLaunchKernelGGL((k_act_bwd<A, T>), dim3(nb), dim3(256), 0, s, dY, Y, G, n)
+  switch (act) {
+    case GNNEA_ACT_IDENTITY: GNNEA_AB(GNNEA_ACT_IDENTITY); break;
+    case GNNEA_ACT_RELU: GNNEA_AB(GNNEA_ACT_RELU); break;
+    case GNNEA_ACT_ELU: GNNEA_AB(GNNEA_ACT_ELU); break;
+    case GNNEA_ACT_LEAKY_RELU: GNNEA_AB(GNNEA_ACT_LEAKY_RELU); break;
+    case GNNEA_ACT_SIGMOID: GNNEA_AB(GNNEA_ACT_SIGMOID); break;
+    case GNNEA_ACT_TANH: GNNEA_AB(GNNEA_ACT_TANH); break;
+    default: return GNNEA_EINVAL;
+  }
+#undef GNNEA_AB
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T>
+static int highway_bwd_t(const T* dY, const T* S, const T* G, const T* resid, int64_t ld,
+                         int64_t n_rows, int32_t D, T* dS_pre, T* dgate, T* dresid, int act,
+                         hipStream_t s) {
+  if (n_rows < 0 || D < 0 || ld < D) return GNNEA_EINVAL;
+  if (n_rows == 0 || D == 0) return 0;
+  if (!dY || !S || !G || !resid || !dS_pre || !dgate) return GNNEA_EINVAL;
+  const int64_t n = n_rows * (int64_t)D;
+  const int nb = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
+#define GNNEA_HWB(A)                                                                         \
+  hipLaunchKernelGGL((k_highway_bwd<A, T>), dim3(nb), dim3(256), 0, s, dY, S, G, resid, ld,  \
+                     n_rows, D, dS_pre, dgate, dresid)
+  switch (act) {
+    case GNNEA_ACT_IDENTITY: GNNEA_HWB(GNNEA_ACT_IDENTITY); break;
+    case GNNEA_ACT_RELU: GNNEA_HWB(GNNEA_ACT_RELU); break;
+    case GNNEA_ACT_ELU: GNNEA_HWB(GNNEA_ACT_ELU); break;
+    case GNNEA_ACT_LEAKY_RELU: GNNEA_HWB(GNNEA_ACT_LEAKY_RELU); break;
+    case GNNEA_ACT_SIGMOID: GNNEA_HWB(GNNEA_ACT_SIGMOID); break;
+    case GNNEA_ACT_TANH: GNNEA_HWB(GNNEA_ACT_TANH); break;
+    default: return GNNEA_EINVAL;
+  }
+#undef GNNEA_HWB
+  GNNEA_LAUNCH_CHECK();
+  return 0;
 }
 
 }  // namespace gnnea
@@ -281,8 +341,9 @@ extern "C" int gnnea_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, con
   if (n_rows < 0 || D < 0) return GNNEA_EINVAL;
   if (n_rows == 0 || D == 0) return 0;
   if (!rowptr || !col || !val || !X || !Y || ldx < D || ldy < D) return GNNEA_EINVAL;
-  return dispatch_act<EPI_ACT>(act, rowptr, col, val, n_rows, D, X, ldx, Y, ldy, nullptr, 0,
-                               nullptr, nullptr, 0, nullptr, nullptr, 0, 0.f, (hipStream_t)stream);
+  return dispatch_act<EPI_ACT, float, float>(act, rowptr, col, val, n_rows, D, X, ldx, Y, ldy,
+                                             nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, 0,
+                                             0.f, (hipStream_t)stream);
 }
 
 extern "C" int gnnea_spmm_csr_beta_f32(const int32_t* rowptr, const int32_t* col,
@@ -292,9 +353,9 @@ extern "C" int gnnea_spmm_csr_beta_f32(const int32_t* rowptr, const int32_t* col
   if (n_rows < 0 || D < 0) return GNNEA_EINVAL;
   if (n_rows == 0 || D == 0) return 0;
   if (!rowptr || !col || !val || !X || !Y || ldx < D || ldy < D) return GNNEA_EINVAL;
-  return dispatch_act<EPI_ACT>(act, rowptr, col, val, n_rows, D, X, ldx, Y, ldy, nullptr, 0,
-                               nullptr, nullptr, 0, nullptr, nullptr, 0, beta,
-                               (hipStream_t)stream);
+  return dispatch_act<EPI_ACT, float, float>(act, rowptr, col, val, n_rows, D, X, ldx, Y, ldy,
+                                             nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, 0,
+                                             beta, (hipStream_t)stream);
 }
 
 extern "C" int gnnea_spmm_highway_f32(const int32_t* rowptr, const int32_t* col,
@@ -308,54 +369,74 @@ extern "C" int gnnea_spmm_highway_f32(const int32_t* rowptr, const int32_t* col,
   if (!rowptr || !col || !val || !X || !Y || !gate_pre || !resid) return GNNEA_EINVAL;
   if (ldx < D || ldy < D || ldg < D || ldr < D || ((save_s || save_g) && lds < D))
     return GNNEA_EINVAL;
-  return dispatch_act<EPI_HIGHWAY>(act, rowptr, col, val, n_rows, D, X, ldx, Y, ldy, gate_pre,
-                                   ldg, bias_gate, resid, ldr, save_s, save_g, lds, 0.f,
-                                   (hipStream_t)stream);
+  return dispatch_act<EPI_HIGHWAY, float, float>(act, rowptr, col, val, n_rows, D, X, ldx, Y,
+                                                 ldy, gate_pre, ldg, bias_gate, resid, ldr,
+                                                 save_s, save_g, lds, 0.f, (hipStream_t)stream);
 }
 
 extern "C" int gnnea_act_bwd_f32(const float* dY, const float* Y, float* G, int64_t n, int act,
                                  void* stream) {
-  if (n < 0) return GNNEA_EINVAL;
-  if (n == 0) return 0;
-  if (!dY || !Y || !G) return GNNEA_EINVAL;
-  const int nb = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
-  hipStream_t s = (hipStream_t)stream;
-  switch (act) {
-    case GNNEA_ACT_IDENTITY: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_IDENTITY>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
-    case GNNEA_ACT_RELU: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_RELU>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
-    case GNNEA_ACT_ELU: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_ELU>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
-    case GNNEA_ACT_LEAKY_RELU: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_LEAKY_RELU>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
-    case GNNEA_ACT_SIGMOID: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_SIGMOID>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
-    case GNNEA_ACT_TANH: hipLaunchKernelGGL(k_act_bwd<GNNEA_ACT_TANH>, dim3(nb), dim3(256), 0, s, dY, Y, G, n); break;
-    default: return GNNEA_EINVAL;
-  }
-  GNNEA_LAUNCH_CHECK();
-  return 0;
+  return act_bwd_t<float>(dY, Y, G, n, act, (hipStream_t)stream);
 }
 
 extern "C" int gnnea_highway_bwd_f32(const float* dY, const float* S, const float* G,
                                      const float* resid, int64_t ld, int64_t n_rows, int32_t D,
                                      float* dS_pre, float* dgate, float* dresid, int act,
                                      void* stream) {
-  if (n_rows < 0 || D < 0 || ld < D) return GNNEA_EINVAL;
+  return highway_bwd_t<float>(dY, S, G, resid, ld, n_rows, D, dS_pre, dgate, dresid, act,
+                              (hipStream_t)stream);
+}
+
+// ---- bf16 storage (cfg-5) ------------------------------------------------------------------
+
+extern "C" int gnnea_spmm_csr_bf16(const int32_t* rowptr, const int32_t* col, const float* val,
+                                   int32_t n_rows, int32_t D, const void* X, int64_t ldx,
+                                   float beta, void* Y, int64_t ldy, int y_dtype, int act,
+                                   void* stream) {
+  if (n_rows < 0 || D < 0) return GNNEA_EINVAL;
   if (n_rows == 0 || D == 0) return 0;
-  if (!dY || !S || !G || !resid || !dS_pre || !dgate) return GNNEA_EINVAL;
-  const int64_t n = n_rows * (int64_t)D;
-  const int nb = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
-  hipStream_t s = (hipStream_t)stream;
-#define GNNEA_HWB(A)                                                                        \
-  hipLaunchKernelGGL(k_highway_bwd<A>, dim3(nb), dim3(256), 0, s, dY, S, G, resid, ld, n_rows, \
-                     D, dS_pre, dgate, dresid)
-  switch (act) {
-    case GNNEA_ACT_IDENTITY: GNNEA_HWB(GNNEA_ACT_IDENTITY); break;
-    case GNNEA_ACT_RELU: GNNEA_HWB(GNNEA_ACT_RELU); break;
-    case GNNEA_ACT_ELU: GNNEA_HWB(GNNEA_ACT_ELU); break;
-    case GNNEA_ACT_LEAKY_RELU: GNNEA_HWB(GNNEA_ACT_LEAKY_RELU); break;
-    case GNNEA_ACT_SIGMOID: GNNEA_HWB(GNNEA_ACT_SIGMOID); break;
-    case GNNEA_ACT_TANH: GNNEA_HWB(GNNEA_ACT_TANH); break;
-    default: return GNNEA_EINVAL;
-  }
-#undef GNNEA_HWB
-  GNNEA_LAUNCH_CHECK();
-  return 0;
+  if (!rowptr || !col || !val || !X || !Y || ldx < D || ldy < D) return GNNEA_EINVAL;
+  if (y_dtype == GNNEA_BF16)
+    return dispatch_act<EPI_ACT, bf16_t, bf16_t>(act, rowptr, col, val, n_rows, D,
+                                                 (const bf16_t*)X, ldx, (bf16_t*)Y, ldy,
+                                                 nullptr, 0, nullptr, nullptr, 0, nullptr,
+                                                 nullptr, 0, beta, (hipStream_t)stream);
+  if (y_dtype == GNNEA_F32)
+    return dispatch_act<EPI_ACT, bf16_t, float>(act, rowptr, col, val, n_rows, D,
+                                                (const bf16_t*)X, ldx, (float*)Y, ldy, nullptr,
+                                                0, nullptr, nullptr, 0, nullptr, nullptr, 0,
+                                                beta, (hipStream_t)stream);
+  return GNNEA_EINVAL;
+}
+
+extern "C" int gnnea_spmm_highway_bf16(const int32_t* rowptr, const int32_t* col,
+                                       const float* val, int32_t n_rows, int32_t D,
+                                       const void* X, int64_t ldx, const void* gate_pre,
+                                       int64_t ldg, const float* bias_gate, const void* resid,
+                                       int64_t ldr, void* Y, int64_t ldy, void* save_s,
+                                       void* save_g, int64_t lds, int act, void* stream) {
+  if (n_rows < 0 || D < 0) return GNNEA_EINVAL;
+  if (n_rows == 0 || D == 0) return 0;
+  if (!rowptr || !col || !val || !X || !Y || !gate_pre || !resid) return GNNEA_EINVAL;
+  if (ldx < D || ldy < D || ldg < D || ldr < D || ((save_s || save_g) && lds < D))
+    return GNNEA_EINVAL;
+  return dispatch_act<EPI_HIGHWAY, bf16_t, bf16_t>(
+      act, rowptr, col, val, n_rows, D, (const bf16_t*)X, ldx, (bf16_t*)Y, ldy,
+      (const bf16_t*)gate_pre, ldg, bias_gate, (const bf16_t*)resid, ldr, (bf16_t*)save_s,
+      (bf16_t*)save_g, lds, 0.f, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_act_bwd_bf16(const void* dY, const void* Y, void* G, int64_t n, int act,
+                                  void* stream) {
+  return act_bwd_t<bf16_t>((const bf16_t*)dY, (const bf16_t*)Y, (bf16_t*)G, n, act,
+                           (hipStream_t)stream);
+}
+
+extern "C" int gnnea_highway_bwd_bf16(const void* dY, const void* S, const void* G,
+                                      const void* resid, int64_t ld, int64_t n_rows, int32_t D,
+                                      void* dS_pre, void* dgate, void* dresid, int act,
+                                      void* stream) {
+  return highway_bwd_t<bf16_t>((const bf16_t*)dY, (const bf16_t*)S, (const bf16_t*)G,
+                               (const bf16_t*)resid, ld, n_rows, D, (bf16_t*)dS_pre,
+                               (bf16_t*)dgate, (bf16_t*)dresid, act, (hipStream_t)stream);
 }

@@ -21,6 +21,7 @@ GNNEA_ACT_TANH = 5
 
 GNNEA_F32 = 0
 GNNEA_F64 = 1
+GNNEA_BF16 = 2
 
 GNNEA_SK_KNOPP = 0
 GNNEA_SK_STAB = 1
@@ -76,6 +77,14 @@ SIGNATURES = {
     "gnnea_act_bwd_f32": (ctypes.c_int, [_p, _p, _p, _i64, ctypes.c_int, _p]),
     "gnnea_highway_bwd_f32": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p,
                                              ctypes.c_int, _p]),
+    "gnnea_spmm_csr_bf16": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _f32, _p, _i64,
+                                           ctypes.c_int, ctypes.c_int, _p]),
+    "gnnea_spmm_highway_bf16": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64, _p,
+                                               _p, _i64, _p, _i64, _p, _p, _i64, ctypes.c_int,
+                                               _p]),
+    "gnnea_act_bwd_bf16": (ctypes.c_int, [_p, _p, _p, _i64, ctypes.c_int, _p]),
+    "gnnea_highway_bwd_bf16": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p,
+                                              ctypes.c_int, _p]),
     "gnnea_gat_scores_f32": (ctypes.c_int, [_p, _i64, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,
                                             _p]),
     "gnnea_gat_fwd_f32": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int, ctypes.c_int, _p, _p,
@@ -87,6 +96,9 @@ SIGNATURES = {
     "gnnea_gat_bwd_dst_f32": (ctypes.c_int, [_p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,
                                              _i64, _p, _p]),
     "gnnea_gemm_ws_bytes": (_i64, [_i64, _i64, _i64]),
+    "gnnea_gemm_bf16_ws_bytes": (_i64, [_i64, _i64, _i64]),
+    "gnnea_gemm_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
+                                       _i64, _p, _f32, _p, _i64, ctypes.c_int, _p, _i64, _p]),
     "gnnea_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
                                       _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
     "gnnea_sinkhorn_ws_bytes": (_i64, [ctypes.c_int, ctypes.c_int]),

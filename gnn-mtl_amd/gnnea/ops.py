@@ -43,6 +43,18 @@ def _f32c(t):
     return t if t.is_contiguous() else t.contiguous()
 
 
+FEATURE_DTYPES = (torch.float32, torch.bfloat16)
+
+
+def _featc(t, dtype=None):
+    """Contiguous feature matrix in fp32 or bf16 storage (converted to ``dtype`` when given)."""
+    if dtype is not None and t.dtype != dtype:
+        t = t.to(dtype)
+    if t.dtype not in FEATURE_DTYPES:
+        raise TypeError("gnnea: fp32 or bf16 features required (got %s)" % t.dtype)
+    return t if t.is_contiguous() else t.contiguous()
+
+
 # ------------------------------------------------------------------------------------------ #
 # dense projection (MFMA)                                                                     #
 # ------------------------------------------------------------------------------------------ #
@@ -58,11 +70,20 @@ def _gemm_ws(device, nbytes):
     return buf
 
 
-def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0):
-    """out = op(a) @ op(b) (+ bias) (+ beta*out) on MFMA f32 (gnnea_gemm_f32)."""
+def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_dtype=None):
+    """out = op(a) @ op(b) (+ bias) (+ beta*out) on MFMA.
+
+    fp32 operands: gnnea_gemm_f32 (exact-f32 MFMA).  A bf16 operand (cfg-5 storage) switches
+    to gnnea_gemm_bf16 (both operands bf16, fp32 accumulate, out bf16 unless an fp32 ``out`` /
+    ``out_dtype`` is given)."""
     _lib.require_device(a, b)
-    a = _f32c(a)
-    b = _f32c(b)
+    bf = a.dtype == torch.bfloat16 or b.dtype == torch.bfloat16
+    if bf:
+        a = _featc(a, torch.bfloat16)
+        b = _featc(b, torch.bfloat16)
+    else:
+        a = _f32c(a)
+        b = _f32c(b)
     M = a.shape[1] if trans_a else a.shape[0]
     K = a.shape[0] if trans_a else a.shape[1]
     Kb = b.shape[1] if trans_b else b.shape[0]
@@ -70,18 +91,29 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0):
     if K != Kb:
         raise ValueError("gnnea.gemm: inner dimensions differ (%d vs %d)" % (K, Kb))
     if out is None:
-        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+        dt = out_dtype or (torch.bfloat16 if bf else torch.float32)
+        out = torch.empty((M, N), dtype=dt, device=a.device)
         beta = 0.0
+    if out.dtype not in FEATURE_DTYPES or (not bf and out.dtype != torch.float32):
+        raise TypeError("gnnea.gemm: out must be fp32 (or bf16 with bf16 operands)")
     if bias is not None:
-        bias = _f32c(bias)
+        bias = _featc(bias, torch.float32)
     L = _lib.lib()
-    ws_bytes = int(L.gnnea_gemm_ws_bytes(M, N, K))
+    ws_fn = L.gnnea_gemm_bf16_ws_bytes if bf else L.gnnea_gemm_ws_bytes
+    ws_bytes = int(ws_fn(M, N, K))
     ws = _gemm_ws(a.device, ws_bytes) if ws_bytes > 0 else None
     with torch.cuda.device(a.device):
-        check(L.gnnea_gemm_f32(int(trans_a), int(trans_b), M, N, K, ptr(a), a.stride(0), ptr(b),
-                               b.stride(0), ptr(bias), float(beta), ptr(out), out.stride(0),
-                               ptr(ws), ws_bytes if ws is not None else 0,
-                               stream_of(a.device)))
+        if bf:
+            cd = _lib.GNNEA_BF16 if out.dtype == torch.bfloat16 else _lib.GNNEA_F32
+            check(L.gnnea_gemm_bf16(int(trans_a), int(trans_b), M, N, K, ptr(a), a.stride(0),
+                                    ptr(b), b.stride(0), ptr(bias), float(beta), ptr(out),
+                                    out.stride(0), cd, ptr(ws),
+                                    ws_bytes if ws is not None else 0, stream_of(a.device)))
+        else:
+            check(L.gnnea_gemm_f32(int(trans_a), int(trans_b), M, N, K, ptr(a), a.stride(0),
+                                   ptr(b), b.stride(0), ptr(bias), float(beta), ptr(out),
+                                   out.stride(0), ptr(ws), ws_bytes if ws is not None else 0,
+                                   stream_of(a.device)))
     return out
 
 
@@ -92,20 +124,22 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        ctx.bias_dtype = bias.dtype if bias is not None else None
         return gemm(x, weight, trans_b=True, bias=bias)
 
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        dy = _f32c(dy)
+        bf = x.dtype == torch.bfloat16 or weight.dtype == torch.bfloat16
+        dy = _featc(dy, torch.bfloat16 if bf else torch.float32)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = gemm(dy, weight)  # [N,out]·[out,in]
+            dx = gemm(dy, weight, out_dtype=x.dtype if bf else None)  # [N,out]·[out,in]
         if ctx.needs_input_grad[1]:
-            dw = gemm(dy, x, trans_a=True)  # [out,N]·[N,in]
+            dw = gemm(dy, x, trans_a=True, out_dtype=weight.dtype if bf else None)  # [out,N]·[N,in]
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            ones = torch.ones((1, dy.shape[0]), dtype=torch.float32, device=dy.device)
-            db = gemm(ones, dy).view(-1)
+            ones = torch.ones((1, dy.shape[0]), dtype=dy.dtype, device=dy.device)
+            db = gemm(ones, dy, out_dtype=ctx.bias_dtype if bf else None).view(-1)
         return dx, dw, db
 
 
@@ -121,9 +155,12 @@ class MatmulFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dy = _f32c(dy)
-        dx = gemm(dy, w, trans_b=True) if ctx.needs_input_grad[0] else None
-        dw = gemm(x, dy, trans_a=True) if ctx.needs_input_grad[1] else None
+        bf = x.dtype == torch.bfloat16 or w.dtype == torch.bfloat16
+        dy = _featc(dy, torch.bfloat16 if bf else torch.float32)
+        dx = gemm(dy, w, trans_b=True, out_dtype=x.dtype if bf else None) \
+            if ctx.needs_input_grad[0] else None
+        dw = gemm(x, dy, trans_a=True, out_dtype=w.dtype if bf else None) \
+            if ctx.needs_input_grad[1] else None
         return dx, dw
 
 
@@ -142,10 +179,10 @@ INFINITY_CACHE_BYTES = 256 << 20
 
 
 def _off(t, r0):
-    """Device pointer of row r0 of a row-major fp32 tensor (None -> NULL)."""
+    """Device pointer of row r0 of a row-major tensor (None -> NULL)."""
     if t is None:
         return None
-    return ctypes.c_void_p(t.data_ptr() + 4 * r0 * t.stride(0))
+    return ctypes.c_void_p(t.data_ptr() + t.element_size() * r0 * t.stride(0))
 
 
 def _off32(t, r0):
@@ -156,27 +193,39 @@ def _off32(t, r0):
 def _blocks(csr, x):
     """Row blocks to launch one after another: the diagonal blocks when the gathered matrix is
     larger than the Infinity Cache (a single launch keeps all blocks' gathers in flight)."""
-    if x.shape[0] * x.shape[1] * 4 <= INFINITY_CACHE_BYTES:
+    if x.shape[0] * x.shape[1] * x.element_size() <= INFINITY_CACHE_BYTES:
         return [(0, csr.n_rows)]
     return csr.row_blocks()
 
 
-def spmm(csr, x, act=_lib.GNNEA_ACT_IDENTITY, out=None, beta=0.0):
-    """out = act(A @ x + beta*out) with the gather-model CSR kernel (gnnea_spmm_csr_*_f32)."""
+def spmm(csr, x, act=_lib.GNNEA_ACT_IDENTITY, out=None, beta=0.0, out_dtype=None):
+    """out = act(A @ x + beta*out) with the gather-model CSR kernel.
+
+    fp32 x: gnnea_spmm_csr_{,beta_}f32.  bf16 x (cfg-5 storage): gnnea_spmm_csr_bf16 with fp32
+    arithmetic and a bf16 (default) or fp32 ``out``.  Other dtypes are computed as fp32."""
     _lib.require_device(x)
-    if x.dtype != torch.float32 or x.stride(1) != 1:
-        x = x.float().contiguous()
+    if x.dtype not in FEATURE_DTYPES or x.stride(1) != 1:
+        x = x.float().contiguous() if x.dtype not in FEATURE_DTYPES else x.contiguous()
     if x.dim() != 2 or x.shape[0] < csr.n_cols:
         raise ValueError("gnnea.spmm: x must be [%d, D]" % csr.n_cols)
     if out is None:
-        out = torch.empty((csr.n_rows, x.shape[1]), dtype=torch.float32, device=x.device)
+        out = torch.empty((csr.n_rows, x.shape[1]), dtype=out_dtype or x.dtype, device=x.device)
         beta = 0.0
+    if x.dtype == torch.float32 and out.dtype != torch.float32:
+        raise TypeError("gnnea.spmm: fp32 x needs an fp32 out")
+    if out.dtype not in FEATURE_DTYPES:
+        raise TypeError("gnnea.spmm: out must be fp32 or bf16")
     L = _lib.lib()
     st = stream_of(x.device)
     with torch.cuda.device(x.device):
         for r0, r1 in _blocks(csr, x):
             rp = ctypes.c_void_p(csr.rowptr.data_ptr() + 4 * r0)
-            if beta == 0.0:
+            if x.dtype == torch.bfloat16:
+                yd = _lib.GNNEA_BF16 if out.dtype == torch.bfloat16 else _lib.GNNEA_F32
+                check(L.gnnea_spmm_csr_bf16(rp, ptr(csr.col), ptr(csr.val), r1 - r0, x.shape[1],
+                                            ptr(x), x.stride(0), float(beta), _off(out, r0),
+                                            out.stride(0), yd, int(act), st))
+            elif beta == 0.0:
                 check(L.gnnea_spmm_csr_f32(rp, ptr(csr.col), ptr(csr.val), r1 - r0, x.shape[1],
                                            ptr(x), x.stride(0), _off(out, r0), out.stride(0),
                                            int(act), st))
@@ -188,12 +237,13 @@ def spmm(csr, x, act=_lib.GNNEA_ACT_IDENTITY, out=None, beta=0.0):
 
 
 def act_bwd(dy, y, act):
-    dy = _f32c(dy)
-    y = _f32c(y)
+    y = _featc(y)
+    dy = _featc(dy, y.dtype)
     g = torch.empty_like(y)
+    fn = _lib.lib().gnnea_act_bwd_bf16 if y.dtype == torch.bfloat16 else \
+        _lib.lib().gnnea_act_bwd_f32
     with torch.cuda.device(y.device):
-        check(_lib.lib().gnnea_act_bwd_f32(ptr(dy), ptr(y), ptr(g), y.numel(), int(act),
-                                           stream_of(y.device)))
+        check(fn(ptr(dy), ptr(y), ptr(g), y.numel(), int(act), stream_of(y.device)))
     return g
 
 
@@ -211,8 +261,9 @@ class AggregateFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (out,) = ctx.saved_tensors
-        g = dy if ctx.act == _lib.GNNEA_ACT_IDENTITY else act_bwd(dy, out, ctx.act)
-        dh = spmm(ctx.csr.transpose(), _f32c(g))
+        g = _featc(dy, out.dtype) if ctx.act == _lib.GNNEA_ACT_IDENTITY else \
+            act_bwd(dy, out, ctx.act)
+        dh = spmm(ctx.csr.transpose(), g)
         return dh, None, None
 
 
@@ -231,17 +282,19 @@ class HighwayFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, hidden, gate_pre, resid, bias_gate, csr, act):
-        hidden = _f32c(hidden)
-        gate_pre = _f32c(gate_pre)
-        resid = _f32c(resid)
+        hidden = _featc(hidden)
+        gate_pre = _featc(gate_pre, hidden.dtype)
+        resid = _featc(resid, hidden.dtype)
         N, D = csr.n_rows, hidden.shape[1]
-        out = torch.empty((N, D), dtype=torch.float32, device=hidden.device)
+        out = torch.empty((N, D), dtype=hidden.dtype, device=hidden.device)
         S = torch.empty_like(out)
         G = torch.empty_like(out)
-        bias = _f32c(bias_gate) if bias_gate is not None else None
+        bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
+        fn = _lib.lib().gnnea_spmm_highway_bf16 if hidden.dtype == torch.bfloat16 else \
+            _lib.lib().gnnea_spmm_highway_f32
         with torch.cuda.device(hidden.device):
             for r0, r1 in _blocks(csr, hidden):
-                check(_lib.lib().gnnea_spmm_highway_f32(
+                check(fn(
                     ctypes.c_void_p(csr.rowptr.data_ptr() + 4 * r0), ptr(csr.col), ptr(csr.val),
                     r1 - r0, D, ptr(hidden), hidden.stride(0), _off(gate_pre, r0),
                     gate_pre.stride(0), ptr(bias), _off(resid, r0), resid.stride(0),
@@ -255,12 +308,14 @@ class HighwayFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         S, G, resid = ctx.saved_tensors
-        dy = _f32c(dy)
+        dy = _featc(dy, S.dtype)
         dS = torch.empty_like(S)
         dgate = torch.empty_like(S)
         dres = torch.empty_like(S) if ctx.needs_input_grad[2] else None
+        fn = _lib.lib().gnnea_highway_bwd_bf16 if S.dtype == torch.bfloat16 else \
+            _lib.lib().gnnea_highway_bwd_f32
         with torch.cuda.device(S.device):
-            check(_lib.lib().gnnea_highway_bwd_f32(
+            check(fn(
                 ptr(dy), ptr(S), ptr(G), ptr(resid), S.stride(0), S.shape[0], S.shape[1],
                 ptr(dS), ptr(dgate), ptr(dres), int(ctx.act), stream_of(S.device)))
         dh = spmm(ctx.csr.transpose(), dS)

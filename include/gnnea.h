@@ -102,6 +102,24 @@ int gnnea_highway_bwd_f32(const float* dY, const float* S, const float* G, const
                           int64_t ld, int64_t n_rows, int32_t D, float* dS_pre, float* dgate,
                           float* dresid, int act, void* stream);
 
+/* bf16 feature storage (cfg-5; SURVEY.md §8b gnnea_spmm_csr_bf16): X, gate_pre, resid, dY, S, G
+ * are bf16 (void*, 2-byte elements), CSR values and bias_gate stay fp32, every product and sum
+ * is fp32, outputs are rounded once to bf16 (round-to-nearest-even, as torch) or written fp32
+ * (y_dtype GNNEA_F32: gradient partials).  Fast path: D, ldx, ldy % 4 == 0 and 8-B aligned rows
+ * (one 8-B load of 4 elements per lane).  beta as gnnea_spmm_csr_beta_f32. */
+int gnnea_spmm_csr_bf16(const int32_t* rowptr, const int32_t* col, const float* val,
+                        int32_t n_rows, int32_t D, const void* X, int64_t ldx, float beta,
+                        void* Y, int64_t ldy, int y_dtype, int act, void* stream);
+int gnnea_spmm_highway_bf16(const int32_t* rowptr, const int32_t* col, const float* val,
+                            int32_t n_rows, int32_t D, const void* X, int64_t ldx,
+                            const void* gate_pre, int64_t ldg, const float* bias_gate,
+                            const void* resid, int64_t ldr, void* Y, int64_t ldy, void* save_s,
+                            void* save_g, int64_t lds, int act, void* stream);
+int gnnea_act_bwd_bf16(const void* dY, const void* Y, void* G, int64_t n, int act, void* stream);
+int gnnea_highway_bwd_bf16(const void* dY, const void* S, const void* G, const void* resid,
+                           int64_t ld, int64_t n_rows, int32_t D, void* dS_pre, void* dgate,
+                           void* dresid, int act, void* stream);
+
 /* ------------------------------------------------------------------------------------------ *
  * a5-a7. Sparse GAT, all heads per edge pass (layers/att_layers.py:29-61, 82-91).
  * H is the head-concatenated projection X·[W_0|...|W_{h-1}] (N x heads*d_head, row stride ldh);
@@ -151,6 +169,15 @@ int64_t gnnea_gemm_ws_bytes(int64_t M, int64_t N, int64_t K);
 int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
                    int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
                    float* C, int64_t ldc, void* ws, int64_t ws_bytes, void* stream);
+
+/* bf16 operands (cfg-5 storage), v_mfma_f32_32x32x16_bf16: A, B bf16 (void*), fp32 accumulate,
+ * bias fp32 (nullable), C bf16 (c_dtype GNNEA_BF16, rounded once, nearest even) or fp32
+ * (GNNEA_F32).  Workspace (split-K slabs) from gnnea_gemm_bf16_ws_bytes; NULL = no split.
+ * Fast path: lda, ldb and the operands' contiguous extents % 4 == 0, 8-B aligned A, B. */
+int64_t gnnea_gemm_bf16_ws_bytes(int64_t M, int64_t N, int64_t K);
+int gnnea_gemm_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const void* A,
+                    int64_t lda, const void* B, int64_t ldb, const float* bias, float beta,
+                    void* C, int64_t ldc, int c_dtype, void* ws, int64_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------ *
  * a9-a12. Sinkhorn solvers in the reference's scaling form, fp64 arithmetic.

@@ -1,0 +1,188 @@
+"""bf16 feature storage (cfg-5) on the HIP path (run on an MI355X).
+
+Tolerances: the kernels read bf16 rows, compute in fp32 and round the result once.  So
+  * with an fp32 output they match the fp64 aggregation of the SAME bf16 inputs to fp32
+    accumulation error (<= 1e-5 norm-relative);
+  * their bf16 output is bit-identical to torch's round-to-nearest-even of that fp32 output;
+  * against the fp32 reference path (fp32 inputs) the stated bf16 tolerance is 1e-2
+    norm-relative.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+TOL_BF16 = 1e-2
+TOL_ACC = 1e-5
+
+
+def _graph(rng, n, nnz, hub=False):
+    r = rng.integers(0, n, nnz)
+    c = rng.integers(0, n, nnz)
+    if hub:  # one row with far more than 64 neighbours
+        r = np.concatenate([r, np.zeros(300, dtype=r.dtype)])
+        c = np.concatenate([c, rng.integers(0, n, 300)])
+    v = rng.standard_normal(r.size).astype(np.float32)
+    return r, c, v
+
+
+def _csr(r, c, v, n, dev):
+    from gnnea.graph import DeviceCSR
+    return DeviceCSR.from_coo(torch.from_numpy(r).to(dev), torch.from_numpy(c).to(dev),
+                              torch.from_numpy(v).to(dev), n, n)
+
+
+def _agg64(r, c, v, n, x64):
+    y = np.zeros((n, x64.shape[1]))
+    np.add.at(y, r, v[:, None].astype(np.float64) * x64[c])
+    return y
+
+
+@pytest.mark.parametrize("D", [4, 75 * 4, 300, 302, 1024])
+@pytest.mark.parametrize("hub", [False, True])
+def test_spmm_bf16_vs_fp64(device, D, hub):
+    from gnnea import ops
+    rng = np.random.default_rng(D + hub)
+    n = 700
+    r, c, v = _graph(rng, n, 6000, hub)
+    csr = _csr(r, c, v, n, device)
+    x = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32)).to(device)
+    xb = x.to(torch.bfloat16)
+    y32 = ops.spmm(csr, xb, out_dtype=torch.float32)
+    assert y32.dtype == torch.float32
+    ref = _agg64(r, c, v, n, xb.float().cpu().double().numpy())
+    assert rel_err(y32.cpu(), ref) < TOL_ACC
+    yb = ops.spmm(csr, xb)
+    assert yb.dtype == torch.bfloat16
+    assert torch.equal(yb.view(torch.int16), y32.to(torch.bfloat16).view(torch.int16))
+    ref32 = _agg64(r, c, v, n, x.cpu().double().numpy())
+    assert rel_err(yb.float().cpu(), ref32) < TOL_BF16
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh"])
+def test_spmm_bf16_act_and_beta(device, act):
+    from gnnea import _lib, ops
+    rng = np.random.default_rng(3)
+    n, D = 500, 300
+    r, c, v = _graph(rng, n, 4000)
+    csr = _csr(r, c, v, n, device)
+    xb = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32)).to(device).bfloat16()
+    code = _lib.GNNEA_ACT_RELU if act == "relu" else _lib.GNNEA_ACT_TANH
+    fn = torch.relu if act == "relu" else torch.tanh
+    base = _agg64(r, c, v, n, xb.float().cpu().double().numpy())
+    y = ops.spmm(csr, xb, act=code, out_dtype=torch.float32)
+    assert rel_err(y.cpu(), fn(torch.from_numpy(base))) < TOL_ACC
+    # beta: out = act(A x + beta * out), out fp32 (gradient partials)
+    prev = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32)).to(device)
+    out = prev.clone()
+    ops.spmm(csr, xb, act=code, out=out, beta=0.5)
+    want = fn(torch.from_numpy(base + 0.5 * prev.cpu().double().numpy()))
+    assert rel_err(out.cpu(), want) < TOL_ACC
+
+
+def test_aggregate_bf16_autograd(device):
+    from gnnea import ops
+    rng = np.random.default_rng(5)
+    n, D = 600, 300
+    r, c, v = _graph(rng, n, 5000)
+    idx = torch.from_numpy(np.stack([r, c]).astype(np.int64))
+    adj = torch.sparse_coo_tensor(idx, torch.from_numpy(v), (n, n)).to(device)
+    x = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32))
+    R = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32))
+    xb = x.to(device).bfloat16().requires_grad_(True)
+    y = ops.aggregate(adj, xb, F.relu)
+    assert y.dtype == torch.bfloat16
+    (y.float() * R.to(device)).sum().backward()
+    assert xb.grad.dtype == torch.bfloat16
+    # reference at the bf16-rounded input: a ReLU boundary flipped by input rounding is a
+    # property of the input precision, not of the kernels
+    xo = xb.detach().float().cpu().double().requires_grad_(True)
+    yo = torch.relu(torch.sparse_coo_tensor(idx, torch.from_numpy(v).double(), (n, n)) @ xo)
+    (yo * R.double()).sum().backward()
+    assert rel_err(y.detach().float().cpu(), yo.detach()) < TOL_BF16
+    assert rel_err(xb.grad.float().cpu(), xo.grad) < 2 * TOL_BF16
+
+
+def test_highway_bf16(device):
+    from gnnea import ops
+    rng = np.random.default_rng(9)
+    n, D = 400, 300
+    r, c, v = _graph(rng, n, 3000)
+    idx = torch.from_numpy(np.stack([r, c]).astype(np.int64))
+    adj = torch.sparse_coo_tensor(idx, torch.from_numpy(v), (n, n)).to(device)
+    f = lambda *s: torch.from_numpy(rng.standard_normal(s).astype(np.float32))
+    hidden, gate_pre, resid, bias, R = f(n, D), f(n, D), f(n, D), f(D), f(n, D)
+    hb = hidden.to(device).bfloat16().requires_grad_(True)
+    gb = gate_pre.to(device).bfloat16().requires_grad_(True)
+    rb = resid.to(device).bfloat16().requires_grad_(True)
+    y = ops.highway(adj, hb, gb, rb, bias.to(device), F.relu)
+    assert y.dtype == torch.bfloat16
+    (y.float() * R.to(device)).sum().backward()
+    A = torch.sparse_coo_tensor(idx, torch.from_numpy(v).double(), (n, n))
+    ho, go, ro = (t.detach().float().cpu().double().requires_grad_(True) for t in (hb, gb, rb))
+    s = torch.relu(A @ ho)
+    g = torch.sigmoid(go + bias.double())
+    yo = g * s + (1 - g) * ro
+    (yo * R.double()).sum().backward()
+    assert rel_err(y.detach().float().cpu(), yo.detach()) < TOL_BF16
+    for got, want in ((hb.grad, ho.grad), (gb.grad, go.grad), (rb.grad, ro.grad)):
+        assert got.dtype == torch.bfloat16
+        assert rel_err(got.float().cpu(), want) < 2 * TOL_BF16
+
+
+def test_bf16_rejects_misaligned_gracefully(device):
+    """Odd strides take the scalar path (no 8-B vector loads) and still agree."""
+    from gnnea import ops
+    rng = np.random.default_rng(11)
+    n, D = 300, 300
+    r, c, v = _graph(rng, n, 2000)
+    csr = _csr(r, c, v, n, device)
+    big = torch.from_numpy(rng.standard_normal((n, D + 3)).astype(np.float32)).to(device)
+    xb = big.bfloat16()[:, 1:D + 1]  # row stride D + 3, offset 2 bytes: scalar path
+    y = ops.spmm(csr, xb, out_dtype=torch.float32)
+    ref = _agg64(r, c, v, n, xb.float().cpu().double().numpy())
+    assert rel_err(y.cpu(), ref) < TOL_ACC
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (37, 300, 300), (300, 75, 300), (513, 600, 300),
+                                   (300, 300, 20000), (5, 300, 7), (2048, 300, 300)])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_bf16_vs_fp64(device, shape, ta, tb):
+    from gnnea import ops
+    M, N, K = shape
+    rng = np.random.default_rng(M + N + K + 10 * ta + tb)
+    a = torch.from_numpy(rng.standard_normal((K, M) if ta else (M, K)).astype(np.float32))
+    b = torch.from_numpy(rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32))
+    bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32))
+    ab, bb = a.to(device).bfloat16(), b.to(device).bfloat16()
+    y32 = ops.gemm(ab, bb, bool(ta), bool(tb), bias=bias.to(device), out_dtype=torch.float32)
+    a64, b64 = ab.float().cpu().double().numpy(), bb.float().cpu().double().numpy()
+    ref = (a64.T if ta else a64) @ (b64.T if tb else b64) + bias.double().numpy()
+    assert rel_err(y32.cpu(), ref) < TOL_ACC
+    yb = ops.gemm(ab, bb, bool(ta), bool(tb), bias=bias.to(device))
+    assert yb.dtype == torch.bfloat16
+    assert torch.equal(yb.view(torch.int16), y32.to(torch.bfloat16).view(torch.int16))
+
+
+def test_linear_bf16_autograd(device):
+    from gnnea import ops
+    rng = np.random.default_rng(21)
+    n, fin, fout = 1000, 300, 300
+    x = torch.from_numpy(rng.standard_normal((n, fin)).astype(np.float32))
+    W = torch.from_numpy((rng.standard_normal((fout, fin)) * 0.05).astype(np.float32))
+    bvec = torch.from_numpy(rng.standard_normal(fout).astype(np.float32))
+    R = torch.from_numpy(rng.standard_normal((n, fout)).astype(np.float32))
+    xb, Wb, bb = (t.to(device).bfloat16().requires_grad_(True) for t in (x, W, bvec))
+    y = ops.linear(xb, Wb, bb)
+    assert y.dtype == torch.bfloat16
+    (y.float() * R.to(device)).sum().backward()
+    xo, Wo, bo = (t.detach().float().cpu().double().requires_grad_(True) for t in (xb, Wb, bb))
+    yo = xo @ Wo.t() + bo
+    (yo * R.double()).sum().backward()
+    assert rel_err(y.detach().float().cpu(), yo.detach()) < TOL_BF16
+    for got, want in ((xb.grad, xo.grad), (Wb.grad, Wo.grad), (bb.grad, bo.grad)):
+        assert got.dtype == torch.bfloat16
+        assert rel_err(got.float().cpu(), want) < TOL_BF16

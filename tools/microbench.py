@@ -76,6 +76,15 @@ def main():
         ms = timeit(lambda: ops.spmm(csr, X, _lib.GNNEA_ACT_RELU, out=Y), args.reps)
         res["spmm_relu"] = {"ms": ms, "GBps_gather_model": gather / ms / 1e6,
                             "edges_per_s": E / ms * 1e3}
+    if want("spmm_bf16"):
+        # cfg-5 storage: bf16 rows gathered, fp32 accumulate, bf16 out (per-KG launches as ops)
+        Xb = X.to(torch.bfloat16)
+        Yb = torch.empty_like(Xb)
+        ms = timeit(lambda: ops.spmm(csr, Xb, _lib.GNNEA_ACT_RELU, out=Yb), args.reps)
+        gb = 4 * (N + 1) + 8 * E + 2 * E * D + 2 * N * D
+        res["spmm_relu_bf16"] = {"ms": ms, "GBps_gather_model": gb / ms / 1e6,
+                                 "edges_per_s": E / ms * 1e3}
+        del Xb, Yb
     if want("spmm_split"):
         # the same SpMM as two launches, one per KG block of rows (block-diagonal adjacency)
         Y = torch.empty_like(X)
@@ -125,6 +134,22 @@ def main():
         res["gemm_dW_splitK"] = {"ms": ms, "TFLOPs": 2.0 * N * D * D / ms / 1e9}
         ms = timeit(lambda: torch.mm(X, W.t()), args.reps)
         res["torch_mm_xWt_hipblaslt"] = {"ms": ms, "TFLOPs": 2.0 * N * D * D / ms / 1e9}
+    if want("gemm_bf16"):
+        Xb = X.to(torch.bfloat16)
+        Wb = (torch.randn(D, D, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+        bvec = torch.zeros(D, device=dev)
+        io = 2 * (2 * N * D + D * D)  # read X, write Y (bf16), W
+        ms = timeit(lambda: ops.gemm(Xb, Wb, trans_b=True, bias=bvec), args.reps)
+        res["gemm_bf16_xWt"] = {"ms": ms, "TFLOPs": 2.0 * N * D * D / ms / 1e9,
+                                "GBps_io": io / ms / 1e6}
+        dYb = torch.randn(N, D, device=dev, generator=g).to(torch.bfloat16)
+        ms = timeit(lambda: ops.gemm(dYb, Xb, trans_a=True), args.reps)
+        res["gemm_bf16_dW_splitK"] = {"ms": ms, "TFLOPs": 2.0 * N * D * D / ms / 1e9}
+        ms = timeit(lambda: ops.gemm(dYb, Wb), args.reps)
+        res["gemm_bf16_dX"] = {"ms": ms, "TFLOPs": 2.0 * N * D * D / ms / 1e9}
+        ms = timeit(lambda: torch.mm(Xb, Wb.t()), args.reps)
+        res["torch_mm_bf16_xWt_hipblaslt"] = {"ms": ms, "TFLOPs": 2.0 * N * D * D / ms / 1e9}
+        del Xb, dYb
     if want("gat"):
         heads, dh = 4, 75
         a_all = torch.randn(heads, 2 * dh, device=dev, generator=g) * 0.1
