@@ -92,8 +92,8 @@ __device__ __forceinline__ constexpr int grp_lane(int v) { return v * ((LPH >= 1
 
 // s1[i,h] = sum_d H[i, h*dh+d] * a[h, d];  s2[i,h] = sum_d H[i, h*dh+d] * a[h, dh+d]
 // A wave walks rows (grid-stride) with the lane's slice of a preloaded.
-template <int H, int EPL>
-__global__ __launch_bounds__(256) void k_gat_scores(const float* __restrict__ Hm, int64_t ldh,
+template <int H, int EPL, typename T>
+__global__ __launch_bounds__(256) void k_gat_scores(const T* __restrict__ Hm, int64_t ldh,
                                                     int n_rows, int dh,
                                                     const float* __restrict__ a,
                                                     float* __restrict__ s1,
@@ -111,10 +111,10 @@ __global__ __launch_bounds__(256) void k_gat_scores(const float* __restrict__ Hm
   }
   const int nw = gridDim.x * 4;
   for (int row = blockIdx.x * 4 + wave_id(); row < n_rows; row += nw) {
-    const float* x = Hm + (int64_t)row * ldh;
+    const T* x = Hm + (int64_t)row * ldh;
     float xv[EPL];
 #pragma unroll
-    for (int t = 0; t < EPL; ++t) xv[t] = x[hl.c[t]];
+    for (int t = 0; t < EPL; ++t) xv[t] = to_f32<T>(x[hl.c[t]]);
     float p[2] = {0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < EPL; ++t) {
@@ -131,14 +131,16 @@ __global__ __launch_bounds__(256) void k_gat_scores(const float* __restrict__ Hm
   }
 }
 
-template <int ACT, int H, int NCH>
+template <int ACT, int H, int NCH, typename T>
 __global__ __launch_bounds__(256) void k_gat_fwd(const int32_t* __restrict__ rowptr,
                                                  const int32_t* __restrict__ col, int n_rows,
-                                                 const float4* __restrict__ Hm, int64_t ldh4,
+                                                 const typename Vec4<T>::raw* __restrict__ Hm,
+                                                 int64_t ldh4,
                                                  int D, int dh, const float* __restrict__ s1,
                                                  const float* __restrict__ s2, float alpha,
                                                  const float* __restrict__ emask,
-                                                 float4* __restrict__ Y, int64_t ldy4,
+                                                 typename Vec4<T>::raw* __restrict__ Y,
+                                                 int64_t ldy4,
                                                  float* __restrict__ m_out,
                                                  float* __restrict__ den_out) {
   constexpr int kFE = 2;  // edges per chunk (measured: 2 beats 1 and 4)
@@ -203,12 +205,12 @@ __global__ __launch_bounds__(256) void k_gat_fwd(const int32_t* __restrict__ row
     // kFE edges at a time: their neighbour rows are gathered together (kFE * NCH loads in
     // flight), then accumulated in edge order
     for (int k = 0; k < cnt; k += kFE) {
-      float4 r[kFE][NCH];
+      typename Vec4<T>::raw r[kFE][NCH];
       float w[kFE][H];
 #pragma unroll
       for (int e = 0; e < kFE; ++e) {
         const int ke = min(k + e, cnt - 1);  // past the chunk: a valid row, not accumulated
-        const float4* x = Hm + (int64_t)readlane_i(mj, ke) * ldh4 + lane;
+        const typename Vec4<T>::raw* x = Hm + (int64_t)readlane_i(mj, ke) * ldh4 + lane;
 #pragma unroll
         for (int h = 0; h < H; ++h) w[e][h] = readlane_f(wl[h], ke);
 #pragma unroll
@@ -221,10 +223,11 @@ __global__ __launch_bounds__(256) void k_gat_fwd(const int32_t* __restrict__ row
 #pragma unroll
         for (int q = 0; q < NCH; ++q)
           if (own[q]) {
-            acc[q].x = fmaf(hsel<H>(w[e], hd[q][0]), r[e][q].x, acc[q].x);
-            acc[q].y = fmaf(hsel<H>(w[e], hd[q][1]), r[e][q].y, acc[q].y);
-            acc[q].z = fmaf(hsel<H>(w[e], hd[q][2]), r[e][q].z, acc[q].z);
-            acc[q].w = fmaf(hsel<H>(w[e], hd[q][3]), r[e][q].w, acc[q].w);
+            const float4 xv = Vec4<T>::get(r[e][q]);
+            acc[q].x = fmaf(hsel<H>(w[e], hd[q][0]), xv.x, acc[q].x);
+            acc[q].y = fmaf(hsel<H>(w[e], hd[q][1]), xv.y, acc[q].y);
+            acc[q].z = fmaf(hsel<H>(w[e], hd[q][2]), xv.z, acc[q].z);
+            acc[q].w = fmaf(hsel<H>(w[e], hd[q][3]), xv.w, acc[q].w);
           }
       }
     }
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd(const int32_t* __restrict__ row
     o.y = hd[q][1] < H ? act_fwd<ACT>(acc[q].y * hsel<H>(rinv, hd[q][1])) : 0.f;
     o.z = hd[q][2] < H ? act_fwd<ACT>(acc[q].z * hsel<H>(rinv, hd[q][2])) : 0.f;
     o.w = hd[q][3] < H ? act_fwd<ACT>(acc[q].w * hsel<H>(rinv, hd[q][3])) : 0.f;
-    Y[(int64_t)row * ldy4 + lane + 64 * q] = o;
+    Y[(int64_t)row * ldy4 + lane + 64 * q] = Vec4<T>::put(o);
   }
   if (lane < H) {
     m_out[(int64_t)row * H + lane] = hsel<H>(mx, lane);
@@ -261,14 +264,15 @@ __global__ __launch_bounds__(256) void k_gat_fwd(const int32_t* __restrict__ row
 //        dH_i += ds1_i (x) a1
 // ---------------------------------------------------------------------------------------- //
 
-template <int ACT, int H, int NCH>
+template <int ACT, int H, int NCH, typename T>
 __global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
-                                                      const float4* __restrict__ dY,
-                                                      const float4* __restrict__ Y, int64_t ld4,
+                                                      const typename Vec4<T>::raw* __restrict__ dY,
+                                                      const typename Vec4<T>::raw* __restrict__ Y,
+                                                      int64_t ld4,
                                                       const float* __restrict__ s1,
                                                       const float* __restrict__ mrow,
                                                       const float* __restrict__ den,
-                                                      float4* __restrict__ G,
+                                                      typename Vec4<T>::raw* __restrict__ G,
                                                       float4* __restrict__ rec) {
   const int row = blockIdx.x * 4 + wave_id();
   if (row >= n_rows) return;
@@ -280,7 +284,8 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
   for (int q = 0; q < NCH; ++q) {
     const int c4 = lane + 64 * q;
     if (4 * c4 >= D) continue;
-    const float4 dy = dY[(int64_t)row * ld4 + c4], y = Y[(int64_t)row * ld4 + c4];
+    const float4 dy = Vec4<T>::get(dY[(int64_t)row * ld4 + c4]);
+    const float4 y = Vec4<T>::get(Y[(int64_t)row * ld4 + c4]);
     const float ys[4] = {y.x, y.y, y.z, y.w};
     float gs[4] = {dy.x, dy.y, dy.z, dy.w};
 #pragma unroll
@@ -292,7 +297,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
 #pragma unroll
       for (int h = 0; h < H; ++h) cp[h] += (hh == h) ? gs[t] * ys[t] : 0.f;
     }
-    G[(int64_t)row * ld4 + c4] = make_float4(gs[0], gs[1], gs[2], gs[3]);
+    G[(int64_t)row * ld4 + c4] = Vec4<T>::put(make_float4(gs[0], gs[1], gs[2], gs[3]));
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) cp[h] = wave_sum(cp[h]);
@@ -306,13 +311,13 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
 // Head-grouped layout: per in-edge (i, j) the lane accumulates alpha*mask*G_i into its own
 // elements and the product G_i . H_j over them; kEB edges' G rows are gathered together (the next
 // chunk's in flight meanwhile) and their per-head dot products reduced by one grp_sum (lane h*LPH + grp_lane(e) gets edge e, head h).
-template <int H, int EPL>
+template <int H, int EPL, typename T>
 __global__ __launch_bounds__(256) void k_gat_bwd_src(
     const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT,
-    const int64_t* __restrict__ permT, int n_rows, int dh, const float* __restrict__ Hm,
+    const int64_t* __restrict__ permT, int n_rows, int dh, const T* __restrict__ Hm,
     int64_t ldh, const float* __restrict__ s2, float alpha, const float* __restrict__ emask,
-    const float4* __restrict__ rec, const float* __restrict__ G, int64_t ldg,
-    const float* __restrict__ a, float* __restrict__ dH, int64_t lddh, float* __restrict__ dzT,
+    const float4* __restrict__ rec, const T* __restrict__ G, int64_t ldg,
+    const float* __restrict__ a, T* __restrict__ dH, int64_t lddh, float* __restrict__ dzT,
     float* __restrict__ ds2) {
   using L = HeadLanes<H, EPL>;
   constexpr int LPH = L::LPH;
@@ -327,10 +332,10 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(
 
   float hj[EPL], acc[EPL];
   {
-    const float* x = Hm + (int64_t)row * ldh;
+    const T* x = Hm + (int64_t)row * ldh;
 #pragma unroll
     for (int t = 0; t < EPL; ++t) {
-      const float v = x[hl.c[t]];
+      const float v = to_f32<T>(x[hl.c[t]]);
       hj[t] = hl.ok[t] ? v : 0.f;
       acc[t] = 0.f;
     }
@@ -348,9 +353,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(
   auto load = [&](float (&g)[kEB][EPL], int mi, int k, int cnt) {
 #pragma unroll
     for (int e = 0; e < kEB; ++e) {
-      const float* gr = G + (int64_t)readlane_i(mi, min(k + e, cnt - 1)) * ldg;
+      const T* gr = G + (int64_t)readlane_i(mi, min(k + e, cnt - 1)) * ldg;
 #pragma unroll
-      for (int t = 0; t < EPL; ++t) g[e][t] = gr[hl.c[t]];
+      for (int t = 0; t < EPL; ++t) g[e][t] = to_f32<T>(gr[hl.c[t]]);
     }
   };
   for (int base = beg; base < end; base += 64) {
@@ -437,18 +442,19 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(
     d2me = hme == h ? d2 : d2me;
     if (lane == 0) ds2[(int64_t)row * H + h] = d2;
   }
-  float* out = dH + (int64_t)row * lddh;
+  T* out = dH + (int64_t)row * lddh;
 #pragma unroll
   for (int t = 0; t < EPL; ++t)
-    if (hl.ok[t]) out[hl.c[t]] = acc[t] + d2me * a[hme * 2 * dh + dh + hl.d0 + t];
+    if (hl.ok[t]) out[hl.c[t]] = from_f32<T>(acc[t] + d2me * a[hme * 2 * dh + dh + hl.d0 + t]);
 }
 
-template <int H, int NCH>
+template <int H, int NCH, typename T>
 __global__ __launch_bounds__(256) void k_gat_bwd_dst(const int32_t* __restrict__ rowptr,
                                                      const int64_t* __restrict__ tpos, int n_rows,
                                                      int D, int dh, const float* __restrict__ dzT,
                                                      const float* __restrict__ a,
-                                                     float4* __restrict__ dH, int64_t lddh4,
+                                                     typename Vec4<T>::raw* __restrict__ dH,
+                                                     int64_t lddh4,
                                                      float* __restrict__ ds1) {
   const int row = blockIdx.x * 4 + wave_id();
   if (row >= n_rows) return;
@@ -468,7 +474,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(const int32_t* __restrict__
   for (int q = 0; q < NCH; ++q) {
     const int c4 = lane + 64 * q;
     if (4 * c4 >= D) continue;
-    float4 v = dH[(int64_t)row * lddh4 + c4];
+    float4 v = Vec4<T>::get(dH[(int64_t)row * lddh4 + c4]);
     float o[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -478,13 +484,12 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(const int32_t* __restrict__
         o[t] += hsel<H>(p, h) * a[h * 2 * dh + (c - h * dh)];
       }
     }
-    dH[(int64_t)row * lddh4 + c4] = make_float4(o[0], o[1], o[2], o[3]);
+    dH[(int64_t)row * lddh4 + c4] = Vec4<T>::put(make_float4(o[0], o[1], o[2], o[3]));
   }
   if (lane < H) ds1[(int64_t)row * H + lane] = hsel<H>(p, lane);
 }
 
 static bool ok_ld(int64_t ld, int D) { return ld % 4 == 0 && ld >= ((D + 3) / 4) * 4; }
-static bool al16(const void* p) { return p == nullptr || (((uintptr_t)p) & 15) == 0; }
 
 }  // namespace gnnea
 
@@ -531,19 +536,23 @@ static int epl_of(int heads, int dh) {
     }                                                                      \
   } while (0)
 
-extern "C" int gnnea_gat_scores_f32(const float* Hm, int64_t ldh, int32_t n_rows, int heads,
-                                    int d_head, const float* a, float* s1, float* s2,
-                                    void* stream) {
+template <typename T>
+static bool alv(const void* p) {  // aligned for one Vec4<T> access (16 B fp32, 8 B bf16)
+  return p == nullptr || (((uintptr_t)p) & (sizeof(typename Vec4<T>::raw) - 1)) == 0;
+}
+
+template <typename T>
+static int gat_scores_t(const T* Hm, int64_t ldh, int32_t n_rows, int heads, int d_head,
+                        const float* a, float* s1, float* s2, hipStream_t s) {
   if (n_rows < 0 || heads < 1 || d_head < 1) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
   const int D = heads * d_head;
   if (!Hm || !a || !s1 || !s2) return GNNEA_EINVAL;
-  if (!ok_ld(ldh, D) || !al16(Hm)) return GNNEA_EALIGN;
+  if (!ok_ld(ldh, D) || !alv<T>(Hm)) return GNNEA_EALIGN;
   const int nb = div_up(n_rows, 4) < 2048 ? div_up(n_rows, 4) : 2048;  // waves walk rows
-  hipStream_t s = (hipStream_t)stream;
 #define CALL(HH, EE)                                                                          \
   case HH * 32 + EE:                                                                          \
-    hipLaunchKernelGGL((k_gat_scores<HH, EE>), dim3(nb), dim3(256), 0, s, Hm, ldh, n_rows,    \
+    hipLaunchKernelGGL((k_gat_scores<HH, EE, T>), dim3(nb), dim3(256), 0, s, Hm, ldh, n_rows, \
                        d_head, a, s1, s2);                                                    \
     break;
   GNNEA_GAT_HL_DISPATCH(CALL);
@@ -552,22 +561,22 @@ extern "C" int gnnea_gat_scores_f32(const float* Hm, int64_t ldh, int32_t n_rows
   return 0;
 }
 
-extern "C" int gnnea_gat_fwd_f32(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
-                                 const float* Hm, int64_t ldh, int heads, int d_head,
-                                 const float* s1, const float* s2, float alpha,
-                                 const float* edge_mask, int act, float* Y, int64_t ldy,
-                                 float* m_out, float* den_out, void* stream) {
+template <typename T>
+static int gat_fwd_t(const int32_t* rowptr, const int32_t* col, int32_t n_rows, const T* Hm,
+                     int64_t ldh, int heads, int d_head, const float* s1, const float* s2,
+                     float alpha, const float* edge_mask, int act, T* Y, int64_t ldy,
+                     float* m_out, float* den_out, hipStream_t s) {
+  typedef typename Vec4<T>::raw R;
   if (n_rows < 0 || heads < 1 || d_head < 1) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
   const int D = heads * d_head, D4 = (D + 3) / 4;
   if (!rowptr || !col || !Hm || !s1 || !s2 || !Y || !m_out || !den_out) return GNNEA_EINVAL;
-  if (!ok_ld(ldh, D) || !ok_ld(ldy, D) || !al16(Hm) || !al16(Y)) return GNNEA_EALIGN;
+  if (!ok_ld(ldh, D) || !ok_ld(ldy, D) || !alv<T>(Hm) || !alv<T>(Y)) return GNNEA_EALIGN;
   const int nb = div_up(n_rows, 4);
-  hipStream_t s = (hipStream_t)stream;
-#define CALL_A(A, HH, NN)                                                                     \
-  hipLaunchKernelGGL((k_gat_fwd<A, HH, NN>), dim3(nb), dim3(256), 0, s, rowptr, col, n_rows,  \
-                     (const float4*)Hm, ldh / 4, D, d_head, s1, s2, alpha, edge_mask,         \
-                     (float4*)Y, ldy / 4, m_out, den_out)
+#define CALL_A(A, HH, NN)                                                                       \
+  hipLaunchKernelGGL((k_gat_fwd<A, HH, NN, T>), dim3(nb), dim3(256), 0, s, rowptr, col, n_rows, \
+                     (const R*)Hm, ldh / 4, D, d_head, s1, s2, alpha, edge_mask, (R*)Y,         \
+                     ldy / 4, m_out, den_out)
 #define CALL(HH, NN)                                                   \
   case HH * 8 + NN:                                                    \
     switch (act) {                                                     \
@@ -584,21 +593,22 @@ extern "C" int gnnea_gat_fwd_f32(const int32_t* rowptr, const int32_t* col, int3
   return 0;
 }
 
-extern "C" int gnnea_gat_bwd_prep_f32(int32_t n_rows, int heads, int d_head, const float* dY,
-                                      const float* Y, int64_t ld, const float* s1,
-                                      const float* m, const float* den, int act, float* G,
-                                      float* rec, void* stream) {
+template <typename T>
+static int gat_bwd_prep_t(int32_t n_rows, int heads, int d_head, const T* dY, const T* Y,
+                          int64_t ld, const float* s1, const float* m, const float* den, int act,
+                          T* G, float* rec, hipStream_t s) {
+  typedef typename Vec4<T>::raw R;
   if (n_rows < 0 || heads < 1 || d_head < 1) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
   const int D = heads * d_head, D4 = (D + 3) / 4;
   if (!dY || !Y || !s1 || !m || !den || !G || !rec) return GNNEA_EINVAL;
-  if (!ok_ld(ld, D) || !al16(dY) || !al16(Y) || !al16(G) || !al16(rec)) return GNNEA_EALIGN;
+  if (!ok_ld(ld, D) || !alv<T>(dY) || !alv<T>(Y) || !alv<T>(G) || !alv<float>(rec))
+    return GNNEA_EALIGN;
   if (act != GNNEA_ACT_IDENTITY && act != GNNEA_ACT_RELU) return GNNEA_EINVAL;
   const int nb = div_up(n_rows, 4);
-  hipStream_t s = (hipStream_t)stream;
 #define CALL_A(A, HH, NN)                                                                      \
-  hipLaunchKernelGGL((k_gat_bwd_prep<A, HH, NN>), dim3(nb), dim3(256), 0, s, n_rows, D, d_head, \
-                     (const float4*)dY, (const float4*)Y, ld / 4, s1, m, den, (float4*)G,      \
+  hipLaunchKernelGGL((k_gat_bwd_prep<A, HH, NN, T>), dim3(nb), dim3(256), 0, s, n_rows, D,    \
+                     d_head, (const R*)dY, (const R*)Y, ld / 4, s1, m, den, (R*)G,            \
                      (float4*)rec)
 #define CALL(HH, NN)                                                        \
   case HH * 8 + NN:                                                         \
@@ -612,25 +622,24 @@ extern "C" int gnnea_gat_bwd_prep_f32(int32_t n_rows, int heads, int d_head, con
   return 0;
 }
 
-extern "C" int gnnea_gat_bwd_src_f32(const int32_t* rowptrT, const int32_t* colT,
-                                     const int64_t* permT, int32_t n_rows, int heads, int d_head,
-                                     const float* H, int64_t ldh, const float* s2, float alpha,
-                                     const float* edge_mask, const float* rec, const float* G,
-                                     int64_t ldg, const float* a, float* dH, int64_t lddh,
-                                     float* dzT, float* ds2, void* stream) {
+template <typename T>
+static int gat_bwd_src_t(const int32_t* rowptrT, const int32_t* colT, const int64_t* permT,
+                         int32_t n_rows, int heads, int d_head, const T* H, int64_t ldh,
+                         const float* s2, float alpha, const float* edge_mask, const float* rec,
+                         const T* G, int64_t ldg, const float* a, T* dH, int64_t lddh,
+                         float* dzT, float* ds2, hipStream_t s) {
   if (n_rows < 0 || heads < 1 || d_head < 1) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
   const int D = heads * d_head;
   if (!rowptrT || !colT || !permT || !H || !s2 || !rec || !G || !a || !dH || !dzT || !ds2)
     return GNNEA_EINVAL;
-  if (!ok_ld(ldh, D) || !ok_ld(ldg, D) || !ok_ld(lddh, D) || !al16(H) || !al16(G) || !al16(dH) ||
-      !al16(rec))
+  if (!ok_ld(ldh, D) || !ok_ld(ldg, D) || !ok_ld(lddh, D) || !alv<T>(H) || !alv<T>(G) ||
+      !alv<T>(dH) || !alv<float>(rec))
     return GNNEA_EALIGN;
   const int nb = div_up(n_rows, 4);
-  hipStream_t s = (hipStream_t)stream;
 #define CALL(HH, EE)                                                                          \
   case HH * 32 + EE:                                                                          \
-    hipLaunchKernelGGL((k_gat_bwd_src<HH, EE>), dim3(nb), dim3(256), 0, s, rowptrT, colT,     \
+    hipLaunchKernelGGL((k_gat_bwd_src<HH, EE, T>), dim3(nb), dim3(256), 0, s, rowptrT, colT,  \
                        permT, n_rows, d_head, H, ldh, s2, alpha, edge_mask,                   \
                        (const float4*)rec, G, ldg, a, dH, lddh, dzT, ds2);                    \
     break;
@@ -640,23 +649,110 @@ extern "C" int gnnea_gat_bwd_src_f32(const int32_t* rowptrT, const int32_t* colT
   return 0;
 }
 
-extern "C" int gnnea_gat_bwd_dst_f32(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows,
-                                     int heads, int d_head, const float* dzT, const float* a,
-                                     float* dH, int64_t lddh, float* ds1, void* stream) {
+template <typename T>
+static int gat_bwd_dst_t(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows, int heads,
+                         int d_head, const float* dzT, const float* a, T* dH, int64_t lddh,
+                         float* ds1, hipStream_t s) {
+  typedef typename Vec4<T>::raw R;
   if (n_rows < 0 || heads < 1 || d_head < 1) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
   const int D = heads * d_head, D4 = (D + 3) / 4;
   if (!rowptr || !tpos || !dzT || !a || !dH || !ds1) return GNNEA_EINVAL;
-  if (!ok_ld(lddh, D) || !al16(dH)) return GNNEA_EALIGN;
+  if (!ok_ld(lddh, D) || !alv<T>(dH)) return GNNEA_EALIGN;
   const int nb = div_up(n_rows, 4);
-  hipStream_t s = (hipStream_t)stream;
 #define CALL(HH, NN)                                                                          \
   case HH * 8 + NN:                                                                           \
-    hipLaunchKernelGGL((k_gat_bwd_dst<HH, NN>), dim3(nb), dim3(256), 0, s, rowptr, tpos,      \
-                       n_rows, D, d_head, dzT, a, (float4*)dH, lddh / 4, ds1);                \
+    hipLaunchKernelGGL((k_gat_bwd_dst<HH, NN, T>), dim3(nb), dim3(256), 0, s, rowptr, tpos,   \
+                       n_rows, D, d_head, dzT, a, (R*)dH, lddh / 4, ds1);                     \
     break;
   GNNEA_GAT_DISPATCH(CALL);
 #undef CALL
   GNNEA_LAUNCH_CHECK();
   return 0;
+}
+
+// ---- C-ABI: fp32 and bf16 feature storage (H, Y, dY, G, dH); logits, records, dz stay fp32 --
+
+extern "C" int gnnea_gat_scores_f32(const float* Hm, int64_t ldh, int32_t n_rows, int heads,
+                                    int d_head, const float* a, float* s1, float* s2,
+                                    void* stream) {
+  return gat_scores_t<float>(Hm, ldh, n_rows, heads, d_head, a, s1, s2, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_fwd_f32(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
+                                 const float* Hm, int64_t ldh, int heads, int d_head,
+                                 const float* s1, const float* s2, float alpha,
+                                 const float* edge_mask, int act, float* Y, int64_t ldy,
+                                 float* m_out, float* den_out, void* stream) {
+  return gat_fwd_t<float>(rowptr, col, n_rows, Hm, ldh, heads, d_head, s1, s2, alpha, edge_mask,
+                          act, Y, ldy, m_out, den_out, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_bwd_prep_f32(int32_t n_rows, int heads, int d_head, const float* dY,
+                                      const float* Y, int64_t ld, const float* s1,
+                                      const float* m, const float* den, int act, float* G,
+                                      float* rec, void* stream) {
+  return gat_bwd_prep_t<float>(n_rows, heads, d_head, dY, Y, ld, s1, m, den, act, G, rec,
+                               (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_bwd_src_f32(const int32_t* rowptrT, const int32_t* colT,
+                                     const int64_t* permT, int32_t n_rows, int heads, int d_head,
+                                     const float* H, int64_t ldh, const float* s2, float alpha,
+                                     const float* edge_mask, const float* rec, const float* G,
+                                     int64_t ldg, const float* a, float* dH, int64_t lddh,
+                                     float* dzT, float* ds2, void* stream) {
+  return gat_bwd_src_t<float>(rowptrT, colT, permT, n_rows, heads, d_head, H, ldh, s2, alpha,
+                              edge_mask, rec, G, ldg, a, dH, lddh, dzT, ds2,
+                              (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_bwd_dst_f32(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows,
+                                     int heads, int d_head, const float* dzT, const float* a,
+                                     float* dH, int64_t lddh, float* ds1, void* stream) {
+  return gat_bwd_dst_t<float>(rowptr, tpos, n_rows, heads, d_head, dzT, a, dH, lddh, ds1,
+                              (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_scores_bf16(const void* Hm, int64_t ldh, int32_t n_rows, int heads,
+                                     int d_head, const float* a, float* s1, float* s2,
+                                     void* stream) {
+  return gat_scores_t<bf16_t>((const bf16_t*)Hm, ldh, n_rows, heads, d_head, a, s1, s2,
+                              (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_fwd_bf16(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
+                                  const void* Hm, int64_t ldh, int heads, int d_head,
+                                  const float* s1, const float* s2, float alpha,
+                                  const float* edge_mask, int act, void* Y, int64_t ldy,
+                                  float* m_out, float* den_out, void* stream) {
+  return gat_fwd_t<bf16_t>(rowptr, col, n_rows, (const bf16_t*)Hm, ldh, heads, d_head, s1, s2,
+                           alpha, edge_mask, act, (bf16_t*)Y, ldy, m_out, den_out,
+                           (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_bwd_prep_bf16(int32_t n_rows, int heads, int d_head, const void* dY,
+                                       const void* Y, int64_t ld, const float* s1,
+                                       const float* m, const float* den, int act, void* G,
+                                       float* rec, void* stream) {
+  return gat_bwd_prep_t<bf16_t>(n_rows, heads, d_head, (const bf16_t*)dY, (const bf16_t*)Y, ld,
+                                s1, m, den, act, (bf16_t*)G, rec, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_bwd_src_bf16(const int32_t* rowptrT, const int32_t* colT,
+                                      const int64_t* permT, int32_t n_rows, int heads,
+                                      int d_head, const void* H, int64_t ldh, const float* s2,
+                                      float alpha, const float* edge_mask, const float* rec,
+                                      const void* G, int64_t ldg, const float* a, void* dH,
+                                      int64_t lddh, float* dzT, float* ds2, void* stream) {
+  return gat_bwd_src_t<bf16_t>(rowptrT, colT, permT, n_rows, heads, d_head, (const bf16_t*)H,
+                               ldh, s2, alpha, edge_mask, rec, (const bf16_t*)G, ldg, a,
+                               (bf16_t*)dH, lddh, dzT, ds2, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_bwd_dst_bf16(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows,
+                                      int heads, int d_head, const float* dzT, const float* a,
+                                      void* dH, int64_t lddh, float* ds1, void* stream) {
+  return gat_bwd_dst_t<bf16_t>(rowptr, tpos, n_rows, heads, d_head, dzT, a, (bf16_t*)dH, lddh,
+                               ds1, (hipStream_t)stream);
 }

@@ -87,13 +87,23 @@ SIGNATURES = {
                                               ctypes.c_int, _p]),
     "gnnea_gat_scores_f32": (ctypes.c_int, [_p, _i64, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,
                                             _p]),
+    "gnnea_gat_scores_bf16": (ctypes.c_int, [_p, _i64, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,
+                                            _p]),
     "gnnea_gat_fwd_f32": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int, ctypes.c_int, _p, _p,
+                                         _f32, _p, ctypes.c_int, _p, _i64, _p, _p, _p]),
+    "gnnea_gat_fwd_bf16": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int, ctypes.c_int, _p, _p,
                                          _f32, _p, ctypes.c_int, _p, _i64, _p, _p, _p]),
     "gnnea_gat_bwd_prep_f32": (ctypes.c_int, [_i32, ctypes.c_int, ctypes.c_int, _p, _p, _i64, _p,
                                               _p, _p, ctypes.c_int, _p, _p, _p]),
+    "gnnea_gat_bwd_prep_bf16": (ctypes.c_int, [_i32, ctypes.c_int, ctypes.c_int, _p, _p, _i64, _p,
+                                              _p, _p, ctypes.c_int, _p, _p, _p]),
     "gnnea_gat_bwd_src_f32": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _i64,
                                              _p, _f32, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
+    "gnnea_gat_bwd_src_bf16": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _i64,
+                                             _p, _f32, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
     "gnnea_gat_bwd_dst_f32": (ctypes.c_int, [_p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,
+                                             _i64, _p, _p]),
+    "gnnea_gat_bwd_dst_bf16": (ctypes.c_int, [_p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,
                                              _i64, _p, _p]),
     "gnnea_gemm_ws_bytes": (_i64, [_i64, _i64, _i64]),
     "gnnea_gemm_bf16_ws_bytes": (_i64, [_i64, _i64, _i64]),

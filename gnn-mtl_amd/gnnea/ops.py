@@ -70,6 +70,15 @@ def _gemm_ws(device, nbytes):
     return buf
 
 
+_SMALL_OPERAND = 1 << 22
+
+
+def _ld(t):
+    """Row stride of a row-major matrix; a single row's stride is meaningless (torch reports 1
+    for a transposed column vector), its width is the valid leading dimension."""
+    return t.stride(0) if t.shape[0] > 1 else max(t.shape[1], 1)
+
+
 def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_dtype=None):
     """out = op(a) @ op(b) (+ bias) (+ beta*out) on MFMA.
 
@@ -81,6 +90,13 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
     if bf:
         a = _featc(a, torch.bfloat16)
         b = _featc(b, torch.bfloat16)
+        # the bf16 kernel stages K-contiguous operands with one 16-B LDS store per chunk and
+        # transposes the others element by element: hand it a small weight pre-transposed
+        # (W is <= a few MB; dY.W in the Linear backward, x.W in GAT / HighWay)
+        if not trans_b and b.numel() <= _SMALL_OPERAND:
+            b, trans_b = b.t().contiguous(), True
+        if trans_a and a.numel() <= _SMALL_OPERAND:
+            a, trans_a = a.t().contiguous(), False
     else:
         a = _f32c(a)
         b = _f32c(b)
@@ -105,14 +121,14 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
     with torch.cuda.device(a.device):
         if bf:
             cd = _lib.GNNEA_BF16 if out.dtype == torch.bfloat16 else _lib.GNNEA_F32
-            check(L.gnnea_gemm_bf16(int(trans_a), int(trans_b), M, N, K, ptr(a), a.stride(0),
-                                    ptr(b), b.stride(0), ptr(bias), float(beta), ptr(out),
-                                    out.stride(0), cd, ptr(ws),
+            check(L.gnnea_gemm_bf16(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a),
+                                    ptr(b), _ld(b), ptr(bias), float(beta), ptr(out),
+                                    _ld(out), cd, ptr(ws),
                                     ws_bytes if ws is not None else 0, stream_of(a.device)))
         else:
-            check(L.gnnea_gemm_f32(int(trans_a), int(trans_b), M, N, K, ptr(a), a.stride(0),
-                                   ptr(b), b.stride(0), ptr(bias), float(beta), ptr(out),
-                                   out.stride(0), ptr(ws), ws_bytes if ws is not None else 0,
+            check(L.gnnea_gemm_f32(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a),
+                                   ptr(b), _ld(b), ptr(bias), float(beta), ptr(out),
+                                   _ld(out), ptr(ws), ws_bytes if ws is not None else 0,
                                    stream_of(a.device)))
     return out
 
@@ -336,53 +352,63 @@ def highway(adj, hidden, gate_pre, resid, bias_gate, act_fn):
 # ------------------------------------------------------------------------------------------ #
 # GAT (all heads, one edge pass)                                                              #
 # ------------------------------------------------------------------------------------------ #
+def _gat_fn(name, dtype):
+    """C-ABI entry of a GAT kernel for the feature storage dtype (fp32 or bf16)."""
+    return getattr(_lib.lib(), name + ("_bf16" if dtype == torch.bfloat16 else "_f32"))
+
+
 def gat_scores(H, a_all, heads, d_head):
     N = H.shape[0]
     s1 = torch.empty((N, heads), dtype=torch.float32, device=H.device)
     s2 = torch.empty_like(s1)
     with torch.cuda.device(H.device):
-        check(_lib.lib().gnnea_gat_scores_f32(ptr(H), H.stride(0), N, heads, d_head, ptr(a_all),
-                                              ptr(s1), ptr(s2), stream_of(H.device)))
+        check(_gat_fn("gnnea_gat_scores", H.dtype)(ptr(H), H.stride(0), N, heads, d_head,
+                                                   ptr(a_all), ptr(s1), ptr(s2),
+                                                   stream_of(H.device)))
     return s1, s2
 
 
-def _pad4(t, D):
-    """[N, roundup4(D)] 16-B aligned row-major tensor whose first D columns are t (the GAT
-    kernels move 16 B per lane); t itself when it already qualifies."""
+def _pad4(t, D, dtype=None):
+    """[N, roundup4(D)] row-major tensor, rows aligned for one 4-element vector per lane (16 B
+    fp32, 8 B bf16), whose first D columns are t (in ``dtype``); t itself when it qualifies."""
+    dtype = dtype or (t.dtype if t.dtype in FEATURE_DTYPES else torch.float32)
     Dp = (D + 3) // 4 * 4
-    if (t.dtype == torch.float32 and t.stride(1) == 1 and t.stride(0) == Dp
-            and t.data_ptr() % 16 == 0
-            and (t.storage_offset() + t.shape[0] * Dp) * 4 <= t.untyped_storage().nbytes()):
+    es = torch.empty((), dtype=dtype).element_size()
+    if (t.dtype == dtype and t.stride(1) == 1 and t.stride(0) == Dp
+            and t.data_ptr() % (4 * es) == 0
+            and (t.storage_offset() + t.shape[0] * Dp) * es <= t.untyped_storage().nbytes()):
         return t
-    out = torch.zeros((t.shape[0], Dp), dtype=torch.float32, device=t.device)
+    out = torch.zeros((t.shape[0], Dp), dtype=dtype, device=t.device)
     out[:, :D] = t
     return out
 
 
 class GATFn(torch.autograd.Function):
     """h'_i = sum_j softmax_j(-LeakyReLU(a·[h_i||h_j])) h_j for all heads at once
-    (layers/att_layers.py:29-61 per head, concatenated at :86)."""
+    (layers/att_layers.py:29-61 per head, concatenated at :86).  H in fp32 or bf16 storage (the
+    output, the saved activations and dH follow it; logits and softmax records are fp32)."""
 
     @staticmethod
     def forward(ctx, H, a_all, csr, heads, d_head, alpha, act, edge_mask):
         D = heads * d_head
         H = _pad4(H, D)
-        a_all = _f32c(a_all)
+        a32 = _featc(a_all, torch.float32)
         N = csr.n_rows
-        s1, s2 = gat_scores(H, a_all, heads, d_head)
-        Y = torch.empty((N, (D + 3) // 4 * 4), dtype=torch.float32, device=H.device)
+        s1, s2 = gat_scores(H, a32, heads, d_head)
+        Y = torch.empty((N, (D + 3) // 4 * 4), dtype=H.dtype, device=H.device)
         m = torch.empty((N, heads), dtype=torch.float32, device=H.device)
         den = torch.empty_like(m)
-        em = _f32c(edge_mask) if edge_mask is not None else None
+        em = _featc(edge_mask, torch.float32) if edge_mask is not None else None
+        fwd = _gat_fn("gnnea_gat_fwd", H.dtype)
         with torch.cuda.device(H.device):
             for r0, r1 in _blocks(csr, H):  # per KG block when H exceeds the Infinity Cache
-                check(_lib.lib().gnnea_gat_fwd_f32(
-                    _off32(csr.rowptr, r0), ptr(csr.col), r1 - r0, ptr(H), H.stride(0), heads,
-                    d_head, _off(s1, r0), ptr(s2), float(alpha), ptr(em), int(act), _off(Y, r0),
-                    Y.stride(0), _off(m, r0), _off(den, r0), stream_of(H.device)))
+                check(fwd(_off32(csr.rowptr, r0), ptr(csr.col), r1 - r0, ptr(H), H.stride(0),
+                          heads, d_head, _off(s1, r0), ptr(s2), float(alpha), ptr(em), int(act),
+                          _off(Y, r0), Y.stride(0), _off(m, r0), _off(den, r0),
+                          stream_of(H.device)))
         ctx.csr = csr
         ctx.meta = (heads, d_head, float(alpha), int(act))
-        ctx.save_for_backward(H, a_all, s1, s2, m, den, Y, em if em is not None else torch.empty(0))
+        ctx.save_for_backward(H, a32, s1, s2, m, den, Y, em if em is not None else torch.empty(0))
         ctx.has_mask = em is not None
         return Y if Y.shape[1] == D else Y[:, :D]
 
@@ -394,12 +420,11 @@ class GATFn(torch.autograd.Function):
         csr = ctx.csr
         csrT = csr.transpose()
         D = heads * d_head
-        dY = _pad4(dY.float(), D)
+        dY = _pad4(dY, D, H.dtype)
         if dY.shape[1] != Y.shape[1]:
-            dY = _pad4(dY[:, :D].contiguous(), D)
+            dY = _pad4(dY[:, :D].contiguous(), D, H.dtype)
         N = csr.n_rows
         dev = H.device
-        L = _lib.lib()
         st = stream_of(dev)
         G = torch.empty_like(Y)
         rec = torch.empty((N, heads, 4), dtype=torch.float32, device=dev)
@@ -410,23 +435,25 @@ class GATFn(torch.autograd.Function):
         tpos = csr.tpos()
         with torch.cuda.device(dev):
             # G = dL/dh' and the per-node record {s1, m, 1/den, G.h'} (relu / identity: Y = h')
-            check(L.gnnea_gat_bwd_prep_f32(N, heads, d_head, ptr(dY), ptr(Y), Y.stride(0),
-                                           ptr(s1), ptr(m), ptr(den), int(act), ptr(G),
-                                           ptr(rec), st))
+            check(_gat_fn("gnnea_gat_bwd_prep", H.dtype)(
+                N, heads, d_head, ptr(dY), ptr(Y), Y.stride(0), ptr(s1), ptr(m), ptr(den),
+                int(act), ptr(G), ptr(rec), st))
+            src = _gat_fn("gnnea_gat_bwd_src", H.dtype)
             for j0, j1 in _blocks(csrT, G):  # source rows j of A^T, per KG block
-                check(L.gnnea_gat_bwd_src_f32(
-                    _off32(csrT.rowptr, j0), ptr(csrT.col), ptr(csrT.perm), j1 - j0, heads,
-                    d_head, _off(H, j0), H.stride(0), _off(s2, j0), alpha, ptr(em), ptr(rec),
-                    ptr(G), G.stride(0), ptr(a_all), _off(dH, j0), dH.stride(0), ptr(dzT),
-                    _off(ds2, j0), st))
-            check(L.gnnea_gat_bwd_dst_f32(ptr(csr.rowptr), ptr(tpos), N, heads, d_head,
-                                          ptr(dzT), ptr(a_all), ptr(dH), dH.stride(0), ptr(ds1),
-                                          st))
+                check(src(_off32(csrT.rowptr, j0), ptr(csrT.col), ptr(csrT.perm), j1 - j0, heads,
+                          d_head, _off(H, j0), H.stride(0), _off(s2, j0), alpha, ptr(em),
+                          ptr(rec), ptr(G), G.stride(0), ptr(a_all), _off(dH, j0), dH.stride(0),
+                          ptr(dzT), _off(ds2, j0), st))
+            check(_gat_fn("gnnea_gat_bwd_dst", H.dtype)(
+                ptr(csr.rowptr), ptr(tpos), N, heads, d_head, ptr(dzT), ptr(a_all), ptr(dH),
+                dH.stride(0), ptr(ds1), st))
         da = None
         if ctx.needs_input_grad[1]:
             # da1[h] = sum_i ds1[i,h] H_i,h ; da2[h] = sum_j ds2[j,h] H_j,h   (MFMA, split-K)
-            p1 = gemm(ds1, H[:, :D], trans_a=True).view(heads, heads, d_head)
-            p2 = gemm(ds2, H[:, :D], trans_a=True).view(heads, heads, d_head)
+            p1 = gemm(ds1, H[:, :D], trans_a=True, out_dtype=torch.float32)
+            p2 = gemm(ds2, H[:, :D], trans_a=True, out_dtype=torch.float32)
+            p1 = p1.view(heads, heads, d_head)
+            p2 = p2.view(heads, heads, d_head)
             idx = torch.arange(heads, device=H.device)
             da = torch.cat([p1[idx, idx], p2[idx, idx]], dim=1)
         return (dH if dH.shape[1] == D else dH[:, :D]), da, None, None, None, None, None, None

@@ -156,6 +156,27 @@ int gnnea_gat_bwd_dst_f32(const int32_t* rowptr, const int64_t* tpos, int32_t n_
                           int d_head, const float* dzT, const float* a, float* dH, int64_t lddh,
                           float* ds1, void* stream);
 
+/* bf16 feature storage (cfg-5): H, Y, dY, G, dH are bf16 (void*, row strides % 4 == 0, 8-B
+ * aligned); s1, s2, m, den, rec, dzT, ds1, ds2, a and edge_mask stay fp32; arithmetic is fp32 and
+ * every bf16 output is rounded once (nearest even). */
+int gnnea_gat_scores_bf16(const void* H, int64_t ldh, int32_t n_rows, int heads, int d_head,
+                          const float* a, float* s1, float* s2, void* stream);
+int gnnea_gat_fwd_bf16(const int32_t* rowptr, const int32_t* col, int32_t n_rows, const void* H,
+                       int64_t ldh, int heads, int d_head, const float* s1, const float* s2,
+                       float alpha, const float* edge_mask, int act, void* Y, int64_t ldy,
+                       float* m, float* den, void* stream);
+int gnnea_gat_bwd_prep_bf16(int32_t n_rows, int heads, int d_head, const void* dY, const void* Y,
+                            int64_t ld, const float* s1, const float* m, const float* den,
+                            int act, void* G, float* rec, void* stream);
+int gnnea_gat_bwd_src_bf16(const int32_t* rowptrT, const int32_t* colT, const int64_t* permT,
+                           int32_t n_rows, int heads, int d_head, const void* H, int64_t ldh,
+                           const float* s2, float alpha, const float* edge_mask, const float* rec,
+                           const void* G, int64_t ldg, const float* a, void* dH, int64_t lddh,
+                           float* dzT, float* ds2, void* stream);
+int gnnea_gat_bwd_dst_bf16(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows, int heads,
+                           int d_head, const float* dzT, const float* a, void* dH, int64_t lddh,
+                           float* ds1, void* stream);
+
 /* ------------------------------------------------------------------------------------------ *
  * Dense projection (nn.Linear at layers/layers.py:32,61,93; torch.mm at att_layers.py:33;
  * torch.spmm(x, kernel_gate) at layers.py:69).  f32-in / f32-accumulate MFMA

@@ -186,3 +186,53 @@ def test_linear_bf16_autograd(device):
     for got, want in ((xb.grad, xo.grad), (Wb.grad, Wo.grad), (bb.grad, bo.grad)):
         assert got.dtype == torch.bfloat16
         assert rel_err(got.float().cpu(), want) < TOL_BF16
+
+
+def _gat_ref64(r, c, n, H, a, heads, d, alpha):
+    """fp64 GAT over given projections H [n, heads*d] (att_layers.py:29-61 per head, concat)."""
+    outs = []
+    for h in range(heads):
+        Hh = H[:, h * d:(h + 1) * d]
+        z = Hh[r] @ a[h, :d] + Hh[c] @ a[h, d:]
+        e = torch.exp(-F.leaky_relu(z, alpha))
+        num = torch.zeros((n, d), dtype=H.dtype).index_add(0, torch.from_numpy(r), e[:, None] * Hh[c])
+        den = torch.zeros(n, dtype=H.dtype).index_add(0, torch.from_numpy(r), e)
+        outs.append(torch.relu(num / den[:, None]))
+    return torch.cat(outs, dim=1)
+
+
+@pytest.mark.parametrize("heads,d", [(4, 75), (1, 300), (8, 16), (3, 20)])
+def test_gat_bf16_vs_fp64(device, heads, d):
+    from gnnea import ops
+    rng = np.random.default_rng(31 + heads)
+    n = 400
+    r = rng.integers(0, n, 3000)
+    c = rng.integers(0, n, 3000)
+    r = np.concatenate([r, np.arange(n), np.zeros(200, dtype=r.dtype)])  # self loops + a hub row
+    c = np.concatenate([c, np.arange(n), rng.integers(0, n, 200)])
+    # one entry per (i, j), as the reference's adjacency (a dict) has
+    pairs = np.unique(np.stack([r, c], axis=1), axis=0)
+    r, c = pairs[:, 0].copy(), pairs[:, 1].copy()
+    v = np.ones(r.size, dtype=np.float32)
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([r, c]).astype(np.int64)),
+                                  torch.from_numpy(v), (n, n)).to(device)
+    D = heads * d
+    H = torch.from_numpy((rng.standard_normal((n, D)) * 0.5).astype(np.float32))
+    A = torch.from_numpy((rng.standard_normal((heads, 2 * d)) * 0.3).astype(np.float32))
+    R = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32))
+    Hb = H.to(device).bfloat16().requires_grad_(True)
+    At = A.to(device).requires_grad_(True)
+    y = ops.gat(adj, Hb, At, heads, d, 0.2, F.relu)
+    assert y.dtype == torch.bfloat16
+    (y.float() * R.to(device)).sum().backward()
+    Ho = Hb.detach().float().cpu().double().requires_grad_(True)
+    Ao = A.double().requires_grad_(True)
+    yo = _gat_ref64(r, c, n, Ho, Ao, heads, d, 0.2)
+    (yo * R.double()).sum().backward()
+    assert rel_err(y.detach().float().cpu(), yo.detach()) < TOL_BF16
+    assert Hb.grad.dtype == torch.bfloat16
+    assert rel_err(Hb.grad.float().cpu(), Ho.grad) < 2 * TOL_BF16
+    assert rel_err(At.grad.cpu(), Ao.grad) < 2 * TOL_BF16
+    # the same storage in fp32 gives the fp32 path's answer to bf16 rounding
+    y32 = ops.gat(adj, Hb.detach().float(), At.detach(), heads, d, 0.2, F.relu)
+    assert rel_err(y.detach().float().cpu(), y32.cpu()) < TOL_BF16

@@ -168,6 +168,23 @@ def main():
         ms = timeit(lambda: torch.autograd.grad(y, (H, a_all), dy, retain_graph=True),
                     max(3, args.reps // 2), warm=1)
         res["gat_bwd"] = {"ms": ms}
+    if want("gat_bf16"):
+        heads, dh = 4, 75
+        a_all = (torch.randn(heads, 2 * dh, device=dev, generator=g) * 0.1).requires_grad_(True)
+        Hb = X.to(torch.bfloat16).requires_grad_(True)
+
+        def fwdb():
+            return ops.GATFn.apply(Hb, a_all, csr, heads, dh, 0.2, _lib.GNNEA_ACT_RELU, None)
+        ms = timeit(fwdb, args.reps)
+        b = 4 * (N + 1) + E * (4 + 2 * D + 4 * heads) + N * (2 * D + 8 * heads)
+        res["gat_fwd_bf16"] = {"ms": ms, "GBps_model": b / ms / 1e6,
+                               "head_edges_per_s": heads * E / ms * 1e3}
+        yb = fwdb()
+        dyb = torch.randn_like(yb)
+        ms = timeit(lambda: torch.autograd.grad(yb, (Hb, a_all), dyb, retain_graph=True),
+                    max(3, args.reps // 2), warm=1)
+        res["gat_bwd_bf16"] = {"ms": ms}
+        del Hb, yb, dyb
     if want("gcn_layer"):
         from layers.layers import GraphConvolution
         idx = torch.stack([torch.from_numpy(r), torch.from_numpy(c)]).to(dev)
