@@ -138,4 +138,6 @@ def margin_loss(outputs, left, right, neg_left, neg_right, neg2_left, neg2_right
         idx = [_idx(a, outputs.device, outputs.shape[0]) for a in arrays]
     if idx[0].numel() != t or any(a.numel() != t * k for a in idx[2:]):
         raise ValueError("gnnea.margin: index arrays must have t and t*k entries")
+    if outputs.dtype == torch.bfloat16:  # bf16 models (cfg-5): the loss is an fp32 reduction
+        outputs = outputs.float()
     return MarginLossFn.apply(outputs, *idx, t, k)

@@ -236,3 +236,58 @@ def test_gat_bf16_vs_fp64(device, heads, d):
     # the same storage in fp32 gives the fp32 path's answer to bf16 rounding
     y32 = ops.gat(adj, Hb.detach().float(), At.detach(), heads, d, 0.2, F.relu)
     assert rel_err(y.detach().float().cpu(), y32.cpu()) < TOL_BF16
+
+
+@pytest.mark.parametrize("model", ["GCN", "GAT", "HGCN"])
+def test_model_bf16_end_to_end(golden, device, model):
+    """A whole drop-in encoder/decoder converted with .bfloat16() runs forward, margin loss and
+    backward on the bf16 kernels and stays within the bf16 tolerance of the fp32 model."""
+    from models.decoders import model2decoder
+    from models.encoders import model2encoder
+    from gnnea.margin import margin_loss
+    from test_dropin_cpu import make_args
+    g = golden("graph_cfg1")
+    a = make_args(model)
+    a.cuda, a.device = 0, device
+    torch.manual_seed(10086)
+    enc = model2encoder[model](a).to(device)
+    dec = model2decoder[model](a).to(device)
+    idx = torch.from_numpy(np.stack([g["row"], g["col"]]).astype(np.int64))
+    adj = torch.sparse_coo_tensor(idx, torch.from_numpy(g["val"]), (2000, 2000)).to(device)
+    x = torch.from_numpy(g["X"]).to(device)
+    rng = np.random.default_rng(0)
+    t, k = 200, 5
+    left, right = rng.integers(0, 1000, t), rng.integers(1000, 2000, t)
+    negs = [rng.integers(0, 2000, t * k) for _ in range(4)]
+
+    def run(dtype):
+        e, d = enc.to(dtype), dec.to(dtype)
+        for m in (e, d):
+            for mod in m.modules():  # HighWay's plain-tensor gate weights follow the model
+                if hasattr(mod, "kernel_gate") and torch.is_tensor(mod.kernel_gate):
+                    mod.kernel_gate = mod.kernel_gate.to(dtype)
+        e.zero_grad()
+        d.zero_grad()
+        out = d.decode(e.encode(x.to(dtype), adj), adj)
+        loss = margin_loss(out, np.repeat(left, 1), right, np.repeat(left, k), negs[0],
+                           negs[1], np.repeat(right, k), t, k)
+        loss.backward()
+        grads = [p.grad.float().cpu().clone() for p in list(e.parameters()) + list(d.parameters())]
+        return out.detach().float().cpu(), float(loss), grads
+
+    out32, loss32, g32 = run(torch.float32)
+    outb, lossb, gb = run(torch.bfloat16)
+    assert rel_err(outb, out32) < 3 * TOL_BF16
+    assert abs(lossb - loss32) <= 3 * TOL_BF16 * abs(loss32)
+    # the margin loss's gradient is a sum of sign(u - v) terms: bf16 rounding of the embeddings
+    # flips the signs of near-zero differences, so the bf16 gradients are compared by direction
+    # (measured cosines 0.85-0.99); the last decoder bias has an analytically zero gradient (the
+    # loss depends on differences of rows only) and is skipped: both runs hold rounding noise
+    top = max(float(p.norm()) for p in g32)
+    for p16, p32 in zip(gb, g32):
+        assert torch.isfinite(p16).all()
+        if float(p32.norm()) < 1e-4 * top:
+            continue
+        cos = float(torch.nn.functional.cosine_similarity(p16.flatten().double(),
+                                                          p32.flatten().double(), dim=0))
+        assert cos > 0.8, cos
