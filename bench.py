@@ -3,8 +3,12 @@
 Workload (BASELINE.json configs[3] graph, the largest single-GPU configuration): the synthetic
 2 x 1M-entity / 2 x 10M-triple KG pair of SURVEY.md §8d (41,999,552 nnz incl. self loops),
 D = 300 fp32 features resident in HBM.  A step = one GCN aggregation pass Y = relu(A · H) over
-the whole graph (layers/layers.py:35-38) — on N > 1 GPUs the rows are sharded per KG group and
-the step includes the RCCL halo all-gather of H inside the group (gnnea/dist.py).
+the whole graph (layers/layers.py:35-38).  On N > 1 GPUs each KG group of N/2 ranks splits the
+feature columns (default, no exchange in the aggregation) or the rows (--partition rows, with
+the RCCL halo all-gather inside the step), gnnea/dist.py.
+
+Side measurement (`train_step`): the row-sharded HGCN-EA training step of configs[3] through
+the drop-in Encoder/Decoder modules with the RCCL halo exchange (tools/dist_step.py).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
@@ -145,6 +149,9 @@ def main():
     ap.add_argument("--partition", choices=("features", "rows"), default="features",
                     help="inside a KG group: feature-column slices (no exchange) or row blocks "
                          "with the RCCL halo all-gather")
+    ap.add_argument("--no-train", action="store_true",
+                    help="skip the side measurement of the row-sharded HGCN-EA training step")
+    ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank logic on ONE device with gloo (halo staged through host)")
     args = ap.parse_args()
@@ -219,6 +226,16 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_nnz / (elapsed / args.steps)
 
+    # side measurement (every rank, same collective sequence): the row-sharded HGCN-EA training
+    # step of BASELINE.json configs[3] through the drop-in modules with the RCCL halo exchange
+    train = None
+    if not args.no_train and not args.rehearse:
+        try:
+            from tools.dist_step import measure
+            train = measure("HGCN", n, rank, world, device, args.train_steps, 1)
+        except Exception as e:  # report, never hide
+            train = {"error": repr(e)}
+
     if rank == 0:
         # the SpMM is launched once per diagonal (KG) block of rows when the gathered matrix is
         # larger than the Infinity Cache (gnnea.ops._blocks): bytes and time per launch
@@ -252,6 +269,8 @@ def main():
                          "model": "gather: 4(N+1)+8E+4ED+4ND (rank 0 shard, D = its slice), "
                                   "split evenly over the per-KG launches"},
         }
+        if train is not None:
+            line["train_step"] = train
         if world == 1 and not args.no_sinkhorn:
             try:
                 line["sinkhorn"] = sinkhorn_rate(device)

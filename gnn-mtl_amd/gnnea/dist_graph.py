@@ -1,0 +1,257 @@
+"""Row-sharded adjacency that the drop-in GCN / HighWay layers accept in place of ``adj``
+(node-sharded HGCN-EA across the GPUs of one node with the halo all-gather).
+
+One process per GPU.  The two-KG adjacency is block-diagonal, so ranks [0, W/2) serve KG1 and
+[W/2, W) serve KG2 (gnnea.dist.Partition, kind "rows"); inside a KG group of g ranks, rank l
+owns the n/g destination rows [l·n/g, (l+1)·n/g) of its KG, and the layers run on those rows
+only.  Per graph layer (layers/layers.py:30-39, 58-77):
+
+  forward   hidden_loc = x_loc·Wᵀ + b                local MFMA GEMM (unchanged drop-in code)
+            hidden_KG  = all_gather(hidden_loc)       RCCL, inside the KG group, overlapped with
+            out_loc    = act(A_own·hidden_loc           the SpMM over the locally owned columns
+                             + A_remote·hidden_KG)
+  backward  G_loc      = dY_loc ⊙ act'(out_loc)
+            P          = A_shardᵀ · G_loc             [n, D]: this rank's share of every row
+            dhidden_loc= reduce_scatter(P)            RCCL, inside the KG group
+            dW, db     = local GEMMs; summed over ALL ranks by allreduce_grads() (one bucket)
+
+The HighWay gate (x_loc·K_g, the blend with x_loc) is row-local.  ``gather_rows`` assembles the
+final embeddings of both KGs on every rank (all_gather over the world) for the EA loss, which
+every rank then evaluates identically; its backward keeps the rank's own rows of the gradient.
+
+The engine (the SpMM / elementwise kernels) is the HIP library; tests substitute a CPU double
+only to check the collective logic with gloo (tests/test_dist_gloo.py).  gloo cannot move
+device tensors: under gloo the exchanges are staged through host memory (the 1-GPU rehearsal).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .dist import Partition, make_groups, shard_coo, split_own_remote
+
+
+class HipEngine:
+    """The product engine: libgnnea kernels through gnnea.ops (device tensors only)."""
+
+    def csr(self, r, c, v, n_rows, n_cols, device):
+        from .graph import DeviceCSR
+        return DeviceCSR.from_coo(torch.from_numpy(np.ascontiguousarray(r, np.int32)).to(device),
+                                  torch.from_numpy(np.ascontiguousarray(c, np.int32)).to(device),
+                                  torch.from_numpy(np.ascontiguousarray(v, np.float32)).to(device),
+                                  n_rows, n_cols)
+
+    def spmm(self, csr, x, act, out=None, beta=0.0):
+        from . import ops
+        return ops.spmm(csr, x, act, out=out, beta=beta)
+
+    def spmm_t(self, csr, x):
+        from . import ops
+        return ops.spmm(csr.transpose(), x)
+
+    def act_bwd(self, dy, y, act):
+        from . import ops
+        return ops.act_bwd(dy, y, act)
+
+    def highway_fwd(self, csr, hidden, gate_pre, resid, bias_gate, act):
+        from . import ops
+        return ops.highway_fwd(csr, hidden, gate_pre, resid, bias_gate, act)
+
+    def highway_bwd(self, dy, S, G, resid, act, want_dresid):
+        from . import ops
+        return ops.highway_bwd(dy, S, G, resid, act, want_dresid)
+
+
+def _is_gloo(group):
+    return dist.get_backend(group) == "gloo"
+
+
+class DistAdj:
+    """This rank's shard of the two-KG adjacency plus its KG group.
+
+    Build it on every rank (group creation is collective) with ``from_triples`` (the synthetic
+    cfg graphs) or from the rank's COO shard (local rows, KG-local columns), then pass it as the
+    ``adj`` of GraphConvolution / HighWayGraphConvolution / Encoder.encode / Decoder.decode with
+    the rank's own feature rows ``x[part.global_row0 : part.global_row0 + part.n_rows]``."""
+
+    def __init__(self, part, r, c, v, device, engine=None):
+        if part.world > 1 and part.kind != "rows":
+            raise ValueError("gnnea.DistAdj: the layers need the row partition")
+        self.part = part
+        self.device = device
+        self.engine = engine or HipEngine()
+        e = self.engine
+        self.nnz = int(np.asarray(r).size)
+        self.csr = e.csr(r, c, v, part.n_rows, part.n_cols, device)
+        if part.g > 1:
+            (ro, co, vo), (rr, cr, vr) = split_own_remote(r, c, v, part)
+            self.csr_own = e.csr(ro, co, vo, part.n_rows, part.n_rows, device)
+            self.csr_remote = e.csr(rr, cr, vr, part.n_rows, part.n_cols, device)
+        else:
+            self.csr_own = self.csr_remote = None
+        self.group = make_groups(part) if part.world > 1 else None
+
+    @classmethod
+    def from_triples(cls, triples, n, t, rank, world, device, engine=None):
+        """Shard of the synthetic cfg pair (gnnea.synth.kg_pair_triples layout: KG k's t triples
+        at rows [k·t, (k+1)·t), entities [k·n, (k+1)·n))."""
+        part = Partition(n, rank, world, "rows")
+        r, c, v = shard_coo(triples, n, t, part)
+        return cls(part, r, c, v, device, engine)
+
+    # ---- the drop-in layer hooks ------------------------------------------------------------
+    def aggregate(self, hidden, act_fn):
+        from .ops import act_code
+        code = act_code(act_fn) if act_fn is not None else _lib.GNNEA_ACT_IDENTITY
+        if code is None:
+            return act_fn(HaloAggregateFn.apply(hidden, self, _lib.GNNEA_ACT_IDENTITY))
+        return HaloAggregateFn.apply(hidden, self, code)
+
+    def highway(self, hidden, gate_pre, resid, bias_gate, act_fn):
+        from .ops import act_code
+        code = act_code(act_fn)
+        if code is None:
+            s = act_fn(HaloAggregateFn.apply(hidden, self, _lib.GNNEA_ACT_IDENTITY))
+            g = torch.sigmoid(gate_pre + bias_gate) if bias_gate is not None else \
+                torch.sigmoid(gate_pre)
+            return g * s + (1.0 - g) * resid
+        return HaloHighwayFn.apply(hidden, gate_pre, resid, bias_gate, self, code)
+
+    def gather_rows(self, out_loc):
+        """[2n, D] embeddings of both KGs in global entity order, on every rank."""
+        return GatherRowsFn.apply(out_loc, self)
+
+    # ---- exchanges ------------------------------------------------------------------------
+    def halo(self, h_loc, async_op=False):
+        """All-gather the KG group's rows: returns (h_KG [n, D], work or None)."""
+        g = self.part.g
+        if g == 1:
+            return h_loc, None
+        h_loc = h_loc.contiguous()
+        if _is_gloo(self.group):
+            hl = h_loc.detach().cpu()
+            parts = [torch.empty_like(hl) for _ in range(g)]
+            dist.all_gather(parts, hl, group=self.group)
+            return torch.cat(parts).to(h_loc.device), None
+        full = torch.empty((g * h_loc.shape[0], h_loc.shape[1]), dtype=h_loc.dtype,
+                           device=h_loc.device)
+        work = dist.all_gather_into_tensor(full, h_loc, group=self.group, async_op=async_op)
+        return full, work
+
+    def reduce_scatter(self, partial):
+        """Sum the group's [n, D] partials and keep this rank's n/g rows."""
+        g = self.part.g
+        if g == 1:
+            return partial
+        partial = partial.contiguous()
+        rows = self.part.n_rows
+        li = self.part.li
+        if _is_gloo(self.group):  # gloo has no reduce_scatter: all_reduce then slice
+            p = partial.detach().cpu()
+            dist.all_reduce(p, group=self.group)
+            return p[li * rows:(li + 1) * rows].to(partial.device)
+        out = torch.empty((rows, partial.shape[1]), dtype=partial.dtype, device=partial.device)
+        dist.reduce_scatter_tensor(out, partial, group=self.group)
+        return out
+
+    def all_rows(self, out_loc):
+        W = self.part.world
+        if W == 1:
+            return out_loc
+        out_loc = out_loc.contiguous()
+        if dist.get_backend() == "gloo":
+            hl = out_loc.detach().cpu()
+            parts = [torch.empty_like(hl) for _ in range(W)]
+            dist.all_gather(parts, hl)
+            return torch.cat(parts).to(out_loc.device)
+        full = torch.empty((W * out_loc.shape[0], out_loc.shape[1]), dtype=out_loc.dtype,
+                           device=out_loc.device)
+        dist.all_gather_into_tensor(full, out_loc)
+        return full
+
+
+class HaloAggregateFn(torch.autograd.Function):
+    """out_loc = act(A_shard · all_gather(hidden_loc)); backward reduce_scatter(A_shardᵀ · G)."""
+
+    @staticmethod
+    def forward(ctx, hidden, dadj, act):
+        e = dadj.engine
+        if dadj.part.g == 1:
+            out = e.spmm(dadj.csr, hidden, act)
+        else:
+            full, work = dadj.halo(hidden, async_op=True)
+            out = e.spmm(dadj.csr_own, hidden, _lib.GNNEA_ACT_IDENTITY)  # overlaps the gather
+            if work is not None:
+                work.wait()
+            e.spmm(dadj.csr_remote, full, act, out=out, beta=1.0)
+        ctx.dadj, ctx.act = dadj, act
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        (out,) = ctx.saved_tensors
+        dadj = ctx.dadj
+        e = dadj.engine
+        g = dy.contiguous() if ctx.act == _lib.GNNEA_ACT_IDENTITY else \
+            e.act_bwd(dy.contiguous(), out, ctx.act)
+        return dadj.reduce_scatter(e.spmm_t(dadj.csr, g)), None, None
+
+
+class HaloHighwayFn(torch.autograd.Function):
+    """HighWay tail on the shard: S = act(A_shard·hidden_KG); g = sigmoid(gate_pre + b_g);
+    out = g*S + (1-g)*resid (gate_pre, resid row-local)."""
+
+    @staticmethod
+    def forward(ctx, hidden, gate_pre, resid, bias_gate, dadj, act):
+        full, _ = dadj.halo(hidden)
+        out, S, G = dadj.engine.highway_fwd(dadj.csr, full, gate_pre, resid, bias_gate, act)
+        ctx.dadj, ctx.act = dadj, act
+        ctx.save_for_backward(S, G, resid)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        S, G, resid = ctx.saved_tensors
+        dadj = ctx.dadj
+        e = dadj.engine
+        dS, dgate, dres = e.highway_bwd(dy.contiguous(), S, G, resid, ctx.act,
+                                        ctx.needs_input_grad[2])
+        dh = dadj.reduce_scatter(e.spmm_t(dadj.csr, dS))
+        return dh, dgate, dres, None, None, None
+
+
+class GatherRowsFn(torch.autograd.Function):
+    """All ranks' rows in global order.  The loss on top is evaluated identically on every
+    rank, so d loss / d out_loc is this rank's slice of the (replicated) gradient."""
+
+    @staticmethod
+    def forward(ctx, out_loc, dadj):
+        ctx.rows = out_loc.shape[0]
+        ctx.rank = dadj.part.rank
+        return dadj.all_rows(out_loc)
+
+    @staticmethod
+    def backward(ctx, dfull):
+        r0 = ctx.rank * ctx.rows
+        return dfull[r0:r0 + ctx.rows].contiguous(), None
+
+
+def allreduce_grads(params, group=None):
+    """Sum the parameter gradients of all ranks in ONE bucket (the weights are replicated and
+    small: 3 x 300 x 300 fp32 for HGCN-EA, so one RCCL all_reduce of < 1.1 MB per step)."""
+    ps = [p for p in params if p.grad is not None]
+    if not ps or dist.get_world_size(group) == 1:
+        return
+    flat = torch.cat([p.grad.reshape(-1) for p in ps])
+    if dist.get_backend(group) == "gloo" and flat.device.type != "cpu":
+        h = flat.cpu()
+        dist.all_reduce(h, group=group)
+        flat = h.to(flat.device)
+    else:
+        dist.all_reduce(flat, group=group)
+    k = 0
+    for p in ps:
+        m = p.grad.numel()
+        p.grad.copy_(flat[k:k + m].view_as(p.grad))
+        k += m

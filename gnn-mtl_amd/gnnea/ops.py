@@ -292,30 +292,58 @@ def aggregate(adj, hidden, act_fn=None):
     return AggregateFn.apply(hidden, csr, code)
 
 
+def highway_fwd(csr, hidden, gate_pre, resid, bias_gate, act):
+    """S = act(A·hidden); g = sigmoid(gate_pre + bias_gate); out = g*S + (1-g)*resid in one
+    kernel (gnnea_spmm_highway_*), per diagonal block.  ``hidden`` has csr.n_cols rows, the
+    others csr.n_rows.  Returns (out, S, g)."""
+    hidden = _featc(hidden)
+    gate_pre = _featc(gate_pre, hidden.dtype)
+    resid = _featc(resid, hidden.dtype)
+    N, D = csr.n_rows, hidden.shape[1]
+    if hidden.shape[0] < csr.n_cols or gate_pre.shape != (N, D) or resid.shape != (N, D):
+        raise ValueError("gnnea.highway: shape mismatch")
+    out = torch.empty((N, D), dtype=hidden.dtype, device=hidden.device)
+    S = torch.empty_like(out)
+    G = torch.empty_like(out)
+    bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
+    fn = _lib.lib().gnnea_spmm_highway_bf16 if hidden.dtype == torch.bfloat16 else \
+        _lib.lib().gnnea_spmm_highway_f32
+    with torch.cuda.device(hidden.device):
+        for r0, r1 in _blocks(csr, hidden):
+            check(fn(
+                ctypes.c_void_p(csr.rowptr.data_ptr() + 4 * r0), ptr(csr.col), ptr(csr.val),
+                r1 - r0, D, ptr(hidden), hidden.stride(0), _off(gate_pre, r0),
+                gate_pre.stride(0), ptr(bias), _off(resid, r0), resid.stride(0),
+                _off(out, r0), out.stride(0), _off(S, r0), _off(G, r0), S.stride(0),
+                int(act), stream_of(hidden.device)))
+    return out, S, G
+
+
+def highway_bwd(dy, S, G, resid, act, want_dresid=True):
+    """Elementwise HighWay backward (gnnea_highway_bwd_*): returns (dS_pre, dgate, dresid)
+    with dS_pre = dy*g*act'(S) (to be aggregated by A^T), dgate = dy*(S-x)*g*(1-g),
+    dresid = dy*(1-g) (None unless wanted)."""
+    dy = _featc(dy, S.dtype)
+    dS = torch.empty_like(S)
+    dgate = torch.empty_like(S)
+    dres = torch.empty_like(S) if want_dresid else None
+    fn = _lib.lib().gnnea_highway_bwd_bf16 if S.dtype == torch.bfloat16 else \
+        _lib.lib().gnnea_highway_bwd_f32
+    with torch.cuda.device(S.device):
+        check(fn(
+            ptr(dy), ptr(S), ptr(G), ptr(resid), S.stride(0), S.shape[0], S.shape[1],
+            ptr(dS), ptr(dgate), ptr(dres), int(act), stream_of(S.device)))
+    return dS, dgate, dres
+
+
 class HighwayFn(torch.autograd.Function):
     """HighWay GCN tail (layers/layers.py:64-76) in one kernel:
     S = act(A·hidden); g = sigmoid(gate_pre + bias_gate); out = g*S + (1-g)*resid."""
 
     @staticmethod
     def forward(ctx, hidden, gate_pre, resid, bias_gate, csr, act):
-        hidden = _featc(hidden)
-        gate_pre = _featc(gate_pre, hidden.dtype)
-        resid = _featc(resid, hidden.dtype)
-        N, D = csr.n_rows, hidden.shape[1]
-        out = torch.empty((N, D), dtype=hidden.dtype, device=hidden.device)
-        S = torch.empty_like(out)
-        G = torch.empty_like(out)
-        bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
-        fn = _lib.lib().gnnea_spmm_highway_bf16 if hidden.dtype == torch.bfloat16 else \
-            _lib.lib().gnnea_spmm_highway_f32
-        with torch.cuda.device(hidden.device):
-            for r0, r1 in _blocks(csr, hidden):
-                check(fn(
-                    ctypes.c_void_p(csr.rowptr.data_ptr() + 4 * r0), ptr(csr.col), ptr(csr.val),
-                    r1 - r0, D, ptr(hidden), hidden.stride(0), _off(gate_pre, r0),
-                    gate_pre.stride(0), ptr(bias), _off(resid, r0), resid.stride(0),
-                    _off(out, r0), out.stride(0), _off(S, r0), _off(G, r0), S.stride(0),
-                    int(act), stream_of(hidden.device)))
+        resid = _featc(resid, _featc(hidden).dtype)
+        out, S, G = highway_fwd(csr, hidden, gate_pre, resid, bias_gate, act)
         ctx.csr = csr
         ctx.act = act
         ctx.save_for_backward(S, G, resid)
@@ -324,16 +352,7 @@ class HighwayFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         S, G, resid = ctx.saved_tensors
-        dy = _featc(dy, S.dtype)
-        dS = torch.empty_like(S)
-        dgate = torch.empty_like(S)
-        dres = torch.empty_like(S) if ctx.needs_input_grad[2] else None
-        fn = _lib.lib().gnnea_highway_bwd_bf16 if S.dtype == torch.bfloat16 else \
-            _lib.lib().gnnea_highway_bwd_f32
-        with torch.cuda.device(S.device):
-            check(fn(
-                ptr(dy), ptr(S), ptr(G), ptr(resid), S.stride(0), S.shape[0], S.shape[1],
-                ptr(dS), ptr(dgate), ptr(dres), int(ctx.act), stream_of(S.device)))
+        dS, dgate, dres = highway_bwd(dy, S, G, resid, ctx.act, ctx.needs_input_grad[2])
         dh = spmm(ctx.csr.transpose(), dS)
         return dh, dgate, dres, None, None, None
 

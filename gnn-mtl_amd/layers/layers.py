@@ -6,6 +6,8 @@ Constructor signatures, parameter creation order (hence RNG consumption under
   hidden = x W^T + b          -> MFMA f32 GEMM   (gnnea_gemm_f32)
   act(A · hidden)             -> CSR gather SpMM with fused activation (gnnea_spmm_csr_f32)
   HighWay gate + blend        -> SpMM with fused sigmoid-gate epilogue (gnnea_spmm_highway_f32)
+Handed a ``gnnea.dist_graph.DistAdj`` instead of the sparse adjacency (and the rank's own rows
+of x), the same layers run row-sharded across GPUs with the RCCL halo exchange.
 """
 import numpy as np
 import torch
@@ -14,6 +16,7 @@ import torch.nn.functional as F
 from torch.nn.modules.module import Module
 
 from gnnea import ops
+from gnnea.dist_graph import DistAdj
 from gnnea.graph import dense_of
 
 
@@ -25,6 +28,8 @@ def get_dim_act(args):
 
 
 def _propagate(adj, hidden, act):
+    if isinstance(adj, DistAdj):  # row shard of a multi-GPU run (gnnea/dist_graph.py)
+        return adj.aggregate(hidden, act)
     if adj.is_sparse:
         return ops.aggregate(adj, hidden, act)
     return act(ops.matmul(adj, hidden))  # dense adjacency: torch.mm branch (:37)
@@ -76,7 +81,9 @@ class HighWayGraphConvolution(GraphConvolution):
         x = dense_of(x)
         hidden = self._hidden(x)
         gate_pre = ops.matmul(x, self.kernel_gate)
-        if adj.is_sparse:
+        if isinstance(adj, DistAdj):
+            out = adj.highway(hidden, gate_pre, x, self.bias_gate, self.act)
+        elif adj.is_sparse:
             out = ops.highway(adj, hidden, gate_pre, x, self.bias_gate, self.act)
         else:
             s = self.act(ops.matmul(adj, hidden))

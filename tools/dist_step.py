@@ -1,0 +1,117 @@
+"""Row-sharded EA encoder training step (BASELINE.json configs[3]: HGCN-EA on the 2 x 1M-entity
+synthetic KG pair, node-sharded with the RCCL halo exchange).
+
+    python tools/dist_step.py [--model HGCN|GCN] [--steps 10] [--warmup 2] [--entities 1000000]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/dist_step.py
+
+A step = the drop-in Encoder.encode + Decoder.decode (models/encoders.py, models/decoders.py;
+HGCN: three HighWay graph convolutions, GCN: two graph convolutions + the GCN decoder) forward
+on this rank's rows with a DistAdj, backward from a fixed upstream gradient on the rank's rows
+(the EA loss is row-local once the embeddings are gathered; the gather is not timed here), and
+the one-bucket RCCL all-reduce of the weight gradients.  Prints one JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+import types
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gnn-mtl_amd"))
+
+from gnnea import synth  # noqa: E402
+from gnnea.dist_graph import DistAdj, allreduce_grads  # noqa: E402
+
+
+def build(model, n, rank, world, device, seed=10086):
+    from models.decoders import model2decoder
+    from models.encoders import model2encoder
+    a = types.SimpleNamespace(model=model, num_layers=3, dim=300, act="relu", dropout=0.0,
+                              bias=1, n_heads=4, alpha=0.2, feat_dim=300, n_classes=300,
+                              cuda=0, device=device)
+    torch.manual_seed(seed)  # replicated weights on every rank (run/train_ea.py:10)
+    enc = model2encoder[model](a).to(device)
+    dec = model2decoder[model](a).to(device)
+    t = synth.CONFIGS["cfg4"]["t"] if n == synth.CONFIGS["cfg4"]["n"] else 10 * n
+    tr = synth.kg_pair_triples(n, t, synth.CONFIGS["cfg4"]["n_rel"])
+    dadj = DistAdj.from_triples(tr, n, t, rank, world, device)
+    return enc, dec, dadj
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="HGCN", choices=("HGCN", "GCN"))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--entities", type=int, default=synth.CONFIGS["cfg4"]["n"])
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    res = measure(args.model, args.entities, rank, world, dev, args.steps, args.warmup)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def measure(model, n, rank, world, dev, steps, warmup):
+    """Time `steps` sharded training steps (after `warmup`), max over ranks; returns the summary
+    (the same dict on every rank).  Every rank runs the same collective sequence."""
+    t0 = time.time()
+    enc, dec, dadj = build(model, n, rank, world, dev)
+    part = dadj.part
+    g = torch.Generator(device=dev).manual_seed(1 + rank)
+    x = torch.randn(part.n_rows, 300, device=dev, generator=g)
+    x /= x.norm(dim=1, keepdim=True)
+    dy = torch.randn(part.n_rows, 300, device=dev, generator=g)
+    params = list(enc.parameters()) + list(dec.parameters())
+    print("rank %d: %d rows, %d nnz, setup %.1fs" % (rank, part.n_rows, dadj.nnz,
+                                                     time.time() - t0), file=sys.stderr)
+
+    def step():
+        for p in params:
+            p.grad = None
+        out = dec.decode(enc.encode(x, dadj), dadj)
+        out.backward(dy)
+        if world > 1:
+            allreduce_grads(params)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    ms = float(el) / steps * 1e3
+    cfg4 = n == synth.CONFIGS["cfg4"]["n"]
+    return {"metric": "EA encoder training steps/s", "model": model + "-EA (encode + decode, "
+            "3 graph convolutions, fwd + bwd + gradient all-reduce)",
+            "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 3),
+            "steps_per_s": round(1e3 / ms, 2),
+            # 3 aggregations forward + 3 transposed aggregations backward per step
+            "edges_per_s_fwd_bwd": round(6 * 41999552 / ms * 1e3, 1) if cfg4 else None,
+            "partition": "single GPU" if world == 1 else
+            "rows: 2 KG groups of %d GPUs, RCCL halo all-gather (fwd) + reduce-scatter (bwd) "
+            "per layer, one-bucket gradient all-reduce" % part.g}
+
+
+if __name__ == "__main__":
+    main()
