@@ -268,8 +268,9 @@ __global__ void k_act_bwd(const T* __restrict__ dY, const T* __restrict__ Y, T* 
 template <int ACT, typename T>
 __global__ void k_highway_bwd(const T* __restrict__ dY, const T* __restrict__ S,
                               const T* __restrict__ Gt, const T* __restrict__ R, int64_t ld,
-                              int64_t n_rows, int D, T* __restrict__ dS_pre,
-                              T* __restrict__ dgate, T* __restrict__ dresid) {
+                              int64_t n_rows, int D, T* __restrict__ dS_pre, int64_t ld_ds,
+                              T* __restrict__ dgate, int64_t ld_dg, T* __restrict__ dresid,
+                              int64_t ld_dr) {
   const int64_t n = n_rows * (int64_t)D;
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -278,9 +279,9 @@ __global__ void k_highway_bwd(const T* __restrict__ dY, const T* __restrict__ S,
     const int64_t i = r * ld + c;
     const float dy = to_f32<T>(dY[i]), s = to_f32<T>(S[i]), g = to_f32<T>(Gt[i]);
     const float x = to_f32<T>(R[i]);
-    dS_pre[i] = from_f32<T>(dy * g * act_grad_from_out<ACT>(s));
-    dgate[i] = from_f32<T>(dy * (s - x) * g * (1.f - g));
-    if (dresid) dresid[i] = from_f32<T>(dy * (1.f - g));
+    dS_pre[r * ld_ds + c] = from_f32<T>(dy * g * act_grad_from_out<ACT>(s));
+    dgate[r * ld_dg + c] = from_f32<T>(dy * (s - x) * g * (1.f - g));
+    if (dresid) dresid[r * ld_dr + c] = from_f32<T>(dy * (1.f - g));
   }
 }
 
@@ -307,16 +308,17 @@ static int act_bwd_t(const T* dY, const T* Y, T* G, int64_t n, int act, hipStrea
 
 template <typename T>
 static int highway_bwd_t(const T* dY, const T* S, const T* G, const T* resid, int64_t ld,
-                         int64_t n_rows, int32_t D, T* dS_pre, T* dgate, T* dresid, int act,
-                         hipStream_t s) {
-  if (n_rows < 0 || D < 0 || ld < D) return GNNEA_EINVAL;
+                         int64_t n_rows, int32_t D, T* dS_pre, int64_t ld_ds, T* dgate,
+                         int64_t ld_dg, T* dresid, int64_t ld_dr, int act, hipStream_t s) {
+  if (n_rows < 0 || D < 0 || ld < D || ld_ds < D || ld_dg < D || (dresid && ld_dr < D))
+    return GNNEA_EINVAL;
   if (n_rows == 0 || D == 0) return 0;
   if (!dY || !S || !G || !resid || !dS_pre || !dgate) return GNNEA_EINVAL;
   const int64_t n = n_rows * (int64_t)D;
   const int nb = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
 #define GNNEA_HWB(A)                                                                         \
   hipLaunchKernelGGL((k_highway_bwd<A, T>), dim3(nb), dim3(256), 0, s, dY, S, G, resid, ld,  \
-                     n_rows, D, dS_pre, dgate, dresid)
+                     n_rows, D, dS_pre, ld_ds, dgate, ld_dg, dresid, ld_dr)
   switch (act) {
     case GNNEA_ACT_IDENTITY: GNNEA_HWB(GNNEA_ACT_IDENTITY); break;
     case GNNEA_ACT_RELU: GNNEA_HWB(GNNEA_ACT_RELU); break;
@@ -383,8 +385,16 @@ extern "C" int gnnea_highway_bwd_f32(const float* dY, const float* S, const floa
                                      const float* resid, int64_t ld, int64_t n_rows, int32_t D,
                                      float* dS_pre, float* dgate, float* dresid, int act,
                                      void* stream) {
-  return highway_bwd_t<float>(dY, S, G, resid, ld, n_rows, D, dS_pre, dgate, dresid, act,
-                              (hipStream_t)stream);
+  return highway_bwd_t<float>(dY, S, G, resid, ld, n_rows, D, dS_pre, ld, dgate, ld, dresid, ld,
+                              act, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_highway_bwd_ld_f32(const float* dY, const float* S, const float* G,
+                                        const float* resid, int64_t ld, int64_t n_rows, int32_t D,
+                                        float* dS_pre, int64_t ld_ds, float* dgate, int64_t ld_dg,
+                                        float* dresid, int64_t ld_dr, int act, void* stream) {
+  return highway_bwd_t<float>(dY, S, G, resid, ld, n_rows, D, dS_pre, ld_ds, dgate, ld_dg,
+                              dresid, ld_dr, act, (hipStream_t)stream);
 }
 
 // ---- bf16 storage (cfg-5) ------------------------------------------------------------------
@@ -437,6 +447,17 @@ extern "C" int gnnea_highway_bwd_bf16(const void* dY, const void* S, const void*
                                       void* dS_pre, void* dgate, void* dresid, int act,
                                       void* stream) {
   return highway_bwd_t<bf16_t>((const bf16_t*)dY, (const bf16_t*)S, (const bf16_t*)G,
-                               (const bf16_t*)resid, ld, n_rows, D, (bf16_t*)dS_pre,
-                               (bf16_t*)dgate, (bf16_t*)dresid, act, (hipStream_t)stream);
+                               (const bf16_t*)resid, ld, n_rows, D, (bf16_t*)dS_pre, ld,
+                               (bf16_t*)dgate, ld, (bf16_t*)dresid, ld, act, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_highway_bwd_ld_bf16(const void* dY, const void* S, const void* G,
+                                         const void* resid, int64_t ld, int64_t n_rows,
+                                         int32_t D, void* dS_pre, int64_t ld_ds, void* dgate,
+                                         int64_t ld_dg, void* dresid, int64_t ld_dr, int act,
+                                         void* stream) {
+  return highway_bwd_t<bf16_t>((const bf16_t*)dY, (const bf16_t*)S, (const bf16_t*)G,
+                               (const bf16_t*)resid, ld, n_rows, D, (bf16_t*)dS_pre, ld_ds,
+                               (bf16_t*)dgate, ld_dg, (bf16_t*)dresid, ld_dr, act,
+                               (hipStream_t)stream);
 }

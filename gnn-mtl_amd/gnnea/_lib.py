@@ -75,6 +75,8 @@ SIGNATURES = {
     "gnnea_spmm_highway_f32": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64, _p, _p,
                                               _i64, _p, _i64, _p, _p, _i64, ctypes.c_int, _p]),
     "gnnea_act_bwd_f32": (ctypes.c_int, [_p, _p, _p, _i64, ctypes.c_int, _p]),
+    "gnnea_highway_bwd_ld_f32": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i32, _p, _i64, _p,
+                                                 _i64, _p, _i64, ctypes.c_int, _p]),
     "gnnea_highway_bwd_f32": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p,
                                              ctypes.c_int, _p]),
     "gnnea_spmm_csr_bf16": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _f32, _p, _i64,
@@ -83,6 +85,8 @@ SIGNATURES = {
                                                _p, _i64, _p, _i64, _p, _p, _i64, ctypes.c_int,
                                                _p]),
     "gnnea_act_bwd_bf16": (ctypes.c_int, [_p, _p, _p, _i64, ctypes.c_int, _p]),
+    "gnnea_highway_bwd_ld_bf16": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i32, _p, _i64, _p,
+                                                  _i64, _p, _i64, ctypes.c_int, _p]),
     "gnnea_highway_bwd_bf16": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i32, _p, _p, _p,
                                               ctypes.c_int, _p]),
     "gnnea_gat_scores_f32": (ctypes.c_int, [_p, _i64, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,

@@ -45,9 +45,9 @@ class HipEngine:
         from . import ops
         return ops.spmm(csr, x, act, out=out, beta=beta)
 
-    def spmm_t(self, csr, x):
+    def spmm_t(self, csr, x, out=None):
         from . import ops
-        return ops.spmm(csr.transpose(), x)
+        return ops.spmm(csr.transpose(), x, out=out)
 
     def act_bwd(self, dy, y, act):
         from . import ops
@@ -116,6 +116,20 @@ class DistAdj:
                 torch.sigmoid(gate_pre)
             return g * s + (1.0 - g) * resid
         return HaloHighwayFn.apply(hidden, gate_pre, resid, bias_gate, self, code)
+
+    def highway_fwd(self, hidden, gate_pre, resid, bias_gate, act):
+        """HighWay tail over the shard (gnnea.ops.HighwayLayerFn's aggregation hook): the
+        group's hidden rows by the halo all-gather, gate_pre / resid row-local."""
+        full, _ = self.halo(hidden)
+        return self.engine.highway_fwd(self.csr, full, gate_pre, resid, bias_gate, act)
+
+    def aggregate_t(self, g, out):
+        """out = (A_shardᵀ·g) summed over the KG group, this rank's rows (HighwayLayerFn's
+        backward hook; out may be a column block of a wider buffer)."""
+        if self.part.g == 1:
+            return self.engine.spmm_t(self.csr, g, out=out)
+        out.copy_(self.reduce_scatter(self.engine.spmm_t(self.csr, g)))
+        return out
 
     def gather_rows(self, out_loc):
         """[2n, D] embeddings of both KGs in global entity order, on every rank."""

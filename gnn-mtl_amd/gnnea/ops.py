@@ -46,6 +46,18 @@ def _f32c(t):
 FEATURE_DTYPES = (torch.float32, torch.bfloat16)
 
 
+def _rows(t, dtype=None):
+    """Row-major matrix with unit column stride; a column block of a wider row-major buffer
+    (row stride > width) is passed through as is (the kernels take a leading dimension)."""
+    if dtype is not None and t.dtype != dtype:
+        t = t.to(dtype)
+    if t.dtype not in FEATURE_DTYPES:
+        raise TypeError("gnnea: fp32 or bf16 features required (got %s)" % t.dtype)
+    if t.dim() == 2 and t.stride(1) == 1 and (t.shape[0] <= 1 or t.stride(0) >= t.shape[1]):
+        return t
+    return t.contiguous()
+
+
 def _featc(t, dtype=None):
     """Contiguous feature matrix in fp32 or bf16 storage (converted to ``dtype`` when given)."""
     if dtype is not None and t.dtype != dtype:
@@ -98,8 +110,10 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
         if trans_a and a.numel() <= _SMALL_OPERAND:
             a, trans_a = a.t().contiguous(), False
     else:
-        a = _f32c(a)
-        b = _f32c(b)
+        if a.dtype != torch.float32 or b.dtype != torch.float32:
+            raise TypeError("gnnea: fp32 tensors required (got %s, %s)" % (a.dtype, b.dtype))
+        a = _rows(a)
+        b = _rows(b)
     M = a.shape[1] if trans_a else a.shape[0]
     K = a.shape[0] if trans_a else a.shape[1]
     Kb = b.shape[1] if trans_b else b.shape[0]
@@ -296,9 +310,9 @@ def highway_fwd(csr, hidden, gate_pre, resid, bias_gate, act):
     """S = act(A·hidden); g = sigmoid(gate_pre + bias_gate); out = g*S + (1-g)*resid in one
     kernel (gnnea_spmm_highway_*), per diagonal block.  ``hidden`` has csr.n_cols rows, the
     others csr.n_rows.  Returns (out, S, g)."""
-    hidden = _featc(hidden)
-    gate_pre = _featc(gate_pre, hidden.dtype)
-    resid = _featc(resid, hidden.dtype)
+    hidden = _rows(hidden)
+    gate_pre = _rows(gate_pre, hidden.dtype)
+    resid = _rows(resid, hidden.dtype)
     N, D = csr.n_rows, hidden.shape[1]
     if hidden.shape[0] < csr.n_cols or gate_pre.shape != (N, D) or resid.shape != (N, D):
         raise ValueError("gnnea.highway: shape mismatch")
@@ -319,21 +333,31 @@ def highway_fwd(csr, hidden, gate_pre, resid, bias_gate, act):
     return out, S, G
 
 
-def highway_bwd(dy, S, G, resid, act, want_dresid=True):
-    """Elementwise HighWay backward (gnnea_highway_bwd_*): returns (dS_pre, dgate, dresid)
+def highway_bwd(dy, S, G, resid, act, want_dresid=True, dS=None, dgate=None, dresid=None):
+    """Elementwise HighWay backward (gnnea_highway_bwd_ld_*): returns (dS_pre, dgate, dresid)
     with dS_pre = dy*g*act'(S) (to be aggregated by A^T), dgate = dy*(S-x)*g*(1-g),
-    dresid = dy*(1-g) (None unless wanted)."""
+    dresid = dy*(1-g) (None unless wanted).  dy, S, G, resid share one row stride; the outputs
+    may be caller-provided column blocks of wider buffers."""
+    S = _featc(S)
     dy = _featc(dy, S.dtype)
-    dS = torch.empty_like(S)
-    dgate = torch.empty_like(S)
-    dres = torch.empty_like(S) if want_dresid else None
-    fn = _lib.lib().gnnea_highway_bwd_bf16 if S.dtype == torch.bfloat16 else \
-        _lib.lib().gnnea_highway_bwd_f32
+    G = _featc(G, S.dtype)
+    resid = _featc(resid, S.dtype)
+    dS = torch.empty_like(S) if dS is None else dS
+    dgate = torch.empty_like(S) if dgate is None else dgate
+    if want_dresid and dresid is None:
+        dresid = torch.empty_like(S)
+    for t in (dS, dgate) + ((dresid,) if want_dresid else ()):
+        if t.shape != S.shape or t.dtype != S.dtype or t.stride(1) != 1:
+            raise ValueError("gnnea.highway_bwd: output block shape / dtype mismatch")
+    fn = _lib.lib().gnnea_highway_bwd_ld_bf16 if S.dtype == torch.bfloat16 else \
+        _lib.lib().gnnea_highway_bwd_ld_f32
+    N, D = S.shape
     with torch.cuda.device(S.device):
         check(fn(
-            ptr(dy), ptr(S), ptr(G), ptr(resid), S.stride(0), S.shape[0], S.shape[1],
-            ptr(dS), ptr(dgate), ptr(dres), int(act), stream_of(S.device)))
-    return dS, dgate, dres
+            ptr(dy), ptr(S), ptr(G), ptr(resid), S.stride(0), N, D, ptr(dS), _ld(dS),
+            ptr(dgate), _ld(dgate), ptr(dresid if want_dresid else None),
+            _ld(dresid) if want_dresid else D, int(act), stream_of(S.device)))
+    return dS, dgate, (dresid if want_dresid else None)
 
 
 class HighwayFn(torch.autograd.Function):
@@ -355,6 +379,81 @@ class HighwayFn(torch.autograd.Function):
         dS, dgate, dres = highway_bwd(dy, S, G, resid, ctx.act, ctx.needs_input_grad[2])
         dh = spmm(ctx.csr.transpose(), dS)
         return dh, dgate, dres, None, None, None
+
+
+def colsum(t):
+    """Column sums of a row-major [N, D] matrix (the bias gradient), as a [1,N]·[N,D] GEMM."""
+    ones = torch.ones((1, t.shape[0]), dtype=t.dtype, device=t.device)
+    return gemm(ones, t).view(-1)
+
+
+class HighwayLayerFn(torch.autograd.Function):
+    """A whole HighWay graph convolution (layers/layers.py:58-77, dropout inactive), fp32:
+
+      forward   Z = x·[Wᵀ | K_g] + [b | 0]        ONE MFMA pass over x (hidden | gate_pre)
+                out, S, g = highway(A, Z[:, :D], Z[:, D:], x, b_g)      (gnnea_spmm_highway)
+      backward  dS, [dh | dgate], dres = highway_bwd(...)   dgate written next to dh
+                dh = Aᵀ·dS                                   into the same [N, 2D] buffer
+                dx = dres + [dh | dgate]·[W ; K_gᵀ]           ONE GEMM accumulating into dres
+                dW = dhᵀ·x,  db = colsum(dh)
+    which replaces two forward GEMMs, two input-gradient GEMMs and the two autograd additions
+    of the three uses of x with one GEMM each way."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, kernel_gate, bias_gate, agg, act):
+        D = weight.shape[0]
+        wcat = torch.cat([weight.t(), kernel_gate.to(weight.dtype)], dim=1)  # [Din, 2D]
+        bcat = torch.cat([bias, torch.zeros_like(bias)]) if bias is not None else None
+        Z = gemm(x, wcat, bias=bcat)
+        out, S, G = agg.highway_fwd(Z[:, :D], Z[:, D:], x, bias_gate, act)
+        ctx.agg, ctx.act = agg, act
+        ctx.save_for_backward(x, weight, kernel_gate, S, G)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, Kg, S, G = ctx.saved_tensors
+        N, D = S.shape
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        P = torch.empty((N, 2 * D), dtype=S.dtype, device=S.device)
+        dS, _, dres = highway_bwd(dy, S, G, x, ctx.act, want_dresid=need_x, dgate=P[:, D:])
+        ctx.agg.aggregate_t(dS, P[:, :D])
+        dh = P[:, :D]
+        dx = dw = db = None
+        if need_x:
+            w2 = torch.cat([weight, Kg.t().to(weight.dtype)], dim=0)  # [2D, Din]
+            dx = gemm(P, w2, out=dres, beta=1.0)
+        if need_w:
+            dw = gemm(dh, x, trans_a=True)
+        if need_b:
+            db = colsum(dh)
+        return dx, dw, db, None, None, None, None
+
+
+class LocalAgg:
+    """The aggregation of one whole adjacency on this device (the sharded counterpart with the
+    same two methods is gnnea.dist_graph.DistAdj)."""
+
+    def __init__(self, csr):
+        self.csr = csr
+
+    def highway_fwd(self, hidden, gate_pre, resid, bias_gate, act):
+        return highway_fwd(self.csr, hidden, gate_pre, resid, bias_gate, act)
+
+    def aggregate_t(self, g, out):
+        """out = Aᵀ·g (out may be a column block of a wider buffer)."""
+        return spmm(self.csr.transpose(), g, out=out)
+
+
+def highway_layer(adj, x, weight, bias, kernel_gate, bias_gate, act_fn):
+    """Fused HighWay layer when it applies (fp32, fusable act), else None.  ``adj``: the
+    reference's sparse adjacency or a DistAdj shard."""
+    code = act_code(act_fn)
+    if code is None or x.dtype != torch.float32 or weight.dtype != torch.float32 or \
+            x.shape[1] != weight.shape[1] or weight.shape[0] != x.shape[1]:
+        return None
+    agg = adj if hasattr(adj, "aggregate_t") else LocalAgg(csr_of(adj))
+    return HighwayLayerFn.apply(_rows(x), weight, bias, kernel_gate, bias_gate, agg, code)
 
 
 def highway(adj, hidden, gate_pre, resid, bias_gate, act_fn):

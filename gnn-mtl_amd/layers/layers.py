@@ -79,6 +79,12 @@ class HighWayGraphConvolution(GraphConvolution):
     def forward(self, input):
         x, adj = input
         x = dense_of(x)
+        if (isinstance(adj, DistAdj) or adj.is_sparse) and \
+                (self.dropout == 0 or not self.training):
+            out = ops.highway_layer(adj, x, self.linear.weight, self.linear.bias,
+                                    self.kernel_gate, self.bias_gate, self.act)
+            if out is not None:  # one GEMM each way (gnnea.ops.HighwayLayerFn)
+                return out, adj
         hidden = self._hidden(x)
         gate_pre = ops.matmul(x, self.kernel_gate)
         if isinstance(adj, DistAdj):

@@ -6,12 +6,19 @@ HGCN decodes with one more HighWay graph convolution (a third SpMM per forward).
 import torch.nn as nn
 import torch.nn.functional as F
 
+from gnnea import _lib, ops
+
 from layers.att_layers import GraphAttentionLayer
 from layers.layers import GraphConvolution, HighWayGraphConvolution, Linear
 
 
 def _identity(x):
     return x
+
+
+# the reference's identity act (models/decoders.py:26,45 ``lambda x: x``) is fused as the
+# kernels' identity epilogue rather than applied as a torch op after the aggregation
+ops.ACT_CODES[_identity] = _lib.GNNEA_ACT_IDENTITY
 
 
 class Decoder(nn.Module):

@@ -101,6 +101,13 @@ int gnnea_act_bwd_f32(const float* dY, const float* Y, float* G, int64_t n, int 
 int gnnea_highway_bwd_f32(const float* dY, const float* S, const float* G, const float* resid,
                           int64_t ld, int64_t n_rows, int32_t D, float* dS_pre, float* dgate,
                           float* dresid, int act, void* stream);
+/* the same with separate row strides for the outputs (dS_pre, dgate, dresid may be column
+ * blocks of wider buffers: the fused HighWay layer writes dgate next to d hidden so that one
+ * GEMM [dh | dgate]·[W ; K_gᵀ] gives the whole input gradient) */
+int gnnea_highway_bwd_ld_f32(const float* dY, const float* S, const float* G, const float* resid,
+                             int64_t ld, int64_t n_rows, int32_t D, float* dS_pre, int64_t ld_ds,
+                             float* dgate, int64_t ld_dg, float* dresid, int64_t ld_dr, int act,
+                             void* stream);
 
 /* bf16 feature storage (cfg-5; SURVEY.md §8b gnnea_spmm_csr_bf16): X, gate_pre, resid, dY, S, G
  * are bf16 (void*, 2-byte elements), CSR values and bias_gate stay fp32, every product and sum
@@ -119,6 +126,10 @@ int gnnea_act_bwd_bf16(const void* dY, const void* Y, void* G, int64_t n, int ac
 int gnnea_highway_bwd_bf16(const void* dY, const void* S, const void* G, const void* resid,
                            int64_t ld, int64_t n_rows, int32_t D, void* dS_pre, void* dgate,
                            void* dresid, int act, void* stream);
+int gnnea_highway_bwd_ld_bf16(const void* dY, const void* S, const void* G, const void* resid,
+                              int64_t ld, int64_t n_rows, int32_t D, void* dS_pre, int64_t ld_ds,
+                              void* dgate, int64_t ld_dg, void* dresid, int64_t ld_dr, int act,
+                              void* stream);
 
 /* ------------------------------------------------------------------------------------------ *
  * a5-a7. Sparse GAT, all heads per edge pass (layers/att_layers.py:29-61, 82-91).

@@ -27,7 +27,7 @@ def test_header_declares_the_hot_path():
                  "gnnea_l1_keys_f32", "gnnea_topk_rows_f32", "gnnea_l1_rank_f32",
                  "gnnea_l1_pairs_f32", "gnnea_margin_fwd_f32", "gnnea_margin_bwd_f32",
                  "gnnea_spmm_csr_bf16", "gnnea_spmm_highway_bf16", "gnnea_act_bwd_bf16",
-                 "gnnea_highway_bwd_bf16", "gnnea_gemm_bf16", "gnnea_gat_scores_bf16",
+                 "gnnea_highway_bwd_bf16", "gnnea_highway_bwd_ld_f32", "gnnea_highway_bwd_ld_bf16", "gnnea_gemm_bf16", "gnnea_gat_scores_bf16",
                  "gnnea_gat_fwd_bf16", "gnnea_gat_bwd_prep_bf16", "gnnea_gat_bwd_src_bf16",
                  "gnnea_gat_bwd_dst_bf16"):
         assert must in names

@@ -5,7 +5,8 @@ input gradients and all-reduced weight gradients equal the single-process comput
   transposed aggregation, row gather for the loss, one-bucket gradient all-reduce) with a CPU
   double of the kernel engine (fp64 torch sparse products) — the engine is the only stand-in.
 * GPU (gloo rehearsal, world 2 / 4 on one MI355X, exchanges staged through host memory): the
-  drop-in GraphConvolution + HighWayGraphConvolution on the HIP kernels, handed a DistAdj,
+  drop-in GraphConvolution + HighWayGraphConvolution (fused and composed) on the HIP kernels,
+  handed a DistAdj,
   against the same layers on the whole adjacency in one process (fp32 tolerance 1e-4).
 """
 import os
@@ -48,8 +49,12 @@ class CpuEngine:
             return out
         return self._act(y, act)
 
-    def spmm_t(self, A, x):
-        return torch.sparse.mm(A.t().coalesce(), x)
+    def spmm_t(self, A, x, out=None):
+        y = torch.sparse.mm(A.t().coalesce(), x)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
 
     def act_bwd(self, dy, y, act):
         return dy * (y > 0) if act == 1 else dy
@@ -113,15 +118,18 @@ def _worker(rank, world, port, mode, q):
             dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev)
             torch.manual_seed(0)
             l1 = GraphConvolution(D, D, 0.0, F.relu, True).to(dev)
-            l2 = HighWayGraphConvolution(D, D, 0.0, lambda t: t, True, 0, dev).to(dev)
-            params = list(l1.parameters()) + list(l2.parameters())
+            # l2: fused HighWay layer (HighwayLayerFn through the DistAdj hooks); l3: an act the
+            # kernels cannot fuse, so the composed path (DistAdj.aggregate + torch blend)
+            l2 = HighWayGraphConvolution(D, D, 0.0, torch.tanh, True, 0, dev).to(dev)
+            l3 = HighWayGraphConvolution(D, D, 0.0, lambda t: t * 0.5, True, 0, dev).to(dev)
+            params = list(l1.parameters()) + list(l2.parameters()) + list(l3.parameters())
             adj_full = torch.sparse_coo_tensor(torch.from_numpy(np.stack([R, C])).long(),
                                                torch.from_numpy(V), (2 * N_KG, 2 * N_KG)).to(dev)
 
             def model(x, adj):
                 if adj is None:
-                    return l2(l1((x, adj_full)))[0]
-                return adj.gather_rows(l2(l1((x, adj)))[0])
+                    return l3(l2(l1((x, adj_full))))[0]
+                return adj.gather_rows(l3(l2(l1((x, adj))))[0])
             tol = 1e-4
 
         # single process, whole graph
