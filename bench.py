@@ -115,6 +115,34 @@ def bf16_rate(shard, H, steps):
                          "model": "gather: 4(N+1)+8E+2ED+2ND"}}
 
 
+def _timed(fn, steps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(steps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / steps
+
+
+def layout_rates(shard, H, Y, steps):
+    """Side measurements of the same aggregation: the row-major table (k_spmm_v4 over 1,200-B
+    rows) and the drop-in path for a row-major hidden no gnnea GEMM produced (pack into slices +
+    sliced aggregation, what ops.AggregateFn does above the Infinity Cache)."""
+    relu = _lib.GNNEA_ACT_RELU
+    D_ = H.shape[1]
+    out = {}
+    for name, fn in (("rowmajor", lambda: ops.spmm(shard.csr, H, relu, out=Y)),
+                     ("pack_then_sliced",
+                      lambda: ops.spmm_sliced(shard.csr, ops.slice_pack(H), D_, relu, out=Y))):
+        ms = _timed(fn, steps)
+        out[name] = {"edges_per_s": round(shard.nnz / ms * 1e3, 1), "ms_per_step": round(ms, 4)}
+    return out
+
+
 def cpu_baseline(shard, H, budget_s=12.0):
     """Reference op on the host: torch.spmm on the uncoalesced COO rows of a bounded sample."""
     from oracle.cpu_baseline import time_reference_spmm
@@ -152,6 +180,9 @@ def main():
     ap.add_argument("--no-train", action="store_true",
                     help="skip the side measurement of the row-sharded HGCN-EA training step")
     ap.add_argument("--train-steps", type=int, default=5)
+    ap.add_argument("--layout", choices=("sliced", "rowmajor"), default="sliced",
+                    help="feature table layout of the aggregation input (sliced: 64-column "
+                         "slices, each one Infinity-Cache-sized table at 1M rows)")
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank logic on ONE device with gloo (halo staged through host)")
     args = ap.parse_args()
@@ -186,9 +217,15 @@ def main():
     h_full = (torch.empty(shard.n_cols, Dl, device=device)
               if shard.g > 1 and part.kind == "rows" else None)
     y = torch.empty(shard.n_rows, Dl, device=device)
+    # H as the projection GEMM of a GCN layer leaves it: slice-major [ceil(D/64)][rows][64]
+    # (gnnea_gemm_sliced_f32 writes this layout; ops.GCNLayerFn) where the table exceeds the
+    # Infinity Cache, row-major otherwise (or with --layout rowmajor)
+    sliced = (args.layout == "sliced" and (shard.g == 1 or part.kind == "features")
+              and ops.use_sliced(shard.n_cols, Dl, torch.float32))
+    hs = ops.slice_pack(h_local) if sliced else None
 
     def step(ev=None):
-        shard.aggregate(h_local, h_full, y, _lib.GNNEA_ACT_RELU, ev)
+        shard.aggregate(h_local, h_full, y, _lib.GNNEA_ACT_RELU, ev, hs=hs)
 
     for _ in range(args.warmup):
         step()
@@ -262,13 +299,22 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_bytes, "traffic_source": pmc_src,
-                         "kernel": "gnnea::k_spmm_v4<relu,act,2>",
+                         "kernel": ("gnnea::k_spmm_sliced<relu,4>" if sliced else
+                                    "gnnea::k_spmm_v4<relu,act,2>"),
                          "launches_per_step": launches,
                          "kernel_ms": round(kernel_ms / launches, 4),
                          "bytes_per_launch": int(traffic / launches),
                          "model": "gather: 4(N+1)+8E+4ED+4ND (rank 0 shard, D = its slice), "
                                   "split evenly over the per-KG launches"},
         }
+        line["config"]["layout"] = ("slice-major [%d][%d][64] fp32 (as gnnea_gemm_sliced_f32 "
+                                    "writes the projection)" % ((Dl + 63) // 64, shard.n_cols)
+                                    if sliced else "row-major [%d][%d] fp32" % (shard.n_cols, Dl))
+        if world == 1:
+            try:
+                line["layouts"] = layout_rates(shard, h_local, y, args.steps)
+            except Exception as e:  # report, never hide
+                line["layouts"] = {"error": repr(e)}
         if train is not None:
             line["train_step"] = train
         if world == 1 and not args.no_sinkhorn:

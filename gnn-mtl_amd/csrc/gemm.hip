@@ -81,12 +81,19 @@ struct Loader {
   }
 };
 
+// Output addressing: element (row, col) of C at (col / 64)·cs + row·ldc + col % 64.  cs = 64 is
+// the plain row-major matrix; ldc = 64, cs = n·64 is the slice-major table [⌈N/64⌉][n][64] that
+// the sliced SpMM gathers from (gnnea_spmm_sliced_f32).
+__device__ __forceinline__ int64_t c_index(int64_t row, int64_t col, int64_t ldc, int64_t cs) {
+  return (col >> 6) * cs + row * ldc + (col & 63);
+}
+
 template <int TA, int TB, int WT, bool VEC>
 __global__ __launch_bounds__(256) void k_gemm_wide(int M, int N, int K, const float* __restrict__ A,
                                                    int64_t lda, const float* __restrict__ B,
                                                    int64_t ldb, const float* __restrict__ bias,
                                                    float beta, float* __restrict__ C,
-                                                   int64_t ldc, int k_per_split,
+                                                   int64_t ldc, int64_t cs, int k_per_split,
                                                    float* __restrict__ slab, int tiles_n) {
   constexpr int BN = 64 * WT;
   constexpr bool AK = TA == 0, BK_ = TB == 1;  // operand contiguous along K?
@@ -163,8 +170,9 @@ __global__ __launch_bounds__(256) void k_gemm_wide(int M, int N, int K, const fl
         slab[((int64_t)split * M + row) * N + col] = v;
       } else {
         float o = v + bv;
-        if (beta != 0.f) o += beta * C[(int64_t)row * ldc + col];
-        C[(int64_t)row * ldc + col] = o;
+        float* c = C + c_index(row, col, ldc, cs);
+        if (beta != 0.f) o += beta * *c;
+        *c = o;
       }
     }
   }
@@ -173,9 +181,10 @@ __global__ __launch_bounds__(256) void k_gemm_wide(int M, int N, int K, const fl
 // slab reduction in fixed split order (deterministic); 4 outputs per thread when the rows allow
 __global__ void k_gemm_reduce(int M, int N, int splits, const float* __restrict__ slab,
                               const float* __restrict__ bias, float beta, float* __restrict__ C,
-                              int64_t ldc) {
+                              int64_t ldc, int64_t cs) {
   const int64_t n = (int64_t)M * N;
-  const bool v4 = (N % 4 == 0) && (ldc % 4 == 0) && ((((uintptr_t)C) & 15) == 0);
+  const bool v4 =
+      (N % 4 == 0) && (ldc % 4 == 0) && (cs % 4 == 0) && ((((uintptr_t)C) & 15) == 0);
   if (v4) {
     const int64_t n4 = n / 4;
     const float4* sl = (const float4*)slab;
@@ -194,7 +203,7 @@ __global__ void k_gemm_reduce(int M, int N, int splits, const float* __restrict_
       }
       float o[4] = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
       const int64_t e = 4 * t, row = e / N, col = e - row * N;
-      float* c = C + row * ldc + col;
+      float* c = C + c_index(row, col, ldc, cs);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (bias) o[k] += bias[col + k];
@@ -210,7 +219,7 @@ __global__ void k_gemm_reduce(int M, int N, int splits, const float* __restrict_
     for (int q = 0; q < splits; ++q) s += slab[(int64_t)q * n + t];
     const int64_t row = t / N, col = t - row * N;
     if (bias) s += bias[col];
-    float* c = C + row * ldc + col;
+    float* c = C + c_index(row, col, ldc, cs);
     if (beta != 0.f) s += beta * *c;
     *c = s;
   }
@@ -239,25 +248,25 @@ static bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 template <int TA, int TB, int WT>
 static void launch_wt(dim3 grid, hipStream_t s, bool vec, int M, int N, int K, const float* A,
                       int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
-                      float* C, int64_t ldc, int kps, float* slab, int tiles_n) {
+                      float* C, int64_t ldc, int64_t cs, int kps, float* slab, int tiles_n) {
   if (vec)
     hipLaunchKernelGGL((k_gemm_wide<TA, TB, WT, true>), grid, dim3(256), 0, s, M, N, K, A, lda, B,
-                       ldb, bias, beta, C, ldc, kps, slab, tiles_n);
+                       ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n);
   else
     hipLaunchKernelGGL((k_gemm_wide<TA, TB, WT, false>), grid, dim3(256), 0, s, M, N, K, A, lda,
-                       B, ldb, bias, beta, C, ldc, kps, slab, tiles_n);
+                       B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n);
 }
 
 template <int TA, int TB>
 static void launch_t(int wt, dim3 grid, hipStream_t s, bool vec, int M, int N, int K,
                      const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
-                     float beta, float* C, int64_t ldc, int kps, float* slab, int tiles_n) {
+                     float beta, float* C, int64_t ldc, int64_t cs, int kps, float* slab, int tiles_n) {
   switch (wt) {
-    case 1: launch_wt<TA, TB, 1>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n); break;
-    case 2: launch_wt<TA, TB, 2>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n); break;
-    case 3: launch_wt<TA, TB, 3>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n); break;
-    case 4: launch_wt<TA, TB, 4>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n); break;
-    default: launch_wt<TA, TB, 5>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n); break;
+    case 1: launch_wt<TA, TB, 1>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n); break;
+    case 2: launch_wt<TA, TB, 2>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n); break;
+    case 3: launch_wt<TA, TB, 3>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n); break;
+    case 4: launch_wt<TA, TB, 4>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n); break;
+    default: launch_wt<TA, TB, 5>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n); break;
   }
 }
 
@@ -270,14 +279,14 @@ extern "C" int64_t gnnea_gemm_ws_bytes(int64_t M, int64_t N, int64_t K) {
   return pick_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
 }
 
-extern "C" int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
-                              const float* A, int64_t lda, const float* B, int64_t ldb,
-                              const float* bias, float beta, float* C, int64_t ldc, void* ws,
-                              int64_t ws_bytes, void* stream) {
+static int gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                    int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
+                    float* C, int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, void* stream) {
   if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
   if (M == 0 || N == 0) return 0;
   if (M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return GNNEA_EINVAL;
-  if (!C || ldc < N || (K > 0 && (!A || !B))) return GNNEA_EINVAL;
+  if (!C || (K > 0 && (!A || !B))) return GNNEA_EINVAL;
+  if (cs == 64 ? ldc < N : (ldc < (N < 64 ? N : 64) || cs < M * ldc)) return GNNEA_EINVAL;
   if (K > 0) {
     if ((trans_a ? lda < M : lda < K) || (trans_b ? ldb < K : ldb < N)) return GNNEA_EINVAL;
   }
@@ -296,17 +305,34 @@ extern "C" int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, in
                    b_contig % 4 == 0 && al16(A) && al16(B);
   const dim3 grid(tiles, splits);
   const int kk = kps > 0 ? kps : GBK;
-  if (!trans_a && !trans_b) launch_t<0, 0>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
-  else if (!trans_a && trans_b) launch_t<0, 1>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
-  else if (trans_a && !trans_b) launch_t<1, 0>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
-  else launch_t<1, 1>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
+  if (!trans_a && !trans_b) launch_t<0, 0>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, cs, kk, slab, tiles_n);
+  else if (!trans_a && trans_b) launch_t<0, 1>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, cs, kk, slab, tiles_n);
+  else if (trans_a && !trans_b) launch_t<1, 0>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, cs, kk, slab, tiles_n);
+  else launch_t<1, 1>(wt, grid, s, vec, (int)M, (int)N, (int)K, A, lda, B, ldb, bias, beta, C, ldc, cs, kk, slab, tiles_n);
   GNNEA_LAUNCH_CHECK();
   if (splits > 1) {
     const int64_t n = M * N;
     const int nb = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
     hipLaunchKernelGGL(k_gemm_reduce, dim3(nb), dim3(256), 0, s, (int)M, (int)N, splits, slab,
-                       bias, beta, C, ldc);
+                       bias, beta, C, ldc, cs);
     GNNEA_LAUNCH_CHECK();
   }
   return 0;
+}
+
+extern "C" int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                              const float* A, int64_t lda, const float* B, int64_t ldb,
+                              const float* bias, float beta, float* C, int64_t ldc, void* ws,
+                              int64_t ws_bytes, void* stream) {
+  return gemm_f32(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, 64, ws,
+                  ws_bytes, stream);
+}
+
+extern "C" int gnnea_gemm_sliced_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                                     const float* A, int64_t lda, const float* B, int64_t ldb,
+                                     const float* bias, float beta, float* Cs, int64_t sstride,
+                                     void* ws, int64_t ws_bytes, void* stream) {
+  if (sstride % 4 != 0) return GNNEA_EINVAL;
+  return gemm_f32(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, Cs, 64, sstride, ws,
+                  ws_bytes, stream);
 }

@@ -152,15 +152,19 @@ class KGShard:
     def n_cols(self):
         return self.part.n_cols
 
-    def aggregate(self, h_local, h_full, out, act, events=None):
+    def aggregate(self, h_local, h_full, out, act, events=None, hs=None):
         """out = act(A_shard · H) for this rank's rows; H's remote rows arrive by the halo
-        all-gather, overlapped with the aggregation over the locally owned rows."""
+        all-gather, overlapped with the aggregation over the locally owned rows.  ``hs``: the
+        same H held slice-major (gnnea.ops.spmm_sliced) for the exchange-free partitions."""
         from . import ops
         from ._lib import GNNEA_ACT_IDENTITY
         rec = (lambda k: events[k].record()) if events is not None else (lambda k: None)
         if self.part.g == 1 or self.part.kind == "features":  # no exchange in the aggregation
             rec(0)
-            ops.spmm(self.csr, h_local, act, out=out)
+            if hs is not None:
+                ops.spmm_sliced(self.csr, hs, h_local.shape[1], act, out=out)
+            else:
+                ops.spmm(self.csr, h_local, act, out=out)
             rec(1)
             return out
         work = halo_gather(h_local, h_full, self.group, self.part.g, async_op=True)

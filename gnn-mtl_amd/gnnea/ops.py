@@ -277,12 +277,122 @@ def act_bwd(dy, y, act):
     return g
 
 
+# ------------------------------------------------------------------------------------------ #
+# slice-major feature tables (gnnea_spmm_sliced_f32)                                          #
+# ------------------------------------------------------------------------------------------ #
+SLICE_W = 64
+SLICED = True  # use the slice-major path where it applies (tests switch it off to compare)
+
+
+def use_sliced(n_src, D, dtype):
+    """The slice-major aggregation applies to fp32 tables wider than one slice whose row-major
+    form exceeds the Infinity Cache (cfg-4: 1M rows x 300 per KG): one 64-column slice of a
+    1M-row KG is 256 MB and its gathers are 256-B line pairs."""
+    return (SLICED and dtype == torch.float32 and D % 4 == 0 and D > SLICE_W
+            and n_src * D * 4 > INFINITY_CACHE_BYTES)
+
+
+def sliced_empty(n, D, device):
+    """Uninitialised [S, n, 64] fp32 table for an [n, D] matrix (S = ceil(D/64)); columns past D
+    in the last slice are never read."""
+    S = (D + SLICE_W - 1) // SLICE_W
+    return torch.empty((S, n, SLICE_W), dtype=torch.float32, device=device)
+
+
+def slice_pack(x):
+    """Row-major fp32 [n, D] -> slice-major table (gnnea_slice_pack_f32)."""
+    x = _rows(x)
+    n, D = x.shape
+    xs = sliced_empty(n, D, x.device)
+    with torch.cuda.device(x.device):
+        check(_lib.lib().gnnea_slice_pack_f32(ptr(x), _ld(x), n, D, ptr(xs), xs.stride(0),
+                                              stream_of(x.device)))
+    return xs
+
+
+def act_bwd_sliced(dy, y, act):
+    """Gs = dy * act'(y) written slice-major (the transposed aggregation's input)."""
+    y = _rows(y)
+    dy = _rows(dy, torch.float32)
+    n, D = y.shape
+    gs = sliced_empty(n, D, y.device)
+    with torch.cuda.device(y.device):
+        check(_lib.lib().gnnea_act_bwd_sliced_f32(ptr(dy), _ld(dy), ptr(y), _ld(y), n, D,
+                                                  int(act), ptr(gs), gs.stride(0),
+                                                  stream_of(y.device)))
+    return gs
+
+
+def spmm_sliced(csr, xs, D, act=_lib.GNNEA_ACT_IDENTITY, out=None):
+    """out = act(A @ X) with X held slice-major in ``xs`` ([S, n_src, 64], S = ceil(D/64)),
+    launched per diagonal (KG) block; out row-major fp32 [n_rows, D]."""
+    _lib.require_device(xs)
+    S = (D + SLICE_W - 1) // SLICE_W
+    if xs.dtype != torch.float32 or xs.dim() != 3 or xs.shape[0] < S or \
+            xs.shape[2] != SLICE_W or xs.shape[1] < csr.n_cols or not xs.is_contiguous():
+        raise ValueError("gnnea.spmm_sliced: xs must be a contiguous fp32 [%d, >=%d, 64] table"
+                         % (S, csr.n_cols))
+    if out is None:
+        out = torch.empty((csr.n_rows, D), dtype=torch.float32, device=xs.device)
+    if out.dtype != torch.float32 or out.shape != (csr.n_rows, D) or out.stride(1) != 1:
+        raise ValueError("gnnea.spmm_sliced: out must be fp32 [%d, %d]" % (csr.n_rows, D))
+    L = _lib.lib()
+    st = stream_of(xs.device)
+    with torch.cuda.device(xs.device):
+        for r0, r1 in csr.row_blocks():
+            check(L.gnnea_spmm_sliced_f32(_off32(csr.rowptr, r0), ptr(csr.col), ptr(csr.val),
+                                          r1 - r0, D, ptr(xs), xs.stride(0), _off(out, r0),
+                                          _ld(out), int(act), st))
+    return out
+
+
+def gemm_sliced(x, weight, bias=None):
+    """hidden = x W^T + b written slice-major (gnnea_gemm_sliced_f32): the projection of a GCN
+    layer hands the aggregation its table at no extra pass."""
+    x = _rows(x)
+    weight = _rows(weight)
+    M, K = x.shape
+    N = weight.shape[0]
+    if weight.shape[1] != K:
+        raise ValueError("gnnea.gemm_sliced: inner dimensions differ")
+    if x.dtype != torch.float32 or weight.dtype != torch.float32:
+        raise TypeError("gnnea.gemm_sliced: fp32 operands required")
+    hs = sliced_empty(M, N, x.device)
+    if bias is not None:
+        bias = _featc(bias, torch.float32)
+    L = _lib.lib()
+    ws_bytes = int(L.gnnea_gemm_ws_bytes(M, N, K))
+    ws = _gemm_ws(x.device, ws_bytes) if ws_bytes > 0 else None
+    with torch.cuda.device(x.device):
+        check(L.gnnea_gemm_sliced_f32(0, 1, M, N, K, ptr(x), _ld(x), ptr(weight), _ld(weight),
+                                      ptr(bias), 0.0, ptr(hs), hs.stride(0), ptr(ws),
+                                      ws_bytes if ws is not None else 0, stream_of(x.device)))
+    return hs
+
+
+def aggregate_t_into(csr, dy, y, act, out=None):
+    """out = Aᵀ·(dy ⊙ act'(y)): the backward of act(A·hidden), slice-major when it applies."""
+    csrT = csr.transpose()
+    D = y.shape[1]
+    if use_sliced(csrT.n_cols, D, y.dtype) and (out is None or out.dtype == torch.float32):
+        gs = act_bwd_sliced(dy, y, act)
+        return spmm_sliced(csrT, gs, D, out=out)
+    g = _featc(dy, y.dtype) if act == _lib.GNNEA_ACT_IDENTITY else act_bwd(dy, y, act)
+    return spmm(csrT, g, out=out)
+
+
 class AggregateFn(torch.autograd.Function):
-    """support = act(A · hidden) (layers/layers.py:34-38); backward A^T · (dY ⊙ act'(Y))."""
+    """support = act(A · hidden) (layers/layers.py:34-38); backward A^T · (dY ⊙ act'(Y)).
+    Above the Infinity Cache (fp32) the aggregation runs over a slice-major copy of hidden
+    (gnnea_slice_pack_f32 + gnnea_spmm_sliced_f32) and the backward writes dY ⊙ act'(Y)
+    slice-major in the same elementwise pass."""
 
     @staticmethod
     def forward(ctx, hidden, csr, act):
-        out = spmm(csr, hidden, act)
+        if use_sliced(csr.n_cols, hidden.shape[1], hidden.dtype):
+            out = spmm_sliced(csr, slice_pack(hidden), hidden.shape[1], act)
+        else:
+            out = spmm(csr, hidden, act)
         ctx.csr = csr
         ctx.act = act
         ctx.save_for_backward(out)
@@ -291,10 +401,44 @@ class AggregateFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (out,) = ctx.saved_tensors
-        g = _featc(dy, out.dtype) if ctx.act == _lib.GNNEA_ACT_IDENTITY else \
-            act_bwd(dy, out, ctx.act)
-        dh = spmm(ctx.csr.transpose(), g)
-        return dh, None, None
+        return aggregate_t_into(ctx.csr, dy, out, ctx.act), None, None
+
+
+class GCNLayerFn(torch.autograd.Function):
+    """A whole graph convolution act(A · (x Wᵀ + b)) (layers/layers.py:30-39, dropout inactive)
+    with the hidden kept slice-major: the projection GEMM writes it as the sliced aggregation
+    reads it (never row-major in HBM); backward dY ⊙ act'(Y) is written slice-major by one
+    elementwise pass, Aᵀ·G gives d hidden row-major for dx = dh·W, dW = dhᵀ·x, db = colsum(dh)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, csr, act):
+        hs = gemm_sliced(x, weight, bias)
+        out = spmm_sliced(csr, hs, weight.shape[0], act)
+        ctx.csr, ctx.act = csr, act
+        ctx.save_for_backward(x, weight, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, out = ctx.saved_tensors
+        dh = aggregate_t_into(ctx.csr, dy, out, ctx.act)
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        dx = gemm(dh, weight) if need_x else None
+        dw = gemm(dh, x, trans_a=True) if need_w else None
+        db = colsum(dh) if need_b else None
+        return dx, dw, db, None, None
+
+
+def gcn_layer(adj, x, weight, bias, act_fn):
+    """Fused GCN layer (GCNLayerFn) when the slice-major path applies, else None."""
+    code = act_code(act_fn)
+    if code is None or not getattr(adj, "is_sparse", False) or x.dtype != torch.float32 or \
+            weight.dtype != torch.float32 or x.shape[1] != weight.shape[1]:
+        return None
+    csr = csr_of(adj)
+    if not use_sliced(csr.n_cols, weight.shape[0], torch.float32) or x.shape[0] != csr.n_cols:
+        return None
+    return GCNLayerFn.apply(_rows(x), weight, bias, csr, code)
 
 
 def aggregate(adj, hidden, act_fn=None):

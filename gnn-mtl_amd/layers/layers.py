@@ -4,7 +4,9 @@ Constructor signatures, parameter creation order (hence RNG consumption under
 ``torch.manual_seed``), attribute names and ``state_dict`` keys are those of the reference, so
 ``run/train_ea.py`` and its saved models work unchanged.  The forward passes run on HIP only:
   hidden = x W^T + b          -> MFMA f32 GEMM   (gnnea_gemm_f32)
-  act(A · hidden)             -> CSR gather SpMM with fused activation (gnnea_spmm_csr_f32)
+  act(A · hidden)             -> CSR gather SpMM with fused activation (gnnea_spmm_csr_f32; above
+                                 the Infinity Cache the hidden is written slice-major by the GEMM
+                                 and gathered by gnnea_spmm_sliced_f32)
   HighWay gate + blend        -> SpMM with fused sigmoid-gate epilogue (gnnea_spmm_highway_f32)
 Handed a ``gnnea.dist_graph.DistAdj`` instead of the sparse adjacency (and the rank's own rows
 of x), the same layers run row-sharded across GPUs with the RCCL halo exchange.
@@ -53,6 +55,11 @@ class GraphConvolution(Module):
     def forward(self, input):
         x, adj = input
         x = dense_of(x)
+        if not isinstance(adj, DistAdj) and adj.is_sparse and \
+                (self.dropout == 0 or not self.training):
+            out = ops.gcn_layer(adj, x, self.linear.weight, self.linear.bias, self.act)
+            if out is not None:  # hidden kept slice-major (gnnea.ops.GCNLayerFn)
+                return out, adj
         return _propagate(adj, self._hidden(x), self.act), adj
 
     def extra_repr(self):

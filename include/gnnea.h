@@ -81,6 +81,25 @@ int gnnea_spmm_csr_beta_f32(const int32_t* rowptr, const int32_t* col, const flo
                             int32_t n_rows, int32_t D, const float* X, int64_t ldx, float beta,
                             float* Y, int64_t ldy, int act, void* stream);
 
+/* Slice-major feature table (replaces the same torch.spmm, layers/layers.py:35, when the gathered
+ * matrix exceeds the 256 MB Infinity Cache): the D columns are cut into S = ceil(D/64) slices,
+ * element (r, c) at Xs[(c/64)*sstride + r*64 + c%64], sstride >= n*64 floats, Xs 16-B aligned.
+ * The aggregation walks the slices in order so each slice's table (256 MB at 1M rows) is what
+ * its gathers touch; Y is row-major.  Requires D % 4 == 0, ldy % 4 == 0, 16-B aligned Y, and
+ * Xs to hold every row the CSR references.  The fp32 sums are taken in a fixed order that
+ * differs from gnnea_spmm_csr_f32's (agreement to fp32 rounding). */
+int gnnea_spmm_sliced_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                          int32_t n_rows, int32_t D, const float* Xs, int64_t sstride, float* Y,
+                          int64_t ldy, int act, void* stream);
+/* row-major [n, D] (row stride ldx) -> slice-major table (the drop-in path for a row-major
+ * hidden that no gnnea GEMM produced) */
+int gnnea_slice_pack_f32(const float* X, int64_t ldx, int64_t n, int32_t D, float* Xs,
+                         int64_t sstride, void* stream);
+/* backward input of the transposed aggregation, written slice-major:  Gs = dY * act'(Y) */
+int gnnea_act_bwd_sliced_f32(const float* dY, int64_t lddy, const float* Y, int64_t ldy,
+                             int64_t n, int32_t D, int act, float* Gs, int64_t sstride,
+                             void* stream);
+
 /* a4. HighWay epilogue (layers/layers.py:64-76):
  *   S = act(A·X);  g = sigmoid(gate_pre + bias_gate);  Y = g*S + (1-g)*resid
  * gate_pre = x·kernel_gate (N x D), bias_gate (D, nullable = 0), resid = x (N x D).
@@ -201,6 +220,14 @@ int64_t gnnea_gemm_ws_bytes(int64_t M, int64_t N, int64_t K);
 int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
                    int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
                    float* C, int64_t ldc, void* ws, int64_t ws_bytes, void* stream);
+
+/* the same GEMM writing C slice-major (the layout gnnea_spmm_sliced_f32 gathers from):
+ * element (r, c) of the M x N product at Cs[(c/64)*sstride + r*64 + c%64], sstride >= M*64.
+ * The projection x W^T of a GCN layer writes its hidden this way at no extra cost. */
+int gnnea_gemm_sliced_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                          const float* A, int64_t lda, const float* B, int64_t ldb,
+                          const float* bias, float beta, float* Cs, int64_t sstride, void* ws,
+                          int64_t ws_bytes, void* stream);
 
 /* bf16 operands (cfg-5 storage), v_mfma_f32_32x32x16_bf16: A, B bf16 (void*), fp32 accumulate,
  * bias fp32 (nullable), C bf16 (c_dtype GNNEA_BF16, rounded once, nearest even) or fp32

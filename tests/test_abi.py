@@ -29,7 +29,8 @@ def test_header_declares_the_hot_path():
                  "gnnea_spmm_csr_bf16", "gnnea_spmm_highway_bf16", "gnnea_act_bwd_bf16",
                  "gnnea_highway_bwd_bf16", "gnnea_highway_bwd_ld_f32", "gnnea_highway_bwd_ld_bf16", "gnnea_gemm_bf16", "gnnea_gat_scores_bf16",
                  "gnnea_gat_fwd_bf16", "gnnea_gat_bwd_prep_bf16", "gnnea_gat_bwd_src_bf16",
-                 "gnnea_gat_bwd_dst_bf16"):
+                 "gnnea_gat_bwd_dst_bf16", "gnnea_spmm_sliced_f32", "gnnea_slice_pack_f32",
+                 "gnnea_act_bwd_sliced_f32", "gnnea_gemm_sliced_f32"):
         assert must in names
 
 
@@ -74,3 +75,10 @@ def test_host_only_entry_points():
     assert L.gnnea_spmm_csr_f32(None, None, None, -1, 300, None, 300, None, 300, 1, None) == -1
     assert L.gnnea_gemm_f32(0, 0, 4, 4, 4, None, 4, None, 4, None, 0.0, None, 4, None, 0,
                             None) == -1
+    # slice-major entry points: D % 4, slice stride and alignment are checked on the host
+    assert L.gnnea_spmm_sliced_f32(None, None, None, -1, 300, None, 64, None, 300, 1, None) == -1
+    assert L.gnnea_spmm_sliced_f32(16, 16, 16, 4, 30, 16, 64 * 4, 16, 32, 1, None) == -1
+    assert L.gnnea_slice_pack_f32(16, 300, 10, 300, 16, 63, None) == -1
+    assert L.gnnea_act_bwd_sliced_f32(16, 300, 16, 300, 10, 302, 1, 16, 640, None) == -1
+    assert L.gnnea_gemm_sliced_f32(0, 1, 10, 300, 8, 16, 8, 16, 8, None, 0.0, 16, 66, None, 0,
+                                   None) == -1

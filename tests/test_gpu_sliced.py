@@ -1,0 +1,166 @@
+"""Slice-major aggregation path (gnnea_spmm_sliced_f32, gnnea_gemm_sliced_f32,
+gnnea_slice_pack_f32, gnnea_act_bwd_sliced_f32) vs the CPU oracle and the row-major path.
+
+The sliced kernel sums each row's neighbours in four interleaved partial sums, so it agrees with
+the oracle (fp64) and the row-major kernel (CSR-order chain) to fp32 rounding: norm-relative
+1e-4, the fp32 tolerance of SURVEY.md §8c.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+TOL32 = 1e-4
+
+
+def _unslice(hs, D):
+    S, n, w = hs.shape
+    return hs.permute(1, 0, 2).reshape(n, S * w)[:, :D]
+
+
+def _graph(rng, n, nnz, device, hub=True):
+    from gnnea.graph import DeviceCSR
+    r = rng.integers(0, n, nnz)
+    c = rng.integers(0, n, nnz)
+    keep = (r > 3) & (r < n - 3)  # empty rows at both ends
+    r, c = r[keep], c[keep]
+    if hub:  # one row with > 64 and > 128 neighbours (several 64-edge batches)
+        r = np.concatenate([r, np.full(300, 17)])
+        c = np.concatenate([c, rng.integers(0, n, 300)])
+    v = rng.standard_normal(r.size).astype(np.float32)
+    csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                             torch.from_numpy(v).to(device), n, n)
+    return r, c, v, csr
+
+
+@pytest.mark.parametrize("D", [4, 60, 68, 128, 132, 300, 512])
+def test_spmm_sliced_vs_oracle(device, D):
+    from gnnea import ops
+    from oracle.gnn import coo_aggregate
+    rng = np.random.default_rng(D + 11)
+    n = 900
+    r, c, v, csr = _graph(rng, n, 8000, device)
+    x = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32)).to(device)
+    xs = ops.slice_pack(x)
+    assert xs.shape == ((D + 63) // 64, n, 64)
+    assert torch.equal(_unslice(xs, D), x)
+    for act, fn in ((0, lambda t: t), (1, torch.relu), (4, torch.sigmoid), (5, torch.tanh)):
+        y = ops.spmm_sliced(csr, xs, D, act).cpu()
+        ref = fn(coo_aggregate(r, c, v, n, x.cpu().double()))
+        assert rel_err(y, ref) < TOL32, (D, act)
+        assert rel_err(y, ops.spmm(csr, x, act).cpu()) < TOL32
+    assert torch.all(ops.spmm_sliced(csr, xs, D)[:4].cpu() == 0)
+
+
+def test_slice_pack_strided_and_rejects(device):
+    from gnnea import ops
+    big = torch.randn(333, 320, device=device)
+    x = big[:, :300]  # row stride 320
+    assert torch.equal(_unslice(ops.slice_pack(x), 300), x)
+    with pytest.raises(Exception):  # D % 4 != 0 has no slice-major form
+        ops.slice_pack(torch.randn(10, 30, device=device)[:, :29])
+
+
+def test_spmm_sliced_output_column_block(device):
+    """out may be a column block of a wider buffer (the HighWay layer's [dh | dgate])."""
+    from gnnea import ops
+    rng = np.random.default_rng(3)
+    n, D = 500, 300
+    _, _, _, csr = _graph(rng, n, 4000, device)
+    x = torch.randn(n, D, device=device)
+    P = torch.full((n, 2 * D), 7.0, device=device)
+    ops.spmm_sliced(csr, ops.slice_pack(x), D, 1, out=P[:, :D])
+    assert rel_err(P[:, :D].cpu(), ops.spmm(csr, x, 1).cpu()) < TOL32
+    assert torch.all(P[:, D:] == 7.0)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 300, 300), (777, 128, 64), (64, 68, 300),
+                                   (4097, 300, 17)])
+def test_gemm_sliced_vs_fp64(device, M, N, K):
+    from gnnea import ops
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=device)
+    W = torch.randn(N, K, device=device)
+    b = torch.randn(N, device=device)
+    hs = ops.gemm_sliced(x, W, b)
+    ref = x.double().cpu() @ W.double().cpu().t() + b.double().cpu()
+    assert rel_err(_unslice(hs, N).cpu(), ref) < TOL32
+    # the same bits as the row-major GEMM (same tiles, only the store address differs)
+    assert torch.equal(_unslice(hs, N), ops.gemm(x, W, trans_b=True, bias=b))
+
+
+@pytest.mark.parametrize("act,fn", [(1, torch.relu), (2, F.elu), (5, torch.tanh)])
+def test_act_bwd_sliced(device, act, fn):
+    from gnnea import ops
+    y = fn(torch.randn(300, 132, device=device))
+    dy = torch.randn(300, 132, device=device)
+    gs = ops.act_bwd_sliced(dy, y, act)
+    assert torch.equal(_unslice(gs, 132), ops.act_bwd(dy, y, act))
+
+
+def test_gcn_layer_sliced_vs_oracle(device, monkeypatch):
+    """GraphConvolution through GCNLayerFn (hidden written slice-major by the GEMM, sliced
+    aggregation, sliced backward) vs the fp64 oracle: output, dx, dW, db."""
+    from gnnea import ops
+    from layers.layers import GraphConvolution
+    from oracle.gnn import gcn_layer, layer_with_grads
+    monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 0)  # force the sliced path at test size
+    rng = np.random.default_rng(5)
+    n = 1200
+    r, c, v, csr = _graph(rng, n, 10000, device)
+    idx = torch.from_numpy(np.stack([r, c]).astype(np.int64))
+    adj = torch.sparse_coo_tensor(idx, torch.from_numpy(v), (n, n)).to(device)
+    torch.manual_seed(0)
+    layer = GraphConvolution(300, 300, 0.0, F.relu, True).to(device)
+    x = torch.from_numpy(rng.standard_normal((n, 300)).astype(np.float32) * 0.1).to(device)
+    R = torch.randn(n, 300, device=device)
+    calls = []
+    orig = ops.gemm_sliced
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+    monkeypatch.setattr(ops, "gemm_sliced", spy)
+    xx = x.clone().requires_grad_(True)
+    out, _ = layer((xx, adj))
+    (out * R).sum().backward()
+    assert calls, "the fused sliced layer was not used"
+    W = layer.linear.weight.detach().cpu().double()
+    b = layer.linear.bias.detach().cpu().double()
+    o_ref, dx_ref, (dW_ref, db_ref) = layer_with_grads(
+        lambda xv, Wv, bv: gcn_layer(xv, Wv, bv, r, c, v), x.cpu().double(), [W, b],
+        R.cpu().double())
+    assert rel_err(out.detach().cpu(), o_ref) < TOL32
+    assert rel_err(xx.grad.cpu(), dx_ref) < TOL32
+    assert rel_err(layer.linear.weight.grad.cpu(), dW_ref) < TOL32
+    assert rel_err(layer.linear.bias.grad.cpu(), db_ref) < TOL32
+
+
+def test_aggregate_sliced_matches_rowmajor_two_kg(device, monkeypatch):
+    """Two-KG graph above the Infinity Cache: AggregateFn takes the pack + sliced path per
+    diagonal block; forward and backward agree with the row-major kernels."""
+    from gnnea import ops, synth
+    from gnnea.graph import DeviceCSR
+    n = 300000
+    tr = synth.kg_pair_triples(n, 3 * n, 500, seed=4)
+    r, c, v = synth.adjacency_coo(tr, 2 * n, reference_order=False)
+    csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                             torch.from_numpy(v).to(device), 2 * n, 2 * n)
+    assert csr.row_blocks() == [(0, n), (n, 2 * n)]
+    h = torch.randn(2 * n, 128, device=device)
+    assert ops.use_sliced(2 * n, 128, torch.float32)
+    dy = torch.randn(2 * n, 128, device=device)
+
+    def run():
+        hh = h.clone().requires_grad_(True)
+        y = ops.AggregateFn.apply(hh, csr, 1)
+        (g,) = torch.autograd.grad(y, (hh,), dy)
+        return y.detach(), g
+    y_s, g_s = run()
+    monkeypatch.setattr(ops, "SLICED", False)
+    y_r, g_r = run()
+    assert rel_err(y_s.cpu(), y_r.cpu()) < TOL32
+    assert rel_err(g_s.cpu(), g_r.cpu()) < TOL32
