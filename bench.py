@@ -43,13 +43,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(world):
-    """Per-launch HBM bytes of the SpMM from the committed rocprofv3 PMC summary (same workload,
-    N = 1; collected by tools/gpu_round.sh pmc + tools/pmc_summary.py)."""
+def pmc_traffic(world, kernel):
+    """Per-launch HBM bytes of the SpMM kernel from the committed rocprofv3 PMC summary of the
+    same workload at N = 1 (tools/gpu_round.sh pmc + tools/pmc_summary.py)."""
     if world != 1:
         return None, None
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_spmm_pmc.json")))
+    files = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_spmm*pmc*.json")))
+             if json.load(open(f)).get("kernel") == kernel]
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -282,7 +283,7 @@ def main():
             launches = len(blocks)
         traffic = gather_model_bytes(shard.n_rows, shard.nnz, Dl)
         achieved = traffic / (kernel_ms * 1e-3) / 1e9
-        pmc_bytes, pmc_src = pmc_traffic(world)
+        pmc_bytes, pmc_src = pmc_traffic(world, "k_spmm_sliced" if sliced else "k_spmm_v4")
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),

@@ -79,16 +79,15 @@ __global__ __launch_bounds__(256) void k_spmm_sliced(const int32_t* __restrict__
 
 // Row-major [n, D] -> slice-major table.  BWD: the table holds G = dY ⊙ act'(Y) (the backward
 // aggregation's input, fused with its activation derivative); otherwise a copy of X = dY.
+// One wave per row (no integer division per element), lane q moves float4 q, q+64, ...
 template <int ACT, bool BWD>
 __global__ __launch_bounds__(256) void k_slice_fill(const float4* __restrict__ dY, int64_t ld4,
                                                     const float4* __restrict__ Yo,
                                                     int64_t ldo4, int64_t n, int D4,
                                                     float4* __restrict__ Gs, int64_t sstride4) {
-  const int64_t total = n * D4;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = t / D4;
-    const int q = (int)(t - r * D4);  // float4 index in the row
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave_id();
+  if (r >= n) return;
+  for (int q = lane_id(); q < D4; q += 64) {
     float4 v = dY[r * ld4 + q];
     if constexpr (BWD) {
       const float4 y = Yo[r * ldo4 + q];
@@ -112,8 +111,8 @@ static int slice_fill(const float* dY, int64_t ld, const float* Y, int64_t ldo, 
   if (D % 4 || ld % 4 || (BWD && ldo % 4) || sstride % 4 || ld < D || (BWD && ldo < D) ||
       sstride < n * kSliceW || !al16(dY) || !al16(Gs) || (BWD && !al16(Y)))
     return GNNEA_EINVAL;
-  const int64_t total = n * (D / 4);
-  const int nb = (int)(total / 256 + 1 < 16384 ? total / 256 + 1 : 16384);
+  if ((n + 3) / 4 >= (1ll << 31)) return GNNEA_EINVAL;
+  const int nb = (int)((n + 3) / 4);
 #define GNNEA_SF(A)                                                                            \
   hipLaunchKernelGGL((k_slice_fill<A, BWD>), dim3(nb), dim3(256), 0, s, (const float4*)dY,     \
                      ld / 4, (const float4*)Y, ldo / 4, n, D / 4, (float4*)Gs, sstride / 4)
