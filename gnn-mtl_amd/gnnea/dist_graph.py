@@ -61,6 +61,25 @@ class HipEngine:
         from . import ops
         return ops.highway_bwd(dy, S, G, resid, act, want_dresid)
 
+    def gat_fwd(self, csr, H, a_all, heads, d_head, alpha, act, row0):
+        """All-head GAT aggregation of the shard's rows over the KG's H rows; returns
+        (Y_loc [n_rows, heads*d_head], saved state for gat_bwd)."""
+        from . import ops
+        D = heads * d_head
+        Hp = ops._pad4(H, D)
+        a32 = ops._featc(a_all, torch.float32)
+        Y, m, den, s1, s2 = ops.gat_forward(csr, Hp, a32, heads, d_head, alpha, act, row0=row0)
+        return (Y if Y.shape[1] == D else Y[:, :D]), (Hp, a32, s1, s2, m, den, Y)
+
+    def gat_bwd(self, csr, saved, dY, heads, d_head, alpha, act, row0, need_da):
+        """(dH partial over every KG row, da partial) of sum(Y_loc ⊙ dY)."""
+        from . import ops
+        Hp, a32, s1, s2, m, den, Y = saved
+        D = heads * d_head
+        dH, da = ops.gat_backward(csr, Hp, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha,
+                                  act, row0=row0, need_da=need_da)
+        return (dH if dH.shape[1] == D else dH[:, :D]), da
+
 
 def _is_gloo(group):
     return dist.get_backend(group) == "gloo"
@@ -116,6 +135,18 @@ class DistAdj:
                 torch.sigmoid(gate_pre)
             return g * s + (1.0 - g) * resid
         return HaloHighwayFn.apply(hidden, gate_pre, resid, bias_gate, self, code)
+
+    def gat(self, H, a_all, heads, d_head, alpha, act_fn):
+        """All heads of a GraphAttentionLayer over the shard (layers/att_layers.py:29-61, 86):
+        H = x_loc·[W_0|...|W_{h-1}] is row-local; the KG group's H rows arrive by the halo
+        all-gather, the logits / softmax / aggregation of the owned rows run on them, and the
+        backward reduce-scatters the gradient of every KG row back to its owner."""
+        from .ops import act_code
+        code = act_code(act_fn) if act_fn is not None else _lib.GNNEA_ACT_IDENTITY
+        if code not in (_lib.GNNEA_ACT_IDENTITY, _lib.GNNEA_ACT_RELU):
+            return act_fn(HaloGATFn.apply(H, a_all, self, heads, d_head, alpha,
+                                          _lib.GNNEA_ACT_IDENTITY))
+        return HaloGATFn.apply(H, a_all, self, heads, d_head, alpha, code)
 
     def highway_fwd(self, hidden, gate_pre, resid, bias_gate, act):
         """HighWay tail over the shard (gnnea.ops.HighwayLayerFn's aggregation hook): the
@@ -233,6 +264,31 @@ class HaloHighwayFn(torch.autograd.Function):
                                         ctx.needs_input_grad[2])
         dh = dadj.reduce_scatter(e.spmm_t(dadj.csr, dS))
         return dh, dgate, dres, None, None, None
+
+
+class HaloGATFn(torch.autograd.Function):
+    """Y_loc = GAT(A_shard, all_gather(H_loc)) for the owned rows; backward: the shard's dH
+    partial over every KG row is reduce-scattered to the owners, da stays a per-rank partial
+    (summed with the other parameter gradients by allreduce_grads)."""
+
+    @staticmethod
+    def forward(ctx, H, a_all, dadj, heads, d_head, alpha, act):
+        full, _ = dadj.halo(H)
+        row0 = dadj.part.row0 if dadj.part.g > 1 else 0
+        Y, saved = dadj.engine.gat_fwd(dadj.csr, full, a_all, heads, d_head, alpha, act, row0)
+        ctx.dadj, ctx.row0 = dadj, row0
+        ctx.meta = (heads, d_head, float(alpha), int(act))
+        ctx.saved = saved
+        return Y
+
+    @staticmethod
+    def backward(ctx, dY):
+        heads, d_head, alpha, act = ctx.meta
+        dadj = ctx.dadj
+        dH, da = dadj.engine.gat_bwd(dadj.csr, ctx.saved, dY.contiguous(), heads, d_head, alpha,
+                                     act, ctx.row0, ctx.needs_input_grad[1])
+        ctx.saved = None
+        return dadj.reduce_scatter(dH), da, None, None, None, None, None
 
 
 class GatherRowsFn(torch.autograd.Function):

@@ -645,6 +645,83 @@ def _pad4(t, D, dtype=None):
     return out
 
 
+def gat_forward(csr, H, a32, heads, d_head, alpha, act, em=None, row0=0):
+    """All heads of the GAT aggregation over ``csr`` (one edge pass per KG block).
+
+    H: the source table (every row the CSR references, row-major, 4-aligned rows: _pad4).
+    The CSR's destination row i is row ``row0 + i`` of H's index space (row0 = 0 for the whole
+    graph; the first owned row for a row shard, gnnea.dist_graph).  Returns (Y [n_rows, Dp],
+    m, den, s1, s2): Y and the per-row softmax records of the destination rows, the logits
+    s1 / s2 of every H row."""
+    D = heads * d_head
+    N = csr.n_rows
+    s1, s2 = gat_scores(H, a32, heads, d_head)
+    Y = torch.empty((N, (D + 3) // 4 * 4), dtype=H.dtype, device=H.device)
+    m = torch.empty((N, heads), dtype=torch.float32, device=H.device)
+    den = torch.empty_like(m)
+    fwd = _gat_fn("gnnea_gat_fwd", H.dtype)
+    with torch.cuda.device(H.device):
+        for r0, r1 in _blocks(csr, H):  # per KG block when H exceeds the Infinity Cache
+            check(fwd(_off32(csr.rowptr, r0), ptr(csr.col), r1 - r0, ptr(H), H.stride(0),
+                      heads, d_head, _off(s1, row0 + r0), ptr(s2), float(alpha), ptr(em),
+                      int(act), _off(Y, r0), Y.stride(0), _off(m, r0), _off(den, r0),
+                      stream_of(H.device)))
+    return Y, m, den, s1, s2
+
+
+def gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha, act, em=None,
+                 row0=0, need_da=True):
+    """Gradients of sum(Y ⊙ dY) for gat_forward's outputs: (dH [rows of H, Dp], da or None).
+
+    One prep pass over the destination rows (G = dY·act', softmax records), one gather sweep
+    over Aᵀ (per source row j: SDDMM, softmax backward, dH_j and ds2_j, no atomics), one pass
+    over the destination rows through the transpose position map (ds1_i, dH_{row0+i} += ...).
+    For a row shard dH and da are this shard's partials (summed across the KG group / world by
+    the caller)."""
+    csrT = csr.transpose()
+    D = heads * d_head
+    dY = _pad4(dY, D, H.dtype)
+    if dY.shape[1] != Y.shape[1]:
+        dY = _pad4(dY[:, :D].contiguous(), D, H.dtype)
+    N = csr.n_rows
+    dev = H.device
+    st = stream_of(dev)
+    G = torch.empty_like(Y)
+    rec = torch.empty((N, heads, 4), dtype=torch.float32, device=dev)
+    dH = torch.empty_like(H)
+    dzT = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=dev)
+    ds1 = torch.empty((N, heads), dtype=torch.float32, device=dev)
+    ds2 = torch.empty((H.shape[0], heads), dtype=torch.float32, device=dev)
+    tpos = csr.tpos()
+    with torch.cuda.device(dev):
+        # G = dL/dh' and the per-node record {s1, m, 1/den, G.h'} (relu / identity: Y = h')
+        check(_gat_fn("gnnea_gat_bwd_prep", H.dtype)(
+            N, heads, d_head, ptr(dY), ptr(Y), Y.stride(0), _off(s1, row0), ptr(m), ptr(den),
+            int(act), ptr(G), ptr(rec), st))
+        src = _gat_fn("gnnea_gat_bwd_src", H.dtype)
+        for j0, j1 in _blocks(csrT, G):  # source rows j of A^T, per KG block
+            check(src(_off32(csrT.rowptr, j0), ptr(csrT.col), ptr(csrT.perm), j1 - j0, heads,
+                      d_head, _off(H, j0), H.stride(0), _off(s2, j0), alpha, ptr(em),
+                      ptr(rec), ptr(G), G.stride(0), ptr(a32), _off(dH, j0), dH.stride(0),
+                      ptr(dzT), _off(ds2, j0), st))
+        if csrT.n_rows < H.shape[0]:  # H rows no edge references: no gradient
+            dH[csrT.n_rows:].zero_()
+            ds2[csrT.n_rows:].zero_()
+        check(_gat_fn("gnnea_gat_bwd_dst", H.dtype)(
+            ptr(csr.rowptr), ptr(tpos), N, heads, d_head, ptr(dzT), ptr(a32), _off(dH, row0),
+            dH.stride(0), ptr(ds1), st))
+    da = None
+    if need_da:
+        # da1[h] = sum_i ds1[i,h] H_{row0+i},h ; da2[h] = sum_j ds2[j,h] H_j,h  (MFMA, split-K)
+        p1 = gemm(ds1, H[row0:row0 + N, :D], trans_a=True, out_dtype=torch.float32)
+        p2 = gemm(ds2, H[:, :D], trans_a=True, out_dtype=torch.float32)
+        p1 = p1.view(heads, heads, d_head)
+        p2 = p2.view(heads, heads, d_head)
+        idx = torch.arange(heads, device=H.device)
+        da = torch.cat([p1[idx, idx], p2[idx, idx]], dim=1)
+    return dH, da
+
+
 class GATFn(torch.autograd.Function):
     """h'_i = sum_j softmax_j(-LeakyReLU(a·[h_i||h_j])) h_j for all heads at once
     (layers/att_layers.py:29-61 per head, concatenated at :86).  H in fp32 or bf16 storage (the
@@ -655,19 +732,8 @@ class GATFn(torch.autograd.Function):
         D = heads * d_head
         H = _pad4(H, D)
         a32 = _featc(a_all, torch.float32)
-        N = csr.n_rows
-        s1, s2 = gat_scores(H, a32, heads, d_head)
-        Y = torch.empty((N, (D + 3) // 4 * 4), dtype=H.dtype, device=H.device)
-        m = torch.empty((N, heads), dtype=torch.float32, device=H.device)
-        den = torch.empty_like(m)
         em = _featc(edge_mask, torch.float32) if edge_mask is not None else None
-        fwd = _gat_fn("gnnea_gat_fwd", H.dtype)
-        with torch.cuda.device(H.device):
-            for r0, r1 in _blocks(csr, H):  # per KG block when H exceeds the Infinity Cache
-                check(fwd(_off32(csr.rowptr, r0), ptr(csr.col), r1 - r0, ptr(H), H.stride(0),
-                          heads, d_head, _off(s1, r0), ptr(s2), float(alpha), ptr(em), int(act),
-                          _off(Y, r0), Y.stride(0), _off(m, r0), _off(den, r0),
-                          stream_of(H.device)))
+        Y, m, den, s1, s2 = gat_forward(csr, H, a32, heads, d_head, alpha, act, em)
         ctx.csr = csr
         ctx.meta = (heads, d_head, float(alpha), int(act))
         ctx.save_for_backward(H, a32, s1, s2, m, den, Y, em if em is not None else torch.empty(0))
@@ -679,45 +745,9 @@ class GATFn(torch.autograd.Function):
         H, a_all, s1, s2, m, den, Y, em = ctx.saved_tensors
         heads, d_head, alpha, act = ctx.meta
         em = em if ctx.has_mask else None
-        csr = ctx.csr
-        csrT = csr.transpose()
         D = heads * d_head
-        dY = _pad4(dY, D, H.dtype)
-        if dY.shape[1] != Y.shape[1]:
-            dY = _pad4(dY[:, :D].contiguous(), D, H.dtype)
-        N = csr.n_rows
-        dev = H.device
-        st = stream_of(dev)
-        G = torch.empty_like(Y)
-        rec = torch.empty((N, heads, 4), dtype=torch.float32, device=dev)
-        dH = torch.empty_like(H)
-        dzT = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=dev)
-        ds1 = torch.empty((N, heads), dtype=torch.float32, device=dev)
-        ds2 = torch.empty_like(ds1)
-        tpos = csr.tpos()
-        with torch.cuda.device(dev):
-            # G = dL/dh' and the per-node record {s1, m, 1/den, G.h'} (relu / identity: Y = h')
-            check(_gat_fn("gnnea_gat_bwd_prep", H.dtype)(
-                N, heads, d_head, ptr(dY), ptr(Y), Y.stride(0), ptr(s1), ptr(m), ptr(den),
-                int(act), ptr(G), ptr(rec), st))
-            src = _gat_fn("gnnea_gat_bwd_src", H.dtype)
-            for j0, j1 in _blocks(csrT, G):  # source rows j of A^T, per KG block
-                check(src(_off32(csrT.rowptr, j0), ptr(csrT.col), ptr(csrT.perm), j1 - j0, heads,
-                          d_head, _off(H, j0), H.stride(0), _off(s2, j0), alpha, ptr(em),
-                          ptr(rec), ptr(G), G.stride(0), ptr(a_all), _off(dH, j0), dH.stride(0),
-                          ptr(dzT), _off(ds2, j0), st))
-            check(_gat_fn("gnnea_gat_bwd_dst", H.dtype)(
-                ptr(csr.rowptr), ptr(tpos), N, heads, d_head, ptr(dzT), ptr(a_all), ptr(dH),
-                dH.stride(0), ptr(ds1), st))
-        da = None
-        if ctx.needs_input_grad[1]:
-            # da1[h] = sum_i ds1[i,h] H_i,h ; da2[h] = sum_j ds2[j,h] H_j,h   (MFMA, split-K)
-            p1 = gemm(ds1, H[:, :D], trans_a=True, out_dtype=torch.float32)
-            p2 = gemm(ds2, H[:, :D], trans_a=True, out_dtype=torch.float32)
-            p1 = p1.view(heads, heads, d_head)
-            p2 = p2.view(heads, heads, d_head)
-            idx = torch.arange(heads, device=H.device)
-            da = torch.cat([p1[idx, idx], p2[idx, idx]], dim=1)
+        dH, da = gat_backward(ctx.csr, H, a_all, s1, s2, m, den, Y, dY, heads, d_head, alpha,
+                              act, em, need_da=ctx.needs_input_grad[1])
         return (dH if dH.shape[1] == D else dH[:, :D]), da, None, None, None, None, None, None
 
 

@@ -5,13 +5,23 @@ The reference runs each head separately and materialises cat(h[row], h[col]) per
 (x · [W_0|...|W_{H-1}]) and ONE edge pass (gnnea_gat_fwd_f32) whose output is already the
 head-concatenated tensor of :86.  Parameters (``attention_{i}.W``, ``attention_{i}.a``), their
 xavier_normal init order and the dropout calls keep the reference's names and RNG order.
+Handed a ``gnnea.dist_graph.DistAdj`` (and the rank's own rows of x) the layers run row-sharded
+with the halo all-gather of the projected rows (dropout inactive).
 """
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from gnnea import ops
+from gnnea.dist_graph import DistAdj
 from gnnea.graph import csr_of, dense_of
+
+
+def _sharded_gat(adj, H, a_all, heads, d_head, alpha, act, p, training):
+    """Row shard of a multi-GPU run (gnnea.dist_graph.DistAdj): halo all-gather of H."""
+    if training and p > 0.0:
+        raise NotImplementedError("gnnea: edge dropout on a row-sharded adjacency")
+    return adj.gat(H, a_all, heads, d_head, alpha, act)
 
 
 def _edge_dropout(nnz, p, training, device, heads):
@@ -41,6 +51,9 @@ class SpGraphAttentionLayer(nn.Module):
     def forward(self, input, adj):
         x = dense_of(input)
         h = ops.matmul(x, self.W)
+        if isinstance(adj, DistAdj):
+            return _sharded_gat(adj, h, self.a.view(1, -1), 1, self.out_features, self.alpha,
+                                self.act, self.dropout.p, self.training)
         csr = csr_of(adj)
         mask = _edge_dropout(csr.nnz, self.dropout.p, self.training, h.device, 1)
         return ops.gat(adj, h, self.a.view(1, -1), 1, self.out_features, self.alpha, self.act,
@@ -73,8 +86,12 @@ class GraphAttentionLayer(nn.Module):
         W_all = torch.cat([att.W for att in self.attentions], dim=1)
         a_all = torch.cat([att.a for att in self.attentions], dim=0)  # [heads, 2*d_head]
         H = ops.matmul(x, W_all)
-        mask = _edge_dropout(csr_of(adj).nnz, self.dropout, self.training, H.device, heads)
-        y = ops.gat(adj, H, a_all, heads, self.output_dim, first.alpha, first.act, mask)
+        if isinstance(adj, DistAdj):
+            y = _sharded_gat(adj, H, a_all, heads, self.output_dim, first.alpha, first.act,
+                             self.dropout, self.training)
+        else:
+            mask = _edge_dropout(csr_of(adj).nnz, self.dropout, self.training, H.device, heads)
+            y = ops.gat(adj, H, a_all, heads, self.output_dim, first.alpha, first.act, mask)
         if not self.concat:
             y = y.view(-1, heads, self.output_dim).mean(dim=1)
         y = F.dropout(y, self.dropout, training=self.training)

@@ -1,4 +1,4 @@
-"""Row-sharded GCN / HighWay layers (gnnea.dist_graph.DistAdj) across ranks: forward rows,
+"""Row-sharded GCN / HighWay / GAT layers (gnnea.dist_graph.DistAdj) across ranks: forward rows,
 input gradients and all-reduced weight gradients equal the single-process computation.
 
 * CPU (gloo, world 2 / 4 / 8): the collective logic (halo all-gather, reduce-scatter of the
@@ -68,6 +68,34 @@ class CpuEngine:
         dS = dy * g * ((S > 0).to(dy.dtype) if act == 1 else 1.0)
         return dS, dy * (S - resid) * g * (1 - g), (dy * (1 - g) if want else None)
 
+    @staticmethod
+    def gat_dense(A, H, a, heads, dh, alpha, act, row0):
+        """layers/att_layers.py:29-61 per head over A's edges (destination i = row0 + row)."""
+        i, j = A.indices()
+        n = A.shape[0]
+        outs = []
+        for h in range(heads):
+            Hh = H[:, h * dh:(h + 1) * dh]
+            z = Hh[row0 + i] @ a[h, :dh] + Hh[j] @ a[h, dh:]
+            e = torch.exp(-torch.nn.functional.leaky_relu(z, alpha))
+            den = torch.zeros(n, dtype=H.dtype).index_add(0, i, e)
+            num = torch.zeros(n, dh, dtype=H.dtype).index_add(0, i, e[:, None] * Hh[j])
+            outs.append(num / den[:, None])
+        y = torch.cat(outs, 1)
+        return torch.relu(y) if act == 1 else y
+
+    def gat_fwd(self, A, H, a_all, heads, dh, alpha, act, row0):
+        Hd = H.detach().clone().requires_grad_(True)
+        ad = a_all.detach().clone().requires_grad_(True)
+        with torch.enable_grad():
+            y = self.gat_dense(A, Hd, ad, heads, dh, alpha, act, row0)
+        return y.detach(), (Hd, ad, y)
+
+    def gat_bwd(self, A, saved, dY, heads, dh, alpha, act, row0, need_da):
+        Hd, ad, y = saved
+        gH, ga = torch.autograd.grad(y, (Hd, ad), dY)
+        return gH, (ga if need_da else None)
+
 
 def _worker(rank, world, port, mode, q):
     import sys
@@ -85,7 +113,43 @@ def _worker(rank, world, port, mode, q):
         R, C, V = synth.adjacency_coo(tr, 2 * N_KG, reference_order=False)
         X = torch.from_numpy(synth.features(2 * N_KG, D, seed=5)).double()
         Rw = torch.from_numpy(np.random.default_rng(9).standard_normal((2 * N_KG, D)))
-        if mode == "cpu":
+        HEADS, DH = 3, D // 3
+        if mode == "gat_cpu":
+            dev = torch.device("cpu")
+            dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev, engine=CpuEngine())
+            torch.manual_seed(0)
+            Wg = torch.randn(D, D, dtype=torch.float64) * 0.3
+            a_all = torch.randn(HEADS, 2 * DH, dtype=torch.float64) * 0.3
+            W2 = torch.randn(D, D, dtype=torch.float64)
+            params = [p.requires_grad_() for p in (Wg, a_all, W2)]
+
+            def model(x, adj):
+                if adj is None:
+                    A = CpuEngine().csr(R, C, V, 2 * N_KG, 2 * N_KG, None)
+                    y = CpuEngine.gat_dense(A, x @ Wg, a_all, HEADS, DH, 0.2, 1, 0)
+                    return CpuEngine.gat_dense(A, y @ W2, a_all, HEADS, DH, 0.2, 0, 0)
+                y = adj.gat(x @ Wg, a_all, HEADS, DH, 0.2, F.relu)
+                return adj.gather_rows(adj.gat(y @ W2, a_all, HEADS, DH, 0.2, None))
+            tol = 1e-12
+        elif mode == "gat_gpu":
+            from layers.att_layers import GraphAttentionLayer
+            dev = torch.device("cuda:0")
+            torch.cuda.set_device(dev)
+            X, Rw = X.float().to(dev), Rw.float().to(dev)
+            dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev)
+            torch.manual_seed(0)
+            g1 = GraphAttentionLayer(D, DH, 0.0, F.relu, 0.2, HEADS, True).to(dev)
+            g2 = GraphAttentionLayer(D, DH, 0.0, F.elu, 0.2, HEADS, True).to(dev)  # torch act
+            params = list(g1.parameters()) + list(g2.parameters())
+            adj_full = torch.sparse_coo_tensor(torch.from_numpy(np.stack([R, C])).long(),
+                                               torch.from_numpy(V), (2 * N_KG, 2 * N_KG)).to(dev)
+
+            def model(x, adj):
+                if adj is None:
+                    return g2(g1((x, adj_full)))[0]
+                return adj.gather_rows(g2(g1((x, adj)))[0])
+            tol = 1e-4
+        elif mode == "cpu":
             dev = torch.device("cpu")
             dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev, engine=CpuEngine())
             torch.manual_seed(0)
@@ -180,3 +244,18 @@ def test_dist_layers_gloo_cpu(world):
 @pytest.mark.parametrize("world", [2, 4])
 def test_dist_layers_rehearsal_on_device(device, world):
     _run(world, "gpu")
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_dist_gat_gloo_cpu(world):
+    """Row-sharded GAT (DistAdj.gat / HaloGATFn): halo all-gather of H, reduce-scatter of the
+    dH partials over every KG row, da partials summed by allreduce_grads."""
+    _run(world, "gat_cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_gat_rehearsal_on_device(device, world):
+    """The drop-in GraphAttentionLayer handed a DistAdj, on the HIP GAT kernels (row offset of
+    the shard's logits and dH), against the same layers on the whole adjacency."""
+    _run(world, "gat_gpu")
