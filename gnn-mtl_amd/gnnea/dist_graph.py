@@ -43,11 +43,19 @@ class HipEngine:
 
     def spmm(self, csr, x, act, out=None, beta=0.0):
         from . import ops
+        if beta == 0.0 and ops.use_sliced(csr.n_cols, x.shape[1], x.dtype) and \
+                (out is None or out.dtype == torch.float32):
+            # above the Infinity Cache: pack into 64-column slices, aggregate slice by slice
+            return ops.spmm_sliced(csr, ops.slice_pack(x), x.shape[1], act, out=out)
         return ops.spmm(csr, x, act, out=out, beta=beta)
 
     def spmm_t(self, csr, x, out=None):
+        return self.spmm(csr.transpose(), x, _lib.GNNEA_ACT_IDENTITY, out=out)
+
+    def act_spmm_t(self, csr, dy, y, act):
+        """Aᵀ·(dy ⊙ act'(y)) (the aggregation's backward; slice-major above the cache)."""
         from . import ops
-        return ops.spmm(csr.transpose(), x, out=out)
+        return ops.aggregate_t_into(csr, dy.contiguous(), y, act)
 
     def act_bwd(self, dy, y, act):
         from . import ops
@@ -237,10 +245,7 @@ class HaloAggregateFn(torch.autograd.Function):
     def backward(ctx, dy):
         (out,) = ctx.saved_tensors
         dadj = ctx.dadj
-        e = dadj.engine
-        g = dy.contiguous() if ctx.act == _lib.GNNEA_ACT_IDENTITY else \
-            e.act_bwd(dy.contiguous(), out, ctx.act)
-        return dadj.reduce_scatter(e.spmm_t(dadj.csr, g)), None, None
+        return dadj.reduce_scatter(dadj.engine.act_spmm_t(dadj.csr, dy, out, ctx.act)), None, None
 
 
 class HaloHighwayFn(torch.autograd.Function):

@@ -285,10 +285,12 @@ SLICED = True  # use the slice-major path where it applies (tests switch it off 
 
 
 def use_sliced(n_src, D, dtype):
-    """The slice-major aggregation applies to fp32 tables wider than one slice whose row-major
-    form exceeds the Infinity Cache (cfg-4: 1M rows x 300 per KG): one 64-column slice of a
-    1M-row KG is 256 MB and its gathers are 256-B line pairs."""
-    return (SLICED and dtype == torch.float32 and D % 4 == 0 and D > SLICE_W
+    """The slice-major aggregation applies to fp32 tables at least two slices wide whose
+    row-major form exceeds the Infinity Cache (cfg-4: 1M rows x 300 per KG): one 64-column
+    slice of a 1M-row KG is 256 MB and its gathers are 256-B line pairs.  Measured on one KG
+    of cfg-4 (profiles/r01_scale_probe_sliced.json): 300 columns 4.28 -> 3.46 ms, 152 columns
+    1.85 -> 1.79 ms, 76 columns 1.08 -> 1.11 ms (row-major kept below 128 columns)."""
+    return (SLICED and dtype == torch.float32 and D % 4 == 0 and D >= 2 * SLICE_W
             and n_src * D * 4 > INFINITY_CACHE_BYTES)
 
 

@@ -59,6 +59,9 @@ class CpuEngine:
     def act_bwd(self, dy, y, act):
         return dy * (y > 0) if act == 1 else dy
 
+    def act_spmm_t(self, A, dy, y, act):
+        return self.spmm_t(A, self.act_bwd(dy, y, act))
+
     def highway_fwd(self, A, h, gate_pre, resid, bias, act):
         S = self._act(torch.sparse.mm(A, h), act)
         g = torch.sigmoid(gate_pre + bias if bias is not None else gate_pre)

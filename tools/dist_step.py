@@ -1,7 +1,7 @@
 """Row-sharded EA encoder training step (BASELINE.json configs[3]: HGCN-EA on the 2 x 1M-entity
 synthetic KG pair, node-sharded with the RCCL halo exchange).
 
-    python tools/dist_step.py [--model HGCN|GCN] [--steps 10] [--warmup 2] [--entities 1000000]
+    python tools/dist_step.py [--model HGCN|GCN|GAT] [--steps 10] [--warmup 2] [--entities 1000000]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/dist_step.py
 
 A step = the drop-in Encoder.encode + Decoder.decode (models/encoders.py, models/decoders.py;
@@ -44,7 +44,7 @@ def build(model, n, rank, world, device, seed=10086):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="HGCN", choices=("HGCN", "GCN"))
+    ap.add_argument("--model", default="HGCN", choices=("HGCN", "GCN", "GAT"))
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--entities", type=int, default=synth.CONFIGS["cfg4"]["n"])

@@ -4,7 +4,7 @@
 
 For world sizes W = 1, 2, 4, 8 this builds the shard that rank r of W would own
 (gnnea.dist.KGShard, feature-column partition: no exchange in the aggregation) and times its
-SpMM alone on the one device.  Ranks of the feature partition are independent, so the slowest
+SpMM alone on the one device (the slice-major table where bench.py uses it, else row-major).  Ranks of the feature partition are independent, so the slowest
 rank's time bounds the W-GPU step: predicted value = nnz(A) / max_r t_r.  This is a prediction
 for the driver's 1/2/4/8-GPU run, not a measurement of it (8-GPU runs are the driver's).
 """
@@ -69,6 +69,14 @@ def main():
             ms = timeit(lambda: ops.spmm(sh.csr, h, _lib.GNNEA_ACT_RELU, out=y), args.reps)
             ent["auto"] = {"ms": round(ms, 4), "GBps_gather_model": round(byt / ms / 1e6, 1)}
             ent["ms"] = ent["auto"]["ms"]
+            if ops.use_sliced(sh.n_cols, Dl, dt):  # what bench.py runs: the slice-major table
+                hs = ops.slice_pack(h)
+                ms = timeit(lambda: ops.spmm_sliced(sh.csr, hs, Dl, _lib.GNNEA_ACT_RELU, out=y),
+                            args.reps)
+                ent["sliced"] = {"ms": round(ms, 4),
+                                 "GBps_gather_model": round(byt / ms / 1e6, 1)}
+                ent["ms"] = ent["sliced"]["ms"]
+                del hs
             per.append(ent)
             print(W, per[-1], flush=True)
             del sh, h, y
