@@ -269,8 +269,8 @@ template <int ACT, typename T>
 __global__ void k_highway_bwd(const T* __restrict__ dY, const T* __restrict__ S,
                               const T* __restrict__ Gt, const T* __restrict__ R, int64_t ld,
                               int64_t n_rows, int D, T* __restrict__ dS_pre, int64_t ld_ds,
-                              T* __restrict__ dgate, int64_t ld_dg, T* __restrict__ dresid,
-                              int64_t ld_dr) {
+                              int64_t cs_ds, T* __restrict__ dgate, int64_t ld_dg,
+                              T* __restrict__ dresid, int64_t ld_dr) {
   const int64_t n = n_rows * (int64_t)D;
   int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -279,7 +279,10 @@ __global__ void k_highway_bwd(const T* __restrict__ dY, const T* __restrict__ S,
     const int64_t i = r * ld + c;
     const float dy = to_f32<T>(dY[i]), s = to_f32<T>(S[i]), g = to_f32<T>(Gt[i]);
     const float x = to_f32<T>(R[i]);
-    dS_pre[r * ld_ds + c] = from_f32<T>(dy * g * act_grad_from_out<ACT>(s));
+    // dS_pre at (c / 64)·cs_ds + r·ld_ds + c % 64: cs_ds = 64 row-major, or the slice-major
+    // table the transposed sliced aggregation reads (ld_ds = 64, cs_ds = slice stride)
+    dS_pre[(c >> 6) * cs_ds + r * ld_ds + (c & 63)] =
+        from_f32<T>(dy * g * act_grad_from_out<ACT>(s));
     dgate[r * ld_dg + c] = from_f32<T>(dy * (s - x) * g * (1.f - g));
     if (dresid) dresid[r * ld_dr + c] = from_f32<T>(dy * (1.f - g));
   }
@@ -309,16 +312,17 @@ static int act_bwd_t(const T* dY, const T* Y, T* G, int64_t n, int act, hipStrea
 template <typename T>
 static int highway_bwd_t(const T* dY, const T* S, const T* G, const T* resid, int64_t ld,
                          int64_t n_rows, int32_t D, T* dS_pre, int64_t ld_ds, T* dgate,
-                         int64_t ld_dg, T* dresid, int64_t ld_dr, int act, hipStream_t s) {
-  if (n_rows < 0 || D < 0 || ld < D || ld_ds < D || ld_dg < D || (dresid && ld_dr < D))
-    return GNNEA_EINVAL;
+                         int64_t ld_dg, T* dresid, int64_t ld_dr, int act, hipStream_t s,
+                         int64_t cs_ds = 64) {
+  if (n_rows < 0 || D < 0 || ld < D || ld_dg < D || (dresid && ld_dr < D)) return GNNEA_EINVAL;
+  if (cs_ds == 64 ? ld_ds < D : (ld_ds != 64 || cs_ds < n_rows * 64)) return GNNEA_EINVAL;
   if (n_rows == 0 || D == 0) return 0;
   if (!dY || !S || !G || !resid || !dS_pre || !dgate) return GNNEA_EINVAL;
   const int64_t n = n_rows * (int64_t)D;
   const int nb = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
 #define GNNEA_HWB(A)                                                                         \
   hipLaunchKernelGGL((k_highway_bwd<A, T>), dim3(nb), dim3(256), 0, s, dY, S, G, resid, ld,  \
-                     n_rows, D, dS_pre, ld_ds, dgate, ld_dg, dresid, ld_dr)
+                     n_rows, D, dS_pre, ld_ds, cs_ds, dgate, ld_dg, dresid, ld_dr)
   switch (act) {
     case GNNEA_ACT_IDENTITY: GNNEA_HWB(GNNEA_ACT_IDENTITY); break;
     case GNNEA_ACT_RELU: GNNEA_HWB(GNNEA_ACT_RELU); break;
@@ -395,6 +399,18 @@ extern "C" int gnnea_highway_bwd_ld_f32(const float* dY, const float* S, const f
                                         float* dresid, int64_t ld_dr, int act, void* stream) {
   return highway_bwd_t<float>(dY, S, G, resid, ld, n_rows, D, dS_pre, ld_ds, dgate, ld_dg,
                               dresid, ld_dr, act, (hipStream_t)stream);
+}
+
+// dS_pre written slice-major ([ceil(D/64)][n_rows][64], slice stride sstride): the input of the
+// transposed sliced aggregation of the fused HighWay layer's backward
+extern "C" int gnnea_highway_bwd_sliced_f32(const float* dY, const float* S, const float* G,
+                                            const float* resid, int64_t ld, int64_t n_rows,
+                                            int32_t D, float* dS_s, int64_t sstride,
+                                            float* dgate, int64_t ld_dg, float* dresid,
+                                            int64_t ld_dr, int act, void* stream) {
+  if (sstride == 64) return GNNEA_EINVAL;  // 64 is the row-major code of the kernel
+  return highway_bwd_t<float>(dY, S, G, resid, ld, n_rows, D, dS_s, 64, dgate, ld_dg, dresid,
+                              ld_dr, act, (hipStream_t)stream, sstride);
 }
 
 // ---- bf16 storage (cfg-5) ------------------------------------------------------------------

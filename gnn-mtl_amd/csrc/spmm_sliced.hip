@@ -21,14 +21,31 @@ namespace gnnea {
 
 constexpr int kSliceW = 64;
 
-template <int ACT, int U>
+// HighWay epilogue operands (layers/layers.py:64-76): gate_pre is read from a slice-major table
+// at column offset goff (the fused HighWay layer's projection Z = x·[Wᵀ | K_g] is ONE sliced
+// table: hidden in columns [0, D), gate_pre in [D, 2D)); resid, S, g are row-major.
+struct SlicedHighway {
+  const float4* gate;  // slice-major table holding gate_pre (nullptr: plain act epilogue)
+  int64_t gsstride4;
+  int goff;
+  const float* bias;   // bias_gate (nullable)
+  const float* resid;
+  int64_t ldr;
+  float* save_s;
+  float* save_g;
+  int64_t lds;
+};
+
+__device__ __forceinline__ float sigm_f(float x) { return 1.f / (1.f + expf(-x)); }
+
+template <int ACT, int U, bool HW>
 __global__ __launch_bounds__(256) void k_spmm_sliced(const int32_t* __restrict__ rowptr,
                                                      const int32_t* __restrict__ col,
                                                      const float* __restrict__ val, int n_rows,
                                                      int nbs, int D,
                                                      const float4* __restrict__ Xs,
                                                      int64_t sstride4, float* __restrict__ Y,
-                                                     int64_t ldy) {
+                                                     int64_t ldy, SlicedHighway hw) {
   const int b = blockIdx.x;
   const int s = b / nbs;
   const int row = xcd_remap(b - s * nbs, nbs) * 4 + wave_id();
@@ -71,9 +88,30 @@ __global__ __launch_bounds__(256) void k_spmm_sliced(const int32_t* __restrict__
   acc.z += __shfl_xor(acc.z, 32, 64);
   acc.w += __shfl_xor(acc.w, 32, 64);
   if (g == 0 && own) {
-    const float4 o = make_float4(act_fwd<ACT>(acc.x), act_fwd<ACT>(acc.y), act_fwd<ACT>(acc.z),
-                                 act_fwd<ACT>(acc.w));
-    *(float4*)(Y + (int64_t)row * ldy + c0) = o;
+    const float4 sv = make_float4(act_fwd<ACT>(acc.x), act_fwd<ACT>(acc.y), act_fwd<ACT>(acc.z),
+                                  act_fwd<ACT>(acc.w));
+    if constexpr (!HW) {
+      *(float4*)(Y + (int64_t)row * ldy + c0) = sv;
+    } else {
+      const int gc = hw.goff + c0;  // gate_pre column in its table (multiple of 4)
+      float4 gp = hw.gate[(int64_t)(gc >> 6) * hw.gsstride4 + (int64_t)row * (kSliceW / 4) +
+                          ((gc & 63) >> 2)];
+      if (hw.bias) {
+        const float4 b = *(const float4*)(hw.bias + c0);
+        gp.x += b.x; gp.y += b.y; gp.z += b.z; gp.w += b.w;
+      }
+      const float4 gt = make_float4(sigm_f(gp.x), sigm_f(gp.y), sigm_f(gp.z), sigm_f(gp.w));
+      const float4 r = *(const float4*)(hw.resid + (int64_t)row * hw.ldr + c0);
+      // reference order: transform_gate * support + carry_gate * residual, carry = 1 - g
+      float4 o;
+      o.x = gt.x * sv.x + (1.f - gt.x) * r.x;
+      o.y = gt.y * sv.y + (1.f - gt.y) * r.y;
+      o.z = gt.z * sv.z + (1.f - gt.z) * r.z;
+      o.w = gt.w * sv.w + (1.f - gt.w) * r.w;
+      *(float4*)(Y + (int64_t)row * ldy + c0) = o;
+      if (hw.save_s) *(float4*)(hw.save_s + (int64_t)row * hw.lds + c0) = sv;
+      if (hw.save_g) *(float4*)(hw.save_g + (int64_t)row * hw.lds + c0) = gt;
+    }
   }
 }
 
@@ -100,7 +138,7 @@ __global__ __launch_bounds__(256) void k_slice_fill(const float4* __restrict__ d
   }
 }
 
-static bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+static bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }  // nullptr passes
 
 template <bool BWD>
 static int slice_fill(const float* dY, int64_t ld, const float* Y, int64_t ldo, int64_t n, int D,
@@ -134,21 +172,28 @@ static int slice_fill(const float* dY, int64_t ld, const float* Y, int64_t ldo, 
 
 using namespace gnnea;
 
-extern "C" int gnnea_spmm_sliced_f32(const int32_t* rowptr, const int32_t* col, const float* val,
-                                     int32_t n_rows, int32_t D, const float* Xs, int64_t sstride,
-                                     float* Y, int64_t ldy, int act, void* stream) {
+namespace gnnea {
+
+template <bool HW>
+static int spmm_sliced(const int32_t* rowptr, const int32_t* col, const float* val,
+                       int32_t n_rows, int32_t D, const float* Xs, int64_t sstride, float* Y,
+                       int64_t ldy, int act, const SlicedHighway& hw, hipStream_t s) {
   if (n_rows < 0 || D < 0) return GNNEA_EINVAL;
   if (n_rows == 0 || D == 0) return 0;
   if (!rowptr || !col || !val || !Xs || !Y) return GNNEA_EINVAL;
   if (D % 4 || ldy % 4 || ldy < D || sstride % 4 || sstride < kSliceW || !al16(Xs) || !al16(Y))
     return GNNEA_EINVAL;
+  if (HW && (!hw.gate || !hw.resid || hw.goff < 0 || hw.goff % 4 || hw.gsstride4 < kSliceW / 4 ||
+             hw.ldr % 4 || hw.ldr < D || !al16(hw.gate) || !al16(hw.resid) || !al16(hw.bias) ||
+             ((hw.save_s || hw.save_g) && (hw.lds % 4 || hw.lds < D)) || !al16(hw.save_s) ||
+             !al16(hw.save_g)))
+    return GNNEA_EINVAL;
   const int nbs = (n_rows + 3) / 4;
   const int S = (D + kSliceW - 1) / kSliceW;
   if ((int64_t)nbs * S >= (1ll << 31)) return GNNEA_EINVAL;
-  hipStream_t s = (hipStream_t)stream;
 #define GNNEA_SS(A)                                                                            \
-  hipLaunchKernelGGL((k_spmm_sliced<A, 4>), dim3(nbs * S), dim3(256), 0, s, rowptr, col, val,  \
-                     n_rows, nbs, D, (const float4*)Xs, sstride / 4, Y, ldy)
+  hipLaunchKernelGGL((k_spmm_sliced<A, 4, HW>), dim3(nbs * S), dim3(256), 0, s, rowptr, col,   \
+                     val, n_rows, nbs, D, (const float4*)Xs, sstride / 4, Y, ldy, hw)
   switch (act) {
     case GNNEA_ACT_IDENTITY: GNNEA_SS(GNNEA_ACT_IDENTITY); break;
     case GNNEA_ACT_RELU: GNNEA_SS(GNNEA_ACT_RELU); break;
@@ -161,6 +206,31 @@ extern "C" int gnnea_spmm_sliced_f32(const int32_t* rowptr, const int32_t* col, 
 #undef GNNEA_SS
   GNNEA_LAUNCH_CHECK();
   return 0;
+}
+
+}  // namespace gnnea
+
+extern "C" int gnnea_spmm_sliced_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                                     int32_t n_rows, int32_t D, const float* Xs, int64_t sstride,
+                                     float* Y, int64_t ldy, int act, void* stream) {
+  const SlicedHighway none{nullptr, 0, 0, nullptr, nullptr, 0, nullptr, nullptr, 0};
+  return spmm_sliced<false>(rowptr, col, val, n_rows, D, Xs, sstride, Y, ldy, act, none,
+                            (hipStream_t)stream);
+}
+
+extern "C" int gnnea_spmm_highway_sliced_f32(const int32_t* rowptr, const int32_t* col,
+                                             const float* val, int32_t n_rows, int32_t D,
+                                             const float* Xs, int64_t sstride,
+                                             const float* gate_s, int64_t gsstride,
+                                             int32_t goff, const float* bias_gate,
+                                             const float* resid, int64_t ldr, float* Y,
+                                             int64_t ldy, float* save_s, float* save_g,
+                                             int64_t lds, int act, void* stream) {
+  if (gsstride % 4) return GNNEA_EINVAL;
+  const SlicedHighway hw{(const float4*)gate_s, gsstride / 4, goff, bias_gate, resid, ldr,
+                         save_s, save_g, lds};
+  return spmm_sliced<true>(rowptr, col, val, n_rows, D, Xs, sstride, Y, ldy, act, hw,
+                           (hipStream_t)stream);
 }
 
 extern "C" int gnnea_slice_pack_f32(const float* X, int64_t ldx, int64_t n, int32_t D,

@@ -162,6 +162,25 @@ class DistAdj:
         full, _ = self.halo(hidden)
         return self.engine.highway_fwd(self.csr, full, gate_pre, resid, bias_gate, act)
 
+    def local_csr(self):
+        """The shard's CSR when this rank aggregates without any exchange (one KG per rank, or
+        the whole graph at world 1) on the HIP engine, else None."""
+        return self.csr if self.part.g == 1 and isinstance(self.engine, HipEngine) else None
+
+    def sliced_ok(self, D, dtype):
+        """Slice-major fused HighWay layer: only without exchange (the halo moves row-major
+        rows)."""
+        from .ops import use_sliced
+        return self.local_csr() is not None and use_sliced(self.csr.n_cols, D, dtype)
+
+    def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act):
+        from . import ops
+        return ops.highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act)
+
+    def aggregate_t_sliced(self, gs, D, out):
+        from . import ops
+        return ops.spmm_sliced(self.csr.transpose(), gs, D, out=out)
+
     def aggregate_t(self, g, out):
         """out = (A_shardᵀ·g) summed over the KG group, this rank's rows (HighwayLayerFn's
         backward hook; out may be a column block of a wider buffer)."""

@@ -432,12 +432,20 @@ class GCNLayerFn(torch.autograd.Function):
 
 
 def gcn_layer(adj, x, weight, bias, act_fn):
-    """Fused GCN layer (GCNLayerFn) when the slice-major path applies, else None."""
+    """Fused GCN layer (GCNLayerFn) when the slice-major path applies, else None.  ``adj``: the
+    reference's sparse adjacency, or a DistAdj whose rank aggregates without exchange."""
     code = act_code(act_fn)
-    if code is None or not getattr(adj, "is_sparse", False) or x.dtype != torch.float32 or \
-            weight.dtype != torch.float32 or x.shape[1] != weight.shape[1]:
+    if code is None or x.dtype != torch.float32 or weight.dtype != torch.float32 or \
+            x.shape[1] != weight.shape[1]:
         return None
-    csr = csr_of(adj)
+    if hasattr(adj, "local_csr"):
+        csr = adj.local_csr()
+        if csr is None:
+            return None
+    elif getattr(adj, "is_sparse", False):
+        csr = csr_of(adj)
+    else:
+        return None
     if not use_sliced(csr.n_cols, weight.shape[0], torch.float32) or x.shape[0] != csr.n_cols:
         return None
     return GCNLayerFn.apply(_rows(x), weight, bias, csr, code)
@@ -527,6 +535,48 @@ class HighwayFn(torch.autograd.Function):
         return dh, dgate, dres, None, None, None
 
 
+def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act):
+    """HighWay tail over the slice-major projection table Zs ([S, N, 64] holding x·[Wᵀ | K_g] +
+    [b | 0]: hidden in columns [0, D), gate_pre in [D, 2D)), per diagonal block
+    (gnnea_spmm_highway_sliced_f32).  Returns (out, S, g), row-major."""
+    resid = _rows(resid, torch.float32)
+    N = csr.n_rows
+    if Zs.dim() != 3 or Zs.shape[2] != SLICE_W or Zs.shape[1] < csr.n_cols or \
+            Zs.shape[0] * SLICE_W < 2 * D or resid.shape != (N, D):
+        raise ValueError("gnnea.highway_sliced: shape mismatch")
+    out = torch.empty((N, D), dtype=torch.float32, device=Zs.device)
+    S = torch.empty_like(out)
+    G = torch.empty_like(out)
+    bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
+    L = _lib.lib()
+    with torch.cuda.device(Zs.device):
+        for r0, r1 in csr.row_blocks():
+            check(L.gnnea_spmm_highway_sliced_f32(
+                _off32(csr.rowptr, r0), ptr(csr.col), ptr(csr.val), r1 - r0, D, ptr(Zs),
+                Zs.stride(0), ctypes.c_void_p(Zs.data_ptr() + 4 * r0 * SLICE_W), Zs.stride(0),
+                D, ptr(bias), _off(resid, r0), resid.stride(0), _off(out, r0), out.stride(0),
+                _off(S, r0), _off(G, r0), S.stride(0), int(act), stream_of(Zs.device)))
+    return out, S, G
+
+
+def highway_bwd_sliced(dy, S, G, resid, act, want_dresid, dgate):
+    """highway_bwd with dS_pre written slice-major (gnnea_highway_bwd_sliced_f32); dgate is a
+    caller-provided row-major (column-block) buffer.  Returns (dS slices, dresid or None)."""
+    S = _featc(S)
+    dy = _featc(dy, S.dtype)
+    G = _featc(G, S.dtype)
+    resid = _featc(resid, S.dtype)
+    N, D = S.shape
+    dSs = sliced_empty(N, D, S.device)
+    dres = torch.empty_like(S) if want_dresid else None
+    with torch.cuda.device(S.device):
+        check(_lib.lib().gnnea_highway_bwd_sliced_f32(
+            ptr(dy), ptr(S), ptr(G), ptr(resid), S.stride(0), N, D, ptr(dSs), dSs.stride(0),
+            ptr(dgate), _ld(dgate), ptr(dres), _ld(dres) if want_dresid else D, int(act),
+            stream_of(S.device)))
+    return dSs, dres
+
+
 def colsum(t):
     """Column sums of a row-major [N, D] matrix (the bias gradient), as a [1,N]·[N,D] GEMM."""
     ones = torch.ones((1, t.shape[0]), dtype=t.dtype, device=t.device)
@@ -550,8 +600,15 @@ class HighwayLayerFn(torch.autograd.Function):
         D = weight.shape[0]
         wcat = torch.cat([weight.t(), kernel_gate.to(weight.dtype)], dim=1)  # [Din, 2D]
         bcat = torch.cat([bias, torch.zeros_like(bias)]) if bias is not None else None
-        Z = gemm(x, wcat, bias=bcat)
-        out, S, G = agg.highway_fwd(Z[:, :D], Z[:, D:], x, bias_gate, act)
+        ctx.sliced = agg.sliced_ok(D, x.dtype)
+        if ctx.sliced:
+            # above the Infinity Cache: Z written slice-major by the GEMM, the HighWay SpMM
+            # gathers the hidden slices and reads gate_pre from the same table at offset D
+            Zs = gemm_sliced(x, wcat.t(), bcat)
+            out, S, G = agg.highway_fwd_sliced(Zs, D, x, bias_gate, act)
+        else:
+            Z = gemm(x, wcat, bias=bcat)
+            out, S, G = agg.highway_fwd(Z[:, :D], Z[:, D:], x, bias_gate, act)
         ctx.agg, ctx.act = agg, act
         ctx.save_for_backward(x, weight, kernel_gate, S, G)
         return out
@@ -562,8 +619,12 @@ class HighwayLayerFn(torch.autograd.Function):
         N, D = S.shape
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         P = torch.empty((N, 2 * D), dtype=S.dtype, device=S.device)
-        dS, _, dres = highway_bwd(dy, S, G, x, ctx.act, want_dresid=need_x, dgate=P[:, D:])
-        ctx.agg.aggregate_t(dS, P[:, :D])
+        if ctx.sliced:
+            dSs, dres = highway_bwd_sliced(dy, S, G, x, ctx.act, need_x, P[:, D:])
+            ctx.agg.aggregate_t_sliced(dSs, D, P[:, :D])
+        else:
+            dS, _, dres = highway_bwd(dy, S, G, x, ctx.act, want_dresid=need_x, dgate=P[:, D:])
+            ctx.agg.aggregate_t(dS, P[:, :D])
         dh = P[:, :D]
         dx = dw = db = None
         if need_x:
@@ -589,6 +650,15 @@ class LocalAgg:
     def aggregate_t(self, g, out):
         """out = Aᵀ·g (out may be a column block of a wider buffer)."""
         return spmm(self.csr.transpose(), g, out=out)
+
+    def sliced_ok(self, D, dtype):
+        return use_sliced(self.csr.n_cols, D, dtype)
+
+    def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act):
+        return highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act)
+
+    def aggregate_t_sliced(self, gs, D, out):
+        return spmm_sliced(self.csr.transpose(), gs, D, out=out)
 
 
 def highway_layer(adj, x, weight, bias, kernel_gate, bias_gate, act_fn):

@@ -55,7 +55,7 @@ class GraphConvolution(Module):
     def forward(self, input):
         x, adj = input
         x = dense_of(x)
-        if not isinstance(adj, DistAdj) and adj.is_sparse and \
+        if (isinstance(adj, DistAdj) or adj.is_sparse) and \
                 (self.dropout == 0 or not self.training):
             out = ops.gcn_layer(adj, x, self.linear.weight, self.linear.bias, self.act)
             if out is not None:  # hidden kept slice-major (gnnea.ops.GCNLayerFn)

@@ -91,6 +91,22 @@ int gnnea_spmm_csr_beta_f32(const int32_t* rowptr, const int32_t* col, const flo
 int gnnea_spmm_sliced_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                           int32_t n_rows, int32_t D, const float* Xs, int64_t sstride, float* Y,
                           int64_t ldy, int act, void* stream);
+/* HighWay layer over a slice-major projection (layers/layers.py:64-76): S = act(A·X) with X the
+ * first D columns of the table Xs, g = sigmoid(gate_pre + bias_gate) with gate_pre read from
+ * the slice-major table gate_s at column offset goff (the fused layer's ONE projection table
+ * Z = x·[W^T | K_g]: gate_s = Xs, goff = D), Y = g*S + (1-g)*resid; resid, Y, S, g row-major. */
+int gnnea_spmm_highway_sliced_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                                  int32_t n_rows, int32_t D, const float* Xs, int64_t sstride,
+                                  const float* gate_s, int64_t gsstride, int32_t goff,
+                                  const float* bias_gate, const float* resid, int64_t ldr,
+                                  float* Y, int64_t ldy, float* save_s, float* save_g,
+                                  int64_t lds, int act, void* stream);
+/* gnnea_highway_bwd_ld_f32 with dS_pre written slice-major (slice stride sstride >= n_rows*64):
+ * the input of the transposed sliced aggregation */
+int gnnea_highway_bwd_sliced_f32(const float* dY, const float* S, const float* G,
+                                 const float* resid, int64_t ld, int64_t n_rows, int32_t D,
+                                 float* dS_s, int64_t sstride, float* dgate, int64_t ld_dg,
+                                 float* dresid, int64_t ld_dr, int act, void* stream);
 /* row-major [n, D] (row stride ldx) -> slice-major table (the drop-in path for a row-major
  * hidden that no gnnea GEMM produced) */
 int gnnea_slice_pack_f32(const float* X, int64_t ldx, int64_t n, int32_t D, float* Xs,

@@ -164,3 +164,87 @@ def test_aggregate_sliced_matches_rowmajor_two_kg(device, monkeypatch):
     y_r, g_r = run()
     assert rel_err(y_s.cpu(), y_r.cpu()) < TOL32
     assert rel_err(g_s.cpu(), g_r.cpu()) < TOL32
+
+
+@pytest.mark.parametrize("act", [F.relu, torch.tanh])
+def test_highway_layer_sliced_matches_rowmajor(device, monkeypatch, act):
+    """HighWayGraphConvolution through the fused layer with the projection Z = x·[Wᵀ | K_g]
+    written slice-major (hidden and gate_pre in ONE table), the sliced HighWay SpMM, dS written
+    slice-major and the transposed sliced aggregation, against the row-major fused layer:
+    output, dx, dW, db."""
+    from gnnea import ops
+    from layers.layers import HighWayGraphConvolution
+    rng = np.random.default_rng(8)
+    n = 1500
+    r, c, v, csr = _graph(rng, n, 12000, device)
+    idx = torch.from_numpy(np.stack([r, c]).astype(np.int64))
+    adj = torch.sparse_coo_tensor(idx, torch.from_numpy(v), (n, n)).to(device)
+    torch.manual_seed(1)
+    layer = HighWayGraphConvolution(300, 300, 0.0, act, True, 0, device).to(device)
+    layer.bias_gate = torch.randn(300, device=device) * 0.1
+    x = torch.from_numpy(rng.standard_normal((n, 300)).astype(np.float32) * 0.1).to(device)
+    R = torch.randn(n, 300, device=device)
+
+    def run():
+        layer.zero_grad()
+        xx = x.clone().requires_grad_(True)
+        out, _ = layer((xx, adj))
+        (out * R).sum().backward()
+        return [out.detach(), xx.grad, layer.linear.weight.grad.clone(),
+                layer.linear.bias.grad.clone()]
+    calls = []
+    orig = ops.highway_fwd_sliced
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+    monkeypatch.setattr(ops, "highway_fwd_sliced", spy)
+    monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 0)  # force the sliced path at test size
+    got = run()
+    assert calls, "the sliced HighWay layer was not used"
+    monkeypatch.setattr(ops, "SLICED", False)
+    ref = run()
+    assert len(calls) == 1
+    for g, w in zip(got, ref):
+        assert rel_err(g.cpu(), w.cpu()) < TOL32
+
+
+def test_distadj_world1_takes_sliced_layers(device, monkeypatch):
+    """A DistAdj whose rank aggregates without exchange (world 1: the whole graph) runs the
+    fused slice-major GCN and HighWay layers; results match the row-major layers on the
+    reference sparse adjacency."""
+    from gnnea import ops, synth
+    from gnnea.dist_graph import DistAdj
+    from layers.layers import GraphConvolution, HighWayGraphConvolution
+    n, t = 600, 2400
+    tr = synth.kg_pair_triples(n, t, 30)
+    dadj = DistAdj.from_triples(tr, n, t, 0, 1, device)
+    R, C, V = synth.adjacency_coo(tr, 2 * n, reference_order=False)
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([R, C])).long(),
+                                  torch.from_numpy(V), (2 * n, 2 * n)).to(device)
+    torch.manual_seed(2)
+    l1 = GraphConvolution(300, 300, 0.0, F.relu, True).to(device)
+    l2 = HighWayGraphConvolution(300, 300, 0.0, F.relu, True, 0, device).to(device)
+    x = torch.from_numpy(synth.features(2 * n, 300, seed=4)).to(device)
+    Rw = torch.randn(2 * n, 300, device=device)
+    used = []
+    for name in ("gemm_sliced", "highway_fwd_sliced"):
+        orig = getattr(ops, name)
+        monkeypatch.setattr(ops, name, (lambda f, nm: lambda *a, **k: (used.append(nm),
+                                                                        f(*a, **k))[1])(orig, name))
+
+    def run(a):
+        l1.zero_grad()
+        l2.zero_grad()
+        xx = x.clone().requires_grad_(True)
+        out = l2(l1((xx, a)))[0]
+        (out * Rw).sum().backward()
+        return [out.detach(), xx.grad] + [p.grad.clone() for p in
+                                          list(l1.parameters()) + list(l2.parameters())]
+    monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 0)
+    got = run(dadj)
+    assert {"gemm_sliced", "highway_fwd_sliced"} <= set(used)
+    monkeypatch.setattr(ops, "SLICED", False)
+    ref = run(adj)
+    for g, w in zip(got, ref):
+        assert rel_err(g.cpu(), w.cpu()) < TOL32
