@@ -27,15 +27,15 @@ from gnnea import synth  # noqa: E402
 from gnnea.dist_graph import DistAdj, allreduce_grads  # noqa: E402
 
 
-def build(model, n, rank, world, device, seed=10086):
+def build(model, n, rank, world, device, seed=10086, dtype=torch.float32):
     from models.decoders import model2decoder
     from models.encoders import model2encoder
     a = types.SimpleNamespace(model=model, num_layers=3, dim=300, act="relu", dropout=0.0,
                               bias=1, n_heads=4, alpha=0.2, feat_dim=300, n_classes=300,
                               cuda=0, device=device)
     torch.manual_seed(seed)  # replicated weights on every rank (run/train_ea.py:10)
-    enc = model2encoder[model](a).to(device)
-    dec = model2decoder[model](a).to(device)
+    enc = model2encoder[model](a).to(device=device, dtype=dtype)
+    dec = model2decoder[model](a).to(device=device, dtype=dtype)
     t = synth.CONFIGS["cfg4"]["t"] if n == synth.CONFIGS["cfg4"]["n"] else 10 * n
     tr = synth.kg_pair_triples(n, t, synth.CONFIGS["cfg4"]["n_rel"])
     dadj = DistAdj.from_triples(tr, n, t, rank, world, device)
@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--entities", type=int, default=synth.CONFIGS["cfg4"]["n"])
+    ap.add_argument("--dtype", default="f32", choices=("f32", "bf16"),
+                    help="feature / weight storage (bf16: configs[4]'s dtype, fp32 arithmetic)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -56,7 +58,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    res = measure(args.model, args.entities, rank, world, dev, args.steps, args.warmup)
+    res = measure(args.model, args.entities, rank, world, dev, args.steps, args.warmup,
+                  torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -64,16 +67,17 @@ def main():
         dist.destroy_process_group()
 
 
-def measure(model, n, rank, world, dev, steps, warmup):
+def measure(model, n, rank, world, dev, steps, warmup, dtype=torch.float32):
     """Time `steps` sharded training steps (after `warmup`), max over ranks; returns the summary
     (the same dict on every rank).  Every rank runs the same collective sequence."""
     t0 = time.time()
-    enc, dec, dadj = build(model, n, rank, world, dev)
+    enc, dec, dadj = build(model, n, rank, world, dev, dtype=dtype)
     part = dadj.part
     g = torch.Generator(device=dev).manual_seed(1 + rank)
     x = torch.randn(part.n_rows, 300, device=dev, generator=g)
     x /= x.norm(dim=1, keepdim=True)
     dy = torch.randn(part.n_rows, 300, device=dev, generator=g)
+    x, dy = x.to(dtype), dy.to(dtype)
     params = list(enc.parameters()) + list(dec.parameters())
     print("rank %d: %d rows, %d nnz, setup %.1fs" % (rank, part.n_rows, dadj.nnz,
                                                      time.time() - t0), file=sys.stderr)
@@ -101,13 +105,17 @@ def measure(model, n, rank, world, dev, steps, warmup):
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     ms = float(el) / steps * 1e3
-    cfg4 = n == synth.CONFIGS["cfg4"]["n"]
+    nnz = torch.tensor([float(dadj.nnz)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(nnz)  # row shards: every edge of the graph once
     return {"metric": "EA encoder training steps/s", "model": model + "-EA (encode + decode, "
             "3 graph convolutions, fwd + bwd + gradient all-reduce)",
+            "graph": "2x%d entities, %d nnz" % (n, int(nnz)),
+            "dtype": "bf16 storage, f32 arithmetic" if dtype == torch.bfloat16 else "f32",
             "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 3),
             "steps_per_s": round(1e3 / ms, 2),
             # 3 aggregations forward + 3 transposed aggregations backward per step
-            "edges_per_s_fwd_bwd": round(6 * 41999552 / ms * 1e3, 1) if cfg4 else None,
+            "edges_per_s_fwd_bwd": round(6 * float(nnz) / ms * 1e3, 1),
             "partition": "single GPU" if world == 1 else
             "rows: 2 KG groups of %d GPUs, RCCL halo all-gather (fwd) + reduce-scatter (bwd) "
             "per layer, one-bucket gradient all-reduce" % part.g}
