@@ -1,0 +1,141 @@
+// a7. GAT attention-vector gradient (autograd of att_layers.py:38, a·[h_i || h_j]):
+//   da1[h] = Σ_i ds1[i,h] · H[i, h-block],   da2[h] = Σ_j ds2[j,h] · H[j, h-block]
+// i.e. out[c] = Σ_r ds[r, c / d_head] · H[r, c] for every column c of the head-concatenated H.
+// One streaming pass over H (N·D·s bytes, HBM bound) instead of an [N, heads]ᵀ·[N, D] GEMM whose
+// off-diagonal head blocks are thrown away: stage 1, a fixed grid of workgroups each sums a
+// contiguous row range into registers (4 waves on interleaved rows, lane = float4 column chunk),
+// combined across the waves in LDS into one partial row per workgroup; stage 2 adds the
+// workgroup partials in workgroup order (deterministic, no atomics).
+#include "common.h"
+
+namespace gnnea {
+
+constexpr int kDaBlocks = 1024;
+
+template <int NCH, typename T>
+__global__ __launch_bounds__(256) void k_gat_da_part(const typename Vec4<T>::raw* __restrict__ H,
+                                                     int64_t ldh4, int64_t n_rows, int heads,
+                                                     int d_head, int D4,
+                                                     const float* __restrict__ ds,
+                                                     float* __restrict__ part) {
+  __shared__ float4 red[4][64 * NCH];
+  const int w = wave_id(), lane = lane_id();
+  const int64_t rpb = (n_rows + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(n_rows, r0 + rpb);
+  float4 acc[NCH];
+  int hd[NCH][4];
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int c = 4 * (lane + 64 * q) + t;
+      hd[q][t] = min(c / d_head, heads - 1);
+    }
+  }
+  for (int64_t r = r0 + w; r < r1; r += 4) {
+    const float* dr = ds + r * heads;
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+      const int c4 = lane + 64 * q;
+      if (c4 < D4) {
+        const float4 h = Vec4<T>::get(H[r * ldh4 + c4]);
+        acc[q].x = fmaf(dr[hd[q][0]], h.x, acc[q].x);
+        acc[q].y = fmaf(dr[hd[q][1]], h.y, acc[q].y);
+        acc[q].z = fmaf(dr[hd[q][2]], h.z, acc[q].z);
+        acc[q].w = fmaf(dr[hd[q][3]], h.w, acc[q].w);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) red[w][lane + 64 * q] = acc[q];
+  __syncthreads();
+  for (int c4 = threadIdx.x; c4 < D4; c4 += 256) {
+    float4 s = red[0][c4];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 o = red[k][c4];
+      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+    }
+    ((float4*)part)[(int64_t)blockIdx.x * D4 + c4] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gat_da_final(const float* __restrict__ part, int nb,
+                                                      int D, float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= D) return;
+  float s0 = 0.f, s1 = 0.f;
+  int b = 0;
+  for (; b + 2 <= nb; b += 2) {
+    s0 += part[(int64_t)b * ((D + 3) & ~3) + c];
+    s1 += part[(int64_t)(b + 1) * ((D + 3) & ~3) + c];
+  }
+  if (b < nb) s0 += part[(int64_t)b * ((D + 3) & ~3) + c];
+  out[c] = s0 + s1;
+}
+
+static int da_blocks(int64_t n_rows) {
+  const int64_t b = (n_rows + 63) / 64;  // >= 64 rows per workgroup
+  return (int)(b < 1 ? 1 : (b > kDaBlocks ? kDaBlocks : b));
+}
+
+template <typename T>
+static int gat_da_t(const T* H, int64_t ldh, int64_t n_rows, int heads, int d_head,
+                    const float* ds, float* out, void* ws, int64_t ws_bytes, hipStream_t s) {
+  if (n_rows < 0 || heads < 1 || d_head < 1) return GNNEA_EINVAL;
+  const int D = heads * d_head;
+  if (!out) return GNNEA_EINVAL;
+  if (n_rows == 0) return (int)hipMemsetAsync(out, 0, sizeof(float) * D, s);
+  // rows are read as whole 4-element vectors up to Dp = roundup4(D) (the GAT layer pads H so);
+  // the columns past D are summed into the partials but never written out
+  const int Dp = (D + 3) & ~3;
+  if (!H || !ds || ldh % 4 || ldh < Dp ||
+      (((uintptr_t)H) & (sizeof(typename Vec4<T>::raw) - 1)))
+    return GNNEA_EINVAL;
+  const int D4 = Dp / 4, nch = (D4 + 63) / 64;
+  const int nb = da_blocks(n_rows);
+  if (!ws || ws_bytes < (int64_t)nb * Dp * 4) return GNNEA_EWORKSPACE;
+  float* part = (float*)ws;
+  typedef typename Vec4<T>::raw R;
+#define GNNEA_DA(N)                                                                            \
+  case N:                                                                                      \
+    hipLaunchKernelGGL((k_gat_da_part<N, T>), dim3(nb), dim3(256), 0, s, (const R*)H, ldh / 4,  \
+                       n_rows, heads, d_head, D4, ds, part);                                   \
+    break;
+  switch (nch) {
+    GNNEA_DA(1)
+    GNNEA_DA(2)
+    GNNEA_DA(3)
+    GNNEA_DA(4)
+    default: return GNNEA_EINVAL;
+  }
+#undef GNNEA_DA
+  GNNEA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_gat_da_final, dim3((D + 255) / 256), dim3(256), 0, s, part, nb, D, out);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace gnnea
+
+using namespace gnnea;
+
+extern "C" int64_t gnnea_gat_da_ws_bytes(int64_t n_rows, int32_t D) {
+  if (n_rows < 0 || D < 0) return GNNEA_EINVAL;
+  return (int64_t)da_blocks(n_rows) * ((D + 3) & ~3) * 4;
+}
+
+extern "C" int gnnea_gat_da_f32(const float* H, int64_t ldh, int64_t n_rows, int heads,
+                                int d_head, const float* ds, float* out, void* ws,
+                                int64_t ws_bytes, void* stream) {
+  return gat_da_t<float>(H, ldh, n_rows, heads, d_head, ds, out, ws, ws_bytes,
+                         (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_da_bf16(const void* H, int64_t ldh, int64_t n_rows, int heads,
+                                 int d_head, const float* ds, float* out, void* ws,
+                                 int64_t ws_bytes, void* stream) {
+  return gat_da_t<bf16_t>((const bf16_t*)H, ldh, n_rows, heads, d_head, ds, out, ws, ws_bytes,
+                          (hipStream_t)stream);
+}

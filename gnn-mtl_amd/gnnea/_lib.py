@@ -119,6 +119,11 @@ SIGNATURES = {
                                              _i64, _p, _p]),
     "gnnea_gat_bwd_dst_bf16": (ctypes.c_int, [_p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,
                                              _i64, _p, _p]),
+    "gnnea_gat_da_ws_bytes": (_i64, [_i64, _i32]),
+    "gnnea_gat_da_f32": (ctypes.c_int, [_p, _i64, _i64, ctypes.c_int, ctypes.c_int, _p, _p, _p,
+                                        _i64, _p]),
+    "gnnea_gat_da_bf16": (ctypes.c_int, [_p, _i64, _i64, ctypes.c_int, ctypes.c_int, _p, _p, _p,
+                                         _i64, _p]),
     "gnnea_gemm_ws_bytes": (_i64, [_i64, _i64, _i64]),
     "gnnea_gemm_bf16_ws_bytes": (_i64, [_i64, _i64, _i64]),
     "gnnea_gemm_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,

@@ -784,14 +784,28 @@ def gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha, act, 
             dH.stride(0), ptr(ds1), st))
     da = None
     if need_da:
-        # da1[h] = sum_i ds1[i,h] H_{row0+i},h ; da2[h] = sum_j ds2[j,h] H_j,h  (MFMA, split-K)
-        p1 = gemm(ds1, H[row0:row0 + N, :D], trans_a=True, out_dtype=torch.float32)
-        p2 = gemm(ds2, H[:, :D], trans_a=True, out_dtype=torch.float32)
-        p1 = p1.view(heads, heads, d_head)
-        p2 = p2.view(heads, heads, d_head)
-        idx = torch.arange(heads, device=H.device)
-        da = torch.cat([p1[idx, idx], p2[idx, idx]], dim=1)
+        # da1[h] = sum_i ds1[i,h] H_{row0+i},h ; da2[h] = sum_j ds2[j,h] H_j,h: one streaming
+        # pass over H each (gnnea_gat_da_*), only the diagonal head blocks
+        p1 = gat_da(H[row0:row0 + N], ds1, heads, d_head)
+        p2 = gat_da(H, ds2, heads, d_head)
+        da = torch.cat([p1.view(heads, d_head), p2.view(heads, d_head)], dim=1)
     return dH, da
+
+
+def gat_da(H, ds, heads, d_head):
+    """out[c] = sum_r ds[r, c // d_head] * H[r, c] (fp32, heads*d_head values)."""
+    L = _lib.lib()
+    n = H.shape[0]
+    D = heads * d_head
+    ws_bytes = int(L.gnnea_gat_da_ws_bytes(n, D))
+    ws = _gemm_ws(H.device, ws_bytes)
+    out = torch.empty(D, dtype=torch.float32, device=H.device)
+    ds = _featc(ds, torch.float32)
+    with torch.cuda.device(H.device):
+        check(_gat_fn("gnnea_gat_da", H.dtype)(ptr(H), H.stride(0), n, heads, d_head, ptr(ds),
+                                               ptr(out), ptr(ws), ws_bytes,
+                                               stream_of(H.device)))
+    return out
 
 
 class GATFn(torch.autograd.Function):

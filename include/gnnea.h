@@ -202,6 +202,17 @@ int gnnea_gat_bwd_dst_f32(const int32_t* rowptr, const int64_t* tpos, int32_t n_
                           int d_head, const float* dzT, const float* a, float* dH, int64_t lddh,
                           float* ds1, void* stream);
 
+/* attention-vector gradient pieces (autograd of att_layers.py:38): out[c] = sum_r ds[r, c/d_head]
+ * * H[r, c] over the n_rows rows of H (ds: n_rows x heads fp32, ds1 or ds2 of the backward),
+ * c < heads*d_head; one streaming pass over H, deterministic two-stage sum.  H rows are read as
+ * 4-element vectors up to roundup4(heads*d_head) (ldh >= that, % 4 == 0, aligned).
+ * Workspace from gnnea_gat_da_ws_bytes. */
+int64_t gnnea_gat_da_ws_bytes(int64_t n_rows, int32_t D);
+int gnnea_gat_da_f32(const float* H, int64_t ldh, int64_t n_rows, int heads, int d_head,
+                     const float* ds, float* out, void* ws, int64_t ws_bytes, void* stream);
+int gnnea_gat_da_bf16(const void* H, int64_t ldh, int64_t n_rows, int heads, int d_head,
+                      const float* ds, float* out, void* ws, int64_t ws_bytes, void* stream);
+
 /* bf16 feature storage (cfg-5): H, Y, dY, G, dH are bf16 (void*, row strides % 4 == 0, 8-B
  * aligned); s1, s2, m, den, rec, dzT, ds1, ds2, a and edge_mask stay fp32; arithmetic is fp32 and
  * every bf16 output is rounded once (nearest even). */

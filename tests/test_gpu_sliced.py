@@ -154,9 +154,9 @@ def test_aggregate_sliced_matches_rowmajor_two_kg(device, monkeypatch):
     assert ops.use_sliced(2 * n, 128, torch.float32)
     dy = torch.randn(2 * n, 128, device=device)
 
-    def run():
+    def run():  # tanh: relu's derivative flips on pre-activations within rounding of 0
         hh = h.clone().requires_grad_(True)
-        y = ops.AggregateFn.apply(hh, csr, 1)
+        y = ops.AggregateFn.apply(hh, csr, 5)
         (g,) = torch.autograd.grad(y, (hh,), dy)
         return y.detach(), g
     y_s, g_s = run()
