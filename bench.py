@@ -93,26 +93,29 @@ def sinkhorn_rate(device, B=3000, reg=0.01):
 
 
 def bf16_rate(shard, H, steps):
-    """The same aggregation with bf16 feature storage (cfg-5's dtype, fp32 arithmetic)."""
+    """The same aggregation with bf16 feature storage (cfg-5's dtype, fp32 arithmetic): the
+    table slice-major (128-column slices, as gnnea_gemm_sliced_bf16 writes it) where it applies,
+    the row-major kernel beside it."""
     Hb = H.to(torch.bfloat16)
     Yb = torch.empty((shard.n_rows, H.shape[1]), dtype=torch.bfloat16, device=H.device)
-    for _ in range(3):
-        ops.spmm(shard.csr, Hb, _lib.GNNEA_ACT_RELU, out=Yb)
-    torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(steps):
-        ops.spmm(shard.csr, Hb, _lib.GNNEA_ACT_RELU, out=Yb)
-    b.record()
-    torch.cuda.synchronize()
-    ms = a.elapsed_time(b) / steps
+    relu = _lib.GNNEA_ACT_RELU
+    sliced = ops.use_sliced(shard.n_cols, H.shape[1], torch.bfloat16)
+    ms_row = _timed(lambda: ops.spmm(shard.csr, Hb, relu, out=Yb), steps)
+    if sliced:
+        Hs = ops.slice_pack(Hb)
+        ms = _timed(lambda: ops.spmm_sliced(shard.csr, Hs, H.shape[1], relu, out=Yb), steps)
+    else:
+        ms = ms_row
     traffic = gather_model_bytes(shard.n_rows, shard.nnz, H.shape[1], elem=2)
     achieved = traffic / (ms * 1e-3) / 1e9
     return {"value": round(shard.nnz / ms * 1e3, 1), "unit": "edges/s", "ms_per_step": round(ms, 4),
             "dtype": "bf16 storage, f32 accumulate", "steps": steps,
+            "layout": "slice-major (128-column slices)" if sliced else "row-major",
+            "rowmajor_edges_per_s": round(shard.nnz / ms_row * 1e3, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "kernel": "gnnea::k_spmm_v4<relu,act,2,bf16,bf16>",
+                         "kernel": ("gnnea::k_spmm_sliced<relu,4,bf16,bf16>" if sliced else
+                                    "gnnea::k_spmm_v4<relu,act,2,bf16,bf16>"),
                          "model": "gather: 4(N+1)+8E+2ED+2ND"}}
 
 

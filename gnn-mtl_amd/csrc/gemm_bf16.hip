@@ -90,12 +90,19 @@ struct HLoader {
   }
 };
 
+// Output addressing: element (row, col) at (col / 128)·cs + row·ldc + col % 128.  cs = 128 is the
+// plain row-major matrix; ldc = 128, cs = n·128 the bf16 slice-major table (256-B slices) that
+// gnnea_spmm_sliced_bf16 gathers from.
+__device__ __forceinline__ int64_t c_index_bf(int64_t row, int64_t col, int64_t ldc, int64_t cs) {
+  return (col >> 7) * cs + row * ldc + (col & 127);
+}
+
 template <int TA, int TB, int WT, bool VEC, typename TC>
 __global__ __launch_bounds__(256) void k_gemm_bf16(int M, int N, int K,
                                                    const bf16_t* __restrict__ A, int64_t lda,
                                                    const bf16_t* __restrict__ B, int64_t ldb,
                                                    const float* __restrict__ bias, float beta,
-                                                   TC* __restrict__ C, int64_t ldc,
+                                                   TC* __restrict__ C, int64_t ldc, int64_t cs,
                                                    int k_per_split, float* __restrict__ slab,
                                                    int tiles_n) {
   constexpr int BN = 64 * WT;
@@ -171,8 +178,9 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(int M, int N, int K,
         slab[((int64_t)split * M + row) * N + col] = v;
       } else {
         float o = v + bv;
-        if (beta != 0.f) o += beta * to_f32<TC>(C[(int64_t)row * ldc + col]);
-        C[(int64_t)row * ldc + col] = from_f32<TC>(o);
+        TC* cp = C + c_index_bf(row, col, ldc, cs);
+        if (beta != 0.f) o += beta * to_f32<TC>(*cp);
+        *cp = from_f32<TC>(o);
       }
     }
   }
@@ -182,7 +190,7 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(int M, int N, int K,
 template <typename TC>
 __global__ void k_gemm_bf16_reduce(int M, int N, int splits, const float* __restrict__ slab,
                                    const float* __restrict__ bias, float beta,
-                                   TC* __restrict__ C, int64_t ldc) {
+                                   TC* __restrict__ C, int64_t ldc, int64_t cs) {
   const int64_t n = (int64_t)M * N;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -196,7 +204,7 @@ __global__ void k_gemm_bf16_reduce(int M, int N, int splits, const float* __rest
     float s = a + b;
     const int64_t row = t / N, col = t - row * N;
     if (bias) s += bias[col];
-    TC* c = C + row * ldc + col;
+    TC* c = C + c_index_bf(row, col, ldc, cs);
     if (beta != 0.f) s += beta * to_f32<TC>(*c);
     *c = from_f32<TC>(s);
   }
@@ -222,24 +230,24 @@ static int bf16_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
 template <int TA, int TB, int WT, typename TC>
 static void launch_bf16_wt(dim3 grid, hipStream_t s, bool vec, int M, int N, int K,
                            const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
-                           const float* bias, float beta, TC* C, int64_t ldc, int kps,
-                           float* slab, int tiles_n) {
+                           const float* bias, float beta, TC* C, int64_t ldc, int64_t cs,
+                           int kps, float* slab, int tiles_n) {
   if (vec)
     hipLaunchKernelGGL((k_gemm_bf16<TA, TB, WT, true, TC>), grid, dim3(256), 0, s, M, N, K, A,
-                       lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n);
+                       lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n);
   else
     hipLaunchKernelGGL((k_gemm_bf16<TA, TB, WT, false, TC>), grid, dim3(256), 0, s, M, N, K, A,
-                       lda, B, ldb, bias, beta, C, ldc, kps, slab, tiles_n);
+                       lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n);
 }
 
 template <int TA, int TB, typename TC>
 static void launch_bf16_t(int wt, dim3 grid, hipStream_t s, bool vec, int M, int N, int K,
                           const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
-                          const float* bias, float beta, TC* C, int64_t ldc, int kps,
-                          float* slab, int tiles_n) {
+                          const float* bias, float beta, TC* C, int64_t ldc, int64_t cs,
+                          int kps, float* slab, int tiles_n) {
 #define GNNEA_WT(W)                                                                          \
   launch_bf16_wt<TA, TB, W, TC>(grid, s, vec, M, N, K, A, lda, B, ldb, bias, beta, C, ldc,   \
-                                kps, slab, tiles_n)
+                                cs, kps, slab, tiles_n)
   switch (wt) {
     case 1: GNNEA_WT(1); break;
     case 2: GNNEA_WT(2); break;
@@ -254,7 +262,7 @@ template <typename TC>
 static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                        const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
                        const float* bias, float beta, TC* C, int64_t ldc, void* ws,
-                       int64_t ws_bytes, hipStream_t s) {
+                       int64_t ws_bytes, hipStream_t s, int64_t cs = 128) {
   const int wt = bf16_wt(N);
   const int64_t bn = 64 * wt;
   const int tiles_n = (int)((N + bn - 1) / bn);
@@ -268,16 +276,16 @@ static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
   const dim3 grid(tiles, splits);
   const int kk = kps > 0 ? kps : HBK;
   const int m = (int)M, n = (int)N, k = (int)K;
-  if (!trans_a && !trans_b) launch_bf16_t<0, 0, TC>(wt, grid, s, vec, m, n, k, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
-  else if (!trans_a && trans_b) launch_bf16_t<0, 1, TC>(wt, grid, s, vec, m, n, k, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
-  else if (trans_a && !trans_b) launch_bf16_t<1, 0, TC>(wt, grid, s, vec, m, n, k, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
-  else launch_bf16_t<1, 1, TC>(wt, grid, s, vec, m, n, k, A, lda, B, ldb, bias, beta, C, ldc, kk, slab, tiles_n);
+  if (!trans_a && !trans_b) launch_bf16_t<0, 0, TC>(wt, grid, s, vec, m, n, k, A, lda, B, ldb, bias, beta, C, ldc, cs, kk, slab, tiles_n);
+  else if (!trans_a && trans_b) launch_bf16_t<0, 1, TC>(wt, grid, s, vec, m, n, k, A, lda, B, ldb, bias, beta, C, ldc, cs, kk, slab, tiles_n);
+  else if (trans_a && !trans_b) launch_bf16_t<1, 0, TC>(wt, grid, s, vec, m, n, k, A, lda, B, ldb, bias, beta, C, ldc, cs, kk, slab, tiles_n);
+  else launch_bf16_t<1, 1, TC>(wt, grid, s, vec, m, n, k, A, lda, B, ldb, bias, beta, C, ldc, cs, kk, slab, tiles_n);
   GNNEA_LAUNCH_CHECK();
   if (splits > 1) {
     const int64_t nn = M * N;
     const int nb = (int)((nn + 255) / 256 < 4096 ? (nn + 255) / 256 : 4096);
     hipLaunchKernelGGL((k_gemm_bf16_reduce<TC>), dim3(nb), dim3(256), 0, s, m, n, splits, slab,
-                       bias, beta, C, ldc);
+                       bias, beta, C, ldc, cs);
     GNNEA_LAUNCH_CHECK();
   }
   return 0;
@@ -313,4 +321,20 @@ extern "C" int gnnea_gemm_bf16(int trans_a, int trans_b, int64_t M, int64_t N, i
                               (const bf16_t*)B, ldb, bias, beta, (float*)C, ldc, ws, ws_bytes,
                               s);
   return GNNEA_EINVAL;
+}
+
+extern "C" int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                                      const void* A, int64_t lda, const void* B, int64_t ldb,
+                                      const float* bias, float beta, void* Cs, int64_t sstride,
+                                      void* ws, int64_t ws_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  if (M == 0 || N == 0) return 0;
+  if (M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return GNNEA_EINVAL;
+  if (!Cs || sstride % 128 || sstride < M * 128 || (K > 0 && (!A || !B))) return GNNEA_EINVAL;
+  if (K > 0) {
+    if ((trans_a ? lda < M : lda < K) || (trans_b ? ldb < K : ldb < N)) return GNNEA_EINVAL;
+  }
+  return gemm_bf16_t<bf16_t>(trans_a, trans_b, M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B,
+                             ldb, bias, beta, (bf16_t*)Cs, 128, ws, ws_bytes,
+                             (hipStream_t)stream, sstride);
 }

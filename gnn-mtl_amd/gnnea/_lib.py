@@ -79,6 +79,11 @@ SIGNATURES = {
                                                      ctypes.c_int, _p]),
     "gnnea_highway_bwd_sliced_f32": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i32, _p, _i64,
                                                     _p, _i64, _p, _i64, ctypes.c_int, _p]),
+    "gnnea_spmm_sliced_bf16": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64,
+                                              ctypes.c_int, ctypes.c_int, _p]),
+    "gnnea_slice_pack_bf16": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, _p]),
+    "gnnea_act_bwd_sliced_bf16": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i32, ctypes.c_int,
+                                                 _p, _i64, _p]),
     "gnnea_slice_pack_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, _p]),
     "gnnea_act_bwd_sliced_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i32, ctypes.c_int, _p,
                                                 _i64, _p]),
@@ -132,6 +137,8 @@ SIGNATURES = {
                                       _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
     "gnnea_gemm_sliced_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p,
                                              _i64, _p, _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
+    "gnnea_gemm_sliced_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p,
+                                              _i64, _p, _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
     "gnnea_sinkhorn_ws_bytes": (_i64, [ctypes.c_int, ctypes.c_int]),
     "gnnea_sinkhorn_init": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p]),
     "gnnea_sinkhorn_iterate": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), ctypes.c_int,

@@ -44,7 +44,7 @@ class HipEngine:
     def spmm(self, csr, x, act, out=None, beta=0.0):
         from . import ops
         if beta == 0.0 and ops.use_sliced(csr.n_cols, x.shape[1], x.dtype) and \
-                (out is None or out.dtype == torch.float32):
+                (out is None or x.dtype == torch.bfloat16 or out.dtype == torch.float32):
             # above the Infinity Cache: pack into 64-column slices, aggregate slice by slice
             return ops.spmm_sliced(csr, ops.slice_pack(x), x.shape[1], act, out=out)
         return ops.spmm(csr, x, act, out=out, beta=beta)
@@ -171,7 +171,8 @@ class DistAdj:
         """Slice-major fused HighWay layer: only without exchange (the halo moves row-major
         rows)."""
         from .ops import use_sliced
-        return self.local_csr() is not None and use_sliced(self.csr.n_cols, D, dtype)
+        return (dtype == torch.float32 and self.local_csr() is not None
+                and use_sliced(self.csr.n_cols, D, dtype))
 
     def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act):
         from . import ops

@@ -278,97 +278,124 @@ def act_bwd(dy, y, act):
 
 
 # ------------------------------------------------------------------------------------------ #
-# slice-major feature tables (gnnea_spmm_sliced_f32)                                          #
+# slice-major feature tables (gnnea_spmm_sliced_*)                                            #
 # ------------------------------------------------------------------------------------------ #
-SLICE_W = 64
+SLICE_BYTES = 256  # one slice row: 64 fp32 / 128 bf16 columns
+SLICE_W = SLICE_BYTES // 4
 SLICED = True  # use the slice-major path where it applies (tests switch it off to compare)
 
 
+def slice_w(dtype):
+    return SLICE_BYTES // torch.empty((), dtype=dtype).element_size()
+
+
 def use_sliced(n_src, D, dtype):
-    """The slice-major aggregation applies to fp32 tables at least two slices wide whose
-    row-major form exceeds the Infinity Cache (cfg-4: 1M rows x 300 per KG): one 64-column
-    slice of a 1M-row KG is 256 MB and its gathers are 256-B line pairs.  Measured on one KG
-    of cfg-4 (profiles/r01_scale_probe_sliced.json): 300 columns 4.28 -> 3.46 ms, 152 columns
-    1.85 -> 1.79 ms, 76 columns 1.08 -> 1.11 ms (row-major kept below 128 columns)."""
-    return (SLICED and dtype == torch.float32 and D % 4 == 0 and D >= 2 * SLICE_W
-            and n_src * D * 4 > INFINITY_CACHE_BYTES)
+    """The slice-major aggregation applies to fp32 / bf16 tables at least two slices wide whose
+    row-major form exceeds the Infinity Cache (cfg-4: 1M rows x 300 per KG): one 256-B slice of
+    a 1M-row KG is 256 MB and its gathers are 256-B line pairs.  Measured on one KG of cfg-4
+    (profiles/r01_scale_probe_sliced.json): 300 fp32 columns 4.28 -> 3.46 ms, 152 columns
+    1.85 -> 1.79 ms, 76 columns 1.08 -> 1.11 ms (row-major kept below two slices)."""
+    if not SLICED or dtype not in FEATURE_DTYPES or D % 4:
+        return False
+    es = 4 if dtype == torch.float32 else 2
+    return D * es >= 2 * SLICE_BYTES and n_src * D * es > INFINITY_CACHE_BYTES
 
 
-def sliced_empty(n, D, device):
-    """Uninitialised [S, n, 64] fp32 table for an [n, D] matrix (S = ceil(D/64)); columns past D
-    in the last slice are never read."""
-    S = (D + SLICE_W - 1) // SLICE_W
-    return torch.empty((S, n, SLICE_W), dtype=torch.float32, device=device)
+def sliced_empty(n, D, device, dtype=torch.float32):
+    """Uninitialised [S, n, W] table for an [n, D] matrix (W = 256 B of ``dtype``,
+    S = ceil(D/W)); columns past D in the last slice are never read."""
+    W = slice_w(dtype)
+    S = (D + W - 1) // W
+    return torch.empty((S, n, W), dtype=dtype, device=device)
+
+
+def _sfn(name, dtype):
+    return getattr(_lib.lib(), name + ("_bf16" if dtype == torch.bfloat16 else "_f32"))
 
 
 def slice_pack(x):
-    """Row-major fp32 [n, D] -> slice-major table (gnnea_slice_pack_f32)."""
+    """Row-major [n, D] (fp32 / bf16) -> slice-major table (gnnea_slice_pack_*)."""
     x = _rows(x)
     n, D = x.shape
-    xs = sliced_empty(n, D, x.device)
+    xs = sliced_empty(n, D, x.device, x.dtype)
     with torch.cuda.device(x.device):
-        check(_lib.lib().gnnea_slice_pack_f32(ptr(x), _ld(x), n, D, ptr(xs), xs.stride(0),
-                                              stream_of(x.device)))
+        check(_sfn("gnnea_slice_pack", x.dtype)(ptr(x), _ld(x), n, D, ptr(xs), xs.stride(0),
+                                               stream_of(x.device)))
     return xs
 
 
 def act_bwd_sliced(dy, y, act):
     """Gs = dy * act'(y) written slice-major (the transposed aggregation's input)."""
     y = _rows(y)
-    dy = _rows(dy, torch.float32)
+    dy = _rows(dy, y.dtype)
     n, D = y.shape
-    gs = sliced_empty(n, D, y.device)
+    gs = sliced_empty(n, D, y.device, y.dtype)
     with torch.cuda.device(y.device):
-        check(_lib.lib().gnnea_act_bwd_sliced_f32(ptr(dy), _ld(dy), ptr(y), _ld(y), n, D,
-                                                  int(act), ptr(gs), gs.stride(0),
-                                                  stream_of(y.device)))
+        check(_sfn("gnnea_act_bwd_sliced", y.dtype)(ptr(dy), _ld(dy), ptr(y), _ld(y), n, D,
+                                                    int(act), ptr(gs), gs.stride(0),
+                                                    stream_of(y.device)))
     return gs
 
 
-def spmm_sliced(csr, xs, D, act=_lib.GNNEA_ACT_IDENTITY, out=None):
-    """out = act(A @ X) with X held slice-major in ``xs`` ([S, n_src, 64], S = ceil(D/64)),
-    launched per diagonal (KG) block; out row-major fp32 [n_rows, D]."""
+def spmm_sliced(csr, xs, D, act=_lib.GNNEA_ACT_IDENTITY, out=None, out_dtype=None):
+    """out = act(A @ X) with X held slice-major in ``xs`` ([S, n_src, W], fp32 or bf16),
+    launched per diagonal (KG) block; out row-major [n_rows, D] (xs's dtype by default; an
+    fp32 out for a bf16 table keeps the sums unrounded)."""
     _lib.require_device(xs)
-    S = (D + SLICE_W - 1) // SLICE_W
-    if xs.dtype != torch.float32 or xs.dim() != 3 or xs.shape[0] < S or \
-            xs.shape[2] != SLICE_W or xs.shape[1] < csr.n_cols or not xs.is_contiguous():
-        raise ValueError("gnnea.spmm_sliced: xs must be a contiguous fp32 [%d, >=%d, 64] table"
-                         % (S, csr.n_cols))
+    if xs.dtype not in FEATURE_DTYPES:
+        raise TypeError("gnnea.spmm_sliced: fp32 or bf16 table required")
+    W = slice_w(xs.dtype)
+    S = (D + W - 1) // W
+    if xs.dim() != 3 or xs.shape[0] < S or xs.shape[2] != W or xs.shape[1] < csr.n_cols or \
+            not xs.is_contiguous():
+        raise ValueError("gnnea.spmm_sliced: xs must be a contiguous [%d, >=%d, %d] table"
+                         % (S, csr.n_cols, W))
     if out is None:
-        out = torch.empty((csr.n_rows, D), dtype=torch.float32, device=xs.device)
-    if out.dtype != torch.float32 or out.shape != (csr.n_rows, D) or out.stride(1) != 1:
-        raise ValueError("gnnea.spmm_sliced: out must be fp32 [%d, %d]" % (csr.n_rows, D))
+        out = torch.empty((csr.n_rows, D), dtype=out_dtype or xs.dtype, device=xs.device)
+    if out.shape != (csr.n_rows, D) or out.stride(1) != 1 or out.dtype not in FEATURE_DTYPES \
+            or (xs.dtype == torch.float32 and out.dtype != torch.float32):
+        raise ValueError("gnnea.spmm_sliced: out must be [%d, %d] (fp32 for an fp32 table)"
+                         % (csr.n_rows, D))
     L = _lib.lib()
     st = stream_of(xs.device)
     with torch.cuda.device(xs.device):
         for r0, r1 in csr.row_blocks():
-            check(L.gnnea_spmm_sliced_f32(_off32(csr.rowptr, r0), ptr(csr.col), ptr(csr.val),
-                                          r1 - r0, D, ptr(xs), xs.stride(0), _off(out, r0),
-                                          _ld(out), int(act), st))
+            if xs.dtype == torch.bfloat16:
+                yd = _lib.GNNEA_BF16 if out.dtype == torch.bfloat16 else _lib.GNNEA_F32
+                check(L.gnnea_spmm_sliced_bf16(_off32(csr.rowptr, r0), ptr(csr.col),
+                                               ptr(csr.val), r1 - r0, D, ptr(xs), xs.stride(0),
+                                               _off(out, r0), _ld(out), yd, int(act), st))
+            else:
+                check(L.gnnea_spmm_sliced_f32(_off32(csr.rowptr, r0), ptr(csr.col),
+                                              ptr(csr.val), r1 - r0, D, ptr(xs), xs.stride(0),
+                                              _off(out, r0), _ld(out), int(act), st))
     return out
 
 
 def gemm_sliced(x, weight, bias=None):
-    """hidden = x W^T + b written slice-major (gnnea_gemm_sliced_f32): the projection of a GCN
-    layer hands the aggregation its table at no extra pass."""
-    x = _rows(x)
-    weight = _rows(weight)
+    """hidden = x W^T + b written slice-major (gnnea_gemm_sliced_{f32,bf16}): the projection of
+    a GCN layer hands the aggregation its table at no extra pass.  bf16 operands give a bf16
+    table (fp32 accumulate)."""
+    bf = x.dtype == torch.bfloat16 or weight.dtype == torch.bfloat16
+    dt = torch.bfloat16 if bf else torch.float32
+    x = _rows(x, dt)
+    weight = _featc(weight, dt) if bf else _rows(weight, dt)
     M, K = x.shape
     N = weight.shape[0]
     if weight.shape[1] != K:
         raise ValueError("gnnea.gemm_sliced: inner dimensions differ")
-    if x.dtype != torch.float32 or weight.dtype != torch.float32:
-        raise TypeError("gnnea.gemm_sliced: fp32 operands required")
-    hs = sliced_empty(M, N, x.device)
+    hs = sliced_empty(M, N, x.device, dt)
     if bias is not None:
         bias = _featc(bias, torch.float32)
     L = _lib.lib()
-    ws_bytes = int(L.gnnea_gemm_ws_bytes(M, N, K))
+    ws_fn = L.gnnea_gemm_bf16_ws_bytes if bf else L.gnnea_gemm_ws_bytes
+    ws_bytes = int(ws_fn(M, N, K))
     ws = _gemm_ws(x.device, ws_bytes) if ws_bytes > 0 else None
+    fn = L.gnnea_gemm_sliced_bf16 if bf else L.gnnea_gemm_sliced_f32
     with torch.cuda.device(x.device):
-        check(L.gnnea_gemm_sliced_f32(0, 1, M, N, K, ptr(x), _ld(x), ptr(weight), _ld(weight),
-                                      ptr(bias), 0.0, ptr(hs), hs.stride(0), ptr(ws),
-                                      ws_bytes if ws is not None else 0, stream_of(x.device)))
+        check(fn(0, 1, M, N, K, ptr(x), _ld(x), ptr(weight), _ld(weight), ptr(bias), 0.0,
+                 ptr(hs), hs.stride(0), ptr(ws), ws_bytes if ws is not None else 0,
+                 stream_of(x.device)))
     return hs
 
 
@@ -376,7 +403,8 @@ def aggregate_t_into(csr, dy, y, act, out=None):
     """out = Aᵀ·(dy ⊙ act'(y)): the backward of act(A·hidden), slice-major when it applies."""
     csrT = csr.transpose()
     D = y.shape[1]
-    if use_sliced(csrT.n_cols, D, y.dtype) and (out is None or out.dtype == torch.float32):
+    if use_sliced(csrT.n_cols, D, y.dtype) and \
+            (out is None or y.dtype == torch.bfloat16 or out.dtype == torch.float32):
         gs = act_bwd_sliced(dy, y, act)
         return spmm_sliced(csrT, gs, D, out=out)
     g = _featc(dy, y.dtype) if act == _lib.GNNEA_ACT_IDENTITY else act_bwd(dy, y, act)
@@ -435,7 +463,7 @@ def gcn_layer(adj, x, weight, bias, act_fn):
     """Fused GCN layer (GCNLayerFn) when the slice-major path applies, else None.  ``adj``: the
     reference's sparse adjacency, or a DistAdj whose rank aggregates without exchange."""
     code = act_code(act_fn)
-    if code is None or x.dtype != torch.float32 or weight.dtype != torch.float32 or \
+    if code is None or x.dtype not in FEATURE_DTYPES or weight.dtype != x.dtype or \
             x.shape[1] != weight.shape[1]:
         return None
     if hasattr(adj, "local_csr"):
@@ -446,7 +474,7 @@ def gcn_layer(adj, x, weight, bias, act_fn):
         csr = csr_of(adj)
     else:
         return None
-    if not use_sliced(csr.n_cols, weight.shape[0], torch.float32) or x.shape[0] != csr.n_cols:
+    if not use_sliced(csr.n_cols, weight.shape[0], x.dtype) or x.shape[0] != csr.n_cols:
         return None
     return GCNLayerFn.apply(_rows(x), weight, bias, csr, code)
 
@@ -652,7 +680,7 @@ class LocalAgg:
         return spmm(self.csr.transpose(), g, out=out)
 
     def sliced_ok(self, D, dtype):
-        return use_sliced(self.csr.n_cols, D, dtype)
+        return dtype == torch.float32 and use_sliced(self.csr.n_cols, D, dtype)
 
     def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act):
         return highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act)

@@ -91,6 +91,17 @@ int gnnea_spmm_csr_beta_f32(const int32_t* rowptr, const int32_t* col, const flo
 int gnnea_spmm_sliced_f32(const int32_t* rowptr, const int32_t* col, const float* val,
                           int32_t n_rows, int32_t D, const float* Xs, int64_t sstride, float* Y,
                           int64_t ldy, int act, void* stream);
+/* bf16 storage (cfg-5): 128-column slices (256 B per slice row), element (r, c) at
+ * Xs[(c/128)*sstride + r*128 + c%128], sstride % 128 == 0; fp32 arithmetic, Y bf16 (y_dtype
+ * GNNEA_BF16, rounded once) or fp32 (GNNEA_F32); D % 4 == 0, 16-B aligned Xs, 8-B aligned Y. */
+int gnnea_spmm_sliced_bf16(const int32_t* rowptr, const int32_t* col, const float* val,
+                           int32_t n_rows, int32_t D, const void* Xs, int64_t sstride, void* Y,
+                           int64_t ldy, int y_dtype, int act, void* stream);
+int gnnea_slice_pack_bf16(const void* X, int64_t ldx, int64_t n, int32_t D, void* Xs,
+                          int64_t sstride, void* stream);
+int gnnea_act_bwd_sliced_bf16(const void* dY, int64_t lddy, const void* Y, int64_t ldy,
+                              int64_t n, int32_t D, int act, void* Gs, int64_t sstride,
+                              void* stream);
 /* HighWay layer over a slice-major projection (layers/layers.py:64-76): S = act(A·X) with X the
  * first D columns of the table Xs, g = sigmoid(gate_pre + bias_gate) with gate_pre read from
  * the slice-major table gate_s at column offset goff (the fused layer's ONE projection table
@@ -264,6 +275,12 @@ int64_t gnnea_gemm_bf16_ws_bytes(int64_t M, int64_t N, int64_t K);
 int gnnea_gemm_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const void* A,
                     int64_t lda, const void* B, int64_t ldb, const float* bias, float beta,
                     void* C, int64_t ldc, int c_dtype, void* ws, int64_t ws_bytes, void* stream);
+/* the bf16 GEMM writing C slice-major (bf16, 128-column slices):
+ * element (r, c) at Cs[(c/128)*sstride + r*128 + c%128], sstride % 128 == 0, >= M*128 */
+int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                           const void* A, int64_t lda, const void* B, int64_t ldb,
+                           const float* bias, float beta, void* Cs, int64_t sstride, void* ws,
+                           int64_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------------------------ *
  * a9-a12. Sinkhorn solvers in the reference's scaling form, fp64 arithmetic.

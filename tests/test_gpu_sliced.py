@@ -248,3 +248,80 @@ def test_distadj_world1_takes_sliced_layers(device, monkeypatch):
     ref = run(adj)
     for g, w in zip(got, ref):
         assert rel_err(g.cpu(), w.cpu()) < TOL32
+
+
+# ---- bf16 storage: 128-column slices (cfg-5's dtype), fp32 arithmetic ------------------------
+TOL_BF16 = 1e-2  # one bf16 rounding of the output (2^-8) plus summation order
+
+
+@pytest.mark.parametrize("D", [4, 128, 132, 300, 512])
+def test_spmm_sliced_bf16_vs_oracle(device, D):
+    from gnnea import ops
+    from oracle.gnn import coo_aggregate
+    rng = np.random.default_rng(D + 23)
+    n = 900
+    r, c, v, csr = _graph(rng, n, 8000, device)
+    xb = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32)).to(device).bfloat16()
+    xs = ops.slice_pack(xb)
+    assert xs.dtype == torch.bfloat16 and xs.shape == ((D + 127) // 128, n, 128)
+    assert torch.equal(_unslice(xs, D), xb)
+    ref32 = coo_aggregate(r, c, v, n, xb.float().cpu().double())
+    for act, fn in ((0, lambda t: t), (1, torch.relu), (5, torch.tanh)):
+        ref = fn(ref32)
+        y32 = ops.spmm_sliced(csr, xs, D, act, out_dtype=torch.float32).cpu()
+        assert rel_err(y32, ref) < TOL32, (D, act)  # exact bf16 inputs, fp32 sums
+        yb = ops.spmm_sliced(csr, xs, D, act).cpu()
+        assert yb.dtype == torch.bfloat16
+        assert rel_err(yb.float(), ref) < TOL_BF16, (D, act)
+        assert rel_err(yb.float(), ops.spmm(csr, xb, act).float().cpu()) < TOL_BF16
+
+
+def test_gemm_and_act_bwd_sliced_bf16(device):
+    from gnnea import ops
+    torch.manual_seed(3)
+    x = torch.randn(1000, 300, device=device).bfloat16()
+    W = torch.randn(300, 300, device=device).bfloat16()
+    b = torch.randn(300, device=device)
+    hs = ops.gemm_sliced(x, W, b)
+    assert hs.dtype == torch.bfloat16 and hs.shape == (3, 1000, 128)
+    assert torch.equal(_unslice(hs, 300), ops.gemm(x, W, trans_b=True, bias=b))
+    y = torch.relu(torch.randn(500, 300, device=device)).bfloat16()
+    dy = torch.randn(500, 300, device=device).bfloat16()
+    gs = ops.act_bwd_sliced(dy, y, 1)
+    assert torch.equal(_unslice(gs, 300), ops.act_bwd(dy, y, 1))
+
+
+def test_gcn_layer_sliced_bf16_matches_rowmajor(device, monkeypatch):
+    """A bf16 GraphConvolution through GCNLayerFn (bf16 GEMM writing 128-column slices, sliced
+    aggregation and backward) against the row-major bf16 layer."""
+    from gnnea import ops
+    from layers.layers import GraphConvolution
+    rng = np.random.default_rng(12)
+    n = 1200
+    r, c, v, csr = _graph(rng, n, 10000, device)
+    idx = torch.from_numpy(np.stack([r, c]).astype(np.int64))
+    adj = torch.sparse_coo_tensor(idx, torch.from_numpy(v), (n, n)).to(device)
+    torch.manual_seed(0)
+    layer = GraphConvolution(300, 300, 0.0, torch.tanh, True).to(device).bfloat16()
+    x = torch.from_numpy(rng.standard_normal((n, 300)).astype(np.float32) * 0.1).to(device)
+    x = x.bfloat16()
+    R = torch.randn(n, 300, device=device).bfloat16()
+
+    def run():
+        layer.zero_grad()
+        xx = x.clone().requires_grad_(True)
+        out, _ = layer((xx, adj))
+        (out.float() * R.float()).sum().backward()
+        return [out.detach(), xx.grad, layer.linear.weight.grad.clone(),
+                layer.linear.bias.grad.clone()]
+    calls = []
+    orig = ops.gemm_sliced
+    monkeypatch.setattr(ops, "gemm_sliced", lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+    monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 0)
+    got = run()
+    assert calls
+    monkeypatch.setattr(ops, "SLICED", False)
+    ref = run()
+    for g, w in zip(got, ref):
+        assert g.dtype == w.dtype
+        assert rel_err(g.float().cpu(), w.float().cpu()) < 2e-2
