@@ -21,6 +21,8 @@
 // A device status block gates every kernel, so iterations enqueued past the stop are no-ops.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace gnnea {
 
 constexpr double kBig = 1e20;   // sinkhorn_loss.py:11
@@ -37,7 +39,15 @@ enum { SD_TNEW = 8, SD_ERR = 8, SD_TPREV = 9, SD_LOSS = 10, SD_TOL = 11 };
 static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
 // rows per sweep workgroup: about 256 workgroups (one per CU) whatever I is
-static int sk_rows_per_wg(int I) { return (I + 255) / 256; }
+// (GNNEA_SK_WGS overrides the workgroup target for tuning experiments; not part of the ABI)
+static int sk_rows_per_wg(int I) {
+  static const int target = [] {
+    const char* e = getenv("GNNEA_SK_WGS");
+    const int v = e ? atoi(e) : 0;
+    return v >= 64 && v <= 512 ? v : 256;
+  }();
+  return (I + target - 1) / target;
+}
 
 struct SkWs {
   int64_t K, u, v, pu, pv, rowbuf, part, errpart, total;
