@@ -31,15 +31,15 @@ struct Tile {
 
 // Load a ROWS x GBK tile of op(X) into registers. op(X)[row][k] = X[row][k] (K_CONTIG) or
 // X[k][row]; rows >= nrows or k >= kend read as 0.  VEC: 16-B loads (ld % 4 == 0, aligned).
-template <bool K_CONTIG, int ROWS, bool VEC>
+template <bool K_CONTIG, int ROWS, bool VEC, int NT = 256>
 struct Loader {
-  static constexpr int NV = ROWS * GBK / 4 / 256;  // float4 per thread (ROWS multiple of 64)
+  static constexpr int NV = ROWS * GBK / 4 / NT;  // float4 per thread (ROWS multiple of 64)
   float4 r[NV];
   __device__ void load(const float* __restrict__ X, int64_t ld, int row0, int nrows, int k0,
                        int kend, int tid) {
 #pragma unroll
     for (int q = 0; q < NV; ++q) {
-      const int idx = tid + 256 * q;
+      const int idx = tid + NT * q;
       int row, k;
       if (K_CONTIG) { row = idx / (GBK / 4); k = (idx % (GBK / 4)) * 4; }
       else { k = idx / (ROWS / 4); row = (idx % (ROWS / 4)) * 4; }
@@ -68,7 +68,7 @@ struct Loader {
   __device__ void store(float* __restrict__ S, int tid) const {
 #pragma unroll
     for (int q = 0; q < NV; ++q) {
-      const int idx = tid + 256 * q;
+      const int idx = tid + NT * q;
       if (K_CONTIG) {
         const int row = idx / (GBK / 4), k = (idx % (GBK / 4)) * 4;
         float* p = S + Tile<true, ROWS>::at(row, k);
@@ -150,6 +150,228 @@ __global__ __launch_bounds__(256) void k_gemm_wide(int M, int N, int K, const fl
     }
     if (more) {
       la.store(As(cur ^ 1), tid);
+      lb.store(Bs(cur ^ 1), tid);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: 32x32 C/D map  col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int t = 0; t < WT; ++t) {
+    const int col = n0 + wn * 32 * WT + t * 32 + li;
+    if (col >= N) continue;
+    const float bv = (bias && !slab) ? bias[col] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      if (row >= M) continue;
+      const float v = acc[t][r];
+      if (slab) {
+        slab[((int64_t)split * M + row) * N + col] = v;
+      } else {
+        float o = v + bv;
+        float* c = C + c_index(row, col, ldc, cs);
+        if (beta != 0.f) o += beta * *c;
+        *c = o;
+      }
+    }
+  }
+}
+
+// ---- fp32 GEMM on the bf16 MFMA: three-way split operands, six products ------------------------
+// Every fp32 operand element x is split exactly into x = h + m + l + r with h = bf16(x),
+// m = bf16(x - h), l = bf16(x - h - m) (|r| <= 2^-24 |x|: the two subtractions are exact), staged
+// in LDS as three bf16 planes.  C = Σ over the six products whose order is <= 2 (l·h, m·m, h·l,
+// m·h, h·m, h·h, small ones first) on v_mfma_f32_32x32x16_bf16 with fp32 accumulation: the
+// dropped terms (m·l, l·m, l·l) are below 2^-24 relative, so the result carries fp32 rounding
+// (emulated on the CPU: 3.6e-7 norm-relative vs fp64 at K = 300, plain fp32 6.7e-7).  Six bf16
+// MFMAs cost 6/16 of one f32 MFMA (bf16 dense 2.5 PF vs f32 157 TF): the 360-GFLOP projections
+// of the training step move from the f32 MFMA bound (2.3 ms) toward their HBM bound (0.76 ms).
+// Tile as k_gemm_wide: BM = 64 x BN = 64*WT, 4 waves 2 x 2, BK = 16 (one MFMA k-step); planes
+// [row][k] K-contiguous with a 48-B row stride (16-B fragments, conflict-free b128 reads); an
+// operand contiguous along M/N is transposed while its planes are written.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+constexpr int XLD = GBK + 8;  // bf16 elements per LDS plane row
+
+// the hardware conversion (v_cvt_pk_bf16_f32, round to nearest even) on plain casts
+__device__ __forceinline__ bf16_t to_bf16_hw(float x) {
+  return __builtin_bit_cast(bf16_t, (__bf16)x);
+}
+__device__ __forceinline__ void split3(float x, bf16_t& h, bf16_t& m, bf16_t& l) {
+  h = to_bf16_hw(x);
+  const float r1 = x - bf16_to_f32(h);
+  m = to_bf16_hw(r1);
+  l = to_bf16_hw(r1 - bf16_to_f32(m));
+}
+
+template <bool K_CONTIG, int ROWS, bool VEC, int NT = 256>
+struct X3Loader : Loader<K_CONTIG, ROWS, VEC, NT> {
+  using Loader<K_CONTIG, ROWS, VEC, NT>::r;
+  static constexpr int NV = Loader<K_CONTIG, ROWS, VEC, NT>::NV;
+  static constexpr int PLANE = ROWS * XLD;
+  // planes at S, S + PLANE, S + 2*PLANE (h, m, l)
+  __device__ void store3(bf16_t* __restrict__ S, int tid) const {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int idx = tid + NT * q;
+      const float v[4] = {r[q].x, r[q].y, r[q].z, r[q].w};
+      bf16_t h[4], m[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split3(v[e], h[e], m[e], l[e]);
+      if (K_CONTIG) {  // 4 consecutive k of one row: one 8-B store per plane
+        const int row = idx / (GBK / 4), k = (idx % (GBK / 4)) * 4;
+        bf16_t* p = S + row * XLD + k;
+        *(uint2*)p = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+        *(uint2*)(p + PLANE) =
+            make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
+        *(uint2*)(p + 2 * PLANE) =
+            make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+      } else {  // 4 consecutive rows at one k
+        const int k = idx / (ROWS / 4), row = (idx % (ROWS / 4)) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bf16_t* p = S + (row + e) * XLD + k;
+          p[0] = h[e];
+          p[PLANE] = m[e];
+          p[2 * PLANE] = l[e];
+        }
+      }
+    }
+  }
+};
+
+// B (the small weight operand) arrives pre-split: three bf16 planes [3][n][ldp] K-contiguous,
+// zero-padded to ldp = roundup16(K) columns (k_split3_planes, once per call), so the kernel splits
+// only A and every B fragment load is a 16-B copy.
+constexpr int kPlaneAlign = 16;
+
+__global__ __launch_bounds__(256) void k_split3_planes(const float* __restrict__ W, int64_t ldw,
+                                                       int trans, int n, int K, int ldp,
+                                                       bf16_t* __restrict__ P, int64_t pstride) {
+  // plane element (r, k), r < n, k < ldp:  W[r][k] (trans = 0: W is [n][K]) or W[k][r]
+  const int64_t total = (int64_t)n * ldp;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(t / ldp), k = (int)(t - (int64_t)r * ldp);
+    const float x = k < K ? (trans ? W[(int64_t)k * ldw + r] : W[(int64_t)r * ldw + k]) : 0.f;
+    bf16_t h, m, l;
+    split3(x, h, m, l);
+    P[t] = h;
+    P[pstride + t] = m;
+    P[2 * pstride + t] = l;
+  }
+}
+
+template <int ROWS, int NT = 256>
+struct PLoader {  // ROWS x GBK of each of the three planes, 16-B chunks of 8 k
+  static constexpr int NCH = 3 * ROWS * (GBK / 8);
+  static constexpr int NQ = (NCH + NT - 1) / NT;
+  uint4 r[NQ];
+  __device__ void load(const bf16_t* __restrict__ P, int64_t ldp, int64_t pstride, int row0,
+                       int nrows, int k0, int tid) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int idx = tid + NT * q;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (idx < NCH) {
+        const int p = idx / (ROWS * 2), rem = idx - p * ROWS * 2;
+        const int row = rem >> 1, k8 = (rem & 1) * 8;
+        if (row0 + row < nrows)
+          v = *(const uint4*)(P + p * pstride + (int64_t)(row0 + row) * ldp + k0 + k8);
+      }
+      r[q] = v;
+    }
+  }
+  __device__ void store(bf16_t* __restrict__ S, int tid) const {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int idx = tid + NT * q;
+      if (idx < NCH) {
+        const int p = idx / (ROWS * 2), rem = idx - p * ROWS * 2;
+        const int row = rem >> 1, k8 = (rem & 1) * 8;
+        *(uint4*)(S + p * ROWS * XLD + row * XLD + k8) = r[q];
+      }
+    }
+  }
+};
+
+constexpr int XBM = 128, XNT = 512;  // 8 waves in 4 x 2, each 32 x 32*WT
+
+template <int WT, bool VEC>
+__global__ __launch_bounds__(XNT) void k_gemm_x3(int M, int N, int K, const float* __restrict__ A,
+                                                 int64_t lda, const bf16_t* __restrict__ Bp,
+                                                 int64_t ldp, int64_t pstride,
+                                                 const float* __restrict__ bias, float beta,
+                                                 float* __restrict__ C, int64_t ldc, int64_t cs,
+                                                 int k_per_split, float* __restrict__ slab,
+                                                 int tiles_n) {
+  constexpr int BN = 64 * WT;
+  constexpr int SA = 3 * XBM * XLD, SB = 3 * BN * XLD;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * (SA + SB)];
+  auto As = [&](int b) { return smem + b * SA; };
+  auto Bs = [&](int b) { return smem + 2 * SA + b * SB; };
+
+  const int t_id = xcd_remap(blockIdx.x, gridDim.x);
+  const int bn = t_id % tiles_n, bm = t_id / tiles_n;
+  const int m0 = bm * XBM, n0 = bn * BN;
+  const int split = blockIdx.y;
+  const int kb = split * k_per_split;
+  const int ke = min(K, kb + k_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int kh = lane >> 5, li = lane & 31;
+
+  f32x16 acc[WT];
+#pragma unroll
+  for (int t = 0; t < WT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  X3Loader<true, XBM, VEC, XNT> la;
+  PLoader<BN, XNT> lb;
+  const int nsteps = ke > kb ? (ke - kb + GBK - 1) / GBK : 0;
+  if (nsteps > 0) {
+    la.load(A, lda, m0, M, kb, ke, tid);
+    lb.load(Bp, ldp, pstride, n0, N, kb, tid);
+    la.store3(As(0), tid);
+    lb.store(Bs(0), tid);
+    __syncthreads();
+  }
+  constexpr int PA = XBM * XLD, PB = BN * XLD;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (more) {  // in flight under the MFMAs below
+      la.load(A, lda, m0, M, kb + (s + 1) * GBK, ke, tid);
+      lb.load(Bp, ldp, pstride, n0, N, kb + (s + 1) * GBK, tid);
+    }
+    const bf16_t* a_s = As(cur) + (wm * 32 + li) * XLD + 8 * kh;
+    const bf16x8_t ah = *(const bf16x8_t*)a_s;
+    const bf16x8_t am = *(const bf16x8_t*)(a_s + PA);
+    const bf16x8_t al = *(const bf16x8_t*)(a_s + 2 * PA);
+    bf16x8_t bh[WT], bm_[WT], bl[WT];
+#pragma unroll
+    for (int t = 0; t < WT; ++t) {
+      const bf16_t* b_s = Bs(cur) + (wn * 32 * WT + t * 32 + li) * XLD + 8 * kh;
+      bh[t] = *(const bf16x8_t*)b_s;
+      bm_[t] = *(const bf16x8_t*)(b_s + PB);
+      bl[t] = *(const bf16x8_t*)(b_s + 2 * PB);
+    }
+    // small products first; each product over the WT independent accumulators
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm_[t], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[t], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm_[t], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t], acc[t], 0, 0, 0);
+    if (more) {
+      la.store3(As(cur ^ 1), tid);
       lb.store(Bs(cur ^ 1), tid);
     }
     __syncthreads();
@@ -335,4 +557,103 @@ extern "C" int gnnea_gemm_sliced_f32(int trans_a, int trans_b, int64_t M, int64_
   if (sstride % 4 != 0) return GNNEA_EINVAL;
   return gemm_f32(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, Cs, 64, sstride, ws,
                   ws_bytes, stream);
+}
+
+// ---- fp32 GEMM through three-way bf16 splits (k_gemm_x3) -----------------------------------
+// op(A) must be K-contiguous (trans_a = 0: the tall operand of the projections); a transposed A
+// (the weight gradients dW = dYᵀ·x, both operands tall) runs on the f32 MFMA kernel instead.
+static int64_t x3_planes_bytes(int64_t N, int64_t K) {
+  const int64_t ldp = (K + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign;
+  return (3 * N * ldp * 2 + 255) & ~(int64_t)255;
+}
+
+static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                   int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
+                   float* C, int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, void* stream) {
+  if (trans_a || K == 0)
+    return gemm_f32(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, ws,
+                    ws_bytes, stream);
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  if (M == 0 || N == 0) return 0;
+  if (M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return GNNEA_EINVAL;
+  if (!C || !A || !B) return GNNEA_EINVAL;
+  if (cs == 64 ? ldc < N : (ldc < (N < 64 ? N : 64) || cs < M * ldc)) return GNNEA_EINVAL;
+  if (lda < K || (trans_b ? ldb < K : ldb < N)) return GNNEA_EINVAL;
+  const int64_t pbytes = x3_planes_bytes(N, K);
+  if (!ws || ws_bytes < pbytes) return GNNEA_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int ldp = (int)((K + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign);
+  const int64_t pstride = N * ldp;
+  bf16_t* planes = (bf16_t*)ws;
+  {
+    const int64_t tot = N * ldp;
+    const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
+    // B op-form [N][K]: trans_b = 1 means B is stored [N][K] (no transpose needed)
+    hipLaunchKernelGGL(k_split3_planes, dim3(nb), dim3(256), 0, s, B, ldb, trans_b ? 0 : 1,
+                       (int)N, (int)K, ldp, planes, pstride);
+    GNNEA_LAUNCH_CHECK();
+  }
+  const int wt = pick_wt(N);
+  const int64_t bn = 64 * wt;
+  const int tiles_n = (int)((N + bn - 1) / bn);
+  const int tiles = (int)(((M + XBM - 1) / XBM) * tiles_n);
+  const int splits = pick_splits(M, N, K, ws_bytes - pbytes);
+  const int kps = (int)(((K + splits - 1) / splits + GBK - 1) / GBK * GBK);
+  float* slab = splits > 1 ? (float*)((char*)ws + pbytes) : nullptr;
+  const bool vec = lda % 4 == 0 && K % 4 == 0 && al16(A);
+  const dim3 grid(tiles, splits);
+#define GNNEA_X3(W)                                                                              \
+  case W:                                                                                        \
+    if (vec)                                                                                     \
+      hipLaunchKernelGGL((k_gemm_x3<W, true>), grid, dim3(XNT), 0, s, (int)M, (int)N, (int)K, A, \
+                         lda, planes, (int64_t)ldp, pstride, bias, beta, C, ldc, cs, kps, slab,  \
+                         tiles_n);                                                               \
+    else                                                                                         \
+      hipLaunchKernelGGL((k_gemm_x3<W, false>), grid, dim3(XNT), 0, s, (int)M, (int)N, (int)K,   \
+                         A, lda, planes, (int64_t)ldp, pstride, bias, beta, C, ldc, cs, kps,     \
+                         slab, tiles_n);                                                         \
+    break;
+  switch (wt) {
+    GNNEA_X3(1)
+    GNNEA_X3(2)
+    GNNEA_X3(3)
+    GNNEA_X3(4)
+    default:
+    GNNEA_X3(5)
+  }
+#undef GNNEA_X3
+  GNNEA_LAUNCH_CHECK();
+  if (splits > 1) {
+    const int64_t n = M * N;
+    const int nb = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+    hipLaunchKernelGGL(k_gemm_reduce, dim3(nb), dim3(256), 0, s, (int)M, (int)N, splits, slab,
+                       bias, beta, C, ldc, cs);
+    GNNEA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+extern "C" int64_t gnnea_gemm_x3_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  return x3_planes_bytes(N, K) + pick_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
+}
+
+// fp32 GEMM through three-way bf16 splits on the bf16 MFMA (k_gemm_x3); workspace from
+// gnnea_gemm_x3_ws_bytes (the split planes of op(B) + split-K slabs)
+extern "C" int gnnea_gemm_x3_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                                 const float* A, int64_t lda, const float* B, int64_t ldb,
+                                 const float* bias, float beta, float* C, int64_t ldc, void* ws,
+                                 int64_t ws_bytes, void* stream) {
+  return gemm_x3(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, 64, ws, ws_bytes,
+                 stream);
+}
+
+extern "C" int gnnea_gemm_x3_sliced_f32(int trans_a, int trans_b, int64_t M, int64_t N,
+                                        int64_t K, const float* A, int64_t lda, const float* B,
+                                        int64_t ldb, const float* bias, float beta, float* Cs,
+                                        int64_t sstride, void* ws, int64_t ws_bytes,
+                                        void* stream) {
+  if (sstride % 4 != 0) return GNNEA_EINVAL;
+  return gemm_x3(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, Cs, 64, sstride, ws,
+                 ws_bytes, stream);
 }

@@ -139,6 +139,12 @@ SIGNATURES = {
                                              _i64, _p, _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
     "gnnea_gemm_sliced_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p,
                                               _i64, _p, _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
+    "gnnea_gemm_x3_ws_bytes": (_i64, [_i64, _i64, _i64]),
+    "gnnea_gemm_x3_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64,
+                                         _p, _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
+    "gnnea_gemm_x3_sliced_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p,
+                                                _i64, _p, _i64, _p, _f32, _p, _i64, _p, _i64,
+                                                _p]),
     "gnnea_sinkhorn_ws_bytes": (_i64, [ctypes.c_int, ctypes.c_int]),
     "gnnea_sinkhorn_init": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p]),
     "gnnea_sinkhorn_iterate": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), ctypes.c_int,

@@ -83,6 +83,20 @@ def _gemm_ws(device, nbytes):
 
 
 _SMALL_OPERAND = 1 << 22
+# fp32 products at least this large (M*N*K) run on the bf16 MFMA with three-way split operands
+# (gnnea_gemm_x3_f32: fp32-level rounding, 6/16 of the f32 MFMA time); smaller ones on the f32
+# MFMA (gnnea_gemm_f32).  GEMM_X3 = False keeps every fp32 product on the f32 MFMA.
+GEMM_X3 = True
+X3_MIN_MNK = 1 << 26
+
+
+def _use_x3(M, N, K, x3, trans_a=False):
+    """x3 splits op(B) into bf16 planes once per call: only for a small B (the weight) times a
+    tall, K-contiguous A.  The weight gradients (trans_a: both operands tall) and the bias
+    column sums (B = the tall gradient) stay on the f32 MFMA."""
+    if trans_a or N * K > _SMALL_OPERAND:
+        return False
+    return (GEMM_X3 and M * N * K >= X3_MIN_MNK) if x3 is None else bool(x3)
 
 
 def _ld(t):
@@ -91,12 +105,14 @@ def _ld(t):
     return t.stride(0) if t.shape[0] > 1 else max(t.shape[1], 1)
 
 
-def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_dtype=None):
+def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_dtype=None,
+         x3=None):
     """out = op(a) @ op(b) (+ bias) (+ beta*out) on MFMA.
 
-    fp32 operands: gnnea_gemm_f32 (exact-f32 MFMA).  A bf16 operand (cfg-5 storage) switches
-    to gnnea_gemm_bf16 (both operands bf16, fp32 accumulate, out bf16 unless an fp32 ``out`` /
-    ``out_dtype`` is given)."""
+    fp32 operands: gnnea_gemm_f32 (exact-f32 MFMA), or for large products gnnea_gemm_x3_f32
+    (three-way bf16 splits, fp32-level rounding; ``x3`` forces either).  A bf16 operand (cfg-5
+    storage) switches to gnnea_gemm_bf16 (both operands bf16, fp32 accumulate, out bf16 unless
+    an fp32 ``out`` / ``out_dtype`` is given)."""
     _lib.require_device(a, b)
     bf = a.dtype == torch.bfloat16 or b.dtype == torch.bfloat16
     if bf:
@@ -129,7 +145,9 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
     if bias is not None:
         bias = _featc(bias, torch.float32)
     L = _lib.lib()
-    ws_fn = L.gnnea_gemm_bf16_ws_bytes if bf else L.gnnea_gemm_ws_bytes
+    x3 = not bf and _use_x3(M, N, K, x3, trans_a)
+    ws_fn = L.gnnea_gemm_bf16_ws_bytes if bf else (
+        L.gnnea_gemm_x3_ws_bytes if x3 else L.gnnea_gemm_ws_bytes)
     ws_bytes = int(ws_fn(M, N, K))
     ws = _gemm_ws(a.device, ws_bytes) if ws_bytes > 0 else None
     with torch.cuda.device(a.device):
@@ -140,10 +158,10 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
                                     _ld(out), cd, ptr(ws),
                                     ws_bytes if ws is not None else 0, stream_of(a.device)))
         else:
-            check(L.gnnea_gemm_f32(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a),
-                                   ptr(b), _ld(b), ptr(bias), float(beta), ptr(out),
-                                   _ld(out), ptr(ws), ws_bytes if ws is not None else 0,
-                                   stream_of(a.device)))
+            fn = L.gnnea_gemm_x3_f32 if x3 else L.gnnea_gemm_f32
+            check(fn(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a), ptr(b), _ld(b),
+                     ptr(bias), float(beta), ptr(out), _ld(out), ptr(ws),
+                     ws_bytes if ws is not None else 0, stream_of(a.device)))
     return out
 
 
@@ -388,10 +406,13 @@ def gemm_sliced(x, weight, bias=None):
     if bias is not None:
         bias = _featc(bias, torch.float32)
     L = _lib.lib()
-    ws_fn = L.gnnea_gemm_bf16_ws_bytes if bf else L.gnnea_gemm_ws_bytes
+    x3 = not bf and _use_x3(M, N, K, None)
+    ws_fn = L.gnnea_gemm_bf16_ws_bytes if bf else (
+        L.gnnea_gemm_x3_ws_bytes if x3 else L.gnnea_gemm_ws_bytes)
     ws_bytes = int(ws_fn(M, N, K))
     ws = _gemm_ws(x.device, ws_bytes) if ws_bytes > 0 else None
-    fn = L.gnnea_gemm_sliced_bf16 if bf else L.gnnea_gemm_sliced_f32
+    fn = L.gnnea_gemm_sliced_bf16 if bf else (
+        L.gnnea_gemm_x3_sliced_f32 if x3 else L.gnnea_gemm_sliced_f32)
     with torch.cuda.device(x.device):
         check(fn(0, 1, M, N, K, ptr(x), _ld(x), ptr(weight), _ld(weight), ptr(bias), 0.0,
                  ptr(hs), hs.stride(0), ptr(ws), ws_bytes if ws is not None else 0,

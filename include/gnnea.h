@@ -259,6 +259,20 @@ int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
                    int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
                    float* C, int64_t ldc, void* ws, int64_t ws_bytes, void* stream);
 
+/* fp32 GEMM on the bf16 MFMA: each operand element split exactly into three bf16 terms
+ * (h = bf16(x), m = bf16(x - h), l = bf16(x - h - m)), the six products of order <= 2 summed
+ * in fp32 (error at fp32 rounding level: the dropped terms are below 2^-24 relative); 6/16 of
+ * the f32 MFMA time.  Arguments and layouts as gnnea_gemm_f32 / _sliced_f32; workspace from
+ * gnnea_gemm_x3_ws_bytes (op(B) split once into three bf16 planes + split-K slabs; required).
+ * A transposed A (trans_a = 1) runs on the f32 MFMA kernel. */
+int64_t gnnea_gemm_x3_ws_bytes(int64_t M, int64_t N, int64_t K);
+int gnnea_gemm_x3_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                      int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
+                      float* C, int64_t ldc, void* ws, int64_t ws_bytes, void* stream);
+int gnnea_gemm_x3_sliced_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                             const float* A, int64_t lda, const float* B, int64_t ldb,
+                             const float* bias, float beta, float* Cs, int64_t sstride, void* ws,
+                             int64_t ws_bytes, void* stream);
 /* the same GEMM writing C slice-major (the layout gnnea_spmm_sliced_f32 gathers from):
  * element (r, c) of the M x N product at Cs[(c/64)*sstride + r*64 + c%64], sstride >= M*64.
  * The projection x W^T of a GCN layer writes its hidden this way at no extra cost. */

@@ -245,6 +245,17 @@ def test_gemm_vs_fp64(device, shape, ta, tb):
                  bool(tb), bias=torch.from_numpy(bias).to(device)).cpu()
     ref = (a.T if ta else a).astype(np.float64) @ (b.T if tb else b).astype(np.float64) + bias
     assert rel_err(y, ref) < 1e-5
+    # the same product through the three-way bf16 split (gnnea_gemm_x3_f32): fp32-level error
+    y3 = ops.gemm(torch.from_numpy(a).to(device), torch.from_numpy(b).to(device), bool(ta),
+                  bool(tb), bias=torch.from_numpy(bias).to(device), x3=True).cpu()
+    assert rel_err(y3, ref) < 1e-5
+    # magnitudes spread over many binades (the split terms of small entries are subnormal-free)
+    scale = np.exp2(rng.integers(-20, 20, a.shape)).astype(np.float32)
+    a2 = a * scale
+    y3 = ops.gemm(torch.from_numpy(a2).to(device), torch.from_numpy(b).to(device), bool(ta),
+                  bool(tb), x3=True).cpu()
+    ref2 = (a2.T if ta else a2).astype(np.float64) @ (b.T if tb else b).astype(np.float64)
+    assert rel_err(y3, ref2) < 1e-5
 
 
 # ------------------------------------------------------------------------------------------ #

@@ -1,4 +1,5 @@
-"""f32 MFMA GEMM shapes of the EA training step (cfg-4, 2M rows), gnnea.ops.gemm vs hipBLASLt
+"""fp32 GEMM shapes of the EA training step (cfg-4, 2M rows): gnnea.ops.gemm on the f32 MFMA and
+through the three-way bf16 split (x3) vs hipBLASLt
 (torch.mm) on the same operands; HIP events, median of reps.
 
     python tools/gemm_bench.py [--rows 2000000] [--reps 10] [--out gpurun_out/gemm_bench.json]
@@ -49,25 +50,29 @@ def main():
     W3 = torch.randn(2 * D, D, device=dev, generator=g)
     b = torch.randn(D, device=dev, generator=g)
     cases = {
-        "NT x.W^T+b [N,300]x[300,300]": (lambda: ops.gemm(X, W, trans_b=True, bias=b),
+        "NT x.W^T+b [N,300]x[300,300]": (lambda x3: ops.gemm(X, W, trans_b=True, bias=b, x3=x3),
                                          lambda: torch.addmm(b, X, W.t()), 2.0 * N * D * D),
-        "NN x.W [N,300]x[300,300]": (lambda: ops.gemm(X, W), lambda: torch.mm(X, W),
+        "NN x.W [N,300]x[300,300]": (lambda x3: ops.gemm(X, W, x3=x3), lambda: torch.mm(X, W),
                                      2.0 * N * D * D),
-        "NN x.[W^T|Kg] [N,300]x[300,600]": (lambda: ops.gemm(X, W2), lambda: torch.mm(X, W2),
-                                            4.0 * N * D * D),
-        "NN [dh|dg].[W;Kg^T] [N,600]x[600,300]": (lambda: ops.gemm(X2, W3),
+        "NN x.[W^T|Kg] [N,300]x[300,600]": (lambda x3: ops.gemm(X, W2, x3=x3),
+                                            lambda: torch.mm(X, W2), 4.0 * N * D * D),
+        "NN [dh|dg].[W;Kg^T] [N,600]x[600,300]": (lambda x3: ops.gemm(X2, W3, x3=x3),
                                                   lambda: torch.mm(X2, W3), 4.0 * N * D * D),
-        "TN dW = dY^T.X [300,N]x[N,300]": (lambda: ops.gemm(X, X, trans_a=True),
+        "TN dW = dY^T.X [300,N]x[N,300]": (lambda x3: ops.gemm(X, X, trans_a=True, x3=x3),
                                            lambda: torch.mm(X.t(), X), 2.0 * N * D * D),
     }
     res = {"rows": N}
     for name, (ours, ref, flop) in cases.items():
-        t0 = timeit(ours, args.reps)
+        t3 = timeit(lambda: ours(True), args.reps)
+        t0 = timeit(lambda: ours(False), args.reps)
         t1 = timeit(ref, args.reps)
-        e = float((ours() - ref()).abs().max() / ref().abs().max())
-        res[name] = {"gnnea_ms": round(t0, 4), "gnnea_TFLOPs": round(flop / t0 / 1e9, 1),
+        r = ref().double()
+        e0 = float((ours(False).double() - r).abs().max() / r.abs().max())
+        e3 = float((ours(True).double() - r).abs().max() / r.abs().max())
+        res[name] = {"x3_ms": round(t3, 4), "x3_TFLOPs": round(flop / t3 / 1e9, 1),
+                     "f32mfma_ms": round(t0, 4), "f32mfma_TFLOPs": round(flop / t0 / 1e9, 1),
                      "hipblaslt_ms": round(t1, 4), "hipblaslt_TFLOPs": round(flop / t1 / 1e9, 1),
-                     "rel_err_vs_hipblaslt": e}
+                     "rel_err_vs_hipblaslt": {"x3": e3, "f32mfma": e0}}
         print(name, res[name], flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
