@@ -91,6 +91,44 @@ __device__ __forceinline__ int64_t c_index(int64_t row, int64_t col, int64_t ldc
   return (col >> 6) * cs + row * ldc + (col & 63);
 }
 
+// Epilogue of the MFMA GEMM kernels: WT accumulator tiles in the 32x32 C/D map (col = lane&31,
+// row = (r&3) + 8*(r>>2) + 4*(lane>>5)) at rows m_w.., columns n_w..; addresses from one row base
+// per r and one column offset per t (no 64-bit multiply per element).  slab: split-K partials.
+template <int WT>
+__device__ __forceinline__ void store_tiles(const f32x16 (&acc)[WT], int M, int N, int m_w, int n_w,
+                                            int kh, int li, const float* __restrict__ bias,
+                                            float beta, float* __restrict__ C, int64_t ldc,
+                                            int64_t cs, float* __restrict__ slab, int split) {
+  int64_t coff[WT];
+  float bv[WT];
+  bool cok[WT];
+#pragma unroll
+  for (int t = 0; t < WT; ++t) {
+    const int col = n_w + t * 32 + li;
+    cok[t] = col < N;
+    coff[t] = slab ? col : c_index(0, col, ldc, cs);
+    bv[t] = (bias && !slab && cok[t]) ? bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m_w + (r & 3) + 8 * (r >> 2) + 4 * kh;
+    if (row >= M) continue;
+    float* base = slab ? slab + ((int64_t)split * M + row) * N : C + (int64_t)row * ldc;
+#pragma unroll
+    for (int t = 0; t < WT; ++t) {
+      if (!cok[t]) continue;
+      float* c = base + coff[t];
+      if (slab) {
+        *c = acc[t][r];
+      } else {
+        float o = acc[t][r] + bv[t];
+        if (beta != 0.f) o += beta * *c;
+        *c = o;
+      }
+    }
+  }
+}
+
 template <int TA, int TB, int WT, bool VEC, int BMX = GBM>
 __global__ __launch_bounds__(4 * BMX) void k_gemm_wide(int M, int N, int K, const float* __restrict__ A,
                                                    int64_t lda, const float* __restrict__ B,
@@ -159,27 +197,8 @@ __global__ __launch_bounds__(4 * BMX) void k_gemm_wide(int M, int N, int K, cons
     __syncthreads();
   }
 
-  // epilogue: 32x32 C/D map  col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-#pragma unroll
-  for (int t = 0; t < WT; ++t) {
-    const int col = n0 + wn * 32 * WT + t * 32 + li;
-    if (col >= N) continue;
-    const float bv = (bias && !slab) ? bias[col] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-      if (row >= M) continue;
-      const float v = acc[t][r];
-      if (slab) {
-        slab[((int64_t)split * M + row) * N + col] = v;
-      } else {
-        float o = v + bv;
-        float* c = C + c_index(row, col, ldc, cs);
-        if (beta != 0.f) o += beta * *c;
-        *c = o;
-      }
-    }
-  }
+  store_tiles<WT>(acc, M, N, m0 + wm * 32, n0 + wn * 32 * WT, kh, li, bias, beta, C, ldc, cs,
+                  slab, split);
 }
 
 // ---- fp32 GEMM on the bf16 MFMA: three-way split operands, six products ------------------------
@@ -384,27 +403,8 @@ __global__ __launch_bounds__(XNT) void k_gemm_x3(int M, int N, int K, const floa
     __syncthreads();
   }
 
-  // epilogue: 32x32 C/D map  col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-#pragma unroll
-  for (int t = 0; t < WT; ++t) {
-    const int col = n0 + wn * 32 * WT + t * 32 + li;
-    if (col >= N) continue;
-    const float bv = (bias && !slab) ? bias[col] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-      if (row >= M) continue;
-      const float v = acc[t][r];
-      if (slab) {
-        slab[((int64_t)split * M + row) * N + col] = v;
-      } else {
-        float o = v + bv;
-        float* c = C + c_index(row, col, ldc, cs);
-        if (beta != 0.f) o += beta * *c;
-        *c = o;
-      }
-    }
-  }
+  store_tiles<WT>(acc, M, N, m0 + wm * 32, n0 + wn * 32 * WT, kh, li, bias, beta, C, ldc, cs,
+                  slab, split);
 }
 
 // slab reduction in fixed split order (deterministic); 4 outputs per thread when the rows allow
