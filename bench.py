@@ -178,9 +178,10 @@ def main():
                     help="entities per KG (default: cfg-4, 1M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sinkhorn", action="store_true")
-    ap.add_argument("--partition", choices=("features", "rows"), default="features",
-                    help="inside a KG group: feature-column slices (no exchange) or row blocks "
-                         "with the RCCL halo all-gather")
+    ap.add_argument("--partition", choices=("tiles", "features", "rows"), default="tiles",
+                    help="inside a KG group: row blocks x 2 feature-column slices (tiles) or "
+                         "feature-column slices of all rows (features) - both exchange-free - or "
+                         "row blocks with the RCCL halo all-gather (rows)")
     ap.add_argument("--no-train", action="store_true",
                     help="skip the side measurement of the row-sharded HGCN-EA training step")
     ap.add_argument("--train-steps", type=int, default=5)
@@ -215,8 +216,9 @@ def main():
     log("rank %d: shard rows %d nnz %d built in %.1fs" % (rank, shard.n_rows, shard.nnz,
                                                          time.time() - t0))
     gen = torch.Generator(device=device).manual_seed(1 + rank)
-    h_local = torch.randn(shard.n_rows if world > 1 else shard.n_cols, Dl, device=device,
-                          generator=gen)
+    free = part.kind in ("features", "tiles")  # exchange-free: the whole KG's column slice
+    h_local = torch.randn(shard.n_cols if (world == 1 or free) else shard.n_rows, Dl,
+                          device=device, generator=gen)
     h_local /= h_local.norm(dim=1, keepdim=True)
     h_full = (torch.empty(shard.n_cols, Dl, device=device)
               if shard.g > 1 and part.kind == "rows" else None)
@@ -224,7 +226,7 @@ def main():
     # H as the projection GEMM of a GCN layer leaves it: slice-major [ceil(D/64)][rows][64]
     # (gnnea_gemm_sliced_f32 writes this layout; ops.GCNLayerFn) where the table exceeds the
     # Infinity Cache, row-major otherwise (or with --layout rowmajor)
-    sliced = (args.layout == "sliced" and (shard.g == 1 or part.kind == "features")
+    sliced = (args.layout == "sliced" and (shard.g == 1 or free)
               and ops.use_sliced(shard.n_cols, Dl, torch.float32))
     hs = ops.slice_pack(h_local) if sliced else None
 
@@ -245,7 +247,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    if shard.g == 1 or part.kind == "features":
+    if shard.g == 1 or free:
         kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     else:  # own-block + remote-block SpMM launches (the wait for the halo excluded)
         kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3])
@@ -281,7 +283,7 @@ def main():
         # the SpMM is launched once per diagonal (KG) block of rows when the gathered matrix is
         # larger than the Infinity Cache (gnnea.ops._blocks): bytes and time per launch
         launches = 1
-        if shard.g == 1 or part.kind == "features":
+        if shard.g == 1 or free:
             blocks = ops._blocks(shard.csr, h_local)
             launches = len(blocks)
         traffic = gather_model_bytes(shard.n_rows, shard.nnz, Dl)
@@ -297,8 +299,8 @@ def main():
                                    % (n, shard_t(n), D),
                        "nnz": int(round(total_nnz)), "nodes": 2 * n, "D": D,
                        "parallelism": "single GPU" if world == 1 else
-                       ("2 KG groups of %d GPUs, feature-column slices (no exchange)" % shard.g
-                        if part.kind == "features" else
+                       ("2 KG groups of %d GPUs, %d row blocks x %d feature-column slices "
+                        "(no exchange)" % (shard.g, part.gr, part.gc) if free else
                         "2 KG groups of %d GPUs, row blocks + RCCL halo all-gather" % shard.g)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

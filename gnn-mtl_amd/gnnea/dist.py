@@ -4,11 +4,15 @@ Layout (one process per GPU, torch.distributed; backend "nccl" is RCCL over xGMI
   * the adjacency is block-diagonal over the two KGs (no cross-KG entries), so ranks
     [0, W/2) serve KG1 and [W/2, W) serve KG2 — no traffic between the two groups
     (W = 1 keeps the whole graph on one GPU; W = 2 is one KG per GPU, nothing to exchange);
-  * inside a KG group of g = W/2 ranks, two partitions are implemented:
+  * inside a KG group of g = W/2 ranks, three partitions are implemented:
     - "features" (default): every rank holds the whole KG adjacency and a 16-B-aligned slice
       of the feature columns (300 = 76+76+76+72 at g = 4).  relu(A·H) is column-separable,
       so the aggregation needs NO exchange; in a full layer the group exchange moves to the
       projection input (all-gather of the previous layer's column slices, same volume);
+    - "tiles": g = gr x gc ranks, gc = 2 column slices (>= 148 columns: slice-major tables)
+      times gr = g/2 blocks of destination rows; every rank gathers from the whole KG's column
+      slice, so again NO exchange (8 GPUs: 2 x 2 tiles of 500k rows x 150 columns instead of
+      four 76-column slices of all rows);
     - "rows": each rank owns n/g destination rows (KG-local column ids) and all-gathers the
       group's projected rows (the halo: on uniform random graphs nearly every remote row is
       referenced) with RCCL, overlapped with the aggregation over its own rows.
@@ -37,6 +41,7 @@ class Partition:
         self.col0, self.col1 = 0, D
         if world == 1:
             self.kg, self.g, self.li = None, 1, 0
+            self.gr = self.gc = 1
             self.n_cols = 2 * n
             self.row0, self.row1 = 0, 2 * n
             self.global_row0 = 0
@@ -44,19 +49,23 @@ class Partition:
             if world % 2:
                 raise ValueError("gnnea.dist: world size must be 1 or even (two KG groups)")
             self.g = world // 2
-            if kind == "rows" and n % self.g:
-                raise ValueError("gnnea.dist: entities per KG must divide by the group size")
-            if kind not in ("rows", "features"):
-                raise ValueError("gnnea.dist: partition must be 'rows' or 'features'")
+            if kind not in ("rows", "features", "tiles"):
+                raise ValueError("gnnea.dist: partition must be 'rows', 'features' or 'tiles'")
+            # tiles: gr row blocks x gc column slices, gc = 2 when the group is even (slices
+            # of >= 148 columns keep the slice-major tables; 76-column slices do not)
+            self.gc = (2 if self.g % 2 == 0 else 1) if kind == "tiles" else \
+                (self.g if kind == "features" else 1)
+            self.gr = self.g // self.gc
+            if n % self.gr:
+                raise ValueError("gnnea.dist: entities per KG must divide by the row blocks")
             self.kg = rank // self.g
             self.li = rank % self.g
             self.n_cols = n
-            if kind == "features":
-                self.row0, self.row1 = 0, n
-                self.col0, self.col1 = feature_slices(D, self.g)[self.li]
-            else:
-                rows = n // self.g
-                self.row0, self.row1 = self.li * rows, (self.li + 1) * rows
+            ri, ci = self.li // self.gc, self.li % self.gc
+            rows = n // self.gr
+            self.row0, self.row1 = ri * rows, (ri + 1) * rows
+            if kind != "rows":
+                self.col0, self.col1 = feature_slices(D, self.gc)[ci]
             self.global_row0 = self.kg * n + self.row0
 
     @property
@@ -130,7 +139,7 @@ class KGShard:
             return DeviceCSR.from_coo(torch.from_numpy(rr.astype(np.int32)).to(device),
                                       torch.from_numpy(cc.astype(np.int32)).to(device),
                                       torch.from_numpy(vv).to(device), self.part.n_rows, ncols)
-        if self.part.g == 1 or kind == "features":
+        if self.part.g == 1 or kind in ("features", "tiles"):
             self.csr = up(r, c, v, self.part.n_cols)
             self.csr_own = self.csr_remote = None
         else:
@@ -159,7 +168,7 @@ class KGShard:
         from . import ops
         from ._lib import GNNEA_ACT_IDENTITY
         rec = (lambda k: events[k].record()) if events is not None else (lambda k: None)
-        if self.part.g == 1 or self.part.kind == "features":  # no exchange in the aggregation
+        if self.part.g == 1 or self.part.kind in ("features", "tiles"):  # no exchange
             rec(0)
             if hs is not None:
                 ops.spmm_sliced(self.csr, hs, h_local.shape[1], act, out=out)

@@ -44,16 +44,22 @@ def _worker(rank, world, port, n, t, q, kind="rows"):
         else:
             h_local = H[part.global_row0:part.global_row0 + part.n_rows]
         h_full = torch.empty(part.n_cols, 16, dtype=torch.float64)
-        if kind == "features" and part.g > 1:
-            # column slice of the whole KG: no exchange; gather slices for the check below
+        if kind in ("features", "tiles") and part.g > 1:
+            # the rank's rows x column slice, gathered from the whole KG's slice: no exchange
             hk = H[part.kg * n:(part.kg + 1) * n, part.col0:part.col1]
             ys = coo_aggregate(r, c, v, part.n_rows, hk)
-            sl = [torch.empty(n, b - a, dtype=torch.float64)
-                  for a, b in (Partition(n, k, world, kind, 16).col0_col1()
-                               for k in part.group_ranks(part.kg))]
-            dist.all_gather(sl, ys, group=group)
-            y = torch.cat(sl, dim=1)
-        elif part.g == 1:
+            outs = [torch.empty_like(ys) for _ in range(world)]
+            dist.all_gather(outs, ys)
+            if rank == 0:
+                full = torch.empty(2 * n, 16, dtype=torch.float64)
+                for k in range(world):
+                    pk = Partition(n, k, world, kind, 16)
+                    full[pk.kg * n + pk.row0:pk.kg * n + pk.row1, pk.col0:pk.col1] = outs[k]
+                R, Cc, V = synth.adjacency_coo(triples, 2 * n, reference_order=False)
+                ref = coo_aggregate(R, Cc, V, 2 * n, H)
+                q.put(float((full - ref).abs().max()))
+            return
+        if part.g == 1:
             y = coo_aggregate(r, c, v, part.n_rows, h_local)
         else:
             # the product's overlap split: owned block from h_local, the rest from the halo
@@ -64,8 +70,6 @@ def _worker(rank, world, port, n, t, q, kind="rows"):
         outs = [torch.empty_like(y) for _ in range(world)]
         dist.all_gather(outs, y)
         if rank == 0:
-            if kind == "features" and part.g > 1:  # every group member holds the whole KG
-                outs = [outs[0], outs[part.g]]
             full = torch.cat(outs)  # ranks are ordered KG1 rows then KG2 rows
             R, Cc, V = synth.adjacency_coo(triples, 2 * n, reference_order=False)
             ref = coo_aggregate(R, Cc, V, 2 * n, H)
@@ -75,7 +79,8 @@ def _worker(rank, world, port, n, t, q, kind="rows"):
 
 
 @pytest.mark.parametrize("world,kind", [(2, "rows"), (4, "rows"), (4, "features"),
-                                        (8, "features")])
+                                        (8, "features"), (4, "tiles"), (8, "tiles"),
+                                        (2, "tiles")])
 def test_sharded_aggregation_matches_single_process(world, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -88,6 +93,23 @@ def test_sharded_aggregation_matches_single_process(world, kind):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) < 1e-12
+
+
+def test_tiles_partition_covers_each_kg_once():
+    from gnnea.dist import Partition
+    n, D = 1000, 300
+    for world in (2, 4, 8):
+        cover = {}
+        for k in range(world):
+            p = Partition(n, k, world, "tiles", D)
+            assert p.n_cols == n and p.gr * p.gc == p.g
+            assert p.g < 2 or (p.col1 - p.col0) >= 148  # slice-major widths
+            for r in range(p.row0, p.row1, 100):
+                cover.setdefault((p.kg, r), []).append((p.col0, p.col1))
+        for sl in cover.values():  # every (KG, row) covered by column slices tiling [0, D)
+            sl.sort()
+            assert sl[0][0] == 0 and sl[-1][1] == D
+            assert all(sl[i][1] == sl[i + 1][0] for i in range(len(sl) - 1))
 
 
 def test_feature_slices_aligned():

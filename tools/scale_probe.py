@@ -45,19 +45,21 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--dtype", default="f32", choices=("f32", "bf16"))
+    ap.add_argument("--kind", default="tiles", choices=("tiles", "features"),
+                    help="exchange-free partition inside a KG group (bench.py --partition)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "scale_probe.json"))
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     n, t = args.n, 10 * args.n
     D = 300
     dt = torch.float32 if args.dtype == "f32" else torch.bfloat16
-    res = {"n": n, "D": D, "dtype": args.dtype, "worlds": {}}
+    res = {"n": n, "D": D, "dtype": args.dtype, "partition": args.kind, "worlds": {}}
     for W in [int(w) for w in args.worlds.split(",")]:
         # ranks of one KG group differ only in their column slice; probe the first and last
         ranks = [0] if W <= 2 else [0, W // 2 - 1]
         per = []
         for rank in ranks:
-            sh = KGShard(n, t, 3000, rank, W, dev, kind="features", D=D)
+            sh = KGShard(n, t, 3000, rank, W, dev, kind=args.kind, D=D)
             Dl = sh.part.col1 - sh.part.col0
             g = torch.Generator(device=dev).manual_seed(1 + rank)
             h = torch.randn(sh.n_cols, Dl, device=dev, generator=g).to(dt)
