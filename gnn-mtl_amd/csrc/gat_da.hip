@@ -61,22 +61,35 @@ __global__ __launch_bounds__(256) void k_gat_da_part(const typename Vec4<T>::raw
   }
 }
 
-__global__ __launch_bounds__(256) void k_gat_da_final(const float* __restrict__ part, int nb,
+// 64 columns per workgroup, the 8 waves stride the partials (4 independent sums per lane),
+// combined in wave order through LDS: deterministic, latency hidden across the waves.
+__global__ __launch_bounds__(512) void k_gat_da_final(const float* __restrict__ part, int nb,
                                                       int D, float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= D) return;
-  float s0 = 0.f, s1 = 0.f;
-  int b = 0;
-  for (; b + 2 <= nb; b += 2) {
-    s0 += part[(int64_t)b * ((D + 3) & ~3) + c];
-    s1 += part[(int64_t)(b + 1) * ((D + 3) & ~3) + c];
+  __shared__ float red[8][64];
+  const int w = wave_id(), lane = lane_id();
+  const int c = blockIdx.x * 64 + lane;
+  const int64_t ld = (D + 3) & ~3;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < D) {
+    int b = w;
+    for (; b + 24 < nb; b += 32) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s[u] += part[(int64_t)(b + 8 * u) * ld + c];
+    }
+    for (int u = 0; b < nb; b += 8, ++u) s[u & 3] += part[(int64_t)b * ld + c];
   }
-  if (b < nb) s0 += part[(int64_t)b * ((D + 3) & ~3) + c];
-  out[c] = s0 + s1;
+  red[w][lane] = (s[0] + s[1]) + (s[2] + s[3]);
+  __syncthreads();
+  if (w == 0 && c < D) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t += red[k][lane];
+    out[c] = t;
+  }
 }
 
 static int da_blocks(int64_t n_rows) {
-  const int64_t b = (n_rows + 63) / 64;  // >= 64 rows per workgroup
+  const int64_t b = (n_rows + 255) / 256;  // >= 256 rows per workgroup
   return (int)(b < 1 ? 1 : (b > kDaBlocks ? kDaBlocks : b));
 }
 
@@ -112,7 +125,7 @@ static int gat_da_t(const T* H, int64_t ldh, int64_t n_rows, int heads, int d_he
   }
 #undef GNNEA_DA
   GNNEA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_gat_da_final, dim3((D + 255) / 256), dim3(256), 0, s, part, nb, D, out);
+  hipLaunchKernelGGL(k_gat_da_final, dim3((D + 63) / 64), dim3(512), 0, s, part, nb, D, out);
   GNNEA_LAUNCH_CHECK();
   return 0;
 }

@@ -4,6 +4,7 @@ The library is loaded after ``import torch`` so that it binds to the HIP runtime
 loaded (same soname, ``libamdhip64.so.7``): device pointers and streams are shared.  There is no
 fallback: if the library is missing every product op raises.
 """
+import contextlib
 import ctypes
 import os
 
@@ -200,8 +201,27 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_of(device):
+    """The caller's current HIP stream on ``device`` (the raw handle query costs ~0.2 us against
+    ~3 us for building a torch Stream object: it runs once per kernel launch)."""
+    if _RAW_STREAM is not None:
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        return ctypes.c_void_p(_RAW_STREAM(idx))
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+_SAME_DEVICE = contextlib.nullcontext()
+
+
+def on_device(device):
+    """torch.cuda.device(device) only when it is not already current (the common case pays no
+    device switch on entry and exit)."""
+    if device.index is None or device.index == torch.cuda.current_device():
+        return _SAME_DEVICE
+    return torch.cuda.device(device)
 
 
 def require_device(*tensors):

@@ -54,7 +54,7 @@ class DeviceCSR:
         val_out = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
         perm = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev) if want_perm else None
         nnz_out = torch.zeros(1, dtype=torch.int64, device=dev)
-        with torch.cuda.device(dev):
+        with _lib.on_device(dev):
             _lib.check(L.gnnea_coo_to_csr(
                 _lib.ptr(row), _lib.ptr(col), row.element_size(), _lib.ptr(val), nnz, n_rows,
                 n_cols, _lib.ptr(rowptr), _lib.ptr(col_out), _lib.ptr(val_out), _lib.ptr(perm),
@@ -69,7 +69,7 @@ class DeviceCSR:
     def row_ids(self):
         L = _lib.lib()
         rows = torch.empty(max(self.nnz, 1), dtype=torch.int32, device=self.device)
-        with torch.cuda.device(self.device):
+        with _lib.on_device(self.device):
             _lib.check(L.gnnea_csr_expand_rows(_lib.ptr(self.rowptr), self.n_rows, self.nnz,
                                                _lib.ptr(rows), _lib.stream_of(self.device)))
         return rows[:self.nnz]
@@ -86,7 +86,7 @@ class DeviceCSR:
         if getattr(self, "_tpos", None) is None:
             t = self.transpose()
             inv = torch.empty(max(self.nnz, 1), dtype=torch.int64, device=self.device)
-            with torch.cuda.device(self.device):
+            with _lib.on_device(self.device):
                 _lib.check(_lib.lib().gnnea_perm_invert(_lib.ptr(t.perm), self.nnz,
                                                         _lib.ptr(inv),
                                                         _lib.stream_of(self.device)))

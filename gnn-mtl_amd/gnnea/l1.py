@@ -32,7 +32,7 @@ def pairs(A, B):
         raise ValueError("gnnea.l1.pairs: shape mismatch %s vs %s" % (A.shape, B.shape))
     n, D = A.shape
     out = torch.empty(n, dtype=torch.float64, device=A.device)
-    with torch.cuda.device(A.device):
+    with _lib.on_device(A.device):
         check(_lib.lib().gnnea_l1_pairs_f32(ptr(A), A.stride(0), ptr(B), B.stride(0), n, D,
                                             ptr(out), stream_of(A.device)))
     return out
@@ -46,7 +46,7 @@ def keys(Q, X):
     if X.shape[1] != D:
         raise ValueError("gnnea.l1.keys: dim mismatch")
     out = torch.empty((nq, nx), dtype=torch.float32, device=Q.device)
-    with torch.cuda.device(Q.device):
+    with _lib.on_device(Q.device):
         check(_lib.lib().gnnea_l1_keys_f32(ptr(Q), Q.stride(0), nq, ptr(X), X.stride(0), nx, D,
                                            ptr(out), nx, stream_of(Q.device)))
     return out
@@ -60,7 +60,7 @@ def ranks(Q, X, diag):
         raise ValueError("gnnea.l1.ranks: need nq <= nx and equal dims")
     diag = diag.to(device=Q.device, dtype=torch.float64).contiguous()
     out = torch.empty(nq, dtype=torch.int32, device=Q.device)
-    with torch.cuda.device(Q.device):
+    with _lib.on_device(Q.device):
         check(_lib.lib().gnnea_l1_rank_f32(ptr(Q), Q.stride(0), nq, ptr(X), X.stride(0),
                                            X.shape[0], D, ptr(diag), ptr(out),
                                            stream_of(Q.device)))
@@ -93,7 +93,7 @@ def topk(Q, X, K, skip=0, want_dist=False):
     chunk = max(1, min(nq, KEY_BUDGET // max(1, 4 * nx)))
     kbuf = torch.empty((min(chunk, nq), nx), dtype=torch.float32, device=dev)
     st = stream_of(dev)
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         for q0 in range(0, nq, chunk):
             n = min(chunk, nq - q0)
             Qc = Q[q0:q0 + n]

@@ -6,8 +6,6 @@ with A, B the L1 distances of the gathered pair / negative-pair rows.  The forwa
 materialises the (t*k) x D gathers; the backward gathers, per output row, the integer-weighted
 sign vectors of the terms that touch it (no atomics: deterministic).
 """
-import weakref
-
 import numpy as np
 import torch
 
@@ -32,7 +30,30 @@ def _idx(a, device, n_rows):
     return torch.from_numpy(arr).to(device)
 
 
-_INCIDENCE = {}
+_DEV_IDX = {}
+
+
+def _idx_cached(a, device, n_rows):
+    """_idx with the device copy of a host index array cached per array: the reference hands the
+    same numpy objects every epoch (data[split][:, 0] views of one array, negatives reassigned
+    every 50 epochs, models/models_ea.py:89-91 / run/train_ea.py:61-62), so the copy, the range
+    check and the incidence build behind it happen once per negative set, not once per step.
+    Keyed by (data pointer, shape, strides, dtype) with the owning array held alive; like the
+    CSR cache per adjacency object, an array modified IN PLACE is not noticed (the reference
+    never does that)."""
+    if not isinstance(a, np.ndarray):
+        return _idx(a, device, n_rows)
+    owner = a.base if a.base is not None else a
+    key = (a.__array_interface__["data"][0], a.shape, a.strides, a.dtype.str, str(device),
+           n_rows)
+    hit = _DEV_IDX.get(key)
+    if hit is not None and hit[0] is owner:
+        return hit[1]
+    t = _idx(a, device, n_rows)
+    if len(_DEV_IDX) >= 48:
+        _DEV_IDX.clear()
+    _DEV_IDX[key] = (owner, t)
+    return t
 
 
 CHUNK = 256  # incidence entries per backward work item
@@ -71,16 +92,18 @@ _INCIDENCE = {}
 
 
 def incidence(idx, n_rows):
-    """Incidence + work items of the six index tensors, cached per tuple of tensor objects: the
-    negatives change every 50 epochs, the loss runs every one."""
-    key = tuple(id(a) for a in idx) + (n_rows,)
+    """Incidence + work items of the six index tensors, cached per tuple of device buffers (data
+    pointer, size; the entry holds the tensors alive so a pointer cannot be reused by other
+    indices): the negatives change every 50 epochs, the loss runs every one.  Keyed by buffer,
+    not by Python object: autograd hands the backward fresh wrappers of its saved tensors."""
+    key = tuple((a.data_ptr(), a.numel(), a.dtype) for a in idx) + (n_rows,)
     hit = _INCIDENCE.get(key)
-    if hit is not None and all(r() is a for r, a in zip(hit[0], idx)):
+    if hit is not None:
         return hit[1]
     inc = Incidence(idx, n_rows)
     if len(_INCIDENCE) > 8:
         _INCIDENCE.clear()
-    _INCIDENCE[key] = (tuple(weakref.ref(a) for a in idx), inc)
+    _INCIDENCE[key] = (tuple(idx), inc)
     return inc
 
 
@@ -96,7 +119,7 @@ class MarginLossFn(torch.autograd.Function):
         A = torch.empty(t, dtype=torch.float32, device=dev)
         h = torch.empty(2 * t * k, dtype=torch.float32, device=dev)
         m = torch.empty(2 * t * k + t, dtype=torch.float32, device=dev)
-        with torch.cuda.device(dev):
+        with _lib.on_device(dev):
             check(_lib.lib().gnnea_margin_fwd_f32(
                 ptr(out), out.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1),
                 ptr(nl2), ptr(nr2), ptr(A), ptr(h), ptr(m), stream_of(dev)))
@@ -113,7 +136,7 @@ class MarginLossFn(torch.autograd.Function):
         grad = torch.zeros((N, D), dtype=torch.float32, device=out.device)
         scratch = torch.empty((max(inc.n_slots, 1), D), dtype=torch.float32, device=out.device)
         g = g.reshape(1).to(torch.float32).contiguous()
-        with torch.cuda.device(out.device):
+        with _lib.on_device(out.device):
             check(_lib.lib().gnnea_margin_bwd_f32(
                 ptr(out), out.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1),
                 ptr(nl2), ptr(nr2), ptr(m), ptr(inc.csr.col), ptr(inc.items),
@@ -135,7 +158,7 @@ def margin_loss(outputs, left, right, neg_left, neg_right, neg2_left, neg2_right
     if checked:
         idx = list(arrays)
     else:
-        idx = [_idx(a, outputs.device, outputs.shape[0]) for a in arrays]
+        idx = [_idx_cached(a, outputs.device, outputs.shape[0]) for a in arrays]
     if idx[0].numel() != t or any(a.numel() != t * k for a in idx[2:]):
         raise ValueError("gnnea.margin: index arrays must have t and t*k entries")
     if outputs.dtype == torch.bfloat16:  # bf16 models (cfg-5): the loss is an fp32 reduction

@@ -82,6 +82,20 @@ def _gemm_ws(device, nbytes):
     return buf
 
 
+_WSQ = {}
+
+
+def _ws_query(fn, M, N, K):
+    """Workspace size of a GEMM shape (a pure function of the shape: cached, it runs per call)."""
+    key = (fn.__name__, M, N, K)
+    v = _WSQ.get(key)
+    if v is None:
+        if len(_WSQ) > 256:
+            _WSQ.clear()
+        v = _WSQ[key] = int(fn(M, N, K))
+    return v
+
+
 _SMALL_OPERAND = 1 << 22
 # fp32 products at least this large (M*N*K) run on the bf16 MFMA with three-way split operands
 # (gnnea_gemm_x3_f32: fp32-level rounding, 6/16 of the f32 MFMA time); smaller ones on the f32
@@ -90,13 +104,18 @@ GEMM_X3 = True
 X3_MIN_MNK = 1 << 26
 
 
+X3_MIN_M = 4096  # tall A only (DBP15K scale, 30k rows: x3 55 us vs f32 MFMA 75 us, measured)
+
+
 def _use_x3(M, N, K, x3, trans_a=False):
     """x3 splits op(B) into bf16 planes once per call: only for a small B (the weight) times a
     tall, K-contiguous A.  The weight gradients (trans_a: both operands tall) and the bias
     column sums (B = the tall gradient) stay on the f32 MFMA."""
     if trans_a or N * K > _SMALL_OPERAND:
         return False
-    return (GEMM_X3 and M * N * K >= X3_MIN_MNK) if x3 is None else bool(x3)
+    if x3 is not None:
+        return bool(x3)
+    return GEMM_X3 and M >= X3_MIN_M and M * N * K >= X3_MIN_MNK
 
 
 def _ld(t):
@@ -148,9 +167,9 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
     x3 = not bf and _use_x3(M, N, K, x3, trans_a)
     ws_fn = L.gnnea_gemm_bf16_ws_bytes if bf else (
         L.gnnea_gemm_x3_ws_bytes if x3 else L.gnnea_gemm_ws_bytes)
-    ws_bytes = int(ws_fn(M, N, K))
+    ws_bytes = _ws_query(ws_fn, M, N, K)
     ws = _gemm_ws(a.device, ws_bytes) if ws_bytes > 0 else None
-    with torch.cuda.device(a.device):
+    with _lib.on_device(a.device):
         if bf:
             cd = _lib.GNNEA_BF16 if out.dtype == torch.bfloat16 else _lib.GNNEA_F32
             check(L.gnnea_gemm_bf16(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a),
@@ -186,8 +205,7 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = gemm(dy, x, trans_a=True, out_dtype=weight.dtype if bf else None)  # [out,N]·[N,in]
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            ones = torch.ones((1, dy.shape[0]), dtype=dy.dtype, device=dy.device)
-            db = gemm(ones, dy, out_dtype=ctx.bias_dtype if bf else None).view(-1)
+            db = colsum(dy, ctx.bias_dtype)
         return dx, dw, db
 
 
@@ -265,7 +283,7 @@ def spmm(csr, x, act=_lib.GNNEA_ACT_IDENTITY, out=None, beta=0.0, out_dtype=None
         raise TypeError("gnnea.spmm: out must be fp32 or bf16")
     L = _lib.lib()
     st = stream_of(x.device)
-    with torch.cuda.device(x.device):
+    with _lib.on_device(x.device):
         for r0, r1 in _blocks(csr, x):
             rp = ctypes.c_void_p(csr.rowptr.data_ptr() + 4 * r0)
             if x.dtype == torch.bfloat16:
@@ -290,7 +308,7 @@ def act_bwd(dy, y, act):
     g = torch.empty_like(y)
     fn = _lib.lib().gnnea_act_bwd_bf16 if y.dtype == torch.bfloat16 else \
         _lib.lib().gnnea_act_bwd_f32
-    with torch.cuda.device(y.device):
+    with _lib.on_device(y.device):
         check(fn(ptr(dy), ptr(y), ptr(g), y.numel(), int(act), stream_of(y.device)))
     return g
 
@@ -336,7 +354,7 @@ def slice_pack(x):
     x = _rows(x)
     n, D = x.shape
     xs = sliced_empty(n, D, x.device, x.dtype)
-    with torch.cuda.device(x.device):
+    with _lib.on_device(x.device):
         check(_sfn("gnnea_slice_pack", x.dtype)(ptr(x), _ld(x), n, D, ptr(xs), xs.stride(0),
                                                stream_of(x.device)))
     return xs
@@ -348,7 +366,7 @@ def act_bwd_sliced(dy, y, act):
     dy = _rows(dy, y.dtype)
     n, D = y.shape
     gs = sliced_empty(n, D, y.device, y.dtype)
-    with torch.cuda.device(y.device):
+    with _lib.on_device(y.device):
         check(_sfn("gnnea_act_bwd_sliced", y.dtype)(ptr(dy), _ld(dy), ptr(y), _ld(y), n, D,
                                                     int(act), ptr(gs), gs.stride(0),
                                                     stream_of(y.device)))
@@ -376,7 +394,7 @@ def spmm_sliced(csr, xs, D, act=_lib.GNNEA_ACT_IDENTITY, out=None, out_dtype=Non
                          % (csr.n_rows, D))
     L = _lib.lib()
     st = stream_of(xs.device)
-    with torch.cuda.device(xs.device):
+    with _lib.on_device(xs.device):
         for r0, r1 in csr.row_blocks():
             if xs.dtype == torch.bfloat16:
                 yd = _lib.GNNEA_BF16 if out.dtype == torch.bfloat16 else _lib.GNNEA_F32
@@ -409,11 +427,11 @@ def gemm_sliced(x, weight, bias=None):
     x3 = not bf and _use_x3(M, N, K, None)
     ws_fn = L.gnnea_gemm_bf16_ws_bytes if bf else (
         L.gnnea_gemm_x3_ws_bytes if x3 else L.gnnea_gemm_ws_bytes)
-    ws_bytes = int(ws_fn(M, N, K))
+    ws_bytes = _ws_query(ws_fn, M, N, K)
     ws = _gemm_ws(x.device, ws_bytes) if ws_bytes > 0 else None
     fn = L.gnnea_gemm_sliced_bf16 if bf else (
         L.gnnea_gemm_x3_sliced_f32 if x3 else L.gnnea_gemm_sliced_f32)
-    with torch.cuda.device(x.device):
+    with _lib.on_device(x.device):
         check(fn(0, 1, M, N, K, ptr(x), _ld(x), ptr(weight), _ld(weight), ptr(bias), 0.0,
                  ptr(hs), hs.stride(0), ptr(ws), ws_bytes if ws is not None else 0,
                  stream_of(x.device)))
@@ -525,7 +543,7 @@ def highway_fwd(csr, hidden, gate_pre, resid, bias_gate, act):
     bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
     fn = _lib.lib().gnnea_spmm_highway_bf16 if hidden.dtype == torch.bfloat16 else \
         _lib.lib().gnnea_spmm_highway_f32
-    with torch.cuda.device(hidden.device):
+    with _lib.on_device(hidden.device):
         for r0, r1 in _blocks(csr, hidden):
             check(fn(
                 ctypes.c_void_p(csr.rowptr.data_ptr() + 4 * r0), ptr(csr.col), ptr(csr.val),
@@ -555,7 +573,7 @@ def highway_bwd(dy, S, G, resid, act, want_dresid=True, dS=None, dgate=None, dre
     fn = _lib.lib().gnnea_highway_bwd_ld_bf16 if S.dtype == torch.bfloat16 else \
         _lib.lib().gnnea_highway_bwd_ld_f32
     N, D = S.shape
-    with torch.cuda.device(S.device):
+    with _lib.on_device(S.device):
         check(fn(
             ptr(dy), ptr(S), ptr(G), ptr(resid), S.stride(0), N, D, ptr(dS), _ld(dS),
             ptr(dgate), _ld(dgate), ptr(dresid if want_dresid else None),
@@ -598,7 +616,7 @@ def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act):
     G = torch.empty_like(out)
     bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
     L = _lib.lib()
-    with torch.cuda.device(Zs.device):
+    with _lib.on_device(Zs.device):
         for r0, r1 in csr.row_blocks():
             check(L.gnnea_spmm_highway_sliced_f32(
                 _off32(csr.rowptr, r0), ptr(csr.col), ptr(csr.val), r1 - r0, D, ptr(Zs),
@@ -618,7 +636,7 @@ def highway_bwd_sliced(dy, S, G, resid, act, want_dresid, dgate):
     N, D = S.shape
     dSs = sliced_empty(N, D, S.device)
     dres = torch.empty_like(S) if want_dresid else None
-    with torch.cuda.device(S.device):
+    with _lib.on_device(S.device):
         check(_lib.lib().gnnea_highway_bwd_sliced_f32(
             ptr(dy), ptr(S), ptr(G), ptr(resid), S.stride(0), N, D, ptr(dSs), dSs.stride(0),
             ptr(dgate), _ld(dgate), ptr(dres), _ld(dres) if want_dresid else D, int(act),
@@ -626,10 +644,33 @@ def highway_bwd_sliced(dy, S, G, resid, act, want_dresid, dgate):
     return dSs, dres
 
 
-def colsum(t):
-    """Column sums of a row-major [N, D] matrix (the bias gradient), as a [1,N]·[N,D] GEMM."""
-    ones = torch.ones((1, t.shape[0]), dtype=t.dtype, device=t.device)
-    return gemm(ones, t).view(-1)
+_ONES = {}
+
+
+def _ones(n, device):
+    key = (str(device), n)
+    o = _ONES.get(key)
+    if o is None:
+        if len(_ONES) > 16:
+            _ONES.clear()
+        o = _ONES[key] = torch.ones((n, 1), dtype=torch.float32, device=device)
+    return o
+
+
+def colsum(t, out_dtype=None):
+    """Column sums of a row-major [N, D] matrix (the bias gradients): one streaming pass with
+    a deterministic two-stage sum (gnnea_gat_da_* with one all-ones head weight) instead of a
+    [1, N]·[N, D] split-K GEMM; fp32 sums, returned in ``out_dtype`` (default t's dtype).  t may
+    be a column block of a wider row-major buffer."""
+    t = _rows(t)
+    N, D = t.shape
+    out_dtype = out_dtype or t.dtype
+    if D % 4 or t.stride(0) % 4 or N == 0:  # rows must be whole 4-element vectors
+        t = _featc(t)
+        ones = torch.ones((1, N), dtype=t.dtype, device=t.device)
+        return gemm(ones, t, out_dtype=out_dtype if t.dtype == torch.bfloat16 else None).view(-1)
+    s = gat_da(t, _ones(N, t.device), 1, D)
+    return s if out_dtype == torch.float32 else s.to(out_dtype)
 
 
 class HighwayLayerFn(torch.autograd.Function):
@@ -744,7 +785,7 @@ def gat_scores(H, a_all, heads, d_head):
     N = H.shape[0]
     s1 = torch.empty((N, heads), dtype=torch.float32, device=H.device)
     s2 = torch.empty_like(s1)
-    with torch.cuda.device(H.device):
+    with _lib.on_device(H.device):
         check(_gat_fn("gnnea_gat_scores", H.dtype)(ptr(H), H.stride(0), N, heads, d_head,
                                                    ptr(a_all), ptr(s1), ptr(s2),
                                                    stream_of(H.device)))
@@ -781,7 +822,7 @@ def gat_forward(csr, H, a32, heads, d_head, alpha, act, em=None, row0=0):
     m = torch.empty((N, heads), dtype=torch.float32, device=H.device)
     den = torch.empty_like(m)
     fwd = _gat_fn("gnnea_gat_fwd", H.dtype)
-    with torch.cuda.device(H.device):
+    with _lib.on_device(H.device):
         for r0, r1 in _blocks(csr, H):  # per KG block when H exceeds the Infinity Cache
             check(fwd(_off32(csr.rowptr, r0), ptr(csr.col), r1 - r0, ptr(H), H.stride(0),
                       heads, d_head, _off(s1, row0 + r0), ptr(s2), float(alpha), ptr(em),
@@ -814,7 +855,7 @@ def gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha, act, 
     ds1 = torch.empty((N, heads), dtype=torch.float32, device=dev)
     ds2 = torch.empty((H.shape[0], heads), dtype=torch.float32, device=dev)
     tpos = csr.tpos()
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         # G = dL/dh' and the per-node record {s1, m, 1/den, G.h'} (relu / identity: Y = h')
         check(_gat_fn("gnnea_gat_bwd_prep", H.dtype)(
             N, heads, d_head, ptr(dY), ptr(Y), Y.stride(0), _off(s1, row0), ptr(m), ptr(den),
@@ -850,7 +891,7 @@ def gat_da(H, ds, heads, d_head):
     ws = _gemm_ws(H.device, ws_bytes)
     out = torch.empty(D, dtype=torch.float32, device=H.device)
     ds = _featc(ds, torch.float32)
-    with torch.cuda.device(H.device):
+    with _lib.on_device(H.device):
         check(_gat_fn("gnnea_gat_da", H.dtype)(ptr(H), H.stride(0), n, heads, d_head, ptr(ds),
                                                ptr(out), ptr(ws), ws_bytes,
                                                stream_of(H.device)))

@@ -16,6 +16,7 @@ ST_DONE, ST_ITERS, ST_REASON, ST_SLOT = 0, 1, 2, 3
 # (falls back to 1 above J = 8192), 1 = fused log-domain passes (no I x J workspace)
 DEFAULT_VARIANT = 0
 SD_ERR, SD_TPREV, SD_LOSS = 8, 9, 10
+MAX_BATCH = 100  # iterations enqueued between two host polls of the status block, at most
 
 
 class SinkhornResult:
@@ -69,29 +70,34 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
         variant=int(variant), reserved=0, ws=ws.data_ptr())
     pp = ctypes.byref(prob)
     st = stream_of(dev)
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         check(L.gnnea_sinkhorn_init(pp, st))
         run = 0
+        # The device decides every stop itself (iterations past it are no-op launches), so the
+        # host polls the status block only between batches that grow geometrically up to
+        # MAX_BATCH: few host syncs on long solves, an overshoot of at most one batch of no-ops.
         if mode == _lib.GNNEA_SK_KNOPP:
-            # utils/ot_loss.py:50  while err > stopThr and cpt < numItermax  (err starts at 1)
+            # utils/ot_loss.py:50  while err > stopThr and cpt < numItermax  (err starts at 1);
+            # iteration k's err is evaluated by iteration k+1's combine: batches end at 10n + 2
             if 1.0 > tol and max_iter > 0:
-                # iteration k's err is evaluated by iteration k+1's combine: batch ends at k+1
-                bounds = [0, 2] + list(range(12, max_iter + 10, 10))
-                for lo, hi in zip(bounds[:-1], bounds[1:]):
+                step, hi = 10, 2
+                while run < max_iter:
                     hi = min(hi, max_iter)
-                    if hi <= lo:
-                        break
-                    check(L.gnnea_sinkhorn_iterate(pp, lo, hi - lo, st))
+                    check(L.gnnea_sinkhorn_iterate(pp, run, hi - run, st))
                     run = hi
                     if _status(ws)[0][ST_DONE].item():
                         break
+                    hi = run + step
+                    step = min(2 * step, MAX_BATCH)
         else:
+            step = max(1, batch)
             while run < max_iter:
-                n = min(batch, max_iter - run)
+                n = min(step, max_iter - run)
                 check(L.gnnea_sinkhorn_iterate(pp, run, n, st))
                 run += n
                 if _status(ws)[0][ST_DONE].item():
                     break
+                step = min(2 * step, max(batch, MAX_BATCH))
         prob.iters_run = run
         plan = torch.empty((I, J), dtype=plan_dtype, device=dev) if want_plan else None
         row_sum = torch.empty(I, dtype=torch.float64, device=dev)

@@ -20,23 +20,10 @@ from utils.ot_loss import sinkhorn
 
 
 def _index(idx, device, n_rows):
-    """Checked device int64 copy of a host index array, cached per array object (negatives are
-    regenerated every 50 epochs; the loss reads them every epoch)."""
-    if torch.is_tensor(idx):
-        return margin._idx(idx, device, n_rows)
-    cache = _index.cache
-    key = id(idx)
-    hit = cache.get(key)
-    if hit is not None and hit[0] is idx and hit[1].device == device and hit[2] == n_rows:
-        return hit[1]
-    t = margin._idx(idx, device, n_rows)
-    if len(cache) > 16:
-        cache.clear()
-    cache[key] = (idx, t, n_rows)
-    return t
-
-
-_index.cache = {}
+    """Checked device int64 copy of a host index array, cached per array (negatives are
+    regenerated every 50 epochs; the loss reads them, and views data[split][:, 0] of the same
+    pair array, every epoch): gnnea.margin._idx_cached."""
+    return margin._idx_cached(idx, device, n_rows)
 
 
 def margin_loss(outputs, left, right, neg_left, neg_right, neg2_left, neg2_right, t, k):

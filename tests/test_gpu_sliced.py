@@ -325,3 +325,20 @@ def test_gcn_layer_sliced_bf16_matches_rowmajor(device, monkeypatch):
     for g, w in zip(got, ref):
         assert g.dtype == w.dtype
         assert rel_err(g.float().cpu(), w.float().cpu()) < 2e-2
+
+
+@pytest.mark.parametrize("N,D,dt", [(1, 300, torch.float32), (2_000_001, 300, torch.float32),
+                                    (30000, 12, torch.bfloat16), (777, 10, torch.float32)])
+def test_colsum_vs_fp64(device, N, D, dt):
+    """Bias gradients: streaming column sums (gnnea_gat_da_*), also over a column block."""
+    from gnnea import ops
+    torch.manual_seed(N)
+    t = torch.randn(N, D, device=device).to(dt)
+    ref = t.double().sum(0).cpu()
+    got = ops.colsum(t)
+    assert got.dtype == dt
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    assert rel_err(got.float().cpu(), ref) < tol
+    if D % 4 == 0:
+        wide = torch.randn(N, 2 * D + 4, device=device).to(dt)
+        assert rel_err(ops.colsum(wide[:, :D]).float().cpu(), wide[:, :D].double().sum(0).cpu()) < tol
