@@ -13,6 +13,7 @@
 // registers before the MFMAs of the current one (one barrier per K step).
 // Large-K / small-output products (weight gradients, K = N_nodes) split K over workgroups into
 // fp32 slabs reduced in fixed order by a second kernel: deterministic, no atomics.
+#include <cstdlib>
 #include "common.h"
 
 namespace gnnea {
@@ -606,7 +607,11 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
                        (int)N, (int)K, ldp, planes, pstride);
     GNNEA_LAUNCH_CHECK();
   }
-  const int wt = pick_wt(N);
+  int wt = pick_wt(N);
+  if (const char* e = getenv("GNNEA_X3_WT")) {  // tuning override only
+    const int v = atoi(e);
+    if (v >= 1 && v <= 5) wt = v;
+  }
   const int64_t bn = 64 * wt;
   const int tiles_n = (int)((N + bn - 1) / bn);
   const int tiles = (int)(((M + XBM - 1) / XBM) * tiles_n);

@@ -58,7 +58,59 @@ __device__ __forceinline__ float l1_rows(const float* __restrict__ a, const floa
 
 __device__ __forceinline__ float sgn(float x) { return (float)((x > 0.f) - (x < 0.f)); }
 
-template <int VEC, int NC>
+// Sign codes of a term (float4 lane map only): byte q = c*64 + lane holds, for its 4 columns,
+// 2 bits each, the 2-bit two's complement of sgn(x_a - x_b): 01 = +1, 11 = -1, 00 = equal.  The backward reads them instead of
+// re-gathering both rows: sgn(x_r - x_other) is +code at the a-end, -code at the b-end, the exact
+// values the row gather would give (same fp32 operands).
+template <int NC>
+__device__ __forceinline__ float l1_rows_code(const float* __restrict__ a,
+                                              const float* __restrict__ b, int D,
+                                              uint8_t* __restrict__ code) {
+  RowFrag<4, NC> x, y;
+  load_row<4, NC>(a, D, x);
+  load_row<4, NC>(b, D, y);
+  const int lane = lane_id();
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    uint32_t byte = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = x.v[c][e] - y.v[c][e];
+      s += fabsf(d);
+      byte |= ((d > 0.f) ? 1u : (d < 0.f) ? 3u : 0u) << (2 * e);
+    }
+    const int q = c * 64 + lane;
+    if (4 * q < D) code[q] = (uint8_t)byte;
+  }
+  return wave_sum(s);
+}
+
+// L1 distance of two loaded row fragments (wave-reduced); CODE also stores the term's sign codes
+// (float4 map, see l1_rows_code).  Same per-lane order and reduction as l1_rows.
+template <int VEC, int NC, bool CODE>
+__device__ __forceinline__ float l1_frag(const RowFrag<VEC, NC>& x, const RowFrag<VEC, NC>& y,
+                                         int D, uint8_t* __restrict__ code) {
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    uint32_t byte = 0;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const float d = x.v[c][e] - y.v[c][e];
+      s += fabsf(d);
+      if constexpr (CODE) byte |= ((d > 0.f) ? 1u : (d < 0.f) ? 3u : 0u) << (2 * e);
+    }
+    if constexpr (CODE) {
+      static_assert(VEC == 4, "sign codes use the float4 lane map");
+      const int q = c * 64 + lane_id();
+      if (4 * q < D) code[q] = (uint8_t)byte;
+    }
+  }
+  return wave_sum(s);
+}
+
+template <int VEC, int NC, bool CODE = false>
 __global__ __launch_bounds__(256) void k_margin_fwd(const float* __restrict__ out, int64_t ld,
                                                     int D, int t, int k,
                                                     const int64_t* __restrict__ left,
@@ -68,13 +120,22 @@ __global__ __launch_bounds__(256) void k_margin_fwd(const float* __restrict__ ou
                                                     const int64_t* __restrict__ nl2,
                                                     const int64_t* __restrict__ nr2,
                                                     float* __restrict__ A, float* __restrict__ h,
-                                                    float* __restrict__ m) {
+                                                    float* __restrict__ m,
+                                                    uint8_t* __restrict__ codes = nullptr,
+                                                    int64_t sb = 0) {
   __shared__ float As;
   __shared__ int nact;
   const int i = blockIdx.x, w = wave_id(), lane = lane_id();
   if (threadIdx.x == 0) nact = 0;
+  const int64_t tk = (int64_t)t * k;
+  auto l1 = [&](int64_t ra, int64_t rb, int64_t term) {
+    if constexpr (CODE)
+      return l1_rows_code<NC>(out + ra * ld, out + rb * ld, D, codes + term * sb);
+    else
+      return l1_rows<VEC, NC>(out + ra * ld, out + rb * ld, D);
+  };
   if (w == 0) {
-    const float a = l1_rows<VEC, NC>(out + left[i] * ld, out + right[i] * ld, D);
+    const float a = l1(left[i], right[i], 2 * tk + i);
     if (lane == 0) {
       As = a;
       A[i] = a;
@@ -82,17 +143,30 @@ __global__ __launch_bounds__(256) void k_margin_fwd(const float* __restrict__ ou
   }
   __syncthreads();
   const float d1 = As + 1.0f;
-  const int64_t tk = (int64_t)t * k;
-  for (int q = w; q < 2 * k; q += 4) {
-    const int s = q >= k, j = q - s * k;
-    const int64_t e = (int64_t)i * k + j;
-    const int64_t ra = s ? nl2[e] : nl1[e], rb = s ? nr2[e] : nr1[e];
-    const float B = l1_rows<VEC, NC>(out + ra * ld, out + rb * ld, D);
-    const float hv = fmaxf(d1 - B, 0.f);
-    if (lane == 0) {
-      h[s * tk + e] = hv;
-      m[s * tk + e] = hv > 0.f ? -1.f : 0.f;
-      if (hv > 0.f) atomicAdd(&nact, 1);
+  // U negative terms per wave per round: all 2U row loads are issued before the first reduction
+  constexpr int U = 4;
+  for (int q0 = w * U; q0 < 2 * k; q0 += 4 * U) {
+    RowFrag<VEC, NC> xa[U], xb[U];
+    int64_t term[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + u < 2 * k ? q0 + u : q0;
+      const int s = q >= k, j = q - s * k;
+      const int64_t e = (int64_t)i * k + j;
+      term[u] = s * tk + e;
+      load_row<VEC, NC>(out + (s ? nl2[e] : nl1[e]) * ld, D, xa[u]);
+      load_row<VEC, NC>(out + (s ? nr2[e] : nr1[e]) * ld, D, xb[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (q0 + u >= 2 * k) break;  // wave-uniform
+      const float B = l1_frag<VEC, NC, CODE>(xa[u], xb[u], D, codes + term[u] * sb);
+      const float hv = fmaxf(d1 - B, 0.f);
+      if (lane == 0) {
+        h[term[u]] = hv;
+        m[term[u]] = hv > 0.f ? -1.f : 0.f;
+        if (hv > 0.f) atomicAdd(&nact, 1);
+      }
     }
   }
   __syncthreads();
@@ -203,6 +277,90 @@ __global__ __launch_bounds__(256) void k_margin_bwd(const float* __restrict__ ou
     if (d >= D) continue;
 #pragma unroll
     for (int e = 0; e < VEC; ++e) dst[d + e] = c0 * acc.v[c][e];
+  }
+}
+
+// Backward from the forward's sign codes: per work item (one row's chunk of incidence entries)
+// the wave reads, for every active incident term, its NC code bytes per lane (coalesced, 64 B per
+// chunk) instead of gathering the other row: no feature-row traffic at all.  Entries are added
+// in incidence order with the same integer multipliers as k_margin_bwd, so the gradient is
+// bit-identical to it.
+template <int NC>
+__global__ __launch_bounds__(256) void k_margin_bwd_code(int D, int64_t M,
+                                                         const float* __restrict__ m,
+                                                         const uint8_t* __restrict__ codes,
+                                                         int64_t sb,
+                                                         const int32_t* __restrict__ inc_ent,
+                                                         const int4* __restrict__ items,
+                                                         int n_items,
+                                                         const float* __restrict__ gout,
+                                                         float inv, float* __restrict__ grad,
+                                                         int64_t ldg,
+                                                         float* __restrict__ scratch) {
+  const int it = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
+  if (it >= n_items) return;
+  const int4 item = items[it];
+  const int row = item.x, beg = item.y, end = item.z, slot = item.w;
+  const int lane = lane_id();
+  bool own[NC];
+  int acc[NC][4];  // integer multipliers x signs: exact, so order-free
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    own[c] = 4 * (c * 64 + lane) < D;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[c][e] = 0;
+  }
+  for (int base = beg; base < end; base += 64) {
+    const int cnt = min(64, end - base);
+    int f = 0;  // signed multiplier: +m_j at the a-end, -m_j at the b-end (|m_j| <= 2k)
+    int64_t j = 0;
+    if (lane < cnt) {
+      const int64_t p = inc_ent[base + lane];
+      const bool role_b = p >= M;
+      j = role_b ? p - M : p;
+      const int mj = (int)m[j];
+      f = role_b ? -mj : mj;
+    }
+    unsigned long long act = __ballot(f != 0);
+    while (act) {
+      // up to U active entries per round, branch-free (an exhausted slot re-reads lane 0's
+      // valid term with multiplier 0) so all U code loads are in flight together
+      constexpr int U = 16;
+      int fq[U];
+      uint32_t cb[U][NC];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool v = act != 0ull;
+        const int q = v ? __builtin_ctzll(act) : 0;
+        act &= act - 1;
+        fq[u] = v ? readlane_i(f, q) : 0;
+        const int64_t jq = ((int64_t)readlane_i((int)(j >> 32), q) << 32) |
+                           (uint32_t)readlane_i((int)(j & 0xffffffff), q);
+        const uint8_t* cp = codes + jq * sb;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) cb[u][c] = own[c] ? cp[c * 64 + lane] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            // v_bfe_i32 of the 2-bit field, then v_mad_i32_i24
+            const int sg = ((int)(cb[u][c] << (30 - 2 * e))) >> 30;
+            acc[c][e] = __mul24(sg, fq[u]) + acc[c][e];
+          }
+      }
+    }
+  }
+  const float c0 = slot < 0 ? gout[0] * inv : 1.0f;
+  float* dst = slot < 0 ? grad + (int64_t)row * ldg : scratch + (int64_t)slot * D;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (!own[c]) continue;
+    const int d = (c * 64 + lane) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dst[d + e] = c0 * (float)acc[c][e];
   }
 }
 
@@ -319,6 +477,72 @@ extern "C" int gnnea_margin_bwd_f32(const float* out, int64_t ld, int32_t D, int
   const bool aligned_out = true;
   GNNEA_MARGIN_DISPATCH(launch_bwd, a, m, inc_ent, (const int4*)items, n_items, grad_loss, scale,
                         grad, ldg, scratch, s);
+  if (n_long > 0)
+    hipLaunchKernelGGL(k_margin_combine, dim3(div_up(n_long, 4)), dim3(256), 0, s, long_rows,
+                       long_ptr, n_long, D, scratch, grad_loss, scale, grad, ldg);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---- sign-code forward / backward (float4 rows: D % 4 == 0, ld % 4 == 0, 16-B aligned out) ----
+extern "C" int gnnea_margin_fwd_code_f32(const float* out, int64_t ld, int32_t D, int32_t t,
+                                         int32_t k, const int64_t* left, const int64_t* right,
+                                         const int64_t* neg_left, const int64_t* neg_right,
+                                         const int64_t* neg2_left, const int64_t* neg2_right,
+                                         float* A, float* h, float* m, void* codes, int64_t sb,
+                                         void* stream) {
+  const MarginArgs a{out, ld, D, t, k, left, right, neg_left, neg_right, neg2_left, neg2_right};
+  if (const int rc = margin_check(a)) return rc;
+  if (a.t == 0) return 0;
+  if (!A || !m || (a.k > 0 && !h) || !codes) return GNNEA_EINVAL;
+  if (D % 4 || ld % 4 || (((uintptr_t)out) & 15) || sb < (D + 3) / 4) return GNNEA_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+#define GNNEA_FC(N)                                                                            \
+  case N:                                                                                      \
+    hipLaunchKernelGGL((k_margin_fwd<4, N, true>), dim3(t), dim3(256), 0, s, out, ld, D, t, k, \
+                       left, right, neg_left, neg_right, neg2_left, neg2_right, A, h, m,       \
+                       (uint8_t*)codes, sb);                                                   \
+    break;
+  switch (div_up(D, 256)) {
+    GNNEA_FC(1)
+    GNNEA_FC(2)
+    GNNEA_FC(3)
+    GNNEA_FC(4)
+    default: return GNNEA_EINVAL;
+  }
+#undef GNNEA_FC
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int gnnea_margin_bwd_code_f32(int32_t D, int32_t t, int32_t k, const float* m,
+                                         const void* codes, int64_t sb, const int32_t* inc_ent,
+                                         const int32_t* items, int32_t n_items,
+                                         const int32_t* long_rows, const int32_t* long_ptr,
+                                         int32_t n_long, float* scratch, const float* grad_loss,
+                                         float scale, float* grad, int64_t ldg, void* stream) {
+  if (n_items < 0 || n_long < 0 || D < 0 || D > 1024 || D % 4 || t < 0 || k < 0)
+    return GNNEA_EINVAL;
+  if (n_items == 0) return 0;
+  if (!m || !codes || !inc_ent || !items || !grad_loss || !grad || ldg < D || sb < (D + 3) / 4)
+    return GNNEA_EINVAL;
+  if (n_long > 0 && (!long_rows || !long_ptr || !scratch)) return GNNEA_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t M = 2ll * t * k + t;
+#define GNNEA_BC(N)                                                                            \
+  case N:                                                                                      \
+    hipLaunchKernelGGL((k_margin_bwd_code<N>), dim3(div_up(n_items, 4)), dim3(256), 0, s, D, M, \
+                       m, (const uint8_t*)codes, sb, inc_ent, (const int4*)items, n_items,     \
+                       grad_loss, scale, grad, ldg, scratch);                                  \
+    break;
+  switch (div_up(D, 256)) {
+    GNNEA_BC(1)
+    GNNEA_BC(2)
+    GNNEA_BC(3)
+    GNNEA_BC(4)
+    default: return GNNEA_EINVAL;
+  }
+#undef GNNEA_BC
   if (n_long > 0)
     hipLaunchKernelGGL(k_margin_combine, dim3(div_up(n_long, 4)), dim3(256), 0, s, long_rows,
                        long_ptr, n_long, D, scratch, grad_loss, scale, grad, ldg);

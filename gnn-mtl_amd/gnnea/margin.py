@@ -57,6 +57,7 @@ def _idx_cached(a, device, n_rows):
 
 
 CHUNK = 256  # incidence entries per backward work item
+CODES = True  # sign-code backward for float4 rows (tests flip it to compare with the row gather)
 
 
 class Incidence:
@@ -116,20 +117,32 @@ class MarginLossFn(torch.autograd.Function):
             raise TypeError("gnnea.margin: outputs must be fp32")
         N, D = out.shape
         dev = out.device
+        M = 2 * t * k + t
         A = torch.empty(t, dtype=torch.float32, device=dev)
         h = torch.empty(2 * t * k, dtype=torch.float32, device=dev)
-        m = torch.empty(2 * t * k + t, dtype=torch.float32, device=dev)
+        m = torch.empty(M, dtype=torch.float32, device=dev)
+        # float4 rows: the forward also stores 2-bit sign codes per column (D/4 bytes per term,
+        # 90 MB at t=4500, k=125, D=300) so the backward reads them instead of both rows
+        use_codes = CODES and D % 4 == 0 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0
         with _lib.on_device(dev):
-            check(_lib.lib().gnnea_margin_fwd_f32(
-                ptr(out), out.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1),
-                ptr(nl2), ptr(nr2), ptr(A), ptr(h), ptr(m), stream_of(dev)))
-        ctx.save_for_backward(out, left, right, nl1, nr1, nl2, nr2, m)
+            if use_codes:
+                sb = D // 4
+                codes = torch.empty(M * sb, dtype=torch.uint8, device=dev)
+                check(_lib.lib().gnnea_margin_fwd_code_f32(
+                    ptr(out), out.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1),
+                    ptr(nl2), ptr(nr2), ptr(A), ptr(h), ptr(m), ptr(codes), sb, stream_of(dev)))
+            else:
+                codes = None
+                check(_lib.lib().gnnea_margin_fwd_f32(
+                    ptr(out), out.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1),
+                    ptr(nl2), ptr(nr2), ptr(A), ptr(h), ptr(m), stream_of(dev)))
+        ctx.save_for_backward(out, left, right, nl1, nr1, nl2, nr2, m, codes)
         ctx.tk = (t, k)
         return torch.sum(h) / (2.0 * t * k)
 
     @staticmethod
     def backward(ctx, g):
-        out, left, right, nl1, nr1, nl2, nr2, m = ctx.saved_tensors
+        out, left, right, nl1, nr1, nl2, nr2, m, codes = ctx.saved_tensors
         t, k = ctx.tk
         N, D = out.shape
         inc = incidence((left, right, nl1, nr1, nl2, nr2), N)
@@ -137,6 +150,13 @@ class MarginLossFn(torch.autograd.Function):
         scratch = torch.empty((max(inc.n_slots, 1), D), dtype=torch.float32, device=out.device)
         g = g.reshape(1).to(torch.float32).contiguous()
         with _lib.on_device(out.device):
+            if codes is not None:
+                check(_lib.lib().gnnea_margin_bwd_code_f32(
+                    D, t, k, ptr(m), ptr(codes), D // 4, ptr(inc.csr.col), ptr(inc.items),
+                    inc.items.shape[0], ptr(inc.long_rows), ptr(inc.long_ptr),
+                    inc.long_rows.numel(), ptr(scratch), ptr(g), 1.0 / (2.0 * t * k), ptr(grad),
+                    D, stream_of(out.device)))
+                return grad, None, None, None, None, None, None, None, None
             check(_lib.lib().gnnea_margin_bwd_f32(
                 ptr(out), out.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1),
                 ptr(nl2), ptr(nr2), ptr(m), ptr(inc.csr.col), ptr(inc.items),

@@ -413,6 +413,23 @@ int gnnea_margin_bwd_f32(const float* out, int64_t ld, int32_t D, int32_t t, int
                          const float* grad_loss, float scale, float* grad, int64_t ldg,
                          void* stream);
 
+/* Sign-code variant (D % 4 == 0, ld % 4 == 0, out 16-B aligned): the forward also writes, per
+ * term j, codes[j*sb + q] for q < ceil(D/4): 2 bits per column of columns 4q..4q+3, the 2-bit
+ * two's complement of sgn(out[a] - out[b]) (01: +1, 11: -1, 00: equal; a/b the term's
+ * first/second end); sb >= D/4.
+ * The backward then reads those codes instead of the rows (no out / index arguments): the same
+ * sum with the same multipliers in the same order, bit-identical to gnnea_margin_bwd_f32. */
+int gnnea_margin_fwd_code_f32(const float* out, int64_t ld, int32_t D, int32_t t, int32_t k,
+                              const int64_t* left, const int64_t* right, const int64_t* neg_left,
+                              const int64_t* neg_right, const int64_t* neg2_left,
+                              const int64_t* neg2_right, float* A, float* h, float* m,
+                              void* codes, int64_t sb, void* stream);
+int gnnea_margin_bwd_code_f32(int32_t D, int32_t t, int32_t k, const float* m, const void* codes,
+                              int64_t sb, const int32_t* inc_ent, const int32_t* items,
+                              int32_t n_items, const int32_t* long_rows, const int32_t* long_ptr,
+                              int32_t n_long, float* scratch, const float* grad_loss, float scale,
+                              float* grad, int64_t ldg, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

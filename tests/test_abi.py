@@ -30,7 +30,8 @@ def test_header_declares_the_hot_path():
                  "gnnea_highway_bwd_bf16", "gnnea_highway_bwd_ld_f32", "gnnea_highway_bwd_ld_bf16", "gnnea_gemm_bf16", "gnnea_gat_scores_bf16",
                  "gnnea_gat_fwd_bf16", "gnnea_gat_bwd_prep_bf16", "gnnea_gat_bwd_src_bf16",
                  "gnnea_gat_bwd_dst_bf16", "gnnea_spmm_sliced_f32", "gnnea_slice_pack_f32",
-                 "gnnea_act_bwd_sliced_f32", "gnnea_gemm_sliced_f32"):
+                 "gnnea_act_bwd_sliced_f32", "gnnea_gemm_sliced_f32",
+                 "gnnea_margin_fwd_code_f32", "gnnea_margin_bwd_code_f32"):
         assert must in names
 
 

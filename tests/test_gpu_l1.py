@@ -190,3 +190,31 @@ def test_margin_backward_deterministic(device):
         margin_loss(x, *idx, t, k).backward()
         grads.append(x.grad.cpu().numpy())
     assert (grads[0] == grads[1]).all() and (grads[0] == grads[2]).all()
+
+
+@pytest.mark.parametrize("N,D,t,k", [(3000, 300, 200, 40), (500, 1024, 30, 9), (60, 8, 50, 6),
+                                     (40, 64, 300, 30)])
+def test_margin_sign_codes_match_row_gather(device, N, D, t, k):
+    """The sign-code backward (the forward stores 2 bits per column, the backward reads them)
+    gives the row-gather backward's gradient bit for bit: hub rows (chunked items), tied columns
+    (duplicate rows: code 00) and every float4 width."""
+    from gnnea import margin
+    rng = np.random.default_rng(D * 7 + k)
+    vec = (0.05 * rng.standard_normal((N, D))).astype(np.float32)
+    vec[: N // 4, : D // 2] = vec[N // 4: 2 * (N // 4), : D // 2]  # exact ties in half the columns
+    x0 = torch.from_numpy(vec).to(device)
+    idx = [rng.integers(0, N // 2, t), rng.integers(0, N, t)] + \
+        [rng.integers(0, 40 if i % 2 == 0 else N // 2, t * k) for i in range(4)]
+    out = []
+    try:
+        for codes in (True, False):
+            margin.CODES = codes
+            x = x0.clone().requires_grad_(True)
+            loss = margin.margin_loss(x, *idx, t, k)
+            loss.backward()
+            out.append((float(loss), x.grad.cpu().numpy()))
+    finally:
+        margin.CODES = True
+    assert out[0][0] == out[1][0]
+    assert (out[0][1] == out[1][1]).all()
+    assert np.abs(out[0][1]).sum() > 0
