@@ -2,23 +2,23 @@
 //   da1[h] = Σ_i ds1[i,h] · H[i, h-block],   da2[h] = Σ_j ds2[j,h] · H[j, h-block]
 // i.e. out[c] = Σ_r ds[r, c / d_head] · H[r, c] for every column c of the head-concatenated H.
 // One streaming pass over H (N·D·s bytes, HBM bound) instead of an [N, heads]ᵀ·[N, D] GEMM whose
-// off-diagonal head blocks are thrown away: stage 1, a fixed grid of workgroups each sums a
-// contiguous row range into registers (4 waves on interleaved rows, lane = float4 column chunk),
-// combined across the waves in LDS into one partial row per workgroup; stage 2 adds the
+// off-diagonal head blocks are thrown away: stage 1, up to 256 workgroups each sums a
+// contiguous row range into registers (16 waves on interleaved rows, 4 rows in flight per wave,
+// lane = float4 column chunk), combined across the waves in LDS into one partial row per workgroup; stage 2 adds the
 // workgroup partials in workgroup order (deterministic, no atomics).
 #include "common.h"
 
 namespace gnnea {
 
-constexpr int kDaBlocks = 1024;
+constexpr int kDaBlocks = 256, kDaWaves = 16;
 
 template <int NCH, typename T>
-__global__ __launch_bounds__(256) void k_gat_da_part(const typename Vec4<T>::raw* __restrict__ H,
+__global__ __launch_bounds__(64 * kDaWaves) void k_gat_da_part(const typename Vec4<T>::raw* __restrict__ H,
                                                      int64_t ldh4, int64_t n_rows, int heads,
                                                      int d_head, int D4,
                                                      const float* __restrict__ ds,
                                                      float* __restrict__ part) {
-  __shared__ float4 red[4][64 * NCH];
+  __shared__ float4 red[kDaWaves][64 * NCH];
   const int w = wave_id(), lane = lane_id();
   const int64_t rpb = (n_rows + gridDim.x - 1) / gridDim.x;
   const int64_t r0 = (int64_t)blockIdx.x * rpb, r1 = min(n_rows, r0 + rpb);
@@ -33,27 +33,45 @@ __global__ __launch_bounds__(256) void k_gat_da_part(const typename Vec4<T>::raw
       hd[q][t] = min(c / d_head, heads - 1);
     }
   }
-  for (int64_t r = r0 + w; r < r1; r += 4) {
+  auto fma_row = [&](int64_t r, const float4 (&h)[NCH]) {
     const float* dr = ds + r * heads;
 #pragma unroll
     for (int q = 0; q < NCH; ++q) {
-      const int c4 = lane + 64 * q;
-      if (c4 < D4) {
-        const float4 h = Vec4<T>::get(H[r * ldh4 + c4]);
-        acc[q].x = fmaf(dr[hd[q][0]], h.x, acc[q].x);
-        acc[q].y = fmaf(dr[hd[q][1]], h.y, acc[q].y);
-        acc[q].z = fmaf(dr[hd[q][2]], h.z, acc[q].z);
-        acc[q].w = fmaf(dr[hd[q][3]], h.w, acc[q].w);
-      }
+      acc[q].x = fmaf(dr[hd[q][0]], h[q].x, acc[q].x);
+      acc[q].y = fmaf(dr[hd[q][1]], h[q].y, acc[q].y);
+      acc[q].z = fmaf(dr[hd[q][2]], h[q].z, acc[q].z);
+      acc[q].w = fmaf(dr[hd[q][3]], h[q].w, acc[q].w);
     }
+  };
+  auto load_row = [&](int64_t r, float4 (&h)[NCH]) {
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+      const int c4 = lane + 64 * q;
+      h[q] = c4 < D4 ? Vec4<T>::get(H[r * ldh4 + c4]) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  // the wave's rows r0+w, r0+w+W, ... in order; four of them loaded before their FMAs
+  constexpr int W = kDaWaves;
+  int64_t r = r0 + w;
+  for (; r + 3 * W < r1; r += 4 * W) {
+    float4 h[4][NCH];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load_row(r + W * u, h[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) fma_row(r + W * u, h[u]);
+  }
+  for (; r < r1; r += W) {
+    float4 h[NCH];
+    load_row(r, h);
+    fma_row(r, h);
   }
 #pragma unroll
   for (int q = 0; q < NCH; ++q) red[w][lane + 64 * q] = acc[q];
   __syncthreads();
-  for (int c4 = threadIdx.x; c4 < D4; c4 += 256) {
+  for (int c4 = threadIdx.x; c4 < D4; c4 += 64 * W) {
     float4 s = red[0][c4];
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
+    for (int k = 1; k < W; ++k) {
       const float4 o = red[k][c4];
       s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
     }
@@ -89,7 +107,7 @@ __global__ __launch_bounds__(512) void k_gat_da_final(const float* __restrict__ 
 }
 
 static int da_blocks(int64_t n_rows) {
-  const int64_t b = (n_rows + 255) / 256;  // >= 256 rows per workgroup
+  const int64_t b = (n_rows + 63) / 64;  // >= 64 rows per workgroup (4 per wave), <= 256 of them
   return (int)(b < 1 ? 1 : (b > kDaBlocks ? kDaBlocks : b));
 }
 
@@ -113,7 +131,7 @@ static int gat_da_t(const T* H, int64_t ldh, int64_t n_rows, int heads, int d_he
   typedef typename Vec4<T>::raw R;
 #define GNNEA_DA(N)                                                                            \
   case N:                                                                                      \
-    hipLaunchKernelGGL((k_gat_da_part<N, T>), dim3(nb), dim3(256), 0, s, (const R*)H, ldh / 4,  \
+    hipLaunchKernelGGL((k_gat_da_part<N, T>), dim3(nb), dim3(64 * kDaWaves), 0, s, (const R*)H, ldh / 4,  \
                        n_rows, heads, d_head, D4, ds, part);                                   \
     break;
   switch (nch) {
