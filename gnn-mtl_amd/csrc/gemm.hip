@@ -14,6 +14,7 @@
 // Large-K / small-output products (weight gradients, K = N_nodes) split K over workgroups into
 // fp32 slabs reduced in fixed order by a second kernel: deterministic, no atomics.
 #include <cstdlib>
+#include <type_traits>
 #include "common.h"
 
 namespace gnnea {
@@ -267,6 +268,54 @@ struct X3Loader : Loader<K_CONTIG, ROWS, VEC, NT> {
   }
 };
 
+// Tile loader for a [K][rows] (rows-contiguous) fp32 source that stages K-contiguous bf16
+// planes: a thread takes one row and 4 consecutive k (four scalar loads, each one coalesced
+// across the wave's 64 consecutive rows), splits them and writes one 8-B store per plane —
+// the element-wise transposed store of X3Loader<false> hit 8-16-way LDS bank conflicts.
+template <int ROWS, int NT>
+struct X3LoaderT {
+  static constexpr int NTOT = ROWS * GBK / 4;
+  static constexpr int NV = (NTOT + NT - 1) / NT;
+  static constexpr int PLANE = ROWS * XLD;
+  float4 r[NV];
+  __device__ void load(const float* __restrict__ X, int64_t ld, int row0, int nrows, int k0,
+                       int kend, int tid) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int idx = tid + NT * q;
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      if (NTOT % NT == 0 || idx < NTOT) {
+        const int row = idx % ROWS, k = (idx / ROWS) * 4;
+        const int gr = row0 + row, gk = k0 + k;
+        if (gr < nrows) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (gk + e < kend) t[e] = X[(int64_t)(gk + e) * ld + gr];
+        }
+      }
+      r[q] = make_float4(t[0], t[1], t[2], t[3]);
+    }
+  }
+  __device__ void store3(bf16_t* __restrict__ S, int tid) const {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int idx = tid + NT * q;
+      if (NTOT % NT != 0 && idx >= NTOT) continue;
+      const int row = idx % ROWS, k = (idx / ROWS) * 4;
+      const float v[4] = {r[q].x, r[q].y, r[q].z, r[q].w};
+      bf16_t h[4], m[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split3(v[e], h[e], m[e], l[e]);
+      bf16_t* p = S + row * XLD + k;
+      *(uint2*)p = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+      *(uint2*)(p + PLANE) =
+          make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
+      *(uint2*)(p + 2 * PLANE) =
+          make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+    }
+  }
+};
+
 // B (the small weight operand) arrives pre-split: three bf16 planes [3][n][ldp] K-contiguous,
 // zero-padded to ldp = roundup16(K) columns (k_split3_planes, once per call), so the kernel splits
 // only A and every B fragment load is a 16-B copy.
@@ -324,10 +373,14 @@ struct PLoader {  // ROWS x GBK of each of the three planes, 16-B chunks of 8 k
 
 constexpr int XBM = 128, XNT = 512;  // 8 waves in 4 x 2, each 32 x 32*WT
 
-template <int WT, bool VEC>
+// TA: the weight-gradient form dW = Aᵀ·B with A stored [K][M] and B stored [K][N] (both tall,
+// M-/N-contiguous): both operands are split on the fly (X3LoaderT), no pre-split planes;
+// split-K fills the chip (the output is only M x N).
+template <int WT, bool VEC, bool TA = false>
 __global__ __launch_bounds__(XNT) void k_gemm_x3(int M, int N, int K, const float* __restrict__ A,
                                                  int64_t lda, const bf16_t* __restrict__ Bp,
                                                  int64_t ldp, int64_t pstride,
+                                                 const float* __restrict__ Braw, int64_t ldb,
                                                  const float* __restrict__ bias, float beta,
                                                  float* __restrict__ C, int64_t ldc, int64_t cs,
                                                  int k_per_split, float* __restrict__ slab,
@@ -354,24 +407,20 @@ __global__ __launch_bounds__(XNT) void k_gemm_x3(int M, int N, int K, const floa
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
-  X3Loader<true, XBM, VEC, XNT> la;
-  PLoader<BN, XNT> lb;
+  typename std::conditional<TA, X3LoaderT<XBM, XNT>, X3Loader<true, XBM, VEC, XNT>>::type la;
+  typename std::conditional<TA, X3LoaderT<BN, XNT>, PLoader<BN, XNT>>::type lb;
+  auto load_b = [&](int k0) {
+    if constexpr (TA) lb.load(Braw, ldb, n0, N, k0, ke, tid);
+    else lb.load(Bp, ldp, pstride, n0, N, k0, tid);
+  };
+  auto store_b = [&](bf16_t* S) {
+    if constexpr (TA) lb.store3(S, tid);
+    else lb.store(S, tid);
+  };
   const int nsteps = ke > kb ? (ke - kb + GBK - 1) / GBK : 0;
-  if (nsteps > 0) {
-    la.load(A, lda, m0, M, kb, ke, tid);
-    lb.load(Bp, ldp, pstride, n0, N, kb, tid);
-    la.store3(As(0), tid);
-    lb.store(Bs(0), tid);
-    __syncthreads();
-  }
   constexpr int PA = XBM * XLD, PB = BN * XLD;
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    const bool more = s + 1 < nsteps;
-    if (more) {  // in flight under the MFMAs below
-      la.load(A, lda, m0, M, kb + (s + 1) * GBK, ke, tid);
-      lb.load(Bp, ldp, pstride, n0, N, kb + (s + 1) * GBK, tid);
-    }
+  // the six products of one 16-deep k-step from LDS buffer cur
+  auto compute = [&](int cur) {
     const bf16_t* a_s = As(cur) + (wm * 32 + li) * XLD + 8 * kh;
     const bf16x8_t ah = *(const bf16x8_t*)a_s;
     const bf16x8_t am = *(const bf16x8_t*)(a_s + PA);
@@ -397,9 +446,26 @@ __global__ __launch_bounds__(XNT) void k_gemm_x3(int M, int N, int K, const floa
     for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm_[t], acc[t], 0, 0, 0);
 #pragma unroll
     for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t], acc[t], 0, 0, 0);
+  };
+  // (a second register stage for the TA form, loads two k-steps ahead, spilled at WT = 5)
+  if (nsteps > 0) {
+    la.load(A, lda, m0, M, kb, ke, tid);
+    load_b(kb);
+    la.store3(As(0), tid);
+    store_b(Bs(0));
+    __syncthreads();
+  }
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (more) {  // in flight under the MFMAs below
+      la.load(A, lda, m0, M, kb + (s + 1) * GBK, ke, tid);
+      load_b(kb + (s + 1) * GBK);
+    }
+    compute(cur);
     if (more) {
       la.store3(As(cur ^ 1), tid);
-      lb.store(Bs(cur ^ 1), tid);
+      store_b(Bs(cur ^ 1));
     }
     __syncthreads();
   }
@@ -581,9 +647,16 @@ static int64_t x3_planes_bytes(int64_t N, int64_t K) {
   return (3 * N * ldp * 2 + 255) & ~(int64_t)255;
 }
 
+static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                      const float* B, int64_t ldb, const float* bias, float beta, float* C,
+                      int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, hipStream_t s);
+
 static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
                    int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
                    float* C, int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, void* stream) {
+  if (trans_a && !trans_b && K > 0)
+    return gemm_x3_ta(M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, ws, ws_bytes,
+                      (hipStream_t)stream);
   if (trans_a || K == 0)
     return gemm_f32(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, ws,
                     ws_bytes, stream);
@@ -624,12 +697,12 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
   case W:                                                                                        \
     if (vec)                                                                                     \
       hipLaunchKernelGGL((k_gemm_x3<W, true>), grid, dim3(XNT), 0, s, (int)M, (int)N, (int)K, A, \
-                         lda, planes, (int64_t)ldp, pstride, bias, beta, C, ldc, cs, kps, slab,  \
-                         tiles_n);                                                               \
+                         lda, planes, (int64_t)ldp, pstride, nullptr, (int64_t)0, bias, beta, C, \
+                         ldc, cs, kps, slab, tiles_n);                                           \
     else                                                                                         \
       hipLaunchKernelGGL((k_gemm_x3<W, false>), grid, dim3(XNT), 0, s, (int)M, (int)N, (int)K,   \
-                         A, lda, planes, (int64_t)ldp, pstride, bias, beta, C, ldc, cs, kps,     \
-                         slab, tiles_n);                                                         \
+                         A, lda, planes, (int64_t)ldp, pstride, nullptr, (int64_t)0, bias, beta, \
+                         C, ldc, cs, kps, slab, tiles_n);                                        \
     break;
   switch (wt) {
     GNNEA_X3(1)
@@ -649,6 +722,70 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
     GNNEA_LAUNCH_CHECK();
   }
   return 0;
+}
+
+// dW = Aᵀ·B on the split-on-the-fly kernel: only split-K slabs in the workspace
+static int64_t x3_ta_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
+  // one 129-KB workgroup per CU: whole waves of 256 (2 per CU), each split >= 8 k-steps
+  const int64_t bn = 64 * pick_wt(N);
+  const int64_t tiles = ((M + XBM - 1) / XBM) * ((N + bn - 1) / bn);
+  if (tiles >= 256 || K < 16 * GBK) return 1;
+  int64_t s = 512 / tiles;
+  const int64_t by_k = K / (8 * GBK);
+  if (s > by_k) s = by_k;
+  while (s > 1 && s * M * N * 4 > ws_bytes) --s;
+  return s < 1 ? 1 : s;
+}
+
+static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                      const float* B, int64_t ldb, const float* bias, float beta, float* C,
+                      int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, hipStream_t s) {
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  if (M == 0 || N == 0) return 0;
+  if (M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return GNNEA_EINVAL;
+  if (!C || !A || !B) return GNNEA_EINVAL;
+  if (cs == 64 ? ldc < N : (ldc < (N < 64 ? N : 64) || cs < M * ldc)) return GNNEA_EINVAL;
+  if (lda < M || ldb < N) return GNNEA_EINVAL;
+  int wt = pick_wt(N);
+  const int64_t bn = 64 * wt;
+  const int tiles_n = (int)((N + bn - 1) / bn);
+  const int tiles = (int)(((M + XBM - 1) / XBM) * tiles_n);
+  const int splits = (int)x3_ta_splits(M, N, K, ws ? ws_bytes : 0);
+  if (splits > 1 && (!ws || ws_bytes < (int64_t)splits * M * N * 4)) return GNNEA_EWORKSPACE;
+  const int kps = (int)(((K + splits - 1) / splits + GBK - 1) / GBK * GBK);
+  float* slab = splits > 1 ? (float*)ws : nullptr;
+  // float4 loads run along M (A) and N (B): both must be 4-aligned
+  const dim3 grid(tiles, splits);
+  // (scalar loads coalesced across rows: no alignment requirement, VEC unused)
+#define GNNEA_X3T(W)                                                                             \
+  case W:                                                                                        \
+    hipLaunchKernelGGL((k_gemm_x3<W, true, true>), grid, dim3(XNT), 0, s, (int)M, (int)N,        \
+                       (int)K, A, lda, nullptr, (int64_t)0, (int64_t)0, B, ldb, bias, beta, C,   \
+                       ldc, cs, kps, slab, tiles_n);                                             \
+    break;
+  switch (wt) {
+    GNNEA_X3T(1)
+    GNNEA_X3T(2)
+    GNNEA_X3T(3)
+    GNNEA_X3T(4)
+    default:
+    GNNEA_X3T(5)
+  }
+#undef GNNEA_X3T
+  GNNEA_LAUNCH_CHECK();
+  if (splits > 1) {
+    const int64_t n = M * N;
+    const int nb = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+    hipLaunchKernelGGL(k_gemm_reduce, dim3(nb), dim3(256), 0, s, (int)M, (int)N, splits, slab,
+                       bias, beta, C, ldc, cs);
+    GNNEA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+extern "C" int64_t gnnea_gemm_x3t_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  return x3_ta_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
 }
 
 extern "C" int64_t gnnea_gemm_x3_ws_bytes(int64_t M, int64_t N, int64_t K) {

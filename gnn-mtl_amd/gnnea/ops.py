@@ -107,11 +107,18 @@ X3_MIN_MNK = 1 << 26
 X3_MIN_M = 4096  # tall A only (DBP15K scale, 30k rows: x3 55 us vs f32 MFMA 75 us, measured)
 
 
-def _use_x3(M, N, K, x3, trans_a=False):
-    """x3 splits op(B) into bf16 planes once per call: only for a small B (the weight) times a
-    tall, K-contiguous A.  The weight gradients (trans_a: both operands tall) and the bias
-    column sums (B = the tall gradient) stay on the f32 MFMA."""
-    if trans_a or N * K > _SMALL_OPERAND:
+def _use_x3(M, N, K, x3, trans_a=False, trans_b=False):
+    """x3 splits op(B) into bf16 planes once per call: for a small B (the weight) times a tall,
+    K-contiguous A.  The weight gradients dW = Aᵀ·B (trans_a, both operands tall, a small M x N
+    output) split both operands on the fly instead (gnnea_gemm_x3_f32's trans_a form, B
+    untransposed).  The bias column sums (B = the tall gradient) stay on the f32 MFMA."""
+    if trans_a:
+        if trans_b or M * N > _SMALL_OPERAND:
+            return False
+        if x3 is not None:
+            return bool(x3)
+        return GEMM_X3 and K >= X3_MIN_M and M * N * K >= X3_MIN_MNK
+    if N * K > _SMALL_OPERAND:
         return False
     if x3 is not None:
         return bool(x3)
@@ -164,9 +171,10 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
     if bias is not None:
         bias = _featc(bias, torch.float32)
     L = _lib.lib()
-    x3 = not bf and _use_x3(M, N, K, x3, trans_a)
+    x3 = not bf and _use_x3(M, N, K, x3, trans_a, trans_b)
     ws_fn = L.gnnea_gemm_bf16_ws_bytes if bf else (
-        L.gnnea_gemm_x3_ws_bytes if x3 else L.gnnea_gemm_ws_bytes)
+        (L.gnnea_gemm_x3t_ws_bytes if trans_a else L.gnnea_gemm_x3_ws_bytes) if x3
+        else L.gnnea_gemm_ws_bytes)
     ws_bytes = _ws_query(ws_fn, M, N, K)
     ws = _gemm_ws(a.device, ws_bytes) if ws_bytes > 0 else None
     with _lib.on_device(a.device):

@@ -264,8 +264,11 @@ int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
  * in fp32 (error at fp32 rounding level: the dropped terms are below 2^-24 relative); 6/16 of
  * the f32 MFMA time.  Arguments and layouts as gnnea_gemm_f32 / _sliced_f32; workspace from
  * gnnea_gemm_x3_ws_bytes (op(B) split once into three bf16 planes + split-K slabs; required).
- * A transposed A (trans_a = 1) runs on the f32 MFMA kernel. */
+ * trans_a = 1 with trans_b = 0 is the weight-gradient form dW = Aᵀ·B (A [K][M], B [K][N], both
+ * tall): both operands are split on the fly, split-K over the long K, workspace from
+ * gnnea_gemm_x3t_ws_bytes (slabs only).  trans_a = trans_b = 1 runs on the f32 MFMA kernel. */
 int64_t gnnea_gemm_x3_ws_bytes(int64_t M, int64_t N, int64_t K);
+int64_t gnnea_gemm_x3t_ws_bytes(int64_t M, int64_t N, int64_t K);
 int gnnea_gemm_x3_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
                       int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
                       float* C, int64_t ldc, void* ws, int64_t ws_bytes, void* stream);
