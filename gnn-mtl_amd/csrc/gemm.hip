@@ -269,10 +269,11 @@ struct X3Loader : Loader<K_CONTIG, ROWS, VEC, NT> {
 };
 
 // Tile loader for a [K][rows] (rows-contiguous) fp32 source that stages K-contiguous bf16
-// planes: a thread takes one row and 4 consecutive k (four scalar loads, each one coalesced
-// across the wave's 64 consecutive rows), splits them and writes one 8-B store per plane —
-// the element-wise transposed store of X3Loader<false> hit 8-16-way LDS bank conflicts.
-template <int ROWS, int NT>
+// planes: a thread loads 4 consecutive rows at one k (one float4) and writes them element-wise,
+// with k fastest across the lanes: each 2-B store instruction covers 16 consecutive k of four
+// 4-row groups (48-dword offsets: conflict-free).  Row-group-fastest lanes (X3Loader<false>)
+// hit the same few banks, 8-16-way conflicted.
+template <int ROWS, int NT, bool VEC>
 struct X3LoaderT {
   static constexpr int NTOT = ROWS * GBK / 4;
   static constexpr int NV = (NTOT + NT - 1) / NT;
@@ -283,17 +284,23 @@ struct X3LoaderT {
 #pragma unroll
     for (int q = 0; q < NV; ++q) {
       const int idx = tid + NT * q;
-      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (NTOT % NT == 0 || idx < NTOT) {
-        const int row = idx % ROWS, k = (idx / ROWS) * 4;
+        const int k = idx % GBK, row = (idx / GBK) * 4;
         const int gr = row0 + row, gk = k0 + k;
-        if (gr < nrows) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (gk + e < kend) t[e] = X[(int64_t)(gk + e) * ld + gr];
+        if (gk < kend) {
+          const float* p = X + (int64_t)gk * ld + gr;
+          if (VEC) {
+            if (gr < nrows) v = *(const float4*)p;
+          } else {
+            v.x = gr < nrows ? p[0] : 0.f;
+            v.y = gr + 1 < nrows ? p[1] : 0.f;
+            v.z = gr + 2 < nrows ? p[2] : 0.f;
+            v.w = gr + 3 < nrows ? p[3] : 0.f;
+          }
         }
       }
-      r[q] = make_float4(t[0], t[1], t[2], t[3]);
+      r[q] = v;
     }
   }
   __device__ void store3(bf16_t* __restrict__ S, int tid) const {
@@ -301,17 +308,17 @@ struct X3LoaderT {
     for (int q = 0; q < NV; ++q) {
       const int idx = tid + NT * q;
       if (NTOT % NT != 0 && idx >= NTOT) continue;
-      const int row = idx % ROWS, k = (idx / ROWS) * 4;
+      const int k = idx % GBK, row = (idx / GBK) * 4;
       const float v[4] = {r[q].x, r[q].y, r[q].z, r[q].w};
-      bf16_t h[4], m[4], l[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) split3(v[e], h[e], m[e], l[e]);
-      bf16_t* p = S + row * XLD + k;
-      *(uint2*)p = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
-      *(uint2*)(p + PLANE) =
-          make_uint2(m[0] | ((uint32_t)m[1] << 16), m[2] | ((uint32_t)m[3] << 16));
-      *(uint2*)(p + 2 * PLANE) =
-          make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+      for (int e = 0; e < 4; ++e) {
+        bf16_t h, m, l;
+        split3(v[e], h, m, l);
+        bf16_t* p = S + (row + e) * XLD + k;
+        p[0] = h;
+        p[PLANE] = m;
+        p[2 * PLANE] = l;
+      }
     }
   }
 };
@@ -407,8 +414,8 @@ __global__ __launch_bounds__(XNT) void k_gemm_x3(int M, int N, int K, const floa
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
-  typename std::conditional<TA, X3LoaderT<XBM, XNT>, X3Loader<true, XBM, VEC, XNT>>::type la;
-  typename std::conditional<TA, X3LoaderT<BN, XNT>, PLoader<BN, XNT>>::type lb;
+  typename std::conditional<TA, X3LoaderT<XBM, XNT, VEC>, X3Loader<true, XBM, VEC, XNT>>::type la;
+  typename std::conditional<TA, X3LoaderT<BN, XNT, VEC>, PLoader<BN, XNT>>::type lb;
   auto load_b = [&](int k0) {
     if constexpr (TA) lb.load(Braw, ldb, n0, N, k0, ke, tid);
     else lb.load(Bp, ldp, pstride, n0, N, k0, tid);
@@ -755,13 +762,19 @@ static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t l
   const int kps = (int)(((K + splits - 1) / splits + GBK - 1) / GBK * GBK);
   float* slab = splits > 1 ? (float*)ws : nullptr;
   // float4 loads run along M (A) and N (B): both must be 4-aligned
+  // float4 loads run along M (A) and N (B): both must be 4-aligned
+  const bool vec = lda % 4 == 0 && M % 4 == 0 && al16(A) && ldb % 4 == 0 && N % 4 == 0 && al16(B);
   const dim3 grid(tiles, splits);
-  // (scalar loads coalesced across rows: no alignment requirement, VEC unused)
 #define GNNEA_X3T(W)                                                                             \
   case W:                                                                                        \
-    hipLaunchKernelGGL((k_gemm_x3<W, true, true>), grid, dim3(XNT), 0, s, (int)M, (int)N,        \
-                       (int)K, A, lda, nullptr, (int64_t)0, (int64_t)0, B, ldb, bias, beta, C,   \
-                       ldc, cs, kps, slab, tiles_n);                                             \
+    if (vec)                                                                                     \
+      hipLaunchKernelGGL((k_gemm_x3<W, true, true>), grid, dim3(XNT), 0, s, (int)M, (int)N,      \
+                         (int)K, A, lda, nullptr, (int64_t)0, (int64_t)0, B, ldb, bias, beta, C, \
+                         ldc, cs, kps, slab, tiles_n);                                           \
+    else                                                                                         \
+      hipLaunchKernelGGL((k_gemm_x3<W, false, true>), grid, dim3(XNT), 0, s, (int)M, (int)N,     \
+                         (int)K, A, lda, nullptr, (int64_t)0, (int64_t)0, B, ldb, bias, beta, C, \
+                         ldc, cs, kps, slab, tiles_n);                                           \
     break;
   switch (wt) {
     GNNEA_X3T(1)

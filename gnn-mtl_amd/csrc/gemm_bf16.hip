@@ -9,7 +9,8 @@
 // as [row][k] with K contiguous (row stride 40 elements = 80 B: 16-B aligned fragments, rows
 // spread over the banks), so every fragment is ONE ds_read_b128.  An operand whose rows are
 // contiguous in memory (op(X) = X^T) is transposed while it is written to LDS (8 2-B stores per
-// 16-B chunk).  Next tile's global loads are in flight under the current tile's MFMAs.
+// 16-B chunk, k fastest across the lanes so each store instruction covers 32 consecutive k of
+// two 8-row groups: conflict-free; row-group-fastest lanes hit 2 banks, 32-way).  Next tile's global loads are in flight under the current tile's MFMAs.
 // Split-K for the weight gradients as in gemm.hip: fp32 slabs, fixed-order reduction.
 #include "common.h"
 
@@ -40,7 +41,7 @@ struct HLoader {
       const int idx = tid + 256 * q;
       int row, k;
       if (K_CONTIG) { row = idx / (HBK / 8); k = (idx % (HBK / 8)) * 8; }
-      else { k = idx / (ROWS / 8); row = (idx % (ROWS / 8)) * 8; }
+      else { k = idx % HBK; row = (idx / HBK) * 8; }
       const int gr = row0 + row, gk = k0 + k;
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (VEC) {
@@ -82,7 +83,7 @@ struct HLoader {
         const int row = idx / (HBK / 8), k = (idx % (HBK / 8)) * 8;
         *(uint4*)(S + row * HLD + k) = r[q];
       } else {
-        const int k = idx / (ROWS / 8), row = (idx % (ROWS / 8)) * 8;
+        const int k = idx % HBK, row = (idx / HBK) * 8;
 #pragma unroll
         for (int e = 0; e < 8; ++e) S[(row + e) * HLD + k] = u4_elem(r[q], e);
       }
