@@ -288,6 +288,41 @@ __global__ void k_highway_bwd(const T* __restrict__ dY, const T* __restrict__ S,
   }
 }
 
+// Row-wise vector form (D, every ld and cs_ds % 4 == 0, 16-B / 8-B aligned bases): one wave per
+// row, lane = 4-column chunk, no per-element 64-bit index division; 4 consecutive columns stay
+// inside one 64-column slice of a slice-major dS_pre.
+template <int ACT, typename T>
+__global__ __launch_bounds__(256) void k_highway_bwd_v4(
+    const T* __restrict__ dY, const T* __restrict__ S, const T* __restrict__ Gt,
+    const T* __restrict__ R, int64_t ld, int64_t n_rows, int D, T* __restrict__ dS_pre,
+    int64_t ld_ds, int64_t cs_ds, T* __restrict__ dgate, int64_t ld_dg, T* __restrict__ dresid,
+    int64_t ld_dr) {
+  typedef typename Vec4<T>::raw V;
+  const int lane = lane_id();
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave_id(); r < n_rows; r += nw) {
+    for (int c = 4 * lane; c < D; c += 256) {
+      const int64_t i = r * ld + c;
+      const float4 dy = Vec4<T>::get(*(const V*)(dY + i)), sv = Vec4<T>::get(*(const V*)(S + i));
+      const float4 g = Vec4<T>::get(*(const V*)(Gt + i)), x = Vec4<T>::get(*(const V*)(R + i));
+      const float dyv[4] = {dy.x, dy.y, dy.z, dy.w}, s4[4] = {sv.x, sv.y, sv.z, sv.w};
+      const float g4[4] = {g.x, g.y, g.z, g.w}, x4[4] = {x.x, x.y, x.z, x.w};
+      float ds[4], dg[4], dr[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ds[e] = dyv[e] * g4[e] * act_grad_from_out<ACT>(s4[e]);
+        dg[e] = dyv[e] * (s4[e] - x4[e]) * g4[e] * (1.f - g4[e]);
+        dr[e] = dyv[e] * (1.f - g4[e]);
+      }
+      *(V*)(dS_pre + (c >> 6) * cs_ds + r * ld_ds + (c & 63)) =
+          Vec4<T>::put(make_float4(ds[0], ds[1], ds[2], ds[3]));
+      *(V*)(dgate + r * ld_dg + c) = Vec4<T>::put(make_float4(dg[0], dg[1], dg[2], dg[3]));
+      if (dresid)
+        *(V*)(dresid + r * ld_dr + c) = Vec4<T>::put(make_float4(dr[0], dr[1], dr[2], dr[3]));
+    }
+  }
+}
+
 template <typename T>
 static int act_bwd_t(const T* dY, const T* Y, T* G, int64_t n, int act, hipStream_t s) {
   if (n < 0) return GNNEA_EINVAL;
@@ -320,9 +355,19 @@ static int highway_bwd_t(const T* dY, const T* S, const T* G, const T* resid, in
   if (!dY || !S || !G || !resid || !dS_pre || !dgate) return GNNEA_EINVAL;
   const int64_t n = n_rows * (int64_t)D;
   const int nb = (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192);
-#define GNNEA_HWB(A)                                                                         \
-  hipLaunchKernelGGL((k_highway_bwd<A, T>), dim3(nb), dim3(256), 0, s, dY, S, G, resid, ld,  \
-                     n_rows, D, dS_pre, ld_ds, cs_ds, dgate, ld_dg, dresid, ld_dr)
+  constexpr uintptr_t al = sizeof(typename Vec4<T>::raw) - 1;
+  const bool v4 = D % 4 == 0 && ld % 4 == 0 && ld_ds % 4 == 0 && cs_ds % 4 == 0 &&
+                  ld_dg % 4 == 0 && (!dresid || ld_dr % 4 == 0) &&
+                  !(((uintptr_t)dY | (uintptr_t)S | (uintptr_t)G | (uintptr_t)resid |
+                     (uintptr_t)dS_pre | (uintptr_t)dgate | (uintptr_t)dresid) & al);
+  const int nbv = (int)((n_rows + 3) / 4 < 16384 ? (n_rows + 3) / 4 : 16384);
+#define GNNEA_HWB(A)                                                                          \
+  if (v4)                                                                                     \
+    hipLaunchKernelGGL((k_highway_bwd_v4<A, T>), dim3(nbv), dim3(256), 0, s, dY, S, G, resid, \
+                       ld, n_rows, D, dS_pre, ld_ds, cs_ds, dgate, ld_dg, dresid, ld_dr);     \
+  else                                                                                        \
+    hipLaunchKernelGGL((k_highway_bwd<A, T>), dim3(nb), dim3(256), 0, s, dY, S, G, resid, ld, \
+                       n_rows, D, dS_pre, ld_ds, cs_ds, dgate, ld_dg, dresid, ld_dr)
   switch (act) {
     case GNNEA_ACT_IDENTITY: GNNEA_HWB(GNNEA_ACT_IDENTITY); break;
     case GNNEA_ACT_RELU: GNNEA_HWB(GNNEA_ACT_RELU); break;
