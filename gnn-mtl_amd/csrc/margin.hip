@@ -285,7 +285,13 @@ __global__ __launch_bounds__(256) void k_margin_bwd(const float* __restrict__ ou
 // chunk) instead of gathering the other row: no feature-row traffic at all.  Entries are added
 // in incidence order with the same integer multipliers as k_margin_bwd, so the gradient is
 // bit-identical to it.
-template <int NC>
+typedef short short2v __attribute__((ext_vector_type(2)));
+
+// PK (|multiplier| <= 2k <= 510, so 64 entries sum below 2^15): each code byte is looked up in a
+// 256-entry LDS table of its four signs as two packed int16 pairs and accumulated with packed
+// 16-bit multiply-adds (2 instructions per 4 columns instead of 8), flushed into the int32
+// accumulators after every 64-entry batch.  Exact like the int32 path.
+template <int NC, bool PK = false>
 __global__ __launch_bounds__(256) void k_margin_bwd_code(int D, int64_t M,
                                                          const float* __restrict__ m,
                                                          const uint8_t* __restrict__ codes,
@@ -297,6 +303,13 @@ __global__ __launch_bounds__(256) void k_margin_bwd_code(int D, int64_t M,
                                                          float inv, float* __restrict__ grad,
                                                          int64_t ldg,
                                                          float* __restrict__ scratch) {
+  __shared__ uint2 lut[PK ? 256 : 1];
+  if constexpr (PK) {
+    const uint32_t b = threadIdx.x;  // 256 threads: one table entry each
+    auto sx = [&](int e) { return (uint32_t)(uint16_t)(int16_t)(((int)(b << (30 - 2 * e))) >> 30); };
+    lut[b] = make_uint2(sx(0) | (sx(1) << 16), sx(2) | (sx(3) << 16));
+    __syncthreads();
+  }
   const int it = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
   if (it >= n_items) return;
   const int4 item = items[it];
@@ -322,6 +335,9 @@ __global__ __launch_bounds__(256) void k_margin_bwd_code(int D, int64_t M,
       f = role_b ? -mj : mj;
     }
     unsigned long long act = __ballot(f != 0);
+    short2v pacc[NC][2];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) pacc[c][0] = pacc[c][1] = (short2v){0, 0};
     while (act) {
       // up to U active entries per round, branch-free (an exhausted slot re-reads lane 0's
       // valid term with multiplier 0) so all U code loads are in flight together
@@ -343,13 +359,30 @@ __global__ __launch_bounds__(256) void k_margin_bwd_code(int D, int64_t M,
 #pragma unroll
       for (int u = 0; u < U; ++u) {
 #pragma unroll
-        for (int c = 0; c < NC; ++c)
+        for (int c = 0; c < NC; ++c) {
+          if constexpr (PK) {
+            const uint2 w = lut[cb[u][c]];
+            const short2v fv = {(short)fq[u], (short)fq[u]};
+            pacc[c][0] += __builtin_bit_cast(short2v, w.x) * fv;
+            pacc[c][1] += __builtin_bit_cast(short2v, w.y) * fv;
+          } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            // v_bfe_i32 of the 2-bit field, then v_mad_i32_i24
-            const int sg = ((int)(cb[u][c] << (30 - 2 * e))) >> 30;
-            acc[c][e] = __mul24(sg, fq[u]) + acc[c][e];
+            for (int e = 0; e < 4; ++e) {
+              // v_bfe_i32 of the 2-bit field, then v_mad_i32_i24
+              const int sg = ((int)(cb[u][c] << (30 - 2 * e))) >> 30;
+              acc[c][e] = __mul24(sg, fq[u]) + acc[c][e];
+            }
           }
+        }
+      }
+    }
+    if constexpr (PK) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        acc[c][0] += pacc[c][0].x;
+        acc[c][1] += pacc[c][0].y;
+        acc[c][2] += pacc[c][1].x;
+        acc[c][3] += pacc[c][1].y;
       }
     }
   }
@@ -529,11 +562,18 @@ extern "C" int gnnea_margin_bwd_code_f32(int32_t D, int32_t t, int32_t k, const 
   if (n_long > 0 && (!long_rows || !long_ptr || !scratch)) return GNNEA_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const int64_t M = 2ll * t * k + t;
-#define GNNEA_BC(N)                                                                            \
-  case N:                                                                                      \
-    hipLaunchKernelGGL((k_margin_bwd_code<N>), dim3(div_up(n_items, 4)), dim3(256), 0, s, D, M, \
-                       m, (const uint8_t*)codes, sb, inc_ent, (const int4*)items, n_items,     \
-                       grad_loss, scale, grad, ldg, scratch);                                  \
+  // packed 16-bit accumulation needs 64 * max|m_j| = 64 * 2k < 2^15
+  const bool pk = k <= 255;
+#define GNNEA_BC(N)                                                                             \
+  case N:                                                                                       \
+    if (pk)                                                                                     \
+      hipLaunchKernelGGL((k_margin_bwd_code<N, true>), dim3(div_up(n_items, 4)), dim3(256), 0,  \
+                         s, D, M, m, (const uint8_t*)codes, sb, inc_ent, (const int4*)items,    \
+                         n_items, grad_loss, scale, grad, ldg, scratch);                        \
+    else                                                                                        \
+      hipLaunchKernelGGL((k_margin_bwd_code<N, false>), dim3(div_up(n_items, 4)), dim3(256), 0, \
+                         s, D, M, m, (const uint8_t*)codes, sb, inc_ent, (const int4*)items,    \
+                         n_items, grad_loss, scale, grad, ldg, scratch);                        \
     break;
   switch (div_up(D, 256)) {
     GNNEA_BC(1)

@@ -193,7 +193,7 @@ def test_margin_backward_deterministic(device):
 
 
 @pytest.mark.parametrize("N,D,t,k", [(3000, 300, 200, 40), (500, 1024, 30, 9), (60, 8, 50, 6),
-                                     (40, 64, 300, 30)])
+                                     (40, 64, 300, 30), (80, 300, 4, 300)])  # k > 255: int32 path
 def test_margin_sign_codes_match_row_gather(device, N, D, t, k):
     """The sign-code backward (the forward stores 2 bits per column, the backward reads them)
     gives the row-gather backward's gradient bit for bit: hub rows (chunked items), tied columns
