@@ -687,9 +687,8 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
                        (int)N, (int)K, ldp, planes, pstride);
     GNNEA_LAUNCH_CHECK();
   }
-  // wider than one 320-column tile: 128-column tiles (WT = 2) keep the LDS at 74 KB, two
-  // workgroups per CU, and measured faster than 2 x 320 (2M x 600 x 300: 5.76 vs 6.05 ms;
-  // 30k rows: 0.109 vs 0.118 ms)
+  // wider than one 320-column tile: 128-column tiles (WT = 2, the finer work split) measured
+  // faster than 2 x 320 (2M x 600 x 300: 5.76 vs 6.05 ms; 30k rows: 0.109 vs 0.118 ms)
   int wt = N > 320 ? 2 : pick_wt(N);
   if (const char* e = getenv("GNNEA_X3_WT")) {  // tuning override only
     const int v = atoi(e);
