@@ -372,8 +372,145 @@ def gen_ingest():
     print("ingest fixtures written to", HERE)
 
 
+def _scale_inputs():
+    """tests/scale_inputs.py (needs the product package's synthetic generator on the path)."""
+    sys.path.insert(0, os.path.join(REPO, "gnn-mtl_amd"))
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import scale_inputs
+    sys.path.pop(0)
+    sys.path.pop(0)
+    for k in [m for m in sys.modules if m == "gnnea" or m.startswith("gnnea.")]:
+        del sys.modules[k]
+    return scale_inputs
+
+
+class _Args:
+    pass
+
+
+def _ea_args(model, N, data, neg_num):
+    a = _Args()
+    a.model, a.num_layers, a.dim, a.act, a.dropout, a.bias = model, 3, 300, "relu", 0.0, 1
+    a.n_heads, a.alpha, a.feat_dim, a.n_classes, a.cuda, a.device = 4, 0.2, 300, 300, -1, "cpu"
+    a.n_nodes, a.neg_num, a.data = N, neg_num, data
+    return a
+
+
+def gen_dbp15k():
+    """BASELINE configs[1] / configs[2] (DBP15K-scale pair, 2 x 15k entities): the reference's
+    layers (GCN, HighWay, 4-head GAT: outputs and input gradients on a row sample, full weight
+    gradients), GCN-EA / GAT-EA / HGCN-EA training steps (loss, parameter gradients, sampled
+    outputs) with seeded negatives.  Inputs are rebuilt from seeds by tests/scale_inputs.py."""
+    si = _scale_inputs()
+    _placeholders()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import layers.layers as RL
+    import layers.att_layers as RA
+    import models.models_ea as RM
+    import utils.data_utils as RDU
+    torch.set_num_threads(8)
+    tr, N, r, c, v = si.dbp15k_graph()
+    n = N // 2
+    adj = RDU.sparse_mx_to_torch_sparse_tensor(
+        RDU.get_sparse_tensor(N, [tuple(x) for x in tr.tolist()]))
+    idx = adj._indices().numpy()
+    # the vectorised builder the tests use must equal the reference's COO here as well
+    assert np.array_equal(idx[0], r) and np.array_equal(idx[1], c)
+    assert np.array_equal(adj._values().numpy(), v)
+    import hashlib
+    out = {"adj_sha256": np.array(hashlib.sha256(idx.astype(np.int64).tobytes() +
+                                                 adj._values().numpy().tobytes()).hexdigest()),
+           "nnz": np.int64(idx.shape[1])}
+    X = si.features(N)
+    R = torch.from_numpy(si.upstream(N))
+    rows = si.sample_rows(N, 512)
+    out["rows"] = rows
+    x = torch.from_numpy(X)
+
+    def run_layer(layer):
+        xx = x.clone().requires_grad_(True)
+        o = layer((xx, adj))[0]
+        (o * R[:, :o.shape[1]]).sum().backward()
+        return o.detach().numpy()[rows], xx.grad.numpy()[rows]
+
+    torch.manual_seed(10086)
+    gc = RL.GraphConvolution(300, 300, 0.0, F.relu, True)
+    o, dx = run_layer(gc)
+    out.update(gcn_out=o, gcn_dx=dx, gcn_dW=gc.linear.weight.grad.numpy(),
+               gcn_db=gc.linear.bias.grad.numpy())
+    torch.manual_seed(10087)
+    hw = RL.HighWayGraphConvolution(300, 300, 0.0, F.relu, True, -1, "cpu")
+    o, dx = run_layer(hw)
+    out.update(hw_out=o, hw_dx=dx, hw_dW=hw.linear.weight.grad.numpy(),
+               hw_db=hw.linear.bias.grad.numpy())
+    torch.manual_seed(10088)
+    ga = RA.GraphAttentionLayer(300, 75, 0.0, F.relu, 0.2, 4, True)
+    o, dx = run_layer(ga)
+    out.update(gat_out=o, gat_dx=dx,
+               gat_dW=np.stack([h.W.grad.numpy() for h in ga.attentions]),
+               gat_da=np.stack([h.a.grad.numpy() for h in ga.attentions]))
+
+    # one training step of run/train_ea.py:55-66 per model, negatives from seeds (k = 125)
+    train = si.ea_pairs(n)
+    t, k = train.shape[0], 125
+    out["train"] = train
+    xs = torch.from_numpy(X).to_sparse()
+    for model in ("GCN", "GAT", "HGCN"):
+        torch.manual_seed(10086)
+        m = RM.EAModel(_ea_args(model, N, {"train": train}, k))
+        m.train()
+        outputs = m.decode(m.encode(xs, adj), adj)
+        m.neg_right = si.negatives(N, t, k, 31)
+        m.neg2_left = si.negatives(N, t, k, 32)
+        loss = m.get_loss(outputs, {"train": train}, "train")
+        loss.backward()
+        out[model + "_loss"] = np.array(float(loss))
+        out[model + "_out"] = outputs.detach().numpy()[rows]
+        for name, p in m.named_parameters():
+            out["%s_grad.%s" % (model, name)] = p.grad.numpy().copy()
+        print(model, "EA step done, loss", float(loss), flush=True)
+    np.savez_compressed(os.path.join(HERE, "dbp15k.npz"), **out)
+    print("dbp15k fixtures written to", HERE)
+
+
+def gen_sinkhorn_scale():
+    """§8d Sinkhorn batches B = 3000 and 15000 (utils/ot_loss.py:5-76 as models_ea.py:217 calls
+    it, a = b = ones, reg 0.01; sinkhorn_iteration at B = 3000): plans on a row sample, their
+    marginals, losses / transports.  The costs come from tests/scale_inputs.sinkhorn_cost."""
+    si = _scale_inputs()
+    _placeholders()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import utils.ot_loss as ROT
+    import SinkhornOT.sinkhorn_loss as RSK
+    torch.set_num_threads(8)
+    out = {}
+    for B in (3000, 15000):
+        M = si.sinkhorn_cost(B)
+        rows = si.sample_rows(B, 32, seed=3)
+        P, loss = ROT.sinkhorn(torch.ones(B), torch.ones(B), M, reg=0.01)
+        out.update({"B%d_rows" % B: rows, "B%d_knopp_P" % B: P.numpy()[rows],
+                    "B%d_knopp_rowsum" % B: P.sum(1).numpy(),
+                    "B%d_knopp_colsum" % B: P.sum(0).numpy(),
+                    "B%d_knopp_loss" % B: loss.numpy()})
+        del P
+        if B == 3000:
+            C = M.double().view(1, B, B)
+            mu = torch.full((1, B, 1), 1.0 / B, dtype=torch.float64)
+            nu = torch.full((1, 1, B), 1.0 / B, dtype=torch.float64)
+            tr_, m1, m2, K = RSK.sinkhorn_iteration(C, mu, nu, 0.01)
+            out.update({"B%d_stab_transport" % B: tr_.numpy(), "B%d_stab_m1" % B: m1.numpy(),
+                        "B%d_stab_m2" % B: m2.numpy(), "B%d_stab_K" % B: K[0].numpy()[rows],
+                        "B%d_stab_Kcolsum" % B: K[0].sum(0).numpy()})
+        print("sinkhorn B =", B, "done", flush=True)
+    np.savez_compressed(os.path.join(HERE, "sinkhorn_scale.npz"), **out)
+    print("sinkhorn scale fixtures written to", HERE)
+
+
 if __name__ == "__main__":
-    sections = {"l1": gen_l1, "train": gen_train_trace, "gw": gen_gw, "ingest": gen_ingest}
+    sections = {"l1": gen_l1, "train": gen_train_trace, "gw": gen_gw, "ingest": gen_ingest,
+                "dbp15k": gen_dbp15k, "sinkhorn_scale": gen_sinkhorn_scale}
     if sys.argv[1:]:
         for name in sys.argv[1:]:
             sections[name]()
@@ -383,3 +520,5 @@ if __name__ == "__main__":
         gen_train_trace()
         gen_gw()
         gen_ingest()
+        gen_dbp15k()
+        gen_sinkhorn_scale()
