@@ -470,6 +470,31 @@ def gen_dbp15k():
         for name, p in m.named_parameters():
             out["%s_grad.%s" % (model, name)] = p.grad.numpy().copy()
         print(model, "EA step done, loss", float(loss), flush=True)
+        # the same step in fp64 (same init: built in fp32 under the seed, then widened; the
+        # HighWay gates are plain tensors, widened by hand; torch.ones in att_layers.py:45 follows
+        # the default dtype).  The margin loss's sign sums make fp32 parameter gradients
+        # rounding-sensitive, so the GPU test measures both fp32 runs against this one.
+        torch.manual_seed(10086)
+        m = RM.EAModel(_ea_args(model, N, {"train": train}, k))
+        m.double()
+        for mod in m.modules():
+            if hasattr(mod, "kernel_gate"):
+                mod.kernel_gate = mod.kernel_gate.double()
+                mod.bias_gate = mod.bias_gate.double()
+        m.train()
+        torch.set_default_dtype(torch.float64)
+        try:
+            outputs = m.decode(m.encode(xs.double(), adj.double()), adj.double())
+            m.neg_right = si.negatives(N, t, k, 31)
+            m.neg2_left = si.negatives(N, t, k, 32)
+            loss = m.get_loss(outputs, {"train": train}, "train")
+            loss.backward()
+        finally:
+            torch.set_default_dtype(torch.float32)
+        out[model + "_loss64"] = np.array(float(loss))
+        for name, p in m.named_parameters():
+            out["%s_grad64.%s" % (model, name)] = p.grad.numpy().copy()
+        print(model, "fp64 EA step done, loss", float(loss), flush=True)
     np.savez_compressed(os.path.join(HERE, "dbp15k.npz"), **out)
     print("dbp15k fixtures written to", HERE)
 

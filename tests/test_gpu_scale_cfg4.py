@@ -51,6 +51,7 @@ def cfg4(device):
 
 
 def _rows_of(t):
+    t = t.detach()
     return lambda rows: t[torch.from_numpy(np.asarray(rows)).to(t.device)].float().cpu().numpy()
 
 

@@ -4,9 +4,12 @@ The fixtures (tests/golden/dbp15k.npz, sinkhorn_scale.npz) were produced by runn
 itself on the DBP15K-scale synthetic pair (2 x 15k entities, 229,940 nnz) and on B = 3000 / 15000
 Sinkhorn costs (tests/golden/gen_golden.py: gen_dbp15k, gen_sinkhorn_scale); the inputs are
 rebuilt here bit-for-bit from their seeds (tests/scale_inputs.py), the outputs are stored on a
-512-row sample.  Tolerances as tests/test_gpu_parity.py: fp32 1e-4 norm-relative, parameter
-gradients of a whole EA step 3e-3 (margin sign sums cancel: the reference's own fp32 and fp64
-gradients differ by 5e-4 at cfg-1), fp64 Sinkhorn 1e-9.
+512-row sample.  Tolerances as tests/test_gpu_parity.py: fp32 1e-4 norm-relative, fp64
+Sinkhorn 1e-9; parameter gradients of a whole EA step against the reference's own fp64 step,
+max(3e-3, 2 x the reference fp32 step's largest error) (the margin loss's sign pattern is
+chaotic under fp32 rounding: at this size the reference's own fp32 and fp64 gradients differ by
+up to 2.2e-2), plus the last layer's gradient against the fp64 loss gradient at our own outputs
+(1e-4), which pins the backward without that chaos.
 """
 import numpy as np
 import pytest
@@ -86,6 +89,9 @@ def test_dbp15k_ea_step_vs_reference(golden, device, dbp, model):
     torch.manual_seed(10086)
     m = EAModel(a).to(device)
     m.train()
+    saved = {}
+    if model != "HGCN":  # MLP decoder (models/decoders.py:50-62): input of its last Linear
+        m.decoder.cls[2].register_forward_hook(lambda mod, i, o: saved.__setitem__("h", i[0]))
     xs = torch.from_numpy(dbp["X"]).to_sparse().to(device)  # sparse-COO features, as the ref
     outputs = m.decode(m.encode(xs, dbp["adj"]), dbp["adj"])
     m.neg_right = si.negatives(N, t, k, 31)
@@ -93,16 +99,39 @@ def test_dbp15k_ea_step_vs_reference(golden, device, dbp, model):
     loss = m.get_loss(outputs, {"train": train}, "train")
     loss.backward()
     assert abs(float(loss) - float(f[model + "_loss"])) <= 1e-5 * abs(float(f[model + "_loss"]))
+    assert abs(float(loss) - float(f[model + "_loss64"])) <= 1e-5 * abs(float(f[model + "_loss64"]))
     rows_t = torch.from_numpy(f["rows"]).to(device)
     assert rel_err(outputs.detach()[rows_t].cpu(), f[model + "_out"]) < TOL32
-    refs = {n: f["%s_grad.%s" % (model, n)] for n, _ in m.named_parameters()}
-    gmax = max(np.abs(r).max() for r in refs.values())
-    for name, p in m.named_parameters():
-        ref = refs[name]
-        if np.abs(ref).max() < 1e-3 * gmax:  # analytically zero (translation-invariant loss)
+    # Parameter gradients vs the reference's own fp64 step.  The margin loss's gradient is a sum
+    # of sign(x_a - x_b) terms and 1e5 of its 3.4e8 term differences lie within 1e-5 of the
+    # output scale, so which of them flip under fp32 rounding is chaotic: the reference's own
+    # fp32 step is up to 2.2e-2 (GCN-EA decoder.cls.2) / 1.1e-2 (GAT-EA encoder layer 1, head 3)
+    # away from its fp64 step, and which parameters land far depends on the rounding.  Each
+    # parameter must be within 3e-3 of fp64 or within twice the reference fp32 step's largest
+    # error, whichever is larger ...
+    params = [(n, p) for n, p in m.named_parameters()]
+    refs64 = [f["%s_grad64.%s" % (model, n)] for n, _ in params]
+    gmax = max(np.abs(r).max() for r in refs64)
+    zero = [np.abs(r).max() < 1e-3 * gmax for r in refs64]  # analytically 0 (last bias)
+    own = max(0.0 if z else rel_err(f["%s_grad.%s" % (model, n)], r)
+              for (n, _), r, z in zip(params, refs64, zero))
+    tol = max(3e-3, 2.0 * own)
+    for (name, p), ref64, z in zip(params, refs64, zero):
+        if z:
             assert np.abs(p.grad.cpu().numpy()).max() < 1e-3 * gmax, name
         else:
-            assert rel_err(p.grad.cpu(), ref) < 3e-3, name
+            assert rel_err(p.grad.cpu(), ref64) < tol, (name, rel_err(p.grad.cpu(), ref64), tol)
+    # ... and the backward itself is pinned without that chaos: the last layer's weight gradient
+    # equals the fp64 gradient of the reference's loss formula (models/models_ea.py:103-123)
+    # evaluated at OUR outputs, times our last-layer input, to 1e-4
+    if model != "HGCN":
+        import fp64_ref
+        o64 = outputs.detach().double().requires_grad_(True)
+        ix = [torch.from_numpy(np.asarray(z, dtype=np.int64)).to(device) for z in
+              (train[:, 0], train[:, 1], m.neg_left, m.neg_right, m.neg2_left, m.neg2_right)]
+        fp64_ref.margin_loss(o64, *ix, t, k).backward()
+        dW64 = o64.grad.t() @ saved["h"].detach().double()
+        assert rel_err(m.decoder.cls[2].linear.weight.grad.cpu(), dW64.cpu()) < TOL32
 
 
 @pytest.fixture(params=[0, 1], ids=["scaling", "logdomain"])
