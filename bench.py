@@ -3,9 +3,13 @@
 Workload (BASELINE.json configs[3] graph, the largest single-GPU configuration): the synthetic
 2 x 1M-entity / 2 x 10M-triple KG pair of SURVEY.md §8d (41,999,552 nnz incl. self loops),
 D = 300 fp32 features resident in HBM.  A step = one GCN aggregation pass Y = relu(A · H) over
-the whole graph (layers/layers.py:35-38).  On N > 1 GPUs each KG group of N/2 ranks splits the
-feature columns (default, no exchange in the aggregation) or the rows (--partition rows, with
-the RCCL halo all-gather inside the step), gnnea/dist.py.
+the whole graph (layers/layers.py:35-38).  On N > 1 GPUs the two KGs go to two groups of N/2
+ranks (N = 2: one KG per GPU, nothing to exchange); inside a group each rank owns a block of
+destination rows and the step includes the halo exchange a graph layer needs — the group's
+projected rows by direct peer transfers over xGMI (gnnea/exchange.py), overlapped with the
+aggregation over the owned rows (default --partition rows).  The exchange-free partitions
+(tiles / features: every rank aggregates a column slice from the whole KG, which a layer can
+only do after an all-gather of its input) are reported as a labelled side number.
 
 Side measurement (`train_step`): the row-sharded HGCN-EA training step of configs[3] through
 the drop-in Encoder/Decoder modules with the RCCL halo exchange (tools/dist_step.py).
@@ -15,8 +19,13 @@ the drop-in Encoder/Decoder modules with the RCCL halo exchange (tools/dist_step
 
 Prints ONE JSON line on rank 0.  `roofline` prices the SpMM kernel with the gather model
 4(N+1) + 8E + 4ED + 4ND bytes per launch over its HIP-event duration on the
-launching stream; `cpu_baseline` times the reference op (torch.spmm on the uncoalesced COO,
-oracle/cpu_baseline.py) on a bounded row sample on the host cores (rank 0, N = 1 only).
+launching stream; at cfg-4 most of those gathered bytes are served by the Infinity Cache
+(each 64-column slice of a KG is a 256 MB table), so `roofline.compulsory` adds the
+compulsory-traffic model (CSR once per slice pass + the table once + Y once) and its fraction
+of HBM.  `cpu_baseline` times the reference ops on the host cores (rank 0, N = 1 only):
+torch.spmm on the uncoalesced COO (all threads and 1 thread), one GAT head
+(layers/att_layers.py:29-61) and the ot_loss Sinkhorn loop (utils/ot_loss.py:50-66), each on a
+bounded sample (oracle/cpu_baseline.py).
 """
 import argparse
 import json
@@ -44,21 +53,31 @@ def log(*a):
 
 
 def pmc_traffic(world, kernel):
-    """Per-launch HBM bytes of the SpMM kernel from the committed rocprofv3 PMC summary of the
-    same workload at N = 1 (tools/gpu_round.sh pmc + tools/pmc_summary.py)."""
+    """Per-launch memory-side bytes of the SpMM kernel from the newest committed rocprofv3 PMC
+    summary of the same workload at N = 1 (tools/prof_sliced.sh + tools/pmc_summary.py):
+    (traffic bytes, source, extra fields)."""
     if world != 1:
-        return None, None
+        return None, None, {}
     import glob
     files = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_spmm*pmc*.json")))
              if json.load(open(f)).get("kernel") == kernel]
     if not files:
-        return None, None
+        return None, None, {}
     d = json.load(open(files[-1]))
-    return d["traffic_bytes"], os.path.relpath(files[-1], ROOT)
+    extra = {k: d[k] for k in ("l2_hit_rate", "dram_side_read_bytes") if k in d}
+    return d.get("traffic_bytes"), os.path.relpath(files[-1], ROOT), extra
 
 
 def gather_model_bytes(n_rows, nnz, d, elem=4):
     return 4 * (n_rows + 1) + 8 * nnz + elem * nnz * d + elem * n_rows * d
+
+
+def compulsory_bytes(n_rows, n_cols, nnz, d, sliced, elem=4, slice_w=64):
+    """Bytes that must cross HBM once per SpMM: the int32 CSR (re-read once per column slice by
+    the slice-major kernel), the feature table once (padded to whole slices), Y once."""
+    passes = (d + slice_w - 1) // slice_w if sliced else 1
+    dt = passes * slice_w if sliced else d
+    return passes * (4 * (n_rows + 1) + 8 * nnz) + elem * n_cols * dt + elem * n_rows * d
 
 
 def sinkhorn_rate(device, B=3000, reg=0.01):
@@ -148,8 +167,10 @@ def layout_rates(shard, H, Y, steps):
 
 
 def cpu_baseline(shard, H, budget_s=12.0):
-    """Reference op on the host: torch.spmm on the uncoalesced COO rows of a bounded sample."""
-    from oracle.cpu_baseline import time_reference_spmm
+    """Reference ops on the host: torch.spmm on the uncoalesced COO rows of a bounded sample
+    (all threads, then 1 thread), one GAT head and the ot_loss Sinkhorn loop."""
+    from oracle.cpu_baseline import (cpu_model, time_reference_gat, time_reference_sinkhorn,
+                                     time_reference_spmm)
     threads = torch.get_num_threads()
     n = shard.n
     tr = synth.kg_pair_triples(n, shard_t(n), synth.CONFIGS["cfg4"]["n_rel"])
@@ -159,10 +180,38 @@ def cpu_baseline(shard, H, budget_s=12.0):
     rate, nnz, dt = time_reference_spmm(r, c, v, N, N, Hc, sample_rows=N // 50)
     want_rows = int(min(N, max(N // 50, rate * budget_s / max(nnz / (N // 50), 1))))
     rate, nnz, dt = time_reference_spmm(r, c, v, N, N, Hc, sample_rows=want_rows)
-    return {"value": round(rate, 1), "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": "torch.spmm(uncoalesced int64 COO, H fp32) over the first %d of %d rows "
-                      "(%d edges, %.1f s) of the same cfg-4 graph, reference entry order" %
-                      (want_rows, N, nnz, dt)}
+    out = {"value": round(rate, 1), "unit": "edges/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(),
+           "sample": "torch.spmm(uncoalesced int64 COO, H fp32) over the first %d of %d rows "
+                     "(%d edges, %.1f s) of the same cfg-4 graph, reference entry order" %
+                     (want_rows, N, nnz, dt)}
+    try:
+        torch.set_num_threads(1)
+        rows1 = max(1000, N // 5)
+        r1, nnz1, dt1 = time_reference_spmm(r, c, v, N, N, Hc, sample_rows=rows1)
+        out["value_1thread"] = round(r1, 1)
+        out["sample_1thread"] = "first %d rows (%d edges, %.1f s)" % (rows1, nnz1, dt1)
+    finally:
+        torch.set_num_threads(threads)
+    # one GAT head (4 x 75 heads per layer at cfg-4): head-edges/s on a row sample
+    g = torch.Generator().manual_seed(3)
+    W = torch.randn(H.shape[1], 75, generator=g) * 0.05
+    a = torch.randn(1, 150, generator=g) * 0.05
+    rows_g = max(1000, N // 100)
+    rg, eg, dtg = time_reference_gat(r, c, v, N, Hc, W, a, rows_g)
+    out["gat_head"] = {"value": round(rg, 1), "unit": "head-edges/s", "cores": threads,
+                       "sample": "one SpGraphAttentionLayer head (layers/att_layers.py:29-61, "
+                                 "300 -> 75) over destination rows < %d (%d edges, %.1f s; "
+                                 "h = x.W over all %d rows included)" % (rows_g, eg, dtg, N)}
+    gs = torch.Generator().manual_seed(0)
+    X = 0.05 * torch.randn(3000, 300, generator=gs)
+    Y = 0.05 * torch.randn(3000, 300, generator=gs)
+    M = torch.cdist(X, Y)
+    rs, dts = time_reference_sinkhorn(M / M.max(), 0.01, 300)
+    out["sinkhorn"] = {"value": round(rs, 1), "unit": "iters/s", "cores": threads, "B": 3000,
+                       "sample": "utils/ot_loss.py:50-66 loop body, fp64, 300 iterations "
+                                 "(%.1f s)" % dts}
+    return out
 
 
 def shard_t(n):
@@ -178,19 +227,26 @@ def main():
                     help="entities per KG (default: cfg-4, 1M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sinkhorn", action="store_true")
-    ap.add_argument("--partition", choices=("tiles", "features", "rows"), default="tiles",
-                    help="inside a KG group: row blocks x 2 feature-column slices (tiles) or "
-                         "feature-column slices of all rows (features) - both exchange-free - or "
-                         "row blocks with the RCCL halo all-gather (rows)")
+    ap.add_argument("--partition", choices=("rows", "tiles", "features"), default="rows",
+                    help="inside a KG group: row blocks with the halo exchange a layer needs "
+                         "(rows, default), or the exchange-free aggregation-only partitions: row "
+                         "blocks x 2 feature-column slices (tiles), feature-column slices of all "
+                         "rows (features)")
+    ap.add_argument("--no-side", action="store_true",
+                    help="N > 1: skip the labelled exchange-free side number (tiles)")
     ap.add_argument("--no-train", action="store_true",
                     help="skip the side measurement of the row-sharded HGCN-EA training step")
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--layout", choices=("sliced", "rowmajor"), default="sliced",
                     help="feature table layout of the aggregation input (sliced: 64-column "
                          "slices, each one Infinity-Cache-sized table at 1M rows)")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="only the headline aggregation (profiling passes): no side numbers")
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank logic on ONE device with gloo (halo staged through host)")
     args = ap.parse_args()
+    if args.headline_only:
+        args.no_cpu_baseline = args.no_sinkhorn = args.no_train = args.no_side = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -269,6 +325,64 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_nnz / (elapsed / args.steps)
 
+    # the exchange alone (rows partition inside a group): bytes each rank receives per step and
+    # the time of K back-to-back exchanges, max over ranks
+    exchange = None
+    if shard.g > 1 and part.kind == "rows" and not args.rehearse:
+        from gnnea import exchange as ex
+        ranks = part.group_ranks(part.kg)
+
+        def xchg():
+            for w in ex.all_gather(h_local, h_full, shard.group, ranks, part.li):
+                w.wait()
+        for _ in range(2):
+            xchg()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            xchg()
+        torch.cuda.synchronize()
+        xt = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=device)
+        dist.all_reduce(xt, op=dist.ReduceOp.MAX)
+        x_ms = float(xt) / args.steps * 1e3
+        x_bytes = (shard.g - 1) * part.n_rows * Dl * 4
+        exchange = {"transport": "direct peer transfers (batch_isend_irecv, one per group peer)"
+                                 if ex.MODE == "p2p" else "RCCL ring all_gather",
+                    "peers": shard.g - 1, "bytes_recv_per_rank_per_step": x_bytes,
+                    "ms_alone": round(x_ms, 4),
+                    "GBps_recv_per_rank": round(x_bytes / (x_ms * 1e-3) / 1e9, 1),
+                    "spmm_kernel_ms": round(kernel_ms, 4)}
+
+    # labelled side number: the exchange-free tiles partition (aggregation only; a layer would
+    # first all-gather its input, which this number does not contain)
+    side = None
+    if world > 2 and part.kind == "rows" and not args.no_side and not args.rehearse:
+        del h_full
+        sh2 = KGShard(n, shard_t(n), synth.CONFIGS["cfg4"]["n_rel"], rank, world, device,
+                      kind="tiles", D=D)
+        p2 = sh2.part
+        D2 = p2.col1 - p2.col0
+        h2 = torch.randn(sh2.n_cols, D2, device=device, generator=gen)
+        y2 = torch.empty(sh2.n_rows, D2, device=device)
+        hs2 = ops.slice_pack(h2) if ops.use_sliced(sh2.n_cols, D2, torch.float32) else None
+        for _ in range(2):
+            sh2.aggregate(h2, None, y2, _lib.GNNEA_ACT_RELU, hs=hs2)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            sh2.aggregate(h2, None, y2, _lib.GNNEA_ACT_RELU, hs=hs2)
+        torch.cuda.synchronize()
+        st = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=device)
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        s_ms = float(st) / args.steps * 1e3
+        side = {"partition": "tiles: %d row blocks x %d feature-column slices per KG group, "
+                             "aggregation only, NO exchange (a layer needs its input "
+                             "all-gathered first)" % (p2.gr, p2.gc),
+                "edges_per_s": round(total_nnz / (s_ms * 1e-3), 1), "ms_per_step": round(s_ms, 4)}
+        del sh2, h2, y2, hs2
+
     # side measurement (every rank, same collective sequence): the row-sharded HGCN-EA training
     # step of BASELINE.json configs[3] through the drop-in modules with the RCCL halo exchange
     train = None
@@ -288,7 +402,10 @@ def main():
             launches = len(blocks)
         traffic = gather_model_bytes(shard.n_rows, shard.nnz, Dl)
         achieved = traffic / (kernel_ms * 1e-3) / 1e9
-        pmc_bytes, pmc_src = pmc_traffic(world, "k_spmm_sliced" if sliced else "k_spmm_v4")
+        comp = compulsory_bytes(shard.n_rows, shard.n_cols, shard.nnz, Dl, sliced)
+        comp_gbs = comp / (kernel_ms * 1e-3) / 1e9
+        pmc_bytes, pmc_src, pmc_extra = pmc_traffic(world, "k_spmm_sliced" if sliced else
+                                                     "k_spmm_v4")
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -300,8 +417,10 @@ def main():
                        "nnz": int(round(total_nnz)), "nodes": 2 * n, "D": D,
                        "parallelism": "single GPU" if world == 1 else
                        ("2 KG groups of %d GPUs, %d row blocks x %d feature-column slices "
-                        "(no exchange)" % (shard.g, part.gr, part.gc) if free else
-                        "2 KG groups of %d GPUs, row blocks + RCCL halo all-gather" % shard.g)},
+                        "(aggregation only, no exchange)" % (shard.g, part.gr, part.gc) if free
+                        else ("2 KG groups (one KG per GPU, nothing to exchange)" if shard.g == 1
+                              else "2 KG groups of %d GPUs, row blocks + halo exchange by direct "
+                                   "peer transfers, inside the timed step" % shard.g))},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_bytes, "traffic_source": pmc_src,
@@ -311,12 +430,33 @@ def main():
                          "kernel_ms": round(kernel_ms / launches, 4),
                          "bytes_per_launch": int(traffic / launches),
                          "model": "gather: 4(N+1)+8E+4ED+4ND (rank 0 shard, D = its slice), "
-                                  "split evenly over the per-KG launches"},
+                                  "split evenly over the per-KG launches",
+                         "bound_detail": "gather rate: each 64-column slice of a KG is a 256 MB "
+                                         "table, so most gathered bytes are Infinity-Cache "
+                                         "(MALL) hits; the gather model counts them, HBM sees "
+                                         "the compulsory bytes" if sliced else
+                                         ("gather rate from HBM (row-major table >> the 256 MB "
+                                          "Infinity Cache)" if shard.n_cols * Dl * 4 > 2 ** 28
+                                          else "gather rate of an Infinity-Cache-resident table"),
+                         "compulsory": {"bytes_per_step": int(comp),
+                                        "achieved": round(comp_gbs, 1),
+                                        "frac": round(comp_gbs / HBM_PEAK_GBS, 4),
+                                        "model": "CSR 4(N+1)+8E once per slice pass (%d) + "
+                                                 "table 4*N*%d once + Y 4*N*D once" %
+                                                 ((Dl + 63) // 64 if sliced else 1,
+                                                  ((Dl + 63) // 64) * 64 if sliced else Dl)}},
         }
+        if pmc_extra:
+            line["roofline"]["pmc"] = dict(pmc_extra, note="memory-side counters include "
+                                           "Infinity-Cache hits (upper bound on HBM bytes)")
+        if exchange is not None:
+            line["exchange"] = exchange
+        if side is not None:
+            line["exchange_free_side"] = side
         line["config"]["layout"] = ("slice-major [%d][%d][64] fp32 (as gnnea_gemm_sliced_f32 "
                                     "writes the projection)" % ((Dl + 63) // 64, shard.n_cols)
                                     if sliced else "row-major [%d][%d] fp32" % (shard.n_cols, Dl))
-        if world == 1:
+        if world == 1 and not args.headline_only:
             try:
                 line["layouts"] = layout_rates(shard, h_local, y, args.steps)
             except Exception as e:  # report, never hide
@@ -328,7 +468,7 @@ def main():
                 line["sinkhorn"] = sinkhorn_rate(device)
             except Exception as e:  # report, never hide
                 line["sinkhorn"] = {"error": repr(e)}
-        if world == 1:
+        if world == 1 and not args.headline_only:
             try:
                 line["bf16"] = bf16_rate(shard, h_local, args.steps)
             except Exception as e:  # report, never hide

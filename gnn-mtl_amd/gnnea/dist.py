@@ -5,7 +5,7 @@ Layout (one process per GPU, torch.distributed; backend "nccl" is RCCL over xGMI
     [0, W/2) serve KG1 and [W/2, W) serve KG2 — no traffic between the two groups
     (W = 1 keeps the whole graph on one GPU; W = 2 is one KG per GPU, nothing to exchange);
   * inside a KG group of g = W/2 ranks, three partitions are implemented:
-    - "features" (default): every rank holds the whole KG adjacency and a 16-B-aligned slice
+    - "features": every rank holds the whole KG adjacency and a 16-B-aligned slice
       of the feature columns (300 = 76+76+76+72 at g = 4).  relu(A·H) is column-separable,
       so the aggregation needs NO exchange; in a full layer the group exchange moves to the
       projection input (all-gather of the previous layer's column slices, same volume);
@@ -13,9 +13,11 @@ Layout (one process per GPU, torch.distributed; backend "nccl" is RCCL over xGMI
       times gr = g/2 blocks of destination rows; every rank gathers from the whole KG's column
       slice, so again NO exchange (8 GPUs: 2 x 2 tiles of 500k rows x 150 columns instead of
       four 76-column slices of all rows);
-    - "rows": each rank owns n/g destination rows (KG-local column ids) and all-gathers the
+    - "rows": each rank owns n/g destination rows (KG-local column ids) and gathers the
       group's projected rows (the halo: on uniform random graphs nearly every remote row is
-      referenced) with RCCL, overlapped with the aggregation over its own rows.
+      referenced) by direct peer transfers over xGMI (gnnea.exchange), overlapped with the
+      aggregation over its own rows.  This is what a graph layer executes, so it is the bench
+      default at N > 1; the two exchange-free partitions time the aggregation alone.
 The partition / exchange logic is device-independent (numpy + torch.distributed) and is
 exercised with gloo on CPU in tests/test_dist_gloo.py; the GPU path adds only the CSR upload.
 """
@@ -107,21 +109,37 @@ def make_groups(part):
     return groups[part.kg]
 
 
-def halo_gather(h_local, h_full, group, group_size, async_op=False):
-    """All-gather the group's projected rows into h_full [group_size * rows, D].
+def halo_gather(h_local, h_full, group, group_size, async_op=False, part=None):
+    """Assemble the group's projected rows in h_full [group_size * rows, D].
 
-    RCCL: one all_gather_into_tensor (async_op=True returns the work so the caller can overlap
-    the locally owned part of the aggregation).  gloo (CPU rehearsal of the multi-rank logic):
-    synchronous, staged through host memory when the tensors live on a device."""
+    Direct peer transfers (gnnea.exchange.all_gather: one send and one receive per group peer
+    in one RCCL group call, each pair on its own xGMI link; async_op=True returns the works so
+    the caller can overlap the locally owned part of the aggregation).  ``part`` gives the
+    group's ranks and this rank's index; without it the group is taken as consecutive ranks.
+    The own block is copied too (callers that read only remote blocks use exchange directly).
+    gloo (CPU rehearsal of the multi-rank logic): synchronous, staged through host memory when
+    the tensors live on a device."""
+    from . import exchange
     if group_size == 1:
         return None
-    if dist.get_backend(group) == "gloo":
-        hl = h_local.detach().cpu().contiguous()
-        parts = [torch.empty_like(hl) for _ in range(group_size)]
-        dist.all_gather(parts, hl, group=group)
-        h_full.copy_(torch.cat(parts))
-        return None
-    return dist.all_gather_into_tensor(h_full, h_local, group=group, async_op=async_op)
+    if part is not None:
+        ranks, li = part.group_ranks(part.kg), part.li
+    else:
+        me = dist.get_rank()
+        base = me - me % group_size
+        ranks, li = list(range(base, base + group_size)), me % group_size
+    works = exchange.all_gather(h_local, h_full, group, ranks, li, copy_own=True,
+                                async_op=async_op)
+    return _Works(works) if works else None
+
+
+class _Works:
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
 
 
 class KGShard:
@@ -176,12 +194,15 @@ class KGShard:
                 ops.spmm(self.csr, h_local, act, out=out)
             rec(1)
             return out
-        work = halo_gather(h_local, h_full, self.group, self.part.g, async_op=True)
+        from . import exchange
+        works = exchange.all_gather(h_local, h_full, self.group,
+                                    self.part.group_ranks(self.part.kg), self.part.li,
+                                    async_op=True)
         rec(0)
         ops.spmm(self.csr_own, h_local, GNNEA_ACT_IDENTITY, out=out)
         rec(1)
-        if work is not None:
-            work.wait()
+        for w in works:
+            w.wait()
         rec(2)
         ops.spmm(self.csr_remote, h_full, act, out=out, beta=1.0)
         rec(3)

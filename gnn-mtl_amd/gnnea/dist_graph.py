@@ -7,12 +7,12 @@ owns the n/g destination rows [l·n/g, (l+1)·n/g) of its KG, and the layers run
 only.  Per graph layer (layers/layers.py:30-39, 58-77):
 
   forward   hidden_loc = x_loc·Wᵀ + b                local MFMA GEMM (unchanged drop-in code)
-            hidden_KG  = all_gather(hidden_loc)       RCCL, inside the KG group, overlapped with
-            out_loc    = act(A_own·hidden_loc           the SpMM over the locally owned columns
+            hidden_KG  = all_gather(hidden_loc)       peer transfers inside the KG group, overlapped
+            out_loc    = act(A_own·hidden_loc           with the SpMM over the owned columns
                              + A_remote·hidden_KG)
   backward  G_loc      = dY_loc ⊙ act'(out_loc)
             P          = A_shardᵀ · G_loc             [n, D]: this rank's share of every row
-            dhidden_loc= reduce_scatter(P)            RCCL, inside the KG group
+            dhidden_loc= reduce_scatter(P)            peer transfers, summed by the owner
             dW, db     = local GEMMs; summed over ALL ranks by allreduce_grads() (one bucket)
 
 The HighWay gate (x_loc·K_g, the blend with x_loc) is row-local.  ``gather_rows`` assembles the
@@ -195,37 +195,30 @@ class DistAdj:
         return GatherRowsFn.apply(out_loc, self)
 
     # ---- exchanges ------------------------------------------------------------------------
-    def halo(self, h_loc, async_op=False):
-        """All-gather the KG group's rows: returns (h_KG [n, D], work or None)."""
+    def halo(self, h_loc, async_op=False, copy_own=True):
+        """The KG group's rows [n, D] by direct peer transfers (gnnea.exchange): returns
+        (h_KG, work or None); copy_own=False leaves the own block unwritten (for the
+        remote-column CSR, which never reads it)."""
+        from . import exchange
+        from .dist import _Works
         g = self.part.g
         if g == 1:
             return h_loc, None
         h_loc = h_loc.contiguous()
-        if _is_gloo(self.group):
-            hl = h_loc.detach().cpu()
-            parts = [torch.empty_like(hl) for _ in range(g)]
-            dist.all_gather(parts, hl, group=self.group)
-            return torch.cat(parts).to(h_loc.device), None
         full = torch.empty((g * h_loc.shape[0], h_loc.shape[1]), dtype=h_loc.dtype,
                            device=h_loc.device)
-        work = dist.all_gather_into_tensor(full, h_loc, group=self.group, async_op=async_op)
-        return full, work
+        works = exchange.all_gather(h_loc, full, self.group, self.part.group_ranks(self.part.kg),
+                                    self.part.li, copy_own=copy_own, async_op=async_op)
+        return full, (_Works(works) if works else None)
 
     def reduce_scatter(self, partial):
-        """Sum the group's [n, D] partials and keep this rank's n/g rows."""
-        g = self.part.g
-        if g == 1:
+        """Sum the group's [n, D] partials and keep this rank's n/g rows (peer transfers, the
+        owner sums in peer order)."""
+        from . import exchange
+        if self.part.g == 1:
             return partial
-        partial = partial.contiguous()
-        rows = self.part.n_rows
-        li = self.part.li
-        if _is_gloo(self.group):  # gloo has no reduce_scatter: all_reduce then slice
-            p = partial.detach().cpu()
-            dist.all_reduce(p, group=self.group)
-            return p[li * rows:(li + 1) * rows].to(partial.device)
-        out = torch.empty((rows, partial.shape[1]), dtype=partial.dtype, device=partial.device)
-        dist.reduce_scatter_tensor(out, partial, group=self.group)
-        return out
+        return exchange.reduce_scatter(partial, self.group, self.part.group_ranks(self.part.kg),
+                                       self.part.li)
 
     def all_rows(self, out_loc):
         W = self.part.world
@@ -252,7 +245,7 @@ class HaloAggregateFn(torch.autograd.Function):
         if dadj.part.g == 1:
             out = e.spmm(dadj.csr, hidden, act)
         else:
-            full, work = dadj.halo(hidden, async_op=True)
+            full, work = dadj.halo(hidden, async_op=True, copy_own=False)
             out = e.spmm(dadj.csr_own, hidden, _lib.GNNEA_ACT_IDENTITY)  # overlaps the gather
             if work is not None:
                 work.wait()

@@ -1,6 +1,8 @@
 #!/bin/bash
-# rocprofv3 evidence for the bench's SpMM: kernel-trace stats of the bench, then FETCH_SIZE and
-# WRITE_SIZE in passes of their own; summary -> gpurun_out/spmm_pmc.json.
+# rocprofv3 evidence for the bench's SpMM: kernel-trace stats of the full bench, then PMC
+# counters of the headline aggregation in passes of their own (each within the per-block limits:
+# FETCH_SIZE uses 3 TCC counters, WRITE_SIZE 2); summary -> gpurun_out/spmm_pmc.json.
+#   bash tools/prof_sliced.sh [kernel substring]
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out
@@ -9,9 +11,11 @@ mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/prof_b" -o run --output-format csv \
   -- python "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-train > "$O/prof_b.log" 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$O/pmc_f" -o run --output-format csv \
-  -- python "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-sinkhorn --no-train > "$O/pmc_f.log" 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$O/pmc_w" -o run --output-format csv \
-  -- python "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-sinkhorn --no-train > "$O/pmc_w.log" 2>&1 || exit $?
-python "$R/tools/pmc_summary.py" $(find "$O/pmc_f" -name "*counter_collection.csv" | head -1) \
-  $(find "$O/pmc_w" -name "*counter_collection.csv" | head -1) "$K" "$O/spmm_pmc.json"
+i=0
+for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_32B_sum"; do
+  i=$((i+1))
+  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $pmc -d "$O/pmc_$i" -o run --output-format csv \
+    -- python "$R/bench.py" --steps 3 --warmup 1 --headline-only > "$O/pmc_$i.log" 2>&1 || exit $?
+done
+python "$R/tools/pmc_summary.py" "$K" "$O/spmm_pmc.json" \
+  $(find "$O"/pmc_1 "$O"/pmc_2 "$O"/pmc_3 -name "*counter_collection.csv")
