@@ -4,12 +4,9 @@ Everything here is dense linear algebra on device tensors: the two products of g
 (C1 · T · C2^T, 2·I·J·(I+J) flops per outer iteration) go to the library GEMM (hipBLASLt through
 torch.mm), elementwise work stays in torch.  The Sinkhorn inner solves that consume these costs
 run on the gnnea kernels (SinkhornOT/sinkhorn_loss.py).  Distance helpers outside the GW path
-(energy distances, ...) are taken from the reference module when it is importable.
+(energy distances, ...) are taken from the reference module when GNNEA_UPSTREAM names its checkout.
 """
-import importlib.util
 import math
-import os
-import sys
 
 import torch
 
@@ -94,21 +91,10 @@ def FGW_cost_matrix(D, constC, hC1, hC2, T, alpha, epsilon, p):
 
 
 def _merge_upstream():
-    here = os.path.dirname(os.path.abspath(__file__))
-    for base in sys.path:
-        cand = os.path.join(os.path.abspath(base or "."), "SinkhornOT", "cderivation.py")
-        if os.path.dirname(cand) == here or not os.path.exists(cand):
-            continue
-        try:
-            spec = importlib.util.spec_from_file_location("SinkhornOT._upstream_cderivation", cand)
-            mod = importlib.util.module_from_spec(spec)
-            spec.loader.exec_module(mod)
-        except Exception:
-            return
-        for k, v in vars(mod).items():
-            if not k.startswith("__"):
-                globals().setdefault(k, v)
-        return
+    """Opt-in (GNNEA_UPSTREAM=<reference checkout>, gnnea/upstream.py): the reference module's
+    remaining helpers."""
+    from gnnea import upstream
+    upstream.merge(globals(), "SinkhornOT/cderivation.py", "SinkhornOT._upstream_cderivation")
 
 
 _merge_upstream()

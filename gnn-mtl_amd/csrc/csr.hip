@@ -3,12 +3,14 @@
 //
 // Pipeline (all on the caller's stream, all scratch in the caller's workspace):
 //   key[e] = row[e] * n_cols + col[e]          (uint64; only the needed bits are sorted)
-//   stable radix sort (key, e)                 (hipcub -> rocPRIM onesweep)
+//   stable radix sort (key, e)                 (rocPRIM onesweep)
 //   head[k] = key[k] != key[k-1]               -> inclusive scan -> output slot
 //   heads sum their duplicate run in input order, write col / val / perm, count rows
 //   rowptr = exclusive scan of row counts
 #include "common.h"
-#include <hipcub/hipcub.hpp>
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 namespace gnnea {
 
@@ -68,13 +70,13 @@ struct CsrWs {
 
 static int plan_ws(int64_t nnz, int64_t n_rows, int end_bit, CsrWs* w) {
   size_t sort_bytes = 0, scan_bytes = 0, scan_rows = 0;
-  hipcub::DoubleBuffer<uint64_t> kb(nullptr, nullptr);
-  hipcub::DoubleBuffer<int64_t> vb(nullptr, nullptr);
-  GNNEA_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, kb, vb, (int)nnz, 0, end_bit));
-  GNNEA_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, scan_bytes, (int*)nullptr, (int*)nullptr,
-                                             (int)nnz));
-  GNNEA_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_rows, (int*)nullptr, (int*)nullptr,
-                                             (int)(n_rows + 1)));
+  rocprim::double_buffer<uint64_t> kb(nullptr, nullptr);
+  rocprim::double_buffer<int64_t> vb(nullptr, nullptr);
+  GNNEA_HIP(rocprim::radix_sort_pairs(nullptr, sort_bytes, kb, vb, (size_t)nnz, 0, end_bit));
+  GNNEA_HIP(rocprim::inclusive_scan(nullptr, scan_bytes, (int*)nullptr, (int*)nullptr,
+                                    (size_t)nnz, rocprim::plus<int>()));
+  GNNEA_HIP(rocprim::exclusive_scan(nullptr, scan_rows, (int*)nullptr, (int*)nullptr, 0,
+                                    (size_t)(n_rows + 1), rocprim::plus<int>()));
   int64_t o = 0;
   w->keys_a = o; o = align_up(o + 8 * nnz);
   w->keys_b = o; o = align_up(o + 8 * nnz);
@@ -158,24 +160,24 @@ extern "C" int gnnea_coo_to_csr(const void* row_idx, const void* col_idx, int in
                        keys_a, idx_a, bad, n_rows);
   GNNEA_LAUNCH_CHECK();
 
-  hipcub::DoubleBuffer<uint64_t> kb(keys_a, keys_b);
-  hipcub::DoubleBuffer<int64_t> vb(idx_a, idx_b);
+  rocprim::double_buffer<uint64_t> kb(keys_a, keys_b);
+  rocprim::double_buffer<int64_t> vb(idx_a, idx_b);
   size_t sort_bytes = w.cub_sort;
-  GNNEA_HIP(hipcub::DeviceRadixSort::SortPairs(cub, sort_bytes, kb, vb, (int)nnz, 0, end_bit,
-                                               stream));
-  const uint64_t* keys = kb.Current();
-  const int64_t* idx = vb.Current();
+  GNNEA_HIP(rocprim::radix_sort_pairs(cub, sort_bytes, kb, vb, (size_t)nnz, 0, end_bit, stream));
+  const uint64_t* keys = kb.current();
+  const int64_t* idx = vb.current();
 
   hipLaunchKernelGGL(k_heads, dim3(nb), dim3(tpb), 0, stream, keys, nnz, head);
   GNNEA_LAUNCH_CHECK();
   size_t scan_bytes = w.cub_scan;
-  GNNEA_HIP(hipcub::DeviceScan::InclusiveSum(cub, scan_bytes, head, slot, (int)nnz, stream));
+  GNNEA_HIP(rocprim::inclusive_scan(cub, scan_bytes, head, slot, (size_t)nnz,
+                                    rocprim::plus<int>(), stream));
   hipLaunchKernelGGL(k_emit, dim3(nb), dim3(tpb), 0, stream, keys, idx, head, slot, nnz,
                      (uint64_t)n_cols, val, col_out, val_out, perm_out, count, nnz_out, bad);
   GNNEA_LAUNCH_CHECK();
   size_t scan_rows = w.cub_scan_rows;
-  GNNEA_HIP(hipcub::DeviceScan::ExclusiveSum(cub, scan_rows, count, rowptr, (int)(n_rows + 1),
-                                             stream));
+  GNNEA_HIP(rocprim::exclusive_scan(cub, scan_rows, count, rowptr, 0, (size_t)(n_rows + 1),
+                                    rocprim::plus<int>(), stream));
   return 0;
 }
 

@@ -34,7 +34,8 @@ constexpr int kMaxJ = 64 * kSweepWaves * 16;
 constexpr int kMaxSweepWg = 64 * 8;  // column partials the update kernel sums in one round
 
 enum { ST_DONE = 0, ST_ITERS = 1, ST_REASON = 2, ST_SLOT = 3, ST_BIG = 4, ST_FAIL = 5 };
-enum { SD_TNEW = 8, SD_ERR = 8, SD_TPREV = 9, SD_LOSS = 10, SD_TOL = 11 };
+enum { SD_ERR = GNNEA_SK_SD_ERR, SD_TPREV = GNNEA_SK_SD_TPREV, SD_LOSS = GNNEA_SK_SD_LOSS,
+       SD_TOL = GNNEA_SK_SD_TOL, SD_TNEW = GNNEA_SK_SD_TNEW };
 
 static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 

@@ -85,7 +85,8 @@ static SkDev sk_dev(const gnnea_sinkhorn* p) {
 }
 
 enum { ST_DONE = 0, ST_ITERS = 1, ST_REASON = 2, ST_SLOT = 3, ST_BIG = 4, ST_FAIL = 5 };
-enum { SD_ERR = 8, SD_TPREV = 9, SD_LOSS = 10, SD_TNEW = 8 };
+enum { SD_ERR = GNNEA_SK_SD_ERR, SD_TPREV = GNNEA_SK_SD_TPREV, SD_LOSS = GNNEA_SK_SD_LOSS,
+       SD_TOL = GNNEA_SK_SD_TOL, SD_TNEW = GNNEA_SK_SD_TNEW };
 
 template <typename T>
 __device__ __forceinline__ double ld_c(const T* C, int64_t idx) {
@@ -179,7 +180,7 @@ __device__ __forceinline__ bool knopp_stop(SkDev& d, int it) {
       double e = 0.0;
       for (int b = lane; b < d.ncb; b += 64) e += d.errpart[b];
       const double err = sqrt(wave_sum(e));
-      if (!(err > d.sd[11])) st = 1;  // sd[11] = stopThr: the loop runs while err > stopThr
+      if (!(err > d.sd[SD_TOL])) st = 1;  // stopThr: the loop runs while err > stopThr
       if (blockIdx.x == 0 && lane == 0) {
         d.sd[SD_ERR] = err;
         if (st) mark_done(d.st, prev + 1, 1, prev & 1);
@@ -487,7 +488,7 @@ __global__ void k_sk_init(SkArgs a, SkDev d, double tol) {
   if (t < 32) {
     if (t < 8) d.st[t] = 0;
     else d.sd[t] = 0.0;
-    if (t == 11) d.sd[11] = tol;
+    if (t == SD_TOL) d.sd[SD_TOL] = tol;
   }
   const bool knopp = a.mode == GNNEA_SK_KNOPP;
   // KNOPP: u = 1/I, v = 1/J stored in slot 1 (the "previous" slot of iteration 0)

@@ -15,7 +15,7 @@ ST_DONE, ST_ITERS, ST_REASON, ST_SLOT = 0, 1, 2, 3
 # path of solve() calls that do not choose one: 0 = scaling form with the resident fp64 K
 # (falls back to 1 above J = 8192), 1 = fused log-domain passes (no I x J workspace)
 DEFAULT_VARIANT = 0
-SD_ERR, SD_TPREV, SD_LOSS = 8, 9, 10
+SD_ERR, SD_TPREV, SD_LOSS, SD_TNEW = 8, 9, 10, 12  # GNNEA_SK_SD_* (include/gnnea.h)
 MAX_BATCH = 100  # iterations enqueued between two host polls of the status block, at most
 
 
@@ -107,5 +107,5 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
             J, ptr(row_sum), ptr(col_sum), st))
         ints, dbl = _status(ws)
     return SinkhornResult(plan, row_sum, col_sum, int(ints[ST_ITERS]), int(ints[ST_REASON]),
-                          float(dbl[SD_ERR]), float(dbl[8]), float(dbl[SD_TPREV]),
+                          float(dbl[SD_ERR]), float(dbl[SD_TNEW]), float(dbl[SD_TPREV]),
                           float(dbl[SD_LOSS]))

@@ -7,12 +7,9 @@ signatures and outputs; the per-line / per-triple Python loops are replaced by t
 library (gnnea.ingest: parallel parsing, counting-sort adjacency in the reference's dict order)
 and vectorised numpy / scipy.  Entry order and fp32 values of the adjacency are bit-identical
 (tests/test_adjacency.py, tests/test_ingest.py).  The other task loaders of the reference module
-(node classification, text) are re-exported from it when it is importable.
+(node classification, text) are re-exported from it when GNNEA_UPSTREAM names its checkout (gnnea/upstream.py).
 """
-import importlib.util
 import json
-import os
-import sys
 
 import numpy as np
 import scipy.sparse as sp
@@ -183,7 +180,7 @@ def load_seperate_data_ea(args):
 
 def load_data(args):
     """(:17-26) task dispatch; the entity-alignment task is served here, the others by the
-    reference module's loaders when it is importable."""
+    reference module's loaders (opt-in: GNNEA_UPSTREAM)."""
     if args.task == 'ea':
         return load_data_ea(args)
     up = globals().get('_upstream_load_data')
@@ -194,28 +191,21 @@ def load_data(args):
 
 
 def _merge_upstream():
-    here = os.path.dirname(os.path.abspath(__file__))
-    for base in sys.path:
-        cand = os.path.join(os.path.abspath(base or "."), "utils", "data_utils.py")
-        if os.path.dirname(cand) == here or not os.path.exists(cand):
-            continue
-        try:
-            spec = importlib.util.spec_from_file_location("utils._upstream_data_utils", cand)
-            mod = importlib.util.module_from_spec(spec)
-            spec.loader.exec_module(mod)
-        except Exception:  # upstream loaders need absent deps (torchtext): keep ours only
-            return
-        ours = {k: globals()[k] for k in (
-            "sparse_mx_to_torch_sparse_tensor", "get_matrix", "get_sparse_tensor",
+    """Opt-in (GNNEA_UPSTREAM=<reference checkout>, gnnea/upstream.py): the reference's loaders
+    for the other tasks; our EA loaders are installed into the reference module."""
+    from gnnea import upstream
+    ours = ("sparse_mx_to_torch_sparse_tensor", "get_matrix", "get_sparse_tensor",
             "get_sparse_tensor_for_one_graph", "loadfile", "rfunc", "get_features",
-            "load_data_ea", "load_seperate_data_ea")}
-        globals()['_upstream_load_data'] = getattr(mod, 'load_data', None)
-        for k, v in vars(mod).items():
-            if not k.startswith("__") and k not in ours:
-                globals().setdefault(k, v)
-        for k, v in ours.items():
-            setattr(mod, k, v)
+            "load_data_ea", "load_seperate_data_ea")
+    mod = upstream.load("utils/data_utils.py", "utils._upstream_data_utils")
+    if mod is None:
         return
+    globals()['_upstream_load_data'] = getattr(mod, 'load_data', None)
+    for k, v in vars(mod).items():
+        if not k.startswith("__") and k not in ours:
+            globals().setdefault(k, v)
+    for k in ours:
+        setattr(mod, k, globals()[k])
 
 
 _merge_upstream()

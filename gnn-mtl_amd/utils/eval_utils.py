@@ -5,11 +5,8 @@ and argsorts every row and column.  Here the rank of the true match is counted d
 device (gnnea_l1_rank_f32: #closer candidates + #equal candidates of lower index), which is the
 position of i in a stable argsort of the same fp64 distances; only the counts come back.
 Node-classification helpers (acc_f1, nc_metrics, ...) are not on the alignment path and are taken
-from the reference module when it is importable.
+from the reference module when GNNEA_UPSTREAM names its checkout (gnnea/upstream.py).
 """
-import importlib.util
-import os
-import sys
 
 import numpy as np
 import torch
@@ -85,21 +82,10 @@ def eval_at_1(outputs, data):
 
 
 def _merge_upstream():
-    here = os.path.dirname(os.path.abspath(__file__))
-    for base in sys.path:
-        cand = os.path.join(os.path.abspath(base or "."), "utils", "eval_utils.py")
-        if os.path.dirname(cand) == here or not os.path.exists(cand):
-            continue
-        try:
-            spec = importlib.util.spec_from_file_location("utils._upstream_eval_utils", cand)
-            mod = importlib.util.module_from_spec(spec)
-            spec.loader.exec_module(mod)
-        except Exception:  # upstream needs sklearn etc.: keep ours only
-            return
-        for k, v in vars(mod).items():
-            if not k.startswith("__"):
-                globals().setdefault(k, v)
-        return
+    """Opt-in (GNNEA_UPSTREAM=<reference checkout>, gnnea/upstream.py): the reference module's
+    remaining helpers."""
+    from gnnea import upstream
+    upstream.merge(globals(), "utils/eval_utils.py", "utils._upstream_eval_utils")
 
 
 _merge_upstream()

@@ -324,8 +324,12 @@ int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64
 #define GNNEA_SK_ST_REASON 2     /* 0 running/max-iter, 1 tolerance, 2 numerical-error break */
 #define GNNEA_SK_ST_SLOT 3       /* ping-pong slot holding the final scalings */
 #define GNNEA_SK_STATUS_BYTES 256
-/* double words after the int block: [8]=err (KNOPP) / transport_new, [9]=transport_prev,
- * [10]=loss (KNOPP: sum P M) */
+/* double words (indices into the block viewed as doubles) */
+#define GNNEA_SK_SD_ERR 8        /* KNOPP: last err = ||v * (K^T u) - b|| */
+#define GNNEA_SK_SD_TPREV 9      /* STAB family: transport at the previous check */
+#define GNNEA_SK_SD_LOSS 10      /* KNOPP: sum P * M */
+#define GNNEA_SK_SD_TOL 11       /* the stop threshold (set by init) */
+#define GNNEA_SK_SD_TNEW 12      /* STAB family: transport at the last check */
 
 typedef struct gnnea_sinkhorn {
   int mode;         /* GNNEA_SK_* */

@@ -5,7 +5,8 @@ synthetic KG pair, node-sharded with the RCCL halo exchange).
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/dist_step.py
 
 A step = the drop-in Encoder.encode + Decoder.decode (models/encoders.py, models/decoders.py;
-HGCN: three HighWay graph convolutions, GCN: two graph convolutions + the GCN decoder) forward
+HGCN: three HighWay graph convolutions; GCN: two graph convolutions + the 3-layer MLP decoder;
+GAT: two 4-head graph attention layers + the MLP decoder, models/decoders.py:76-81) forward
 on this rank's rows with a DistAdj, backward from a fixed upstream gradient on the rank's rows
 (the EA loss is row-local once the embeddings are gathered; the gather is not timed here), and
 the one-bucket RCCL all-reduce of the weight gradients.  Prints one JSON line on rank 0.
@@ -108,8 +109,11 @@ def measure(model, n, rank, world, dev, steps, warmup, dtype=torch.float32):
     nnz = torch.tensor([float(dadj.nnz)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(nnz)  # row shards: every edge of the graph once
+    layers = {"HGCN": "3 HighWay graph convolutions",
+              "GCN": "2 graph convolutions + 3-layer MLP decoder",
+              "GAT": "2 four-head graph attention layers + 3-layer MLP decoder"}[model]
     return {"metric": "EA encoder training steps/s", "model": model + "-EA (encode + decode, "
-            "3 graph convolutions, fwd + bwd + gradient all-reduce)",
+            "%s, fwd + bwd + gradient all-reduce)" % layers,
             "graph": "2x%d entities, %d nnz" % (n, int(nnz)),
             "dtype": "bf16 storage, f32 arithmetic" if dtype == torch.bfloat16 else "f32",
             "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 3),
