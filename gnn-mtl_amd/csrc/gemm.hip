@@ -345,6 +345,34 @@ __global__ __launch_bounds__(256) void k_split3_planes(const float* __restrict__
   }
 }
 
+// the same planes k-block-major for k_gemm_x3p: P[p][kb][r][16] (r < NP = N rounded up to the
+// column tile, zero rows past N; kb < KP/16), so one k-step's B tile of a plane is one contiguous
+// run of 32-B rows (its DMA reads whole cache lines).  With a bias, plane row k = K holds the
+// bias split three ways (the kernel multiplies it by an A column of ones: exact, the bias joins
+// the fp32 accumulation instead of being added in the epilogue); KP >= K + 1 then.
+__global__ __launch_bounds__(256) void k_split3_planes_kb(const float* __restrict__ W, int64_t ldw,
+                                                          int trans, int n, int K, int NP, int KP,
+                                                          const float* __restrict__ bias,
+                                                          bf16_t* __restrict__ P) {
+  const int64_t total = (int64_t)NP * KP;  // per plane
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int kb = (int)(t / ((int64_t)NP * GBK));
+    const int rem = (int)(t - (int64_t)kb * NP * GBK);
+    const int r = rem / GBK, k = kb * GBK + rem % GBK;
+    float x = 0.f;
+    if (r < n) {
+      if (k < K) x = trans ? W[(int64_t)k * ldw + r] : W[(int64_t)r * ldw + k];
+      else if (k == K && bias) x = bias[r];
+    }
+    bf16_t h, m, l;
+    split3(x, h, m, l);
+    P[t] = h;
+    P[total + t] = m;
+    P[2 * total + t] = l;
+  }
+}
+
 template <int ROWS, int NT = 256>
 struct PLoader {  // ROWS x GBK of each of the three planes, 16-B chunks of 8 k
   static constexpr int NCH = 3 * ROWS * (GBK / 8);
@@ -479,6 +507,349 @@ __global__ __launch_bounds__(XNT) void k_gemm_x3(int M, int N, int K, const floa
 
   store_tiles<WT>(acc, M, N, m0 + wm * 32, n0 + wn * 32 * WT, kh, li, bias, beta, C, ldc, cs,
                   slab, split);
+}
+
+// ---- k_gemm_x3p: the projection form (A [M][K] K-contiguous fp32, B pre-split planes) with an
+// LDS-DMA pipeline, two workgroups per CU.
+// k_gemm_x3 above (one 512-thread workgroup per CU, register-staged, A split once per k-step into
+// LDS planes) measured MFMA busy ≈ 27 %: it is latency-bound — one 16-deep k-step of MFMA work
+// (≈0.8 µs per SIMD) is all that covers the next step's loads, the split + LDS-write phase runs
+// with the matrix cores idle, and the 160-KB epilogue of every 128 x 320 tile is not overlapped.
+// Here a 256-thread workgroup owns a 128 x 32*WT tile (4 waves stacked along M, each 32 rows x
+// all 32*WT columns: the same per-wave work as k_gemm_x3's 32 x 32*WT), 3-stage LDS ring of
+// ≈23 KB stages (WT = 5: the raw fp32 A tile, 128 rows x 64 B, and the three bf16 planes of the B
+// tile, 160 rows x 32 B each), ≈70 KB in all, so two workgroups share a CU (two waves per SIMD,
+// up to 256 registers each) and each one's barriers and epilogue hide under the other's MFMAs,
+// with two k-steps of DMA in flight behind the one being multiplied.  Staging is
+// global_load_lds (16 B per lane, no registers).  Each wave reads its A rows as fp32 and splits
+// them in registers (no LDS plane writes).  Counted vmcnt + raw s_barrier (no vmcnt(0) in the
+// loop); the fragment reads are inline asm, because hipcc waits vmcnt(0) before any LDS read
+// while an LDS-DMA is in flight (it cannot tell the ring's buffers apart).  LDS images are
+// lane-linear (DMA destination = base + lane * 16), so the bank swizzles go on the SOURCE
+// addresses and the same XOR on the reads: A row r's 16-B slot s at s ^ ((r >> 2) & 3), B row
+// r's 16-B half h at h ^ ((r >> 3) & 1) (16 consecutive lanes of a b128 read then hit 16
+// distinct slots).  The six products and their order are k_gemm_x3's.  A is read once per column
+// tile (2 at N = 300); the two tiles of an M block are adjacent ids, i.e. on one XCD at once.
+// Requirements (host-checked): K % 4 == 0, lda % 4 == 0, A 16-B aligned; rows >= M / N read a
+// clamped valid row (their outputs are not stored), A quads with k >= K read a valid address and
+// are zeroed in registers, the B planes are zero-padded to ldp.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const lds_void_t*)p;
+}
+__device__ __forceinline__ u32x4 ds_read128(uint32_t addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+// (a float result type, not a per-element __builtin_bit_cast of a u32x4 lane: hipcc 7.2
+// miscompiles bit_cast of an ext-vector element lvalue to element 0)
+__device__ __forceinline__ f32x4_t ds_read128f(uint32_t addr) {
+  f32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+// NW waves stacked along M (4: two workgroups per CU, 3-stage ring; 8: one per CU, 4 stages,
+// half the B-tile traffic per row of A)
+template <int WT, int NW>
+struct X3P {
+  static constexpr int BM = 32 * NW, NT = 64 * NW;
+  static constexpr int NS = NW == 8 ? 4 : 3;                    // ring stages
+  static constexpr int BN = 32 * WT;
+  static constexpr int A_CHUNKS = BM * GBK * 4 / 1024;          // 16 rows x 64 B each: 2 per wave
+  static constexpr int A_BYTES = A_CHUNKS * 1024;
+  static constexpr int PLANE_BYTES = BN * GBK * 2;              // BN rows x 32 B
+  static constexpr int B_CHUNKS = 3 * PLANE_BYTES / 1024;       // 3*WT
+  static constexpr int B_CHUNKS_PAD = (B_CHUNKS + NW - 1) / NW * NW;  // same count on every wave
+  static constexpr int DMA_BYTES = A_BYTES + B_CHUNKS_PAD * 1024;
+  static constexpr int EPI_LD = NW == 8 ? 32 : 36;               // epilogue row stride (floats)
+  static constexpr int EPI_BYTES = NW * 32 * EPI_LD * 4;         // the waves' epilogue regions
+  static constexpr int STAGE = DMA_BYTES > EPI_BYTES ? DMA_BYTES : (EPI_BYTES + 1023) / 1024 * 1024;
+  static constexpr int LOADS = A_CHUNKS / NW + B_CHUNKS_PAD / NW;  // DMA instr. / wave / stage
+  static_assert(A_CHUNKS == 2 * NW, "A: two 1-KB chunks per wave");
+};
+
+// One 32 x 32 accumulator tile of a wave, written to C with 16-B stores through a private LDS
+// region (32 rows of LD floats; LD = 36 keeps the two half-waves' rows on different banks):
+// lanes write their column, then read 4 consecutive columns of a row (8 lanes per 128-B row
+// piece).  The LDS accesses are inline asm (hipcc would wait vmcnt(0) for the ring's DMA before
+// plain ones).  vec4 (N % 4 == 0, ldc % 4 == 0, cs % 4 == 0, C 16-B aligned): EXACTLY four
+// 16-B stores per lane per tile, out-of-range lanes storing to `dummy` (the k-loop counts them in
+// its vmcnt waits); otherwise scalar stores.
+__device__ __forceinline__ void ds_write32(uint32_t addr, float v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v));
+}
+template <int LD>  // epilogue row stride in floats
+__device__ __forceinline__ void store_tile_v4(const f32x16& acc, uint32_t region, int M, int N,
+                                              int m_w, int n_t, int kh, int li, int lane,
+                                              float beta, float* __restrict__ C, int64_t ldc,
+                                              int64_t cs, bool vec4, float* __restrict__ dummy) {
+  const uint32_t wb = region + (4 * kh) * LD * 4 + li * 4;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) ds_write32(wb + ((r & 3) + 8 * (r >> 2)) * LD * 4, acc[r]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const uint32_t rbase = region + (lane >> 3) * LD * 4 + (lane & 7) * 16;
+  f32x4_t v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = ds_read128f(rbase + i * 8 * LD * 4);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (lane >> 3) + 8 * i, c4 = (lane & 7) * 4;
+    const int grow = m_w + row, gcol = n_t + c4;
+    float o[4] = {v[i][0], v[i][1], v[i][2], v[i][3]};
+    if (vec4) {
+      const bool ok = grow < M && gcol < N;
+      float* c = ok ? C + c_index(grow, gcol, ldc, cs) : dummy + 4 * lane;
+      if (beta != 0.f && ok) {
+        const float4 cc = *(const float4*)c;
+        o[0] += beta * cc.x; o[1] += beta * cc.y; o[2] += beta * cc.z; o[3] += beta * cc.w;
+      }
+      *(float4*)c = make_float4(o[0], o[1], o[2], o[3]);
+    } else if (grow < M) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (gcol + e >= N) continue;
+        float* c = C + c_index(grow, gcol + e, ldc, cs);
+        float x = o[e];
+        if (beta != 0.f) x += beta * *c;
+        *c = x;
+      }
+    }
+  }
+}
+
+// Persistent: 2 workgroups per CU, each walks tiles blockIdx.x, + gridDim.x, ... (XCD-remapped)
+// as ONE stream of k-steps, so the DMA ring runs across tile boundaries (the next tile's first
+// stages are in flight while the last ones of the current tile are multiplied) and a tile's
+// epilogue (16-B stores through LDS) is written while the next tile's stages land.
+template <int WT, int NW, int MODE = 0>  // MODE (timing experiments only): 1 = no MFMA,
+                            // 2 = no DMA, 3 = no DMA and no A split, 4 = no DMA and no epilogue stores
+__global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const float* __restrict__ A,
+                                                  int64_t lda, const bf16_t* __restrict__ Bp,
+                                                  int64_t ldp, int64_t pstride,
+                                                  const float* __restrict__ bias, float beta,
+                                                  float* __restrict__ C, int64_t ldc, int64_t cs,
+                                                  int tiles_n, int ntiles, int vec4,
+                                                  float* __restrict__ dummy) {
+  using G = X3P<WT, NW>;
+  constexpr int NS = G::NS;
+  static_assert(32 * WT * GBK * 2 % 1024 == 0, "B plane must be whole 1-KB DMA chunks");
+  static_assert(G::EPI_BYTES <= G::STAGE, "epilogue regions must fit one stage");
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * G::STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kh = lane >> 5, li = lane & 31;
+  // with a bias, A gets a column of ones at k = K (the planes hold the bias there)
+  const bool hb = bias != nullptr;
+  const int nsteps = (K + (hb ? 1 : 0) + GBK - 1) / GBK;
+  const int gsz = gridDim.x;
+  const int nq = (int)blockIdx.x < ntiles ? (ntiles - (int)blockIdx.x + gsz - 1) / gsz : 0;
+  const int total = nq * nsteps;
+  auto tile_of = [&](int q, int& m0, int& n0) {
+    const int t_id = xcd_remap((int)blockIdx.x + q * gsz, ntiles);
+    m0 = (t_id / tiles_n) * G::BM;
+    n0 = (t_id % tiles_n) * G::BN;
+  };
+
+  // ---- issue side: the next stage of the stream (tile iq, k-step is) ----
+  int iq = 0, is = 0;
+  const float* a_src[2];
+  int a_slot[2];
+  const bf16_t* b_src[G::B_CHUNKS_PAD / NW];
+  auto set_issue_tile = [&](int q) {
+    int m0, n0;
+    tile_of(q, m0, n0);
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const int ar = 16 * (w + NW * qq) + (lane >> 2);  // A row in the tile
+      a_slot[qq] = (lane & 3) ^ ((ar >> 2) & 3);       // logical 16-B slot
+      a_src[qq] = A + (int64_t)min(m0 + ar, M - 1) * lda + 4 * a_slot[qq];
+    }
+    // k-block-major planes: plane p, k-block kb, row n at ((p * KB + kb) * NP + n) * 16
+#pragma unroll
+    for (int qq = 0; qq < G::B_CHUNKS_PAD / NW; ++qq) {
+      int c = w + NW * qq;
+      if (c >= G::B_CHUNKS) c = G::B_CHUNKS - 1;  // padding chunk: any valid source
+      const int p = c / WT, r = (c % WT) * 32 + (lane >> 1);
+      const int h = (lane & 1) ^ ((r >> 3) & 1);
+      b_src[qq] = Bp + p * pstride + (int64_t)(n0 + r) * GBK + 8 * h;
+    }
+  };
+  auto issue_next = [&](int buf) {
+    if (is == 0) set_issue_tile(iq);
+    unsigned char* st = smem + buf * G::STAGE;
+    const int k0 = is * GBK;
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      // a quad past K reads a valid address (k = 0 of the row) and is zeroed at use
+      const float* ap = (k0 + 4 * a_slot[qq] < K) ? a_src[qq] + k0 : a_src[qq] - 4 * a_slot[qq];
+      // (MODE 5 timing experiment: the A stream re-reads the tile's first k-block)
+      glds16(MODE == 5 ? a_src[qq] : ap, st + (w + NW * qq) * 1024);
+    }
+#pragma unroll
+    for (int qq = 0; qq < G::B_CHUNKS_PAD / NW; ++qq)  // (MODE 6: B stream re-reads k-block 0)
+      glds16(b_src[qq] + (MODE == 6 ? 0 : (int64_t)is * ldp), st + G::A_BYTES + (w + NW * qq) * 1024);
+    if (++is == nsteps) { is = 0; ++iq; }
+  };
+
+  f32x16 acc[WT];
+#pragma unroll
+  for (int t = 0; t < WT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // per-lane LDS read offsets (bytes within a stage)
+  const int ra = w * 32 + li;
+  const int a_off0 = ra * 64 + 16 * ((2 * kh) ^ ((ra >> 2) & 3));
+  const int a_off1 = ra * 64 + 16 * ((2 * kh + 1) ^ ((ra >> 2) & 3));
+  int b_off[WT];
+#pragma unroll
+  for (int t = 0; t < WT; ++t) {
+    const int rb = t * 32 + li;
+    b_off[t] = G::A_BYTES + rb * 32 + 16 * (kh ^ ((rb >> 3) & 1));
+  }
+
+  const uint32_t smem_lds = lds_addr(smem);
+  auto epilogue = [&](int q, int buf) {
+    int m0, n0;
+    tile_of(q, m0, n0);
+    if (MODE == 4) {  // timing experiment: one store per wave keeps the accumulators live
+      float t = 0.f;
+#pragma unroll
+      for (int qq = 0; qq < WT; ++qq)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[qq][r];
+      if (t == 12345.f) C[tid] = t;
+      return;
+    }
+    const uint32_t region = smem_lds + buf * G::STAGE + w * 32 * G::EPI_LD * 4;
+#pragma unroll
+    for (int t = 0; t < WT; ++t)
+      store_tile_v4<G::EPI_LD>(acc[t], region, M, N, m0 + w * 32, n0 + 32 * t, kh, li, lane, beta, C, ldc,
+                    cs, vec4 != 0, dummy);
+  };
+  // vmcnt allowance for the first step after an epilogue: its 16-B stores (exactly 4 per tile
+  // of 32 columns when vec4 and no beta loads) were issued after the DMA that step waits for
+  const bool count_stores = vec4 != 0 && beta == 0.f && MODE != 4;
+
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < total) issue_next(i);
+  int cur = 0, s = 0, q = 0;
+  for (int g = 0; g < total; ++g) {
+    const bool epi = s == 0 && q > 0;
+    // wait for this wave's DMA of stage g; stage g + 1 stays in flight, and at the step after
+    // an epilogue also that epilogue's stores (issued between the two DMAs).  Then one barrier:
+    // every wave's stage g has landed AND every wave has finished reading buffer (g - 1) % 3
+    // (its reads were waited for before its MFMAs), which stage g + 2 then refills
+    {
+      const int later = total - 1 - g < NS - 2 ? total - 1 - g : NS - 2;  // stages issued after g
+      if (later == NS - 2 && count_stores && q > 0 && s >= 1 && s <= NS - 2) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LOADS * (NS - 2) + 4 * WT) : "memory");
+      } else if (later == NS - 2) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LOADS * (NS - 2)) : "memory");
+      } else if (later == 1) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LOADS) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int prev = cur == 0 ? NS - 1 : cur - 1;
+    if (epi) {  // the previous tile's outputs, through buffer prev, then a clean accumulator
+      epilogue(q - 1, prev);
+      __builtin_amdgcn_s_barrier();  // every wave's epilogue reads of prev are done
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int t = 0; t < WT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    }
+    if (MODE < 2 && g + NS - 1 < total) issue_next(prev);
+    const uint32_t st = smem_lds + cur * G::STAGE;
+    const f32x4_t x0 = ds_read128f(st + a_off0);
+    const f32x4_t x1 = ds_read128f(st + a_off1);
+    u32x4 braw[3 * WT];
+#pragma unroll
+    for (int t = 0; t < WT; ++t) {
+      braw[3 * t] = ds_read128(st + b_off[t]);
+      braw[3 * t + 1] = ds_read128(st + b_off[t] + G::PLANE_BYTES);
+      braw[3 * t + 2] = ds_read128(st + b_off[t] + 2 * G::PLANE_BYTES);
+    }
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(3 * WT) : "memory");  // the two A reads
+    __builtin_amdgcn_sched_barrier(0);
+    float xa[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      xa[j] = x0[j];
+      xa[4 + j] = x1[j];
+    }
+    const int kval = K - (s * GBK + 8 * kh);  // valid k of this lane's 8
+    if (kval < 8) {  // past K: zeros, and the column of ones at k = K under a bias
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j >= kval) xa[j] = (hb && j == kval) ? 1.f : 0.f;
+    }
+    bf16x8_t ah, am, al;
+    if (MODE == 3) {
+      ah = __builtin_bit_cast(bf16x8_t, x0);
+      am = __builtin_bit_cast(bf16x8_t, x1);
+      al = ah;
+    } else
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bf16_t h, m, l;
+      split3(xa[j], h, m, l);
+      ah[j] = __builtin_bit_cast(__bf16, h);
+      am[j] = __builtin_bit_cast(__bf16, m);
+      al[j] = __builtin_bit_cast(__bf16, l);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8_t bh[WT], bm_[WT], bl[WT];
+#pragma unroll
+    for (int t = 0; t < WT; ++t) {
+      bh[t] = __builtin_bit_cast(bf16x8_t, braw[3 * t]);
+      bm_[t] = __builtin_bit_cast(bf16x8_t, braw[3 * t + 1]);
+      bl[t] = __builtin_bit_cast(bf16x8_t, braw[3 * t + 2]);
+    }
+    if (MODE == 1) {  // timing experiment: keep the data live, skip the matrix cores
+#pragma unroll
+      for (int t = 0; t < WT; ++t)
+        acc[t][0] += (float)(ah[0] + am[1] + al[2] + bh[t][0] + bm_[t][1] + bl[t][2]);
+    } else {
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm_[t], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[t], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm_[t], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t], acc[t], 0, 0, 0);
+    }
+    cur = cur == NS - 1 ? 0 : cur + 1;
+    if (++s == nsteps) { s = 0; ++q; }
+  }
+  if (total > 0) {  // the last tile: every DMA has landed (vmcnt(0) at the last step)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    epilogue(q - 1, 0);
+  }
 }
 
 // slab reduction in fixed split order (deterministic); 4 outputs per thread when the rows allow
@@ -649,9 +1020,12 @@ extern "C" int gnnea_gemm_sliced_f32(int trans_a, int trans_b, int64_t M, int64_
 // ---- fp32 GEMM through three-way bf16 splits (k_gemm_x3) -----------------------------------
 // op(A) must be K-contiguous (trans_a = 0: the tall operand of the projections); a transposed A
 // (the weight gradients dW = dYᵀ·x, both operands tall) runs on the f32 MFMA kernel instead.
+// planes for either kernel (k_gemm_x3p: rows padded to its column tile, one more k for the
+// bias row) + a 1-KB dummy store target for k_gemm_x3p's out-of-range lanes
 static int64_t x3_planes_bytes(int64_t N, int64_t K) {
-  const int64_t ldp = (K + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign;
-  return (3 * N * ldp * 2 + 255) & ~(int64_t)255;
+  const int64_t kp = (K + 1 + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign;
+  const int64_t np = (N + 159) / 160 * 160;  // k_gemm_x3p's padded rows (>= N)
+  return ((3 * np * kp * 2 + 255) & ~(int64_t)255) + 1024;
 }
 
 static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
@@ -679,13 +1053,93 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
   const int ldp = (int)((K + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign);
   const int64_t pstride = N * ldp;
   bf16_t* planes = (bf16_t*)ws;
-  {
+  const bool vec = lda % 4 == 0 && K % 4 == 0 && al16(A);
+  const int splits = pick_splits(M, N, K, ws_bytes - pbytes);
+  static const bool pipe = [] {
+    const char* e = getenv("GNNEA_X3_PIPE");  // A/B comparison only
+    return !(e && e[0] == '0');
+  }();
+  if (!(pipe && vec && splits == 1)) {
     const int64_t tot = N * ldp;
     const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
     // B op-form [N][K]: trans_b = 1 means B is stored [N][K] (no transpose needed)
     hipLaunchKernelGGL(k_split3_planes, dim3(nb), dim3(256), 0, s, B, ldb, trans_b ? 0 : 1,
                        (int)N, (int)K, ldp, planes, pstride);
     GNNEA_LAUNCH_CHECK();
+  }
+  if (pipe && vec && splits == 1) {  // k_gemm_x3p: LDS-DMA pipeline, two workgroups per CU
+    // 32*WT-column tiles, WT <= 5 (N = 300: two 160-column tiles)
+    int wtp = (int)((N + 31) / 32 < 5 ? (N + 31) / 32 : 5);
+    if (const char* e = getenv("GNNEA_X3_WT")) {  // tuning override only
+      const int v = atoi(e);
+      if (v >= 1 && v <= 5) wtp = v;
+    }
+    const int tn = (int)((N + 32 * wtp - 1) / (32 * wtp));
+    const int np = tn * 32 * wtp;  // <= the 160-row rounding x3_planes_bytes reserves
+    const int kp = (int)((K + (bias ? 1 : 0) + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign);
+    float* dummy = (float*)((char*)ws + pbytes - 1024);
+    {
+      const int64_t tot = (int64_t)np * kp;
+      const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
+      hipLaunchKernelGGL(k_split3_planes_kb, dim3(nb), dim3(256), 0, s, B, ldb, trans_b ? 0 : 1,
+                         (int)N, (int)K, np, kp, bias, planes);
+      GNNEA_LAUNCH_CHECK();
+    }
+    // 8 waves (256-row tiles, one workgroup per CU) for tall operands, else 4 (128 rows, two)
+    int nw = M >= 65536 ? 8 : 4;
+    if (const char* e = getenv("GNNEA_X3P_NW")) {  // tuning override only
+      const int v = atoi(e);
+      if (v == 4 || v == 8) nw = v;
+    }
+    const int64_t tm = (M + 32 * nw - 1) / (32 * nw);
+    if (tm * tn >= (1ll << 31)) return GNNEA_EINVAL;
+    const int ntiles = (int)(tm * tn);
+    static const int ncu = [] {
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+      return n;
+    }();
+    const int per_cu = nw == 8 ? 1 : 2;  // persistent: as many workgroups as fit at once
+    const dim3 grid((unsigned)(ntiles < per_cu * ncu ? ntiles : per_cu * ncu));
+    const int vec4 = N % 4 == 0 && ldc % 4 == 0 && cs % 4 == 0 && al16(C);
+    static const int mode = [] {  // timing experiments only (GNNEA_X3P_MODE=1..4, WT = 5)
+      const char* e = getenv("GNNEA_X3P_MODE");
+      return e ? atoi(e) : 0;
+    }();
+#define GNNEA_X3P_L(W, NWV, MD)                                                                  \
+  hipLaunchKernelGGL((k_gemm_x3p<W, NWV, MD>), grid, dim3(64 * NWV), 0, s, (int)M, (int)N,       \
+                     (int)K, A, lda, planes, (int64_t)np * GBK, (int64_t)np * kp, bias, beta, C, \
+                     ldc, cs, tn, ntiles, vec4, dummy)
+#define GNNEA_X3P(W)                                                                             \
+  case W:                                                                                        \
+    if (nw == 8) {                                                                               \
+      if (W == 5 && mode == 1) GNNEA_X3P_L(W, 8, 1);                                             \
+      else if (W == 5 && mode == 2) GNNEA_X3P_L(W, 8, 2);                                        \
+      else if (W == 5 && mode == 4) GNNEA_X3P_L(W, 8, 4);                                        \
+      else GNNEA_X3P_L(W, 8, 0);                                                                 \
+    } else {                                                                                     \
+      if (W == 5 && mode == 1) GNNEA_X3P_L(W, 4, 1);                                             \
+      else if (W == 5 && mode == 5) GNNEA_X3P_L(W, 4, 5);                                        \
+      else if (W == 5 && mode == 6) GNNEA_X3P_L(W, 4, 6);                                        \
+      else if (W == 5 && mode == 2) GNNEA_X3P_L(W, 4, 2);                                        \
+      else if (W == 5 && mode == 4) GNNEA_X3P_L(W, 4, 4);                                        \
+      else GNNEA_X3P_L(W, 4, 0);                                                                 \
+    }                                                                                            \
+    break;
+    switch (wtp) {
+      GNNEA_X3P(1)
+      GNNEA_X3P(2)
+      GNNEA_X3P(3)
+      GNNEA_X3P(4)
+      default:
+      GNNEA_X3P(5)
+    }
+#undef GNNEA_X3P
+#undef GNNEA_X3P_L
+    GNNEA_LAUNCH_CHECK();
+    return 0;
   }
   // wider than one 320-column tile: 128-column tiles (WT = 2, the finer work split) measured
   // faster than 2 x 320 (2M x 600 x 300: 5.76 vs 6.05 ms; 30k rows: 0.109 vs 0.118 ms)
@@ -697,10 +1151,8 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
   const int64_t bn = 64 * wt;
   const int tiles_n = (int)((N + bn - 1) / bn);
   const int tiles = (int)(((M + XBM - 1) / XBM) * tiles_n);
-  const int splits = pick_splits(M, N, K, ws_bytes - pbytes);
   const int kps = (int)(((K + splits - 1) / splits + GBK - 1) / GBK * GBK);
   float* slab = splits > 1 ? (float*)((char*)ws + pbytes) : nullptr;
-  const bool vec = lda % 4 == 0 && K % 4 == 0 && al16(A);
   const dim3 grid(tiles, splits);
 #define GNNEA_X3(W)                                                                              \
   case W:                                                                                        \

@@ -232,7 +232,7 @@ def test_gat_fwd_bwd_vs_oracle(device, heads, d, hub):
 
 
 @pytest.mark.parametrize("shape", [(1, 1, 1), (37, 300, 300), (300, 75, 300), (513, 600, 300),
-                                   (300, 300, 20000), (5, 300, 7)])
+                                   (300, 300, 20000), (5, 300, 7), (70, 40, 12), (129, 321, 36)])
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 def test_gemm_vs_fp64(device, shape, ta, tb):
     from gnnea import ops

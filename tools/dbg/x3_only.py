@@ -1,4 +1,5 @@
-"""Run the x3 projection GEMM (cfg-4 shape) a few times: a short program for rocprofv3 --pmc."""
+"""Run the x3 projection GEMM (cfg-4 shape) a few times: a short program for rocprofv3 --pmc.
+GNNEA_X3_PIPE=0 selects the register-staged k_gemm_x3 instead of k_gemm_x3p."""
 import os
 import sys
 import torch
@@ -11,6 +12,5 @@ X = torch.randn(2000000, 300, device=dev)
 W = torch.randn(300, 300, device=dev)
 for _ in range(3):
     ops.gemm(X, W, trans_b=True, x3=True)
-    ops.gemm(X, W, trans_b=True, x3=False)
 torch.cuda.synchronize()
 print("done")
