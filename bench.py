@@ -80,7 +80,7 @@ def compulsory_bytes(n_rows, n_cols, nnz, d, sliced, elem=4, slice_w=64):
     return passes * (4 * (n_rows + 1) + 8 * nnz) + elem * n_cols * dt + elem * n_rows * d
 
 
-def sinkhorn_rate(device, B=3000, reg=0.01):
+def sinkhorn_rate(device, B=3000, reg=0.01, n0=100, n1=1100, variant=None):
     """Marginal iters/s of utils/ot_loss.sinkhorn and SinkhornOT sinkhorn_iteration at B x B."""
     from gnnea.sinkhorn import solve
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -91,24 +91,56 @@ def sinkhorn_rate(device, B=3000, reg=0.01):
     out = {}
     # ot_loss.sinkhorn as models_ea.py:217 calls it (a = b = ones); sinkhorn_iteration with the
     # uniform marginals mu = nu = 1/B
-    for name, mode, w, n0, n1 in (("ot_loss.sinkhorn", _lib.GNNEA_SK_KNOPP, 1.0, 100, 1100),
-                                  ("sinkhorn_iteration", _lib.GNNEA_SK_STAB, 1.0 / B, 100, 1100)):
+    for name, mode, w in (("ot_loss.sinkhorn", _lib.GNNEA_SK_KNOPP, 1.0),
+                          ("sinkhorn_iteration", _lib.GNNEA_SK_STAB, 1.0 / B)):
         la_m = torch.full((B,), w, dtype=torch.float64, device=device)
         lb = la_m
         C = M if mode == _lib.GNNEA_SK_KNOPP else M.double()
         ts = []
         for n_it in (n0, n1):
             # tol = -1: never converges, so exactly n_it iterations run
-            solve(mode, C, la_m, lb, reg, -1.0, n_it, want_plan=False, batch=100)  # warm
+            solve(mode, C, la_m, lb, reg, -1.0, n_it, want_plan=False, batch=100,
+                  variant=variant)  # warm
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            res = solve(mode, C, la_m, lb, reg, -1.0, n_it, want_plan=False, batch=100)
+            res = solve(mode, C, la_m, lb, reg, -1.0, n_it, want_plan=False, batch=100,
+                        variant=variant)
             assert res.iters == n_it, (name, res.iters, n_it)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         out[name] = round((n1 - n0) / (ts[1] - ts[0]), 1)
     return {"iters_per_s": out, "B": B, "reg": reg, "dtype": "f64 (C fp32/fp64)",
-            "method": "marginal (T(1100)-T(100))/1000 incl. host batch syncs"}
+            "method": "marginal (T(%d)-T(%d))/%d incl. host batch syncs" % (n1, n0, n1 - n0)}
+
+
+def sinkhorn_large(device):
+    """B = 15000 (J > 8192: the fused log-domain passes, nothing I x J kept): marginal iters/s
+    and the bandwidth of the C stream (fp32 C read twice per iteration: the row pass and the
+    column pass, 2 * I * J * 4 bytes)."""
+    r = sinkhorn_rate(device, B=15000, n0=20, n1=120)
+    B = 15000
+    per_it = 2 * B * B * 4
+    r["bytes_per_iter"] = per_it
+    r["GBps_knopp"] = round(r["iters_per_s"]["ot_loss.sinkhorn"] * per_it / 1e9, 1)
+    r["bound"] = ("fp64 exp (VALU): 2 * I * J exponentials per iteration; the C stream alone "
+                  "would allow %.0f iters/s at 8 TB/s" % (8e12 / per_it))
+    return r
+
+
+def gw_rate(device, B=3000):
+    """One GW outer-iteration cost rebuild (SinkhornOT/cderivation.py:160-162, get_LT:
+    constC - C1 . T . C2^T) in fp64 on the f64 MFMA GEMM, 2 * I * J * (I + J) flops."""
+    from SinkhornOT.cderivation import get_LT
+    g = torch.Generator(device="cpu").manual_seed(0)
+    C1 = torch.rand(B, B, generator=g, dtype=torch.float64).to(device)
+    C2 = torch.rand(B, B, generator=g, dtype=torch.float64).to(device)
+    T = torch.full((B, B), 1.0 / (B * B), dtype=torch.float64, device=device)
+    constC = torch.rand(B, B, generator=g, dtype=torch.float64).to(device)
+    ms = _timed(lambda: get_LT(constC, C1, C2, T), 5)
+    flop = 2.0 * B * B * (B + B)
+    return {"ms": round(ms, 3), "TFLOPs": round(flop / ms / 1e9, 1), "I": B, "J": B,
+            "dtype": "f64", "kernel": "gnnea::k_gemm_f64 (v_mfma_f64_16x16x4_f64), 2 launches",
+            "peak_TFLOPs": 78.6, "peak_source": "AMD MI355X spec FP64 matrix (not in MI355X_MICROARCH.md)"}
 
 
 def bf16_rate(shard, H, steps):
@@ -468,6 +500,14 @@ def main():
                 line["sinkhorn"] = sinkhorn_rate(device)
             except Exception as e:  # report, never hide
                 line["sinkhorn"] = {"error": repr(e)}
+            try:
+                line["sinkhorn_B15000"] = sinkhorn_large(device)
+            except Exception as e:  # report, never hide
+                line["sinkhorn_B15000"] = {"error": repr(e)}
+            try:
+                line["gw_cost"] = gw_rate(device)
+            except Exception as e:  # report, never hide
+                line["gw_cost"] = {"error": repr(e)}
         if world == 1 and not args.headline_only:
             try:
                 line["bf16"] = bf16_rate(shard, h_local, args.steps)

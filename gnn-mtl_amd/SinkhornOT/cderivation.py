@@ -1,14 +1,20 @@
 """Cost-matrix algebra of the GW / FGW outer loops (drop-in for SinkhornOT/cderivation.py, §8f #3).
 
-Everything here is dense linear algebra on device tensors: the two products of get_LT
-(C1 · T · C2^T, 2·I·J·(I+J) flops per outer iteration) go to the library GEMM (hipBLASLt through
-torch.mm), elementwise work stays in torch.  The Sinkhorn inner solves that consume these costs
-run on the gnnea kernels (SinkhornOT/sinkhorn_loss.py).  Distance helpers outside the GW path
+Everything here is dense linear algebra on device tensors.  The two products of get_LT
+(C1 · T · C2^T, 2·I·J·(I+J) flops per outer iteration) run on gnnea's own matrix-core GEMMs:
+fp64 (the reference path's dtype) on the f64 MFMA kernel gnnea_gemm_f64 with the subtraction
+from constC fused into the second product's epilogue (L = constC - C1·X in one launch), fp32 /
+bf16 on gnnea.ops.gemm.  get_init_matrices' two products are matrix-vector products in
+disguise (every column of C1²·repeat(mu) is C1²·mu): they run as [I, 1] / [J, 1] GEMMs and
+constC is their broadcast sum.  Elementwise work stays in torch.  The Sinkhorn inner solves
+that consume these costs run on the gnnea kernels (SinkhornOT/sinkhorn_loss.py).  Distance helpers outside the GW path
 (energy distances, ...) are taken from the reference module when GNNEA_UPSTREAM names its checkout.
 """
 import math
 
 import torch
+
+from gnnea import _lib, ops
 
 big = 1e20
 huge = 1e30
@@ -50,21 +56,38 @@ def get_inter_sim(x, y, sim_func):
     return sim_func(x.detach(), y.detach())
 
 
+def _mm(a, b, trans_b=False):
+    """a @ op(b) on the device GEMMs (fp64: gnnea_gemm_f64; fp32 / bf16: gnnea.ops.gemm)."""
+    _lib.require_device(a, b)
+    if a.dtype == torch.float64 or b.dtype == torch.float64:
+        return ops.gemm_f64(a.double(), b.double(), trans_b=trans_b)
+    return ops.gemm(a, b, trans_b=trans_b, out_dtype=torch.float32).to(a.dtype)
+
+
 def get_init_matrices(C1, C2, mu, nu, div_type="l2"):
     """cderivation.py:146-157: the T-independent part of the square-loss GW cost,
-    constC_ij = 1/2 sum_k C1_ik^2 mu_k + 1/2 sum_l nu_l C2_jl^2 (each term a matrix product, as
-    the reference forms them), and hC1 = C1, hC2 = C2."""
+    constC_ij = 1/2 sum_k C1_ik^2 mu_k + 1/2 sum_l nu_l C2_jl^2, and hC1 = C1, hC2 = C2.
+    The reference forms both terms as [I, J] matrix products of repeated vectors; each is one
+    [I, 1] / [J, 1] product here (the same exact products, summed in k order)."""
     I, J = C1.shape[0], C2.shape[0]
-    mu_col = mu.reshape(I, 1)
-    nu_row = nu.reshape(1, J)
-    A = 0.5 * torch.matmul(C1 ** 2, mu_col.repeat(1, J))
-    B = 0.5 * torch.matmul(nu_row.repeat(I, 1), C2.t() ** 2)
-    return A + B, C1, C2
+    a = _mm(C1 ** 2, mu.reshape(I, 1).to(C1.dtype))
+    b = _mm(C2 ** 2, nu.reshape(J, 1).to(C2.dtype))
+    return 0.5 * a + 0.5 * b.reshape(1, J), C1, C2
 
 
 def get_LT(constC, hC1, hC2, T):
-    """cderivation.py:160-162: L(C1, C2) (x) T = constC - C1 · T · C2^T."""
-    return constC - torch.matmul(hC1, torch.matmul(T, hC2.t()))
+    """cderivation.py:160-162: L(C1, C2) (x) T = constC - C1 · (T · C2^T); in fp64 the
+    subtraction is the second GEMM's epilogue (alpha = -1, beta = 1, E = constC)."""
+    _lib.require_device(constC, hC1, hC2, T)
+    if T.dim() > 2:  # a batch of plans (the Sinkhorn solvers return [bt, I, J]): as matmul
+        lead = T.shape[:-2]
+        Ts = T.reshape(-1, *T.shape[-2:])
+        return torch.stack([get_LT(constC, hC1, hC2, t) for t in Ts]).reshape(
+            *lead, *Ts.shape[-2:])
+    if T.dtype == torch.float64:
+        X = ops.gemm_f64(T, hC2.double(), trans_b=True)
+        return ops.gemm_f64(hC1.double(), X, alpha=-1.0, e=constC.double(), beta=1.0)
+    return constC - _mm(hC1, _mm(T, hC2, trans_b=True))
 
 
 def w2_cost_matrix(D, device):

@@ -3,13 +3,14 @@
 ``sinkhorn_iteration`` / ``gsinkhorn_iteration`` / ``forward_relax_sinkhorn_iteration`` keep
 the reference signatures and return ``(transport, margin1, margin2, K)``.  The scaling-with-
 absorption loop runs on the device in the reference's own form (fp64 K resident in HBM,
-absorption schedule, 1e30 clamps, 1e20 trigger, relative-tolerance break).  The batch dimension
-is solved one problem at a time.
+absorption schedule, 1e30 clamps, 1e20 trigger, relative-tolerance break).  A batch [bt, I, J]
+runs as one launch sequence (gnnea.sinkhorn.solve_batch: every problem's iterations enqueued
+round by round on one stream, one status read-back per round for the whole batch).
 """
 import torch
 
 from gnnea import _lib
-from gnnea.sinkhorn import solve
+from gnnea.sinkhorn import solve_batch
 
 big = 1e20
 huge = 1e30
@@ -38,23 +39,24 @@ def _run(mode, C, mu, nu, epsilon, numIterMax, tol, lambdda, debug, out_dtype, p
     _lib.require_device(C)
     p = lambdda / (lambdda + epsilon) if mode != _lib.GNNEA_SK_STAB else 1.0
     Cb = C.reshape(-1, I, J)
-    mub = mu.reshape(-1, I)
-    nub = nu.reshape(-1, J)
+    bt = Cb.shape[0]
+    mub = mu.reshape(-1, I).double()
+    nub = nu.reshape(-1, J).double()
+    mub = mub.expand(bt, I) if mub.shape[0] == 1 else mub
+    nub = nub.expand(bt, J) if nub.shape[0] == 1 else nub
+    if Cb.dtype not in (torch.float32, torch.float64):
+        Cb = Cb.to(out_dtype)
+    res = solve_batch(mode, Cb, mub, nub, epsilon, tol, numIterMax, p=p,
+                      plan_dtype=torch.float64)
     Ks, trans, m1, m2 = [], [], [], []
-    for k in range(Cb.shape[0]):
-        c = Cb[k]
-        if c.dtype not in (torch.float32, torch.float64):
-            c = c.to(out_dtype)
-        res = solve(mode, c, mub[k % mub.shape[0]].double(),
-                    nub[k % nub.shape[0]].double(), epsilon, tol, numIterMax, p=p,
-                    plan_dtype=torch.float64)
-        K = res.plan
+    for k, r in enumerate(res):
+        K = r.plan
         if debug:
             assert not torch.isnan(K).any()
-        t = res.transport_prev if prev_transport else res.transport_new
+        t = r.transport_prev if prev_transport else r.transport_new
         trans.append(torch.tensor(t, dtype=torch.float64, device=C.device))
-        m1.append(kl_div(res.row_sum, mub[k % mub.shape[0]].double()).sum())
-        m2.append(kl_div(res.col_sum, nub[k % nub.shape[0]].double()).sum())
+        m1.append(kl_div(r.row_sum, mub[k]).sum())
+        m2.append(kl_div(r.col_sum, nub[k]).sum())
         Ks.append(K)
     K = torch.stack(Ks).reshape(*lead, I, J).to(out_dtype)
     squeeze = lambda v: torch.stack(v).to(out_dtype).squeeze()  # noqa: E731

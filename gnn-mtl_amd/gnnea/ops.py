@@ -192,6 +192,42 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
     return out
 
 
+def _rows64(t):
+    if t.dim() == 2 and t.stride(1) == 1 and (t.shape[0] <= 1 or t.stride(0) >= t.shape[1]):
+        return t
+    return t.contiguous()
+
+
+def gemm_f64(a, b, trans_a=False, trans_b=False, alpha=1.0, e=None, beta=0.0, out=None):
+    """out = alpha * op(a) @ op(b) + beta * e, fp64 on the f64 matrix cores (gnnea_gemm_f64; the
+    GW / FGW products of SinkhornOT/cderivation.py).  ``e`` may be ``out``."""
+    _lib.require_device(a, b)
+    if a.dtype != torch.float64 or b.dtype != torch.float64:
+        raise TypeError("gnnea.gemm_f64: fp64 tensors required (got %s, %s)" % (a.dtype, b.dtype))
+    a = _rows64(a)
+    b = _rows64(b)
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    Kb = b.shape[1] if trans_b else b.shape[0]
+    N = b.shape[0] if trans_b else b.shape[1]
+    if K != Kb:
+        raise ValueError("gnnea.gemm_f64: inner dimensions differ (%d vs %d)" % (K, Kb))
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float64, device=a.device)
+    if out.shape != (M, N) or out.dtype != torch.float64 or out.stride(1) != 1:
+        raise ValueError("gnnea.gemm_f64: out must be a row-major fp64 [M, N] tensor")
+    if e is not None:
+        if e.shape != (M, N) or e.dtype != torch.float64:
+            raise ValueError("gnnea.gemm_f64: e must be fp64 [M, N]")
+        e = _rows64(e)
+    L = _lib.lib()
+    with _lib.on_device(a.device):
+        check(L.gnnea_gemm_f64(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a), ptr(b),
+                               _ld(b), float(alpha), ptr(e), _ld(e) if e is not None else 0,
+                               float(beta), ptr(out), _ld(out), stream_of(a.device)))
+    return out
+
+
 class LinearFn(torch.autograd.Function):
     """y = x W^T + b  (nn.Linear.forward at layers/layers.py:32,61,93) on MFMA."""
 

@@ -109,3 +109,76 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
     return SinkhornResult(plan, row_sum, col_sum, int(ints[ST_ITERS]), int(ints[ST_REASON]),
                           float(dbl[SD_ERR]), float(dbl[SD_TNEW]), float(dbl[SD_TPREV]),
                           float(dbl[SD_LOSS]))
+
+
+def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64, batch=10,
+                variant=None):
+    """Solve a batch of problems of one shape [bt, I, J] as ONE launch sequence: every problem's
+    iterations are enqueued batch by batch on the same stream and ONE device->host copy of all
+    status blocks per round decides which problems continue (solve() polls once per problem
+    per round).  Cs [bt, I, J], As [bt, I], Bs [bt, J] on the device; returns SinkhornResults."""
+    _lib.require_device(Cs, As, Bs)
+    if variant is None:
+        variant = DEFAULT_VARIANT
+    bt, I, J = Cs.shape
+    if Cs.dtype not in (torch.float32, torch.float64):
+        Cs = Cs.double()
+    dev = Cs.device
+    L = _lib.lib()
+    ws_bytes = int(L.gnnea_sinkhorn_ws_bytes(I, J))
+    if ws_bytes < 0:
+        check(ws_bytes)
+    stride = (ws_bytes + 255) // 256 * 256
+    ws = torch.empty(bt * stride, dtype=torch.uint8, device=dev)
+    wa = As.reshape(bt, I).to(torch.float64).contiguous()
+    wb = Bs.reshape(bt, J).to(torch.float64).contiguous()
+    probs = []
+    for k in range(bt):
+        C = Cs[k] if Cs[k].stride(1) == 1 else Cs[k].contiguous()
+        probs.append((C, SinkhornProblem(
+            mode=mode, c_dtype=_lib.GNNEA_F32 if C.dtype == torch.float32 else _lib.GNNEA_F64,
+            I=I, J=J, ldc=C.stride(0), C=C.data_ptr(), a=wa[k].data_ptr(), b=wb[k].data_ptr(),
+            eps=float(eps), p=float(p), tol=float(tol), max_iter=int(max_iter), iters_run=0,
+            variant=int(variant), reserved=0, ws=ws[k * stride:].data_ptr())))
+    st = stream_of(dev)
+    status = ws.view(bt, stride)[:, :_lib.GNNEA_SK_STATUS_BYTES]
+    results = []
+    with _lib.on_device(dev):
+        for _, pr in probs:
+            check(L.gnnea_sinkhorn_init(ctypes.byref(pr), st))
+        run = 0
+        live = list(range(bt))
+        knopp = mode == _lib.GNNEA_SK_KNOPP
+        if knopp and not (1.0 > tol and max_iter > 0):
+            live = []
+        step, hi = (10, 2) if knopp else (max(1, batch), max(1, batch))
+        while live and run < max_iter:
+            hi = min(hi, max_iter)
+            for k in live:
+                check(L.gnnea_sinkhorn_iterate(ctypes.byref(probs[k][1]), run, hi - run, st))
+            for k in live:
+                probs[k][1].iters_run = hi
+            run = hi
+            done = status[:, :8].contiguous().view(torch.int64)[:, ST_DONE].cpu()  # one sync
+            live = [k for k in live if not int(done[k])]
+            hi = run + step
+            step = min(2 * step, MAX_BATCH)
+        for k, (C, pr) in enumerate(probs):
+            pr.iters_run = max(pr.iters_run, 0)
+            plan = torch.empty((I, J), dtype=plan_dtype, device=dev)
+            row_sum = torch.empty(I, dtype=torch.float64, device=dev)
+            col_sum = torch.empty(J, dtype=torch.float64, device=dev)
+            check(L.gnnea_sinkhorn_finish(
+                ctypes.byref(pr), ptr(plan),
+                _lib.GNNEA_F32 if plan_dtype == torch.float32 else _lib.GNNEA_F64, J,
+                ptr(row_sum), ptr(col_sum), st))
+            results.append((plan, row_sum, col_sum))
+        raw = status.contiguous().cpu()
+    out = []
+    for k, (plan, row_sum, col_sum) in enumerate(results):
+        ints = raw[k].view(torch.int64)
+        dbl = raw[k].view(torch.float64)
+        out.append(SinkhornResult(plan, row_sum, col_sum, int(ints[ST_ITERS]),
+                                  int(ints[ST_REASON]), float(dbl[SD_ERR]), float(dbl[SD_TNEW]),
+                                  float(dbl[SD_TPREV]), float(dbl[SD_LOSS])))
+    return out

@@ -284,6 +284,15 @@ int gnnea_gemm_sliced_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_
                           const float* bias, float beta, float* Cs, int64_t sstride, void* ws,
                           int64_t ws_bytes, void* stream);
 
+/* fp64 GEMM on the f64 matrix cores (v_mfma_f64_16x16x4_f64) for the GW / FGW outer loops
+ * (SinkhornOT/cderivation.py:146-188: C1 · T · C2ᵀ and the constC products):
+ *   D[M,N] = alpha · op(A)[M,K] · op(B)[K,N] + beta · E[M,N]   (E nullable, may alias D)
+ * Row-major, leading dimensions in elements, caller's stream, no workspace.
+ * Replaces torch.matmul at cderivation.py:150-151,161. */
+int gnnea_gemm_f64(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const double* A,
+                   int64_t lda, const double* B, int64_t ldb, double alpha, const double* E,
+                   int64_t lde, double beta, double* D, int64_t ldd, void* stream);
+
 /* bf16 operands (cfg-5 storage), v_mfma_f32_32x32x16_bf16: A, B bf16 (void*), fp32 accumulate,
  * bias fp32 (nullable), C bf16 (c_dtype GNNEA_BF16, rounded once, nearest even) or fp32
  * (GNNEA_F32).  Workspace (split-K slabs) from gnnea_gemm_bf16_ws_bytes; NULL = no split.

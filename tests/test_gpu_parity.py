@@ -555,3 +555,45 @@ def test_spmm_block_diagonal_launches(device, monkeypatch):
     csr2 = DeviceCSR.from_coo(torch.from_numpy(r2).to(device), torch.from_numpy(c2).to(device),
                               torch.from_numpy(v2).to(device), 2 * n, 2 * n)
     assert csr2.row_blocks() == [(0, 2 * n)]
+
+
+@pytest.mark.parametrize("mode_name", ["STAB", "RELAX", "KNOPP"])
+def test_sinkhorn_batch_one_launch_sequence(device, mode_name):
+    """gnnea.sinkhorn.solve_batch ([bt, I, J] as one launch sequence, one status read-back per
+    round) equals solving each problem alone with solve(): same kernels, same stops."""
+    from gnnea import _lib
+    from gnnea.sinkhorn import solve, solve_batch
+    mode = getattr(_lib, "GNNEA_SK_" + mode_name)
+    g = torch.Generator().manual_seed(7)
+    bt, I, J = 3, 70, 90
+    C = torch.rand(bt, I, J, generator=g, dtype=torch.float64).to(device)
+    C[1] *= 4.0  # different conditioning: the problems stop at different iterations
+    a = torch.full((bt, I), 1.0 / I, dtype=torch.float64, device=device)
+    b = torch.full((bt, J), 1.0 / J, dtype=torch.float64, device=device)
+    eps, tol, it = (0.05, 1e-9, 200)
+    p = 0.8 if mode_name == "RELAX" else 1.0
+    res = solve_batch(mode, C, a, b, eps, tol, it, p=p)
+    for k in range(bt):
+        r1 = solve(mode, C[k], a[k], b[k], eps, tol, it, p=p)
+        assert res[k].iters == r1.iters and res[k].reason == r1.reason
+        assert torch.equal(res[k].plan, r1.plan)
+        assert res[k].transport_new == r1.transport_new or mode_name == "KNOPP"
+        assert res[k].loss == r1.loss or mode_name != "KNOPP"
+
+
+def test_gemm_f64_vs_numpy(device):
+    """gnnea_gemm_f64 (f64 MFMA) in all transpose forms with the fused alpha / beta * E epilogue
+    (the GW products of SinkhornOT/cderivation.py:146-162) vs numpy fp64."""
+    from gnnea import ops
+    rng = np.random.default_rng(5)
+    for (M, N, K) in [(1, 1, 1), (70, 90, 33), (128, 64, 300), (257, 130, 129)]:
+        for ta in (0, 1):
+            for tb in (0, 1):
+                a = rng.standard_normal((K, M) if ta else (M, K))
+                b = rng.standard_normal((N, K) if tb else (K, N))
+                e = rng.standard_normal((M, N))
+                out = ops.gemm_f64(torch.from_numpy(a).to(device), torch.from_numpy(b).to(device),
+                                   bool(ta), bool(tb), alpha=-1.0,
+                                   e=torch.from_numpy(e).to(device), beta=1.0).cpu().numpy()
+                ref = e - (a.T if ta else a) @ (b.T if tb else b)
+                assert rel_err(out, ref) < 1e-14, (M, N, K, ta, tb)
