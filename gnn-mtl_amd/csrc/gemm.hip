@@ -591,7 +591,8 @@ template <int LD>  // epilogue row stride in floats
 __device__ __forceinline__ void store_tile_v4(const f32x16& acc, uint32_t region, int M, int N,
                                               int m_w, int n_t, int kh, int li, int lane,
                                               float beta, float* __restrict__ C, int64_t ldc,
-                                              int64_t cs, bool vec4, float* __restrict__ dummy) {
+                                              int64_t cs, bool vec4, float* __restrict__ dummy,
+                                              float* __restrict__ C2, int64_t cs2) {
   const uint32_t wb = region + (4 * kh) * LD * 4 + li * 4;
 #pragma unroll
   for (int r = 0; r < 16; ++r) ds_write32(wb + ((r & 3) + 8 * (r >> 2)) * LD * 4, acc[r]);
@@ -615,6 +616,10 @@ __device__ __forceinline__ void store_tile_v4(const f32x16& acc, uint32_t region
         o[0] += beta * cc.x; o[1] += beta * cc.y; o[2] += beta * cc.z; o[3] += beta * cc.w;
       }
       *(float4*)c = make_float4(o[0], o[1], o[2], o[3]);
+      if (C2) {  // the slice-major copy [ceil(N/64)][M][64] (exactly one more store per i)
+        float* c2 = ok ? C2 + c_index(grow, gcol, 64, cs2) : dummy + 4 * lane;
+        *(float4*)c2 = make_float4(o[0], o[1], o[2], o[3]);
+      }
     } else if (grow < M) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -623,6 +628,7 @@ __device__ __forceinline__ void store_tile_v4(const f32x16& acc, uint32_t region
         float x = o[e];
         if (beta != 0.f) x += beta * *c;
         *c = x;
+        if (C2) C2[c_index(grow, gcol + e, 64, cs2)] = x;
       }
     }
   }
@@ -640,7 +646,8 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
                                                   const float* __restrict__ bias, float beta,
                                                   float* __restrict__ C, int64_t ldc, int64_t cs,
                                                   int tiles_n, int ntiles, int vec4,
-                                                  float* __restrict__ dummy) {
+                                                  float* __restrict__ dummy,
+                                                  float* __restrict__ C2, int64_t cs2) {
   using G = X3P<WT, NW>;
   constexpr int NS = G::NS;
   static_assert(32 * WT * GBK * 2 % 1024 == 0, "B plane must be whole 1-KB DMA chunks");
@@ -736,7 +743,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
 #pragma unroll
     for (int t = 0; t < WT; ++t)
       store_tile_v4<G::EPI_LD>(acc[t], region, M, N, m0 + w * 32, n0 + 32 * t, kh, li, lane, beta, C, ldc,
-                    cs, vec4 != 0, dummy);
+                    cs, vec4 != 0, dummy, C2, cs2);
   };
   // vmcnt allowance for the first step after an epilogue: its 16-B stores (exactly 4 per tile
   // of 32 columns when vec4 and no beta loads) were issued after the DMA that step waits for
@@ -755,7 +762,10 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
     {
       const int later = total - 1 - g < NS - 2 ? total - 1 - g : NS - 2;  // stages issued after g
       if (later == NS - 2 && count_stores && q > 0 && s >= 1 && s <= NS - 2) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LOADS * (NS - 2) + 4 * WT) : "memory");
+        if (C2)
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LOADS * (NS - 2) + 8 * WT) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LOADS * (NS - 2) + 4 * WT) : "memory");
       } else if (later == NS - 2) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LOADS * (NS - 2)) : "memory");
       } else if (later == 1) {
@@ -1034,7 +1044,20 @@ static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t l
 
 static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
                    int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
-                   float* C, int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, void* stream) {
+                   float* C, int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, void* stream,
+                   float* C2 = nullptr, int64_t cs2 = 0) {
+  if (C2) {  // a slice-major copy as well: fused into k_gemm_x3p's epilogue, else packed after
+    if (cs2 % 4 != 0 || cs2 < M * 64 || cs != 64) return GNNEA_EINVAL;
+    const bool lda_ok = !trans_a && lda % 4 == 0 && K % 4 == 0 && (((uintptr_t)A) & 15) == 0;
+    const int64_t pb = x3_planes_bytes(N, K);
+    const bool fused = lda_ok && ws && ws_bytes >= pb && pick_splits(M, N, K, ws_bytes - pb) == 1;
+    if (!fused) {
+      const int rc = gemm_x3(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs,
+                             ws, ws_bytes, stream);
+      if (rc) return rc;
+      return gnnea_slice_pack_f32(C, ldc, (int32_t)M, (int32_t)N, C2, cs2, stream);
+    }
+  }
   if (trans_a && !trans_b && K > 0)
     return gemm_x3_ta(M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, ws, ws_bytes,
                       (hipStream_t)stream);
@@ -1111,7 +1134,7 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
 #define GNNEA_X3P_L(W, NWV, MD)                                                                  \
   hipLaunchKernelGGL((k_gemm_x3p<W, NWV, MD>), grid, dim3(64 * NWV), 0, s, (int)M, (int)N,       \
                      (int)K, A, lda, planes, (int64_t)np * GBK, (int64_t)np * kp, bias, beta, C, \
-                     ldc, cs, tn, ntiles, vec4, dummy)
+                     ldc, cs, tn, ntiles, vec4, dummy, C2, cs2)
 #define GNNEA_X3P(W)                                                                             \
   case W:                                                                                        \
     if (nw == 8) {                                                                               \
@@ -1268,6 +1291,19 @@ extern "C" int gnnea_gemm_x3_f32(int trans_a, int trans_b, int64_t M, int64_t N,
                                  int64_t ws_bytes, void* stream) {
   return gemm_x3(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, 64, ws, ws_bytes,
                  stream);
+}
+
+// C row-major AND its slice-major copy C2s [ceil(N/64)][M][64] (slice stride sstride2) from one
+// GEMM: the second store rides the epilogue of k_gemm_x3p (the GAT projection feeds the
+// row-major backward and the sliced forward aggregation)
+extern "C" int gnnea_gemm_x3_dual_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                                      const float* A, int64_t lda, const float* B, int64_t ldb,
+                                      const float* bias, float beta, float* C, int64_t ldc,
+                                      float* C2s, int64_t sstride2, void* ws, int64_t ws_bytes,
+                                      void* stream) {
+  if (!C2s) return GNNEA_EINVAL;
+  return gemm_x3(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, 64, ws, ws_bytes,
+                 stream, C2s, sstride2);
 }
 
 extern "C" int gnnea_gemm_x3_sliced_f32(int trans_a, int trans_b, int64_t M, int64_t N,

@@ -140,6 +140,9 @@ SIGNATURES = {
                                              _i64, _p, _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
     "gnnea_gemm_sliced_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p,
                                               _i64, _p, _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
+    "gnnea_gat_fwd_sliced_f32": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int,
+                                                ctypes.c_int, _p, _p, _f32, _p, ctypes.c_int, _p,
+                                                _i64, _p, _p, _p, _p]),
     "gnnea_gemm_f64": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
                                       _i64, ctypes.c_double, _p, _i64, ctypes.c_double, _p, _i64,
                                       _p]),
@@ -147,6 +150,9 @@ SIGNATURES = {
     "gnnea_gemm_x3_ws_bytes": (_i64, [_i64, _i64, _i64]),
     "gnnea_gemm_x3_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64,
                                          _p, _i64, _p, _f32, _p, _i64, _p, _i64, _p]),
+    "gnnea_gemm_x3_dual_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p,
+                                              _i64, _p, _i64, _p, _f32, _p, _i64, _p, _i64, _p,
+                                              _i64, _p]),
     "gnnea_gemm_x3_sliced_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p,
                                                 _i64, _p, _i64, _p, _f32, _p, _i64, _p, _i64,
                                                 _p]),

@@ -4,6 +4,7 @@ Every function here launches libgnnea kernels on the tensor's current stream; no
 path (``_lib.require_device``).  Reference call sites each op replaces are cited per function.
 """
 import ctypes
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -132,7 +133,7 @@ def _ld(t):
 
 
 def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_dtype=None,
-         x3=None):
+         x3=None, sliced_out=None):
     """out = op(a) @ op(b) (+ bias) (+ beta*out) on MFMA.
 
     fp32 operands: gnnea_gemm_f32 (exact-f32 MFMA), or for large products gnnea_gemm_x3_f32
@@ -184,11 +185,21 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
                                     ptr(b), _ld(b), ptr(bias), float(beta), ptr(out),
                                     _ld(out), cd, ptr(ws),
                                     ws_bytes if ws is not None else 0, stream_of(a.device)))
+        elif sliced_out is not None and x3 and not trans_a:
+            # row-major out AND the slice-major copy from one GEMM epilogue
+            check(L.gnnea_gemm_x3_dual_f32(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a),
+                                           ptr(b), _ld(b), ptr(bias), float(beta), ptr(out),
+                                           _ld(out), ptr(sliced_out), sliced_out.stride(0),
+                                           ptr(ws), ws_bytes if ws is not None else 0,
+                                           stream_of(a.device)))
         else:
             fn = L.gnnea_gemm_x3_f32 if x3 else L.gnnea_gemm_f32
             check(fn(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a), ptr(b), _ld(b),
                      ptr(bias), float(beta), ptr(out), _ld(out), ptr(ws),
                      ws_bytes if ws is not None else 0, stream_of(a.device)))
+            if sliced_out is not None:
+                check(L.gnnea_slice_pack_f32(ptr(out), _ld(out), M, N, ptr(sliced_out),
+                                             sliced_out.stride(0), stream_of(a.device)))
     return out
 
 
@@ -253,13 +264,41 @@ class LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+# slice-major copies of GEMM outputs written by the GEMM itself (gnnea_gemm_x3_dual_f32), keyed
+# by the row-major output's storage: the GAT forward finds the projection's sliced table here
+# instead of packing it (a stale entry is ignored: the tensor's version must match)
+_SLICED_COPIES = {}
+
+
+def sliced_copy_of(t, D):
+    e = _SLICED_COPIES.get(t.data_ptr())
+    if e is None:
+        return None
+    ref, ver, shape, xs = e
+    src = ref()
+    if src is None or src._version != ver or tuple(src.shape) != tuple(t.shape) or \
+            t.shape[1] < D or t.stride(1) != 1:
+        return None
+    return xs
+
+
 class MatmulFn(torch.autograd.Function):
     """y = x W  (torch.mm(input, self.W) at layers/att_layers.py:33, torch.spmm(x, kernel_gate)
-    at layers/layers.py:69) on MFMA."""
+    at layers/layers.py:69) on MFMA.  ``sliced``: also write y slice-major from the same GEMM
+    epilogue when the aggregation that follows uses the sliced table (GAT above the Infinity
+    Cache), registered for sliced_copy_of."""
 
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, sliced=False):
         ctx.save_for_backward(x, w)
+        M, N = x.shape[0], w.shape[1]
+        if sliced and x.dtype == torch.float32 and w.dtype == torch.float32 and N % 4 == 0 \
+                and use_sliced(M, N, torch.float32):
+            xs = sliced_empty(M, N, x.device, torch.float32)
+            y = gemm(x, w, sliced_out=xs)
+            _SLICED_COPIES.clear()  # one live copy: the layer's projection
+            _SLICED_COPIES[y.data_ptr()] = (weakref.ref(y), y._version, tuple(y.shape), xs)
+            return y
         return gemm(x, w)
 
     @staticmethod
@@ -271,15 +310,15 @@ class MatmulFn(torch.autograd.Function):
             if ctx.needs_input_grad[0] else None
         dw = gemm(x, dy, trans_a=True, out_dtype=w.dtype if bf else None) \
             if ctx.needs_input_grad[1] else None
-        return dx, dw
+        return dx, dw, None
 
 
 def linear(x, weight, bias=None):
     return LinearFn.apply(x, weight, bias)
 
 
-def matmul(x, w):
-    return MatmulFn.apply(x, w)
+def matmul(x, w, sliced=False):
+    return MatmulFn.apply(x, w, sliced)
 
 
 # ------------------------------------------------------------------------------------------ #
@@ -851,6 +890,9 @@ def _pad4(t, D, dtype=None):
     return out
 
 
+GAT_SLICED = True  # tests switch it off to compare with the row-major edge pass
+
+
 def gat_forward(csr, H, a32, heads, d_head, alpha, act, em=None, row0=0):
     """All heads of the GAT aggregation over ``csr`` (one edge pass per KG block).
 
@@ -865,6 +907,22 @@ def gat_forward(csr, H, a32, heads, d_head, alpha, act, em=None, row0=0):
     Y = torch.empty((N, (D + 3) // 4 * 4), dtype=H.dtype, device=H.device)
     m = torch.empty((N, heads), dtype=torch.float32, device=H.device)
     den = torch.empty_like(m)
+    if (GAT_SLICED and H.dtype == torch.float32 and d_head >= 32 and D % 4 == 0
+            and Y.shape[1] == D and use_sliced(H.shape[0], D, H.dtype)):
+        # above the Infinity Cache: the table slice-major (64-column slices, one 256-MB table
+        # per KG slice), row statistics once, then the slices one after another
+        Hs = sliced_copy_of(H, D)
+        if Hs is None:
+            Hs = slice_pack(H[:, :D])
+        wgt = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=H.device)
+        fs = _lib.lib().gnnea_gat_fwd_sliced_f32
+        with _lib.on_device(H.device):
+            for r0, r1 in _blocks(csr, H):
+                check(fs(_off32(csr.rowptr, r0), ptr(csr.col), r1 - r0, ptr(Hs), Hs.stride(0),
+                         heads, d_head, _off(s1, row0 + r0), ptr(s2), float(alpha), ptr(em),
+                         int(act), _off(Y, r0), Y.stride(0), _off(m, r0), _off(den, r0),
+                         ptr(wgt), stream_of(H.device)))
+        return Y, m, den, s1, s2
     fwd = _gat_fn("gnnea_gat_fwd", H.dtype)
     with _lib.on_device(H.device):
         for r0, r1 in _blocks(csr, H):  # per KG block when H exceeds the Infinity Cache

@@ -85,7 +85,9 @@ class GraphAttentionLayer(nn.Module):
         first = self.attentions[0]
         W_all = torch.cat([att.W for att in self.attentions], dim=1)
         a_all = torch.cat([att.a for att in self.attentions], dim=0)  # [heads, 2*d_head]
-        H = ops.matmul(x, W_all)
+        # above the Infinity Cache the GEMM also writes H slice-major for the GAT forward
+        # (a row shard exchanges row-major H: only without exchange)
+        H = ops.matmul(x, W_all, sliced=not isinstance(adj, DistAdj) or adj.part.g == 1)
         if isinstance(adj, DistAdj):
             y = _sharded_gat(adj, H, a_all, heads, self.output_dim, first.alpha, first.act,
                              self.dropout, self.training)

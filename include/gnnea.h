@@ -193,6 +193,16 @@ int gnnea_gat_fwd_f32(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
                       int64_t ldh, int heads, int d_head, const float* s1, const float* s2,
                       float alpha, const float* edge_mask, int act, float* Y, int64_t ldy,
                       float* m_out, float* den_out, void* stream);
+/* The same forward over a slice-major source table Hs [ceil(D/64)][n_src][64] fp32 (slice
+ * stride sstride floats, the gnnea_spmm_sliced_f32 layout): row max / denominator records first
+ * (m_out, den_out) and every edge's masked numerator weight (wgt: nnz x heads fp32, by CSR
+ * position, workspace), then the aggregation slice by slice (each KG slice a 256-MB table).
+ * d_head >= 32, heads <= 8, D % 4 == 0, act identity / relu; Y row-major (ldy % 4 == 0). */
+int gnnea_gat_fwd_sliced_f32(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
+                             const float* Hs, int64_t sstride, int heads, int d_head,
+                             const float* s1, const float* s2, float alpha,
+                             const float* edge_mask, int act, float* Y, int64_t ldy,
+                             float* m_out, float* den_out, float* wgt, void* stream);
 /* Backward in one gather sweep over A^T (autograd of att_layers.py:38-58):
  *  prep (rows i):   G_i = dY_i * act'(Y_i) (act: identity / relu, Y = h' there) and the per-node
  *                   record rec[i,h] = {s1, m, 1/den, c = G_i,h . h'_i,h}  (float4 per head);
@@ -276,6 +286,13 @@ int gnnea_gemm_x3_sliced_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
                              const float* A, int64_t lda, const float* B, int64_t ldb,
                              const float* bias, float beta, float* Cs, int64_t sstride, void* ws,
                              int64_t ws_bytes, void* stream);
+/* C row-major AND a slice-major copy C2s (element (r, c) at C2s[(c/64)*sstride2 + r*64 + c%64]):
+ * the second store rides the GEMM epilogue (the GAT projection: row-major for the backward,
+ * slice-major for gnnea_gat_fwd_sliced_f32).  Workspace from gnnea_gemm_x3_ws_bytes. */
+int gnnea_gemm_x3_dual_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                           const float* A, int64_t lda, const float* B, int64_t ldb,
+                           const float* bias, float beta, float* C, int64_t ldc, float* C2s,
+                           int64_t sstride2, void* ws, int64_t ws_bytes, void* stream);
 /* the same GEMM writing C slice-major (the layout gnnea_spmm_sliced_f32 gathers from):
  * element (r, c) of the M x N product at Cs[(c/64)*sstride + r*64 + c%64], sstride >= M*64.
  * The projection x W^T of a GCN layer writes its hidden this way at no extra cost. */

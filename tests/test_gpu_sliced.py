@@ -342,3 +342,64 @@ def test_colsum_vs_fp64(device, N, D, dt):
     if D % 4 == 0:
         wide = torch.randn(N, 2 * D + 4, device=device).to(dt)
         assert rel_err(ops.colsum(wide[:, :D]).float().cpu(), wide[:, :D].double().sum(0).cpu()) < tol
+
+
+@pytest.mark.parametrize("heads,d_head,act", [(4, 75, 1), (2, 64, 0), (1, 300, 1), (8, 32, 1)])
+def test_gat_fwd_sliced_vs_rowmajor_and_oracle(device, monkeypatch, heads, d_head, act):
+    """gnnea_gat_fwd_sliced_f32 (slice-major table, row statistics first) vs the fp64 oracle
+    (att_layers.py:29-61 x heads, oracle/gnn.gat_layer) and vs the row-major edge pass; the
+    saved row max / denominator are the row-major kernel's; the backward runs on them."""
+    from gnnea import ops, synth
+    from oracle.gnn import gat_layer
+    n = 700
+    tr = synth.kg_pair_triples(n, 4 * n, 40, seed=11)
+    r, c, v = synth.adjacency_coo(tr, 2 * n, reference_order=False)
+    adj = torch.sparse_coo_tensor(torch.from_numpy(np.stack([r, c])), torch.from_numpy(v),
+                                  (2 * n, 2 * n)).to(device)
+    rng = np.random.default_rng(heads * 100 + d_head)
+    D = heads * d_head
+    x = rng.standard_normal((2 * n, 64)).astype(np.float32)
+    W = (rng.standard_normal((heads, 64, d_head)) * 0.2).astype(np.float32)
+    A = (rng.standard_normal((heads, 1, 2 * d_head)) * 0.3).astype(np.float32)
+    R = rng.standard_normal((2 * n, D)).astype(np.float32)
+    actf = torch.relu if act else (lambda z: z)
+
+    def run(sliced):
+        monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 1 if sliced else 1 << 40)
+        monkeypatch.setattr(ops, "GAT_SLICED", sliced)
+        xt = torch.from_numpy(x).to(device).requires_grad_(True)
+        H = ops.matmul(xt, torch.cat(list(torch.from_numpy(W).to(device)), dim=1))
+        y = ops.gat(adj, H, torch.from_numpy(A).to(device).view(heads, 2 * d_head), heads,
+                    d_head, 0.2, actf if act else None)
+        (y * torch.from_numpy(R).to(device)).sum().backward()
+        return y.detach().cpu(), xt.grad.cpu()
+
+    ys, gs = run(True)
+    yr, gr = run(False)
+    xo = torch.from_numpy(x).double()
+    yo = gat_layer(xo, torch.from_numpy(W).double(), torch.from_numpy(A).double(), r, c, 0.2,
+                   act=actf)
+    assert rel_err(ys, yo) < 1e-4
+    assert rel_err(ys, yr) < 1e-5
+    assert rel_err(gs, gr) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K,bias", [(5000, 300, 300, True), (4100, 128, 64, False),
+                                        (300, 300, 36, False)])
+def test_gemm_x3_dual_output(device, M, N, K, bias):
+    """gnnea_gemm_x3_dual_f32: the row-major product and its slice-major copy from one GEMM
+    (the copy is stored from the same registers: bit-identical to packing the product)."""
+    from gnnea import ops
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    a = torch.randn(M, K, generator=g).to(device)
+    b = torch.randn(K, N, generator=g).to(device)
+    bb = torch.randn(N, generator=g).to(device) if bias else None
+    xs = ops.sliced_empty(M, N, device, torch.float32)
+    y = ops.gemm(a, b, bias=bb, x3=True, sliced_out=xs)
+    ref = ops.gemm(a, b, bias=bb, x3=True)
+    assert torch.equal(y, ref)
+    assert torch.equal(ops.slice_pack(y), xs) or all(
+        torch.equal(xs[s, :, :min(64, N - 64 * s)], y[:, 64 * s:64 * s + 64])
+        for s in range(xs.shape[0]))
+    ref64 = a.double() @ b.double() + (bb.double() if bias else 0)
+    assert rel_err(y.cpu(), ref64.cpu()) < 1e-5
