@@ -536,6 +536,10 @@ def test_spmm_block_diagonal_launches(device, monkeypatch):
     a_all = (torch.randn(heads, 2 * dh, device=device) * 0.1).requires_grad_(True)
     dy = torch.randn(2 * n, heads * dh, device=device)
 
+    # the row-major edge pass launched per block vs once (the sliced pass, which the default
+    # cache size selects here, has its own tests in test_gpu_sliced.py)
+    monkeypatch.setattr(ops, "GAT_SLICED", False)
+
     def gat_run():
         y = ops.GATFn.apply(H, a_all, csr, heads, dh, 0.2, 1, None)
         gH, ga = torch.autograd.grad(y, (H, a_all), dy)
