@@ -549,6 +549,13 @@ __device__ __forceinline__ u32x4 ds_read128(uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
   return v;
 }
+template <int OFF>  // immediate byte offset (ds_* offsets are 16-bit)
+__device__ __forceinline__ u32x4 ds_read128_o(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
 // (a float result type, not a per-element __builtin_bit_cast of a u32x4 lane: hipcc 7.2
 // miscompiles bit_cast of an ext-vector element lvalue to element 0)
 __device__ __forceinline__ f32x4_t ds_read128f(uint32_t addr) {
@@ -559,10 +566,21 @@ __device__ __forceinline__ f32x4_t ds_read128f(uint32_t addr) {
 
 // NW waves stacked along M (4: two workgroups per CU, 3-stage ring; 8: one per CU, 4 stages,
 // half the B-tile traffic per row of A)
+template <int I>
+struct IntC {
+  static constexpr int value = I;
+};
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(IntC<I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
 template <int WT, int NW>
 struct X3P {
   static constexpr int BM = 32 * NW, NT = 64 * NW;
-  static constexpr int NS = NW == 8 ? 4 : 3;                    // ring stages
   static constexpr int BN = 32 * WT;
   static constexpr int A_CHUNKS = BM * GBK * 4 / 1024;          // 16 rows x 64 B each: 2 per wave
   static constexpr int A_BYTES = A_CHUNKS * 1024;
@@ -574,6 +592,8 @@ struct X3P {
   static constexpr int EPI_BYTES = NW * 32 * EPI_LD * 4;         // the waves' epilogue regions
   static constexpr int STAGE = DMA_BYTES > EPI_BYTES ? DMA_BYTES : (EPI_BYTES + 1023) / 1024 * 1024;
   static constexpr int LOADS = A_CHUNKS / NW + B_CHUNKS_PAD / NW;  // DMA instr. / wave / stage
+  // ring stages: 4 when they fit one workgroup per CU (NW = 8), 3 for two per CU (NW = 4)
+  static constexpr int NS = NW == 8 ? (4 * STAGE <= 160 * 1024 ? 4 : 3) : 3;
   static_assert(A_CHUNKS == 2 * NW, "A: two 1-KB chunks per wave");
 };
 
@@ -650,6 +670,8 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
                                                   float* __restrict__ C2, int64_t cs2) {
   using G = X3P<WT, NW>;
   constexpr int NS = G::NS;
+  constexpr int TH = WT > 5 ? WT / 2 : WT, NH = WT / TH;  // column tiles per half, halves
+  static_assert(TH * NH == WT && NH <= 2, "WT > 5 must be 2 x TH");
   static_assert(32 * WT * GBK * 2 % 1024 == 0, "B plane must be whole 1-KB DMA chunks");
   static_assert(G::EPI_BYTES <= G::STAGE, "epilogue regions must fit one stage");
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * G::STAGE];
@@ -719,12 +741,8 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
   const int ra = w * 32 + li;
   const int a_off0 = ra * 64 + 16 * ((2 * kh) ^ ((ra >> 2) & 3));
   const int a_off1 = ra * 64 + 16 * ((2 * kh + 1) ^ ((ra >> 2) & 3));
-  int b_off[WT];
-#pragma unroll
-  for (int t = 0; t < WT; ++t) {
-    const int rb = t * 32 + li;
-    b_off[t] = G::A_BYTES + rb * 32 + 16 * (kh ^ ((rb >> 3) & 1));
-  }
+  // B row t*32 + li: bit 3 of the row is li's, so every column tile's offset is b_off0 + t KB
+  const int b_off0 = G::A_BYTES + li * 32 + 16 * (kh ^ ((li >> 3) & 1));
 
   const uint32_t smem_lds = lds_addr(smem);
   auto epilogue = [&](int q, int buf) {
@@ -747,7 +765,8 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
   };
   // vmcnt allowance for the first step after an epilogue: its 16-B stores (exactly 4 per tile
   // of 32 columns when vec4 and no beta loads) were issued after the DMA that step waits for
-  const bool count_stores = vec4 != 0 && beta == 0.f && MODE != 4;
+  const bool count_stores = vec4 != 0 && beta == 0.f && MODE != 4 &&
+                            G::LOADS * (NS - 2) + (C2 ? 8 : 4) * WT <= 63;
 
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i)
@@ -763,7 +782,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
       const int later = total - 1 - g < NS - 2 ? total - 1 - g : NS - 2;  // stages issued after g
       if (later == NS - 2 && count_stores && q > 0 && s >= 1 && s <= NS - 2) {
         if (C2)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LOADS * (NS - 2) + 8 * WT) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LOADS * (NS - 2) + 8 * WT > 63 ? 63 : G::LOADS * (NS - 2) + 8 * WT) : "memory");
         else
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::LOADS * (NS - 2) + 4 * WT) : "memory");
       } else if (later == NS - 2) {
@@ -790,14 +809,15 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
     const uint32_t st = smem_lds + cur * G::STAGE;
     const f32x4_t x0 = ds_read128f(st + a_off0);
     const f32x4_t x1 = ds_read128f(st + a_off1);
-    u32x4 braw[3 * WT];
-#pragma unroll
-    for (int t = 0; t < WT; ++t) {
-      braw[3 * t] = ds_read128(st + b_off[t]);
-      braw[3 * t + 1] = ds_read128(st + b_off[t] + G::PLANE_BYTES);
-      braw[3 * t + 2] = ds_read128(st + b_off[t] + 2 * G::PLANE_BYTES);
-    }
-    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(3 * WT) : "memory");  // the two A reads
+    u32x4 braw[3 * TH];
+    const uint32_t bst = st + b_off0;
+    static_for<TH>([&](auto tt) {
+      constexpr int t = decltype(tt)::value;
+      braw[3 * t] = ds_read128_o<t * 1024>(bst);
+      braw[3 * t + 1] = ds_read128_o<t * 1024 + G::PLANE_BYTES>(bst);
+      braw[3 * t + 2] = ds_read128_o<t * 1024 + 2 * G::PLANE_BYTES>(bst);
+    });
+    asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(3 * TH) : "memory");  // the two A reads
     __builtin_amdgcn_sched_barrier(0);
     float xa[8];
 #pragma unroll
@@ -825,32 +845,47 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
       am[j] = __builtin_bit_cast(__bf16, m);
       al[j] = __builtin_bit_cast(__bf16, l);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    bf16x8_t bh[WT], bm_[WT], bl[WT];
+    // the wave's column tiles in NH halves of TH (a 320-wide wave tile keeps 160 accumulator
+    // registers; its B fragments are read half by half, the second half's reads in flight
+    // under the first half's MFMAs)
 #pragma unroll
-    for (int t = 0; t < WT; ++t) {
-      bh[t] = __builtin_bit_cast(bf16x8_t, braw[3 * t]);
-      bm_[t] = __builtin_bit_cast(bf16x8_t, braw[3 * t + 1]);
-      bl[t] = __builtin_bit_cast(bf16x8_t, braw[3 * t + 2]);
-    }
-    if (MODE == 1) {  // timing experiment: keep the data live, skip the matrix cores
+    for (int hf = 0; hf < NH; ++hf) {
+      if (hf > 0) {  // (NH <= 2: the second half)
+        static_for<TH>([&](auto tt) {
+          constexpr int t = decltype(tt)::value + TH;
+          braw[3 * (t - TH)] = ds_read128_o<t * 1024>(bst);
+          braw[3 * (t - TH) + 1] = ds_read128_o<t * 1024 + G::PLANE_BYTES>(bst);
+          braw[3 * (t - TH) + 2] = ds_read128_o<t * 1024 + 2 * G::PLANE_BYTES>(bst);
+        });
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8_t bh[TH], bm_[TH], bl[TH];
 #pragma unroll
-      for (int t = 0; t < WT; ++t)
-        acc[t][0] += (float)(ah[0] + am[1] + al[2] + bh[t][0] + bm_[t][1] + bl[t][2]);
-    } else {
+      for (int t = 0; t < TH; ++t) {
+        bh[t] = __builtin_bit_cast(bf16x8_t, braw[3 * t]);
+        bm_[t] = __builtin_bit_cast(bf16x8_t, braw[3 * t + 1]);
+        bl[t] = __builtin_bit_cast(bf16x8_t, braw[3 * t + 2]);
+      }
+      f32x16* ac = acc + hf * TH;
+      if (MODE == 1) {  // timing experiment: keep the data live, skip the matrix cores
 #pragma unroll
-    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t], acc[t], 0, 0, 0);
+        for (int t = 0; t < TH; ++t)
+          ac[t][0] += (float)(ah[0] + am[1] + al[2] + bh[t][0] + bm_[t][1] + bl[t][2]);
+      } else {
 #pragma unroll
-    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm_[t], acc[t], 0, 0, 0);
+      for (int t = 0; t < TH; ++t) ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t], ac[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t], acc[t], 0, 0, 0);
+      for (int t = 0; t < TH; ++t) ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bm_[t], ac[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[t], acc[t], 0, 0, 0);
+      for (int t = 0; t < TH; ++t) ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t], ac[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm_[t], acc[t], 0, 0, 0);
+      for (int t = 0; t < TH; ++t) ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am, bh[t], ac[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < WT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t], acc[t], 0, 0, 0);
+      for (int t = 0; t < TH; ++t) ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm_[t], ac[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < TH; ++t) ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t], ac[t], 0, 0, 0);
+      }
     }
     cur = cur == NS - 1 ? 0 : cur + 1;
     if (++s == nsteps) { s = 0; ++q; }
@@ -1034,7 +1069,7 @@ extern "C" int gnnea_gemm_sliced_f32(int trans_a, int trans_b, int64_t M, int64_
 // bias row) + a 1-KB dummy store target for k_gemm_x3p's out-of-range lanes
 static int64_t x3_planes_bytes(int64_t N, int64_t K) {
   const int64_t kp = (K + 1 + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign;
-  const int64_t np = (N + 159) / 160 * 160;  // k_gemm_x3p's padded rows (>= N)
+  const int64_t np = (N + 319) / 320 * 320;  // k_gemm_x3p's padded rows (>= N, any tile width)
   return ((3 * np * kp * 2 + 255) & ~(int64_t)255) + 1024;
 }
 
@@ -1095,10 +1130,10 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
     int wtp = (int)((N + 31) / 32 < 5 ? (N + 31) / 32 : 5);
     if (const char* e = getenv("GNNEA_X3_WT")) {  // tuning override only
       const int v = atoi(e);
-      if (v >= 1 && v <= 5) wtp = v;
+      if ((v >= 1 && v <= 5) || v == 10) wtp = v;
     }
     const int tn = (int)((N + 32 * wtp - 1) / (32 * wtp));
-    const int np = tn * 32 * wtp;  // <= the 160-row rounding x3_planes_bytes reserves
+    const int np = tn * 32 * wtp;  // <= the 320-row rounding x3_planes_bytes reserves
     const int kp = (int)((K + (bias ? 1 : 0) + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign);
     float* dummy = (float*)((char*)ws + pbytes - 1024);
     {
@@ -1114,6 +1149,7 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
       const int v = atoi(e);
       if (v == 4 || v == 8) nw = v;
     }
+    if (wtp == 10) nw = 8;  // the 320-wide wave tile: 8 waves, one workgroup per CU
     const int64_t tm = (M + 32 * nw - 1) / (32 * nw);
     if (tm * tn >= (1ll << 31)) return GNNEA_EINVAL;
     const int ntiles = (int)(tm * tn);
@@ -1156,6 +1192,9 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
       GNNEA_X3P(2)
       GNNEA_X3P(3)
       GNNEA_X3P(4)
+      case 10:
+        GNNEA_X3P_L(10, 8, 0);
+        break;
       default:
       GNNEA_X3P(5)
     }
