@@ -127,6 +127,41 @@ def sinkhorn_large(device):
     return r
 
 
+def sinkhorn_sharded(device, rank, world, B=15000, reg=0.01, n0=20, n1=120):
+    """§8e: utils/ot_loss.sinkhorn at B = 15000 with the cost rows sharded over the ranks
+    (gnnea.sinkhorn.solve_row_sharded: per iteration one all-gather of W x (2B + 2) doubles of
+    column (max, sum-exp) pairs).  Marginal iters/s, max over ranks; every rank calls this."""
+    from gnnea.sinkhorn import solve_row_sharded
+    g = torch.Generator(device="cpu").manual_seed(0)
+    X = (0.05 * torch.randn(B, 300, generator=g)).to(device)
+    Y = (0.05 * torch.randn(B, 300, generator=g)).to(device)
+    r0, r1 = B * rank // world, B * (rank + 1) // world
+    M = torch.cdist(X[r0:r1], Y)
+    mx = M.max().reshape(1)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    M = (M / mx).contiguous()
+    del X, Y
+    a = torch.ones(r1 - r0, dtype=torch.float64, device=device)
+    b = torch.ones(B, dtype=torch.float64, device=device)
+    ts = []
+    for n_it in (n0, n0, n1):  # the first solve warms the kernels and the communicator
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = solve_row_sharded(M, a, b, reg, -1.0, n_it, want_plan=False)
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        assert res.iters == n_it, (res.iters, n_it)
+        ts.append(t.item())
+    return {"iters_per_s": round((n1 - n0) / (ts[2] - ts[1]), 1), "B": B, "reg": reg,
+            "ranks": world, "rows_per_rank": r1 - r0,
+            "exchange_bytes_per_iter_per_rank": world * (2 * B + 2) * 8,
+            "method": "marginal (T(%d)-T(%d))/%d, max over ranks, incl. the per-iteration "
+                      "all-gather and host batch syncs" % (n1, n0, n1 - n0),
+            "kernels": "gnnea_sinkhorn_shard_* (csrc/sinkhorn_shard.hip)"}
+
+
 def gw_rate(device, B=3000):
     """One GW outer-iteration cost rebuild (SinkhornOT/cderivation.py:160-162, get_LT:
     constC - C1 . T . C2^T) in fp64 on the f64 MFMA GEMM, 2 * I * J * (I + J) flops."""
@@ -424,6 +459,12 @@ def main():
             train = measure("HGCN", n, rank, world, device, args.train_steps, 1)
         except Exception as e:  # report, never hide
             train = {"error": repr(e)}
+    sk_shard = None
+    if world > 1 and not args.no_sinkhorn and not args.rehearse:
+        try:
+            sk_shard = sinkhorn_sharded(device, rank, world)
+        except Exception as e:  # report, never hide
+            sk_shard = {"error": repr(e)}
 
     if rank == 0:
         # the SpMM is launched once per diagonal (KG) block of rows when the gathered matrix is
@@ -495,6 +536,8 @@ def main():
                 line["layouts"] = {"error": repr(e)}
         if train is not None:
             line["train_step"] = train
+        if sk_shard is not None:
+            line["sinkhorn_B15000_row_sharded"] = sk_shard
         if world == 1 and not args.no_sinkhorn:
             try:
                 line["sinkhorn"] = sinkhorn_rate(device)

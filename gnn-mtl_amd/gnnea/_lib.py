@@ -162,7 +162,19 @@ SIGNATURES = {
                                               ctypes.c_int, _p]),
     "gnnea_sinkhorn_finish": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p, ctypes.c_int,
                                              _i64, _p, _p, _p]),
-    "gnnea_l1_keys_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _i64, _p]),
+    "gnnea_sinkhorn_shard_ws_bytes": (_i64, [ctypes.c_int, ctypes.c_int]),
+    "gnnea_sinkhorn_shard_init": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), ctypes.c_int,
+                                                 _p]),
+    "gnnea_sinkhorn_shard_colpart": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem),
+                                                    ctypes.c_int, _p, _p]),
+    "gnnea_sinkhorn_shard_step": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), ctypes.c_int,
+                                                 _p, ctypes.c_int, _p]),
+    "gnnea_sinkhorn_shard_flag": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p, _p]),
+    "gnnea_sinkhorn_shard_close": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p,
+                                                  ctypes.c_int, _p]),
+    "gnnea_sinkhorn_shard_finish": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p,
+                                                   ctypes.c_int, _i64, _p, _p, _p, _p]),
+    "gnnea_l1_keys_f32":(ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _i64, _p]),
     "gnnea_l1_pairs_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i32, _i32, _p, _p]),
     "gnnea_l1_rank_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _p, _p]),
     "gnnea_topk_rows_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _i64, _p, _i64, _i32,

@@ -182,3 +182,163 @@ def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.fl
                                   int(ints[ST_REASON]), float(dbl[SD_ERR]), float(dbl[SD_TNEW]),
                                   float(dbl[SD_TPREV]), float(dbl[SD_LOSS])))
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# §8e: KNOPP with the cost rows sharded over ranks (gnnea_sinkhorn_shard_*, sinkhorn_shard.hip).
+# Rank r holds a contiguous block of rows; per iteration every rank reduces its rows to (max,
+# sum-exp) pairs per column, the pairs are all-gathered (one collective of W x (2J + 2) doubles)
+# and each rank merges them in rank order, so g and all stop decisions are bit-identical on every
+# rank: the ranks poll their own status block and leave the loop on the same iteration.
+
+class _Shard:
+    """One rank's row block as a gnnea_sinkhorn problem (KNOPP)."""
+
+    def __init__(self, C, a, b, reg, tol, max_iter, I_global):
+        _lib.require_device(C, a, b)
+        if C.dim() != 2:
+            raise ValueError("gnnea.sinkhorn: C must be 2-D")
+        if C.dtype not in (torch.float32, torch.float64):
+            C = C.double()
+        if C.stride(1) != 1:
+            C = C.contiguous()
+        self.C = C
+        self.I, self.J = C.shape
+        self.a = a.reshape(-1).to(torch.float64).contiguous()
+        self.b = b.reshape(-1).to(torch.float64).contiguous()
+        if self.a.numel() != self.I or self.b.numel() != self.J:
+            raise ValueError("gnnea.sinkhorn: weights must have I_local and J entries")
+        L = _lib.lib()
+        nb = int(L.gnnea_sinkhorn_shard_ws_bytes(self.I, self.J))
+        if nb < 0:
+            check(nb)
+        dev = C.device
+        self.ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        self.pair = torch.empty(2 * self.J + 2, dtype=torch.float64, device=dev)
+        self.flag = torch.empty(1, dtype=torch.float64, device=dev)
+        self.prob = SinkhornProblem(
+            mode=_lib.GNNEA_SK_KNOPP,
+            c_dtype=_lib.GNNEA_F32 if C.dtype == torch.float32 else _lib.GNNEA_F64,
+            I=self.I, J=self.J, ldc=C.stride(0), C=C.data_ptr(), a=self.a.data_ptr(),
+            b=self.b.data_ptr(), eps=float(reg), p=1.0, tol=float(tol), max_iter=int(max_iter),
+            iters_run=0, variant=1, reserved=0, ws=self.ws.data_ptr())
+        self.pp = ctypes.byref(self.prob)
+        self.st = stream_of(dev)
+        check(L.gnnea_sinkhorn_shard_init(self.pp, int(I_global), self.st))
+
+
+def _run_shards(shards, gather, reduce_sum, max_iter, tol, want_plan, plan_dtype):
+    """The iteration loop over the shards this process drives; gather(list of local [n] tensors)
+    -> [W, n] in rank order, reduce_sum(list of local tensors) -> their sum over all ranks."""
+    L = _lib.lib()
+    ref = shards[0]
+    run = 0
+    if 1.0 > tol and max_iter > 0:  # utils/ot_loss.py:50 (err starts at 1)
+        step, hi = 10, 2
+        while run < max_iter:
+            hi = min(hi, max_iter)
+            for it in range(run, hi):
+                for s in shards:
+                    check(L.gnnea_sinkhorn_shard_colpart(s.pp, it, ptr(s.pair), s.st))
+                pairs = gather([s.pair for s in shards])
+                W = pairs.shape[0]
+                for s in shards:
+                    check(L.gnnea_sinkhorn_shard_step(s.pp, it, ptr(pairs), W, s.st))
+            run = hi
+            if _status(ref.ws)[0][ST_DONE].item():
+                break
+            hi = run + step
+            step = min(2 * step, MAX_BATCH)
+    for s in shards:
+        s.prob.iters_run = run
+        check(L.gnnea_sinkhorn_shard_flag(s.pp, ptr(s.flag), s.st))
+    flags = gather([s.flag for s in shards])
+    W = flags.shape[0]
+    out = []
+    for s in shards:
+        check(L.gnnea_sinkhorn_shard_close(s.pp, ptr(flags), W, s.st))
+        plan = (torch.empty((s.I, s.J), dtype=plan_dtype, device=s.C.device)
+                if want_plan else None)
+        row_sum = torch.empty(s.I, dtype=torch.float64, device=s.C.device)
+        loss = torch.empty(1, dtype=torch.float64, device=s.C.device)
+        col = torch.empty(s.J, dtype=torch.float64, device=s.C.device)
+        check(L.gnnea_sinkhorn_shard_finish(
+            s.pp, ptr(plan), _lib.GNNEA_F32 if plan_dtype == torch.float32 else _lib.GNNEA_F64,
+            s.J, ptr(row_sum), ptr(loss), ptr(col), s.st))
+        out.append((plan, row_sum, loss, col))
+    loss = reduce_sum([o[2] for o in out])
+    col_sum = reduce_sum([o[3] for o in out])
+    results = []
+    for s, (plan, row_sum, _, _) in zip(shards, out):
+        ints, dbl = _status(s.ws)
+        results.append(SinkhornResult(plan, row_sum, col_sum, int(ints[ST_ITERS]),
+                                      int(ints[ST_REASON]), float(dbl[SD_ERR]), 0.0, 0.0,
+                                      float(loss.item())))
+    return results
+
+
+def solve_row_sharded(C_loc, a_loc, b, reg, tol, max_iter, group=None,
+                      plan_dtype=torch.float64, want_plan=True):
+    """KNOPP over this rank's cost rows C_loc [I_loc, J] (ranks hold consecutive row blocks in
+    rank order), a_loc its rows' source weights, b all J target weights.  One all-gather of the
+    column pairs per iteration over `group` (RCCL on HIP devices).  Returns this rank's
+    SinkhornResult: plan / row_sum of its rows, col_sum and loss of the whole plan."""
+    import torch.distributed as dist
+    W = dist.get_world_size(group)
+    dev = C_loc.device
+    n = torch.tensor([C_loc.shape[0]], dtype=torch.int64)
+    if dist.get_backend(group) != "gloo":
+        n = n.to(dev)
+    dist.all_reduce(n, group=group)
+
+    # gloo (CPU tests, a single-GPU rehearsal) exchanges host copies; RCCL the device buffers
+    host = dist.get_backend(group) == "gloo"
+
+    def gather(ts):
+        (t,) = ts
+        src = t.cpu() if host else t
+        out = torch.empty(W * t.numel(), dtype=t.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, src, group=group)
+        return out.view(W, t.numel()).to(dev)
+
+    def reduce_sum(ts):
+        (t,) = ts
+        t = t.cpu() if host else t.clone()
+        dist.all_reduce(t, group=group)
+        return t.to(dev)
+
+    with _lib.on_device(dev):
+        shard = _Shard(C_loc, a_loc, b, reg, tol, max_iter, int(n.item()))
+        return _run_shards([shard], gather, reduce_sum, max_iter, tol, want_plan, plan_dtype)[0]
+
+
+def solve_row_blocks(C, a, b, reg, tol, max_iter, row_splits, plan_dtype=torch.float64,
+                     want_plan=True):
+    """The row-sharded solve with every shard driven by this process on C's device (the
+    exchange is a stack of the shards' pair rows in rank order): the same kernels and the same
+    merge order as solve_row_sharded over len(row_splits) + 1 ranks, for tests and for a single
+    device.  row_splits: the first row of shards 1..W-1.  Returns (plan, SinkhornResult)."""
+    _lib.require_device(C, a, b)
+    I = C.shape[0]
+    bounds = [0] + list(row_splits) + [I]
+    if any(bounds[k] >= bounds[k + 1] for k in range(len(bounds) - 1)):
+        raise ValueError("gnnea.sinkhorn: row blocks must be non-empty and increasing")
+    with _lib.on_device(C.device):
+        shards = [_Shard(C[bounds[k]:bounds[k + 1]], a.reshape(-1)[bounds[k]:bounds[k + 1]], b,
+                         reg, tol, max_iter, I) for k in range(len(bounds) - 1)]
+
+        def gather(ts):
+            return torch.stack(ts)
+
+        def reduce_sum(ts):
+            out = ts[0].clone()
+            for t in ts[1:]:
+                out += t
+            return out
+
+        res = _run_shards(shards, gather, reduce_sum, max_iter, tol, want_plan, plan_dtype)
+    plan = torch.cat([r.plan for r in res]) if want_plan else None
+    r0 = res[0]
+    row_sum = torch.cat([r.row_sum for r in res])
+    return plan, SinkhornResult(plan, row_sum, r0.col_sum, r0.iters, r0.reason, r0.err, 0.0, 0.0,
+                                r0.loss)

@@ -4,11 +4,16 @@
 semantics and arithmetic (fp64, K = exp(M / -reg) built once on the device, u = 1/I and v = 1/J
 start, err = ||v (K^T u) - b||_2 checked every 10th iteration, revert-and-break on K^T u == 0 /
 inf / NaN); the loop runs on the device, the host only reads the stop flag between batches.
+
+``sinkhorn_row_sharded(a_loc, b, M_loc, reg, ...)`` is the same solve with M's rows split over
+the ranks of a torch.distributed group (consecutive row blocks in rank order):
+one all-gather of the column log-sum-exp pairs per iteration, identical stop decisions on every
+rank.  It returns this rank's plan rows and the loss of the whole plan.
 """
 import torch
 
 from gnnea import _lib
-from gnnea.sinkhorn import solve
+from gnnea.sinkhorn import solve, solve_row_sharded
 
 
 def sinkhorn(a, b, M, reg, numItermax=1000, stopThr=1e-9, verbose=False):
@@ -31,3 +36,18 @@ def sinkhorn(a, b, M, reg, numItermax=1000, stopThr=1e-9, verbose=False):
         print("{:5d}|{:.6e}".format(res.iters, res.err))
     loss = torch.tensor(res.loss, dtype=torch.float64, device=M.device)
     return res.plan, loss
+
+
+def sinkhorn_row_sharded(a_loc, b, M_loc, reg, numItermax=1000, stopThr=1e-9, verbose=False,
+                         group=None):
+    _lib.require_device(M_loc)
+    a_loc = a_loc.double()
+    b = b.double()
+    assert len(a_loc) == M_loc.shape[0] and len(b) == M_loc.shape[1], \
+        "the dimension of weights and distance matrix don't match"
+    res = solve_row_sharded(M_loc, a_loc, b, reg, stopThr, numItermax, group=group)
+    if res.reason == 2:
+        print("Warning: numerical errors at iteration ", res.iters)
+    if verbose:
+        print("{:5d}|{:.6e}".format(res.iters, res.err))
+    return res.plan, torch.tensor(res.loss, dtype=torch.float64, device=M_loc.device)

@@ -388,6 +388,32 @@ int gnnea_sinkhorn_iterate(const gnnea_sinkhorn* prob, int first, int count, voi
 int gnnea_sinkhorn_finish(const gnnea_sinkhorn* prob, void* plan, int plan_dtype, int64_t ldp,
                           double* row_sum, double* col_sum, void* stream);
 
+/* §8e. KNOPP (utils/ot_loss.py:5-76) with the cost rows sharded over W ranks (rank r holds a
+ * contiguous block of rows, rank order = row order).  `prob` is the rank's own problem: I = its
+ * rows, C = its cost rows, a = its rows' source weights, b = all J target weights, mode KNOPP.
+ * Per iteration it (host loop, every rank):
+ *   gnnea_sinkhorn_shard_colpart(prob, it, pair)      pair: 2J + 2 doubles (its column LSE pairs)
+ *   <all-gather the W pair rows into pairs [W][2J + 2], rank order>
+ *   gnnea_sinkhorn_shard_step(prob, it, pairs, W)     g, stop decisions, its row pass
+ * Every rank takes the same decisions from the same gathered data; the status block (ws) is
+ * read as for gnnea_sinkhorn_iterate.  After the loop (iters_run = iterations enqueued):
+ *   gnnea_sinkhorn_shard_flag(prob, flag)  -> all-gather the W flags ->
+ *   gnnea_sinkhorn_shard_close(prob, flags, W)        settles the last iteration's u check
+ *   gnnea_sinkhorn_shard_finish(...)                  its plan rows / row sums, loss_part[1] =
+ *                                                     its sum P.M, col_part[J] = its column sums
+ * The caller sums loss_part and col_part over the ranks. */
+int64_t gnnea_sinkhorn_shard_ws_bytes(int I_local, int J);
+int gnnea_sinkhorn_shard_init(const gnnea_sinkhorn* prob, int I_global, void* stream);
+int gnnea_sinkhorn_shard_colpart(const gnnea_sinkhorn* prob, int it, double* pair, void* stream);
+int gnnea_sinkhorn_shard_step(const gnnea_sinkhorn* prob, int it, const double* pairs, int W,
+                              void* stream);
+int gnnea_sinkhorn_shard_flag(const gnnea_sinkhorn* prob, double* flag, void* stream);
+int gnnea_sinkhorn_shard_close(const gnnea_sinkhorn* prob, const double* flags, int W,
+                               void* stream);
+int gnnea_sinkhorn_shard_finish(const gnnea_sinkhorn* prob, void* plan, int plan_dtype,
+                                int64_t ldp, double* row_sum, double* loss_part, double* col_part,
+                                void* stream);
+
 /* ------------------------------------------------------------------------------------------ *
  * §8f #1. L1 (cityblock) distance search.  scipy.spatial.distance.cdist(.., 'cityblock') as
  * used by BaseModel.get_neg (models/models_ea.py:19-30), get_hits (utils/eval_utils.py:71-98)
