@@ -14,16 +14,6 @@
 
 namespace gnnea {
 
-template <int H>
-__device__ __forceinline__ float hsel(const float (&w)[H], int h) {
-  float r = w[0];
-#pragma unroll
-  for (int k = 1; k < H; ++k) r = (h == k) ? w[k] : r;
-  return r;
-}
-
-__device__ __forceinline__ float lrelu(float z, float alpha) { return z > 0.f ? z : alpha * z; }
-
 // ---------------------------------------------------------------------------------------- //
 // Head-grouped lane layout (scores and backward src pass).  With HP = H rounded up to a power of
 // two, each head owns LPH = 64 / HP consecutive lanes and lane s of a head owns the EPL
@@ -49,46 +39,6 @@ struct HeadLanes {
     }
   }
 };
-
-// Sums of NV values over each head's LPH lanes at once, by reduce-scatter: DPP steps on lane bits
-// 3 (row_mirror, only when a head spans whole rows), 2 (row_half_mirror), 1 (quad reverse), 0
-// (quad swap) each pair a lane with a partner that agrees on the bits split before, halving the
-// live values; heads wider than a row add xor-16 / xor-32 steps on the one remaining value.
-// Afterwards lane h*LPH + grp_lane<NV, LPH>(v) holds head h's full sum of value v.
-template <int CTRL, int CNT, int NV>
-__device__ __forceinline__ void rs_step(float (&p)[NV], bool up) {
-  if constexpr (CNT > 1) {
-    constexpr int half = CNT / 2;
-#pragma unroll
-    for (int t = 0; t < half; ++t) {
-      const float keep = up ? p[t + half] : p[t];
-      const float send = up ? p[t] : p[t + half];
-      p[t] = keep + mov_dpp_f32<CTRL>(send);
-    }
-  } else {
-    p[0] += mov_dpp_f32<CTRL>(p[0]);
-  }
-}
-template <int NV, int LPH>
-__device__ __forceinline__ float grp_sum(float (&p)[NV], int lane) {
-  static_assert(LPH >= 8 && (NV & (NV - 1)) == 0 && NV <= (LPH >= 16 ? 16 : 8), "grp_sum shape");
-  if constexpr (LPH >= 16) {
-    rs_step<0x140, NV, NV>(p, lane & 8);      // row_mirror: lane ^ 15
-    rs_step<0x141, NV / 2, NV>(p, lane & 4);  // row_half_mirror: lane ^ 7
-    rs_step<0x1B, NV / 4, NV>(p, lane & 2);   // quad_perm [3,2,1,0]: lane ^ 3
-    rs_step<0xB1, NV / 8, NV>(p, lane & 1);   // quad_perm [1,0,3,2]: lane ^ 1
-  } else {
-    rs_step<0x141, NV, NV>(p, lane & 4);
-    rs_step<0x1B, NV / 2, NV>(p, lane & 2);
-    rs_step<0xB1, NV / 4, NV>(p, lane & 1);
-  }
-  float v = p[0];
-  if constexpr (LPH >= 32) v += __shfl_xor(v, 16, 64);
-  if constexpr (LPH >= 64) v += __shfl_xor(v, 32, 64);
-  return v;
-}
-template <int NV, int LPH>
-__device__ __forceinline__ constexpr int grp_lane(int v) { return v * ((LPH >= 16 ? 16 : 8) / NV); }
 
 // s1[i,h] = sum_d H[i, h*dh+d] * a[h, d];  s2[i,h] = sum_d H[i, h*dh+d] * a[h, dh+d]
 // A wave walks rows (grid-stride) with the lane's slice of a preloaded.

@@ -23,8 +23,6 @@
 
 namespace gnnea {
 
-__device__ __forceinline__ float lrelu_s(float z, float alpha) { return z > 0.f ? z : alpha * z; }
-
 template <int H>
 __global__ __launch_bounds__(256) void k_gat_rowstats(const int32_t* __restrict__ rowptr,
                                                       const int32_t* __restrict__ col, int n_rows,
@@ -48,7 +46,7 @@ __global__ __launch_bounds__(256) void k_gat_rowstats(const int32_t* __restrict_
   for (int e = beg + lane; e < end; e += 64) {
     const int j = col[e];
 #pragma unroll
-    for (int h = 0; h < H; ++h) mx[h] = fmaxf(mx[h], -lrelu_s(si[h] + s2[(int64_t)j * H + h], alpha));
+    for (int h = 0; h < H; ++h) mx[h] = fmaxf(mx[h], -lrelu(si[h] + s2[(int64_t)j * H + h], alpha));
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) mx[h] = wave_max(mx[h]);
@@ -56,7 +54,7 @@ __global__ __launch_bounds__(256) void k_gat_rowstats(const int32_t* __restrict_
     const int j = col[e];
 #pragma unroll
     for (int h = 0; h < H; ++h) {
-      const float w = __expf(-lrelu_s(si[h] + s2[(int64_t)j * H + h], alpha) - mx[h]);
+      const float w = __expf(-lrelu(si[h] + s2[(int64_t)j * H + h], alpha) - mx[h]);
       den[h] += w;  // the row sum uses the un-dropped weights (att_layers.py:45-51)
       wgt[(int64_t)e * H + h] = emask ? w * emask[(int64_t)e * H + h] : w;
     }
@@ -142,6 +140,311 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
   *(RY*)(Y + (int64_t)row * ldy + c0) = Vec4<TY>::put(make_float4(o[0], o[1], o[2], o[3]));
 }
 
+// ---------------------------------------------------------------------------------------- //
+// Backward over the slice-major G (the k_gat_bwd_prep / _src / _dst scheme of gat.hip, with the
+// source-side gather cut into 64-column slices as the forward above).  k_gat_bwd_src gathers
+// each in-neighbour's whole 1,200-B G row from a 1.2-GB KG table; here:
+//   k_gat_bwd_prep_s (dest rows i): G = dY * act'(Y) written slice-major, records {s1, m, 1/den,
+//                     c = G_i . h'_i} as gat.hip;
+//   k_gat_bwd_w      (source rows j, 16 lanes per row): wT[e][h] = alpha_ij * mask_ij in A^T
+//                     order (one record gather per edge, once);
+//   k_gat_bwd_src_sl (slice, source row j) as k_gat_fwd_sliced: dH_j[slice] = sum_i w_ij G_i,
+//                     and per edge the slice's share of the per-head products G_i,h . H_j,h for
+//                     the (at most two) heads the slice holds — reduced over each 16-lane group
+//                     by reduce-scatter (grp_sum) and stored as pd[s][e][2];
+//   k_gat_bwd_edge   (source rows j, 16 lanes per row): da_ij,h = the head's slice partials
+//                     summed in slice order, dz_ij = -LeakyReLU'(z) alpha (mask da - c_i) in A^T
+//                     order (coalesced; storing it at A positions instead measured 1.69 -> 3.65
+//                     ms per cfg-4 launch against 2.77 -> 2.28 for the destination pass),
+//                     ds2_j = sum_i dz; optionally dH_j += ds2_j (x) a2;
+//   k_gat_bwd_dst_s  (dest rows i): its dH row loaded first (in flight under the dz gathers),
+//                     ds1_i through the transpose position map, dH_i += ds1_i (x) a1
+//                     (+ ds2_i (x) a2 when the edge pass left it, square unsharded case).
+// fp32 throughout; sums in a different order from gat.hip's single pass (fp32 rounding level).
+// ---------------------------------------------------------------------------------------- //
+
+template <int ACT, int H, int NCH>
+__global__ __launch_bounds__(256) void k_gat_bwd_prep_s(int n_rows, int D, int dh,
+                                                        const float4* __restrict__ dY,
+                                                        const float4* __restrict__ Y, int64_t ld4,
+                                                        const float* __restrict__ s1,
+                                                        const float* __restrict__ mrow,
+                                                        const float* __restrict__ den,
+                                                        float4* __restrict__ Gs, int64_t sstride4,
+                                                        float4* __restrict__ rec) {
+  const int row = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
+  if (row >= n_rows) return;
+  const int lane = lane_id();
+  float cp[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) cp[h] = 0.f;
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    const int c4 = lane + 64 * q;
+    if (4 * c4 >= D) continue;
+    const float4 dy = dY[(int64_t)row * ld4 + c4];
+    const float4 y = Y[(int64_t)row * ld4 + c4];
+    const float ys[4] = {y.x, y.y, y.z, y.w};
+    float gs[4] = {dy.x, dy.y, dy.z, dy.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int c = 4 * c4 + t;
+      gs[t] = c < D ? gs[t] * act_grad_from_out<ACT>(ys[t]) : 0.f;
+      const int hh = c < D ? c / dh : H;
+#pragma unroll
+      for (int h = 0; h < H; ++h) cp[h] += (hh == h) ? gs[t] * ys[t] : 0.f;
+    }
+    // column 4*c4 -> slice c4 / 16, offset 4 * (c4 % 16)
+    Gs[(int64_t)(c4 >> 4) * sstride4 + (int64_t)row * 16 + (c4 & 15)] =
+        make_float4(gs[0], gs[1], gs[2], gs[3]);
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) cp[h] = wave_sum(cp[h]);
+  if (lane < H) {
+    const int64_t o = (int64_t)row * H + lane;
+    const float dv = den[o];
+    rec[o] = make_float4(s1[o], mrow[o], dv > 0.f ? 1.f / dv : 0.f, hsel<H>(cp, lane));
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void k_gat_bwd_w(const int32_t* __restrict__ rowptrT,
+                                                   const int32_t* __restrict__ colT,
+                                                   const int64_t* __restrict__ permT, int n_rows,
+                                                   const float* __restrict__ s2, float alpha,
+                                                   const float* __restrict__ emask,
+                                                   const float4* __restrict__ rec,
+                                                   float* __restrict__ wT) {
+  const int row = xcd_remap(blockIdx.x, gridDim.x) * 16 + (threadIdx.x >> 4);
+  if (row >= n_rows) return;
+  const int l = threadIdx.x & 15;
+  float sj[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) sj[h] = s2[(int64_t)row * H + h];
+  const int end = rowptrT[row + 1];
+  for (int e = rowptrT[row] + l; e < end; e += 16) {
+    const int i = colT[e];
+    const int64_t pe = emask ? permT[e] : 0;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float4 r = rec[(int64_t)i * H + h];  // {s1_i, m_i, 1/den_i, c_i}
+      const float al = __expf(-lrelu(r.x + sj[h], alpha) - r.y) * r.z;
+      wT[(int64_t)e * H + h] = emask ? al * emask[pe * H + h] : al;
+    }
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
+    const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT, int n_rows, int nbs,
+    int H, int D, int dh, const uint4* __restrict__ Gs, int64_t sstride16,
+    const float* __restrict__ Hm, int64_t ldh, const float* __restrict__ wT,
+    float* __restrict__ dH, int64_t lddh, float* __restrict__ pd, int64_t pstride) {
+  const int b = blockIdx.x;
+  const int s = b / nbs;
+  const int row = xcd_remap(b - s * nbs, nbs) * 4 + wave_id();
+  if (row >= n_rows) return;
+  const int lane = lane_id(), g = lane >> 4, c = lane & 15;
+  const int c0 = s * 64 + 4 * c;
+  const bool own = c0 < D;
+  const int h0 = min((s * 64) / dh, H - 1);
+  const int h1 = min((s * 64 + 63) / dh, H - 1);
+  const bool two = h1 != h0;  // uniform per slice
+  bool second[4];
+  float hj0[4], hj1[4];
+  {
+    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (own) hv = *(const float4*)(Hm + (int64_t)row * ldh + c0);
+    const float v[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      second[t] = (c0 + t) / dh != h0;
+      hj0[t] = second[t] ? 0.f : v[t];
+      hj1[t] = second[t] ? v[t] : 0.f;
+    }
+  }
+  const uint4* X = Gs + (int64_t)s * sstride16 + c;
+  float* pds = pd + (int64_t)s * pstride;
+  const int beg = rowptrT[row], end = rowptrT[row + 1];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int base = beg; base < end; base += 64) {
+    const int cnt = min(64, end - base);
+    int mj = 0;
+    float w0 = 0.f, w1 = 0.f;
+    if (lane < cnt) {
+      mj = colT[base + lane];
+      w0 = wT[(int64_t)(base + lane) * H + h0];
+      w1 = wT[(int64_t)(base + lane) * H + h1];
+    }
+    for (int k = 0; k < cnt; k += 4 * U) {
+      uint4 r[U];
+      float v0[U], v1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = k + 4 * u + g;
+        const int j = __shfl(mj, e & 63, 64);
+        v0[u] = __shfl(w0, e & 63, 64);
+        v1[u] = __shfl(w1, e & 63, 64);
+        if (e < cnt && own) {
+          r[u] = X[(int64_t)j * 16];
+        } else {
+          r[u] = make_uint4(0u, 0u, 0u, 0u);
+          v0[u] = v1[u] = 0.f;
+        }
+      }
+      float q[2 * U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float f[4] = {__builtin_bit_cast(float, r[u].x), __builtin_bit_cast(float, r[u].y),
+                            __builtin_bit_cast(float, r[u].z), __builtin_bit_cast(float, r[u].w)};
+        float qa = 0.f, qb = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          acc[t] = fmaf(second[t] ? v1[u] : v0[u], f[t], acc[t]);
+          qa = fmaf(f[t], hj0[t], qa);
+          qb = fmaf(f[t], hj1[t], qb);
+        }
+        q[u] = qa;
+        q[U + u] = qb;
+      }
+      // per-group sums of the 16 lanes: value v (edge u = v % U, head slot v / U) lands on lane
+      // grp_lane(v) of the group; that lane stores it
+      if (two) {
+        const float sum = grp_sum<2 * U, 16>(q, lane);
+        constexpr int SP = 16 / (2 * U);
+        const int v = c / SP, e = k + 4 * (v % U) + g;
+        if (c % SP == 0 && e < cnt) pds[(int64_t)(base + e) * 2 + v / U] = sum;
+      } else {
+        float qq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) qq[u] = q[u];
+        const float sum = grp_sum<U, 16>(qq, lane);
+        constexpr int SP = 16 / U;
+        const int e = k + 4 * (c / SP) + g;
+        if (c % SP == 0 && e < cnt) pds[(int64_t)(base + e) * 2] = sum;
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] += __shfl_xor(acc[t], 16, 64);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] += __shfl_xor(acc[t], 32, 64);
+  if (g != 0 || !own) return;
+  *(float4*)(dH + (int64_t)row * lddh + c0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void k_gat_bwd_edge(
+    const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT,
+    const int64_t* __restrict__ permT, int n_rows, int S, int D, int dh,
+    const float* __restrict__ s2, float alpha, const float* __restrict__ emask,
+    const float4* __restrict__ rec, const float2* __restrict__ pd, int64_t pstride2,
+    const float* __restrict__ a, float* __restrict__ dH, int64_t lddh, float* __restrict__ dzT,
+    float* __restrict__ ds2) {
+  const int row = xcd_remap(blockIdx.x, gridDim.x) * 16 + (threadIdx.x >> 4);
+  if (row >= n_rows) return;  // whole 16-lane groups leave together
+  const int l = threadIdx.x & 15;
+  float sj[H], d2[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    sj[h] = s2[(int64_t)row * H + h];
+    d2[h] = 0.f;
+  }
+  const int end = rowptrT[row + 1];
+  for (int e = rowptrT[row] + l; e < end; e += 16) {
+    const int i = colT[e];
+    const int64_t pe = emask ? permT[e] : 0;
+    float da[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) da[h] = 0.f;
+    for (int s = 0; s < S; ++s) {  // the head's slice partials in slice order
+      const float2 p = pd[(int64_t)s * pstride2 + e];
+      const int h0 = min((s * 64) / dh, H - 1), h1 = min((s * 64 + 63) / dh, H - 1);
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        if (h == h0) da[h] += p.x;
+        else if (h == h1) da[h] += p.y;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float4 r = rec[(int64_t)i * H + h];
+      const float z = r.x + sj[h];
+      const float al = __expf(-lrelu(z, alpha) - r.y) * r.z;
+      const float ml = emask ? emask[pe * H + h] : 1.f;
+      const float dz = -(al * (ml * da[h] - r.w)) * (z > 0.f ? 1.f : alpha);
+      dzT[(int64_t)e * H + h] = dz;
+      d2[h] += dz;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) d2[h] += __shfl_xor(d2[h], o, 16);
+  }
+  if (l < H) ds2[(int64_t)row * H + l] = hsel<H>(d2, l);
+  if (!dH) return;
+  float* out = dH + (int64_t)row * lddh;
+  for (int c4 = l; 4 * c4 < D; c4 += 16) {
+    float4 v = *(float4*)(out + 4 * c4);
+    float o[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int cc = 4 * c4 + t, h = cc / dh;
+      o[t] += hsel<H>(d2, h) * a[h * 2 * dh + dh + (cc - h * dh)];
+    }
+    *(float4*)(out + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+template <int H, int NCH>
+__global__ __launch_bounds__(256) void k_gat_bwd_dst_s(const int32_t* __restrict__ rowptr,
+                                                       const int64_t* __restrict__ tpos,
+                                                       int n_rows, int D, int dh,
+                                                       const float* __restrict__ dzT,
+                                                       const float* __restrict__ a,
+                                                       const float* __restrict__ ds2,
+                                                       float4* __restrict__ dH, int64_t lddh4,
+                                                       float* __restrict__ ds1) {
+  const int row = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
+  if (row >= n_rows) return;
+  const int lane = lane_id();
+  const int beg = rowptr[row], end = rowptr[row + 1];
+  float4 v[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {  // independent of dz: issued before the gather chain
+    const int c4 = lane + 64 * k;
+    v[k] = 4 * c4 < D ? dH[(int64_t)row * lddh4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float p[H], q[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) p[h] = 0.f;
+  for (int e = beg + lane; e < end; e += 64) {
+    const int64_t t = tpos[e];
+#pragma unroll
+    for (int h = 0; h < H; ++h) p[h] += dzT[t * H + h];
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    p[h] = wave_sum(p[h]);
+    q[h] = ds2 ? ds2[(int64_t)row * H + h] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c4 = lane + 64 * k;
+    if (4 * c4 >= D) continue;
+    float o[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int c = 4 * c4 + t, h = c / dh, d = c - h * dh;
+      o[t] += hsel<H>(p, h) * a[h * 2 * dh + d];
+      if (ds2) o[t] += hsel<H>(q, h) * a[h * 2 * dh + dh + d];
+    }
+    dH[(int64_t)row * lddh4 + c4] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+  if (lane < H) ds1[(int64_t)row * H + lane] = hsel<H>(p, lane);
+}
+
 }  // namespace gnnea
 
 using namespace gnnea;
@@ -187,6 +490,154 @@ extern "C" int gnnea_gat_fwd_sliced_f32(const int32_t* rowptr, const int32_t* co
     hipLaunchKernelGGL((k_gat_fwd_sliced<GNNEA_ACT_IDENTITY, 4, float>), grid, dim3(256), 0, st,
                        rowptr, col, n_rows, nbs, heads, D, d_head, (const uint4*)Hs, sstride / 4,
                        wgt, den_out, Y, ldy);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---- sliced backward entry points -------------------------------------------------------- //
+#define GNNEA_HEADS_SWITCH(CASE) \
+  switch (heads) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
+
+static bool gat_sl_shape(int heads, int d_head, int64_t sstride) {
+  const int D = heads * d_head;
+  return heads >= 1 && heads <= 8 && d_head >= 32 && D % 4 == 0 && D <= 1024 && sstride % 64 == 0;
+}
+
+// G (slice-major [ceil(D/64)][n_rows][64], sstride floats per slice) and the records
+extern "C" int gnnea_gat_bwd_prep_sliced_f32(int32_t n_rows, int heads, int d_head,
+                                             const float* dY, const float* Y, int64_t ldy,
+                                             const float* s1, const float* m, const float* den,
+                                             int act, float* Gs, int64_t sstride, float* rec,
+                                             void* stream) {
+  const int D = heads * d_head;
+  if (n_rows < 0 || !gat_sl_shape(heads, d_head, sstride) || ldy % 4 || ldy < D)
+    return GNNEA_EINVAL;
+  if (act != GNNEA_ACT_IDENTITY && act != GNNEA_ACT_RELU) return GNNEA_EINVAL;
+  if (n_rows == 0) return 0;
+  if (!dY || !Y || !s1 || !m || !den || !Gs || !rec) return GNNEA_EINVAL;
+  if (((uintptr_t)dY | (uintptr_t)Y | (uintptr_t)Gs) & 15) return GNNEA_EALIGN;
+  const int nch = (D / 4 + 63) / 64;
+  const dim3 grid(div_up(n_rows, 4));
+  hipStream_t st = (hipStream_t)stream;
+#define GNNEA_PREP(ACT, HH, NC)                                                              \
+  hipLaunchKernelGGL((k_gat_bwd_prep_s<ACT, HH, NC>), grid, dim3(256), 0, st, n_rows, D,     \
+                     d_head, (const float4*)dY, (const float4*)Y, ldy / 4, s1, m, den,       \
+                     (float4*)Gs, sstride / 4, (float4*)rec)
+#define GNNEA_PREP_NC(ACT, HH)            \
+  switch (nch) {                          \
+    case 1: GNNEA_PREP(ACT, HH, 1); break; \
+    case 2: GNNEA_PREP(ACT, HH, 2); break; \
+    case 3: GNNEA_PREP(ACT, HH, 3); break; \
+    default: GNNEA_PREP(ACT, HH, 4); break; \
+  }
+#define GNNEA_PREP_H(HH)                                                    \
+  case HH:                                                                  \
+    if (act == GNNEA_ACT_RELU) { GNNEA_PREP_NC(GNNEA_ACT_RELU, HH) }        \
+    else { GNNEA_PREP_NC(GNNEA_ACT_IDENTITY, HH) }                         \
+    break;
+  GNNEA_HEADS_SWITCH(GNNEA_PREP_H)
+#undef GNNEA_PREP_H
+#undef GNNEA_PREP_NC
+#undef GNNEA_PREP
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+// source rows j of A^T (one KG block): per-edge weights wT, then the slice passes writing
+// dH_j = sum_i w_ij G_i (row-major, ldh) and the per-slice product partials pd [S][nnzT][2];
+// wT / pd are indexed by the absolute A^T position (rowptrT values), nnzT = A^T's entry count
+extern "C" int gnnea_gat_bwd_src_sliced_f32(const int32_t* rowptrT, const int32_t* colT,
+                                            const int64_t* permT, int32_t n_rows, int heads,
+                                            int d_head, const float* Hm, int64_t ldh,
+                                            const float* s2, float alpha, const float* emask,
+                                            const float* rec, const float* Gs, int64_t sstride,
+                                            float* wT, float* pd, int64_t nnzT, float* dH,
+                                            int64_t lddh, void* stream) {
+  const int D = heads * d_head;
+  if (n_rows < 0 || !gat_sl_shape(heads, d_head, sstride) || ldh % 4 || ldh < D ||
+      lddh % 4 || lddh < D || nnzT < 0)
+    return GNNEA_EINVAL;
+  if (n_rows == 0) return 0;
+  if (!rowptrT || !colT || !Hm || !s2 || !rec || !Gs || !wT || !pd || !dH ||
+      (emask && !permT))
+    return GNNEA_EINVAL;
+  if (((uintptr_t)Hm | (uintptr_t)Gs | (uintptr_t)dH) & 15) return GNNEA_EALIGN;
+  hipStream_t st = (hipStream_t)stream;
+#define GNNEA_W(HH)                                                                           \
+  case HH:                                                                                    \
+    hipLaunchKernelGGL(k_gat_bwd_w<HH>, dim3(div_up(n_rows, 16)), dim3(256), 0, st, rowptrT,  \
+                       colT, permT, n_rows, s2, alpha, emask, (const float4*)rec, wT);        \
+    break;
+  GNNEA_HEADS_SWITCH(GNNEA_W)
+#undef GNNEA_W
+  GNNEA_LAUNCH_CHECK();
+  const int S = div_up(D, 64), nbs = div_up(n_rows, 4);
+  hipLaunchKernelGGL((k_gat_bwd_src_sl<4>), dim3((unsigned)((int64_t)S * nbs)), dim3(256), 0, st,
+                     rowptrT, colT, n_rows, nbs, heads, D, d_head, (const uint4*)Gs,
+                     sstride / 4, Hm, ldh, wT, dH, lddh, pd, 2 * nnzT);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+// dz (A^T order), ds2 and, when dH is non-NULL, dH_j += ds2_j (x) a2 for the source rows
+extern "C" int gnnea_gat_bwd_edge_sliced_f32(const int32_t* rowptrT, const int32_t* colT,
+                                             const int64_t* permT, int32_t n_rows, int heads,
+                                             int d_head, const float* s2, float alpha,
+                                             const float* emask, const float* rec,
+                                             const float* pd, int64_t nnzT, const float* a,
+                                             float* dH, int64_t lddh, float* dzT, float* ds2,
+                                             void* stream) {
+  const int D = heads * d_head;
+  if (n_rows < 0 || !gat_sl_shape(heads, d_head, 64) || nnzT < 0 ||
+      (dH && (lddh % 4 || lddh < D)))
+    return GNNEA_EINVAL;
+  if (n_rows == 0) return 0;
+  if (!rowptrT || !colT || !s2 || !rec || !pd || !a || !dzT || !ds2 || (emask && !permT))
+    return GNNEA_EINVAL;
+  if ((uintptr_t)dH & 15) return GNNEA_EALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  const int S = div_up(D, 64);
+#define GNNEA_E(HH)                                                                             \
+  case HH:                                                                                      \
+    hipLaunchKernelGGL(k_gat_bwd_edge<HH>, dim3(div_up(n_rows, 16)), dim3(256), 0, st, rowptrT, \
+                       colT, permT, n_rows, S, D, d_head, s2, alpha, emask, (const float4*)rec,  \
+                       (const float2*)pd, nnzT, a, dH, lddh, dzT, ds2);                         \
+    break;
+  GNNEA_HEADS_SWITCH(GNNEA_E)
+#undef GNNEA_E
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+// ds1 and dH_i += ds1_i (x) a1 (+ ds2_i (x) a2 when ds2 is non-NULL) for the destination rows
+extern "C" int gnnea_gat_bwd_dst_sliced_f32(const int32_t* rowptr, const int64_t* tpos,
+                                            int32_t n_rows, int heads, int d_head,
+                                            const float* dzT, const float* a, const float* ds2,
+                                            float* dH, int64_t lddh, float* ds1, void* stream) {
+  const int D = heads * d_head;
+  if (n_rows < 0 || !gat_sl_shape(heads, d_head, 64) || lddh % 4 || lddh < D)
+    return GNNEA_EINVAL;
+  if (n_rows == 0) return 0;
+  if (!rowptr || !tpos || !dzT || !a || !dH || !ds1) return GNNEA_EINVAL;
+  if ((uintptr_t)dH & 15) return GNNEA_EALIGN;
+  hipStream_t st = (hipStream_t)stream;
+  const int nch = (D / 4 + 63) / 64;
+  const dim3 grid(div_up(n_rows, 4));
+#define GNNEA_D(HH, NC)                                                                        \
+  hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC>), grid, dim3(256), 0, st, rowptr, tpos, n_rows, D, \
+                     d_head, dzT, a, ds2, (float4*)dH, lddh / 4, ds1)
+#define GNNEA_D_H(HH)                        \
+  case HH:                                   \
+    switch (nch) {                           \
+      case 1: GNNEA_D(HH, 1); break;         \
+      case 2: GNNEA_D(HH, 2); break;         \
+      case 3: GNNEA_D(HH, 3); break;         \
+      default: GNNEA_D(HH, 4); break;        \
+    }                                        \
+    break;
+  GNNEA_HEADS_SWITCH(GNNEA_D_H)
+#undef GNNEA_D_H
+#undef GNNEA_D
   GNNEA_LAUNCH_CHECK();
   return 0;
 }

@@ -617,7 +617,8 @@ static SkArgs sk_args(const gnnea_sinkhorn* p) {
 // others are kept from the round-1 A/B timing (profiles/r01_microbench_sk_variants.json).
 //   row: 0 wave/row CH 8 | 1 wave/row CH 4 | 2 wave/row CH 16 | 3 4 waves/row CH 12 | 4 2 waves/row CH 8
 //   col: 0 fused 16 cols CH 16 | 1 split 64-col CH 8 + combine | 2 fused 8 cols CH 12 | 3 split CH 4
-// Default (0) = fastest measured at B = 3000 (profiles/r01_microbench_sk_variants.json).
+// Row 0 = fastest measured at B = 3000 (profiles/r01_microbench_sk_variants.json); column 0 up
+// to I = 4096, column 1 above (sk_iter_t).
 template <typename T, bool KNOPP>
 static void launch_row(int rv, const T* C, const SkArgs& a, const SkDev& d, int it, int si,
                        int so, hipStream_t s) {
@@ -670,7 +671,15 @@ template <typename T>
 static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t s) {
   SkArgs a = sk_args(p);
   SkDev d = sk_dev(p);
-  const int rv = 0, cv = 0;  // default pass configuration (variant field selects the path)
+  // default pass configuration: the fused column pass serialises I / 64 rows per thread, the
+  // split pass (row splits + combine) fills the chip at large I: 1.065 -> 0.780 ms per KNOPP
+  // iteration at B = 15000, equal within 5 % at B = 3000 (tools/dbg/sk_log_cfg.py)
+  int rv = 0, cv = p->I > 4096 ? 1 : 0;
+  if (const char* e = getenv("GNNEA_SK_LOG_CFG")) {  // tuning override only: 10*row + col
+    const int v = atoi(e);
+    rv = v / 10;
+    cv = v % 10;
+  }
   const dim3 gabs(div_up(p->I, 4));
   const T* C = (const T*)p->C;
   for (int it = first; it < first + count; ++it) {

@@ -940,6 +940,8 @@ def gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha, act, 
     One prep pass over the destination rows (G = dY·act', softmax records), one gather sweep
     over Aᵀ (per source row j: SDDMM, softmax backward, dH_j and ds2_j, no atomics), one pass
     over the destination rows through the transpose position map (ds1_i, dH_{row0+i} += ...).
+    Above the Infinity Cache (use_sliced) G is slice-major and the sweep runs slice by slice
+    (_gat_backward_sliced), as gat_forward does.
     For a row shard dH and da are this shard's partials (summed across the KG group / world by
     the caller)."""
     csrT = csr.transpose()
@@ -949,14 +951,73 @@ def gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha, act, 
         dY = _pad4(dY[:, :D].contiguous(), D, H.dtype)
     N = csr.n_rows
     dev = H.device
-    st = stream_of(dev)
-    G = torch.empty_like(Y)
     rec = torch.empty((N, heads, 4), dtype=torch.float32, device=dev)
     dH = torch.empty_like(H)
     dzT = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=dev)
     ds1 = torch.empty((N, heads), dtype=torch.float32, device=dev)
     ds2 = torch.empty((H.shape[0], heads), dtype=torch.float32, device=dev)
+    if (GAT_SLICED and H.dtype == torch.float32 and d_head >= 32 and D % 4 == 0
+            and Y.shape[1] == D and use_sliced(H.shape[0], D, H.dtype)):
+        _gat_backward_sliced(csr, csrT, H, a32, s1, s2, m, den, Y, dY, heads, d_head,
+                             alpha, act, em, row0, rec, dH, dzT, ds1, ds2)
+    else:
+        _gat_backward_rows(csr, csrT, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha,
+                           act, em, row0, rec, dH, dzT, ds1, ds2)
+    da = None
+    if need_da:
+        # da1[h] = sum_i ds1[i,h] H_{row0+i},h ; da2[h] = sum_j ds2[j,h] H_j,h: one streaming
+        # pass over H each (gnnea_gat_da_*), only the diagonal head blocks
+        p1 = gat_da(H[row0:row0 + N], ds1, heads, d_head)
+        p2 = gat_da(H, ds2, heads, d_head)
+        da = torch.cat([p1.view(heads, d_head), p2.view(heads, d_head)], dim=1)
+    return dH, da
+
+
+def _gat_backward_sliced(csr, csrT, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha,
+                         act, em, row0, rec, dH, dzT, ds1, ds2):
+    """The backward over a slice-major G (gnnea_gat_bwd_*_sliced_f32): G's 64-column slices are
+    256-MB tables per KG that the source-side gathers of one slice pass stay inside."""
+    L = _lib.lib()
+    D = heads * d_head
+    N = csr.n_rows
+    dev = H.device
+    st = stream_of(dev)
+    Gs = sliced_empty(N, D, dev)
+    S = Gs.shape[0]
+    nnzT = csrT.nnz
+    wT = torch.empty((max(nnzT, 1), heads), dtype=torch.float32, device=dev)
+    pd = torch.empty((S, max(nnzT, 1), 2), dtype=torch.float32, device=dev)
+    # ds2 (x) a2 rides the destination pass when source and destination rows coincide
+    fold = row0 == 0 and H.shape[0] == N and csrT.n_rows == N
+    with _lib.on_device(dev):
+        check(L.gnnea_gat_bwd_prep_sliced_f32(
+            N, heads, d_head, ptr(dY), ptr(Y), Y.stride(0), _off(s1, row0), ptr(m), ptr(den),
+            int(act), ptr(Gs), Gs.stride(0), ptr(rec), st))
+        for j0, j1 in _blocks(csrT, Y):  # source rows j of A^T, per KG block
+            check(L.gnnea_gat_bwd_src_sliced_f32(
+                _off32(csrT.rowptr, j0), ptr(csrT.col), ptr(csrT.perm), j1 - j0, heads, d_head,
+                _off(H, j0), H.stride(0), _off(s2, j0), alpha, ptr(em), ptr(rec), ptr(Gs),
+                Gs.stride(0), ptr(wT), ptr(pd), nnzT, _off(dH, j0), dH.stride(0), st))
+        check(L.gnnea_gat_bwd_edge_sliced_f32(
+            ptr(csrT.rowptr), ptr(csrT.col), ptr(csrT.perm), csrT.n_rows, heads, d_head, ptr(s2),
+            alpha, ptr(em), ptr(rec), ptr(pd), nnzT, ptr(a32), None if fold else ptr(dH),
+            dH.stride(0), ptr(dzT), ptr(ds2), st))
+        if csrT.n_rows < H.shape[0]:  # H rows no edge references: no gradient
+            dH[csrT.n_rows:].zero_()
+            ds2[csrT.n_rows:].zero_()
+        check(L.gnnea_gat_bwd_dst_sliced_f32(
+            ptr(csr.rowptr), ptr(csr.tpos()), N, heads, d_head, ptr(dzT), ptr(a32),
+            ptr(ds2) if fold else None, _off(dH, row0), dH.stride(0), ptr(ds1), st))
+
+
+def _gat_backward_rows(csr, csrT, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha,
+                       act, em, row0, rec, dH, dzT, ds1, ds2):
+    """The backward over row-major G (gnnea_gat_bwd_prep / _src / _dst)."""
     tpos = csr.tpos()
+    N = csr.n_rows
+    dev = H.device
+    st = stream_of(dev)
+    G = torch.empty_like(Y)
     with _lib.on_device(dev):
         # G = dL/dh' and the per-node record {s1, m, 1/den, G.h'} (relu / identity: Y = h')
         check(_gat_fn("gnnea_gat_bwd_prep", H.dtype)(
@@ -974,14 +1035,6 @@ def gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha, act, 
         check(_gat_fn("gnnea_gat_bwd_dst", H.dtype)(
             ptr(csr.rowptr), ptr(tpos), N, heads, d_head, ptr(dzT), ptr(a32), _off(dH, row0),
             dH.stride(0), ptr(ds1), st))
-    da = None
-    if need_da:
-        # da1[h] = sum_i ds1[i,h] H_{row0+i},h ; da2[h] = sum_j ds2[j,h] H_j,h: one streaming
-        # pass over H each (gnnea_gat_da_*), only the diagonal head blocks
-        p1 = gat_da(H[row0:row0 + N], ds1, heads, d_head)
-        p2 = gat_da(H, ds2, heads, d_head)
-        da = torch.cat([p1.view(heads, d_head), p2.view(heads, d_head)], dim=1)
-    return dH, da
 
 
 def gat_da(H, ds, heads, d_head):

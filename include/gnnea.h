@@ -203,6 +203,36 @@ int gnnea_gat_fwd_sliced_f32(const int32_t* rowptr, const int32_t* col, int32_t 
                              const float* s1, const float* s2, float alpha,
                              const float* edge_mask, int act, float* Y, int64_t ldy,
                              float* m_out, float* den_out, float* wgt, void* stream);
+/* The backward over a slice-major G (fp32, d_head >= 32, heads <= 8, D % 4 == 0, D <= 1024):
+ *   prep_sliced (dest rows i): G = dY * act'(Y) into Gs ([ceil(D/64)][n_rows][64], sstride
+ *                floats per slice) and the records rec (n_rows x heads x 4: s1, m, 1/den, G.h');
+ *   src_sliced  (source rows j of A^T, one KG block per call): per-edge weights wT (nnzT x heads,
+ *                by A^T position), then slice by slice dH_j = sum_i w_ij G_i (row-major) and the
+ *                slice partials of G_i,h . H_j,h in pd (ceil(D/64) x nnzT x 2);
+ *   edge_sliced (source rows): dzT (A^T order), ds2, and dH_j += ds2_j (x) a2 when dH != NULL;
+ *   dst_sliced  (dest rows): ds1 (dzT through tpos, the A -> A^T position map) and
+ *                dH_i += ds1_i (x) a1 (+ ds2_i (x) a2 when ds2 != NULL).
+ * Same results as prep / src / dst below up to fp32 summation order (att_layers.py:38-58). */
+int gnnea_gat_bwd_prep_sliced_f32(int32_t n_rows, int heads, int d_head, const float* dY,
+                                  const float* Y, int64_t ldy, const float* s1, const float* m,
+                                  const float* den, int act, float* Gs, int64_t sstride,
+                                  float* rec, void* stream);
+int gnnea_gat_bwd_src_sliced_f32(const int32_t* rowptrT, const int32_t* colT,
+                                 const int64_t* permT, int32_t n_rows, int heads, int d_head,
+                                 const float* Hm, int64_t ldh, const float* s2, float alpha,
+                                 const float* edge_mask, const float* rec, const float* Gs,
+                                 int64_t sstride, float* wT, float* pd, int64_t nnzT, float* dH,
+                                 int64_t lddh, void* stream);
+int gnnea_gat_bwd_edge_sliced_f32(const int32_t* rowptrT, const int32_t* colT,
+                                  const int64_t* permT, int32_t n_rows, int heads, int d_head,
+                                  const float* s2, float alpha, const float* edge_mask,
+                                  const float* rec, const float* pd, int64_t nnzT,
+                                  const float* a, float* dH, int64_t lddh, float* dzT,
+                                  float* ds2, void* stream);
+int gnnea_gat_bwd_dst_sliced_f32(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows,
+                                 int heads, int d_head, const float* dzT, const float* a,
+                                 const float* ds2, float* dH, int64_t lddh, float* ds1,
+                                 void* stream);
 /* Backward in one gather sweep over A^T (autograd of att_layers.py:38-58):
  *  prep (rows i):   G_i = dY_i * act'(Y_i) (act: identity / relu, Y = h' there) and the per-node
  *                   record rec[i,h] = {s1, m, 1/den, c = G_i,h . h'_i,h}  (float4 per head);

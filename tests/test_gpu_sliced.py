@@ -403,3 +403,51 @@ def test_gemm_x3_dual_output(device, M, N, K, bias):
         for s in range(xs.shape[0]))
     ref64 = a.double() @ b.double() + (bb.double() if bias else 0)
     assert rel_err(y.cpu(), ref64.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("heads,d_head,act,mask,row0", [
+    (4, 75, 1, True, 0), (2, 64, 0, False, 0), (1, 300, 1, True, 0), (8, 32, 1, False, 0),
+    (3, 48, 1, True, 0), (4, 75, 1, True, 300), (2, 64, 0, False, 250)])
+def test_gat_bwd_sliced_vs_rowmajor(device, monkeypatch, heads, d_head, act, mask, row0):
+    """gnnea_gat_bwd_{prep,src,edge,dst}_sliced_f32 (G slice-major, per-slice product partials
+    summed per head in slice order) against the row-major backward on the same forward records:
+    dH and da.  row0 > 0: a row shard (destination rows row0.. of a wider H, ds2 (x) a2 applied
+    by the edge pass instead of the destination pass)."""
+    from gnnea import ops
+    from gnnea.graph import DeviceCSR
+    rng = np.random.default_rng(heads * 1000 + d_head + row0)
+    n = 1500
+    N = n if row0 == 0 else 700
+    D = heads * d_head
+    r = rng.integers(0, N, 14000)
+    c = rng.integers(0, n, 14000)
+    keep = (r > 2) & (r < N - 2)
+    r = np.concatenate([r[keep], np.full(200, 9)])  # one row with several 64-edge chunks
+    c = np.concatenate([c[keep], rng.integers(0, n, 200)])
+    c[:50] = 7  # and a source row with many in-edges
+    v = np.ones(r.size, np.float32)
+    csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                             torch.from_numpy(v).to(device), N, n)
+    H = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32) * 0.5).to(device)
+    a32 = torch.from_numpy(rng.standard_normal((heads, 2 * d_head)).astype(np.float32)
+                           * 0.3).to(device)
+    em = None
+    if mask:
+        em = torch.from_numpy(((rng.random((csr.nnz, heads)) > 0.3) / 0.7).astype(np.float32)
+                              ).to(device)
+    monkeypatch.setattr(ops, "GAT_SLICED", False)
+    Y, m, den, s1, s2 = ops.gat_forward(csr, H, a32, heads, d_head, 0.2, act, em, row0=row0)
+    dY = torch.from_numpy(rng.standard_normal((N, D)).astype(np.float32)).to(device)
+    dH_r, da_r = ops.gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, 0.2, act,
+                                  em, row0=row0)
+    calls = []
+    orig = ops._gat_backward_sliced
+    monkeypatch.setattr(ops, "_gat_backward_sliced",
+                        lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+    monkeypatch.setattr(ops, "GAT_SLICED", True)
+    monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 1)
+    dH_s, da_s = ops.gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, 0.2, act,
+                                  em, row0=row0)
+    assert calls, "the sliced backward was not taken"
+    assert rel_err(dH_s.cpu(), dH_r.cpu()) < 1e-5
+    assert rel_err(da_s.cpu(), da_r.cpu()) < 1e-5
