@@ -114,16 +114,22 @@ def sinkhorn_rate(device, B=3000, reg=0.01, n0=100, n1=1100, variant=None):
 
 
 def sinkhorn_large(device):
-    """B = 15000 (J > 8192: the fused log-domain passes, nothing I x J kept): marginal iters/s
-    and the bandwidth of the C stream (fp32 C read twice per iteration: the row pass and the
-    column pass, 2 * I * J * 4 bytes)."""
-    r = sinkhorn_rate(device, B=15000, n0=20, n1=120)
+    """B = 15000 through the default path (the scaling form with the fp64 K resident, one sweep
+    per iteration: I * J * 8 bytes of K per iteration) and through the log-domain passes (variant
+    1: fp32 C read twice per iteration, 2 * I * J * 4 bytes, exp-bound): marginal iters/s."""
     B = 15000
-    per_it = 2 * B * B * 4
-    r["bytes_per_iter"] = per_it
-    r["GBps_knopp"] = round(r["iters_per_s"]["ot_loss.sinkhorn"] * per_it / 1e9, 1)
-    r["bound"] = ("fp64 exp (VALU): 2 * I * J exponentials per iteration; the C stream alone "
-                  "would allow %.0f iters/s at 8 TB/s" % (8e12 / per_it))
+    r = sinkhorn_rate(device, B=B, n0=20, n1=120)
+    k_bytes = B * B * 8
+    r["path"] = "scaling form, fp64 K resident (k_sk_sweep, wide: column scaling in LDS)"
+    r["bytes_per_iter"] = k_bytes
+    r["GBps_knopp"] = round(r["iters_per_s"]["ot_loss.sinkhorn"] * k_bytes / 1e9, 1)
+    r["bound"] = ("HBM: the K stream (%.2f GB per iteration; %.0f iters/s at 8 TB/s)"
+                  % (k_bytes / 1e9, 8e12 / k_bytes))
+    lg = sinkhorn_rate(device, B=B, n0=20, n1=120, variant=1)
+    c_bytes = 2 * B * B * 4
+    r["logdomain"] = {"iters_per_s": lg["iters_per_s"], "bytes_per_iter": c_bytes,
+                      "bound": "fp64 exp (VALU): 2 * I * J exponentials per iteration (the fp32 "
+                               "C stream alone would allow %.0f iters/s)" % (8e12 / c_bytes)}
     return r
 
 

@@ -28,9 +28,10 @@ namespace gnnea {
 constexpr double kBig = 1e20;   // sinkhorn_loss.py:11
 constexpr double kHuge = 1e30;  // sinkhorn_loss.py:12
 constexpr int kSweepWaves = 8;  // waves (rows per group) of a sweep workgroup
-// widest J the fused sweep serves: its column slices live in registers (NCM <= 16); beyond it the
-// log-domain passes are faster (B = 15000: 1.07 vs 1.22 ms per iteration, measured)
-constexpr int kMaxJ = 64 * kSweepWaves * 16;
+// widest J the fused sweep serves: its column slices live in registers (NCM <= 32 per lane; above
+// 16 the column scaling moves to LDS so the K double buffer still fits); beyond it the log-domain
+// passes take over
+constexpr int kMaxJ = 64 * kSweepWaves * 32;
 constexpr int kMaxSweepWg = 64 * 8;  // column partials the update kernel sums in one round
 
 enum { ST_DONE = 0, ST_ITERS = 1, ST_REASON = 2, ST_SLOT = 3, ST_BIG = 4, ST_FAIL = 5 };
@@ -71,7 +72,8 @@ static SkWs sk_plan(int I, int J) {
   w.rowbuf = o; o = al256(o + 8ll * I);
   w.part = o; o = al256(o + 8ll * w.ns * J);
   w.errpart = o; o = al256(o + 8ll * w.nfin);
-  w.K = o; o = al256(o + 8ll * I * J);
+  // + 64 KB: the wide sweep's unclamped loads run up to ~2,600 elements past the last row's end
+  w.K = o; o = al256(o + 8ll * I * J + 65536);
   w.total = o;
   return w;
 }
@@ -230,34 +232,55 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d
                                                                const double* __restrict__ yin,
                                                                int gate) {
   constexpr int G = NCM <= 8 ? 32 / NCM : (NCM <= 16 ? 2 : 1);  // rows per group
+  // NCM > 16 (J > 8192): the wave's slice of the column scaling x lives in LDS (each lane reads
+  // back only what it wrote: no barrier), which keeps K double-buffered in registers
+  constexpr bool XL = NCM > 16;
   __shared__ double red[2][kSweepWaves][G];
+  __shared__ double xsh[XL ? kSweepWaves * NCM * 64 : 1];
   const int w = wave_id(), lane = lane_id();
   const int wg = blockIdx.x;
   const int r0 = wg * a.rpw, r1 = min(a.I, r0 + a.rpw);
   const int cw = ((a.J + kSweepWaves - 1) / kSweepWaves + 63) & ~63;
   const int c0 = w * cw;
-  bool ok[NCM];
-  double xs[NCM], acc[NCM];
+  bool ok[XL ? 1 : NCM];
+  double xs[XL ? 1 : NCM], acc[NCM];
   const double* __restrict__ x = d.v + (int64_t)slot_in * a.J;
 #pragma unroll
   for (int k = 0; k < NCM; ++k) {
     const int c = c0 + 64 * k + lane;
-    ok[k] = 64 * k < cw && c < a.J;
-    xs[k] = (PH1 && ok[k]) ? x[c] : 0.0;
+    const bool okk = 64 * k < cw && c < a.J;
+    if constexpr (!XL) ok[k] = okk;
+    const double xv = (PH1 && okk) ? x[c] : 0.0;
+    if constexpr (XL) xsh[(w * NCM + k) * 64 + lane] = xv;
+    else xs[k] = xv;
     acc[k] = 0.0;
   }
+  auto xs_at = [&](int k) -> double {
+    if constexpr (XL) return xsh[(w * NCM + k) * 64 + lane];
+    else return xs[k];
+  };
   // branch-free loads: out-of-range rows / columns read a clamped in-range address, then zero
-  int cidx[NCM];
+  // (XL: indices and masks recomputed per load instead of held in 2 * NCM registers)
+  int cidx[XL ? 1 : NCM];
+  if constexpr (!XL) {
 #pragma unroll
-  for (int k = 0; k < NCM; ++k) cidx[k] = min(c0 + 64 * k + lane, a.J - 1);
+    for (int k = 0; k < NCM; ++k) cidx[k] = min(c0 + 64 * k + lane, a.J - 1);
+  }
+  // XL validity of column c0 + 64 k + lane as one compare: 64 k < lim (inside the wave's slice and J)
+  const int lim = min(c0 + cw, a.J) - c0 - lane;
   auto load = [&](double (&kv)[G][NCM], int g0) {
 #pragma unroll
     for (int r = 0; r < G; ++r) {
       const double* __restrict__ Kr = d.K + (int64_t)min(g0 + r, r1 - 1) * a.J;
 #pragma unroll
       for (int k = 0; k < NCM; ++k) {
-        const double t = Kr[cidx[k]];
-        kv[r][k] = ok[k] ? t : 0.0;
+        if constexpr (XL) {  // unclamped: one base + immediate offsets (K is padded, sk_plan)
+          const double t = Kr[c0 + 64 * k + lane];
+          kv[r][k] = 64 * k < lim ? t : 0.0;
+        } else {
+          const double t = Kr[cidx[k]];
+          kv[r][k] = ok[k] ? t : 0.0;
+        }
       }
     }
   };
@@ -271,7 +294,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d
         if (r < nr) {
           const double inva = KNOPP ? 1.0 / a.a[g0 + r] : 1.0;
 #pragma unroll
-          for (int k = 0; k < NCM; ++k) p = fma(KNOPP ? inva * kv[r][k] : kv[r][k], xs[k], p);
+          for (int k = 0; k < NCM; ++k) p = fma(KNOPP ? inva * kv[r][k] : kv[r][k], xs_at(k), p);
         }
         p = wave_sum_f64(p);
         if (lane == 0) red[par][w][r] = p;
@@ -330,7 +353,7 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d
   double* __restrict__ part = d.part + (int64_t)wg * a.J + c0 + lane;
 #pragma unroll
   for (int k = 0; k < NCM; ++k)
-    if (ok[k]) part[64 * k] = acc[k];
+    if (64 * k < cw && c0 + 64 * k + lane < a.J) part[64 * k] = acc[k];
 }
 
 // Column update: s_j = sum_q part[q][j], then

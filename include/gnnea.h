@@ -363,7 +363,7 @@ int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64
  *   GNNEA_SK_RELAX : SinkhornOT/sinkhorn_loss.py:291-356 forward_relax_sinkhorn_iteration
  * The cost may be stored fp32 (widened exactly, as the reference's .type(torch.DoubleTensor)) or
  * fp64.  Default path: the fp64 kernel matrix K (I*J*8 bytes) lives in `ws`, built once (KNOPP) or
- * at every absorption (STAB family), one sweep over it per iteration.  variant 1 (or J > 8192):
+ * at every absorption (STAB family), one sweep over it per iteration.  variant 1 (or J > 16384):
  * log-domain passes with online log-sum-exp, nothing I*J-sized kept.  The host drives the data-dependent loop with
  * gnnea_sinkhorn_iterate() batches and reads the status block (first GNNEA_SK_STATUS_BYTES of ws)
  * between batches.  Kernels of an iteration after the stop condition are no-ops, so
@@ -400,9 +400,9 @@ typedef struct gnnea_sinkhorn {
   double tol;       /* stopThr (KNOPP) or tol */
   int max_iter;     /* numItermax / numIterMax */
   int iters_run;    /* iterations enqueued so far (read by gnnea_sinkhorn_finish) */
-  int variant;      /* 0: scaling form with the fp64 K resident in ws (J <= 8192);
+  int variant;      /* 0: scaling form with the fp64 K resident in ws (J <= 16384);
                        1: fused log-domain passes recomputing every term from C (no I*J state,
-                       any J; used automatically above J = 8192) */
+                       any J; used automatically above J = 16384) */
   int reserved;
   void* ws;         /* device workspace of gnnea_sinkhorn_ws_bytes(I, J) bytes */
 } gnnea_sinkhorn;

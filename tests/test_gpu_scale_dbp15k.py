@@ -166,10 +166,14 @@ def test_sinkhorn_B3000_vs_reference(golden, device, sk_path):
     assert rel_err(K[0].sum(0).cpu(), f["B3000_stab_Kcolsum"]) < TOL64
 
 
-def test_sinkhorn_B15000_vs_reference(golden, device):
-    """B = 15000 (J > 8192: the fused log-domain passes, no I x J workspace) vs the reference's
-    scaling-form run of utils/ot_loss.sinkhorn: plan rows, marginals, loss."""
+@pytest.mark.parametrize("variant", [0, 1], ids=["scaling", "logdomain"])
+def test_sinkhorn_B15000_vs_reference(golden, device, monkeypatch, variant):
+    """B = 15000 vs the reference's scaling-form run of utils/ot_loss.sinkhorn: plan rows,
+    marginals, loss — through the resident-K scaling form (the wide sweep: J > 8192 keeps the
+    column scaling in LDS) and through the fused log-domain passes (no I x J workspace)."""
+    import gnnea.sinkhorn
     from utils.ot_loss import sinkhorn
+    monkeypatch.setattr(gnnea.sinkhorn, "DEFAULT_VARIANT", variant)
     f = golden("sinkhorn_scale")
     B = 15000
     M = si.sinkhorn_cost(B).to(device)
@@ -179,3 +183,22 @@ def test_sinkhorn_B15000_vs_reference(golden, device):
     assert rel_err(P.sum(1).cpu(), f["B15000_knopp_rowsum"]) < TOL64
     assert rel_err(P.sum(0).cpu(), f["B15000_knopp_colsum"]) < TOL64
     assert abs(loss.item() - float(f["B15000_knopp_loss"])) <= TOL64 * abs(loss.item())
+
+
+@pytest.mark.parametrize("I,J", [(9000, 9000), (4000, 16384), (700, 12001)])
+def test_sinkhorn_wide_sweep_matches_logdomain(device, I, J):
+    """The scaling form's wide sweep (8192 < J <= 16384: column scaling in LDS, unclamped K
+    loads into the padded workspace) against the log-domain passes, KNOPP and STAB: same
+    iteration counts and stop reasons, plans within fp64 reassociation."""
+    from gnnea import _lib
+    from gnnea.sinkhorn import solve
+    g = torch.Generator(device="cpu").manual_seed(I + J)
+    M = torch.rand(I, J, generator=g, dtype=torch.float64).to(device)
+    for mode, w in ((_lib.GNNEA_SK_KNOPP, 1.0), (_lib.GNNEA_SK_STAB, None)):
+        a = torch.full((I,), w if w else 1.0 / I, dtype=torch.float64, device=device)
+        b = torch.full((J,), w if w else 1.0 / J, dtype=torch.float64, device=device)
+        r0 = solve(mode, M, a, b, 0.02, 1e-9, 120, variant=0)
+        r1 = solve(mode, M, a, b, 0.02, 1e-9, 120, variant=1)
+        assert (r0.iters, r0.reason) == (r1.iters, r1.reason), mode
+        assert rel_err(r0.plan.cpu(), r1.plan.cpu()) < 1e-11, mode
+        assert rel_err(r0.col_sum.cpu(), r1.col_sum.cpu()) < 1e-11, mode
