@@ -593,6 +593,7 @@ struct X3P {
   static constexpr int STAGE = DMA_BYTES > EPI_BYTES ? DMA_BYTES : (EPI_BYTES + 1023) / 1024 * 1024;
   static constexpr int LOADS = A_CHUNKS / NW + B_CHUNKS_PAD / NW;  // DMA instr. / wave / stage
   // ring stages: 4 when they fit one workgroup per CU (NW = 8), 3 for two per CU (NW = 4)
+  // (a 5-stage ring, which fits 160 KB at WT = 5, measured no faster: 2.52 vs 2.50 ms)
   static constexpr int NS = NW == 8 ? (4 * STAGE <= 160 * 1024 ? 4 : 3) : 3;
   static_assert(A_CHUNKS == 2 * NW, "A: two 1-KB chunks per wave");
 };
@@ -659,7 +660,9 @@ __device__ __forceinline__ void store_tile_v4(const f32x16& acc, uint32_t region
 // stages are in flight while the last ones of the current tile are multiplied) and a tile's
 // epilogue (16-B stores through LDS) is written while the next tile's stages land.
 template <int WT, int NW, int MODE = 0>  // MODE (timing experiments only): 1 = no MFMA,
-                            // 2 = no DMA, 3 = no DMA and no A split, 4 = no DMA and no epilogue stores
+                            // 2 = no DMA, 3 = no DMA and no A split, 4 = no DMA and no epilogue
+                            // stores, 8 = every epilogue store to the 1-KB dummy (no C traffic), 9 = DMA on, no
+                            // epilogue stores
 __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const float* __restrict__ A,
                                                   int64_t lda, const bf16_t* __restrict__ Bp,
                                                   int64_t ldp, int64_t pstride,
@@ -748,7 +751,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
   auto epilogue = [&](int q, int buf) {
     int m0, n0;
     tile_of(q, m0, n0);
-    if (MODE == 4) {  // timing experiment: one store per wave keeps the accumulators live
+    if (MODE == 4 || MODE == 9) {  // timing experiment: one store per wave keeps the accumulators live
       float t = 0.f;
 #pragma unroll
       for (int qq = 0; qq < WT; ++qq)
@@ -760,12 +763,12 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
     const uint32_t region = smem_lds + buf * G::STAGE + w * 32 * G::EPI_LD * 4;
 #pragma unroll
     for (int t = 0; t < WT; ++t)
-      store_tile_v4<G::EPI_LD>(acc[t], region, M, N, m0 + w * 32, n0 + 32 * t, kh, li, lane, beta, C, ldc,
+      store_tile_v4<G::EPI_LD>(acc[t], region, MODE == 8 ? 0 : M, N, m0 + w * 32, n0 + 32 * t, kh, li, lane, beta, C, ldc,
                     cs, vec4 != 0, dummy, C2, cs2);
   };
   // vmcnt allowance for the first step after an epilogue: its 16-B stores (exactly 4 per tile
   // of 32 columns when vec4 and no beta loads) were issued after the DMA that step waits for
-  const bool count_stores = vec4 != 0 && beta == 0.f && MODE != 4 &&
+  const bool count_stores = vec4 != 0 && beta == 0.f && MODE != 4 && MODE != 9 &&
                             G::LOADS * (NS - 2) + (C2 ? 8 : 4) * WT <= 63;
 
 #pragma unroll
@@ -805,7 +808,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
     }
-    if (MODE < 2 && g + NS - 1 < total) issue_next(prev);
+    if ((MODE < 2 || MODE >= 8) && g + NS - 1 < total) issue_next(prev);
     const uint32_t st = smem_lds + cur * G::STAGE;
     const f32x4_t x0 = ds_read128f(st + a_off0);
     const f32x4_t x1 = ds_read128f(st + a_off1);
@@ -1177,6 +1180,8 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
       if (W == 5 && mode == 1) GNNEA_X3P_L(W, 8, 1);                                             \
       else if (W == 5 && mode == 2) GNNEA_X3P_L(W, 8, 2);                                        \
       else if (W == 5 && mode == 4) GNNEA_X3P_L(W, 8, 4);                                        \
+      else if (W == 5 && mode == 8) GNNEA_X3P_L(W, 8, 8);                                        \
+      else if (W == 5 && mode == 9) GNNEA_X3P_L(W, 8, 9);                                        \
       else GNNEA_X3P_L(W, 8, 0);                                                                 \
     } else {                                                                                     \
       if (W == 5 && mode == 1) GNNEA_X3P_L(W, 4, 1);                                             \
