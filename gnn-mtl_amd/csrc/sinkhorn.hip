@@ -226,7 +226,9 @@ __device__ __forceinline__ bool knopp_stop(const SkArgs& a, SkDev& d, int it) {
 //   !PH1: y_r = yin[r] (column sums of the final plan);
 // then the same registers accumulate acc_j += y_r K_rj: part[wg][j] = sum over the workgroup's
 // rows, in row order.  K is read exactly once.
-template <bool KNOPP, bool PH1, int NCM>
+// PW: the row exponent p_row may differ from 1 (GEN): only then does the sweep contain pow's
+// out-of-line call, whose register saves would otherwise spill the K double buffer in the loop
+template <bool KNOPP, bool PH1, int NCM, bool PW = false>
 __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d, int it,
                                                                int slot_in, int slot_out,
                                                                const double* __restrict__ yin,
@@ -311,7 +313,8 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d
           if (KNOPP) {
             y = 1.0 / sum;  // u = 1 / (Kp v)
           } else {
-            y = myclamp(powp(a.a[g0 + r] / sum, a.p_row));  // a = clamp((mu / K b)^p)
+            const double qr = a.a[g0 + r] / sum;  // a = clamp((mu / K b)^p)
+            y = myclamp(PW ? powp(qr, a.p_row) : qr);
           }
           if (w == 0 && lane == r) {
             d.u[(int64_t)slot_out * a.I + g0 + r] = y;
@@ -562,19 +565,28 @@ static bool sk_valid(const gnnea_sinkhorn* p) {
   return true;
 }
 
-template <bool KNOPP, bool PH1>
-static void launch_sweep(const SkArgs& a, const SkDev& d, int it, int si, int so, const double* yin,
-                         int gate, hipStream_t s) {
+template <bool KNOPP, bool PH1, bool PW>
+static void launch_sweep_pw(const SkArgs& a, const SkDev& d, int it, int si, int so,
+                            const double* yin, int gate, hipStream_t s) {
   const dim3 g(a.ns), b(64 * kSweepWaves);
   const int nc = (((a.J + kSweepWaves - 1) / kSweepWaves + 63) & ~63) / 64;
   if (nc <= 4)
-    hipLaunchKernelGGL((k_sk_sweep<KNOPP, PH1, 4>), g, b, 0, s, a, d, it, si, so, yin, gate);
+    hipLaunchKernelGGL((k_sk_sweep<KNOPP, PH1, 4, PW>), g, b, 0, s, a, d, it, si, so, yin, gate);
   else if (nc <= 8)
-    hipLaunchKernelGGL((k_sk_sweep<KNOPP, PH1, 8>), g, b, 0, s, a, d, it, si, so, yin, gate);
+    hipLaunchKernelGGL((k_sk_sweep<KNOPP, PH1, 8, PW>), g, b, 0, s, a, d, it, si, so, yin, gate);
   else if (nc <= 16)
-    hipLaunchKernelGGL((k_sk_sweep<KNOPP, PH1, 16>), g, b, 0, s, a, d, it, si, so, yin, gate);
+    hipLaunchKernelGGL((k_sk_sweep<KNOPP, PH1, 16, PW>), g, b, 0, s, a, d, it, si, so, yin, gate);
   else
-    hipLaunchKernelGGL((k_sk_sweep<KNOPP, PH1, 32>), g, b, 0, s, a, d, it, si, so, yin, gate);
+    hipLaunchKernelGGL((k_sk_sweep<KNOPP, PH1, 32, PW>), g, b, 0, s, a, d, it, si, so, yin, gate);
+}
+
+template <bool KNOPP, bool PH1>
+static void launch_sweep(const SkArgs& a, const SkDev& d, int it, int si, int so, const double* yin,
+                         int gate, hipStream_t s) {
+  if (!KNOPP && PH1 && a.p_row != 1.0)
+    launch_sweep_pw<KNOPP, PH1, true>(a, d, it, si, so, yin, gate, s);
+  else
+    launch_sweep_pw<KNOPP, PH1, false>(a, d, it, si, so, yin, gate, s);
 }
 
 template <typename T>

@@ -1,3 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-for m in 0 9 4 8 9; do GNNEA_X3P_MODE=$m timeout -k 10 100 python tools/dbg/x3_modes.py || exit 1; done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_scale_dbp15k.py tests/test_gpu_parity.py tests/test_gpu_sinkhorn_shard.py -x -q -k "sinkhorn or gw or fgw" --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/sk_tests.log 2>&1; rc=$?; tail -3 gpurun_out/sk_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/dbg/sk_wide.py 2>&1 | grep -v amdgpu.ids
