@@ -143,8 +143,13 @@ def sinkhorn_sharded(device, rank, world, B=15000, reg=0.01, n0=20, n1=120):
     Y = (0.05 * torch.randn(B, 300, generator=g)).to(device)
     r0, r1 = B * rank // world, B * (rank + 1) // world
     M = torch.cdist(X[r0:r1], Y)
-    mx = M.max().reshape(1)
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    host = dist.get_backend() == "gloo"  # --rehearse: the logic on one device, host-staged
+
+    def allreduce_max(t):
+        t = t.cpu() if host else t
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.to(device)
+    mx = allreduce_max(M.max().reshape(1))
     M = (M / mx).contiguous()
     del X, Y
     a = torch.ones(r1 - r0, dtype=torch.float64, device=device)
@@ -156,8 +161,8 @@ def sinkhorn_sharded(device, rank, world, B=15000, reg=0.01, n0=20, n1=120):
         t0 = time.perf_counter()
         res = solve_row_sharded(M, a, b, reg, -1.0, n_it, want_plan=False)
         torch.cuda.synchronize()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = allreduce_max(torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                                       device=device))
         assert res.iters == n_it, (res.iters, n_it)
         ts.append(t.item())
     return {"iters_per_s": round((n1 - n0) / (ts[2] - ts[1]), 1), "B": B, "reg": reg,
@@ -466,8 +471,8 @@ def main():
         except Exception as e:  # report, never hide
             train = {"error": repr(e)}
     sk_shard = None
-    if world > 1 and not args.no_sinkhorn and not args.rehearse:
-        try:
+    if world > 1 and not args.no_sinkhorn:
+        try:  # (--rehearse: the code path only; the rate means nothing there)
             sk_shard = sinkhorn_sharded(device, rank, world)
         except Exception as e:  # report, never hide
             sk_shard = {"error": repr(e)}
