@@ -34,7 +34,7 @@ constexpr int kSweepWaves = 8;  // waves (rows per group) of a sweep workgroup
 constexpr int kMaxJ = 64 * kSweepWaves * 32;
 constexpr int kMaxSweepWg = 64 * 8;  // column partials the update kernel sums in one round
 
-enum { ST_DONE = 0, ST_ITERS = 1, ST_REASON = 2, ST_SLOT = 3, ST_BIG = 4, ST_FAIL = 5 };
+enum { ST_DONE = 0, ST_ITERS = 1, ST_REASON = 2, ST_SLOT = 3, ST_BIG = 4, ST_FAIL = 5, ST_UFAIL = 6 };
 enum { SD_ERR = GNNEA_SK_SD_ERR, SD_TPREV = GNNEA_SK_SD_TPREV, SD_LOSS = GNNEA_SK_SD_LOSS,
        SD_TOL = GNNEA_SK_SD_TOL, SD_TNEW = GNNEA_SK_SD_TNEW };
 
@@ -80,6 +80,8 @@ static SkWs sk_plan(int I, int J) {
 
 struct SkArgs {
   int mode, I, J, ns, nfin, rpw;
+  int ig;     // rows of the whole problem (u0 = 1/ig); I unless the rows are sharded
+  int shard;  // row-sharded (gnnea_sinkhorn_shard_*): a bad u is flagged, not decided locally
   int64_t ldc;
   double eps, p_row, p_col;
   const double *a, *b;  // source / target weights (a, b or mu, nu)
@@ -124,6 +126,8 @@ static SkArgs sk_args(const gnnea_sinkhorn* p) {
   a.p_col = (gen || relax) ? p->p : 1.0;
   a.a = p->a;
   a.b = p->b;
+  a.ig = p->I;
+  a.shard = 0;
   return a;
 }
 
@@ -318,7 +322,10 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d
           }
           if (w == 0 && lane == r) {
             d.u[(int64_t)slot_out * a.I + g0 + r] = y;
-            if (KNOPP && (y != y || isinf(y))) mark_done(d.st, it, 2, (it + 1) & 1);
+            if (KNOPP && (y != y || isinf(y))) {
+              if (a.shard) atomicOr((unsigned long long*)&d.st[ST_UFAIL], 1ull);  // all ranks decide
+              else mark_done(d.st, it, 2, (it + 1) & 1);
+            }
             if (!KNOPP && y > kBig) atomicOr((unsigned long long*)&d.st[ST_BIG], 1ull);
           }
         }
@@ -492,7 +499,7 @@ __global__ void k_sk_init(SkArgs a, SkDev d, double tol) {
   for (int i = t; i < a.I; i += gridDim.x * blockDim.x) {
     d.pu[i] = 0.0;
     d.u[i] = 0.0;
-    d.u[a.I + i] = knopp ? 1.0 / (double)a.I : 1.0;
+    d.u[a.I + i] = knopp ? 1.0 / (double)a.ig : 1.0;
   }
   for (int j = t; j < a.J; j += gridDim.x * blockDim.x) {
     d.pv[j] = 0.0;
@@ -617,6 +624,172 @@ static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t 
   }
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------- //
+// §8e, row-sharded KNOPP in the scaling form (the dispatch of gnnea_sinkhorn_shard_*,
+// sinkhorn_shard.hip, for J <= kMaxJ): every rank keeps the fp64 K of its rows resident and runs
+// the same fused sweep; the sweep's column partials of K^T u are summed over the rank's
+// workgroups in order (k_sk_shard_combine) into one J-row, the rows of all ranks are all-gathered
+// by the caller and summed in rank order (k_sk_shard_colfin), so v and every stop decision are
+// bit-identical on all ranks.  A bad u (inf / NaN) is flagged (ST_UFAIL), travels with the
+// rank's row and ends the loop one iteration later on every rank, reverting to iterate it-2 (the
+// merge then leaves v's slot untouched).  Pair row: J sums, then the flag at J (J + 2 doubles).
+// ---------------------------------------------------------------------------------------- //
+__global__ __launch_bounds__(256) void k_sk_shard_combine(SkArgs a, SkDev d,
+                                                          double* __restrict__ pair) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < a.J) {
+    double s0 = 0.0, s1 = 0.0;
+    int q = 0;
+    for (; q + 2 <= a.ns; q += 2) {
+      s0 += d.part[(int64_t)q * a.J + j];
+      s1 += d.part[(int64_t)(q + 1) * a.J + j];
+    }
+    if (q < a.ns) s0 += d.part[(int64_t)q * a.J + j];
+    pair[j] = s0 + s1;
+  }
+  if (j == 0) {
+    pair[a.J] = (!d.st[ST_DONE] && d.st[ST_UFAIL]) ? 1.0 : 0.0;
+    pair[a.J + 1] = 0.0;
+  }
+}
+
+__device__ __forceinline__ bool shard_ufail(const double* __restrict__ pairs, int W,
+                                            int64_t stride, int J) {
+  bool u = false;
+  for (int r = 0; r < W; ++r) u |= pairs[(int64_t)r * stride + J] != 0.0;
+  return u;
+}
+
+// v_it from the W gathered rows (rank order), err^2 partials of iterate it-1, K^T u == 0 / bad v
+// flags (read by the sweep's knopp_stop exactly as in the unsharded loop)
+__global__ __launch_bounds__(256) void k_sk_shard_colfin(SkArgs a, SkDev d,
+                                                         const double* __restrict__ pairs, int W,
+                                                         int64_t stride, int it) {
+  if (d.st[ST_DONE]) return;
+  if (shard_ufail(pairs, W, stride, a.J)) {  // iteration it-1 broke on u: keep iterate it-2
+    if (blockIdx.x == 0 && threadIdx.x == 0) mark_done(d.st, it - 1, 2, it & 1);
+    return;
+  }
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int cur = it & 1, prev = cur ^ 1;
+  double errp = 0.0;
+  bool fail = false;
+  if (j < a.J) {
+    double s = 0.0;
+    for (int r = 0; r < W; ++r) s += pairs[(int64_t)r * stride + j];
+    const double t = d.v[(int64_t)prev * a.J + j] * s - a.b[j];  // (utils/ot_loss.py:65-66)
+    errp = t * t;
+    const double vj = a.b[j] / s;  // (:54)
+    fail = s == 0.0 || vj != vj || isinf(vj);
+    d.v[(int64_t)cur * a.J + j] = vj;
+  }
+  errp = wave_sum(errp);
+  __shared__ double red[4];
+  if (lane_id() == 0) red[wave_id()] = errp;
+  if (__any(fail) && lane_id() == 0) atomicOr((unsigned long long*)&d.st[ST_FAIL], 1ull);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    d.errpart[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (blockIdx.x == 0) d.st[ST_UFAIL] = 0;  // consumed (it travelled in the gathered rows)
+  }
+}
+
+namespace skscale {
+
+bool shard_ok(const gnnea_sinkhorn* p) {
+  return p && p->variant == 0 && p->mode == GNNEA_SK_KNOPP && p->J <= kMaxJ && sk_valid(p);
+}
+int64_t shard_ws_bytes(int I, int J) {
+  if (J > kMaxJ) return 0;
+  const SkWs w = sk_plan(I, J);
+  // the colfin's err partials (one per 256 columns) must fit the errpart slots (one per 16)
+  return w.total;
+}
+int shard_pair_len(const gnnea_sinkhorn* p) { return p->J + 2; }
+
+static SkArgs shard_args(const gnnea_sinkhorn* p, int I_global) {
+  SkArgs a = sk_args(p);
+  a.ig = I_global;
+  a.shard = 1;
+  return a;
+}
+
+int shard_init(const gnnea_sinkhorn* p, int I_global, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const SkArgs a = shard_args(p, I_global);
+  const SkDev d = sk_dev(p);
+  const int n = p->I > p->J ? p->I : p->J;
+  hipLaunchKernelGGL(k_sk_init, dim3(div_up(n > 32 ? n : 32, 256)), dim3(256), 0, s, a, d,
+                     p->tol);
+  // the err partials the sharded colfin does not write (slots past ceil(J / 256)) stay zero
+  if (hipMemsetAsync(d.errpart, 0, 8 * (size_t)a.nfin, s) != hipSuccess) return GNNEA_EINVAL;
+  const dim3 grow(div_up(p->I, 4));
+  if (p->c_dtype == GNNEA_F32)
+    hipLaunchKernelGGL((k_sk_kbuild<float, true>), grow, dim3(256), 0, s, (const float*)p->C, a,
+                       d, 0, p->max_iter, 1);
+  else
+    hipLaunchKernelGGL((k_sk_kbuild<double, true>), grow, dim3(256), 0, s, (const double*)p->C,
+                       a, d, 0, p->max_iter, 1);
+  launch_sweep<true, false>(a, d, 0, 1, 1, d.u + p->I, 0, s);  // K^T u0 partials (u0 in slot 1)
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+int shard_colpart(const gnnea_sinkhorn* p, double* pair, void* stream) {
+  const SkArgs a = shard_args(p, p->I);
+  hipLaunchKernelGGL(k_sk_shard_combine, dim3(div_up(p->J, 256)), dim3(256), 0,
+                     (hipStream_t)stream, a, sk_dev(p), pair);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+int shard_step(const gnnea_sinkhorn* p, int it, const double* pairs, int W, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const SkArgs a = shard_args(p, p->I);
+  const SkDev d = sk_dev(p);
+  hipLaunchKernelGGL(k_sk_shard_colfin, dim3(div_up(p->J, 256)), dim3(256), 0, s, a, d, pairs, W,
+                     (int64_t)shard_pair_len(p), it);
+  const int cur = it & 1;
+  launch_sweep<true, true>(a, d, it, cur, cur, nullptr, 1, s);  // u_it and K^T u_it partials
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+// after the close step (the status block holds the final slot): plan rows, row sums, this
+// rank's sum P.M (loss_part[0]) and column sums (col_part)
+int shard_finish(const gnnea_sinkhorn* p, void* plan, int plan_dtype, int64_t ldp,
+                 double* row_sum, double* loss_part, double* col_part, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const SkArgs a = shard_args(p, p->I);
+  const SkDev d = sk_dev(p);
+  const dim3 grow(div_up(p->I, 4));
+  double* xcol = d.pu;
+#define GNNEA_PLAN(T, PT)                                                                   \
+  hipLaunchKernelGGL((k_sk_plan<T, PT>), grow, dim3(256), 0, s, (const T*)p->C, a, d,      \
+                     p->iters_run, (PT*)plan, ldp, row_sum, xcol)
+  if (p->c_dtype == GNNEA_F32) {
+    if (plan_dtype == GNNEA_F32) GNNEA_PLAN(float, float);
+    else GNNEA_PLAN(float, double);
+  } else {
+    if (plan_dtype == GNNEA_F32) GNNEA_PLAN(double, float);
+    else GNNEA_PLAN(double, double);
+  }
+#undef GNNEA_PLAN
+  hipLaunchKernelGGL(k_sk_loss, dim3(1), dim3(1024), 0, s, a, d, p->iters_run);
+  GNNEA_LAUNCH_CHECK();
+  if (hipMemcpyAsync(loss_part, d.sd + SD_LOSS, 8, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return GNNEA_EINVAL;
+  if (col_part) {
+    launch_sweep<true, false>(a, d, 0, 0, 0, xcol, 0, s);
+    hipLaunchKernelGGL(k_sk_colfin<FIN_SUM>, dim3(a.nfin), dim3(1024), 0, s, a, d, 0, 0,
+                       col_part);
+    GNNEA_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+}  // namespace skscale
 
 // the memory-lean log-domain path (sinkhorn_log.hip)
 namespace sklog {

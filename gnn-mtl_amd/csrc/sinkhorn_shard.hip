@@ -17,7 +17,9 @@
 //   - K^T u == 0 or v inf / NaN in iteration it: break, iterate it-1 kept.
 // A u failure of the very last iteration is settled by gnnea_sinkhorn_shard_close.  Plan rows,
 // the local part of sum P.M and the local column sums follow (gnnea_sinkhorn_shard_finish); the
-// caller all-reduces the two partial sums.
+// caller all-reduces the two partial sums.  This file is the log-domain form (variant 1, or J
+// above the scaling form's sweep limit); variant 0 with J <= 16384 dispatches to the scaling form
+// with K resident per rank (sinkhorn.hip, skscale::shard_*): same protocol, J + 2 doubles a row.
 #include "common.h"
 
 namespace gnnea {
@@ -323,6 +325,20 @@ __global__ __launch_bounds__(256) void k_sh_colsum(const T* __restrict__ C, int6
 }  // namespace skshard
 }  // namespace gnnea
 
+// the scaling-form variant (sinkhorn.hip): taken for variant 0 and J <= its sweep's limit
+namespace gnnea {
+namespace skscale {
+bool shard_ok(const gnnea_sinkhorn* p);
+int64_t shard_ws_bytes(int I, int J);
+int shard_pair_len(const gnnea_sinkhorn* p);
+int shard_init(const gnnea_sinkhorn* p, int I_global, void* stream);
+int shard_colpart(const gnnea_sinkhorn* p, double* pair, void* stream);
+int shard_step(const gnnea_sinkhorn* p, int it, const double* pairs, int W, void* stream);
+int shard_finish(const gnnea_sinkhorn* p, void* plan, int plan_dtype, int64_t ldp,
+                 double* row_sum, double* loss_part, double* col_part, void* stream);
+}  // namespace skscale
+}  // namespace gnnea
+
 using namespace gnnea;
 using namespace gnnea::skshard;
 
@@ -385,11 +401,20 @@ static bool sh_ok(const gnnea_sinkhorn* p) {
 
 extern "C" int64_t gnnea_sinkhorn_shard_ws_bytes(int I_local, int J) {
   if (I_local < 1 || J < 1) return GNNEA_EINVAL;
-  return sh_plan(I_local, J).total;
+  const int64_t lg = sh_plan(I_local, J).total, sc = skscale::shard_ws_bytes(I_local, J);
+  return sc > lg ? sc : lg;
+}
+
+// doubles per rank of the gathered row: J + 2 (scaling form: column sums, flag) or 2J + 2
+// (log domain: (max, sum-exp) pairs, flag)
+extern "C" int gnnea_sinkhorn_shard_pair_len(const gnnea_sinkhorn* p) {
+  if (!sh_ok(p)) return GNNEA_EINVAL;
+  return skscale::shard_ok(p) ? skscale::shard_pair_len(p) : 2 * p->J + 2;
 }
 
 extern "C" int gnnea_sinkhorn_shard_init(const gnnea_sinkhorn* p, int I_global, void* stream) {
   if (!sh_ok(p) || I_global < p->I) return GNNEA_EINVAL;
+  if (skscale::shard_ok(p)) return skscale::shard_init(p, I_global, stream);
   const int n = p->I > p->J ? p->I : p->J;
   hipLaunchKernelGGL(k_sh_init, dim3(div_up(n > 32 ? n : 32, 256)), dim3(256), 0,
                      (hipStream_t)stream, p->I, p->J, I_global, p->tol, p->a, p->b, sh_dev(p));
@@ -400,6 +425,7 @@ extern "C" int gnnea_sinkhorn_shard_init(const gnnea_sinkhorn* p, int I_global, 
 extern "C" int gnnea_sinkhorn_shard_colpart(const gnnea_sinkhorn* p, int it, double* pair,
                                             void* stream) {
   if (!sh_ok(p) || it < 0 || !pair) return GNNEA_EINVAL;
+  if (skscale::shard_ok(p)) return skscale::shard_colpart(p, pair, stream);
   hipStream_t s = (hipStream_t)stream;
   const Dev d = sh_dev(p);
   const int ns = sh_splits(p->I, p->J);
@@ -421,6 +447,7 @@ extern "C" int gnnea_sinkhorn_shard_colpart(const gnnea_sinkhorn* p, int it, dou
 extern "C" int gnnea_sinkhorn_shard_step(const gnnea_sinkhorn* p, int it, const double* pairs,
                                          int W, void* stream) {
   if (!sh_ok(p) || it < 0 || !pairs || W < 1) return GNNEA_EINVAL;
+  if (skscale::shard_ok(p)) return skscale::shard_step(p, it, pairs, W, stream);
   hipStream_t s = (hipStream_t)stream;
   const Dev d = sh_dev(p);
   const double inv_reg = 1.0 / p->eps;
@@ -458,6 +485,8 @@ extern "C" int gnnea_sinkhorn_shard_finish(const gnnea_sinkhorn* p, void* plan, 
   if (!sh_ok(p) || !loss_part) return GNNEA_EINVAL;
   if (plan && ((plan_dtype != GNNEA_F32 && plan_dtype != GNNEA_F64) || ldp < p->J))
     return GNNEA_EINVAL;
+  if (skscale::shard_ok(p))
+    return skscale::shard_finish(p, plan, plan_dtype, ldp, row_sum, loss_part, col_part, stream);
   hipStream_t s = (hipStream_t)stream;
   const Dev d = sh_dev(p);
   double* loss_rows = (double*)((char*)p->ws + sh_plan(p->I, p->J).loss);

@@ -174,6 +174,7 @@ SIGNATURES = {
     "gnnea_sinkhorn_finish": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p, ctypes.c_int,
                                              _i64, _p, _p, _p]),
     "gnnea_sinkhorn_shard_ws_bytes": (_i64, [ctypes.c_int, ctypes.c_int]),
+    "gnnea_sinkhorn_shard_pair_len": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem)]),
     "gnnea_sinkhorn_shard_init": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), ctypes.c_int,
                                                  _p]),
     "gnnea_sinkhorn_shard_colpart": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem),

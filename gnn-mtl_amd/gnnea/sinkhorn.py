@@ -185,16 +185,18 @@ def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.fl
 
 
 # ------------------------------------------------------------------------------------------------
-# §8e: KNOPP with the cost rows sharded over ranks (gnnea_sinkhorn_shard_*, sinkhorn_shard.hip).
-# Rank r holds a contiguous block of rows; per iteration every rank reduces its rows to (max,
-# sum-exp) pairs per column, the pairs are all-gathered (one collective of W x (2J + 2) doubles)
-# and each rank merges them in rank order, so g and all stop decisions are bit-identical on every
-# rank: the ranks poll their own status block and leave the loop on the same iteration.
+# §8e: KNOPP with the cost rows sharded over ranks (gnnea_sinkhorn_shard_*).  Rank r holds a
+# contiguous block of rows; per iteration every rank reduces its rows to one row per column —
+# the column sums of K^T u in the scaling form (variant 0, J <= 16384: the rank's fp64 K resident,
+# sinkhorn.hip) or (max, sum-exp) pairs in the log domain (variant 1, sinkhorn_shard.hip) — the
+# rows are all-gathered (one collective of W x pair_len doubles) and each rank merges them in
+# rank order, so v and all stop decisions are bit-identical on every rank: the ranks poll their
+# own status block and leave the loop on the same iteration.
 
 class _Shard:
     """One rank's row block as a gnnea_sinkhorn problem (KNOPP)."""
 
-    def __init__(self, C, a, b, reg, tol, max_iter, I_global):
+    def __init__(self, C, a, b, reg, tol, max_iter, I_global, variant=0):
         _lib.require_device(C, a, b)
         if C.dim() != 2:
             raise ValueError("gnnea.sinkhorn: C must be 2-D")
@@ -214,15 +216,19 @@ class _Shard:
             check(nb)
         dev = C.device
         self.ws = torch.empty(nb, dtype=torch.uint8, device=dev)
-        self.pair = torch.empty(2 * self.J + 2, dtype=torch.float64, device=dev)
         self.flag = torch.empty(1, dtype=torch.float64, device=dev)
         self.prob = SinkhornProblem(
             mode=_lib.GNNEA_SK_KNOPP,
             c_dtype=_lib.GNNEA_F32 if C.dtype == torch.float32 else _lib.GNNEA_F64,
             I=self.I, J=self.J, ldc=C.stride(0), C=C.data_ptr(), a=self.a.data_ptr(),
             b=self.b.data_ptr(), eps=float(reg), p=1.0, tol=float(tol), max_iter=int(max_iter),
-            iters_run=0, variant=1, reserved=0, ws=self.ws.data_ptr())
+            iters_run=0, variant=int(variant), reserved=0, ws=self.ws.data_ptr())
         self.pp = ctypes.byref(self.prob)
+        # the gathered row: column sums (scaling form, K resident) or (max, sum-exp) pairs
+        n = int(L.gnnea_sinkhorn_shard_pair_len(self.pp))
+        if n < 0:
+            check(n)
+        self.pair = torch.empty(n, dtype=torch.float64, device=dev)
         self.st = stream_of(dev)
         check(L.gnnea_sinkhorn_shard_init(self.pp, int(I_global), self.st))
 
@@ -278,7 +284,7 @@ def _run_shards(shards, gather, reduce_sum, max_iter, tol, want_plan, plan_dtype
 
 
 def solve_row_sharded(C_loc, a_loc, b, reg, tol, max_iter, group=None,
-                      plan_dtype=torch.float64, want_plan=True):
+                      plan_dtype=torch.float64, want_plan=True, variant=None):
     """KNOPP over this rank's cost rows C_loc [I_loc, J] (ranks hold consecutive row blocks in
     rank order), a_loc its rows' source weights, b all J target weights.  One all-gather of the
     column pairs per iteration over `group` (RCCL on HIP devices).  Returns this rank's
@@ -308,12 +314,13 @@ def solve_row_sharded(C_loc, a_loc, b, reg, tol, max_iter, group=None,
         return t.to(dev)
 
     with _lib.on_device(dev):
-        shard = _Shard(C_loc, a_loc, b, reg, tol, max_iter, int(n.item()))
+        shard = _Shard(C_loc, a_loc, b, reg, tol, max_iter, int(n.item()),
+                       DEFAULT_VARIANT if variant is None else variant)
         return _run_shards([shard], gather, reduce_sum, max_iter, tol, want_plan, plan_dtype)[0]
 
 
 def solve_row_blocks(C, a, b, reg, tol, max_iter, row_splits, plan_dtype=torch.float64,
-                     want_plan=True):
+                     want_plan=True, variant=None):
     """The row-sharded solve with every shard driven by this process on C's device (the
     exchange is a stack of the shards' pair rows in rank order): the same kernels and the same
     merge order as solve_row_sharded over len(row_splits) + 1 ranks, for tests and for a single
@@ -324,8 +331,9 @@ def solve_row_blocks(C, a, b, reg, tol, max_iter, row_splits, plan_dtype=torch.f
     if any(bounds[k] >= bounds[k + 1] for k in range(len(bounds) - 1)):
         raise ValueError("gnnea.sinkhorn: row blocks must be non-empty and increasing")
     with _lib.on_device(C.device):
+        var = DEFAULT_VARIANT if variant is None else variant
         shards = [_Shard(C[bounds[k]:bounds[k + 1]], a.reshape(-1)[bounds[k]:bounds[k + 1]], b,
-                         reg, tol, max_iter, I) for k in range(len(bounds) - 1)]
+                         reg, tol, max_iter, I, var) for k in range(len(bounds) - 1)]
 
         def gather(ts):
             return torch.stack(ts)

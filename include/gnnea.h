@@ -422,8 +422,8 @@ int gnnea_sinkhorn_finish(const gnnea_sinkhorn* prob, void* plan, int plan_dtype
  * contiguous block of rows, rank order = row order).  `prob` is the rank's own problem: I = its
  * rows, C = its cost rows, a = its rows' source weights, b = all J target weights, mode KNOPP.
  * Per iteration it (host loop, every rank):
- *   gnnea_sinkhorn_shard_colpart(prob, it, pair)      pair: 2J + 2 doubles (its column LSE pairs)
- *   <all-gather the W pair rows into pairs [W][2J + 2], rank order>
+ *   gnnea_sinkhorn_shard_colpart(prob, it, pair)      pair: gnnea_sinkhorn_shard_pair_len doubles
+ *   <all-gather the W pair rows into pairs [W][pair_len], rank order>
  *   gnnea_sinkhorn_shard_step(prob, it, pairs, W)     g, stop decisions, its row pass
  * Every rank takes the same decisions from the same gathered data; the status block (ws) is
  * read as for gnnea_sinkhorn_iterate.  After the loop (iters_run = iterations enqueued):
@@ -433,6 +433,10 @@ int gnnea_sinkhorn_finish(const gnnea_sinkhorn* prob, void* plan, int plan_dtype
  *                                                     its sum P.M, col_part[J] = its column sums
  * The caller sums loss_part and col_part over the ranks. */
 int64_t gnnea_sinkhorn_shard_ws_bytes(int I_local, int J);
+/* doubles per rank of the gathered row ("pair"): J + 2 for the scaling form (variant 0,
+ * J <= 16384: fp64 K of the rank's rows resident, column sums gathered) or 2J + 2 for the
+ * log-domain form (variant 1 or wider J: (max, sum-exp) pairs); the flag sits at index J resp. 2J */
+int gnnea_sinkhorn_shard_pair_len(const gnnea_sinkhorn* prob);
 int gnnea_sinkhorn_shard_init(const gnnea_sinkhorn* prob, int I_global, void* stream);
 int gnnea_sinkhorn_shard_colpart(const gnnea_sinkhorn* prob, int it, double* pair, void* stream);
 int gnnea_sinkhorn_shard_step(const gnnea_sinkhorn* prob, int it, const double* pairs, int W,

@@ -22,9 +22,16 @@ def _blocks(I, W):
     return [I * k // W for k in range(1, W)]
 
 
+@pytest.fixture(params=[0, 1], ids=["scaling", "logdomain"])
+def var(request):
+    """Both sharded forms: the scaling form with each shard's fp64 K resident (variant 0) and the
+    log-domain passes (variant 1)."""
+    return request.param
+
+
 @pytest.mark.parametrize("W", [2, 3])
 @pytest.mark.parametrize("tag,reg", [("s", 0.05), ("m", 0.01), ("m", 0.05)])
-def test_shard_vs_reference_fixture(golden, device, tag, reg, W):
+def test_shard_vs_reference_fixture(golden, device, tag, reg, W, var):
     from gnnea.sinkhorn import solve_row_blocks
     S = golden("sinkhorn")
     M = torch.from_numpy(S["%s_M" % tag]).to(device)
@@ -32,14 +39,14 @@ def test_shard_vs_reference_fixture(golden, device, tag, reg, W):
     key = "%s_r%g" % (tag, reg)
     a = torch.ones(I, dtype=torch.float64, device=device)
     b = torch.ones(J, dtype=torch.float64, device=device)
-    P, res = solve_row_blocks(M, a, b, reg, 1e-9, 1000, _blocks(I, W))
+    P, res = solve_row_blocks(M, a, b, reg, 1e-9, 1000, _blocks(I, W), variant=var)
     assert rel_err(P.cpu(), S[key + "_knopp_P"]) < TOL64
     ref_loss = float(S[key + "_knopp_loss"])
     assert abs(res.loss - ref_loss) <= TOL64 * abs(ref_loss)
     assert rel_err(res.col_sum.cpu(), P.sum(0).cpu()) < 1e-12
 
 
-def test_shard_underflow_break(golden, device):
+def test_shard_underflow_break(golden, device, var):
     from gnnea.sinkhorn import solve_row_blocks
     S = golden("sinkhorn")
     M = torch.from_numpy(S["under_M"]).to(device)
@@ -47,14 +54,14 @@ def test_shard_underflow_break(golden, device):
     a = torch.ones(I, dtype=torch.float64, device=device)
     b = torch.ones(J, dtype=torch.float64, device=device)
     for W in (2, 4):
-        P, res = solve_row_blocks(M, a, b, 0.01, 1e-9, 1000, _blocks(I, W))
+        P, res = solve_row_blocks(M, a, b, 0.01, 1e-9, 1000, _blocks(I, W), variant=var)
         assert rel_err(P.cpu(), S["under_P"]) < TOL64
         assert res.reason == 2
 
 
 @pytest.mark.parametrize("I,J,reg,W", [(50, 70, 0.1, 2), (257, 129, 0.02, 3), (1000, 1000, 0.01, 4),
                                        (3, 40, 0.05, 3)])
-def test_shard_vs_oracle_and_unsharded(device, I, J, reg, W):
+def test_shard_vs_oracle_and_unsharded(device, I, J, reg, W, var):
     from gnnea.sinkhorn import solve, solve_row_blocks
     from oracle import sinkhorn as osk
     import gnnea._lib as L
@@ -64,17 +71,17 @@ def test_shard_vs_oracle_and_unsharded(device, I, J, reg, W):
     b = rng.uniform(0.5, 1.5, J)
     b *= a.sum() / b.sum()
     Md, ad, bd = (torch.from_numpy(x).to(device) for x in (M, a, b))
-    P, res = solve_row_blocks(Md, ad, bd, reg, 1e-9, 300, _blocks(I, W))
+    P, res = solve_row_blocks(Md, ad, bd, reg, 1e-9, 300, _blocks(I, W), variant=var)
     Po, lo, cpt, broke = osk.knopp(a, b, M, reg, 300)
     assert rel_err(P.cpu(), Po) < TOL64
     assert abs(res.loss - lo) <= TOL64 * abs(lo)
     assert res.iters == cpt and (res.reason == 2) == broke
-    ref = solve(L.GNNEA_SK_KNOPP, Md, ad, bd, reg, 1e-9, 300, variant=1)
+    ref = solve(L.GNNEA_SK_KNOPP, Md, ad, bd, reg, 1e-9, 300, variant=var)
     assert res.iters == ref.iters and res.reason == ref.reason
     assert rel_err(P.cpu(), ref.plan.cpu()) < 1e-11
 
 
-def test_shard_tolerance_stop(device):
+def test_shard_tolerance_stop(device, var):
     """A loose stopThr ends the loop on the err test of an iterate 10n: same cpt as the
     reference loop (the sharded path evaluates it from the next iteration's gathered pairs)."""
     from gnnea.sinkhorn import solve_row_blocks
@@ -86,14 +93,14 @@ def test_shard_tolerance_stop(device):
     b = np.full(J, 1.0 / J)
     for tol in (1e-3, 1e-6):
         P, res = solve_row_blocks(*(torch.from_numpy(x).to(device) for x in (M, a, b)), reg, tol,
-                                  1000, _blocks(I, 3))
+                                  1000, _blocks(I, 3), variant=var)
         Po, lo, cpt, broke = osk.knopp(a, b, M, reg, 1000, tol)
         assert res.reason == 1 and res.iters == cpt and not broke, (tol, res.iters, cpt)
         assert rel_err(P.cpu(), Po) < TOL64
 
 
 @pytest.mark.parametrize("max_iter", [1, 7, 300])
-def test_shard_u_overflow_break(device, max_iter):
+def test_shard_u_overflow_break(device, max_iter, var):
     """A row whose K is all zero (cost 100 at reg 0.1: exp(-1000) underflows) makes u infinite
     in iteration 0: the reference reverts to the initial scalings and stops with cpt = 0.  The
     sharded loop learns of it one iteration late (or in the close step when max_iter = 1)."""
@@ -109,15 +116,15 @@ def test_shard_u_overflow_break(device, max_iter):
     Md, ad, bd = (torch.from_numpy(x).to(device) for x in (M, a, b))
     Po, lo, cpt, broke = osk.knopp(a, b, M, reg, max_iter)
     assert broke and cpt == 0
-    P, res = solve_row_blocks(Md, ad, bd, reg, 1e-9, max_iter, _blocks(I, 2))
+    P, res = solve_row_blocks(Md, ad, bd, reg, 1e-9, max_iter, _blocks(I, 2), variant=var)
     assert res.reason == 2 and res.iters == 0
     assert rel_err(P.cpu(), Po) < TOL64
-    ref = solve(L.GNNEA_SK_KNOPP, Md, ad, bd, reg, 1e-9, max_iter, variant=1)
+    ref = solve(L.GNNEA_SK_KNOPP, Md, ad, bd, reg, 1e-9, max_iter, variant=var)
     assert ref.reason == 2 and ref.iters == 0
     assert rel_err(P.cpu(), ref.plan.cpu()) < 1e-12
 
 
-def test_shard_b15000_vs_unsharded(device):
+def test_shard_b15000_vs_unsharded(device, var):
     """BASELINE's large Sinkhorn size (B = 15000), fp32 cost as ot_loss receives
     it: 4 row shards against the unsharded log-domain solve, 60 iterations, and the tolerance
     stop of the same problem (it converges in a few tens of iterations at stopThr 1e-9)."""
@@ -128,16 +135,19 @@ def test_shard_b15000_vs_unsharded(device):
     M = torch.rand((B, B), generator=g, device=device, dtype=torch.float32)
     a = torch.full((B,), 1.0 / B, dtype=torch.float64, device=device)
     # stopThr < 0: the err test never passes, exactly 60 iterations run on both paths
-    P, res = solve_row_blocks(M, a, a, 0.05, -1.0, 60, _blocks(B, 4), plan_dtype=torch.float32)
-    ref = solve(L.GNNEA_SK_KNOPP, M, a, a, 0.05, -1.0, 60, plan_dtype=torch.float32, variant=1)
+    P, res = solve_row_blocks(M, a, a, 0.05, -1.0, 60, _blocks(B, 4), plan_dtype=torch.float32,
+                              variant=var)
+    ref = solve(L.GNNEA_SK_KNOPP, M, a, a, 0.05, -1.0, 60, plan_dtype=torch.float32,
+                variant=var)
     assert res.iters == ref.iters == 60 and res.reason == ref.reason == 0
     d = (P - ref.plan).abs().max().item() / ref.plan.abs().max().item()
     assert d < 1e-6, d  # fp32 plan storage
     assert abs(res.loss - ref.loss) <= 1e-10 * abs(ref.loss)
     assert torch.allclose(res.col_sum, ref.col_sum, rtol=1e-10, atol=0)
     del P, ref
-    _, res = solve_row_blocks(M, a, a, 0.05, 1e-9, 1000, _blocks(B, 4), want_plan=False)
-    ref = solve(L.GNNEA_SK_KNOPP, M, a, a, 0.05, 1e-9, 1000, want_plan=False, variant=1)
+    _, res = solve_row_blocks(M, a, a, 0.05, 1e-9, 1000, _blocks(B, 4), want_plan=False,
+                              variant=var)
+    ref = solve(L.GNNEA_SK_KNOPP, M, a, a, 0.05, 1e-9, 1000, want_plan=False, variant=var)
     assert res.iters == ref.iters < 1000 and res.reason == ref.reason == 1
     assert abs(res.loss - ref.loss) <= 1e-10 * abs(ref.loss)
 

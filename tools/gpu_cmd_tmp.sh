@@ -1,4 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_scale_dbp15k.py tests/test_gpu_parity.py tests/test_gpu_sinkhorn_shard.py -x -q -k "sinkhorn or gw or fgw" --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/sk_tests.log 2>&1; rc=$?; tail -3 gpurun_out/sk_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/dbg/sk_wide.py 2>&1 | grep -v amdgpu.ids
+timeout -k 10 300 python -u tools/dbg/sk_shard_rate.py 2>&1 | grep -v amdgpu.ids
