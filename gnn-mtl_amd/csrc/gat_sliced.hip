@@ -21,6 +21,8 @@
 // sliced SpMM's, so outputs agree with k_gat_fwd to fp32 rounding.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace gnnea {
 
 template <int H>
@@ -146,18 +148,19 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
 // each in-neighbour's whole 1,200-B G row from a 1.2-GB KG table; here:
 //   k_gat_bwd_prep_s (dest rows i): G = dY * act'(Y) written slice-major, records {s1, m, 1/den,
 //                     c = G_i . h'_i} as gat.hip;
-//   k_gat_bwd_w      (source rows j, 16 lanes per row): wT[e][h] = alpha_ij * mask_ij in A^T
+//   k_gat_bwd_w      (source rows j, 32 lanes per row): wT[e][h] = alpha_ij * mask_ij in A^T
 //                     order (one record gather per edge, once);
 //   k_gat_bwd_src_sl (slice, source row j) as k_gat_fwd_sliced: dH_j[slice] = sum_i w_ij G_i,
 //                     and per edge the slice's share of the per-head products G_i,h . H_j,h for
 //                     the (at most two) heads the slice holds — reduced over each 16-lane group
 //                     by reduce-scatter (grp_sum) and stored as pd[s][e][2];
-//   k_gat_bwd_edge   (source rows j, 16 lanes per row): da_ij,h = the head's slice partials
+//   k_gat_bwd_edge   (source rows j, 32 lanes per row): da_ij,h = the head's slice partials
 //                     summed in slice order, dz_ij = -LeakyReLU'(z) alpha (mask da - c_i) in A^T
 //                     order (coalesced; storing it at A positions instead measured 1.69 -> 3.65
 //                     ms per cfg-4 launch against 2.77 -> 2.28 for the destination pass),
 //                     ds2_j = sum_i dz; optionally dH_j += ds2_j (x) a2;
-//   k_gat_bwd_dst_s  (dest rows i): its dH row loaded first (in flight under the dz gathers),
+//   k_gat_bwd_dst_s  (dest rows i, 32 lanes per row): its dH row loaded first (in flight under
+//                     the dz gathers),
 //                     ds1_i through the transpose position map, dH_i += ds1_i (x) a1
 //                     (+ ds2_i (x) a2 when the edge pass left it, square unsharded case).
 // fp32 throughout; sums in a different order from gat.hip's single pass (fp32 rounding level).
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_s(int n_rows, int D, int d
   }
 }
 
-template <int H>
+template <int H, int LPR>  // LPR lanes per source row
 __global__ __launch_bounds__(256) void k_gat_bwd_w(const int32_t* __restrict__ rowptrT,
                                                    const int32_t* __restrict__ colT,
                                                    const int64_t* __restrict__ permT, int n_rows,
@@ -215,14 +218,14 @@ __global__ __launch_bounds__(256) void k_gat_bwd_w(const int32_t* __restrict__ r
                                                    const float* __restrict__ emask,
                                                    const float4* __restrict__ rec,
                                                    float* __restrict__ wT) {
-  const int row = xcd_remap(blockIdx.x, gridDim.x) * 16 + (threadIdx.x >> 4);
+  const int row = xcd_remap(blockIdx.x, gridDim.x) * (256 / LPR) + threadIdx.x / LPR;
   if (row >= n_rows) return;
-  const int l = threadIdx.x & 15;
+  const int l = threadIdx.x % LPR;
   float sj[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) sj[h] = s2[(int64_t)row * H + h];
   const int end = rowptrT[row + 1];
-  for (int e = rowptrT[row] + l; e < end; e += 16) {
+  for (int e = rowptrT[row] + l; e < end; e += LPR) {
     const int i = colT[e];
     const int64_t pe = emask ? permT[e] : 0;
 #pragma unroll
@@ -333,7 +336,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
   *(float4*)(dH + (int64_t)row * lddh + c0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
 }
 
-template <int H>
+template <int H, int LPR>  // LPR lanes per source row
 __global__ __launch_bounds__(256) void k_gat_bwd_edge(
     const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT,
     const int64_t* __restrict__ permT, int n_rows, int S, int D, int dh,
@@ -341,9 +344,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_edge(
     const float4* __restrict__ rec, const float2* __restrict__ pd, int64_t pstride2,
     const float* __restrict__ a, float* __restrict__ dH, int64_t lddh, float* __restrict__ dzT,
     float* __restrict__ ds2) {
-  const int row = xcd_remap(blockIdx.x, gridDim.x) * 16 + (threadIdx.x >> 4);
-  if (row >= n_rows) return;  // whole 16-lane groups leave together
-  const int l = threadIdx.x & 15;
+  const int row = xcd_remap(blockIdx.x, gridDim.x) * (256 / LPR) + threadIdx.x / LPR;
+  if (row >= n_rows) return;  // whole LPR-lane groups leave together
+  const int l = threadIdx.x % LPR;
   float sj[H], d2[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) {
@@ -351,7 +354,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_edge(
     d2[h] = 0.f;
   }
   const int end = rowptrT[row + 1];
-  for (int e = rowptrT[row] + l; e < end; e += 16) {
+  for (int e = rowptrT[row] + l; e < end; e += LPR) {
     const int i = colT[e];
     const int64_t pe = emask ? permT[e] : 0;
     float da[H];
@@ -380,12 +383,12 @@ __global__ __launch_bounds__(256) void k_gat_bwd_edge(
 #pragma unroll
   for (int h = 0; h < H; ++h) {
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) d2[h] += __shfl_xor(d2[h], o, 16);
+    for (int o = LPR / 2; o > 0; o >>= 1) d2[h] += __shfl_xor(d2[h], o, LPR);
   }
   if (l < H) ds2[(int64_t)row * H + l] = hsel<H>(d2, l);
   if (!dH) return;
   float* out = dH + (int64_t)row * lddh;
-  for (int c4 = l; 4 * c4 < D; c4 += 16) {
+  for (int c4 = l; 4 * c4 < D; c4 += LPR) {
     float4 v = *(float4*)(out + 4 * c4);
     float o[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_edge(
   }
 }
 
-template <int H, int NCH>
+template <int H, int NCH, int L>  // L lanes per destination row (NCH: float4 slots at 64 lanes)
 __global__ __launch_bounds__(256) void k_gat_bwd_dst_s(const int32_t* __restrict__ rowptr,
                                                        const int64_t* __restrict__ tpos,
                                                        int n_rows, int D, int dh,
@@ -406,32 +409,34 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_s(const int32_t* __restrict
                                                        const float* __restrict__ ds2,
                                                        float4* __restrict__ dH, int64_t lddh4,
                                                        float* __restrict__ ds1) {
-  const int row = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
-  if (row >= n_rows) return;
-  const int lane = lane_id();
+  constexpr int NC = NCH * 64 / L;
+  const int row = xcd_remap(blockIdx.x, gridDim.x) * (256 / L) + threadIdx.x / L;
+  if (row >= n_rows) return;  // whole L-lane groups leave together
+  const int l = threadIdx.x % L;
   const int beg = rowptr[row], end = rowptr[row + 1];
-  float4 v[NCH];
+  float4 v[NC];
 #pragma unroll
-  for (int k = 0; k < NCH; ++k) {  // independent of dz: issued before the gather chain
-    const int c4 = lane + 64 * k;
+  for (int k = 0; k < NC; ++k) {  // independent of dz: issued before the gather chain
+    const int c4 = l + L * k;
     v[k] = 4 * c4 < D ? dH[(int64_t)row * lddh4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float p[H], q[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) p[h] = 0.f;
-  for (int e = beg + lane; e < end; e += 64) {
+  for (int e = beg + l; e < end; e += L) {
     const int64_t t = tpos[e];
 #pragma unroll
     for (int h = 0; h < H; ++h) p[h] += dzT[t * H + h];
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) {
-    p[h] = wave_sum(p[h]);
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1) p[h] += __shfl_xor(p[h], o, L);
     q[h] = ds2 ? ds2[(int64_t)row * H + h] : 0.f;
   }
 #pragma unroll
-  for (int k = 0; k < NCH; ++k) {
-    const int c4 = lane + 64 * k;
+  for (int k = 0; k < NC; ++k) {
+    const int c4 = l + L * k;
     if (4 * c4 >= D) continue;
     float o[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
@@ -442,7 +447,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_s(const int32_t* __restrict
     }
     dH[(int64_t)row * lddh4 + c4] = make_float4(o[0], o[1], o[2], o[3]);
   }
-  if (lane < H) ds1[(int64_t)row * H + lane] = hsel<H>(p, lane);
+  if (l < H) ds1[(int64_t)row * H + l] = hsel<H>(p, l);
 }
 
 }  // namespace gnnea
@@ -497,6 +502,28 @@ extern "C" int gnnea_gat_fwd_sliced_f32(const int32_t* rowptr, const int32_t* co
 // ---- sliced backward entry points -------------------------------------------------------- //
 #define GNNEA_HEADS_SWITCH(CASE) \
   switch (heads) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
+
+// lanes per source row of the weight and edge passes: 32 (cfg-4, mean in-degree 21: edge pass
+// 1.70 / 1.45 / 2.02 ms and weights 0.68 / 0.60 / 0.84 ms at 16 / 32 / 8 lanes; GNNEA_GAT_LPR
+// = 8 / 16 / 64 overrides, tuning only)
+static int gat_lpr() {
+  static const int v = [] {
+    const char* e = getenv("GNNEA_GAT_LPR");
+    const int x = e ? atoi(e) : 32;
+    return x == 8 || x == 16 || x == 64 ? x : 32;
+  }();
+  return v;
+}
+
+// lanes per row of the destination pass: 32 (two rows per wave; 2.37 vs 3.13 ms per cfg-4
+// layer at 64) by default, 64 with GNNEA_GAT_DST_LANES=64 (tuning only)
+static int gat_dst_lanes() {
+  static const int v = [] {
+    const char* e = getenv("GNNEA_GAT_DST_LANES");
+    return e && atoi(e) == 64 ? 64 : 32;
+  }();
+  return v;
+}
 
 static bool gat_sl_shape(int heads, int d_head, int64_t sstride) {
   const int D = heads * d_head;
@@ -563,13 +590,19 @@ extern "C" int gnnea_gat_bwd_src_sliced_f32(const int32_t* rowptrT, const int32_
     return GNNEA_EINVAL;
   if (((uintptr_t)Hm | (uintptr_t)Gs | (uintptr_t)dH) & 15) return GNNEA_EALIGN;
   hipStream_t st = (hipStream_t)stream;
-#define GNNEA_W(HH)                                                                           \
-  case HH:                                                                                    \
-    hipLaunchKernelGGL(k_gat_bwd_w<HH>, dim3(div_up(n_rows, 16)), dim3(256), 0, st, rowptrT,  \
-                       colT, permT, n_rows, s2, alpha, emask, (const float4*)rec, wT);        \
+#define GNNEA_W1(HH, LP)                                                                        \
+  hipLaunchKernelGGL((k_gat_bwd_w<HH, LP>), dim3(div_up(n_rows, 256 / LP)), dim3(256), 0, st,   \
+                     rowptrT, colT, permT, n_rows, s2, alpha, emask, (const float4*)rec, wT)
+#define GNNEA_W(HH)                                              \
+  case HH:                                                       \
+    if (gat_lpr() == 8) GNNEA_W1(HH, 8);                         \
+    else if (gat_lpr() == 16) GNNEA_W1(HH, 16);                  \
+    else if (gat_lpr() == 64) GNNEA_W1(HH, 64);                  \
+    else GNNEA_W1(HH, 32);                                       \
     break;
   GNNEA_HEADS_SWITCH(GNNEA_W)
 #undef GNNEA_W
+#undef GNNEA_W1
   GNNEA_LAUNCH_CHECK();
   const int S = div_up(D, 64), nbs = div_up(n_rows, 4);
   hipLaunchKernelGGL((k_gat_bwd_src_sl<4>), dim3((unsigned)((int64_t)S * nbs)), dim3(256), 0, st,
@@ -597,14 +630,20 @@ extern "C" int gnnea_gat_bwd_edge_sliced_f32(const int32_t* rowptrT, const int32
   if ((uintptr_t)dH & 15) return GNNEA_EALIGN;
   hipStream_t st = (hipStream_t)stream;
   const int S = div_up(D, 64);
-#define GNNEA_E(HH)                                                                             \
-  case HH:                                                                                      \
-    hipLaunchKernelGGL(k_gat_bwd_edge<HH>, dim3(div_up(n_rows, 16)), dim3(256), 0, st, rowptrT, \
-                       colT, permT, n_rows, S, D, d_head, s2, alpha, emask, (const float4*)rec,  \
-                       (const float2*)pd, nnzT, a, dH, lddh, dzT, ds2);                         \
+#define GNNEA_E1(HH, LP)                                                                        \
+  hipLaunchKernelGGL((k_gat_bwd_edge<HH, LP>), dim3(div_up(n_rows, 256 / LP)), dim3(256), 0, st, \
+                     rowptrT, colT, permT, n_rows, S, D, d_head, s2, alpha, emask,               \
+                     (const float4*)rec, (const float2*)pd, nnzT, a, dH, lddh, dzT, ds2)
+#define GNNEA_E(HH)                                              \
+  case HH:                                                       \
+    if (gat_lpr() == 8) GNNEA_E1(HH, 8);                         \
+    else if (gat_lpr() == 16) GNNEA_E1(HH, 16);                  \
+    else if (gat_lpr() == 64) GNNEA_E1(HH, 64);                  \
+    else GNNEA_E1(HH, 32);                                       \
     break;
   GNNEA_HEADS_SWITCH(GNNEA_E)
 #undef GNNEA_E
+#undef GNNEA_E1
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
@@ -622,10 +661,13 @@ extern "C" int gnnea_gat_bwd_dst_sliced_f32(const int32_t* rowptr, const int64_t
   if ((uintptr_t)dH & 15) return GNNEA_EALIGN;
   hipStream_t st = (hipStream_t)stream;
   const int nch = (D / 4 + 63) / 64;
-  const dim3 grid(div_up(n_rows, 4));
-#define GNNEA_D(HH, NC)                                                                        \
-  hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC>), grid, dim3(256), 0, st, rowptr, tpos, n_rows, D, \
-                     d_head, dzT, a, ds2, (float4*)dH, lddh / 4, ds1)
+#define GNNEA_D(HH, NC)                                                                          \
+  if (gat_dst_lanes() == 64)                                                                     \
+    hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC, 64>), dim3(div_up(n_rows, 4)), dim3(256), 0, st, \
+                       rowptr, tpos, n_rows, D, d_head, dzT, a, ds2, (float4*)dH, lddh / 4, ds1); \
+  else                                                                                           \
+    hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC, 32>), dim3(div_up(n_rows, 8)), dim3(256), 0, st, \
+                       rowptr, tpos, n_rows, D, d_head, dzT, a, ds2, (float4*)dH, lddh / 4, ds1)
 #define GNNEA_D_H(HH)                        \
   case HH:                                   \
     switch (nch) {                           \
