@@ -110,7 +110,8 @@ def sinkhorn_rate(device, B=3000, reg=0.01, n0=100, n1=1100, variant=None):
             ts.append(time.perf_counter() - t0)
         out[name] = round((n1 - n0) / (ts[1] - ts[0]), 1)
     return {"iters_per_s": out, "B": B, "reg": reg, "dtype": "f64 (C fp32/fp64)",
-            "method": "marginal (T(%d)-T(%d))/%d incl. host batch syncs" % (n1, n0, n1 - n0)}
+            "method": "marginal (T(%d)-T(%d))/%d incl. the host's look-ahead status reads"
+                      % (n1, n0, n1 - n0)}
 
 
 def sinkhorn_large(device):

@@ -40,6 +40,31 @@ def _status(ws):
     return ints, dbl
 
 
+class _StatusPoll:
+    """Look-ahead read of the device status block: after enqueueing batch k the host reads the
+    status copied after batch k-1 (an async copy into pinned memory and an event), so the queue
+    never drains while the host decides — the GPU runs batch k meanwhile — at the price of one
+    batch of no-op launches after the stop.  ``done()`` is None until a copy is in flight."""
+
+    def __init__(self, ws, rows=1, stride=None):
+        self.src = ws if stride is None else ws.view(rows, stride)
+        self.buf = torch.empty((rows, 8), dtype=torch.int64, pin_memory=True)
+        self.ev = None
+
+    def post(self):
+        src = self.src[:64].view(torch.int64).view(1, 8) if self.src.dim() == 1 else \
+            self.src[:, :64].contiguous().view(torch.int64)
+        self.buf.copy_(src, non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+
+    def done(self):
+        if self.ev is None:
+            return None
+        self.ev.synchronize()
+        return self.buf[:, ST_DONE].clone()
+
+
 def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
           want_plan=True, batch=10, variant=None):
     """Run one Sinkhorn solve; C is [I, J] fp32 / fp64 on a HIP device, a / b the weights."""
@@ -74,8 +99,10 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
         check(L.gnnea_sinkhorn_init(pp, st))
         run = 0
         # The device decides every stop itself (iterations past it are no-op launches), so the
-        # host polls the status block only between batches that grow geometrically up to
-        # MAX_BATCH: few host syncs on long solves, an overshoot of at most one batch of no-ops.
+        # host reads the status block only between batches that grow geometrically up to
+        # MAX_BATCH, one batch behind (_StatusPoll: the GPU never waits for the host), at the
+        # price of at most two batches of no-ops after the stop.
+        poll = _StatusPoll(ws)
         if mode == _lib.GNNEA_SK_KNOPP:
             # utils/ot_loss.py:50  while err > stopThr and cpt < numItermax  (err starts at 1);
             # iteration k's err is evaluated by iteration k+1's combine: batches end at 10n + 2
@@ -85,8 +112,10 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
                     hi = min(hi, max_iter)
                     check(L.gnnea_sinkhorn_iterate(pp, run, hi - run, st))
                     run = hi
-                    if _status(ws)[0][ST_DONE].item():
+                    done = poll.done()
+                    if done is not None and done[0].item():
                         break
+                    poll.post()
                     hi = run + step
                     step = min(2 * step, MAX_BATCH)
         else:
@@ -95,8 +124,10 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
                 n = min(step, max_iter - run)
                 check(L.gnnea_sinkhorn_iterate(pp, run, n, st))
                 run += n
-                if _status(ws)[0][ST_DONE].item():
+                done = poll.done()
+                if done is not None and done[0].item():
                     break
+                poll.post()
                 step = min(2 * step, max(batch, MAX_BATCH))
         prob.iters_run = run
         plan = torch.empty((I, J), dtype=plan_dtype, device=dev) if want_plan else None
@@ -152,6 +183,7 @@ def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.fl
         if knopp and not (1.0 > tol and max_iter > 0):
             live = []
         step, hi = (10, 2) if knopp else (max(1, batch), max(1, batch))
+        poll = _StatusPoll(ws, bt, stride)  # one look-ahead read of all status blocks per round
         while live and run < max_iter:
             hi = min(hi, max_iter)
             for k in live:
@@ -159,8 +191,10 @@ def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.fl
             for k in live:
                 probs[k][1].iters_run = hi
             run = hi
-            done = status[:, :8].contiguous().view(torch.int64)[:, ST_DONE].cpu()  # one sync
-            live = [k for k in live if not int(done[k])]
+            done = poll.done()
+            if done is not None:
+                live = [k for k in live if not int(done[k])]
+            poll.post()
             hi = run + step
             step = min(2 * step, MAX_BATCH)
         for k, (C, pr) in enumerate(probs):
