@@ -1258,7 +1258,12 @@ static int64_t x3_ta_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
   const int64_t bn = 64 * pick_wt(N);
   const int64_t tiles = ((M + XBM - 1) / XBM) * ((N + bn - 1) / bn);
   if (tiles >= 256 || K < 16 * GBK) return 1;
-  int64_t s = 512 / tiles;
+  static const int64_t target = [] {  // workgroups to aim for (GNNEA_X3TA_WGS: tuning only)
+    const char* e = getenv("GNNEA_X3TA_WGS");
+    const int v = e ? atoi(e) : 512;
+    return (int64_t)(v >= 64 && v <= 4096 ? v : 512);
+  }();
+  int64_t s = target / tiles;
   const int64_t by_k = K / (8 * GBK);
   if (s > by_k) s = by_k;
   while (s > 1 && s * M * N * 4 > ws_bytes) --s;
@@ -1282,7 +1287,6 @@ static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t l
   if (splits > 1 && (!ws || ws_bytes < (int64_t)splits * M * N * 4)) return GNNEA_EWORKSPACE;
   const int kps = (int)(((K + splits - 1) / splits + GBK - 1) / GBK * GBK);
   float* slab = splits > 1 ? (float*)ws : nullptr;
-  // float4 loads run along M (A) and N (B): both must be 4-aligned
   // float4 loads run along M (A) and N (B): both must be 4-aligned
   const bool vec = lda % 4 == 0 && M % 4 == 0 && al16(A) && ldb % 4 == 0 && N % 4 == 0 && al16(B);
   const dim3 grid(tiles, splits);
