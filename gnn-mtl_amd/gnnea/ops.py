@@ -908,7 +908,8 @@ def gat_forward(csr, H, a32, heads, d_head, alpha, act, em=None, row0=0):
     m = torch.empty((N, heads), dtype=torch.float32, device=H.device)
     den = torch.empty_like(m)
     if (GAT_SLICED and H.dtype == torch.float32 and d_head >= 32 and D % 4 == 0
-            and Y.shape[1] == D and use_sliced(H.shape[0], D, H.dtype)):
+            and heads <= 8 and D <= 1024 and Y.shape[1] == D
+            and use_sliced(H.shape[0], D, H.dtype)):
         # above the Infinity Cache: the table slice-major (64-column slices, one 256-MB table
         # per KG slice), row statistics once, then the slices one after another
         Hs = sliced_copy_of(H, D)
@@ -957,7 +958,8 @@ def gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha, act, 
     ds1 = torch.empty((N, heads), dtype=torch.float32, device=dev)
     ds2 = torch.empty((H.shape[0], heads), dtype=torch.float32, device=dev)
     if (GAT_SLICED and H.dtype == torch.float32 and d_head >= 32 and D % 4 == 0
-            and Y.shape[1] == D and use_sliced(H.shape[0], D, H.dtype)):
+            and heads <= 8 and D <= 1024 and Y.shape[1] == D
+            and use_sliced(H.shape[0], D, H.dtype)):
         _gat_backward_sliced(csr, csrT, H, a32, s1, s2, m, den, Y, dY, heads, d_head,
                              alpha, act, em, row0, rec, dH, dzT, ds1, ds2)
     else:
