@@ -412,7 +412,8 @@ def main():
         ranks = part.group_ranks(part.kg)
 
         def xchg():
-            for w in ex.all_gather(h_local, h_full, shard.group, ranks, part.li):
+            for w in ex.all_gather(h_local, h_full, shard.group, ranks, part.li,
+                                   other=part.other_ranks()):
                 w.wait()
         for _ in range(2):
             xchg()
@@ -426,8 +427,11 @@ def main():
         dist.all_reduce(xt, op=dist.ReduceOp.MAX)
         x_ms = float(xt) / args.steps * 1e3
         x_bytes = (shard.g - 1) * part.n_rows * Dl * 4
-        exchange = {"transport": "direct peer transfers (batch_isend_irecv, one per group peer)"
-                                 if ex.MODE == "p2p" else "RCCL ring all_gather",
+        relay = ex.relay_applies(ranks, part.other_ranks())
+        exchange = {"transport": "RCCL ring all_gather" if ex.MODE == "ring" else
+                    ("two-phase relay: quarters direct and through the other group's GPUs "
+                     "(batch_isend_irecv, every link one quarter per phase)" if relay else
+                     "direct peer transfers (batch_isend_irecv, one per group peer)"),
                     "peers": shard.g - 1, "bytes_recv_per_rank_per_step": x_bytes,
                     "ms_alone": round(x_ms, 4),
                     "GBps_recv_per_rank": round(x_bytes / (x_ms * 1e-3) / 1e9, 1),

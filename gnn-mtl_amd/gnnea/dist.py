@@ -80,6 +80,10 @@ class Partition:
     def group_ranks(self, kg):
         return list(range(kg * self.g, (kg + 1) * self.g))
 
+    def other_ranks(self):
+        """The other KG group's ranks (relay hops of gnnea.exchange), None on one GPU."""
+        return None if self.kg is None else self.group_ranks(1 - self.kg)
+
 
 def shard_coo(triples, n, t, part):
     """Local COO (rows relative to the shard, KG-local columns), sorted by (row, col)."""
@@ -129,7 +133,8 @@ def halo_gather(h_local, h_full, group, group_size, async_op=False, part=None):
         base = me - me % group_size
         ranks, li = list(range(base, base + group_size)), me % group_size
     works = exchange.all_gather(h_local, h_full, group, ranks, li, copy_own=True,
-                                async_op=async_op)
+                                async_op=async_op,
+                                other=part.other_ranks() if part is not None else None)
     return _Works(works) if works else None
 
 
@@ -197,7 +202,7 @@ class KGShard:
         from . import exchange
         works = exchange.all_gather(h_local, h_full, self.group,
                                     self.part.group_ranks(self.part.kg), self.part.li,
-                                    async_op=True)
+                                    async_op=True, other=self.part.other_ranks())
         rec(0)
         ops.spmm(self.csr_own, h_local, GNNEA_ACT_IDENTITY, out=out)
         rec(1)

@@ -208,7 +208,8 @@ class DistAdj:
         full = torch.empty((g * h_loc.shape[0], h_loc.shape[1]), dtype=h_loc.dtype,
                            device=h_loc.device)
         works = exchange.all_gather(h_loc, full, self.group, self.part.group_ranks(self.part.kg),
-                                    self.part.li, copy_own=copy_own, async_op=async_op)
+                                    self.part.li, copy_own=copy_own, async_op=async_op,
+                                    other=self.part.other_ranks())
         return full, (_Works(works) if works else None)
 
     def reduce_scatter(self, partial):

@@ -65,7 +65,7 @@ def _worker(rank, world, port, n, t, q, kind="rows"):
             # the product's overlap split: owned block from h_local, the rest from the halo
             (ro, co, vo), (rr, cr, vr) = split_own_remote(r, c, v, part)
             y = coo_aggregate(ro, co, vo, part.n_rows, h_local)
-            halo_gather(h_local, h_full, group, part.g)
+            halo_gather(h_local, h_full, group, part.g, part=part)  # relayed at world 4
             y = y + coo_aggregate(rr, cr, vr, part.n_rows, h_full)
         outs = [torch.empty_like(y) for _ in range(world)]
         dist.all_gather(outs, y)
@@ -131,3 +131,46 @@ def test_partition_covers_every_row_once():
         assert np.all(seen == 1)
     with pytest.raises(ValueError):
         Partition(1000, 0, 3)
+
+
+def _relay_worker(rank, world, port, rows, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "gnn-mtl_amd"))
+    from gnnea import exchange
+    from gnnea.dist import Partition, make_groups
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        part = Partition(2 * rows, rank, world, "rows", 3)
+        group = make_groups(part)
+        ranks = part.group_ranks(part.kg)
+        assert exchange.relay_applies(ranks, part.other_ranks())
+        h = torch.arange(rows * 3, dtype=torch.float64).reshape(rows, 3) + 1000 * rank
+        full = torch.full((2 * rows, 3), -1.0, dtype=torch.float64)
+        exchange.all_gather(h, full, group, ranks, part.li, copy_own=True,
+                            other=part.other_ranks())
+        partner = ranks[1 - part.li]
+        want = torch.cat([torch.arange(rows * 3, dtype=torch.float64).reshape(rows, 3)
+                          + 1000 * r for r in ranks])
+        q.put((rank, partner, float((full - want).abs().max())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("rows", [1, 7, 100])
+def test_relay_exchange_world4(rows):
+    """The two-phase relay (quarters direct and through the other group's two GPUs) delivers
+    exactly the partner's block, for row counts that do not split into equal quarters."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_relay_worker, args=(r, 4, port, rows, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [q.get(timeout=5) for _ in range(4)]
+    assert all(err == 0.0 for _, _, err in res), res
