@@ -219,7 +219,7 @@ class DistAdj:
         if self.part.g == 1:
             return partial
         return exchange.reduce_scatter(partial, self.group, self.part.group_ranks(self.part.kg),
-                                       self.part.li)
+                                       self.part.li, other=self.part.other_ranks())
 
     def all_rows(self, out_loc):
         W = self.part.world

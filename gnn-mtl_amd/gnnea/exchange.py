@@ -154,13 +154,22 @@ def all_gather(h_loc, full, group, ranks, li, copy_own=False, async_op=False, ot
     return works
 
 
-def reduce_scatter(partial, group, ranks, li):
-    """This rank's rows of the group sum of the [g·rows, D] partials."""
+def reduce_scatter(partial, group, ranks, li, other=None):
+    """This rank's rows of the group sum of the [g·rows, D] partials.  ``other`` as in
+    all_gather: with two groups of two the partner's block travels by the relayed schedule."""
     g = len(ranks)
     partial = partial.contiguous()
     if g == 1:
         return partial
     blocks = _blocks(partial, g)
+    if relay_applies(ranks, other):
+        # one block each way between the partners: the relay with the partner's block as the
+        # payload; the owner adds it to its own (the order of the direct schedule's sum)
+        stage = _gloo(group) and partial.is_cuda
+        send = blocks[1 - li].detach().cpu() if stage else blocks[1 - li]
+        recv = torch.empty_like(send)
+        _relay(send, recv, ranks, li, other, True)
+        return blocks[li] + (recv.to(partial.device) if stage else recv)
     if not _gloo(group) and MODE == "ring":
         out = torch.empty_like(blocks[li])
         dist.reduce_scatter_tensor(out, partial, group=group)

@@ -1,3 +1,5 @@
 set -o pipefail
-for m in 0 11 0 11; do GNNEA_X3P_MODE=$m timeout -k 10 100 python tools/dbg/x3_modes.py 2>&1 | grep -v amdgpu.ids || exit 1; done
-GNNEA_X3P_MODE=11 timeout -k 10 200 python tools/dbg/x3p_big.py 2>&1 | grep -v amdgpu.ids || exit 1
+mkdir -p gpurun_out
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 4 --rehearse --entities 200000 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/rehearse4.log 2>&1 || { tail -30 gpurun_out/rehearse4.log; exit 1; }
+tail -1 gpurun_out/rehearse4.log | cut -c1-600
+bash tools/round_gpu_bench.sh
