@@ -15,16 +15,19 @@ Both take the KG group, its global ranks and this rank's index; gloo (the CPU re
 tests) runs the same point-to-point schedule on host tensors, staging device tensors through
 host memory.  GNNEA_HALO=ring selects the RCCL ring collectives instead (comparison only).
 
-Relay (4 GPUs, two KG groups of 2): the group's exchange alone would load ONE link per direction
-(the pair's), while the links to the other group's two GPUs sit idle.  ``all_gather`` given the
-other group's ranks (``other``) splits the block into quarters: q0 goes direct in phase 1, q1
-direct in phase 2, q2 / q3 go in phase 1 to the other group's GPUs, which forward them to the
-partner in phase 2 while this rank forwards theirs.  Every link carries one quarter per
-direction per phase, so the exchange takes two quarter-transfers instead of one whole-block
-transfer (half the time).  Both phases are world-group RCCL group calls issued back to back on
-the same communicator (stream-ordered: a phase-1 receive completes before the phase-2 send that
-forwards it); every rank of both groups must call it at the same point.  GNNEA_HALO=p2p keeps
-the direct schedule.
+Relay (two KG groups of g): the group's exchange alone loads the g-1 links inside the group
+while the g links to the other group's GPUs sit idle.  ``all_gather`` given the other group's
+ranks (``other``) cuts a rank's block into 2g units of rows: D1 (1 unit) and D2 (g-1 units) go
+direct to every group peer in phases 1 and 2; R_k (1 unit each, k < g) goes in phase 1 to the
+other group's k-th GPU, which forwards it in phase 2 to every one of this rank's group peers
+(the payload is the same for all of them, so each relayed byte crosses one first hop) while
+this rank forwards the other group's parts the same way.  Per direction every in-group link
+carries 1 unit in phase 1 and g-1 in phase 2, every cross-group link 1 unit in phase 1 and g-1
+in phase 2: g units in all instead of 2g, half the direct time at any g.  Both phases are
+world-group RCCL group calls issued back to back on the same communicator (stream-ordered: a
+phase-1 receive completes before the phase-2 send that forwards it); every rank of both groups
+must call it at the same point.  The reduce-scatter relays only at g = 2 (one block each way
+between the partners, the same schedule); GNNEA_HALO=p2p keeps the direct schedule.
 """
 import os
 
@@ -44,48 +47,57 @@ def _blocks(t, g):
 
 
 def relay_applies(ranks, other):
-    return MODE == "relay" and other is not None and len(ranks) == 2 and len(other) == 2
+    return MODE == "relay" and other is not None and len(ranks) == len(other) >= 2
 
 
-def _quarters(rows):
-    """Row ranges [q0, q1, q2, q3) of a block of ``rows`` rows (near-equal quarters)."""
-    cut = [rows * k // 4 for k in range(5)]
-    return [(cut[k], cut[k + 1]) for k in range(4)]
+def _units(rows, g):
+    """Row ranges of D1, D2, R_0..R_{g-1} (1, g-1, 1, ..., 1 of 2g near-equal units)."""
+    cut = [rows * j // (2 * g) for j in range(2 * g + 1)]
+    return [(cut[0], cut[1]), (cut[1], cut[g])] + [(cut[g + k], cut[g + k + 1]) for k in range(g)]
 
 
-def _relay(h_loc, part_full, ranks, li, other, sync):
-    """Two-phase relayed exchange of a 2-rank group (module docstring).  ``part_full``: the
-    partner's block of ``full``.  Global ranks throughout (world group)."""
-    me, partner = ranks[li], ranks[1 - li]
-    q = _quarters(h_loc.shape[0])
+def _relay(h_loc, full_parts, ranks, li, other, sync):
+    """Two-phase relayed all-gather over two groups of g (module docstring).  ``full_parts``:
+    the g blocks of ``full`` (this rank's is not written).  Global ranks throughout."""
+    me = ranks[li]
+    mine, theirs = sorted(ranks), sorted(other)
+    g = len(mine)
+    u = _units(h_loc.shape[0], g)
+    peers = [p for p in mine if p != me]
+    blk = {p: full_parts[ranks.index(p)] for p in peers}
 
-    def rows(t, k):
-        return t[q[k][0]:q[k][1]]
+    def rows(t, j):
+        return t[u[j][0]:u[j][1]]
 
-    # phase 1: q0 direct; q2 / q3 to the other group's GPUs (sorted); receive the other
-    # group's quarters this rank forwards (source s sends quarter 2 + index of me in the
-    # sorted ranks of this group)
-    mine = sorted(ranks)
-    stage = {s: torch.empty_like(rows(h_loc, 2 + mine.index(me))) for s in other}
-    ops1 = [dist.P2POp(dist.isend, rows(h_loc, 0), partner),
-            dist.P2POp(dist.irecv, rows(part_full, 0), partner)]
-    for k, o in enumerate(sorted(other)):
+    # phase 1: D1 to every group peer; R_k to the other group's k-th GPU; receive the other
+    # group's parts this rank forwards (source s sends R_{index of me among my group})
+    ki = mine.index(me)
+    stage = {s: torch.empty_like(rows(h_loc, 2 + ki)) for s in theirs}
+    ops1 = []
+    for p in peers:
+        ops1.append(dist.P2POp(dist.isend, rows(h_loc, 0), p))
+        ops1.append(dist.P2POp(dist.irecv, rows(blk[p], 0), p))
+    for k, o in enumerate(theirs):
         ops1.append(dist.P2POp(dist.isend, rows(h_loc, 2 + k), o))
-    for s in other:
-        ops1.append(dist.P2POp(dist.irecv, stage[s], s))
+        ops1.append(dist.P2POp(dist.irecv, stage[o], o))
     w1 = dist.batch_isend_irecv(ops1)
     if sync:
         for w in w1:
             w.wait()
-    # phase 2: q1 direct; forward each staged quarter to its source's partner; receive the
-    # partner's q2 / q3 from the relays
-    ops2 = [dist.P2POp(dist.isend, rows(h_loc, 1), partner),
-            dist.P2POp(dist.irecv, rows(part_full, 1), partner)]
-    for s in other:
-        dst = [r for r in other if r != s][0]
-        ops2.append(dist.P2POp(dist.isend, stage[s], dst))
-    for k, o in enumerate(sorted(other)):
-        ops2.append(dist.P2POp(dist.irecv, rows(part_full, 2 + k), o))
+    # phase 2: D2 to every group peer; forward each staged part to every other-group GPU but
+    # its source (destinations ascending, sources ascending); receive from the other group's
+    # k-th GPU the R_k of every group peer (same order)
+    ops2 = []
+    for p in peers:
+        ops2.append(dist.P2POp(dist.isend, rows(h_loc, 1), p))
+        ops2.append(dist.P2POp(dist.irecv, rows(blk[p], 1), p))
+    for dst in theirs:
+        for s in theirs:
+            if s != dst:
+                ops2.append(dist.P2POp(dist.isend, stage[s], dst))
+    for k, o in enumerate(theirs):
+        for p in peers:
+            ops2.append(dist.P2POp(dist.irecv, rows(blk[p], 2 + k), o))
     w2 = dist.batch_isend_irecv(ops2)
     if sync:
         for w in w2:
@@ -107,7 +119,7 @@ class _Keep:
 def all_gather(h_loc, full, group, ranks, li, copy_own=False, async_op=False, other=None):
     """Assemble the group's rows in ``full`` ([g·rows, D], contiguous).  Returns the works to
     wait on (an empty list when done synchronously).  ``other``: the other KG group's ranks;
-    with two groups of two the relayed schedule is taken (every rank must pass it then)."""
+    with two KG groups the relayed schedule is taken (every rank must pass it then)."""
     g = len(ranks)
     h_loc = h_loc.contiguous()
     parts = _blocks(full, g)
@@ -116,13 +128,14 @@ def all_gather(h_loc, full, group, ranks, li, copy_own=False, async_op=False, ot
     if g == 1:
         return []
     if relay_applies(ranks, other):
-        pf = parts[1 - li]
         if _gloo(group) and h_loc.is_cuda:  # host-staged rehearsal
-            hb = torch.empty(pf.shape, dtype=pf.dtype)
+            hb = [torch.empty(pp.shape, dtype=pp.dtype) for pp in parts]
             _relay(h_loc.detach().cpu(), hb, ranks, li, other, True)
-            pf.copy_(hb)
+            for p in range(g):
+                if p != li:
+                    parts[p].copy_(hb[p])
             return []
-        return _relay(h_loc, pf, ranks, li, other, _gloo(group) or not async_op)
+        return _relay(h_loc, parts, ranks, li, other, _gloo(group) or not async_op)
     if _gloo(group):
         src = h_loc.detach().cpu() if h_loc.is_cuda else h_loc
         bufs = [torch.empty_like(src) if full.is_cuda else parts[p] for p in range(g)]
@@ -162,13 +175,13 @@ def reduce_scatter(partial, group, ranks, li, other=None):
     if g == 1:
         return partial
     blocks = _blocks(partial, g)
-    if relay_applies(ranks, other):
+    if g == 2 and relay_applies(ranks, other):
         # one block each way between the partners: the relay with the partner's block as the
         # payload; the owner adds it to its own (the order of the direct schedule's sum)
         stage = _gloo(group) and partial.is_cuda
         send = blocks[1 - li].detach().cpu() if stage else blocks[1 - li]
         recv = torch.empty_like(send)
-        _relay(send, recv, ranks, li, other, True)
+        _relay(send, [recv, recv], ranks, li, other, True)
         return blocks[li] + (recv.to(partial.device) if stage else recv)
     if not _gloo(group) and MODE == "ring":
         out = torch.empty_like(blocks[li])

@@ -143,34 +143,34 @@ def _relay_worker(rank, world, port, rows, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        part = Partition(2 * rows, rank, world, "rows", 3)
+        part = Partition(world // 2 * rows, rank, world, "rows", 3)
         group = make_groups(part)
         ranks = part.group_ranks(part.kg)
         assert exchange.relay_applies(ranks, part.other_ranks())
         h = torch.arange(rows * 3, dtype=torch.float64).reshape(rows, 3) + 1000 * rank
-        full = torch.full((2 * rows, 3), -1.0, dtype=torch.float64)
+        full = torch.full((world // 2 * rows, 3), -1.0, dtype=torch.float64)
         exchange.all_gather(h, full, group, ranks, part.li, copy_own=True,
                             other=part.other_ranks())
-        partner = ranks[1 - part.li]
         want = torch.cat([torch.arange(rows * 3, dtype=torch.float64).reshape(rows, 3)
                           + 1000 * r for r in ranks])
-        q.put((rank, partner, float((full - want).abs().max())))
+        q.put((rank, float((full - want).abs().max())))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("rows", [1, 7, 100])
-def test_relay_exchange_world4(rows):
-    """The two-phase relay (quarters direct and through the other group's two GPUs) delivers
-    exactly the partner's block, for row counts that do not split into equal quarters."""
+@pytest.mark.parametrize("world,rows", [(4, 1), (4, 7), (4, 100), (8, 5), (8, 77)])
+def test_relay_exchange(world, rows):
+    """The two-phase relay (units direct and through the other group's GPUs) delivers exactly
+    every group peer's block, for row counts that do not split into equal units."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_relay_worker, args=(r, 4, port, rows, q)) for r in range(4)]
+    procs = [ctx.Process(target=_relay_worker, args=(r, world, port, rows, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    res = [q.get(timeout=5) for _ in range(4)]
-    assert all(err == 0.0 for _, _, err in res), res
+    res = [q.get(timeout=5) for _ in range(world)]
+    assert all(err == 0.0 for _, err in res), res
