@@ -26,8 +26,9 @@ carries 1 unit in phase 1 and g-1 in phase 2, every cross-group link 1 unit in p
 in phase 2: g units in all instead of 2g, half the direct time at any g.  Both phases are
 world-group RCCL group calls issued back to back on the same communicator (stream-ordered: a
 phase-1 receive completes before the phase-2 send that forwards it); every rank of both groups
-must call it at the same point.  The reduce-scatter relays only at g = 2 (one block each way
-between the partners, the same schedule); GNNEA_HALO=p2p keeps the direct schedule.
+must call it at the same point.  The reduce-scatter relays too (``_relay_rs``: its payloads
+differ per destination, so the split is g-1 / g-1 / 1.. units of 3g-2: 0.5 of the direct time at
+g = 2, 0.6 at g = 4); GNNEA_HALO=p2p keeps the direct schedule.
 """
 import os
 
@@ -50,10 +51,64 @@ def relay_applies(ranks, other):
     return MODE == "relay" and other is not None and len(ranks) == len(other) >= 2
 
 
-def _units(rows, g):
-    """Row ranges of D1, D2, R_0..R_{g-1} (1, g-1, 1, ..., 1 of 2g near-equal units)."""
-    cut = [rows * j // (2 * g) for j in range(2 * g + 1)]
-    return [(cut[0], cut[1]), (cut[1], cut[g])] + [(cut[g + k], cut[g + k + 1]) for k in range(g)]
+def _units(rows, g, d1=1, d2=None):
+    """Row ranges of D1, D2, R_0..R_{g-1}: d1, d2 (default g-1) and 1 each of near-equal units
+    (all-gather: 1, g-1, 1.. of 2g; reduce-scatter: g-1, g-1, 1.. of 3g-2)."""
+    d2 = g - 1 if d2 is None else d2
+    n = d1 + d2 + g
+    cut = [rows * j // n for j in range(n + 1)]
+    e = d1 + d2
+    return [(cut[0], cut[d1]), (cut[d1], cut[e])] + [(cut[e + k], cut[e + k + 1]) for k in range(g)]
+
+
+def _relay_rs(blocks, recv, ranks, li, other):
+    """Relayed exchange of a reduce-scatter over two groups of g: ``blocks[i]`` (this rank's
+    partial of group rank i's rows) goes to rank i, its D1 / D2 (g-1 units each) direct in
+    phases 1 / 2 and its R_k (1 unit of 3g-2) through the other group's k-th GPU; ``recv[p]``
+    receives peer p's partial of this rank's rows.  Per direction every link carries g-1 units
+    per phase: 2(g-1) of 3g-2 against the whole block direct (0.5 at g = 2, 0.6 at g = 4)."""
+    me = ranks[li]
+    mine, theirs = sorted(ranks), sorted(other)
+    g = len(mine)
+    u = _units(blocks[li].shape[0], g, g - 1, g - 1)
+    peers = [p for p in mine if p != me]
+
+    def rows(t, j):
+        return t[u[j][0]:u[j][1]]
+
+    def blk(p):
+        return blocks[ranks.index(p)]
+
+    ki = mine.index(me)
+    # stage[(s, dst)]: other-group source s's partial for dst, unit R_ki (this rank relays it)
+    stage = {(s, d): torch.empty_like(rows(blocks[li], 2 + ki))
+             for s in theirs for d in theirs if d != s}
+    ops1 = []
+    for p in peers:
+        ops1.append(dist.P2POp(dist.isend, rows(blk(p), 0), p))
+        ops1.append(dist.P2POp(dist.irecv, rows(recv[p], 0), p))
+    for k, o in enumerate(theirs):
+        for d in peers:
+            ops1.append(dist.P2POp(dist.isend, rows(blk(d), 2 + k), o))
+    for s_ in theirs:
+        for d in theirs:
+            if d != s_:
+                ops1.append(dist.P2POp(dist.irecv, stage[(s_, d)], s_))
+    for w in dist.batch_isend_irecv(ops1):
+        w.wait()
+    ops2 = []
+    for p in peers:
+        ops2.append(dist.P2POp(dist.isend, rows(blk(p), 1), p))
+        ops2.append(dist.P2POp(dist.irecv, rows(recv[p], 1), p))
+    for d in theirs:
+        for s_ in theirs:
+            if s_ != d:
+                ops2.append(dist.P2POp(dist.isend, stage[(s_, d)], d))
+    for k, o in enumerate(theirs):
+        for p in peers:
+            ops2.append(dist.P2POp(dist.irecv, rows(recv[p], 2 + k), o))
+    for w in dist.batch_isend_irecv(ops2):
+        w.wait()
 
 
 def _relay(h_loc, full_parts, ranks, li, other, sync):
@@ -169,20 +224,22 @@ def all_gather(h_loc, full, group, ranks, li, copy_own=False, async_op=False, ot
 
 def reduce_scatter(partial, group, ranks, li, other=None):
     """This rank's rows of the group sum of the [g·rows, D] partials.  ``other`` as in
-    all_gather: with two groups of two the partner's block travels by the relayed schedule."""
+    all_gather: the relayed schedule (``_relay_rs``) when given."""
     g = len(ranks)
     partial = partial.contiguous()
     if g == 1:
         return partial
     blocks = _blocks(partial, g)
-    if g == 2 and relay_applies(ranks, other):
-        # one block each way between the partners: the relay with the partner's block as the
-        # payload; the owner adds it to its own (the order of the direct schedule's sum)
+    if relay_applies(ranks, other):
         stage = _gloo(group) and partial.is_cuda
-        send = blocks[1 - li].detach().cpu() if stage else blocks[1 - li]
-        recv = torch.empty_like(send)
-        _relay(send, [recv, recv], ranks, li, other, True)
-        return blocks[li] + (recv.to(partial.device) if stage else recv)
+        send = [b.detach().cpu() if stage else b for b in blocks]
+        recv = {p: torch.empty_like(send[li]) for p in ranks if p != ranks[li]}
+        _relay_rs(send, recv, ranks, li, other)
+        out = blocks[li].clone()
+        for p in ranks:  # peer order, as the direct schedule sums
+            if p != ranks[li]:
+                out += recv[p].to(out.device) if stage else recv[p]
+        return out
     if not _gloo(group) and MODE == "ring":
         out = torch.empty_like(blocks[li])
         dist.reduce_scatter_tensor(out, partial, group=group)

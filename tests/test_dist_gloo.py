@@ -153,15 +153,25 @@ def _relay_worker(rank, world, port, rows, q):
                             other=part.other_ranks())
         want = torch.cat([torch.arange(rows * 3, dtype=torch.float64).reshape(rows, 3)
                           + 1000 * r for r in ranks])
-        q.put((rank, float((full - want).abs().max())))
+        err = float((full - want).abs().max())
+        # reduce-scatter: rank r's partial of every group row is (r + 1) * base; the owner's
+        # rows must come back summed over the group
+        g = len(ranks)
+        base = torch.arange(g * rows * 3, dtype=torch.float64).reshape(g * rows, 3)
+        got = exchange.reduce_scatter((rank + 1) * base, group, ranks, part.li,
+                                      other=part.other_ranks())
+        want_rs = sum(r + 1 for r in ranks) * base[part.li * rows:(part.li + 1) * rows]
+        err = max(err, float((got - want_rs).abs().max()))
+        q.put((rank, err))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,rows", [(4, 1), (4, 7), (4, 100), (8, 5), (8, 77)])
 def test_relay_exchange(world, rows):
-    """The two-phase relay (units direct and through the other group's GPUs) delivers exactly
-    every group peer's block, for row counts that do not split into equal units."""
+    """The two-phase relays (units direct and through the other group's GPUs) deliver exactly
+    every group peer's block (all-gather) and the group sum of the owner's rows (reduce-scatter),
+    for row counts that do not split into equal units."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
