@@ -14,6 +14,10 @@
 // Split-K for the weight gradients as in gemm.hip: fp32 slabs, fixed-order reduction.
 #include "common.h"
 
+#include <stdlib.h>
+
+#include <type_traits>
+
 namespace gnnea {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -98,7 +102,7 @@ __device__ __forceinline__ int64_t c_index_bf(int64_t row, int64_t col, int64_t 
   return (col >> 7) * cs + row * ldc + (col & 127);
 }
 
-template <int TA, int TB, int WT, bool VEC, typename TC>
+template <int TA, int TB, int WT, bool VEC, typename TC, int EPI = 0>
 __global__ __launch_bounds__(256) void k_gemm_bf16(int M, int N, int K,
                                                    const bf16_t* __restrict__ A, int64_t lda,
                                                    const bf16_t* __restrict__ B, int64_t ldb,
@@ -165,6 +169,36 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(int M, int N, int K,
   }
 
   // epilogue: 32x32 C/D map  col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  if constexpr (EPI == 1) {
+    // bf16 C, no split, beta = 0, 8-B aligned rows (host-checked): the tile is rounded into LDS
+    // (free after the loop's last barrier; [64][BN + 8] bf16 <= the operand buffers) and leaves
+    // as 8-B row chunks, consecutive lanes on consecutive chunks of a row, instead of one 2-B
+    // store per element per lane
+    constexpr int TLD = BN + 8;
+    bf16_t* T = smem;
+#pragma unroll
+    for (int t = 0; t < WT; ++t) {
+      const int cl = wn * 32 * WT + t * 32 + li;
+      const float bv = (bias && n0 + cl < N) ? bias[n0 + cl] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        T[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh) * TLD + cl] = from_f32<bf16_t>(acc[t][r] + bv);
+    }
+    __syncthreads();
+    for (int idx = tid; idx < HBM * (BN / 4); idx += 256) {
+      const int rl = idx / (BN / 4), c4 = idx - rl * (BN / 4);
+      const int row = m0 + rl, col = n0 + 4 * c4;
+      if (row >= M || col >= N) continue;
+      const bf16_t* src = T + rl * TLD + 4 * c4;
+      bf16_t* dst = (bf16_t*)C + c_index_bf(row, col, ldc, cs);
+      if (col + 4 <= N) {
+        *(uint2*)dst = *(const uint2*)src;
+      } else {
+        for (int e = 0; col + e < N; ++e) dst[e] = src[e];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < WT; ++t) {
     const int col = n0 + wn * 32 * WT + t * 32 + li;
@@ -228,11 +262,27 @@ static int bf16_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
   return (int)(s < 1 ? 1 : s);
 }
 
+static bool bf16_lds_epilogue() {
+  static const bool on = [] {  // A/B comparison only (GNNEA_BF16_EPI=0: per-element stores)
+    const char* e = getenv("GNNEA_BF16_EPI");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int TA, int TB, int WT, typename TC>
 static void launch_bf16_wt(dim3 grid, hipStream_t s, bool vec, int M, int N, int K,
                            const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
                            const float* bias, float beta, TC* C, int64_t ldc, int64_t cs,
                            int kps, float* slab, int tiles_n) {
+  if constexpr (std::is_same<TC, bf16_t>::value) {
+    if (vec && !slab && beta == 0.f && (((uintptr_t)C) & 7) == 0 && ldc % 4 == 0 &&
+        cs % 4 == 0 && bf16_lds_epilogue()) {
+      hipLaunchKernelGGL((k_gemm_bf16<TA, TB, WT, true, TC, 1>), grid, dim3(256), 0, s, M, N,
+                         K, A, lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n);
+      return;
+    }
+  }
   if (vec)
     hipLaunchKernelGGL((k_gemm_bf16<TA, TB, WT, true, TC>), grid, dim3(256), 0, s, M, N, K, A,
                        lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n);
