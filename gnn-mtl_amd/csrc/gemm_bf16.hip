@@ -24,6 +24,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16_b __attribute__((ext_vector_type(16)));
 
 constexpr int HBM = 64, HBK = 32, HLD = HBK + 8;
+#ifndef GNNEA_BF16_TRANS_QUADS
+#define GNNEA_BF16_TRANS_QUADS 1
+#endif
+constexpr bool TRANS_QUADS = GNNEA_BF16_TRANS_QUADS;  // 0: HLoader's 2-B transposing stores
 
 __device__ __forceinline__ bf16_t u4_elem(const uint4& v, int e) {
   const uint32_t w = e < 2 ? v.x : e < 4 ? v.y : e < 6 ? v.z : v.w;
@@ -95,6 +99,59 @@ struct HLoader {
   }
 };
 
+// ROWS x HBK tile of op(X) = X^T (rows contiguous in memory, VEC layout) in registers as quads
+// of 4 k x 8 rows (four 16-B row-runs, each two 8-B loads), written to LDS as 8 ds_write_b64 of
+// 4 consecutive k per row: a quarter of the store instructions of HLoader's 2-B transposing
+// stores.  Taken for the wide operand only (ROWS >= 256: the B tile): on the 64-row A tile the
+// 64 quads fall to one wave, whose longer load/store chain every k-step then waits on (dW =
+// dY^T X with both tall operands quad-loaded measured 3.7x slower), and only without split-K
+// (QT: the split-K weight gradients, 800 k-steps per workgroup at 2M rows, measured 2.4x slower
+// with the quad B tile as well; dX = dY W, K = 300, 1.91 -> 1.37 ms at 2M rows with it).
+template <int ROWS>
+struct HLoaderT {
+  static constexpr int NQ = ROWS * HBK / 32;     // quads per tile
+  static constexpr int NQT = (NQ + 255) / 256;   // per thread (the last pass partly idle)
+  uint4 r[NQT][4];
+  __device__ void load(const bf16_t* __restrict__ X, int64_t ld, int row0, int nrows, int k0,
+                       int kend, int tid) {
+#pragma unroll
+    for (int q = 0; q < NQT; ++q) {
+      const int idx = tid + 256 * q;
+      const int k = (idx % (HBK / 4)) * 4, gr = row0 + (idx / (HBK / 4)) * 8;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        uint2 lo = make_uint2(0u, 0u), hi = make_uint2(0u, 0u);
+        const int gk = k0 + k + kk;
+        if ((NQ % 256 == 0 || idx < NQ) && gk < kend) {
+          const bf16_t* p = X + (int64_t)gk * ld + gr;
+          if (gr < nrows) lo = *(const uint2*)p;
+          if (gr + 4 < nrows) hi = *(const uint2*)(p + 4);
+        }
+        r[q][kk] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+    }
+  }
+  __device__ void store(bf16_t* __restrict__ S, int tid) const {
+#pragma unroll
+    for (int q = 0; q < NQT; ++q) {
+      const int idx = tid + 256 * q;
+      if (NQ % 256 != 0 && idx >= NQ) continue;
+      const int k = (idx % (HBK / 4)) * 4, row = (idx / (HBK / 4)) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t lo = (uint32_t)u4_elem(r[q][0], e) | ((uint32_t)u4_elem(r[q][1], e) << 16);
+        const uint32_t hi = (uint32_t)u4_elem(r[q][2], e) | ((uint32_t)u4_elem(r[q][3], e) << 16);
+        *(uint2*)(S + (row + e) * HLD + k) = make_uint2(lo, hi);
+      }
+    }
+  }
+};
+
+template <bool K_CONTIG, int ROWS, bool VEC, bool QT>
+using HLoad = typename std::conditional<!K_CONTIG && VEC && QT && TRANS_QUADS && ROWS >= 256,
+                                        HLoaderT<ROWS>,
+                                        HLoader<K_CONTIG, ROWS, VEC>>::type;
+
 // Output addressing: element (row, col) at (col / 128)·cs + row·ldc + col % 128.  cs = 128 is the
 // plain row-major matrix; ldc = 128, cs = n·128 the bf16 slice-major table (256-B slices) that
 // gnnea_spmm_sliced_bf16 gathers from.
@@ -102,7 +159,7 @@ __device__ __forceinline__ int64_t c_index_bf(int64_t row, int64_t col, int64_t 
   return (col >> 7) * cs + row * ldc + (col & 127);
 }
 
-template <int TA, int TB, int WT, bool VEC, typename TC, int EPI = 0>
+template <int TA, int TB, int WT, bool VEC, typename TC, int EPI = 0, bool QT = false>
 __global__ __launch_bounds__(256) void k_gemm_bf16(int M, int N, int K,
                                                    const bf16_t* __restrict__ A, int64_t lda,
                                                    const bf16_t* __restrict__ B, int64_t ldb,
@@ -133,8 +190,8 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(int M, int N, int K,
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
 
-  HLoader<AK, HBM, VEC> la;
-  HLoader<BKc, BN, VEC> lb;
+  HLoad<AK, HBM, VEC, QT> la;
+  HLoad<BKc, BN, VEC, QT> lb;
   const int nsteps = ke > kb ? (ke - kb + HBK - 1) / HBK : 0;
   if (nsteps > 0) {
     la.load(A, lda, m0, M, kb, ke, tid);
@@ -278,10 +335,15 @@ static void launch_bf16_wt(dim3 grid, hipStream_t s, bool vec, int M, int N, int
   if constexpr (std::is_same<TC, bf16_t>::value) {
     if (vec && !slab && beta == 0.f && (((uintptr_t)C) & 7) == 0 && ldc % 4 == 0 &&
         cs % 4 == 0 && bf16_lds_epilogue()) {
-      hipLaunchKernelGGL((k_gemm_bf16<TA, TB, WT, true, TC, 1>), grid, dim3(256), 0, s, M, N,
-                         K, A, lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n);
+      hipLaunchKernelGGL((k_gemm_bf16<TA, TB, WT, true, TC, 1, true>), grid, dim3(256), 0, s, M,
+                         N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n);
       return;
     }
+  }
+  if (vec && !slab && TB == 0) {
+    hipLaunchKernelGGL((k_gemm_bf16<TA, TB, WT, true, TC, 0, true>), grid, dim3(256), 0, s, M, N,
+                       K, A, lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n);
+    return;
   }
   if (vec)
     hipLaunchKernelGGL((k_gemm_bf16<TA, TB, WT, true, TC>), grid, dim3(256), 0, s, M, N, K, A,

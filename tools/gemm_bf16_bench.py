@@ -53,7 +53,18 @@ def main():
     ms = timeit(lambda: ops.gemm(X, W, trans_b=True, bias=b), args.reps)
     bl = b.to(torch.bfloat16)
     ms_t = timeit(lambda: torch.nn.functional.linear(X, W, bl), args.reps)
+    dY = torch.randn(M, D, device=dev, generator=g).to(torch.bfloat16)
+    dW = ops.gemm(dY, X, trans_a=True)
+    refw = dY[:65536].float().t() @ X[:65536].float()
+    dW_part = ops.gemm(dY[:65536], X[:65536], trans_a=True)
+    errw = float(((dW_part.float() - refw).abs() / (refw.abs() + 1e-1)).max())
+    ms_w = timeit(lambda: ops.gemm(dY, X, trans_a=True), args.reps)
+    ms_wt = timeit(lambda: torch.mm(dY.t(), X), args.reps)
+    ms_x = timeit(lambda: ops.gemm(dY, W), args.reps)
+    del dW
     print(json.dumps({"rows": M, "epilogue": os.environ.get("GNNEA_BF16_EPI", "1"),
+                      "dW_ms": round(ms_w, 4), "dW_hipblaslt_ms": round(ms_wt, 4),
+                      "dW_max_rel_err_vs_fp32": errw, "dX_ms": round(ms_x, 4),
                       "gnnea_ms": round(ms, 4), "gnnea_GBps_io": round(io / ms / 1e6, 1),
                       "gnnea_TFLOPs": round(2.0 * M * D * D / ms / 1e9, 1),
                       "hipblaslt_ms": round(ms_t, 4), "max_rel_err_vs_fp32": err}))
