@@ -315,7 +315,7 @@ def main():
                     help="N > 1: skip the labelled exchange-free side number (tiles)")
     ap.add_argument("--no-train", action="store_true",
                     help="skip the side measurement of the row-sharded HGCN-EA training step")
-    ap.add_argument("--train-steps", type=int, default=5)
+    ap.add_argument("--train-steps", type=int, default=21)
     ap.add_argument("--layout", choices=("sliced", "rowmajor"), default="sliced",
                     help="feature table layout of the aggregation input (sliced: 64-column "
                          "slices, each one Infinity-Cache-sized table at 1M rows)")
@@ -472,7 +472,7 @@ def main():
     if not args.no_train and not args.rehearse:
         try:
             from tools.dist_step import measure
-            train = measure("HGCN", n, rank, world, device, args.train_steps, 1)
+            train = measure("HGCN", n, rank, world, device, args.train_steps, 3)
         except Exception as e:  # report, never hide
             train = {"error": repr(e)}
     sk_shard = None

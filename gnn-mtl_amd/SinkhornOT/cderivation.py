@@ -8,7 +8,7 @@ bf16 on gnnea.ops.gemm.  get_init_matrices' two products are matrix-vector produ
 disguise (every column of C1²·repeat(mu) is C1²·mu): they run as [I, 1] / [J, 1] GEMMs and
 constC is their broadcast sum.  Elementwise work stays in torch.  The Sinkhorn inner solves
 that consume these costs run on the gnnea kernels (SinkhornOT/sinkhorn_loss.py).  Distance helpers outside the GW path
-(energy distances, ...) are taken from the reference module when GNNEA_UPSTREAM names its checkout.
+(energy distances, ...) are out of scope.
 """
 import math
 
@@ -111,13 +111,3 @@ def FGW_cost_matrix(D, constC, hC1, hC2, T, alpha, epsilon, p):
     """cderivation.py:185-188: fused cost (1 - alpha) D^p + alpha L^p and its entropic form."""
     A = (1 - alpha) * D ** p + alpha * get_LT(constC, hC1, hC2, T) ** p
     return A, A - epsilon * torch.log(T)
-
-
-def _merge_upstream():
-    """Opt-in (GNNEA_UPSTREAM=<reference checkout>, gnnea/upstream.py): the reference module's
-    remaining helpers."""
-    from gnnea import upstream
-    upstream.merge(globals(), "SinkhornOT/cderivation.py", "SinkhornOT._upstream_cderivation")
-
-
-_merge_upstream()

@@ -72,6 +72,19 @@ __global__ __launch_bounds__(256) void k_gat_rowstats(const int32_t* __restrict_
   }
 }
 
+// every 64-column slice must hold at most two heads (the kernels keep h0 / h1 per slice and two
+// product partials per edge): d_head >= 64, or d_head in [32, 63] with no slice straddling three
+// heads (d_head 40: slice 1 = columns 64..127 = heads 1, 2, 3 -> refused)
+static bool gat_two_heads_per_slice(int heads, int d_head) {
+  if (heads < 1 || d_head < 32) return false;
+  const int D = heads * d_head;
+  for (int s = 0; 64 * s < D; ++s) {
+    const int h0 = (64 * s) / d_head, h1 = min((64 * s + 63) / d_head, heads - 1);
+    if (h1 - h0 > 1) return false;
+  }
+  return true;
+}
+
 template <int ACT, int U, typename TY>
 __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, int n_rows, int nbs,
@@ -465,8 +478,8 @@ extern "C" int gnnea_gat_fwd_sliced_f32(const int32_t* rowptr, const int32_t* co
                                         void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int D = heads * d_head;
-  if (n_rows < 0 || heads < 1 || heads > 8 || d_head < 32 || D % 4 || sstride % 64 ||
-      ldy % 4 || ldy < D)
+  if (n_rows < 0 || heads < 1 || heads > 8 || !gat_two_heads_per_slice(heads, d_head) ||
+      D % 4 || sstride % 64 || ldy % 4 || ldy < D)
     return GNNEA_EINVAL;
   if (act != GNNEA_ACT_IDENTITY && act != GNNEA_ACT_RELU) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
@@ -527,7 +540,8 @@ static int gat_dst_lanes() {
 
 static bool gat_sl_shape(int heads, int d_head, int64_t sstride) {
   const int D = heads * d_head;
-  return heads >= 1 && heads <= 8 && d_head >= 32 && D % 4 == 0 && D <= 1024 && sstride % 64 == 0;
+  return heads >= 1 && heads <= 8 && gat_two_heads_per_slice(heads, d_head) && D % 4 == 0 &&
+         D <= 1024 && sstride % 64 == 0;
 }
 
 // G (slice-major [ceil(D/64)][n_rows][64], sstride floats per slice) and the records

@@ -893,6 +893,24 @@ def _pad4(t, D, dtype=None):
 GAT_SLICED = True  # tests switch it off to compare with the row-major edge pass
 
 
+def gat_two_heads_per_slice(heads, d_head):
+    """The sliced GAT kernels keep two heads per 64-column slice (h0 / h1, two product partials
+    per edge): every slice s must satisfy min((64s+63)//d, H-1) - (64s)//d <= 1 (d_head >= 64,
+    or 32 / 48 / ...; d_head = 40 puts heads 1, 2, 3 in slice 1 and is refused)."""
+    if heads < 1 or d_head < 32:
+        return False
+    D = heads * d_head
+    return all(min((64 * s + 63) // d_head, heads - 1) - (64 * s) // d_head <= 1
+               for s in range((D + 63) // 64))
+
+
+def _gat_sliced_applies(H, heads, d_head, Y):
+    D = heads * d_head
+    return (GAT_SLICED and H.dtype == torch.float32 and gat_two_heads_per_slice(heads, d_head)
+            and D % 4 == 0 and heads <= 8 and D <= 1024 and Y.shape[1] == D
+            and use_sliced(H.shape[0], D, H.dtype))
+
+
 def gat_forward(csr, H, a32, heads, d_head, alpha, act, em=None, row0=0):
     """All heads of the GAT aggregation over ``csr`` (one edge pass per KG block).
 
@@ -907,9 +925,7 @@ def gat_forward(csr, H, a32, heads, d_head, alpha, act, em=None, row0=0):
     Y = torch.empty((N, (D + 3) // 4 * 4), dtype=H.dtype, device=H.device)
     m = torch.empty((N, heads), dtype=torch.float32, device=H.device)
     den = torch.empty_like(m)
-    if (GAT_SLICED and H.dtype == torch.float32 and d_head >= 32 and D % 4 == 0
-            and heads <= 8 and D <= 1024 and Y.shape[1] == D
-            and use_sliced(H.shape[0], D, H.dtype)):
+    if _gat_sliced_applies(H, heads, d_head, Y):
         # above the Infinity Cache: the table slice-major (64-column slices, one 256-MB table
         # per KG slice), row statistics once, then the slices one after another
         Hs = sliced_copy_of(H, D)
@@ -957,9 +973,7 @@ def gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha, act, 
     dzT = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=dev)
     ds1 = torch.empty((N, heads), dtype=torch.float32, device=dev)
     ds2 = torch.empty((H.shape[0], heads), dtype=torch.float32, device=dev)
-    if (GAT_SLICED and H.dtype == torch.float32 and d_head >= 32 and D % 4 == 0
-            and heads <= 8 and D <= 1024 and Y.shape[1] == D
-            and use_sliced(H.shape[0], D, H.dtype)):
+    if _gat_sliced_applies(H, heads, d_head, Y):
         _gat_backward_sliced(csr, csrT, H, a32, s1, s2, m, den, Y, dY, heads, d_head,
                              alpha, act, em, row0, rec, dH, dzT, ds1, ds2)
     else:

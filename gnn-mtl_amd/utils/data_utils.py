@@ -7,7 +7,7 @@ signatures and outputs; the per-line / per-triple Python loops are replaced by t
 library (gnnea.ingest: parallel parsing, counting-sort adjacency in the reference's dict order)
 and vectorised numpy / scipy.  Entry order and fp32 values of the adjacency are bit-identical
 (tests/test_adjacency.py, tests/test_ingest.py).  The other task loaders of the reference module
-(node classification, text) are re-exported from it when GNNEA_UPSTREAM names its checkout (gnnea/upstream.py).
+(node classification, text) are out of scope.
 """
 import json
 
@@ -179,33 +179,8 @@ def load_seperate_data_ea(args):
 
 
 def load_data(args):
-    """(:17-26) task dispatch; the entity-alignment task is served here, the others by the
-    reference module's loaders (opt-in: GNNEA_UPSTREAM)."""
+    """(:17-26) task dispatch; only the entity-alignment task is on this tier's path."""
     if args.task == 'ea':
         return load_data_ea(args)
-    up = globals().get('_upstream_load_data')
-    if up is None:
-        raise NotImplementedError("gnnea: only task 'ea' is rebuilt; the reference's "
-                                  "utils/data_utils.py is needed for task %r" % args.task)
-    return up(args)
-
-
-def _merge_upstream():
-    """Opt-in (GNNEA_UPSTREAM=<reference checkout>, gnnea/upstream.py): the reference's loaders
-    for the other tasks; our EA loaders are installed into the reference module."""
-    from gnnea import upstream
-    ours = ("sparse_mx_to_torch_sparse_tensor", "get_matrix", "get_sparse_tensor",
-            "get_sparse_tensor_for_one_graph", "loadfile", "rfunc", "get_features",
-            "load_data_ea", "load_seperate_data_ea")
-    mod = upstream.load("utils/data_utils.py", "utils._upstream_data_utils")
-    if mod is None:
-        return
-    globals()['_upstream_load_data'] = getattr(mod, 'load_data', None)
-    for k, v in vars(mod).items():
-        if not k.startswith("__") and k not in ours:
-            globals().setdefault(k, v)
-    for k in ours:
-        setattr(mod, k, globals()[k])
-
-
-_merge_upstream()
+    raise NotImplementedError("gnnea: only task 'ea' is rebuilt (the reference's NC / LP / text "
+                              "loaders are out of scope, DESIGN.md §7); got task %r" % args.task)

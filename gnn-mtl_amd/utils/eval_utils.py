@@ -4,8 +4,8 @@ get_hits (utils/eval_utils.py:71-98) builds the full fp64 cityblock matrix with 
 and argsorts every row and column.  Here the rank of the true match is counted directly on the
 device (gnnea_l1_rank_f32: #closer candidates + #equal candidates of lower index), which is the
 position of i in a stable argsort of the same fp64 distances; only the counts come back.
-Node-classification helpers (acc_f1, nc_metrics, ...) are not on the alignment path and are taken
-from the reference module when GNNEA_UPSTREAM names its checkout (gnnea/upstream.py).
+Node-classification helpers (acc_f1, nc_metrics, ...) are not on the alignment path and are out
+of scope.
 """
 
 import numpy as np
@@ -79,13 +79,3 @@ def eval_at_1(outputs, data):
     idx, _ = l1.nearest(outputs[li], outputs[ri])
     cnt = (idx == torch.arange(len(li), device=outputs.device)).float()
     return torch.sum(cnt) / len(cnt) * 100
-
-
-def _merge_upstream():
-    """Opt-in (GNNEA_UPSTREAM=<reference checkout>, gnnea/upstream.py): the reference module's
-    remaining helpers."""
-    from gnnea import upstream
-    upstream.merge(globals(), "utils/eval_utils.py", "utils._upstream_eval_utils")
-
-
-_merge_upstream()

@@ -91,21 +91,41 @@ def measure(model, n, rank, world, dev, steps, warmup, dtype=torch.float32):
         if world > 1:
             allreduce_grads(params)
 
-    for _ in range(warmup):
+    # SURVEY.md §8d timing: >= 3 warm-ups, then per-step HIP events on the launching stream,
+    # median of >= 21 steps (max over ranks step by step); the wall-clock mean is kept beside it
+    warmup, steps = max(3, warmup), max(21, steps)
+    wev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(warmup)]
+    for a, b in wev:  # timed too: first-use costs (allocator growth, lazy transposes) show here
+        a.record()
         step()
+        b.record()
     torch.cuda.synchronize()
+    warm_ms = [round(a.elapsed_time(b), 2) for a, b in wev]
     if world > 1:
         dist.barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
     t1 = time.perf_counter()
-    for _ in range(steps):
+    for a, b in evs:
+        a.record()
         step()
+        b.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+    per = torch.tensor([a.elapsed_time(b) for a, b in evs] + [(time.perf_counter() - t1) * 1e3],
+                       dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    ms = float(el) / steps * 1e3
+        dist.all_reduce(per, op=dist.ReduceOp.MAX)
+    per = per.cpu()
+    wall_ms = float(per[-1]) / steps
+    per = per[:-1]
+    ms = float(per.median())
+    if rank == 0:
+        print("warm-up ms: %s; per-step ms: %s" % (warm_ms, " ".join("%.2f" % v
+                                                                  for v in per.tolist())),
+              file=sys.stderr)
     nnz = torch.tensor([float(dadj.nnz)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(nnz)  # row shards: every edge of the graph once
@@ -117,6 +137,9 @@ def measure(model, n, rank, world, dev, steps, warmup, dtype=torch.float32):
             "graph": "2x%d entities, %d nnz" % (n, int(nnz)),
             "dtype": "bf16 storage, f32 arithmetic" if dtype == torch.bfloat16 else "f32",
             "n_gpus": world, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 3),
+            "timing": "median of per-step HIP events (max over ranks)",
+            "ms_min_max": [round(float(per.min()), 3), round(float(per.max()), 3)],
+            "ms_wall_mean": round(wall_ms, 3), "ms_warmup_steps_rank0": warm_ms,
             "steps_per_s": round(1e3 / ms, 2),
             # 3 aggregations forward + 3 transposed aggregations backward per step
             "edges_per_s_fwd_bwd": round(6 * float(nnz) / ms * 1e3, 1),
