@@ -190,44 +190,81 @@ def gw_rate(device, B=3000):
             "peak_TFLOPs": 78.6, "peak_source": "AMD MI355X spec FP64 matrix (not in MI355X_MICROARCH.md)"}
 
 
-def bf16_rate(shard, H, steps):
-    """The same aggregation with bf16 feature storage (cfg-5's dtype, fp32 arithmetic): the
-    table slice-major (128-column slices, as gnnea_gemm_sliced_bf16 writes it) where it applies,
-    the row-major kernel beside it."""
-    Hb = H.to(torch.bfloat16)
-    Yb = torch.empty((shard.n_rows, H.shape[1]), dtype=torch.bfloat16, device=H.device)
+def bf16_rate(device, steps):
+    """The aggregation with bf16 feature storage (cfg-5's dtype, fp32 arithmetic) on cfg-5's
+    own graph (synth.CONFIGS["cfg5"]: 2 x 2M entities, 2 x 20M triples, ~84M nnz): the table
+    slice-major (ops.spmm_sliced's bf16 layout) and the row-major kernel beside it."""
+    cf = synth.CONFIGS["cfg5"]
+    t0 = time.time()
+    shard = KGShard(cf["n"], cf["t"], cf["n_rel"], 0, 1, device, kind="rows", D=D)
+    build_s = time.time() - t0
+    gen = torch.Generator(device=device).manual_seed(5)
+    Hb = torch.randn(shard.n_cols, D, device=device, generator=gen)
+    Hb /= Hb.norm(dim=1, keepdim=True)
+    Hb = Hb.to(torch.bfloat16)
+    Yb = torch.empty((shard.n_rows, D), dtype=torch.bfloat16, device=device)
     relu = _lib.GNNEA_ACT_RELU
-    sliced = ops.use_sliced(shard.n_cols, H.shape[1], torch.bfloat16)
+    sliced = ops.use_sliced(shard.n_cols, D, torch.bfloat16)
     ms_row = _timed(lambda: ops.spmm(shard.csr, Hb, relu, out=Yb), steps)
+    W = ops.slice_w(torch.bfloat16)
     if sliced:
         Hs = ops.slice_pack(Hb)
-        ms = _timed(lambda: ops.spmm_sliced(shard.csr, Hs, H.shape[1], relu, out=Yb), steps)
+        ms = _timed(lambda: ops.spmm_sliced(shard.csr, Hs, D, relu, out=Yb), steps)
+        del Hs
     else:
         ms = ms_row
-    traffic = gather_model_bytes(shard.n_rows, shard.nnz, H.shape[1], elem=2)
+    traffic = gather_model_bytes(shard.n_rows, shard.nnz, D, elem=2)
+    launches = len(shard.csr.row_blocks())
     achieved = traffic / (ms * 1e-3) / 1e9
-    return {"value": round(shard.nnz / ms * 1e3, 1), "unit": "edges/s", "ms_per_step": round(ms, 4),
-            "dtype": "bf16 storage, f32 accumulate", "steps": steps,
-            "layout": "slice-major (128-column slices)" if sliced else "row-major",
-            "rowmajor_edges_per_s": round(shard.nnz / ms_row * 1e3, 1),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "kernel": ("gnnea::k_spmm_sliced<relu,4,bf16,bf16>" if sliced else
-                                    "gnnea::k_spmm_v4<relu,act,2,bf16,bf16>"),
-                         "model": "gather: 4(N+1)+8E+2ED+2ND"}}
+    out = {"graph": "cfg-5: 2x%d entities, 2x%d triples, %d nnz (built in %.1f s)"
+                    % (cf["n"], cf["t"], shard.nnz, build_s),
+           "value": round(shard.nnz / ms * 1e3, 1), "unit": "edges/s", "ms_per_step": round(ms, 4),
+           "dtype": "bf16 storage, f32 accumulate", "timing": TIMING,
+           "layout": ("slice-major (%d-column slices: %d MB per KG slice)"
+                      % (W, cf["n"] * W * 2 >> 20)) if sliced else "row-major",
+           "rowmajor_edges_per_s": round(shard.nnz / ms_row * 1e3, 1),
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "kernel": ("gnnea::k_spmm_sliced<relu,4,bf16,bf16>" if sliced else
+                                   "gnnea::k_spmm_v4<relu,act,2,bf16,bf16>"),
+                        "launches_per_step": launches,
+                        "model": "gather: 4(N+1)+8E+2ED+2ND"}}
+    del shard, Hb, Yb
+    torch.cuda.empty_cache()
+    return out
+
+
+TIMING = "median of >= 21 per-call HIP events after 3 warm-ups"
 
 
 def _timed(fn, steps):
+    """Median of max(21, steps) per-call HIP-event durations (ms) after 3 warm-up calls
+    (SURVEY.md §8d)."""
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(steps):
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(max(21, steps))]
+    for a, b in evs:
+        a.record()
         fn()
-    b.record()
+        b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / steps
+    return float(np.median([a.elapsed_time(b) for a, b in evs]))
+
+
+def copy_rate(device, nbytes=4 << 30):
+    """Device-to-device copy bandwidth of one HBM buffer into another (read + write bytes per
+    second), to report beside the 8 TB/s datasheet figure."""
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=device).fill_(1.0)
+    dst = torch.empty_like(src)
+    ms = _timed(lambda: dst.copy_(src), 21)
+    del src, dst
+    torch.cuda.empty_cache()
+    return {"GBps": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "bytes": 2 * nbytes,
+            "ms": round(ms, 4), "peak_spec_GBps": HBM_PEAK_GBS,
+            "frac_of_spec": round(2 * nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "method": "torch copy_ of a %d-MiB fp32 buffer, %s" % (nbytes >> 20, TIMING)}
 
 
 def layout_rates(shard, H, Y, steps):
@@ -355,8 +392,6 @@ def main():
     h_local = torch.randn(shard.n_cols if (world == 1 or free) else shard.n_rows, Dl,
                           device=device, generator=gen)
     h_local /= h_local.norm(dim=1, keepdim=True)
-    h_full = (torch.empty(shard.n_cols, Dl, device=device)
-              if shard.g > 1 and part.kind == "rows" else None)
     y = torch.empty(shard.n_rows, Dl, device=device)
     # H as the projection GEMM of a GCN layer leaves it: slice-major [ceil(D/64)][rows][64]
     # (gnnea_gemm_sliced_f32 writes this layout; ops.GCNLayerFn) where the table exceeds the
@@ -365,13 +400,16 @@ def main():
               and ops.use_sliced(shard.n_cols, Dl, torch.float32))
     hs = ops.slice_pack(h_local) if sliced else None
 
+    n_slices = len(shard.slices(Dl)) if shard.g > 1 and part.kind == "rows" else 0
+
     def step(ev=None):
-        shard.aggregate(h_local, h_full, y, _lib.GNNEA_ACT_RELU, ev, hs=hs)
+        shard.aggregate(h_local, y, _lib.GNNEA_ACT_RELU, ev, hs=hs)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2 + 2 * n_slices)]
+           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -384,9 +422,9 @@ def main():
     elapsed = time.perf_counter() - t_start
     if shard.g == 1 or free:
         kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    else:  # own-block + remote-block SpMM launches (the wait for the halo excluded)
-        kernel_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[2].elapsed_time(e[3])
-                                   for e in evs]))
+    else:  # the per-slice aggregations (each after its slice's exchange has landed)
+        kernel_ms = float(np.mean([sum(e[2 + 2 * q].elapsed_time(e[3 + 2 * q])
+                                       for q in range(n_slices)) for e in evs]))
     # units = edge aggregations over the full feature width: a rank that aggregates its KG's
     # edges over Dl of the D columns contributes nnz * Dl / D of them (the slices of a KG group
     # add up to each edge exactly once); row shards contribute their own rows' edges
@@ -403,6 +441,9 @@ def main():
         total_nnz = units
     ms_per_step = elapsed / args.steps * 1e3
     value = total_nnz / (elapsed / args.steps)
+    # per-step HIP events on the launching stream (median; rank 0): the SURVEY §8d statistic,
+    # reported beside the contract's wall-clock mean over the K steps
+    step_ms = [e[0].elapsed_time(e[1]) for e in evs]
 
     # the exchange alone (rows partition inside a group): bytes each rank receives per step and
     # the time of K back-to-back exchanges, max over ranks
@@ -411,10 +452,13 @@ def main():
         from gnnea import exchange as ex
         ranks = part.group_ranks(part.kg)
 
-        def xchg():
-            for w in ex.all_gather(h_local, h_full, shard.group, ranks, part.li,
-                                   other=part.other_ranks()):
-                w.wait()
+        tables = shard.halo_tables(Dl)
+
+        def xchg():  # the same per-slice exchanges as the step, without the aggregation
+            for ws in ex.all_gather_slices(list(tables), part.row0, part.n_rows, shard.group,
+                                           ranks, part.li, other=part.other_ranks()):
+                for w in ws:
+                    w.wait()
         for _ in range(2):
             xchg()
         torch.cuda.synchronize()
@@ -435,13 +479,20 @@ def main():
                     "peers": shard.g - 1, "bytes_recv_per_rank_per_step": x_bytes,
                     "ms_alone": round(x_ms, 4),
                     "GBps_recv_per_rank": round(x_bytes / (x_ms * 1e-3) / 1e9, 1),
-                    "spmm_kernel_ms": round(kernel_ms, 4)}
+                    "spmm_kernel_ms": round(kernel_ms, 4),
+                    # SURVEY §8e overlap: the exchange and the aggregation cut into column
+                    # slices, slice q aggregated while slices > q move; the hidden fraction of
+                    # the exchange = (exchange alone + aggregation - step) / exchange alone
+                    "pipeline": "%d column slices (64 fp32 columns; slice-major KG tables)"
+                                % n_slices,
+                    "step_ms": round(ms_per_step, 4),
+                    "exchange_hidden_frac": round(min(1.0, max(0.0, (x_ms + kernel_ms
+                                                                     - ms_per_step) / x_ms)), 3)}
 
     # labelled side number: the exchange-free tiles partition (aggregation only; a layer would
     # first all-gather its input, which this number does not contain)
     side = None
     if world > 2 and part.kind == "rows" and not args.no_side and not args.rehearse:
-        del h_full
         sh2 = KGShard(n, shard_t(n), synth.CONFIGS["cfg4"]["n_rel"], rank, world, device,
                       kind="tiles", D=D)
         p2 = sh2.part
@@ -450,12 +501,12 @@ def main():
         y2 = torch.empty(sh2.n_rows, D2, device=device)
         hs2 = ops.slice_pack(h2) if ops.use_sliced(sh2.n_cols, D2, torch.float32) else None
         for _ in range(2):
-            sh2.aggregate(h2, None, y2, _lib.GNNEA_ACT_RELU, hs=hs2)
+            sh2.aggregate(h2, y2, _lib.GNNEA_ACT_RELU, hs=hs2)
         torch.cuda.synchronize()
         dist.barrier()
         t1 = time.perf_counter()
         for _ in range(args.steps):
-            sh2.aggregate(h2, None, y2, _lib.GNNEA_ACT_RELU, hs=hs2)
+            sh2.aggregate(h2, y2, _lib.GNNEA_ACT_RELU, hs=hs2)
         torch.cuda.synchronize()
         st = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=device)
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
@@ -468,19 +519,22 @@ def main():
 
     # side measurement (every rank, same collective sequence): the row-sharded HGCN-EA training
     # step of BASELINE.json configs[3] through the drop-in modules with the RCCL halo exchange
+    # these legs run collectives at N > 1: an exception there propagates (the run exits non-zero)
+    # instead of being recorded on one rank while the others wait in the next collective
     train = None
     if not args.no_train and not args.rehearse:
-        try:
-            from tools.dist_step import measure
+        from tools.dist_step import measure
+        if world == 1:
+            try:
+                train = measure("HGCN", n, rank, world, device, args.train_steps, 3)
+            except Exception as e:  # report, never hide
+                train = {"error": repr(e)}
+        else:
             train = measure("HGCN", n, rank, world, device, args.train_steps, 3)
-        except Exception as e:  # report, never hide
-            train = {"error": repr(e)}
     sk_shard = None
     if world > 1 and not args.no_sinkhorn:
-        try:  # (--rehearse: the code path only; the rate means nothing there)
-            sk_shard = sinkhorn_sharded(device, rank, world)
-        except Exception as e:  # report, never hide
-            sk_shard = {"error": repr(e)}
+        # (--rehearse: the code path only; the rate means nothing there)
+        sk_shard = sinkhorn_sharded(device, rank, world)
 
     if rank == 0:
         # the SpMM is launched once per diagonal (KG) block of rows when the gathered matrix is
@@ -489,6 +543,9 @@ def main():
         if shard.g == 1 or free:
             blocks = ops._blocks(shard.csr, h_local)
             launches = len(blocks)
+        else:  # one sliced launch per column slice over the KG halo tables
+            launches = n_slices
+            sliced = True
         traffic = gather_model_bytes(shard.n_rows, shard.nnz, Dl)
         achieved = traffic / (kernel_ms * 1e-3) / 1e9
         comp = compulsory_bytes(shard.n_rows, shard.n_cols, shard.nnz, Dl, sliced)
@@ -500,6 +557,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic",
+            "ms_per_step_events_median": round(float(np.median(step_ms)), 4),
+            "edges_per_s_events_median": round(total_nnz / (float(np.median(step_ms)) * 1e-3), 1),
             "config": {"workload": "GCN aggregation relu(A.H) (layers/layers.py:35-38) on the "
                                    "cfg-4 synthetic 2x%d-entity / 2x%d-triple KG pair, D=%d"
                                    % (n, shard_t(n), D),
@@ -508,8 +567,9 @@ def main():
                        ("2 KG groups of %d GPUs, %d row blocks x %d feature-column slices "
                         "(aggregation only, no exchange)" % (shard.g, part.gr, part.gc) if free
                         else ("2 KG groups (one KG per GPU, nothing to exchange)" if shard.g == 1
-                              else "2 KG groups of %d GPUs, row blocks + halo exchange by direct "
-                                   "peer transfers, inside the timed step" % shard.g))},
+                              else "2 KG groups of %d GPUs, row blocks + per-column-slice halo "
+                                   "exchange (relayed peer transfers) pipelined with the "
+                                   "per-slice aggregation, inside the timed step" % shard.g))},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_bytes, "traffic_source": pmc_src,
@@ -569,7 +629,13 @@ def main():
                 line["gw_cost"] = {"error": repr(e)}
         if world == 1 and not args.headline_only:
             try:
-                line["bf16"] = bf16_rate(shard, h_local, args.steps)
+                line["hbm_copy"] = copy_rate(device)
+            except Exception as e:  # report, never hide
+                line["hbm_copy"] = {"error": repr(e)}
+            try:
+                del hs
+                torch.cuda.empty_cache()
+                line["bf16"] = bf16_rate(device, args.steps)
             except Exception as e:  # report, never hide
                 line["bf16"] = {"error": repr(e)}
         if world == 1 and not args.no_cpu_baseline:

@@ -161,9 +161,11 @@ template <> struct Vec4<float> {
   typedef float4 raw;
   static __device__ __forceinline__ float4 get(const raw& r) { return r; }
   static __device__ __forceinline__ raw put(float4 v) { return v; }
+  static __device__ __forceinline__ raw zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 };
 template <> struct Vec4<bf16_t> {
   typedef uint2 raw;
+  static __device__ __forceinline__ raw zero() { return make_uint2(0u, 0u); }
   static __device__ __forceinline__ float4 get(const raw& r) {
     return make_float4(__builtin_bit_cast(float, r.x << 16),
                        __builtin_bit_cast(float, r.x & 0xffff0000u),
@@ -177,6 +179,22 @@ template <> struct Vec4<bf16_t> {
     return r;
   }
 };
+// 16 bytes of a feature row: 4 fp32 or 8 bf16 values
+__device__ __forceinline__ void unpack16(const uint4& u, float (&f)[4]) {
+  f[0] = __builtin_bit_cast(float, u.x);
+  f[1] = __builtin_bit_cast(float, u.y);
+  f[2] = __builtin_bit_cast(float, u.z);
+  f[3] = __builtin_bit_cast(float, u.w);
+}
+__device__ __forceinline__ void unpack16(const uint4& u, float (&f)[8]) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[2 * k] = __builtin_bit_cast(float, w[k] << 16);
+    f[2 * k + 1] = __builtin_bit_cast(float, w[k] & 0xffff0000u);
+  }
+}
+
 template <typename T> __device__ __forceinline__ float to_f32(T v);
 template <> __device__ __forceinline__ float to_f32<float>(float v) { return v; }
 template <> __device__ __forceinline__ float to_f32<bf16_t>(bf16_t v) { return bf16_to_f32(v); }

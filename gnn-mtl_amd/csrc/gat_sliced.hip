@@ -85,28 +85,66 @@ static bool gat_two_heads_per_slice(int heads, int d_head) {
   return true;
 }
 
-template <int ACT, int U, typename TY>
+// Lane map of the gather passes over a 64-column slice: every lane loads 16 B of the row piece
+// (E = 4 fp32 / 8 bf16 columns), LPG = 64 / E lanes per piece (fp32 16: 256 B; bf16 8: one
+// 128-B line), NG = 64 / LPG groups per wave each on its own neighbour (fp32 4, bf16 8).  One
+// 16-B load per lane per neighbour for both storage types: 8-B bf16 loads would halve the bytes
+// per load instruction (cfg-5 measured 6.4 ms fwd / 8.7 ms src per KG at 8 B against 3.6 / 4.1
+// for fp32 at cfg-4 on the same gathered bytes).
+template <typename T>
+struct GatLanes {
+  static constexpr int E = 16 / (int)sizeof(T);
+  static constexpr int LPG = 64 / E;
+  static constexpr int NG = 64 / LPG;
+};
+
+// E consecutive columns from c0 of a row-major row (4-column chunks; columns >= D read as 0)
+template <typename T, int E>
+__device__ __forceinline__ void load_cols(const T* row, int c0, int D, float (&v)[E]) {
+  typedef typename Vec4<T>::raw R;
+#pragma unroll
+  for (int k = 0; k < E / 4; ++k) {
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c0 + 4 * k < D) f = Vec4<T>::get(*(const R*)(row + c0 + 4 * k));
+    v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
+  }
+}
+template <typename T, int E>
+__device__ __forceinline__ void store_cols(T* row, int c0, int D, const float (&v)[E]) {
+  typedef typename Vec4<T>::raw R;
+#pragma unroll
+  for (int k = 0; k < E / 4; ++k)
+    if (c0 + 4 * k < D)
+      *(R*)(row + c0 + 4 * k) =
+          Vec4<T>::put(make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]));
+}
+
+template <int ACT, int U, typename TX, typename TY>
 __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, int n_rows, int nbs,
     int H, int D, int dh, const uint4* __restrict__ Hs, int64_t sstride16,
     const float* __restrict__ wgt, const float* __restrict__ den_in, TY* __restrict__ Y,
     int64_t ldy) {
+  constexpr int E = GatLanes<TX>::E, LPG = GatLanes<TX>::LPG, NG = GatLanes<TX>::NG;
   const int b = blockIdx.x;
   const int s = b / nbs;
   const int row = xcd_remap(b - s * nbs, nbs) * 4 + wave_id();
   if (row >= n_rows) return;
-  const int lane = lane_id(), g = lane >> 4, c = lane & 15;
-  const int c0 = s * 64 + 4 * c;
+  const int lane = lane_id(), g = lane / LPG, c = lane % LPG;
+  const int c0 = s * 64 + E * c;
   const bool own = c0 < D;
-  // the slice's heads (d_head >= 32: at most two per 64 columns) and this lane's columns' heads
+  // the slice's heads (at most two per 64 columns, gat_two_heads_per_slice) and this lane's
+  // columns' heads
   const int h0 = min((s * 64) / dh, H - 1);
   const int h1 = min((s * 64 + 63) / dh, H - 1);
-  bool second[4];
+  bool second[E];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) second[t] = (c0 + t) / dh != h0;
+  for (int t = 0; t < E; ++t) second[t] = (c0 + t) / dh != h0;
   const uint4* X = Hs + (int64_t)s * sstride16 + c;
   const int beg = rowptr[row], end = rowptr[row + 1];
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float acc[E];
+#pragma unroll
+  for (int t = 0; t < E; ++t) acc[t] = 0.f;
   for (int base = beg; base < end; base += 64) {
     const int cnt = min(64, end - base);
     int mj = 0;
@@ -116,17 +154,17 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
       w0 = wgt[(int64_t)(base + lane) * H + h0];
       w1 = wgt[(int64_t)(base + lane) * H + h1];
     }
-    for (int k = 0; k < cnt; k += 4 * U) {
+    for (int k = 0; k < cnt; k += NG * U) {
       uint4 r[U];
       float v0[U], v1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = k + 4 * u + g;  // <= 63: k is a multiple of 4U that divides 64
+        const int e = k + NG * u + g;  // <= 63: k is a multiple of NG*U that divides 64
         const int j = __shfl(mj, e & 63, 64);
         v0[u] = __shfl(w0, e & 63, 64);
         v1[u] = __shfl(w1, e & 63, 64);
         if (e < cnt && own) {
-          r[u] = X[(int64_t)j * 16];
+          r[u] = X[(int64_t)j * LPG];
         } else {
           r[u] = make_uint4(0u, 0u, 0u, 0u);
           v0[u] = v1[u] = 0.f;
@@ -134,25 +172,40 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const float f[4] = {__builtin_bit_cast(float, r[u].x), __builtin_bit_cast(float, r[u].y),
-                            __builtin_bit_cast(float, r[u].z), __builtin_bit_cast(float, r[u].w)};
+        float f[E];
+        unpack16(r[u], f);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = fmaf(second[t] ? v1[u] : v0[u], f[t], acc[t]);
+        for (int t = 0; t < E; ++t) acc[t] = fmaf(second[t] ? v1[u] : v0[u], f[t], acc[t]);
       }
     }
   }
+  // the group partials in fixed order (xor LPG, 2 LPG, ...)
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] += __shfl_xor(acc[t], 16, 64);
+  for (int o = LPG; o < 64; o <<= 1) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] += __shfl_xor(acc[t], 32, 64);
+    for (int t = 0; t < E; ++t) acc[t] += __shfl_xor(acc[t], o, 64);
+  }
   if (g != 0 || !own) return;
   const float d0 = den_in[(int64_t)row * H + h0], d1 = den_in[(int64_t)row * H + h1];
   const float r0 = d0 > 0.f ? 1.f / d0 : 0.f, r1 = d1 > 0.f ? 1.f / d1 : 0.f;
-  float o[4];
+  float o[E];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) o[t] = c0 + t < D ? act_fwd<ACT>(acc[t] * (second[t] ? r1 : r0)) : 0.f;
-  typedef typename Vec4<TY>::raw RY;
-  *(RY*)(Y + (int64_t)row * ldy + c0) = Vec4<TY>::put(make_float4(o[0], o[1], o[2], o[3]));
+  for (int t = 0; t < E; ++t) o[t] = act_fwd<ACT>(acc[t] * (second[t] ? r1 : r0));
+  store_cols<TY, E>(Y + (int64_t)row * ldy, c0, D, o);
+}
+
+// Row-major [n, D] -> 64-column slice-major table [ceil(D/64)][n][64] (the GAT layout for both
+// storage types: 256 B per fp32 slice row, 128 B = one line per bf16 slice row, so one bf16 KG
+// slice of a 2M-row cfg-5 KG is 256 MB), one wave per row.
+template <typename T>
+__global__ __launch_bounds__(256) void k_pack64(const typename Vec4<T>::raw* __restrict__ X,
+                                                int64_t ld4, int64_t n, int D4,
+                                                typename Vec4<T>::raw* __restrict__ Xs,
+                                                int64_t sstride4) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave_id();
+  if (r >= n) return;
+  for (int q = lane_id(); q < D4; q += 64)
+    Xs[(int64_t)(q >> 4) * sstride4 + r * 16 + (q & 15)] = X[r * ld4 + q];
 }
 
 // ---------------------------------------------------------------------------------------- //
@@ -176,17 +229,20 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
 //                     the dz gathers),
 //                     ds1_i through the transpose position map, dH_i += ds1_i (x) a1
 //                     (+ ds2_i (x) a2 when the edge pass left it, square unsharded case).
-// fp32 throughout; sums in a different order from gat.hip's single pass (fp32 rounding level).
+// fp32 arithmetic; G, H and dH in the storage type T (fp32, or bf16 for cfg-5: 64-column slices of
+// 128 B, every stored value rounded once per pass); sums in a different order from gat.hip's
+// single pass (fp32 rounding level).
 // ---------------------------------------------------------------------------------------- //
 
-template <int ACT, int H, int NCH>
+template <int ACT, int H, int NCH, typename T>
 __global__ __launch_bounds__(256) void k_gat_bwd_prep_s(int n_rows, int D, int dh,
-                                                        const float4* __restrict__ dY,
-                                                        const float4* __restrict__ Y, int64_t ld4,
-                                                        const float* __restrict__ s1,
+                                                        const typename Vec4<T>::raw* __restrict__ dY,
+                                                        const typename Vec4<T>::raw* __restrict__ Y,
+                                                        int64_t ld4, const float* __restrict__ s1,
                                                         const float* __restrict__ mrow,
                                                         const float* __restrict__ den,
-                                                        float4* __restrict__ Gs, int64_t sstride4,
+                                                        typename Vec4<T>::raw* __restrict__ Gs,
+                                                        int64_t sstride4,
                                                         float4* __restrict__ rec) {
   const int row = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
   if (row >= n_rows) return;
@@ -198,21 +254,28 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_s(int n_rows, int D, int d
   for (int q = 0; q < NCH; ++q) {
     const int c4 = lane + 64 * q;
     if (4 * c4 >= D) continue;
-    const float4 dy = dY[(int64_t)row * ld4 + c4];
-    const float4 y = Y[(int64_t)row * ld4 + c4];
+    const float4 dy = Vec4<T>::get(dY[(int64_t)row * ld4 + c4]);
+    const float4 y = Vec4<T>::get(Y[(int64_t)row * ld4 + c4]);
     const float ys[4] = {y.x, y.y, y.z, y.w};
     float gs[4] = {dy.x, dy.y, dy.z, dy.w};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int c = 4 * c4 + t;
       gs[t] = c < D ? gs[t] * act_grad_from_out<ACT>(ys[t]) : 0.f;
+    }
+    // the record's G.h' uses the G the source pass gathers (rounded to T once)
+    const typename Vec4<T>::raw gr = Vec4<T>::put(make_float4(gs[0], gs[1], gs[2], gs[3]));
+    const float4 gq = Vec4<T>::get(gr);
+    const float gv[4] = {gq.x, gq.y, gq.z, gq.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int c = 4 * c4 + t;
       const int hh = c < D ? c / dh : H;
 #pragma unroll
-      for (int h = 0; h < H; ++h) cp[h] += (hh == h) ? gs[t] * ys[t] : 0.f;
+      for (int h = 0; h < H; ++h) cp[h] += (hh == h) ? gv[t] * ys[t] : 0.f;
     }
     // column 4*c4 -> slice c4 / 16, offset 4 * (c4 % 16)
-    Gs[(int64_t)(c4 >> 4) * sstride4 + (int64_t)row * 16 + (c4 & 15)] =
-        make_float4(gs[0], gs[1], gs[2], gs[3]);
+    Gs[(int64_t)(c4 >> 4) * sstride4 + (int64_t)row * 16 + (c4 & 15)] = gr;
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) cp[h] = wave_sum(cp[h]);
@@ -250,30 +313,30 @@ __global__ __launch_bounds__(256) void k_gat_bwd_w(const int32_t* __restrict__ r
   }
 }
 
-template <int U>
+template <int U, typename T>
 __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
     const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT, int n_rows, int nbs,
     int H, int D, int dh, const uint4* __restrict__ Gs, int64_t sstride16,
-    const float* __restrict__ Hm, int64_t ldh, const float* __restrict__ wT,
-    float* __restrict__ dH, int64_t lddh, float* __restrict__ pd, int64_t pstride) {
+    const T* __restrict__ Hm, int64_t ldh, const float* __restrict__ wT,
+    T* __restrict__ dH, int64_t lddh, float* __restrict__ pd, int64_t pstride) {
+  constexpr int E = GatLanes<T>::E, LPG = GatLanes<T>::LPG, NG = GatLanes<T>::NG;
   const int b = blockIdx.x;
   const int s = b / nbs;
   const int row = xcd_remap(b - s * nbs, nbs) * 4 + wave_id();
   if (row >= n_rows) return;
-  const int lane = lane_id(), g = lane >> 4, c = lane & 15;
-  const int c0 = s * 64 + 4 * c;
+  const int lane = lane_id(), g = lane / LPG, c = lane % LPG;
+  const int c0 = s * 64 + E * c;
   const bool own = c0 < D;
   const int h0 = min((s * 64) / dh, H - 1);
   const int h1 = min((s * 64 + 63) / dh, H - 1);
   const bool two = h1 != h0;  // uniform per slice
-  bool second[4];
-  float hj0[4], hj1[4];
+  bool second[E];
+  float hj0[E], hj1[E];  // H_j split by head; zero past D (the table's padding is never read)
   {
-    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (own) hv = *(const float4*)(Hm + (int64_t)row * ldh + c0);
-    const float v[4] = {hv.x, hv.y, hv.z, hv.w};
+    float v[E];
+    load_cols<T, E>(Hm + (int64_t)row * ldh, c0, D, v);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < E; ++t) {
       second[t] = (c0 + t) / dh != h0;
       hj0[t] = second[t] ? 0.f : v[t];
       hj1[t] = second[t] ? v[t] : 0.f;
@@ -282,7 +345,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
   const uint4* X = Gs + (int64_t)s * sstride16 + c;
   float* pds = pd + (int64_t)s * pstride;
   const int beg = rowptrT[row], end = rowptrT[row + 1];
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float acc[E];
+#pragma unroll
+  for (int t = 0; t < E; ++t) acc[t] = 0.f;
   for (int base = beg; base < end; base += 64) {
     const int cnt = min(64, end - base);
     int mj = 0;
@@ -292,17 +357,17 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
       w0 = wT[(int64_t)(base + lane) * H + h0];
       w1 = wT[(int64_t)(base + lane) * H + h1];
     }
-    for (int k = 0; k < cnt; k += 4 * U) {
+    for (int k = 0; k < cnt; k += NG * U) {
       uint4 r[U];
       float v0[U], v1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = k + 4 * u + g;
+        const int e = k + NG * u + g;
         const int j = __shfl(mj, e & 63, 64);
         v0[u] = __shfl(w0, e & 63, 64);
         v1[u] = __shfl(w1, e & 63, 64);
         if (e < cnt && own) {
-          r[u] = X[(int64_t)j * 16];
+          r[u] = X[(int64_t)j * LPG];
         } else {
           r[u] = make_uint4(0u, 0u, 0u, 0u);
           v0[u] = v1[u] = 0.f;
@@ -311,11 +376,12 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
       float q[2 * U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const float f[4] = {__builtin_bit_cast(float, r[u].x), __builtin_bit_cast(float, r[u].y),
-                            __builtin_bit_cast(float, r[u].z), __builtin_bit_cast(float, r[u].w)};
+        float f[E];
+        unpack16(r[u], f);
         float qa = 0.f, qb = 0.f;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < E; ++t) {
+          f[t] = c0 + t < D ? f[t] : 0.f;  // G's padding columns are never written
           acc[t] = fmaf(second[t] ? v1[u] : v0[u], f[t], acc[t]);
           qa = fmaf(f[t], hj0[t], qa);
           qb = fmaf(f[t], hj1[t], qb);
@@ -323,39 +389,40 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
         q[u] = qa;
         q[U + u] = qb;
       }
-      // per-group sums of the 16 lanes: value v (edge u = v % U, head slot v / U) lands on lane
-      // grp_lane(v) of the group; that lane stores it
+      // per-group sums of the LPG lanes: value v (edge u = v % U, head slot v / U) lands on
+      // lane grp_lane(v) of the group; that lane stores it
       if (two) {
-        const float sum = grp_sum<2 * U, 16>(q, lane);
-        constexpr int SP = 16 / (2 * U);
-        const int v = c / SP, e = k + 4 * (v % U) + g;
+        const float sum = grp_sum<2 * U, LPG>(q, lane);
+        constexpr int SP = (LPG >= 16 ? 16 : 8) / (2 * U);
+        const int v = c / SP, e = k + NG * (v % U) + g;
         if (c % SP == 0 && e < cnt) pds[(int64_t)(base + e) * 2 + v / U] = sum;
       } else {
         float qq[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) qq[u] = q[u];
-        const float sum = grp_sum<U, 16>(qq, lane);
-        constexpr int SP = 16 / U;
-        const int e = k + 4 * (c / SP) + g;
+        const float sum = grp_sum<U, LPG>(qq, lane);
+        constexpr int SP = (LPG >= 16 ? 16 : 8) / U;
+        const int e = k + NG * (c / SP) + g;
         if (c % SP == 0 && e < cnt) pds[(int64_t)(base + e) * 2] = sum;
       }
     }
   }
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] += __shfl_xor(acc[t], 16, 64);
+  for (int o = LPG; o < 64; o <<= 1) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] += __shfl_xor(acc[t], 32, 64);
+    for (int t = 0; t < E; ++t) acc[t] += __shfl_xor(acc[t], o, 64);
+  }
   if (g != 0 || !own) return;
-  *(float4*)(dH + (int64_t)row * lddh + c0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  store_cols<T, E>(dH + (int64_t)row * lddh, c0, D, acc);
 }
 
-template <int H, int LPR>  // LPR lanes per source row
+template <int H, int LPR, typename T>  // LPR lanes per source row
 __global__ __launch_bounds__(256) void k_gat_bwd_edge(
     const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT,
     const int64_t* __restrict__ permT, int n_rows, int S, int D, int dh,
     const float* __restrict__ s2, float alpha, const float* __restrict__ emask,
     const float4* __restrict__ rec, const float2* __restrict__ pd, int64_t pstride2,
-    const float* __restrict__ a, float* __restrict__ dH, int64_t lddh, float* __restrict__ dzT,
+    const float* __restrict__ a, T* __restrict__ dH, int64_t lddh, float* __restrict__ dzT,
     float* __restrict__ ds2) {
   const int row = xcd_remap(blockIdx.x, gridDim.x) * (256 / LPR) + threadIdx.x / LPR;
   if (row >= n_rows) return;  // whole LPR-lane groups leave together
@@ -400,28 +467,29 @@ __global__ __launch_bounds__(256) void k_gat_bwd_edge(
   }
   if (l < H) ds2[(int64_t)row * H + l] = hsel<H>(d2, l);
   if (!dH) return;
-  float* out = dH + (int64_t)row * lddh;
+  typedef typename Vec4<T>::raw RX;
+  T* out = dH + (int64_t)row * lddh;
   for (int c4 = l; 4 * c4 < D; c4 += LPR) {
-    float4 v = *(float4*)(out + 4 * c4);
+    const float4 v = Vec4<T>::get(*(RX*)(out + 4 * c4));
     float o[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int cc = 4 * c4 + t, h = cc / dh;
       o[t] += hsel<H>(d2, h) * a[h * 2 * dh + dh + (cc - h * dh)];
     }
-    *(float4*)(out + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
+    *(RX*)(out + 4 * c4) = Vec4<T>::put(make_float4(o[0], o[1], o[2], o[3]));
   }
 }
 
-template <int H, int NCH, int L>  // L lanes per destination row (NCH: float4 slots at 64 lanes)
+template <int H, int NCH, int L, typename T>  // L lanes per destination row (NCH: 4-element slots at 64 lanes)
 __global__ __launch_bounds__(256) void k_gat_bwd_dst_s(const int32_t* __restrict__ rowptr,
                                                        const int64_t* __restrict__ tpos,
                                                        int n_rows, int D, int dh,
                                                        const float* __restrict__ dzT,
                                                        const float* __restrict__ a,
                                                        const float* __restrict__ ds2,
-                                                       float4* __restrict__ dH, int64_t lddh4,
-                                                       float* __restrict__ ds1) {
+                                                       typename Vec4<T>::raw* __restrict__ dH,
+                                                       int64_t lddh4, float* __restrict__ ds1) {
   constexpr int NC = NCH * 64 / L;
   const int row = xcd_remap(blockIdx.x, gridDim.x) * (256 / L) + threadIdx.x / L;
   if (row >= n_rows) return;  // whole L-lane groups leave together
@@ -431,7 +499,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_s(const int32_t* __restrict
 #pragma unroll
   for (int k = 0; k < NC; ++k) {  // independent of dz: issued before the gather chain
     const int c4 = l + L * k;
-    v[k] = 4 * c4 < D ? dH[(int64_t)row * lddh4 + c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[k] = 4 * c4 < D ? Vec4<T>::get(dH[(int64_t)row * lddh4 + c4]) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float p[H], q[H];
 #pragma unroll
@@ -458,25 +526,32 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_s(const int32_t* __restrict
       o[t] += hsel<H>(p, h) * a[h * 2 * dh + d];
       if (ds2) o[t] += hsel<H>(q, h) * a[h * 2 * dh + dh + d];
     }
-    dH[(int64_t)row * lddh4 + c4] = make_float4(o[0], o[1], o[2], o[3]);
+    dH[(int64_t)row * lddh4 + c4] = Vec4<T>::put(make_float4(o[0], o[1], o[2], o[3]));
   }
   if (l < H) ds1[(int64_t)row * H + l] = hsel<H>(p, l);
 }
 
 }  // namespace gnnea
 
+
 using namespace gnnea;
 
-// the sliced forward: rowstats (m_out, den_out, per-edge weights in wgt: nnz x heads fp32,
-// indexed by the absolute CSR position) + the aggregation; Hs slice-major fp32
-// [ceil(D/64)][n_src][64] (sstride floats per slice), D % 4 == 0, d_head >= 32, ldy % 4 == 0
-extern "C" int gnnea_gat_fwd_sliced_f32(const int32_t* rowptr, const int32_t* col,
-                                        int32_t n_rows, const float* Hs, int64_t sstride,
-                                        int heads, int d_head, const float* s1, const float* s2,
-                                        float alpha, const float* edge_mask, int act, float* Y,
-                                        int64_t ldy, float* m_out, float* den_out, float* wgt,
-                                        void* stream) {
-  hipStream_t st = (hipStream_t)stream;
+namespace {
+
+template <typename T>
+bool alv(const void* p) {  // aligned for one Vec4<T> (nullptr passes)
+  return (((uintptr_t)p) & (sizeof(typename Vec4<T>::raw) - 1)) == 0;
+}
+
+// neighbours in flight per lane group: 4 x 16 B per lane (fp32: 4 groups x 16 lanes; bf16: 8 x 8)
+template <typename T>
+constexpr int kGatU = 4;
+
+template <typename T>
+int gat_fwd_sliced(const int32_t* rowptr, const int32_t* col, int32_t n_rows, const T* Hs,
+                   int64_t sstride, int heads, int d_head, const float* s1, const float* s2,
+                   float alpha, const float* edge_mask, int act, T* Y, int64_t ldy, float* m_out,
+                   float* den_out, float* wgt, hipStream_t st) {
   const int D = heads * d_head;
   if (n_rows < 0 || heads < 1 || heads > 8 || !gat_two_heads_per_slice(heads, d_head) ||
       D % 4 || sstride % 64 || ldy % 4 || ldy < D)
@@ -485,7 +560,7 @@ extern "C" int gnnea_gat_fwd_sliced_f32(const int32_t* rowptr, const int32_t* co
   if (n_rows == 0) return 0;
   if (!rowptr || !col || !Hs || !s1 || !s2 || !Y || !m_out || !den_out || !wgt)
     return GNNEA_EINVAL;
-  if (((uintptr_t)Hs & 15) || ((uintptr_t)Y & 15)) return GNNEA_EALIGN;
+  if (((uintptr_t)Hs & 15) || !alv<T>(Y)) return GNNEA_EALIGN;
   const int nbs = div_up(n_rows, 4);
   switch (heads) {
 #define GNNEA_RS(HH)                                                                             \
@@ -500,16 +575,71 @@ extern "C" int gnnea_gat_fwd_sliced_f32(const int32_t* rowptr, const int32_t* co
   GNNEA_LAUNCH_CHECK();
   const int S = div_up(D, 64);
   const dim3 grid((unsigned)((int64_t)S * nbs));
+  const int64_t ss16 = sstride * (int64_t)sizeof(T) / 16;
   if (act == GNNEA_ACT_RELU)
-    hipLaunchKernelGGL((k_gat_fwd_sliced<GNNEA_ACT_RELU, 4, float>), grid, dim3(256), 0, st,
-                       rowptr, col, n_rows, nbs, heads, D, d_head, (const uint4*)Hs, sstride / 4,
+    hipLaunchKernelGGL((k_gat_fwd_sliced<GNNEA_ACT_RELU, kGatU<T>, T, T>), grid, dim3(256), 0, st,
+                       rowptr, col, n_rows, nbs, heads, D, d_head, (const uint4*)Hs, ss16,
                        wgt, den_out, Y, ldy);
   else
-    hipLaunchKernelGGL((k_gat_fwd_sliced<GNNEA_ACT_IDENTITY, 4, float>), grid, dim3(256), 0, st,
-                       rowptr, col, n_rows, nbs, heads, D, d_head, (const uint4*)Hs, sstride / 4,
+    hipLaunchKernelGGL((k_gat_fwd_sliced<GNNEA_ACT_IDENTITY, kGatU<T>, T, T>), grid, dim3(256), 0,
+                       st, rowptr, col, n_rows, nbs, heads, D, d_head, (const uint4*)Hs, ss16,
                        wgt, den_out, Y, ldy);
   GNNEA_LAUNCH_CHECK();
   return 0;
+}
+
+template <typename T>
+int pack64(const T* X, int64_t ldx, int64_t n, int32_t D, T* Xs, int64_t sstride,
+           hipStream_t st) {
+  if (n < 0 || D < 0) return GNNEA_EINVAL;
+  if (n == 0 || D == 0) return 0;
+  if (!X || !Xs || D % 4 || ldx % 4 || ldx < D || sstride % 64 || sstride < n * 64)
+    return GNNEA_EINVAL;
+  if (!alv<T>(X) || !alv<T>(Xs)) return GNNEA_EALIGN;
+  if ((n + 3) / 4 >= (1ll << 31)) return GNNEA_EINVAL;
+  typedef typename Vec4<T>::raw R;
+  hipLaunchKernelGGL((k_pack64<T>), dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st,
+                     (const R*)X, ldx / 4, n, D / 4, (R*)Xs, sstride / 4);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+
+// the sliced forward: rowstats (m_out, den_out, per-edge weights in wgt: nnz x heads fp32,
+// indexed by the absolute CSR position) + the aggregation; Hs slice-major 64-column table
+// [ceil(D/64)][n_src][64] (sstride elements per slice), D % 4 == 0, every slice at most two heads
+// (gat_two_heads_per_slice), ldy % 4 == 0
+extern "C" int gnnea_gat_fwd_sliced_f32(const int32_t* rowptr, const int32_t* col,
+                                        int32_t n_rows, const float* Hs, int64_t sstride,
+                                        int heads, int d_head, const float* s1, const float* s2,
+                                        float alpha, const float* edge_mask, int act, float* Y,
+                                        int64_t ldy, float* m_out, float* den_out, float* wgt,
+                                        void* stream) {
+  return gat_fwd_sliced<float>(rowptr, col, n_rows, Hs, sstride, heads, d_head, s1, s2, alpha,
+                               edge_mask, act, Y, ldy, m_out, den_out, wgt, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_fwd_sliced_bf16(const int32_t* rowptr, const int32_t* col,
+                                         int32_t n_rows, const void* Hs, int64_t sstride,
+                                         int heads, int d_head, const float* s1, const float* s2,
+                                         float alpha, const float* edge_mask, int act, void* Y,
+                                         int64_t ldy, float* m_out, float* den_out, float* wgt,
+                                         void* stream) {
+  return gat_fwd_sliced<bf16_t>(rowptr, col, n_rows, (const bf16_t*)Hs, sstride, heads, d_head,
+                                s1, s2, alpha, edge_mask, act, (bf16_t*)Y, ldy, m_out, den_out,
+                                wgt, (hipStream_t)stream);
+}
+
+// row-major [n, D] -> the 64-column slice-major GAT table (sstride elements per slice)
+extern "C" int gnnea_slice_pack64_f32(const float* X, int64_t ldx, int64_t n, int32_t D,
+                                      float* Xs, int64_t sstride, void* stream) {
+  return pack64<float>(X, ldx, n, D, Xs, sstride, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_slice_pack64_bf16(const void* X, int64_t ldx, int64_t n, int32_t D,
+                                       void* Xs, int64_t sstride, void* stream) {
+  return pack64<bf16_t>((const bf16_t*)X, ldx, n, D, (bf16_t*)Xs, sstride, (hipStream_t)stream);
 }
 
 // ---- sliced backward entry points -------------------------------------------------------- //
@@ -544,26 +674,26 @@ static bool gat_sl_shape(int heads, int d_head, int64_t sstride) {
          D <= 1024 && sstride % 64 == 0;
 }
 
-// G (slice-major [ceil(D/64)][n_rows][64], sstride floats per slice) and the records
-extern "C" int gnnea_gat_bwd_prep_sliced_f32(int32_t n_rows, int heads, int d_head,
-                                             const float* dY, const float* Y, int64_t ldy,
-                                             const float* s1, const float* m, const float* den,
-                                             int act, float* Gs, int64_t sstride, float* rec,
-                                             void* stream) {
+namespace {
+
+template <typename T>
+int gat_bwd_prep_sliced(int32_t n_rows, int heads, int d_head, const T* dY, const T* Y,
+                        int64_t ldy, const float* s1, const float* m, const float* den, int act,
+                        T* Gs, int64_t sstride, float* rec, hipStream_t st) {
   const int D = heads * d_head;
   if (n_rows < 0 || !gat_sl_shape(heads, d_head, sstride) || ldy % 4 || ldy < D)
     return GNNEA_EINVAL;
   if (act != GNNEA_ACT_IDENTITY && act != GNNEA_ACT_RELU) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
   if (!dY || !Y || !s1 || !m || !den || !Gs || !rec) return GNNEA_EINVAL;
-  if (((uintptr_t)dY | (uintptr_t)Y | (uintptr_t)Gs) & 15) return GNNEA_EALIGN;
+  if (!alv<T>(dY) || !alv<T>(Y) || !alv<T>(Gs) || ((uintptr_t)rec & 15)) return GNNEA_EALIGN;
   const int nch = (D / 4 + 63) / 64;
   const dim3 grid(div_up(n_rows, 4));
-  hipStream_t st = (hipStream_t)stream;
+  typedef typename Vec4<T>::raw R;
 #define GNNEA_PREP(ACT, HH, NC)                                                              \
-  hipLaunchKernelGGL((k_gat_bwd_prep_s<ACT, HH, NC>), grid, dim3(256), 0, st, n_rows, D,     \
-                     d_head, (const float4*)dY, (const float4*)Y, ldy / 4, s1, m, den,       \
-                     (float4*)Gs, sstride / 4, (float4*)rec)
+  hipLaunchKernelGGL((k_gat_bwd_prep_s<ACT, HH, NC, T>), grid, dim3(256), 0, st, n_rows, D,  \
+                     d_head, (const R*)dY, (const R*)Y, ldy / 4, s1, m, den, (R*)Gs,         \
+                     sstride / 4, (float4*)rec)
 #define GNNEA_PREP_NC(ACT, HH)            \
   switch (nch) {                          \
     case 1: GNNEA_PREP(ACT, HH, 1); break; \
@@ -584,16 +714,12 @@ extern "C" int gnnea_gat_bwd_prep_sliced_f32(int32_t n_rows, int heads, int d_he
   return 0;
 }
 
-// source rows j of A^T (one KG block): per-edge weights wT, then the slice passes writing
-// dH_j = sum_i w_ij G_i (row-major, ldh) and the per-slice product partials pd [S][nnzT][2];
-// wT / pd are indexed by the absolute A^T position (rowptrT values), nnzT = A^T's entry count
-extern "C" int gnnea_gat_bwd_src_sliced_f32(const int32_t* rowptrT, const int32_t* colT,
-                                            const int64_t* permT, int32_t n_rows, int heads,
-                                            int d_head, const float* Hm, int64_t ldh,
-                                            const float* s2, float alpha, const float* emask,
-                                            const float* rec, const float* Gs, int64_t sstride,
-                                            float* wT, float* pd, int64_t nnzT, float* dH,
-                                            int64_t lddh, void* stream) {
+template <typename T>
+int gat_bwd_src_sliced(const int32_t* rowptrT, const int32_t* colT, const int64_t* permT,
+                       int32_t n_rows, int heads, int d_head, const T* Hm, int64_t ldh,
+                       const float* s2, float alpha, const float* emask, const float* rec,
+                       const T* Gs, int64_t sstride, float* wT, float* pd, int64_t nnzT, T* dH,
+                       int64_t lddh, hipStream_t st) {
   const int D = heads * d_head;
   if (n_rows < 0 || !gat_sl_shape(heads, d_head, sstride) || ldh % 4 || ldh < D ||
       lddh % 4 || lddh < D || nnzT < 0)
@@ -602,8 +728,7 @@ extern "C" int gnnea_gat_bwd_src_sliced_f32(const int32_t* rowptrT, const int32_
   if (!rowptrT || !colT || !Hm || !s2 || !rec || !Gs || !wT || !pd || !dH ||
       (emask && !permT))
     return GNNEA_EINVAL;
-  if (((uintptr_t)Hm | (uintptr_t)Gs | (uintptr_t)dH) & 15) return GNNEA_EALIGN;
-  hipStream_t st = (hipStream_t)stream;
+  if (!alv<T>(Hm) || ((uintptr_t)Gs & 15) || !alv<T>(dH)) return GNNEA_EALIGN;
 #define GNNEA_W1(HH, LP)                                                                        \
   hipLaunchKernelGGL((k_gat_bwd_w<HH, LP>), dim3(div_up(n_rows, 256 / LP)), dim3(256), 0, st,   \
                      rowptrT, colT, permT, n_rows, s2, alpha, emask, (const float4*)rec, wT)
@@ -619,21 +744,20 @@ extern "C" int gnnea_gat_bwd_src_sliced_f32(const int32_t* rowptrT, const int32_
 #undef GNNEA_W1
   GNNEA_LAUNCH_CHECK();
   const int S = div_up(D, 64), nbs = div_up(n_rows, 4);
-  hipLaunchKernelGGL((k_gat_bwd_src_sl<4>), dim3((unsigned)((int64_t)S * nbs)), dim3(256), 0, st,
-                     rowptrT, colT, n_rows, nbs, heads, D, d_head, (const uint4*)Gs,
-                     sstride / 4, Hm, ldh, wT, dH, lddh, pd, 2 * nnzT);
+  hipLaunchKernelGGL((k_gat_bwd_src_sl<kGatU<T>, T>), dim3((unsigned)((int64_t)S * nbs)),
+                     dim3(256), 0, st, rowptrT, colT, n_rows, nbs, heads, D, d_head,
+                     (const uint4*)Gs, sstride * (int64_t)sizeof(T) / 16, Hm, ldh, wT, dH, lddh,
+                     pd, 2 * nnzT);
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
 
-// dz (A^T order), ds2 and, when dH is non-NULL, dH_j += ds2_j (x) a2 for the source rows
-extern "C" int gnnea_gat_bwd_edge_sliced_f32(const int32_t* rowptrT, const int32_t* colT,
-                                             const int64_t* permT, int32_t n_rows, int heads,
-                                             int d_head, const float* s2, float alpha,
-                                             const float* emask, const float* rec,
-                                             const float* pd, int64_t nnzT, const float* a,
-                                             float* dH, int64_t lddh, float* dzT, float* ds2,
-                                             void* stream) {
+template <typename T>
+int gat_bwd_edge_sliced(const int32_t* rowptrT, const int32_t* colT, const int64_t* permT,
+                        int32_t n_rows, int heads, int d_head, const float* s2, float alpha,
+                        const float* emask, const float* rec, const float* pd, int64_t nnzT,
+                        const float* a, T* dH, int64_t lddh, float* dzT, float* ds2,
+                        hipStream_t st) {
   const int D = heads * d_head;
   if (n_rows < 0 || !gat_sl_shape(heads, d_head, 64) || nnzT < 0 ||
       (dH && (lddh % 4 || lddh < D)))
@@ -641,12 +765,11 @@ extern "C" int gnnea_gat_bwd_edge_sliced_f32(const int32_t* rowptrT, const int32
   if (n_rows == 0) return 0;
   if (!rowptrT || !colT || !s2 || !rec || !pd || !a || !dzT || !ds2 || (emask && !permT))
     return GNNEA_EINVAL;
-  if ((uintptr_t)dH & 15) return GNNEA_EALIGN;
-  hipStream_t st = (hipStream_t)stream;
+  if (!alv<T>(dH)) return GNNEA_EALIGN;
   const int S = div_up(D, 64);
 #define GNNEA_E1(HH, LP)                                                                        \
-  hipLaunchKernelGGL((k_gat_bwd_edge<HH, LP>), dim3(div_up(n_rows, 256 / LP)), dim3(256), 0, st, \
-                     rowptrT, colT, permT, n_rows, S, D, d_head, s2, alpha, emask,               \
+  hipLaunchKernelGGL((k_gat_bwd_edge<HH, LP, T>), dim3(div_up(n_rows, 256 / LP)), dim3(256), 0, \
+                     st, rowptrT, colT, permT, n_rows, S, D, d_head, s2, alpha, emask,          \
                      (const float4*)rec, (const float2*)pd, nnzT, a, dH, lddh, dzT, ds2)
 #define GNNEA_E(HH)                                              \
   case HH:                                                       \
@@ -662,26 +785,25 @@ extern "C" int gnnea_gat_bwd_edge_sliced_f32(const int32_t* rowptrT, const int32
   return 0;
 }
 
-// ds1 and dH_i += ds1_i (x) a1 (+ ds2_i (x) a2 when ds2 is non-NULL) for the destination rows
-extern "C" int gnnea_gat_bwd_dst_sliced_f32(const int32_t* rowptr, const int64_t* tpos,
-                                            int32_t n_rows, int heads, int d_head,
-                                            const float* dzT, const float* a, const float* ds2,
-                                            float* dH, int64_t lddh, float* ds1, void* stream) {
+template <typename T>
+int gat_bwd_dst_sliced(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows, int heads,
+                       int d_head, const float* dzT, const float* a, const float* ds2, T* dH,
+                       int64_t lddh, float* ds1, hipStream_t st) {
   const int D = heads * d_head;
   if (n_rows < 0 || !gat_sl_shape(heads, d_head, 64) || lddh % 4 || lddh < D)
     return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
   if (!rowptr || !tpos || !dzT || !a || !dH || !ds1) return GNNEA_EINVAL;
-  if ((uintptr_t)dH & 15) return GNNEA_EALIGN;
-  hipStream_t st = (hipStream_t)stream;
+  if (!alv<T>(dH)) return GNNEA_EALIGN;
   const int nch = (D / 4 + 63) / 64;
-#define GNNEA_D(HH, NC)                                                                          \
-  if (gat_dst_lanes() == 64)                                                                     \
-    hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC, 64>), dim3(div_up(n_rows, 4)), dim3(256), 0, st, \
-                       rowptr, tpos, n_rows, D, d_head, dzT, a, ds2, (float4*)dH, lddh / 4, ds1); \
-  else                                                                                           \
-    hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC, 32>), dim3(div_up(n_rows, 8)), dim3(256), 0, st, \
-                       rowptr, tpos, n_rows, D, d_head, dzT, a, ds2, (float4*)dH, lddh / 4, ds1)
+  typedef typename Vec4<T>::raw R;
+#define GNNEA_D(HH, NC)                                                                            \
+  if (gat_dst_lanes() == 64)                                                                       \
+    hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC, 64, T>), dim3(div_up(n_rows, 4)), dim3(256), 0,    \
+                       st, rowptr, tpos, n_rows, D, d_head, dzT, a, ds2, (R*)dH, lddh / 4, ds1);   \
+  else                                                                                             \
+    hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC, 32, T>), dim3(div_up(n_rows, 8)), dim3(256), 0,    \
+                       st, rowptr, tpos, n_rows, D, d_head, dzT, a, ds2, (R*)dH, lddh / 4, ds1)
 #define GNNEA_D_H(HH)                        \
   case HH:                                   \
     switch (nch) {                           \
@@ -696,4 +818,92 @@ extern "C" int gnnea_gat_bwd_dst_sliced_f32(const int32_t* rowptr, const int64_t
 #undef GNNEA_D
   GNNEA_LAUNCH_CHECK();
   return 0;
+}
+
+}  // namespace
+
+// G (slice-major [ceil(D/64)][n_rows][64], sstride elements per slice) and the records
+extern "C" int gnnea_gat_bwd_prep_sliced_f32(int32_t n_rows, int heads, int d_head,
+                                             const float* dY, const float* Y, int64_t ldy,
+                                             const float* s1, const float* m, const float* den,
+                                             int act, float* Gs, int64_t sstride, float* rec,
+                                             void* stream) {
+  return gat_bwd_prep_sliced<float>(n_rows, heads, d_head, dY, Y, ldy, s1, m, den, act, Gs,
+                                    sstride, rec, (hipStream_t)stream);
+}
+extern "C" int gnnea_gat_bwd_prep_sliced_bf16(int32_t n_rows, int heads, int d_head,
+                                              const void* dY, const void* Y, int64_t ldy,
+                                              const float* s1, const float* m, const float* den,
+                                              int act, void* Gs, int64_t sstride, float* rec,
+                                              void* stream) {
+  return gat_bwd_prep_sliced<bf16_t>(n_rows, heads, d_head, (const bf16_t*)dY, (const bf16_t*)Y,
+                                     ldy, s1, m, den, act, (bf16_t*)Gs, sstride, rec,
+                                     (hipStream_t)stream);
+}
+
+// source rows j of A^T (one KG block): per-edge weights wT, then the slice passes writing
+// dH_j = sum_i w_ij G_i (row-major, ldh) and the per-slice product partials pd [S][nnzT][2];
+// wT / pd are indexed by the absolute A^T position (rowptrT values), nnzT = A^T's entry count
+extern "C" int gnnea_gat_bwd_src_sliced_f32(const int32_t* rowptrT, const int32_t* colT,
+                                            const int64_t* permT, int32_t n_rows, int heads,
+                                            int d_head, const float* Hm, int64_t ldh,
+                                            const float* s2, float alpha, const float* emask,
+                                            const float* rec, const float* Gs, int64_t sstride,
+                                            float* wT, float* pd, int64_t nnzT, float* dH,
+                                            int64_t lddh, void* stream) {
+  return gat_bwd_src_sliced<float>(rowptrT, colT, permT, n_rows, heads, d_head, Hm, ldh, s2,
+                                   alpha, emask, rec, Gs, sstride, wT, pd, nnzT, dH, lddh,
+                                   (hipStream_t)stream);
+}
+extern "C" int gnnea_gat_bwd_src_sliced_bf16(const int32_t* rowptrT, const int32_t* colT,
+                                             const int64_t* permT, int32_t n_rows, int heads,
+                                             int d_head, const void* Hm, int64_t ldh,
+                                             const float* s2, float alpha, const float* emask,
+                                             const float* rec, const void* Gs, int64_t sstride,
+                                             float* wT, float* pd, int64_t nnzT, void* dH,
+                                             int64_t lddh, void* stream) {
+  return gat_bwd_src_sliced<bf16_t>(rowptrT, colT, permT, n_rows, heads, d_head,
+                                    (const bf16_t*)Hm, ldh, s2, alpha, emask, rec,
+                                    (const bf16_t*)Gs, sstride, wT, pd, nnzT, (bf16_t*)dH, lddh,
+                                    (hipStream_t)stream);
+}
+
+// dz (A^T order), ds2 and, when dH is non-NULL, dH_j += ds2_j (x) a2 for the source rows
+extern "C" int gnnea_gat_bwd_edge_sliced_f32(const int32_t* rowptrT, const int32_t* colT,
+                                             const int64_t* permT, int32_t n_rows, int heads,
+                                             int d_head, const float* s2, float alpha,
+                                             const float* emask, const float* rec,
+                                             const float* pd, int64_t nnzT, const float* a,
+                                             float* dH, int64_t lddh, float* dzT, float* ds2,
+                                             void* stream) {
+  return gat_bwd_edge_sliced<float>(rowptrT, colT, permT, n_rows, heads, d_head, s2, alpha,
+                                    emask, rec, pd, nnzT, a, dH, lddh, dzT, ds2,
+                                    (hipStream_t)stream);
+}
+extern "C" int gnnea_gat_bwd_edge_sliced_bf16(const int32_t* rowptrT, const int32_t* colT,
+                                              const int64_t* permT, int32_t n_rows, int heads,
+                                              int d_head, const float* s2, float alpha,
+                                              const float* emask, const float* rec,
+                                              const float* pd, int64_t nnzT, const float* a,
+                                              void* dH, int64_t lddh, float* dzT, float* ds2,
+                                              void* stream) {
+  return gat_bwd_edge_sliced<bf16_t>(rowptrT, colT, permT, n_rows, heads, d_head, s2, alpha,
+                                     emask, rec, pd, nnzT, a, (bf16_t*)dH, lddh, dzT, ds2,
+                                     (hipStream_t)stream);
+}
+
+// ds1 and dH_i += ds1_i (x) a1 (+ ds2_i (x) a2 when ds2 is non-NULL) for the destination rows
+extern "C" int gnnea_gat_bwd_dst_sliced_f32(const int32_t* rowptr, const int64_t* tpos,
+                                            int32_t n_rows, int heads, int d_head,
+                                            const float* dzT, const float* a, const float* ds2,
+                                            float* dH, int64_t lddh, float* ds1, void* stream) {
+  return gat_bwd_dst_sliced<float>(rowptr, tpos, n_rows, heads, d_head, dzT, a, ds2, dH, lddh,
+                                   ds1, (hipStream_t)stream);
+}
+extern "C" int gnnea_gat_bwd_dst_sliced_bf16(const int32_t* rowptr, const int64_t* tpos,
+                                             int32_t n_rows, int heads, int d_head,
+                                             const float* dzT, const float* a, const float* ds2,
+                                             void* dH, int64_t lddh, float* ds1, void* stream) {
+  return gat_bwd_dst_sliced<bf16_t>(rowptr, tpos, n_rows, heads, d_head, dzT, a, ds2,
+                                    (bf16_t*)dH, lddh, ds1, (hipStream_t)stream);
 }

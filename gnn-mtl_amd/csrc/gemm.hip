@@ -1080,6 +1080,15 @@ static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t l
                       const float* B, int64_t ldb, const float* bias, float beta, float* C,
                       int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, hipStream_t s);
 
+// k_gemm_x3p on (default) or off (GNNEA_X3_PIPE=0: the register-staged k_gemm_x3, A/B comparison)
+static bool x3_pipe_on() {
+  static const bool pipe = [] {
+    const char* e = getenv("GNNEA_X3_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return pipe;
+}
+
 static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
                    int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
                    float* C, int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, void* stream,
@@ -1088,7 +1097,10 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
     if (cs2 % 4 != 0 || cs2 < M * 64 || cs != 64) return GNNEA_EINVAL;
     const bool lda_ok = !trans_a && lda % 4 == 0 && K % 4 == 0 && (((uintptr_t)A) & 15) == 0;
     const int64_t pb = x3_planes_bytes(N, K);
-    const bool fused = lda_ok && ws && ws_bytes >= pb && pick_splits(M, N, K, ws_bytes - pb) == 1;
+    // the same condition as k_gemm_x3p's launch below (pipe on, float4 A, no split-K): any other
+    // kernel leaves C2 unwritten, so it is packed after
+    const bool fused = x3_pipe_on() && lda_ok && ws && ws_bytes >= pb &&
+                       pick_splits(M, N, K, ws_bytes - pb) == 1;
     if (!fused) {
       const int rc = gemm_x3(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs,
                              ws, ws_bytes, stream);
@@ -1116,10 +1128,7 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
   bf16_t* planes = (bf16_t*)ws;
   const bool vec = lda % 4 == 0 && K % 4 == 0 && al16(A);
   const int splits = pick_splits(M, N, K, ws_bytes - pbytes);
-  static const bool pipe = [] {
-    const char* e = getenv("GNNEA_X3_PIPE");  // A/B comparison only
-    return !(e && e[0] == '0');
-  }();
+  const bool pipe = x3_pipe_on();
   if (!(pipe && vec && splits == 1)) {
     const int64_t tot = N * ldp;
     const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
@@ -1132,8 +1141,12 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
     // 32*WT-column tiles, WT <= 5 (N = 300: two 160-column tiles)
     int wtp = (int)((N + 31) / 32 < 5 ? (N + 31) / 32 : 5);
     if (const char* e = getenv("GNNEA_X3_WT")) {  // tuning override only
+      // taken only when its padded plane rows fit the 320-row rounding x3_planes_bytes reserves
+      // (N = 300 with WT 3 / 4 would pad to 384 rows and overrun the planes)
       const int v = atoi(e);
-      if ((v >= 1 && v <= 5) || v == 10) wtp = v;
+      if (((v >= 1 && v <= 5) || v == 10) &&
+          (N + 32 * v - 1) / (32 * v) * (32 * v) <= (N + 319) / 320 * 320)
+        wtp = v;
     }
     const int tn = (int)((N + 32 * wtp - 1) / (32 * wtp));
     const int np = tn * 32 * wtp;  // <= the 320-row rounding x3_planes_bytes reserves

@@ -28,21 +28,6 @@ struct SliceOf {
 };
 constexpr int kSliceW = SliceOf<float>::W;
 
-__device__ __forceinline__ void unpack16(const uint4& u, float (&f)[4]) {
-  f[0] = __builtin_bit_cast(float, u.x);
-  f[1] = __builtin_bit_cast(float, u.y);
-  f[2] = __builtin_bit_cast(float, u.z);
-  f[3] = __builtin_bit_cast(float, u.w);
-}
-__device__ __forceinline__ void unpack16(const uint4& u, float (&f)[8]) {
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    f[2 * k] = __builtin_bit_cast(float, w[k] << 16);
-    f[2 * k + 1] = __builtin_bit_cast(float, w[k] & 0xffff0000u);
-  }
-}
-
 // HighWay epilogue operands (layers/layers.py:64-76), fp32 tables only: gate_pre is read from a
 // slice-major table at column offset goff (the fused HighWay layer's projection
 // Z = x·[Wᵀ | K_g] is ONE sliced table: hidden in columns [0, D), gate_pre in [D, 2D)); resid,

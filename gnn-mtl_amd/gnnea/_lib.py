@@ -154,6 +154,22 @@ SIGNATURES = {
                                                      _p, _p]),
     "gnnea_gat_bwd_dst_sliced_f32": (ctypes.c_int, [_p, _p, _i32, ctypes.c_int, ctypes.c_int, _p,
                                                     _p, _p, _p, _i64, _p, _p]),
+    "gnnea_gat_fwd_sliced_bf16": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int,
+                                                 ctypes.c_int, _p, _p, _f32, _p, ctypes.c_int, _p,
+                                                 _i64, _p, _p, _p, _p]),
+    "gnnea_gat_bwd_prep_sliced_bf16": (ctypes.c_int, [_i32, ctypes.c_int, ctypes.c_int, _p, _p,
+                                                      _i64, _p, _p, _p, ctypes.c_int, _p, _i64,
+                                                      _p, _p]),
+    "gnnea_gat_bwd_src_sliced_bf16": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int,
+                                                     ctypes.c_int, _p, _i64, _p, _f32, _p, _p, _p,
+                                                     _i64, _p, _p, _i64, _p, _i64, _p]),
+    "gnnea_gat_bwd_edge_sliced_bf16": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int,
+                                                      ctypes.c_int, _p, _f32, _p, _p, _p, _i64,
+                                                      _p, _p, _i64, _p, _p, _p]),
+    "gnnea_gat_bwd_dst_sliced_bf16": (ctypes.c_int, [_p, _p, _i32, ctypes.c_int, ctypes.c_int,
+                                                     _p, _p, _p, _p, _i64, _p, _p]),
+    "gnnea_slice_pack64_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, _p]),
+    "gnnea_slice_pack64_bf16": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, _p]),
     "gnnea_gemm_f64": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
                                       _i64, ctypes.c_double, _p, _i64, ctypes.c_double, _p, _i64,
                                       _p]),

@@ -15,9 +15,12 @@ Layout (one process per GPU, torch.distributed; backend "nccl" is RCCL over xGMI
       four 76-column slices of all rows);
     - "rows": each rank owns n/g destination rows (KG-local column ids) and gathers the
       group's projected rows (the halo: on uniform random graphs nearly every remote row is
-      referenced) by direct peer transfers over xGMI (gnnea.exchange), overlapped with the
-      aggregation over its own rows.  This is what a graph layer executes, so it is the bench
-      default at N > 1; the two exchange-free partitions time the aggregation alone.
+      referenced) by peer transfers over xGMI (gnnea.exchange), slice by slice: the KG's
+      table is held slice-major ([S][n][64] fp32, one Infinity-Cache-sized table per slice),
+      every slice's exchange is issued at once and slice q is aggregated over the shard's CSR
+      as soon as it has landed, while the later slices move (SURVEY.md §8e overlap).  This is
+      what a graph layer executes (gnnea.dist_graph), so it is the bench default at N > 1;
+      the two exchange-free partitions time the aggregation alone.
 The partition / exchange logic is device-independent (numpy + torch.distributed) and is
 exercised with gloo on CPU in tests/test_dist_gloo.py; the GPU path adds only the CSR upload.
 """
@@ -98,13 +101,6 @@ def shard_coo(triples, n, t, part):
     return r[keep] - part.row0, c[keep], v[keep]
 
 
-def split_own_remote(r, c, v, part):
-    """Entries whose source row is owned locally (columns re-based to the local rows) and the
-    rest (KG-local columns, read from the all-gathered halo)."""
-    own = (c >= part.row0) & (c < part.row1)
-    return (r[own], c[own] - part.row0, v[own]), (r[~own], c[~own], v[~own])
-
-
 def make_groups(part):
     """Both KG groups (every rank must create every group, in the same order)."""
     if part.world == 1:
@@ -162,15 +158,9 @@ class KGShard:
             return DeviceCSR.from_coo(torch.from_numpy(rr.astype(np.int32)).to(device),
                                       torch.from_numpy(cc.astype(np.int32)).to(device),
                                       torch.from_numpy(vv).to(device), self.part.n_rows, ncols)
-        if self.part.g == 1 or kind in ("features", "tiles"):
-            self.csr = up(r, c, v, self.part.n_cols)
-            self.csr_own = self.csr_remote = None
-        else:
-            (ro, co, vo), (rr, cr, vr) = split_own_remote(r, c, v, self.part)
-            self.csr = None
-            self.csr_own = up(ro, co, vo, self.part.n_rows)
-            self.csr_remote = up(rr, cr, vr, self.part.n_cols)
+        self.csr = up(r, c, v, self.part.n_cols)
         self.group = make_groups(self.part) if kind == "rows" else None
+        self._tables = None
 
     @property
     def g(self):
@@ -184,12 +174,28 @@ class KGShard:
     def n_cols(self):
         return self.part.n_cols
 
-    def aggregate(self, h_local, h_full, out, act, events=None, hs=None):
-        """out = act(A_shard · H) for this rank's rows; H's remote rows arrive by the halo
-        all-gather, overlapped with the aggregation over the locally owned rows.  ``hs``: the
-        same H held slice-major (gnnea.ops.spmm_sliced) for the exchange-free partitions."""
+    def halo_tables(self, D, dtype=torch.float32):
+        """The KG's slice tables [S][n][W] (own rows packed in by aggregate), allocated once."""
         from . import ops
-        from ._lib import GNNEA_ACT_IDENTITY
+        W = ops.slice_w(dtype)
+        S = (D + W - 1) // W
+        t = self._tables
+        if t is None or t.shape != (S, self.n_cols, W) or t.dtype != dtype:
+            t = self._tables = torch.empty((S, self.n_cols, W), dtype=dtype, device=self.device)
+        return t
+
+    def slices(self, D, dtype=torch.float32):
+        from . import ops
+        W = ops.slice_w(dtype)
+        return [(c0, min(D, c0 + W)) for c0 in range(0, D, W)]
+
+    def aggregate(self, h_local, out, act, events=None, hs=None):
+        """out = act(A_shard · H) for this rank's rows.  Row shards of a KG group: the own rows
+        packed into the KG's slice tables, every slice's halo exchange issued at once, slice q
+        aggregated as soon as it has landed (``events``: [start, end] + a pair per slice around
+        its aggregation).  ``hs``: H held slice-major (gnnea.ops.spmm_sliced) for the
+        exchange-free partitions."""
+        from . import exchange, ops
         rec = (lambda k: events[k].record()) if events is not None else (lambda k: None)
         if self.part.g == 1 or self.part.kind in ("features", "tiles"):  # no exchange
             rec(0)
@@ -199,16 +205,22 @@ class KGShard:
                 ops.spmm(self.csr, h_local, act, out=out)
             rec(1)
             return out
-        from . import exchange
-        works = exchange.all_gather(h_local, h_full, self.group,
-                                    self.part.group_ranks(self.part.kg), self.part.li,
-                                    async_op=True, other=self.part.other_ranks())
+        D = h_local.shape[1]
+        tables = self.halo_tables(D, h_local.dtype)
         rec(0)
-        ops.spmm(self.csr_own, h_local, GNNEA_ACT_IDENTITY, out=out)
+        with torch.cuda.device(self.device):
+            ops.check(ops._sfn("gnnea_slice_pack", h_local.dtype)(
+                ops.ptr(h_local), ops._ld(h_local), self.n_rows, D,
+                ops._off(tables[0], self.part.row0), tables.stride(0),
+                ops.stream_of(self.device)))
+        works = exchange.all_gather_slices(list(tables), self.part.row0, self.n_rows, self.group,
+                                           self.part.group_ranks(self.part.kg), self.part.li,
+                                           other=self.part.other_ranks())
+        for q, (c0, c1) in enumerate(self.slices(D, h_local.dtype)):
+            for w in works[q]:
+                w.wait()
+            rec(2 + 2 * q)
+            ops.spmm_sliced(self.csr, tables[q:q + 1], c1 - c0, act, out=out[:, c0:c1])
+            rec(3 + 2 * q)
         rec(1)
-        for w in works:
-            w.wait()
-        rec(2)
-        ops.spmm(self.csr_remote, h_full, act, out=out, beta=1.0)
-        rec(3)
         return out

@@ -15,6 +15,15 @@ only.  Per graph layer (layers/layers.py:30-39, 58-77):
             dhidden_loc= reduce_scatter(P)            peer transfers, summed by the owner
             dW, db     = local GEMMs; summed over ALL ranks by allreduce_grads() (one bucket)
 
+Overlap (§8e): the halo exchange and the aggregation are cut into column slices of the
+feature table (the slice-major layout's 64-column fp32 / 128-column bf16 slices; one KG slice of
+cfg-4 is 256 MB).  The own rows are packed into the KG's [S][n][W] table, every slice's exchange
+is issued at once (gnnea.exchange.all_gather_slices), and slice q is aggregated over the whole
+shard CSR (KG-local columns, Infinity-Cache-sized table) as soon as it has landed, while the
+later slices are in flight.  Backward mirrors it: Aᵀ·G of slice q is computed and its
+reduce-scatter issued at once (exchange.reduce_scatter_start), the next slice computing while
+it moves; the owners sum once every slice has arrived.
+
 The HighWay gate (x_loc·K_g, the blend with x_loc) is row-local.  ``gather_rows`` assembles the
 final embeddings of both KGs on every rank (all_gather over the world) for the EA loss, which
 every rank then evaluates identically; its backward keeps the rank's own rows of the gradient.
@@ -28,7 +37,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .dist import Partition, make_groups, shard_coo, split_own_remote
+from .dist import Partition, make_groups, shard_coo
 
 
 class HipEngine:
@@ -79,6 +88,60 @@ class HipEngine:
         Y, m, den, s1, s2 = ops.gat_forward(csr, Hp, a32, heads, d_head, alpha, act, row0=row0)
         return (Y if Y.shape[1] == D else Y[:, :D]), (Hp, a32, s1, s2, m, den, Y)
 
+    # ---- column-slice stages (the pipelined halo of DistAdj) ---------------------------
+    def slice_w(self, dtype):
+        """Columns per exchange / aggregation stage: one slice of the slice-major table (256 B
+        of row: 64 fp32 / 128 bf16 columns; one KG slice of cfg-4 is 256 MB)."""
+        from . import ops
+        return ops.slice_w(dtype)
+
+    def pack_slices(self, x, tables, row0):
+        """tables[q, row0:row0+rows, :w_q] = x[:, q-th column block] (one pass)."""
+        from . import ops
+        x = ops._rows(x)
+        S, n, W = tables.shape
+        with _lib.on_device(x.device):
+            _lib.check(ops._sfn("gnnea_slice_pack", x.dtype)(
+                _lib.ptr(x), ops._ld(x), x.shape[0], x.shape[1],
+                ops._off(tables[0], row0), n * W, _lib.stream_of(x.device)))
+        return tables
+
+    def spmm_slice(self, csr, table, w, act, out):
+        """out (a [rows, w] column block) = act(A · table[:, :w]) over one slice table."""
+        from . import ops
+        return ops.spmm_sliced(csr, table.unsqueeze(0), w, act, out=out)
+
+    def spmm_t_slice(self, csr, table, w):
+        """Aᵀ · table[:, :w] ([csr.n_cols, w]) over one slice table of the shard's rows."""
+        from . import ops
+        return ops.spmm_sliced(csr.transpose(), table.unsqueeze(0), w)
+
+    def act_bwd_slices(self, dy, y, act):
+        """dy ⊙ act'(y) written slice-major ([S][rows][W])."""
+        from . import ops
+        return ops.act_bwd_sliced(dy, y, act)
+
+    def highway_slice(self, csr, table, w, gates, c0, bias_gate, resid, out, S, G, act):
+        """Columns [c0, c0+w) of the HighWay tail (layers/layers.py:64-76) from one slice
+        table of the hidden rows: gate_pre from the shard's own slice-major gate table."""
+        from . import ops
+        L = _lib.lib()
+        with _lib.on_device(table.device):
+            for r0, r1 in csr.row_blocks():
+                _lib.check(L.gnnea_spmm_highway_sliced_f32(
+                    ops._off32(csr.rowptr, r0), _lib.ptr(csr.col), _lib.ptr(csr.val), r1 - r0, w,
+                    _lib.ptr(table), table.numel(), ops._off(gates[0], r0), gates.stride(0), c0,
+                    None if bias_gate is None else ops._off(bias_gate.view(1, -1), 0, c0),
+                    ops._off(resid, r0, c0), resid.stride(0), ops._off(out, r0, c0),
+                    out.stride(0), ops._off(S, r0, c0), ops._off(G, r0, c0), S.stride(0),
+                    int(act), _lib.stream_of(table.device)))
+        return out
+
+    def highway_bwd_slices(self, dy, S, G, resid, act, want_dresid, dgate):
+        """(dS slice-major, dresid): dS = dy·g·act'(S), dgate written into ``dgate``."""
+        from . import ops
+        return ops.highway_bwd_sliced(dy, S, G, resid, act, want_dresid, dgate)
+
     def gat_bwd(self, csr, saved, dY, heads, d_head, alpha, act, row0, need_da):
         """(dH partial over every KG row, da partial) of sum(Y_loc ⊙ dY)."""
         from . import ops
@@ -110,12 +173,6 @@ class DistAdj:
         e = self.engine
         self.nnz = int(np.asarray(r).size)
         self.csr = e.csr(r, c, v, part.n_rows, part.n_cols, device)
-        if part.g > 1:
-            (ro, co, vo), (rr, cr, vr) = split_own_remote(r, c, v, part)
-            self.csr_own = e.csr(ro, co, vo, part.n_rows, part.n_rows, device)
-            self.csr_remote = e.csr(rr, cr, vr, part.n_rows, part.n_cols, device)
-        else:
-            self.csr_own = self.csr_remote = None
         self.group = make_groups(part) if part.world > 1 else None
 
     @classmethod
@@ -159,8 +216,96 @@ class DistAdj:
     def highway_fwd(self, hidden, gate_pre, resid, bias_gate, act):
         """HighWay tail over the shard (gnnea.ops.HighwayLayerFn's aggregation hook): the
         group's hidden rows by the halo all-gather, gate_pre / resid row-local."""
+        if self.staged(hidden, highway=True):
+            return self.staged_highway(hidden, gate_pre, resid, bias_gate, act)
         full, _ = self.halo(hidden)
         return self.engine.highway_fwd(self.csr, full, gate_pre, resid, bias_gate, act)
+
+    # ---- the per-slice pipeline (§8e overlap) ------------------------------------------------
+    def staged(self, t, highway=False):
+        """The halo of ``t`` moves slice by slice, overlapped with the per-slice aggregation:
+        every row shard (g > 1) whose engine has the slice operations; fp32 / bf16 with whole
+        4-column chunks (the HighWay epilogue: fp32)."""
+        if self.part.g == 1 or not hasattr(self.engine, "slice_w") or t.shape[1] % 4:
+            return False
+        if isinstance(self.engine, HipEngine):
+            return t.dtype == torch.float32 or (t.dtype == torch.bfloat16 and not highway)
+        return True
+
+    def stages(self, D, dtype):
+        """Column blocks [(c0, c1)] of width W = the engine's slice width."""
+        W = self.engine.slice_w(dtype)
+        return W, [(c0, min(D, c0 + W)) for c0 in range(0, D, W)]
+
+    def _peers(self):
+        return self.part.group_ranks(self.part.kg), self.part.li, self.part.other_ranks()
+
+    def halo_slices(self, h_loc):
+        """Pack the own rows into the KG's slice tables [S][n][W] and issue every slice's
+        exchange: returns (tables, stages, works per slice)."""
+        from . import exchange
+        D = h_loc.shape[1]
+        W, st = self.stages(D, h_loc.dtype)
+        tables = torch.empty((len(st), self.part.n_cols, W), dtype=h_loc.dtype,
+                             device=h_loc.device)
+        self.engine.pack_slices(h_loc, tables, self.part.row0)
+        ranks, li, other = self._peers()
+        works = exchange.all_gather_slices(list(tables), self.part.row0, self.part.n_rows,
+                                           self.group, ranks, li, other)
+        return tables, st, works
+
+    def staged_aggregate(self, hidden, act, events=None):
+        """out = act(A_shard · hidden_KG), slice q aggregated as soon as it has landed."""
+        tables, st, works = self.halo_slices(hidden)
+        out = torch.empty((self.part.n_rows, hidden.shape[1]), dtype=hidden.dtype,
+                          device=hidden.device)
+        for q, (c0, c1) in enumerate(st):
+            for w in works[q]:
+                w.wait()
+            if events is not None:
+                events[q][0].record()
+            self.engine.spmm_slice(self.csr, tables[q], c1 - c0, act, out[:, c0:c1])
+            if events is not None:
+                events[q][1].record()
+        return out
+
+    def staged_aggregate_t(self, Gs, D, out=None):
+        """This rank's rows of sum_group A_shardᵀ·G from G held as local slice tables
+        ([S][rows][W]): per slice, Aᵀ·G_q then its reduce-scatter issued at once (the owner sums
+        in peer order once every slice has arrived).  ``out``: [rows, D] (a column block of a
+        wider buffer is fine)."""
+        from . import exchange
+        _, st = self.stages(D, Gs.dtype)
+        if out is None:
+            out = torch.empty((self.part.n_rows, D), dtype=Gs.dtype, device=Gs.device)
+        ranks, li, other = self._peers()
+        pend = []
+        for q, (c0, c1) in enumerate(st):
+            P = self.engine.spmm_t_slice(self.csr, Gs[q], c1 - c0)
+            pend.append(exchange.reduce_scatter_start(P, self.group, ranks, li, other,
+                                                      out=out[:, c0:c1]))
+        for p in pend:
+            p.finish()
+        return out
+
+    def staged_highway(self, hidden, gate_pre, resid, bias_gate, act):
+        """HighWay tail (layers/layers.py:64-76) slice by slice over the halo tables; the gate
+        is row-local (packed into the shard's own slice tables)."""
+        tables, st, works = self.halo_slices(hidden)
+        n_rows, D = self.part.n_rows, hidden.shape[1]
+        gates = torch.empty((len(st), n_rows, tables.shape[2]), dtype=hidden.dtype,
+                            device=hidden.device)
+        self.engine.pack_slices(gate_pre, gates, 0)
+        out = torch.empty((n_rows, D), dtype=hidden.dtype, device=hidden.device)
+        S = torch.empty_like(out)
+        G = torch.empty_like(out)
+        resid = resid.contiguous()
+        for q, (c0, c1) in enumerate(st):
+            for w in works[q]:
+                w.wait()
+            self.engine.highway_slice(self.csr, tables[q], c1 - c0, gates, c0, bias_gate, resid,
+                                      out, S, G, act)
+        return out, S, G
 
     def local_csr(self):
         """The shard's CSR when this rank aggregates without any exchange (one KG per rank, or
@@ -187,6 +332,11 @@ class DistAdj:
         backward hook; out may be a column block of a wider buffer)."""
         if self.part.g == 1:
             return self.engine.spmm_t(self.csr, g, out=out)
+        if self.staged(g):
+            W, st = self.stages(g.shape[1], g.dtype)
+            Gs = torch.empty((len(st), self.part.n_rows, W), dtype=g.dtype, device=g.device)
+            self.engine.pack_slices(g, Gs, 0)
+            return self.staged_aggregate_t(Gs, g.shape[1], out)
         out.copy_(self.reduce_scatter(self.engine.spmm_t(self.csr, g)))
         return out
 
@@ -245,12 +395,11 @@ class HaloAggregateFn(torch.autograd.Function):
         e = dadj.engine
         if dadj.part.g == 1:
             out = e.spmm(dadj.csr, hidden, act)
+        elif dadj.staged(hidden):
+            out = dadj.staged_aggregate(hidden, act)  # per-slice exchange / aggregation
         else:
-            full, work = dadj.halo(hidden, async_op=True, copy_own=False)
-            out = e.spmm(dadj.csr_own, hidden, _lib.GNNEA_ACT_IDENTITY)  # overlaps the gather
-            if work is not None:
-                work.wait()
-            e.spmm(dadj.csr_remote, full, act, out=out, beta=1.0)
+            full, _ = dadj.halo(hidden)
+            out = e.spmm(dadj.csr, full, act)
         ctx.dadj, ctx.act = dadj, act
         ctx.save_for_backward(out)
         return out
@@ -259,6 +408,9 @@ class HaloAggregateFn(torch.autograd.Function):
     def backward(ctx, dy):
         (out,) = ctx.saved_tensors
         dadj = ctx.dadj
+        if dadj.part.g > 1 and dadj.staged(out):
+            Gs = dadj.engine.act_bwd_slices(dy.contiguous(), out, ctx.act)
+            return dadj.staged_aggregate_t(Gs, out.shape[1]), None, None
         return dadj.reduce_scatter(dadj.engine.act_spmm_t(dadj.csr, dy, out, ctx.act)), None, None
 
 
@@ -268,8 +420,7 @@ class HaloHighwayFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, hidden, gate_pre, resid, bias_gate, dadj, act):
-        full, _ = dadj.halo(hidden)
-        out, S, G = dadj.engine.highway_fwd(dadj.csr, full, gate_pre, resid, bias_gate, act)
+        out, S, G = dadj.highway_fwd(hidden, gate_pre, resid, bias_gate, act)
         ctx.dadj, ctx.act = dadj, act
         ctx.save_for_backward(S, G, resid)
         return out
@@ -279,6 +430,11 @@ class HaloHighwayFn(torch.autograd.Function):
         S, G, resid = ctx.saved_tensors
         dadj = ctx.dadj
         e = dadj.engine
+        if dadj.part.g > 1 and dadj.staged(S, highway=True):
+            dgate = torch.empty_like(S)
+            dSs, dres = e.highway_bwd_slices(dy.contiguous(), S, G, resid, ctx.act,
+                                             ctx.needs_input_grad[2], dgate)
+            return (dadj.staged_aggregate_t(dSs, S.shape[1]), dgate, dres, None, None, None)
         dS, dgate, dres = e.highway_bwd(dy.contiguous(), S, G, resid, ctx.act,
                                         ctx.needs_input_grad[2])
         dh = dadj.reduce_scatter(e.spmm_t(dadj.csr, dS))

@@ -61,7 +61,7 @@ def _units(rows, g, d1=1, d2=None):
     return [(cut[0], cut[d1]), (cut[d1], cut[e])] + [(cut[e + k], cut[e + k + 1]) for k in range(g)]
 
 
-def _relay_rs(blocks, recv, ranks, li, other):
+def _relay_rs(blocks, recv, ranks, li, other, sync=True):
     """Relayed exchange of a reduce-scatter over two groups of g: ``blocks[i]`` (this rank's
     partial of group rank i's rows) goes to rank i, its D1 / D2 (g-1 units each) direct in
     phases 1 / 2 and its R_k (1 unit of 3g-2) through the other group's k-th GPU; ``recv[p]``
@@ -94,8 +94,10 @@ def _relay_rs(blocks, recv, ranks, li, other):
         for d in theirs:
             if d != s_:
                 ops1.append(dist.P2POp(dist.irecv, stage[(s_, d)], s_))
-    for w in dist.batch_isend_irecv(ops1):
-        w.wait()
+    w1 = dist.batch_isend_irecv(ops1)
+    if sync:
+        for w in w1:
+            w.wait()
     ops2 = []
     for p in peers:
         ops2.append(dist.P2POp(dist.isend, rows(blk(p), 1), p))
@@ -107,8 +109,12 @@ def _relay_rs(blocks, recv, ranks, li, other):
     for k, o in enumerate(theirs):
         for p in peers:
             ops2.append(dist.P2POp(dist.irecv, rows(recv[p], 2 + k), o))
-    for w in dist.batch_isend_irecv(ops2):
-        w.wait()
+    w2 = dist.batch_isend_irecv(ops2)
+    if sync:
+        for w in w2:
+            w.wait()
+        return []
+    return w1 + w2 + [_Keep(stage)]
 
 
 def _relay(h_loc, full_parts, ranks, li, other, sync):
@@ -222,6 +228,70 @@ def all_gather(h_loc, full, group, ranks, li, copy_own=False, async_op=False, ot
     return works
 
 
+class PendingSum:
+    """An issued reduce-scatter: ``finish()`` waits for the receives (stream-ordered on the
+    caller's stream for RCCL) and returns the owner's rows: its own partial plus the peers'
+    partials in peer order (deterministic, no RCCL reduction kernel)."""
+
+    def __init__(self, own, recv, works, out=None):
+        self.own, self.recv, self.works, self.out = own, recv, works, out
+
+    def finish(self):
+        for w in self.works:
+            w.wait()
+        out = self.out
+        if out is None:
+            out = self.own.clone()
+        else:
+            out.copy_(self.own)
+        for r in self.recv:
+            out += r.to(out.device) if r.device != out.device else r
+        self.own = self.recv = self.works = None
+        return out
+
+
+def reduce_scatter_start(partial, group, ranks, li, other=None, out=None):
+    """Issue the reduce-scatter of ``partial`` ([g·rows, w], this rank's partial of every group
+    row) without waiting: returns a PendingSum whose finish() gives this rank's rows (into
+    ``out`` when given, e.g. a column block of a wider buffer).  Several can be in flight at once
+    (the per-slice pipeline of gnnea.dist_graph); under gloo the exchange completes here."""
+    g = len(ranks)
+    partial = partial.contiguous()
+    if g == 1:
+        return PendingSum(partial, [], [], out)
+    blocks = _blocks(partial, g)
+    stage = _gloo(group) and partial.is_cuda
+    send = [b.detach().cpu() if stage else b for b in blocks]
+    if relay_applies(ranks, other):
+        recv = {p: torch.empty_like(send[li]) for p in ranks if p != ranks[li]}
+        works = _relay_rs(send, recv, ranks, li, other, sync=_gloo(group))
+        return PendingSum(blocks[li], [recv[p] for p in ranks if p != ranks[li]], works, out)
+    recv = [torch.empty_like(send[li]) for p in range(g) if p != li]
+    ops = []
+    k = 0
+    for p in range(g):
+        if p != li:
+            ops.append(dist.P2POp(dist.isend, send[p], ranks[p], group=group))
+            ops.append(dist.P2POp(dist.irecv, recv[k], ranks[p], group=group))
+            k += 1
+    works = dist.batch_isend_irecv(ops)
+    if _gloo(group):
+        for w in works:
+            w.wait()
+        works = []
+    return PendingSum(blocks[li], recv, works, out)
+
+
+def all_gather_slices(tables, row0, rows, group, ranks, li, other=None):
+    """The halo exchange cut into column slices (SURVEY.md §8e overlap): ``tables`` are the
+    KG group's feature tables, one contiguous [g·rows, w] table per column slice, this rank's
+    rows [row0, row0 + rows) already in place.  Every slice's exchange is issued at once (in
+    slice order on the communicator); returns one list of works per slice, so the caller can
+    aggregate slice q as soon as its works are done while the later slices are in flight."""
+    return [all_gather(t[row0:row0 + rows], t, group, ranks, li, copy_own=False, async_op=True,
+                       other=other) for t in tables]
+
+
 def reduce_scatter(partial, group, ranks, li, other=None):
     """This rank's rows of the group sum of the [g·rows, D] partials.  ``other`` as in
     all_gather: the relayed schedule (``_relay_rs``) when given."""
@@ -234,7 +304,7 @@ def reduce_scatter(partial, group, ranks, li, other=None):
         stage = _gloo(group) and partial.is_cuda
         send = [b.detach().cpu() if stage else b for b in blocks]
         recv = {p: torch.empty_like(send[li]) for p in ranks if p != ranks[li]}
-        _relay_rs(send, recv, ranks, li, other)
+        _relay_rs(send, recv, ranks, li, other, sync=True)
         out = blocks[li].clone()
         for p in ranks:  # peer order, as the direct schedule sums
             if p != ranks[li]:

@@ -4,6 +4,7 @@ Every function here launches libgnnea kernels on the tensor's current stream; no
 path (``_lib.require_device``).  Reference call sites each op replaces are cited per function.
 """
 import ctypes
+import os
 import weakref
 
 import torch
@@ -271,7 +272,10 @@ _SLICED_COPIES = {}
 
 
 def sliced_copy_of(t, D):
-    e = _SLICED_COPIES.get(t.data_ptr())
+    """The slice-major copy of ``t`` written by its projection GEMM, or None; the entry is
+    removed (it is used once, by the layer's forward, and would otherwise keep an H-sized table
+    alive through the backward)."""
+    e = _SLICED_COPIES.pop(t.data_ptr(), None)
     if e is None:
         return None
     ref, ver, shape, xs = e
@@ -327,11 +331,11 @@ def matmul(x, w, sliced=False):
 INFINITY_CACHE_BYTES = 256 << 20
 
 
-def _off(t, r0):
-    """Device pointer of row r0 of a row-major tensor (None -> NULL)."""
+def _off(t, r0, c0=0):
+    """Device pointer of element (r0, c0) of a row-major tensor (None -> NULL)."""
     if t is None:
         return None
-    return ctypes.c_void_p(t.data_ptr() + t.element_size() * r0 * t.stride(0))
+    return ctypes.c_void_p(t.data_ptr() + t.element_size() * (r0 * t.stride(0) + c0))
 
 
 def _off32(t, r0):
@@ -420,10 +424,11 @@ def use_sliced(n_src, D, dtype):
     return D * es >= 2 * SLICE_BYTES and n_src * D * es > INFINITY_CACHE_BYTES
 
 
-def sliced_empty(n, D, device, dtype=torch.float32):
-    """Uninitialised [S, n, W] table for an [n, D] matrix (W = 256 B of ``dtype``,
-    S = ceil(D/W)); columns past D in the last slice are never read."""
-    W = slice_w(dtype)
+def sliced_empty(n, D, device, dtype=torch.float32, W=None):
+    """Uninitialised [S, n, W] table for an [n, D] matrix (W = 256 B of ``dtype`` by default,
+    64 columns for the GAT tables; S = ceil(D/W)); columns past D in the last slice are never
+    read."""
+    W = W or slice_w(dtype)
     S = (D + W - 1) // W
     return torch.empty((S, n, W), dtype=dtype, device=device)
 
@@ -890,7 +895,8 @@ def _pad4(t, D, dtype=None):
     return out
 
 
-GAT_SLICED = True  # tests switch it off to compare with the row-major edge pass
+# tests switch it off to compare with the row-major edge pass (GNNEA_GAT_SLICED=0: A/B timing)
+GAT_SLICED = os.environ.get("GNNEA_GAT_SLICED", "1") != "0"
 
 
 def gat_two_heads_per_slice(heads, d_head):
@@ -905,10 +911,24 @@ def gat_two_heads_per_slice(heads, d_head):
 
 
 def _gat_sliced_applies(H, heads, d_head, Y):
+    """The GAT passes run over 64-column slice-major tables (fp32: 256 B, bf16: 128 B per row
+    piece; one KG slice of cfg-4 fp32 / cfg-5 bf16 is 256 MB) when the row-major table exceeds
+    the Infinity Cache and spans at least two slices."""
     D = heads * d_head
-    return (GAT_SLICED and H.dtype == torch.float32 and gat_two_heads_per_slice(heads, d_head)
-            and D % 4 == 0 and heads <= 8 and D <= 1024 and Y.shape[1] == D
-            and use_sliced(H.shape[0], D, H.dtype))
+    return (GAT_SLICED and H.dtype in FEATURE_DTYPES and gat_two_heads_per_slice(heads, d_head)
+            and D % 4 == 0 and heads <= 8 and 128 <= D <= 1024 and Y.shape[1] == D
+            and H.shape[0] * D * H.element_size() > INFINITY_CACHE_BYTES)
+
+
+def slice_pack64(x):
+    """Row-major [n, D] (fp32 / bf16) -> the 64-column slice-major GAT table."""
+    x = _rows(x)
+    n, D = x.shape
+    xs = sliced_empty(n, D, x.device, x.dtype, W=64)
+    with _lib.on_device(x.device):
+        check(_sfn("gnnea_slice_pack64", x.dtype)(ptr(x), _ld(x), n, D, ptr(xs), xs.stride(0),
+                                                 stream_of(x.device)))
+    return xs
 
 
 def gat_forward(csr, H, a32, heads, d_head, alpha, act, em=None, row0=0):
@@ -928,11 +948,11 @@ def gat_forward(csr, H, a32, heads, d_head, alpha, act, em=None, row0=0):
     if _gat_sliced_applies(H, heads, d_head, Y):
         # above the Infinity Cache: the table slice-major (64-column slices, one 256-MB table
         # per KG slice), row statistics once, then the slices one after another
-        Hs = sliced_copy_of(H, D)
+        Hs = sliced_copy_of(H, D) if H.dtype == torch.float32 else None
         if Hs is None:
-            Hs = slice_pack(H[:, :D])
+            Hs = slice_pack64(H[:, :D])
         wgt = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=H.device)
-        fs = _lib.lib().gnnea_gat_fwd_sliced_f32
+        fs = _gat_fn("gnnea_gat_fwd_sliced", H.dtype)
         with _lib.on_device(H.device):
             for r0, r1 in _blocks(csr, H):
                 check(fs(_off32(csr.rowptr, r0), ptr(csr.col), r1 - r0, ptr(Hs), Hs.stride(0),
@@ -991,14 +1011,14 @@ def gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha, act, 
 
 def _gat_backward_sliced(csr, csrT, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha,
                          act, em, row0, rec, dH, dzT, ds1, ds2):
-    """The backward over a slice-major G (gnnea_gat_bwd_*_sliced_f32): G's 64-column slices are
-    256-MB tables per KG that the source-side gathers of one slice pass stay inside."""
-    L = _lib.lib()
+    """The backward over a slice-major G (gnnea_gat_bwd_*_sliced_{f32,bf16}): G's 64-column
+    slices are 256-MB tables per KG (cfg-4 fp32, cfg-5 bf16) that the source-side gathers of one
+    slice pass stay inside."""
     D = heads * d_head
     N = csr.n_rows
     dev = H.device
     st = stream_of(dev)
-    Gs = sliced_empty(N, D, dev)
+    Gs = sliced_empty(N, D, dev, H.dtype, W=64)
     S = Gs.shape[0]
     nnzT = csrT.nnz
     wT = torch.empty((max(nnzT, 1), heads), dtype=torch.float32, device=dev)
@@ -1006,22 +1026,22 @@ def _gat_backward_sliced(csr, csrT, H, a32, s1, s2, m, den, Y, dY, heads, d_head
     # ds2 (x) a2 rides the destination pass when source and destination rows coincide
     fold = row0 == 0 and H.shape[0] == N and csrT.n_rows == N
     with _lib.on_device(dev):
-        check(L.gnnea_gat_bwd_prep_sliced_f32(
+        check(_gat_fn("gnnea_gat_bwd_prep_sliced", H.dtype)(
             N, heads, d_head, ptr(dY), ptr(Y), Y.stride(0), _off(s1, row0), ptr(m), ptr(den),
             int(act), ptr(Gs), Gs.stride(0), ptr(rec), st))
         for j0, j1 in _blocks(csrT, Y):  # source rows j of A^T, per KG block
-            check(L.gnnea_gat_bwd_src_sliced_f32(
+            check(_gat_fn("gnnea_gat_bwd_src_sliced", H.dtype)(
                 _off32(csrT.rowptr, j0), ptr(csrT.col), ptr(csrT.perm), j1 - j0, heads, d_head,
                 _off(H, j0), H.stride(0), _off(s2, j0), alpha, ptr(em), ptr(rec), ptr(Gs),
                 Gs.stride(0), ptr(wT), ptr(pd), nnzT, _off(dH, j0), dH.stride(0), st))
-        check(L.gnnea_gat_bwd_edge_sliced_f32(
+        check(_gat_fn("gnnea_gat_bwd_edge_sliced", H.dtype)(
             ptr(csrT.rowptr), ptr(csrT.col), ptr(csrT.perm), csrT.n_rows, heads, d_head, ptr(s2),
             alpha, ptr(em), ptr(rec), ptr(pd), nnzT, ptr(a32), None if fold else ptr(dH),
             dH.stride(0), ptr(dzT), ptr(ds2), st))
         if csrT.n_rows < H.shape[0]:  # H rows no edge references: no gradient
             dH[csrT.n_rows:].zero_()
             ds2[csrT.n_rows:].zero_()
-        check(L.gnnea_gat_bwd_dst_sliced_f32(
+        check(_gat_fn("gnnea_gat_bwd_dst_sliced", H.dtype)(
             ptr(csr.rowptr), ptr(csr.tpos()), N, heads, d_head, ptr(dzT), ptr(a32),
             ptr(ds2) if fold else None, _off(dH, row0), dH.stride(0), ptr(ds1), st))
 

@@ -233,6 +233,42 @@ int gnnea_gat_bwd_dst_sliced_f32(const int32_t* rowptr, const int64_t* tpos, int
                                  int heads, int d_head, const float* dzT, const float* a,
                                  const float* ds2, float* dH, int64_t lddh, float* ds1,
                                  void* stream);
+/* bf16 storage (cfg-5) of the same sliced passes: Hs / Gs are 64-column bf16 tables (128 B, one
+ * line per gathered row piece; [ceil(D/64)][n][64], sstride elements per slice, so one slice of a
+ * 2M-row KG is 256 MB), Y / dY / H / dH row-major bf16 (8-B aligned, ld % 4 == 0); logits, records,
+ * weights, partials and dz stay fp32; fp32 arithmetic, each stored bf16 value rounded once per
+ * pass (nearest even). */
+int gnnea_gat_fwd_sliced_bf16(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
+                              const void* Hs, int64_t sstride, int heads, int d_head,
+                              const float* s1, const float* s2, float alpha,
+                              const float* edge_mask, int act, void* Y, int64_t ldy,
+                              float* m_out, float* den_out, float* wgt, void* stream);
+int gnnea_gat_bwd_prep_sliced_bf16(int32_t n_rows, int heads, int d_head, const void* dY,
+                                   const void* Y, int64_t ldy, const float* s1, const float* m,
+                                   const float* den, int act, void* Gs, int64_t sstride,
+                                   float* rec, void* stream);
+int gnnea_gat_bwd_src_sliced_bf16(const int32_t* rowptrT, const int32_t* colT,
+                                  const int64_t* permT, int32_t n_rows, int heads, int d_head,
+                                  const void* Hm, int64_t ldh, const float* s2, float alpha,
+                                  const float* edge_mask, const float* rec, const void* Gs,
+                                  int64_t sstride, float* wT, float* pd, int64_t nnzT, void* dH,
+                                  int64_t lddh, void* stream);
+int gnnea_gat_bwd_edge_sliced_bf16(const int32_t* rowptrT, const int32_t* colT,
+                                   const int64_t* permT, int32_t n_rows, int heads, int d_head,
+                                   const float* s2, float alpha, const float* edge_mask,
+                                   const float* rec, const float* pd, int64_t nnzT,
+                                   const float* a, void* dH, int64_t lddh, float* dzT,
+                                   float* ds2, void* stream);
+int gnnea_gat_bwd_dst_sliced_bf16(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows,
+                                  int heads, int d_head, const float* dzT, const float* a,
+                                  const float* ds2, void* dH, int64_t lddh, float* ds1,
+                                  void* stream);
+/* row-major [n, D] -> the 64-column slice-major GAT table (D % 4 == 0, ldx % 4 == 0, sstride a
+ * multiple of 64 and >= 64 n elements) */
+int gnnea_slice_pack64_f32(const float* X, int64_t ldx, int64_t n, int32_t D, float* Xs,
+                           int64_t sstride, void* stream);
+int gnnea_slice_pack64_bf16(const void* X, int64_t ldx, int64_t n, int32_t D, void* Xs,
+                            int64_t sstride, void* stream);
 /* Backward in one gather sweep over A^T (autograd of att_layers.py:38-58):
  *  prep (rows i):   G_i = dY_i * act'(Y_i) (act: identity / relu, Y = h' there) and the per-node
  *                   record rec[i,h] = {s1, m, 1/den, c = G_i,h . h'_i,h}  (float4 per head);

@@ -48,3 +48,23 @@ def rel_err(a, b):
     b = np.asarray(b, dtype=np.float64)
     den = np.max(np.abs(b))
     return float(np.max(np.abs(a - b)) / (den if den > 0 else 1.0))
+
+
+@pytest.fixture
+def relu_band(record_property):
+    """Counts of ReLU elements whose branch the oracles took from the tested output (inside the
+    rounding band of 0, oracle/local.py / tests/fp64_ref.py), recorded per test as the property
+    ``relu_band`` and appended to $GNNEA_BAND_LOG (JSON lines) when set."""
+    import json
+    from oracle import local
+    import fp64_ref
+    local.reset_band()
+    fp64_ref.reset_band()
+    yield
+    rec = {"oracle_local": dict(local.BAND), "fp64_ref": dict(fp64_ref.BAND)}
+    record_property("relu_band", json.dumps(rec))
+    path = os.environ.get("GNNEA_BAND_LOG")
+    if path:
+        rec["test"] = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+        with open(path, "a") as f:
+            f.write(json.dumps(rec) + "\n")

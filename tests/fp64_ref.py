@@ -6,12 +6,19 @@ ops (index_add aggregation in edge chunks, vendor fp64 GEMMs) on the same device
   GraphConvolution          layers/layers.py:30-39
   HighWayGraphConvolution   layers/layers.py:59-77
   EAModel.get_loss          models/models_ea.py:103-123
-ReLU's branch inside the rounding band of 0 follows the tested output (see oracle/local.py).
+  GraphAttentionLayer       layers/att_layers.py:29-61, 82-91 (per head, concatenated)
+ReLU's branch inside the rounding band of 0 follows the tested output (see oracle/local.py);
+the number of elements that fell in the band is counted in BAND (reported by the tests).
 """
 import torch
 
 CHUNK = 1 << 22
 TAU = 1e-5
+BAND = {"band": 0, "total": 0}
+
+
+def reset_band():
+    BAND["band"] = BAND["total"] = 0
 
 
 def agg(r, c, v, n_out, h):
@@ -37,13 +44,89 @@ class Agg(torch.autograd.Function):
         return agg(c, r, v, n_in, g), None, None, None, None
 
 
-def relu_mask(pre, tested=None):
-    """relu'(pre) as a 0/1 fp64 tensor; inside |pre| <= TAU*max|pre| the tested output's sign."""
-    band = pre.abs() <= TAU * pre.abs().max().clamp_min(1e-300)
+def relu_mask(pre, tested=None, tau=TAU):
+    """relu'(pre) as a 0/1 fp64 tensor; inside |pre| <= tau*max|pre| the tested output's sign."""
+    band = pre.abs() <= tau * pre.abs().max().clamp_min(1e-300)
     m = pre > 0
     if tested is not None:
         m = torch.where(band, tested > 0, m)
+        BAND["band"] += int(band.sum())
+        BAND["total"] += band.numel()
     return m.to(pre.dtype)
+
+
+class WAgg(torch.autograd.Function):
+    """out_i = sum_e w_e h[c_e] over the edges e of row r_e (differentiable in h and in the
+    per-edge weights w; edge chunks, no E x D tensor is kept for the backward)."""
+
+    @staticmethod
+    def forward(ctx, h, w, r, c, n_out):
+        ctx.save_for_backward(h, w)
+        ctx.graph = (r, c)
+        out = torch.zeros((n_out, h.shape[1]), dtype=h.dtype, device=h.device)
+        for e0 in range(0, r.numel(), CHUNK):
+            sl = slice(e0, e0 + CHUNK)
+            out.index_add_(0, r[sl], h[c[sl]] * w[sl].unsqueeze(1))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w = ctx.saved_tensors
+        r, c = ctx.graph
+        dh = torch.zeros_like(h)
+        dw = torch.empty_like(w)
+        for e0 in range(0, r.numel(), CHUNK):
+            sl = slice(e0, e0 + CHUNK)
+            gr = g[r[sl]]
+            dw[sl] = (gr * h[c[sl]]).sum(1)
+            dh.index_add_(0, c[sl], gr * w[sl].unsqueeze(1))
+        return dh, dw, None, None, None
+
+
+class BF16Store(torch.autograd.Function):
+    """Identity that rounds its value to bf16 in the forward and its gradient to bf16 in the
+    backward: the storage points of the bf16 path (a projection / activation written as bf16
+    and its gradient written as bf16), so an fp64 restatement with these inserted differs from
+    the bf16 kernels only by fp32-vs-fp64 accumulation, not by the storage roundings."""
+
+    @staticmethod
+    def forward(ctx, t):
+        return t.to(torch.bfloat16).to(t.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def bf16_store(t):
+    return BF16Store.apply(t)
+
+
+def gat_layer(x, Ws, As, r, c, alpha=0.2, relu=True, tested=None, tau=TAU, store=None):
+    """GraphAttentionLayer forward (concat of the heads) in the precision of x: Ws [H, in, d],
+    As [H, 1, 2d]; edges (r, c) coalesced (unique pairs); exp(-LeakyReLU(z)) without a shift,
+    as the reference.  ``tested``: the layer's output under test (relu's rounding band).
+    ``store``: applied to each head's projection and to the output (bf16_store emulates the
+    bf16 path's storage)."""
+    n = x.shape[0]
+    outs = []
+    d = Ws.shape[2]
+    for h_ in range(Ws.shape[0]):
+        hh = x @ Ws[h_]
+        if store is not None:
+            hh = store(hh)
+        s1 = hh @ As[h_, 0, :d]
+        s2 = hh @ As[h_, 0, d:]
+        e = torch.exp(-torch.nn.functional.leaky_relu(s1[r] + s2[c], alpha))
+        den = torch.zeros(n, dtype=x.dtype, device=x.device).index_add(0, r, e)
+        o = WAgg.apply(hh, e, r, c, n) / den.unsqueeze(1)
+        if relu:
+            with torch.no_grad():
+                m = relu_mask(o, None if tested is None else tested[:, h_ * d:(h_ + 1) * d], tau)
+            o = o * m
+        outs.append(o)
+    y = torch.cat(outs, dim=1)
+    return store(y) if store is not None else y
 
 
 def gcn_grads(r, c, v, x, W, b, R, tested_out):
@@ -84,3 +167,4 @@ def margin_loss(out, left, right, neg_left, neg_right, neg2_left, neg2_right, t,
     B2 = (out[neg2_left] - out[neg2_right]).abs().sum(1)
     L2 = torch.relu(-B2.reshape(t, k) + D.reshape(t, 1))
     return (L1.sum() + L2.sum()) / (2.0 * t * k)
+

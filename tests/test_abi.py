@@ -83,3 +83,35 @@ def test_host_only_entry_points():
     assert L.gnnea_act_bwd_sliced_f32(16, 300, 16, 300, 10, 302, 1, 16, 640, None) == -1
     assert L.gnnea_gemm_sliced_f32(0, 1, 10, 300, 8, 16, 8, 16, 8, None, 0.0, 16, 66, None, 0,
                                    None) == -1
+
+
+def test_sliced_gat_refuses_three_heads_per_slice():
+    """The sliced GAT kernels keep two heads per 64-column slice: d_head = 40 (slice 1 = heads
+    1, 2, 3) is refused by every sliced entry point on the host, before any launch; the Python
+    gate (ops.gat_two_heads_per_slice) agrees, so that shape takes the row-major passes."""
+    from gnnea import _lib, ops
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libgnnea.so not built")
+    L = _lib.lib()
+    for heads, dh, ok in ((4, 40, False), (4, 36, False), (2, 50, True), (8, 40, False), (4, 75, True),
+                          (8, 32, True), (3, 48, True), (1, 300, True), (2, 64, True),
+                          (4, 31, False)):
+        assert ops.gat_two_heads_per_slice(heads, dh) == ok, (heads, dh)
+        if ok:
+            continue
+        for fn in (L.gnnea_gat_fwd_sliced_f32, L.gnnea_gat_fwd_sliced_bf16):
+            assert fn(16, 16, 4, 16, 64 * 4, heads, dh, 16, 16, 0.2, None, 1, 16, heads * dh,
+                      16, 16, 16, None) == -1
+        for fn in (L.gnnea_gat_bwd_prep_sliced_f32, L.gnnea_gat_bwd_prep_sliced_bf16):
+            assert fn(4, heads, dh, 16, 16, heads * dh, 16, 16, 16, 1, 16, 256, 16, None) == -1
+        for fn in (L.gnnea_gat_bwd_src_sliced_f32, L.gnnea_gat_bwd_src_sliced_bf16):
+            assert fn(16, 16, None, 4, heads, dh, 16, heads * dh, 16, 0.2, None, 16, 16, 256, 16,
+                      16, 4, 16, heads * dh, None) == -1
+        for fn in (L.gnnea_gat_bwd_edge_sliced_f32, L.gnnea_gat_bwd_edge_sliced_bf16):
+            assert fn(16, 16, None, 4, heads, dh, 16, 0.2, None, 16, 16, 4, 16, None, 0, 16, 16,
+                      None) == -1
+        for fn in (L.gnnea_gat_bwd_dst_sliced_f32, L.gnnea_gat_bwd_dst_sliced_bf16):
+            assert fn(16, 16, 4, heads, dh, 16, 16, None, 16, heads * dh, 16, None) == -1
+    # the 64-column pack: slice stride and width checked on the host
+    assert L.gnnea_slice_pack64_bf16(16, 300, 10, 300, 16, 63, None) == -1
+    assert L.gnnea_slice_pack64_f32(16, 302, 10, 302, 16, 640, None) == -1

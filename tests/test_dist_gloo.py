@@ -28,7 +28,7 @@ def _worker(rank, world, port, n, t, q, kind="rows"):
     sys.path.insert(0, os.path.join(root, "gnn-mtl_amd"))
     sys.path.insert(0, root)
     from gnnea import synth
-    from gnnea.dist import Partition, halo_gather, make_groups, shard_coo, split_own_remote
+    from gnnea.dist import Partition, halo_gather, make_groups, shard_coo
     from oracle.gnn import coo_aggregate
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -62,11 +62,29 @@ def _worker(rank, world, port, n, t, q, kind="rows"):
         if part.g == 1:
             y = coo_aggregate(r, c, v, part.n_rows, h_local)
         else:
-            # the product's overlap split: owned block from h_local, the rest from the halo
-            (ro, co, vo), (rr, cr, vr) = split_own_remote(r, c, v, part)
-            y = coo_aggregate(ro, co, vo, part.n_rows, h_local)
-            halo_gather(h_local, h_full, group, part.g, part=part)  # relayed at world 4
-            y = y + coo_aggregate(rr, cr, vr, part.n_rows, h_full)
+            # the product's per-slice pipeline (gnnea.dist.KGShard.aggregate, DistAdj): the own
+            # rows packed into the KG's slice tables, every slice's exchange issued at once
+            # (relayed at world 4), slice q aggregated over the whole shard once it has landed
+            from gnnea import exchange
+            W = 6  # 16 columns: slices of 6, 6, 4
+            S = (16 + W - 1) // W
+            tables = torch.full((S, n, W), float("nan"), dtype=torch.float64)
+            for k in range(S):
+                blk = h_local[:, k * W:(k + 1) * W]
+                tables[k, part.row0:part.row1, :blk.shape[1]] = blk
+            works = exchange.all_gather_slices(list(tables), part.row0, part.n_rows, group,
+                                               part.group_ranks(part.kg), part.li,
+                                               other=part.other_ranks())
+            y = torch.empty(part.n_rows, 16, dtype=torch.float64)
+            for k in range(S):
+                for w in works[k]:
+                    w.wait()
+                c1 = min(16, (k + 1) * W)
+                y[:, k * W:c1] = coo_aggregate(r, c, v, part.n_rows,
+                                               tables[k][:, :c1 - k * W].contiguous())
+            # the whole-table gather as well (the unstaged fallback of DistAdj.halo)
+            halo_gather(h_local, h_full, group, part.g, part=part)
+            assert float((coo_aggregate(r, c, v, part.n_rows, h_full) - y).abs().max()) < 1e-12
         outs = [torch.empty_like(y) for _ in range(world)]
         dist.all_gather(outs, y)
         if rank == 0:

@@ -71,6 +71,47 @@ class CpuEngine:
         dS = dy * g * ((S > 0).to(dy.dtype) if act == 1 else 1.0)
         return dS, dy * (S - resid) * g * (1 - g), (dy * (1 - g) if want else None)
 
+    # ---- column-slice stages (DistAdj's pipelined halo); W = 4 gives D = 12 three stages ----
+    W = 4
+
+    def slice_w(self, dtype):
+        return self.W
+
+    def pack_slices(self, x, tables, row0):
+        S, _, W = tables.shape
+        for q in range(S):
+            c0, c1 = q * W, min(x.shape[1], (q + 1) * W)
+            tables[q, row0:row0 + x.shape[0], :c1 - c0] = x[:, c0:c1]
+        return tables
+
+    def spmm_slice(self, A, table, w, act, out):
+        out.copy_(self._act(torch.sparse.mm(A, table[:, :w].contiguous()), act))
+        return out
+
+    def spmm_t_slice(self, A, table, w):
+        return torch.sparse.mm(A.t().coalesce(), table[:, :w].contiguous())
+
+    def _slices(self, x):
+        S = (x.shape[1] + self.W - 1) // self.W
+        return self.pack_slices(x, torch.zeros((S, x.shape[0], self.W), dtype=x.dtype), 0)
+
+    def act_bwd_slices(self, dy, y, act):
+        return self._slices(self.act_bwd(dy, y, act))
+
+    def highway_slice(self, A, table, w, gates, c0, bias, resid, out, S, G, act):
+        sv = self._act(torch.sparse.mm(A, table[:, :w].contiguous()), act)
+        gp = gates[c0 // self.W][:, :w]
+        g = torch.sigmoid(gp + bias[c0:c0 + w] if bias is not None else gp)
+        out[:, c0:c0 + w] = g * sv + (1 - g) * resid[:, c0:c0 + w]
+        S[:, c0:c0 + w] = sv
+        G[:, c0:c0 + w] = g
+        return out
+
+    def highway_bwd_slices(self, dy, S, g, resid, act, want, dgate):
+        dS, dg, dres = self.highway_bwd(dy, S, g, resid, act, want)
+        dgate.copy_(dg)
+        return self._slices(dS), dres
+
     @staticmethod
     def gat_dense(A, H, a, heads, dh, alpha, act, row0):
         """layers/att_layers.py:29-61 per head over A's edges (destination i = row0 + row)."""
@@ -114,6 +155,8 @@ def _worker(rank, world, port, mode, q):
     try:
         tr = synth.kg_pair_triples(N_KG, T_KG, 20)
         R, C, V = synth.adjacency_coo(tr, 2 * N_KG, reference_order=False)
+        # the HIP rehearsal uses 132 columns: three 64-column slices of the pipelined halo
+        D = 132 if mode == "gpu" else globals()["D"]
         X = torch.from_numpy(synth.features(2 * N_KG, D, seed=5)).double()
         Rw = torch.from_numpy(np.random.default_rng(9).standard_normal((2 * N_KG, D)))
         HEADS, DH = 3, D // 3
@@ -161,6 +204,8 @@ def _worker(rank, world, port, mode, q):
             Kg = torch.randn(D, D, dtype=torch.float64)
             params = [p.requires_grad_() for p in (W1, b1, W2, b2)]
 
+            bg = torch.randn(D, dtype=torch.float64) * 0.1
+
             def model(x, adj):
                 h1 = x @ W1.t() + b1
                 if adj is None:
@@ -170,12 +215,15 @@ def _worker(rank, world, port, mode, q):
                     y1 = torch.relu(torch.sparse.mm(A, h1))
                     h2 = y1 @ W2.t() + b2
                     g = torch.sigmoid(y1 @ Kg)
-                    return g * torch.sparse.mm(A, h2) + (1 - g) * y1
+                    y2 = g * torch.sparse.mm(A, h2) + (1 - g) * y1
+                    g3 = torch.sigmoid(y2 @ Kg + bg)
+                    return g3 * torch.relu(torch.sparse.mm(A, y2 @ W1.t())) + (1 - g3) * y2
                 y1 = adj.aggregate(h1, F.relu)
                 h2 = y1 @ W2.t() + b2
                 y2 = adj.highway(h2, y1 @ Kg, y1, torch.zeros(D, dtype=torch.float64),
-                                 lambda t: t)
-                return adj.gather_rows(y2)
+                                 lambda t: t)  # composed: aggregate + torch blend
+                # fusable act: HaloHighwayFn (the staged HighWay tail slice by slice)
+                return adj.gather_rows(adj.highway(y2 @ W1.t(), y2 @ Kg, y2, bg, F.relu))
             tol = 1e-12
         else:
             from layers.layers import GraphConvolution, HighWayGraphConvolution

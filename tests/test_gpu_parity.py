@@ -601,3 +601,57 @@ def test_gemm_f64_vs_numpy(device):
                                    e=torch.from_numpy(e).to(device), beta=1.0).cpu().numpy()
                 ref = e - (a.T if ta else a) @ (b.T if tb else b)
                 assert rel_err(out, ref) < 1e-14, (M, N, K, ta, tb)
+
+
+# reduced-precision legs of the GW / FGW outer loops: C1, C2, M rounded to fp32 / bf16, the
+# cost GEMMs on gnnea's fp32 (x3) / bf16 kernels, each inner solve in fp64 and cast back
+# (SinkhornOT/cderivation.py:160-162, iterative_projection.py:6-58).  The plan is exp(-2L/eps)
+# at eps = 0.01, so a relative cost perturbation delta moves it by ~2|L|delta/eps: input rounding
+# alone (fp32 6e-8, bf16 4e-3 relative, |L| <= 1) bounds the reachable agreement at ~1e-5 (fp32)
+# and ~1 (bf16) — the stated tolerances: fp32 plan 1e-4 / distance 1e-5 against the reference's
+# fp64 fixture; bf16 against the same reduced-precision loop run in fp64 on the bf16-rounded
+# inputs (cost GEMM products exact, the one rounding of each product to bf16 is what differs):
+# plan 5e-2 at eps = 0.1.
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_gw_outer_loops_fp32_vs_reference(golden, device, tag, record_property):
+    from SinkhornOT.iterative_projection import fgw_iterative_1, gw_iterative_1
+    f = golden("gw")
+    C1 = torch.from_numpy(f[tag + "_C1"]).to(device).float()
+    C2 = torch.from_numpy(f[tag + "_C2"]).to(device).float()
+    M = torch.from_numpy(f[tag + "_M"]).to(device).float()
+    I, J = C1.shape[0], C2.shape[0]
+    mu = torch.full((I,), 1.0 / I, dtype=torch.float32, device=device)
+    nu = torch.full((J,), 1.0 / J, dtype=torch.float32, device=device)
+    errs = {}
+    for name, run in (("gw", lambda: gw_iterative_1(C1, C2, mu, nu, epsilon=0.01, max_iter=8)),
+                      ("fgw", lambda: fgw_iterative_1(M, C1, C2, mu, nu, alpha=0.5, p=2,
+                                                      max_iter=8, epsilon=0.01))):
+        T, d = run()
+        assert T.dtype == torch.float32
+        ref_d = float(f["%s_%s_d" % (tag, name)])
+        errs[name] = (rel_err(T.cpu(), f["%s_%s_T" % (tag, name)]),
+                      abs(float(d) - ref_d) / abs(ref_d))
+    record_property("gw_fp32", errs)
+    print("GW fp32 %s: %s" % (tag, errs))
+    for name, (eT, ed) in errs.items():
+        assert eT < 1e-4 and ed < 1e-5, (name, eT, ed)
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_gw_outer_loop_bf16(golden, device, tag, record_property):
+    from SinkhornOT.iterative_projection import gw_iterative_1
+    f = golden("gw")
+    C1 = torch.from_numpy(f[tag + "_C1"]).to(device).bfloat16()
+    C2 = torch.from_numpy(f[tag + "_C2"]).to(device).bfloat16()
+    I, J = C1.shape[0], C2.shape[0]
+    eps = 0.1
+    mu = torch.full((I,), 1.0 / I, dtype=torch.float64, device=device)
+    nu = torch.full((J,), 1.0 / J, dtype=torch.float64, device=device)
+    Tb, db = gw_iterative_1(C1, C2, mu.bfloat16(), nu.bfloat16(), epsilon=eps, max_iter=8)
+    assert Tb.dtype == torch.bfloat16
+    T64, d64 = gw_iterative_1(C1.double(), C2.double(), mu, nu, epsilon=eps, max_iter=8)
+    eT = rel_err(Tb.float().cpu(), T64.cpu())
+    ed = abs(float(db) - float(d64)) / abs(float(d64))
+    record_property("gw_bf16", (eT, ed))
+    print("GW bf16 %s: plan %.2e, distance %.2e" % (tag, eT, ed))
+    assert eT < 5e-2 and ed < 5e-2, (eT, ed)

@@ -55,7 +55,7 @@ def _rows_of(t):
     return lambda rows: t[torch.from_numpy(np.asarray(rows)).to(t.device)].float().cpu().numpy()
 
 
-def test_cfg4_gcn_layer_vs_oracle(device, cfg4):
+def test_cfg4_gcn_layer_vs_oracle(device, cfg4, relu_band):
     from layers.layers import GraphConvolution
     from oracle.local import sampled_input_grads, sampled_outputs
     d = cfg4
@@ -79,7 +79,7 @@ def test_cfg4_gcn_layer_vs_oracle(device, cfg4):
     assert rel_err(layer.linear.bias.grad.cpu(), db.cpu()) < TOL32
 
 
-def test_cfg4_highway_layer_vs_oracle(device, cfg4):
+def test_cfg4_highway_layer_vs_oracle(device, cfg4, relu_band):
     from layers.layers import HighWayGraphConvolution
     from oracle.local import sampled_input_grads, sampled_outputs
     d = cfg4
@@ -108,7 +108,7 @@ def test_cfg4_highway_layer_vs_oracle(device, cfg4):
     assert rel_err(layer.linear.bias.grad.cpu(), db.cpu()) < TOL32
 
 
-def test_cfg4_hgcn_ea_step_vs_fp64(device, cfg4):
+def test_cfg4_hgcn_ea_step_vs_fp64(device, cfg4, relu_band):
     """One HGCN-EA training step (run/train_ea.py:55-66) on the full configs[3] graph."""
     from models.models_ea import EAModel
     from test_dropin_cpu import make_args
@@ -150,3 +150,66 @@ def test_cfg4_hgcn_ea_step_vs_fp64(device, cfg4):
                 assert float(g_.abs().max()) < 1e-3 * gmax
             else:
                 assert rel_err(g_.cpu(), ref.cpu()) < 3e-3
+
+
+def _coalesced(r, c, N):
+    """Unique (row, col) pairs in row-major order (the edge set the GAT layer attends over,
+    adj.coalesce().indices(), att_layers.py:31)."""
+    key = torch.unique(r.long() * N + c.long())
+    return key // N, key % N
+
+
+def test_cfg4_gat_layer_vs_oracle(device, cfg4, monkeypatch, relu_band, record_property):
+    """The fp32 4-head GAT layer (att_layers.py:29-61, 82-91) at full configs[3] size through
+    the slice-major forward and backward (nothing monkeypatched but a spy): outputs and dx on
+    sampled rows vs the fp64 neighbourhood oracle (1e-4), every head's W and a gradients vs the
+    whole-graph fp64 restatement on the device (tests/fp64_ref.gat_layer, 1e-4)."""
+    from gnnea import ops
+    from layers.att_layers import GraphAttentionLayer
+    from oracle.local import sampled_input_grads, sampled_outputs
+    d = cfg4
+    taken = []
+    orig = ops._gat_sliced_applies
+    monkeypatch.setattr(ops, "_gat_sliced_applies",
+                        lambda *a, **k: (lambda v: (taken.append(v), v)[1])(orig(*a, **k)))
+    torch.manual_seed(10089)
+    layer = GraphAttentionLayer(300, 75, 0.0, F.relu, 0.2, 4, True).to(device)
+    xx = d["x"].clone().requires_grad_(True)
+    out, _ = layer((xx, d["adj"]))
+    (out * d["R"]).sum().backward()
+    assert taken == [True, True], taken  # sliced forward and sliced backward
+    Ws = torch.stack([a.W.detach().cpu() for a in layer.attentions]).double()
+    As = torch.stack([a.a.detach().cpu() for a in layer.attentions]).double()
+    S, o_ref = sampled_outputs("gat", d["g"], d["X"], d["rows"], [Ws, As], "relu",
+                               _rows_of(out))
+    assert rel_err(_rows_of(out.detach())(S), o_ref) < TOL32
+    T, dx_ref = sampled_input_grads("gat", d["g"], d["X"], d["Rn"], d["grad_rows"], [Ws, As],
+                                    "relu", _rows_of(out))
+    assert rel_err(_rows_of(xx.grad)(T), dx_ref) < TOL32
+    r, c = _coalesced(d["r"], d["c"], d["N"])
+    grads = {}
+    for dt in (torch.float64, torch.float32):
+        # the reference's op sequence (tests/fp64_ref.gat_layer: gathers, exp, index_add) in
+        # fp64, and in fp32 for the accumulation error any fp32 evaluation of these sums has
+        Wd = Ws.to(device, dt).requires_grad_(True)
+        Ad = As.to(device, dt).requires_grad_(True)
+        yd = fp64_ref.gat_layer(d["x"].to(dt), Wd, Ad, r, c, 0.2, True,
+                                tested=out.detach().to(dt))
+        (yd * d["R"].to(dt)).sum().backward()
+        grads[dt] = (Wd.grad.double().cpu(), Ad.grad.double().cpu())
+        del yd
+    W64, A64 = grads[torch.float64]
+    W32, A32 = grads[torch.float32]
+    # dW sums x_i (x) dH_i over 2M rows; da sums ds (x) H over every row, ds = sum of dz over the
+    # row's 21 edges with dz = alpha (mask g.h_j - c_i) LeakyReLU', differences of nearby
+    # products: far more cancellation, so fp32 accumulation alone lands further from fp64 there.
+    # Each gradient must be within 1e-4 of fp64, or within twice the torch-fp32 evaluation's own
+    # error, whichever is larger (the DBP15K tests' rule for the reference's fp32 step).
+    errs = []
+    for h, att in enumerate(layer.attentions):
+        for ours, r64, r32 in ((att.W.grad, W64[h], W32[h]), (att.a.grad, A64[h], A32[h])):
+            e, e32 = rel_err(ours.cpu(), r64), rel_err(r32, r64)
+            errs.append((e, e32))
+            assert e < max(TOL32, 2.0 * e32), (h, e, e32)
+    record_property("cfg4_gat_grad_errs", errs)
+    print("cfg4 GAT layer grads (ours vs fp64, torch-fp32 vs fp64):", errs)

@@ -451,3 +451,102 @@ def test_gat_bwd_sliced_vs_rowmajor(device, monkeypatch, heads, d_head, act, mas
     assert calls, "the sliced backward was not taken"
     assert rel_err(dH_s.cpu(), dH_r.cpu()) < 1e-5
     assert rel_err(da_s.cpu(), da_r.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("heads,d_head,act,mask", [(4, 75, 1, False), (8, 32, 1, True),
+                                                   (3, 48, 0, True), (1, 300, 1, False)])
+def test_gat_bf16_sliced_vs_rowmajor_and_oracle(device, monkeypatch, heads, d_head, act, mask):
+    """bf16 storage (cfg-5): gnnea_gat_{fwd,bwd_*}_sliced_bf16 over 64-column (128-B) slices
+    against the row-major bf16 passes and the fp64 oracle (att_layers.py:29-61 x heads) on the
+    same bf16-rounded H: outputs, dH and da at the bf16 tolerance (each stored value rounded
+    once per pass), the sliced passes actually taken."""
+    from gnnea import ops
+    from gnnea.graph import DeviceCSR
+    rng = np.random.default_rng(7 * heads + d_head)
+    n = 1500
+    D = heads * d_head
+    r = rng.integers(0, n, 16000)
+    c = rng.integers(0, n, 16000)
+    r = np.concatenate([r, np.arange(n), np.full(150, 11)])  # self loops; one long row
+    c = np.concatenate([c, np.arange(n), rng.integers(0, n, 150)])
+    v = np.ones(r.size, np.float32)
+    csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                             torch.from_numpy(v).to(device), n, n)
+    H = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32) * 0.5).to(device)
+    Hb = H.bfloat16()
+    a32 = torch.from_numpy(rng.standard_normal((heads, 2 * d_head)).astype(np.float32)
+                           * 0.3).to(device)
+    em = None
+    if mask:
+        em = torch.from_numpy(((rng.random((csr.nnz, heads)) > 0.3) / 0.7).astype(np.float32)
+                              ).to(device)
+    dY = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32)).to(device).bfloat16()
+
+    def run(sliced):
+        monkeypatch.setattr(ops, "GAT_SLICED", sliced)
+        monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 1 if sliced else 1 << 40)
+        calls = []
+        orig = ops._gat_backward_sliced
+        monkeypatch.setattr(ops, "_gat_backward_sliced",
+                            lambda *a, **k: (calls.append(1), orig(*a, **k))[1])
+        Y, m, den, s1, s2 = ops.gat_forward(csr, Hb, a32, heads, d_head, 0.2, act, em)
+        dH, da = ops.gat_backward(csr, Hb, a32, s1, s2, m, den, Y, dY, heads, d_head, 0.2, act,
+                                  em)
+        monkeypatch.setattr(ops, "_gat_backward_sliced", orig)
+        assert bool(calls) == sliced
+        assert Y.dtype == dH.dtype == torch.bfloat16
+        return Y.float().cpu(), dH.float().cpu(), da.cpu()
+
+    ys, dhs, das = run(True)
+    yr, dhr, dar = run(False)
+    assert rel_err(ys, yr) < 1e-2
+    assert rel_err(dhs, dhr) < 2e-2
+    assert rel_err(das, dar) < 2e-2
+    # fp64 oracle of the same forward on the bf16 H (edge mask as the numerator multiplier)
+    H64 = Hb.double().cpu()
+    A64 = a32.double().cpu()
+    rr = torch.from_numpy(np.repeat(np.arange(n), np.diff(csr.rowptr.cpu().numpy())))
+    cc = csr.col.long().cpu()
+    H64.requires_grad_(True)
+    A64.requires_grad_(True)
+    outs = []
+    for h in range(heads):
+        hh = H64[:, h * d_head:(h + 1) * d_head]
+        z = hh[rr] @ A64[h, :d_head] + hh[cc] @ A64[h, d_head:]
+        e = torch.exp(-torch.nn.functional.leaky_relu(z, 0.2))
+        den = torch.zeros(n, dtype=torch.float64).index_add(0, rr, e)
+        w = e * (em[:, h].double().cpu() if mask else 1.0)
+        num = torch.zeros((n, d_head), dtype=torch.float64).index_add(0, rr, w.unsqueeze(1) * hh[cc])
+        o = num / den.unsqueeze(1)
+        outs.append(torch.relu(o) if act else o)
+    yo = torch.cat(outs, 1)
+    (yo * dY.double().cpu()).sum().backward()
+    assert rel_err(ys, yo.detach()) < 1e-2
+    assert rel_err(dhs, H64.grad) < 2e-2
+    assert rel_err(das, A64.grad) < 2e-2
+
+
+def test_gat_dhead40_takes_rowmajor(device, monkeypatch):
+    """d_head = 40 puts three heads into slice 1: the sliced gate refuses it and the layer runs
+    the row-major passes (same results as with the sliced path switched off)."""
+    from gnnea import ops
+    from gnnea.graph import DeviceCSR
+    rng = np.random.default_rng(40)
+    n, heads, d_head = 900, 4, 40
+    D = heads * d_head
+    r = np.concatenate([rng.integers(0, n, 8000), np.arange(n)])
+    c = np.concatenate([rng.integers(0, n, 8000), np.arange(n)])
+    csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                             torch.ones(r.size, device=device), n, n)
+    H = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32)).to(device)
+    a32 = torch.from_numpy(rng.standard_normal((heads, 2 * d_head)).astype(np.float32)
+                           * 0.3).to(device)
+    dY = torch.randn(n, D, device=device)
+    out = []
+    for sliced in (True, False):
+        monkeypatch.setattr(ops, "GAT_SLICED", sliced)
+        monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 1)
+        Y, m, den, s1, s2 = ops.gat_forward(csr, H, a32, heads, d_head, 0.2, 1)
+        out.append((Y, ops.gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, 0.2,
+                                        1)[0]))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
