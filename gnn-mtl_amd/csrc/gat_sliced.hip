@@ -85,17 +85,16 @@ static bool gat_two_heads_per_slice(int heads, int d_head) {
   return true;
 }
 
-// Lane map of the gather passes over a 64-column slice: every lane loads 16 B of the row piece
-// (E = 4 fp32 / 8 bf16 columns), LPG = 64 / E lanes per piece (fp32 16: 256 B; bf16 8: one
-// 128-B line), NG = 64 / LPG groups per wave each on its own neighbour (fp32 4, bf16 8).  One
-// 16-B load per lane per neighbour for both storage types: 8-B bf16 loads would halve the bytes
-// per load instruction (cfg-5 measured 6.4 ms fwd / 8.7 ms src per KG at 8 B against 3.6 / 4.1
-// for fp32 at cfg-4 on the same gathered bytes).
+// Lane map of the gather passes over a 64-column slice: every lane owns E = 4 columns of the
+// row piece (one 16-B fp32 / 8-B bf16 load per neighbour), LPG = 16 lanes per piece, NG = 4
+// groups per wave each on its own neighbour.  (bf16 with 16-B lanes -- 8 columns, 8 groups of 8
+// -- measured slower at cfg-5: 11.6 vs 8.7 ms for the source pass per KG, 6.5 vs 6.4 forward.)
 template <typename T>
 struct GatLanes {
-  static constexpr int E = 16 / (int)sizeof(T);
+  static constexpr int E = 4;
   static constexpr int LPG = 64 / E;
   static constexpr int NG = 64 / LPG;
+  typedef typename Vec4<T>::raw R;  // one lane's load
 };
 
 // E consecutive columns from c0 of a row-major row (4-column chunks; columns >= D read as 0)
@@ -122,10 +121,11 @@ __device__ __forceinline__ void store_cols(T* row, int c0, int D, const float (&
 template <int ACT, int U, typename TX, typename TY>
 __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, int n_rows, int nbs,
-    int H, int D, int dh, const uint4* __restrict__ Hs, int64_t sstride16,
+    int H, int D, int dh, const typename GatLanes<TX>::R* __restrict__ Hs, int64_t sstrideR,
     const float* __restrict__ wgt, const float* __restrict__ den_in, TY* __restrict__ Y,
     int64_t ldy) {
   constexpr int E = GatLanes<TX>::E, LPG = GatLanes<TX>::LPG, NG = GatLanes<TX>::NG;
+  typedef typename GatLanes<TX>::R RX;
   const int b = blockIdx.x;
   const int s = b / nbs;
   const int row = xcd_remap(b - s * nbs, nbs) * 4 + wave_id();
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
   bool second[E];
 #pragma unroll
   for (int t = 0; t < E; ++t) second[t] = (c0 + t) / dh != h0;
-  const uint4* X = Hs + (int64_t)s * sstride16 + c;
+  const RX* X = Hs + (int64_t)s * sstrideR + c;
   const int beg = rowptr[row], end = rowptr[row + 1];
   float acc[E];
 #pragma unroll
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
       w1 = wgt[(int64_t)(base + lane) * H + h1];
     }
     for (int k = 0; k < cnt; k += NG * U) {
-      uint4 r[U];
+      RX r[U];
       float v0[U], v1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -166,14 +166,14 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
         if (e < cnt && own) {
           r[u] = X[(int64_t)j * LPG];
         } else {
-          r[u] = make_uint4(0u, 0u, 0u, 0u);
+          r[u] = Vec4<TX>::zero();
           v0[u] = v1[u] = 0.f;
         }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        float f[E];
-        unpack16(r[u], f);
+        const float4 fv = Vec4<TX>::get(r[u]);
+        float f[E] = {fv.x, fv.y, fv.z, fv.w};
 #pragma unroll
         for (int t = 0; t < E; ++t) acc[t] = fmaf(second[t] ? v1[u] : v0[u], f[t], acc[t]);
       }
@@ -316,10 +316,11 @@ __global__ __launch_bounds__(256) void k_gat_bwd_w(const int32_t* __restrict__ r
 template <int U, typename T>
 __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
     const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT, int n_rows, int nbs,
-    int H, int D, int dh, const uint4* __restrict__ Gs, int64_t sstride16,
+    int H, int D, int dh, const typename GatLanes<T>::R* __restrict__ Gs, int64_t sstrideR,
     const T* __restrict__ Hm, int64_t ldh, const float* __restrict__ wT,
     T* __restrict__ dH, int64_t lddh, float* __restrict__ pd, int64_t pstride) {
   constexpr int E = GatLanes<T>::E, LPG = GatLanes<T>::LPG, NG = GatLanes<T>::NG;
+  typedef typename GatLanes<T>::R RX;
   const int b = blockIdx.x;
   const int s = b / nbs;
   const int row = xcd_remap(b - s * nbs, nbs) * 4 + wave_id();
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
       hj1[t] = second[t] ? v[t] : 0.f;
     }
   }
-  const uint4* X = Gs + (int64_t)s * sstride16 + c;
+  const RX* X = Gs + (int64_t)s * sstrideR + c;
   float* pds = pd + (int64_t)s * pstride;
   const int beg = rowptrT[row], end = rowptrT[row + 1];
   float acc[E];
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
       w1 = wT[(int64_t)(base + lane) * H + h1];
     }
     for (int k = 0; k < cnt; k += NG * U) {
-      uint4 r[U];
+      RX r[U];
       float v0[U], v1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -369,15 +370,15 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
         if (e < cnt && own) {
           r[u] = X[(int64_t)j * LPG];
         } else {
-          r[u] = make_uint4(0u, 0u, 0u, 0u);
+          r[u] = Vec4<T>::zero();
           v0[u] = v1[u] = 0.f;
         }
       }
       float q[2 * U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        float f[E];
-        unpack16(r[u], f);
+        const float4 fv = Vec4<T>::get(r[u]);
+        float f[E] = {fv.x, fv.y, fv.z, fv.w};
         float qa = 0.f, qb = 0.f;
 #pragma unroll
         for (int t = 0; t < E; ++t) {
@@ -543,9 +544,9 @@ bool alv(const void* p) {  // aligned for one Vec4<T> (nullptr passes)
   return (((uintptr_t)p) & (sizeof(typename Vec4<T>::raw) - 1)) == 0;
 }
 
-// neighbours in flight per lane group: 4 x 16 B per lane (fp32: 4 groups x 16 lanes; bf16: 8 x 8)
+// neighbours in flight per 16-lane group: 4 x 16 B (fp32) / 8 x 8 B (bf16) per lane
 template <typename T>
-constexpr int kGatU = 4;
+constexpr int kGatU = sizeof(T) == 4 ? 4 : 8;
 
 template <typename T>
 int gat_fwd_sliced(const int32_t* rowptr, const int32_t* col, int32_t n_rows, const T* Hs,
@@ -560,7 +561,7 @@ int gat_fwd_sliced(const int32_t* rowptr, const int32_t* col, int32_t n_rows, co
   if (n_rows == 0) return 0;
   if (!rowptr || !col || !Hs || !s1 || !s2 || !Y || !m_out || !den_out || !wgt)
     return GNNEA_EINVAL;
-  if (((uintptr_t)Hs & 15) || !alv<T>(Y)) return GNNEA_EALIGN;
+  if (!alv<T>(Hs) || !alv<T>(Y)) return GNNEA_EALIGN;
   const int nbs = div_up(n_rows, 4);
   switch (heads) {
 #define GNNEA_RS(HH)                                                                             \
@@ -575,14 +576,14 @@ int gat_fwd_sliced(const int32_t* rowptr, const int32_t* col, int32_t n_rows, co
   GNNEA_LAUNCH_CHECK();
   const int S = div_up(D, 64);
   const dim3 grid((unsigned)((int64_t)S * nbs));
-  const int64_t ss16 = sstride * (int64_t)sizeof(T) / 16;
+  typedef typename GatLanes<T>::R R;
   if (act == GNNEA_ACT_RELU)
     hipLaunchKernelGGL((k_gat_fwd_sliced<GNNEA_ACT_RELU, kGatU<T>, T, T>), grid, dim3(256), 0, st,
-                       rowptr, col, n_rows, nbs, heads, D, d_head, (const uint4*)Hs, ss16,
+                       rowptr, col, n_rows, nbs, heads, D, d_head, (const R*)Hs, sstride / 4,
                        wgt, den_out, Y, ldy);
   else
     hipLaunchKernelGGL((k_gat_fwd_sliced<GNNEA_ACT_IDENTITY, kGatU<T>, T, T>), grid, dim3(256), 0,
-                       st, rowptr, col, n_rows, nbs, heads, D, d_head, (const uint4*)Hs, ss16,
+                       st, rowptr, col, n_rows, nbs, heads, D, d_head, (const R*)Hs, sstride / 4,
                        wgt, den_out, Y, ldy);
   GNNEA_LAUNCH_CHECK();
   return 0;
@@ -728,7 +729,7 @@ int gat_bwd_src_sliced(const int32_t* rowptrT, const int32_t* colT, const int64_
   if (!rowptrT || !colT || !Hm || !s2 || !rec || !Gs || !wT || !pd || !dH ||
       (emask && !permT))
     return GNNEA_EINVAL;
-  if (!alv<T>(Hm) || ((uintptr_t)Gs & 15) || !alv<T>(dH)) return GNNEA_EALIGN;
+  if (!alv<T>(Hm) || !alv<T>(Gs) || !alv<T>(dH)) return GNNEA_EALIGN;
 #define GNNEA_W1(HH, LP)                                                                        \
   hipLaunchKernelGGL((k_gat_bwd_w<HH, LP>), dim3(div_up(n_rows, 256 / LP)), dim3(256), 0, st,   \
                      rowptrT, colT, permT, n_rows, s2, alpha, emask, (const float4*)rec, wT)
@@ -746,7 +747,7 @@ int gat_bwd_src_sliced(const int32_t* rowptrT, const int32_t* colT, const int64_
   const int S = div_up(D, 64), nbs = div_up(n_rows, 4);
   hipLaunchKernelGGL((k_gat_bwd_src_sl<kGatU<T>, T>), dim3((unsigned)((int64_t)S * nbs)),
                      dim3(256), 0, st, rowptrT, colT, n_rows, nbs, heads, D, d_head,
-                     (const uint4*)Gs, sstride * (int64_t)sizeof(T) / 16, Hm, ldh, wT, dH, lddh,
+                     (const typename GatLanes<T>::R*)Gs, sstride / 4, Hm, ldh, wT, dH, lddh,
                      pd, 2 * nnzT);
   GNNEA_LAUNCH_CHECK();
   return 0;

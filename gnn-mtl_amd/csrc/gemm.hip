@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <type_traits>
 #include "common.h"
+#include "lds_dma.h"
 
 namespace gnnea {
 
@@ -533,51 +534,8 @@ __global__ __launch_bounds__(XNT) void k_gemm_x3(int M, int N, int K, const floa
 // Requirements (host-checked): K % 4 == 0, lda % 4 == 0, A 16-B aligned; rows >= M / N read a
 // clamped valid row (their outputs are not stored), A quads with k >= K read a valid address and
 // are zeroed in registers, the B planes are zero-padded to ldp.
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void gbl_void_t;
-
-__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
-}
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const lds_void_t*)p;
-}
-__device__ __forceinline__ u32x4 ds_read128(uint32_t addr) {
-  u32x4 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-template <int OFF>  // immediate byte offset (ds_* offsets are 16-bit)
-__device__ __forceinline__ u32x4 ds_read128_o(uint32_t addr) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
-  u32x4 v;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
-  return v;
-}
-// (a float result type, not a per-element __builtin_bit_cast of a u32x4 lane: hipcc 7.2
-// miscompiles bit_cast of an ext-vector element lvalue to element 0)
-__device__ __forceinline__ f32x4_t ds_read128f(uint32_t addr) {
-  f32x4_t v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
-  return v;
-}
-
 // NW waves stacked along M (4: two workgroups per CU, 3-stage ring; 8: one per CU, 4 stages,
 // half the B-tile traffic per row of A)
-template <int I>
-struct IntC {
-  static constexpr int value = I;
-};
-template <int N, int I = 0, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(IntC<I>{});
-    static_for<N, I + 1>(f);
-  }
-}
-
 template <int WT, int NW>
 struct X3P {
   static constexpr int BM = 32 * NW, NT = 64 * NW;
@@ -605,9 +563,6 @@ struct X3P {
 // plain ones).  vec4 (N % 4 == 0, ldc % 4 == 0, cs % 4 == 0, C 16-B aligned): EXACTLY four
 // 16-B stores per lane per tile, out-of-range lanes storing to `dummy` (the k-loop counts them in
 // its vmcnt waits); otherwise scalar stores.
-__device__ __forceinline__ void ds_write32(uint32_t addr, float v) {
-  asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v));
-}
 template <int LD>  // epilogue row stride in floats
 __device__ __forceinline__ void store_tile_v4(const f32x16& acc, uint32_t region, int M, int N,
                                               int m_w, int n_t, int kh, int li, int lane,

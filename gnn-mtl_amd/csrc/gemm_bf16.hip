@@ -13,6 +13,7 @@
 // two 8-row groups: conflict-free; row-group-fastest lanes hit 2 banks, 32-way).  Next tile's global loads are in flight under the current tile's MFMAs.
 // Split-K for the weight gradients as in gemm.hip: fp32 slabs, fixed-order reduction.
 #include "common.h"
+#include "lds_dma.h"
 
 #include <stdlib.h>
 
@@ -278,6 +279,313 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(int M, int N, int K,
   }
 }
 
+// ---- k_gemm_bf16p: the projection form (A [M][K] K-contiguous bf16, B the small weight) on the
+// persistent LDS-DMA pipeline of gemm.hip's k_gemm_x3p, one product instead of six.
+// k_gemm_bf16 above re-stages the whole 300 x 300 weight through registers for every 64-row tile,
+// keeps one k-step of loads in flight and runs a 10-step k-loop per tile (cfg-5, 4M x 300 x 300:
+// 2.8 ms = 1.7 TB/s of the 4.8 GB of compulsory I/O).  Here one 512-thread workgroup per CU walks
+// its 256-row x 32*WT-column tiles as ONE stream of 32-deep k-stages through a 4-stage LDS ring
+// filled by global_load_lds (no registers): the next tile's stages land while the current tile's
+// last ones are multiplied, and a tile's epilogue (through LDS, whole 8-B / 16-B row chunks) runs
+// while the next tile's stages land.  A stage = the A tile (256 rows x 64 B) and the B tile
+// (32*WT rows x 64 B) of the weight, pre-packed once per call k-block-major ([kb][NP][32] bf16,
+// zero-padded; with a bias, rows k = K, K+1, K+2 hold it split three ways into bf16 and A gets
+// ones there: the bias joins the fp32 accumulation exactly).  A rows of K = 300 bf16 are 600 B:
+// only 8-B aligned, and a 16-B piece at k = 296 would run into the next row (past the allocation
+// on the last one), so A moves in 4-B granules (AW = 4; AW = 16 when K, lda % 8 == 0 and A is
+// 16-B aligned).  LDS images are lane-linear; the bank swizzle (16-B slot s of row r at
+// s ^ ((r >> 2) & 3), as k_gemm_x3p's A) goes on the source addresses and the reads.
+template <int WT, int AW>
+struct BFP {
+  static constexpr int NW = 8, BM = 32 * NW, NT = 64 * NW, BN = 32 * WT;
+  static constexpr int KS = 32;                                  // k per stage (2 MFMA k-steps)
+  static constexpr int A_BYTES = BM * KS * 2;                    // 16 KB
+  static constexpr int A_LOADS = A_BYTES / (64 * AW) / NW;       // per wave: 2 (AW 16), 8 (AW 4)
+  static constexpr int B_CHUNKS = BN * KS * 2 / 1024;            // 1-KB chunks of 16 rows
+  // every wave DMAs B_FULL chunks, waves w < B_EXTRA one more (no padding chunks)
+  static constexpr int B_FULL = B_CHUNKS / NW, B_EXTRA = B_CHUNKS % NW;
+  static constexpr int EPI_BYTES = NW * 32 * 32 * 4;            // the waves' epilogue regions
+  static constexpr int STAGE = A_BYTES + B_CHUNKS * 1024 > EPI_BYTES ? A_BYTES + B_CHUNKS * 1024
+                                                                     : EPI_BYTES;
+  static constexpr int LOADS_LO = A_LOADS + B_FULL;              // DMA instr. / wave / stage
+  static constexpr int LOADS_HI = LOADS_LO + (B_EXTRA ? 1 : 0);
+  static constexpr int NS = 4;
+  static constexpr int EPI_LD = 32;                              // epilogue row stride (floats)
+  static_assert(NW * 32 * EPI_LD * 4 <= STAGE, "epilogue regions must fit one stage");
+  static_assert(NS * STAGE <= 160 * 1024, "LDS");
+};
+
+// 32 x 32 accumulator tile -> C (TC = bf16 / fp32) through the wave's private LDS region: lanes
+// write their column, read 4 consecutive columns of a row back, store them as one 8-B (bf16) /
+// 16-B (fp32) chunk.  vec4: EXACTLY four stores per lane (out-of-range lanes to `dummy`), which
+// the k-loop's vmcnt waits count.  Element (row, col) at c_index_bf(row, col, ldc, cs).
+template <typename TC>
+__device__ __forceinline__ void bfp_store_tile(const f32x16_b& acc, uint32_t region, int M, int N,
+                                               int m_w, int n_t, int kh, int li, int lane,
+                                               float beta, TC* __restrict__ C, int64_t ldc,
+                                               int64_t cs, bool vec4, TC* __restrict__ dummy) {
+  constexpr int LD = 32;
+  const uint32_t wb = region + (4 * kh) * LD * 4 + li * 4;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) ds_write32(wb + ((r & 3) + 8 * (r >> 2)) * LD * 4, acc[r]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const uint32_t rbase = region + (lane >> 3) * LD * 4 + (lane & 7) * 16;
+  f32x4_t v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = ds_read128f(rbase + i * 8 * LD * 4);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  typedef typename Vec4<TC>::raw R;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int grow = m_w + (lane >> 3) + 8 * i, gcol = n_t + (lane & 7) * 4;
+    float4 o = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
+    if (vec4) {
+      const bool ok = grow < M && gcol < N;
+      TC* c = ok ? C + c_index_bf(grow, gcol, ldc, cs) : dummy + 4 * lane;
+      if (beta != 0.f && ok) {
+        const float4 cc = Vec4<TC>::get(*(const R*)c);
+        o.x += beta * cc.x; o.y += beta * cc.y; o.z += beta * cc.z; o.w += beta * cc.w;
+      }
+      *(R*)c = Vec4<TC>::put(o);
+    } else if (grow < M) {
+      const float oo[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (gcol + e >= N) continue;
+        TC* c = C + c_index_bf(grow, gcol + e, ldc, cs);
+        float x = oo[e];
+        if (beta != 0.f) x += beta * to_f32<TC>(*c);
+        *c = from_f32<TC>(x);
+      }
+    }
+  }
+}
+
+// wait for this wave's DMA of the stage about to be read, with `later` stages issued after it
+// still in flight (and, right after an epilogue, that epilogue's 4 * WT stores, issued between)
+template <int L, int NS, int WT>
+__device__ __forceinline__ void bfp_wait(int later, bool stores_after) {
+  if (later == NS - 2 && stores_after)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NS - 2) + 4 * WT) : "memory");
+  else if (later == NS - 2)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NS - 2)) : "memory");
+  else if (later == 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int WT, int AW, typename TC, int MODE = 0>  // MODE (timing experiments only): 1 = no
+                            // MFMA, 2 = no DMA, 4 = no epilogue stores (accumulators kept live)
+__global__ __launch_bounds__(512) void k_gemm_bf16p(int M, int N, int K,
+                                                   const bf16_t* __restrict__ A, int64_t lda,
+                                                   const bf16_t* __restrict__ Bp, int NP, int hb,
+                                                   float beta, TC* __restrict__ C, int64_t ldc,
+                                                   int64_t cs, int tiles_n, int ntiles, int vec4,
+                                                   TC* __restrict__ dummy) {
+  using G = BFP<WT, AW>;
+  constexpr int NW = G::NW, NS = G::NS;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * G::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kh = lane >> 5, li = lane & 31;
+  const int nsteps = (K + (hb ? 3 : 0) + G::KS - 1) / G::KS;
+  const int gsz = gridDim.x;
+  const int nq = (int)blockIdx.x < ntiles ? (ntiles - (int)blockIdx.x + gsz - 1) / gsz : 0;
+  const int total = nq * nsteps;
+  auto tile_of = [&](int q, int& m0, int& n0) {
+    const int t_id = xcd_remap((int)blockIdx.x + q * gsz, ntiles);
+    m0 = (t_id / tiles_n) * G::BM;
+    n0 = (t_id % tiles_n) * G::BN;
+  };
+
+  // ---- issue side: the next stage of the stream (tile iq, k-stage is) ----
+  int iq = 0, is = 0;
+  const bf16_t* a_src[G::A_LOADS];  // row base + the lane's (swizzled) k offset in the stage
+  int a_koff[G::A_LOADS];
+  const bf16_t* b_src[G::B_FULL + 1];
+  const bool b_extra = G::B_EXTRA > 0 && w < G::B_EXTRA;  // wave-uniform
+  auto set_issue_tile = [&](int q) {
+    int m0, n0;
+    tile_of(q, m0, n0);
+#pragma unroll
+    for (int i = 0; i < G::A_LOADS; ++i) {
+      const int ci = w + NW * i;  // the workgroup's i-th A instruction of this wave
+      int row, koff;
+      if (AW == 16) {  // 16 rows x 4 slots of 16 B
+        row = 16 * ci + (lane >> 2);
+        koff = 8 * ((lane & 3) ^ ((row >> 2) & 3));
+      } else {  // 4 rows x 16 dwords
+        row = 4 * ci + (lane >> 4);
+        koff = 8 * (((lane >> 2) & 3) ^ ((row >> 2) & 3)) + 2 * (lane & 3);
+      }
+      a_koff[i] = koff;
+      a_src[i] = A + (int64_t)min(m0 + row, M - 1) * lda;
+    }
+#pragma unroll
+    for (int i = 0; i <= G::B_FULL; ++i) {
+      const int cb = i < G::B_FULL ? w + NW * i : NW * G::B_FULL + (b_extra ? w : 0);
+      const int row = 16 * cb + (lane >> 2);
+      b_src[i] = Bp + (int64_t)(n0 + row) * G::KS + 8 * ((lane & 3) ^ ((row >> 2) & 3));
+    }
+  };
+  auto issue_next = [&](int buf) {
+    if (is == 0) set_issue_tile(iq);
+    unsigned char* st = smem + buf * G::STAGE;
+    const int k0 = is * G::KS;
+#pragma unroll
+    for (int i = 0; i < G::A_LOADS; ++i) {
+      // a granule past K reads the row's k = 0 (valid) and is zeroed at use
+      const int k = k0 + a_koff[i];
+      const bf16_t* ap = a_src[i] + (k < K ? k : 0);
+      if (AW == 16) glds16(ap, st + (w + NW * i) * 1024);
+      else glds4(ap, st + (w + NW * i) * 256);
+    }
+#pragma unroll
+    for (int i = 0; i < G::B_FULL; ++i)
+      glds16(b_src[i] + (int64_t)is * NP * G::KS, st + G::A_BYTES + (w + NW * i) * 1024);
+    if (b_extra)
+      glds16(b_src[G::B_FULL] + (int64_t)is * NP * G::KS,
+             st + G::A_BYTES + (NW * G::B_FULL + w) * 1024);
+    if (++is == nsteps) { is = 0; ++iq; }
+  };
+
+  f32x16_b acc[WT];
+#pragma unroll
+  for (int t = 0; t < WT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // per-lane LDS read offsets (bytes within a stage); rows of 64 B, slot 2*ks + kh swizzled
+  const int ra = w * 32 + li;
+  const int a_off[2] = {ra * 64 + 16 * ((0 + kh) ^ ((ra >> 2) & 3)),
+                        ra * 64 + 16 * ((2 + kh) ^ ((ra >> 2) & 3))};
+  // B row t*32 + li: (row >> 2) & 3 is li's, so tile t's offset is b_off + t * 2 KB
+  const int b_off[2] = {G::A_BYTES + li * 64 + 16 * ((0 + kh) ^ ((li >> 2) & 3)),
+                        G::A_BYTES + li * 64 + 16 * ((2 + kh) ^ ((li >> 2) & 3))};
+  const uint32_t smem_lds = lds_addr(smem);
+  auto epilogue = [&](int q, int buf) {
+    int m0, n0;
+    tile_of(q, m0, n0);
+    if (MODE == 4) {  // timing experiment: one store per wave keeps the accumulators live
+      float t = 0.f;
+#pragma unroll
+      for (int qq = 0; qq < WT; ++qq)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) t += acc[qq][r];
+      if (t == 12345.f) C[tid] = from_f32<TC>(t);
+      return;
+    }
+    const uint32_t region = smem_lds + buf * G::STAGE + w * 32 * G::EPI_LD * 4;
+#pragma unroll
+    for (int t = 0; t < WT; ++t)
+      bfp_store_tile<TC>(acc[t], region, M, N, m0 + w * 32, n0 + 32 * t, kh, li, lane, beta, C,
+                         ldc, cs, vec4 != 0, dummy);
+  };
+  // vmcnt allowance for the first steps after an epilogue: its stores (exactly 4 per tile when
+  // vec4 and no beta loads) were issued after the DMA those steps wait for
+  const bool count_stores = vec4 != 0 && beta == 0.f && MODE != 4 &&
+                            G::LOADS_HI * (NS - 2) + 4 * WT <= 63;
+
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (MODE != 2 && i < total) issue_next(i);
+  int cur = 0, s = 0, q = 0;
+  for (int g = 0; g < total; ++g) {
+    const bool epi = s == 0 && q > 0;
+    {
+      const int later = total - 1 - g < NS - 2 ? total - 1 - g : NS - 2;  // stages issued after g
+      const bool st_after = count_stores && q > 0 && s >= 1 && s <= NS - 2;
+      if (b_extra) bfp_wait<G::LOADS_HI, NS, WT>(later, st_after);
+      else bfp_wait<G::LOADS_LO, NS, WT>(later, st_after);
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int prev = cur == 0 ? NS - 1 : cur - 1;
+    if (epi) {  // the previous tile's outputs, through buffer prev, then a clean accumulator
+      epilogue(q - 1, prev);
+      __builtin_amdgcn_s_barrier();  // every wave's epilogue reads of prev are done
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int t = 0; t < WT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    }
+    if (MODE != 2 && g + NS - 1 < total) issue_next(prev);
+    const uint32_t st = smem_lds + cur * G::STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      u32x4 araw = ds_read128(st + a_off[ks]);
+      u32x4 braw[WT];
+      static_for<WT>([&](auto tt) {
+        constexpr int t = decltype(tt)::value;
+        braw[t] = ds_read128_o<t * 2048>(st + b_off[ks]);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const int kb0 = s * G::KS + ks * 16 + 8 * kh;  // this lane's first k
+      if (kb0 + 8 > K) {  // past K: zeros; ones at k = K, K+1, K+2 under a bias
+        uint32_t d[4] = {araw.x, araw.y, araw.z, araw.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = kb0 + j;
+          const uint32_t val = k < K ? ((d[j >> 1] >> (16 * (j & 1))) & 0xffffu)
+                                     : ((hb && k < K + 3) ? 0x3f80u : 0u);
+          d[j >> 1] = (d[j >> 1] & ~(0xffffu << (16 * (j & 1)))) | (val << (16 * (j & 1)));
+        }
+        araw = u32x4{d[0], d[1], d[2], d[3]};
+      }
+      const bf16x8 a = __builtin_bit_cast(bf16x8, araw);
+      if (MODE == 1) {  // timing experiment: keep the data live, skip the matrix cores
+#pragma unroll
+        for (int t = 0; t < WT; ++t) acc[t][0] += (float)(a[0] + __builtin_bit_cast(bf16x8, braw[t])[1]);
+      } else {
+#pragma unroll
+        for (int t = 0; t < WT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, __builtin_bit_cast(bf16x8, braw[t]),
+                                                           acc[t], 0, 0, 0);
+      }
+    }
+    cur = cur == NS - 1 ? 0 : cur + 1;
+    if (++s == nsteps) { s = 0; ++q; }
+  }
+  if (total > 0) {  // the last tile: every DMA has landed (vmcnt(0) at the last step)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    epilogue(q - 1, 0);
+  }
+}
+
+// the weight op(B) [N][K] packed k-block-major for k_gemm_bf16p: P[kb][r][32] bf16, r < NP (the
+// column tiles' rows, zero past N), kb < KP / 32; with a bias, rows k = K, K+1, K+2 hold it split
+// into three bf16 terms (h + m + l = bias to fp32 rounding; A's ones there add it exactly in fp32)
+__global__ __launch_bounds__(256) void k_pack_bf16_planes(const bf16_t* __restrict__ B,
+                                                          int64_t ldb, int b_nk, int N, int K,
+                                                          int NP, int KP,
+                                                          const float* __restrict__ bias,
+                                                          bf16_t* __restrict__ P) {
+  const int64_t total = (int64_t)NP * KP;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int kb = (int)(t / ((int64_t)NP * 32));
+    const int rem = (int)(t - (int64_t)kb * NP * 32);
+    const int r = rem / 32, k = kb * 32 + rem % 32;
+    bf16_t v = 0;
+    if (r < N) {
+      if (k < K) {
+        v = b_nk ? B[(int64_t)r * ldb + k] : B[(int64_t)k * ldb + r];
+      } else if (bias && k < K + 3) {
+        const float x = bias[r];
+        const bf16_t h = f32_to_bf16(x);
+        const float r1 = x - bf16_to_f32(h);
+        const bf16_t m = f32_to_bf16(r1);
+        v = k == K ? h : (k == K + 1 ? m : f32_to_bf16(r1 - bf16_to_f32(m)));
+      }
+    }
+    P[t] = v;
+  }
+}
+
 // fixed-order reduction of the split-K slabs into C (bf16 or fp32)
 template <typename TC>
 __global__ void k_gemm_bf16_reduce(int M, int N, int splits, const float* __restrict__ slab,
@@ -371,11 +679,89 @@ static void launch_bf16_t(int wt, dim3 grid, hipStream_t s, bool vec, int M, int
 #undef GNNEA_WT
 }
 
+// k_gemm_bf16p applies to the tall projection form: A [M][K] K-contiguous (rows 4-B aligned, K
+// even), M >= 64K rows, the whole output 2 column tiles of 160 at most per 320 (N > 128)
+static bool bf16p_on() {
+  static const bool on = [] {  // A/B comparison only (GNNEA_BF16_PIPE=0: k_gemm_bf16)
+    const char* e = getenv("GNNEA_BF16_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+static bool bf16p_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda,
+                          const void* A) {
+  return bf16p_on() && !trans_a && M >= 65536 && N > 128 && N <= 4096 && K > 0 && K % 2 == 0 &&
+         lda % 2 == 0 && (((uintptr_t)A) & 3) == 0;
+}
+static int64_t bf16p_planes_bytes(int64_t N, int64_t K) {  // + a 2-KB dummy store target
+  const int64_t np = (N + 159) / 160 * 160, kp = (K + 3 + 31) / 32 * 32;
+  return ((np * kp * 2 + 255) & ~(int64_t)255) + 2048;
+}
+
+template <int AW, typename TC>
+static void launch_bf16p(hipStream_t s, int grid, int M, int N, int K, const bf16_t* A,
+                         int64_t lda, const bf16_t* P, int NP, int hb, float beta, TC* C,
+                         int64_t ldc, int64_t cs, int tiles_n, int ntiles, int vec4, TC* dummy) {
+  static const int mode = [] {  // timing experiments only (GNNEA_BF16P_MODE = 1, 2, 4)
+    const char* e = getenv("GNNEA_BF16P_MODE");
+    return e ? atoi(e) : 0;
+  }();
+#define GNNEA_BFP(MD)                                                                          \
+  hipLaunchKernelGGL((k_gemm_bf16p<5, AW, TC, MD>), dim3(grid), dim3(512), 0, s, M, N, K, A,   \
+                     lda, P, NP, hb, beta, C, ldc, cs, tiles_n, ntiles, vec4, dummy)
+  if (std::is_same<TC, bf16_t>::value && mode == 1) GNNEA_BFP(1);
+  else if (std::is_same<TC, bf16_t>::value && mode == 2) GNNEA_BFP(2);
+  else if (std::is_same<TC, bf16_t>::value && mode == 4) GNNEA_BFP(4);
+  else GNNEA_BFP(0);
+#undef GNNEA_BFP
+}
+
+template <typename TC>
+static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t* A,
+                      int64_t lda, const bf16_t* B, int64_t ldb, const float* bias, float beta,
+                      TC* C, int64_t ldc, int64_t cs, void* ws, hipStream_t s) {
+  const int NP = (int)((N + 159) / 160 * 160), KP = (int)((K + 3 + 31) / 32 * 32);
+  bf16_t* P = (bf16_t*)ws;
+  TC* dummy = (TC*)((char*)ws + bf16p_planes_bytes(N, K) - 2048);
+  {
+    const int64_t tot = (int64_t)NP * KP;
+    const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
+    hipLaunchKernelGGL(k_pack_bf16_planes, dim3(nb), dim3(256), 0, s, B, ldb, trans_b ? 1 : 0,
+                       (int)N, (int)K, NP, KP, bias, P);
+    GNNEA_LAUNCH_CHECK();
+  }
+  const int tiles_n = NP / 160;
+  const int64_t tm = (M + 255) / 256;
+  if (tm * tiles_n >= (1ll << 31)) return GNNEA_EINVAL;
+  const int ntiles = (int)(tm * tiles_n);
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  const int grid = ntiles < ncu ? ntiles : ncu;  // persistent: one 512-thread workgroup per CU
+  const int vec4 = N % 4 == 0 && ldc % 4 == 0 && cs % 4 == 0 &&
+                   (((uintptr_t)C) & (4 * sizeof(TC) - 1)) == 0;
+  const bool aw16 = K % 8 == 0;  // 16-B granules never cross the end of a row
+  if (aw16)
+    launch_bf16p<16, TC>(s, grid, (int)M, (int)N, (int)K, A, lda, P, NP, bias != nullptr, beta,
+                         C, ldc, cs, tiles_n, ntiles, vec4, dummy);
+  else
+    launch_bf16p<4, TC>(s, grid, (int)M, (int)N, (int)K, A, lda, P, NP, bias != nullptr, beta,
+                        C, ldc, cs, tiles_n, ntiles, vec4, dummy);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
 template <typename TC>
 static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                        const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
                        const float* bias, float beta, TC* C, int64_t ldc, void* ws,
                        int64_t ws_bytes, hipStream_t s, int64_t cs = 128) {
+  if (bf16p_applies(trans_a, M, N, K, lda, A) && ws && ws_bytes >= bf16p_planes_bytes(N, K))
+    return gemm_bf16p<TC>(trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, ws, s);
   const int wt = bf16_wt(N);
   const int64_t bn = 64 * wt;
   const int tiles_n = (int)((N + bn - 1) / bn);
@@ -410,7 +796,9 @@ using namespace gnnea;
 
 extern "C" int64_t gnnea_gemm_bf16_ws_bytes(int64_t M, int64_t N, int64_t K) {
   if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
-  return bf16_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
+  const int64_t split = bf16_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
+  const int64_t planes = bf16p_planes_bytes(N, K);  // k_gemm_bf16p (shape-dependent use)
+  return split > planes ? split : planes;
 }
 
 extern "C" int gnnea_gemm_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

@@ -897,6 +897,12 @@ def _pad4(t, D, dtype=None):
 
 # tests switch it off to compare with the row-major edge pass (GNNEA_GAT_SLICED=0: A/B timing)
 GAT_SLICED = os.environ.get("GNNEA_GAT_SLICED", "1") != "0"
+# bf16 storage (cfg-5): the sliced passes are built and parity-tested but not the default.  At
+# cfg-5 (2 x 2M rows, 84M edges) the passes are bound by per-edge work, not by gathered bytes:
+# five 128-B slice passes cost five times the per-edge overhead of one 600-B row-major pass
+# (per KG: forward 6.4 ms sliced + 1.3 ms row statistics vs 6.3 ms row-major; source pass 8.7
+# vs 10.8 ms but the side passes add ~6 ms per layer; GAT-EA step 145 vs 133 ms).
+GAT_SLICED_BF16 = os.environ.get("GNNEA_GAT_SLICED_BF16", "0") != "0"
 
 
 def gat_two_heads_per_slice(heads, d_head):
@@ -915,7 +921,9 @@ def _gat_sliced_applies(H, heads, d_head, Y):
     piece; one KG slice of cfg-4 fp32 / cfg-5 bf16 is 256 MB) when the row-major table exceeds
     the Infinity Cache and spans at least two slices."""
     D = heads * d_head
-    return (GAT_SLICED and H.dtype in FEATURE_DTYPES and gat_two_heads_per_slice(heads, d_head)
+    return (GAT_SLICED and (H.dtype == torch.float32 or
+                            (H.dtype == torch.bfloat16 and GAT_SLICED_BF16))
+            and gat_two_heads_per_slice(heads, d_head)
             and D % 4 == 0 and heads <= 8 and 128 <= D <= 1024 and Y.shape[1] == D
             and H.shape[0] * D * H.element_size() > INFINITY_CACHE_BYTES)
 

@@ -167,6 +167,40 @@ def test_gemm_bf16_vs_fp64(device, shape, ta, tb):
     assert torch.equal(yb.view(torch.int16), y32.to(torch.bfloat16).view(torch.int16))
 
 
+@pytest.mark.parametrize("M,N,K", [(70001, 300, 300), (65536, 256, 256), (131077, 600, 300),
+                                   (66000, 200, 64), (65600, 300, 30)])
+@pytest.mark.parametrize("tb", [0, 1])
+def test_gemm_bf16_pipelined_vs_fp64(device, M, N, K, tb):
+    """The tall projection form on k_gemm_bf16p (persistent LDS-DMA ring; M >= 64K): fp32 and
+    bf16 outputs vs fp64 of the same bf16 operands, the bias joined exactly (three bf16 terms
+    against A's ones), 4-B (K % 8 != 0) and 16-B (K % 8 == 0) A granules, ragged M / N, the
+    slice-major bf16 output and beta accumulation."""
+    from gnnea import ops
+    rng = np.random.default_rng(M + N + K + tb)
+    a = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32)).to(device).bfloat16()
+    b = torch.from_numpy(rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32))
+    bb = b.to(device).bfloat16()
+    bias = torch.from_numpy(rng.standard_normal(N).astype(np.float32)).to(device)
+    ref = a.double() @ (bb.double().t() if tb else bb.double()) + bias.double()
+    y32 = ops.gemm(a, bb, False, bool(tb), bias=bias, out_dtype=torch.float32)
+    assert rel_err(y32.cpu(), ref.cpu()) < TOL_ACC
+    yb = ops.gemm(a, bb, False, bool(tb), bias=bias)
+    assert torch.equal(yb.view(torch.int16), y32.to(torch.bfloat16).view(torch.int16))
+    y0 = ops.gemm(a, bb, False, bool(tb), out_dtype=torch.float32)  # no bias
+    assert rel_err(y0.cpu(), (ref - bias.double()).cpu()) < TOL_ACC
+    prev = torch.from_numpy(rng.standard_normal((M, N)).astype(np.float32)).to(device)
+    acc = prev.clone()
+    ops.gemm(a, bb, False, bool(tb), out=acc, beta=0.5)
+    assert rel_err(acc.cpu(), (y0.double() + 0.5 * prev.double()).cpu()) < TOL_ACC
+    if N % 4 == 0 and not tb:  # the slice-major bf16 table (gnnea_gemm_sliced_bf16)
+        hs = ops.gemm_sliced(a, bb.t().contiguous(), bias)
+        W = hs.shape[2]
+        for q in range(hs.shape[0]):
+            c1 = min(N, (q + 1) * W)
+            assert torch.equal(hs[q, :, :c1 - q * W].view(torch.int16),
+                               yb[:, q * W:c1].view(torch.int16))
+
+
 def test_linear_bf16_autograd(device):
     from gnnea import ops
     rng = np.random.default_rng(21)

@@ -1,7 +1,8 @@
 """BASELINE configs[4] shape on one MI355X: the 4-head GAT path in bf16 storage on the
 2 x 2M-entity / 2 x 20M-triple pair (~84M nnz) — the production bf16 path (bf16 MFMA projection,
-64-column slice-major bf16 GAT passes above the Infinity Cache, bf16 backward), nothing
-monkeypatched but spies.
+the row-major all-heads bf16 GAT passes — the 64-column sliced bf16 passes are parity-tested at
+small size in test_gpu_sliced.py but not the default, see ops.GAT_SLICED_BF16 — bf16 backward),
+nothing monkeypatched but spies.
 
 Checked against
   * the fp64 CPU oracle over the sampled rows' neighbourhoods (oracle/local.py) on the SAME
@@ -80,7 +81,7 @@ def test_cfg5_gat_bf16_layer_vs_oracle(device, cfg5, monkeypatch, relu_band, rec
     assert out.dtype == torch.bfloat16
     (out.float() * d["R"]).sum().backward()
     assert xx.grad.dtype == torch.bfloat16
-    assert taken == [True, True], taken  # the 64-column sliced bf16 forward and backward
+    assert taken == [False, False], taken  # bf16: the row-major passes (ops.GAT_SLICED_BF16)
     Ws = torch.stack([a.W.detach().float().cpu() for a in layer.attentions]).double()
     As = torch.stack([a.a.detach().float().cpu() for a in layer.attentions]).double()
 
@@ -151,7 +152,7 @@ def test_cfg5_gat_ea_step_vs_fp64(device, cfg5, monkeypatch, relu_band, record_p
     m.neg2_left = si.negatives(N, t, k, 32)
     loss = m.get_loss(outputs, {"train": train}, "train")
     loss.backward()
-    assert taken == [True, True, True, True], taken  # 2 layers x (forward, backward) sliced
+    assert taken == [False] * 4, taken  # bf16 default: row-major passes (ops.GAT_SLICED_BF16)
     ix = [torch.from_numpy(np.asarray(z, dtype=np.int64)).to(device) for z in
           (train[:, 0], train[:, 1], m.neg_left, m.neg_right, m.neg2_left, m.neg2_right)]
     # fp64 restatement: 2 GAT layers (relu), MLP decoder relu / relu / identity

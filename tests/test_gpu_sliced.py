@@ -482,6 +482,8 @@ def test_gat_bf16_sliced_vs_rowmajor_and_oracle(device, monkeypatch, heads, d_he
                               ).to(device)
     dY = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32)).to(device).bfloat16()
 
+    monkeypatch.setattr(ops, "GAT_SLICED_BF16", True)
+
     def run(sliced):
         monkeypatch.setattr(ops, "GAT_SLICED", sliced)
         monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 1 if sliced else 1 << 40)

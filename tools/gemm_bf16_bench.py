@@ -39,18 +39,26 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=4000000)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--k", type=int, default=300, help="inner dimension of the projection")
+    ap.add_argument("--only-fwd", action="store_true", help="only x.W^T + b (mode sweeps)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
-    M, D = args.rows, 300
-    X = torch.randn(M, D, device=dev, generator=g).to(torch.bfloat16)
-    W = (torch.randn(D, D, device=dev, generator=g) * 0.05).to(torch.bfloat16)
+    M, D, K = args.rows, 300, args.k
+    X = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    W = (torch.randn(D, K, device=dev, generator=g) * 0.05).to(torch.bfloat16)
     b = torch.randn(D, device=dev, generator=g) * 0.1
     Y = ops.gemm(X, W, trans_b=True, bias=b)
     ref = (X[:65536].float() @ W.float().t() + b)
     err = float(((Y[:65536].float() - ref).abs() / (ref.abs() + 1e-2)).max())
-    io = 2 * (2 * M * D + D * D)
+    io = 2 * (M * K + M * D + D * K)
     ms = timeit(lambda: ops.gemm(X, W, trans_b=True, bias=b), args.reps)
+    if args.only_fwd:
+        print(json.dumps({"rows": M, "K": K, "pipe": os.environ.get("GNNEA_BF16_PIPE", "1"),
+                          "mode": os.environ.get("GNNEA_BF16P_MODE", "0"),
+                          "gnnea_ms": round(ms, 4), "gnnea_GBps_io": round(io / ms / 1e6, 1),
+                          "max_rel_err_vs_fp32": err}))
+        return
     bl = b.to(torch.bfloat16)
     ms_t = timeit(lambda: torch.nn.functional.linear(X, W, bl), args.reps)
     dY = torch.randn(M, D, device=dev, generator=g).to(torch.bfloat16)
@@ -63,10 +71,11 @@ def main():
     ms_x = timeit(lambda: ops.gemm(dY, W), args.reps)
     del dW
     print(json.dumps({"rows": M, "epilogue": os.environ.get("GNNEA_BF16_EPI", "1"),
+                      "pipe": os.environ.get("GNNEA_BF16_PIPE", "1"),
                       "dW_ms": round(ms_w, 4), "dW_hipblaslt_ms": round(ms_wt, 4),
                       "dW_max_rel_err_vs_fp32": errw, "dX_ms": round(ms_x, 4),
                       "gnnea_ms": round(ms, 4), "gnnea_GBps_io": round(io / ms / 1e6, 1),
-                      "gnnea_TFLOPs": round(2.0 * M * D * D / ms / 1e9, 1),
+                      "gnnea_TFLOPs": round(2.0 * M * D * K / ms / 1e9, 1),
                       "hipblaslt_ms": round(ms_t, 4), "max_rel_err_vs_fp32": err}))
 
 
