@@ -291,13 +291,15 @@ __global__ __launch_bounds__(256) void k_gemm_bf16(int M, int N, int K,
 // (32*WT rows x 64 B) of the weight, pre-packed once per call k-block-major ([kb][NP][32] bf16,
 // zero-padded; with a bias, rows k = K, K+1, K+2 hold it split three ways into bf16 and A gets
 // ones there: the bias joins the fp32 accumulation exactly).  A rows of K = 300 bf16 are 600 B:
-// only 8-B aligned, and a 16-B piece at k = 296 would run into the next row (past the allocation
-// on the last one), so A moves in 4-B granules (AW = 4; AW = 16 when K, lda % 8 == 0 and A is
-// 16-B aligned).  LDS images are lane-linear; the bank swizzle (16-B slot s of row r at
+// 16-B LDS-DMA granules from 4-B aligned addresses are exact on gfx950
+// (tools/ubench/probe_glds.hip); the granule at k = 296 runs 4 elements into the next row, which
+// the k-mask zeroes, so the last row (no next row) is left to the register-staged kernel
+// (gemm_bf16p).  AW = 4 (4-B granules, no overrun) is kept as an alternative: 2.27 vs 2.02 ms
+// at 4M x 300 x 300 measured for the 16-B form.  LDS images are lane-linear; the bank swizzle (16-B slot s of row r at
 // s ^ ((r >> 2) & 3), as k_gemm_x3p's A) goes on the source addresses and the reads.
-template <int WT, int AW>
+template <int WT, int AW, int NW_>
 struct BFP {
-  static constexpr int NW = 8, BM = 32 * NW, NT = 64 * NW, BN = 32 * WT;
+  static constexpr int NW = NW_, BM = 32 * NW, NT = 64 * NW, BN = 32 * WT;
   static constexpr int KS = 32;                                  // k per stage (2 MFMA k-steps)
   static constexpr int A_BYTES = BM * KS * 2;                    // 16 KB
   static constexpr int A_LOADS = A_BYTES / (64 * AW) / NW;       // per wave: 2 (AW 16), 8 (AW 4)
@@ -316,45 +318,69 @@ struct BFP {
 };
 
 // 32 x 32 accumulator tile -> C (TC = bf16 / fp32) through the wave's private LDS region: lanes
-// write their column, read 4 consecutive columns of a row back, store them as one 8-B (bf16) /
-// 16-B (fp32) chunk.  vec4: EXACTLY four stores per lane (out-of-range lanes to `dummy`), which
-// the k-loop's vmcnt waits count.  Element (row, col) at c_index_bf(row, col, ldc, cs).
+// write their column, read a row's consecutive columns back and store them as one 16-B chunk:
+// 8 bf16 columns (two stores per lane per tile) or 4 fp32 columns (four).  vec: EXACTLY that many
+// stores per lane (out-of-range lanes to `dummy`), which the k-loop's vmcnt waits count.
+// Element (row, col) at c_index_bf(row, col, ldc, cs).
+template <typename TC>
+struct BfpEpi {
+  static constexpr int CPL = 16 / sizeof(TC);  // columns per lane-store
+  static constexpr int STORES = 32 * 32 / 64 / CPL;
+};
 template <typename TC>
 __device__ __forceinline__ void bfp_store_tile(const f32x16_b& acc, uint32_t region, int M, int N,
                                                int m_w, int n_t, int kh, int li, int lane,
                                                float beta, TC* __restrict__ C, int64_t ldc,
-                                               int64_t cs, bool vec4, TC* __restrict__ dummy) {
-  constexpr int LD = 32;
+                                               int64_t cs, bool vec, TC* __restrict__ dummy) {
+  constexpr int LD = 32, CPL = BfpEpi<TC>::CPL, RPI = 64 / (32 / CPL);  // rows per instruction
   const uint32_t wb = region + (4 * kh) * LD * 4 + li * 4;
 #pragma unroll
   for (int r = 0; r < 16; ++r) ds_write32(wb + ((r & 3) + 8 * (r >> 2)) * LD * 4, acc[r]);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  const uint32_t rbase = region + (lane >> 3) * LD * 4 + (lane & 7) * 16;
-  f32x4_t v[4];
+  const int lr = lane / (32 / CPL), lc = (lane % (32 / CPL)) * CPL;  // row in the group, column
+  const uint32_t rbase = region + lr * LD * 4 + lc * 4;
+  f32x4_t v[2 * BfpEpi<TC>::STORES];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = ds_read128f(rbase + i * 8 * LD * 4);
+  for (int i = 0; i < BfpEpi<TC>::STORES; ++i) {
+    v[2 * i] = ds_read128f(rbase + i * RPI * LD * 4);
+    if (CPL == 8) v[2 * i + 1] = ds_read128f(rbase + i * RPI * LD * 4 + 16);
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  typedef typename Vec4<TC>::raw R;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int grow = m_w + (lane >> 3) + 8 * i, gcol = n_t + (lane & 7) * 4;
-    float4 o = make_float4(v[i][0], v[i][1], v[i][2], v[i][3]);
-    if (vec4) {
+  for (int i = 0; i < BfpEpi<TC>::STORES; ++i) {
+    const int grow = m_w + lr + RPI * i, gcol = n_t + lc;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = v[2 * i][e];
+      o[4 + e] = CPL == 8 ? v[2 * i + 1][e] : 0.f;
+    }
+    if (vec) {
       const bool ok = grow < M && gcol < N;
-      TC* c = ok ? C + c_index_bf(grow, gcol, ldc, cs) : dummy + 4 * lane;
+      TC* c = ok ? C + c_index_bf(grow, gcol, ldc, cs) : dummy + CPL * lane;
       if (beta != 0.f && ok) {
-        const float4 cc = Vec4<TC>::get(*(const R*)c);
-        o.x += beta * cc.x; o.y += beta * cc.y; o.z += beta * cc.z; o.w += beta * cc.w;
-      }
-      *(R*)c = Vec4<TC>::put(o);
-    } else if (grow < M) {
-      const float oo[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < CPL; ++e) o[e] += beta * to_f32<TC>(c[e]);
+      }
+      if constexpr (CPL == 8) {
+        uint4 u;
+        u.x = (uint32_t)f32_to_bf16(o[0]) | ((uint32_t)f32_to_bf16(o[1]) << 16);
+        u.y = (uint32_t)f32_to_bf16(o[2]) | ((uint32_t)f32_to_bf16(o[3]) << 16);
+        u.z = (uint32_t)f32_to_bf16(o[4]) | ((uint32_t)f32_to_bf16(o[5]) << 16);
+        u.w = (uint32_t)f32_to_bf16(o[6]) | ((uint32_t)f32_to_bf16(o[7]) << 16);
+        // the row's last chunk may hold 4 columns (N % 8 == 4): one 8-B store (still ONE store)
+        if (!ok || gcol + 8 <= N) *(uint4*)c = u;
+        else *(uint2*)c = make_uint2(u.x, u.y);
+      } else {
+        *(float4*)c = make_float4(o[0], o[1], o[2], o[3]);
+      }
+    } else if (grow < M) {
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) {
         if (gcol + e >= N) continue;
         TC* c = C + c_index_bf(grow, gcol + e, ldc, cs);
-        float x = oo[e];
+        float x = o[e];
         if (beta != 0.f) x += beta * to_f32<TC>(*c);
         *c = from_f32<TC>(x);
       }
@@ -362,12 +388,57 @@ __device__ __forceinline__ void bfp_store_tile(const f32x16_b& acc, uint32_t reg
   }
 }
 
+// Two adjacent 32 x 32 tiles -> bf16 C as 64-column (128-B) row pieces: the tile pair is rounded
+// to bf16 into the wave's [32][64] LDS region (4 KB; 16-B chunk c of row r at c ^ (r & 7)), read
+// back as 8 rows x 8 chunks per instruction and stored as 16-B chunks, 128 B of every row per
+// instruction (a single tile leaves 64-B row pieces, which measured 0.8 ms of stores at
+// 4M x 300: 2.4 GB).  EXACTLY four stores per lane when vec (dummy for out-of-range lanes; a row's
+// last chunk with 4 valid columns is one 8-B store).
+__device__ __forceinline__ void ds_write16(uint32_t addr, uint32_t v) {
+  asm volatile("ds_write_b16 %0, %1" ::"v"(addr), "v"(v));
+}
+__device__ __forceinline__ void bfp_store_pair_bf16(const f32x16_b& a0, const f32x16_b& a1,
+                                                    uint32_t region, int M, int N, int m_w,
+                                                    int n_t, int kh, int li, int lane,
+                                                    bf16_t* __restrict__ C, int64_t ldc,
+                                                    int64_t cs, bf16_t* __restrict__ dummy) {
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const int col = 32 * ct + li;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
+      const uint32_t a = region + row * 128 + 16 * ((col >> 3) ^ (row & 7)) + 2 * (col & 7);
+      ds_write16(a, (uint32_t)f32_to_bf16(ct == 0 ? a0[r] : a1[r]));
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  u32x4 v[4];
+  const int lr = lane >> 3, ch = lane & 7;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = lr + 8 * i;
+    v[i] = ds_read128(region + row * 128 + 16 * (ch ^ (row & 7)));
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int grow = m_w + lr + 8 * i, gcol = n_t + 8 * ch;
+    const bool ok = grow < M && gcol < N;
+    bf16_t* c = ok ? C + c_index_bf(grow, gcol, ldc, cs) : dummy + 8 * lane;
+    const uint4 u = make_uint4(v[i].x, v[i].y, v[i].z, v[i].w);
+    if (!ok || gcol + 8 <= N) *(uint4*)c = u;
+    else *(uint2*)c = make_uint2(u.x, u.y);
+  }
+}
+
 // wait for this wave's DMA of the stage about to be read, with `later` stages issued after it
-// still in flight (and, right after an epilogue, that epilogue's 4 * WT stores, issued between)
-template <int L, int NS, int WT>
+// still in flight (and, right after an epilogue, that epilogue's ST stores, issued between)
+template <int L, int NS, int ST>  // ST: the epilogue's stores per lane
 __device__ __forceinline__ void bfp_wait(int later, bool stores_after) {
   if (later == NS - 2 && stores_after)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NS - 2) + 4 * WT) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NS - 2) + ST) : "memory");
   else if (later == NS - 2)
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L * (NS - 2)) : "memory");
   else if (later == 1)
@@ -376,15 +447,15 @@ __device__ __forceinline__ void bfp_wait(int later, bool stores_after) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int WT, int AW, typename TC, int MODE = 0>  // MODE (timing experiments only): 1 = no
-                            // MFMA, 2 = no DMA, 4 = no epilogue stores (accumulators kept live)
-__global__ __launch_bounds__(512) void k_gemm_bf16p(int M, int N, int K,
+template <int WT, int AW, int NW_, typename TC, int MODE = 0>  // MODE (timing experiments
+                  // only): 1 = no MFMA, 2 = no DMA, 4 = no epilogue stores (accumulators live)
+__global__ __launch_bounds__(64 * NW_) void k_gemm_bf16p(int M, int N, int K,
                                                    const bf16_t* __restrict__ A, int64_t lda,
                                                    const bf16_t* __restrict__ Bp, int NP, int hb,
                                                    float beta, TC* __restrict__ C, int64_t ldc,
-                                                   int64_t cs, int tiles_n, int ntiles, int vec4,
+                                                   int64_t cs, int tiles_n, int ntiles, int vec,
                                                    TC* __restrict__ dummy) {
-  using G = BFP<WT, AW>;
+  using G = BFP<WT, AW, NW_>;
   constexpr int NW = G::NW, NS = G::NS;
   __shared__ __attribute__((aligned(1024))) unsigned char smem[NS * G::STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -477,15 +548,28 @@ __global__ __launch_bounds__(512) void k_gemm_bf16p(int M, int N, int K,
       return;
     }
     const uint32_t region = smem_lds + buf * G::STAGE + w * 32 * G::EPI_LD * 4;
+    if constexpr (std::is_same<TC, bf16_t>::value) {
+      if (vec != 0 && beta == 0.f) {  // tile pairs as 128-B row pieces
+#pragma unroll
+        for (int t = 0; t + 1 < WT; t += 2)
+          bfp_store_pair_bf16(acc[t], acc[t + 1], region, M, N, m0 + w * 32, n0 + 32 * t, kh, li,
+                              lane, C, ldc, cs, dummy);
+        if (WT % 2)
+          bfp_store_tile<TC>(acc[WT - 1], region, M, N, m0 + w * 32, n0 + 32 * (WT - 1), kh, li,
+                             lane, beta, C, ldc, cs, true, dummy);
+        return;
+      }
+    }
 #pragma unroll
     for (int t = 0; t < WT; ++t)
       bfp_store_tile<TC>(acc[t], region, M, N, m0 + w * 32, n0 + 32 * t, kh, li, lane, beta, C,
-                         ldc, cs, vec4 != 0, dummy);
+                         ldc, cs, vec != 0, dummy);
   };
   // vmcnt allowance for the first steps after an epilogue: its stores (exactly 4 per tile when
-  // vec4 and no beta loads) were issued after the DMA those steps wait for
-  const bool count_stores = vec4 != 0 && beta == 0.f && MODE != 4 &&
-                            G::LOADS_HI * (NS - 2) + 4 * WT <= 63;
+  // vec and no beta loads) were issued after the DMA those steps wait for
+  // epilogue stores per lane: bf16 tile pairs 4 + a single tile 2 (= 2 per tile), fp32 4 per tile
+  constexpr int ST = BfpEpi<TC>::STORES * WT;
+  const bool count_stores = vec != 0 && beta == 0.f && MODE != 4 && G::LOADS_HI * (NS - 2) + ST <= 63;
 
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i)
@@ -496,8 +580,8 @@ __global__ __launch_bounds__(512) void k_gemm_bf16p(int M, int N, int K,
     {
       const int later = total - 1 - g < NS - 2 ? total - 1 - g : NS - 2;  // stages issued after g
       const bool st_after = count_stores && q > 0 && s >= 1 && s <= NS - 2;
-      if (b_extra) bfp_wait<G::LOADS_HI, NS, WT>(later, st_after);
-      else bfp_wait<G::LOADS_LO, NS, WT>(later, st_after);
+      if (b_extra) bfp_wait<G::LOADS_HI, NS, ST>(later, st_after);
+      else bfp_wait<G::LOADS_LO, NS, ST>(later, st_after);
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -698,23 +782,40 @@ static int64_t bf16p_planes_bytes(int64_t N, int64_t K) {  // + a 2-KB dummy sto
   return ((np * kp * 2 + 255) & ~(int64_t)255) + 2048;
 }
 
-template <int AW, typename TC>
+template <int AW, int NW, typename TC>
 static void launch_bf16p(hipStream_t s, int grid, int M, int N, int K, const bf16_t* A,
                          int64_t lda, const bf16_t* P, int NP, int hb, float beta, TC* C,
-                         int64_t ldc, int64_t cs, int tiles_n, int ntiles, int vec4, TC* dummy) {
+                         int64_t ldc, int64_t cs, int tiles_n, int ntiles, int vec, TC* dummy) {
   static const int mode = [] {  // timing experiments only (GNNEA_BF16P_MODE = 1, 2, 4)
     const char* e = getenv("GNNEA_BF16P_MODE");
     return e ? atoi(e) : 0;
   }();
-#define GNNEA_BFP(MD)                                                                          \
-  hipLaunchKernelGGL((k_gemm_bf16p<5, AW, TC, MD>), dim3(grid), dim3(512), 0, s, M, N, K, A,   \
-                     lda, P, NP, hb, beta, C, ldc, cs, tiles_n, ntiles, vec4, dummy)
-  if (std::is_same<TC, bf16_t>::value && mode == 1) GNNEA_BFP(1);
-  else if (std::is_same<TC, bf16_t>::value && mode == 2) GNNEA_BFP(2);
-  else if (std::is_same<TC, bf16_t>::value && mode == 4) GNNEA_BFP(4);
+#define GNNEA_BFP(MD)                                                                           \
+  hipLaunchKernelGGL((k_gemm_bf16p<5, AW, NW, TC, MD>), dim3(grid), dim3(64 * NW), 0, s, M, N,  \
+                     K, A, lda, P, NP, hb, beta, C, ldc, cs, tiles_n, ntiles, vec, dummy)
+  constexpr bool modes = std::is_same<TC, bf16_t>::value && AW == 16;
+  if (modes && mode == 1) GNNEA_BFP(modes ? 1 : 0);
+  else if (modes && mode == 2) GNNEA_BFP(modes ? 2 : 0);
+  else if (modes && mode == 4) GNNEA_BFP(modes ? 4 : 0);
   else GNNEA_BFP(0);
 #undef GNNEA_BFP
 }
+
+// waves per workgroup: 8 (256-row tiles, one workgroup per CU) or 4 (128-row tiles, two per CU:
+// one's barriers and epilogue under the other's MFMAs); GNNEA_BF16P_NW overrides (tuning)
+static int bf16p_nw() {
+  static const int v = [] {
+    const char* e = getenv("GNNEA_BF16P_NW");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  return v;
+}
+
+template <typename TC>
+static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                       const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
+                       const float* bias, float beta, TC* C, int64_t ldc, void* ws,
+                       int64_t ws_bytes, hipStream_t s, int64_t cs = 128);
 
 template <typename TC>
 static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t* A,
@@ -730,8 +831,14 @@ static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
                        (int)N, (int)K, NP, KP, bias, P);
     GNNEA_LAUNCH_CHECK();
   }
+  // A in 16-B granules: a row's last granule may run (8 - K % 8) % 8 elements past K, into the
+  // row's padding or the next row (zeroed at use); the last row has no next row, so without
+  // enough padding it is computed by the register-staged kernel instead
+  const int over = (8 - (int)(K % 8)) % 8;
+  const int64_t Mp = lda - K >= over ? M : M - 1;
+  const int nw = bf16p_nw();
   const int tiles_n = NP / 160;
-  const int64_t tm = (M + 255) / 256;
+  const int64_t tm = (Mp + 32 * nw - 1) / (32 * nw);
   if (tm * tiles_n >= (1ll << 31)) return GNNEA_EINVAL;
   const int ntiles = (int)(tm * tiles_n);
   static const int ncu = [] {
@@ -741,17 +848,20 @@ static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
       n = 256;
     return n;
   }();
-  const int grid = ntiles < ncu ? ntiles : ncu;  // persistent: one 512-thread workgroup per CU
-  const int vec4 = N % 4 == 0 && ldc % 4 == 0 && cs % 4 == 0 &&
-                   (((uintptr_t)C) & (4 * sizeof(TC) - 1)) == 0;
-  const bool aw16 = K % 8 == 0;  // 16-B granules never cross the end of a row
-  if (aw16)
-    launch_bf16p<16, TC>(s, grid, (int)M, (int)N, (int)K, A, lda, P, NP, bias != nullptr, beta,
-                         C, ldc, cs, tiles_n, ntiles, vec4, dummy);
+  const int per_cu = nw == 8 ? 1 : 2;  // persistent: as many workgroups as fit at once
+  const int grid = ntiles < per_cu * ncu ? ntiles : per_cu * ncu;
+  const int vec = N % 4 == 0 && ldc % 4 == 0 && cs % 4 == 0 &&
+                  (((uintptr_t)C) & (4 * sizeof(TC) - 1)) == 0;
+  if (nw == 8)
+    launch_bf16p<16, 8, TC>(s, grid, (int)Mp, (int)N, (int)K, A, lda, P, NP, bias != nullptr,
+                            beta, C, ldc, cs, tiles_n, ntiles, vec, dummy);
   else
-    launch_bf16p<4, TC>(s, grid, (int)M, (int)N, (int)K, A, lda, P, NP, bias != nullptr, beta,
-                        C, ldc, cs, tiles_n, ntiles, vec4, dummy);
+    launch_bf16p<16, 4, TC>(s, grid, (int)Mp, (int)N, (int)K, A, lda, P, NP, bias != nullptr,
+                            beta, C, ldc, cs, tiles_n, ntiles, vec, dummy);
   GNNEA_LAUNCH_CHECK();
+  if (Mp < M)  // the last row (its own launch; no workspace: no split-K)
+    return gemm_bf16_t<TC>(0, trans_b, 1, N, K, A + Mp * lda, lda, B, ldb, bias, beta,
+                           C + Mp * ldc, ldc, nullptr, 0, s, cs);
   return 0;
 }
 
@@ -759,7 +869,7 @@ template <typename TC>
 static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                        const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
                        const float* bias, float beta, TC* C, int64_t ldc, void* ws,
-                       int64_t ws_bytes, hipStream_t s, int64_t cs = 128) {
+                       int64_t ws_bytes, hipStream_t s, int64_t cs) {
   if (bf16p_applies(trans_a, M, N, K, lda, A) && ws && ws_bytes >= bf16p_planes_bytes(N, K))
     return gemm_bf16p<TC>(trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, ws, s);
   const int wt = bf16_wt(N);
@@ -816,11 +926,11 @@ extern "C" int gnnea_gemm_bf16(int trans_a, int trans_b, int64_t M, int64_t N, i
   if (c_dtype == GNNEA_BF16)
     return gemm_bf16_t<bf16_t>(trans_a, trans_b, M, N, K, (const bf16_t*)A, lda,
                                (const bf16_t*)B, ldb, bias, beta, (bf16_t*)C, ldc, ws, ws_bytes,
-                               s);
+                               s, 128);
   if (c_dtype == GNNEA_F32)
     return gemm_bf16_t<float>(trans_a, trans_b, M, N, K, (const bf16_t*)A, lda,
                               (const bf16_t*)B, ldb, bias, beta, (float*)C, ldc, ws, ws_bytes,
-                              s);
+                              s, 128);
   return GNNEA_EINVAL;
 }
 
