@@ -777,12 +777,16 @@ static bool bf16p_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t 
   return bf16p_on() && !trans_a && M >= 65536 && N > 128 && N <= 4096 && K > 0 && K % 2 == 0 &&
          lda % 2 == 0 && (((uintptr_t)A) & 3) == 0;
 }
+// column tile of k_gemm_bf16p: 32 * 5 = 160 columns (a 320-wide tile that reads A once at
+// N = 300 needs 160 accumulator registers per lane: at two waves per SIMD it spilled to scratch,
+// 36 ms at 4M x 300 x 300 against 2.2 ms)
+constexpr int kBf16pWT = 5;
 static int64_t bf16p_planes_bytes(int64_t N, int64_t K) {  // + a 2-KB dummy store target
-  const int64_t np = (N + 159) / 160 * 160, kp = (K + 3 + 31) / 32 * 32;
+  const int64_t np = (N + 319) / 320 * 320, kp = (K + 3 + 31) / 32 * 32;
   return ((np * kp * 2 + 255) & ~(int64_t)255) + 2048;
 }
 
-template <int AW, int NW, typename TC>
+template <int WT, int AW, int NW, typename TC>
 static void launch_bf16p(hipStream_t s, int grid, int M, int N, int K, const bf16_t* A,
                          int64_t lda, const bf16_t* P, int NP, int hb, float beta, TC* C,
                          int64_t ldc, int64_t cs, int tiles_n, int ntiles, int vec, TC* dummy) {
@@ -791,7 +795,7 @@ static void launch_bf16p(hipStream_t s, int grid, int M, int N, int K, const bf1
     return e ? atoi(e) : 0;
   }();
 #define GNNEA_BFP(MD)                                                                           \
-  hipLaunchKernelGGL((k_gemm_bf16p<5, AW, NW, TC, MD>), dim3(grid), dim3(64 * NW), 0, s, M, N,  \
+  hipLaunchKernelGGL((k_gemm_bf16p<WT, AW, NW, TC, MD>), dim3(grid), dim3(64 * NW), 0, s, M, N, \
                      K, A, lda, P, NP, hb, beta, C, ldc, cs, tiles_n, ntiles, vec, dummy)
   constexpr bool modes = std::is_same<TC, bf16_t>::value && AW == 16;
   if (modes && mode == 1) GNNEA_BFP(modes ? 1 : 0);
@@ -821,7 +825,8 @@ template <typename TC>
 static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t* A,
                       int64_t lda, const bf16_t* B, int64_t ldb, const float* bias, float beta,
                       TC* C, int64_t ldc, int64_t cs, void* ws, hipStream_t s) {
-  const int NP = (int)((N + 159) / 160 * 160), KP = (int)((K + 3 + 31) / 32 * 32);
+  constexpr int BN = 32 * kBf16pWT;
+  const int NP = (int)((N + BN - 1) / BN * BN), KP = (int)((K + 3 + 31) / 32 * 32);
   bf16_t* P = (bf16_t*)ws;
   TC* dummy = (TC*)((char*)ws + bf16p_planes_bytes(N, K) - 2048);
   {
@@ -837,7 +842,7 @@ static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
   const int over = (8 - (int)(K % 8)) % 8;
   const int64_t Mp = lda - K >= over ? M : M - 1;
   const int nw = bf16p_nw();
-  const int tiles_n = NP / 160;
+  const int tiles_n = NP / BN;
   const int64_t tm = (Mp + 32 * nw - 1) / (32 * nw);
   if (tm * tiles_n >= (1ll << 31)) return GNNEA_EINVAL;
   const int ntiles = (int)(tm * tiles_n);
@@ -853,11 +858,11 @@ static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
   const int vec = N % 4 == 0 && ldc % 4 == 0 && cs % 4 == 0 &&
                   (((uintptr_t)C) & (4 * sizeof(TC) - 1)) == 0;
   if (nw == 8)
-    launch_bf16p<16, 8, TC>(s, grid, (int)Mp, (int)N, (int)K, A, lda, P, NP, bias != nullptr,
-                            beta, C, ldc, cs, tiles_n, ntiles, vec, dummy);
+    launch_bf16p<5, 16, 8, TC>(s, grid, (int)Mp, (int)N, (int)K, A, lda, P, NP, bias != nullptr,
+                               beta, C, ldc, cs, tiles_n, ntiles, vec, dummy);
   else
-    launch_bf16p<16, 4, TC>(s, grid, (int)Mp, (int)N, (int)K, A, lda, P, NP, bias != nullptr,
-                            beta, C, ldc, cs, tiles_n, ntiles, vec, dummy);
+    launch_bf16p<5, 16, 4, TC>(s, grid, (int)Mp, (int)N, (int)K, A, lda, P, NP, bias != nullptr,
+                               beta, C, ldc, cs, tiles_n, ntiles, vec, dummy);
   GNNEA_LAUNCH_CHECK();
   if (Mp < M)  // the last row (its own launch; no workspace: no split-K)
     return gemm_bf16_t<TC>(0, trans_b, 1, N, K, A + Mp * lda, lda, B, ldb, bias, beta,

@@ -33,6 +33,10 @@ constexpr int kSweepWaves = 8;  // waves (rows per group) of a sweep workgroup
 // passes take over
 constexpr int kMaxJ = 64 * kSweepWaves * 32;
 constexpr int kMaxSweepWg = 64 * 8;  // column partials the update kernel sums in one round
+// the on-chip KNOPP kernel (k_sk_res): thread tile rows / columns, tile rows kept in VGPRs
+constexpr int kResRA = 9, kResCA = 16, kResRR = 5, kResLR = kResRA - kResRR;
+constexpr int kResRows = 16 * kResRA, kResCols = 16 * kResCA;  // 144 x 256 per workgroup
+constexpr int kResMaxWg = 256;
 
 enum { ST_DONE = 0, ST_ITERS = 1, ST_REASON = 2, ST_SLOT = 3, ST_BIG = 4, ST_FAIL = 5, ST_UFAIL = 6 };
 enum { SD_ERR = GNNEA_SK_SD_ERR, SD_TPREV = GNNEA_SK_SD_TPREV, SD_LOSS = GNNEA_SK_SD_LOSS,
@@ -53,10 +57,12 @@ static int sk_rows_per_wg(int I) {
 
 struct SkWs {
   int64_t K, u, v, pu, pv, rowbuf, part, errpart, total;
+  int64_t flags, rowpart, colpart, rowaux, colaux;  // the on-chip KNOPP path (k_sk_res)
   int ns, nfin, rpw;
 };
 
 constexpr int kFinCols = 16;  // columns per update workgroup (64 slots split the partials)
+constexpr int64_t kResFlagBytes = 4 * (2 * kResMaxWg + 64);  // rflag[256], cflag[256], entry counter
 
 static SkWs sk_plan(int I, int J) {
   SkWs w;
@@ -74,6 +80,14 @@ static SkWs sk_plan(int I, int J) {
   w.errpart = o; o = al256(o + 8ll * w.nfin);
   // + 64 KB: the wide sweep's unclamped loads run up to ~2,600 elements past the last row's end
   w.K = o; o = al256(o + 8ll * I * J + 65536);
+  // k_sk_res: flags (row / column phase epochs per workgroup, the entry counter) and the
+  // double-buffered row / column partials (sized for the largest grid, kResMaxWg workgroups)
+  const int P = div_up(I, kResRows), Q = div_up(J, kResCols);  // res_geom's grid
+  w.flags = o; o = al256(o + kResFlagBytes);
+  w.rowpart = o; o = al256(o + 8ll * 2 * Q * I);
+  w.colpart = o; o = al256(o + 8ll * 2 * P * J);
+  w.rowaux = o; o = al256(o + 8ll * 2 * 2 * kResMaxWg);
+  w.colaux = o; o = al256(o + 8ll * 2 * kResMaxWg);
   w.total = o;
   return w;
 }
@@ -91,6 +105,8 @@ struct SkDev {
   int64_t* st;   // status ints
   double* sd;    // status doubles
   double *K, *u, *v, *pu, *pv, *rowbuf, *part, *errpart;
+  double *rowpart, *colpart, *rowaux, *colaux;
+  unsigned *rflag, *cflag, *ecnt;
 };
 
 static SkDev sk_dev(const gnnea_sinkhorn* p) {
@@ -107,6 +123,13 @@ static SkDev sk_dev(const gnnea_sinkhorn* p) {
   d.rowbuf = (double*)(b + w.rowbuf);
   d.part = (double*)(b + w.part);
   d.errpart = (double*)(b + w.errpart);
+  d.rowpart = (double*)(b + w.rowpart);
+  d.colpart = (double*)(b + w.colpart);
+  d.rowaux = (double*)(b + w.rowaux);
+  d.colaux = (double*)(b + w.colaux);
+  d.rflag = (unsigned*)(b + w.flags);
+  d.cflag = d.rflag + kResMaxWg;
+  d.ecnt = d.rflag + 2 * kResMaxWg;
   return d;
 }
 
@@ -596,12 +619,400 @@ static void launch_sweep(const SkArgs& a, const SkDev& d, int it, int si, int so
     launch_sweep_pw<KNOPP, PH1, false>(a, d, it, si, so, yin, gate, s);
 }
 
+// ---------------------------------------------------------------------------------------- //
+// KNOPP with K resident ON CHIP (utils/ot_loss.py:50-66 at the EA batch, B = 3000 and alike).
+// At I * J <= ~9.4M the fp64 K fits the chip's registers + LDS: one workgroup per CU owns a
+// block of at most 144 rows x 256 columns (P row blocks x Q column blocks, P * Q <= #CUs), keeps
+// it in VGPRs (5 of 9 thread-tile rows) and LDS (the other 4) for a whole batch of iterations, and
+// one persistent launch runs the batch.  Thread t = (ra, cb) = (t >> 4, t & 15) holds rows
+// ra + 16 i (i < 9) and columns cb + 16 j (j < 16) of the block.  Per iteration `it`:
+//   1. v_it = b / (K^T u_{it-1}) for the block's columns: the P row blocks' column partials of
+//      K^T u_{it-1} summed in row-block order, and the err^2 terms of iterate it-1 (ot_loss.py:65);
+//   2. row partials s_i = sum_j K_ij v_j over the block's columns (16-lane DPP sums, fixed order);
+//   3. the Q column blocks' row partials summed in column-block order, u_it = 1 / ((1/a_i) s_i);
+//      the stop decisions of knopp_stop (err of it-1, K^T u == 0 / bad v) taken identically by
+//      every workgroup from the same published words;
+//   4. column partials sum_i K_ij u_i over the block's rows for step 1 of iteration it + 1.
+// K is read from HBM once per launch.  Hand-offs (cdna_hip_programming.md §6 Guideline 16, the
+// all-sc1 form): payload words stored and loaded write-through (agent-scope relaxed atomics =
+// global_store / global_load ... sc1), every storing wave drains (s_waitcnt vmcnt(0)), then a
+// workgroup barrier and ONE lane's sc1 flag store carrying the phase epoch (row partials of
+// iteration it: it + 1; column partials of iteration it: it + 2); a consumer's wave 0 polls the
+// flags of the workgroups it reads (>= epoch, bounded spin), the other waves load after a
+// workgroup barrier.  Payloads are double-buffered by iteration parity: a producer can run at
+// most one iteration ahead of any consumer of the same buffer (it needs that consumer's next
+// publication first).  Every spin is bounded (kResSpinTicks of the 100 MHz real-time counter):
+// a timed-out workgroup sets GNNEA_SK_ST_TIMEOUT, marks the loop done and exits, and its peers
+// time out in turn.  An entry barrier (monotonic arrival counter) separates every workgroup's read
+// of ST_DONE from any write of it in the same launch, so all workgroups take the same decision.
+// ---------------------------------------------------------------------------------------- //
+constexpr uint64_t kResSpinTicks = 25000000ull;  // 250 ms at 100 MHz
+enum { ST_TMO = GNNEA_SK_ST_TIMEOUT };
+
+typedef __attribute__((address_space(1))) double res_gd;
+typedef __attribute__((address_space(1))) unsigned int res_gu;
+
+struct ResGeom {
+  int P, Q, R, Cb;
+  bool ok;
+};
+
+static ResGeom res_geom(int I, int J) {
+  ResGeom g;
+  g.P = div_up(I, kResRows);
+  g.Q = div_up(J, kResCols);
+  g.R = div_up(I, g.P);
+  g.Cb = div_up(J, g.Q);
+  g.ok = (int64_t)g.P * g.Q <= kResMaxWg;
+  return g;
+}
+
+__device__ __forceinline__ void res_st(double* p, double x) {
+  __hip_atomic_store((res_gd*)p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double res_ld(const double* p) {
+  return __hip_atomic_load((res_gd*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned res_ldu(const unsigned* p) {
+  return __hip_atomic_load((res_gu*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void res_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// sum_{k < n} p[k * stride] in a fixed order (even / odd k, then the two), every load of a chunk
+// of 32 in flight at once: one round trip per chunk instead of one per partial
+__device__ __forceinline__ double res_sum_strided(const double* p, int64_t stride, int n) {
+  double s0 = 0.0, s1 = 0.0;
+  for (int k0 = 0; k0 < n; k0 += 32) {
+    double x[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) x[k] = k0 + k < n ? res_ld(p + (int64_t)(k0 + k) * stride) : 0.0;
+#pragma unroll
+    for (int k = 0; k < 32; k += 2) {
+      s0 += x[k];
+      s1 += x[k + 1];
+    }
+  }
+  return s0 + s1;
+}
+
+// one wave: until flags[base + k * stride] >= epoch for every k < n; false on timeout
+__device__ bool res_wait(const unsigned* flags, int base, int stride, int n, unsigned epoch) {
+  const int lane = lane_id();
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ok = true;
+    for (int k = lane; k < n; k += 64) ok &= res_ldu(flags + base + k * stride) >= epoch;
+    if (__all(ok)) return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kResSpinTicks) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__device__ __forceinline__ void res_timeout(SkDev& d) {
+  atomicOr((unsigned long long*)&d.st[ST_TMO], 1ull);
+  mark_done(d.st, 0, 3, 0);
+}
+
+// workgroup sum in a fixed order (lanes by DPP, then waves 0..3): the same value on every
+// workgroup that sums the same per-thread terms
+__device__ __forceinline__ double res_block_sum(double x, double* red4) {
+  x = wave_sum_f64(x);
+  __syncthreads();  // red4 may still be read by the previous call
+  if (lane_id() == 0) red4[wave_id()] = x;
+  __syncthreads();
+  return (red4[0] + red4[1]) + (red4[2] + red4[3]);
+}
+
+__global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g, int first,
+                                                   int count) {
+  // K rows kResRR..kResRA-1 of the thread tile, column pairs as one 16-B word per lane
+  __shared__ double2 klds[kResLR * (kResCA / 2) * 256];
+  __shared__ double vsh[kResCols], ush[kResRows], colred[4][kResCols];
+  __shared__ double red4[4], peer[kResMaxWg];
+  __shared__ int peerf[kResMaxWg];
+  __shared__ int sh_state;
+  const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+  const int ra = t >> 4, cb = t & 15;
+  const int wg = blockIdx.x, p = wg / g.Q, q = wg - (wg / g.Q) * g.Q;
+  const unsigned nwg = (unsigned)(g.P * g.Q);
+  const int r0 = p * g.R, c0 = q * g.Cb;
+  const int nr = max(0, min(g.R, a.I - r0)), nc = max(0, min(g.Cb, a.J - c0));
+  const int64_t J = a.J, I = a.I;
+  double* rowpart = d.rowpart;  // [2][Q][I]
+  double* colpart = d.colpart;  // [2][P][J]
+  double* rowaux = d.rowaux;    // [2][P*Q][2]: err^2 of the column block, bad-v flag
+  double* colaux = d.colaux;    // [2][P*Q]: bad-u flag of the row block
+  // -- the K block (zeros outside the matrix) --
+  double kr[kResRR][kResCA];
+#pragma unroll
+  for (int i = 0; i < kResRA; ++i) {
+    const int lr = ra + 16 * i;
+    const bool rok = lr < nr;
+    const double* Kr = d.K + (int64_t)(r0 + (rok ? lr : 0)) * J + c0;
+#pragma unroll
+    for (int j = 0; j < kResCA; j += 2) {
+      const int lc0 = cb + 16 * j, lc1 = lc0 + 16;
+      const double k0 = rok && lc0 < nc ? Kr[lc0] : 0.0;
+      const double k1 = rok && lc1 < nc ? Kr[lc1] : 0.0;
+      if (i < kResRR) {
+        kr[i][j] = k0;
+        kr[i][j + 1] = k1;
+      } else {
+        klds[((i - kResRR) * (kResCA / 2) + j / 2) * 256 + t] = make_double2(k0, k1);
+      }
+    }
+  }
+  const double inva = t < nr ? 1.0 / a.a[r0 + t] : 0.0;  // row t of the block (step 3)
+  const double bj = t < nc ? a.b[c0 + t] : 0.0;         // column t of the block (step 1)
+  double vprev = t < nc ? d.v[(int64_t)((first + 1) & 1) * J + c0 + t] : 0.0;  // v_{first-1}
+  // -- entry barrier: every workgroup reads ST_DONE before any can write it --
+  if (t == 0) {
+    const int64_t done = __hip_atomic_load(&d.st[ST_DONE], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    res_drain();
+    const unsigned v = __hip_atomic_fetch_add((res_gu*)d.ecnt, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    int st = done ? 1 : 0;
+    if (!st) {
+      const unsigned target = (v / nwg + 1) * nwg;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (res_ldu(d.ecnt) < target) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kResSpinTicks) {
+          st = 2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    sh_state = st;
+  }
+  __syncthreads();
+  if (sh_state) {
+    if (sh_state == 2 && t == 0) res_timeout(d);
+    return;
+  }
+
+  // column pass: colpart[par][p][c0 + c] = sum over the block's rows of K_rc u_r (ush), published
+  // with the block's bad-u flag under epoch ep
+  auto col_pass = [&](int par, unsigned ep, bool ufail) {
+    double u[kResRA];
+#pragma unroll
+    for (int i = 0; i < kResRA; ++i) u[i] = ush[ra + 16 * i];
+#pragma unroll
+    for (int j = 0; j < kResCA; j += 2) {
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int i = 0; i < kResRA; ++i) {
+        double k0, k1;
+        if (i < kResRR) {
+          k0 = kr[i][j];
+          k1 = kr[i][j + 1];
+        } else {
+          const double2 kk = klds[((i - kResRR) * (kResCA / 2) + j / 2) * 256 + t];
+          k0 = kk.x;
+          k1 = kk.y;
+        }
+        s0 = fma(u[i], k0, s0);
+        s1 = fma(u[i], k1, s1);
+      }
+      s0 += __shfl_xor(s0, 16, 64);
+      s1 += __shfl_xor(s1, 16, 64);
+      s0 += __shfl_xor(s0, 32, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      if (lane < 16) {
+        colred[w][cb + 16 * j] = s0;
+        colred[w][cb + 16 * (j + 1)] = s1;
+      }
+    }
+    __syncthreads();
+    if (t < nc)
+      res_st(colpart + ((int64_t)par * g.P + p) * J + c0 + t,
+             (colred[0][t] + colred[1][t]) + (colred[2][t] + colred[3][t]));
+    if (t == 0) res_st(colaux + (int64_t)par * nwg + wg, ufail ? 1.0 : 0.0);
+    res_drain();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store((res_gu*)(d.cflag + wg), ep, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  };
+
+  if (first == 0) {  // K^T u_0, u_0 = 1 / I (ot_loss.py:39), published as iteration -1
+    if (t < kResRows) ush[t] = t < nr ? 1.0 / (double)a.ig : 0.0;
+    __syncthreads();
+    col_pass(1, 1u, false);
+  }
+  for (int it = first; it < first + count; ++it) {
+    const int cur = it & 1, prv = cur ^ 1;
+    // 1. v_it from the column partials of iterate it-1 (wave 0 polls; then every load of the
+    //    step -- the partials and the row blocks' bad-u flags -- goes out in one round trip)
+    if (w == 0) {
+      const bool ok = res_wait(d.cflag, q, g.Q, g.P, (unsigned)(it + 1));
+      if (lane == 0) sh_state = ok ? 0 : 2;
+    }
+    __syncthreads();
+    if (sh_state) {
+      if (t == 0) res_timeout(d);
+      return;
+    }
+    double errp = 0.0, vj = 0.0;
+    bool vfail = false;
+    if (t < nc) {
+      const double s = res_sum_strided(colpart + (int64_t)prv * g.P * J + c0 + t, J, g.P);
+      const double tt = vprev * s - bj;  // err of iterate it-1 (ot_loss.py:65-66), s = K^T u_{it-1}
+      errp = tt * tt;
+      vj = bj / s;  // ot_loss.py:54
+      vfail = s == 0.0 || vj != vj || isinf(vj);
+    }
+    vsh[t] = vj;
+    if (w == 0) {
+      bool uf = false;
+      for (int k = lane; k < g.P; k += 64)
+        uf |= res_ld(colaux + (int64_t)prv * nwg + k * g.Q + q) != 0.0;
+      const bool any_uf = __any(uf);
+      if (lane == 0) sh_state = any_uf ? 1 : 0;  // iteration it-1 broke on u (marked by its rows)
+    }
+    const double err2_blk = res_block_sum(errp, red4);  // barriers: vsh and sh_state published
+    if (sh_state) return;
+    const bool vfail_blk = __syncthreads_or(vfail);
+    if (t < nc) {
+      if (p == 0) d.v[(int64_t)cur * J + c0 + t] = vj;
+      vprev = vj;
+    }
+    // 2. row partials over the block's columns
+    double acc[kResRA];
+#pragma unroll
+    for (int i = 0; i < kResRA; ++i) acc[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < kResCA; j += 2) {
+      const double v0 = vsh[cb + 16 * j], v1 = vsh[cb + 16 * (j + 1)];
+#pragma unroll
+      for (int i = 0; i < kResRA; ++i) {
+        double k0, k1;
+        if (i < kResRR) {
+          k0 = kr[i][j];
+          k1 = kr[i][j + 1];
+        } else {
+          const double2 kk = klds[((i - kResRR) * (kResCA / 2) + j / 2) * 256 + t];
+          k0 = kk.x;
+          k1 = kk.y;
+        }
+        acc[i] = fma(k0, v0, acc[i]);
+        acc[i] = fma(k1, v1, acc[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kResRA; ++i) {  // sum over the 16 lanes of a DPP row (same ra)
+      double x = acc[i];
+      x += mov_dpp_f64<0xB1>(x);
+      x += mov_dpp_f64<0x4E>(x);
+      x += mov_dpp_f64<0x141>(x);
+      x += mov_dpp_f64<0x140>(x);
+      const int lr = ra + 16 * i;
+      if (cb == 0 && lr < nr) res_st(rowpart + ((int64_t)cur * g.Q + q) * I + r0 + lr, x);
+    }
+    if (t == 0) {
+      res_st(rowaux + ((int64_t)cur * nwg + wg) * 2, err2_blk);
+      res_st(rowaux + ((int64_t)cur * nwg + wg) * 2 + 1, vfail_blk ? 1.0 : 0.0);
+    }
+    res_drain();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store((res_gu*)(d.rflag + wg), (unsigned)(it + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    // 3. the row block's partials; the stop decisions of knopp_stop, identical everywhere
+    if (w == 0) {
+      const bool ok = res_wait(d.rflag, p * g.Q, 1, g.Q, (unsigned)(it + 1));
+      if (lane == 0) sh_state = ok ? 0 : 2;
+    }
+    __syncthreads();
+    if (sh_state) {
+      if (t == 0) res_timeout(d);
+      return;
+    }
+    const double srow =
+        t < nr ? res_sum_strided(rowpart + (int64_t)cur * g.Q * I + r0 + t, I, g.Q) : 0.0;
+    if (w == 0) {
+      for (int k = lane; k < g.Q; k += 64) {
+        const double* ax = rowaux + ((int64_t)cur * nwg + p * g.Q + k) * 2;
+        peer[k] = res_ld(ax);
+        peerf[k] = res_ld(ax + 1) != 0.0;
+      }
+      if (lane == 0) {
+        double e2 = 0.0;
+        bool vf = false;
+        int st = 0;
+        for (int k = 0; k < g.Q; ++k) {  // column-block order: every workgroup the same sum
+          vf |= peerf[k] != 0;
+          e2 += peer[k];
+        }
+        const int prev = it - 1;
+        if (prev >= 0 && prev % 10 == 0) {
+          const double err = sqrt(e2);
+          if (wg == 0) d.sd[SD_ERR] = err;
+          if (!(err > d.sd[SD_TOL])) {
+            st = 1;
+            if (wg == 0) mark_done(d.st, prev + 1, 1, prev & 1);
+          }
+        }
+        if (!st && vf) {
+          st = 1;
+          if (wg == 0) mark_done(d.st, it, 2, (it + 1) & 1);
+        }
+        sh_state = st;
+      }
+    }
+    __syncthreads();
+    if (sh_state) return;
+    bool ufail = false;
+    if (t < kResRows) {
+      double u = 0.0;
+      if (t < nr) {
+        u = 1.0 / (inva * srow);  // u = 1 / (Kp v), Kp = (1/a) K   (ot_loss.py:45, :55)
+        ufail = u != u || isinf(u);
+        if (q == 0) d.u[(int64_t)cur * I + r0 + t] = u;
+      }
+      ush[t] = u;
+    }
+    const bool ufail_blk = __syncthreads_or(ufail);
+    if (ufail_blk && t == 0) mark_done(d.st, it, 2, (it + 1) & 1);  // every later step stops
+    // 4. column partials of K^T u_it for iteration it + 1
+    col_pass(cur, (unsigned)(it + 2), ufail_blk);
+  }
+}
+
+// the on-chip path serves KNOPP (variant 0, unsharded) when the blocks fit the device's CUs
+// (GNNEA_SK_RESIDENT=0 disables it, for A/B measurements)
+static int res_num_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  return n;
+}
+
+static bool res_applies(const gnnea_sinkhorn* p) {
+  if (p->mode != GNNEA_SK_KNOPP || p->variant != 0 || p->J > kMaxJ) return false;
+  const char* e = getenv("GNNEA_SK_RESIDENT");
+  if (e && e[0] == '0') return false;
+  const ResGeom g = res_geom(p->I, p->J);
+  return g.ok && g.P * g.Q <= res_num_cus();
+}
+
+static int res_launch(const gnnea_sinkhorn* p, int first, int count, hipStream_t s) {
+  SkArgs a = sk_args(p);
+  SkDev d = sk_dev(p);
+  ResGeom g = res_geom(p->I, p->J);
+  void* args[] = {&a, &d, &g, &first, &count};
+  // cooperative: the runtime rejects a grid that cannot be resident at once
+  GNNEA_HIP(hipLaunchCooperativeKernel((const void*)k_sk_res, dim3(g.P * g.Q), dim3(256), args, 0,
+                                       s));
+  return 0;
+}
+
 template <typename T>
 static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t s) {
   const SkArgs a = sk_args(p);
   const SkDev d = sk_dev(p);
   const dim3 grow(div_up(p->I, 4)), gfin(a.nfin);
   const bool knopp = p->mode == GNNEA_SK_KNOPP;
+  if (res_applies(p)) return res_launch(p, first, count, s);
   for (int it = first; it < first + count; ++it) {
     const int cur = it & 1, prev = cur ^ 1;
     if (knopp) {
@@ -834,7 +1245,11 @@ extern "C" int gnnea_sinkhorn_init(const gnnea_sinkhorn* p, void* stream) {
     else
       hipLaunchKernelGGL((k_sk_kbuild<double, true>), grow, dim3(256), 0, s,
                          (const double*)p->C, a, d, 0, p->max_iter, 1);
-    launch_sweep<true, false>(a, d, 0, 1, 1, d.u + p->I, 0, s);  // K^T u0, u0 = 1/I (slot 1)
+    if (res_applies(p)) {  // k_sk_res computes K^T u0 itself; its flags start at 0
+      if (hipMemsetAsync(d.rflag, 0, kResFlagBytes, s) != hipSuccess) return GNNEA_EINVAL;
+    } else {
+      launch_sweep<true, false>(a, d, 0, 1, 1, d.u + p->I, 0, s);  // K^T u0, u0 = 1/I (slot 1)
+    }
   } else {  // K0 with zero potentials and transport = sum K0 . C   (sinkhorn_loss.py:193-195)
     if (f32)
       hipLaunchKernelGGL((k_sk_kbuild<float, false>), grow, dim3(256), 0, s, (const float*)p->C,

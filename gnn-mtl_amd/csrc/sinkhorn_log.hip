@@ -141,18 +141,71 @@ __device__ __forceinline__ void mark_done(int64_t* st, int64_t iters, int64_t re
   }
 }
 
+// exp(x) of the LSE terms (x <= 0, -inf for a masked term, NaN kept NaN) by the 64-entry table
+// 2^(j/64) (exactly rounded, in LDS: lse_table) and a degree-5 polynomial on |r| <= ln2 / 128:
+//   x = (64 t' + j) ln2/64 + r,  exp(x) = 2^t' * 2^(j/64) * (1 + (e^r - 1)),
+// truncation r^6 / 720 < 3.5e-17, about 1 ulp in all -- 14 fp64 operations against exp_f64's 19,
+// the inner-loop cost of both LSE passes (2 I J exponentials per iteration).
+__device__ const double kExp2Tab64[64] = {
+    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
+    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
+    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
+    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
+    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
+    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
+    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
+    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
+    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
+    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
+    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
+    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
+    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
+    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
+    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
+    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951};
+
+struct LseTable {
+  double t[64];
+};
+// every thread of the workgroup calls it (a barrier inside)
+__device__ __forceinline__ const double* lse_table(LseTable& sh) {
+  if (threadIdx.x < 64) sh.t[threadIdx.x] = kExp2Tab64[threadIdx.x];
+  __syncthreads();
+  return sh.t;
+}
+
+__device__ __forceinline__ double exp_tab(double x, const double* __restrict__ tab) {
+  constexpr double kInvL = 92.33248261689366;         // 64 / ln 2
+  constexpr double kLHi = 0.010830424696249145;       // ln 2 / 64, high part
+  constexpr double kLLo = 3.623510646634843e-19;      // ln 2 / 64 - kLHi
+  const double xc = fmax(x, -1.0e4);  // -inf -> -1e4: 2^-14427 underflows to 0 below
+  const double t = __builtin_rint(xc * kInvL);
+  double r = __builtin_fma(-t, kLHi, xc);
+  r = __builtin_fma(-t, kLLo, r);
+  const int ti = (int)t;
+  double p = __builtin_fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  p = __builtin_fma(p, r, 1.0 / 6.0);
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  p *= r;  // e^r - 1
+  const double tj = tab[ti & 63];
+  const double y = __builtin_ldexp(__builtin_fma(tj, p, tj), ti >> 6);
+  return x != x ? x : y;
+}
+
 // Chunked, branch-free online LSE: per chunk of CH values one rescale exp + one exp per value
 // (a per-element "if (x > m)" diverges across lanes and costs two exps per element).
 template <int CH>
-__device__ __forceinline__ void lse_chunk(Lse& l, const double (&x)[CH]) {
+__device__ __forceinline__ void lse_chunk(Lse& l, const double (&x)[CH],
+                                          const double* __restrict__ tab) {
   double cm = x[0];
 #pragma unroll
   for (int k = 1; k < CH; ++k) cm = fmax(cm, x[k]);
   if (cm == -INFINITY) return;  // whole chunk masked (K == 0)
   const double nm = fmax(l.m, cm);
-  double acc = l.m == -INFINITY ? 0.0 : l.s * exp_f64(l.m - nm);
+  double acc = l.m == -INFINITY ? 0.0 : l.s * exp_tab(l.m - nm, tab);
 #pragma unroll
-  for (int k = 0; k < CH; ++k) acc += exp_f64(x[k] - nm);  // exp_f64(-inf) == 0
+  for (int k = 0; k < CH; ++k) acc += exp_tab(x[k] - nm, tab);  // exp_tab(-inf) == 0
   l.m = nm;
   l.s = acc;
 }
@@ -218,6 +271,8 @@ __global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs 
   if (d.st[ST_DONE]) return;
   if (KNOPP && knopp_stop(d, it)) return;
   __shared__ double wm[4], ws[4];
+  __shared__ LseTable tab_sh;
+  const double* tab = lse_table(tab_sh);
   const int w = wave_id(), lane = lane_id();
   const int i = blockIdx.x * (4 / WPR) + w / WPR;
   const int t = (w % WPR) * 64 + lane;  // thread index inside the row's team
@@ -240,7 +295,7 @@ __global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs 
           x[k] = sk_term<KNOPP>(uai, vj, (double)Ci[j], a.inv_eps, a.kclamp, g[j] - vj);
         }
       }
-      lse_chunk<CH>(l, x);
+      lse_chunk<CH>(l, x, tab);
     }
   }
   l = wave_lse(l);
@@ -288,6 +343,8 @@ __global__ __launch_bounds__(1024) void k_sk_col_fused(const T* __restrict__ C, 
   if (d.st[ST_DONE]) return;
   constexpr int RG = 1024 / COLS;
   __shared__ double sm[RG][COLS], ss[RG][COLS];
+  __shared__ LseTable tab_sh;
+  const double* tab = lse_table(tab_sh);
   const int c = threadIdx.x % COLS, rg = threadIdx.x / COLS;
   const int j = blockIdx.x * COLS + c;
   const double* __restrict__ f = d.f + (int64_t)slot_f * a.I;
@@ -308,7 +365,7 @@ __global__ __launch_bounds__(1024) void k_sk_col_fused(const T* __restrict__ C, 
                                 f[i] - ui);
         }
       }
-      lse_chunk<CH>(l, x);
+      lse_chunk<CH>(l, x, tab);
     }
   }
   sm[rg][c] = l.m;
@@ -348,6 +405,8 @@ __global__ __launch_bounds__(1024) void k_sk_col_part(const T* __restrict__ C, S
                                                       int slot_f, int rows_per_split) {
   if (d.st[ST_DONE]) return;
   __shared__ double sm[16][64], ss[16][64];
+  __shared__ LseTable tab_sh;
+  const double* tab = lse_table(tab_sh);
   const int lane = lane_id(), w = wave_id();
   const int j = blockIdx.x * 64 + lane;
   const int r0 = blockIdx.y * rows_per_split, r1 = min(a.I, r0 + rows_per_split);
@@ -369,7 +428,7 @@ __global__ __launch_bounds__(1024) void k_sk_col_part(const T* __restrict__ C, S
                                 f[i] - ui);
         }
       }
-      lse_chunk<CH>(l, x);
+      lse_chunk<CH>(l, x, tab);
     }
   }
   sm[w][lane] = l.m;

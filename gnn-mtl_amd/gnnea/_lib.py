@@ -29,6 +29,7 @@ GNNEA_SK_STAB = 1
 GNNEA_SK_GEN = 2
 GNNEA_SK_RELAX = 3
 GNNEA_SK_STATUS_BYTES = 256
+GNNEA_SK_ST_TIMEOUT = 16  # status word: an inter-workgroup wait of k_sk_res timed out
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32

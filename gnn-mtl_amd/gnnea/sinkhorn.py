@@ -37,6 +37,9 @@ def _status(ws):
     raw = ws[:_lib.GNNEA_SK_STATUS_BYTES].cpu()  # sync point between batches
     ints = raw.view(torch.int64)
     dbl = raw.view(torch.float64)
+    if int(ints[_lib.GNNEA_SK_ST_TIMEOUT]):
+        raise RuntimeError("gnnea.sinkhorn: a wait between the workgroups of the on-chip KNOPP "
+                           "kernel timed out (results invalid)")
     return ints, dbl
 
 
@@ -212,6 +215,8 @@ def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.fl
     for k, (plan, row_sum, col_sum) in enumerate(results):
         ints = raw[k].view(torch.int64)
         dbl = raw[k].view(torch.float64)
+        if int(ints[_lib.GNNEA_SK_ST_TIMEOUT]):
+            raise RuntimeError("gnnea.sinkhorn: an inter-workgroup wait timed out (problem %d)" % k)
         out.append(SinkhornResult(plan, row_sum, col_sum, int(ints[ST_ITERS]),
                                   int(ints[ST_REASON]), float(dbl[SD_ERR]), float(dbl[SD_TNEW]),
                                   float(dbl[SD_TPREV]), float(dbl[SD_LOSS])))

@@ -415,6 +415,8 @@ int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64
 #define GNNEA_SK_ST_ITERS 1      /* reference's final iteration counter (cpt / ii) */
 #define GNNEA_SK_ST_REASON 2     /* 0 running/max-iter, 1 tolerance, 2 numerical-error break */
 #define GNNEA_SK_ST_SLOT 3       /* ping-pong slot holding the final scalings */
+#define GNNEA_SK_ST_TIMEOUT 16   /* nonzero: a wait between the workgroups of the on-chip KNOPP
+                                    kernel timed out (the loop was stopped; results invalid) */
 #define GNNEA_SK_STATUS_BYTES 256
 /* double words (indices into the block viewed as doubles) */
 #define GNNEA_SK_SD_ERR 8        /* KNOPP: last err = ||v * (K^T u) - b|| */

@@ -27,6 +27,13 @@ import scipy.sparse as sp
 import torch
 
 TAU = 1e-5
+# elements whose relu branch was taken from the tested output (|pre| inside the rounding band),
+# and all relu elements evaluated: reported by the BASELINE-size tests
+BAND = {"band": 0, "total": 0}
+
+
+def reset_band():
+    BAND["band"] = BAND["total"] = 0
 
 
 class LocalGraph:
@@ -69,6 +76,8 @@ def _relu_hybrid(pre, gpu_rows, tau=TAU):
         mask = pre > 0
         if gpu_rows is not None:
             mask = torch.where(band, torch.as_tensor(gpu_rows).double() > 0, mask)
+            BAND["band"] += int(band.sum())
+            BAND["total"] += band.numel()
     return pre * mask.to(pre.dtype)
 
 

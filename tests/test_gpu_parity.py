@@ -261,11 +261,16 @@ def test_gemm_vs_fp64(device, shape, ta, tb):
 # ------------------------------------------------------------------------------------------ #
 # a9-a12: Sinkhorn family vs the reference fixtures                                           #
 # ------------------------------------------------------------------------------------------ #
-@pytest.fixture(params=[0, 1], ids=["scaling", "logdomain"])
+@pytest.fixture(params=["onchip", "sweep", "logdomain"])
 def sk_path(request, monkeypatch):
-    """Run a Sinkhorn test through both device paths (resident-K scaling form, log domain)."""
+    """Run a Sinkhorn test through every device path."""
     import gnnea.sinkhorn
-    monkeypatch.setattr(gnnea.sinkhorn, "DEFAULT_VARIANT", request.param)
+    # onchip: KNOPP with K held in registers + LDS by the persistent k_sk_res where it fits
+    # (STAB family and larger problems take the sweep); sweep: GNNEA_SK_RESIDENT=0, the
+    # resident-K sweep for every mode; logdomain: variant 1
+    monkeypatch.setattr(gnnea.sinkhorn, "DEFAULT_VARIANT", 1 if request.param == "logdomain" else 0)
+    if request.param == "sweep":
+        monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
     return request.param
 
 
@@ -334,6 +339,71 @@ def test_sinkhorn_vs_oracle_random(device):
         assert abs(loss.item() - lo) <= TOL64 * abs(lo)
 
 
+@pytest.mark.parametrize("I,J,reg,tol", [(1, 1, 0.1, 1e-9), (3, 5, 0.1, 1e-9),
+                                         (144, 256, 0.05, 1e-9), (145, 257, 0.05, 1e-12),
+                                         (1000, 1000, 0.01, 1e-9), (3000, 3000, 0.01, 1e-9),
+                                         (5000, 1500, 0.02, 1e-10), (700, 9000, 0.02, 1e-9)])
+def test_sinkhorn_onchip_matches_sweep(device, monkeypatch, I, J, reg, tol):
+    """The persistent on-chip KNOPP kernel (k_sk_res: K in registers + LDS, workgroups exchanging
+    row / column partials inside one launch per batch) against the resident-K sweep and the fp64
+    oracle: same stop iteration and reason, plan and loss at 1e-12 (the two sum in different
+    orders), over block shapes at and past the 144 x 256 tile, grids of 1 to 252 workgroups and
+    solves spanning several launches (the host's batches 2, 10, 20, ...)."""
+    from gnnea import sinkhorn as gsk
+    from gnnea import _lib
+    from oracle import sinkhorn as osk
+    rng = np.random.default_rng(I * 7 + J)
+    M = rng.uniform(0, 1, (I, J))
+    a = rng.uniform(0.5, 1.5, I)
+    b = rng.uniform(0.5, 1.5, J)
+    b *= a.sum() / b.sum()
+    Mt, at, bt = (torch.from_numpy(x).to(device) for x in (M, a, b))
+    res = {}
+    for path in ("onchip", "sweep"):
+        if path == "sweep":
+            monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
+        res[path] = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, reg, tol, 400)
+    r0, r1 = res["onchip"], res["sweep"]
+    assert (r0.iters, r0.reason) == (r1.iters, r1.reason), ((r0.iters, r0.reason),
+                                                            (r1.iters, r1.reason))
+    assert rel_err(r0.plan.cpu(), r1.plan.cpu()) < 1e-12
+    assert abs(r0.loss - r1.loss) <= 1e-12 * abs(r1.loss)
+    # err = ||v (K^T u) - b||: absolute rounding ~1e-16 ||b|| once converged
+    assert abs(r0.err - r1.err) <= 1e-9 * abs(r1.err) + 1e-12 * float(np.linalg.norm(b))
+    if I * J <= 1_000_000:
+        Po, lo, _, _ = osk.knopp(a, b, M, reg, 400, stop_thr=tol)
+        assert rel_err(r0.plan.cpu(), Po) < TOL64
+        assert abs(r0.loss - lo) <= TOL64 * abs(lo)
+
+
+def test_sinkhorn_onchip_bad_u_break(device):
+    """k_sk_res's numerical-error break on u (ot_loss.py:57-62: a row of K underflows to 0, so
+    Kp v = 0 and u = inf at iteration 0): the same iteration count, reason and reverted plan as
+    the sweep path."""
+    import os
+    from gnnea import sinkhorn as gsk
+    from gnnea import _lib
+    rng = np.random.default_rng(3)
+    I, J = 600, 500
+    M = rng.uniform(0, 1, (I, J))
+    M[17] = 50.0  # exp(-50 / 0.05) underflows: K row 17 is 0
+    a, b = np.ones(I), np.ones(J) * I / J
+    Mt, at, bt = (torch.from_numpy(x).to(device) for x in (M, a, b))
+    out = []
+    for env in ("1", "0"):
+        os.environ["GNNEA_SK_RESIDENT"] = env
+        try:
+            out.append(gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, 0.05, 1e-9, 50))
+        finally:
+            os.environ.pop("GNNEA_SK_RESIDENT", None)
+    r0, r1 = out
+    assert (r0.iters, r0.reason) == (r1.iters, r1.reason) and r0.reason == 2, \
+        ((r0.iters, r0.reason), (r1.iters, r1.reason))
+    assert torch.equal(torch.isfinite(r0.plan), torch.isfinite(r1.plan))
+    f = torch.isfinite(r1.plan)
+    assert rel_err(r0.plan[f].cpu(), r1.plan[f].cpu()) < 1e-12
+
+
 def test_spmm_beta_accumulate(device):
     from gnnea import ops
     from gnnea.graph import DeviceCSR
@@ -352,11 +422,13 @@ def test_spmm_beta_accumulate(device):
 
 
 @pytest.mark.parametrize("world", [4, 8])
-def test_shard_own_remote_split_on_device(device, world):
-    """The multi-GPU aggregation (owned block from the local rows, the rest from the halo,
-    accumulated with beta = 1) reproduces the single-GPU rows, per rank, on one device."""
+def test_shard_slice_pipeline_on_device(device, world):
+    """The row-shard aggregation as the multi-GPU path runs it (gnnea.dist.KGShard.aggregate,
+    gnnea.dist_graph.DistAdj.staged_aggregate): the KG's 64-column slice tables, slice q
+    aggregated over the shard's CSR (KG-local columns) into the output's column block, per rank
+    on one device (the halo filled locally); equal to the single-GPU rows."""
     from gnnea import ops, synth
-    from gnnea.dist import Partition, shard_coo, split_own_remote
+    from gnnea.dist import Partition, shard_coo
     from gnnea.graph import DeviceCSR
     n, t = 800, 3000
     tr = synth.kg_pair_triples(n, t, 50)
@@ -368,14 +440,13 @@ def test_shard_own_remote_split_on_device(device, world):
     for rank in range(world):
         p = Partition(n, rank, world)
         r, c, v = shard_coo(tr, n, t, p)
-        (ro, co, vo), (rr, cr, vr) = split_own_remote(r, c, v, p)
-        up = lambda a, b, w, nc: DeviceCSR.from_coo(  # noqa: E731
-            torch.from_numpy(a).to(device), torch.from_numpy(b).to(device),
-            torch.from_numpy(w).to(device), p.n_rows, nc)
-        h_kg = H[p.kg * n:(p.kg + 1) * n]
-        h_local = h_kg[p.row0:p.row1]
-        y = ops.spmm(up(ro, co, vo, p.n_rows), h_local, 0)
-        ops.spmm(up(rr, cr, vr, n), h_kg, 1, out=y, beta=1.0)
+        csr = DeviceCSR.from_coo(torch.from_numpy(r).to(device), torch.from_numpy(c).to(device),
+                                 torch.from_numpy(v).to(device), p.n_rows, n)
+        tables = ops.slice_pack(H[p.kg * n:(p.kg + 1) * n])
+        y = torch.empty(p.n_rows, 300, device=device)
+        for q in range(tables.shape[0]):
+            c0, c1 = 64 * q, min(300, 64 * q + 64)
+            ops.spmm_sliced(csr, tables[q:q + 1], c1 - c0, 1, out=y[:, c0:c1])
         g0 = p.global_row0
         assert rel_err(y.cpu(), ref[g0:g0 + p.n_rows]) < TOL32
 

@@ -134,10 +134,15 @@ def test_dbp15k_ea_step_vs_reference(golden, device, dbp, model):
         assert rel_err(m.decoder.cls[2].linear.weight.grad.cpu(), dW64.cpu()) < TOL32
 
 
-@pytest.fixture(params=[0, 1], ids=["scaling", "logdomain"])
+@pytest.fixture(params=["onchip", "sweep", "logdomain"])
 def sk_path(request, monkeypatch):
     import gnnea.sinkhorn
-    monkeypatch.setattr(gnnea.sinkhorn, "DEFAULT_VARIANT", request.param)
+    # onchip: KNOPP with K held in registers + LDS by the persistent k_sk_res where it fits
+    # (STAB family and larger problems take the sweep); sweep: GNNEA_SK_RESIDENT=0, the
+    # resident-K sweep for every mode; logdomain: variant 1
+    monkeypatch.setattr(gnnea.sinkhorn, "DEFAULT_VARIANT", 1 if request.param == "logdomain" else 0)
+    if request.param == "sweep":
+        monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
     return request.param
 
 

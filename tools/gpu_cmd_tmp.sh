@@ -1,5 +1,9 @@
 set -o pipefail
 mkdir -p gpurun_out
-rm -rf gpurun_out/prof_cfg5
-timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cfg5 -o run --output-format csv -- python tools/dist_step.py --model GAT --entities 2000000 --dtype bf16 --steps 3 --warmup 1 > gpurun_out/prof_cfg5.log 2>&1 || { tail -20 gpurun_out/prof_cfg5.log; exit 1; }
-find gpurun_out/prof_cfg5 -name "*kernel_stats.csv"
+export TMPDIR=/tmp
+T="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+timeout -k 10 300 $T -x tests/test_gpu_parity.py -k "onchip" > gpurun_out/t_skres.log 2>&1 || { grep -E "FAIL|Error|assert|Timeout" gpurun_out/t_skres.log | head -30; tail -5 gpurun_out/t_skres.log; exit 1; }
+tail -1 gpurun_out/t_skres.log
+timeout -k 10 200 python tools/sk_bench.py 3000 1000
+timeout -k 10 400 $T -x tests/test_gpu_parity.py tests/test_gpu_scale_dbp15k.py -k "sinkhorn" > gpurun_out/t_sk.log 2>&1 || { grep -E "FAIL|Error|assert|Timeout" gpurun_out/t_sk.log | head -30; tail -5 gpurun_out/t_sk.log; exit 1; }
+tail -1 gpurun_out/t_sk.log

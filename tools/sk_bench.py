@@ -1,0 +1,20 @@
+"""Sinkhorn iters/s at the EA batch through each KNOPP device path (A/B of k_sk_res vs the
+resident-K sweep): python tools/sk_bench.py [B ...]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import bench  # noqa: E402
+import torch  # noqa: E402
+
+dev = torch.device("cuda", 0)
+for B in [int(x) for x in sys.argv[1:]] or [3000]:
+    for env in ("1", "0"):
+        os.environ["GNNEA_SK_RESIDENT"] = env
+        r = bench.sinkhorn_rate(dev, B=B)
+        print(json.dumps({"B": B, "onchip": env == "1", **r["iters_per_s"]}), flush=True)
+if os.environ.get("SK_LOG"):
+    os.environ["GNNEA_SK_RESIDENT"] = "1"
+    r = bench.sinkhorn_rate(dev, B=15000, n0=20, n1=120, variant=1)
+    print(json.dumps({"B": 15000, "logdomain": True, **r["iters_per_s"]}), flush=True)
