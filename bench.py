@@ -88,7 +88,7 @@ def sinkhorn_rate(device, B=3000, reg=0.01, n0=100, n1=1100, variant=None):
     Y = 0.05 * torch.randn(B, 300, generator=g)
     M = torch.cdist(X, Y)
     M = (M / M.max()).to(device)
-    out = {}
+    out, paths = {}, {}
     # ot_loss.sinkhorn as models_ea.py:217 calls it (a = b = ones); sinkhorn_iteration with the
     # uniform marginals mu = nu = 1/B
     for name, mode, w in (("ot_loss.sinkhorn", _lib.GNNEA_SK_KNOPP, 1.0),
@@ -109,7 +109,8 @@ def sinkhorn_rate(device, B=3000, reg=0.01, n0=100, n1=1100, variant=None):
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         out[name] = round((n1 - n0) / (ts[1] - ts[0]), 1)
-    return {"iters_per_s": out, "B": B, "reg": reg, "dtype": "f64 (C fp32/fp64)",
+        paths[name] = res.path
+    return {"iters_per_s": out, "B": B, "reg": reg, "dtype": "f64 (C fp32/fp64)", "path": paths,
             "method": "marginal (T(%d)-T(%d))/%d incl. the host's look-ahead status reads"
                       % (n1, n0, n1 - n0)}
 
@@ -121,7 +122,7 @@ def sinkhorn_large(device):
     B = 15000
     r = sinkhorn_rate(device, B=B, n0=20, n1=120)
     k_bytes = B * B * 8
-    r["path"] = "scaling form, fp64 K resident (k_sk_sweep, wide: column scaling in LDS)"
+    r["kernels"] = "scaling form, fp64 K resident in HBM (k_sk_sweep, wide: column scaling in LDS)"
     r["bytes_per_iter"] = k_bytes
     r["GBps_knopp"] = round(r["iters_per_s"]["ot_loss.sinkhorn"] * k_bytes / 1e9, 1)
     r["bound"] = ("HBM: the K stream (%.2f GB per iteration; %.0f iters/s at 8 TB/s)"

@@ -12,7 +12,9 @@ namespace gnnea {
 
 constexpr int kDaBlocks = 256, kDaWaves = 16;
 
-template <int NCH, typename T>
+// HH: the head count when it is 4 (one 16-B load of a row's ds, broadcast to the wave, and a
+// per-element select of its lane's head), 0 = any (one ds load per element)
+template <int NCH, typename T, int HH>
 __global__ __launch_bounds__(64 * kDaWaves) void k_gat_da_part(const typename Vec4<T>::raw* __restrict__ H,
                                                      int64_t ldh4, int64_t n_rows, int heads,
                                                      int d_head, int D4,
@@ -35,12 +37,24 @@ __global__ __launch_bounds__(64 * kDaWaves) void k_gat_da_part(const typename Ve
   }
   auto fma_row = [&](int64_t r, const float4 (&h)[NCH]) {
     const float* dr = ds + r * heads;
+    if constexpr (HH == 4) {  // r is wave-uniform: one 16-B load, selects per element
+      const float4 d4 = *(const float4*)dr;
+      auto sel = [&](int k) { return k == 0 ? d4.x : (k == 1 ? d4.y : (k == 2 ? d4.z : d4.w)); };
 #pragma unroll
-    for (int q = 0; q < NCH; ++q) {
-      acc[q].x = fmaf(dr[hd[q][0]], h[q].x, acc[q].x);
-      acc[q].y = fmaf(dr[hd[q][1]], h[q].y, acc[q].y);
-      acc[q].z = fmaf(dr[hd[q][2]], h[q].z, acc[q].z);
-      acc[q].w = fmaf(dr[hd[q][3]], h[q].w, acc[q].w);
+      for (int q = 0; q < NCH; ++q) {
+        acc[q].x = fmaf(sel(hd[q][0]), h[q].x, acc[q].x);
+        acc[q].y = fmaf(sel(hd[q][1]), h[q].y, acc[q].y);
+        acc[q].z = fmaf(sel(hd[q][2]), h[q].z, acc[q].z);
+        acc[q].w = fmaf(sel(hd[q][3]), h[q].w, acc[q].w);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NCH; ++q) {
+        acc[q].x = fmaf(dr[hd[q][0]], h[q].x, acc[q].x);
+        acc[q].y = fmaf(dr[hd[q][1]], h[q].y, acc[q].y);
+        acc[q].z = fmaf(dr[hd[q][2]], h[q].z, acc[q].z);
+        acc[q].w = fmaf(dr[hd[q][3]], h[q].w, acc[q].w);
+      }
     }
   };
   auto load_row = [&](int64_t r, float4 (&h)[NCH]) {
@@ -129,10 +143,15 @@ static int gat_da_t(const T* H, int64_t ldh, int64_t n_rows, int heads, int d_he
   if (!ws || ws_bytes < (int64_t)nb * Dp * 4) return GNNEA_EWORKSPACE;
   float* part = (float*)ws;
   typedef typename Vec4<T>::raw R;
+  const bool h4 = heads == 4 && (((uintptr_t)ds) & 15) == 0;
 #define GNNEA_DA(N)                                                                            \
   case N:                                                                                      \
-    hipLaunchKernelGGL((k_gat_da_part<N, T>), dim3(nb), dim3(64 * kDaWaves), 0, s, (const R*)H, ldh / 4,  \
-                       n_rows, heads, d_head, D4, ds, part);                                   \
+    if (h4)                                                                                    \
+      hipLaunchKernelGGL((k_gat_da_part<N, T, 4>), dim3(nb), dim3(64 * kDaWaves), 0, s,        \
+                         (const R*)H, ldh / 4, n_rows, heads, d_head, D4, ds, part);           \
+    else                                                                                       \
+      hipLaunchKernelGGL((k_gat_da_part<N, T, 0>), dim3(nb), dim3(64 * kDaWaves), 0, s,        \
+                         (const R*)H, ldh / 4, n_rows, heads, d_head, D4, ds, part);           \
     break;
   switch (nch) {
     GNNEA_DA(1)

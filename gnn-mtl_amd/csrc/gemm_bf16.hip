@@ -870,11 +870,215 @@ static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
   return 0;
 }
 
+// ---- k_gemm_bf16w: the projection form with the weight RESIDENT in LDS and the activations
+// streamed straight into registers (no LDS staging, no barrier in the k-loop).  For the cfg-5
+// shapes (K <= 320, a 160-column weight tile = 97 KB bf16 fits the LDS) the product is computed
+// transposed, D^T = W_tile . A^T on v_mfma_f32_32x32x16_bf16: the weight tile is the MFMA's A
+// operand (ds_read_b128 from the resident image), 32 activation rows per wave are its B operand
+// (one 16-B global load per lane per k-step), and a lane's accumulators come out as runs of 4
+// consecutive output COLUMNS of one row -- stored as 8-B (bf16) / 16-B (fp32) pieces straight
+// from registers.  The k dimension is permuted (A and W alike): lanes of k-half kh hold k in
+// [kh Kh + 8 s, +8) at step s, Kh = 8 kc, so each lane streams one contiguous run of its row.
+// One wave per SIMD (512 registers): the next tile's activations (kc fragments) are in flight
+// while the current tile is multiplied.  Workgroup b owns column tile (b / 8) % ntn and the row
+// stream of the blocks b and b + 8 * (ntn - 1)... (so the column tiles of the same rows run on
+// one XCD, sharing its L2 for the activations).
+constexpr int kBwCols = 160, kBwKC = 20;  // column tile, max k-steps (K <= 320)
+
+__global__ __launch_bounds__(256) void k_pack_bf16w(const bf16_t* __restrict__ B, int64_t ldb,
+                                                    int b_nk, int N, int K, int kc, int ntn,
+                                                    bf16_t* __restrict__ P) {
+  // P[nt][s][kh][n][8]: element e = W_op[nt*160 + n][kh*8kc + 8s + e] (zero outside)
+  const int64_t total = (int64_t)ntn * kc * 2 * kBwCols * 8;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(t & 7);
+    int64_t r = t >> 3;
+    const int n = (int)(r % kBwCols);
+    r /= kBwCols;
+    const int kh = (int)(r & 1);
+    r >>= 1;
+    const int s = (int)(r % kc);
+    const int nt = (int)(r / kc);
+    const int col = nt * kBwCols + n, k = kh * 8 * kc + 8 * s + e;
+    bf16_t v = 0;
+    if (col < N && k < K) v = b_nk ? B[(int64_t)col * ldb + k] : B[(int64_t)k * ldb + col];
+    P[t] = v;
+  }
+}
+
+template <typename TC, int KC>
+__global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int ntn,
+                                                      const bf16_t* __restrict__ A, int64_t lda,
+                                                      const bf16_t* __restrict__ P,
+                                                      const float* __restrict__ bias,
+                                                      TC* __restrict__ C, int64_t ldc,
+                                                      int64_t cs) {
+  __shared__ __attribute__((aligned(16))) uint4 wl[KC * 2 * kBwCols];  // [s][kh][n] x 16 B
+  // the tile's bias in LDS: a global load in the epilogue would wait (vmcnt counts in order)
+  // for the next tile's activation loads issued before it
+  __shared__ __attribute__((aligned(16))) float bsh[kBwCols];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kh = lane >> 5, li = lane & 31;
+  const int b = blockIdx.x;
+  const int nt = (b / 8) % ntn;
+  const int rs = (b / (8 * ntn)) * 8 + b % 8, nrs = (int)gridDim.x / ntn;
+  const int n0 = nt * kBwCols;
+  constexpr int Kh = 8 * KC;
+  {  // the resident weight tile
+    const uint4* src = (const uint4*)(P + (int64_t)nt * KC * 2 * kBwCols * 8);
+    for (int i = tid; i < KC * 2 * kBwCols; i += 256) wl[i] = src[i];
+    if (tid < kBwCols) bsh[tid] = bias && n0 + tid < N ? bias[n0 + tid] : 0.f;
+  }
+  __syncthreads();
+  const int tm = (M + 127) / 128;  // 128-row tiles: 4 waves x 32 rows
+  // one k-step fragment of the lane's row: 8 bf16 at k = kh Kh + 8 s.  Only the last two steps
+  // of the upper half can reach K (K > 16 (KC - 1)); there a chunk holding K is read as the 16 B
+  // ending at K (in bounds, K even) and shifted down by words, a chunk past K is zero.
+  auto issue = [&](uint4 (&f)[KC], int rt) {
+    const bf16_t* p = A + (int64_t)min(rt * 128 + w * 32 + li, M - 1) * lda + kh * Kh;
+#pragma unroll
+    for (int s = 0; s < KC - 2; ++s) f[s] = *(const uint4*)(p + 8 * s);
+#pragma unroll
+    for (int s = KC - 2; s < KC; ++s) {
+      const int k0 = kh * Kh + 8 * s;
+      if (k0 + 8 <= K) {
+        f[s] = *(const uint4*)(p + 8 * s);
+      } else if (k0 >= K) {
+        f[s] = make_uint4(0, 0, 0, 0);
+      } else {
+        const uint4 v = *(const uint4*)(p + (K - 8 - kh * Kh));
+        const int sh = (k0 + 8 - K) >> 1;  // 1..3 words
+        f[s] = make_uint4(sh == 1 ? v.y : (sh == 2 ? v.z : v.w), sh == 1 ? v.z : (sh == 2 ? v.w : 0u),
+                          sh == 1 ? v.w : 0u, 0u);
+      }
+    }
+  };
+  const uint4* wlane = wl + kh * kBwCols + li;  // + (2 s) * 160 + 32 t
+  auto compute_store = [&](const uint4 (&f)[KC], int rt) {
+    f32x16_b acc[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+    uint4 wc[5], wn[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) wc[t] = wlane[32 * t];
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      if (s + 1 < KC) {  // the next step's weight fragments in flight under this step's MFMAs
+#pragma unroll
+        for (int t = 0; t < 5; ++t) wn[t] = wlane[(2 * (s + 1)) * kBwCols + 32 * t];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 x = __builtin_bit_cast(bf16x8, f[s]);
+#pragma unroll
+      for (int t = 0; t < 5; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wc[t]), x,
+                                                         acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 5; ++t) wc[t] = wn[t];
+    }
+    // lane: output row m, columns n0 + 32 t + 8 g + 4 kh + (0..3) = acc[t][4 g .. 4 g + 3]
+    const int m = rt * 128 + w * 32 + li;
+    if (m >= M) return;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + 32 * t + 8 * g + 4 * kh;
+        if (n < N) {  // N % 4 == 0: a group is wholly in or out
+          float4 o = make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2],
+                                 acc[t][4 * g + 3]);
+          const float4 bv = *(const float4*)(bsh + (n - n0));
+          o.x += bv.x; o.y += bv.y; o.z += bv.z; o.w += bv.w;
+          TC* c = C + c_index_bf(m, n, ldc, cs);
+          if constexpr (std::is_same<TC, bf16_t>::value) {
+            *(uint2*)c = make_uint2((uint32_t)f32_to_bf16(o.x) | ((uint32_t)f32_to_bf16(o.y) << 16),
+                                    (uint32_t)f32_to_bf16(o.z) | ((uint32_t)f32_to_bf16(o.w) << 16));
+          } else {
+            *(float4*)c = o;
+          }
+        }
+      }
+    }
+  };
+  uint4 fa[KC], fb[KC];
+  int rt = rs;
+  if (rt < tm) issue(fa, rt);
+  while (rt < tm) {
+    const int r1 = rt + nrs;
+    if (r1 < tm) issue(fb, r1);
+    compute_store(fa, rt);
+    if (r1 >= tm) break;
+    const int r2 = r1 + nrs;
+    if (r2 < tm) issue(fa, r2);
+    compute_store(fb, r1);
+    rt = r2;
+  }
+}
+
+static bool bf16w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda,
+                          const void* A) {
+  const char* e = getenv("GNNEA_BF16_WRES");  // A/B comparison only (=0: k_gemm_bf16p)
+  const bool on = !(e && e[0] == '0');
+  // instantiated for 19 and 20 k-steps of 16 (K in (288, 320]: the 300-wide cfg-5 products)
+  return on && !trans_a && M >= 65536 && N > 128 && N <= 4096 && N % 4 == 0 && K > 288 &&
+         K <= 16 * kBwKC && K % 2 == 0 && lda % 2 == 0 && (((uintptr_t)A) & 3) == 0;
+}
+static int bf16w_kc(int64_t K) { return (int)(((K + 7) / 8 + 1) / 2); }
+static int64_t bf16w_planes_bytes(int64_t N, int64_t K) {
+  const int64_t ntn = (N + kBwCols - 1) / kBwCols;
+  return ntn * bf16w_kc(K) * 2 * kBwCols * 16;
+}
+
+template <typename TC>
+static int gemm_bf16w(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t* A,
+                      int64_t lda, const bf16_t* B, int64_t ldb, const float* bias, TC* C,
+                      int64_t ldc, int64_t cs, void* ws, hipStream_t s) {
+  const int kc = bf16w_kc(K), ntn = (int)((N + kBwCols - 1) / kBwCols);
+  bf16_t* P = (bf16_t*)ws;
+  {
+    const int64_t tot = (int64_t)ntn * kc * 2 * kBwCols * 8;
+    const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
+    hipLaunchKernelGGL(k_pack_bf16w, dim3(nb), dim3(256), 0, s, B, ldb, trans_b ? 1 : 0, (int)N,
+                       (int)K, kc, ntn, P);
+    GNNEA_LAUNCH_CHECK();
+  }
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  // persistent grid: a multiple of 8 * ntn workgroups (column tiles of a row stream 8 apart)
+  const int unit = 8 * ntn;
+  const int64_t tm = (M + 127) / 128;
+  int grid = ncu / unit * unit;
+  if (grid < unit) grid = unit;
+  if ((int64_t)grid / ntn > tm) grid = (int)((tm + 7) / 8 * 8 * ntn);
+  if (kc == 19)
+    hipLaunchKernelGGL((k_gemm_bf16w<TC, 19>), dim3(grid), dim3(256), 0, s, (int)M, (int)N,
+                       (int)K, ntn, A, lda, P, bias, C, ldc, cs);
+  else
+    hipLaunchKernelGGL((k_gemm_bf16w<TC, 20>), dim3(grid), dim3(256), 0, s, (int)M, (int)N,
+                       (int)K, ntn, A, lda, P, bias, C, ldc, cs);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
 template <typename TC>
 static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                        const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
                        const float* bias, float beta, TC* C, int64_t ldc, void* ws,
                        int64_t ws_bytes, hipStream_t s, int64_t cs) {
+  // (beta != 0: the old C would be loaded behind the next tile's activations: k_gemm_bf16p)
+  if (beta == 0.f && bf16w_applies(trans_a, M, N, K, lda, A) && ws &&
+      ws_bytes >= bf16w_planes_bytes(N, K) && ldc % 4 == 0 && cs % 4 == 0 &&
+      (((uintptr_t)C) & (4 * sizeof(TC) - 1)) == 0)
+    return gemm_bf16w<TC>(trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, cs, ws, s);
   if (bf16p_applies(trans_a, M, N, K, lda, A) && ws && ws_bytes >= bf16p_planes_bytes(N, K))
     return gemm_bf16p<TC>(trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, ws, s);
   const int wt = bf16_wt(N);
@@ -912,7 +1116,8 @@ using namespace gnnea;
 extern "C" int64_t gnnea_gemm_bf16_ws_bytes(int64_t M, int64_t N, int64_t K) {
   if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
   const int64_t split = bf16_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
-  const int64_t planes = bf16p_planes_bytes(N, K);  // k_gemm_bf16p (shape-dependent use)
+  int64_t planes = bf16p_planes_bytes(N, K);  // k_gemm_bf16p / k_gemm_bf16w (shape-dependent)
+  if (bf16w_planes_bytes(N, K) > planes) planes = bf16w_planes_bytes(N, K);
   return split > planes ? split : planes;
 }
 

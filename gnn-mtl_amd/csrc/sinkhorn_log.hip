@@ -33,7 +33,7 @@ constexpr double kLnTrueMin = -744.4400719213812;     // log(DBL_TRUE_MIN)
 constexpr double kExpOverflow = 709.782712893384;     // exp_f64(x) == inf above
 
 struct SkWs {
-  int64_t f, g, ua, va, rowbuf, errpart, part_m, part_s, la, lb, total;
+  int64_t f, g, ua, va, rowbuf, errpart, part_m, part_s, la, lb, fs, gs, total;
   int ncb;
 };
 
@@ -55,6 +55,8 @@ static SkWs sk_plan(int I, int J) {
   w.part_s = o; o = al256(o + 8ll * kMaxSplits * J);
   w.la = o; o = al256(o + 8ll * I);
   w.lb = o; o = al256(o + 8ll * J);
+  w.fs = o; o = al256(o + 2 * 8ll * I);  // KNOPP fast path: f, g in units of ln2 / 64
+  w.gs = o; o = al256(o + 2 * 8ll * J);
   w.total = o;
   return w;
 }
@@ -63,6 +65,7 @@ struct SkDev {
   int64_t* st;   // status ints
   double* sd;    // status doubles (sd[8] ...)
   double *f, *g, *ua, *va, *rowbuf, *errpart, *pm, *ps;
+  double *fs, *gs;  // f, g scaled by 64 / ln 2 (KNOPP fast path)
   int ncb;  // errpart slots written by the column pass of the active variant
 };
 
@@ -80,11 +83,16 @@ static SkDev sk_dev(const gnnea_sinkhorn* p) {
   d.errpart = (double*)(b + w.errpart);
   d.pm = (double*)(b + w.part_m);
   d.ps = (double*)(b + w.part_s);
+  d.fs = (double*)(b + w.fs);
+  d.gs = (double*)(b + w.gs);
   d.ncb = w.ncb;
   return d;
 }
 
 enum { ST_DONE = 0, ST_ITERS = 1, ST_REASON = 2, ST_SLOT = 3, ST_BIG = 4, ST_FAIL = 5 };
+// set by init when C holds a non-finite value: the KNOPP passes then keep the NaN-propagating
+// natural-unit terms instead of the scaled fast path (whose clamp would hide a NaN)
+enum { ST_CNAN = 17 };
 enum { SD_ERR = GNNEA_SK_SD_ERR, SD_TPREV = GNNEA_SK_SD_TPREV, SD_LOSS = GNNEA_SK_SD_LOSS,
        SD_TOL = GNNEA_SK_SD_TOL, SD_TNEW = GNNEA_SK_SD_TNEW };
 
@@ -210,6 +218,55 @@ __device__ __forceinline__ void lse_chunk(Lse& l, const double (&x)[CH],
   l.s = acc;
 }
 
+// KNOPP fast path: terms in units of ln2 / 64 (x~ = x * 64 / ln 2), so the table exponential
+// needs no range-reduction multiply: t = rint(x~), r = x~ - t (exact), 2^(x~/64) =
+// 2^(t >> 6) * 2^((t & 63) / 64) * e^(r ln2/64), |r ln2 / 64| <= ln2 / 128 as in exp_tab.  A term
+// x~ = fma(k, 64 / ln 2, g~) replaces k + g: 13 VALU per exponential against exp_tab's 17 (NaN
+// guard and reduction multiply gone; C was checked finite by init, ST_CNAN).
+constexpr double kScale = 92.33248261689366;     // 64 / ln 2
+constexpr double kUnscale = 0.010830424696249145;  // ln 2 / 64
+__device__ __forceinline__ double exp2t(double xs, const double* __restrict__ tab) {
+  constexpr double c1 = 0.010830424696249145, c2 = 5.86490495505617e-05,
+                   c3 = 2.1173137155464776e-07, c4 = 5.732851688640402e-10,
+                   c5 = 1.2417843701716925e-12;  // (ln2/64)^k / k!
+  const double xc = fmax(xs, -1.0e6);  // -inf -> 2^-15625: 0 below
+  const double t = __builtin_rint(xc);
+  const double r = xc - t;
+  const int ti = (int)t;
+  double p = __builtin_fma(r, c5, c4);
+  p = __builtin_fma(p, r, c3);
+  p = __builtin_fma(p, r, c2);
+  p = __builtin_fma(p, r, c1);
+  p *= r;  // e^(r ln2/64) - 1
+  const double tj = tab[ti & 63];
+  return __builtin_ldexp(__builtin_fma(tj, p, tj), ti >> 6);
+}
+
+// lse_chunk on scaled terms (l.m scaled too until lse_unscale)
+template <int CH>
+__device__ __forceinline__ void lse2_chunk(Lse& l, const double (&x)[CH],
+                                           const double* __restrict__ tab) {
+  double cm = x[0];
+#pragma unroll
+  for (int k = 1; k < CH; ++k) cm = fmax(cm, x[k]);
+  if (cm == -INFINITY) return;
+  const double nm = fmax(l.m, cm);
+  double acc = l.m == -INFINITY ? 0.0 : l.s * exp2t(l.m - nm, tab);
+#pragma unroll
+  for (int k = 0; k < CH; ++k) acc += exp2t(x[k] - nm, tab);
+  l.m = nm;
+  l.s = acc;
+}
+__device__ __forceinline__ void lse_unscale(Lse& l) {
+  if (l.m != -INFINITY) l.m *= kUnscale;
+}
+
+// KNOPP scaled term: -inf where K_ij underflows (the same test on k as sk_term)
+__device__ __forceinline__ double sk_term_s(double c, double inv_eps, double pot_s) {
+  const double k = -c * inv_eps;
+  return k < kExpUnderflow ? -INFINITY : __builtin_fma(k, kScale, pot_s);
+}
+
 // logit of the reference's K_ij * scaling: -inf where K_ij underflows to 0 in fp64
 template <bool KNOPP>
 __device__ __forceinline__ double sk_term(double ua, double va, double c, double inv_eps,
@@ -255,6 +312,7 @@ __device__ __forceinline__ void finish_row(const SkArgs& a, SkDev& d, int i, Lse
   double la = a.p_row * (a.la[i] - ls);
   if (knopp) {
     d.f[(int64_t)slot_out * a.I + i] = la;  // u = 1/(Kp v)
+    d.fs[(int64_t)slot_out * a.I + i] = la * kScale;
     if (!(la <= kExpOverflow)) mark_done(d.st, it, 2, (it + 1) & 1);  // u inf / NaN
   } else {
     if (la > kLn1e30) la = kLn1e30;  // a = clamp(., 0, 1e30)
@@ -279,7 +337,32 @@ __global__ __launch_bounds__(256) void k_sk_row(const T* __restrict__ C, SkArgs 
   constexpr int NT = 64 * WPR;
   Lse l;
   l.init();
-  if (i < a.I) {
+  if (KNOPP && !d.st[ST_CNAN]) {  // fast path (uniform): scaled terms, unmasked full chunks
+    if (i < a.I) {
+      const double* __restrict__ gs = d.gs + (int64_t)slot_in * a.J;
+      const T* __restrict__ Ci = C + (int64_t)i * a.ldc;
+      int j0 = 0;
+      for (; j0 + NT * CH <= a.J; j0 += NT * CH) {
+        double x[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+          const int j = j0 + NT * k + t;
+          x[k] = sk_term_s((double)Ci[j], a.inv_eps, gs[j]);
+        }
+        lse2_chunk<CH>(l, x, tab);
+      }
+      if (j0 < a.J) {
+        double x[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+          const int j = j0 + NT * k + t;
+          x[k] = j < a.J ? sk_term_s((double)Ci[j], a.inv_eps, gs[j]) : -INFINITY;
+        }
+        lse2_chunk<CH>(l, x, tab);
+      }
+      lse_unscale(l);
+    }
+  } else if (i < a.I) {
     const double* __restrict__ g = d.g + (int64_t)slot_in * a.J;
     const double* __restrict__ va = d.va;
     const double uai = KNOPP ? 0.0 : d.ua[i];
@@ -325,6 +408,7 @@ __device__ __forceinline__ void finish_col(const SkArgs& a, SkDev& d, int j, dou
     const double gj = a.lb[j] - ls;
     fail = fail || !(gj <= kExpOverflow);  // v inf / NaN   (:58-59)
     d.g[(int64_t)slot_g_out * a.J + j] = gj;
+    d.gs[(int64_t)slot_g_out * a.J + j] = gj * kScale;
   } else {
     double lb = a.p_col * (a.lb[j] - ls);
     if (lb > kLn1e30) lb = kLn1e30;
@@ -351,7 +435,22 @@ __global__ __launch_bounds__(1024) void k_sk_col_fused(const T* __restrict__ C, 
   const double* __restrict__ ua = d.ua;
   Lse l;
   l.init();
-  if (j < a.J) {
+  if (KNOPP && !d.st[ST_CNAN]) {  // fast path: scaled terms
+    if (j < a.J) {
+      const double* __restrict__ fs = d.fs + (int64_t)slot_f * a.I;
+      for (int i0 = rg; i0 < a.I; i0 += RG * CH) {
+        double x[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+          const int i = i0 + RG * k;
+          x[k] = i < a.I ? sk_term_s((double)C[(int64_t)i * a.ldc + j], a.inv_eps, fs[i])
+                         : -INFINITY;
+        }
+        lse2_chunk<CH>(l, x, tab);
+      }
+      lse_unscale(l);
+    }
+  } else if (j < a.J) {
     const double vaj = KNOPP ? 0.0 : d.va[j];
     for (int i0 = rg; i0 < a.I; i0 += RG * CH) {
       double x[CH];
@@ -414,7 +513,32 @@ __global__ __launch_bounds__(1024) void k_sk_col_part(const T* __restrict__ C, S
   const double* __restrict__ ua = d.ua;
   Lse l;
   l.init();
-  if (j < a.J) {
+  if (KNOPP && !d.st[ST_CNAN]) {  // fast path: scaled terms, unmasked full chunks
+    if (j < a.J) {
+      const double* __restrict__ fs = d.fs + (int64_t)slot_f * a.I;
+      int i0 = r0 + w;
+      for (; i0 + 16 * (CH - 1) < r1; i0 += 16 * CH) {
+        double x[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+          const int i = i0 + 16 * k;
+          x[k] = sk_term_s((double)C[(int64_t)i * a.ldc + j], a.inv_eps, fs[i]);
+        }
+        lse2_chunk<CH>(l, x, tab);
+      }
+      if (i0 < r1) {
+        double x[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+          const int i = i0 + 16 * k;
+          x[k] = i < r1 ? sk_term_s((double)C[(int64_t)i * a.ldc + j], a.inv_eps, fs[i])
+                        : -INFINITY;
+        }
+        lse2_chunk<CH>(l, x, tab);
+      }
+      lse_unscale(l);
+    }
+  } else if (j < a.J) {
     const double vaj = KNOPP ? 0.0 : d.va[j];
     for (int i0 = r0 + w; i0 < r1; i0 += 16 * CH) {
       double x[CH];
@@ -535,6 +659,19 @@ __global__ __launch_bounds__(1024) void k_sk_absorb_final(SkArgs a, SkDev d, int
   if (it == max_iter - 1) mark_done(d.st, max_iter, 0, slot);
 }
 
+// ST_CNAN: does C hold a NaN or an infinity (KNOPP: the passes then take the exact terms)
+template <typename T>
+__global__ __launch_bounds__(256) void k_sk_cscan(const T* __restrict__ C, int I, int J,
+                                                  int64_t ldc, int64_t* st) {
+  bool bad = false;
+  const int64_t n = (int64_t)I * J;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int64_t i = e / J, j = e - i * J;
+    bad |= !isfinite((double)C[i * ldc + j]);
+  }
+  if (__any(bad) && lane_id() == 0) atomicOr((unsigned long long*)&st[ST_CNAN], 1ull);
+}
+
 __global__ void k_sk_logw(const double* __restrict__ wa, const double* __restrict__ wb, int I,
                           int J, double* __restrict__ la, double* __restrict__ lb) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -555,11 +692,13 @@ __global__ void k_sk_init(SkArgs a, SkDev d, double tol) {
     d.ua[i] = 0.0;
     d.f[i] = 0.0;
     d.f[a.I + i] = knopp ? -log((double)a.I) : 0.0;
+    d.fs[a.I + i] = knopp ? -log((double)a.I) * kScale : 0.0;
   }
   for (int j = t; j < a.J; j += gridDim.x * blockDim.x) {
     d.va[j] = 0.0;
     d.g[j] = 0.0;
     d.g[a.J + j] = knopp ? -log((double)a.J) : 0.0;
+    d.gs[a.J + j] = knopp ? -log((double)a.J) * kScale : 0.0;
   }
 }
 
@@ -776,6 +915,17 @@ int init(const gnnea_sinkhorn* p, void* stream) {
   hipLaunchKernelGGL(k_sk_init, dim3(div_up(n > 32 ? n : 32, 256)), dim3(256), 0, s, a, d,
                      p->tol);
   GNNEA_LAUNCH_CHECK();
+  if (p->mode == GNNEA_SK_KNOPP) {
+    const int nb = div_up((int64_t)p->I * p->J, 256) < 2048 ? div_up((int64_t)p->I * p->J, 256)
+                                                             : 2048;
+    if (p->c_dtype == GNNEA_F32)
+      hipLaunchKernelGGL(k_sk_cscan<float>, dim3(nb), dim3(256), 0, s, (const float*)p->C, p->I,
+                         p->J, p->ldc, d.st);
+    else
+      hipLaunchKernelGGL(k_sk_cscan<double>, dim3(nb), dim3(256), 0, s, (const double*)p->C,
+                         p->I, p->J, p->ldc, d.st);
+    GNNEA_LAUNCH_CHECK();
+  }
   if (p->mode != GNNEA_SK_KNOPP) {  // initial transport = sum K0 . C   (sinkhorn_loss.py:195)
     const dim3 grow(div_up(p->I, 4));
     if (p->c_dtype == GNNEA_F32)

@@ -29,6 +29,7 @@ GNNEA_SK_STAB = 1
 GNNEA_SK_GEN = 2
 GNNEA_SK_RELAX = 3
 GNNEA_SK_STATUS_BYTES = 256
+GNNEA_SK_PATH_SWEEP, GNNEA_SK_PATH_ONCHIP, GNNEA_SK_PATH_LOG = 0, 1, 2
 GNNEA_SK_ST_TIMEOUT = 16  # status word: an inter-workgroup wait of k_sk_res timed out
 
 _p = ctypes.c_void_p
@@ -185,6 +186,7 @@ SIGNATURES = {
                                                 _i64, _p, _i64, _p, _f32, _p, _i64, _p, _i64,
                                                 _p]),
     "gnnea_sinkhorn_ws_bytes": (_i64, [ctypes.c_int, ctypes.c_int]),
+    "gnnea_sinkhorn_path": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem)]),
     "gnnea_sinkhorn_init": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), _p]),
     "gnnea_sinkhorn_iterate": (ctypes.c_int, [ctypes.POINTER(SinkhornProblem), ctypes.c_int,
                                               ctypes.c_int, _p]),

@@ -99,6 +99,7 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
     pp = ctypes.byref(prob)
     st = stream_of(dev)
     with _lib.on_device(dev):
+        path = L.gnnea_sinkhorn_path(pp)
         check(L.gnnea_sinkhorn_init(pp, st))
         run = 0
         # The device decides every stop itself (iterations past it are no-op launches), so the
@@ -140,9 +141,11 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
             pp, ptr(plan), _lib.GNNEA_F32 if plan_dtype == torch.float32 else _lib.GNNEA_F64,
             J, ptr(row_sum), ptr(col_sum), st))
         ints, dbl = _status(ws)
-    return SinkhornResult(plan, row_sum, col_sum, int(ints[ST_ITERS]), int(ints[ST_REASON]),
-                          float(dbl[SD_ERR]), float(dbl[SD_TNEW]), float(dbl[SD_TPREV]),
-                          float(dbl[SD_LOSS]))
+    res = SinkhornResult(plan, row_sum, col_sum, int(ints[ST_ITERS]), int(ints[ST_REASON]),
+                         float(dbl[SD_ERR]), float(dbl[SD_TNEW]), float(dbl[SD_TPREV]),
+                         float(dbl[SD_LOSS]))
+    res.path = ("sweep", "onchip", "logdomain")[path]  # gnnea_sinkhorn_path
+    return res
 
 
 def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64, batch=10,

@@ -455,6 +455,16 @@ int gnnea_sinkhorn_iterate(const gnnea_sinkhorn* prob, int first, int count, voi
  * block. */
 int gnnea_sinkhorn_finish(const gnnea_sinkhorn* prob, void* plan, int plan_dtype, int64_t ldp,
                           double* row_sum, double* col_sum, void* stream);
+/* which device path gnnea_sinkhorn_* take for this problem on the current device (host-side
+ * query, no launch): GNNEA_SK_PATH_SWEEP -- the scaling form streaming the resident fp64 K
+ * (k_sk_sweep); GNNEA_SK_PATH_ONCHIP -- KNOPP with K held in registers + LDS by one persistent
+ * launch per batch (k_sk_res: I x J fits P x Q <= #CUs blocks of 144 x 256); GNNEA_SK_PATH_LOG --
+ * the log-domain passes (variant 1 or J > 16384).  GNNEA_SK_RESIDENT=0 in the environment
+ * disables the on-chip path (A/B measurements).  Negative on an invalid problem. */
+#define GNNEA_SK_PATH_SWEEP 0
+#define GNNEA_SK_PATH_ONCHIP 1
+#define GNNEA_SK_PATH_LOG 2
+int gnnea_sinkhorn_path(const gnnea_sinkhorn* prob);
 
 /* §8e. KNOPP (utils/ot_loss.py:5-76) with the cost rows sharded over W ranks (rank r holds a
  * contiguous block of rows, rank order = row order).  `prob` is the rank's own problem: I = its

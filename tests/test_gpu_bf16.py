@@ -168,14 +168,20 @@ def test_gemm_bf16_vs_fp64(device, shape, ta, tb):
 
 
 @pytest.mark.parametrize("M,N,K", [(70001, 300, 300), (65536, 256, 256), (131077, 600, 300),
-                                   (66000, 200, 64), (65600, 300, 30)])
+                                   (66000, 200, 64), (65600, 300, 30), (65536, 164, 290),
+                                   (66000, 320, 320), (65601, 300, 298)])
 @pytest.mark.parametrize("tb", [0, 1])
-def test_gemm_bf16_pipelined_vs_fp64(device, M, N, K, tb):
-    """The tall projection form on k_gemm_bf16p (persistent LDS-DMA ring; M >= 64K): fp32 and
-    bf16 outputs vs fp64 of the same bf16 operands, the bias joined exactly (three bf16 terms
-    against A's ones), 4-B (K % 8 != 0) and 16-B (K % 8 == 0) A granules, ragged M / N, the
-    slice-major bf16 output and beta accumulation."""
+@pytest.mark.parametrize("wres", ["1", "0"])
+def test_gemm_bf16_pipelined_vs_fp64(device, monkeypatch, M, N, K, tb, wres):
+    """The tall projection form (M >= 64K): with K in (288, 320] and N % 4 == 0 on
+    k_gemm_bf16w (the weight tile resident in LDS, activations streamed into registers, the
+    transposed product stored from registers; wres=1), otherwise -- and with
+    GNNEA_BF16_WRES=0 -- on k_gemm_bf16p (persistent LDS-DMA ring, the bias joined exactly as
+    three bf16 terms against A's ones, 4-B / 16-B A granules).  fp32 and bf16 outputs vs fp64 of
+    the same bf16 operands, ragged M / N, K tails inside a 16-B chunk (290, 298), the slice-major
+    bf16 output and beta accumulation."""
     from gnnea import ops
+    monkeypatch.setenv("GNNEA_BF16_WRES", wres)
     rng = np.random.default_rng(M + N + K + tb)
     a = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32)).to(device).bfloat16()
     b = torch.from_numpy(rng.standard_normal((N, K) if tb else (K, N)).astype(np.float32))

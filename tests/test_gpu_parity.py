@@ -364,6 +364,7 @@ def test_sinkhorn_onchip_matches_sweep(device, monkeypatch, I, J, reg, tol):
             monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
         res[path] = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, reg, tol, 400)
     r0, r1 = res["onchip"], res["sweep"]
+    assert (r0.path, r1.path) == ("onchip", "sweep")
     assert (r0.iters, r0.reason) == (r1.iters, r1.reason), ((r0.iters, r0.reason),
                                                             (r1.iters, r1.reason))
     assert rel_err(r0.plan.cpu(), r1.plan.cpu()) < 1e-12
@@ -397,11 +398,37 @@ def test_sinkhorn_onchip_bad_u_break(device):
         finally:
             os.environ.pop("GNNEA_SK_RESIDENT", None)
     r0, r1 = out
+    assert (r0.path, r1.path) == ("onchip", "sweep")
     assert (r0.iters, r0.reason) == (r1.iters, r1.reason) and r0.reason == 2, \
         ((r0.iters, r0.reason), (r1.iters, r1.reason))
     assert torch.equal(torch.isfinite(r0.plan), torch.isfinite(r1.plan))
     f = torch.isfinite(r1.plan)
     assert rel_err(r0.plan[f].cpu(), r1.plan[f].cpu()) < 1e-12
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("-inf")])
+def test_sinkhorn_logdomain_nonfinite_cost(device, monkeypatch, bad):
+    """A NaN (or -inf) in M: the reference breaks at iteration 0 (K^T u has a NaN / inf, so v
+    does, ot_loss.py:57-62) and returns the initial scalings' plan.  The log-domain KNOPP
+    passes scan C at init and keep the NaN-propagating exact terms then (their scaled fast path
+    clamps -inf / NaN exponents): same stop iteration and reason as the scaling form, the same
+    plan where it is finite."""
+    from gnnea import sinkhorn as gsk
+    from gnnea import _lib
+    monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
+    rng = np.random.default_rng(8)
+    M = rng.uniform(0, 1, (300, 200))
+    M[7, 11] = bad
+    w = torch.ones(300, dtype=torch.float64, device=device)
+    wb = torch.full((200,), 1.5, dtype=torch.float64, device=device)
+    Mt = torch.from_numpy(M).to(device)
+    r0 = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, w, wb, 0.05, 1e-9, 50, variant=0)
+    r1 = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, w, wb, 0.05, 1e-9, 50, variant=1)
+    assert (r1.iters, r1.reason) == (r0.iters, r0.reason), ((r1.iters, r1.reason),
+                                                            (r0.iters, r0.reason))
+    f = torch.isfinite(r0.plan)
+    assert torch.equal(f, torch.isfinite(r1.plan))
+    assert rel_err(r1.plan[f].cpu(), r0.plan[f].cpu()) < 1e-12
 
 
 def test_spmm_beta_accumulate(device):

@@ -55,6 +55,7 @@ def main():
     ms = timeit(lambda: ops.gemm(X, W, trans_b=True, bias=b), args.reps)
     if args.only_fwd:
         print(json.dumps({"rows": M, "K": K, "pipe": os.environ.get("GNNEA_BF16_PIPE", "1"),
+                          "wres": os.environ.get("GNNEA_BF16_WRES", "1"),
                           "mode": os.environ.get("GNNEA_BF16P_MODE", "0"),
                           "gnnea_ms": round(ms, 4), "gnnea_GBps_io": round(io / ms / 1e6, 1),
                           "max_rel_err_vs_fp32": err}))
@@ -70,7 +71,7 @@ def main():
     ms_wt = timeit(lambda: torch.mm(dY.t(), X), args.reps)
     ms_x = timeit(lambda: ops.gemm(dY, W), args.reps)
     del dW
-    print(json.dumps({"rows": M, "epilogue": os.environ.get("GNNEA_BF16_EPI", "1"),
+    print(json.dumps({"rows": M, "wres": os.environ.get("GNNEA_BF16_WRES", "1"),
                       "pipe": os.environ.get("GNNEA_BF16_PIPE", "1"),
                       "dW_ms": round(ms_w, 4), "dW_hipblaslt_ms": round(ms_wt, 4),
                       "dW_max_rel_err_vs_fp32": errw, "dX_ms": round(ms_x, 4),
