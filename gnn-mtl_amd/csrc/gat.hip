@@ -261,14 +261,18 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
 // Head-grouped layout: per in-edge (i, j) the lane accumulates alpha*mask*G_i into its own
 // elements and the product G_i . H_j over them; kEB edges' G rows are gathered together (the next
 // chunk's in flight meanwhile) and their per-head dot products reduced by one grp_sum (lane h*LPH + grp_lane(e) gets edge e, head h).
-template <int H, int EPL, typename T>
+// WIN (bf16, EPL <= 6, g_rows known): a lane's EPL consecutive elements of G_i are read as ONE
+// 16-B load of the 4-B aligned window holding them (one load instruction per edge instead of EPL
+// 2-B loads; the window may run into the next row, so G's last row takes the element loads --
+// the gathered row is wave-uniform per edge, so the choice is a uniform branch).
+template <int H, int EPL, typename T, bool WIN = false>
 __global__ __launch_bounds__(256) void k_gat_bwd_src(
     const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT,
     const int64_t* __restrict__ permT, int n_rows, int dh, const T* __restrict__ Hm,
     int64_t ldh, const float* __restrict__ s2, float alpha, const float* __restrict__ emask,
     const float4* __restrict__ rec, const T* __restrict__ G, int64_t ldg,
     const float* __restrict__ a, T* __restrict__ dH, int64_t lddh, float* __restrict__ dzT,
-    float* __restrict__ ds2) {
+    float* __restrict__ ds2, int64_t g_rows) {
   using L = HeadLanes<H, EPL>;
   constexpr int LPH = L::LPH;
   constexpr int kEB = 2;  // edges per chunk (measured: 2 beats 4 and 8 once double-buffered)
@@ -300,12 +304,26 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(
   // chunk loads depend only on the in-neighbour ids: chunk c + 1 is in flight while chunk c is
   // reduced (register double buffer), and chunk 0 goes out before the attention records arrive
   float gA[kEB][EPL], gB[kEB][EPL];
+  const int wbyte = (2 * hl.c[0]) & ~3;  // WIN: the lane's window, halfword shift
+  const bool wsh = (hl.c[0] & 1) != 0;
   auto load = [&](float (&g)[kEB][EPL], int mi, int k, int cnt) {
 #pragma unroll
     for (int e = 0; e < kEB; ++e) {
-      const T* gr = G + (int64_t)readlane_i(mi, min(k + e, cnt - 1)) * ldg;
+      const int r = readlane_i(mi, min(k + e, cnt - 1));
+      const T* gr = G + (int64_t)r * ldg;
+      if (WIN && r + 1 < g_rows) {
+        const uint4 v = *(const uint4*)((const char*)gr + wbyte);
+        const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int t = 0; t < EPL; ++t) g[e][t] = to_f32<T>(gr[hl.c[t]]);
+        for (int t = 0; t < EPL; ++t) {  // halfword t + wsh of the window, widened to f32
+          const uint32_t lo = (t & 1) ? (dw[t >> 1] & 0xffff0000u) : (dw[t >> 1] << 16);
+          const uint32_t hi = (t & 1) ? (dw[(t + 1) >> 1] << 16) : (dw[t >> 1] & 0xffff0000u);
+          g[e][t] = __uint_as_float(wsh ? hi : lo);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < EPL; ++t) g[e][t] = to_f32<T>(gr[hl.c[t]]);
+      }
     }
   };
   for (int base = beg; base < end; base += 64) {
@@ -577,7 +595,7 @@ static int gat_bwd_src_t(const int32_t* rowptrT, const int32_t* colT, const int6
                          int32_t n_rows, int heads, int d_head, const T* H, int64_t ldh,
                          const float* s2, float alpha, const float* edge_mask, const float* rec,
                          const T* G, int64_t ldg, const float* a, T* dH, int64_t lddh,
-                         float* dzT, float* ds2, hipStream_t s) {
+                         float* dzT, float* ds2, hipStream_t s, int64_t g_rows = 0) {
   if (n_rows < 0 || heads < 1 || d_head < 1) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
   const int D = heads * d_head;
@@ -587,11 +605,20 @@ static int gat_bwd_src_t(const int32_t* rowptrT, const int32_t* colT, const int6
       !alv<T>(dH) || !alv<float>(rec))
     return GNNEA_EALIGN;
   const int nb = div_up(n_rows, 4);
+  // the window path: bf16 rows with 4-B aligned starts (the runs of EPL <= 6 elements fit 16 B)
+  const bool win = std::is_same<T, bf16_t>::value && g_rows > 1 && ldg % 2 == 0 &&
+                   (((uintptr_t)G) & 3) == 0;
 #define CALL(HH, EE)                                                                          \
   case HH * 32 + EE:                                                                          \
-    hipLaunchKernelGGL((k_gat_bwd_src<HH, EE, T>), dim3(nb), dim3(256), 0, s, rowptrT, colT,  \
-                       permT, n_rows, d_head, H, ldh, s2, alpha, edge_mask,                   \
-                       (const float4*)rec, G, ldg, a, dH, lddh, dzT, ds2);                    \
+    if (EE <= 6 && win)                                                                       \
+      hipLaunchKernelGGL((k_gat_bwd_src<HH, EE, T, (EE <= 6 && std::is_same<T, bf16_t>::value)>), \
+                         dim3(nb), dim3(256), 0, s,                                           \
+                         rowptrT, colT, permT, n_rows, d_head, H, ldh, s2, alpha, edge_mask,  \
+                         (const float4*)rec, G, ldg, a, dH, lddh, dzT, ds2, g_rows);          \
+    else                                                                                      \
+      hipLaunchKernelGGL((k_gat_bwd_src<HH, EE, T>), dim3(nb), dim3(256), 0, s, rowptrT,      \
+                         colT, permT, n_rows, d_head, H, ldh, s2, alpha, edge_mask,           \
+                         (const float4*)rec, G, ldg, a, dH, lddh, dzT, ds2, (int64_t)0);      \
     break;
   GNNEA_GAT_HL_DISPATCH(CALL);
 #undef CALL
@@ -698,6 +725,19 @@ extern "C" int gnnea_gat_bwd_src_bf16(const int32_t* rowptrT, const int32_t* col
   return gat_bwd_src_t<bf16_t>(rowptrT, colT, permT, n_rows, heads, d_head, (const bf16_t*)H,
                                ldh, s2, alpha, edge_mask, rec, (const bf16_t*)G, ldg, a,
                                (bf16_t*)dH, lddh, dzT, ds2, (hipStream_t)stream);
+}
+
+extern "C" int gnnea_gat_bwd_src_rows_bf16(const int32_t* rowptrT, const int32_t* colT,
+                                           const int64_t* permT, int32_t n_rows, int heads,
+                                           int d_head, const void* H, int64_t ldh,
+                                           const float* s2, float alpha, const float* edge_mask,
+                                           const float* rec, const void* G, int64_t ldg,
+                                           int64_t g_rows, const float* a, void* dH,
+                                           int64_t lddh, float* dzT, float* ds2, void* stream) {
+  if (g_rows < 0) return GNNEA_EINVAL;
+  return gat_bwd_src_t<bf16_t>(rowptrT, colT, permT, n_rows, heads, d_head, (const bf16_t*)H,
+                               ldh, s2, alpha, edge_mask, rec, (const bf16_t*)G, ldg, a,
+                               (bf16_t*)dH, lddh, dzT, ds2, (hipStream_t)stream, g_rows);
 }
 
 extern "C" int gnnea_gat_bwd_dst_bf16(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows,

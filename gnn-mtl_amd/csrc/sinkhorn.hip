@@ -57,12 +57,12 @@ static int sk_rows_per_wg(int I) {
 
 struct SkWs {
   int64_t K, u, v, pu, pv, rowbuf, part, errpart, total;
-  int64_t flags, rowpart, colpart, rowaux, colaux, res_end;  // the on-chip KNOPP path
+  int64_t flags, rowpart, colpart, rowaux, colaux;  // the on-chip KNOPP path (k_sk_res)
   int ns, nfin, rpw;
 };
 
 constexpr int kFinCols = 16;  // columns per update workgroup (64 slots split the partials)
-constexpr int64_t kResFlagBytes = 256;  // k_sk_res's entry counter
+constexpr int64_t kResFlagBytes = 4 * (2 * kResMaxWg + 64);  // rflag[256], cflag[256], entry counter
 
 static SkWs sk_plan(int I, int J) {
   SkWs w;
@@ -84,11 +84,10 @@ static SkWs sk_plan(int I, int J) {
   // double-buffered row / column partials (sized for the largest grid, kResMaxWg workgroups)
   const int P = div_up(I, kResRows), Q = div_up(J, kResCols);  // res_geom's grid
   w.flags = o; o = al256(o + kResFlagBytes);
-  w.rowaux = o; o = al256(o + 8ll * 2 * 4 * kResMaxWg);
+  w.rowpart = o; o = al256(o + 8ll * 2 * Q * I);
+  w.colpart = o; o = al256(o + 8ll * 2 * P * J);
+  w.rowaux = o; o = al256(o + 8ll * 2 * 2 * kResMaxWg);
   w.colaux = o; o = al256(o + 8ll * 2 * kResMaxWg);
-  w.rowpart = o; o = al256(o + 16ll * 2 * Q * I);
-  w.colpart = o; o = al256(o + 16ll * 2 * P * J);
-  w.res_end = o;  // [flags, res_end) is zeroed by init (no granule tag is an epoch)
   w.total = o;
   return w;
 }
@@ -106,8 +105,8 @@ struct SkDev {
   int64_t* st;   // status ints
   double* sd;    // status doubles
   double *K, *u, *v, *pu, *pv, *rowbuf, *part, *errpart;
-  unsigned long long *rowpart, *colpart, *rowaux, *colaux;  // k_sk_res granules
-  unsigned* ecnt;
+  double *rowpart, *colpart, *rowaux, *colaux;
+  unsigned *rflag, *cflag, *ecnt;
 };
 
 static SkDev sk_dev(const gnnea_sinkhorn* p) {
@@ -124,11 +123,13 @@ static SkDev sk_dev(const gnnea_sinkhorn* p) {
   d.rowbuf = (double*)(b + w.rowbuf);
   d.part = (double*)(b + w.part);
   d.errpart = (double*)(b + w.errpart);
-  d.rowpart = (unsigned long long*)(b + w.rowpart);
-  d.colpart = (unsigned long long*)(b + w.colpart);
-  d.rowaux = (unsigned long long*)(b + w.rowaux);
-  d.colaux = (unsigned long long*)(b + w.colaux);
-  d.ecnt = (unsigned*)(b + w.flags);
+  d.rowpart = (double*)(b + w.rowpart);
+  d.colpart = (double*)(b + w.colpart);
+  d.rowaux = (double*)(b + w.rowaux);
+  d.colaux = (double*)(b + w.colaux);
+  d.rflag = (unsigned*)(b + w.flags);
+  d.cflag = d.rflag + kResMaxWg;
+  d.ecnt = d.rflag + 2 * kResMaxWg;
   return d;
 }
 
@@ -632,28 +633,24 @@ static void launch_sweep(const SkArgs& a, const SkDev& d, int it, int si, int so
 //      the stop decisions of knopp_stop (err of it-1, K^T u == 0 / bad v) taken identically by
 //      every workgroup from the same published words;
 //   4. column partials sum_i K_ij u_i over the block's rows for step 1 of iteration it + 1.
-// K is read from HBM once per launch.  Hand-offs (cdna_hip_programming.md §6 Guideline 16, R2:
-// the data is the flag): every published double travels as two 8-byte granules {tag, 32-bit
-// half} stored by one agent-scope relaxed atomic each (global_store_dwordx2 ... sc1, single-copy
-// atomic); the consumer re-reads the granules it needs (sc1 loads) until every tag equals the
-// phase epoch -- no drain, barrier or flag on the producer side, no separate poll on the
-// consumer's.  Epochs: row partials of iteration it carry it + 1, column partials it + 2 (the
-// in-launch K^T u_0 is iteration -1).  Payloads are double-buffered by iteration parity: a
-// producer can run at most one iteration ahead of any consumer of the same buffer (it needs that
-// consumer's next publication first), so a slot is never rewritten before it is read and a
-// tag is either the awaited epoch or the previous use's.  Every spin is bounded (kResSpinTicks of
-// the 100 MHz real-time counter): a timed-out workgroup sets GNNEA_SK_ST_TIMEOUT, marks the loop
-// done and exits, and its peers time out in turn.  An entry barrier (monotonic arrival counter)
-// separates every workgroup's read of ST_DONE from any write of it in the same launch, so all
-// workgroups take the same decision.  Init zeroes the granules (tags 0, no epoch is 0).
+// K is read from HBM once per launch.  Hand-offs (cdna_hip_programming.md §6 Guideline 16, the
+// all-sc1 form): payload words stored and loaded write-through (agent-scope relaxed atomics =
+// global_store / global_load ... sc1), every storing wave drains (s_waitcnt vmcnt(0)), then a
+// workgroup barrier and ONE lane's sc1 flag store carrying the phase epoch (row partials of
+// iteration it: it + 1; column partials of iteration it: it + 2); a consumer's wave 0 polls the
+// flags of the workgroups it reads (>= epoch, bounded spin), the other waves load after a
+// workgroup barrier.  Payloads are double-buffered by iteration parity: a producer can run at
+// most one iteration ahead of any consumer of the same buffer (it needs that consumer's next
+// publication first).  Every spin is bounded (kResSpinTicks of the 100 MHz real-time counter):
+// a timed-out workgroup sets GNNEA_SK_ST_TIMEOUT, marks the loop done and exits, and its peers
+// time out in turn.  An entry barrier (monotonic arrival counter) separates every workgroup's read
+// of ST_DONE from any write of it in the same launch, so all workgroups take the same decision.
 // ---------------------------------------------------------------------------------------- //
 constexpr uint64_t kResSpinTicks = 25000000ull;  // 250 ms at 100 MHz
-constexpr int kResChunk = 24;                    // partials gathered per round trip
 enum { ST_TMO = GNNEA_SK_ST_TIMEOUT };
 
-typedef __attribute__((address_space(1))) unsigned long long res_g64;
+typedef __attribute__((address_space(1))) double res_gd;
 typedef __attribute__((address_space(1))) unsigned int res_gu;
-typedef unsigned long long gran_t;
 
 struct ResGeom {
   int P, Q, R, Cb;
@@ -670,76 +667,42 @@ static ResGeom res_geom(int I, int J) {
   return g;
 }
 
-__device__ __forceinline__ void gr_put(gran_t* g, unsigned epoch, unsigned v) {
-  __hip_atomic_store((res_g64*)g, ((gran_t)epoch << 32) | v, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void res_st(double* p, double x) {
+  __hip_atomic_store((res_gd*)p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void gr_put_d(gran_t* g, unsigned epoch, double x) {  // 2 granules
-  const gran_t b = (gran_t)__double_as_longlong(x);
-  gr_put(g, epoch, (unsigned)b);
-  gr_put(g + 1, epoch, (unsigned)(b >> 32));
-}
-__device__ __forceinline__ gran_t gr_get(const gran_t* g) {
-  return __hip_atomic_load((res_g64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool gr_ok(gran_t v, unsigned epoch) {
-  return (unsigned)(v >> 32) == epoch;
-}
-__device__ __forceinline__ double gr_double(gran_t lo, gran_t hi) {
-  return __longlong_as_double((long long)((lo & 0xffffffffull) | (hi << 32)));
+__device__ __forceinline__ double res_ld(const double* p) {
+  return __hip_atomic_load((res_gd*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ unsigned res_ldu(const unsigned* p) {
   return __hip_atomic_load((res_gu*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void res_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// sum over k < n of the doubles published at g + k * stride (granule pairs, tags == epoch), in
-// a fixed order (even / odd k, then the two); polls each chunk of kResChunk until every tag
-// matches; false on timeout.  One thread's gather: no barrier between the poll and the use.
-__device__ bool res_gather_sum(const gran_t* g, int64_t stride, int n, unsigned epoch,
-                               double& out) {
+// sum_{k < n} p[k * stride] in a fixed order (even / odd k, then the two), every load of a chunk
+// of 32 in flight at once: one round trip per chunk instead of one per partial
+__device__ __forceinline__ double res_sum_strided(const double* p, int64_t stride, int n) {
   double s0 = 0.0, s1 = 0.0;
-  for (int k0 = 0; k0 < n; k0 += kResChunk) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    gran_t lo[kResChunk], hi[kResChunk];
-    for (;;) {
-      bool ok = true;
+  for (int k0 = 0; k0 < n; k0 += 32) {
+    double x[32];
 #pragma unroll
-      for (int k = 0; k < kResChunk; ++k) {
-        if (k0 + k < n) {
-          lo[k] = gr_get(g + (int64_t)(k0 + k) * stride);
-          hi[k] = gr_get(g + (int64_t)(k0 + k) * stride + 1);
-        } else {
-          lo[k] = hi[k] = (gran_t)epoch << 32;  // a zero
-        }
-      }
+    for (int k = 0; k < 32; ++k) x[k] = k0 + k < n ? res_ld(p + (int64_t)(k0 + k) * stride) : 0.0;
 #pragma unroll
-      for (int k = 0; k < kResChunk; ++k) ok &= gr_ok(lo[k], epoch) && gr_ok(hi[k], epoch);
-      if (ok) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kResSpinTicks) return false;
-      __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int k = 0; k < kResChunk; k += 2) {
-      s0 += gr_double(lo[k], hi[k]);
-      s1 += gr_double(lo[k + 1], hi[k + 1]);
+    for (int k = 0; k < 32; k += 2) {
+      s0 += x[k];
+      s1 += x[k + 1];
     }
   }
-  out = s0 + s1;
-  return true;
+  return s0 + s1;
 }
 
-// one lane: the n granules g[k * stride] (k < n, tags == epoch) into v[]; false on timeout
-__device__ bool res_gather_words(const gran_t* g, int64_t stride, int n, unsigned epoch,
-                                 unsigned* v) {
+// one wave: until flags[base + k * stride] >= epoch for every k < n; false on timeout
+__device__ bool res_wait(const unsigned* flags, int base, int stride, int n, unsigned epoch) {
+  const int lane = lane_id();
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     bool ok = true;
-    for (int k = 0; k < n; ++k) {
-      const gran_t x = gr_get(g + (int64_t)k * stride);
-      ok &= gr_ok(x, epoch);
-      v[k] = (unsigned)x;
-    }
-    if (ok) return true;
+    for (int k = lane; k < n; k += 64) ok &= res_ldu(flags + base + k * stride) >= epoch;
+    if (__all(ok)) return true;
     if (__builtin_amdgcn_s_memrealtime() - t0 > kResSpinTicks) return false;
     __builtin_amdgcn_s_sleep(1);
   }
@@ -765,8 +728,9 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
   // K rows kResRR..kResRA-1 of the thread tile, column pairs as one 16-B word per lane
   __shared__ double2 klds[kResLR * (kResCA / 2) * 256];
   __shared__ double vsh[kResCols], ush[kResRows], colred[4][kResCols];
-  __shared__ double red4[4];
-  __shared__ int sh_state, sh_tmo;
+  __shared__ double red4[4], peer[kResMaxWg];
+  __shared__ int peerf[kResMaxWg];
+  __shared__ int sh_state;
   const int t = threadIdx.x, w = wave_id(), lane = lane_id();
   const int ra = t >> 4, cb = t & 15;
   const int wg = blockIdx.x, p = wg / g.Q, q = wg - (wg / g.Q) * g.Q;
@@ -774,10 +738,10 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
   const int r0 = p * g.R, c0 = q * g.Cb;
   const int nr = max(0, min(g.R, a.I - r0)), nc = max(0, min(g.Cb, a.J - c0));
   const int64_t J = a.J, I = a.I;
-  gran_t* rowpart = d.rowpart;  // [2][Q][I][2]: row partials (granule pairs)
-  gran_t* colpart = d.colpart;  // [2][P][J][2]: column partials
-  gran_t* rowaux = d.rowaux;    // [2][P*Q][4]: err^2 of the column block (pair), bad-v flag
-  gran_t* colaux = d.colaux;    // [2][P*Q]: bad-u flag of the row block
+  double* rowpart = d.rowpart;  // [2][Q][I]
+  double* colpart = d.colpart;  // [2][P][J]
+  double* rowaux = d.rowaux;    // [2][P*Q][2]: err^2 of the column block, bad-v flag
+  double* colaux = d.colaux;    // [2][P*Q]: bad-u flag of the row block
   // -- the K block (zeros outside the matrix) --
   double kr[kResRR][kResCA];
 #pragma unroll
@@ -805,7 +769,7 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
   if (t == 0) {
     const int64_t done = __hip_atomic_load(&d.st[ST_DONE], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    res_drain();
     const unsigned v = __hip_atomic_fetch_add((res_gu*)d.ecnt, 1u, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
     int st = done ? 1 : 0;
@@ -821,7 +785,6 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
       }
     }
     sh_state = st;
-    sh_tmo = 0;
   }
   __syncthreads();
   if (sh_state) {
@@ -863,9 +826,13 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
     }
     __syncthreads();
     if (t < nc)
-      gr_put_d(colpart + (((int64_t)par * g.P + p) * J + c0 + t) * 2, ep,
-               (colred[0][t] + colred[1][t]) + (colred[2][t] + colred[3][t]));
-    if (t == 0) gr_put(colaux + (int64_t)par * nwg + wg, ep, ufail ? 1u : 0u);
+      res_st(colpart + ((int64_t)par * g.P + p) * J + c0 + t,
+             (colred[0][t] + colred[1][t]) + (colred[2][t] + colred[3][t]));
+    if (t == 0) res_st(colaux + (int64_t)par * nwg + wg, ufail ? 1.0 : 0.0);
+    res_drain();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store((res_gu*)(d.cflag + wg), ep, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
   };
 
   if (first == 0) {  // K^T u_0, u_0 = 1 / I (ot_loss.py:39), published as iteration -1
@@ -875,36 +842,36 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
   }
   for (int it = first; it < first + count; ++it) {
     const int cur = it & 1, prv = cur ^ 1;
-    const unsigned ep_col = (unsigned)(it + 1), ep_row = (unsigned)(it + 1);
-    // 1. v_it from the column partials of iterate it-1 (each thread gathers its column's P
-    //    partials; wave 0 the row blocks' bad-u flags)
+    // 1. v_it from the column partials of iterate it-1 (wave 0 polls; then every load of the
+    //    step -- the partials and the row blocks' bad-u flags -- goes out in one round trip)
+    if (w == 0) {
+      const bool ok = res_wait(d.cflag, q, g.Q, g.P, (unsigned)(it + 1));
+      if (lane == 0) sh_state = ok ? 0 : 2;
+    }
+    __syncthreads();
+    if (sh_state) {
+      if (t == 0) res_timeout(d);
+      return;
+    }
     double errp = 0.0, vj = 0.0;
-    bool vfail = false, tmo = false;
+    bool vfail = false;
     if (t < nc) {
-      double s = 0.0;
-      tmo = !res_gather_sum(colpart + ((int64_t)prv * g.P * J + c0 + t) * 2, J * 2, g.P, ep_col, s);
+      const double s = res_sum_strided(colpart + (int64_t)prv * g.P * J + c0 + t, J, g.P);
       const double tt = vprev * s - bj;  // err of iterate it-1 (ot_loss.py:65-66), s = K^T u_{it-1}
       errp = tt * tt;
       vj = bj / s;  // ot_loss.py:54
       vfail = s == 0.0 || vj != vj || isinf(vj);
     }
     vsh[t] = vj;
-    bool uf = false;
     if (w == 0) {
-      for (int k = lane; k < g.P; k += 64) {
-        unsigned f;
-        if (!res_gather_words(colaux + (int64_t)prv * nwg + k * g.Q + q, 1, 1, ep_col, &f)) tmo = true;
-        else uf |= f != 0u;
-      }
+      bool uf = false;
+      for (int k = lane; k < g.P; k += 64)
+        uf |= res_ld(colaux + (int64_t)prv * nwg + k * g.Q + q) != 0.0;
+      const bool any_uf = __any(uf);
+      if (lane == 0) sh_state = any_uf ? 1 : 0;  // iteration it-1 broke on u (marked by its rows)
     }
-    if (tmo) sh_tmo = 1;
-    const bool any_uf = __syncthreads_or(uf);
-    if (sh_tmo) {
-      if (t == 0) res_timeout(d);
-      return;
-    }
-    if (any_uf) return;  // iteration it-1 broke on u (marked by the rows that saw it)
-    const double err2_blk = res_block_sum(errp, red4);  // barriers: vsh published
+    const double err2_blk = res_block_sum(errp, red4);  // barriers: vsh and sh_state published
+    if (sh_state) return;
     const bool vfail_blk = __syncthreads_or(vfail);
     if (t < nc) {
       if (p == 0) d.v[(int64_t)cur * J + c0 + t] = vj;
@@ -940,34 +907,42 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
       x += mov_dpp_f64<0x141>(x);
       x += mov_dpp_f64<0x140>(x);
       const int lr = ra + 16 * i;
-      if (cb == 0 && lr < nr)
-        gr_put_d(rowpart + (((int64_t)cur * g.Q + q) * I + r0 + lr) * 2, ep_row, x);
+      if (cb == 0 && lr < nr) res_st(rowpart + ((int64_t)cur * g.Q + q) * I + r0 + lr, x);
     }
     if (t == 0) {
-      gran_t* ax = rowaux + ((int64_t)cur * nwg + wg) * 4;
-      gr_put_d(ax, ep_row, err2_blk);
-      gr_put(ax + 2, ep_row, vfail_blk ? 1u : 0u);
+      res_st(rowaux + ((int64_t)cur * nwg + wg) * 2, err2_blk);
+      res_st(rowaux + ((int64_t)cur * nwg + wg) * 2 + 1, vfail_blk ? 1.0 : 0.0);
     }
+    res_drain();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store((res_gu*)(d.rflag + wg), (unsigned)(it + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
     // 3. the row block's partials; the stop decisions of knopp_stop, identical everywhere
-    double srow = 0.0;
-    tmo = false;
-    if (t < nr)
-      tmo = !res_gather_sum(rowpart + ((int64_t)cur * g.Q * I + r0 + t) * 2, I * 2, g.Q, ep_row,
-                            srow);
-    if (t == 0) {
-      double e2 = 0.0;
-      bool vf = false;
-      for (int k = 0; k < g.Q && !tmo; ++k) {  // column-block order: every workgroup the same sum
-        unsigned wv[3];
-        if (!res_gather_words(rowaux + ((int64_t)cur * nwg + p * g.Q + k) * 4, 1, 3, ep_row, wv)) {
-          tmo = true;
-          break;
-        }
-        e2 += __longlong_as_double((long long)((gran_t)wv[0] | ((gran_t)wv[1] << 32)));
-        vf |= wv[2] != 0u;
+    if (w == 0) {
+      const bool ok = res_wait(d.rflag, p * g.Q, 1, g.Q, (unsigned)(it + 1));
+      if (lane == 0) sh_state = ok ? 0 : 2;
+    }
+    __syncthreads();
+    if (sh_state) {
+      if (t == 0) res_timeout(d);
+      return;
+    }
+    const double srow =
+        t < nr ? res_sum_strided(rowpart + (int64_t)cur * g.Q * I + r0 + t, I, g.Q) : 0.0;
+    if (w == 0) {
+      for (int k = lane; k < g.Q; k += 64) {
+        const double* ax = rowaux + ((int64_t)cur * nwg + p * g.Q + k) * 2;
+        peer[k] = res_ld(ax);
+        peerf[k] = res_ld(ax + 1) != 0.0;
       }
-      int st = 0;
-      if (!tmo) {
+      if (lane == 0) {
+        double e2 = 0.0;
+        bool vf = false;
+        int st = 0;
+        for (int k = 0; k < g.Q; ++k) {  // column-block order: every workgroup the same sum
+          vf |= peerf[k] != 0;
+          e2 += peer[k];
+        }
         const int prev = it - 1;
         if (prev >= 0 && prev % 10 == 0) {
           const double err = sqrt(e2);
@@ -981,15 +956,10 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
           st = 1;
           if (wg == 0) mark_done(d.st, it, 2, (it + 1) & 1);
         }
+        sh_state = st;
       }
-      sh_state = st;
     }
-    if (tmo) sh_tmo = 1;
     __syncthreads();
-    if (sh_tmo) {
-      if (t == 0) res_timeout(d);
-      return;
-    }
     if (sh_state) return;
     bool ufail = false;
     if (t < kResRows) {
@@ -1282,8 +1252,7 @@ extern "C" int gnnea_sinkhorn_init(const gnnea_sinkhorn* p, void* stream) {
       hipLaunchKernelGGL((k_sk_kbuild<double, true>), grow, dim3(256), 0, s,
                          (const double*)p->C, a, d, 0, p->max_iter, 1);
     if (res_applies(p)) {  // k_sk_res computes K^T u0 itself; its flags start at 0
-      const SkWs w = sk_plan(p->I, p->J);
-      if (hipMemsetAsync(d.ecnt, 0, w.res_end - w.flags, s) != hipSuccess) return GNNEA_EINVAL;
+      if (hipMemsetAsync(d.rflag, 0, kResFlagBytes, s) != hipSuccess) return GNNEA_EINVAL;
     } else {
       launch_sweep<true, false>(a, d, 0, 1, 1, d.u + p->I, 0, s);  // K^T u0, u0 = 1/I (slot 1)
     }

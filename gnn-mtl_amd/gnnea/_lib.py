@@ -123,6 +123,9 @@ SIGNATURES = {
                                              _p, _f32, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
     "gnnea_gat_bwd_src_bf16": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _i64,
                                              _p, _f32, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _p]),
+    "gnnea_gat_bwd_src_rows_bf16": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int, ctypes.c_int,
+                                                   _p, _i64, _p, _f32, _p, _p, _p, _i64, _i64, _p,
+                                                   _p, _i64, _p, _p, _p]),
     "gnnea_gat_bwd_dst_f32": (ctypes.c_int, [_p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,
                                              _i64, _p, _p]),
     "gnnea_gat_bwd_dst_bf16": (ctypes.c_int, [_p, _p, _i32, ctypes.c_int, ctypes.c_int, _p, _p, _p,

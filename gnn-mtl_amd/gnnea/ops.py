@@ -1068,7 +1068,15 @@ def _gat_backward_rows(csr, csrT, H, a32, s1, s2, m, den, Y, dY, heads, d_head, 
             N, heads, d_head, ptr(dY), ptr(Y), Y.stride(0), _off(s1, row0), ptr(m), ptr(den),
             int(act), ptr(G), ptr(rec), st))
         src = _gat_fn("gnnea_gat_bwd_src", H.dtype)
+        L = _lib.lib()
         for j0, j1 in _blocks(csrT, G):  # source rows j of A^T, per KG block
+            if H.dtype == torch.bfloat16:  # G rows gathered as 16-B windows (G's rows known)
+                check(L.gnnea_gat_bwd_src_rows_bf16(
+                    _off32(csrT.rowptr, j0), ptr(csrT.col), ptr(csrT.perm), j1 - j0, heads,
+                    d_head, _off(H, j0), H.stride(0), _off(s2, j0), alpha, ptr(em), ptr(rec),
+                    ptr(G), G.stride(0), G.shape[0], ptr(a32), _off(dH, j0), dH.stride(0),
+                    ptr(dzT), _off(ds2, j0), st))
+                continue
             check(src(_off32(csrT.rowptr, j0), ptr(csrT.col), ptr(csrT.perm), j1 - j0, heads,
                       d_head, _off(H, j0), H.stride(0), _off(s2, j0), alpha, ptr(em),
                       ptr(rec), ptr(G), G.stride(0), ptr(a32), _off(dH, j0), dH.stride(0),

@@ -317,6 +317,15 @@ int gnnea_gat_bwd_src_bf16(const int32_t* rowptrT, const int32_t* colT, const in
                            const float* s2, float alpha, const float* edge_mask, const float* rec,
                            const void* G, int64_t ldg, const float* a, void* dH, int64_t lddh,
                            float* dzT, float* ds2, void* stream);
+/* gnnea_gat_bwd_src_bf16 for a G of g_rows rows: the in-neighbours' G rows are read as one
+ * 16-B window per lane (the head-grouped run of <= 6 elements; the window may run into the next
+ * row, so G's last row is read element-wise) -- one load instruction per edge. */
+int gnnea_gat_bwd_src_rows_bf16(const int32_t* rowptrT, const int32_t* colT,
+                                const int64_t* permT, int32_t n_rows, int heads, int d_head,
+                                const void* H, int64_t ldh, const float* s2, float alpha,
+                                const float* edge_mask, const float* rec, const void* G,
+                                int64_t ldg, int64_t g_rows, const float* a, void* dH,
+                                int64_t lddh, float* dzT, float* ds2, void* stream);
 int gnnea_gat_bwd_dst_bf16(const int32_t* rowptr, const int64_t* tpos, int32_t n_rows, int heads,
                            int d_head, const float* dzT, const float* a, void* dH, int64_t lddh,
                            float* ds1, void* stream);
