@@ -459,6 +459,378 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(const int32_t* __restrict__
 
 static bool ok_ld(int64_t ld, int D) { return ld % 4 == 0 && ld >= ((D + 3) / 4) * 4; }
 
+// ---------------------------------------------------------------------------------------- //
+// Head-grouped, pipelined row-major passes (the default where they apply).                   //
+// The passes above are latency-chain bound, not bandwidth bound: a gathered row read inside a //
+// uniform branch (the bf16 window / element choice, the edge mask) is waited on right where   //
+// it is issued, so one neighbour row per wave is in flight, and the forward's per-edge logit  //
+// and mask loads are serialised behind the same kind of branch.  Here every lane reads its    //
+// head's EPL consecutive elements of a gathered row as ONE window of W dwords (bf16: the 4-B  //
+// aligned dwords holding them, a halfword shift when the first element is odd; fp32: the      //
+// EPL dwords), issued unconditionally (indices clamped to the chunk, the surplus tail loads   //
+// re-read the last edge's row) in groups of F edges, two groups in flight (register double    //
+// buffer), the edge mask a template flag.  Rows are still one wave each, in CSR order, and     //
+// every per-element sum runs in edge order: the forward's outputs equal k_gat_fwd's.           //
+// Host-checked: every lane's window ends inside the row's ld (no read past the table).        //
+// ---------------------------------------------------------------------------------------- //
+struct __attribute__((aligned(4))) U3 { uint32_t x, y, z; };
+
+template <int W>
+__device__ __forceinline__ void load_dw(const char* p, uint32_t* d) {
+  if constexpr (W >= 4) {
+    const uint4 v = *(const uint4*)p;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    if constexpr (W > 4) load_dw<W - 4>(p + 16, d + 4);
+  } else if constexpr (W == 3) {
+    const U3 v = *(const U3*)p;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z;
+  } else if constexpr (W == 2) {
+    const uint2 v = *(const uint2*)p;
+    d[0] = v.x; d[1] = v.y;
+  } else {
+    d[0] = *(const uint32_t*)p;
+  }
+}
+
+template <typename T, int EPL> struct RowWin;
+template <int EPL> struct RowWin<float, EPL> {
+  static constexpr int W = EPL;
+  static __host__ __device__ int64_t byte_off(int c) { return 4 * (int64_t)c; }
+  static __device__ __forceinline__ void unpack(const uint32_t (&d)[W], bool, float (&f)[EPL]) {
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) f[t] = __builtin_bit_cast(float, d[t]);
+  }
+};
+template <int EPL> struct RowWin<bf16_t, EPL> {
+  static constexpr int W = (EPL + 2) / 2;  // EPL halfwords + a possible leading one
+  static __host__ __device__ int64_t byte_off(int c) { return (2 * (int64_t)c) & ~(int64_t)3; }
+  static __device__ __forceinline__ void unpack(const uint32_t (&d)[W], bool sh, float (&f)[EPL]) {
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) {  // halfword t + sh of the window, widened to f32
+      const uint32_t lo = (t & 1) ? (d[t >> 1] & 0xffff0000u) : (d[t >> 1] << 16);
+      const uint32_t hi = (t & 1) ? (d[(t + 1) >> 1] << 16) : (d[t >> 1] & 0xffff0000u);
+      f[t] = __builtin_bit_cast(float, sh ? hi : lo);
+    }
+  }
+};
+
+template <int H>
+__device__ __forceinline__ void load_heads(const float* p, float (&v)[H]) {
+  if constexpr (H == 4) {  // 16-B aligned rows (host-checked)
+    const float4 q = *(const float4*)p;
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+#pragma unroll
+    for (int h = 0; h < H; ++h) v[h] = p[h];
+  }
+}
+
+// the lane's head weight of edge k (lane k holds every head's weight of its edge)
+template <int H>
+__device__ __forceinline__ float head_w(const float (&wl)[H], int k, int hme) {
+  float we = 0.f;
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const float v = readlane_f(wl[h], k);
+    we = hme == h ? v : we;
+  }
+  return we;
+}
+
+template <int H, int EPL, typename T, bool EM, int F>
+__global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ rowptr,
+                                                    const int32_t* __restrict__ col, int n_rows,
+                                                    const T* __restrict__ Hm, int64_t ldh, int D,
+                                                    int dh, const float* __restrict__ s1,
+                                                    const float* __restrict__ s2, float alpha,
+                                                    const float* __restrict__ emask, int act,
+                                                    T* __restrict__ Y, int64_t ldy,
+                                                    float* __restrict__ m_out,
+                                                    float* __restrict__ den_out) {
+  using L = HeadLanes<H, EPL>;
+  using WN = RowWin<T, EPL>;
+  constexpr int W = WN::W;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = blk * 4 + wave_id();
+  if (row >= n_rows) return;
+  const int lane = lane_id();
+  const int beg = rowptr[row], end = rowptr[row + 1];
+  const L hl(lane, dh);
+  const int hme = hl.h < H ? hl.h : 0;
+  const int64_t woff = WN::byte_off(hl.c[0]);
+  const bool wsh = (hl.c[0] & 1) != 0;
+  const char* Hb = (const char*)Hm + woff;
+  const int64_t ldb = ldh * (int64_t)sizeof(T);
+
+  float si[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) si[h] = s1[(int64_t)row * H + h];
+
+  // lane k of a chunk: edge base + k's neighbour and logits (-LeakyReLU(s1_i + s2_j))
+  int mj = 0;
+  float sc[H];
+  auto chunk = [&](int base, int cnt) {
+    mj = col[base + min(lane, cnt - 1)];
+    float v[H];
+    load_heads<H>(s2 + (int64_t)mj * H, v);
+    // (a select on the loaded value would let the compiler sink the load into a branch)
+    const float pen = lane < cnt ? 0.f : -INFINITY;
+#pragma unroll
+    for (int h = 0; h < H; ++h) sc[h] = pen - lrelu(si[h] + v[h], alpha);
+  };
+  float mx[H], den[H], acc[EPL];
+#pragma unroll
+  for (int h = 0; h < H; ++h) den[h] = 0.f;
+#pragma unroll
+  for (int t = 0; t < EPL; ++t) acc[t] = 0.f;
+  if (end > beg) {
+    chunk(beg, min(64, end - beg));
+    if (end - beg > 64) {  // long rows: the row maximum over every chunk first
+      float m2[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) m2[h] = sc[h];
+      for (int base = beg + 64; base < end; base += 64) {
+        chunk(base, min(64, end - base));
+#pragma unroll
+        for (int h = 0; h < H; ++h) m2[h] = fmaxf(m2[h], sc[h]);
+      }
+#pragma unroll
+      for (int h = 0; h < H; ++h) mx[h] = wave_max(m2[h]);
+      chunk(beg, min(64, end - beg));
+    } else {
+#pragma unroll
+      for (int h = 0; h < H; ++h) mx[h] = wave_max(sc[h]);
+    }
+    for (int base = beg; base < end; base += 64) {
+      const int cnt = min(64, end - base);
+      if (base != beg) chunk(base, cnt);
+      uint32_t ga[F][W], gb[F][W];
+      auto issue = [&](uint32_t (&g)[F][W], int k) {
+#pragma unroll
+        for (int e = 0; e < F; ++e) {
+          const int j = readlane_i(mj, min(k + e, cnt - 1));
+          load_dw<W>(Hb + (int64_t)j * ldb, g[e]);
+        }
+      };
+      issue(ga, 0);  // depends on the neighbour ids only: out before the weights are known
+      float em[H];
+      if constexpr (EM) load_heads<H>(emask + (int64_t)(base + min(lane, cnt - 1)) * H, em);
+      float wl[H];
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        const float w = __expf(sc[h] - mx[h]);  // 0 past the chunk (sc = -inf there)
+        den[h] += w;  // the row sum uses the un-dropped weights (att_layers.py:45-51)
+        wl[h] = EM ? w * em[h] : w;
+      }
+      // no early exits between a group's issue and its use: every edge of a group is consumed
+      // (edges past the chunk leave acc unchanged through a uniform select), so the compiler's
+      // wait counts stay exact across the loop's back edge
+      auto consume = [&](const uint32_t (&g)[F][W], int k) {
+#pragma unroll
+        for (int e = 0; e < F; ++e) {
+          const bool live = k + e < cnt;  // uniform
+          const float we = head_w<H>(wl, min(k + e, 63), hme);
+          float x[EPL];
+          WN::unpack(g[e], wsh, x);
+#pragma unroll
+          for (int t = 0; t < EPL; ++t) {
+            const float v = fmaf(we, x[t], acc[t]);
+            acc[t] = live ? v : acc[t];
+          }
+        }
+      };
+      // (sched_barrier: keep each group's loads ahead of the previous group's arithmetic)
+      for (int k = 0; k < cnt; k += 2 * F) {
+        issue(gb, k + F);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(ga, k);
+        issue(ga, k + 2 * F);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(gb, k + F);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < H; ++h) mx[h] = -INFINITY;
+  }
+  float rinv[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    den[h] = wave_sum(den[h]);
+    rinv[h] = den[h] > 0.f ? 1.f / den[h] : 0.f;
+  }
+  const float ri = hsel<H>(rinv, hme);
+  T* y = Y + (int64_t)row * ldy;
+#pragma unroll
+  for (int t = 0; t < EPL; ++t) {
+    if (!hl.ok[t]) continue;
+    const float v = acc[t] * ri;
+    y[hl.c[t]] = from_f32<T>(act == GNNEA_ACT_RELU ? act_fwd<GNNEA_ACT_RELU>(v)
+                             : act == GNNEA_ACT_ELU ? act_fwd<GNNEA_ACT_ELU>(v) : v);
+  }
+  const int Dp = (D + 3) & ~3;  // the row's padding columns hold zeros (k_gat_fwd's layout)
+  if (lane < Dp - D) y[D + lane] = from_f32<T>(0.f);
+  if (lane < H) {
+    m_out[(int64_t)row * H + lane] = hsel<H>(mx, lane);
+    den_out[(int64_t)row * H + lane] = hsel<H>(den, lane);
+  }
+}
+
+// The source pass of the backward (k_gat_bwd_src's math) with G gathered as pipelined windows:
+// F edges per group, two groups in flight; per group one grp_sum gives every edge's per-head
+// G_i . H_j; dz = -(alpha (mask da - c_i)) LeakyReLU'(z) lands in the edge's lane.
+template <int H, int EPL, typename T, bool EM, int F>
+__global__ __launch_bounds__(256) void k_gat_bwd_src_hg(
+    const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT,
+    const int64_t* __restrict__ permT, int n_rows, int dh, const T* __restrict__ Hm,
+    int64_t ldh, const float* __restrict__ s2, float alpha, const float* __restrict__ emask,
+    const float4* __restrict__ rec, const T* __restrict__ G, int64_t ldg,
+    const float* __restrict__ a, T* __restrict__ dH, int64_t lddh, float* __restrict__ dzT,
+    float* __restrict__ ds2) {
+  using L = HeadLanes<H, EPL>;
+  using WN = RowWin<T, EPL>;
+  constexpr int W = WN::W;
+  constexpr int LPH = L::LPH;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = blk * 4 + wave_id();  // source node j
+  if (row >= n_rows) return;
+  const int lane = lane_id();
+  const int beg = rowptrT[row], end = rowptrT[row + 1];
+  const L hl(lane, dh);
+  const int hme = hl.h < H ? hl.h : 0;
+  const char* Gb = (const char*)G + WN::byte_off(hl.c[0]);
+  const bool wsh = (hl.c[0] & 1) != 0;
+  const int64_t ldb = ldg * (int64_t)sizeof(T);
+
+  float hj[EPL], acc[EPL];
+  {
+    const T* x = Hm + (int64_t)row * ldh;
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) {
+      const float v = to_f32<T>(x[hl.c[t]]);
+      hj[t] = hl.ok[t] ? v : 0.f;
+      acc[t] = 0.f;
+    }
+  }
+  float ds2p[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) ds2p[h] = 0.f;
+
+  for (int base = beg; base < end; base += 64) {
+    const int cnt = min(64, end - base);
+    const int el = base + min(lane, cnt - 1);
+    const int mi = colT[el];  // destination row i of the forward edge (i, j)
+    uint32_t ga[F][W], gb[F][W];
+    auto issue = [&](uint32_t (&g)[F][W], int k) {
+#pragma unroll
+      for (int e = 0; e < F; ++e) {
+        const int r = readlane_i(mi, min(k + e, cnt - 1));
+        load_dw<W>(Gb + (int64_t)r * ldb, g[e]);
+      }
+    };
+    issue(ga, 0);  // depends on the neighbour ids only
+    float4 rr[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) rr[h] = rec[(int64_t)mi * H + h];  // {s1_i, m_i, 1/den_i, c_i}
+    float ml[H];
+    if constexpr (EM) load_heads<H>(emask + permT[el] * H, ml);
+    float al[H], cl[H], sl[H], wl[H], dzl[H];
+    const float msk = lane < cnt ? 1.f : 0.f;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const float z = rr[h].x + s2[(int64_t)row * H + h];
+      // lanes past the chunk hold a valid edge's record: scaled to 0 (a select on the loaded
+      // values would let the compiler sink their loads into a branch)
+      al[h] = __expf(-lrelu(z, alpha) - rr[h].y) * rr[h].z * msk;
+      cl[h] = rr[h].w;
+      sl[h] = z > 0.f ? 1.f : alpha;
+      if constexpr (!EM) ml[h] = 1.f;
+      wl[h] = EM ? al[h] * ml[h] : al[h];
+      dzl[h] = 0.f;
+    }
+    auto consume = [&](const uint32_t (&g)[F][W], int k) {
+      float pd[F];
+#pragma unroll
+      for (int e = 0; e < F; ++e) {
+        float x[EPL];
+        WN::unpack(g[e], wsh, x);
+        const bool live = k + e < cnt;  // uniform; no branch between issue and use
+        const float we = head_w<H>(wl, min(k + e, 63), hme);
+        float q = 0.f;
+#pragma unroll
+        for (int t = 0; t < EPL; ++t) {
+          const float gv = hl.ok[t] ? x[t] : 0.f;
+          const float u = fmaf(we, gv, acc[t]);
+          acc[t] = live ? u : acc[t];
+          q = fmaf(gv, hj[t], q);
+        }
+        pd[e] = q;
+      }
+      const float v = grp_sum<F, LPH>(pd, lane);
+#pragma unroll
+      for (int e = 0; e < F; ++e) {  // lanes past the chunk take a dz that is never stored
+        float da[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) da[h] = readlane_f(v, h * LPH + grp_lane<F, LPH>(e));
+        if (lane == k + e) {
+#pragma unroll
+          for (int h = 0; h < H; ++h) dzl[h] = -(al[h] * (ml[h] * da[h] - cl[h])) * sl[h];
+        }
+      }
+    };
+    for (int k = 0; k < cnt; k += 2 * F) {
+      issue(gb, k + F);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(ga, k);
+      issue(ga, k + 2 * F);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(gb, k + F);
+    }
+    if (lane < cnt) {
+#pragma unroll
+      for (int h = 0; h < H; ++h) {
+        dzT[(int64_t)(base + lane) * H + h] = dzl[h];
+        ds2p[h] += dzl[h];
+      }
+    }
+  }
+  float d2me = 0.f;
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    const float d2 = wave_sum(ds2p[h]);
+    d2me = hme == h ? d2 : d2me;
+    if (lane == 0) ds2[(int64_t)row * H + h] = d2;
+  }
+  T* out = dH + (int64_t)row * lddh;
+#pragma unroll
+  for (int t = 0; t < EPL; ++t)
+    if (hl.ok[t]) out[hl.c[t]] = from_f32<T>(acc[t] + d2me * a[hme * 2 * dh + dh + hl.d0 + t]);
+}
+
+// the head-grouped passes: on unless GNNEA_GAT_HG=0 (A/B timing against k_gat_fwd / _bwd_src)
+static bool gat_hg_on() {
+  static const bool on = [] {
+    const char* e = getenv("GNNEA_GAT_HG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// every lane's window ends inside the row's ld (elements, T-sized) for this head layout
+template <typename T, int EPL>
+static bool hg_window_fits(int heads, int dh, int64_t ld) {
+  const int hp = heads <= 1 ? 1 : heads <= 2 ? 2 : heads <= 4 ? 4 : 8, lph = 64 / hp;
+  for (int h = 0; h < heads; ++h)
+    for (int s = 0; s < lph; ++s) {
+      const int d0 = s * EPL;
+      if (d0 >= dh) continue;  // an idle lane reads the row's start
+      const int c = h * dh + d0;
+      if (RowWin<T, EPL>::byte_off(c) + 4 * RowWin<T, EPL>::W > ld * (int64_t)sizeof(T))
+        return false;
+    }
+  return true;
+}
+
 }  // namespace gnnea
 
 using namespace gnnea;
@@ -509,6 +881,49 @@ static bool alv(const void* p) {  // aligned for one Vec4<T> access (16 B fp32, 
   return p == nullptr || (((uintptr_t)p) & (sizeof(typename Vec4<T>::raw) - 1)) == 0;
 }
 
+// ---- head-grouped pipelined passes: heads in {1,2,4,8}, EPL in {2,3,4,5,6,8} ----
+static int hg_epl(int heads, int dh) {
+  if (heads != 1 && heads != 2 && heads != 4 && heads != 8) return -1;
+  const int e = (dh + 64 / heads - 1) / (64 / heads);
+  static const int opts[] = {2, 3, 4, 5, 6, 8};
+  for (int o : opts)
+    if (e <= o) return o;
+  return -1;
+}
+static int hg_group() {  // edges per pipelined group (tuning override GNNEA_GAT_HG_F = 2 / 4 / 8)
+  static const int f = [] {
+    const char* e = getenv("GNNEA_GAT_HG_F");
+    const int v = e ? atoi(e) : 4;
+    return v == 2 || v == 8 ? v : 4;
+  }();
+  return f;
+}
+template <typename T>
+static bool hg_applies(int heads, int dh, int64_t ld, const float* s2, const float* emask) {
+  if (!gat_hg_on()) return false;
+  const int epl = hg_epl(heads, dh);
+  bool fits = false;
+  switch (epl) {
+    case 2: fits = hg_window_fits<T, 2>(heads, dh, ld); break;
+    case 3: fits = hg_window_fits<T, 3>(heads, dh, ld); break;
+    case 4: fits = hg_window_fits<T, 4>(heads, dh, ld); break;
+    case 5: fits = hg_window_fits<T, 5>(heads, dh, ld); break;
+    case 6: fits = hg_window_fits<T, 6>(heads, dh, ld); break;
+    case 8: fits = hg_window_fits<T, 8>(heads, dh, ld); break;
+    default: return false;
+  }
+  // four heads: the per-edge logits / mask rows are read as one 16-B load
+  return fits && (heads != 4 || ((((uintptr_t)s2) & 15) == 0 && (((uintptr_t)emask) & 15) == 0));
+}
+#define GNNEA_GAT_HG_DISPATCH(CALL)                                                          \
+  switch (heads * 32 + hg_epl(heads, d_head)) {                                              \
+    CALL(1, 2) CALL(1, 3) CALL(1, 4) CALL(1, 5) CALL(1, 6) CALL(1, 8)                        \
+    CALL(2, 2) CALL(2, 3) CALL(2, 4) CALL(2, 5) CALL(2, 6) CALL(2, 8)                        \
+    CALL(4, 2) CALL(4, 3) CALL(4, 4) CALL(4, 5) CALL(4, 6) CALL(4, 8)                        \
+    CALL(8, 2) CALL(8, 3) CALL(8, 4) CALL(8, 5) CALL(8, 6) CALL(8, 8)                        \
+    default: return GNNEA_EINVAL;                                                            \
+  }
+
 template <typename T>
 static int gat_scores_t(const T* Hm, int64_t ldh, int32_t n_rows, int heads, int d_head,
                         const float* a, float* s1, float* s2, hipStream_t s) {
@@ -541,6 +956,24 @@ static int gat_fwd_t(const int32_t* rowptr, const int32_t* col, int32_t n_rows, 
   if (!rowptr || !col || !Hm || !s1 || !s2 || !Y || !m_out || !den_out) return GNNEA_EINVAL;
   if (!ok_ld(ldh, D) || !ok_ld(ldy, D) || !alv<T>(Hm) || !alv<T>(Y)) return GNNEA_EALIGN;
   const int nb = div_up(n_rows, 4);
+  if (hg_applies<T>(heads, d_head, ldh, s2, edge_mask) &&
+      (act == GNNEA_ACT_IDENTITY || act == GNNEA_ACT_RELU || act == GNNEA_ACT_ELU)) {
+#define GNNEA_HG_L(HH, EE, EMV, FF)                                                           \
+  hipLaunchKernelGGL((k_gat_fwd_hg<HH, EE, T, EMV, FF>), dim3(nb), dim3(256), 0, s, rowptr,   \
+                     col, n_rows, Hm, ldh, D, d_head, s1, s2, alpha, edge_mask, act, Y, ldy,  \
+                     m_out, den_out)
+#define CALL(HH, EE)                                                                          \
+  case HH * 32 + EE:                                                                          \
+    if (edge_mask) GNNEA_HG_L(HH, EE, true, 4);                                               \
+    else if (HH == 4 && EE == 5 && hg_group() == 8) GNNEA_HG_L(HH, EE, false, 8);             \
+    else GNNEA_HG_L(HH, EE, false, 4);                                                        \
+    break;
+    GNNEA_GAT_HG_DISPATCH(CALL);
+#undef CALL
+#undef GNNEA_HG_L
+    GNNEA_LAUNCH_CHECK();
+    return 0;
+  }
 #define CALL_A(A, HH, NN)                                                                       \
   hipLaunchKernelGGL((k_gat_fwd<A, HH, NN, T>), dim3(nb), dim3(256), 0, s, rowptr, col, n_rows, \
                      (const R*)Hm, ldh / 4, D, d_head, s1, s2, alpha, edge_mask, (R*)Y,         \
@@ -605,6 +1038,23 @@ static int gat_bwd_src_t(const int32_t* rowptrT, const int32_t* colT, const int6
       !alv<T>(dH) || !alv<float>(rec))
     return GNNEA_EALIGN;
   const int nb = div_up(n_rows, 4);
+  if (hg_applies<T>(heads, d_head, ldg, s2, edge_mask) && (((uintptr_t)rec) & 15) == 0) {
+#define GNNEA_HG_L(HH, EE, EMV, FF)                                                           \
+  hipLaunchKernelGGL((k_gat_bwd_src_hg<HH, EE, T, EMV, FF>), dim3(nb), dim3(256), 0, s,       \
+                     rowptrT, colT, permT, n_rows, d_head, H, ldh, s2, alpha, edge_mask,      \
+                     (const float4*)rec, G, ldg, a, dH, lddh, dzT, ds2)
+#define CALL(HH, EE)                                                                          \
+  case HH * 32 + EE:                                                                          \
+    if (edge_mask) GNNEA_HG_L(HH, EE, true, 4);                                               \
+    else if (HH == 4 && EE == 5 && hg_group() == 8) GNNEA_HG_L(HH, EE, false, 8);             \
+    else GNNEA_HG_L(HH, EE, false, 4);                                                        \
+    break;
+    GNNEA_GAT_HG_DISPATCH(CALL);
+#undef CALL
+#undef GNNEA_HG_L
+    GNNEA_LAUNCH_CHECK();
+    return 0;
+  }
   // the window path: bf16 rows with 4-B aligned starts (the runs of EPL <= 6 elements fit 16 B)
   const bool win = std::is_same<T, bf16_t>::value && g_rows > 1 && ldg % 2 == 0 &&
                    (((uintptr_t)G) & 3) == 0;

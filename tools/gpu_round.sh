@@ -32,6 +32,17 @@ for s in $steps; do
           --no-cpu-baseline ) > "$OUT/prof.log" 2>&1
       rc=$?; echo "== prof rc=$rc"; tail -n 3 "$OUT/prof.log"
       case $rc in 124|137|134|139) exit $rc ;; esac ;;
+    gat5|gat4|hgcn)  # kernel trace of one EA training-step run (tools/dist_step.py)
+      case $s in
+        gat5) a="--model GAT --dtype bf16 --entities 2000000" ;;
+        gat4) a="--model GAT" ;;
+        hgcn) a="--model HGCN" ;;
+      esac
+      ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$s" -o run \
+          --output-format csv -- python "$ROOT/tools/dist_step.py" $a --steps 21 --warmup 3 ) \
+          > "$OUT/prof_$s.log" 2>&1
+      rc=$?; echo "== prof_$s rc=$rc"; tail -n 2 "$OUT/prof_$s.log"
+      case $rc in 124|137|134|139) exit $rc ;; esac ;;
     pmc)
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/pmc_fetch" \
           -o run --output-format csv -- python "$ROOT/bench.py" --steps 3 --warmup 1 \
