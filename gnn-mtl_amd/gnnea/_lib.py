@@ -135,6 +135,12 @@ SIGNATURES = {
                                         _i64, _p]),
     "gnnea_gat_da_bf16": (ctypes.c_int, [_p, _i64, _i64, ctypes.c_int, ctypes.c_int, _p, _p, _p,
                                          _i64, _p]),
+    "gnnea_gat_da2_f32": (ctypes.c_int, [_p, _i64, _i64, ctypes.c_int, ctypes.c_int, _p, _p, _p,
+                                         _p, _p, _i64, _p]),
+    "gnnea_gat_da2_bf16": (ctypes.c_int, [_p, _i64, _i64, ctypes.c_int, ctypes.c_int, _p, _p, _p,
+                                          _p, _p, _i64, _p]),
+    "gnnea_colsum_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _i64, _p]),
+    "gnnea_colsum_bf16": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _i64, _p]),
     "gnnea_gemm_ws_bytes": (_i64, [_i64, _i64, _i64]),
     "gnnea_gemm_bf16_ws_bytes": (_i64, [_i64, _i64, _i64]),
     "gnnea_gemm_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,

@@ -747,17 +747,25 @@ def _ones(n, device):
 
 def colsum(t, out_dtype=None):
     """Column sums of a row-major [N, D] matrix (the bias gradients): one streaming pass with
-    a deterministic two-stage sum (gnnea_gat_da_* with one all-ones head weight) instead of a
-    [1, N]·[N, D] split-K GEMM; fp32 sums, returned in ``out_dtype`` (default t's dtype).  t may
-    be a column block of a wider row-major buffer."""
+    a deterministic two-stage sum (gnnea_colsum_*, the attention-gradient pass with unit
+    weights) instead of a [1, N]·[N, D] split-K GEMM; fp32 sums, returned in ``out_dtype``
+    (default t's dtype).  t may be a column block of a wider row-major buffer."""
     t = _rows(t)
     N, D = t.shape
     out_dtype = out_dtype or t.dtype
-    if D % 4 or t.stride(0) % 4 or N == 0:  # rows must be whole 4-element vectors
+    es = t.element_size()
+    if ((t.stride(0) * es) % 4 or t.data_ptr() % 4 or N == 0 or t.stride(0) < D
+            or t.dtype not in FEATURE_DTYPES):
         t = _featc(t)
         ones = torch.ones((1, N), dtype=t.dtype, device=t.device)
         return gemm(ones, t, out_dtype=out_dtype if t.dtype == torch.bfloat16 else None).view(-1)
-    s = gat_da(t, _ones(N, t.device), 1, D)
+    L = _lib.lib()
+    ws_bytes = int(L.gnnea_gat_da_ws_bytes(N, D))
+    ws = _gemm_ws(t.device, ws_bytes)
+    s = torch.empty(D, dtype=torch.float32, device=t.device)
+    fn = L.gnnea_colsum_bf16 if t.dtype == torch.bfloat16 else L.gnnea_colsum_f32
+    with _lib.on_device(t.device):
+        check(fn(ptr(t), t.stride(0), N, D, ptr(s), ptr(ws), ws_bytes, stream_of(t.device)))
     return s if out_dtype == torch.float32 else s.to(out_dtype)
 
 
@@ -1011,8 +1019,11 @@ def gat_backward(csr, H, a32, s1, s2, m, den, Y, dY, heads, d_head, alpha, act, 
     if need_da:
         # da1[h] = sum_i ds1[i,h] H_{row0+i},h ; da2[h] = sum_j ds2[j,h] H_j,h: one streaming
         # pass over H each (gnnea_gat_da_*), only the diagonal head blocks
-        p1 = gat_da(H[row0:row0 + N], ds1, heads, d_head)
-        p2 = gat_da(H, ds2, heads, d_head)
+        if row0 == 0 and H.shape[0] == N:  # both weight the same rows: one pass
+            p1, p2 = gat_da(H, ds1, heads, d_head, ds2)
+        else:
+            p1 = gat_da(H[row0:row0 + N], ds1, heads, d_head)
+            p2 = gat_da(H, ds2, heads, d_head)
         da = torch.cat([p1.view(heads, d_head), p2.view(heads, d_head)], dim=1)
     return dH, da
 
@@ -1089,8 +1100,9 @@ def _gat_backward_rows(csr, csrT, H, a32, s1, s2, m, den, Y, dY, heads, d_head, 
             dH.stride(0), ptr(ds1), st))
 
 
-def gat_da(H, ds, heads, d_head):
-    """out[c] = sum_r ds[r, c // d_head] * H[r, c] (fp32, heads*d_head values)."""
+def gat_da(H, ds, heads, d_head, ds2=None):
+    """out[c] = sum_r ds[r, c // d_head] * H[r, c] (fp32, heads*d_head values); with ``ds2`` the
+    pair (out from ds, out from ds2) in one pass over H (gnnea_gat_da2_*)."""
     L = _lib.lib()
     n = H.shape[0]
     D = heads * d_head
@@ -1099,6 +1111,13 @@ def gat_da(H, ds, heads, d_head):
     out = torch.empty(D, dtype=torch.float32, device=H.device)
     ds = _featc(ds, torch.float32)
     with _lib.on_device(H.device):
+        if ds2 is not None:
+            ds2 = _featc(ds2, torch.float32)
+            out2 = torch.empty(D, dtype=torch.float32, device=H.device)
+            check(_gat_fn("gnnea_gat_da2", H.dtype)(ptr(H), H.stride(0), n, heads, d_head,
+                                                    ptr(ds), ptr(ds2), ptr(out), ptr(out2),
+                                                    ptr(ws), ws_bytes, stream_of(H.device)))
+            return out, out2
         check(_gat_fn("gnnea_gat_da", H.dtype)(ptr(H), H.stride(0), n, heads, d_head, ptr(ds),
                                                ptr(out), ptr(ws), ws_bytes,
                                                stream_of(H.device)))

@@ -292,13 +292,29 @@ int gnnea_gat_bwd_dst_f32(const int32_t* rowptr, const int64_t* tpos, int32_t n_
 /* attention-vector gradient pieces (autograd of att_layers.py:38): out[c] = sum_r ds[r, c/d_head]
  * * H[r, c] over the n_rows rows of H (ds: n_rows x heads fp32, ds1 or ds2 of the backward),
  * c < heads*d_head; one streaming pass over H, deterministic two-stage sum.  H rows are read as
- * 4-element vectors up to roundup4(heads*d_head) (ldh >= that, % 4 == 0, aligned).
+ * 16-B granules within their row stride (ldh >= heads*d_head, rows 4-B aligned; the table's
+ * last row element by element when its final granule would pass the table's end).
  * Workspace from gnnea_gat_da_ws_bytes. */
 int64_t gnnea_gat_da_ws_bytes(int64_t n_rows, int32_t D);
 int gnnea_gat_da_f32(const float* H, int64_t ldh, int64_t n_rows, int heads, int d_head,
                      const float* ds, float* out, void* ws, int64_t ws_bytes, void* stream);
 int gnnea_gat_da_bf16(const void* H, int64_t ldh, int64_t n_rows, int heads, int d_head,
                       const float* ds, float* out, void* ws, int64_t ws_bytes, void* stream);
+/* both pieces of one layer in ONE pass over H when they weight the same rows (the whole-graph
+ * backward: ds1 and ds2 are both n_rows x heads): out1 from ds1, out2 from ds2 */
+int gnnea_gat_da2_f32(const float* H, int64_t ldh, int64_t n_rows, int heads, int d_head,
+                      const float* ds1, const float* ds2, float* out1, float* out2, void* ws,
+                      int64_t ws_bytes, void* stream);
+int gnnea_gat_da2_bf16(const void* H, int64_t ldh, int64_t n_rows, int heads, int d_head,
+                       const float* ds1, const float* ds2, float* out1, float* out2, void* ws,
+                       int64_t ws_bytes, void* stream);
+/* column sums out[c] = sum_r X[r, c], c < D (the bias gradients, autograd of nn.Linear's bias,
+ * layers/layers.py:32): the same streaming pass with unit weights, fp32 sums; workspace from
+ * gnnea_gat_da_ws_bytes(n_rows, D); X rows 4-B aligned */
+int gnnea_colsum_f32(const float* X, int64_t ldx, int64_t n_rows, int32_t D, float* out,
+                     void* ws, int64_t ws_bytes, void* stream);
+int gnnea_colsum_bf16(const void* X, int64_t ldx, int64_t n_rows, int32_t D, float* out,
+                      void* ws, int64_t ws_bytes, void* stream);
 
 /* bf16 feature storage (cfg-5): H, Y, dY, G, dH are bf16 (void*, row strides % 4 == 0, 8-B
  * aligned); s1, s2, m, den, rec, dzT, ds1, ds2, a and edge_mask stay fp32; arithmetic is fp32 and

@@ -328,9 +328,12 @@ def test_gcn_layer_sliced_bf16_matches_rowmajor(device, monkeypatch):
 
 
 @pytest.mark.parametrize("N,D,dt", [(1, 300, torch.float32), (2_000_001, 300, torch.float32),
-                                    (30000, 12, torch.bfloat16), (777, 10, torch.float32)])
+                                    (30000, 12, torch.bfloat16), (777, 10, torch.float32),
+                                    (100_003, 300, torch.bfloat16), (1001, 302, torch.bfloat16),
+                                    (513, 7, torch.bfloat16), (4_000_000, 300, torch.bfloat16)])
 def test_colsum_vs_fp64(device, N, D, dt):
-    """Bias gradients: streaming column sums (gnnea_gat_da_*), also over a column block."""
+    """Bias gradients: streaming column sums (gnnea_colsum_*), also over a column block (bf16
+    D = 300: the table's last row ends inside a 16-B granule and takes the element path)."""
     from gnnea import ops
     torch.manual_seed(N)
     t = torch.randn(N, D, device=device).to(dt)
@@ -339,9 +342,33 @@ def test_colsum_vs_fp64(device, N, D, dt):
     assert got.dtype == dt
     tol = 1e-5 if dt == torch.float32 else 1e-2
     assert rel_err(got.float().cpu(), ref) < tol
-    if D % 4 == 0:
+    if D % 4 == 0 and N < 3_000_000:
         wide = torch.randn(N, 2 * D + 4, device=device).to(dt)
         assert rel_err(ops.colsum(wide[:, :D]).float().cpu(), wide[:, :D].double().sum(0).cpu()) < tol
+
+
+@pytest.mark.parametrize("N,heads,d_head,dt", [
+    (4_000_000, 4, 75, torch.bfloat16), (2_000_000, 4, 75, torch.float32),
+    (10_007, 1, 300, torch.float32), (10_007, 2, 64, torch.bfloat16), (999, 8, 32, torch.float32),
+    (3001, 4, 6, torch.bfloat16), (3001, 3, 50, torch.float32), (1, 4, 75, torch.bfloat16)])
+def test_gat_da_pair_vs_fp64(device, N, heads, d_head, dt):
+    """Attention-vector gradient pieces out[c] = sum_r ds[r, c // d_head] H[r, c]: one set
+    (gnnea_gat_da_*) and both sets in one pass over H (gnnea_gat_da2_*) vs fp64; four heads with
+    d_head >= a granule's elements pick a granule's two heads once, the rest read per element."""
+    from gnnea import ops
+    torch.manual_seed(N + heads)
+    D = heads * d_head
+    Hm = torch.randn(N, D, device=device).to(dt)
+    ds1 = torch.randn(N, heads, device=device)
+    ds2 = torch.randn(N, heads, device=device)
+    Hd = Hm.double().view(N, heads, d_head)
+    ref1 = (Hd * ds1.double()[:, :, None]).sum(0).reshape(-1).cpu()
+    ref2 = (Hd * ds2.double()[:, :, None]).sum(0).reshape(-1).cpu()
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    p1, p2 = ops.gat_da(Hm, ds1, heads, d_head, ds2)
+    assert rel_err(p1.cpu(), ref1) < tol and rel_err(p2.cpu(), ref2) < tol
+    q1 = ops.gat_da(Hm, ds1, heads, d_head)
+    assert torch.equal(q1, p1)  # the same per-lane chains and the same partial order
 
 
 @pytest.mark.parametrize("heads,d_head,act", [(4, 75, 1), (2, 64, 0), (1, 300, 1), (8, 32, 1)])
