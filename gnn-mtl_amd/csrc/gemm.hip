@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <type_traits>
 #include "common.h"
+#include "gemm_ta.h"
 #include "lds_dma.h"
 
 namespace gnnea {
@@ -1247,6 +1248,19 @@ static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t l
   if (!C || !A || !B) return GNNEA_EINVAL;
   if (cs == 64 ? ldc < N : (ldc < (N < 64 ? N : 64) || cs < M * ldc)) return GNNEA_EINVAL;
   if (lda < M || ldb < N) return GNNEA_EINVAL;
+  if (gemm_ta_applies(M, N, K, lda, ldb, A, B, 4)) {  // whole-width tiles (gemm_ta.hip)
+    float* slab = nullptr;
+    int used = 0;
+    const int rc = gemm_ta_launch<float>(M, N, K, A, lda, B, ldb, ws, ws ? ws_bytes : 0, s,
+                                         &slab, &used);
+    if (rc) return rc;
+    const int64_t n = M * N;
+    const int nb = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+    hipLaunchKernelGGL(k_gemm_reduce, dim3(nb), dim3(256), 0, s, (int)M, (int)N, used, slab,
+                       bias, beta, C, ldc, cs);
+    GNNEA_LAUNCH_CHECK();
+    return 0;
+  }
   int wt = pick_wt(N);
   const int64_t bn = 64 * wt;
   const int tiles_n = (int)((N + bn - 1) / bn);
@@ -1291,7 +1305,9 @@ static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t l
 
 extern "C" int64_t gnnea_gemm_x3t_ws_bytes(int64_t M, int64_t N, int64_t K) {
   if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
-  return x3_ta_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
+  const int64_t a = x3_ta_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
+  const int64_t b = gemm_ta_ws_bytes(M, N, K);  // whole-width form (gemm_ta.hip)
+  return a > b ? a : b;
 }
 
 extern "C" int64_t gnnea_gemm_x3_ws_bytes(int64_t M, int64_t N, int64_t K) {

@@ -13,6 +13,7 @@
 // two 8-row groups: conflict-free; row-group-fastest lanes hit 2 banks, 32-way).  Next tile's global loads are in flight under the current tile's MFMAs.
 // Split-K for the weight gradients as in gemm.hip: fp32 slabs, fixed-order reduction.
 #include "common.h"
+#include "gemm_ta.h"
 #include "lds_dma.h"
 
 #include <stdlib.h>
@@ -1085,6 +1086,19 @@ static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K
   const int64_t bn = 64 * wt;
   const int tiles_n = (int)((N + bn - 1) / bn);
   const int tiles = (int)(((M + HBM - 1) / HBM) * tiles_n);
+  if (trans_a && !trans_b && cs == 128 && gemm_ta_applies(M, N, K, lda, ldb, A, B, 2)) {
+    float* slab = nullptr;  // whole-width weight-gradient tiles (gemm_ta.hip)
+    int used = 0;
+    const int rc = gemm_ta_launch<bf16_t>(M, N, K, A, lda, B, ldb, ws, ws ? ws_bytes : 0, s,
+                                          &slab, &used);
+    if (rc) return rc;
+    const int64_t nn = M * N;
+    const int nb = (int)((nn + 255) / 256 < 4096 ? (nn + 255) / 256 : 4096);
+    hipLaunchKernelGGL((k_gemm_bf16_reduce<TC>), dim3(nb), dim3(256), 0, s, (int)M, (int)N, used,
+                       slab, bias, beta, C, ldc, cs);
+    GNNEA_LAUNCH_CHECK();
+    return 0;
+  }
   const int splits = ws ? bf16_splits(M, N, K, ws_bytes) : 1;
   const int kps = (int)(((K + splits - 1) / splits + HBK - 1) / HBK * HBK);
   float* slab = splits > 1 ? (float*)ws : nullptr;
@@ -1115,7 +1129,8 @@ using namespace gnnea;
 
 extern "C" int64_t gnnea_gemm_bf16_ws_bytes(int64_t M, int64_t N, int64_t K) {
   if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
-  const int64_t split = bf16_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
+  int64_t split = bf16_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
+  if (gemm_ta_ws_bytes(M, N, K) > split) split = gemm_ta_ws_bytes(M, N, K);  // gemm_ta.hip
   int64_t planes = bf16p_planes_bytes(N, K);  // k_gemm_bf16p / k_gemm_bf16w (shape-dependent)
   if (bf16w_planes_bytes(N, K) > planes) planes = bf16w_planes_bytes(N, K);
   return split > planes ? split : planes;

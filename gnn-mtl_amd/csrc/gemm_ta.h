@@ -1,0 +1,16 @@
+// Full-width weight-gradient GEMM (gemm_ta.hip): dW partials = Aᵀ·B for A [K][M], B [K][N] with
+// M <= 320, N <= 320, written as split-K fp32 slabs that the caller reduces (k_gemm_reduce /
+// k_gemm_bf16_reduce).  Internal to libgnnea (no C-ABI entry of its own).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gnnea {
+bool gemm_ta_applies(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* A,
+                     const void* B, int es);
+int64_t gemm_ta_ws_bytes(int64_t M, int64_t N, int64_t K);
+template <typename T>
+int gemm_ta_launch(int64_t M, int64_t N, int64_t K, const T* A, int64_t lda, const T* B,
+                   int64_t ldb, void* ws, int64_t ws_bytes, hipStream_t s, float** slab_out,
+                   int* splits_out);
+}  // namespace gnnea

@@ -331,3 +331,37 @@ def test_model_bf16_end_to_end(golden, device, model):
         cos = float(torch.nn.functional.cosine_similarity(p16.flatten().double(),
                                                           p32.flatten().double(), dim=0))
         assert cos > 0.8, cos
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 300, 4_000_000), (300, 300, 1_000_003), (152, 300, 4099),
+                                   (300, 168, 999), (8, 8, 128), (320, 320, 100_000),
+                                   (300, 300, 20_000)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gemm_weight_grad_full_width(device, M, N, K, dt):
+    """dW = Aᵀ·B (A [K][M], B [K][N]) on the whole-width split-K kernel (gemm_ta.hip: all M
+    rows x a 160-column half per workgroup, operands read transposed from LDS): fp32 through the
+    three-way bf16 split (fp32-level error), bf16 operands with fp32 / bf16 output; a column
+    block of a wider buffer as A (the fused HighWay layer's dh = P[:, :D]), bias and beta, K tails
+    inside a 32-row step, the table's last row ending inside a 16-B chunk (bf16 M = 300)."""
+    from gnnea import ops
+    torch.manual_seed(M + N + K)
+    if K >= 1_000_000 and dt == torch.float32:
+        K //= 2  # the cfg-4 row count
+    wide = torch.randn(K, M + 4, device=device).to(dt)
+    a = wide[:, :M]
+    b = torch.randn(K, N, device=device).to(dt)
+    bias = torch.randn(N, device=device)
+    ref = (a.double().t() @ b.double()).cpu()
+    tol = 1e-5 if dt == torch.float32 else TOL_ACC
+    y = ops.gemm(a, b, trans_a=True, out_dtype=torch.float32)
+    assert rel_err(y.cpu(), ref) < tol
+    yb = ops.gemm(a, b, trans_a=True, bias=bias, out_dtype=torch.float32)
+    assert rel_err(yb.cpu(), ref + bias.double().cpu()) < tol
+    prev = torch.randn(M, N, device=device)
+    acc = prev.clone()
+    ops.gemm(a, b, trans_a=True, out=acc, beta=0.5)
+    assert rel_err(acc.cpu(), ref + 0.5 * prev.double().cpu()) < tol
+    if dt == torch.bfloat16:
+        y16 = ops.gemm(a, b, trans_a=True)
+        assert y16.dtype == torch.bfloat16
+        assert torch.equal(y16.view(torch.int16), y.to(torch.bfloat16).view(torch.int16))

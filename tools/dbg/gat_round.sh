@@ -8,10 +8,11 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   -p no:cacheprovider -k "gat or GAT or bf16 or colsum ${EXTRA_K:-}" > $OUT/gat_tests.log 2>&1
 rc=$?; tail -3 $OUT/gat_tests.log; [ $rc -eq 0 ] || exit $rc
-for s in gat5 gat4; do
+for s in ${STEPS:-gat5 gat4}; do
   case $s in
     gat5) a="--model GAT --dtype bf16 --entities 2000000" ;;
     gat4) a="--model GAT" ;;
+    hgcn) a="--model HGCN" ;;
   esac
   rm -rf $OUT/prof_$s
   ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$s" -o run \
