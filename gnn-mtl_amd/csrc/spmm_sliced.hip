@@ -19,6 +19,8 @@
 // so the two agree to fp32 rounding, not bit for bit.
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace gnnea {
 
 template <typename T>
@@ -46,7 +48,13 @@ struct SlicedHighway {
 
 __device__ __forceinline__ float sigm_f(float x) { return 1.f / (1.f + expf(-x)); }
 
-template <int ACT, int U, bool HW, typename TX, typename TY>
+// PIPE (default): the gathers of a row are issued unconditionally (edges past the chunk re-read
+// its last edge's piece with weight 0; lanes past D read their group's first 16 B and discard
+// the sum), in batches of 4U edges with the next batch in flight while one is summed (register
+// double buffer), so no gathered piece is waited on inside a branch; !PIPE: one batch at a time
+// behind per-lane conditions (A/B timing, GNNEA_SPMM_PIPE=0).  The per-lane sum order is the
+// same either way (edge k + 4u + g, u ascending).
+template <int ACT, int U, bool HW, typename TX, typename TY, bool PIPE = true>
 __global__ __launch_bounds__(256) void k_spmm_sliced(const int32_t* __restrict__ rowptr,
                                                      const int32_t* __restrict__ col,
                                                      const float* __restrict__ val, int n_rows,
@@ -67,6 +75,46 @@ __global__ __launch_bounds__(256) void k_spmm_sliced(const int32_t* __restrict__
   float acc[E];
 #pragma unroll
   for (int k = 0; k < E; ++k) acc[k] = 0.f;
+  if constexpr (PIPE) {
+    const uint4* Xp = Xs + (int64_t)s * sstride16 + (own ? c : 0);
+    for (int base = beg; base < end; base += 64) {
+      const int cnt = min(64, end - base);
+      const int el = base + min(lane, cnt - 1);
+      const int mc = col[el];
+      const float mv = val[el] * (lane < cnt ? 1.f : 0.f);  // (a select would sink the load)
+      uint4 ra[U], rb[U];
+      auto issue = [&](uint4 (&r)[U], int k) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int j = __shfl(mc, min(k + 4 * u + g, cnt - 1), 64);
+          r[u] = Xp[(int64_t)j * 16];
+        }
+      };
+      auto consume = [&](const uint4 (&r)[U], int k) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = k + 4 * u + g;
+          // (the shuffle runs in every lane: a bpermute from a lane masked off by the
+          // condition would return its inactive value)
+          const float vs = __shfl(mv, e & 63, 64);
+          const float v = e < cnt ? vs : 0.f;
+          float f[E];
+          unpack16(r[u], f);
+#pragma unroll
+          for (int q = 0; q < E; ++q) acc[q] = fmaf(v, f[q], acc[q]);
+        }
+      };
+      issue(ra, 0);
+      for (int k = 0; k < cnt; k += 8 * U) {
+        issue(rb, k + 4 * U);
+        __builtin_amdgcn_sched_barrier(0);  // the next batch's gathers ahead of this batch's FMAs
+        consume(ra, k);
+        issue(ra, k + 8 * U);
+        __builtin_amdgcn_sched_barrier(0);
+        consume(rb, k + 4 * U);
+      }
+    }
+  } else
   for (int base = beg; base < end; base += 64) {
     const int cnt = min(64, end - base);
     const int mc = lane < cnt ? col[base + lane] : 0;
@@ -215,9 +263,17 @@ static int spmm_sliced(const int32_t* rowptr, const int32_t* col, const float* v
   const int S = (D + W - 1) / W;
   if ((int64_t)nbs * S >= (1ll << 31)) return GNNEA_EINVAL;
   const int64_t ss16 = sstride * (int64_t)sizeof(TX) / 16;
+  static const bool pipe = [] {  // A/B timing only (GNNEA_SPMM_PIPE=0: one batch at a time)
+    const char* e = getenv("GNNEA_SPMM_PIPE");
+    return !(e && e[0] == '0');
+  }();
 #define GNNEA_SS(A)                                                                            \
-  hipLaunchKernelGGL((k_spmm_sliced<A, 4, HW, TX, TY>), dim3(nbs * S), dim3(256), 0, s,        \
-                     rowptr, col, val, n_rows, nbs, D, (const uint4*)Xs, ss16, Y, ldy, hw)
+  if (pipe)                                                                                    \
+    hipLaunchKernelGGL((k_spmm_sliced<A, 2, HW, TX, TY, true>), dim3(nbs * S), dim3(256), 0, s, \
+                       rowptr, col, val, n_rows, nbs, D, (const uint4*)Xs, ss16, Y, ldy, hw);  \
+  else                                                                                         \
+    hipLaunchKernelGGL((k_spmm_sliced<A, 4, HW, TX, TY, false>), dim3(nbs * S), dim3(256), 0,  \
+                       s, rowptr, col, val, n_rows, nbs, D, (const uint4*)Xs, ss16, Y, ldy, hw)
   switch (act) {
     case GNNEA_ACT_IDENTITY: GNNEA_SS(GNNEA_ACT_IDENTITY); break;
     case GNNEA_ACT_RELU: GNNEA_SS(GNNEA_ACT_RELU); break;
