@@ -25,8 +25,11 @@
 // writes, one or two k-steps behind the loads (bf16: two register sets in flight).  The table's
 // last row never reads past the table: a 16-B chunk that would (bf16, M·2 % 16 == 8) is read 8 B
 // earlier and shifted down.
+#include <type_traits>
+
 #include "common.h"
 #include "gemm_ta.h"
+#include "lds_dma.h"
 
 namespace gnnea {
 
@@ -277,7 +280,227 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta(int M, int N, int K,
   }
 }
 
+// ---- k_gemm_ta_x3d: the fp32 form fed by LDS-DMA, split at the fragment read ----
+// k_gemm_ta<float> splits every element into h / m / l planes when it writes LDS: a 97.5-KB image
+// per 32-row k-step, so there is one stage, one register set of loads in flight, and the split +
+// write phase of every step runs with the matrix cores idle (2.61 ms at 2M x 300 x 300, ~5.2k
+// cycles per k-step above the MFMA time).  Here the RAW fp32 tiles go to LDS by global_load_lds
+// (A [32][320] + B [32][160] = 60 KB per stage, two stages: the next step's DMA in flight under
+// this step's MFMAs, one barrier per step, no load registers) and each wave splits the fragments
+// it reads: lane l of a 16x16x32 operand needs rows k = 8 (l / 16) + 0..7 of its column, eight
+// ds_read_b32 (image rows 1280 / 640 B apart; the 16-B chunks of rows 8..15 mod 16 XOR 4, so the
+// two 16-lane row groups of a half-wave hit disjoint banks), then three v_cvt_pk_bf16_f32 rounds
+// per pair give the h / m / l operands already packed.  A's five fragments are split once per step
+// and stay in registers (60); B's are split one column tile at a time, the next one's reads in
+// flight under the current tile's 30 MFMAs.  Same six products in the same order as k_gemm_ta.
+// LDS reads are inline asm (hipcc would wait vmcnt(0) for the in-flight DMA before plain ones)
+// with explicit lgkmcnt waits.  Rows past a split's end are DMA'd from its last row and zeroed in
+// registers (one uniform branch, last step only).
+constexpr int TD_RSA = 1280, TD_RSB = 640;                   // image row strides (bytes)
+constexpr int TD_IMG_A = TA_BK * TD_RSA, TD_IMG_B = TA_BK * TD_RSB;
+constexpr int TD_STAGE = TD_IMG_A + TD_IMG_B;                // 61,440 B
+constexpr int TD_DMA = TD_STAGE / 1024;                      // 1-KB DMA blocks per stage (60)
+constexpr int TD_PER_WAVE = (TD_DMA + 7) / 8;                // 8
+
+__device__ __forceinline__ float td_ld(uint32_t addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ float td_ld_o(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
+  float v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
+  return v;
+}
+
+struct TdTriple {
+  ta_bf16x8 h, m, l;
+};
+
+// x = h + m + l exactly (the x3 split of gemm.hip / k_gemm_ta, round to nearest even)
+__device__ __forceinline__ TdTriple td_split(const float (&x)[8]) {
+  TdTriple t;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 h = (__bf16)x[e];
+    const float r1 = x[e] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    const __bf16 l = (__bf16)(r1 - (float)m);
+    t.h[e] = h;
+    t.m[e] = m;
+    t.l[e] = l;
+  }
+  return t;
+}
+
+template <int RS>
+__device__ __forceinline__ void td_read8(uint32_t addr, float (&x)[8]) {
+  static_for<8>([&](auto ee) {
+    constexpr int e = decltype(ee)::value;
+    x[e] = td_ld_o<e * RS>(addr);
+  });
+}
+
+__global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
+                                                          const float* __restrict__ A,
+                                                          int64_t lda,
+                                                          const float* __restrict__ B,
+                                                          int64_t ldb, int kps, int tiles_n,
+                                                          float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TD_STAGE];
+  const int t_id = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = t_id % tiles_n, split = t_id / tiles_n;
+  const int n0 = tn * TA_NP;
+  const int kb = split * kps;
+  const int ke = min(K, kb + kps);
+  if (kb >= ke) return;  // (the host sizes the grid so that every split has rows)
+  const int nsteps = (ke - kb + TA_BK - 1) / TA_BK;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w & 3, wn = w >> 2;
+
+  // DMA block i = w + 8 t of a stage: image bytes [i KB, i KB + 1 KB), lane-linear; the lane's
+  // source row / column follow from its image position (chunk positions XOR-swizzled)
+  int d_row[TD_PER_WAVE], d_off[TD_PER_WAVE];
+  bool d_isa[TD_PER_WAVE];
+#pragma unroll
+  for (int t = 0; t < TD_PER_WAVE; ++t) {
+    int i = w + 8 * t;
+    if (i >= TD_DMA) i = TD_DMA - 1;  // waves 4..7 repeat the last block (same bytes, same slot)
+    const int off = i * 1024 + lane * 16;
+    const bool isa = off < TD_IMG_A;
+    const int o2 = isa ? off : off - TD_IMG_A;
+    const int rs = isa ? TD_RSA : TD_RSB;
+    const int row = o2 / rs;
+    const int pos = (o2 - row * rs) / 16;
+    const int c = pos ^ (((row >> 3) & 1) << 2);   // logical 16-B chunk of the row
+    int col = (isa ? 0 : n0) + 4 * c;
+    if (col >= (isa ? M : N)) col = isa ? 0 : n0;  // past the row: a valid chunk (never stored)
+    d_row[t] = row;
+    d_off[t] = col;
+    d_isa[t] = isa;
+  }
+  auto issue = [&](int s, int buf) {
+    const int k0 = kb + s * TA_BK;
+    const bool tail = k0 + TA_BK > ke;  // uniform
+    unsigned char* st = smem + buf * TD_STAGE;
+#pragma unroll
+    for (int t = 0; t < TD_PER_WAVE; ++t) {
+      int i = w + 8 * t;
+      if (i >= TD_DMA) i = TD_DMA - 1;
+      const int r = tail ? min(k0 + d_row[t], ke - 1) : k0 + d_row[t];
+      const float* src = d_isa[t] ? A + (int64_t)r * lda + d_off[t] : B + (int64_t)r * ldb + d_off[t];
+      glds16(src, st + i * 1024);
+    }
+  };
+
+  ta_f32x4 acc[5][5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[i][j] = ta_f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read addresses (stage 0): lane l -> column l % 16 of a 16-wide tile, rows
+  // 8 (l / 16) + e; chunk (col / 4) ^ (4 * ((l / 16) & 1)), dword col % 4
+  const int g = lane >> 4, cl = lane & 15;
+  const uint32_t base = lds_addr(smem);
+  uint32_t a_ad[5], b_ad[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int m = wm * 80 + 16 * i + cl;
+    a_ad[i] = base + 8 * g * TD_RSA + (((m >> 2) ^ ((g & 1) << 2)) << 4) + (m & 3) * 4;
+    const int n = wn * 80 + 16 * i + cl;
+    b_ad[i] = base + TD_IMG_A + 8 * g * TD_RSB + (((n >> 2) ^ ((g & 1) << 2)) << 4) + (n & 3) * 4;
+  }
+
+  issue(0, 0);
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of step s
+    __builtin_amdgcn_s_barrier();  // everyone's landed; everyone is done with buffer buf ^ 1
+    asm volatile("" ::: "memory");
+    if (s + 1 < nsteps) issue(s + 1, buf ^ 1);
+    const uint32_t so = buf * TD_STAGE;
+    const int k0 = kb + s * TA_BK;
+    const int kval = ke - k0 - 8 * g;  // valid rows of this lane's eight (>= 8 but at the tail)
+    const bool tail = k0 + TA_BK > ke;  // uniform
+
+    // A fragment i + 1 (the last time: B's first) in flight while fragment i is split
+    TdTriple at[5];
+    float xa[2][8], xb[8];
+    td_read8<TD_RSA>(a_ad[0] + so, xa[0]);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      if (i + 1 < 5)
+        td_read8<TD_RSA>(a_ad[i + 1] + so, xa[(i + 1) & 1]);
+      else
+        td_read8<TD_RSB>(b_ad[0] + so, xb);
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      float (&x)[8] = xa[i & 1];
+      if (tail) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = e < kval ? x[e] : 0.f;
+      }
+      at[i] = td_split(x);
+    }
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (tail) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xb[e] = e < kval ? xb[e] : 0.f;
+      }
+      const TdTriple bt = td_split(xb);
+      if (j + 1 < 5) td_read8<TD_RSB>(b_ad[j + 1] + so, xb);  // in flight under the MFMAs
+      // product-major: five independent accumulators between two dependent MFMAs (each
+      // accumulator still sums its six products in k_gemm_ta's order)
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[i].l, bt.h, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[i].m, bt.m, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[i].h, bt.l, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[i].m, bt.h, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[i].h, bt.m, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[i].h, bt.h, acc[i][j], 0, 0, 0);
+    }
+  }
+
+  float* out = slab + (int64_t)split * M * N;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int n = n0 + wn * 80 + 16 * j + (lane & 15);
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = wm * 80 + 16 * i + 4 * (lane >> 4) + r;
+        if (m < M) out[(int64_t)m * N + n] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // ---- host side ----
+
+static bool ta_x3d_on() {  // A/B comparison only (GNNEA_TA_X3D=0: k_gemm_ta<float>)
+  static const bool on = [] {
+    const char* e = getenv("GNNEA_TA_X3D");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 static int ta_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
   const int tiles_n = (int)((N + TA_NP - 1) / TA_NP);
@@ -316,8 +539,12 @@ int gemm_ta_launch(int64_t M, int64_t N, int64_t K, const T* A, int64_t lda, con
   // every split must own rows (kps rounding can leave the last ones empty): trim the grid
   const int used = (int)((K + kps - 1) / kps);
   float* slab = (float*)ws;
-  hipLaunchKernelGGL((k_gemm_ta<T>), dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M, (int)N,
-                     (int)K, A, lda, B, ldb, kps, tiles_n, slab);
+  if (std::is_same<T, float>::value && ta_x3d_on())
+    hipLaunchKernelGGL(k_gemm_ta_x3d, dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M, (int)N,
+                       (int)K, (const float*)A, lda, (const float*)B, ldb, kps, tiles_n, slab);
+  else
+    hipLaunchKernelGGL((k_gemm_ta<T>), dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M, (int)N,
+                       (int)K, A, lda, B, ldb, kps, tiles_n, slab);
   GNNEA_LAUNCH_CHECK();
   *slab_out = slab;
   *splits_out = used;
