@@ -691,10 +691,23 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hg(
   using WN = RowWin<T, EPL>;
   constexpr int W = WN::W;
   constexpr int LPH = L::LPH;
+  // per wave: the chunk's edge weights [edge][head] (each lane then loads its head's weight of an
+  // edge: one broadcast ds_read instead of H readlanes + selects) and the per-edge per-head
+  // G_i . H_j sums, written by the lanes grp_sum leaves them in and read back by the edge's lane
+  // once per chunk (instead of H readlanes + selects per edge)
+  __shared__ float sh_w[4][64 * H];
+  __shared__ float sh_d[4][64 * H];
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const int row = blk * 4 + wave_id();  // source node j
   if (row >= n_rows) return;
   const int lane = lane_id();
+  float* shw = sh_w[wave_id()];
+  float* shd = sh_d[wave_id()];
+  // the lane holding (edge e, head h) of a group's grp_sum: h * LPH + S e, S = 16 / F (8 / F)
+  constexpr int GS = (LPH >= 16 ? 16 : 8) / F;
+  const int gp = lane % LPH;
+  const bool g_hold = gp < GS * F && gp % GS == 0 && lane / LPH < H;
+  const int g_slot = (gp / GS) * H + lane / LPH;  // + k * H
   const int beg = rowptrT[row], end = rowptrT[row + 1];
   const L hl(lane, dh);
   const int hme = hl.h < H ? hl.h : 0;
@@ -746,37 +759,30 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hg(
       sl[h] = z > 0.f ? 1.f : alpha;
       if constexpr (!EM) ml[h] = 1.f;
       wl[h] = EM ? al[h] * ml[h] : al[h];
-      dzl[h] = 0.f;
+      shw[lane * H + h] = wl[h];  // lanes past the chunk: 0
     }
     auto consume = [&](const uint32_t (&g)[F][W], int k) {
-      float pd[F];
+      float pd[F], we[F];
+#pragma unroll
+      for (int e = 0; e < F; ++e) we[e] = shw[min(k + e, 63) * H + hme];
 #pragma unroll
       for (int e = 0; e < F; ++e) {
         float x[EPL];
         WN::unpack(g[e], wsh, x);
         const bool live = k + e < cnt;  // uniform; no branch between issue and use
-        const float we = head_w<H>(wl, min(k + e, 63), hme);
         float q = 0.f;
 #pragma unroll
         for (int t = 0; t < EPL; ++t) {
           const float gv = hl.ok[t] ? x[t] : 0.f;
-          const float u = fmaf(we, gv, acc[t]);
+          const float u = fmaf(we[e], gv, acc[t]);
           acc[t] = live ? u : acc[t];
           q = fmaf(gv, hj[t], q);
         }
         pd[e] = q;
       }
       const float v = grp_sum<F, LPH>(pd, lane);
-#pragma unroll
-      for (int e = 0; e < F; ++e) {  // lanes past the chunk take a dz that is never stored
-        float da[H];
-#pragma unroll
-        for (int h = 0; h < H; ++h) da[h] = readlane_f(v, h * LPH + grp_lane<F, LPH>(e));
-        if (lane == k + e) {
-#pragma unroll
-          for (int h = 0; h < H; ++h) dzl[h] = -(al[h] * (ml[h] * da[h] - cl[h])) * sl[h];
-        }
-      }
+      // slots past the chunk (k + e >= cnt, still < 64) take sums that are never read
+      if (g_hold) shd[k * H + g_slot] = v;
     };
     for (int k = 0; k < cnt; k += 2 * F) {
       issue(gb, k + F);
@@ -785,6 +791,11 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hg(
       issue(ga, k + 2 * F);
       __builtin_amdgcn_sched_barrier(0);
       consume(gb, k + F);
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {  // the edge's lane: dz = -(alpha (mask da - c_i)) LReLU'(z)
+      const float da = shd[lane * H + h];
+      dzl[h] = -(al[h] * (ml[h] * da - cl[h])) * sl[h];
     }
     if (lane < cnt) {
 #pragma unroll
