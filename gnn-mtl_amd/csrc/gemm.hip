@@ -17,6 +17,7 @@
 #include <type_traits>
 #include "common.h"
 #include "gemm_ta.h"
+#include "gemm_x3w.h"
 #include "lds_dma.h"
 
 namespace gnnea {
@@ -1029,7 +1030,9 @@ extern "C" int gnnea_gemm_sliced_f32(int trans_a, int trans_b, int64_t M, int64_
 static int64_t x3_planes_bytes(int64_t N, int64_t K) {
   const int64_t kp = (K + 1 + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign;
   const int64_t np = (N + 319) / 320 * 320;  // k_gemm_x3p's padded rows (>= N, any tile width)
-  return ((3 * np * kp * 2 + 255) & ~(int64_t)255) + 1024;
+  const int64_t p = (3 * np * kp * 2 + 255) & ~(int64_t)255;
+  const int64_t w = gemm_x3w_ws_bytes(N);  // or gemm_x3w.hip's weight tiles
+  return (p > w ? p : w) + 1024;
 }
 
 static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
@@ -1049,8 +1052,14 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
                    int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
                    float* C, int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, void* stream,
                    float* C2 = nullptr, int64_t cs2 = 0) {
+  if (C2 && (cs2 % 4 != 0 || cs2 < M * 64 || cs != 64)) return GNNEA_EINVAL;
+  // the weight-resident form (gemm_x3w.hip) for the tall K <= 320 projections; it writes C2 too
+  if (B && ldc >= N && (trans_b ? ldb >= K : ldb >= N) &&
+      gemm_x3w_applies(trans_a, M, N, K, lda, A, beta, ldc, cs, C, C2, cs2) && ws &&
+      ws_bytes >= gemm_x3w_ws_bytes(N))
+    return gemm_x3w_launch(trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, cs, C2, cs2, ws,
+                           ws_bytes, (hipStream_t)stream);
   if (C2) {  // a slice-major copy as well: fused into k_gemm_x3p's epilogue, else packed after
-    if (cs2 % 4 != 0 || cs2 < M * 64 || cs != 64) return GNNEA_EINVAL;
     const bool lda_ok = !trans_a && lda % 4 == 0 && K % 4 == 0 && (((uintptr_t)A) & 15) == 0;
     const int64_t pb = x3_planes_bytes(N, K);
     // the same condition as k_gemm_x3p's launch below (pipe on, float4 A, no split-K): any other

@@ -1,0 +1,306 @@
+// fp32 projection GEMM through the three-way bf16 split with the WEIGHT RESIDENT in LDS
+// (k_gemm_x3w): C[M][N] = A[M][K] · op(B) (+ bias) for the EA layers' projections (x·Wᵀ + b,
+// dX = dY·W, x·[Wᵀ|K_g]: layers/layers.py:32,61, att_layers.py:33 and their autograd), K in
+// (256, 320], M tall.
+//
+// k_gemm_x3p streams both operands through an LDS-DMA ring (2.45 ms at 2M x 300 x 300): the B
+// tile is re-read from L2 for every 256-row tile, each k-step costs a barrier and DMA issue slots
+// beside the MFMAs, and timing modes put the DMA feed at ~0.7 ms of it.  Here (as gemm_bf16.hip's
+// k_gemm_bf16w for bf16) an 80-column tile of the weight, split h / m / l, stays in LDS for the
+// whole launch (3 planes x 320 k x 80 n bf16 = 150 KB, one 8-wave workgroup per CU) and the
+// activations go straight from HBM into registers: no barrier and no LDS traffic for A.  The
+// product is computed transposed, Dᵀ = W_tile · Aᵀ on v_mfma_f32_16x16x32_bf16: the weight tile is
+// the MFMA's A operand (ds_read_b128 of 8 k per lane, conflict-free), 16 activation rows per wave
+// its B operand, split in registers; a lane's accumulators come out as 4 consecutive output
+// columns of one row (16-B stores straight from registers, the bias added from LDS).  The k
+// dimension is permuted alike for both operands: at step s the lanes of k-quarter kq hold
+// k = 32 s + 4 kq + {0..3} and 32 s + 16 + 4 kq + {0..3}, so a wave-instruction's 64 lanes read
+// 16 rows x 64 contiguous bytes (an operand lane order that reads 16 B from 64 different lines
+// per instruction measured no faster than k_gemm_x3p).  Each wave holds its next row tile's
+// activations (20 x 16 B) in flight while it multiplies the current one.  Workgroup b owns column tile (b / 8) % ntn and the row stream
+// (b / (8 ntn)) * 8 + b % 8: the column tiles of the same rows are on one XCD (b mod 8), so A
+// is read from HBM once and from L2 by the other tiles.  Same six products, same pairing as
+// gemm.hip's x3 (small ones first); the bias joins in the epilogue (one fp32 rounding).
+#include "common.h"
+#include "gemm_x3w.h"
+
+namespace gnnea {
+
+typedef __bf16 w3_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float w3_f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int W3_NC = 80;   // columns per tile
+constexpr int W3_KC = 10;   // k-steps of 32 (K <= 320)
+constexpr int W3_NW = 4;    // waves per workgroup (one per SIMD, 512 registers)
+constexpr int W3_MF = 1;    // 16-row fragments per wave (the compute loop assumes 1)
+constexpr int W3_BM = 16 * W3_MF * W3_NW;
+constexpr int W3_PLANE = W3_KC * 4 * W3_NC;  // 16-B units per plane of a tile
+constexpr int64_t W3_TILE_BYTES = 3ll * W3_PLANE * 16;
+
+// P[nt][p][s][kq][n][8]: element e = plane p of W_op[nt*80 + n][32 s + 16 (e / 4) + 4 kq + e % 4]
+// (0 outside): lane kq's eight k of step s, the activation side's permutation
+__global__ __launch_bounds__(256) void k_pack_x3w(const float* __restrict__ B, int64_t ldb,
+                                                  int b_nk, int N, int K, int ntn,
+                                                  bf16_t* __restrict__ P) {
+  const int64_t per_plane = (int64_t)W3_PLANE * 8;
+  const int64_t total = (int64_t)ntn * per_plane;  // elements of one plane, all tiles
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(t & 7);
+    int64_t r = t >> 3;
+    const int n = (int)(r % W3_NC);
+    r /= W3_NC;
+    const int kq = (int)(r & 3);
+    r >>= 2;
+    const int s = (int)(r % W3_KC);
+    const int nt = (int)(r / W3_KC);
+    const int col = nt * W3_NC + n, k = 32 * s + 16 * (e >> 2) + 4 * kq + (e & 3);
+    float x = 0.f;
+    if (col < N && k < K) x = b_nk ? B[(int64_t)col * ldb + k] : B[(int64_t)k * ldb + col];
+    const __bf16 h = (__bf16)x;
+    const float r1 = x - (float)h;
+    const __bf16 m = (__bf16)r1;
+    const __bf16 l = (__bf16)(r1 - (float)m);
+    bf16_t* dst = P + (int64_t)nt * 3 * per_plane + (t - (int64_t)nt * per_plane);
+    dst[0] = __builtin_bit_cast(bf16_t, h);
+    dst[per_plane] = __builtin_bit_cast(bf16_t, m);
+    dst[2 * per_plane] = __builtin_bit_cast(bf16_t, l);
+  }
+}
+
+struct W3Split {
+  w3_bf16x8 h, m, l;
+};
+
+__device__ __forceinline__ W3Split w3_split(const uint4& q0, const uint4& q1) {
+  const float x[8] = {__builtin_bit_cast(float, q0.x), __builtin_bit_cast(float, q0.y),
+                      __builtin_bit_cast(float, q0.z), __builtin_bit_cast(float, q0.w),
+                      __builtin_bit_cast(float, q1.x), __builtin_bit_cast(float, q1.y),
+                      __builtin_bit_cast(float, q1.z), __builtin_bit_cast(float, q1.w)};
+  W3Split t;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 h = (__bf16)x[e];
+    const float r1 = x[e] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    t.h[e] = h;
+    t.m[e] = m;
+    t.l[e] = (__bf16)(r1 - (float)m);
+  }
+  return t;
+}
+
+__global__ __launch_bounds__(64 * W3_NW, 1) void k_gemm_x3w(int M, int N, int K, int ntn,
+                                                            const float* __restrict__ A,
+                                                            int64_t lda,
+                                                            const bf16_t* __restrict__ P,
+                                                            const float* __restrict__ bias,
+                                                            float* __restrict__ C, int64_t ldc,
+                                                            int64_t cs, float* __restrict__ C2,
+                                                            int64_t cs2) {
+  __shared__ __attribute__((aligned(16))) uint4 wl[3 * W3_PLANE];
+  __shared__ __attribute__((aligned(16))) float bsh[W3_NC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x;
+  const int nt = (b / 8) % ntn;
+  const int rs = (b / (8 * ntn)) * 8 + b % 8, nrs = (int)gridDim.x / ntn;
+  const int n0 = nt * W3_NC;
+  {  // the resident weight tile
+    const uint4* src = (const uint4*)(P + (int64_t)nt * 3 * W3_PLANE * 8);
+    for (int i = tid; i < 3 * W3_PLANE; i += 64 * W3_NW) wl[i] = src[i];
+    if (tid < W3_NC) bsh[tid] = bias && n0 + tid < N ? bias[n0 + tid] : 0.f;
+  }
+  __syncthreads();
+  const int tm = (M + W3_BM - 1) / W3_BM;
+  const int kq = lane >> 4, ml = lane & 15;
+  // this lane's quads at step s: row m, k = 32 s + 16 j + 4 kq (j = 0, 1): the four k-quarter
+  // lanes of a row read 64 contiguous bytes per load (16 lines per wave-instruction) and the two
+  // loads of a step one whole 128-B line; a quad at or past K reads the row's first quad (finite,
+  // valid) and is zeroed at use (K % 4 == 0: quads are whole)
+  // first step holding a quad past K (the zeroing branch is uniform)
+  const int s_tail = K / 32;
+  auto issue = [&](uint4 (&f)[W3_MF][2 * W3_KC], int rt) {
+#pragma unroll
+    for (int mf = 0; mf < W3_MF; ++mf) {
+      const float* p = A + (int64_t)min(rt * W3_BM + w * 16 * W3_MF + 16 * mf + ml, M - 1) * lda;
+#pragma unroll
+      for (int s = 0; s < W3_KC; ++s)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int k = 32 * s + 16 * j + 4 * kq;
+          f[mf][2 * s + j] = *(const uint4*)(p + (k < K ? k : 0));
+        }
+    }
+  };
+  // weight fragment (plane p, step s, column block jn) of this lane: unit ((p*KC + s)*4 + kq)*80 +
+  // 16 jn + ml
+  const uint4* wlane = wl + kq * W3_NC + ml;
+  auto compute_store = [&](const uint4 (&f)[W3_MF][2 * W3_KC], int rt) {
+    w3_f32x4 acc[W3_MF][5];
+#pragma unroll
+    for (int mf = 0; mf < W3_MF; ++mf)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) acc[mf][j] = w3_f32x4{0.f, 0.f, 0.f, 0.f};
+    // the raw activation fragment of step s (quads at or past K zeroed: uniform branch)
+    auto raw_step = [&](int s, float (&x)[8]) {
+      uint4 q0 = f[0][2 * s], q1 = f[0][2 * s + 1];
+      if (s >= s_tail) {
+        const int k = 32 * s + 4 * kq;
+        if (k >= K) q0 = make_uint4(0u, 0u, 0u, 0u);
+        if (k + 16 >= K) q1 = make_uint4(0u, 0u, 0u, 0u);
+      }
+      x[0] = __builtin_bit_cast(float, q0.x); x[1] = __builtin_bit_cast(float, q0.y);
+      x[2] = __builtin_bit_cast(float, q0.z); x[3] = __builtin_bit_cast(float, q0.w);
+      x[4] = __builtin_bit_cast(float, q1.x); x[5] = __builtin_bit_cast(float, q1.y);
+      x[6] = __builtin_bit_cast(float, q1.z); x[7] = __builtin_bit_cast(float, q1.w);
+    };
+    auto split_el = [&](const float (&x)[8], int e, W3Split& t) {
+      const __bf16 h = (__bf16)x[e];
+      const float r1 = x[e] - (float)h;
+      const __bf16 m = (__bf16)r1;
+      t.h[e] = h;
+      t.m[e] = m;
+      t.l[e] = (__bf16)(r1 - (float)m);
+    };
+    W3Split acur;
+    uint4 wc[3], wn[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) wc[p] = wlane[p * W3_PLANE];
+    {
+      float x[8];
+      raw_step(0, x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) split_el(x, e, acur);
+    }
+#pragma unroll
+    for (int s = 0; s < W3_KC; ++s) {
+      // one step's weight fragments live at a time (the scheduler would hoist them all); the
+      // next step's activation split rides between the column blocks' MFMAs, two elements per
+      // block (the MFMAs leave half the vector issue cycles free)
+      __builtin_amdgcn_sched_barrier(0);
+      float xn[8];
+      if (s + 1 < W3_KC) raw_step(s + 1, xn);
+      W3Split anx;
+      const uint4* wp = wlane + s * 4 * W3_NC;
+      // (the last block prefetches the next step's first: step 0's after the last step)
+      const uint4* wq = wlane + ((s + 1) % W3_KC) * 4 * W3_NC;
+#pragma unroll
+      for (int jn = 0; jn < 5; ++jn) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          wn[p] = jn + 1 < 5 ? wp[p * W3_PLANE + 16 * (jn + 1)] : wq[p * W3_PLANE];
+        __builtin_amdgcn_sched_barrier(0);
+        const w3_bf16x8 wh = __builtin_bit_cast(w3_bf16x8, wc[0]);
+        const w3_bf16x8 wm = __builtin_bit_cast(w3_bf16x8, wc[1]);
+        const w3_bf16x8 wlo = __builtin_bit_cast(w3_bf16x8, wc[2]);
+        // gemm.hip's x3 order: small products first (activation x weight)
+        w3_f32x4& c = acc[0][jn];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.l, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, acur.m, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, acur.h, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.m, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, acur.h, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.h, c, 0, 0, 0);
+        if (s + 1 < W3_KC && jn < 4) {
+          split_el(xn, 2 * jn, anx);
+          split_el(xn, 2 * jn + 1, anx);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) wc[p] = wn[p];
+      }
+      if (s + 1 < W3_KC) acur = anx;
+    }
+    // Dᵀ tile: lane holds row m = l % 16 of the wave's 16, columns 16 jn + 4 (l / 16) + 0..3
+#pragma unroll
+    for (int mf = 0; mf < W3_MF; ++mf) {
+      const int m = rt * W3_BM + w * 16 * W3_MF + 16 * mf + ml;
+      if (m >= M) continue;
+#pragma unroll
+      for (int jn = 0; jn < 5; ++jn) {
+        const int c = 16 * jn + 4 * kq;
+        const int n = n0 + c;
+        if (n < N) {  // N % 4 == 0: a group is wholly in or out
+          const float4 bv = *(const float4*)(bsh + c);
+          const w3_f32x4 a4 = acc[mf][jn];
+          const float4 o = make_float4(a4[0] + bv.x, a4[1] + bv.y, a4[2] + bv.z, a4[3] + bv.w);
+          *(float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63))) = o;
+          if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
+        }
+      }
+    }
+  };
+  uint4 fa[W3_MF][2 * W3_KC], fb[W3_MF][2 * W3_KC];
+  int rt = rs;
+  if (rt < tm) issue(fa, rt);
+  while (rt < tm) {
+    const int r1 = rt + nrs;
+    if (r1 < tm) issue(fb, r1);
+    compute_store(fa, rt);
+    if (r1 >= tm) break;
+    const int r2 = r1 + nrs;
+    if (r2 < tm) issue(fa, r2);
+    compute_store(fb, r1);
+    rt = r2;
+  }
+}
+
+// ---- host side ----
+
+static bool x3w_on() {  // A/B comparison only (GNNEA_X3W=0: k_gemm_x3p)
+  static const bool on = [] {
+    const char* e = getenv("GNNEA_X3W");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int64_t gemm_x3w_ws_bytes(int64_t N) {
+  return (N + W3_NC - 1) / W3_NC * W3_TILE_BYTES;
+}
+
+bool gemm_x3w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda, const void* A,
+                      float beta, int64_t ldc, int64_t cs, const void* C, const void* C2,
+                      int64_t cs2) {
+  return x3w_on() && !trans_a && beta == 0.f && A && C && M >= 65536 && M < (1ll << 31) &&
+         N >= 64 && N <= 4096 && N % 4 == 0 && K > 256 && K <= 32 * W3_KC && K % 4 == 0 &&
+         lda >= K && lda % 4 == 0 && (((uintptr_t)A) & 15) == 0 &&
+         ldc % 4 == 0 && cs % 4 == 0 && (((uintptr_t)C) & 15) == 0 &&
+         (!C2 || (cs2 % 4 == 0 && (((uintptr_t)C2) & 15) == 0));
+}
+
+int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                    const float* B, int64_t ldb, const float* bias, float* C, int64_t ldc,
+                    int64_t cs, float* C2, int64_t cs2, void* ws, int64_t ws_bytes,
+                    hipStream_t s) {
+  const int ntn = (int)((N + W3_NC - 1) / W3_NC);
+  if (!ws || ws_bytes < gemm_x3w_ws_bytes(N)) return GNNEA_EWORKSPACE;
+  bf16_t* P = (bf16_t*)ws;
+  {
+    const int64_t tot = (int64_t)ntn * W3_PLANE * 8;
+    const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
+    // B op-form [N][K]: trans_b = 1 means B is stored [N][K]
+    hipLaunchKernelGGL(k_pack_x3w, dim3(nb), dim3(256), 0, s, B, ldb, trans_b ? 1 : 0, (int)N,
+                       (int)K, ntn, P);
+    GNNEA_LAUNCH_CHECK();
+  }
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  // persistent grid: a multiple of 8 * ntn workgroups (column tiles of a row stream 8 apart)
+  const int unit = 8 * ntn;
+  const int64_t tm = (M + W3_BM - 1) / W3_BM;
+  int grid = ncu / unit * unit;
+  if (grid < unit) grid = unit;
+  if ((int64_t)grid / ntn > tm) grid = (int)((tm + 7) / 8 * 8 * ntn);
+  hipLaunchKernelGGL(k_gemm_x3w, dim3(grid), dim3(64 * W3_NW), 0, s, (int)M, (int)N, (int)K, ntn,
+                     A, lda, P, bias, C, ldc, cs, C2, cs2);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace gnnea
