@@ -1054,7 +1054,8 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
                    float* C2 = nullptr, int64_t cs2 = 0) {
   if (C2 && (cs2 % 4 != 0 || cs2 < M * 64 || cs != 64)) return GNNEA_EINVAL;
   // the weight-resident form (gemm_x3w.hip) for the tall K <= 320 projections; it writes C2 too
-  if (B && ldc >= N && (trans_b ? ldb >= K : ldb >= N) &&
+  if (B && (cs == 64 ? ldc >= N : (ldc >= 64 && cs >= M * ldc)) &&
+      (trans_b ? ldb >= K : ldb >= N) &&
       gemm_x3w_applies(trans_a, M, N, K, lda, A, beta, ldc, cs, C, C2, cs2) && ws &&
       ws_bytes >= gemm_x3w_ws_bytes(N))
     return gemm_x3w_launch(trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, cs, C2, cs2, ws,

@@ -78,7 +78,7 @@ def test_spmm_sliced_output_column_block(device):
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 300, 300), (777, 128, 64), (64, 68, 300),
-                                   (4097, 300, 17)])
+                                   (4097, 300, 17), (70001, 300, 300), (65600, 600, 296)])
 def test_gemm_sliced_vs_fp64(device, M, N, K):
     from gnnea import ops
     torch.manual_seed(M + N)
@@ -412,7 +412,8 @@ def test_gat_fwd_sliced_vs_rowmajor_and_oracle(device, monkeypatch, heads, d_hea
 
 
 @pytest.mark.parametrize("M,N,K,bias", [(5000, 300, 300, True), (4100, 128, 64, False),
-                                        (300, 300, 36, False)])
+                                        (300, 300, 36, False), (70001, 300, 300, True),
+                                        (66000, 128, 320, False)])
 def test_gemm_x3_dual_output(device, M, N, K, bias):
     """gnnea_gemm_x3_dual_f32: the row-major product and its slice-major copy from one GEMM
     (the copy is stored from the same registers: bit-identical to packing the product)."""
