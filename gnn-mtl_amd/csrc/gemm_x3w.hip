@@ -245,15 +245,153 @@ __global__ __launch_bounds__(64 * W3_NW, 1) void k_gemm_x3w(int M, int N, int K,
   }
 }
 
+// The same product with 8 waves (two per SIMD: each one's LDS-read latency and split under the
+// other's MFMAs) and a register ring instead of a whole-tile double buffer: a wave keeps ONE tile's
+// 20 activation quads, and the quads of step s are replaced by the next tile's step s as soon as
+// they have been read (a prefetch distance of one tile, 80 registers instead of 160).
+__global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int ntn,
+                                                       const float* __restrict__ A, int64_t lda,
+                                                       const bf16_t* __restrict__ P,
+                                                       const float* __restrict__ bias,
+                                                       float* __restrict__ C, int64_t ldc,
+                                                       int64_t cs, float* __restrict__ C2,
+                                                       int64_t cs2) {
+  constexpr int NW = 8, BM = 16 * NW;
+  __shared__ __attribute__((aligned(16))) uint4 wl[3 * W3_PLANE];
+  __shared__ __attribute__((aligned(16))) float bsh[W3_NC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x;
+  const int nt = (b / 8) % ntn;
+  const int rs = (b / (8 * ntn)) * 8 + b % 8, nrs = (int)gridDim.x / ntn;
+  const int n0 = nt * W3_NC;
+  {  // the resident weight tile
+    const uint4* src = (const uint4*)(P + (int64_t)nt * 3 * W3_PLANE * 8);
+    for (int i = tid; i < 3 * W3_PLANE; i += 64 * NW) wl[i] = src[i];
+    if (tid < W3_NC) bsh[tid] = bias && n0 + tid < N ? bias[n0 + tid] : 0.f;
+  }
+  __syncthreads();
+  const int tm = (M + BM - 1) / BM;
+  const int kq = lane >> 4, ml = lane & 15;
+  const uint4* wlane = wl + kq * W3_NC + ml;
+  uint4 f[2 * W3_KC];
+  auto row_ptr = [&](int rt) {
+    return A + (int64_t)min(rt * BM + w * 16 + ml, M - 1) * lda;
+  };
+  // K in (288, 320]: steps 0..8 are inside every row (immediate offsets from the lane's base);
+  // only the last step's quads can reach K (clamped to the row's first quad, zeroed at use)
+  auto load_step = [&](const float* p, int s) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (s < W3_KC - 1) {
+        f[2 * s + j] = *(const uint4*)(p + 4 * kq + 32 * s + 16 * j);
+      } else {
+        const int k = 32 * s + 16 * j + 4 * kq;
+        f[2 * s + j] = *(const uint4*)(p + (k < K ? k : 0));
+      }
+    }
+  };
+  auto raw_step = [&](int s, float (&x)[8]) {
+    uint4 q0 = f[2 * s], q1 = f[2 * s + 1];
+    if (s == W3_KC - 1) {
+      const int k = 32 * s + 4 * kq;
+      if (k >= K) q0 = make_uint4(0u, 0u, 0u, 0u);
+      if (k + 16 >= K) q1 = make_uint4(0u, 0u, 0u, 0u);
+    }
+    x[0] = __builtin_bit_cast(float, q0.x); x[1] = __builtin_bit_cast(float, q0.y);
+    x[2] = __builtin_bit_cast(float, q0.z); x[3] = __builtin_bit_cast(float, q0.w);
+    x[4] = __builtin_bit_cast(float, q1.x); x[5] = __builtin_bit_cast(float, q1.y);
+    x[6] = __builtin_bit_cast(float, q1.z); x[7] = __builtin_bit_cast(float, q1.w);
+  };
+  auto split_el = [&](const float (&x)[8], int e, W3Split& t) {
+    const __bf16 h = (__bf16)x[e];
+    const float r1 = x[e] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    t.h[e] = h;
+    t.m[e] = m;
+    t.l[e] = (__bf16)(r1 - (float)m);
+  };
+  if (rs < tm) {
+    const float* p = row_ptr(rs);
+#pragma unroll
+    for (int s = 0; s < W3_KC; ++s) load_step(p, s);
+  }
+  for (int rt = rs; rt < tm; rt += nrs) {
+    // the next tile's rows (past the end: a valid row, loaded and never used)
+    const float* pn = row_ptr(rt + nrs < tm ? rt + nrs : rt);
+    w3_f32x4 acc[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[j] = w3_f32x4{0.f, 0.f, 0.f, 0.f};
+    W3Split acur;
+    {
+      float x[8];
+      raw_step(0, x);
+      load_step(pn, 0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) split_el(x, e, acur);
+    }
+#pragma unroll
+    for (int s = 0; s < W3_KC; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      // the next step's quads are split straight from the ring, then replaced by the next
+      // tile's (after the block loop); the weight fragments are read per block (the partner
+      // wave on the SIMD covers their latency)
+      float xn[8];
+      if (s + 1 < W3_KC) raw_step(s + 1, xn);
+      W3Split anx;
+      const uint4* wp = wlane + s * 4 * W3_NC;
+#pragma unroll
+      for (int jn = 0; jn < 5; ++jn) {
+        __builtin_amdgcn_sched_barrier(0);
+        const w3_bf16x8 wh = __builtin_bit_cast(w3_bf16x8, wp[16 * jn]);
+        const w3_bf16x8 wm = __builtin_bit_cast(w3_bf16x8, wp[W3_PLANE + 16 * jn]);
+        const w3_bf16x8 wlo = __builtin_bit_cast(w3_bf16x8, wp[2 * W3_PLANE + 16 * jn]);
+        w3_f32x4& c = acc[jn];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.l, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, acur.m, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, acur.h, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.m, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, acur.h, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.h, c, 0, 0, 0);
+        if (s + 1 < W3_KC && jn < 4) {
+          split_el(xn, 2 * jn, anx);
+          split_el(xn, 2 * jn + 1, anx);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (s + 1 < W3_KC) {
+        acur = anx;
+        load_step(pn, s + 1);
+      }
+    }
+    const int m = rt * BM + w * 16 + ml;
+    if (m < M) {
+#pragma unroll
+      for (int jn = 0; jn < 5; ++jn) {
+        const int c = 16 * jn + 4 * kq;
+        const int n = n0 + c;
+        if (n < N) {  // N % 4 == 0: a group is wholly in or out
+          const float4 bv = *(const float4*)(bsh + c);
+          const w3_f32x4 a4 = acc[jn];
+          const float4 o = make_float4(a4[0] + bv.x, a4[1] + bv.y, a4[2] + bv.z, a4[3] + bv.w);
+          *(float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63))) = o;
+          if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
+        }
+      }
+    }
+  }
+}
+
 // ---- host side ----
 
-static bool x3w_on() {  // A/B comparison only (GNNEA_X3W=0: k_gemm_x3p)
-  static const bool on = [] {
+// A/B comparison only: GNNEA_X3W=0 k_gemm_x3p, 1 k_gemm_x3w, 2 (default) k_gemm_x3w_ring
+static int x3w_mode() {
+  static const int mode = [] {
     const char* e = getenv("GNNEA_X3W");
-    return !(e && e[0] == '0');
+    return e ? atoi(e) : 2;
   }();
-  return on;
+  return mode;
 }
+static bool x3w_on() { return x3w_mode() != 0; }
 
 int64_t gemm_x3w_ws_bytes(int64_t N) {
   return (N + W3_NC - 1) / W3_NC * W3_TILE_BYTES;
@@ -263,7 +401,7 @@ bool gemm_x3w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda,
                       float beta, int64_t ldc, int64_t cs, const void* C, const void* C2,
                       int64_t cs2) {
   return x3w_on() && !trans_a && beta == 0.f && A && C && M >= 65536 && M < (1ll << 31) &&
-         N >= 64 && N <= 4096 && N % 4 == 0 && K > 256 && K <= 32 * W3_KC && K % 4 == 0 &&
+         N >= 64 && N <= 4096 && N % 4 == 0 && K > 32 * (W3_KC - 1) && K <= 32 * W3_KC && K % 4 == 0 &&
          lda >= K && lda % 4 == 0 && (((uintptr_t)A) & 15) == 0 &&
          ldc % 4 == 0 && cs % 4 == 0 && (((uintptr_t)C) & 15) == 0 &&
          (!C2 || (cs2 % 4 == 0 && (((uintptr_t)C2) & 15) == 0));
@@ -292,13 +430,18 @@ int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A
     return n;
   }();
   // persistent grid: a multiple of 8 * ntn workgroups (column tiles of a row stream 8 apart)
+  const bool ring = x3w_mode() == 2;
   const int unit = 8 * ntn;
-  const int64_t tm = (M + W3_BM - 1) / W3_BM;
+  const int64_t tm = (M + (ring ? 128 : W3_BM) - 1) / (ring ? 128 : W3_BM);
   int grid = ncu / unit * unit;
   if (grid < unit) grid = unit;
   if ((int64_t)grid / ntn > tm) grid = (int)((tm + 7) / 8 * 8 * ntn);
-  hipLaunchKernelGGL(k_gemm_x3w, dim3(grid), dim3(64 * W3_NW), 0, s, (int)M, (int)N, (int)K, ntn,
-                     A, lda, P, bias, C, ldc, cs, C2, cs2);
+  if (ring)
+    hipLaunchKernelGGL(k_gemm_x3w_ring, dim3(grid), dim3(512), 0, s, (int)M, (int)N, (int)K, ntn,
+                       A, lda, P, bias, C, ldc, cs, C2, cs2);
+  else
+    hipLaunchKernelGGL(k_gemm_x3w, dim3(grid), dim3(64 * W3_NW), 0, s, (int)M, (int)N, (int)K,
+                       ntn, A, lda, P, bias, C, ldc, cs, C2, cs2);
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
