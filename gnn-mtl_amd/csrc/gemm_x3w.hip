@@ -368,7 +368,10 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
 #pragma unroll
       for (int jn = 0; jn < 5; ++jn) {
         const int c = 16 * jn + 4 * kq;
-        const int n = n0 + c;
+        int n = n0 + c;
+        // (opaque to loop-invariant code motion: hoisted out of the tile loop, the 64-bit column
+        // offsets are spilled, and a scratch reload waits vmcnt(0), draining the ring's loads)
+        asm volatile("" : "+v"(n));
         if (n < N) {  // N % 4 == 0: a group is wholly in or out
           const float4 bv = *(const float4*)(bsh + c);
           const w3_f32x4 a4 = acc[jn];
