@@ -14,8 +14,13 @@ only do after an all-gather of its input) are reported as a labelled side number
 Side measurement (`train_step`): the row-sharded HGCN-EA training step of configs[3] through
 the drop-in Encoder/Decoder modules with the RCCL halo exchange (tools/dist_step.py).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W]   (N > 1: starts its own N ranks)
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, this process is only the launcher
+(tools/launch.py): before anything imports torch it starts N children of this script with the
+rank environment set (one per GPU, rendezvous on 127.0.0.1), relays their output and exits with
+the first failing child's status.  Under torch.distributed.run each process is already a rank.
 
 Prints ONE JSON line on rank 0.  `roofline` prices the SpMM kernel with the gather model
 4(N+1) + 8E + 4ED + 4ND bytes per launch over its HIP-event duration on the
@@ -33,11 +38,30 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def self_launch(argv, script=None):
+    """Launcher path: N > 1 ranks asked for and none set up (tools/launch.py).  Returns the exit
+    status to leave with, or None when this process is a rank itself.  Runs before torch is
+    imported, so the launcher process never initialises HIP."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    from tools import launch
+    if not launch.needs_launch(argv):
+        return None
+    return launch.spawn(launch.requested_ranks(argv), script or os.path.abspath(__file__), argv)
+
+
+if __name__ == "__main__":
+    _rc = self_launch(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
 sys.path.insert(0, os.path.join(ROOT, "gnn-mtl_amd"))
 
 from gnnea import _lib, ops, synth  # noqa: E402
@@ -401,7 +425,9 @@ def main():
               and ops.use_sliced(shard.n_cols, Dl, torch.float32))
     hs = ops.slice_pack(h_local) if sliced else None
 
-    n_slices = len(shard.slices(Dl)) if shard.g > 1 and part.kind == "rows" else 0
+    from gnnea import exchange as _ex
+    n_slices = (len(shard.slices(Dl)) if _ex.STAGED else 1) \
+        if shard.g > 1 and part.kind == "rows" else 0
 
     def step(ev=None):
         shard.aggregate(h_local, y, _lib.GNNEA_ACT_RELU, ev, hs=hs)
@@ -645,7 +671,26 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    # deterministic teardown: the package's cached buffers and torch's cached device / pinned
+    # blocks go back to the runtime now, not from the C-level exit handlers
+    del shard, h_local, y
+    if os.environ.get("GNNEA_EXIT_CLEANUP", "1") != "0":
+        import gnnea
+        gnnea.release()
+
+
+def _dump_maps_at_exit(path):
+    """Diagnostics (GNNEA_EXIT_MAPS=file): copy /proc/self/maps when the interpreter finalises, so
+    the PCs of a crash in a C-level exit handler can be symbolised (tools/symbolize_crash.py)."""
+    import atexit
+
+    def dump():
+        with open("/proc/self/maps") as src, open(path, "w") as dst:
+            dst.write(src.read())
+    atexit.register(dump)
 
 
 if __name__ == "__main__":
+    if os.environ.get("GNNEA_EXIT_MAPS"):
+        _dump_maps_at_exit(os.environ["GNNEA_EXIT_MAPS"])
     main()

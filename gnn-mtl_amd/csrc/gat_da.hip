@@ -227,7 +227,8 @@ static int da_t(const T* H, int64_t ldh, int64_t n_rows, int heads, int d_head, 
   const int Dp = (D + 3) & ~3;
   if (!ws || ws_bytes < (int64_t)nb * K * Dp * 4) return GNNEA_EWORKSPACE;
   // rows whose last granule stays inside the table (the final row may end inside a granule)
-  const int64_t n_fast = (int64_t)G * E <= ldh ? n_rows : n_rows - 1;
+  // (a column block of a wider buffer may end at the buffer end: only D bounds the row)
+  const int64_t n_fast = (int64_t)G * E <= D ? n_rows : n_rows - 1;
   const int64_t rpb = (n_rows + nb - 1) / nb;
   float* part = (float*)ws;
 #define GNNEA_DA_L(NGV, KV, HV)                                                                \

@@ -123,12 +123,13 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, int n_rows, int nbs,
     int H, int D, int dh, const typename GatLanes<TX>::R* __restrict__ Hs, int64_t sstrideR,
     const float* __restrict__ wgt, const float* __restrict__ den_in, TY* __restrict__ Y,
-    int64_t ldy) {
+    int64_t ldy, int s0) {
   constexpr int E = GatLanes<TX>::E, LPG = GatLanes<TX>::LPG, NG = GatLanes<TX>::NG;
   typedef typename GatLanes<TX>::R RX;
   const int b = blockIdx.x;
-  const int s = b / nbs;
-  const int row = xcd_remap(b - s * nbs, nbs) * 4 + wave_id();
+  const int sb = b / nbs;
+  const int s = s0 + sb;  // slices [s0, s0 + gridDim.x / nbs) of this launch
+  const int row = xcd_remap(b - sb * nbs, nbs) * 4 + wave_id();
   if (row >= n_rows) return;
   const int lane = lane_id(), g = lane / LPG, c = lane % LPG;
   const int c0 = s * 64 + E * c;
@@ -317,13 +318,15 @@ template <int U, typename T>
 __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
     const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT, int n_rows, int nbs,
     int H, int D, int dh, const typename GatLanes<T>::R* __restrict__ Gs, int64_t sstrideR,
-    const T* __restrict__ Hm, int64_t ldh, const float* __restrict__ wT,
-    T* __restrict__ dH, int64_t lddh, float* __restrict__ pd, int64_t pstride) {
+    const T* __restrict__ Hm, int64_t ldh, int64_t hss, const float* __restrict__ wT,
+    T* __restrict__ dH, int64_t lddh, int64_t dhss, float* __restrict__ pd, int64_t pstride,
+    int s0) {
   constexpr int E = GatLanes<T>::E, LPG = GatLanes<T>::LPG, NG = GatLanes<T>::NG;
   typedef typename GatLanes<T>::R RX;
   const int b = blockIdx.x;
-  const int s = b / nbs;
-  const int row = xcd_remap(b - s * nbs, nbs) * 4 + wave_id();
+  const int sb = b / nbs;
+  const int s = s0 + sb;  // slices [s0, s0 + gridDim.x / nbs) of this launch
+  const int row = xcd_remap(b - sb * nbs, nbs) * 4 + wave_id();
   if (row >= n_rows) return;
   const int lane = lane_id(), g = lane / LPG, c = lane % LPG;
   const int c0 = s * 64 + E * c;
@@ -335,7 +338,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
   float hj0[E], hj1[E];  // H_j split by head; zero past D (the table's padding is never read)
   {
     float v[E];
-    load_cols<T, E>(Hm + (int64_t)row * ldh, c0, D, v);
+    // H_j's columns of slice s: Hm + s * hss + row * ldh + (c - 64 s) (row-major: hss = 64;
+    // a slice-major table: ldh = 64, hss = its slice stride)
+    load_cols<T, E>(Hm + (int64_t)s * (hss - 64) + (int64_t)row * ldh, c0, D, v);
 #pragma unroll
     for (int t = 0; t < E; ++t) {
       second[t] = (c0 + t) / dh != h0;
@@ -414,7 +419,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
     for (int t = 0; t < E; ++t) acc[t] += __shfl_xor(acc[t], o, 64);
   }
   if (g != 0 || !own) return;
-  store_cols<T, E>(dH + (int64_t)row * lddh, c0, D, acc);
+  store_cols<T, E>(dH + (int64_t)s * (dhss - 64) + (int64_t)row * lddh, c0, D, acc);
 }
 
 template <int H, int LPR, typename T>  // LPR lanes per source row
@@ -552,18 +557,22 @@ template <typename T>
 int gat_fwd_sliced(const int32_t* rowptr, const int32_t* col, int32_t n_rows, const T* Hs,
                    int64_t sstride, int heads, int d_head, const float* s1, const float* s2,
                    float alpha, const float* edge_mask, int act, T* Y, int64_t ldy, float* m_out,
-                   float* den_out, float* wgt, hipStream_t st) {
+                   float* den_out, float* wgt, hipStream_t st, int s_begin = 0, int s_end = -1,
+                   bool stats = true) {
   const int D = heads * d_head;
   if (n_rows < 0 || heads < 1 || heads > 8 || !gat_two_heads_per_slice(heads, d_head) ||
       D % 4 || sstride % 64 || ldy % 4 || ldy < D)
     return GNNEA_EINVAL;
   if (act != GNNEA_ACT_IDENTITY && act != GNNEA_ACT_RELU) return GNNEA_EINVAL;
+  const int S = div_up(D, 64);
+  if (s_end < 0) s_end = S;
+  if (s_begin < 0 || s_begin > s_end || s_end > S) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
-  if (!rowptr || !col || !Hs || !s1 || !s2 || !Y || !m_out || !den_out || !wgt)
-    return GNNEA_EINVAL;
+  if (!rowptr || !col || !s1 || !s2 || !m_out || !den_out || !wgt) return GNNEA_EINVAL;
+  if (s_end > s_begin && (!Hs || !Y)) return GNNEA_EINVAL;
   if (!alv<T>(Hs) || !alv<T>(Y)) return GNNEA_EALIGN;
   const int nbs = div_up(n_rows, 4);
-  switch (heads) {
+  if (stats) switch (heads) {
 #define GNNEA_RS(HH)                                                                             \
   case HH:                                                                                       \
     hipLaunchKernelGGL(k_gat_rowstats<HH>, dim3(nbs), dim3(256), 0, st, rowptr, col, n_rows, s1, \
@@ -574,17 +583,17 @@ int gat_fwd_sliced(const int32_t* rowptr, const int32_t* col, int32_t n_rows, co
 #undef GNNEA_RS
   }
   GNNEA_LAUNCH_CHECK();
-  const int S = div_up(D, 64);
-  const dim3 grid((unsigned)((int64_t)S * nbs));
+  if (s_end == s_begin) return 0;
+  const dim3 grid((unsigned)((int64_t)(s_end - s_begin) * nbs));
   typedef typename GatLanes<T>::R R;
   if (act == GNNEA_ACT_RELU)
     hipLaunchKernelGGL((k_gat_fwd_sliced<GNNEA_ACT_RELU, kGatU<T>, T, T>), grid, dim3(256), 0, st,
                        rowptr, col, n_rows, nbs, heads, D, d_head, (const R*)Hs, sstride / 4,
-                       wgt, den_out, Y, ldy);
+                       wgt, den_out, Y, ldy, s_begin);
   else
     hipLaunchKernelGGL((k_gat_fwd_sliced<GNNEA_ACT_IDENTITY, kGatU<T>, T, T>), grid, dim3(256), 0,
                        st, rowptr, col, n_rows, nbs, heads, D, d_head, (const R*)Hs, sstride / 4,
-                       wgt, den_out, Y, ldy);
+                       wgt, den_out, Y, ldy, s_begin);
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
@@ -715,21 +724,32 @@ int gat_bwd_prep_sliced(int32_t n_rows, int heads, int d_head, const T* dY, cons
   return 0;
 }
 
+// a table operand of the source pass: row-major (ss = 64: row stride ld >= D) or slice-major
+// (ld = 64, ss = the slice stride, at least n rows of 64)
+static bool gat_tab_ok(int64_t ld, int64_t ss, int D, int64_t n) {
+  if (ss == 64) return ld % 4 == 0 && ld >= D;
+  return ld == 64 && ss % 64 == 0 && ss >= n * 64;
+}
+
 template <typename T>
 int gat_bwd_src_sliced(const int32_t* rowptrT, const int32_t* colT, const int64_t* permT,
                        int32_t n_rows, int heads, int d_head, const T* Hm, int64_t ldh,
                        const float* s2, float alpha, const float* emask, const float* rec,
                        const T* Gs, int64_t sstride, float* wT, float* pd, int64_t nnzT, T* dH,
-                       int64_t lddh, hipStream_t st) {
+                       int64_t lddh, hipStream_t st, int64_t hss = 64, int64_t dhss = 64,
+                       int s_begin = 0, int s_end = -1, bool weights = true) {
   const int D = heads * d_head;
-  if (n_rows < 0 || !gat_sl_shape(heads, d_head, sstride) || ldh % 4 || ldh < D ||
-      lddh % 4 || lddh < D || nnzT < 0)
+  if (n_rows < 0 || !gat_sl_shape(heads, d_head, sstride) || !gat_tab_ok(ldh, hss, D, n_rows) ||
+      !gat_tab_ok(lddh, dhss, D, n_rows) || nnzT < 0)
     return GNNEA_EINVAL;
+  const int S = div_up(D, 64);
+  if (s_end < 0) s_end = S;
+  if (s_begin < 0 || s_begin > s_end || s_end > S) return GNNEA_EINVAL;
   if (n_rows == 0) return 0;
-  if (!rowptrT || !colT || !Hm || !s2 || !rec || !Gs || !wT || !pd || !dH ||
-      (emask && !permT))
-    return GNNEA_EINVAL;
+  if (!rowptrT || !colT || !s2 || !rec || !wT || !pd || (emask && !permT)) return GNNEA_EINVAL;
+  if (s_end > s_begin && (!Hm || !Gs || !dH)) return GNNEA_EINVAL;
   if (!alv<T>(Hm) || !alv<T>(Gs) || !alv<T>(dH)) return GNNEA_EALIGN;
+  if (weights) {
 #define GNNEA_W1(HH, LP)                                                                        \
   hipLaunchKernelGGL((k_gat_bwd_w<HH, LP>), dim3(div_up(n_rows, 256 / LP)), dim3(256), 0, st,   \
                      rowptrT, colT, permT, n_rows, s2, alpha, emask, (const float4*)rec, wT)
@@ -744,11 +764,13 @@ int gat_bwd_src_sliced(const int32_t* rowptrT, const int32_t* colT, const int64_
 #undef GNNEA_W
 #undef GNNEA_W1
   GNNEA_LAUNCH_CHECK();
-  const int S = div_up(D, 64), nbs = div_up(n_rows, 4);
-  hipLaunchKernelGGL((k_gat_bwd_src_sl<kGatU<T>, T>), dim3((unsigned)((int64_t)S * nbs)),
-                     dim3(256), 0, st, rowptrT, colT, n_rows, nbs, heads, D, d_head,
-                     (const typename GatLanes<T>::R*)Gs, sstride / 4, Hm, ldh, wT, dH, lddh,
-                     pd, 2 * nnzT);
+  }
+  if (s_end == s_begin) return 0;
+  const int nbs = div_up(n_rows, 4);
+  hipLaunchKernelGGL((k_gat_bwd_src_sl<kGatU<T>, T>),
+                     dim3((unsigned)((int64_t)(s_end - s_begin) * nbs)), dim3(256), 0, st, rowptrT,
+                     colT, n_rows, nbs, heads, D, d_head, (const typename GatLanes<T>::R*)Gs,
+                     sstride / 4, Hm, ldh, hss, wT, dH, lddh, dhss, pd, 2 * nnzT, s_begin);
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
@@ -907,4 +929,57 @@ extern "C" int gnnea_gat_bwd_dst_sliced_bf16(const int32_t* rowptr, const int64_
                                              void* dH, int64_t lddh, float* ds1, void* stream) {
   return gat_bwd_dst_sliced<bf16_t>(rowptr, tpos, n_rows, heads, d_head, dzT, a, ds2,
                                     (bf16_t*)dH, lddh, ds1, (hipStream_t)stream);
+}
+
+// ---- slice ranges (the staged halo of a row-sharded GAT layer, gnnea/dist_graph.py) ---------- //
+// the forward over slices [s_begin, s_end) of Hs only; stats != 0 runs the row statistics /
+// edge weights first (m_out, den_out, wgt) — with s_begin == s_end that is all it does
+extern "C" int gnnea_gat_fwd_sliced_range_f32(const int32_t* rowptr, const int32_t* col,
+                                              int32_t n_rows, const float* Hs, int64_t sstride,
+                                              int heads, int d_head, const float* s1,
+                                              const float* s2, float alpha,
+                                              const float* edge_mask, int act, float* Y,
+                                              int64_t ldy, float* m_out, float* den_out,
+                                              float* wgt, int s_begin, int s_end, int stats,
+                                              void* stream) {
+  return gat_fwd_sliced<float>(rowptr, col, n_rows, Hs, sstride, heads, d_head, s1, s2, alpha,
+                               edge_mask, act, Y, ldy, m_out, den_out, wgt, (hipStream_t)stream,
+                               s_begin, s_end, stats != 0);
+}
+extern "C" int gnnea_gat_fwd_sliced_range_bf16(const int32_t* rowptr, const int32_t* col,
+                                               int32_t n_rows, const void* Hs, int64_t sstride,
+                                               int heads, int d_head, const float* s1,
+                                               const float* s2, float alpha,
+                                               const float* edge_mask, int act, void* Y,
+                                               int64_t ldy, float* m_out, float* den_out,
+                                               float* wgt, int s_begin, int s_end, int stats,
+                                               void* stream) {
+  return gat_fwd_sliced<bf16_t>(rowptr, col, n_rows, (const bf16_t*)Hs, sstride, heads, d_head,
+                                s1, s2, alpha, edge_mask, act, (bf16_t*)Y, ldy, m_out, den_out,
+                                wgt, (hipStream_t)stream, s_begin, s_end, stats != 0);
+}
+
+// the source pass over slices [s_begin, s_end) (weights != 0: the per-edge weights wT first);
+// H and dH each row-major (hss / dhss = 64, ldh / lddh >= D) or slice-major 64-column tables
+// (ldh / lddh = 64, hss / dhss = their slice strides) — the halo's slice tables of a row shard
+extern "C" int gnnea_gat_bwd_src_sliced_range_f32(
+    const int32_t* rowptrT, const int32_t* colT, const int64_t* permT, int32_t n_rows, int heads,
+    int d_head, const float* Hm, int64_t ldh, int64_t hss, const float* s2, float alpha,
+    const float* emask, const float* rec, const float* Gs, int64_t sstride, float* wT, float* pd,
+    int64_t nnzT, float* dH, int64_t lddh, int64_t dhss, int s_begin, int s_end, int weights,
+    void* stream) {
+  return gat_bwd_src_sliced<float>(rowptrT, colT, permT, n_rows, heads, d_head, Hm, ldh, s2,
+                                   alpha, emask, rec, Gs, sstride, wT, pd, nnzT, dH, lddh,
+                                   (hipStream_t)stream, hss, dhss, s_begin, s_end, weights != 0);
+}
+extern "C" int gnnea_gat_bwd_src_sliced_range_bf16(
+    const int32_t* rowptrT, const int32_t* colT, const int64_t* permT, int32_t n_rows, int heads,
+    int d_head, const void* Hm, int64_t ldh, int64_t hss, const float* s2, float alpha,
+    const float* emask, const float* rec, const void* Gs, int64_t sstride, float* wT, float* pd,
+    int64_t nnzT, void* dH, int64_t lddh, int64_t dhss, int s_begin, int s_end, int weights,
+    void* stream) {
+  return gat_bwd_src_sliced<bf16_t>(rowptrT, colT, permT, n_rows, heads, d_head,
+                                    (const bf16_t*)Hm, ldh, s2, alpha, emask, rec,
+                                    (const bf16_t*)Gs, sstride, wT, pd, nnzT, (bf16_t*)dH, lddh,
+                                    (hipStream_t)stream, hss, dhss, s_begin, s_end, weights != 0);
 }

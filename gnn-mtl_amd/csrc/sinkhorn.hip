@@ -989,6 +989,7 @@ static int res_num_cus() {
 
 static bool res_applies(const gnnea_sinkhorn* p) {
   if (p->mode != GNNEA_SK_KNOPP || p->variant != 0 || p->J > kMaxJ) return false;
+  if (p->flags & GNNEA_SK_NO_ONCHIP) return false;
   const char* e = getenv("GNNEA_SK_RESIDENT");
   if (e && e[0] == '0') return false;
   const ResGeom g = res_geom(p->I, p->J);

@@ -31,6 +31,7 @@ GNNEA_SK_RELAX = 3
 GNNEA_SK_STATUS_BYTES = 256
 GNNEA_SK_PATH_SWEEP, GNNEA_SK_PATH_ONCHIP, GNNEA_SK_PATH_LOG = 0, 1, 2
 GNNEA_SK_ST_TIMEOUT = 16  # status word: an inter-workgroup wait of k_sk_res timed out
+GNNEA_SK_NO_ONCHIP = 1  # gnnea_sinkhorn.flags: never the on-chip cooperative path
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -57,7 +58,7 @@ class SinkhornProblem(ctypes.Structure):
         ("max_iter", ctypes.c_int),
         ("iters_run", ctypes.c_int),
         ("variant", ctypes.c_int),
-        ("reserved", ctypes.c_int),
+        ("flags", ctypes.c_int),
         ("ws", _p),
     ]
 
@@ -179,6 +180,25 @@ SIGNATURES = {
                                                       _p, _p, _i64, _p, _p, _p]),
     "gnnea_gat_bwd_dst_sliced_bf16": (ctypes.c_int, [_p, _p, _i32, ctypes.c_int, ctypes.c_int,
                                                      _p, _p, _p, _p, _i64, _p, _p]),
+    "gnnea_gat_fwd_sliced_range_f32": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int,
+                                                      ctypes.c_int, _p, _p, _f32, _p, ctypes.c_int,
+                                                      _p, _i64, _p, _p, _p, ctypes.c_int,
+                                                      ctypes.c_int, ctypes.c_int, _p]),
+    "gnnea_gat_fwd_sliced_range_bf16": (ctypes.c_int, [_p, _p, _i32, _p, _i64, ctypes.c_int,
+                                                       ctypes.c_int, _p, _p, _f32, _p,
+                                                       ctypes.c_int, _p, _i64, _p, _p, _p,
+                                                       ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                       _p]),
+    "gnnea_gat_bwd_src_sliced_range_f32": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int,
+                                                          ctypes.c_int, _p, _i64, _i64, _p, _f32,
+                                                          _p, _p, _p, _i64, _p, _p, _i64, _p,
+                                                          _i64, _i64, ctypes.c_int, ctypes.c_int,
+                                                          ctypes.c_int, _p]),
+    "gnnea_gat_bwd_src_sliced_range_bf16": (ctypes.c_int, [_p, _p, _p, _i32, ctypes.c_int,
+                                                           ctypes.c_int, _p, _i64, _i64, _p, _f32,
+                                                           _p, _p, _p, _i64, _p, _p, _i64, _p,
+                                                           _i64, _i64, ctypes.c_int,
+                                                           ctypes.c_int, ctypes.c_int, _p]),
     "gnnea_slice_pack64_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, _p]),
     "gnnea_slice_pack64_bf16": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, _p]),
     "gnnea_gemm_f64": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,

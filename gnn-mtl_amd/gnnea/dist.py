@@ -160,7 +160,7 @@ class KGShard:
                                       torch.from_numpy(vv).to(device), self.part.n_rows, ncols)
         self.csr = up(r, c, v, self.part.n_cols)
         self.group = make_groups(self.part) if kind == "rows" else None
-        self._tables = None
+        self._tables = self._full = None
 
     @property
     def g(self):
@@ -193,7 +193,8 @@ class KGShard:
         """out = act(A_shard · H) for this rank's rows.  Row shards of a KG group: the own rows
         packed into the KG's slice tables, every slice's halo exchange issued at once, slice q
         aggregated as soon as it has landed (``events``: [start, end] + a pair per slice around
-        its aggregation).  ``hs``: H held slice-major (gnnea.ops.spmm_sliced) for the
+        its aggregation); with GNNEA_HALO_STAGED=0 the whole halo first, then one aggregation
+        (one event pair around it).  ``hs``: H held slice-major (gnnea.ops.spmm_sliced) for the
         exchange-free partitions."""
         from . import exchange, ops
         rec = (lambda k: events[k].record()) if events is not None else (lambda k: None)
@@ -206,6 +207,22 @@ class KGShard:
             rec(1)
             return out
         D = h_local.shape[1]
+        if not exchange.STAGED:  # the whole halo row-major, then one aggregation
+            rec(0)
+            full = self._full
+            if full is None or full.shape != (self.n_cols, D) or full.dtype != h_local.dtype:
+                full = self._full = torch.empty((self.n_cols, D), dtype=h_local.dtype,
+                                                device=self.device)
+            exchange.all_gather(h_local, full, self.group, self.part.group_ranks(self.part.kg),
+                                self.part.li, copy_own=True, other=self.part.other_ranks())
+            rec(2)
+            if ops.use_sliced(self.n_cols, D, h_local.dtype):
+                ops.spmm_sliced(self.csr, ops.slice_pack(full), D, act, out=out)
+            else:
+                ops.spmm(self.csr, full, act, out=out)
+            rec(3)
+            rec(1)
+            return out
         tables = self.halo_tables(D, h_local.dtype)
         rec(0)
         with torch.cuda.device(self.device):

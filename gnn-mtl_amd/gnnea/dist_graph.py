@@ -226,7 +226,9 @@ class DistAdj:
         """The halo of ``t`` moves slice by slice, overlapped with the per-slice aggregation:
         every row shard (g > 1) whose engine has the slice operations; fp32 / bf16 with whole
         4-column chunks (the HighWay epilogue: fp32)."""
-        if self.part.g == 1 or not hasattr(self.engine, "slice_w") or t.shape[1] % 4:
+        from . import exchange
+        if (self.part.g == 1 or not exchange.STAGED or not hasattr(self.engine, "slice_w")
+                or t.shape[1] % 4):
             return False
         if isinstance(self.engine, HipEngine):
             return t.dtype == torch.float32 or (t.dtype == torch.bfloat16 and not highway)

@@ -36,6 +36,10 @@ import torch
 import torch.distributed as dist
 
 MODE = os.environ.get("GNNEA_HALO", "relay")
+# the per-column-slice pipeline (all_gather_slices / reduce_scatter_start, several exchanges in
+# flight, overlapped with the per-slice aggregation); GNNEA_HALO_STAGED=0 keeps the unstaged
+# path: the whole halo row-major, then one aggregation (and one blocking reduce-scatter back)
+STAGED = os.environ.get("GNNEA_HALO_STAGED", "1") != "0"
 
 
 def _gloo(group):
@@ -266,6 +270,10 @@ def reduce_scatter_start(partial, group, ranks, li, other=None, out=None):
         recv = {p: torch.empty_like(send[li]) for p in ranks if p != ranks[li]}
         works = _relay_rs(send, recv, ranks, li, other, sync=_gloo(group))
         return PendingSum(blocks[li], [recv[p] for p in ranks if p != ranks[li]], works, out)
+    if not _gloo(group) and MODE == "ring":  # RCCL's reduce-scatter, as reduce_scatter does
+        red = torch.empty_like(blocks[li])
+        w = dist.reduce_scatter_tensor(red, partial, group=group, async_op=True)
+        return PendingSum(red, [], [w], out)
     recv = [torch.empty_like(send[li]) for p in range(g) if p != li]
     ops = []
     k = 0

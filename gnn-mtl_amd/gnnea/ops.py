@@ -924,16 +924,23 @@ def gat_two_heads_per_slice(heads, d_head):
                for s in range((D + 63) // 64))
 
 
-def _gat_sliced_applies(H, heads, d_head, Y):
+def gat_sliced_wanted(n_rows, heads, d_head, dtype):
     """The GAT passes run over 64-column slice-major tables (fp32: 256 B, bf16: 128 B per row
-    piece; one KG slice of cfg-4 fp32 / cfg-5 bf16 is 256 MB) when the row-major table exceeds
-    the Infinity Cache and spans at least two slices."""
+    piece; one KG slice of cfg-4 fp32 / cfg-5 bf16 is 256 MB) when the row-major table of
+    ``n_rows`` projected rows exceeds the Infinity Cache and spans at least two slices.  The
+    projection GEMM asks this before writing its sliced copy (att_layers.GraphAttentionLayer),
+    so no copy is made that the forward would not consume."""
     D = heads * d_head
-    return (GAT_SLICED and (H.dtype == torch.float32 or
-                            (H.dtype == torch.bfloat16 and GAT_SLICED_BF16))
+    es = torch.tensor([], dtype=dtype).element_size()
+    return (GAT_SLICED and (dtype == torch.float32 or
+                            (dtype == torch.bfloat16 and GAT_SLICED_BF16))
             and gat_two_heads_per_slice(heads, d_head)
-            and D % 4 == 0 and heads <= 8 and 128 <= D <= 1024 and Y.shape[1] == D
-            and H.shape[0] * D * H.element_size() > INFINITY_CACHE_BYTES)
+            and D % 4 == 0 and heads <= 8 and 128 <= D <= 1024
+            and n_rows * D * es > INFINITY_CACHE_BYTES)
+
+
+def _gat_sliced_applies(H, heads, d_head, Y):
+    return Y.shape[1] == heads * d_head and gat_sliced_wanted(H.shape[0], heads, d_head, H.dtype)
 
 
 def slice_pack64(x):

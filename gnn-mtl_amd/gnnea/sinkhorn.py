@@ -33,13 +33,19 @@ class SinkhornResult:
         self.loss = loss
 
 
+class SinkhornTimeout(RuntimeError):
+    """A wait between the workgroups of the on-chip KNOPP kernel timed out (results invalid):
+    its cooperative grid was not all resident, e.g. because another stream's kernel (an RCCL
+    collective) held CUs.  solve() / solve_batch() re-run the problem on the sweep path."""
+
+
 def _status(ws):
     raw = ws[:_lib.GNNEA_SK_STATUS_BYTES].cpu()  # sync point between batches
     ints = raw.view(torch.int64)
     dbl = raw.view(torch.float64)
     if int(ints[_lib.GNNEA_SK_ST_TIMEOUT]):
-        raise RuntimeError("gnnea.sinkhorn: a wait between the workgroups of the on-chip KNOPP "
-                           "kernel timed out (results invalid)")
+        raise SinkhornTimeout("gnnea.sinkhorn: a wait between the workgroups of the on-chip "
+                              "KNOPP kernel timed out (results invalid)")
     return ints, dbl
 
 
@@ -70,7 +76,18 @@ class _StatusPoll:
 
 def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
           want_plan=True, batch=10, variant=None):
-    """Run one Sinkhorn solve; C is [I, J] fp32 / fp64 on a HIP device, a / b the weights."""
+    """Run one Sinkhorn solve; C is [I, J] fp32 / fp64 on a HIP device, a / b the weights.
+    An on-chip solve whose inter-workgroup wait timed out is solved again from the start on
+    the sweep path (same iterates: both paths run the reference's operations)."""
+    try:
+        return _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch,
+                      variant, 0)
+    except SinkhornTimeout:
+        return _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch,
+                      variant, _lib.GNNEA_SK_NO_ONCHIP)
+
+
+def _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch, variant, flags):
     _lib.require_device(C, a, b)
     if variant is None:
         variant = DEFAULT_VARIANT
@@ -95,7 +112,7 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
         mode=mode, c_dtype=_lib.GNNEA_F32 if C.dtype == torch.float32 else _lib.GNNEA_F64,
         I=I, J=J, ldc=C.stride(0), C=C.data_ptr(), a=wa.data_ptr(), b=wb.data_ptr(),
         eps=float(eps), p=float(p), tol=float(tol), max_iter=int(max_iter), iters_run=0,
-        variant=int(variant), reserved=0, ws=ws.data_ptr())
+        variant=int(variant), flags=flags, ws=ws.data_ptr())
     pp = ctypes.byref(prob)
     st = stream_of(dev)
     with _lib.on_device(dev):
@@ -153,7 +170,16 @@ def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.fl
     """Solve a batch of problems of one shape [bt, I, J] as ONE launch sequence: every problem's
     iterations are enqueued batch by batch on the same stream and ONE device->host copy of all
     status blocks per round decides which problems continue (solve() polls once per problem
-    per round).  Cs [bt, I, J], As [bt, I], Bs [bt, J] on the device; returns SinkhornResults."""
+    per round).  Cs [bt, I, J], As [bt, I], Bs [bt, J] on the device; returns SinkhornResults.
+    A timed-out on-chip wait re-runs the batch on the sweep path, as solve() does."""
+    try:
+        return _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, variant, 0)
+    except SinkhornTimeout:
+        return _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, variant,
+                            _lib.GNNEA_SK_NO_ONCHIP)
+
+
+def _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, variant, flags):
     _lib.require_device(Cs, As, Bs)
     if variant is None:
         variant = DEFAULT_VARIANT
@@ -176,7 +202,7 @@ def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.fl
             mode=mode, c_dtype=_lib.GNNEA_F32 if C.dtype == torch.float32 else _lib.GNNEA_F64,
             I=I, J=J, ldc=C.stride(0), C=C.data_ptr(), a=wa[k].data_ptr(), b=wb[k].data_ptr(),
             eps=float(eps), p=float(p), tol=float(tol), max_iter=int(max_iter), iters_run=0,
-            variant=int(variant), reserved=0, ws=ws[k * stride:].data_ptr())))
+            variant=int(variant), flags=flags, ws=ws[k * stride:].data_ptr())))
     st = stream_of(dev)
     status = ws.view(bt, stride)[:, :_lib.GNNEA_SK_STATUS_BYTES]
     results = []
@@ -219,7 +245,8 @@ def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.fl
         ints = raw[k].view(torch.int64)
         dbl = raw[k].view(torch.float64)
         if int(ints[_lib.GNNEA_SK_ST_TIMEOUT]):
-            raise RuntimeError("gnnea.sinkhorn: an inter-workgroup wait timed out (problem %d)" % k)
+            raise SinkhornTimeout("gnnea.sinkhorn: an inter-workgroup wait timed out (problem %d)"
+                                  % k)
         out.append(SinkhornResult(plan, row_sum, col_sum, int(ints[ST_ITERS]),
                                   int(ints[ST_REASON]), float(dbl[SD_ERR]), float(dbl[SD_TNEW]),
                                   float(dbl[SD_TPREV]), float(dbl[SD_LOSS])))
@@ -264,7 +291,7 @@ class _Shard:
             c_dtype=_lib.GNNEA_F32 if C.dtype == torch.float32 else _lib.GNNEA_F64,
             I=self.I, J=self.J, ldc=C.stride(0), C=C.data_ptr(), a=self.a.data_ptr(),
             b=self.b.data_ptr(), eps=float(reg), p=1.0, tol=float(tol), max_iter=int(max_iter),
-            iters_run=0, variant=int(variant), reserved=0, ws=self.ws.data_ptr())
+            iters_run=0, variant=int(variant), flags=0, ws=self.ws.data_ptr())
         self.pp = ctypes.byref(self.prob)
         # the gathered row: column sums (scaling form, K resident) or (max, sum-exp) pairs
         n = int(L.gnnea_sinkhorn_shard_pair_len(self.pp))

@@ -86,8 +86,10 @@ class GraphAttentionLayer(nn.Module):
         W_all = torch.cat([att.W for att in self.attentions], dim=1)
         a_all = torch.cat([att.a for att in self.attentions], dim=0)  # [heads, 2*d_head]
         # above the Infinity Cache the GEMM also writes H slice-major for the GAT forward
-        # (a row shard exchanges row-major H: only without exchange)
-        H = ops.matmul(x, W_all, sliced=not isinstance(adj, DistAdj) or adj.part.g == 1)
+        # (a row shard exchanges row-major H: only without exchange), only when the forward
+        # takes the sliced passes for this shape (ops.gat_sliced_wanted)
+        H = ops.matmul(x, W_all, sliced=(not isinstance(adj, DistAdj) or adj.part.g == 1)
+                       and ops.gat_sliced_wanted(x.shape[0], heads, self.output_dim, x.dtype))
         if isinstance(adj, DistAdj):
             y = _sharded_gat(adj, H, a_all, heads, self.output_dim, first.alpha, first.act,
                              self.dropout, self.training)

@@ -263,6 +263,44 @@ int gnnea_gat_bwd_dst_sliced_bf16(const int32_t* rowptr, const int64_t* tpos, in
                                   int heads, int d_head, const float* dzT, const float* a,
                                   const float* ds2, void* dH, int64_t lddh, float* ds1,
                                   void* stream);
+/* Slice ranges of the sliced GAT passes, for the staged halo of a row-sharded layer
+ * (gnnea/dist_graph.py: slice q is aggregated as soon as its exchange has landed; the backward's
+ * source pass per slice, each slice's dH partial reduce-scattered while the next computes).
+ *   fwd_sliced_range: slices [s_begin, s_end) of Hs only; stats != 0 first computes m_out,
+ *                     den_out and wgt (s_begin == s_end: only that).  Same outputs as
+ *                     gnnea_gat_fwd_sliced_* over all slices.
+ *   bwd_src_sliced_range: slices [s_begin, s_end); weights != 0 first computes wT.  H and dH
+ *                     each row-major (hss / dhss = 64, ldh / lddh >= D) or slice-major 64-column
+ *                     tables (ldh / lddh = 64, hss / dhss = the slice stride >= 64 n_rows).
+ * Replaces: the halo exchange around att_layers.py:33-58 (reference: one process, no exchange). */
+int gnnea_gat_fwd_sliced_range_f32(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
+                                   const float* Hs, int64_t sstride, int heads, int d_head,
+                                   const float* s1, const float* s2, float alpha,
+                                   const float* edge_mask, int act, float* Y, int64_t ldy,
+                                   float* m_out, float* den_out, float* wgt, int s_begin,
+                                   int s_end, int stats, void* stream);
+int gnnea_gat_fwd_sliced_range_bf16(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
+                                    const void* Hs, int64_t sstride, int heads, int d_head,
+                                    const float* s1, const float* s2, float alpha,
+                                    const float* edge_mask, int act, void* Y, int64_t ldy,
+                                    float* m_out, float* den_out, float* wgt, int s_begin,
+                                    int s_end, int stats, void* stream);
+int gnnea_gat_bwd_src_sliced_range_f32(const int32_t* rowptrT, const int32_t* colT,
+                                       const int64_t* permT, int32_t n_rows, int heads,
+                                       int d_head, const float* Hm, int64_t ldh, int64_t hss,
+                                       const float* s2, float alpha, const float* edge_mask,
+                                       const float* rec, const float* Gs, int64_t sstride,
+                                       float* wT, float* pd, int64_t nnzT, float* dH,
+                                       int64_t lddh, int64_t dhss, int s_begin, int s_end,
+                                       int weights, void* stream);
+int gnnea_gat_bwd_src_sliced_range_bf16(const int32_t* rowptrT, const int32_t* colT,
+                                        const int64_t* permT, int32_t n_rows, int heads,
+                                        int d_head, const void* Hm, int64_t ldh, int64_t hss,
+                                        const float* s2, float alpha, const float* edge_mask,
+                                        const float* rec, const void* Gs, int64_t sstride,
+                                        float* wT, float* pd, int64_t nnzT, void* dH,
+                                        int64_t lddh, int64_t dhss, int s_begin, int s_end,
+                                        int weights, void* stream);
 /* row-major [n, D] -> the 64-column slice-major GAT table (D % 4 == 0, ldx % 4 == 0, sstride a
  * multiple of 64 and >= 64 n elements) */
 int gnnea_slice_pack64_f32(const float* X, int64_t ldx, int64_t n, int32_t D, float* Xs,
@@ -466,9 +504,12 @@ typedef struct gnnea_sinkhorn {
   int variant;      /* 0: scaling form with the fp64 K resident in ws (J <= 16384);
                        1: fused log-domain passes recomputing every term from C (no I*J state,
                        any J; used automatically above J = 16384) */
-  int reserved;
+  int flags;        /* GNNEA_SK_NO_ONCHIP: never take the on-chip cooperative KNOPP path (the
+                       host's retry after an inter-workgroup wait timed out); 0 otherwise */
   void* ws;         /* device workspace of gnnea_sinkhorn_ws_bytes(I, J) bytes */
 } gnnea_sinkhorn;
+
+#define GNNEA_SK_NO_ONCHIP 1
 
 int64_t gnnea_sinkhorn_ws_bytes(int I, int J);
 int gnnea_sinkhorn_init(const gnnea_sinkhorn* prob, void* stream);

@@ -141,13 +141,14 @@ class CpuEngine:
         return gH, (ga if need_da else None)
 
 
-def _worker(rank, world, port, mode, q):
+def _worker(rank, world, port, mode, q, staged=True):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "gnn-mtl_amd"))
     sys.path.insert(0, root)
     import torch.nn.functional as F
-    from gnnea import synth
+    from gnnea import exchange, synth
+    exchange.STAGED = staged  # GNNEA_HALO_STAGED: per-slice pipeline or the whole halo at once
     from gnnea.dist_graph import DistAdj, allreduce_grads
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -271,11 +272,12 @@ def _worker(rank, world, port, mode, q):
         dist.destroy_process_group()
 
 
-def _run(world, mode):
+def _run(world, mode, staged=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q, staged))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -291,10 +293,16 @@ def test_dist_layers_gloo_cpu(world):
     _run(world, "cpu")
 
 
+@pytest.mark.parametrize("world", [4, 8])
+def test_dist_layers_gloo_cpu_unstaged(world):
+    """GNNEA_HALO_STAGED=0: the whole halo, one aggregation, one blocking reduce-scatter."""
+    _run(world, "cpu", staged=False)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
-def test_dist_layers_rehearsal_on_device(device, world):
-    _run(world, "gpu")
+@pytest.mark.parametrize("world,staged", [(2, True), (4, True), (4, False)])
+def test_dist_layers_rehearsal_on_device(device, world, staged):
+    _run(world, "gpu", staged)
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])

@@ -345,6 +345,12 @@ def test_colsum_vs_fp64(device, N, D, dt):
     if D % 4 == 0 and N < 3_000_000:
         wide = torch.randn(N, 2 * D + 4, device=device).to(dt)
         assert rel_err(ops.colsum(wide[:, :D]).float().cpu(), wide[:, :D].double().sum(0).cpu()) < tol
+        # a right-hand block whose last row ends at the buffer's end (bf16 D = 300: the granules
+        # cover 304 columns, so the last row must not read past the allocation)
+        right = wide[:, D + 4:]
+        assert right.data_ptr() + right.shape[1] * right.element_size() == \
+            wide.data_ptr() + wide.shape[1] * wide.element_size()
+        assert rel_err(ops.colsum(right).float().cpu(), right.double().sum(0).cpu()) < tol
 
 
 @pytest.mark.parametrize("N,heads,d_head,dt", [

@@ -1,0 +1,43 @@
+"""Host logic of the Sinkhorn driver (no device): an on-chip solve whose inter-workgroup wait
+timed out is solved again from the start with the on-chip path disabled (gnnea_sinkhorn.flags =
+GNNEA_SK_NO_ONCHIP), once; a timeout on that path propagates."""
+import pytest
+
+from gnnea import _lib, sinkhorn
+
+
+def _fake(calls, fail_flags):
+    def f(*args):
+        flags = args[-1]
+        calls.append(flags)
+        if flags in fail_flags:
+            raise sinkhorn.SinkhornTimeout("timed out")
+        return ("solved", flags)
+    return f
+
+
+def test_solve_retries_on_the_sweep_path(monkeypatch):
+    calls = []
+    monkeypatch.setattr(sinkhorn, "_solve", _fake(calls, {0}))
+    assert sinkhorn.solve(0, None, None, None, 0.01, 1e-9, 10) == ("solved",
+                                                                   _lib.GNNEA_SK_NO_ONCHIP)
+    assert calls == [0, _lib.GNNEA_SK_NO_ONCHIP]
+
+
+def test_solve_batch_retries_and_second_timeout_propagates(monkeypatch):
+    calls = []
+    monkeypatch.setattr(sinkhorn, "_solve_batch", _fake(calls, {0}))
+    assert sinkhorn.solve_batch(0, None, None, None, 0.01, 1e-9, 10)[1] == \
+        _lib.GNNEA_SK_NO_ONCHIP
+    calls.clear()
+    monkeypatch.setattr(sinkhorn, "_solve", _fake(calls, {0, _lib.GNNEA_SK_NO_ONCHIP}))
+    with pytest.raises(sinkhorn.SinkhornTimeout):
+        sinkhorn.solve(0, None, None, None, 0.01, 1e-9, 10)
+    assert calls == [0, _lib.GNNEA_SK_NO_ONCHIP]
+
+
+def test_problem_struct_carries_flags():
+    p = _lib.SinkhornProblem(flags=_lib.GNNEA_SK_NO_ONCHIP)
+    assert p.flags == 1
+    names = [f[0] for f in _lib.SinkhornProblem._fields_]
+    assert names[-2:] == ["flags", "ws"]
