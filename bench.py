@@ -215,6 +215,44 @@ def gw_rate(device, B=3000):
             "peak_TFLOPs": 78.6, "peak_source": "AMD MI355X spec FP64 matrix (not in MI355X_MICROARCH.md)"}
 
 
+def fgw_rate(device, B=3000, outer=4, eps=0.1, alpha=0.5):
+    """The FGW outer loop of configs[4] (SinkhornOT/iterative_projection.py:125 fgw_iterative_1,
+    cderivation.py:147-189) at the EA batch B = 3000 in fp32 and bf16 inputs: per outer
+    iteration the cost rebuild C1·T·C2ᵀ (two GEMMs, x3 fp32 / bf16 MFMA) and the stabilised
+    Sinkhorn solve on it (sinkhorn_iteration, <= 100 iterations, fp64 on the device).  ms per
+    outer iteration = (T(outer) - T(1)) / (outer - 1) with tol = -1 (every iteration runs)."""
+    from SinkhornOT.cderivation import get_LT
+    from SinkhornOT.iterative_projection import fgw_iterative_1
+    g = torch.Generator(device="cpu").manual_seed(0)
+    X = 0.05 * torch.randn(B, 300, generator=g)
+    Y = 0.05 * torch.randn(B, 300, generator=g)
+    out = {"B": B, "epsilon": eps, "alpha": alpha, "p": 1, "inner": "sinkhorn_iteration "
+           "(numIterMax 100, tol 1e-9)", "method": "(T(%d) - T(1)) / %d outer iterations, "
+           "tol = -1" % (outer, outer - 1)}
+    for name, dt in (("f32", torch.float32), ("bf16", torch.bfloat16)):
+        C1 = torch.cdist(X, X)
+        C2 = torch.cdist(Y, Y)
+        D_ = torch.cdist(X, Y)
+        C1, C2, D_ = [(m / m.max()).to(device=device, dtype=dt) for m in (C1, C2, D_)]
+        mu = torch.full((B,), 1.0 / B, dtype=dt, device=device)
+        nu = torch.full((B,), 1.0 / B, dtype=dt, device=device)
+        ts = []
+        for n_out in (1, outer):
+            fgw_iterative_1(D_, C1, C2, mu, nu, alpha, 1, n_out, eps, tol=-1.0)  # warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fgw_iterative_1(D_, C1, C2, mu, nu, alpha, 1, n_out, eps, tol=-1.0)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        T = torch.full((B, B), 1.0 / (B * B), dtype=dt, device=device)
+        constC = torch.rand(B, B, generator=g).to(device=device, dtype=dt)
+        ms_lt = _timed(lambda: get_LT(constC, C1, C2, T), 5)
+        out[name] = {"ms_per_outer_iteration": round((ts[1] - ts[0]) / (outer - 1) * 1e3, 3),
+                     "cost_rebuild_ms": round(ms_lt, 3),
+                     "cost_rebuild_TFLOPs": round(4.0 * B ** 3 / ms_lt / 1e9, 1)}
+    return out
+
+
 def bf16_rate(device, steps):
     """The aggregation with bf16 feature storage (cfg-5's dtype, fp32 arithmetic) on cfg-5's
     own graph (synth.CONFIGS["cfg5"]: 2 x 2M entities, 2 x 20M triples, ~84M nnz): the table
@@ -278,18 +316,43 @@ def _timed(fn, steps):
     return float(np.median([a.elapsed_time(b) for a, b in evs]))
 
 
-def copy_rate(device, nbytes=4 << 30):
-    """Device-to-device copy bandwidth of one HBM buffer into another (read + write bytes per
-    second), to report beside the 8 TB/s datasheet figure."""
-    src = torch.empty(nbytes // 4, dtype=torch.float32, device=device).fill_(1.0)
+def anchors(device, copy_bytes=4 << 30, n_gather=16 << 20):
+    """The bandwidth anchors the roofline fractions are read against (csrc/ubench.hip): a
+    hand-written streaming copy (16 B per lane) and uniform-random whole-row gathers from tables
+    far larger than the 256-MB Infinity Cache, at the row sizes of the gather passes: 600 B (a
+    bf16 cfg-5 row, the row-major GAT passes), 1200 B (an fp32 cfg-4 row), 256 B (a 64-column
+    fp32 slice row of the sliced passes); median of 21 HIP-event timings each."""
+    L = _lib.lib()
+    st = lambda: _lib.stream_of(device)  # noqa: E731
+    out = {}
+    src = torch.empty(copy_bytes // 4, dtype=torch.float32, device=device).fill_(1.0)
     dst = torch.empty_like(src)
-    ms = _timed(lambda: dst.copy_(src), 21)
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    ms = _timed(lambda: _lib.check(L.gnnea_ub_copy(_lib.ptr(src), _lib.ptr(dst), copy_bytes,
+                                                   8 * ncu, st())), 21)
+    out["copy"] = {"GBps": round(2 * copy_bytes / (ms * 1e-3) / 1e9, 1), "ms": round(ms, 4),
+                   "bytes": 2 * copy_bytes, "kernel": "gnnea::k_ub_copy (16 B per lane)"}
+    ms_t = _timed(lambda: dst.copy_(src), 21)
+    out["torch_copy"] = {"GBps": round(2 * copy_bytes / (ms_t * 1e-3) / 1e9, 1),
+                         "ms": round(ms_t, 4)}
     del src, dst
     torch.cuda.empty_cache()
-    return {"GBps": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "bytes": 2 * nbytes,
-            "ms": round(ms, 4), "peak_spec_GBps": HBM_PEAK_GBS,
-            "frac_of_spec": round(2 * nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "method": "torch copy_ of a %d-MiB fp32 buffer, %s" % (nbytes >> 20, TIMING)}
+    g = torch.Generator(device=device).manual_seed(11)
+    res = torch.empty((n_gather + 63) // 64, dtype=torch.float32, device=device)
+    for row_bytes, rows in ((600, 4_000_000), (1200, 2_000_000), (256, 4_000_000)):
+        table = torch.empty(rows * row_bytes, dtype=torch.uint8, device=device).fill_(3)
+        idx = torch.randint(0, rows, (n_gather,), dtype=torch.int32, device=device, generator=g)
+        ms = _timed(lambda: _lib.check(L.gnnea_ub_gather(_lib.ptr(table), row_bytes,
+                                                         _lib.ptr(idx), n_gather, _lib.ptr(res),
+                                                         st())), 21)
+        out["gather_%dB" % row_bytes] = {
+            "GBps": round(n_gather * row_bytes / (ms * 1e-3) / 1e9, 1), "ms": round(ms, 4),
+            "table_MB": rows * row_bytes >> 20, "rows_gathered": n_gather,
+            "kernel": "gnnea::k_ub_gather (8-B chunks, 4 rows in flight per wave)"}
+        del table, idx
+        torch.cuda.empty_cache()
+    out["peak_spec_GBps"] = HBM_PEAK_GBS
+    return out
 
 
 def layout_rates(shard, H, Y, steps):
@@ -654,11 +717,15 @@ def main():
                 line["gw_cost"] = gw_rate(device)
             except Exception as e:  # report, never hide
                 line["gw_cost"] = {"error": repr(e)}
+            try:
+                line["fgw_outer"] = fgw_rate(device)
+            except Exception as e:  # report, never hide
+                line["fgw_outer"] = {"error": repr(e)}
         if world == 1 and not args.headline_only:
             try:
-                line["hbm_copy"] = copy_rate(device)
+                line["hbm_anchors"] = anchors(device)
             except Exception as e:  # report, never hide
-                line["hbm_copy"] = {"error": repr(e)}
+                line["hbm_anchors"] = {"error": repr(e)}
             try:
                 del hs
                 torch.cuda.empty_cache()

@@ -202,6 +202,29 @@ template <typename T> __device__ __forceinline__ T from_f32(float v);
 template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16_t from_f32<bf16_t>(float v) { return f32_to_bf16(v); }
 
+// ---- the x3 split (fp32 GEMMs on the bf16 matrix cores): x = h + m + l, each bf16, round to
+// nearest even: h = bf16(x), m = bf16(x - h), l = bf16(x - h - m).  Two elements at a time into
+// packed bf16 pairs (dword q of an 8-element MFMA operand holds elements 2q, 2q + 1): one
+// v_cvt_pk_bf16_f32 per level, the residuals as packed fp32 subtractions -- the same values as
+// element-wise casts with about half the vector instructions.
+typedef float x3_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 x3_bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t x3_cvt2(x3_f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, x3_bf16x2));
+}
+__device__ __forceinline__ x3_f32x2 x3_unpk(uint32_t p) {  // a packed bf16 pair -> two fp32
+  return x3_f32x2{__builtin_bit_cast(float, p << 16), __builtin_bit_cast(float, p & 0xffff0000u)};
+}
+__device__ __forceinline__ void x3_split_pair(float x0, float x1, uint32_t& h, uint32_t& m,
+                                              uint32_t& l) {
+  const x3_f32x2 xv = {x0, x1};
+  h = x3_cvt2(xv);
+  const x3_f32x2 r = xv - x3_unpk(h);
+  m = x3_cvt2(r);
+  l = x3_cvt2(r - x3_unpk(m));
+}
+
 inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 // fp64 exp for the log-sum-exp inner loops (arguments are shifted logits, x <= ~0):

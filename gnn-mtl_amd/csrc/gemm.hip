@@ -1059,7 +1059,25 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
       gemm_x3w_applies(trans_a, M, N, K, lda, A, beta, ldc, cs, C, C2, cs2) && ws &&
       ws_bytes >= gemm_x3w_ws_bytes(N))
     return gemm_x3w_launch(trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, cs, C2, cs2, ws,
-                           ws_bytes, (hipStream_t)stream);
+                           ws_bytes, (hipStream_t)stream, beta);
+  // K in (576, 640] (the HighWay input gradient [dh | dgate]·[W ; K_gᵀ], K = 600): two
+  // weight-resident launches over the k halves, the second accumulating into C (beta = 1); the
+  // packing of the second half's weight tiles waits for the first launch on the stream
+  {
+    const int64_t K1 = (K / 2 + 3) / 4 * 4;
+    if (B && K1 < K && (cs == 64 ? ldc >= N : (ldc >= 64 && cs >= M * ldc)) &&
+        (trans_b ? ldb >= K : ldb >= N) &&
+        gemm_x3w_applies(trans_a, M, N, K1, lda, A, beta, ldc, cs, C, nullptr, 0) &&
+        gemm_x3w_applies(trans_a, M, N, K - K1, lda, A + K1, 1.f, ldc, cs, C, C2, cs2) && ws &&
+        ws_bytes >= gemm_x3w_ws_bytes(N)) {
+      const int rc = gemm_x3w_launch(trans_b, M, N, K1, A, lda, B, ldb, bias, C, ldc, cs,
+                                     nullptr, 0, ws, ws_bytes, (hipStream_t)stream, beta);
+      if (rc) return rc;
+      const float* B2 = trans_b ? B + K1 : B + K1 * ldb;
+      return gemm_x3w_launch(trans_b, M, N, K - K1, A + K1, lda, B2, ldb, nullptr, C, ldc, cs, C2,
+                             cs2, ws, ws_bytes, (hipStream_t)stream, 1.f);
+    }
+  }
   if (C2) {  // a slice-major copy as well: fused into k_gemm_x3p's epilogue, else packed after
     const bool lda_ok = !trans_a && lda % 4 == 0 && K % 4 == 0 && (((uintptr_t)A) & 15) == 0;
     const int64_t pb = x3_planes_bytes(N, K);

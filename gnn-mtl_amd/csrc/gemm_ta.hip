@@ -319,19 +319,18 @@ struct TdTriple {
   ta_bf16x8 h, m, l;
 };
 
-// x = h + m + l exactly (the x3 split of gemm.hip / k_gemm_ta, round to nearest even)
+// x = h + m + l exactly (the x3 split of gemm.hip / k_gemm_ta, round to nearest even), pairwise
+// (common.h x3_split_pair: the same values, about half the vector instructions)
 __device__ __forceinline__ TdTriple td_split(const float (&x)[8]) {
+  uint4 h, m, l;
+  x3_split_pair(x[0], x[1], h.x, m.x, l.x);
+  x3_split_pair(x[2], x[3], h.y, m.y, l.y);
+  x3_split_pair(x[4], x[5], h.z, m.z, l.z);
+  x3_split_pair(x[6], x[7], h.w, m.w, l.w);
   TdTriple t;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const __bf16 h = (__bf16)x[e];
-    const float r1 = x[e] - (float)h;
-    const __bf16 m = (__bf16)r1;
-    const __bf16 l = (__bf16)(r1 - (float)m);
-    t.h[e] = h;
-    t.m[e] = m;
-    t.l[e] = l;
-  }
+  t.h = __builtin_bit_cast(ta_bf16x8, h);
+  t.m = __builtin_bit_cast(ta_bf16x8, m);
+  t.l = __builtin_bit_cast(ta_bf16x8, l);
   return t;
 }
 

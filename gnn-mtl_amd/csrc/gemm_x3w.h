@@ -1,5 +1,6 @@
 // Weight-resident fp32 projection GEMM through the three-way bf16 split (gemm_x3w.hip): C = A·op(B)
-// (+ bias) for tall A with K in (256, 320].  Internal to libgnnea (gemm.hip's gemm_x3 dispatches
+// (+ bias + beta·C) for tall A with K in (288, 320] (gemm.hip runs K in (576, 640] as two
+// launches, the second accumulating).  Internal to libgnnea (gemm.hip's gemm_x3 dispatches
 // to it; no C-ABI entry of its own).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -13,5 +14,5 @@ int64_t gemm_x3w_ws_bytes(int64_t N);
 int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                     const float* B, int64_t ldb, const float* bias, float* C, int64_t ldc,
                     int64_t cs, float* C2, int64_t cs2, void* ws, int64_t ws_bytes,
-                    hipStream_t s);
+                    hipStream_t s, float beta = 0.f);
 }  // namespace gnnea

@@ -245,6 +245,51 @@ __global__ __launch_bounds__(64 * W3_NW, 1) void k_gemm_x3w(int M, int N, int K,
   }
 }
 
+// The activation split of the ring kernel, two elements at a time into packed bf16 pairs
+// (dword q of a fragment = elements 2q, 2q + 1).  GNNEA_X3W_SPLIT (a tuning switch, default 0):
+//   0  round-to-nearest-even: h = bf16(x), m = bf16(x - h), l = bf16(x - h - m)  (gemm.hip's split)
+//   2  truncation: h = the top 16 bits of x, m = the top 16 bits of x - h, l = bf16(x - h - m);
+//      x = h + m + l exactly (each residual keeps at most 16, then 8 significant bits), the two
+//      residuals as packed fp32 subtractions and the h / m pairs as byte permutes (fewer vector
+//      instructions per element; the dropped products m*l, l*m, l*l stay below 2^-21 |a||w|)
+//   1  timing only: h = m = l = the top halves (NOT a split; measures the split's cost)
+#ifndef GNNEA_X3W_SPLIT
+#define GNNEA_X3W_SPLIT 0
+#endif
+struct W3SplitP {
+  uint32_t h[4], m[4], l[4];
+  __device__ __forceinline__ w3_bf16x8 vh() const { return __builtin_bit_cast(w3_bf16x8, *(const uint4*)h); }
+  __device__ __forceinline__ w3_bf16x8 vm() const { return __builtin_bit_cast(w3_bf16x8, *(const uint4*)m); }
+  __device__ __forceinline__ w3_bf16x8 vl() const { return __builtin_bit_cast(w3_bf16x8, *(const uint4*)l); }
+};
+
+__device__ __forceinline__ uint32_t w3_pk(__bf16 a, __bf16 b) {
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+
+template <int MODE>
+__device__ __forceinline__ void w3_split_pair(float x0, float x1, uint32_t& h, uint32_t& m,
+                                              uint32_t& l) {
+  if constexpr (MODE == 0) {  // the same values as per-element casts, pairwise instructions
+    x3_split_pair(x0, x1, h, m, l);
+  } else if constexpr (MODE == 2) {
+    const uint32_t u0 = __builtin_bit_cast(uint32_t, x0), u1 = __builtin_bit_cast(uint32_t, x1);
+    const x3_f32x2 hv = {__builtin_bit_cast(float, u0 & 0xffff0000u),
+                         __builtin_bit_cast(float, u1 & 0xffff0000u)};
+    const x3_f32x2 r = x3_f32x2{x0, x1} - hv;
+    const uint32_t v0 = __builtin_bit_cast(uint32_t, r.x), v1 = __builtin_bit_cast(uint32_t, r.y);
+    const x3_f32x2 mv = {__builtin_bit_cast(float, v0 & 0xffff0000u),
+                         __builtin_bit_cast(float, v1 & 0xffff0000u)};
+    const x3_f32x2 q = r - mv;
+    h = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+    m = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
+    l = x3_cvt2(q);
+  } else {
+    const uint32_t u0 = __builtin_bit_cast(uint32_t, x0), u1 = __builtin_bit_cast(uint32_t, x1);
+    h = m = l = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+  }
+}
+
 // The same product with 8 waves (two per SIMD: each one's LDS-read latency and split under the
 // other's MFMAs) and a register ring instead of a whole-tile double buffer: a wave keeps ONE tile's
 // 20 activation quads, and the quads of step s are replaced by the next tile's step s as soon as
@@ -255,7 +300,7 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
                                                        const float* __restrict__ bias,
                                                        float* __restrict__ C, int64_t ldc,
                                                        int64_t cs, float* __restrict__ C2,
-                                                       int64_t cs2) {
+                                                       int64_t cs2, float beta) {
   constexpr int NW = 8, BM = 16 * NW;
   __shared__ __attribute__((aligned(16))) uint4 wl[3 * W3_PLANE];
   __shared__ __attribute__((aligned(16))) float bsh[W3_NC];
@@ -302,13 +347,8 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
     x[4] = __builtin_bit_cast(float, q1.x); x[5] = __builtin_bit_cast(float, q1.y);
     x[6] = __builtin_bit_cast(float, q1.z); x[7] = __builtin_bit_cast(float, q1.w);
   };
-  auto split_el = [&](const float (&x)[8], int e, W3Split& t) {
-    const __bf16 h = (__bf16)x[e];
-    const float r1 = x[e] - (float)h;
-    const __bf16 m = (__bf16)r1;
-    t.h[e] = h;
-    t.m[e] = m;
-    t.l[e] = (__bf16)(r1 - (float)m);
+  auto split_pair = [&](const float (&x)[8], int q, W3SplitP& t) {
+    w3_split_pair<GNNEA_X3W_SPLIT>(x[2 * q], x[2 * q + 1], t.h[q], t.m[q], t.l[q]);
   };
   if (rs < tm) {
     const float* p = row_ptr(rs);
@@ -321,13 +361,13 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
     w3_f32x4 acc[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) acc[j] = w3_f32x4{0.f, 0.f, 0.f, 0.f};
-    W3Split acur;
+    W3SplitP acur;
     {
       float x[8];
       raw_step(0, x);
       load_step(pn, 0);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) split_el(x, e, acur);
+      for (int q = 0; q < 4; ++q) split_pair(x, q, acur);
     }
 #pragma unroll
     for (int s = 0; s < W3_KC; ++s) {
@@ -337,8 +377,9 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
       // wave on the SIMD covers their latency)
       float xn[8];
       if (s + 1 < W3_KC) raw_step(s + 1, xn);
-      W3Split anx;
+      W3SplitP anx;
       const uint4* wp = wlane + s * 4 * W3_NC;
+      const w3_bf16x8 ah = acur.vh(), am = acur.vm(), al = acur.vl();
 #pragma unroll
       for (int jn = 0; jn < 5; ++jn) {
         __builtin_amdgcn_sched_barrier(0);
@@ -346,16 +387,13 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
         const w3_bf16x8 wm = __builtin_bit_cast(w3_bf16x8, wp[W3_PLANE + 16 * jn]);
         const w3_bf16x8 wlo = __builtin_bit_cast(w3_bf16x8, wp[2 * W3_PLANE + 16 * jn]);
         w3_f32x4& c = acc[jn];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.l, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, acur.m, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, acur.h, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.m, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, acur.h, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.h, c, 0, 0, 0);
-        if (s + 1 < W3_KC && jn < 4) {
-          split_el(xn, 2 * jn, anx);
-          split_el(xn, 2 * jn + 1, anx);
-        }
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, al, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, am, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, ah, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, am, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, ah, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, ah, c, 0, 0, 0);
+        if (s + 1 < W3_KC && jn < 4) split_pair(xn, jn, anx);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (s + 1 < W3_KC) {
@@ -375,8 +413,13 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
         if (n < N) {  // N % 4 == 0: a group is wholly in or out
           const float4 bv = *(const float4*)(bsh + c);
           const w3_f32x4 a4 = acc[jn];
-          const float4 o = make_float4(a4[0] + bv.x, a4[1] + bv.y, a4[2] + bv.z, a4[3] + bv.w);
-          *(float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63))) = o;
+          float4 o = make_float4(a4[0] + bv.x, a4[1] + bv.y, a4[2] + bv.z, a4[3] + bv.w);
+          float4* cp = (float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63)));
+          if (beta != 0.f) {  // C = A·B + bias + beta C (uniform branch)
+            const float4 cv = *cp;
+            o.x += beta * cv.x; o.y += beta * cv.y; o.z += beta * cv.z; o.w += beta * cv.w;
+          }
+          *cp = o;
           if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
         }
       }
@@ -403,7 +446,8 @@ int64_t gemm_x3w_ws_bytes(int64_t N) {
 bool gemm_x3w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda, const void* A,
                       float beta, int64_t ldc, int64_t cs, const void* C, const void* C2,
                       int64_t cs2) {
-  return x3w_on() && !trans_a && beta == 0.f && A && C && M >= 65536 && M < (1ll << 31) &&
+  return x3w_on() && !trans_a && (beta == 0.f || x3w_mode() == 2) && A && C && M >= 65536 &&
+         M < (1ll << 31) &&
          N >= 64 && N <= 4096 && N % 4 == 0 && K > 32 * (W3_KC - 1) && K <= 32 * W3_KC && K % 4 == 0 &&
          lda >= K && lda % 4 == 0 && (((uintptr_t)A) & 15) == 0 &&
          ldc % 4 == 0 && cs % 4 == 0 && (((uintptr_t)C) & 15) == 0 &&
@@ -413,7 +457,7 @@ bool gemm_x3w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda,
 int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                     const float* B, int64_t ldb, const float* bias, float* C, int64_t ldc,
                     int64_t cs, float* C2, int64_t cs2, void* ws, int64_t ws_bytes,
-                    hipStream_t s) {
+                    hipStream_t s, float beta) {
   const int ntn = (int)((N + W3_NC - 1) / W3_NC);
   if (!ws || ws_bytes < gemm_x3w_ws_bytes(N)) return GNNEA_EWORKSPACE;
   bf16_t* P = (bf16_t*)ws;
@@ -441,7 +485,7 @@ int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A
   if ((int64_t)grid / ntn > tm) grid = (int)((tm + 7) / 8 * 8 * ntn);
   if (ring)
     hipLaunchKernelGGL(k_gemm_x3w_ring, dim3(grid), dim3(512), 0, s, (int)M, (int)N, (int)K, ntn,
-                       A, lda, P, bias, C, ldc, cs, C2, cs2);
+                       A, lda, P, bias, C, ldc, cs, C2, cs2, beta);
   else
     hipLaunchKernelGGL(k_gemm_x3w, dim3(grid), dim3(64 * W3_NW), 0, s, (int)M, (int)N, (int)K,
                        ntn, A, lda, P, bias, C, ldc, cs, C2, cs2);

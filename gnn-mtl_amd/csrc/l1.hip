@@ -240,9 +240,49 @@ __global__ __launch_bounds__(256) void k_topk_rows(const float* __restrict__ key
   }
 }
 
+// Per-term L1 distances over a column block (the column-sharded EA loss, gnnea/dist_loss.py):
+// out[j] = sum_d |X[a_j][d] - X[b_j][d]| in fp64 (every term exact, summed in a fixed lane order),
+// LPT lanes per term (LPT | 64, so a term's lanes leave together), 4-B loads, consecutive lanes on
+// consecutive columns of the two gathered rows.
+template <int LPT>
+__global__ __launch_bounds__(256) void k_l1_terms(const float* __restrict__ X, int64_t ldx, int D,
+                                                  int64_t n, const int64_t* __restrict__ a,
+                                                  const int64_t* __restrict__ b,
+                                                  double* __restrict__ out) {
+  const int64_t term = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LPT;
+  if (term >= n) return;
+  const int l = threadIdx.x % LPT;
+  const float* xa = X + a[term] * ldx;
+  const float* xb = X + b[term] * ldx;
+  double s = 0.0;
+  for (int d = l; d < D; d += LPT) s += fabs((double)xa[d] - (double)xb[d]);
+#pragma unroll
+  for (int o = LPT / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, LPT);
+  if (l == 0) out[term] = s;
+}
+
 }  // namespace gnnea
 
 using namespace gnnea;
+
+extern "C" int gnnea_l1_terms_f32(const float* X, int64_t ldx, int32_t D, int64_t n,
+                                  const int64_t* a, const int64_t* b, double* out, void* stream) {
+  if (n < 0 || D < 0 || ldx < D) return GNNEA_EINVAL;
+  if (n == 0) return 0;
+  if (!X || !a || !b || !out) return GNNEA_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const int lpt = D <= 16 ? 16 : D <= 64 ? 32 : 64;  // lanes per term
+  const int64_t nb = (n * lpt + 255) / 256;
+  if (nb >= (1ll << 31)) return GNNEA_EINVAL;
+  if (lpt == 16)
+    hipLaunchKernelGGL(k_l1_terms<16>, dim3((unsigned)nb), dim3(256), 0, s, X, ldx, D, n, a, b, out);
+  else if (lpt == 32)
+    hipLaunchKernelGGL(k_l1_terms<32>, dim3((unsigned)nb), dim3(256), 0, s, X, ldx, D, n, a, b, out);
+  else
+    hipLaunchKernelGGL(k_l1_terms<64>, dim3((unsigned)nb), dim3(256), 0, s, X, ldx, D, n, a, b, out);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" int gnnea_l1_keys_f32(const float* Q, int64_t ldq, int32_t nq, const float* X,
                                  int64_t ldx, int32_t nx, int32_t D, float* keys, int64_t ldk,

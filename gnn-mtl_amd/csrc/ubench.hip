@@ -1,0 +1,105 @@
+// Bandwidth anchors for the roofline fractions bench.py quotes ("measure a
+// device-copy bandwidth on the box and report it next to the datasheet value").  torch's copy_
+// (5.0 TB/s) is one implementation's rate, not the hardware's; these two kernels are the
+// reference points the gather-bound passes are judged against:
+//   k_ub_copy    a streaming copy, 16 B per lane per access, every lane of a wave on consecutive
+//                16-B chunks (1 KB per wave instruction), four accesses in flight per lane, a
+//                grid of a few workgroups per CU striding over the buffer;
+//   k_ub_gather  whole-row gathers: one wave per 64 rows of an index list, each row read by the
+//                lanes of the wave as 8-B chunks (row_bytes % 8 == 0: a 600-B row is 75 chunks),
+//                summed into one accumulator per lane (nothing is written per row, so only the
+//                gathered bytes cross HBM) — the access pattern of the row-major GAT passes
+//                (600-B bf16 rows at cfg-5) when the index list is uniform random over a table
+//                much larger than the 256-MB Infinity Cache.
+#include "common.h"
+
+namespace gnnea {
+
+__global__ __launch_bounds__(256) void k_ub_copy(const uint4* __restrict__ src,
+                                                 uint4* __restrict__ dst, int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+// wave w handles index entries [64 w, 64 w + 64): the 64 row ids are loaded once (one per lane)
+// and broadcast; for each row every lane reads its 8-B chunk(s), U rows in flight
+template <int NCH>
+__global__ __launch_bounds__(256) void k_ub_gather(const unsigned char* __restrict__ table,
+                                                   int64_t row_bytes, const int32_t* __restrict__ idx,
+                                                   int64_t n, float* __restrict__ out) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + wave_id();
+  const int64_t base = w * 64;
+  if (base >= n) return;
+  const int lane = lane_id();
+  const int cnt = (int)min((int64_t)64, n - base);
+  const int my = idx[base + min(lane, cnt - 1)];
+  const int nfull = (int)(row_bytes / 8);
+  uint32_t acc = 0;
+  constexpr int U = 4;
+  for (int k = 0; k < cnt; k += U) {
+    uint2 v[U][NCH];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = __shfl(my, min(k + u, cnt - 1), 64);
+      const unsigned char* row = table + (int64_t)r * row_bytes;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int ch = lane + 64 * c;
+        // chunks past the row re-read the row's first chunk (no branch around the load)
+        v[u][c] = *(const uint2*)(row + 8 * (ch < nfull ? ch : 0));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) acc ^= v[u][c].x ^ v[u][c].y;
+  }
+  // one value per lane keeps the loads live; written once per wave
+  if (lane == 0) out[w] = (float)(acc & 0xffff);
+}
+
+}  // namespace gnnea
+
+using namespace gnnea;
+
+extern "C" int gnnea_ub_copy(const void* src, void* dst, int64_t bytes, int32_t blocks,
+                             void* stream) {
+  if (bytes < 0 || bytes % 16 || blocks <= 0) return GNNEA_EINVAL;
+  if (bytes == 0) return 0;
+  if (!src || !dst || (((uintptr_t)src | (uintptr_t)dst) & 15)) return GNNEA_EALIGN;
+  hipLaunchKernelGGL(k_ub_copy, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)src, (uint4*)dst, bytes / 16);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int gnnea_ub_gather(const void* table, int64_t row_bytes, const int32_t* idx,
+                               int64_t n, float* out, void* stream) {
+  if (row_bytes <= 0 || row_bytes % 8 || row_bytes > 2 * 1024 || n < 0) return GNNEA_EINVAL;
+  if (n == 0) return 0;
+  if (!table || !idx || !out || (((uintptr_t)table) & 7)) return GNNEA_EINVAL;
+  const int64_t waves = (n + 63) / 64, nb = (waves + 3) / 4;
+  if (nb >= (1ll << 31)) return GNNEA_EINVAL;
+  const int nch = (int)((row_bytes / 8 + 63) / 64);
+  hipStream_t s = (hipStream_t)stream;
+  switch (nch) {
+    case 1: hipLaunchKernelGGL(k_ub_gather<1>, dim3((unsigned)nb), dim3(256), 0, s,
+                               (const unsigned char*)table, row_bytes, idx, n, out); break;
+    case 2: hipLaunchKernelGGL(k_ub_gather<2>, dim3((unsigned)nb), dim3(256), 0, s,
+                               (const unsigned char*)table, row_bytes, idx, n, out); break;
+    case 3: hipLaunchKernelGGL(k_ub_gather<3>, dim3((unsigned)nb), dim3(256), 0, s,
+                               (const unsigned char*)table, row_bytes, idx, n, out); break;
+    default: hipLaunchKernelGGL(k_ub_gather<4>, dim3((unsigned)nb), dim3(256), 0, s,
+                                (const unsigned char*)table, row_bytes, idx, n, out); break;
+  }
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}

@@ -236,6 +236,9 @@ SIGNATURES = {
                                                    ctypes.c_int, _i64, _p, _p, _p, _p]),
     "gnnea_l1_keys_f32":(ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _i64, _p]),
     "gnnea_l1_pairs_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i32, _i32, _p, _p]),
+    "gnnea_l1_terms_f32": (ctypes.c_int, [_p, _i64, _i32, _i64, _p, _p, _p, _p]),
+    "gnnea_ub_copy": (ctypes.c_int, [_p, _p, _i64, _i32, _p]),
+    "gnnea_ub_gather": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _p]),
     "gnnea_l1_rank_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _p, _p]),
     "gnnea_topk_rows_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _i64, _p, _i64, _i32,
                                            _i32, _p, _p, _i32, _p, _p]),

@@ -142,6 +142,146 @@ class HipEngine:
         from . import ops
         return ops.highway_bwd_sliced(dy, S, G, resid, act, want_dresid, dgate)
 
+    # ---- the staged GAT halo (64-column slices of the head-concatenated projection) -------
+    def gat_slice_w(self, dtype):
+        """Columns per GAT stage: the sliced GAT kernels' 64-column tables (256 B fp32, 128 B
+        bf16 per row piece)."""
+        return 64
+
+    def gat_staged_ok(self, heads, d_head):
+        from . import ops
+        D = heads * d_head
+        return ops.gat_two_heads_per_slice(heads, d_head) and D % 4 == 0 and heads <= 8 and \
+            D <= 1024
+
+    def gat_pack(self, x, tables, row0):
+        """tables[q, row0:row0+rows, :] = x's q-th 64-column block (the GAT tables)."""
+        from . import ops
+        x = ops._rows(x)
+        S, n, W = tables.shape
+        with _lib.on_device(x.device):
+            _lib.check(ops._sfn("gnnea_slice_pack64", x.dtype)(
+                _lib.ptr(x), ops._ld(x), x.shape[0], x.shape[1], ops._off(tables[0], row0),
+                n * W, _lib.stream_of(x.device)))
+        return tables
+
+    def gat_scores(self, H, a_all, heads, d_head):
+        """Per-row logits (s1, s2) [rows, heads] of the rank's own projected rows."""
+        from . import ops
+        return ops.gat_scores(H, ops._featc(a_all, torch.float32), heads, d_head)
+
+    def gat_rowstats(self, csr, s1, s2, heads, d_head, alpha):
+        """Row max / denominator of the shard's rows and every edge's weight (the sliced
+        forward's statistics pass: s1 of the own rows, s2 of every KG row)."""
+        from . import ops
+        N = csr.n_rows
+        dev = s1.device
+        m = torch.empty((N, heads), dtype=torch.float32, device=dev)
+        den = torch.empty_like(m)
+        wgt = torch.empty((max(csr.nnz, 1), heads), dtype=torch.float32, device=dev)
+        D = heads * d_head
+        fn = ops._gat_fn("gnnea_gat_fwd_sliced_range", torch.float32)
+        with _lib.on_device(dev):
+            _lib.check(fn(_lib.ptr(csr.rowptr), _lib.ptr(csr.col), N, None, 64, heads, d_head,
+                          _lib.ptr(s1), _lib.ptr(s2), float(alpha), None, _lib.GNNEA_ACT_IDENTITY,
+                          None, (D + 3) // 4 * 4, _lib.ptr(m), _lib.ptr(den), _lib.ptr(wgt), 0, 0,
+                          1, _lib.stream_of(dev)))
+        return m, den, wgt
+
+    def gat_fwd_slice(self, csr, tables, q, s1, s2, stats, heads, d_head, alpha, act, Y):
+        """Y's columns of slice q from the slice-q table (weights from gat_rowstats)."""
+        from . import ops
+        m, den, wgt = stats
+        S, n, W = tables.shape
+        fn = ops._gat_fn("gnnea_gat_fwd_sliced_range", tables.dtype)
+        with _lib.on_device(Y.device):
+            _lib.check(fn(_lib.ptr(csr.rowptr), _lib.ptr(csr.col), csr.n_rows, _lib.ptr(tables),
+                          n * W, heads, d_head, _lib.ptr(s1), _lib.ptr(s2), float(alpha), None,
+                          int(act), _lib.ptr(Y), Y.stride(0), _lib.ptr(m), _lib.ptr(den),
+                          _lib.ptr(wgt), q, q + 1, 0, _lib.stream_of(Y.device)))
+        return Y
+
+    def gat_bwd_prep(self, dY, Y, s1, stats, heads, d_head, act):
+        """(G slice-major [S][rows][64], records) of the shard's destination rows."""
+        from . import ops
+        m, den, _ = stats
+        N = Y.shape[0]
+        D = heads * d_head
+        dY = ops._pad4(dY, D, Y.dtype)
+        Gs = ops.sliced_empty(N, D, Y.device, Y.dtype, W=64)
+        rec = torch.empty((N, heads, 4), dtype=torch.float32, device=Y.device)
+        with _lib.on_device(Y.device):
+            _lib.check(ops._gat_fn("gnnea_gat_bwd_prep_sliced", Y.dtype)(
+                N, heads, d_head, _lib.ptr(dY), _lib.ptr(Y), Y.stride(0), _lib.ptr(s1),
+                _lib.ptr(m), _lib.ptr(den), int(act), _lib.ptr(Gs), Gs.stride(0), _lib.ptr(rec),
+                _lib.stream_of(Y.device)))
+        return Gs, rec
+
+    def gat_bwd_buffers(self, csrT, S, heads, n_src, dtype, device):
+        """(wT, pd, P): per-edge weights, per-slice head-product partials, and the slice-major
+        dH partial [S][n_src][64] of every KG row."""
+        nnzT = max(csrT.nnz, 1)
+        return (torch.empty((nnzT, heads), dtype=torch.float32, device=device),
+                torch.empty((S, nnzT, 2), dtype=torch.float32, device=device),
+                torch.empty((S, n_src, 64), dtype=dtype, device=device))
+
+    def gat_bwd_src_slice(self, csrT, tables, q, s2, rec, Gs, bufs, heads, d_head, alpha,
+                          weights):
+        """P[q] = sum_i w_ij G_i over slice q for every KG source row j, and slice q's share of
+        the per-edge head products G_i . H_j (H_j read from the halo's slice-q table)."""
+        from . import ops
+        wT, pd, P = bufs
+        S, n, W = tables.shape
+        with _lib.on_device(P.device):
+            _lib.check(ops._gat_fn("gnnea_gat_bwd_src_sliced_range", tables.dtype)(
+                _lib.ptr(csrT.rowptr), _lib.ptr(csrT.col), _lib.ptr(csrT.perm), csrT.n_rows,
+                heads, d_head, _lib.ptr(tables), 64, n * W, _lib.ptr(s2), float(alpha), None,
+                _lib.ptr(rec), _lib.ptr(Gs), Gs.stride(0), _lib.ptr(wT), _lib.ptr(pd),
+                csrT.nnz, _lib.ptr(P), 64, P.stride(0), q, q + 1, 1 if weights else 0,
+                _lib.stream_of(P.device)))
+        return P[q]
+
+    def gat_bwd_edge(self, csrT, s2, rec, bufs, a, heads, d_head, alpha):
+        """(dz in A^T order, ds2 partial of every KG row); dH is left alone."""
+        from . import ops
+        a32 = ops._featc(a, torch.float32)
+        _, pd, _ = bufs
+        dev = s2.device
+        dzT = torch.empty((max(csrT.nnz, 1), heads), dtype=torch.float32, device=dev)
+        ds2 = torch.empty((csrT.n_rows, heads), dtype=torch.float32, device=dev)
+        with _lib.on_device(dev):
+            _lib.check(ops._gat_fn("gnnea_gat_bwd_edge_sliced", torch.float32)(
+                _lib.ptr(csrT.rowptr), _lib.ptr(csrT.col), _lib.ptr(csrT.perm), csrT.n_rows,
+                heads, d_head, _lib.ptr(s2), float(alpha), None, _lib.ptr(rec), _lib.ptr(pd),
+                csrT.nnz, _lib.ptr(a32), None, heads * d_head, _lib.ptr(dzT), _lib.ptr(ds2),
+                _lib.stream_of(dev)))
+        return dzT, ds2
+
+    def gat_bwd_dst(self, csr, dzT, a, ds2, dH, heads, d_head):
+        """ds1 of the shard's rows and dH_i += ds1_i (x) a1 + ds2_i (x) a2 (own rows)."""
+        from . import ops
+        a32 = ops._featc(a, torch.float32)
+        dev = dH.device
+        ds1 = torch.empty((csr.n_rows, heads), dtype=torch.float32, device=dev)
+        with _lib.on_device(dev):
+            _lib.check(ops._gat_fn("gnnea_gat_bwd_dst_sliced", dH.dtype)(
+                _lib.ptr(csr.rowptr), _lib.ptr(csr.tpos()), csr.n_rows, heads, d_head,
+                _lib.ptr(dzT), _lib.ptr(a32), _lib.ptr(ds2), _lib.ptr(dH), dH.stride(0),
+                _lib.ptr(ds1), _lib.stream_of(dev)))
+        return ds1
+
+    def gat_da(self, H, ds, heads, d_head):
+        from . import ops
+        return ops.gat_da(H, ds, heads, d_head)
+
+    def transpose(self, csr):
+        return csr.transpose()
+
+    def unpack64(self, Ts, D):
+        """[S][rows][64] slice-major -> row-major [rows, D] (a view of a [rows, 64 S] copy)."""
+        S, n, W = Ts.shape
+        return Ts.permute(1, 0, 2).reshape(n, S * W)[:, :D]
+
     def gat_bwd(self, csr, saved, dY, heads, d_head, alpha, act, row0, need_da):
         """(dH partial over every KG row, da partial) of sum(Y_loc ⊙ dY)."""
         from . import ops
@@ -242,15 +382,30 @@ class DistAdj:
     def _peers(self):
         return self.part.group_ranks(self.part.kg), self.part.li, self.part.other_ranks()
 
-    def halo_slices(self, h_loc):
+    def staged_gat(self, heads, d_head):
+        """The GAT halo moves slice by slice (64-column tables), overlapped with the per-slice
+        aggregation: row shards (g > 1) whose engine has the staged GAT operations."""
+        from . import exchange
+        return (self.part.g > 1 and exchange.STAGED and hasattr(self.engine, "gat_fwd_slice")
+                and self.engine.gat_staged_ok(heads, d_head))
+
+    def halo_slices(self, h_loc, gat=False):
         """Pack the own rows into the KG's slice tables [S][n][W] and issue every slice's
-        exchange: returns (tables, stages, works per slice)."""
+        exchange: returns (tables, stages, works per slice).  gat: the GAT kernels' 64-column
+        tables for either storage type."""
         from . import exchange
         D = h_loc.shape[1]
-        W, st = self.stages(D, h_loc.dtype)
+        if gat:
+            W = self.engine.gat_slice_w(h_loc.dtype)
+            st = [(c0, min(D, c0 + W)) for c0 in range(0, D, W)]
+        else:
+            W, st = self.stages(D, h_loc.dtype)
         tables = torch.empty((len(st), self.part.n_cols, W), dtype=h_loc.dtype,
                              device=h_loc.device)
-        self.engine.pack_slices(h_loc, tables, self.part.row0)
+        if gat:
+            self.engine.gat_pack(h_loc, tables, self.part.row0)
+        else:
+            self.engine.pack_slices(h_loc, tables, self.part.row0)
         ranks, li, other = self._peers()
         works = exchange.all_gather_slices(list(tables), self.part.row0, self.part.n_rows,
                                            self.group, ranks, li, other)
@@ -341,6 +496,63 @@ class DistAdj:
             return self.staged_aggregate_t(Gs, g.shape[1], out)
         out.copy_(self.reduce_scatter(self.engine.spmm_t(self.csr, g)))
         return out
+
+    def gat_staged_forward(self, H, a_all, heads, d_head, alpha, act):
+        """GAT of the shard's rows with the halo cut into 64-column slices: the logits s2 of
+        every KG row first (one small all-gather: the row statistics need them), the row
+        statistics and edge weights while the slices move, then slice q aggregated as soon as
+        it has landed.  Returns (Y [rows, D], saved state for gat_staged_backward)."""
+        from . import exchange
+        e = self.engine
+        D = heads * d_head
+        s1, s2_loc = e.gat_scores(H, a_all, heads, d_head)
+        s2 = torch.empty((self.part.n_cols, heads), dtype=s2_loc.dtype, device=s2_loc.device)
+        ranks, li, other = self._peers()
+        exchange.all_gather(s2_loc, s2, self.group, ranks, li, copy_own=True, other=other)
+        tables, st, works = self.halo_slices(H, gat=True)
+        stats = e.gat_rowstats(self.csr, s1, s2, heads, d_head, alpha)
+        Y = torch.empty((self.part.n_rows, D), dtype=H.dtype, device=H.device)
+        for q in range(len(st)):
+            for w in works[q]:
+                w.wait()
+            e.gat_fwd_slice(self.csr, tables, q, s1, s2, stats, heads, d_head, alpha, act, Y)
+        return Y, (tables, s1, s2, stats, Y, H)
+
+    def gat_staged_backward(self, saved, dY, a_all, heads, d_head, alpha, act, need_da):
+        """Backward of gat_staged_forward: the source pass slice by slice over every KG row,
+        each slice's dH partial reduce-scattered as soon as it is computed (the next slice
+        computing while it moves); the edge pass's ds2 partials reduce-scattered too (tiny), so
+        the owners add ds1 (x) a1 + ds2 (x) a2 to their rows; da from the own rows only."""
+        from . import exchange
+        tables, s1, s2, stats, Y, H = saved
+        e = self.engine
+        D = heads * d_head
+        a = a_all.detach()
+        Gs, rec = e.gat_bwd_prep(dY, Y, s1, stats, heads, d_head, act)
+        csrT = e.transpose(self.csr)
+        S = tables.shape[0]
+        bufs = e.gat_bwd_buffers(csrT, S, heads, self.part.n_cols, Y.dtype, Y.device)
+        out = torch.empty((S, self.part.n_rows, tables.shape[2]), dtype=Y.dtype,
+                          device=Y.device)
+        ranks, li, other = self._peers()
+        pend = []
+        for q in range(S):
+            P = e.gat_bwd_src_slice(csrT, tables, q, s2, rec, Gs, bufs, heads, d_head, alpha,
+                                    q == 0)
+            pend.append(exchange.reduce_scatter_start(P, self.group, ranks, li, other,
+                                                      out=out[q]))
+        dzT, ds2 = e.gat_bwd_edge(csrT, s2, rec, bufs, a, heads, d_head, alpha)
+        ds2_own = self.reduce_scatter(ds2)
+        for p in pend:
+            p.finish()
+        dH = e.unpack64(out, D)
+        ds1 = e.gat_bwd_dst(self.csr, dzT, a, ds2_own, dH, heads, d_head)
+        da = None
+        if need_da:
+            p1 = e.gat_da(H, ds1, heads, d_head)
+            p2 = e.gat_da(H, ds2_own, heads, d_head)
+            da = torch.cat([p1.view(heads, d_head), p2.view(heads, d_head)], dim=1)
+        return dH, da
 
     def gather_rows(self, out_loc):
         """[2n, D] embeddings of both KGs in global entity order, on every rank."""
@@ -450,11 +662,18 @@ class HaloGATFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, H, a_all, dadj, heads, d_head, alpha, act):
+        ctx.dadj = dadj
+        ctx.meta = (heads, d_head, float(alpha), int(act))
+        ctx.staged = dadj.staged_gat(heads, d_head) and H.shape[1] == heads * d_head
+        if ctx.staged:  # per-slice exchange / aggregation (§8e overlap)
+            Y, ctx.saved = dadj.gat_staged_forward(H.contiguous(), a_all, heads, d_head, alpha,
+                                                   act)
+            ctx.a_all = a_all.detach()
+            return Y
         full, _ = dadj.halo(H)
         row0 = dadj.part.row0 if dadj.part.g > 1 else 0
         Y, saved = dadj.engine.gat_fwd(dadj.csr, full, a_all, heads, d_head, alpha, act, row0)
-        ctx.dadj, ctx.row0 = dadj, row0
-        ctx.meta = (heads, d_head, float(alpha), int(act))
+        ctx.row0 = row0
         ctx.saved = saved
         return Y
 
@@ -462,6 +681,11 @@ class HaloGATFn(torch.autograd.Function):
     def backward(ctx, dY):
         heads, d_head, alpha, act = ctx.meta
         dadj = ctx.dadj
+        if ctx.staged:
+            dH, da = dadj.gat_staged_backward(ctx.saved, dY.contiguous(), ctx.a_all, heads,
+                                              d_head, alpha, act, ctx.needs_input_grad[1])
+            ctx.saved = None
+            return dH, da, None, None, None, None, None
         dH, da = dadj.engine.gat_bwd(dadj.csr, ctx.saved, dY.contiguous(), heads, d_head, alpha,
                                      act, ctx.row0, ctx.needs_input_grad[1])
         ctx.saved = None

@@ -166,6 +166,28 @@ class MarginLossFn(torch.autograd.Function):
         return grad, None, None, None, None, None, None, None, None
 
 
+def grad_from_multipliers(X, idx, m, t, k, g):
+    """d loss / d X of the margin loss for given term multipliers m [2tk + t] (the forward's
+    format: negatives of side 1, of side 2, then the pairs), scaled by g / (2tk): the row-gather
+    backward kernel (any D; X may be a column block of the embedding, the column-sharded loss of
+    gnnea.dist_loss)."""
+    left, right, nl1, nr1, nl2, nr2 = idx
+    X = X if X.stride(1) == 1 else X.contiguous()
+    N, D = X.shape
+    inc = incidence(tuple(idx), N)
+    grad = torch.zeros((N, D), dtype=torch.float32, device=X.device)
+    scratch = torch.empty((max(inc.n_slots, 1), D), dtype=torch.float32, device=X.device)
+    g = g.reshape(1).to(device=X.device, dtype=torch.float32).contiguous()
+    m = m.to(torch.float32).contiguous()
+    with _lib.on_device(X.device):
+        check(_lib.lib().gnnea_margin_bwd_f32(
+            ptr(X), X.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1), ptr(nl2),
+            ptr(nr2), ptr(m), ptr(inc.csr.col), ptr(inc.items), inc.items.shape[0],
+            ptr(inc.long_rows), ptr(inc.long_ptr), inc.long_rows.numel(), ptr(scratch), ptr(g),
+            1.0 / (2.0 * t * k), ptr(grad), D, stream_of(X.device)))
+    return grad
+
+
 def margin_loss(outputs, left, right, neg_left, neg_right, neg2_left, neg2_right, t, k,
                 checked=False):
     """Index arrays may be numpy (int or the reference's float64 np.ones products) or tensors;

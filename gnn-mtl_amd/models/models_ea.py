@@ -13,6 +13,8 @@ import torch
 import torch.nn as nn
 
 from gnnea import l1, margin
+from gnnea.dist_graph import DistAdj
+from gnnea.dist_loss import sharded_margin_loss
 from models.decoders import model2decoder
 from models.encoders import model2encoder
 from utils.eval_utils import get_hits
@@ -107,6 +109,9 @@ class EAModel(BaseModel):
         self.neg2_left = None
 
     def encode(self, x, adj):
+        # a row-sharded adjacency of several ranks (gnnea.dist_graph.DistAdj): get_loss then
+        # evaluates the loss column-sharded on the rank's output rows (gnnea.dist_loss)
+        self._dadj = adj if isinstance(adj, DistAdj) and adj.part.world > 1 else None
         return self.encoder.encode(x, adj)
 
     def decode(self, h, adj):
@@ -114,6 +119,11 @@ class EAModel(BaseModel):
 
     def get_loss(self, outputs, data, split):
         ILL = data[split]
+        dadj = getattr(self, "_dadj", None)
+        if dadj is not None and outputs.shape[0] == dadj.part.n_rows:
+            return sharded_margin_loss(outputs, dadj, ILL[:, 0], ILL[:, 1], self.neg_left,
+                                       self.neg_right, self.neg2_left, self.neg2_right, len(ILL),
+                                       self.neg_num)
         return margin_loss(outputs, ILL[:, 0], ILL[:, 1], self.neg_left, self.neg_right,
                            self.neg2_left, self.neg2_right, len(ILL), self.neg_num)
 

@@ -571,6 +571,19 @@ int gnnea_sinkhorn_shard_finish(const gnnea_sinkhorn* prob, void* plan, int plan
 /* keys[q*ldk + x] = (float) L1(Q[q], X[x])   (nq x nx; monotone rounding of the exact value) */
 int gnnea_l1_keys_f32(const float* Q, int64_t ldq, int32_t nq, const float* X, int64_t ldx,
                       int32_t nx, int32_t D, float* keys, int64_t ldk, void* stream);
+/* out[j] = sum_d |X[a[j]][d] - X[b[j]][d]| in fp64, j < n (row indices int64, in range: the
+ * caller checks).  The per-term partial distances of the column-sharded EA margin loss: every
+ * rank sums its column block, one all-reduce of the n partials gives the distances
+ * (models/models_ea.py:103-123 over a row-sharded embedding, gnnea/dist_loss.py). */
+int gnnea_l1_terms_f32(const float* X, int64_t ldx, int32_t D, int64_t n, const int64_t* a,
+                       const int64_t* b, double* out, void* stream);
+/* Bandwidth anchors of the bench (csrc/ubench.hip; measurement aids, no reference call):
+ *   gnnea_ub_copy:   dst = src, bytes % 16 == 0, 16-B aligned, `blocks` workgroups of 256 striding;
+ *   gnnea_ub_gather: reads the rows idx[0..n) of a row-major table (row_bytes % 8 == 0, <= 2 KB)
+ *                    as 8-B chunks, writes one value per 64 rows to out[(n + 63) / 64]. */
+int gnnea_ub_copy(const void* src, void* dst, int64_t bytes, int32_t blocks, void* stream);
+int gnnea_ub_gather(const void* table, int64_t row_bytes, const int32_t* idx, int64_t n,
+                    float* out, void* stream);
 /* out[i] = L1(A[i], B[i]) in fp64 (the diagonal of cdist(A, B)) */
 int gnnea_l1_pairs_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int32_t n,
                        int32_t D, double* out, void* stream);

@@ -128,6 +128,117 @@ class CpuEngine:
         y = torch.cat(outs, 1)
         return torch.relu(y) if act == 1 else y
 
+    # ---- staged GAT halo (DistAdj.gat_staged_*): the same stages in fp64 torch ----------
+    GW = 8  # GAT slice width: D = 12 = slices of 8 + 4, slice 0 holds heads 0 and 1
+
+    def gat_slice_w(self, dtype):
+        return self.GW
+
+    def gat_staged_ok(self, heads, d_head):
+        return True
+
+    def gat_pack(self, x, tables, row0):
+        S, _, W = tables.shape
+        for q in range(S):
+            c0, c1 = q * W, min(x.shape[1], (q + 1) * W)
+            tables[q, row0:row0 + x.shape[0], :c1 - c0] = x[:, c0:c1]
+        return tables
+
+    @staticmethod
+    def _heads(H, heads, dh):
+        return H.reshape(H.shape[0], heads, dh)
+
+    def gat_scores(self, H, a, heads, dh):
+        Hh = self._heads(H, heads, dh)
+        return (Hh * a[:, :dh]).sum(-1), (Hh * a[:, dh:]).sum(-1)
+
+    def gat_rowstats(self, A, s1, s2, heads, dh, alpha):
+        i, j = A.indices()
+        sc = -torch.nn.functional.leaky_relu(s1[i] + s2[j], alpha)
+        m = torch.full((A.shape[0], heads), -float("inf"), dtype=s1.dtype)
+        m = m.scatter_reduce(0, i[:, None].expand(-1, heads), sc, "amax")
+        w = torch.exp(sc - m[i])
+        den = torch.zeros((A.shape[0], heads), dtype=s1.dtype).index_add(0, i, w)
+        return m, den, w
+
+    def gat_fwd_slice(self, A, tables, q, s1, s2, stats, heads, dh, alpha, act, Y):
+        _, den, w = stats
+        i, j = A.indices()
+        W = tables.shape[2]
+        c0, c1 = q * W, min(heads * dh, (q + 1) * W)
+        hc = torch.arange(c0, c1) // dh
+        num = torch.zeros((A.shape[0], c1 - c0), dtype=Y.dtype).index_add(
+            0, i, w[:, hc] * tables[q][j, :c1 - c0])
+        y = num / den[:, hc]
+        Y[:, c0:c1] = torch.relu(y) if act == 1 else y
+        return Y
+
+    def gat_bwd_prep(self, dY, Y, s1, stats, heads, dh, act):
+        m, den, _ = stats
+        G = dY * (Y > 0) if act == 1 else dY.clone()
+        c = self._heads(G * Y, heads, dh).sum(-1)
+        return self._slices_w(G, self.GW), (s1, m, den, c)
+
+    def _slices_w(self, x, W):
+        S = (x.shape[1] + W - 1) // W
+        t = torch.zeros((S, x.shape[0], W), dtype=x.dtype)
+        for q in range(S):
+            c0, c1 = q * W, min(x.shape[1], (q + 1) * W)
+            t[q, :, :c1 - c0] = x[:, c0:c1]
+        return t
+
+    def gat_bwd_buffers(self, AT, S, heads, n_src, dtype, device):
+        return {"pd": torch.zeros((S, AT._nnz(), heads), dtype=dtype),
+                "P": torch.zeros((S, n_src, self.GW), dtype=dtype)}
+
+    def _alpha(self, AT, s2, rec, alpha):
+        s1, m, den, _ = rec
+        j, i = AT.indices()
+        z = s1[i] + s2[j]
+        return z, torch.exp(-torch.nn.functional.leaky_relu(z, alpha) - m[i]) / den[i]
+
+    def gat_bwd_src_slice(self, AT, tables, q, s2, rec, Gs, bufs, heads, dh, alpha, weights):
+        j, i = AT.indices()
+        _, al = self._alpha(AT, s2, rec, alpha)
+        W = tables.shape[2]
+        c0, c1 = q * W, min(heads * dh, (q + 1) * W)
+        hc = torch.arange(c0, c1) // dh
+        G = Gs[q][i, :c1 - c0]
+        Hj = tables[q][j, :c1 - c0]
+        P = bufs["P"]
+        P[q].zero_()
+        P[q][:, :c1 - c0] = torch.zeros((AT.shape[0], c1 - c0), dtype=G.dtype).index_add(
+            0, j, al[:, hc] * G)
+        bufs["pd"][q] = torch.zeros((AT._nnz(), heads), dtype=G.dtype).index_add(
+            1, hc, G * Hj)
+        return P[q]
+
+    def gat_bwd_edge(self, AT, s2, rec, bufs, a, heads, dh, alpha):
+        j, i = AT.indices()
+        z, al = self._alpha(AT, s2, rec, alpha)
+        da = bufs["pd"].sum(0)
+        dz = -(al * (da - rec[3][i])) * torch.where(z > 0, z.new_tensor(1.0), z.new_tensor(alpha))
+        ds2 = torch.zeros((AT.shape[0], heads), dtype=dz.dtype).index_add(0, j, dz)
+        return dz, ds2
+
+    def gat_bwd_dst(self, A, dzT, a, ds2, dH, heads, dh):
+        AT = A.t().coalesce()
+        ds1 = torch.zeros((A.shape[0], heads), dtype=dzT.dtype).index_add(0, AT.indices()[1],
+                                                                           dzT)
+        upd = ds1[:, :, None] * a[None, :, :dh] + ds2[:, :, None] * a[None, :, dh:]
+        dH += upd.reshape(dH.shape)
+        return ds1
+
+    def gat_da(self, H, ds, heads, dh):
+        return (ds[:, :, None] * self._heads(H, heads, dh)).sum(0).reshape(-1)
+
+    def transpose(self, A):
+        return A.t().coalesce()
+
+    def unpack64(self, Ts, D):
+        S, n, W = Ts.shape
+        return Ts.permute(1, 0, 2).reshape(n, S * W)[:, :D]
+
     def gat_fwd(self, A, H, a_all, heads, dh, alpha, act, row0):
         Hd = H.detach().clone().requires_grad_(True)
         ad = a_all.detach().clone().requires_grad_(True)
@@ -139,6 +250,43 @@ class CpuEngine:
         Hd, ad, y = saved
         gH, ga = torch.autograd.grad(y, (Hd, ad), dY)
         return gH, (ga if need_da else None)
+
+
+class CpuLossEngine:
+    """fp64 torch double of gnnea.dist_loss.HipLossEngine (test stand-in, never shipped)."""
+
+    def l1_terms(self, X, a, b):
+        return (X[a] - X[b]).abs().sum(1).double()
+
+    def margin_grad(self, X, idx, m, t, k, g):
+        left, right, nl1, nr1, nl2, nr2 = idx
+        a, b = torch.cat([nl1, nl2, left]), torch.cat([nr1, nr2, right])
+        s = torch.sign(X[a] - X[b])
+        coef = (m.to(X.dtype) * g.to(X.dtype) / (2.0 * t * k))[:, None]
+        grad = torch.zeros_like(X)
+        grad.index_add_(0, a, coef * s)
+        grad.index_add_(0, b, -coef * s)
+        return grad
+
+
+def _ref_margin(out, left, right, nl1, nr1, nl2, nr2, t, k):
+    """models/models_ea.py:103-123 on the whole embedding (torch ops)."""
+    A = (out[left] - out[right]).abs().sum(1)
+    B1 = (out[nl1] - out[nr1]).abs().sum(1).view(t, k)
+    B2 = (out[nl2] - out[nr2]).abs().sum(1).view(t, k)
+    D_ = (A + 1.0).view(t, 1)
+    return (torch.relu(D_ - B1).sum() + torch.relu(D_ - B2).sum()) / (2.0 * t * k)
+
+
+def _loss_indices(n_kg, t=10, k=5):
+    rng = np.random.default_rng(3)
+    left = rng.choice(n_kg, t, replace=False)
+    right = n_kg + rng.choice(n_kg, t, replace=False)
+    nl1 = np.repeat(left, k)
+    nr1 = rng.integers(0, 2 * n_kg, t * k)
+    nl2 = rng.integers(0, 2 * n_kg, t * k)
+    nr2 = np.repeat(right, k)
+    return [left, right, nl1, nr1, nl2, nr2], t, k
 
 
 def _worker(rank, world, port, mode, q, staged=True):
@@ -196,6 +344,55 @@ def _worker(rank, world, port, mode, q, staged=True):
                     return g2(g1((x, adj_full)))[0]
                 return adj.gather_rows(g2(g1((x, adj)))[0])
             tol = 1e-4
+        elif mode == "loss_cpu":
+            # the column-sharded EA margin loss (gnnea.dist_loss) on a GCN + HighWay shard
+            # against the reference loss on the whole graph's output
+            from gnnea.dist_loss import sharded_margin_loss
+            dev = torch.device("cpu")
+            dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev, engine=CpuEngine())
+            torch.manual_seed(0)
+            W1, b1 = torch.randn(D, D, dtype=torch.float64), torch.randn(D, dtype=torch.float64)
+            Kg = torch.randn(D, D, dtype=torch.float64)
+            params = [p.requires_grad_() for p in (W1, b1, Kg)]
+            idx, t_, k_ = _loss_indices(N_KG)
+
+            def model(x, adj):
+                h1 = x @ W1.t() + b1
+                if adj is None:
+                    A = torch.sparse_coo_tensor(torch.from_numpy(np.stack([R, C])).long(),
+                                                torch.from_numpy(V).double(),
+                                                (2 * N_KG, 2 * N_KG))
+                    y1 = torch.relu(torch.sparse.mm(A, h1))
+                    g = torch.sigmoid(y1 @ Kg)
+                    y2 = g * torch.relu(torch.sparse.mm(A, y1 @ W1.t())) + (1 - g) * y1
+                    ti = [torch.from_numpy(np.asarray(a)) for a in idx]
+                    return _ref_margin(y2, *ti, t_, k_)
+                y1 = adj.aggregate(h1, F.relu)
+                y2 = adj.highway(y1 @ W1.t(), y1 @ Kg, y1, None, F.relu)
+                return sharded_margin_loss(y2, adj, *idx, t_, k_, engine=CpuLossEngine())
+            tol = 1e-12
+        elif mode == "loss_gpu":
+            # the column-sharded loss on the HIP kernels (gnnea_l1_terms_f32, the multiplier
+            # backward) against the gathered loss of the single-GPU kernels (gnnea.margin)
+            from layers.layers import GraphConvolution
+            from gnnea.dist_loss import sharded_margin_loss
+            from gnnea.margin import margin_loss
+            dev = torch.device("cuda:0")
+            torch.cuda.set_device(dev)
+            X = X.float().to(dev)
+            dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev)
+            torch.manual_seed(0)
+            l1 = GraphConvolution(D, D, 0.0, F.relu, True).to(dev)
+            params = list(l1.parameters())
+            adj_full = torch.sparse_coo_tensor(torch.from_numpy(np.stack([R, C])).long(),
+                                               torch.from_numpy(V), (2 * N_KG, 2 * N_KG)).to(dev)
+            idx, t_, k_ = _loss_indices(N_KG)
+
+            def model(x, adj):
+                if adj is None:
+                    return margin_loss(l1((x, adj_full))[0], *idx, t_, k_)
+                return sharded_margin_loss(l1((x, adj))[0], adj, *idx, t_, k_)
+            tol = 1e-5
         elif mode == "cpu":
             dev = torch.device("cpu")
             dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev, engine=CpuEngine())
@@ -251,7 +448,7 @@ def _worker(rank, world, port, mode, q, staged=True):
         # single process, whole graph
         xr = X.clone().requires_grad_()
         out_ref = model(xr, None)
-        (out_ref * Rw).sum().backward()
+        (out_ref if out_ref.dim() == 0 else (out_ref * Rw).sum()).backward()
         g_ref = [p.grad.clone() for p in params]
         for p in params:
             p.grad = None
@@ -259,7 +456,7 @@ def _worker(rank, world, port, mode, q, staged=True):
         p0 = dadj.part.global_row0
         xl = X[p0:p0 + dadj.part.n_rows].clone().requires_grad_()
         out = model(xl, dadj)
-        (out * Rw).sum().backward()
+        (out if out.dim() == 0 else (out * Rw).sum()).backward()
         allreduce_grads(params)
 
         def rel(a, b):
@@ -306,15 +503,39 @@ def test_dist_layers_rehearsal_on_device(device, world, staged):
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_dist_gat_gloo_cpu(world):
-    """Row-sharded GAT (DistAdj.gat / HaloGATFn): halo all-gather of H, reduce-scatter of the
-    dH partials over every KG row, da partials summed by allreduce_grads."""
-    _run(world, "gat_cpu")
+def test_dist_margin_loss_gloo_cpu(world):
+    """Column-sharded EA margin loss (gnnea.dist_loss: all-to-all to column blocks, one
+    all-reduce of the per-term partial distances, reverse all-to-all of the gradient): loss,
+    input and parameter gradients equal the reference loss on the whole graph's output."""
+    _run(world, "loss_cpu")
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 4])
-def test_dist_gat_rehearsal_on_device(device, world):
+def test_dist_margin_loss_rehearsal_on_device(device, world):
+    _run(world, "loss_gpu")
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_dist_gat_gloo_cpu(world):
+    """Row-sharded GAT (DistAdj.gat / HaloGATFn): at world >= 4 the staged halo (s2 of every
+    KG row first, 64-column slices of H exchanged and aggregated one after another, the
+    backward's per-slice dH partials reduce-scattered as each is computed, ds2 reduce-scattered,
+    da from the own rows), at world 2 nothing to exchange; da partials summed by
+    allreduce_grads."""
+    _run(world, "gat_cpu")
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_dist_gat_gloo_cpu_unstaged(world):
+    """GNNEA_HALO_STAGED=0: the whole H halo, one aggregation, one blocking reduce-scatter."""
+    _run(world, "gat_cpu", staged=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,staged", [(2, True), (4, True), (4, False)])
+def test_dist_gat_rehearsal_on_device(device, world, staged):
     """The drop-in GraphAttentionLayer handed a DistAdj, on the HIP GAT kernels (row offset of
-    the shard's logits and dH), against the same layers on the whole adjacency."""
-    _run(world, "gat_gpu")
+    the shard's logits and dH), against the same layers on the whole adjacency; world 4 with the
+    staged halo (gnnea_gat_fwd_sliced_range / gnnea_gat_bwd_src_sliced_range) and without."""
+    _run(world, "gat_gpu", staged)
