@@ -542,13 +542,21 @@ def main():
         from gnnea import exchange as ex
         ranks = part.group_ranks(part.kg)
 
-        tables = shard.halo_tables(Dl)
+        if ex.STAGED:
+            tables = shard.halo_tables(Dl)
 
-        def xchg():  # the same per-slice exchanges as the step, without the aggregation
-            for ws in ex.all_gather_slices(list(tables), part.row0, part.n_rows, shard.group,
-                                           ranks, part.li, other=part.other_ranks()):
-                for w in ws:
-                    w.wait()
+            def xchg():  # the same per-slice exchanges as the step, without the aggregation
+                for ws in ex.all_gather_slices(list(tables), part.row0, part.n_rows,
+                                               shard.group, ranks, part.li,
+                                               other=part.other_ranks()):
+                    for w in ws:
+                        w.wait()
+        else:
+            full = torch.empty((shard.n_cols, Dl), dtype=h_local.dtype, device=device)
+
+            def xchg():  # the step's whole-halo exchange, without the aggregation
+                ex.all_gather(h_local, full, shard.group, ranks, part.li, copy_own=True,
+                              other=part.other_ranks())
         for _ in range(2):
             xchg()
         torch.cuda.synchronize()
@@ -573,8 +581,10 @@ def main():
                     # SURVEY §8e overlap: the exchange and the aggregation cut into column
                     # slices, slice q aggregated while slices > q move; the hidden fraction of
                     # the exchange = (exchange alone + aggregation - step) / exchange alone
-                    "pipeline": "%d column slices (64 fp32 columns; slice-major KG tables)"
-                                % n_slices,
+                    "pipeline": ("%d column slices (64 fp32 columns; slice-major KG tables)"
+                                 % n_slices) if ex.STAGED else
+                                "none (GNNEA_HALO_STAGED=0: the whole halo, then the "
+                                "aggregation)",
                     "step_ms": round(ms_per_step, 4),
                     "exchange_hidden_frac": round(min(1.0, max(0.0, (x_ms + kernel_ms
                                                                      - ms_per_step) / x_ms)), 3)}
@@ -657,9 +667,13 @@ def main():
                        ("2 KG groups of %d GPUs, %d row blocks x %d feature-column slices "
                         "(aggregation only, no exchange)" % (shard.g, part.gr, part.gc) if free
                         else ("2 KG groups (one KG per GPU, nothing to exchange)" if shard.g == 1
-                              else "2 KG groups of %d GPUs, row blocks + per-column-slice halo "
-                                   "exchange (relayed peer transfers) pipelined with the "
-                                   "per-slice aggregation, inside the timed step" % shard.g))},
+                              else ("2 KG groups of %d GPUs, row blocks + per-column-slice halo "
+                                    "exchange (relayed peer transfers) pipelined with the "
+                                    "per-slice aggregation, inside the timed step" % shard.g)
+                              if _ex.STAGED else
+                              ("2 KG groups of %d GPUs, row blocks + the whole halo exchange "
+                               "(relayed peer transfers), then the aggregation, inside the "
+                               "timed step" % shard.g)))},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_bytes, "traffic_source": pmc_src,

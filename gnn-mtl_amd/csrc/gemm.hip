@@ -796,14 +796,15 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
       ah = __builtin_bit_cast(bf16x8_t, x0);
       am = __builtin_bit_cast(bf16x8_t, x1);
       al = ah;
-    } else
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bf16_t h, m, l;
-      split3(xa[j], h, m, l);
-      ah[j] = __builtin_bit_cast(__bf16, h);
-      am[j] = __builtin_bit_cast(__bf16, m);
-      al[j] = __builtin_bit_cast(__bf16, l);
+    } else {  // pairwise (common.h x3_split_pair: split3's values, half the instructions)
+      uint4 h4, m4, l4;
+      x3_split_pair(xa[0], xa[1], h4.x, m4.x, l4.x);
+      x3_split_pair(xa[2], xa[3], h4.y, m4.y, l4.y);
+      x3_split_pair(xa[4], xa[5], h4.z, m4.z, l4.z);
+      x3_split_pair(xa[6], xa[7], h4.w, m4.w, l4.w);
+      ah = __builtin_bit_cast(bf16x8_t, h4);
+      am = __builtin_bit_cast(bf16x8_t, m4);
+      al = __builtin_bit_cast(bf16x8_t, l4);
     }
     // the wave's column tiles in NH halves of TH (a 320-wide wave tile keeps 160 accumulator
     // registers; its B fragments are read half by half, the second half's reads in flight
@@ -1060,24 +1061,6 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
       ws_bytes >= gemm_x3w_ws_bytes(N))
     return gemm_x3w_launch(trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, cs, C2, cs2, ws,
                            ws_bytes, (hipStream_t)stream, beta);
-  // K in (576, 640] (the HighWay input gradient [dh | dgate]·[W ; K_gᵀ], K = 600): two
-  // weight-resident launches over the k halves, the second accumulating into C (beta = 1); the
-  // packing of the second half's weight tiles waits for the first launch on the stream
-  {
-    const int64_t K1 = (K / 2 + 3) / 4 * 4;
-    if (B && K1 < K && (cs == 64 ? ldc >= N : (ldc >= 64 && cs >= M * ldc)) &&
-        (trans_b ? ldb >= K : ldb >= N) &&
-        gemm_x3w_applies(trans_a, M, N, K1, lda, A, beta, ldc, cs, C, nullptr, 0) &&
-        gemm_x3w_applies(trans_a, M, N, K - K1, lda, A + K1, 1.f, ldc, cs, C, C2, cs2) && ws &&
-        ws_bytes >= gemm_x3w_ws_bytes(N)) {
-      const int rc = gemm_x3w_launch(trans_b, M, N, K1, A, lda, B, ldb, bias, C, ldc, cs,
-                                     nullptr, 0, ws, ws_bytes, (hipStream_t)stream, beta);
-      if (rc) return rc;
-      const float* B2 = trans_b ? B + K1 : B + K1 * ldb;
-      return gemm_x3w_launch(trans_b, M, N, K - K1, A + K1, lda, B2, ldb, nullptr, C, ldc, cs, C2,
-                             cs2, ws, ws_bytes, (hipStream_t)stream, 1.f);
-    }
-  }
   if (C2) {  // a slice-major copy as well: fused into k_gemm_x3p's epilogue, else packed after
     const bool lda_ok = !trans_a && lda % 4 == 0 && K % 4 == 0 && (((uintptr_t)A) & 15) == 0;
     const int64_t pb = x3_planes_bytes(N, K);

@@ -1,6 +1,5 @@
 // Weight-resident fp32 projection GEMM through the three-way bf16 split (gemm_x3w.hip): C = A·op(B)
-// (+ bias + beta·C) for tall A with K in (288, 320] (gemm.hip runs K in (576, 640] as two
-// launches, the second accumulating).  Internal to libgnnea (gemm.hip's gemm_x3 dispatches
+// (+ bias + beta·C) for tall A with K in (288, 320].  Internal to libgnnea (gemm.hip's gemm_x3 dispatches
 // to it; no C-ABI entry of its own).
 #pragma once
 #include <hip/hip_runtime.h>

@@ -1000,10 +1000,14 @@ static int res_launch(const gnnea_sinkhorn* p, int first, int count, hipStream_t
   SkArgs a = sk_args(p);
   SkDev d = sk_dev(p);
   ResGeom g = res_geom(p->I, p->J);
-  void* args[] = {&a, &d, &g, &first, &count};
-  // cooperative: the runtime rejects a grid that cannot be resident at once
-  GNNEA_HIP(hipLaunchCooperativeKernel((const void*)k_sk_res, dim3(g.P * g.Q), dim3(256), args, 0,
-                                       s));
+  // a plain launch of at most one workgroup per CU (res_applies).  Not hipLaunchCooperativeKernel:
+  // the HIP runtime then keeps a dedicated cooperative queue whose teardown at process exit
+  // crashed inside libhsa-runtime64 under rocprofv3's kernel tracing (the queue destroyed after
+  // the tool's finalisation).  Co-residency is not guaranteed by a plain launch when another
+  // stream holds CUs: every inter-workgroup wait is bounded (kResSpinTicks), a timed-out solve
+  // sets GNNEA_SK_ST_TIMEOUT and the host solves it again on the sweep path (gnnea/sinkhorn.py).
+  hipLaunchKernelGGL(k_sk_res, dim3(g.P * g.Q), dim3(256), 0, s, a, d, g, first, count);
+  GNNEA_LAUNCH_CHECK();
   return 0;
 }
 

@@ -35,7 +35,7 @@ class SinkhornResult:
 
 class SinkhornTimeout(RuntimeError):
     """A wait between the workgroups of the on-chip KNOPP kernel timed out (results invalid):
-    its cooperative grid was not all resident, e.g. because another stream's kernel (an RCCL
+    its persistent grid was not all resident, e.g. because another stream's kernel (an RCCL
     collective) held CUs.  solve() / solve_batch() re-run the problem on the sweep path."""
 
 
