@@ -270,10 +270,16 @@ def bf16_rate(device, steps):
     sliced = ops.use_sliced(shard.n_cols, D, torch.bfloat16)
     ms_row = _timed(lambda: ops.spmm(shard.csr, Hb, relu, out=Yb), steps)
     W = ops.slice_w(torch.bfloat16)
+    ms128 = None
     if sliced:
         Hs = ops.slice_pack(Hb)
-        ms = _timed(lambda: ops.spmm_sliced(shard.csr, Hs, D, relu, out=Yb), steps)
+        ms128 = _timed(lambda: ops.spmm_sliced(shard.csr, Hs, D, relu, out=Yb), steps)
         del Hs
+        # 64-column slices (128 B per row piece): one KG slice = n * 128 B = 256 MB at 2M rows
+        Hs = ops.slice_pack64(Hb)
+        ms = _timed(lambda: ops.spmm_sliced64(shard.csr, Hs, D, relu, out=Yb), steps)
+        del Hs
+        W = 64
     else:
         ms = ms_row
     traffic = gather_model_bytes(shard.n_rows, shard.nnz, D, elem=2)
@@ -286,9 +292,10 @@ def bf16_rate(device, steps):
            "layout": ("slice-major (%d-column slices: %d MB per KG slice)"
                       % (W, cf["n"] * W * 2 >> 20)) if sliced else "row-major",
            "rowmajor_edges_per_s": round(shard.nnz / ms_row * 1e3, 1),
+           "slices128_edges_per_s": round(shard.nnz / ms128 * 1e3, 1) if ms128 else None,
            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "kernel": ("gnnea::k_spmm_sliced<relu,4,bf16,bf16>" if sliced else
+                        "kernel": ("gnnea::k_spmm_sliced64_bf16<relu,4,bf16>" if sliced else
                                    "gnnea::k_spmm_v4<relu,act,2,bf16,bf16>"),
                         "launches_per_step": launches,
                         "model": "gather: 4(N+1)+8E+2ED+2ND"}}

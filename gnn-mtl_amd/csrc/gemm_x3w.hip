@@ -427,9 +427,147 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
   }
 }
 
+// Two 16-row fragments per wave (GNNEA_X3W=3, A/B): every weight fragment read from LDS feeds
+// 12 MFMAs (two independent accumulator chains, interleaved) instead of 6, halving the LDS reads
+// per MFMA; the activation ring holds 5 steps of both fragments (a prefetch distance of half a
+// tile: 80 registers, as the one-fragment ring), refilled with step s + 5 -- the next tile's
+// step s - 5 past the tile's end -- as soon as step s has been split.  256-row tiles.
+__global__ __launch_bounds__(512) void k_gemm_x3w_ring2(int M, int N, int K, int ntn,
+                                                        const float* __restrict__ A, int64_t lda,
+                                                        const bf16_t* __restrict__ P,
+                                                        const float* __restrict__ bias,
+                                                        float* __restrict__ C, int64_t ldc,
+                                                        int64_t cs, float* __restrict__ C2,
+                                                        int64_t cs2, float beta) {
+  constexpr int NW = 8, BM = 32 * NW, RS = 5;  // ring slots (steps in flight)
+  __shared__ __attribute__((aligned(16))) uint4 wl[3 * W3_PLANE];
+  __shared__ __attribute__((aligned(16))) float bsh[W3_NC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x;
+  const int nt = (b / 8) % ntn;
+  const int rs = (b / (8 * ntn)) * 8 + b % 8, nrs = (int)gridDim.x / ntn;
+  const int n0 = nt * W3_NC;
+  {
+    const uint4* src = (const uint4*)(P + (int64_t)nt * 3 * W3_PLANE * 8);
+    for (int i = tid; i < 3 * W3_PLANE; i += 64 * NW) wl[i] = src[i];
+    if (tid < W3_NC) bsh[tid] = bias && n0 + tid < N ? bias[n0 + tid] : 0.f;
+  }
+  __syncthreads();
+  const int tm = (M + BM - 1) / BM;
+  const int kq = lane >> 4, ml = lane & 15;
+  const uint4* wlane = wl + kq * W3_NC + ml;
+  uint4 f[RS][2][2];  // [slot][fragment][quad]
+  auto row_ptr = [&](int rt, int fr) {
+    return A + (int64_t)min(rt * BM + w * 32 + 16 * fr + ml, M - 1) * lda;
+  };
+  auto load_step = [&](const float* p0, const float* p1, int s, uint4 (&slot)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = 32 * s + 16 * j + 4 * kq;
+      const int ko = (s < W3_KC - 1 || k < K) ? k : 0;  // the last step's quads past K: clamped
+      slot[0][j] = *(const uint4*)(p0 + ko);
+      slot[1][j] = *(const uint4*)(p1 + ko);
+    }
+  };
+  auto split_step = [&](int s, const uint4 (&slot)[2][2], W3SplitP (&t)[2]) {
+#pragma unroll
+    for (int fr = 0; fr < 2; ++fr) {
+      uint4 q0 = slot[fr][0], q1 = slot[fr][1];
+      if (s == W3_KC - 1) {
+        const int k = 32 * s + 4 * kq;
+        if (k >= K) q0 = make_uint4(0u, 0u, 0u, 0u);
+        if (k + 16 >= K) q1 = make_uint4(0u, 0u, 0u, 0u);
+      }
+      const float x[8] = {__builtin_bit_cast(float, q0.x), __builtin_bit_cast(float, q0.y),
+                          __builtin_bit_cast(float, q0.z), __builtin_bit_cast(float, q0.w),
+                          __builtin_bit_cast(float, q1.x), __builtin_bit_cast(float, q1.y),
+                          __builtin_bit_cast(float, q1.z), __builtin_bit_cast(float, q1.w)};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        w3_split_pair<GNNEA_X3W_SPLIT>(x[2 * q], x[2 * q + 1], t[fr].h[q], t[fr].m[q], t[fr].l[q]);
+    }
+  };
+  if (rs < tm) {
+    const float* p0 = row_ptr(rs, 0);
+    const float* p1 = row_ptr(rs, 1);
+#pragma unroll
+    for (int s = 0; s < RS; ++s) load_step(p0, p1, s, f[s]);
+  }
+  for (int rt = rs; rt < tm; rt += nrs) {
+    const float* c0p = row_ptr(rt, 0);
+    const float* c1p = row_ptr(rt, 1);
+    const int rn = rt + nrs < tm ? rt + nrs : rt;  // past the end: valid rows, never used
+    const float* n0p = row_ptr(rn, 0);
+    const float* n1p = row_ptr(rn, 1);
+    w3_f32x4 acc[2][5];
+#pragma unroll
+    for (int fr = 0; fr < 2; ++fr)
+#pragma unroll
+      for (int j = 0; j < 5; ++j) acc[fr][j] = w3_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < W3_KC; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      W3SplitP a[2];
+      split_step(s, f[s % RS], a);
+      // refill the slot with step s + RS (this tile's, or the next tile's step s + RS - KC)
+      if (s + RS < W3_KC) load_step(c0p, c1p, s + RS, f[s % RS]);
+      else load_step(n0p, n1p, s + RS - W3_KC, f[s % RS]);
+      const w3_bf16x8 a0h = a[0].vh(), a0m = a[0].vm(), a0l = a[0].vl();
+      const w3_bf16x8 a1h = a[1].vh(), a1m = a[1].vm(), a1l = a[1].vl();
+      const uint4* wp = wlane + s * 4 * W3_NC;
+#pragma unroll
+      for (int jn = 0; jn < 5; ++jn) {
+        __builtin_amdgcn_sched_barrier(0);
+        const w3_bf16x8 wh = __builtin_bit_cast(w3_bf16x8, wp[16 * jn]);
+        const w3_bf16x8 wm = __builtin_bit_cast(w3_bf16x8, wp[W3_PLANE + 16 * jn]);
+        const w3_bf16x8 wlo = __builtin_bit_cast(w3_bf16x8, wp[2 * W3_PLANE + 16 * jn]);
+        w3_f32x4& c0 = acc[0][jn];
+        w3_f32x4& c1 = acc[1][jn];
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a0l, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a1l, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, a0m, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, a1m, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, a0h, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, a1h, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a0m, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a1m, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, a0h, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, a1h, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a0h, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a1h, c1, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int fr = 0; fr < 2; ++fr) {
+      const int m = rt * BM + w * 32 + 16 * fr + ml;
+      if (m >= M) continue;
+#pragma unroll
+      for (int jn = 0; jn < 5; ++jn) {
+        const int c = 16 * jn + 4 * kq;
+        int n = n0 + c;
+        asm volatile("" : "+v"(n));  // (as the ring: keep the column offsets out of LICM)
+        if (n < N) {
+          const float4 bv = *(const float4*)(bsh + c);
+          const w3_f32x4 a4 = acc[fr][jn];
+          float4 o = make_float4(a4[0] + bv.x, a4[1] + bv.y, a4[2] + bv.z, a4[3] + bv.w);
+          float4* cp = (float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63)));
+          if (beta != 0.f) {
+            const float4 cv = *cp;
+            o.x += beta * cv.x; o.y += beta * cv.y; o.z += beta * cv.z; o.w += beta * cv.w;
+          }
+          *cp = o;
+          if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
+        }
+      }
+    }
+  }
+}
+
 // ---- host side ----
 
-// A/B comparison only: GNNEA_X3W=0 k_gemm_x3p, 1 k_gemm_x3w, 2 (default) k_gemm_x3w_ring
+// A/B comparison only: GNNEA_X3W=0 k_gemm_x3p, 1 k_gemm_x3w, 2 (default) k_gemm_x3w_ring,
+// 3 k_gemm_x3w_ring2
 static int x3w_mode() {
   static const int mode = [] {
     const char* e = getenv("GNNEA_X3W");
@@ -446,7 +584,7 @@ int64_t gemm_x3w_ws_bytes(int64_t N) {
 bool gemm_x3w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda, const void* A,
                       float beta, int64_t ldc, int64_t cs, const void* C, const void* C2,
                       int64_t cs2) {
-  return x3w_on() && !trans_a && (beta == 0.f || x3w_mode() == 2) && A && C && M >= 65536 &&
+  return x3w_on() && !trans_a && (beta == 0.f || x3w_mode() >= 2) && A && C && M >= 65536 &&
          M < (1ll << 31) &&
          N >= 64 && N <= 4096 && N % 4 == 0 && K > 32 * (W3_KC - 1) && K <= 32 * W3_KC && K % 4 == 0 &&
          lda >= K && lda % 4 == 0 && (((uintptr_t)A) & 15) == 0 &&
@@ -477,13 +615,17 @@ int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A
     return n;
   }();
   // persistent grid: a multiple of 8 * ntn workgroups (column tiles of a row stream 8 apart)
-  const bool ring = x3w_mode() == 2;
+  const bool ring = x3w_mode() == 2, ring2 = x3w_mode() == 3;
   const int unit = 8 * ntn;
-  const int64_t tm = (M + (ring ? 128 : W3_BM) - 1) / (ring ? 128 : W3_BM);
+  const int bm = ring2 ? 256 : ring ? 128 : W3_BM;
+  const int64_t tm = (M + bm - 1) / bm;
   int grid = ncu / unit * unit;
   if (grid < unit) grid = unit;
   if ((int64_t)grid / ntn > tm) grid = (int)((tm + 7) / 8 * 8 * ntn);
-  if (ring)
+  if (ring2)
+    hipLaunchKernelGGL(k_gemm_x3w_ring2, dim3(grid), dim3(512), 0, s, (int)M, (int)N, (int)K,
+                       ntn, A, lda, P, bias, C, ldc, cs, C2, cs2, beta);
+  else if (ring)
     hipLaunchKernelGGL(k_gemm_x3w_ring, dim3(grid), dim3(512), 0, s, (int)M, (int)N, (int)K, ntn,
                        A, lda, P, bias, C, ldc, cs, C2, cs2, beta);
   else

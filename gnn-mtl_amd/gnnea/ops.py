@@ -496,6 +496,32 @@ def spmm_sliced(csr, xs, D, act=_lib.GNNEA_ACT_IDENTITY, out=None, out_dtype=Non
     return out
 
 
+def spmm_sliced64(csr, xs, D, act=_lib.GNNEA_ACT_IDENTITY, out=None, out_dtype=None):
+    """out = act(A @ X) for a bf16 X held in 64-column slices ([S, n_src, 64]: 128 B per row
+    piece, one cfg-5 KG slice = 256 MB; slice_pack64's layout), per diagonal (KG) block."""
+    _lib.require_device(xs)
+    if xs.dtype != torch.bfloat16:
+        raise TypeError("gnnea.spmm_sliced64: bf16 table required")
+    S = (D + 63) // 64
+    if xs.dim() != 3 or xs.shape[0] < S or xs.shape[2] != 64 or xs.shape[1] < csr.n_cols or \
+            not xs.is_contiguous():
+        raise ValueError("gnnea.spmm_sliced64: xs must be a contiguous [%d, >=%d, 64] table"
+                         % (S, csr.n_cols))
+    if out is None:
+        out = torch.empty((csr.n_rows, D), dtype=out_dtype or xs.dtype, device=xs.device)
+    if out.shape != (csr.n_rows, D) or out.stride(1) != 1 or out.dtype not in FEATURE_DTYPES:
+        raise ValueError("gnnea.spmm_sliced64: out must be [%d, %d]" % (csr.n_rows, D))
+    L = _lib.lib()
+    st = stream_of(xs.device)
+    yd = _lib.GNNEA_BF16 if out.dtype == torch.bfloat16 else _lib.GNNEA_F32
+    with _lib.on_device(xs.device):
+        for r0, r1 in csr.row_blocks():
+            check(L.gnnea_spmm_sliced64_bf16(_off32(csr.rowptr, r0), ptr(csr.col), ptr(csr.val),
+                                             r1 - r0, D, ptr(xs), xs.stride(0), _off(out, r0),
+                                             _ld(out), yd, int(act), st))
+    return out
+
+
 def gemm_sliced(x, weight, bias=None):
     """hidden = x W^T + b written slice-major (gnnea_gemm_sliced_{f32,bf16}): the projection of
     a GCN layer hands the aggregation its table at no extra pass.  bf16 operands give a bf16

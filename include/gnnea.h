@@ -99,6 +99,12 @@ int gnnea_spmm_sliced_bf16(const int32_t* rowptr, const int32_t* col, const floa
                            int64_t ldy, int y_dtype, int act, void* stream);
 int gnnea_slice_pack_bf16(const void* X, int64_t ldx, int64_t n, int32_t D, void* Xs,
                           int64_t sstride, void* stream);
+/* the same aggregation over 64-column bf16 slices (128 B per row piece, one cfg-5 KG slice =
+ * 256 MB, the Infinity Cache's size): the layout of gnnea_slice_pack64_bf16, element (r, c) at
+ * Xs[(c/64)*sstride + r*64 + c%64], sstride % 64 == 0, 8-B aligned Xs */
+int gnnea_spmm_sliced64_bf16(const int32_t* rowptr, const int32_t* col, const float* val,
+                             int32_t n_rows, int32_t D, const void* Xs, int64_t sstride, void* Y,
+                             int64_t ldy, int y_dtype, int act, void* stream);
 int gnnea_act_bwd_sliced_bf16(const void* dY, int64_t lddy, const void* Y, int64_t ldy,
                               int64_t n, int32_t D, int act, void* Gs, int64_t sstride,
                               void* stream);

@@ -55,6 +55,32 @@ def test_spmm_sliced_vs_oracle(device, D):
     assert torch.all(ops.spmm_sliced(csr, xs, D)[:4].cpu() == 0)
 
 
+@pytest.mark.parametrize("D", [4, 60, 68, 128, 132, 300])
+def test_spmm_sliced64_bf16_vs_oracle(device, D):
+    """bf16 over 64-column slices (gnnea_spmm_sliced64_bf16, 128-B row pieces): vs the fp64
+    oracle on the bf16-rounded table (fp32 sums, one bf16 rounding of the output: 1e-2; fp32
+    output 1e-4) and vs the 128-column bf16 kernel on the same table."""
+    from gnnea import ops
+    from oracle.gnn import coo_aggregate
+    rng = np.random.default_rng(D + 29)
+    n = 900
+    r, c, v, csr = _graph(rng, n, 8000, device)
+    x = torch.from_numpy(rng.standard_normal((n, D)).astype(np.float32)).to(device)
+    xb = x.to(torch.bfloat16)
+    xs = ops.slice_pack64(xb)
+    assert xs.shape == ((D + 63) // 64, n, 64)
+    for act, fn in ((0, lambda t: t), (1, torch.relu), (5, torch.tanh)):
+        ref = fn(coo_aggregate(r, c, v, n, xb.float().cpu().double()))
+        y32 = ops.spmm_sliced64(csr, xs, D, act, out_dtype=torch.float32).cpu()
+        assert rel_err(y32, ref) < TOL32, (D, act)
+        y16 = ops.spmm_sliced64(csr, xs, D, act).cpu()
+        assert y16.dtype == torch.bfloat16 and rel_err(y16.float(), ref) < 1e-2, (D, act)
+        if D % 4 == 0 and D >= 128:
+            y128 = ops.spmm_sliced(csr, ops.slice_pack(xb), D, act, out_dtype=torch.float32)
+            assert rel_err(y32, y128.cpu()) < TOL32
+    assert torch.all(ops.spmm_sliced64(csr, xs, D)[:4].float().cpu() == 0)
+
+
 def test_slice_pack_strided_and_rejects(device):
     from gnnea import ops
     big = torch.randn(333, 320, device=device)
@@ -437,6 +463,25 @@ def test_gemm_x3_dual_output(device, M, N, K, bias):
         for s in range(xs.shape[0]))
     ref64 = a.double() @ b.double() + (bb.double() if bias else 0)
     assert rel_err(y.cpu(), ref64.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K,bias", [(70001, 300, 300, True), (66000, 600, 300, False),
+                                        (65536, 128, 320, True)])
+def test_gemm_x3_tall_accumulate(device, M, N, K, bias):
+    """The weight-resident kernel (tall M, K in (288, 320]) with C = A·B + bias + C (beta = 1,
+    the epilogue reads C) against fp64."""
+    from gnnea import ops
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    a = torch.randn(M, K, generator=g).to(device)
+    b = torch.randn(K, N, generator=g).to(device)
+    bb = torch.randn(N, generator=g).to(device) if bias else None
+    c0 = torch.randn(M, N, generator=g).to(device)
+    y = ops.gemm(a, b, bias=bb, x3=True, out=c0.clone(), beta=1.0)
+    ref = c0.double() + a.double() @ b.double() + (bb.double() if bias else 0)
+    assert rel_err(y.cpu(), ref.cpu()) < 1e-5
+    y0 = ops.gemm(a, b, bias=bb, x3=True)
+    ref0 = a.double() @ b.double() + (bb.double() if bias else 0)
+    assert rel_err(y0.cpu(), ref0.cpu()) < 1e-5
 
 
 @pytest.mark.parametrize("heads,d_head,act,mask,row0", [

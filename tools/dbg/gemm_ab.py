@@ -1,6 +1,7 @@
 """A/B timing of the fp32 (x3) GEMM shapes of the EA step from alternative builds of the library
-(debug tool): python tools/dbg/gemm_ab.py libgnnea.so libgnnea_<variant>.so ...
-Each library is loaded in its own child process; median of 21 HIP-event timings per shape."""
+(debug tool): python tools/dbg/gemm_ab.py libgnnea.so libgnnea_<variant>.so libgnnea.so:GNNEA_X3W=3
+Each library (optionally with one environment setting) is loaded in its own child process;
+median of 21 HIP-event timings per shape."""
 import json
 import os
 import subprocess
@@ -54,9 +55,15 @@ print(json.dumps({sys.argv[1]: res}), flush=True)
 ''' % ROOT
 
 out = {}
-for lib in sys.argv[1:]:
+for spec in sys.argv[1:]:
+    lib, _, kv = spec.partition(":")
+    env = dict(os.environ)
+    if kv:
+        k, v = kv.split("=", 1)
+        env[k] = v
     r = subprocess.run([sys.executable, "-c", CHILD, lib], capture_output=True, text=True,
-                       timeout=300)
+                       timeout=300, env=env)
+    lib = spec
     sys.stderr.write(r.stderr[-2000:])
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     out.update(json.loads(line[-1]) if line else {lib: {"rc": r.returncode}})
