@@ -140,9 +140,11 @@ def sinkhorn_rate(device, B=3000, reg=0.01, n0=100, n1=1100, variant=None):
 
 
 def sinkhorn_large(device):
-    """B = 15000 through the default path (the scaling form with the fp64 K resident, one sweep
-    per iteration: I * J * 8 bytes of K per iteration) and through the log-domain passes (variant
-    1: fp32 C read twice per iteration, 2 * I * J * 4 bytes, exp-bound): marginal iters/s."""
+    """B = 15000 through the scaling form with the fp64 K resident (variant 0: one sweep per
+    iteration, I * J * 8 bytes of K) and through the log-domain path (variant 1): the fused
+    KNOPP sweep (fp32 C read once per iteration, I * J * 4 bytes, one exponential per element;
+    csrc/sinkhorn_log.hip k_lsk_sweep) and, beside it, the two-pass form it replaced
+    (GNNEA_SK_FUSED=0: C read twice, two exponentials per element): marginal iters/s."""
     B = 15000
     r = sinkhorn_rate(device, B=B, n0=20, n1=120)
     k_bytes = B * B * 8
@@ -152,10 +154,22 @@ def sinkhorn_large(device):
     r["bound"] = ("HBM: the K stream (%.2f GB per iteration; %.0f iters/s at 8 TB/s)"
                   % (k_bytes / 1e9, 8e12 / k_bytes))
     lg = sinkhorn_rate(device, B=B, n0=20, n1=120, variant=1)
-    c_bytes = 2 * B * B * 4
-    r["logdomain"] = {"iters_per_s": lg["iters_per_s"], "bytes_per_iter": c_bytes,
-                      "bound": "fp64 exp (VALU): 2 * I * J exponentials per iteration (the fp32 "
-                               "C stream alone would allow %.0f iters/s)" % (8e12 / c_bytes)}
+    c_bytes = B * B * 4
+    knopp = lg["iters_per_s"]["ot_loss.sinkhorn"]
+    r["logdomain"] = {
+        "iters_per_s": lg["iters_per_s"], "bytes_per_iter_knopp": c_bytes,
+        "GBps_knopp": round(knopp * c_bytes / 1e9, 1),
+        "kernels_knopp": "fused sweep k_lsk_sweep + k_lsk_colfin (one pass over fp32 C, one "
+                         "table exponential per element)",
+        "bound_knopp": "HBM: the fp32 C stream (%.2f GB per iteration; %.0f iters/s at 8 TB/s) "
+                       "against 2.25e8 fp64 exponentials per iteration" % (c_bytes / 1e9,
+                                                                             8e12 / c_bytes)}
+    os.environ["GNNEA_SK_FUSED"] = "0"
+    try:
+        two = sinkhorn_rate(device, B=B, n0=20, n1=120, variant=1)
+    finally:
+        os.environ.pop("GNNEA_SK_FUSED", None)
+    r["logdomain"]["two_pass_iters_per_s"] = two["iters_per_s"]
     return r
 
 
@@ -335,10 +349,27 @@ def anchors(device, copy_bytes=4 << 30, n_gather=16 << 20):
     src = torch.empty(copy_bytes // 4, dtype=torch.float32, device=device).fill_(1.0)
     dst = torch.empty_like(src)
     ncu = torch.cuda.get_device_properties(device).multi_processor_count
-    ms = _timed(lambda: _lib.check(L.gnnea_ub_copy(_lib.ptr(src), _lib.ptr(dst), copy_bytes,
-                                                   8 * ncu, st())), 21)
-    out["copy"] = {"GBps": round(2 * copy_bytes / (ms * 1e-3) / 1e9, 1), "ms": round(ms, 4),
-                   "bytes": 2 * copy_bytes, "kernel": "gnnea::k_ub_copy (16 B per lane)"}
+    # the copy (and its loads alone) over grids of 4 / 8 / 16 workgroups per CU, 4 or 8 accesses
+    # in flight, plain or nontemporal: the best of each is the anchor, the whole sweep is kept
+    sweep = {}
+    for ro in (0, _lib.GNNEA_UB_READ_ONLY):
+        for fl in (0, _lib.GNNEA_UB_NT, _lib.GNNEA_UB_DEEP, _lib.GNNEA_UB_NT | _lib.GNNEA_UB_DEEP):
+            for per_cu in (4, 8, 16):
+                f = ro | fl
+                ms = _timed(lambda: _lib.check(L.gnnea_ub_copy(_lib.ptr(src), _lib.ptr(dst),
+                                                               copy_bytes, per_cu * ncu, f,
+                                                               st())), 11)
+                moved = copy_bytes if ro else 2 * copy_bytes
+                sweep["%s%s%s/%dpercu" % ("read" if ro else "copy", "_nt" if fl & 1 else "",
+                                          "_deep" if fl & 2 else "", per_cu)] = round(
+                    moved / (ms * 1e-3) / 1e9, 1)
+    best_copy = max((k for k in sweep if k.startswith("copy")), key=sweep.get)
+    best_read = max((k for k in sweep if k.startswith("read")), key=sweep.get)
+    out["copy"] = {"GBps": sweep[best_copy], "config": best_copy, "bytes": 2 * copy_bytes,
+                   "kernel": "gnnea::k_ub_copy (16 B per lane)"}
+    out["read"] = {"GBps": sweep[best_read], "config": best_read, "bytes": copy_bytes,
+                   "kernel": "gnnea::k_ub_copy read only (16 B per lane)"}
+    out["copy_sweep_GBps"] = sweep
     ms_t = _timed(lambda: dst.copy_(src), 21)
     out["torch_copy"] = {"GBps": round(2 * copy_bytes / (ms_t * 1e-3) / 1e9, 1),
                          "ms": round(ms_t, 4)}

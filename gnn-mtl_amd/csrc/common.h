@@ -135,6 +135,12 @@ __device__ __forceinline__ float act_grad_from_out(float y) {
   else return 1.f - y * y;
 }
 
+// act_fwd<GNNEA_ACT_RELU> on four values (x > 0 ? x : 0, the library's relu everywhere)
+__device__ __forceinline__ float4 f4_relu(float4 v) {
+  return make_float4(v.x > 0.f ? v.x : 0.f, v.y > 0.f ? v.y : 0.f, v.z > 0.f ? v.z : 0.f,
+                     v.w > 0.f ? v.w : 0.f);
+}
+
 __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 acc) {
   acc.x = fmaf(a, x.x, acc.x);
   acc.y = fmaf(a, x.y, acc.y);

@@ -18,6 +18,7 @@
 #include "common.h"
 #include "gemm_ta.h"
 #include "gemm_x3w.h"
+#include "act.h"
 #include "lds_dma.h"
 
 namespace gnnea {
@@ -1052,15 +1053,23 @@ static bool x3_pipe_on() {
 static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
                    int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
                    float* C, int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, void* stream,
-                   float* C2 = nullptr, int64_t cs2 = 0) {
+                   float* C2 = nullptr, int64_t cs2 = 0, int act = GNNEA_ACT_IDENTITY) {
   if (C2 && (cs2 % 4 != 0 || cs2 < M * 64 || cs != 64)) return GNNEA_EINVAL;
   // the weight-resident form (gemm_x3w.hip) for the tall K <= 320 projections; it writes C2 too
+  // and applies a relu in its epilogue
   if (B && (cs == 64 ? ldc >= N : (ldc >= 64 && cs >= M * ldc)) &&
       (trans_b ? ldb >= K : ldb >= N) &&
-      gemm_x3w_applies(trans_a, M, N, K, lda, A, beta, ldc, cs, C, C2, cs2) && ws &&
+      gemm_x3w_applies(trans_a, M, N, K, lda, A, beta, ldc, cs, C, C2, cs2, act) && ws &&
       ws_bytes >= gemm_x3w_ws_bytes(N))
     return gemm_x3w_launch(trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, cs, C2, cs2, ws,
-                           ws_bytes, (hipStream_t)stream, beta);
+                           ws_bytes, (hipStream_t)stream, beta, act);
+  if (act != GNNEA_ACT_IDENTITY) {  // any other kernel: the product, then the act in place
+    if (C2 || cs != 64) return GNNEA_EINVAL;
+    const int rc = gemm_x3(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, ws,
+                           ws_bytes, stream);
+    if (rc) return rc;
+    return act_rows_f32(C, ldc, M, N, act, (hipStream_t)stream);
+  }
   if (C2) {  // a slice-major copy as well: fused into k_gemm_x3p's epilogue, else packed after
     const bool lda_ok = !trans_a && lda % 4 == 0 && K % 4 == 0 && (((uintptr_t)A) & 15) == 0;
     const int64_t pb = x3_planes_bytes(N, K);
@@ -1334,6 +1343,17 @@ extern "C" int gnnea_gemm_x3_f32(int trans_a, int trans_b, int64_t M, int64_t N,
                                  int64_t ws_bytes, void* stream) {
   return gemm_x3(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, 64, ws, ws_bytes,
                  stream);
+}
+
+// C = act(A·op(B) + bias): the Linear layer with its act (layers/layers.py:121-122); relu rides
+// the weight-resident ring's epilogue, any other (kernel, act) pair runs the act in place after
+extern "C" int gnnea_gemm_x3_act_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                                     const float* A, int64_t lda, const float* B, int64_t ldb,
+                                     const float* bias, int act, float* C, int64_t ldc, void* ws,
+                                     int64_t ws_bytes, void* stream) {
+  if (act < GNNEA_ACT_IDENTITY || act > GNNEA_ACT_TANH) return GNNEA_EINVAL;
+  return gemm_x3(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, 0.f, C, ldc, 64, ws, ws_bytes,
+                 stream, nullptr, 0, act);
 }
 
 // C row-major AND its slice-major copy C2s [ceil(N/64)][M][64] (slice stride sstride2) from one

@@ -15,6 +15,7 @@
 #include "common.h"
 #include "gemm_ta.h"
 #include "lds_dma.h"
+#include "act.h"
 
 #include <stdlib.h>
 
@@ -820,7 +821,8 @@ template <typename TC>
 static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                        const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
                        const float* bias, float beta, TC* C, int64_t ldc, void* ws,
-                       int64_t ws_bytes, hipStream_t s, int64_t cs = 128);
+                       int64_t ws_bytes, hipStream_t s, int64_t cs = 128,
+                       int act = GNNEA_ACT_IDENTITY);
 
 template <typename TC>
 static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t* A,
@@ -914,7 +916,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
                                                       const bf16_t* __restrict__ P,
                                                       const float* __restrict__ bias,
                                                       TC* __restrict__ C, int64_t ldc,
-                                                      int64_t cs) {
+                                                      int64_t cs, int relu) {
   __shared__ __attribute__((aligned(16))) uint4 wl[KC * 2 * kBwCols];  // [s][kh][n] x 16 B
   // the tile's bias in LDS: a global load in the epilogue would wait (vmcnt counts in order)
   // for the next tile's activation loads issued before it
@@ -994,6 +996,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
                                  acc[t][4 * g + 3]);
           const float4 bv = *(const float4*)(bsh + (n - n0));
           o.x += bv.x; o.y += bv.y; o.z += bv.z; o.w += bv.w;
+          if (relu) o = f4_relu(o);  // the Linear's act (layers/layers.py:121-122), uniform
           TC* c = C + c_index_bf(m, n, ldc, cs);
           if constexpr (std::is_same<TC, bf16_t>::value) {
             *(uint2*)c = make_uint2((uint32_t)f32_to_bf16(o.x) | ((uint32_t)f32_to_bf16(o.y) << 16),
@@ -1037,7 +1040,7 @@ static int64_t bf16w_planes_bytes(int64_t N, int64_t K) {
 template <typename TC>
 static int gemm_bf16w(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t* A,
                       int64_t lda, const bf16_t* B, int64_t ldb, const float* bias, TC* C,
-                      int64_t ldc, int64_t cs, void* ws, hipStream_t s) {
+                      int64_t ldc, int64_t cs, void* ws, hipStream_t s, int relu) {
   const int kc = bf16w_kc(K), ntn = (int)((N + kBwCols - 1) / kBwCols);
   bf16_t* P = (bf16_t*)ws;
   {
@@ -1062,10 +1065,10 @@ static int gemm_bf16w(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
   if ((int64_t)grid / ntn > tm) grid = (int)((tm + 7) / 8 * 8 * ntn);
   if (kc == 19)
     hipLaunchKernelGGL((k_gemm_bf16w<TC, 19>), dim3(grid), dim3(256), 0, s, (int)M, (int)N,
-                       (int)K, ntn, A, lda, P, bias, C, ldc, cs);
+                       (int)K, ntn, A, lda, P, bias, C, ldc, cs, relu);
   else
     hipLaunchKernelGGL((k_gemm_bf16w<TC, 20>), dim3(grid), dim3(256), 0, s, (int)M, (int)N,
-                       (int)K, ntn, A, lda, P, bias, C, ldc, cs);
+                       (int)K, ntn, A, lda, P, bias, C, ldc, cs, relu);
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
@@ -1074,12 +1077,22 @@ template <typename TC>
 static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                        const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
                        const float* bias, float beta, TC* C, int64_t ldc, void* ws,
-                       int64_t ws_bytes, hipStream_t s, int64_t cs) {
+                       int64_t ws_bytes, hipStream_t s, int64_t cs, int act) {
   // (beta != 0: the old C would be loaded behind the next tile's activations: k_gemm_bf16p)
   if (beta == 0.f && bf16w_applies(trans_a, M, N, K, lda, A) && ws &&
       ws_bytes >= bf16w_planes_bytes(N, K) && ldc % 4 == 0 && cs % 4 == 0 &&
-      (((uintptr_t)C) & (4 * sizeof(TC) - 1)) == 0)
-    return gemm_bf16w<TC>(trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, cs, ws, s);
+      (((uintptr_t)C) & (4 * sizeof(TC) - 1)) == 0 &&
+      (act == GNNEA_ACT_IDENTITY || act == GNNEA_ACT_RELU))
+    return gemm_bf16w<TC>(trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, cs, ws, s,
+                          act == GNNEA_ACT_RELU ? 1 : 0);
+  if (act != GNNEA_ACT_IDENTITY) {  // any other kernel: the product, then the act in place
+    if (cs != 128) return GNNEA_EINVAL;
+    const int rc = gemm_bf16_t<TC>(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc,
+                                   ws, ws_bytes, s, cs);
+    if (rc) return rc;
+    if constexpr (std::is_same<TC, bf16_t>::value) return act_rows_bf16(C, ldc, M, N, act, s);
+    else return act_rows_f32(C, ldc, M, N, act, s);
+  }
   if (bf16p_applies(trans_a, M, N, K, lda, A) && ws && ws_bytes >= bf16p_planes_bytes(N, K))
     return gemm_bf16p<TC>(trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, ws, s);
   const int wt = bf16_wt(N);
@@ -1156,6 +1169,32 @@ extern "C" int gnnea_gemm_bf16(int trans_a, int trans_b, int64_t M, int64_t N, i
     return gemm_bf16_t<float>(trans_a, trans_b, M, N, K, (const bf16_t*)A, lda,
                               (const bf16_t*)B, ldb, bias, beta, (float*)C, ldc, ws, ws_bytes,
                               s, 128);
+  return GNNEA_EINVAL;
+}
+
+// C = act(A·op(B) + bias) (the Linear layer with its act, layers/layers.py:121-122): relu rides
+// the weight-resident kernel's epilogue, any other (kernel, act) pair runs the act in place after
+extern "C" int gnnea_gemm_bf16_act(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                                   const void* A, int64_t lda, const void* B, int64_t ldb,
+                                   const float* bias, int act, void* C, int64_t ldc, int c_dtype,
+                                   void* ws, int64_t ws_bytes, void* stream) {
+  if (act < GNNEA_ACT_IDENTITY || act > GNNEA_ACT_TANH) return GNNEA_EINVAL;
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  if (M == 0 || N == 0) return 0;
+  if (M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return GNNEA_EINVAL;
+  if (!C || ldc < N || (K > 0 && (!A || !B))) return GNNEA_EINVAL;
+  if (K > 0) {
+    if ((trans_a ? lda < M : lda < K) || (trans_b ? ldb < K : ldb < N)) return GNNEA_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (c_dtype == GNNEA_BF16)
+    return gemm_bf16_t<bf16_t>(trans_a, trans_b, M, N, K, (const bf16_t*)A, lda,
+                               (const bf16_t*)B, ldb, bias, 0.f, (bf16_t*)C, ldc, ws, ws_bytes,
+                               s, 128, act);
+  if (c_dtype == GNNEA_F32)
+    return gemm_bf16_t<float>(trans_a, trans_b, M, N, K, (const bf16_t*)A, lda,
+                              (const bf16_t*)B, ldb, bias, 0.f, (float*)C, ldc, ws, ws_bytes, s,
+                              128, act);
   return GNNEA_EINVAL;
 }
 

@@ -300,7 +300,7 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
                                                        const float* __restrict__ bias,
                                                        float* __restrict__ C, int64_t ldc,
                                                        int64_t cs, float* __restrict__ C2,
-                                                       int64_t cs2, float beta) {
+                                                       int64_t cs2, float beta, int relu) {
   constexpr int NW = 8, BM = 16 * NW;
   __shared__ __attribute__((aligned(16))) uint4 wl[3 * W3_PLANE];
   __shared__ __attribute__((aligned(16))) float bsh[W3_NC];
@@ -419,6 +419,7 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
             const float4 cv = *cp;
             o.x += beta * cv.x; o.y += beta * cv.y; o.z += beta * cv.z; o.w += beta * cv.w;
           }
+          if (relu) o = f4_relu(o);  // the Linear's act (layers/layers.py:121-122), uniform
           *cp = o;
           if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
         }
@@ -438,7 +439,7 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring2(int M, int N, int K, int
                                                         const float* __restrict__ bias,
                                                         float* __restrict__ C, int64_t ldc,
                                                         int64_t cs, float* __restrict__ C2,
-                                                        int64_t cs2, float beta) {
+                                                        int64_t cs2, float beta, int relu) {
   constexpr int NW = 8, BM = 32 * NW, RS = 5;  // ring slots (steps in flight)
   __shared__ __attribute__((aligned(16))) uint4 wl[3 * W3_PLANE];
   __shared__ __attribute__((aligned(16))) float bsh[W3_NC];
@@ -556,6 +557,7 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring2(int M, int N, int K, int
             const float4 cv = *cp;
             o.x += beta * cv.x; o.y += beta * cv.y; o.z += beta * cv.z; o.w += beta * cv.w;
           }
+          if (relu) o = f4_relu(o);  // the Linear's act (layers/layers.py:121-122), uniform
           *cp = o;
           if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
         }
@@ -583,8 +585,10 @@ int64_t gemm_x3w_ws_bytes(int64_t N) {
 
 bool gemm_x3w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda, const void* A,
                       float beta, int64_t ldc, int64_t cs, const void* C, const void* C2,
-                      int64_t cs2) {
-  return x3w_on() && !trans_a && (beta == 0.f || x3w_mode() >= 2) && A && C && M >= 65536 &&
+                      int64_t cs2, int act) {
+  // beta != 0 and a fused act only on the ring forms (modes 2 and 3)
+  return x3w_on() && !trans_a && ((beta == 0.f && act == GNNEA_ACT_IDENTITY) || x3w_mode() >= 2) &&
+         (act == GNNEA_ACT_IDENTITY || act == GNNEA_ACT_RELU) && A && C && M >= 65536 &&
          M < (1ll << 31) &&
          N >= 64 && N <= 4096 && N % 4 == 0 && K > 32 * (W3_KC - 1) && K <= 32 * W3_KC && K % 4 == 0 &&
          lda >= K && lda % 4 == 0 && (((uintptr_t)A) & 15) == 0 &&
@@ -595,8 +599,9 @@ bool gemm_x3w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda,
 int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                     const float* B, int64_t ldb, const float* bias, float* C, int64_t ldc,
                     int64_t cs, float* C2, int64_t cs2, void* ws, int64_t ws_bytes,
-                    hipStream_t s, float beta) {
+                    hipStream_t s, float beta, int act) {
   const int ntn = (int)((N + W3_NC - 1) / W3_NC);
+  const int relu = act == GNNEA_ACT_RELU ? 1 : 0;
   if (!ws || ws_bytes < gemm_x3w_ws_bytes(N)) return GNNEA_EWORKSPACE;
   bf16_t* P = (bf16_t*)ws;
   {
@@ -624,10 +629,10 @@ int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A
   if ((int64_t)grid / ntn > tm) grid = (int)((tm + 7) / 8 * 8 * ntn);
   if (ring2)
     hipLaunchKernelGGL(k_gemm_x3w_ring2, dim3(grid), dim3(512), 0, s, (int)M, (int)N, (int)K,
-                       ntn, A, lda, P, bias, C, ldc, cs, C2, cs2, beta);
+                       ntn, A, lda, P, bias, C, ldc, cs, C2, cs2, beta, relu);
   else if (ring)
     hipLaunchKernelGGL(k_gemm_x3w_ring, dim3(grid), dim3(512), 0, s, (int)M, (int)N, (int)K, ntn,
-                       A, lda, P, bias, C, ldc, cs, C2, cs2, beta);
+                       A, lda, P, bias, C, ldc, cs, C2, cs2, beta, relu);
   else
     hipLaunchKernelGGL(k_gemm_x3w, dim3(grid), dim3(64 * W3_NW), 0, s, (int)M, (int)N, (int)K,
                        ntn, A, lda, P, bias, C, ldc, cs, C2, cs2);

@@ -33,13 +33,18 @@ constexpr double kLnTrueMin = -744.4400719213812;     // log(DBL_TRUE_MIN)
 constexpr double kExpOverflow = 709.782712893384;     // exp_f64(x) == inf above
 
 struct SkWs {
-  int64_t f, g, ua, va, rowbuf, errpart, part_m, part_s, la, lb, fs, gs, total;
-  int ncb;
+  int64_t f, g, ua, va, rowbuf, errpart, part_m, part_s, la, lb, fs, gs, fpart, ftab, total;
+  int ncb, nsf;
 };
 
 static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
 constexpr int kMaxSplits = 16;  // row splits of the partial column pass
+
+// fused KNOPP sweep (k_lsk_sweep): waves per workgroup, exp table size, widest J, workgroups
+constexpr int kFW = 8, kFTab = 2048, kFMaxJ = 64 * kFW * 32, kFWgTarget = 256;
+static int fused_rpw(int I) { return (I + kFWgTarget - 1) / kFWgTarget; }
+static int fused_wgs(int I) { return (I + fused_rpw(I) - 1) / fused_rpw(I); }
 
 static SkWs sk_plan(int I, int J) {
   SkWs w;
@@ -57,6 +62,10 @@ static SkWs sk_plan(int I, int J) {
   w.lb = o; o = al256(o + 8ll * J);
   w.fs = o; o = al256(o + 2 * 8ll * I);  // KNOPP fast path: f, g in units of ln2 / 64
   w.gs = o; o = al256(o + 2 * 8ll * J);
+  // fused KNOPP sweep (J <= kFMaxJ): column partials of its workgroups and the 2^(j/2048) table
+  w.nsf = fused_wgs(I);
+  w.fpart = o; o = al256(o + 8ll * w.nsf * J);
+  w.ftab = o; o = al256(o + 8ll * kFTab);
   w.total = o;
   return w;
 }
@@ -66,6 +75,7 @@ struct SkDev {
   double* sd;    // status doubles (sd[8] ...)
   double *f, *g, *ua, *va, *rowbuf, *errpart, *pm, *ps;
   double *fs, *gs;  // f, g scaled by 64 / ln 2 (KNOPP fast path)
+  double *fpart, *ftab;  // fused KNOPP sweep: column partials [nsf][J], 2^(j/2048) table
   int ncb;  // errpart slots written by the column pass of the active variant
 };
 
@@ -85,6 +95,8 @@ static SkDev sk_dev(const gnnea_sinkhorn* p) {
   d.ps = (double*)(b + w.part_s);
   d.fs = (double*)(b + w.fs);
   d.gs = (double*)(b + w.gs);
+  d.fpart = (double*)(b + w.fpart);
+  d.ftab = (double*)(b + w.ftab);
   d.ncb = w.ncb;
   return d;
 }
@@ -138,6 +150,7 @@ struct SkArgs {
   int64_t ldc;
   double inv_eps, p_row, p_col, kclamp;  // kclamp: ln 1e30 for STAB modes, +inf for KNOPP
   const double *la, *lb;
+  const double *wa, *wb;  // the weights a, b themselves (the fused sweep's u_new / u_old, err)
 };
 
 __device__ __forceinline__ void mark_done(int64_t* st, int64_t iters, int64_t reason,
@@ -280,7 +293,8 @@ __device__ __forceinline__ double sk_term(double ua, double va, double c, double
 // iterate it-1 (when (it-1)%10 == 0), then the K^T u == 0 / inf / NaN break of iteration it
 // flagged by this iteration's column pass.  Evaluated by wave 0 of every row workgroup (all
 // take the same decision); returns true when the workgroup must stop.
-__device__ __forceinline__ bool knopp_stop(SkDev& d, int it) {
+// out of line (once per launch): keeps its registers out of the streaming kernels' budget
+__device__ __noinline__ bool knopp_stop(SkDev& d, int it) {
   __shared__ int stop;
   const int lane = lane_id();
   if (wave_id() == 0) {
@@ -808,7 +822,282 @@ static SkArgs sk_args(const gnnea_sinkhorn* p) {
   const SkWs w = sk_plan(p->I, p->J);
   a.la = (const double*)((const char*)p->ws + w.la);  // log a, log b: filled by init
   a.lb = (const double*)((const char*)p->ws + w.lb);
+  a.wa = p->a;
+  a.wb = p->b;
   return a;
+}
+
+// ---------------------------------------------------------------------------------------- //
+// Fused KNOPP sweep: ONE pass over C per iteration and ONE exponential per element.
+//
+// The reference's scaling-form iteration (utils/ot_loss.py:53-55, v = b / K^T u then
+// u = 1 / (Kp v)) on potentials f = log u, g = log v, the kernel recomputed from C in the pass.
+// Row i of iteration it (g = g_it complete, written by the column update before the sweep):
+//   x_ij = g_j + k_ij (k_ij = -C_ij / reg, masked to -inf where exp_f64 underflows, as sk_term),
+//   each wave w: M_w = max over its columns, e_ij = exp(x_ij - M_w) <= 1, s_w = sum e_ij;
+//   the workgroup: M = max_w M_w, s = sum_w s_w exp(M_w - M), LSE_j(x_ij) = M + log s,
+//   f_it,i = log a_i - LSE   (u = a / (K v)),
+// and the same e_ij, scaled by exp(M_w - M) a_i / s, ARE the entries of P(u_it, v_it) =
+// u_it K v_it (<= a_i: no overflow; an entry lost to underflow is below 2^-1022 a_i).
+// Accumulated down the workgroup's rows they are its partial of S_j = v_it (K^T u_it)_j; the
+// column update (k_lsk_colfin) sums the partials in fixed order:
+//   err^2 term of iterate it   (S_j - b_j)^2                    (utils/ot_loss.py:64-66)
+//   g_{it+1} = log b_j - log S_j + g_{it,j}                      (v = b / K^T u, :53-54)
+// A column whose S_j is outside [2^-600, 2^600] (K^T u underflowing, an all-masked column, inf,
+// NaN) is recomputed there from C and f with a running maximum, so the fast path never trades
+// accuracy.  The breaks are the two-pass path's: K^T u == 0 (column LSE below ln DBL_TRUE_MIN)
+// or v inf / NaN flagged by the column update, u inf / NaN by the row update, the err test of
+// iterate it-1 at the start of sweep it.
+//
+// Layout (as k_sk_sweep of the scaling form): a 512-thread workgroup owns rows [r0, r1) (about
+// one workgroup per CU); wave w owns the column slice c0 + 64 k + lane (k < NCM) of every row, the
+// slice's g in LDS; the next row's C values are in flight (buffer loads: columns past J read 0,
+// no clamp per column) while a row is reduced; one barrier per row.  Per element: the fp64 term
+// (one multiply, the underflow mask, one fma), the running max, the table exponential
+// (2^(x/2048): 2048-entry table in LDS + degree-3 polynomial, truncation 3.4e-17), the row sum
+// and the column fma -- against two exponentials, two running maxima and two passes over C in the
+// two-pass form.  C is read once per iteration: I J sizeof(T) bytes (0.9 GB fp32 at B = 15000).
+constexpr double kFScale = 2954.639443740597;  // 2048 / ln 2
+// out of line: called by one lane per row, its registers stay out of the sweep's budget
+__device__ __noinline__ double lsk_log(double x) { return log(x); }
+constexpr double kFLo = 0x1p-600, kFHi = 0x1p600;
+
+__global__ void k_lsk_tab(double* __restrict__ tab) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < kFTab) tab[j] = exp2((double)j / (double)kFTab);
+}
+
+// 2^(x / 2048): t = rint(x), r = x - t in [-1/2, 1/2], 2^(t >> 11) * tab[t & 2047] * e^(r ln2/2048)
+// (e^y - 1 to degree 3, |y| <= 1.7e-4).  x = -huge (a masked term) gives 0: t saturates in the
+// int conversion, ldexp underflows.  NaN stays NaN.
+__device__ __forceinline__ double exp2x(double x, const double* __restrict__ tab) {
+  constexpr double c1 = 0.0003384507717577858, c2 = 5.72744624517204e-08,
+                   c3 = 6.461528672932365e-12;  // (ln2/2048)^k / k!
+  const double t = __builtin_rint(x);
+  const double r = x - t;
+  const int ti = (int)t;
+  double p = __builtin_fma(r, c3, c2);
+  p = __builtin_fma(p, r, c1);
+  p *= r;
+  const double tj = tab[ti & (kFTab - 1)];
+  return __builtin_ldexp(__builtin_fma(tj, p, tj), ti >> 11);
+}
+
+// natural-unit logit of K_ij (masked: -inf where exp_f64(-C/reg) underflows, as sk_term)
+__device__ __forceinline__ double lsk_k(double c, double inv_eps) {
+  const double k = -c * inv_eps;
+  return k < kExpUnderflow ? -INFINITY : k;
+}
+
+// PH0 (init): no row update, P(u_0, v_0) = exp(f_0 + g_0 + k) directly: the partials of
+// v_0 K^T u_0 for the first column update.
+template <typename T, int NCM, bool PH0>
+__global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                        int it, int slot_fp, int slot_g,
+                                                        int slot_fo, int rpw) {
+  __shared__ double tab[kFTab];
+  __shared__ double gsh[kFW * NCM * 64];
+  __shared__ double redm[2][kFW], reds[2][kFW];
+  if (!PH0 && d.st[ST_DONE]) return;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  for (int q = tid; q < kFTab; q += 64 * kFW) tab[q] = d.ftab[q];
+  const int r0 = blockIdx.x * rpw, r1 = min(a.I, r0 + rpw);
+  const int cw = ((a.J + kFW - 1) / kFW + 63) & ~63;
+  const int c0 = w * cw;
+  const int lim = min(c0 + cw, a.J) - c0 - lane;  // column c0 + 64 k + lane is valid iff 64 k < lim
+  const double* __restrict__ g = d.g + (int64_t)slot_g * a.J;
+  double* __restrict__ gl = gsh + w * NCM * 64 + lane;  // this lane's slice of g (scaled)
+#pragma unroll
+  for (int k = 0; k < NCM; ++k) gl[64 * k] = 64 * k < lim ? g[c0 + 64 * k + lane] * kFScale : -1e300;
+  __syncthreads();
+  T kA[NCM], kB[NCM];
+  // buffer loads over the row (J elements): one lane offset, the 64 k steps as scalar offsets;
+  // columns past J read 0 (their g slice is -1e300: no contribution) without a clamp per column
+  const uint32_t voff = (uint32_t)(c0 + lane) * sizeof(T);
+  auto load = [&](T (&kv)[NCM], int r) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(C + (int64_t)r * a.ldc), (short)0, a.J * (int)sizeof(T), 0x00020000);
+#pragma unroll
+    for (int k = 0; k < NCM; ++k) {
+      if constexpr (sizeof(T) == 4)
+        kv[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, 256 * k, 0));
+      else
+        kv[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 512 * k, 0));
+    }
+  };
+  // the first row's loads go out before the stop decision (round trips on the status block)
+  if (r0 < r1) load(kA, r0);
+  if (!PH0 && knopp_stop(d, it)) return;
+  double acc[NCM];
+#pragma unroll
+  for (int k = 0; k < NCM; ++k) acc[k] = 0.0;
+  const double neg_s = -a.inv_eps;
+  auto process = [&](const T (&kv)[NCM], int r, int par) {
+    // x = (g_j + k_ij) in units of ln2 / 2048; masked terms -3e303 (exp2x -> 0).  The slice of g
+    // is re-read from LDS per row (opaque to hoisting: held in registers it would cost 2 NCM)
+    asm volatile("" ::: "memory");
+    double e[NCM];
+    if (PH0) {
+      const double f0 = d.f[(int64_t)slot_fp * a.I + r] * kFScale;
+#pragma unroll
+      for (int k = 0; k < NCM; ++k) {
+        const double kn = (double)kv[k] * neg_s;
+        const double kk = kn < kExpUnderflow ? -1e300 : kn;
+        e[k] = exp2x(__builtin_fma(kk, kFScale, gl[64 * k] + f0), tab);
+        acc[k] += e[k];
+      }
+      return;
+    }
+    double mw = -1e308;
+#pragma unroll
+    for (int k = 0; k < NCM; ++k) {
+      const double kn = (double)kv[k] * neg_s;
+      const double kk = kn < kExpUnderflow ? -1e300 : kn;
+      e[k] = __builtin_fma(kk, kFScale, gl[64 * k]);
+      mw = fmax(mw, e[k]);
+      if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound the live temporaries
+    }
+    mw = wave_max(mw);
+    double sw = 0.0;
+#pragma unroll
+    for (int k = 0; k < NCM; ++k) {
+      e[k] = exp2x(e[k] - mw, tab);  // <= 1
+      sw += e[k];
+      if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    sw = wave_sum_f64(sw);
+    if (lane == 0) {
+      redm[par][w] = mw;
+      reds[par][w] = sw;
+    }
+    __syncthreads();  // double-buffered by row parity: one barrier per row
+    // the row's LSE from the wave pairs, lane q holding wave q's (every wave the same sums):
+    // M = max_q M_q, s = sum_q s_q 2^((M_q - M) / 2048)
+    const double mq = lane < kFW ? redm[par][lane] : -1e308;
+    const double M = wave_max(mq);
+    const double sr = wave_sum_f64(lane < kFW ? reds[par][lane] * exp2x(mq - M, tab) : 0.0);
+    // f_new = log a - LSE_j(g_j + k_ij) (u = a / (K v)); P(u_new, v)_ij = e_ij 2^(M_w - M) a / s
+    const double wi = exp2x(mw - M, tab) * (a.wa[r] / sr);
+    if (w == 0 && lane == 0) {
+      const double fnew = a.la[r] - (M / kFScale + lsk_log(sr));
+      d.f[(int64_t)slot_fo * a.I + r] = fnew;
+      if (!(fnew <= kExpOverflow)) mark_done(d.st, it, 2, (it + 1) & 1);  // u inf / NaN
+    }
+#pragma unroll
+    for (int k = 0; k < NCM; ++k) acc[k] = __builtin_fma(e[k], wi, acc[k]);
+  };
+  int r = r0, par = 0;
+  while (r < r1) {
+    if (r + 1 < r1) load(kB, r + 1);
+    process(kA, r, par);
+    if (r + 1 >= r1) break;
+    if (r + 2 < r1) load(kA, r + 2);
+    process(kB, r + 1, par ^ 1);
+    r += 2;
+  }
+  double* __restrict__ part = d.fpart + (int64_t)blockIdx.x * a.J + c0 + lane;
+#pragma unroll
+  for (int k = 0; k < NCM; ++k)
+    if (64 * k < lim) part[64 * k] = acc[k];
+}
+
+// Column update of the fused sweep: S_j = sum of the workgroup partials (fixed order), the
+// err^2 term of the iterate the partials belong to, g = log b - log S + g_prev, the break flags.
+// 16 columns per 1024-thread workgroup (errpart slots: div_up(J, 16)); a column whose S is out
+// of [2^-600, 2^600] (or not finite) is recomputed from C and f exactly (running maximum).
+template <typename T>
+__global__ __launch_bounds__(1024) void k_lsk_colfin(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                     int ns, int slot_f, int slot_g_prev,
+                                                     int slot_g_out) {
+  if (d.st[ST_DONE]) return;
+  constexpr int NC = 16;
+  __shared__ double red[64][NC], lm[64][NC];
+  __shared__ int need;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int cl = lane & (NC - 1), slot = w * 4 + (lane >> 4);
+  const int j = blockIdx.x * NC + cl;
+  const int jc = min(j, a.J - 1);
+  if (tid == 0) need = 0;
+  double s = 0.0;
+  for (int q = slot; q < ns; q += 64) s += d.fpart[(int64_t)q * a.J + jc];
+  red[slot][cl] = s;
+  __syncthreads();
+  double S = 0.0;
+  bool slow = false;
+  if (tid < NC) {
+#pragma unroll 8
+    for (int q = 0; q < 64; ++q) S += red[q][cl];
+    slow = j < a.J && !(S >= kFLo && S <= kFHi);
+    if (slow) need = 1;
+  }
+  __syncthreads();
+  double L = 0.0;
+  if (need) {  // uniform: the whole workgroup recomputes its flagged columns
+    const double* __restrict__ f = d.f + (int64_t)slot_f * a.I;
+    Lse l;
+    l.init();
+    for (int i = slot; i < a.I; i += 64) l.add(f[i] + lsk_k((double)C[(int64_t)i * a.ldc + jc], a.inv_eps));
+    lm[slot][cl] = l.m;
+    red[slot][cl] = l.s;
+    __syncthreads();
+    if (tid < NC) {
+      Lse t;
+      t.init();
+      for (int q = 0; q < 64; ++q) t.merge(lm[q][cl], red[q][cl]);
+      L = t.value();  // log K^T u_j
+    }
+  }
+  if (tid >= 64) return;
+  double errp = 0.0;
+  bool fail = false;
+  if (tid < NC && j < a.J) {
+    const double gp = d.g[(int64_t)slot_g_prev * a.J + j];
+    double gj;
+    if (!slow) {
+      const double t = S - a.wb[j];  // v_prev (K^T u) - b
+      errp = t * t;
+      gj = a.lb[j] - log(S) + gp;
+    } else {
+      const double t = exp_f64(gp + L) - a.wb[j];
+      errp = t * t;
+      fail = !(L >= kLnTrueMin);  // K^T u == 0 (or NaN)   (ot_loss.py:57)
+      gj = a.lb[j] - L;
+    }
+    fail = fail || !(gj <= kExpOverflow);  // v inf / NaN   (:58-59)
+    d.g[(int64_t)slot_g_out * a.J + j] = gj;
+  }
+#pragma unroll
+  for (int o = NC / 2; o > 0; o >>= 1) errp += __shfl_xor(errp, o, 64);
+  const unsigned long long anyfail = __ballot(fail) & ((1ull << NC) - 1);
+  if (tid == 0) {
+    d.errpart[blockIdx.x] = errp;
+    if (anyfail) atomicOr((unsigned long long*)&d.st[ST_FAIL], 1ull);
+  }
+}
+
+// the fused sweep serves KNOPP for J <= kFMaxJ (GNNEA_SK_FUSED=0 keeps the two passes: A/B only)
+static bool fused_applies(const gnnea_sinkhorn* p) {
+  const char* e = getenv("GNNEA_SK_FUSED");  // read per call: tests switch it between solves
+  const bool on = !(e && e[0] == '0');
+  // fp64 C: the slice's loads double, J <= kFMaxJ / 2 keeps them in registers
+  return on && p->mode == GNNEA_SK_KNOPP &&
+         p->J <= (p->c_dtype == GNNEA_F64 ? kFMaxJ / 2 : kFMaxJ);
+}
+
+template <typename T, bool PH0>
+static void launch_fused_sweep(const T* C, const SkArgs& a, const SkDev& d, int it, int sfp,
+                               int sg, int sfo, hipStream_t s) {
+  const int rpw = fused_rpw(a.I), ns = fused_wgs(a.I);
+  const int nc = (((a.J + kFW - 1) / kFW + 63) & ~63) / 64;
+  const dim3 g(ns), b(64 * kFW);
+  if (nc <= 4)
+    hipLaunchKernelGGL((k_lsk_sweep<T, 4, PH0>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+  else if (nc <= 8)
+    hipLaunchKernelGGL((k_lsk_sweep<T, 8, PH0>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+  else if (sizeof(T) == 8 || nc <= 16)  // (fp64 C: fused_applies bounds nc by 16)
+    hipLaunchKernelGGL((k_lsk_sweep<T, 16, PH0>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+  else if constexpr (sizeof(T) == 4)
+    hipLaunchKernelGGL((k_lsk_sweep<T, 32, PH0>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
 }
 
 // Launch configurations of the two passes (10*row + col); the path runs configuration 0, the
@@ -880,9 +1169,16 @@ static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t 
   }
   const dim3 gabs(div_up(p->I, 4));
   const T* C = (const T*)p->C;
+  const bool fused = fused_applies(p);
   for (int it = first; it < first + count; ++it) {
     const int cur = it & 1, prev = (it + 1) & 1;
-    if (p->mode == GNNEA_SK_KNOPP) {
+    if (p->mode == GNNEA_SK_KNOPP && fused) {
+      // column update from the previous sweep's partials (P(u_prev, v_prev)), then the sweep
+      d.ncb = div_up(a.J, 16);
+      hipLaunchKernelGGL(k_lsk_colfin<T>, dim3(d.ncb), dim3(1024), 0, s, C, a, d,
+                         fused_wgs(a.I), prev, prev, cur);
+      launch_fused_sweep<T, false>(C, a, d, it, prev, cur, cur, s);
+    } else if (p->mode == GNNEA_SK_KNOPP) {
       launch_col<T, true>(cv, C, a, d, it, prev, prev, cur, s);  // sets d.ncb for the row pass
       launch_row<T, true>(rv, C, a, d, it, cur, cur, s);
     } else {
@@ -925,6 +1221,14 @@ int init(const gnnea_sinkhorn* p, void* stream) {
       hipLaunchKernelGGL(k_sk_cscan<double>, dim3(nb), dim3(256), 0, s, (const double*)p->C,
                          p->I, p->J, p->ldc, d.st);
     GNNEA_LAUNCH_CHECK();
+    if (fused_applies(p)) {  // the table, then the partials of v_0 K^T u_0 (slot 1: u_0, v_0)
+      hipLaunchKernelGGL(k_lsk_tab, dim3(div_up(kFTab, 256)), dim3(256), 0, s, d.ftab);
+      if (p->c_dtype == GNNEA_F32)
+        launch_fused_sweep<float, true>((const float*)p->C, a, d, 0, 1, 1, 1, s);
+      else
+        launch_fused_sweep<double, true>((const double*)p->C, a, d, 0, 1, 1, 1, s);
+      GNNEA_LAUNCH_CHECK();
+    }
   }
   if (p->mode != GNNEA_SK_KNOPP) {  // initial transport = sum K0 . C   (sinkhorn_loss.py:195)
     const dim3 grow(div_up(p->I, 4));

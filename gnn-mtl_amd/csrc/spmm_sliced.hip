@@ -292,73 +292,87 @@ constexpr SlicedHighway kNoHighway{nullptr, 0, 0, nullptr, nullptr, 0, nullptr, 
 
 // bf16 over 64-column slices (the GAT tables' layout, gnnea_slice_pack64_bf16): a slice row piece
 // is 128 B = one line and one cfg-5 KG slice (2M rows) is 256 MB, the Infinity Cache's size (the
-// 128-column form above is 512 MB per KG slice).  Lane c of a 16-lane group owns 4 columns (8 B),
-// the 4 groups take neighbours g, g + 4, ...; gathers issued unconditionally in double-buffered
-// batches of 4U edges per group (the PIPE scheme of k_spmm_sliced), fp32 sums, group partials
-// summed in fixed order, group 0 writes the row piece with the activation fused.
+// 128-column form above is 512 MB per KG slice).  Lane c of an 8-lane group owns 8 columns (16 B:
+// 8-B lane accesses run at 0.54-0.70 of the 16-B rate, MI355X_MICROARCH.md), the 8 groups take
+// neighbours g, g + 8, ...: one wave instruction gathers 8 whole row pieces.  Gathers issued
+// unconditionally in double-buffered batches of 8U edges (the PIPE scheme of k_spmm_sliced),
+// fp32 sums, the group partials summed in fixed order (xor 8, 16, 32), group 0 writes the row
+// piece with the activation fused (a last slice ending 4 columns into a lane's 8 stores 4).
 template <int ACT, int U, typename TY>
 __global__ __launch_bounds__(256) void k_spmm_sliced64_bf16(const int32_t* __restrict__ rowptr,
                                                             const int32_t* __restrict__ col,
                                                             const float* __restrict__ val,
                                                             int n_rows, int nbs, int D,
-                                                            const uint2* __restrict__ Xs,
-                                                            int64_t sstride8, TY* __restrict__ Y,
+                                                            const uint4* __restrict__ Xs,
+                                                            int64_t sstride16, TY* __restrict__ Y,
                                                             int64_t ldy) {
   const int b = blockIdx.x;
   const int s = b / nbs;
   const int row = xcd_remap(b - s * nbs, nbs) * 4 + wave_id();
   if (row >= n_rows) return;
-  const int lane = lane_id(), g = lane >> 4, c = lane & 15;
-  const int c0 = s * 64 + 4 * c;
+  const int lane = lane_id(), g = lane >> 3, c = lane & 7;
+  const int c0 = s * 64 + 8 * c;
   const bool own = c0 < D;
-  const uint2* Xp = Xs + (int64_t)s * sstride8 + (own ? c : 0);
+  const uint4* Xp = Xs + (int64_t)s * sstride16 + (own ? c : 0);
   const int beg = rowptr[row], end = rowptr[row + 1];
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int base = beg; base < end; base += 64) {
     const int cnt = min(64, end - base);
     const int el = base + min(lane, cnt - 1);
     const int mc = col[el];
     const float mv = val[el] * (lane < cnt ? 1.f : 0.f);
-    uint2 ra[U], rb[U];
-    auto issue = [&](uint2 (&r)[U], int k) {
+    uint4 ra[U], rb[U];
+    auto issue = [&](uint4 (&r)[U], int k) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int j = __shfl(mc, min(k + 4 * u + g, cnt - 1), 64);
-        r[u] = Xp[(int64_t)j * 16];
+        const int j = __shfl(mc, min(k + 8 * u + g, cnt - 1), 64);
+        r[u] = Xp[(int64_t)j * 8];
       }
     };
-    auto consume = [&](const uint2 (&r)[U], int k) {
+    auto consume = [&](const uint4 (&r)[U], int k) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = k + 4 * u + g;
+        const int e = k + 8 * u + g;
         const float vs = __shfl(mv, e & 63, 64);
         const float v = e < cnt ? vs : 0.f;
-        const float4 f = Vec4<bf16_t>::get(r[u]);
-        acc[0] = fmaf(v, f.x, acc[0]);
-        acc[1] = fmaf(v, f.y, acc[1]);
-        acc[2] = fmaf(v, f.z, acc[2]);
-        acc[3] = fmaf(v, f.w, acc[3]);
+        const float4 lo = Vec4<bf16_t>::get(make_uint2(r[u].x, r[u].y));
+        const float4 hi = Vec4<bf16_t>::get(make_uint2(r[u].z, r[u].w));
+        acc[0] = fmaf(v, lo.x, acc[0]);
+        acc[1] = fmaf(v, lo.y, acc[1]);
+        acc[2] = fmaf(v, lo.z, acc[2]);
+        acc[3] = fmaf(v, lo.w, acc[3]);
+        acc[4] = fmaf(v, hi.x, acc[4]);
+        acc[5] = fmaf(v, hi.y, acc[5]);
+        acc[6] = fmaf(v, hi.z, acc[6]);
+        acc[7] = fmaf(v, hi.w, acc[7]);
       }
     };
     issue(ra, 0);
-    for (int k = 0; k < cnt; k += 8 * U) {
-      issue(rb, k + 4 * U);
+    for (int k = 0; k < cnt; k += 16 * U) {
+      issue(rb, k + 8 * U);
       __builtin_amdgcn_sched_barrier(0);
       consume(ra, k);
-      issue(ra, k + 8 * U);
+      issue(ra, k + 16 * U);
       __builtin_amdgcn_sched_barrier(0);
-      consume(rb, k + 4 * U);
+      consume(rb, k + 8 * U);
     }
   }
 #pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] += __shfl_xor(acc[q], 16, 64);
+  for (int q = 0; q < 8; ++q) acc[q] += __shfl_xor(acc[q], 8, 64);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] += __shfl_xor(acc[q], 32, 64);
+  for (int q = 0; q < 8; ++q) acc[q] += __shfl_xor(acc[q], 16, 64);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] += __shfl_xor(acc[q], 32, 64);
   if (g != 0 || !own) return;
-  const float4 sv = make_float4(act_fwd<ACT>(acc[0]), act_fwd<ACT>(acc[1]), act_fwd<ACT>(acc[2]),
-                                act_fwd<ACT>(acc[3]));
   typedef typename Vec4<TY>::raw RY;
-  *(RY*)(Y + (int64_t)row * ldy + c0) = Vec4<TY>::put(sv);
+  const float4 s0 = make_float4(act_fwd<ACT>(acc[0]), act_fwd<ACT>(acc[1]), act_fwd<ACT>(acc[2]),
+                                act_fwd<ACT>(acc[3]));
+  *(RY*)(Y + (int64_t)row * ldy + c0) = Vec4<TY>::put(s0);
+  if (c0 + 4 < D) {  // D % 4 == 0: the lane's second 4 columns are wholly in or out
+    const float4 s1 = make_float4(act_fwd<ACT>(acc[4]), act_fwd<ACT>(acc[5]),
+                                  act_fwd<ACT>(acc[6]), act_fwd<ACT>(acc[7]));
+    *(RY*)(Y + (int64_t)row * ldy + c0 + 4) = Vec4<TY>::put(s1);
+  }
 }
 
 template <typename TY>
@@ -369,14 +383,14 @@ static int spmm_sliced64_bf16(const int32_t* rowptr, const int32_t* col, const f
   if (n_rows == 0 || D == 0) return 0;
   if (!rowptr || !col || !val || !Xs || !Y) return GNNEA_EINVAL;
   if (D % 4 || ldy % 4 || ldy < D || sstride % 64 || sstride < 64) return GNNEA_EINVAL;
-  if ((((uintptr_t)Xs) & 7) || !aln<TY>(Y)) return GNNEA_EALIGN;
+  if ((((uintptr_t)Xs) & 15) || !aln<TY>(Y)) return GNNEA_EALIGN;
   const int nbs = (n_rows + 3) / 4;
   const int S = (D + 63) / 64;
   if ((int64_t)nbs * S >= (1ll << 31)) return GNNEA_EINVAL;
-  const int64_t ss8 = sstride / 4;  // 8-B units
+  const int64_t ss16 = sstride / 8;  // 16-B units
 #define GNNEA_S64(A)                                                                           \
-  hipLaunchKernelGGL((k_spmm_sliced64_bf16<A, 4, TY>), dim3(nbs * S), dim3(256), 0, s, rowptr, \
-                     col, val, n_rows, nbs, D, (const uint2*)Xs, ss8, Y, ldy)
+  hipLaunchKernelGGL((k_spmm_sliced64_bf16<A, 2, TY>), dim3(nbs * S), dim3(256), 0, s, rowptr, \
+                     col, val, n_rows, nbs, D, (const uint4*)Xs, ss16, Y, ldy)
   switch (act) {
     case GNNEA_ACT_IDENTITY: GNNEA_S64(GNNEA_ACT_IDENTITY); break;
     case GNNEA_ACT_RELU: GNNEA_S64(GNNEA_ACT_RELU); break;

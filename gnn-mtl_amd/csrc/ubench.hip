@@ -3,8 +3,9 @@
 // (5.0 TB/s) is one implementation's rate, not the hardware's; these two kernels are the
 // reference points the gather-bound passes are judged against:
 //   k_ub_copy    a streaming copy, 16 B per lane per access, every lane of a wave on consecutive
-//                16-B chunks (1 KB per wave instruction), four accesses in flight per lane, a
-//                grid of a few workgroups per CU striding over the buffer;
+//                16-B chunks (1 KB per wave instruction), four or eight accesses in flight per
+//                lane, plain or nontemporal, a grid of a few workgroups per CU striding over the
+//                buffer; or the same loads alone (read only);
 //   k_ub_gather  whole-row gathers: one wave per 64 rows of an index list, each row read by the
 //                lanes of the wave as 8-B chunks (row_bytes % 8 == 0: a 600-B row is 75 chunks),
 //                summed into one accumulator per lane (nothing is written per row, so only the
@@ -15,18 +16,42 @@
 
 namespace gnnea {
 
+// U accesses of 16 B in flight per lane; NT: nontemporal loads and stores; RO: read only (the
+// loaded words xor-folded, one word per lane written at the end: a read-bandwidth anchor)
+typedef unsigned int ub_u32x4 __attribute__((ext_vector_type(4)));
+
+template <int U, bool NT, bool RO>
 __global__ __launch_bounds__(256) void k_ub_copy(const uint4* __restrict__ src,
                                                  uint4* __restrict__ dst, int64_t n16) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2 * stride] = c;
-    dst[i + 3 * stride] = d;
+  uint32_t x = 0;
+  for (; i + (U - 1) * stride < n16; i += U * stride) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (NT) {
+        const ub_u32x4 t = __builtin_nontemporal_load((const ub_u32x4*)(src + i + u * stride));
+        v[u] = make_uint4(t.x, t.y, t.z, t.w);
+      } else {
+        v[u] = src[i + u * stride];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if constexpr (RO) x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+      else if constexpr (NT)
+        __builtin_nontemporal_store(ub_u32x4{v[u].x, v[u].y, v[u].z, v[u].w},
+                                    (ub_u32x4*)(dst + i + u * stride));
+      else dst[i + u * stride] = v[u];
+    }
   }
-  for (; i < n16; i += stride) dst[i] = src[i];
+  for (; i < n16; i += stride) {
+    const uint4 v = src[i];
+    if constexpr (RO) x ^= v.x ^ v.y ^ v.z ^ v.w;
+    else dst[i] = v;
+  }
+  if constexpr (RO) ((uint32_t*)dst)[(int64_t)blockIdx.x * 256 + threadIdx.x] = x;
 }
 
 // wave w handles index entries [64 w, 64 w + 64): the 64 row ids are loaded once (one per lane)
@@ -71,12 +96,27 @@ __global__ __launch_bounds__(256) void k_ub_gather(const unsigned char* __restri
 using namespace gnnea;
 
 extern "C" int gnnea_ub_copy(const void* src, void* dst, int64_t bytes, int32_t blocks,
-                             void* stream) {
-  if (bytes < 0 || bytes % 16 || blocks <= 0) return GNNEA_EINVAL;
+                             int32_t flags, void* stream) {
+  if (bytes < 0 || bytes % 16 || blocks <= 0 || flags < 0 || flags > 7) return GNNEA_EINVAL;
   if (bytes == 0) return 0;
   if (!src || !dst || (((uintptr_t)src | (uintptr_t)dst) & 15)) return GNNEA_EALIGN;
-  hipLaunchKernelGGL(k_ub_copy, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                     (const uint4*)src, (uint4*)dst, bytes / 16);
+  // read only: dst receives one word per thread of the grid
+  if ((flags & GNNEA_UB_READ_ONLY) && (int64_t)blocks * 256 * 4 > bytes) return GNNEA_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const uint4* a = (const uint4*)src;
+  uint4* b = (uint4*)dst;
+  const int64_t n = bytes / 16;
+  const dim3 g(blocks), t(256);
+  switch (flags) {
+    case 0: hipLaunchKernelGGL((k_ub_copy<4, false, false>), g, t, 0, s, a, b, n); break;
+    case 1: hipLaunchKernelGGL((k_ub_copy<4, true, false>), g, t, 0, s, a, b, n); break;
+    case 2: hipLaunchKernelGGL((k_ub_copy<8, false, false>), g, t, 0, s, a, b, n); break;
+    case 3: hipLaunchKernelGGL((k_ub_copy<8, true, false>), g, t, 0, s, a, b, n); break;
+    case 4: hipLaunchKernelGGL((k_ub_copy<4, false, true>), g, t, 0, s, a, b, n); break;
+    case 5: hipLaunchKernelGGL((k_ub_copy<4, true, true>), g, t, 0, s, a, b, n); break;
+    case 6: hipLaunchKernelGGL((k_ub_copy<8, false, true>), g, t, 0, s, a, b, n); break;
+    default: hipLaunchKernelGGL((k_ub_copy<8, true, true>), g, t, 0, s, a, b, n); break;
+  }
   GNNEA_LAUNCH_CHECK();
   return 0;
 }

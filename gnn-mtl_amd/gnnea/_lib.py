@@ -19,6 +19,9 @@ GNNEA_ACT_ELU = 2
 GNNEA_ACT_LEAKY_RELU = 3
 GNNEA_ACT_SIGMOID = 4
 GNNEA_ACT_TANH = 5
+GNNEA_UB_NT = 1  # gnnea_ub_copy flags (include/gnnea.h)
+GNNEA_UB_DEEP = 2
+GNNEA_UB_READ_ONLY = 4
 
 GNNEA_F32 = 0
 GNNEA_F64 = 1
@@ -143,6 +146,19 @@ SIGNATURES = {
     "gnnea_gat_da2_bf16": (ctypes.c_int, [_p, _i64, _i64, ctypes.c_int, ctypes.c_int, _p, _p, _p,
                                           _p, _p, _i64, _p]),
     "gnnea_colsum_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _i64, _p]),
+    "gnnea_act_fwd_f32": (ctypes.c_int, [_p, _p, _i64, ctypes.c_int, _p]),
+    "gnnea_act_fwd_bf16": (ctypes.c_int, [_p, _p, _i64, ctypes.c_int, _p]),
+    "gnnea_act_bwd_colsum_ws_bytes": (_i64, [_i64, _i32]),
+    "gnnea_act_bwd_colsum_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i32, ctypes.c_int, _p,
+                                                _i64, _p, _p, _i64, _p]),
+    "gnnea_act_bwd_colsum_bf16": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i32, ctypes.c_int, _p,
+                                                 _i64, _p, _p, _i64, _p]),
+    "gnnea_gemm_bf16_act": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64,
+                                           _p, _i64, _p, ctypes.c_int, _p, _i64, ctypes.c_int, _p,
+                                           _i64, _p]),
+    "gnnea_gemm_x3_act_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p,
+                                             _i64, _p, _i64, _p, ctypes.c_int, _p, _i64, _p, _i64,
+                                             _p]),
     "gnnea_colsum_bf16": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _i64, _p]),
     "gnnea_gemm_ws_bytes": (_i64, [_i64, _i64, _i64]),
     "gnnea_gemm_bf16_ws_bytes": (_i64, [_i64, _i64, _i64]),
@@ -239,7 +255,7 @@ SIGNATURES = {
     "gnnea_l1_keys_f32":(ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _i64, _p]),
     "gnnea_l1_pairs_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i32, _i32, _p, _p]),
     "gnnea_l1_terms_f32": (ctypes.c_int, [_p, _i64, _i32, _i64, _p, _p, _p, _p]),
-    "gnnea_ub_copy": (ctypes.c_int, [_p, _p, _i64, _i32, _p]),
+    "gnnea_ub_copy": (ctypes.c_int, [_p, _p, _i64, _i32, _i32, _p]),
     "gnnea_ub_gather": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _p]),
     "gnnea_l1_rank_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _p, _p]),
     "gnnea_topk_rows_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _i64, _p, _i64, _i32,

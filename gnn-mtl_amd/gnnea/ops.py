@@ -134,14 +134,21 @@ def _ld(t):
 
 
 def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_dtype=None,
-         x3=None, sliced_out=None):
+         x3=None, sliced_out=None, act=None):
     """out = op(a) @ op(b) (+ bias) (+ beta*out) on MFMA.
 
     fp32 operands: gnnea_gemm_f32 (exact-f32 MFMA), or for large products gnnea_gemm_x3_f32
     (three-way bf16 splits, fp32-level rounding; ``x3`` forces either).  A bf16 operand (cfg-5
     storage) switches to gnnea_gemm_bf16 (both operands bf16, fp32 accumulate, out bf16 unless
-    an fp32 ``out`` / ``out_dtype`` is given)."""
+    an fp32 ``out`` / ``out_dtype`` is given).  ``act`` (a GNNEA_ACT_* code; beta = 0, no
+    sliced_out): out = act(op(a) @ op(b) + bias) -- gnnea_gemm_x3_act_f32 / gnnea_gemm_bf16_act,
+    relu in the weight-resident kernels' epilogue; after gnnea_gemm_f32 the act runs in place
+    (gnnea_act_fwd_f32)."""
     _lib.require_device(a, b)
+    if act == _lib.GNNEA_ACT_IDENTITY:
+        act = None
+    if act is not None and (beta != 0.0 or sliced_out is not None):
+        raise ValueError("gnnea.gemm: act needs beta = 0 and no sliced_out")
     bf = a.dtype == torch.bfloat16 or b.dtype == torch.bfloat16
     if bf:
         a = _featc(a, torch.bfloat16)
@@ -180,7 +187,18 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
     ws_bytes = _ws_query(ws_fn, M, N, K)
     ws = _gemm_ws(a.device, ws_bytes) if ws_bytes > 0 else None
     with _lib.on_device(a.device):
-        if bf:
+        if bf and act is not None:
+            cd = _lib.GNNEA_BF16 if out.dtype == torch.bfloat16 else _lib.GNNEA_F32
+            check(L.gnnea_gemm_bf16_act(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a),
+                                        ptr(b), _ld(b), ptr(bias), int(act), ptr(out), _ld(out),
+                                        cd, ptr(ws), ws_bytes if ws is not None else 0,
+                                        stream_of(a.device)))
+        elif act is not None and x3:
+            check(L.gnnea_gemm_x3_act_f32(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a),
+                                          ptr(b), _ld(b), ptr(bias), int(act), ptr(out),
+                                          _ld(out), ptr(ws), ws_bytes if ws is not None else 0,
+                                          stream_of(a.device)))
+        elif bf:
             cd = _lib.GNNEA_BF16 if out.dtype == torch.bfloat16 else _lib.GNNEA_F32
             check(L.gnnea_gemm_bf16(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a),
                                     ptr(b), _ld(b), ptr(bias), float(beta), ptr(out),
@@ -198,6 +216,11 @@ def gemm(a, b, trans_a=False, trans_b=False, bias=None, out=None, beta=0.0, out_
             check(fn(int(trans_a), int(trans_b), M, N, K, ptr(a), _ld(a), ptr(b), _ld(b),
                      ptr(bias), float(beta), ptr(out), _ld(out), ptr(ws),
                      ws_bytes if ws is not None else 0, stream_of(a.device)))
+            if act is not None:  # the exact-f32 kernel has no act epilogue
+                if not out.is_contiguous():
+                    raise ValueError("gnnea.gemm: act needs a contiguous out on this path")
+                check(L.gnnea_act_fwd_f32(ptr(out), ptr(out), out.numel(), int(act),
+                                          stream_of(a.device)))
             if sliced_out is not None:
                 check(L.gnnea_slice_pack_f32(ptr(out), _ld(out), M, N, ptr(sliced_out),
                                              sliced_out.stride(0), stream_of(a.device)))
@@ -265,6 +288,38 @@ class LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
+class LinearActFn(torch.autograd.Function):
+    """y = act(x Wᵀ + b)  (Linear.forward at layers/layers.py:121-122 with dropout inactive; the
+    MLPDecoder's relu layers, models/decoders.py:57-63): the act in the GEMM's epilogue, and in
+    the backward the act's derivative and the bias gradient in one pass over dY and y."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, act):
+        y = gemm(x, weight, trans_b=True, bias=bias, act=act)
+        ctx.save_for_backward(x, weight, y)
+        ctx.act = act
+        ctx.has_bias = bias is not None
+        ctx.bias_dtype = bias.dtype if bias is not None else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, y = ctx.saved_tensors
+        bf = x.dtype == torch.bfloat16 or weight.dtype == torch.bfloat16
+        dy = _featc(dy, y.dtype)
+        want_db = ctx.has_bias and ctx.needs_input_grad[2]
+        g, db = act_bwd_colsum(dy, y, ctx.act, want_db)
+        g = _featc(g, torch.bfloat16 if bf else torch.float32)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(g, weight, out_dtype=x.dtype if bf else None)
+        if ctx.needs_input_grad[1]:
+            dw = gemm(g, x, trans_a=True, out_dtype=weight.dtype if bf else None)
+        if db is not None and db.dtype != ctx.bias_dtype:
+            db = db.to(ctx.bias_dtype)
+        return dx, dw, db, None
+
+
 # slice-major copies of GEMM outputs written by the GEMM itself (gnnea_gemm_x3_dual_f32), keyed
 # by the row-major output's storage: the GAT forward finds the projection's sliced table here
 # instead of packing it (a stale entry is ignored: the tensor's version must match)
@@ -317,8 +372,32 @@ class MatmulFn(torch.autograd.Function):
         return dx, dw, None
 
 
-def linear(x, weight, bias=None):
-    return LinearFn.apply(x, weight, bias)
+def linear(x, weight, bias=None, act=None):
+    """x Wᵀ + b, or act(x Wᵀ + b) for a GNNEA_ACT_* code ``act`` (the act fused into the GEMM)."""
+    if act is None or act == _lib.GNNEA_ACT_IDENTITY:
+        return LinearFn.apply(x, weight, bias)
+    return LinearActFn.apply(x, weight, bias, int(act))
+
+
+def act_bwd_colsum(dy, y, act, want_db=True):
+    """(G, db): G = dy * act'(y) (y = the act's output) and db = column sums of G, one pass
+    (gnnea_act_bwd_colsum_*; db fp32, None when not wanted -- then gnnea_act_bwd alone)."""
+    if not want_db:
+        return act_bwd(dy, y, act), None
+    y = _rows(y)
+    dy = _rows(dy, y.dtype)
+    n, D = y.shape
+    L = _lib.lib()
+    g = torch.empty_like(y)
+    db = torch.empty(D, dtype=torch.float32, device=y.device)
+    ws_bytes = int(L.gnnea_act_bwd_colsum_ws_bytes(n, D))
+    ws = _gemm_ws(y.device, ws_bytes)
+    fn = L.gnnea_act_bwd_colsum_bf16 if y.dtype == torch.bfloat16 else \
+        L.gnnea_act_bwd_colsum_f32
+    with _lib.on_device(y.device):
+        check(fn(ptr(dy), _ld(dy), ptr(y), _ld(y), n, D, int(act), ptr(g), _ld(g), ptr(db),
+                 ptr(ws), ws_bytes, stream_of(y.device)))
+    return g, db
 
 
 def matmul(x, w, sliced=False):

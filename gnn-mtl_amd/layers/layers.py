@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.nn.modules.module import Module
 
-from gnnea import ops
+from gnnea import _lib, ops
 from gnnea.dist_graph import DistAdj
 from gnnea.graph import dense_of
 
@@ -118,5 +118,13 @@ class Linear(Module):
         self.act = act
 
     def forward(self, x):
+        code = ops.act_code(self.act)
+        drop = self.training and self.dropout > 0
+        # the act in the GEMM epilogue when that is the same value: always without dropout, and
+        # for relu also with it (relu(s·h) = s·relu(h) for the dropout's scale s >= 0)
+        if code is not None and code != _lib.GNNEA_ACT_IDENTITY and \
+                (not drop or code == _lib.GNNEA_ACT_RELU):
+            h = ops.linear(dense_of(x), self.linear.weight, self.linear.bias, act=code)
+            return F.dropout(h, self.dropout, training=self.training)
         h = ops.linear(dense_of(x), self.linear.weight, self.linear.bias)
         return self.act(F.dropout(h, self.dropout, training=self.training))

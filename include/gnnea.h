@@ -101,7 +101,7 @@ int gnnea_slice_pack_bf16(const void* X, int64_t ldx, int64_t n, int32_t D, void
                           int64_t sstride, void* stream);
 /* the same aggregation over 64-column bf16 slices (128 B per row piece, one cfg-5 KG slice =
  * 256 MB, the Infinity Cache's size): the layout of gnnea_slice_pack64_bf16, element (r, c) at
- * Xs[(c/64)*sstride + r*64 + c%64], sstride % 64 == 0, 8-B aligned Xs */
+ * Xs[(c/64)*sstride + r*64 + c%64], sstride % 64 == 0, 16-B aligned Xs */
 int gnnea_spmm_sliced64_bf16(const int32_t* rowptr, const int32_t* col, const float* val,
                              int32_t n_rows, int32_t D, const void* Xs, int64_t sstride, void* Y,
                              int64_t ldy, int y_dtype, int act, void* stream);
@@ -145,6 +145,24 @@ int gnnea_spmm_highway_f32(const int32_t* rowptr, const int32_t* col, const floa
 
 /* Elementwise activation backward through the output:  G = dY * act'(Y)  (n elements). */
 int gnnea_act_bwd_f32(const float* dY, const float* Y, float* G, int64_t n, int act, void* stream);
+
+/* The Linear layer's act (layers/layers.py:111-122, MLPDecoder models/decoders.py:57-63),
+ * csrc/act.hip.  Y = act(X) over n contiguous elements (Y may be X): the path of a Linear whose
+ * GEMM kernel has no fused act epilogue. */
+int gnnea_act_fwd_f32(const float* X, float* Y, int64_t n, int act, void* stream);
+int gnnea_act_fwd_bf16(const void* X, void* Y, int64_t n, int act, void* stream);
+/* The act's backward and the bias gradient in one pass (autograd of act(x·Wᵀ + b),
+ * layers/layers.py:121-122):  G = dY * act'(Y) (row-major, ld's in elements; bf16 G rounded
+ * once),  db[c] = sum_r G[r][c]  (fp32, summed from the stored G, deterministic: fixed row
+ * ranges per workgroup, fp64 fold of their partials).  Workspace: gnnea_act_bwd_colsum_ws_bytes
+ * (required).  bf16: dY, Y, G bf16; db fp32. */
+int64_t gnnea_act_bwd_colsum_ws_bytes(int64_t n_rows, int32_t D);
+int gnnea_act_bwd_colsum_f32(const float* dY, int64_t lddy, const float* Y, int64_t ldy,
+                             int64_t n_rows, int32_t D, int act, float* G, int64_t ldg, float* db,
+                             void* ws, int64_t ws_bytes, void* stream);
+int gnnea_act_bwd_colsum_bf16(const void* dY, int64_t lddy, const void* Y, int64_t ldy,
+                              int64_t n_rows, int32_t D, int act, void* G, int64_t ldg, float* db,
+                              void* ws, int64_t ws_bytes, void* stream);
 
 /* HighWay backward, elementwise part (autograd of layers/layers.py:67-76):
  *   dS_pre  = dY * g * act'(S)            (-> SpMM^T gives d hidden)
@@ -421,6 +439,13 @@ int gnnea_gemm_x3_sliced_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
                              const float* A, int64_t lda, const float* B, int64_t ldb,
                              const float* bias, float beta, float* Cs, int64_t sstride, void* ws,
                              int64_t ws_bytes, void* stream);
+/* C = act(A·op(B) + bias), beta = 0 (nn.Linear + its act, layers/layers.py:121-122): relu is
+ * applied in the epilogue of the weight-resident ring kernel (K in (288, 320], tall M), every
+ * other case runs the product and then the act in place.  Workspace as gnnea_gemm_x3_f32. */
+int gnnea_gemm_x3_act_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
+                          const float* A, int64_t lda, const float* B, int64_t ldb,
+                          const float* bias, int act, float* C, int64_t ldc, void* ws,
+                          int64_t ws_bytes, void* stream);
 /* C row-major AND a slice-major copy C2s (element (r, c) at C2s[(c/64)*sstride2 + r*64 + c%64]):
  * the second store rides the GEMM epilogue (the GAT projection: row-major for the backward,
  * slice-major for gnnea_gat_fwd_sliced_f32).  Workspace from gnnea_gemm_x3_ws_bytes. */
@@ -453,6 +478,13 @@ int64_t gnnea_gemm_bf16_ws_bytes(int64_t M, int64_t N, int64_t K);
 int gnnea_gemm_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const void* A,
                     int64_t lda, const void* B, int64_t ldb, const float* bias, float beta,
                     void* C, int64_t ldc, int c_dtype, void* ws, int64_t ws_bytes, void* stream);
+/* C = act(A·op(B) + bias), beta = 0 (the bf16 Linear + its act, layers/layers.py:121-122):
+ * relu in the weight-resident kernel's epilogue (K in (288, 320], tall M), otherwise the product
+ * then the act in place.  Workspace as gnnea_gemm_bf16. */
+int gnnea_gemm_bf16_act(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const void* A,
+                        int64_t lda, const void* B, int64_t ldb, const float* bias, int act,
+                        void* C, int64_t ldc, int c_dtype, void* ws, int64_t ws_bytes,
+                        void* stream);
 /* the bf16 GEMM writing C slice-major (bf16, 128-column slices):
  * element (r, c) at Cs[(c/128)*sstride + r*128 + c%128], sstride % 128 == 0, >= M*128 */
 int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
@@ -585,9 +617,16 @@ int gnnea_l1_terms_f32(const float* X, int64_t ldx, int32_t D, int64_t n, const 
                        const int64_t* b, double* out, void* stream);
 /* Bandwidth anchors of the bench (csrc/ubench.hip; measurement aids, no reference call):
  *   gnnea_ub_copy:   dst = src, bytes % 16 == 0, 16-B aligned, `blocks` workgroups of 256 striding;
+ *                    flags: GNNEA_UB_NT nontemporal loads / stores, GNNEA_UB_DEEP 8 (not 4)
+ *                    16-B accesses in flight per lane, GNNEA_UB_READ_ONLY loads only (dst gets one
+ *                    word per thread, blocks * 1 KB <= bytes);
  *   gnnea_ub_gather: reads the rows idx[0..n) of a row-major table (row_bytes % 8 == 0, <= 2 KB)
  *                    as 8-B chunks, writes one value per 64 rows to out[(n + 63) / 64]. */
-int gnnea_ub_copy(const void* src, void* dst, int64_t bytes, int32_t blocks, void* stream);
+#define GNNEA_UB_NT 1
+#define GNNEA_UB_DEEP 2
+#define GNNEA_UB_READ_ONLY 4
+int gnnea_ub_copy(const void* src, void* dst, int64_t bytes, int32_t blocks, int32_t flags,
+                  void* stream);
 int gnnea_ub_gather(const void* table, int64_t row_bytes, const int32_t* idx, int64_t n,
                     float* out, void* stream);
 /* out[i] = L1(A[i], B[i]) in fp64 (the diagonal of cdist(A, B)) */

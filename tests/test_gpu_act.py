@@ -1,0 +1,123 @@
+"""The Linear layer's act fused into the GEMM (layers/layers.py:111-122, the MLPDecoder's relu
+layers at models/decoders.py:57-63): gnnea_gemm_x3_act_f32 / gnnea_gemm_bf16_act (relu in the
+weight-resident kernels' epilogue, other acts in place after the product) and
+gnnea_act_bwd_colsum_* (the act's backward and the bias gradient in one pass).
+
+Checks:
+  * the fused forward equals the unfused one (the same GEMM, then F.relu) bit for bit, and the
+    fused backward's input / weight gradients equal the unfused ones bit for bit (the act's
+    derivative is 0 / 1, so G is exact either way);
+  * against an fp64 restatement (fp32 tolerance 1e-5 norm-relative for the x3 GEMM; the relu
+    branch of the backward taken from the tested output, whose elements inside the rounding band
+    of 0 are ~1e-7 of the norm);
+  * the one-pass act backward + column sums vs fp64 on row-major, strided (column block of a
+    wider buffer), unvectorised (D % 4 != 0), > 1024-wide and empty inputs.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+TOL32 = 1e-5
+
+
+def _inputs(device, M, K, N, dtype=torch.float32, seed=0):
+    g = torch.Generator(device=device).manual_seed(seed)
+    x = torch.randn(M, K, device=device, generator=g).to(dtype)
+    W = (torch.randn(N, K, device=device, generator=g) / K ** 0.5).to(dtype)
+    b = (0.1 * torch.randn(N, device=device, generator=g)).to(dtype)
+    R = torch.randn(M, N, device=device, generator=g)
+    return x, W, b, R
+
+
+def _run(fn, x, W, b, R):
+    x = x.clone().requires_grad_(True)
+    W = W.clone().requires_grad_(True)
+    b = b.clone().requires_grad_(True)
+    y = fn(x, W, b)
+    (y.float() * R).sum().backward()
+    return y.detach(), x.grad, W.grad, b.grad
+
+
+@pytest.mark.parametrize("M,K,N", [(70000, 300, 300),   # weight-resident ring: relu epilogue
+                                   (70000, 600, 300),   # k_gemm_x3p, act in place after
+                                   (1000, 300, 300)])   # small: exact-f32 GEMM + act pass
+def test_linear_relu_fused_vs_unfused_and_fp64(device, M, K, N):
+    from gnnea import _lib, ops
+    x, W, b, R = _inputs(device, M, K, N)
+    relu = _lib.GNNEA_ACT_RELU
+    yf, dxf, dWf, dbf = _run(lambda x, W, b: ops.linear(x, W, b, act=relu), x, W, b, R)
+    yu, dxu, dWu, dbu = _run(lambda x, W, b: F.relu(ops.linear(x, W, b)), x, W, b, R)
+    assert torch.equal(yf, yu)
+    assert torch.equal(dxf, dxu) and torch.equal(dWf, dWu)
+    assert rel_err(dbf.cpu(), dbu.cpu()) < 1e-6
+    x64, W64, b64, R64 = x.double(), W.double(), b.double(), R.double()
+    y64 = torch.relu(x64 @ W64.t() + b64)
+    assert rel_err(yf.cpu(), y64.cpu()) < TOL32
+    G = R64 * (yf > 0).double()  # the branch of the tested output
+    assert rel_err(dxf.cpu(), (G @ W64).cpu()) < TOL32
+    assert rel_err(dWf.cpu(), (G.t() @ x64).cpu()) < TOL32
+    assert rel_err(dbf.cpu(), G.sum(0).cpu()) < TOL32
+
+
+@pytest.mark.parametrize("act", ["elu", "tanh", "sigmoid", "leaky_relu"])
+def test_linear_other_acts_vs_fp64(device, act):
+    from gnnea import ops
+    fn = {"elu": F.elu, "tanh": torch.tanh, "sigmoid": torch.sigmoid,
+          "leaky_relu": F.leaky_relu}[act]
+    code = ops.act_code(fn)
+    x, W, b, R = _inputs(device, 70000, 300, 300, seed=3)
+    yf, dxf, dWf, dbf = _run(lambda x, W, b: ops.linear(x, W, b, act=code), x, W, b, R)
+    x64, W64, b64, R64 = (t.double().requires_grad_(True) for t in (x, W, b, R))
+    y64 = fn(x64 @ W64.t() + b64)
+    (y64 * R64).sum().backward()
+    assert rel_err(yf.cpu(), y64.detach().cpu()) < TOL32
+    assert rel_err(dxf.cpu(), x64.grad.cpu()) < 3 * TOL32
+    assert rel_err(dWf.cpu(), W64.grad.cpu()) < 3 * TOL32
+    assert rel_err(dbf.cpu(), b64.grad.cpu()) < 3 * TOL32
+
+
+def test_linear_relu_bf16_fused_vs_unfused(device):
+    """cfg-5 storage: bf16 x / W, the weight-resident bf16 kernel's relu epilogue."""
+    from gnnea import _lib, ops
+    x, W, b, R = _inputs(device, 70000, 300, 300, dtype=torch.bfloat16, seed=5)
+    relu = _lib.GNNEA_ACT_RELU
+    yf, dxf, dWf, dbf = _run(lambda x, W, b: ops.linear(x, W, b, act=relu), x, W, b, R)
+    yu, dxu, dWu, dbu = _run(lambda x, W, b: F.relu(ops.linear(x, W, b)), x, W, b, R)
+    assert yf.dtype == torch.bfloat16 and dxf.dtype == torch.bfloat16
+    assert torch.equal(yf, yu)  # relu commutes with the one bf16 rounding
+    assert torch.equal(dxf, dxu) and torch.equal(dWf, dWu)
+    G = (R.bfloat16().double() * (yf > 0).double())
+    assert rel_err(dbf.float().cpu(), G.sum(0).cpu()) < 1e-2  # the bf16 bias gradient's rounding
+
+
+@pytest.mark.parametrize("n,D,ld,dtype", [(50000, 300, 300, torch.float32),
+                                          (50000, 300, 600, torch.float32),   # column block
+                                          (3001, 30, 30, torch.float32),      # D % 4 != 0
+                                          (2000, 1100, 1100, torch.float32),  # > 1024 wide
+                                          (50000, 300, 300, torch.bfloat16),
+                                          (777, 302, 302, torch.bfloat16),
+                                          (0, 300, 300, torch.float32)])
+def test_act_bwd_colsum_vs_fp64(device, n, D, ld, dtype):
+    from gnnea import _lib, ops
+    g = torch.Generator(device=device).manual_seed(n + D)
+    buf_y = torch.randn(n, ld, device=device, generator=g).to(dtype)
+    buf_d = torch.randn(n, ld, device=device, generator=g).to(dtype)
+    y, dy = buf_y[:, :D], buf_d[:, :D]
+    for act in (_lib.GNNEA_ACT_RELU, _lib.GNNEA_ACT_TANH):
+        G, db = ops.act_bwd_colsum(dy, y, act)
+        y64, dy64 = y.double(), dy.double()
+        d = (y64 > 0).double() if act == _lib.GNNEA_ACT_RELU else 1 - y64 * y64
+        G64 = dy64 * d
+        tol = 1e-2 if dtype == torch.bfloat16 else 1e-6
+        assert G.shape == (n, D) and db.shape == (D,) and db.dtype == torch.float32
+        if n == 0:
+            assert torch.all(db == 0)
+            continue
+        assert rel_err(G.double().cpu(), G64.cpu()) < tol
+        # the column sums are of the stored G (exactly what the bias gradient sums)
+        assert rel_err(db.cpu(), G.double().sum(0).cpu()) < 1e-6
+        G2, db2 = ops.act_bwd_colsum(dy, y, act)
+        assert torch.equal(G, G2) and torch.equal(db, db2)  # deterministic

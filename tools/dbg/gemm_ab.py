@@ -63,10 +63,10 @@ for spec in sys.argv[1:]:
         env[k] = v
     r = subprocess.run([sys.executable, "-c", CHILD, lib], capture_output=True, text=True,
                        timeout=300, env=env)
-    lib = spec
     sys.stderr.write(r.stderr[-2000:])
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    out.update(json.loads(line[-1]) if line else {lib: {"rc": r.returncode}})
-    print(json.dumps({lib: out[lib]}), flush=True)
+    # the child keys its result by the library file; keyed here by the whole spec
+    out[spec] = next(iter(json.loads(line[-1]).values())) if line else {"rc": r.returncode}
+    print(json.dumps({spec: out[spec]}), flush=True)
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 json.dump(out, open(os.path.join(ROOT, "gpurun_out", "gemm_ab.json"), "w"), indent=1)
