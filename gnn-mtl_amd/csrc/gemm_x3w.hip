@@ -256,6 +256,12 @@ __global__ __launch_bounds__(64 * W3_NW, 1) void k_gemm_x3w(int M, int N, int K,
 #ifndef GNNEA_X3W_SPLIT
 #define GNNEA_X3W_SPLIT 0
 #endif
+#ifndef GNNEA_X3W_AHOT
+#define GNNEA_X3W_AHOT 0
+#endif
+#ifndef GNNEA_X3W_NOSTORE
+#define GNNEA_X3W_NOSTORE 0
+#endif
 struct W3SplitP {
   uint32_t h[4], m[4], l[4];
   __device__ __forceinline__ w3_bf16x8 vh() const { return __builtin_bit_cast(w3_bf16x8, *(const uint4*)h); }
@@ -320,6 +326,9 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
   const uint4* wlane = wl + kq * W3_NC + ml;
   uint4 f[2 * W3_KC];
   auto row_ptr = [&](int rt) {
+#if GNNEA_X3W_AHOT  // timing experiment only: every tile re-reads the first 8 row tiles (L2-hot)
+    rt = rt % 8;
+#endif
     return A + (int64_t)min(rt * BM + w * 16 + ml, M - 1) * lda;
   };
   // K in (288, 320]: steps 0..8 are inside every row (immediate offsets from the lane's base);
@@ -420,7 +429,11 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
             o.x += beta * cv.x; o.y += beta * cv.y; o.z += beta * cv.z; o.w += beta * cv.w;
           }
           if (relu) o = f4_relu(o);  // the Linear's act (layers/layers.py:121-122), uniform
+#if GNNEA_X3W_NOSTORE  // timing experiment only: no C traffic (the accumulators kept live)
+          if (o.x == 1.2345e-30f) *cp = o;
+#else
           *cp = o;
+#endif
           if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
         }
       }

@@ -1,5 +1,5 @@
 """Run one side leg of bench.py on cuda:0 and print its JSON (debug tool):
-python tools/dbg/bench_leg.py {bf16|anchors|fgw|sinkhorn|sinkhorn_large}"""
+python tools/dbg/bench_leg.py {bf16|anchors|fgw|sinkhorn|sinkhorn_large} [libgnnea_<variant>.so]"""
 import json
 import os
 import sys
@@ -7,6 +7,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
+sys.path.insert(0, os.path.join(ROOT, "gnn-mtl_amd"))
+from gnnea import _lib  # noqa: E402
+if len(sys.argv) > 2:  # an A/B build of the library, loaded instead of the default one
+    _lib.LIB_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), sys.argv[2])
 import bench  # noqa: E402
 
 dev = torch.device("cuda:0")
