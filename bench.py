@@ -382,11 +382,26 @@ def anchors(device, copy_bytes=4 << 30, n_gather=16 << 20):
         idx = torch.randint(0, rows, (n_gather,), dtype=torch.int32, device=device, generator=g)
         ms = _timed(lambda: _lib.check(L.gnnea_ub_gather(_lib.ptr(table), row_bytes,
                                                          _lib.ptr(idx), n_gather, _lib.ptr(res),
-                                                         st())), 21)
+                                                         0, st())), 21)
         out["gather_%dB" % row_bytes] = {
             "GBps": round(n_gather * row_bytes / (ms * 1e-3) / 1e9, 1), "ms": round(ms, 4),
             "table_MB": rows * row_bytes >> 20, "rows_gathered": n_gather,
             "kernel": "gnnea::k_ub_gather (8-B chunks, 4 rows in flight per wave)"}
+        del table, idx
+        torch.cuda.empty_cache()
+    # the row-major bf16 GAT passes' access shapes: 600-B rows read as 12-B windows per lane
+    # (their layout) against rows padded to 608 B read 16 B per lane (38 lanes)
+    for name, mode, row_bytes in (("gat_win12_600B", _lib.GNNEA_UB_GAT_WIN12, 600),
+                                  ("gat_v16_608B", _lib.GNNEA_UB_GAT_V16, 608)):
+        rows = 4_000_000
+        table = torch.empty(rows * row_bytes, dtype=torch.uint8, device=device).fill_(3)
+        idx = torch.randint(0, rows, (n_gather,), dtype=torch.int32, device=device, generator=g)
+        ms = _timed(lambda: _lib.check(L.gnnea_ub_gather(_lib.ptr(table), row_bytes,
+                                                         _lib.ptr(idx), n_gather, _lib.ptr(res),
+                                                         mode, st())), 21)
+        out[name] = {"GBps_row_bytes": round(n_gather * row_bytes / (ms * 1e-3) / 1e9, 1),
+                     "GBps_600B_payload": round(n_gather * 600 / (ms * 1e-3) / 1e9, 1),
+                     "ms": round(ms, 4), "table_MB": rows * row_bytes >> 20}
         del table, idx
         torch.cuda.empty_cache()
     out["peak_spec_GBps"] = HBM_PEAK_GBS

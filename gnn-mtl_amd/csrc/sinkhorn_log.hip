@@ -33,7 +33,7 @@ constexpr double kLnTrueMin = -744.4400719213812;     // log(DBL_TRUE_MIN)
 constexpr double kExpOverflow = 709.782712893384;     // exp_f64(x) == inf above
 
 struct SkWs {
-  int64_t f, g, ua, va, rowbuf, errpart, part_m, part_s, la, lb, fs, gs, fpart, ftab, total;
+  int64_t f, g, ua, va, rowbuf, errpart, part_m, part_s, la, lb, fs, gs, fpart, ftab, fbrows, fbcnt, total;
   int ncb, nsf;
 };
 
@@ -66,6 +66,8 @@ static SkWs sk_plan(int I, int J) {
   w.nsf = fused_wgs(I);
   w.fpart = o; o = al256(o + 8ll * w.nsf * J);
   w.ftab = o; o = al256(o + 8ll * kFTab);
+  w.fbrows = o; o = al256(o + 4ll * w.nsf * fused_rpw(I));  // rows listed for k_lsk_fix
+  w.fbcnt = o; o = al256(o + 4ll * w.nsf);
   w.total = o;
   return w;
 }
@@ -76,6 +78,7 @@ struct SkDev {
   double *f, *g, *ua, *va, *rowbuf, *errpart, *pm, *ps;
   double *fs, *gs;  // f, g scaled by 64 / ln 2 (KNOPP fast path)
   double *fpart, *ftab;  // fused KNOPP sweep: column partials [nsf][J], 2^(j/2048) table
+  int *fbrows, *fbcnt;   // rows each sweep workgroup left for the exact update (k_lsk_fix)
   int ncb;  // errpart slots written by the column pass of the active variant
 };
 
@@ -97,6 +100,8 @@ static SkDev sk_dev(const gnnea_sinkhorn* p) {
   d.gs = (double*)(b + w.gs);
   d.fpart = (double*)(b + w.fpart);
   d.ftab = (double*)(b + w.ftab);
+  d.fbrows = (int*)(b + w.fbrows);
+  d.fbcnt = (int*)(b + w.fbcnt);
   d.ncb = w.ncb;
   return d;
 }
@@ -293,8 +298,7 @@ __device__ __forceinline__ double sk_term(double ua, double va, double c, double
 // iterate it-1 (when (it-1)%10 == 0), then the K^T u == 0 / inf / NaN break of iteration it
 // flagged by this iteration's column pass.  Evaluated by wave 0 of every row workgroup (all
 // take the same decision); returns true when the workgroup must stop.
-// out of line (once per launch): keeps its registers out of the streaming kernels' budget
-__device__ __noinline__ bool knopp_stop(SkDev& d, int it) {
+__device__ __forceinline__ bool knopp_stop(SkDev& d, int it) {
   __shared__ int stop;
   const int lane = lane_id();
   if (wave_id() == 0) {
@@ -858,8 +862,6 @@ static SkArgs sk_args(const gnnea_sinkhorn* p) {
 // and the column fma -- against two exponentials, two running maxima and two passes over C in the
 // two-pass form.  C is read once per iteration: I J sizeof(T) bytes (0.9 GB fp32 at B = 15000).
 constexpr double kFScale = 2954.639443740597;  // 2048 / ln 2
-// out of line: called by one lane per row, its registers stay out of the sweep's budget
-__device__ __noinline__ double lsk_log(double x) { return log(x); }
 constexpr double kFLo = 0x1p-600, kFHi = 0x1p600;
 
 __global__ void k_lsk_tab(double* __restrict__ tab) {
@@ -891,7 +893,7 @@ __device__ __forceinline__ double lsk_k(double c, double inv_eps) {
 
 // PH0 (init): no row update, P(u_0, v_0) = exp(f_0 + g_0 + k) directly: the partials of
 // v_0 K^T u_0 for the first column update.
-template <typename T, int NCM, bool PH0>
+template <typename T, int NCM, bool PH0, bool SH>
 __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C, SkArgs a, SkDev d,
                                                         int it, int slot_fp, int slot_g,
                                                         int slot_fo, int rpw) {
@@ -932,6 +934,7 @@ __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C,
 #pragma unroll
   for (int k = 0; k < NCM; ++k) acc[k] = 0.0;
   const double neg_s = -a.inv_eps;
+  int nfb = 0;  // SH: rows listed for the exact update (k_lsk_fix)
   auto process = [&](const T (&kv)[NCM], int r, int par) {
     // x = (g_j + k_ij) in units of ln2 / 2048; masked terms -3e303 (exp2x -> 0).  The slice of g
     // is re-read from LDS per row (opaque to hoisting: held in registers it would cost 2 NCM)
@@ -948,6 +951,47 @@ __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C,
       }
       return;
     }
+    const bool exact = !SH;  // the running-maximum form (GNNEA_SK_FUSED=max)
+    if (SH) {
+      // shifted by f_prev: x + f_prev = log P(u_prev, v_it)_ij <= log b_j (v_it = b / K^T u_prev),
+      // so e_ij = P(u_prev, v_it)_ij needs no running maximum; s_i = u_prev (K v_it)_i
+      const double fp = d.f[(int64_t)slot_fp * a.I + r];
+      const double fps = fp * kFScale;
+      double rsum = 0.0;
+#pragma unroll
+      for (int k = 0; k < NCM; ++k) {
+        const double kn = (double)kv[k] * neg_s;
+        const double kk = kn < kExpUnderflow ? -1e300 : kn;
+        e[k] = exp2x(__builtin_fma(kk, kFScale, gl[64 * k] + fps), tab);
+        rsum += e[k];
+        if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+      rsum = wave_sum_f64(rsum);
+      if (lane == 0) reds[par][w] = rsum;
+      __syncthreads();  // double-buffered by row parity: one barrier per row
+      double sr = 0.0;
+#pragma unroll
+      for (int q = 0; q < kFW; ++q) sr += reds[par][q];  // every wave, the same order
+      // (NaN -- in C or a potential -- propagates through the fast path; the row update flags it)
+      if ((sr >= kFLo && sr <= kFHi) || sr != sr) {  // u_it / u_prev = a / s
+        const double wi = a.wa[r] / sr;
+        // f_it = f_prev + log a - log s, written by k_lsk_fix (no log in the streaming kernel)
+        if (w == 0 && lane == 0) d.rowbuf[r] = sr;
+#pragma unroll
+        for (int k = 0; k < NCM; ++k) acc[k] = __builtin_fma(e[k], wi, acc[k]);
+        return;
+      }
+      // out of range (uniform: every wave summed the same partials): the row is listed for
+      // k_lsk_fix, which writes its exact update and adds its column contributions to this
+      // workgroup's partial row after the sweep; nothing of it goes into acc
+      if (w == 0 && lane == 0) {
+        d.fbrows[(int64_t)blockIdx.x * rpw + nfb] = r;
+        d.rowbuf[r] = -1.0;  // (k_lsk_fix: listed, not a row sum)
+      }
+      ++nfb;
+      return;
+    }
+    if (!exact) return;
     double mw = -1e308;
 #pragma unroll
     for (int k = 0; k < NCM; ++k) {
@@ -979,7 +1023,7 @@ __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C,
     // f_new = log a - LSE_j(g_j + k_ij) (u = a / (K v)); P(u_new, v)_ij = e_ij 2^(M_w - M) a / s
     const double wi = exp2x(mw - M, tab) * (a.wa[r] / sr);
     if (w == 0 && lane == 0) {
-      const double fnew = a.la[r] - (M / kFScale + lsk_log(sr));
+      const double fnew = a.la[r] - (M / kFScale + log(sr));
       d.f[(int64_t)slot_fo * a.I + r] = fnew;
       if (!(fnew <= kExpOverflow)) mark_done(d.st, it, 2, (it + 1) & 1);  // u inf / NaN
     }
@@ -999,6 +1043,64 @@ __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C,
 #pragma unroll
   for (int k = 0; k < NCM; ++k)
     if (64 * k < lim) part[64 * k] = acc[k];
+  if (SH && !PH0 && tid == 0) d.fbcnt[blockIdx.x] = nfb;
+}
+
+// The exact row update for the rows a fused sweep workgroup listed (k_lsk_sweep, SH): per row in
+// list order, the LSE with a running maximum (natural units, the workgroup's waves over column
+// slices, merged in fixed order), f_new = log a - LSE, and P(u_new, v)_ij = exp(f_new + g_j +
+// k_ij) added to that workgroup's partial row.  A workgroup with an empty list returns at once.
+template <typename T>
+__global__ __launch_bounds__(64 * kFW) void k_lsk_fix(const T* __restrict__ C, SkArgs a, SkDev d,
+                                                      int it, int slot_fp, int slot_g, int slot_fo,
+                                                      int rpw) {
+  if (d.st[ST_DONE]) return;
+  {  // the row update of the workgroup's rows from their sums: f_it = f_prev + log a - log s
+    const int r0 = blockIdx.x * rpw, r1 = min(a.I, r0 + rpw);
+    bool bad = false;
+    for (int r = r0 + (int)threadIdx.x; r < r1; r += 64 * kFW) {
+      const double sr = d.rowbuf[r];
+      if (sr == -1.0) continue;  // listed: the exact update below
+      const double fnew = d.f[(int64_t)slot_fp * a.I + r] + (a.la[r] - log(sr));
+      d.f[(int64_t)slot_fo * a.I + r] = fnew;
+      bad |= !(fnew <= kExpOverflow);  // u inf / NaN
+    }
+    if (bad) mark_done(d.st, it, 2, (it + 1) & 1);
+  }
+  const int n = d.fbcnt[blockIdx.x];
+  if (n == 0) return;
+  __shared__ double fbm[kFW], fbs[kFW];
+  const int w = wave_id(), lane = lane_id();
+  const int cw = ((a.J + kFW - 1) / kFW + 63) & ~63;
+  const int c0 = w * cw, c1 = min(c0 + cw, a.J);
+  const double* __restrict__ g = d.g + (int64_t)slot_g * a.J;
+  double* __restrict__ fb = d.fpart + (int64_t)blockIdx.x * a.J;
+  for (int q = 0; q < n; ++q) {
+    const int r = d.fbrows[(int64_t)blockIdx.x * rpw + q];
+    const T* __restrict__ Cr = C + (int64_t)r * a.ldc;
+    Lse l;
+    l.init();
+    for (int c = c0 + lane; c < c1; c += 64) l.add(lsk_k((double)Cr[c], a.inv_eps) + g[c]);
+    l = wave_lse(l);
+    if (lane == 0) {
+      fbm[w] = l.m;
+      fbs[w] = l.s;
+    }
+    __syncthreads();
+    Lse t;
+    t.init();
+    for (int v = 0; v < kFW; ++v) t.merge(fbm[v], fbs[v]);
+    __syncthreads();  // fbm / fbs read by every wave before the next row reuses them
+    const double fnew = a.la[r] - t.value();  // u = a / (K v): +inf when K v == 0
+    for (int c = c0 + lane; c < c1; c += 64) {
+      const double kn = lsk_k((double)Cr[c], a.inv_eps);
+      fb[c] += kn != -INFINITY ? exp_f64(fnew + g[c] + kn) : 0.0;
+    }
+    if (w == 0 && lane == 0) {
+      d.f[(int64_t)slot_fo * a.I + r] = fnew;
+      if (!(fnew <= kExpOverflow)) mark_done(d.st, it, 2, (it + 1) & 1);  // u inf / NaN
+    }
+  }
 }
 
 // Column update of the fused sweep: S_j = sum of the workgroup partials (fixed order), the
@@ -1084,20 +1186,35 @@ static bool fused_applies(const gnnea_sinkhorn* p) {
          p->J <= (p->c_dtype == GNNEA_F64 ? kFMaxJ / 2 : kFMaxJ);
 }
 
-template <typename T, bool PH0>
-static void launch_fused_sweep(const T* C, const SkArgs& a, const SkDev& d, int it, int sfp,
-                               int sg, int sfo, hipStream_t s) {
+template <typename T, bool PH0, bool SH>
+static void launch_fused_sweep_sh(const T* C, const SkArgs& a, const SkDev& d, int it, int sfp,
+                                  int sg, int sfo, hipStream_t s) {
   const int rpw = fused_rpw(a.I), ns = fused_wgs(a.I);
   const int nc = (((a.J + kFW - 1) / kFW + 63) & ~63) / 64;
   const dim3 g(ns), b(64 * kFW);
   if (nc <= 4)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 4, PH0>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+    hipLaunchKernelGGL((k_lsk_sweep<T, 4, PH0, SH>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
   else if (nc <= 8)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 8, PH0>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+    hipLaunchKernelGGL((k_lsk_sweep<T, 8, PH0, SH>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
   else if (sizeof(T) == 8 || nc <= 16)  // (fp64 C: fused_applies bounds nc by 16)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 16, PH0>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+    hipLaunchKernelGGL((k_lsk_sweep<T, 16, PH0, SH>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
   else if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 32, PH0>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+    hipLaunchKernelGGL((k_lsk_sweep<T, 32, PH0, SH>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+}
+
+// GNNEA_SK_FUSED=max: the per-row running-maximum form of the row pass (A/B only)
+static bool fused_shift() {
+  const char* e = getenv("GNNEA_SK_FUSED");
+  return !(e && e[0] == 'm');
+}
+
+template <typename T, bool PH0>
+static void launch_fused_sweep(const T* C, const SkArgs& a, const SkDev& d, int it, int sfp,
+                               int sg, int sfo, hipStream_t s) {
+  if (PH0 || fused_shift())  // (PH0 has no row update: one instantiation)
+    launch_fused_sweep_sh<T, PH0, true>(C, a, d, it, sfp, sg, sfo, s);
+  else
+    launch_fused_sweep_sh<T, PH0, false>(C, a, d, it, sfp, sg, sfo, s);
 }
 
 // Launch configurations of the two passes (10*row + col); the path runs configuration 0, the
@@ -1178,6 +1295,9 @@ static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t 
       hipLaunchKernelGGL(k_lsk_colfin<T>, dim3(d.ncb), dim3(1024), 0, s, C, a, d,
                          fused_wgs(a.I), prev, prev, cur);
       launch_fused_sweep<T, false>(C, a, d, it, prev, cur, cur, s);
+      if (fused_shift())
+        hipLaunchKernelGGL(k_lsk_fix<T>, dim3(fused_wgs(a.I)), dim3(64 * kFW), 0, s, C, a, d, it,
+                           prev, cur, cur, fused_rpw(a.I));
     } else if (p->mode == GNNEA_SK_KNOPP) {
       launch_col<T, true>(cv, C, a, d, it, prev, prev, cur, s);  // sets d.ncb for the row pass
       launch_row<T, true>(rv, C, a, d, it, cur, cur, s);

@@ -91,6 +91,45 @@ __global__ __launch_bounds__(256) void k_ub_gather(const unsigned char* __restri
   if (lane == 0) out[w] = (float)(acc & 0xffff);
 }
 
+// The two access shapes of a row-major bf16 GAT pass over 300-column rows, as pure gathers:
+//   WIN12  600-B rows (8-B aligned), lane l reads the 12-B dword window holding its 5 columns
+//          5 l .. 5 l + 4 (byte offset (10 l) & ~3; 60 lanes), as k_gat_fwd_hg / k_gat_bwd_src_hg;
+//   !WIN12 rows padded to row_bytes % 16 == 0 (608 B), 16 B per lane (38 lanes).
+template <bool WIN12>
+__global__ __launch_bounds__(256) void k_ub_gather_gat(const unsigned char* __restrict__ table,
+                                                       int64_t row_bytes,
+                                                       const int32_t* __restrict__ idx, int64_t n,
+                                                       float* __restrict__ out) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + wave_id();
+  const int64_t base = w * 64;
+  if (base >= n) return;
+  const int lane = lane_id();
+  const int cnt = (int)min((int64_t)64, n - base);
+  const int my = idx[base + min(lane, cnt - 1)];
+  const int lanes = WIN12 ? 60 : (int)(row_bytes / 16);
+  const int off = WIN12 ? ((10 * min(lane, lanes - 1)) & ~3) : 16 * min(lane, lanes - 1);
+  uint32_t acc = 0;
+  constexpr int U = 8;
+  for (int k = 0; k < cnt; k += U) {
+    uint32_t v[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = __shfl(my, min(k + u, cnt - 1), 64);
+      const unsigned char* p = table + (int64_t)r * row_bytes + off;
+      if constexpr (WIN12) {
+        const HIP_vector_type<unsigned int, 3> t = *(const HIP_vector_type<unsigned int, 3>*)p;
+        v[u][0] = t.x; v[u][1] = t.y; v[u][2] = t.z; v[u][3] = 0;
+      } else {
+        const uint4 t = *(const uint4*)p;
+        v[u][0] = t.x; v[u][1] = t.y; v[u][2] = t.z; v[u][3] = t.w;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
+  }
+  if (lane == 0) out[w] = (float)(acc & 0xffff);
+}
+
 }  // namespace gnnea
 
 using namespace gnnea;
@@ -122,7 +161,26 @@ extern "C" int gnnea_ub_copy(const void* src, void* dst, int64_t bytes, int32_t 
 }
 
 extern "C" int gnnea_ub_gather(const void* table, int64_t row_bytes, const int32_t* idx,
-                               int64_t n, float* out, void* stream) {
+                               int64_t n, float* out, int32_t mode, void* stream) {
+  if (mode == GNNEA_UB_GAT_WIN12 || mode == GNNEA_UB_GAT_V16) {  // the GAT access shapes
+    if (n < 0 || !table || !idx || !out) return GNNEA_EINVAL;
+    if (mode == GNNEA_UB_GAT_WIN12 ? row_bytes != 600 : (row_bytes % 16 || row_bytes > 1024 ||
+                                                         row_bytes < 16))
+      return GNNEA_EINVAL;
+    if (((uintptr_t)table) & 15) return GNNEA_EALIGN;
+    if (n == 0) return 0;
+    const int64_t nb = ((n + 63) / 64 + 3) / 4;
+    if (nb >= (1ll << 31)) return GNNEA_EINVAL;
+    if (mode == GNNEA_UB_GAT_WIN12)
+      hipLaunchKernelGGL(k_ub_gather_gat<true>, dim3((unsigned)nb), dim3(256), 0,
+                         (hipStream_t)stream, (const unsigned char*)table, row_bytes, idx, n, out);
+    else
+      hipLaunchKernelGGL(k_ub_gather_gat<false>, dim3((unsigned)nb), dim3(256), 0,
+                         (hipStream_t)stream, (const unsigned char*)table, row_bytes, idx, n, out);
+    GNNEA_LAUNCH_CHECK();
+    return 0;
+  }
+  if (mode != 0) return GNNEA_EINVAL;
   if (row_bytes <= 0 || row_bytes % 8 || row_bytes > 2 * 1024 || n < 0) return GNNEA_EINVAL;
   if (n == 0) return 0;
   if (!table || !idx || !out || (((uintptr_t)table) & 7)) return GNNEA_EINVAL;

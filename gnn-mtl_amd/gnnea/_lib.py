@@ -22,6 +22,8 @@ GNNEA_ACT_TANH = 5
 GNNEA_UB_NT = 1  # gnnea_ub_copy flags (include/gnnea.h)
 GNNEA_UB_DEEP = 2
 GNNEA_UB_READ_ONLY = 4
+GNNEA_UB_GAT_WIN12 = 1  # gnnea_ub_gather modes
+GNNEA_UB_GAT_V16 = 2
 
 GNNEA_F32 = 0
 GNNEA_F64 = 1
@@ -256,7 +258,7 @@ SIGNATURES = {
     "gnnea_l1_pairs_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i32, _i32, _p, _p]),
     "gnnea_l1_terms_f32": (ctypes.c_int, [_p, _i64, _i32, _i64, _p, _p, _p, _p]),
     "gnnea_ub_copy": (ctypes.c_int, [_p, _p, _i64, _i32, _i32, _p]),
-    "gnnea_ub_gather": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _p]),
+    "gnnea_ub_gather": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _i32, _p]),
     "gnnea_l1_rank_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _p, _p]),
     "gnnea_topk_rows_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _i64, _p, _i64, _i32,
                                            _i32, _p, _p, _i32, _p, _p]),

@@ -621,14 +621,17 @@ int gnnea_l1_terms_f32(const float* X, int64_t ldx, int32_t D, int64_t n, const 
  *                    16-B accesses in flight per lane, GNNEA_UB_READ_ONLY loads only (dst gets one
  *                    word per thread, blocks * 1 KB <= bytes);
  *   gnnea_ub_gather: reads the rows idx[0..n) of a row-major table (row_bytes % 8 == 0, <= 2 KB)
- *                    as 8-B chunks, writes one value per 64 rows to out[(n + 63) / 64]. */
+ *                    as 8-B chunks (mode 0), or in the access shapes of the bf16 GAT passes
+ *                    (mode GNNEA_UB_GAT_*), writes one value per 64 rows to out[(n + 63) / 64]. */
 #define GNNEA_UB_NT 1
 #define GNNEA_UB_DEEP 2
 #define GNNEA_UB_READ_ONLY 4
 int gnnea_ub_copy(const void* src, void* dst, int64_t bytes, int32_t blocks, int32_t flags,
                   void* stream);
+#define GNNEA_UB_GAT_WIN12 1 /* 600-B rows, a 12-B window per lane (the bf16 GAT passes) */
+#define GNNEA_UB_GAT_V16 2   /* rows padded to a multiple of 16 B, 16 B per lane */
 int gnnea_ub_gather(const void* table, int64_t row_bytes, const int32_t* idx, int64_t n,
-                    float* out, void* stream);
+                    float* out, int32_t mode, void* stream);
 /* out[i] = L1(A[i], B[i]) in fp64 (the diagonal of cdist(A, B)) */
 int gnnea_l1_pairs_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int32_t n,
                        int32_t D, double* out, void* stream);
