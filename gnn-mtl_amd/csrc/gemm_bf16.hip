@@ -886,7 +886,12 @@ static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
 // while the current tile is multiplied.  Workgroup b owns column tile (b / 8) % ntn and the row
 // stream of the blocks b and b + 8 * (ntn - 1)... (so the column tiles of the same rows run on
 // one XCD, sharing its L2 for the activations).
+#ifndef GNNEA_BW_STAGE  // A/B builds only: 0 = the bf16 output stored from the accumulators
+#define GNNEA_BW_STAGE 1
+#endif
 constexpr int kBwCols = 160, kBwKC = 20;  // column tile, max k-steps (K <= 320)
+// a wave's staged bf16 output tile: 32 rows of 320 B, row stride padded by 16 B (bank spread)
+constexpr int kBwStageRS = 2 * kBwCols + 16, kBwStageBytes = 32 * kBwStageRS;
 
 __global__ __launch_bounds__(256) void k_pack_bf16w(const bf16_t* __restrict__ B, int64_t ldb,
                                                     int b_nk, int N, int K, int kc, int ntn,
@@ -921,6 +926,10 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
   // the tile's bias in LDS: a global load in the epilogue would wait (vmcnt counts in order)
   // for the next tile's activation loads issued before it
   __shared__ __attribute__((aligned(16))) float bsh[kBwCols];
+  // bf16 C: each wave's 32 x 160 output tile staged here, then written as row-contiguous 16-B
+  // pieces (the accumulator layout puts a lane's 8 B in 32 different rows per store instruction)
+  constexpr bool kStage = std::is_same<TC, bf16_t>::value && GNNEA_BW_STAGE;
+  __shared__ __attribute__((aligned(16))) unsigned char stage[kStage ? 4 * kBwStageBytes : 16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int kh = lane >> 5, li = lane & 31;
   const int b = blockIdx.x;
@@ -985,6 +994,38 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
     }
     // lane: output row m, columns n0 + 32 t + 8 g + 4 kh + (0..3) = acc[t][4 g .. 4 g + 3]
     const int m = rt * 128 + w * 32 + li;
+    if constexpr (kStage) {
+      unsigned char* sw = stage + w * kBwStageBytes;
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = 32 * t + 8 * g + 4 * kh;
+          float4 o = make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2],
+                                 acc[t][4 * g + 3]);
+          const float4 bv = *(const float4*)(bsh + c);
+          o.x += bv.x; o.y += bv.y; o.z += bv.z; o.w += bv.w;
+          if (relu) o = f4_relu(o);
+          *(uint2*)(sw + li * kBwStageRS + 2 * c) =
+              make_uint2((uint32_t)f32_to_bf16(o.x) | ((uint32_t)f32_to_bf16(o.y) << 16),
+                         (uint32_t)f32_to_bf16(o.z) | ((uint32_t)f32_to_bf16(o.w) << 16));
+        }
+      }
+      // (the wave's own LDS writes are ordered before its reads; no other wave touches sw)
+      const int r0 = rt * 128 + w * 32;
+#pragma unroll
+      for (int i = 0; i < 10; ++i) {  // 32 rows x 20 pieces of 8 columns: 10 per lane
+        const int q = lane + 64 * i, row = q / 20, pc = q - 20 * row;
+        const int mr = r0 + row, n = n0 + 8 * pc;
+        if (mr < M && n < N) {
+          const uint4 v = *(const uint4*)(sw + row * kBwStageRS + 16 * pc);
+          bf16_t* c = (bf16_t*)C + c_index_bf(mr, n, ldc, cs);
+          if (n + 8 <= N) *(uint4*)c = v;  // (dword-aligned: ldc, cs even)
+          else *(uint2*)c = make_uint2(v.x, v.y);  // N % 4 == 0: the piece's first 4 columns
+        }
+      }
+      return;
+    }
     if (m >= M) return;
 #pragma unroll
     for (int t = 0; t < 5; ++t) {
