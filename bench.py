@@ -140,36 +140,37 @@ def sinkhorn_rate(device, B=3000, reg=0.01, n0=100, n1=1100, variant=None):
 
 
 def sinkhorn_large(device):
-    """B = 15000 through the scaling form with the fp64 K resident (variant 0: one sweep per
-    iteration, I * J * 8 bytes of K) and through the log-domain path (variant 1): the fused
-    KNOPP sweep (fp32 C read once per iteration, I * J * 4 bytes, one exponential per element;
-    csrc/sinkhorn_log.hip k_lsk_sweep) and, beside it, the two-pass form it replaced
+    """B = 15000 through the default path (GNNEA_SK_AUTO): KNOPP (utils/ot_loss.sinkhorn) on the
+    fused log-domain sweep (fp32 C read once per iteration, I * J * 4 bytes, one exponential per
+    element; csrc/sinkhorn_log.hip k_lsk_sweep), STAB on the scaling form with the fp64 K
+    resident; beside it the scaling form for KNOPP too (variant 0: one sweep over the fp64 K per
+    iteration, I * J * 8 bytes) and the two-pass log-domain form the fused sweep replaced
     (GNNEA_SK_FUSED=0: C read twice, two exponentials per element): marginal iters/s."""
     B = 15000
     r = sinkhorn_rate(device, B=B, n0=20, n1=120)
-    k_bytes = B * B * 8
-    r["kernels"] = "scaling form, fp64 K resident in HBM (k_sk_sweep, wide: column scaling in LDS)"
-    r["bytes_per_iter"] = k_bytes
-    r["GBps_knopp"] = round(r["iters_per_s"]["ot_loss.sinkhorn"] * k_bytes / 1e9, 1)
-    r["bound"] = ("HBM: the K stream (%.2f GB per iteration; %.0f iters/s at 8 TB/s)"
-                  % (k_bytes / 1e9, 8e12 / k_bytes))
-    lg = sinkhorn_rate(device, B=B, n0=20, n1=120, variant=1)
     c_bytes = B * B * 4
-    knopp = lg["iters_per_s"]["ot_loss.sinkhorn"]
-    r["logdomain"] = {
-        "iters_per_s": lg["iters_per_s"], "bytes_per_iter_knopp": c_bytes,
-        "GBps_knopp": round(knopp * c_bytes / 1e9, 1),
-        "kernels_knopp": "fused sweep k_lsk_sweep + k_lsk_colfin (one pass over fp32 C, one "
-                         "table exponential per element)",
-        "bound_knopp": "HBM: the fp32 C stream (%.2f GB per iteration; %.0f iters/s at 8 TB/s) "
-                       "against 2.25e8 fp64 exponentials per iteration" % (c_bytes / 1e9,
-                                                                             8e12 / c_bytes)}
+    knopp = r["iters_per_s"]["ot_loss.sinkhorn"]
+    r["kernels_knopp"] = ("fused log-domain sweep k_lsk_sweep + k_lsk_colfin + k_lsk_fix (one pass "
+                          "over fp32 C, one table exponential per element)")
+    r["bytes_per_iter_knopp"] = c_bytes
+    r["GBps_knopp"] = round(knopp * c_bytes / 1e9, 1)
+    r["bound_knopp"] = ("the fp32 C stream (%.2f GB per iteration; %.0f iters/s at 8 TB/s) against "
+                        "2.25e8 fp64 table exponentials per iteration" % (c_bytes / 1e9,
+                                                                          8e12 / c_bytes))
+    sc = sinkhorn_rate(device, B=B, n0=20, n1=120, variant=0)
+    k_bytes = B * B * 8
+    r["scaling_form"] = {
+        "iters_per_s": sc["iters_per_s"], "path": sc["path"], "bytes_per_iter": k_bytes,
+        "GBps_knopp": round(sc["iters_per_s"]["ot_loss.sinkhorn"] * k_bytes / 1e9, 1),
+        "kernels": "fp64 K resident in HBM (k_sk_sweep, wide: column scaling in LDS)",
+        "bound": "HBM: the K stream (%.2f GB per iteration; %.0f iters/s at 8 TB/s)"
+                 % (k_bytes / 1e9, 8e12 / k_bytes)}
     os.environ["GNNEA_SK_FUSED"] = "0"
     try:
         two = sinkhorn_rate(device, B=B, n0=20, n1=120, variant=1)
     finally:
         os.environ.pop("GNNEA_SK_FUSED", None)
-    r["logdomain"]["two_pass_iters_per_s"] = two["iters_per_s"]
+    r["logdomain_two_pass_iters_per_s"] = two["iters_per_s"]
     return r
 
 

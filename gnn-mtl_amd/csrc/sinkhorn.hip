@@ -988,7 +988,9 @@ static int res_num_cus() {
 }
 
 static bool res_applies(const gnnea_sinkhorn* p) {
-  if (p->mode != GNNEA_SK_KNOPP || p->variant != 0 || p->J > kMaxJ) return false;
+  if (p->mode != GNNEA_SK_KNOPP || (p->variant != 0 && p->variant != GNNEA_SK_AUTO) ||
+      p->J > kMaxJ)
+    return false;
   if (p->flags & GNNEA_SK_NO_ONCHIP) return false;
   const char* e = getenv("GNNEA_SK_RESIDENT");
   if (e && e[0] == '0') return false;
@@ -1113,8 +1115,9 @@ __global__ __launch_bounds__(256) void k_sk_shard_colfin(SkArgs a, SkDev d,
 
 namespace skscale {
 
-bool shard_ok(const gnnea_sinkhorn* p) {
-  return p && p->variant == 0 && p->mode == GNNEA_SK_KNOPP && p->J <= kMaxJ && sk_valid(p);
+bool shard_ok(const gnnea_sinkhorn* p) {  // (GNNEA_SK_AUTO: the scaling form when sharded)
+  return p && (p->variant == 0 || p->variant == GNNEA_SK_AUTO) && p->mode == GNNEA_SK_KNOPP &&
+         p->J <= kMaxJ && sk_valid(p);
 }
 int64_t shard_ws_bytes(int I, int J) {
   if (J > kMaxJ) return 0;
@@ -1214,10 +1217,17 @@ int init(const gnnea_sinkhorn* p, void* stream);
 int iterate(const gnnea_sinkhorn* p, int first, int count, void* stream);
 int finish(const gnnea_sinkhorn* p, void* plan, int plan_dtype, int64_t ldp, double* row_sum,
            double* col_sum, void* stream);
+bool fused_ok(const gnnea_sinkhorn* p);
 }  // namespace sklog
 
-// variant 1, or J beyond the sweep's register tiles: log-domain passes, no I x J workspace
-static bool use_log(const gnnea_sinkhorn* p) { return p->variant == 1 || p->J > kMaxJ; }
+// variant 1, or J beyond the sweep's register tiles: log-domain passes, no I x J workspace;
+// GNNEA_SK_AUTO: KNOPP that the on-chip kernel cannot hold takes the fused log-domain sweep (one
+// pass over C per iteration against the resident K's I*J*8 bytes per iteration, and no K build)
+static bool use_log(const gnnea_sinkhorn* p) {
+  if (p->variant == 1 || p->J > kMaxJ) return true;
+  return p->variant == GNNEA_SK_AUTO && p->mode == GNNEA_SK_KNOPP && sk_valid(p) &&
+         !res_applies(p) && sklog::fused_ok(p);
+}
 
 }  // namespace gnnea
 

@@ -1186,6 +1186,8 @@ static bool fused_applies(const gnnea_sinkhorn* p) {
          p->J <= (p->c_dtype == GNNEA_F64 ? kFMaxJ / 2 : kFMaxJ);
 }
 
+bool fused_ok(const gnnea_sinkhorn* p) { return p && fused_applies(p); }
+
 template <typename T, bool PH0, bool SH>
 static void launch_fused_sweep_sh(const T* C, const SkArgs& a, const SkDev& d, int it, int sfp,
                                   int sg, int sfo, hipStream_t s) {

@@ -37,6 +37,7 @@ GNNEA_SK_STATUS_BYTES = 256
 GNNEA_SK_PATH_SWEEP, GNNEA_SK_PATH_ONCHIP, GNNEA_SK_PATH_LOG = 0, 1, 2
 GNNEA_SK_ST_TIMEOUT = 16  # status word: an inter-workgroup wait of k_sk_res timed out
 GNNEA_SK_NO_ONCHIP = 1  # gnnea_sinkhorn.flags: never the on-chip persistent path
+GNNEA_SK_AUTO = 3  # gnnea_sinkhorn.variant: on chip / fused log-domain sweep / scaling form
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32

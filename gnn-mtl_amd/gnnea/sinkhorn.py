@@ -13,8 +13,10 @@ from ._lib import SinkhornProblem, check, ptr, stream_of
 
 ST_DONE, ST_ITERS, ST_REASON, ST_SLOT = 0, 1, 2, 3
 # path of solve() calls that do not choose one: 0 = scaling form with the resident fp64 K
-# (falls back to 1 above J = 16384), 1 = fused log-domain passes (no I x J workspace)
-DEFAULT_VARIANT = 0
+# (falls back to 1 above J = 16384), 1 = log-domain passes (no I x J workspace; KNOPP: the fused
+# sweep), 3 = GNNEA_SK_AUTO: KNOPP on chip where it fits, else the fused log-domain sweep (one
+# pass over C per iteration), the STAB family as 0
+DEFAULT_VARIANT = _lib.GNNEA_SK_AUTO
 SD_ERR, SD_TPREV, SD_LOSS, SD_TNEW = 8, 9, 10, 12  # GNNEA_SK_SD_* (include/gnnea.h)
 MAX_BATCH = 100  # iterations enqueued between two host polls of the status block, at most
 

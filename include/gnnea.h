@@ -539,15 +539,21 @@ typedef struct gnnea_sinkhorn {
   double tol;       /* stopThr (KNOPP) or tol */
   int max_iter;     /* numItermax / numIterMax */
   int iters_run;    /* iterations enqueued so far (read by gnnea_sinkhorn_finish) */
-  int variant;      /* 0: scaling form with the fp64 K resident in ws (J <= 16384);
-                       1: fused log-domain passes recomputing every term from C (no I*J state,
-                       any J; used automatically above J = 16384) */
+  int variant;      /* 0: scaling form with the fp64 K resident in ws (J <= 16384; KNOPP on
+                          chip where the blocks fit the CUs);
+                       1: log-domain passes recomputing every term from C (no I*J state, any J;
+                          used automatically above J = 16384; KNOPP: the fused sweep, one pass
+                          over C per iteration, for J <= 16384 fp32 / 8192 fp64 C);
+                       GNNEA_SK_AUTO (3, the Python default): KNOPP on chip where it fits, else
+                          the fused log-domain sweep, else variant 0 / 1 as above; the STAB
+                          family as variant 0 (sharded KNOPP: as variant 0) */
   int flags;        /* GNNEA_SK_NO_ONCHIP: never take the on-chip cooperative KNOPP path (the
                        host's retry after an inter-workgroup wait timed out); 0 otherwise */
   void* ws;         /* device workspace of gnnea_sinkhorn_ws_bytes(I, J) bytes */
 } gnnea_sinkhorn;
 
 #define GNNEA_SK_NO_ONCHIP 1
+#define GNNEA_SK_AUTO 3
 
 int64_t gnnea_sinkhorn_ws_bytes(int I, int J);
 int gnnea_sinkhorn_init(const gnnea_sinkhorn* prob, void* stream);

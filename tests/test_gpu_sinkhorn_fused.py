@@ -123,3 +123,29 @@ def test_fused_breaks(device, monkeypatch, what):
     f = torch.isfinite(r2.plan)
     assert torch.equal(torch.isfinite(rf.plan), f)
     assert rel_err(rf.plan[f].cpu(), r2.plan[f].cpu()) < 1e-12
+
+
+def test_auto_routing(device, monkeypatch):
+    """GNNEA_SK_AUTO (the default): KNOPP on chip where the blocks fit the CUs, else the fused
+    log-domain sweep; the STAB family on the scaling form; fp64 C past the fused sweep's limit
+    (J > 8192) on the scaling form too.  The fused result equals the explicit variant 1's."""
+    from gnnea import _lib
+    from gnnea.sinkhorn import solve
+    monkeypatch.delenv("GNNEA_SK_FUSED", raising=False)
+    monkeypatch.delenv("GNNEA_SK_RESIDENT", raising=False)
+    rng = np.random.default_rng(21)
+
+    def run(I, J, mode, dtype, variant=None):
+        M = torch.from_numpy(rng.uniform(0, 1, (I, J))).to(device=device, dtype=dtype)
+        a = torch.ones(I, dtype=torch.float64, device=device)
+        b = torch.full((J,), I / J, dtype=torch.float64, device=device)
+        if mode == _lib.GNNEA_SK_STAB:
+            a, b = a / I, b / I
+        return M, a, b, solve(mode, M, a, b, 0.02, 1e-9, 60, variant=variant)
+    assert run(500, 400, _lib.GNNEA_SK_KNOPP, torch.float32)[3].path == "onchip"
+    M, a, b, r = run(6000, 5000, _lib.GNNEA_SK_KNOPP, torch.float32)
+    assert r.path == "logdomain"
+    r1 = solve(_lib.GNNEA_SK_KNOPP, M, a, b, 0.02, 1e-9, 60, variant=1)
+    assert (r.iters, r.reason) == (r1.iters, r1.reason) and torch.equal(r.plan, r1.plan)
+    assert run(3000, 2000, _lib.GNNEA_SK_STAB, torch.float64)[3].path == "sweep"
+    assert run(300, 9000, _lib.GNNEA_SK_KNOPP, torch.float64)[3].path in ("sweep", "onchip")
