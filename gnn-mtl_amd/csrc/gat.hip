@@ -59,24 +59,34 @@ __global__ __launch_bounds__(256) void k_gat_scores(const T* __restrict__ Hm, in
     a1[t] = hl.ok[t] ? a[hh * 2 * dh + d] : 0.f;
     a2[t] = hl.ok[t] ? a[hh * 2 * dh + dh + d] : 0.f;
   }
+  // four rows per round, every element load of the four issued before any is used (one row's
+  // loads in flight per wave left the pass latency-bound); the per-row arithmetic is unchanged
   const int nw = gridDim.x * 4;
-  for (int row = blockIdx.x * 4 + wave_id(); row < n_rows; row += nw) {
-    const T* x = Hm + (int64_t)row * ldh;
-    float xv[EPL];
+  for (int base = blockIdx.x * 4 + wave_id(); base < n_rows; base += 4 * nw) {
+    float xv[4][EPL];
 #pragma unroll
-    for (int t = 0; t < EPL; ++t) xv[t] = to_f32<T>(x[hl.c[t]]);
-    float p[2] = {0.f, 0.f};
+    for (int k = 0; k < 4; ++k) {
+      const T* x = Hm + (int64_t)min(base + k * nw, n_rows - 1) * ldh;
 #pragma unroll
-    for (int t = 0; t < EPL; ++t) {
-      const float v = hl.ok[t] ? xv[t] : 0.f;
-      p[0] = fmaf(v, a1[t], p[0]);
-      p[1] = fmaf(v, a2[t], p[1]);
+      for (int t = 0; t < EPL; ++t) xv[k][t] = to_f32<T>(x[hl.c[t]]);
     }
-    const float r = grp_sum<2, L::LPH>(p, lane);
-    const int o = lane % L::LPH;
-    if (hl.h < H) {
-      if (o == grp_lane<2, L::LPH>(0)) s1[(int64_t)row * H + hl.h] = r;
-      if (o == grp_lane<2, L::LPH>(1)) s2[(int64_t)row * H + hl.h] = r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = base + k * nw;
+      if (row >= n_rows) break;  // uniform
+      float p[2] = {0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < EPL; ++t) {
+        const float v = hl.ok[t] ? xv[k][t] : 0.f;
+        p[0] = fmaf(v, a1[t], p[0]);
+        p[1] = fmaf(v, a2[t], p[1]);
+      }
+      const float r = grp_sum<2, L::LPH>(p, lane);
+      const int o = lane % L::LPH;
+      if (hl.h < H) {
+        if (o == grp_lane<2, L::LPH>(0)) s1[(int64_t)row * H + hl.h] = r;
+        if (o == grp_lane<2, L::LPH>(1)) s2[(int64_t)row * H + hl.h] = r;
+      }
     }
   }
 }
@@ -255,6 +265,69 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
     const int64_t o = (int64_t)row * H + lane;
     const float dv = den[o];
     rec[o] = make_float4(s1[o], mrow[o], dv > 0.f ? 1.f / dv : 0.f, hsel<H>(cp, lane));
+  }
+}
+
+// The same prep over FOUR rows per wave (the default): every dY / Y load of the four rows issued
+// before any is used (k_gat_bwd_prep keeps one row's loads in flight per wave); per row the same
+// element arithmetic and the same wave-sum order, so G and rec are bit-identical to it.
+template <int ACT, int H, int NCH, typename T>
+__global__ __launch_bounds__(256) void k_gat_bwd_prep4(int n_rows, int D, int dh,
+                                                       const typename Vec4<T>::raw* __restrict__ dY,
+                                                       const typename Vec4<T>::raw* __restrict__ Y,
+                                                       int64_t ld4,
+                                                       const float* __restrict__ s1,
+                                                       const float* __restrict__ mrow,
+                                                       const float* __restrict__ den,
+                                                       typename Vec4<T>::raw* __restrict__ G,
+                                                       float4* __restrict__ rec) {
+  typedef typename Vec4<T>::raw R;
+  const int r0 = (blockIdx.x * 4 + wave_id()) * 4;
+  if (r0 >= n_rows) return;
+  const int lane = lane_id();
+  R vd[4][NCH], vy[4][NCH];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int64_t rw = min(r0 + rr, n_rows - 1);
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+      const int c4 = min(lane + 64 * q, (D + 3) / 4 - 1);
+      vd[rr][q] = dY[rw * ld4 + c4];
+      vy[rr][q] = Y[rw * ld4 + c4];
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int row = r0 + rr;
+    if (row >= n_rows) break;  // uniform
+    float cp[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) cp[h] = 0.f;
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+      const int c4 = lane + 64 * q;
+      if (4 * c4 >= D) continue;
+      const float4 dy = Vec4<T>::get(vd[rr][q]);
+      const float4 y = Vec4<T>::get(vy[rr][q]);
+      const float ys[4] = {y.x, y.y, y.z, y.w};
+      float gs[4] = {dy.x, dy.y, dy.z, dy.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int c = 4 * c4 + t;
+        gs[t] = c < D ? gs[t] * act_grad_from_out<ACT>(ys[t]) : 0.f;
+        const int hh = c < D ? c / dh : H;
+#pragma unroll
+        for (int h = 0; h < H; ++h) cp[h] += (hh == h) ? gs[t] * ys[t] : 0.f;
+      }
+      G[(int64_t)row * ld4 + c4] = Vec4<T>::put(make_float4(gs[0], gs[1], gs[2], gs[3]));
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) cp[h] = wave_sum(cp[h]);
+    if (lane < H) {
+      const int64_t o = (int64_t)row * H + lane;
+      const float dv = den[o];
+      rec[o] = make_float4(s1[o], mrow[o], dv > 0.f ? 1.f / dv : 0.f, hsel<H>(cp, lane));
+    }
   }
 }
 
@@ -455,6 +528,82 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(const int32_t* __restrict__
     dH[(int64_t)row * lddh4 + c4] = Vec4<T>::put(make_float4(o[0], o[1], o[2], o[3]));
   }
   if (lane < H) ds1[(int64_t)row * H + lane] = hsel<H>(p, lane);
+}
+
+// The same pass with FOUR destination rows per wave (the default): k_gat_bwd_dst is a chain of
+// dependent loads per row (rowptr -> tpos -> dzT -> the dH row's read-modify-write) with one row
+// in flight per wave.  Here lane group g (16 lanes) walks row r0 + g's edges (ds1 partials summed
+// over the group in fixed order: lane-strided edges, then xor 1, 2, 4, 8), and the wave then
+// updates the four dH rows with all of their loads issued before any is used.
+template <int H, int NCH, typename T>
+__global__ __launch_bounds__(256) void k_gat_bwd_dst4(const int32_t* __restrict__ rowptr,
+                                                      const int64_t* __restrict__ tpos,
+                                                      int n_rows, int D, int dh,
+                                                      const float* __restrict__ dzT,
+                                                      const float* __restrict__ a,
+                                                      typename Vec4<T>::raw* __restrict__ dH,
+                                                      int64_t lddh4,
+                                                      float* __restrict__ ds1) {
+  const int r0 = (blockIdx.x * 4 + wave_id()) * 4;
+  if (r0 >= n_rows) return;
+  const int lane = lane_id(), g = lane >> 4, l16 = lane & 15;
+  const bool live = r0 + g < n_rows;
+  const int row = live ? r0 + g : n_rows - 1;
+  const int beg = rowptr[row], end = live ? rowptr[row + 1] : beg;
+  float p[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) p[h] = 0.f;
+  for (int e = beg + l16; e < end; e += 16) {
+    const int64_t t = tpos[e];
+    if constexpr (H == 4) {
+      const float4 v = *(const float4*)(dzT + t * 4);
+      p[0] += v.x; p[1] += v.y; p[2] += v.z; p[3] += v.w;
+    } else {
+#pragma unroll
+      for (int h = 0; h < H; ++h) p[h] += dzT[t * H + h];
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) p[h] += __shfl_xor(p[h], o, 64);
+  }
+  if (live && l16 < H) ds1[(int64_t)row * H + l16] = hsel<H>(p, l16);
+  // the four rows' dH pieces: every load first
+  typedef typename Vec4<T>::raw R;
+  R v[4][NCH];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int rw = min(r0 + rr, n_rows - 1);
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+      const int c4 = min(lane + 64 * q, (D + 3) / 4 - 1);
+      v[rr][q] = dH[(int64_t)rw * lddh4 + c4];
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    if (r0 + rr >= n_rows) break;  // uniform
+    float ph[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) ph[h] = __shfl(p[h], 16 * rr, 64);
+#pragma unroll
+    for (int q = 0; q < NCH; ++q) {
+      const int c4 = lane + 64 * q;
+      if (4 * c4 >= D) continue;
+      const float4 x = Vec4<T>::get(v[rr][q]);
+      float o[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int c = 4 * c4 + t;
+        if (c < D) {
+          const int h = c / dh;
+          o[t] += hsel<H>(ph, h) * a[h * 2 * dh + (c - h * dh)];
+        }
+      }
+      dH[(int64_t)(r0 + rr) * lddh4 + c4] = Vec4<T>::put(make_float4(o[0], o[1], o[2], o[3]));
+    }
+  }
 }
 
 static bool ok_ld(int64_t ld, int D) { return ld % 4 == 0 && ld >= ((D + 3) / 4) * 4; }
@@ -1017,11 +1166,20 @@ static int gat_bwd_prep_t(int32_t n_rows, int heads, int d_head, const T* dY, co
   if (!ok_ld(ld, D) || !alv<T>(dY) || !alv<T>(Y) || !alv<T>(G) || !alv<float>(rec))
     return GNNEA_EALIGN;
   if (act != GNNEA_ACT_IDENTITY && act != GNNEA_ACT_RELU) return GNNEA_EINVAL;
-  const int nb = div_up(n_rows, 4);
+  static const bool four = [] {  // A/B comparison only (GNNEA_GAT_PREP4=0: a row per wave)
+    const char* e = getenv("GNNEA_GAT_PREP4");
+    return !(e && e[0] == '0');
+  }();
+  const int nb = four ? div_up(n_rows, 16) : div_up(n_rows, 4);
 #define CALL_A(A, HH, NN)                                                                      \
-  hipLaunchKernelGGL((k_gat_bwd_prep<A, HH, NN, T>), dim3(nb), dim3(256), 0, s, n_rows, D,    \
-                     d_head, (const R*)dY, (const R*)Y, ld / 4, s1, m, den, (R*)G,            \
-                     (float4*)rec)
+  if (four)                                                                                    \
+    hipLaunchKernelGGL((k_gat_bwd_prep4<A, HH, NN, T>), dim3(nb), dim3(256), 0, s, n_rows, D, \
+                       d_head, (const R*)dY, (const R*)Y, ld / 4, s1, m, den, (R*)G,          \
+                       (float4*)rec);                                                          \
+  else                                                                                         \
+    hipLaunchKernelGGL((k_gat_bwd_prep<A, HH, NN, T>), dim3(nb), dim3(256), 0, s, n_rows, D,  \
+                       d_head, (const R*)dY, (const R*)Y, ld / 4, s1, m, den, (R*)G,          \
+                       (float4*)rec)
 #define CALL(HH, NN)                                                        \
   case HH * 8 + NN:                                                         \
     if (act == GNNEA_ACT_RELU) CALL_A(GNNEA_ACT_RELU, HH, NN);              \
@@ -1097,11 +1255,19 @@ static int gat_bwd_dst_t(const int32_t* rowptr, const int64_t* tpos, int32_t n_r
   const int D = heads * d_head, D4 = (D + 3) / 4;
   if (!rowptr || !tpos || !dzT || !a || !dH || !ds1) return GNNEA_EINVAL;
   if (!ok_ld(lddh, D) || !alv<T>(dH)) return GNNEA_EALIGN;
-  const int nb = div_up(n_rows, 4);
+  static const bool four = [] {  // A/B comparison only (GNNEA_GAT_DST4=0: a row per wave)
+    const char* e = getenv("GNNEA_GAT_DST4");
+    return !(e && e[0] == '0');
+  }();
+  const int nb = four ? div_up(n_rows, 16) : div_up(n_rows, 4);
 #define CALL(HH, NN)                                                                          \
   case HH * 8 + NN:                                                                           \
-    hipLaunchKernelGGL((k_gat_bwd_dst<HH, NN, T>), dim3(nb), dim3(256), 0, s, rowptr, tpos,   \
-                       n_rows, D, d_head, dzT, a, (R*)dH, lddh / 4, ds1);                     \
+    if (four)                                                                                 \
+      hipLaunchKernelGGL((k_gat_bwd_dst4<HH, NN, T>), dim3(nb), dim3(256), 0, s, rowptr,      \
+                         tpos, n_rows, D, d_head, dzT, a, (R*)dH, lddh / 4, ds1);             \
+    else                                                                                      \
+      hipLaunchKernelGGL((k_gat_bwd_dst<HH, NN, T>), dim3(nb), dim3(256), 0, s, rowptr, tpos, \
+                         n_rows, D, d_head, dzT, a, (R*)dH, lddh / 4, ds1);                   \
     break;
   GNNEA_GAT_DISPATCH(CALL);
 #undef CALL
