@@ -342,44 +342,13 @@ __device__ __forceinline__ void td_read8(uint32_t addr, float (&x)[8]) {
   });
 }
 
-// BS (default; GNNEA_TA_BSPLIT=0 for A/B): B's tile is split ONCE per k-step by the whole
-// workgroup into three bf16 plane images (k_gemm_ta's [k][n] layout, 30 KB after the two DMA
-// stages) and its fragments are read transposed from them (ds_read_b64_tr_b16), instead of being
-// split by each of the four waves that read it: 1 x 160 instead of 4 x 160 split columns per k-row
-// (A stays split at the read, 2 x 320).  One more barrier per step.
-template <int OFF>
-__device__ __forceinline__ ta_v4s td_tr_o(uint32_t addr) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
-  ta_v4s v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF));
-  return v;
-}
-template <int OFF>  // one plane's fragment: image rows 8 g + q (+ 4)
-__device__ __forceinline__ ta_bf16x8 td_plane_frag(uint32_t addr) {
-  const ta_v4s lo = td_tr_o<OFF>(addr);
-  const ta_v4s hi = td_tr_o<OFF + 4 * TA_RSB>(addr);
-  return __builtin_bit_cast(ta_bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-__device__ __forceinline__ TdTriple td_plane_triple(uint32_t addr) {
-  TdTriple t;
-  t.h = td_plane_frag<0>(addr);
-  t.m = td_plane_frag<TA_IMG_B>(addr);
-  t.l = td_plane_frag<2 * TA_IMG_B>(addr);
-  return t;
-}
-__device__ __forceinline__ void td_ds_write64(uint32_t addr, uint32_t lo, uint32_t hi) {
-  asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(make_uint2(lo, hi)) : "memory");
-}
-
-template <bool BS>
 __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
                                                           const float* __restrict__ A,
                                                           int64_t lda,
                                                           const float* __restrict__ B,
                                                           int64_t ldb, int kps, int tiles_n,
                                                           float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TD_STAGE +
-                                                               (BS ? 3 * TA_IMG_B : 0)];
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TD_STAGE];
   const int t_id = xcd_remap(blockIdx.x, gridDim.x);
   const int tn = t_id % tiles_n, split = t_id / tiles_n;
   const int n0 = tn * TA_NP;
@@ -444,13 +413,6 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
     b_ad[i] = base + TD_IMG_A + 8 * g * TD_RSB + (((n >> 2) ^ ((g & 1) << 2)) << 4) + (n & 3) * 4;
   }
 
-  // BS: the plane images and this lane's transposed-read offset in them (k_gemm_ta's b_at)
-  const uint32_t bpl = base + 2 * TD_STAGE;
-  const uint32_t bp_lane = bpl + (8 * g + ((lane >> 2) & 3)) * TA_RSB;
-  auto bp_at = [&](int j) -> uint32_t {
-    return bp_lane + ((2 * (wn * 80 + 16 * j + 4 * (lane & 3))) ^ ((g & 1) << 5));
-  };
-
   issue(0, 0);
   for (int s = 0; s < nsteps; ++s) {
     const int buf = s & 1;
@@ -462,39 +424,6 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
     const int k0 = kb + s * TA_BK;
     const int kval = ke - k0 - 8 * g;  // valid rows of this lane's eight (>= 8 but at the tail)
     const bool tail = k0 + TA_BK > ke;  // uniform
-    if constexpr (BS) {
-      // B's raw [32][160] fp32 image -> h / m / l bf16 planes: 1,280 16-B chunks, <= 3 per thread
-      // (rows past the split's end written as zeros); the planes of step s - 1 were last read
-      // before this step's barrier
-      constexpr int kCh = TA_BK * (TA_NP / 4);
-      f32x4_t v[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int idx = min(tid + TA_NT * q, kCh - 1);
-        const int row = idx / (TA_NP / 4), c = idx - row * (TA_NP / 4);
-        v[q] = ds_read128f(base + so + TD_IMG_A + row * TD_RSB +
-                           ((c ^ (((row >> 3) & 1) << 2)) << 4));
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int idx = tid + TA_NT * q;
-        if (idx < kCh) {
-          const int row = idx / (TA_NP / 4), c = idx - row * (TA_NP / 4);
-          const bool live = k0 + row < ke;
-          uint32_t h0, m0, l0, h1, m1, l1;
-          x3_split_pair(live ? v[q][0] : 0.f, live ? v[q][1] : 0.f, h0, m0, l0);
-          x3_split_pair(live ? v[q][2] : 0.f, live ? v[q][3] : 0.f, h1, m1, l1);
-          const uint32_t d = bpl + row * TA_RSB + ((c * 8) ^ (((row >> 3) & 1) << 5));
-          td_ds_write64(d, h0, h1);
-          td_ds_write64(d + TA_IMG_B, m0, m1);
-          td_ds_write64(d + 2 * TA_IMG_B, l0, l1);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // the planes of step s are complete
-      asm volatile("" ::: "memory");
-    }
 
     // A fragment i + 1 (the last time: B's first) in flight while fragment i is split
     TdTriple at[5];
@@ -502,15 +431,11 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
     td_read8<TD_RSA>(a_ad[0] + so, xa[0]);
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-      if (i + 1 < 5) {
+      if (i + 1 < 5)
         td_read8<TD_RSA>(a_ad[i + 1] + so, xa[(i + 1) & 1]);
-        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-      } else if constexpr (!BS) {
+      else
         td_read8<TD_RSB>(b_ad[0] + so, xb);
-        asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
       float (&x)[8] = xa[i & 1];
       if (tail) {
 #pragma unroll
@@ -518,23 +443,15 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
       }
       at[i] = td_split(x);
     }
-    TdTriple bnx;
-    if constexpr (BS) bnx = td_plane_triple(bp_at(0));
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      TdTriple bt;
-      if constexpr (BS) {
-        bt = bnx;
-        if (j + 1 < 5) bnx = td_plane_triple(bp_at(j + 1));  // in flight under the MFMAs
-      } else {
-        if (tail) {
+      if (tail) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) xb[e] = e < kval ? xb[e] : 0.f;
-        }
-        bt = td_split(xb);
-        if (j + 1 < 5) td_read8<TD_RSB>(b_ad[j + 1] + so, xb);  // in flight under the MFMAs
+        for (int e = 0; e < 8; ++e) xb[e] = e < kval ? xb[e] : 0.f;
       }
+      const TdTriple bt = td_split(xb);
+      if (j + 1 < 5) td_read8<TD_RSB>(b_ad[j + 1] + so, xb);  // in flight under the MFMAs
       // product-major: five independent accumulators between two dependent MFMAs (each
       // accumulator still sums its six products in k_gemm_ta's order)
 #pragma unroll
@@ -621,18 +538,9 @@ int gemm_ta_launch(int64_t M, int64_t N, int64_t K, const T* A, int64_t lda, con
   // every split must own rows (kps rounding can leave the last ones empty): trim the grid
   const int used = (int)((K + kps - 1) / kps);
   float* slab = (float*)ws;
-  static const bool bsplit = [] {  // A/B comparison only (GNNEA_TA_BSPLIT=0: split at the read)
-    const char* e = getenv("GNNEA_TA_BSPLIT");
-    return !(e && e[0] == '0');
-  }();
-  if (std::is_same<T, float>::value && ta_x3d_on() && bsplit)
-    hipLaunchKernelGGL(k_gemm_ta_x3d<true>, dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M,
-                       (int)N, (int)K, (const float*)A, lda, (const float*)B, ldb, kps, tiles_n,
-                       slab);
-  else if (std::is_same<T, float>::value && ta_x3d_on())
-    hipLaunchKernelGGL(k_gemm_ta_x3d<false>, dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M,
-                       (int)N, (int)K, (const float*)A, lda, (const float*)B, ldb, kps, tiles_n,
-                       slab);
+  if (std::is_same<T, float>::value && ta_x3d_on())
+    hipLaunchKernelGGL(k_gemm_ta_x3d, dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M, (int)N,
+                       (int)K, (const float*)A, lda, (const float*)B, ldb, kps, tiles_n, slab);
   else
     hipLaunchKernelGGL((k_gemm_ta<T>), dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M, (int)N,
                        (int)K, A, lda, B, ldb, kps, tiles_n, slab);
