@@ -886,8 +886,12 @@ static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
 // while the current tile is multiplied.  Workgroup b owns column tile (b / 8) % ntn and the row
 // stream of the blocks b and b + 8 * (ntn - 1)... (so the column tiles of the same rows run on
 // one XCD, sharing its L2 for the activations).
-#ifndef GNNEA_BW_STAGE  // A/B builds only: 0 = the bf16 output stored from the accumulators
-#define GNNEA_BW_STAGE 1
+// GNNEA_BW_STAGE=1 (A/B builds only) stages a wave's bf16 output tile in LDS and stores 16-B
+// row pieces instead; measured 6-8% SLOWER on the 2M x 300 x 300 projection (0.939 vs 0.887 ms,
+// relu 0.907 vs 0.841 ms; profiles/r04_gemm_bf16_epilogue_ab.json), so the default stores the
+// 8-B pieces straight from the accumulators.
+#ifndef GNNEA_BW_STAGE
+#define GNNEA_BW_STAGE 0
 #endif
 constexpr int kBwCols = 160, kBwKC = 20;  // column tile, max k-steps (K <= 320)
 // a wave's staged bf16 output tile: 32 rows of 320 B, row stride padded by 16 B (bank spread)

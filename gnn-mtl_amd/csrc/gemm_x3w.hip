@@ -579,10 +579,254 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring2(int M, int N, int K, int
   }
 }
 
+// ---- k_gemm_f16x2_ring: the same projection through a TWO-way fp16 split, three products ----
+// The x3 forms above spend six bf16 MFMAs per fp32 product (h·l, m·m, l·h, h·m, m·h, h·h).  fp16
+// carries 11 significant bits to bf16's 8, so two fp16 pieces hold 22 bits of an fp32 operand:
+//   x = hi + lo,  hi = f16(x·s),  lo = f16(x·s - hi)            (|lo| <= 2^-11 |hi|)
+// and a·w = (hi_a hi_w + hi_a lo_w + lo_a hi_w) / (s_a t_w) up to lo_a·lo_w and lo's rounding, each
+// <= 2^-22 |a||w| (x3 mode 2's dropped products are at 2^-21; fp32 accumulation's K·2^-24 bound
+// dominates both at K ~ 300).  fp16's exponent range is what needs care: every activation ROW
+// and every weight COLUMN is scaled by a power of two s = 2^(14 - floor(log2 max|x|)) so that its
+// largest element lands in [2^14, 2^15) (the scaling and its inverse are exact); elements more
+// than 2^24 below their row's maximum become fp16 subnormals (absolute error <= 2^-25 of the
+// row's maximum there, nothing relative to the dot product's magnitude).  Non-finite inputs
+// propagate (an inf row maximum gives inf / NaN outputs, as the fp32 product would).  Half the
+// MFMAs of the x3 ring, same fp16 rate as bf16 (v_mfma_f32_16x16x32_f16).
+// Structure: the ring kernel's (80-column weight tile resident in LDS, now two fp16 planes =
+// 100 KB; 8 waves, 16 rows each; column tiles of a row stream on one XCD), except that a tile's
+// activations are split WHOLE at its start (the row maximum needs all of them): the 20 raw
+// quads -> 10 hi + 10 lo fragments, then the next tile's 20 quads are issued into the freed
+// registers, a full tile of MFMAs ahead of their use.
+typedef _Float16 f2_f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f2_f16x2 __attribute__((ext_vector_type(2)));
+
+// exponent of the scale: e = floor(log2 m) clamped to [-112, 127] (m = 0 / fp32-subnormal:
+// -112, so the scale stays a normal fp32 2^(14 - e) <= 2^126; inf / NaN: 127)
+__device__ __forceinline__ int f2_exp(float m) {
+  const int e = (int)((__builtin_bit_cast(uint32_t, m) >> 23) & 255u) - 127;
+  return e < -112 ? -112 : (e > 127 ? 127 : e);
+}
+__device__ __forceinline__ float f2_pow2(int e) {  // 2^e for e in [-126, 127]
+  return __builtin_bit_cast(float, (uint32_t)(e + 127) << 23);
+}
+// (x0, x1) -> packed fp16 pairs hi = f16(x s), lo = f16(x s - hi): four v_fma_mix (the scaling
+// inside the fused multiply-add, the residual read back from hi's fp16 halves); the compiler's own
+// form recomputes hi for the residual (seven instructions per pair)
+__device__ __forceinline__ uint32_t f2_split_pair(float x0, float x1, float s, uint32_t& lo) {
+  uint32_t h, l;
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(h) : "v"(x0), "v"(s));
+  asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(h) : "v"(x1), "v"(s));
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(x0), "v"(s), "v"(h));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "+v"(l) : "v"(x1), "v"(s), "v"(h));
+  lo = l;
+  return h;
+}
+// mx = max(mx, |a|, |b|) in one instruction (fmaxf's NaN canonicalisation of loaded values would
+// add one v_max per element)
+__device__ __forceinline__ float f2_max3abs(float mx, float a, float b) {
+  asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(a), "v"(b));
+  return mx;
+}
+
+// column scales of the weight operand: tsc[n] = 2^(14 - e_n), tinv[n] = 2^(e_n - 14) over
+// W_op[n][0..K) (n < ntn * 80; past N: 1)
+__global__ __launch_bounds__(256) void k_colscale_f16x2(const float* __restrict__ B, int64_t ldb,
+                                                        int b_nk, int N, int K, int nn,
+                                                        float* __restrict__ tsc,
+                                                        float* __restrict__ tinv) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= nn) return;
+  float m = 0.f;
+  if (n < N)
+    for (int k = 0; k < K; ++k)
+      m = fmaxf(m, fabsf(b_nk ? B[(int64_t)n * ldb + k] : B[(int64_t)k * ldb + n]));
+  const int e = f2_exp(m);
+  tsc[n] = f2_pow2(14 - e);
+  tinv[n] = f2_pow2(e - 14);
+}
+
+// P[nt][p][s][kq][n][8], p = 0 hi / 1 lo: the x3 pack's layout (kc k-steps, nc-column tiles)
+// with two fp16 planes of the column-scaled weight
+__global__ __launch_bounds__(256) void k_pack_f16x2(const float* __restrict__ B, int64_t ldb,
+                                                    int b_nk, int N, int K, int ntn, int kc,
+                                                    int nc, const float* __restrict__ tsc,
+                                                    uint16_t* __restrict__ P) {
+  const int64_t per_plane = (int64_t)kc * 4 * nc * 8;
+  const int64_t total = (int64_t)ntn * per_plane;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int e = (int)(t & 7);
+    int64_t r = t >> 3;
+    const int n = (int)(r % nc);
+    r /= nc;
+    const int kq = (int)(r & 3);
+    r >>= 2;
+    const int s = (int)(r % kc);
+    const int nt = (int)(r / kc);
+    const int col = nt * nc + n, k = 32 * s + 16 * (e >> 2) + 4 * kq + (e & 3);
+    float x = 0.f;
+    if (col < N && k < K) x = (b_nk ? B[(int64_t)col * ldb + k] : B[(int64_t)k * ldb + col]) * tsc[col];
+    const _Float16 h = (_Float16)x;
+    const _Float16 l = (_Float16)(x - (float)h);
+    uint16_t* dst = P + (int64_t)nt * 2 * per_plane + (t - (int64_t)nt * per_plane);
+    dst[0] = __builtin_bit_cast(uint16_t, h);
+    dst[per_plane] = __builtin_bit_cast(uint16_t, l);
+  }
+}
+
+// KC k-steps of 32 (K in (32 (KC - 1), 32 KC]), NC-column weight tiles.  The k dimension runs in
+// CHUNKS of up to 10 steps, each with its own row scale and accumulators (K = 600: two): a
+// chunk's 20 raw quads are split whole once they have landed, and the next chunk's (this tile's
+// or the next tile's first) are issued into the freed registers, one chunk of MFMAs ahead.
+template <int KC, int NC>
+__global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, int ntn,
+                                                         const float* __restrict__ A, int64_t lda,
+                                                         const uint16_t* __restrict__ P,
+                                                         const float* __restrict__ tinv_g,
+                                                         const float* __restrict__ bias,
+                                                         float* __restrict__ C, int64_t ldc,
+                                                         int64_t cs, float* __restrict__ C2,
+                                                         int64_t cs2, float beta, int relu) {
+  constexpr int NW = 8, BM = 16 * NW, NJ = NC / 16;
+  constexpr int PL = KC * 4 * NC;      // 16-B units per plane of a tile
+  constexpr int NCH = (KC + 9) / 10;   // k-chunks
+  static_assert(NC % 16 == 0 && NCH <= 2, "tile shape");
+  __shared__ __attribute__((aligned(16))) uint4 wl[2 * PL];
+  __shared__ __attribute__((aligned(16))) float bsh[NC];
+  __shared__ __attribute__((aligned(16))) float tsh[NC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x;
+  const int nt = (b / 8) % ntn;
+  const int rs = (b / (8 * ntn)) * 8 + b % 8, nrs = (int)gridDim.x / ntn;
+  const int n0 = nt * NC;
+  {  // the resident weight tile, its column scales' inverses and the bias
+    const uint4* src = (const uint4*)(P + (int64_t)nt * 2 * PL * 8);
+    for (int i = tid; i < 2 * PL; i += 64 * NW) wl[i] = src[i];
+    if (tid < NC) {
+      bsh[tid] = bias && n0 + tid < N ? bias[n0 + tid] : 0.f;
+      tsh[tid] = tinv_g[n0 + tid];
+    }
+  }
+  __syncthreads();
+  const int tm = (M + BM - 1) / BM;
+  const int kq = lane >> 4, ml = lane & 15;
+  const uint4* wlane = wl + kq * NC + ml;
+  uint4 f[20];
+  auto row_ptr = [&](int rt) { return A + (int64_t)min(rt * BM + w * 16 + ml, M - 1) * lda; };
+  // chunk c's quads: steps 10 c .. ; steps before the last are inside every row, the last one's
+  // quads past K read the row's first quad (valid) and are zeroed at use
+  auto load_chunk = [&](const float* p, const int c) {
+#pragma unroll
+    for (int i = 0; i < 20; ++i) {
+      const int st = 10 * c + i / 2, j = i & 1;
+      if (st < KC - 1) {
+        f[i] = *(const uint4*)(p + 4 * kq + 32 * st + 16 * j);
+      } else if (st == KC - 1) {
+        const int k = 32 * st + 16 * j + 4 * kq;
+        f[i] = *(const uint4*)(p + (k < K ? k : 0));
+      }
+    }
+  };
+  if (rs < tm) load_chunk(row_ptr(rs), 0);
+  for (int rt = rs; rt < tm; rt += nrs) {
+    w3_f32x4 acc[NCH][NJ];
+    float rinv[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int s0 = 10 * c, ns = KC - s0 < 10 ? KC - s0 : 10;
+      __builtin_amdgcn_sched_barrier(0);
+      if (s0 + ns == KC) {
+        const int k = 32 * (KC - 1) + 4 * kq, i = 2 * (KC - 1 - s0);
+        if (k >= K) f[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (k + 16 >= K) f[i + 1] = make_uint4(0u, 0u, 0u, 0u);
+      }
+      // the row's maximum over the chunk: this lane's elements, then the row's k-quarter lanes
+      float mx = 0.f;
+#pragma unroll
+      for (int q = 0; q < 2 * ns; ++q) {
+        mx = f2_max3abs(mx, __builtin_bit_cast(float, f[q].x), __builtin_bit_cast(float, f[q].y));
+        mx = f2_max3abs(mx, __builtin_bit_cast(float, f[q].z), __builtin_bit_cast(float, f[q].w));
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16));
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const int er = f2_exp(mx);
+      const float sr = f2_pow2(14 - er);
+      rinv[c] = f2_pow2(er - 14);
+      uint32_t ah[20][2], al[20][2];
+#pragma unroll
+      for (int q = 0; q < 2 * ns; ++q) {
+        ah[q][0] = f2_split_pair(__builtin_bit_cast(float, f[q].x),
+                                 __builtin_bit_cast(float, f[q].y), sr, al[q][0]);
+        ah[q][1] = f2_split_pair(__builtin_bit_cast(float, f[q].z),
+                                 __builtin_bit_cast(float, f[q].w), sr, al[q][1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // the next chunk's activations, a chunk of MFMAs ahead (past the last tile: none)
+      if (c + 1 < NCH)
+        load_chunk(row_ptr(rt), c + 1);
+      else if (rt + nrs < tm)
+        load_chunk(row_ptr(rt + nrs), 0);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[c][j] = w3_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < ns; ++s) {
+        const f2_f16x8 xh = __builtin_bit_cast(
+            f2_f16x8, make_uint4(ah[2 * s][0], ah[2 * s][1], ah[2 * s + 1][0], ah[2 * s + 1][1]));
+        const f2_f16x8 xl = __builtin_bit_cast(
+            f2_f16x8, make_uint4(al[2 * s][0], al[2 * s][1], al[2 * s + 1][0], al[2 * s + 1][1]));
+        const uint4* wp = wlane + (s0 + s) * 4 * NC;
+#pragma unroll
+        for (int jn = 0; jn < NJ; ++jn) {
+          __builtin_amdgcn_sched_barrier(0);
+          const f2_f16x8 wh = __builtin_bit_cast(f2_f16x8, wp[16 * jn]);
+          const f2_f16x8 wlo = __builtin_bit_cast(f2_f16x8, wp[PL + 16 * jn]);
+          w3_f32x4& cc = acc[c][jn];
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wlo, xh, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, cc, 0, 0, 0);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const int m = rt * BM + w * 16 + ml;
+    if (m < M) {
+#pragma unroll
+      for (int jn = 0; jn < NJ; ++jn) {
+        const int c = 16 * jn + 4 * kq;
+        int n = n0 + c;
+        asm volatile("" : "+v"(n));  // (see k_gemm_x3w_ring)
+        if (n < N) {
+          const float4 bv = *(const float4*)(bsh + c);
+          const float4 tv = *(const float4*)(tsh + c);
+          // unscaled exactly (powers of two, the column's first), the chunks summed, the bias
+          float o4[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float t = i == 0 ? tv.x : i == 1 ? tv.y : i == 2 ? tv.z : tv.w;
+            float v = acc[0][jn][i] * t * rinv[0];
+            if constexpr (NCH > 1) v += acc[1][jn][i] * t * rinv[1];
+            o4[i] = v;
+          }
+          float4 o = make_float4(o4[0] + bv.x, o4[1] + bv.y, o4[2] + bv.z, o4[3] + bv.w);
+          float4* cp = (float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63)));
+          if (beta != 0.f) {
+            const float4 cv = *cp;
+            o.x += beta * cv.x; o.y += beta * cv.y; o.z += beta * cv.z; o.w += beta * cv.w;
+          }
+          if (relu) o = f4_relu(o);
+          *cp = o;
+          if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
+        }
+      }
+    }
+  }
+}
+
 // ---- host side ----
 
-// A/B comparison only: GNNEA_X3W=0 k_gemm_x3p, 1 k_gemm_x3w, 2 (default) k_gemm_x3w_ring,
-// 3 k_gemm_x3w_ring2
+// GNNEA_X3W: 0 k_gemm_x3p, 1 k_gemm_x3w, 2 (default) k_gemm_x3w_ring, 3 k_gemm_x3w_ring2,
+// 4 k_gemm_f16x2_ring (two fp16 pieces, three products)
 static int x3w_mode() {
   static const int mode = [] {
     const char* e = getenv("GNNEA_X3W");
@@ -592,30 +836,110 @@ static int x3w_mode() {
 }
 static bool x3w_on() { return x3w_mode() != 0; }
 
-int64_t gemm_x3w_ws_bytes(int64_t N) {
-  return (N + W3_NC - 1) / W3_NC * W3_TILE_BYTES;
+// the f16x2 forms: K in (288, 320] on 80-column tiles, K in (576, 608] (the HighWay input
+// gradient [dh | dg]·[W ; K_gᵀ], K = 600) on 64-column tiles (2 planes x 19 steps x 64 columns =
+// 152 KB of LDS)
+constexpr int F2_NC_WIDE = 64, F2_KC_WIDE = 19;
+static bool f16x2_k(int64_t K, int* kc, int* nc) {
+  if (K > 32 * (W3_KC - 1) && K <= 32 * W3_KC) {
+    *kc = W3_KC, *nc = W3_NC;
+    return true;
+  }
+  if (K > 32 * (F2_KC_WIDE - 1) && K <= 32 * F2_KC_WIDE) {
+    *kc = F2_KC_WIDE, *nc = F2_NC_WIDE;
+    return true;
+  }
+  return false;
+}
+static int64_t f16x2_ws_bytes(int64_t N, int kc, int nc) {
+  const int64_t ntn = (N + nc - 1) / nc;
+  return ntn * (2ll * kc * 4 * nc * 16 + 2ll * nc * 4);
+}
+
+int64_t gemm_x3w_ws_bytes(int64_t N) {  // the largest of the forms
+  const int64_t x3 = (N + W3_NC - 1) / W3_NC * W3_TILE_BYTES;
+  const int64_t f2 = f16x2_ws_bytes(N, F2_KC_WIDE, F2_NC_WIDE);
+  return x3 > f2 ? x3 : f2;
 }
 
 bool gemm_x3w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda, const void* A,
                       float beta, int64_t ldc, int64_t cs, const void* C, const void* C2,
                       int64_t cs2, int act) {
-  // beta != 0 and a fused act only on the ring forms (modes 2 and 3)
+  // beta != 0 and a fused act only on the ring forms (modes 2 - 4)
+  int kc, nc;
+  const bool kok = x3w_mode() == 4 ? f16x2_k(K, &kc, &nc)
+                                   : (K > 32 * (W3_KC - 1) && K <= 32 * W3_KC);
   return x3w_on() && !trans_a && ((beta == 0.f && act == GNNEA_ACT_IDENTITY) || x3w_mode() >= 2) &&
          (act == GNNEA_ACT_IDENTITY || act == GNNEA_ACT_RELU) && A && C && M >= 65536 &&
-         M < (1ll << 31) &&
-         N >= 64 && N <= 4096 && N % 4 == 0 && K > 32 * (W3_KC - 1) && K <= 32 * W3_KC && K % 4 == 0 &&
+         M < (1ll << 31) && N >= 64 && N <= 4096 && N % 4 == 0 && kok && K % 4 == 0 &&
          lda >= K && lda % 4 == 0 && (((uintptr_t)A) & 15) == 0 &&
          ldc % 4 == 0 && cs % 4 == 0 && (((uintptr_t)C) & 15) == 0 &&
          (!C2 || (cs2 % 4 == 0 && (((uintptr_t)C2) & 15) == 0));
+}
+
+static int cu_count() {
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  return ncu;
+}
+
+// persistent grid: a multiple of 8 * ntn workgroups (column tiles of a row stream 8 apart)
+static int ring_grid(int ntn, int64_t M, int bm) {
+  const int unit = 8 * ntn;
+  const int64_t tm = (M + bm - 1) / bm;
+  int grid = cu_count() / unit * unit;
+  if (grid < unit) grid = unit;
+  if ((int64_t)grid / ntn > tm) grid = (int)((tm + 7) / 8 * 8 * ntn);
+  return grid;
+}
+
+static int f16x2_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                        const float* B, int64_t ldb, const float* bias, float* C, int64_t ldc,
+                        int64_t cs, float* C2, int64_t cs2, void* ws, int64_t ws_bytes,
+                        hipStream_t s, float beta, int relu) {
+  int kc, nc;
+  if (!f16x2_k(K, &kc, &nc)) return GNNEA_EINVAL;
+  if (ws_bytes < f16x2_ws_bytes(N, kc, nc)) return GNNEA_EWORKSPACE;
+  const int ntn = (int)((N + nc - 1) / nc);
+  float* tsc = (float*)((char*)ws + (int64_t)ntn * 2 * kc * 4 * nc * 16);  // after the planes
+  float* tinv = tsc + (int64_t)ntn * nc;
+  const int nn = ntn * nc;
+  hipLaunchKernelGGL(k_colscale_f16x2, dim3((nn + 255) / 256), dim3(256), 0, s, B, ldb,
+                     trans_b ? 1 : 0, (int)N, (int)K, nn, tsc, tinv);
+  GNNEA_LAUNCH_CHECK();
+  const int64_t tot = (int64_t)ntn * kc * 4 * nc * 8;
+  const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
+  hipLaunchKernelGGL(k_pack_f16x2, dim3(nb), dim3(256), 0, s, B, ldb, trans_b ? 1 : 0, (int)N,
+                     (int)K, ntn, kc, nc, (const float*)tsc, (uint16_t*)ws);
+  GNNEA_LAUNCH_CHECK();
+  const int grid = ring_grid(ntn, M, 128);
+  if (kc == W3_KC)
+    hipLaunchKernelGGL((k_gemm_f16x2_ring<W3_KC, W3_NC>), dim3(grid), dim3(512), 0, s, (int)M,
+                       (int)N, (int)K, ntn, A, lda, (const uint16_t*)ws, (const float*)tinv, bias,
+                       C, ldc, cs, C2, cs2, beta, relu);
+  else
+    hipLaunchKernelGGL((k_gemm_f16x2_ring<F2_KC_WIDE, F2_NC_WIDE>), dim3(grid), dim3(512), 0, s,
+                       (int)M, (int)N, (int)K, ntn, A, lda, (const uint16_t*)ws,
+                       (const float*)tinv, bias, C, ldc, cs, C2, cs2, beta, relu);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
 }
 
 int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                     const float* B, int64_t ldb, const float* bias, float* C, int64_t ldc,
                     int64_t cs, float* C2, int64_t cs2, void* ws, int64_t ws_bytes,
                     hipStream_t s, float beta, int act) {
-  const int ntn = (int)((N + W3_NC - 1) / W3_NC);
   const int relu = act == GNNEA_ACT_RELU ? 1 : 0;
   if (!ws || ws_bytes < gemm_x3w_ws_bytes(N)) return GNNEA_EWORKSPACE;
+  if (x3w_mode() == 4)
+    return f16x2_launch(trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, cs, C2, cs2, ws, ws_bytes,
+                        s, beta, relu);
+  const int ntn = (int)((N + W3_NC - 1) / W3_NC);
   bf16_t* P = (bf16_t*)ws;
   {
     const int64_t tot = (int64_t)ntn * W3_PLANE * 8;
@@ -625,21 +949,8 @@ int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A
                        (int)K, ntn, P);
     GNNEA_LAUNCH_CHECK();
   }
-  static const int ncu = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    return n;
-  }();
-  // persistent grid: a multiple of 8 * ntn workgroups (column tiles of a row stream 8 apart)
   const bool ring = x3w_mode() == 2, ring2 = x3w_mode() == 3;
-  const int unit = 8 * ntn;
-  const int bm = ring2 ? 256 : ring ? 128 : W3_BM;
-  const int64_t tm = (M + bm - 1) / bm;
-  int grid = ncu / unit * unit;
-  if (grid < unit) grid = unit;
-  if ((int64_t)grid / ntn > tm) grid = (int)((tm + 7) / 8 * 8 * ntn);
+  const int grid = ring_grid(ntn, M, ring2 ? 256 : ring ? 128 : W3_BM);
   if (ring2)
     hipLaunchKernelGGL(k_gemm_x3w_ring2, dim3(grid), dim3(512), 0, s, (int)M, (int)N, (int)K,
                        ntn, A, lda, P, bias, C, ldc, cs, C2, cs2, beta, relu);

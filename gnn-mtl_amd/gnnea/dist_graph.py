@@ -126,6 +126,22 @@ class HipEngine:
         table of the hidden rows: gate_pre from the shard's own slice-major gate table."""
         from . import ops
         L = _lib.lib()
+        if table.dtype == torch.bfloat16:
+            # a bf16 slice table [n, 128] is a row-major matrix of w columns (ld 128), and so
+            # is the shard's own gate slice: the row-major HighWay kernel over the column block
+            W = table.shape[1]
+            gq = gates[c0 // W]
+            with _lib.on_device(table.device):
+                for r0, r1 in csr.row_blocks():
+                    _lib.check(L.gnnea_spmm_highway_bf16(
+                        ops._off32(csr.rowptr, r0), _lib.ptr(csr.col), _lib.ptr(csr.val),
+                        r1 - r0, w, _lib.ptr(table), W, ops._off(gq, r0), W,
+                        None if bias_gate is None else
+                        ops._off(ops._featc(bias_gate, torch.float32).view(1, -1), 0, c0),
+                        ops._off(resid, r0, c0), resid.stride(0), ops._off(out, r0, c0),
+                        out.stride(0), ops._off(S, r0, c0), ops._off(G, r0, c0), S.stride(0),
+                        int(act), _lib.stream_of(table.device)))
+            return out
         with _lib.on_device(table.device):
             for r0, r1 in csr.row_blocks():
                 _lib.check(L.gnnea_spmm_highway_sliced_f32(
@@ -140,7 +156,26 @@ class HipEngine:
     def highway_bwd_slices(self, dy, S, G, resid, act, want_dresid, dgate):
         """(dS slice-major, dresid): dS = dy·g·act'(S), dgate written into ``dgate``."""
         from . import ops
-        return ops.highway_bwd_sliced(dy, S, G, resid, act, want_dresid, dgate)
+        if S.dtype != torch.bfloat16:
+            return ops.highway_bwd_sliced(dy, S, G, resid, act, want_dresid, dgate)
+        # bf16: each 128-column slice table of dS is a row-major [rows, 128] matrix, written
+        # by the row-major elementwise backward over the slice's column block
+        S = ops._featc(S)
+        dy, G, resid = (ops._featc(t, S.dtype) for t in (dy, G, resid))
+        N, D = S.shape
+        dSs = ops.sliced_empty(N, D, S.device, S.dtype)
+        W = dSs.shape[2]
+        dres = torch.empty_like(S) if want_dresid else None
+        L = _lib.lib()
+        with _lib.on_device(S.device):
+            for q in range(dSs.shape[0]):
+                c0 = q * W
+                _lib.check(L.gnnea_highway_bwd_ld_bf16(
+                    ops._off(dy, 0, c0), ops._off(S, 0, c0), ops._off(G, 0, c0),
+                    ops._off(resid, 0, c0), S.stride(0), N, min(W, D - c0), _lib.ptr(dSs[q]), W,
+                    ops._off(dgate, 0, c0), ops._ld(dgate),
+                    ops._off(dres, 0, c0), D, int(act), _lib.stream_of(S.device)))
+        return dSs, dres
 
     # ---- the staged GAT halo (64-column slices of the head-concatenated projection) -------
     def gat_slice_w(self, dtype):
@@ -365,13 +400,14 @@ class DistAdj:
     def staged(self, t, highway=False):
         """The halo of ``t`` moves slice by slice, overlapped with the per-slice aggregation:
         every row shard (g > 1) whose engine has the slice operations; fp32 / bf16 with whole
-        4-column chunks (the HighWay epilogue: fp32)."""
+        4-column chunks (the HighWay tail too: the fp32 sliced kernel, or for bf16 the
+        row-major kernel over each 128-column slice table)."""
         from . import exchange
         if (self.part.g == 1 or not exchange.STAGED or not hasattr(self.engine, "slice_w")
                 or t.shape[1] % 4):
             return False
         if isinstance(self.engine, HipEngine):
-            return t.dtype == torch.float32 or (t.dtype == torch.bfloat16 and not highway)
+            return t.dtype in (torch.float32, torch.bfloat16)
         return True
 
     def stages(self, D, dtype):

@@ -393,6 +393,32 @@ def _worker(rank, world, port, mode, q, staged=True):
                     return margin_loss(l1((x, adj_full))[0], *idx, t_, k_)
                 return sharded_margin_loss(l1((x, adj))[0], adj, *idx, t_, k_)
             tol = 1e-5
+        elif mode == "gpu_bf16":
+            # bf16 storage through the DistAdj hooks: the aggregation and the fused HighWay
+            # tail (HaloHighwayFn; staged: the 128-column bf16 slice tables, a partial last
+            # slice at D = 132) against an fp32 torch restatement on the whole graph
+            dev = torch.device("cuda:0")
+            torch.cuda.set_device(dev)
+            X, Rw = X.bfloat16().to(dev), Rw.float().to(dev)
+            dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev)
+            torch.manual_seed(0)
+            W1 = (torch.randn(D, D) / D ** 0.5).bfloat16().to(dev)
+            Kg = (torch.randn(D, D) / D ** 0.5).bfloat16().to(dev)
+            bg = (0.1 * torch.randn(D)).to(dev)
+            params = [p.requires_grad_() for p in (W1, Kg)]
+            A = torch.sparse_coo_tensor(torch.from_numpy(np.stack([R, C])).long(),
+                                        torch.from_numpy(V).float(), (2 * N_KG, 2 * N_KG)).to(dev)
+
+            def model(x, adj):
+                if adj is None:
+                    xf, Wf, Kf = x.float(), W1.float(), Kg.float()
+                    y1 = torch.relu(torch.sparse.mm(A, xf @ Wf.t()))
+                    g = torch.sigmoid(y1 @ Kf + bg)
+                    return g * torch.relu(torch.sparse.mm(A, y1 @ Wf.t())) + (1 - g) * y1
+                y1 = adj.aggregate(x @ W1.t(), F.relu)
+                y2 = adj.highway(y1 @ W1.t(), y1 @ Kg, y1, bg, F.relu)
+                return adj.gather_rows(y2)
+            tol = 5e-2
         elif mode == "cpu":
             dev = torch.device("cpu")
             dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev, engine=CpuEngine())
@@ -500,6 +526,16 @@ def test_dist_layers_gloo_cpu_unstaged(world):
 @pytest.mark.parametrize("world,staged", [(2, True), (4, True), (4, False)])
 def test_dist_layers_rehearsal_on_device(device, world, staged):
     _run(world, "gpu", staged)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("staged", [True, False])
+def test_dist_layers_bf16_rehearsal_on_device(device, staged):
+    """bf16 storage on the HIP engine, world 4 (two ranks per KG): the staged halo carries the
+    HighWay tail on the 128-column bf16 slice tables (gnnea_spmm_highway_bf16 per slice,
+    gnnea_highway_bwd_ld_bf16 per slice into the dS tables), and without staging the whole
+    halo; both against an fp32 restatement at bf16 tolerance (5e-2 of the max)."""
+    _run(4, "gpu_bf16", staged)
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
