@@ -262,6 +262,9 @@ __global__ __launch_bounds__(64 * W3_NW, 1) void k_gemm_x3w(int M, int N, int K,
 #ifndef GNNEA_X3W_NOSTORE
 #define GNNEA_X3W_NOSTORE 0
 #endif
+#ifndef GNNEA_F2_NOMFMA
+#define GNNEA_F2_NOMFMA 0
+#endif
 struct W3SplitP {
   uint32_t h[4], m[4], l[4];
   __device__ __forceinline__ w3_bf16x8 vh() const { return __builtin_bit_cast(w3_bf16x8, *(const uint4*)h); }
@@ -713,7 +716,12 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
   const int kq = lane >> 4, ml = lane & 15;
   const uint4* wlane = wl + kq * NC + ml;
   uint4 f[20];
-  auto row_ptr = [&](int rt) { return A + (int64_t)min(rt * BM + w * 16 + ml, M - 1) * lda; };
+  auto row_ptr = [&](int rt) {
+#if GNNEA_X3W_AHOT  // timing experiment only: every tile re-reads the first 8 row tiles (L2-hot)
+    rt = rt % 8;
+#endif
+    return A + (int64_t)min(rt * BM + w * 16 + ml, M - 1) * lda;
+  };
   // chunk c's quads: steps 10 c .. ; steps before the last are inside every row, the last one's
   // quads past K read the row's first quad (valid) and are zeroed at use
   auto load_chunk = [&](const float* p, const int c) {
@@ -782,9 +790,13 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
           const f2_f16x8 wh = __builtin_bit_cast(f2_f16x8, wp[16 * jn]);
           const f2_f16x8 wlo = __builtin_bit_cast(f2_f16x8, wp[PL + 16 * jn]);
           w3_f32x4& cc = acc[c][jn];
+#if GNNEA_F2_NOMFMA  // timing experiment only: no MFMAs (operands kept live by one add)
+          cc[0] += (float)wh[0] * (float)xl[0] + (float)wlo[1] * (float)xh[1];
+#else
           cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, cc, 0, 0, 0);
           cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wlo, xh, cc, 0, 0, 0);
           cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, cc, 0, 0, 0);
+#endif
         }
       }
     }
@@ -815,7 +827,11 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
             o.x += beta * cv.x; o.y += beta * cv.y; o.z += beta * cv.z; o.w += beta * cv.w;
           }
           if (relu) o = f4_relu(o);
+#if GNNEA_X3W_NOSTORE  // timing experiment only: no C traffic (the accumulators kept live)
+          if (o.x == 1.2345e-30f) *cp = o;
+#else
           *cp = o;
+#endif
           if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
         }
       }

@@ -5,7 +5,8 @@ to sum_k |a_ik||w_kj| (the bound an fp32 GEMM's own rounding is stated in).
 
 Rows of x are scaled by 10^U(-20, 20), columns of W by 10^U(-10, 10), one row is all zeros, one
 row holds values 2^30 apart (the small ones fall to fp16 subnormals after scaling, inside the
-bound), and K = 300 / 292 / 320 (tail quads)."""
+bound), and K = 300 / 292 / 320 (tail quads) and 600 / 584 (the f16x2 form's two k-chunks, each with
+its own row scale)."""
 import numpy as np
 import pytest
 import torch
@@ -26,7 +27,8 @@ def _case(device, M, K, N, seed):
 
 
 @pytest.mark.parametrize("mode", ["2", "4"])
-@pytest.mark.parametrize("M,K,N", [(70000, 300, 300), (70000, 292, 600), (66000, 320, 96)])
+@pytest.mark.parametrize("M,K,N", [(70000, 300, 300), (70000, 292, 600), (66000, 320, 96),
+                                   (70000, 600, 300), (66000, 584, 132)])
 def test_gemm_split_range_vs_fp64(device, mode, M, K, N):
     import subprocess
     import sys

@@ -362,7 +362,9 @@ def test_sinkhorn_onchip_matches_sweep(device, monkeypatch, I, J, reg, tol):
     for path in ("onchip", "sweep"):
         if path == "sweep":
             monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
-        res[path] = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, reg, tol, 400)
+        # the scaling form (variant 0): with resident K off, GNNEA_SK_AUTO would take the fused
+        # log-domain sweep instead
+        res[path] = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, reg, tol, 400, variant=0)
     r0, r1 = res["onchip"], res["sweep"]
     assert (r0.path, r1.path) == ("onchip", "sweep")
     assert (r0.iters, r0.reason) == (r1.iters, r1.reason), ((r0.iters, r0.reason),
@@ -394,7 +396,7 @@ def test_sinkhorn_onchip_bad_u_break(device):
     for env in ("1", "0"):
         os.environ["GNNEA_SK_RESIDENT"] = env
         try:
-            out.append(gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, 0.05, 1e-9, 50))
+            out.append(gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, 0.05, 1e-9, 50, variant=0))
         finally:
             os.environ.pop("GNNEA_SK_RESIDENT", None)
     r0, r1 = out

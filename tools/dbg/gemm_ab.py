@@ -41,6 +41,8 @@ res["proj x.W^T+b 300"] = run(lambda: ops.gemm(X, W, trans_b=True, bias=b, x3=Tr
 res["proj x.[W^T|Kg] 600"] = run(lambda: ops.gemm(X, W2, x3=True))
 res["dX [dh|dg].[W;Kg^T] K600 +C"] = run(lambda: ops.gemm(X2, W3, out=Cb.copy_(C0), beta=1.0, x3=True))
 res["dW X^T.X"] = run(lambda: ops.gemm(X, X, trans_a=True, x3=True))
+W80 = W[:80].contiguous()
+res["proj x.W80^T 80 (one column tile)"] = run(lambda: ops.gemm(X, W80, trans_b=True, x3=True))
 # accuracy on a row sample (fp64 reference)
 y = ops.gemm(X2[:200000], W3, x3=True); r = X2[:200000].double() @ W3.double()
 res["err dX K600"] = float((y.double() - r).abs().max() / r.abs().max())
