@@ -738,8 +738,9 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
   };
   if (rs < tm) load_chunk(row_ptr(rs), 0);
   for (int rt = rs; rt < tm; rt += nrs) {
-    w3_f32x4 acc[NCH][NJ];
-    float rinv[NCH];
+    w3_f32x4 acc[NJ];
+    int er = 0;     // the row's scale exponent so far (the largest chunk maximum's)
+    float4 cv[NJ];  // beta != 0: the tile's C, loaded ahead of the next tile's activations
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int s0 = 10 * c, ns = KC - s0 < 10 ? KC - s0 : 10;
@@ -758,9 +759,21 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16));
       mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const int er = f2_exp(mx);
+      // one scale per row: a chunk with a larger maximum than the earlier ones rescales their
+      // accumulated sums down by the exact power of two (what falls below fp32's range there is
+      // < 2^-100 of the row's largest term); a smaller one is split at the row's scale
+      const int ec = f2_exp(mx);
+      if (c == 0) {
+        er = ec;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] = w3_f32x4{0.f, 0.f, 0.f, 0.f};
+      } else if (ec > er) {
+        const float d = er - ec < -126 ? 0.f : f2_pow2(er - ec);  // (beyond: fp32 underflow)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] *= d;
+        er = ec;
+      }
       const float sr = f2_pow2(14 - er);
-      rinv[c] = f2_pow2(er - 14);
       uint32_t ah[20][2], al[20][2];
 #pragma unroll
       for (int q = 0; q < 2 * ns; ++q) {
@@ -770,13 +783,21 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
                                  __builtin_bit_cast(float, f[q].w), sr, al[q][1]);
       }
       __builtin_amdgcn_sched_barrier(0);
+      // beta != 0 (uniform): C's tile is read before the next tile's activations are issued, so
+      // the epilogue waits for these loads only, not for the activations in flight behind them
+      if (c == NCH - 1 && beta != 0.f) {
+        const int mm = min(rt * BM + w * 16 + ml, M - 1);
+#pragma unroll
+        for (int jn = 0; jn < NJ; ++jn) {
+          const int nn = min(n0 + 16 * jn + 4 * kq, N - 4);
+          cv[jn] = *(const float4*)(C + ((int64_t)(nn >> 6) * cs + (int64_t)mm * ldc + (nn & 63)));
+        }
+      }
       // the next chunk's activations, a chunk of MFMAs ahead (past the last tile: none)
       if (c + 1 < NCH)
         load_chunk(row_ptr(rt), c + 1);
       else if (rt + nrs < tm)
         load_chunk(row_ptr(rt + nrs), 0);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[c][j] = w3_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < ns; ++s) {
         const f2_f16x8 xh = __builtin_bit_cast(
@@ -786,10 +807,12 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
         const uint4* wp = wlane + (s0 + s) * 4 * NC;
 #pragma unroll
         for (int jn = 0; jn < NJ; ++jn) {
+          // (the weight fragments read per block: reading them one block ahead measured no
+          // faster, 1.89 vs 1.91 ms at 2M x 300 x 300, profiles/r04_gemm_ab_f16x2_v2.json)
           __builtin_amdgcn_sched_barrier(0);
           const f2_f16x8 wh = __builtin_bit_cast(f2_f16x8, wp[16 * jn]);
           const f2_f16x8 wlo = __builtin_bit_cast(f2_f16x8, wp[PL + 16 * jn]);
-          w3_f32x4& cc = acc[c][jn];
+          w3_f32x4& cc = acc[jn];
 #if GNNEA_F2_NOMFMA  // timing experiment only: no MFMAs (operands kept live by one add)
           cc[0] += (float)wh[0] * (float)xl[0] + (float)wlo[1] * (float)xh[1];
 #else
@@ -801,6 +824,7 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
       }
     }
     __builtin_amdgcn_sched_barrier(0);
+    const float rinv = f2_pow2(er - 14);
     const int m = rt * BM + w * 16 + ml;
     if (m < M) {
 #pragma unroll
@@ -811,20 +835,14 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
         if (n < N) {
           const float4 bv = *(const float4*)(bsh + c);
           const float4 tv = *(const float4*)(tsh + c);
-          // unscaled exactly (powers of two, the column's first), the chunks summed, the bias
-          float o4[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float t = i == 0 ? tv.x : i == 1 ? tv.y : i == 2 ? tv.z : tv.w;
-            float v = acc[0][jn][i] * t * rinv[0];
-            if constexpr (NCH > 1) v += acc[1][jn][i] * t * rinv[1];
-            o4[i] = v;
-          }
-          float4 o = make_float4(o4[0] + bv.x, o4[1] + bv.y, o4[2] + bv.z, o4[3] + bv.w);
+          // unscaled exactly (powers of two, the column's first), then one rounding with the bias
+          const w3_f32x4 a4 = acc[jn];
+          float4 o = make_float4(a4[0] * tv.x * rinv + bv.x, a4[1] * tv.y * rinv + bv.y,
+                                 a4[2] * tv.z * rinv + bv.z, a4[3] * tv.w * rinv + bv.w);
           float4* cp = (float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63)));
           if (beta != 0.f) {
-            const float4 cv = *cp;
-            o.x += beta * cv.x; o.y += beta * cv.y; o.z += beta * cv.z; o.w += beta * cv.w;
+            const float4 c4 = cv[jn];
+            o.x += beta * c4.x; o.y += beta * c4.y; o.z += beta * c4.z; o.w += beta * c4.w;
           }
           if (relu) o = f4_relu(o);
 #if GNNEA_X3W_NOSTORE  // timing experiment only: no C traffic (the accumulators kept live)
@@ -841,12 +859,14 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
 
 // ---- host side ----
 
-// GNNEA_X3W: 0 k_gemm_x3p, 1 k_gemm_x3w, 2 (default) k_gemm_x3w_ring, 3 k_gemm_x3w_ring2,
-// 4 k_gemm_f16x2_ring (two fp16 pieces, three products)
+// GNNEA_X3W: 0 k_gemm_x3p, 1 k_gemm_x3w, 2 k_gemm_x3w_ring, 3 k_gemm_x3w_ring2, 4 (default)
+// k_gemm_f16x2_ring (two fp16 pieces, three products; measured against mode 2 on one box:
+// 2M x 300 x 300 1.89 vs 2.18 ms, x·[Wᵀ|K_g] 3.92 vs 4.25, the K = 600 input gradient with
+// +C 5.34 vs 6.16 on the chunked form instead of k_gemm_x3p; profiles/r04_gemm_ab_f16x2_v2.json)
 static int x3w_mode() {
   static const int mode = [] {
     const char* e = getenv("GNNEA_X3W");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 4;
   }();
   return mode;
 }
