@@ -429,7 +429,12 @@ int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
  * gnnea_gemm_x3_ws_bytes (op(B) split once into three bf16 planes + split-K slabs; required).
  * trans_a = 1 with trans_b = 0 is the weight-gradient form dW = Aᵀ·B (A [K][M], B [K][N], both
  * tall): both operands are split on the fly, split-K over the long K, workspace from
- * gnnea_gemm_x3t_ws_bytes (slabs only).  trans_a = trans_b = 1 runs on the f32 MFMA kernel. */
+ * gnnea_gemm_x3t_ws_bytes (slabs only).  trans_a = trans_b = 1 runs on the f32 MFMA kernel.
+ * Tall projections (trans_a = 0, M >= 65536, K in (288, 320] or (576, 608]) run on the fp16
+ * MFMA instead: two fp16 pieces per element (hi = f16(x s), lo = f16(x s - hi)), every row of A
+ * and column of op(B) scaled by a power of two s into fp16's range, three products (hi·lo,
+ * lo·hi, hi·hi; the dropped lo·lo and lo's rounding each <= 2^-22 |a||b|), the inverse scales
+ * applied exactly in the epilogue (csrc/gemm_x3w.hip k_gemm_f16x2_ring). */
 int64_t gnnea_gemm_x3_ws_bytes(int64_t M, int64_t N, int64_t K);
 int64_t gnnea_gemm_x3t_ws_bytes(int64_t M, int64_t N, int64_t K);
 int gnnea_gemm_x3_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
