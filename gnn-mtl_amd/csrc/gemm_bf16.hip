@@ -893,6 +893,17 @@ static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
 #ifndef GNNEA_BW_STAGE
 #define GNNEA_BW_STAGE 0
 #endif
+// activation register sets in flight (A/B builds: 2 = one tile ahead, 3 = two tiles ahead;
+// measured equal, 0.887 vs 0.871-0.892 ms)
+#ifndef GNNEA_BW_DEPTH
+#define GNNEA_BW_DEPTH 2
+#endif
+// the k permutation of a lane's fragments (A and W alike): 0 = k-half kh holds k in
+// [kh Kh + 8 s, +8) (a wave-instruction reads 16 B from each of 64 rows' lines), 1 = k in
+// [16 s + 8 kh, +8) (the row's two lanes read 32 contiguous bytes: 32 lines per instruction)
+#ifndef GNNEA_BW_KPERM
+#define GNNEA_BW_KPERM 0
+#endif
 constexpr int kBwCols = 160, kBwKC = 20;  // column tile, max k-steps (K <= 320)
 // a wave's staged bf16 output tile: 32 rows of 320 B, row stride padded by 16 B (bank spread)
 constexpr int kBwStageRS = 2 * kBwCols + 16, kBwStageBytes = 32 * kBwStageRS;
@@ -912,7 +923,7 @@ __global__ __launch_bounds__(256) void k_pack_bf16w(const bf16_t* __restrict__ B
     r >>= 1;
     const int s = (int)(r % kc);
     const int nt = (int)(r / kc);
-    const int col = nt * kBwCols + n, k = kh * 8 * kc + 8 * s + e;
+    const int col = nt * kBwCols + n, k = (GNNEA_BW_KPERM ? 16 * s + 8 * kh : kh * 8 * kc + 8 * s) + e;
     bf16_t v = 0;
     if (col < N && k < K) v = b_nk ? B[(int64_t)col * ldb + k] : B[(int64_t)k * ldb + col];
     P[t] = v;
@@ -952,6 +963,22 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
   // of the upper half can reach K (K > 16 (KC - 1)); there a chunk holding K is read as the 16 B
   // ending at K (in bounds, K even) and shifted down by words, a chunk past K is zero.
   auto issue = [&](uint4 (&f)[KC], int rt) {
+#if GNNEA_BW_KPERM
+    // k = 16 s + 8 kh: steps before the last are inside every row (K > 16 (KC - 1))
+    const bf16_t* p = A + (int64_t)min(rt * 128 + w * 32 + li, M - 1) * lda + 8 * kh;
+    constexpr int s_gen = KC - 1;
+#pragma unroll
+    for (int s = 0; s < s_gen; ++s) f[s] = *(const uint4*)(p + 16 * s);
+#pragma unroll
+    for (int s = s_gen; s < KC; ++s) {
+      const int k0 = 16 * s + 8 * kh;
+      if (k0 + 8 <= K) {
+        f[s] = *(const uint4*)(p + 16 * s);
+      } else if (k0 >= K) {
+        f[s] = make_uint4(0, 0, 0, 0);
+      } else {
+        const uint4 v = *(const uint4*)(p + (K - 8 - 8 * kh));
+#else
     const bf16_t* p = A + (int64_t)min(rt * 128 + w * 32 + li, M - 1) * lda + kh * Kh;
 #pragma unroll
     for (int s = 0; s < KC - 2; ++s) f[s] = *(const uint4*)(p + 8 * s);
@@ -964,6 +991,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
         f[s] = make_uint4(0, 0, 0, 0);
       } else {
         const uint4 v = *(const uint4*)(p + (K - 8 - kh * Kh));
+#endif
         const int sh = (k0 + 8 - K) >> 1;  // 1..3 words
         f[s] = make_uint4(sh == 1 ? v.y : (sh == 2 ? v.z : v.w), sh == 1 ? v.z : (sh == 2 ? v.w : 0u),
                           sh == 1 ? v.w : 0u, 0u);
@@ -1053,6 +1081,28 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
       }
     }
   };
+#if GNNEA_BW_DEPTH == 3
+  // three register sets: a tile's activations are issued two tiles ahead of their MFMAs
+  uint4 fa[KC], fb[KC], fc[KC];
+  int rt = rs, r1 = rs + nrs;
+  if (rt < tm) issue(fa, rt);
+  if (r1 < tm) issue(fb, r1);
+  while (rt < tm) {
+    const int r2 = r1 + nrs;
+    if (r2 < tm) issue(fc, r2);
+    compute_store(fa, rt);
+    if (r1 >= tm) break;
+    const int r3 = r2 + nrs;
+    if (r3 < tm) issue(fa, r3);
+    compute_store(fb, r1);
+    if (r2 >= tm) break;
+    const int r4 = r3 + nrs;
+    if (r4 < tm) issue(fb, r4);
+    compute_store(fc, r2);
+    rt = r3;
+    r1 = r4;
+  }
+#else
   uint4 fa[KC], fb[KC];
   int rt = rs;
   if (rt < tm) issue(fa, rt);
@@ -1066,6 +1116,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
     compute_store(fb, r1);
     rt = r2;
   }
+#endif
 }
 
 static bool bf16w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda,

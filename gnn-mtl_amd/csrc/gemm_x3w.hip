@@ -633,20 +633,25 @@ __device__ __forceinline__ float f2_max3abs(float mx, float a, float b) {
 }
 
 // column scales of the weight operand: tsc[n] = 2^(14 - e_n), tinv[n] = 2^(e_n - 14) over
-// W_op[n][0..K) (n < ntn * 80; past N: 1)
-__global__ __launch_bounds__(256) void k_colscale_f16x2(const float* __restrict__ B, int64_t ldb,
-                                                        int b_nk, int N, int K, int nn,
-                                                        float* __restrict__ tsc,
-                                                        float* __restrict__ tinv) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+// W_op[n][0..K) (n < ntn * nc; past N: 1).  One wave per column, the k range strided over its
+// lanes (a serial loop per column took 69 us per call)
+__global__ __launch_bounds__(64) void k_colscale_f16x2(const float* __restrict__ B, int64_t ldb,
+                                                       int b_nk, int N, int K, int nn,
+                                                       float* __restrict__ tsc,
+                                                       float* __restrict__ tinv) {
+  const int n = blockIdx.x, lane = threadIdx.x;
   if (n >= nn) return;
   float m = 0.f;
   if (n < N)
-    for (int k = 0; k < K; ++k)
+    for (int k = lane; k < K; k += 64)
       m = fmaxf(m, fabsf(b_nk ? B[(int64_t)n * ldb + k] : B[(int64_t)k * ldb + n]));
-  const int e = f2_exp(m);
-  tsc[n] = f2_pow2(14 - e);
-  tinv[n] = f2_pow2(e - 14);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (lane == 0) {
+    const int e = f2_exp(m);
+    tsc[n] = f2_pow2(14 - e);
+    tinv[n] = f2_pow2(e - 14);
+  }
 }
 
 // P[nt][p][s][kq][n][8], p = 0 hi / 1 lo: the x3 pack's layout (kc k-steps, nc-column tiles)
@@ -740,7 +745,10 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
   for (int rt = rs; rt < tm; rt += nrs) {
     w3_f32x4 acc[NJ];
     int er = 0;     // the row's scale exponent so far (the largest chunk maximum's)
-    float4 cv[NJ];  // beta != 0: the tile's C, loaded ahead of the next tile's activations
+    // beta != 0 on the wide (K = 600) form: the tile's C, loaded ahead of the next tile's
+    // activations (the 80 / 112-column forms have no registers to spare: C read in the epilogue)
+    constexpr bool CAHEAD = KC > 10;
+    float4 cv[CAHEAD ? NJ : 1];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int s0 = 10 * c, ns = KC - s0 < 10 ? KC - s0 : 10;
@@ -785,7 +793,7 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
       __builtin_amdgcn_sched_barrier(0);
       // beta != 0 (uniform): C's tile is read before the next tile's activations are issued, so
       // the epilogue waits for these loads only, not for the activations in flight behind them
-      if (c == NCH - 1 && beta != 0.f) {
+      if (CAHEAD && c == NCH - 1 && beta != 0.f) {
         const int mm = min(rt * BM + w * 16 + ml, M - 1);
 #pragma unroll
         for (int jn = 0; jn < NJ; ++jn) {
@@ -841,7 +849,7 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
                                  a4[2] * tv.z * rinv + bv.z, a4[3] * tv.w * rinv + bv.w);
           float4* cp = (float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63)));
           if (beta != 0.f) {
-            const float4 c4 = cv[jn];
+            const float4 c4 = CAHEAD ? cv[CAHEAD ? jn : 0] : *cp;
             o.x += beta * c4.x; o.y += beta * c4.y; o.z += beta * c4.z; o.w += beta * c4.w;
           }
           if (relu) o = f4_relu(o);
@@ -876,9 +884,18 @@ static bool x3w_on() { return x3w_mode() != 0; }
 // gradient [dh | dg]·[W ; K_gᵀ], K = 600) on 64-column tiles (2 planes x 19 steps x 64 columns =
 // 152 KB of LDS)
 constexpr int F2_NC_WIDE = 64, F2_KC_WIDE = 19;
+// K <= 320 tile width: 80 columns, or 112 (GNNEA_F2_NC=112, A/B: 143 KB of weight, the
+// activations re-read by 3 instead of 4 column tiles at N = 300)
+static int f16x2_nc() {
+  static const int nc = [] {
+    const char* e = getenv("GNNEA_F2_NC");
+    return e && atoi(e) == 112 ? 112 : W3_NC;
+  }();
+  return nc;
+}
 static bool f16x2_k(int64_t K, int* kc, int* nc) {
   if (K > 32 * (W3_KC - 1) && K <= 32 * W3_KC) {
-    *kc = W3_KC, *nc = W3_NC;
+    *kc = W3_KC, *nc = f16x2_nc();
     return true;
   }
   if (K > 32 * (F2_KC_WIDE - 1) && K <= 32 * F2_KC_WIDE) {
@@ -895,7 +912,9 @@ static int64_t f16x2_ws_bytes(int64_t N, int kc, int nc) {
 int64_t gemm_x3w_ws_bytes(int64_t N) {  // the largest of the forms
   const int64_t x3 = (N + W3_NC - 1) / W3_NC * W3_TILE_BYTES;
   const int64_t f2 = f16x2_ws_bytes(N, F2_KC_WIDE, F2_NC_WIDE);
-  return x3 > f2 ? x3 : f2;
+  const int64_t f3 = f16x2_ws_bytes(N, W3_KC, 112);
+  const int64_t m = x3 > f2 ? x3 : f2;
+  return m > f3 ? m : f3;
 }
 
 bool gemm_x3w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda, const void* A,
@@ -945,8 +964,8 @@ static int f16x2_launch(int trans_b, int64_t M, int64_t N, int64_t K, const floa
   float* tsc = (float*)((char*)ws + (int64_t)ntn * 2 * kc * 4 * nc * 16);  // after the planes
   float* tinv = tsc + (int64_t)ntn * nc;
   const int nn = ntn * nc;
-  hipLaunchKernelGGL(k_colscale_f16x2, dim3((nn + 255) / 256), dim3(256), 0, s, B, ldb,
-                     trans_b ? 1 : 0, (int)N, (int)K, nn, tsc, tinv);
+  hipLaunchKernelGGL(k_colscale_f16x2, dim3(nn), dim3(64), 0, s, B, ldb, trans_b ? 1 : 0, (int)N,
+                     (int)K, nn, tsc, tinv);
   GNNEA_LAUNCH_CHECK();
   const int64_t tot = (int64_t)ntn * kc * 4 * nc * 8;
   const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
@@ -954,7 +973,11 @@ static int f16x2_launch(int trans_b, int64_t M, int64_t N, int64_t K, const floa
                      (int)K, ntn, kc, nc, (const float*)tsc, (uint16_t*)ws);
   GNNEA_LAUNCH_CHECK();
   const int grid = ring_grid(ntn, M, 128);
-  if (kc == W3_KC)
+  if (kc == W3_KC && nc == 112)
+    hipLaunchKernelGGL((k_gemm_f16x2_ring<W3_KC, 112>), dim3(grid), dim3(512), 0, s, (int)M,
+                       (int)N, (int)K, ntn, A, lda, (const uint16_t*)ws, (const float*)tinv, bias,
+                       C, ldc, cs, C2, cs2, beta, relu);
+  else if (kc == W3_KC)
     hipLaunchKernelGGL((k_gemm_f16x2_ring<W3_KC, W3_NC>), dim3(grid), dim3(512), 0, s, (int)M,
                        (int)N, (int)K, ntn, A, lda, (const uint16_t*)ws, (const float*)tinv, bias,
                        C, ldc, cs, C2, cs2, beta, relu);

@@ -37,6 +37,12 @@ res["bf16 x.W 300 (bf16 out)"] = run(lambda: ops.gemm(X, W))
 res["bf16 relu(x.W^T+b) 300"] = run(lambda: ops.gemm(X, W, trans_b=True, bias=b, act=1))
 res["bf16 x.W^T+b 300 (fp32 out)"] = run(lambda: ops.gemm(X, W, trans_b=True, bias=b,
                                                           out_dtype=torch.float32))
+y = ops.gemm(X[:100000], W, trans_b=True, bias=b).float()
+r = X[:100000].float() @ W.float().t() + b
+res["err x.W^T+b (norm-rel, bf16 out)"] = float((y - r).norm() / r.norm())
+y = ops.gemm(X[:100000], W).float()
+r = X[:100000].float() @ W.float()
+res["err x.W (norm-rel, bf16 out)"] = float((y - r).norm() / r.norm())
 print(json.dumps({sys.argv[1]: res}), flush=True)
 ''' % ROOT
 
