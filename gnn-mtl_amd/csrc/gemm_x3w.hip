@@ -884,12 +884,14 @@ static bool x3w_on() { return x3w_mode() != 0; }
 // gradient [dh | dg]·[W ; K_gᵀ], K = 600) on 64-column tiles (2 planes x 19 steps x 64 columns =
 // 152 KB of LDS)
 constexpr int F2_NC_WIDE = 64, F2_KC_WIDE = 19;
-// K <= 320 tile width: 80 columns, or 112 (GNNEA_F2_NC=112, A/B: 143 KB of weight, the
-// activations re-read by 3 instead of 4 column tiles at N = 300)
+// K <= 320 tile width: 112 columns (143 KB of weight; the activations re-read by 3 column
+// tiles at N = 300 instead of 4, 6 at N = 600 instead of 8; 12 % of the MFMAs on padding at
+// N = 300): 2M x 300 x 300 1.79 vs 1.87 ms, x·[Wᵀ|K_g] 3.45 vs 3.81, HGCN-EA step 88.0 vs 89.3
+// (profiles/r04_gemm_ab_f16x2_nc112.json); GNNEA_F2_NC=80 the 80-column tile (A/B)
 static int f16x2_nc() {
   static const int nc = [] {
     const char* e = getenv("GNNEA_F2_NC");
-    return e && atoi(e) == 112 ? 112 : W3_NC;
+    return e && atoi(e) == 80 ? W3_NC : 112;
   }();
   return nc;
 }
