@@ -11,7 +11,9 @@ import os
 import torch  # noqa: F401  (must be imported before the HIP library is dlopen'ed)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgnnea.so")
+# GNNEA_LIB_FILE: another build of the library next to this one (A/B timing of variant builds
+# only; a file name, not a path)
+LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ.get("GNNEA_LIB_FILE", "libgnnea.so")))
 
 GNNEA_ACT_IDENTITY = 0
 GNNEA_ACT_RELU = 1
