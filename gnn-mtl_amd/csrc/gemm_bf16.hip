@@ -904,6 +904,12 @@ static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
 #ifndef GNNEA_BW_KPERM
 #define GNNEA_BW_KPERM 0
 #endif
+#ifndef GNNEA_BW_NOMFMA
+#define GNNEA_BW_NOMFMA 0
+#endif
+#ifndef GNNEA_BW_NOSTORE
+#define GNNEA_BW_NOSTORE 0
+#endif
 constexpr int kBwCols = 160, kBwKC = 20;  // column tile, max k-steps (K <= 320)
 // a wave's staged bf16 output tile: 32 rows of 320 B, row stride padded by 16 B (bank spread)
 constexpr int kBwStageRS = 2 * kBwCols + 16, kBwStageBytes = 32 * kBwStageRS;
@@ -1016,10 +1022,17 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
       }
       __builtin_amdgcn_sched_barrier(0);
       const bf16x8 x = __builtin_bit_cast(bf16x8, f[s]);
+#if GNNEA_BW_NOMFMA  // timing experiment only: no MFMAs (operands kept live by one add)
+    (void)x;
+#pragma unroll
+      for (int t = 0; t < 5; ++t)
+        acc[t][0] += __builtin_bit_cast(float, wc[t].x ^ wc[t].w ^ f[s].x ^ f[s].y ^ f[s].z ^ f[s].w);
+#else
 #pragma unroll
       for (int t = 0; t < 5; ++t)
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wc[t]), x,
                                                          acc[t], 0, 0, 0);
+#endif
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < 5; ++t) wc[t] = wn[t];
@@ -1071,6 +1084,9 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
           o.x += bv.x; o.y += bv.y; o.z += bv.z; o.w += bv.w;
           if (relu) o = f4_relu(o);  // the Linear's act (layers/layers.py:121-122), uniform
           TC* c = C + c_index_bf(m, n, ldc, cs);
+#if GNNEA_BW_NOSTORE  // timing experiment only: no C traffic
+          if (o.x != 1.2345e-30f) continue;
+#endif
           if constexpr (std::is_same<TC, bf16_t>::value) {
             *(uint2*)c = make_uint2((uint32_t)f32_to_bf16(o.x) | ((uint32_t)f32_to_bf16(o.y) << 16),
                                     (uint32_t)f32_to_bf16(o.z) | ((uint32_t)f32_to_bf16(o.w) << 16));
