@@ -965,44 +965,37 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
   }
   __syncthreads();
   const int tm = (M + 127) / 128;  // 128-row tiles: 4 waves x 32 rows
-  // one k-step fragment of the lane's row: 8 bf16 at k = kh Kh + 8 s.  Only the last two steps
-  // of the upper half can reach K (K > 16 (KC - 1)); there a chunk holding K is read as the 16 B
-  // ending at K (in bounds, K even) and shifted down by words, a chunk past K is zero.
-  auto issue = [&](uint4 (&f)[KC], int rt) {
+  // one k-step fragment of the lane's row: 8 bf16 at k = kh Kh + 8 s (GNNEA_BW_KPERM: 16 s +
+  // 8 kh).  Only the last steps can reach K (K > 16 (KC - 1)); there a chunk holding K is read
+  // as the 16 B ending at K (in bounds, K even) and a chunk past K reads the same 16 B; both
+  // are fixed up when they are USED (tail_fix: shifted down by words / zeroed).  Fixing them
+  // up here, as loads are issued, made the compiler wait vmcnt(0) right after the next tile's
+  // loads — the whole tile's load latency exposed every tile (0.89 ms -> see DESIGN §9).
 #if GNNEA_BW_KPERM
-    // k = 16 s + 8 kh: steps before the last are inside every row (K > 16 (KC - 1))
-    const bf16_t* p = A + (int64_t)min(rt * 128 + w * 32 + li, M - 1) * lda + 8 * kh;
-    constexpr int s_gen = KC - 1;
-#pragma unroll
-    for (int s = 0; s < s_gen; ++s) f[s] = *(const uint4*)(p + 16 * s);
-#pragma unroll
-    for (int s = s_gen; s < KC; ++s) {
-      const int k0 = 16 * s + 8 * kh;
-      if (k0 + 8 <= K) {
-        f[s] = *(const uint4*)(p + 16 * s);
-      } else if (k0 >= K) {
-        f[s] = make_uint4(0, 0, 0, 0);
-      } else {
-        const uint4 v = *(const uint4*)(p + (K - 8 - 8 * kh));
+  constexpr int s_tail = KC - 1;
+  auto k0_of = [&](int s) { return 16 * s + 8 * kh; };
 #else
-    const bf16_t* p = A + (int64_t)min(rt * 128 + w * 32 + li, M - 1) * lda + kh * Kh;
-#pragma unroll
-    for (int s = 0; s < KC - 2; ++s) f[s] = *(const uint4*)(p + 8 * s);
-#pragma unroll
-    for (int s = KC - 2; s < KC; ++s) {
-      const int k0 = kh * Kh + 8 * s;
-      if (k0 + 8 <= K) {
-        f[s] = *(const uint4*)(p + 8 * s);
-      } else if (k0 >= K) {
-        f[s] = make_uint4(0, 0, 0, 0);
-      } else {
-        const uint4 v = *(const uint4*)(p + (K - 8 - kh * Kh));
+  constexpr int s_tail = KC - 2;
+  auto k0_of = [&](int s) { return kh * Kh + 8 * s; };
 #endif
-        const int sh = (k0 + 8 - K) >> 1;  // 1..3 words
-        f[s] = make_uint4(sh == 1 ? v.y : (sh == 2 ? v.z : v.w), sh == 1 ? v.z : (sh == 2 ? v.w : 0u),
-                          sh == 1 ? v.w : 0u, 0u);
-      }
+  auto issue = [&](uint4 (&f)[KC], int rt) {
+    const bf16_t* row = A + (int64_t)min(rt * 128 + w * 32 + li, M - 1) * lda;
+#pragma unroll
+    for (int s = 0; s < s_tail; ++s) f[s] = *(const uint4*)(row + k0_of(s));
+#pragma unroll
+    for (int s = s_tail; s < KC; ++s) {
+      const int k0 = k0_of(s);
+      f[s] = *(const uint4*)(row + (k0 + 8 <= K ? k0 : K - 8));
     }
+  };
+  auto tail_fix = [&](int s, uint4 v) {
+    if (s < s_tail) return v;
+    const int k0 = k0_of(s);
+    if (k0 + 8 <= K) return v;
+    if (k0 >= K) return make_uint4(0, 0, 0, 0);
+    const int sh = (k0 + 8 - K) >> 1;  // 1..3 words
+    return make_uint4(sh == 1 ? v.y : (sh == 2 ? v.z : v.w), sh == 1 ? v.z : (sh == 2 ? v.w : 0u),
+                      sh == 1 ? v.w : 0u, 0u);
   };
   const uint4* wlane = wl + kh * kBwCols + li;  // + (2 s) * 160 + 32 t
   auto compute_store = [&](const uint4 (&f)[KC], int rt) {
@@ -1021,7 +1014,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
         for (int t = 0; t < 5; ++t) wn[t] = wlane[(2 * (s + 1)) * kBwCols + 32 * t];
       }
       __builtin_amdgcn_sched_barrier(0);
-      const bf16x8 x = __builtin_bit_cast(bf16x8, f[s]);
+      const bf16x8 x = __builtin_bit_cast(bf16x8, tail_fix(s, f[s]));
 #if GNNEA_BW_NOMFMA  // timing experiment only: no MFMAs (operands kept live by one add)
     (void)x;
 #pragma unroll
@@ -1119,17 +1112,22 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
     r1 = r4;
   }
 #else
+  // every iteration issues the next tile's loads unconditionally (past the last tile: the last
+  // tile again, never used), so that the outstanding-load count at each use is the same on
+  // every path through the loop and the compiler's waits cover only the tile being used
+  if (rs >= tm) return;
   uint4 fa[KC], fb[KC];
   int rt = rs;
-  if (rt < tm) issue(fa, rt);
-  while (rt < tm) {
+  issue(fa, rt);
+  while (true) {
     const int r1 = rt + nrs;
-    if (r1 < tm) issue(fb, r1);
+    issue(fb, min(r1, tm - 1));
     compute_store(fa, rt);
     if (r1 >= tm) break;
     const int r2 = r1 + nrs;
-    if (r2 < tm) issue(fa, r2);
+    issue(fa, min(r2, tm - 1));
     compute_store(fb, r1);
+    if (r2 >= tm) break;
     rt = r2;
   }
 #endif

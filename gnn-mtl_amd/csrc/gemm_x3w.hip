@@ -802,10 +802,12 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
         }
       }
       // the next chunk's activations, a chunk of MFMAs ahead (past the last tile: none)
+      // (unconditional, past the last tile the last tile again: the same outstanding-load
+      // count on every path, so the compiler's waits never cover the loads in flight)
       if (c + 1 < NCH)
         load_chunk(row_ptr(rt), c + 1);
-      else if (rt + nrs < tm)
-        load_chunk(row_ptr(rt + nrs), 0);
+      else
+        load_chunk(row_ptr(rt + nrs < tm ? rt + nrs : rt), 0);
 #pragma unroll
       for (int s = 0; s < ns; ++s) {
         const f2_f16x8 xh = __builtin_bit_cast(
