@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(
   const L hl(lane, dh);
   const int hme = hl.h < H ? hl.h : 0;
 
-  float hj[EPL], acc[EPL];
+  float hj[EPL], acc[EPL], a2l[EPL];
   {
     const T* x = Hm + (int64_t)row * ldh;
 #pragma unroll
@@ -365,6 +365,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(
       const float v = to_f32<T>(x[hl.c[t]]);
       hj[t] = hl.ok[t] ? v : 0.f;
       acc[t] = 0.f;
+      // the epilogue's a_2 terms, read now: read there, each was a serial L2 round trip between
+      // the row's last edge and its stores
+      a2l[t] = hl.ok[t] ? a[hme * 2 * dh + dh + hl.d0 + t] : 0.f;
     }
   }
   float sj[H], ds2p[H];
@@ -486,7 +489,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(
   T* out = dH + (int64_t)row * lddh;
 #pragma unroll
   for (int t = 0; t < EPL; ++t)
-    if (hl.ok[t]) out[hl.c[t]] = from_f32<T>(acc[t] + d2me * a[hme * 2 * dh + dh + hl.d0 + t]);
+    if (hl.ok[t]) out[hl.c[t]] = from_f32<T>(acc[t] + d2me * a2l[t]);
 }
 
 template <int H, int NCH, typename T>
@@ -880,7 +883,7 @@ __global__ __launch_bounds__(256) GNNEA_HG_ATTR_SRC void k_gat_bwd_src_hg(
   const bool wsh = (hl.c[0] & 1) != 0;
   const int64_t ldb = ldg * (int64_t)sizeof(T);
 
-  float hj[EPL], acc[EPL];
+  float hj[EPL], acc[EPL], a2l[EPL];
   {
     const T* x = Hm + (int64_t)row * ldh;
 #pragma unroll
@@ -888,6 +891,9 @@ __global__ __launch_bounds__(256) GNNEA_HG_ATTR_SRC void k_gat_bwd_src_hg(
       const float v = to_f32<T>(x[hl.c[t]]);
       hj[t] = hl.ok[t] ? v : 0.f;
       acc[t] = 0.f;
+      // the epilogue's a_2 terms, read now: read there, each was a serial L2 round trip between
+      // the row's last edge and its stores
+      a2l[t] = hl.ok[t] ? a[hme * 2 * dh + dh + hl.d0 + t] : 0.f;
     }
   }
   float ds2p[H];
@@ -980,7 +986,7 @@ __global__ __launch_bounds__(256) GNNEA_HG_ATTR_SRC void k_gat_bwd_src_hg(
   T* out = dH + (int64_t)row * lddh;
 #pragma unroll
   for (int t = 0; t < EPL; ++t)
-    if (hl.ok[t]) out[hl.c[t]] = from_f32<T>(acc[t] + d2me * a[hme * 2 * dh + dh + hl.d0 + t]);
+    if (hl.ok[t]) out[hl.c[t]] = from_f32<T>(acc[t] + d2me * a2l[t]);
 }
 
 // the head-grouped passes: on unless GNNEA_GAT_HG=0 (A/B timing against k_gat_fwd / _bwd_src)
