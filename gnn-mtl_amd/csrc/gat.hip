@@ -520,13 +520,18 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(const int32_t* __restrict__
     if (4 * c4 >= D) continue;
     float4 v = Vec4<T>::get(dH[(int64_t)row * lddh4 + c4]);
     float o[4] = {v.x, v.y, v.z, v.w};
+    // the attention-vector terms read unconditionally (a clamped column) and together: read
+    // inside the per-element branch they were four serial L2 round trips per group
+    float av[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int c = min(4 * c4 + t, D - 1), h = c / dh;
+      av[t] = a[h * 2 * dh + (c - h * dh)];
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int c = 4 * c4 + t;
-      if (c < D) {
-        const int h = c / dh;
-        o[t] += hsel<H>(p, h) * a[h * 2 * dh + (c - h * dh)];
-      }
+      if (c < D) o[t] += hsel<H>(p, c / dh) * av[t];
     }
     dH[(int64_t)row * lddh4 + c4] = Vec4<T>::put(make_float4(o[0], o[1], o[2], o[3]));
   }
@@ -596,13 +601,16 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst4(const int32_t* __restrict_
       if (4 * c4 >= D) continue;
       const float4 x = Vec4<T>::get(v[rr][q]);
       float o[4] = {x.x, x.y, x.z, x.w};
+      float av[4];  // (read together, as in k_gat_bwd_dst)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int c = min(4 * c4 + t, D - 1), h = c / dh;
+        av[t] = a[h * 2 * dh + (c - h * dh)];
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int c = 4 * c4 + t;
-        if (c < D) {
-          const int h = c / dh;
-          o[t] += hsel<H>(ph, h) * a[h * 2 * dh + (c - h * dh)];
-        }
+        if (c < D) o[t] += hsel<H>(ph, c / dh) * av[t];
       }
       dH[(int64_t)(r0 + rr) * lddh4 + c4] = Vec4<T>::put(make_float4(o[0], o[1], o[2], o[3]));
     }
