@@ -149,6 +149,40 @@ __global__ __launch_bounds__(512) void k_colsum_parts(const float* __restrict__ 
   }
 }
 
+// The non-concatenated GAT layer's head mean (layers/att_layers.py:89-91, torch.mean over the
+// stacked heads): Y[i][d] = (sum_h X[i][h dh + d]) / heads, the sum in fp32 in head order, one
+// rounding; backward dX[i][h dh + d] = dY[i][d] / heads.  (torch's mean on bf16 ran as an
+// upcast copy, the reduction and a downcast copy per layer and direction.)
+template <typename T>
+__global__ __launch_bounds__(256) void k_head_mean(const T* __restrict__ X, int64_t ldx, int64_t n,
+                                                   int heads, int dh, T* __restrict__ Y,
+                                                   int64_t ldy) {
+  const int64_t total = n * dh;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / dh;
+    const int d = (int)(e - i * dh);
+    const T* x = X + i * ldx + d;
+    float s = 0.f;
+    for (int h = 0; h < heads; ++h) s += to_f32<T>(x[(int64_t)h * dh]);
+    Y[i * ldy + d] = from_f32<T>(s / (float)heads);
+  }
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_head_mean_bwd(const T* __restrict__ dY, int64_t ldy,
+                                                       int64_t n, int heads, int dh,
+                                                       T* __restrict__ dX, int64_t ldx) {
+  const int64_t total = n * dh;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / dh;
+    const int d = (int)(e - i * dh);
+    const T v = from_f32<T>(to_f32<T>(dY[i * ldy + d]) / (float)heads);
+    T* x = dX + i * ldx + d;
+    for (int h = 0; h < heads; ++h) x[(int64_t)h * dh] = v;
+  }
+}
+
 // ---- host side ----
 
 static int act_grid(int64_t n) { return (int)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192); }
@@ -277,4 +311,32 @@ extern "C" int gnnea_act_bwd_colsum_bf16(const void* dY, int64_t lddy, const voi
                                          void* stream) {
   return act_bwd_colsum_t<bf16_t>((const bf16_t*)dY, lddy, (const bf16_t*)Y, ldy, n_rows, D, act,
                                   (bf16_t*)G, ldg, db, ws, ws_bytes, (hipStream_t)stream);
+}
+
+template <typename T>
+static int head_mean_t(const T* X, int64_t ldx, int64_t n, int heads, int dh, T* Y, int64_t ldy,
+                       int bwd, hipStream_t s) {
+  if (n < 0 || heads < 1 || dh < 1) return GNNEA_EINVAL;
+  if (n == 0) return 0;
+  if (!X || !Y) return GNNEA_EINVAL;
+  // forward: X [n][heads dh] (ld ldx), Y [n][dh] (ld ldy); backward: X = dY [n][dh], Y = dX
+  if (bwd ? (ldx < dh || ldy < (int64_t)heads * dh) : (ldx < (int64_t)heads * dh || ldy < dh))
+    return GNNEA_EINVAL;
+  const int nb = act_grid(n * dh);
+  if (bwd)
+    hipLaunchKernelGGL(k_head_mean_bwd<T>, dim3(nb), dim3(256), 0, s, X, ldx, n, heads, dh, Y, ldy);
+  else
+    hipLaunchKernelGGL(k_head_mean<T>, dim3(nb), dim3(256), 0, s, X, ldx, n, heads, dh, Y, ldy);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int gnnea_head_mean_f32(const float* X, int64_t ldx, int64_t n, int32_t heads,
+                                   int32_t dh, float* Y, int64_t ldy, int bwd, void* stream) {
+  return head_mean_t<float>(X, ldx, n, heads, dh, Y, ldy, bwd, (hipStream_t)stream);
+}
+extern "C" int gnnea_head_mean_bf16(const void* X, int64_t ldx, int64_t n, int32_t heads,
+                                    int32_t dh, void* Y, int64_t ldy, int bwd, void* stream) {
+  return head_mean_t<bf16_t>((const bf16_t*)X, ldx, n, heads, dh, (bf16_t*)Y, ldy, bwd,
+                             (hipStream_t)stream);
 }

@@ -153,6 +153,10 @@ SIGNATURES = {
     "gnnea_colsum_f32": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _p, _i64, _p]),
     "gnnea_act_fwd_f32": (ctypes.c_int, [_p, _p, _i64, ctypes.c_int, _p]),
     "gnnea_act_fwd_bf16": (ctypes.c_int, [_p, _p, _i64, ctypes.c_int, _p]),
+    "gnnea_head_mean_f32": (ctypes.c_int, [_p, _i64, _i64, ctypes.c_int, ctypes.c_int, _p, _i64,
+                                           ctypes.c_int, _p]),
+    "gnnea_head_mean_bf16": (ctypes.c_int, [_p, _i64, _i64, ctypes.c_int, ctypes.c_int, _p, _i64,
+                                            ctypes.c_int, _p]),
     "gnnea_act_bwd_colsum_ws_bytes": (_i64, [_i64, _i32]),
     "gnnea_act_bwd_colsum_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i32, ctypes.c_int, _p,
                                                 _i64, _p, _p, _i64, _p]),

@@ -372,6 +372,41 @@ class MatmulFn(torch.autograd.Function):
         return dx, dw, None
 
 
+class HeadMeanFn(torch.autograd.Function):
+    """y = x.view(-1, heads, dh).mean(dim=1) (the non-concatenated GAT layer, att_layers.py:89-91)
+    in one pass each way (gnnea_head_mean_*)."""
+
+    @staticmethod
+    def forward(ctx, x, heads, dh):
+        x = _rows(x)
+        n = x.shape[0]
+        y = torch.empty((n, dh), dtype=x.dtype, device=x.device)
+        with _lib.on_device(x.device):
+            check(_sfn("gnnea_head_mean", x.dtype)(ptr(x), _ld(x), n, heads, dh, ptr(y), _ld(y), 0,
+                                                   stream_of(x.device)))
+        ctx.meta = (heads, dh, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        heads, dh, dt = ctx.meta
+        dy = _rows(dy, dt)
+        n = dy.shape[0]
+        dx = torch.empty((n, heads * dh), dtype=dt, device=dy.device)
+        with _lib.on_device(dy.device):
+            check(_sfn("gnnea_head_mean", dt)(ptr(dy), _ld(dy), n, heads, dh, ptr(dx), _ld(dx), 1,
+                                              stream_of(dy.device)))
+        return dx, None, None
+
+
+def head_mean(x, heads, dh):
+    """Mean over the heads of a head-concatenated [N, heads*dh] matrix (fp32 / bf16 on HIP)."""
+    _lib.require_device(x)
+    if x.dim() != 2 or x.shape[1] != heads * dh:
+        raise ValueError("gnnea.head_mean: x must be [N, heads*dh]")
+    return HeadMeanFn.apply(x, heads, dh)
+
+
 def linear(x, weight, bias=None, act=None):
     """x Wᵀ + b, or act(x Wᵀ + b) for a GNNEA_ACT_* code ``act`` (the act fused into the GEMM)."""
     if act is None or act == _lib.GNNEA_ACT_IDENTITY:

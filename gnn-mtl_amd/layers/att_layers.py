@@ -96,7 +96,7 @@ class GraphAttentionLayer(nn.Module):
         else:
             mask = _edge_dropout(csr_of(adj).nnz, self.dropout, self.training, H.device, heads)
             y = ops.gat(adj, H, a_all, heads, self.output_dim, first.alpha, first.act, mask)
-        if not self.concat:
-            y = y.view(-1, heads, self.output_dim).mean(dim=1)
+        if not self.concat:  # mean of the heads (:89-91), one pass each way
+            y = ops.head_mean(y, heads, self.output_dim)
         y = F.dropout(y, self.dropout, training=self.training)
         return (y, adj)

@@ -164,6 +164,15 @@ int gnnea_act_bwd_colsum_bf16(const void* dY, int64_t lddy, const void* Y, int64
                               int64_t n_rows, int32_t D, int act, void* G, int64_t ldg, float* db,
                               void* ws, int64_t ws_bytes, void* stream);
 
+/* The non-concatenated GAT layer's head mean (layers/att_layers.py:89-91, torch.mean over the
+ * stacked heads), csrc/act.hip.  bwd = 0: Y[i][d] = (sum_h X[i][h dh + d]) / heads (X [n][heads
+ * dh], Y [n][dh]; fp32 sum in head order, one rounding); bwd = 1: X is dY [n][dh] and Y receives
+ * dX[i][h dh + d] = dY[i][d] / heads.  ld's in elements. */
+int gnnea_head_mean_f32(const float* X, int64_t ldx, int64_t n, int32_t heads, int32_t dh,
+                        float* Y, int64_t ldy, int bwd, void* stream);
+int gnnea_head_mean_bf16(const void* X, int64_t ldx, int64_t n, int32_t heads, int32_t dh,
+                         void* Y, int64_t ldy, int bwd, void* stream);
+
 /* HighWay backward, elementwise part (autograd of layers/layers.py:67-76):
  *   dS_pre  = dY * g * act'(S)            (-> SpMM^T gives d hidden)
  *   dgate   = dY * (S - resid) * g*(1-g)  (-> d gate_pre; x-grad via kernel_gate^T)
