@@ -237,6 +237,10 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
   const int row = blockIdx.x * 4 + wave_id();
   if (row >= n_rows) return;
   const int lane = lane_id();
+  // the record's row statistics, read up front (read in the epilogue they were one more serial
+  // round trip per row after the wave sums)
+  const int64_t ro = (int64_t)row * H + (lane < H ? lane : 0);
+  const float rs1 = s1[ro], rmx = mrow[ro], rdv = den[ro];
   float cp[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) cp[h] = 0.f;
@@ -261,11 +265,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) cp[h] = wave_sum(cp[h]);
-  if (lane < H) {
-    const int64_t o = (int64_t)row * H + lane;
-    const float dv = den[o];
-    rec[o] = make_float4(s1[o], mrow[o], dv > 0.f ? 1.f / dv : 0.f, hsel<H>(cp, lane));
-  }
+  if (lane < H)
+    rec[(int64_t)row * H + lane] =
+        make_float4(rs1, rmx, rdv > 0.f ? 1.f / rdv : 0.f, hsel<H>(cp, lane));
 }
 
 // The same prep over FOUR rows per wave (the default): every dY / Y load of the four rows issued
@@ -286,9 +288,14 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep4(int n_rows, int D, int dh
   if (r0 >= n_rows) return;
   const int lane = lane_id();
   R vd[4][NCH], vy[4][NCH];
+  float rs1[4], rmx[4], rdv[4];  // the records' row statistics, read with the rows
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int64_t rw = min(r0 + rr, n_rows - 1);
+    const int64_t ro = rw * H + (lane < H ? lane : 0);
+    rs1[rr] = s1[ro];
+    rmx[rr] = mrow[ro];
+    rdv[rr] = den[ro];
 #pragma unroll
     for (int q = 0; q < NCH; ++q) {
       const int c4 = min(lane + 64 * q, (D + 3) / 4 - 1);
@@ -323,11 +330,10 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep4(int n_rows, int D, int dh
     }
 #pragma unroll
     for (int h = 0; h < H; ++h) cp[h] = wave_sum(cp[h]);
-    if (lane < H) {
-      const int64_t o = (int64_t)row * H + lane;
-      const float dv = den[o];
-      rec[o] = make_float4(s1[o], mrow[o], dv > 0.f ? 1.f / dv : 0.f, hsel<H>(cp, lane));
-    }
+    if (lane < H)
+      rec[(int64_t)row * H + lane] = make_float4(rs1[rr], rmx[rr],
+                                                 rdv[rr] > 0.f ? 1.f / rdv[rr] : 0.f,
+                                                 hsel<H>(cp, lane));
   }
 }
 

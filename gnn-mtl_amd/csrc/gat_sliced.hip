@@ -248,6 +248,10 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_s(int n_rows, int D, int d
   const int row = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
   if (row >= n_rows) return;
   const int lane = lane_id();
+  // the record's row statistics, read up front (read in the epilogue they were one more serial
+  // round trip per row after the wave sums)
+  const int64_t ro = (int64_t)row * H + (lane < H ? lane : 0);
+  const float rs1 = s1[ro], rmx = mrow[ro], rdv = den[ro];
   float cp[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) cp[h] = 0.f;
@@ -280,11 +284,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_s(int n_rows, int D, int d
   }
 #pragma unroll
   for (int h = 0; h < H; ++h) cp[h] = wave_sum(cp[h]);
-  if (lane < H) {
-    const int64_t o = (int64_t)row * H + lane;
-    const float dv = den[o];
-    rec[o] = make_float4(s1[o], mrow[o], dv > 0.f ? 1.f / dv : 0.f, hsel<H>(cp, lane));
-  }
+  if (lane < H)
+    rec[(int64_t)row * H + lane] =
+        make_float4(rs1, rmx, rdv > 0.f ? 1.f / rdv : 0.f, hsel<H>(cp, lane));
 }
 
 template <int H, int LPR>  // LPR lanes per source row
