@@ -104,7 +104,7 @@ def compulsory_bytes(n_rows, n_cols, nnz, d, sliced, elem=4, slice_w=64):
     return passes * (4 * (n_rows + 1) + 8 * nnz) + elem * n_cols * dt + elem * n_rows * d
 
 
-def sinkhorn_rate(device, B=3000, reg=0.01, n0=100, n1=1100, variant=None):
+def sinkhorn_rate(device, B=3000, reg=0.01, n0=100, n1=1100, variant=None, flags=0):
     """Marginal iters/s of utils/ot_loss.sinkhorn and SinkhornOT sinkhorn_iteration at B x B."""
     from gnnea.sinkhorn import solve
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -124,11 +124,11 @@ def sinkhorn_rate(device, B=3000, reg=0.01, n0=100, n1=1100, variant=None):
         for n_it in (n0, n1):
             # tol = -1: never converges, so exactly n_it iterations run
             solve(mode, C, la_m, lb, reg, -1.0, n_it, want_plan=False, batch=100,
-                  variant=variant)  # warm
+                  variant=variant, flags=flags)  # warm
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             res = solve(mode, C, la_m, lb, reg, -1.0, n_it, want_plan=False, batch=100,
-                        variant=variant)
+                        variant=variant, flags=flags)
             assert res.iters == n_it, (name, res.iters, n_it)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
@@ -145,7 +145,7 @@ def sinkhorn_large(device):
     element; csrc/sinkhorn_log.hip k_lsk_sweep), STAB on the scaling form with the fp64 K
     resident; beside it the scaling form for KNOPP too (variant 0: one sweep over the fp64 K per
     iteration, I * J * 8 bytes) and the two-pass log-domain form the fused sweep replaced
-    (GNNEA_SK_FUSED=0: C read twice, two exponentials per element): marginal iters/s."""
+    (flag GNNEA_SK_TWO_PASS: C read twice, two exponentials per element): marginal iters/s."""
     B = 15000
     r = sinkhorn_rate(device, B=B, n0=20, n1=120)
     c_bytes = B * B * 4
@@ -165,11 +165,7 @@ def sinkhorn_large(device):
         "kernels": "fp64 K resident in HBM (k_sk_sweep, wide: column scaling in LDS)",
         "bound": "HBM: the K stream (%.2f GB per iteration; %.0f iters/s at 8 TB/s)"
                  % (k_bytes / 1e9, 8e12 / k_bytes)}
-    os.environ["GNNEA_SK_FUSED"] = "0"
-    try:
-        two = sinkhorn_rate(device, B=B, n0=20, n1=120, variant=1)
-    finally:
-        os.environ.pop("GNNEA_SK_FUSED", None)
+    two = sinkhorn_rate(device, B=B, n0=20, n1=120, variant=1, flags=_lib.GNNEA_SK_TWO_PASS)
     r["logdomain_two_pass_iters_per_s"] = two["iters_per_s"]
     return r
 
@@ -522,10 +518,14 @@ def main():
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
+        # an explicit collective timeout: a rank stuck in a collective (e.g. the staged halo
+        # misbehaving on RCCL) ends the run with a logged error instead of at the driver's kill
+        import datetime
+        tmo = datetime.timedelta(seconds=float(os.environ.get("GNNEA_PG_TIMEOUT_S", "300")))
         if args.rehearse:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
         else:
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=device, timeout=tmo)
 
     t0 = time.time()
     n = args.entities
@@ -549,6 +549,19 @@ def main():
     hs = ops.slice_pack(h_local) if sliced else None
 
     from gnnea import exchange as _ex
+    # N > 1, row shards: prove the per-slice staged halo on THESE ranks (RCCL) before using it --
+    # one HighWay, one GCN and one GAT layer fwd + bwd staged and unstaged on the same inputs
+    # (gnnea.dist_graph.validate_staged); the step and train_step take the staged path only when
+    # every rank saw them agree (GNNEA_HALO_STAGED=0 / 1 forces it off / on)
+    halo_ab = None
+    if shard.g > 1 and part.kind == "rows":
+        from gnnea.dist_graph import DistAdj, validate_staged
+        t_ab = time.time()
+        halo_ab = validate_staged(DistAdj.from_shard(shard), D=D)
+        log("rank %d: halo_ab match=%s err=%.3g staged %.2f ms / unstaged %.2f ms (%.1fs)"
+            % (rank, halo_ab["match"], halo_ab["max_norm_rel_err"], halo_ab["staged_ms"],
+               halo_ab["unstaged_ms"], time.time() - t_ab))
+        torch.cuda.empty_cache()
     n_slices = (len(shard.slices(Dl)) if _ex.STAGED else 1) \
         if shard.g > 1 and part.kind == "rows" else 0
 
@@ -594,6 +607,33 @@ def main():
     # per-step HIP events on the launching stream (median; rank 0): the SURVEY §8d statistic,
     # reported beside the contract's wall-clock mean over the K steps
     step_ms = [e[0].elapsed_time(e[1]) for e in evs]
+
+    # the same headline step in the other halo mode (staged <-> unstaged), for halo_ab
+    if halo_ab is not None:
+        other = {}
+        keep = _ex.STAGED
+        for mode in (True, False):
+            if mode == keep:
+                other[mode] = ms_per_step
+                continue
+            if mode and not halo_ab["match"]:
+                continue  # never time a pipeline that did not validate
+            _ex.STAGED = mode
+            try:
+                for _ in range(2):
+                    step()
+                torch.cuda.synchronize()
+                dist.barrier()
+                t1 = time.perf_counter()
+                for _ in range(args.steps):
+                    step()
+                torch.cuda.synchronize()
+                dist.barrier()
+                other[mode] = (time.perf_counter() - t1) / args.steps * 1e3
+            finally:
+                _ex.STAGED = keep
+        halo_ab["headline_step_ms"] = {("staged" if m else "unstaged"): round(v, 4)
+                                       for m, v in other.items()}
 
     # the exchange alone (rows partition inside a group): bytes each rank receives per step and
     # the time of K back-to-back exchanges, max over ranks
@@ -764,6 +804,10 @@ def main():
                                            "Infinity-Cache hits (upper bound on HBM bytes)")
         if exchange is not None:
             line["exchange"] = exchange
+        if halo_ab is not None:
+            if exchange is not None:
+                halo_ab["exchange_hidden_frac"] = exchange["exchange_hidden_frac"]
+            line["halo_ab"] = halo_ab
         if side is not None:
             line["exchange_free_side"] = side
         line["config"]["layout"] = ("slice-major [%d][%d][64] fp32 (as gnnea_gemm_sliced_f32 "

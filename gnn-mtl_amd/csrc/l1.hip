@@ -98,10 +98,11 @@ __global__ void k_l1_pairs(const float* __restrict__ A, int64_t lda, const float
   if (i < n) out[i] = l1_exact(A + (int64_t)i * lda, B + (int64_t)i * ldb, D);
 }
 
-// rank[q] += #{x : d(q,x) < diag[q]  or (d == diag[q] and x < q)}   (stable-sort position)
+// rank[q] += #{x : d(q,x) < diag[q]  or (d == diag[q] and x_off + x < q)}   (stable-sort
+// position; X a block of the candidates starting at candidate x_off)
 __global__ __launch_bounds__(256) void k_l1_rank(const float* __restrict__ Q, int64_t ldq, int nq,
                                                  const float* __restrict__ X, int64_t ldx, int nx,
-                                                 int D, const double* __restrict__ diag,
+                                                 int D, const double* __restrict__ diag, int x_off,
                                                  int* __restrict__ rank) {
   __shared__ __attribute__((aligned(16))) float Qs[LK * LLD];
   __shared__ __attribute__((aligned(16))) float Xs[LK * LLD];
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(256) void k_l1_rank(const float* __restrict__ Q, in
     for (int b = 0; b < 4; ++b) {
       const int x = x0 + 4 * tx + b;
       const double v = t.acc[a][b];
-      c += (x < nx && (v < dq || (v == dq && x < q))) ? 1 : 0;
+      c += (x < nx && (v < dq || (v == dq && x_off + x < q))) ? 1 : 0;
     }
     if (c) atomicAdd(&cnt[4 * ty + a], c);
   }
@@ -317,7 +318,24 @@ extern "C" int gnnea_l1_rank_f32(const float* Q, int64_t ldq, int32_t nq, const 
   GNNEA_HIP(hipMemsetAsync(rank, 0, sizeof(int32_t) * nq, s));
   if (nx == 0) return 0;
   hipLaunchKernelGGL(k_l1_rank, dim3(div_up(nx, LT), div_up(nq, LT)), dim3(256), 0, s, Q, ldq, nq,
-                     X, ldx, nx, D, diag, rank);
+                     X, ldx, nx, D, diag, 0, rank);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
+
+// The count over one block of the candidates, [x_off, x_off + nx) (the rank's share of get_hits
+// across GPUs, gnnea/dist_search.py): the per-block counts sum to gnnea_l1_rank_f32's.
+extern "C" int gnnea_l1_rank_range_f32(const float* Q, int64_t ldq, int32_t nq, const float* X,
+                                       int64_t ldx, int32_t nx, int32_t D, const double* diag,
+                                       int32_t x_off, int32_t* rank, void* stream) {
+  if (nq < 0 || nx < 0 || D < 0 || x_off < 0) return GNNEA_EINVAL;
+  if (nq == 0) return 0;
+  if (!Q || !diag || !rank || ldq < D || (nx > 0 && (!X || ldx < D))) return GNNEA_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  GNNEA_HIP(hipMemsetAsync(rank, 0, sizeof(int32_t) * nq, s));
+  if (nx == 0) return 0;
+  hipLaunchKernelGGL(k_l1_rank, dim3(div_up(nx, LT), div_up(nq, LT)), dim3(256), 0, s, Q, ldq, nq,
+                     X, ldx, nx, D, diag, x_off, rank);
   GNNEA_LAUNCH_CHECK();
   return 0;
 }

@@ -45,15 +45,7 @@ enum { SD_ERR = GNNEA_SK_SD_ERR, SD_TPREV = GNNEA_SK_SD_TPREV, SD_LOSS = GNNEA_S
 static inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 
 // rows per sweep workgroup: about 256 workgroups (one per CU) whatever I is
-// (GNNEA_SK_WGS overrides the workgroup target for tuning experiments; not part of the ABI)
-static int sk_rows_per_wg(int I) {
-  static const int target = [] {
-    const char* e = getenv("GNNEA_SK_WGS");
-    const int v = e ? atoi(e) : 0;
-    return v >= 64 && v <= 512 ? v : 256;
-  }();
-  return (I + target - 1) / target;
-}
+static int sk_rows_per_wg(int I) { return (I + 255) / 256; }
 
 struct SkWs {
   int64_t K, u, v, pu, pv, rowbuf, part, errpart, total;
@@ -655,6 +647,7 @@ typedef __attribute__((address_space(1))) unsigned int res_gu;
 struct ResGeom {
   int P, Q, R, Cb;
   bool ok;
+  uint64_t spin;  // bound of every inter-workgroup wait, real-time ticks (GNNEA_SK_DEBUG_SPIN: 0)
 };
 
 static ResGeom res_geom(int I, int J) {
@@ -664,6 +657,7 @@ static ResGeom res_geom(int I, int J) {
   g.R = div_up(I, g.P);
   g.Cb = div_up(J, g.Q);
   g.ok = (int64_t)g.P * g.Q <= kResMaxWg;
+  g.spin = kResSpinTicks;
   return g;
 }
 
@@ -696,14 +690,15 @@ __device__ __forceinline__ double res_sum_strided(const double* p, int64_t strid
 }
 
 // one wave: until flags[base + k * stride] >= epoch for every k < n; false on timeout
-__device__ bool res_wait(const unsigned* flags, int base, int stride, int n, unsigned epoch) {
+__device__ bool res_wait(const unsigned* flags, int base, int stride, int n, unsigned epoch,
+                         uint64_t spin) {
   const int lane = lane_id();
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     bool ok = true;
     for (int k = lane; k < n; k += 64) ok &= res_ldu(flags + base + k * stride) >= epoch;
     if (__all(ok)) return true;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > kResSpinTicks) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > spin) return false;
     __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -777,7 +772,7 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
       const unsigned target = (v / nwg + 1) * nwg;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (res_ldu(d.ecnt) < target) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kResSpinTicks) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > g.spin) {
           st = 2;
           break;
         }
@@ -845,7 +840,7 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
     // 1. v_it from the column partials of iterate it-1 (wave 0 polls; then every load of the
     //    step -- the partials and the row blocks' bad-u flags -- goes out in one round trip)
     if (w == 0) {
-      const bool ok = res_wait(d.cflag, q, g.Q, g.P, (unsigned)(it + 1));
+      const bool ok = res_wait(d.cflag, q, g.Q, g.P, (unsigned)(it + 1), g.spin);
       if (lane == 0) sh_state = ok ? 0 : 2;
     }
     __syncthreads();
@@ -919,7 +914,7 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
                                    __HIP_MEMORY_SCOPE_AGENT);
     // 3. the row block's partials; the stop decisions of knopp_stop, identical everywhere
     if (w == 0) {
-      const bool ok = res_wait(d.rflag, p * g.Q, 1, g.Q, (unsigned)(it + 1));
+      const bool ok = res_wait(d.rflag, p * g.Q, 1, g.Q, (unsigned)(it + 1), g.spin);
       if (lane == 0) sh_state = ok ? 0 : 2;
     }
     __syncthreads();
@@ -979,7 +974,7 @@ __global__ __launch_bounds__(256, 1) void k_sk_res(SkArgs a, SkDev d, ResGeom g,
 }
 
 // the on-chip path serves KNOPP (variant 0, unsharded) when the blocks fit the device's CUs
-// (GNNEA_SK_RESIDENT=0 disables it, for A/B measurements)
+// (flag GNNEA_SK_NO_ONCHIP disables it: the host's retry after a timeout, and A/B measurements)
 static int res_num_cus() {
   int dev = 0, n = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -992,8 +987,6 @@ static bool res_applies(const gnnea_sinkhorn* p) {
       p->J > kMaxJ)
     return false;
   if (p->flags & GNNEA_SK_NO_ONCHIP) return false;
-  const char* e = getenv("GNNEA_SK_RESIDENT");
-  if (e && e[0] == '0') return false;
   const ResGeom g = res_geom(p->I, p->J);
   return g.ok && g.P * g.Q <= res_num_cus();
 }
@@ -1002,6 +995,10 @@ static int res_launch(const gnnea_sinkhorn* p, int first, int count, hipStream_t
   SkArgs a = sk_args(p);
   SkDev d = sk_dev(p);
   ResGeom g = res_geom(p->I, p->J);
+  // GNNEA_SK_DEBUG_SPIN: every wait's bound is 0 ticks, so a workgroup that finds a peer not yet
+  // arrived times out at once -- the timeout path (ST_TIMEOUT, the host's re-solve on the sweep
+  // path) exercised on the device by the tests
+  if (p->flags & GNNEA_SK_DEBUG_SPIN) g.spin = 0;
   // a plain launch of at most one workgroup per CU (res_applies).  Not hipLaunchCooperativeKernel:
   // the HIP runtime then keeps a dedicated cooperative queue whose teardown at process exit
   // crashed inside libhsa-runtime64 under rocprofv3's kernel tracing (the queue destroyed after

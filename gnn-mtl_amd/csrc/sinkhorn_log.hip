@@ -891,159 +891,167 @@ __device__ __forceinline__ double lsk_k(double c, double inv_eps) {
   return k < kExpUnderflow ? -INFINITY : k;
 }
 
+// The sweep's per-row barrier: the wave partials in LDS are complete (lgkmcnt(0)), then a raw
+// s_barrier.  __syncthreads() is a workgroup fence as well, which waits vmcnt(0): it drained the
+// next row's C loads (the prefetch) at every row.  The LDS hand-off needs no vector-memory wait.
+__device__ __forceinline__ void row_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // PH0 (init): no row update, P(u_0, v_0) = exp(f_0 + g_0 + k) directly: the partials of
 // v_0 K^T u_0 for the first column update.
-template <typename T, int NCM, bool PH0, bool SH>
+// PAIR (fp32 C, J and ldc even): lane l owns the column PAIRS c0 + 128 p + 2 l + {0, 1}, read as
+// one 8-B buffer load each (NCM / 2 loads per row instead of NCM: two rows in flight stay below
+// the 63 outstanding loads vmcnt can count), g as one 16-B LDS read per pair.
+template <typename T, int NCM, bool PH0, bool PAIR>
 __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C, SkArgs a, SkDev d,
                                                         int it, int slot_fp, int slot_g,
                                                         int slot_fo, int rpw) {
   __shared__ double tab[kFTab];
   __shared__ double gsh[kFW * NCM * 64];
-  __shared__ double redm[2][kFW], reds[2][kFW];
+  __shared__ double reds[2][kFW];
   if (!PH0 && d.st[ST_DONE]) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  for (int q = tid; q < kFTab; q += 64 * kFW) tab[q] = d.ftab[q];
+  {
+    double tv[kFTab / (64 * kFW)];
+#pragma unroll
+    for (int q = 0; q < kFTab / (64 * kFW); ++q) tv[q] = d.ftab[tid + q * 64 * kFW];
+#pragma unroll
+    for (int q = 0; q < kFTab / (64 * kFW); ++q) tab[tid + q * 64 * kFW] = tv[q];
+  }
   const int r0 = blockIdx.x * rpw, r1 = min(a.I, r0 + rpw);
   const int cw = ((a.J + kFW - 1) / kFW + 63) & ~63;
   const int c0 = w * cw;
   const int lim = min(c0 + cw, a.J) - c0 - lane;  // column c0 + 64 k + lane is valid iff 64 k < lim
   const double* __restrict__ g = d.g + (int64_t)slot_g * a.J;
-  double* __restrict__ gl = gsh + w * NCM * 64 + lane;  // this lane's slice of g (scaled)
+  {  // the wave's slice of g (scaled), column c0 + q at gsh[w NCM 64 + q]; every load issued
+     // first from a clamped column (a load under the validity branch waited for each in turn)
+    double* __restrict__ gf = gsh + w * NCM * 64 + lane;
+    double gv[NCM];
 #pragma unroll
-  for (int k = 0; k < NCM; ++k) gl[64 * k] = 64 * k < lim ? g[c0 + 64 * k + lane] * kFScale : -1e300;
+    for (int k = 0; k < NCM; ++k) gv[k] = g[min(c0 + 64 * k + lane, a.J - 1)];
+#pragma unroll
+    for (int k = 0; k < NCM; ++k) gf[64 * k] = 64 * k < lim ? gv[k] * kFScale : -1e300;
+  }
   __syncthreads();
+  // element k of this lane: column c0 + lbase + eo(k)
+  constexpr auto eo = [](int k) { return PAIR ? 128 * (k >> 1) + (k & 1) : 64 * k; };
+  const int lbase = PAIR ? 2 * lane : lane;
+  const int limv = min(c0 + cw, a.J) - c0 - lbase;  // element k valid iff eo(k) < limv
+  const double* __restrict__ gl = gsh + w * NCM * 64 + lbase;
   T kA[NCM], kB[NCM];
+  // the row's two scalars (f_prev, a) ride with its C loads, issued FIRST: a row's scalars are
+  // then older than the next row's C loads in flight, and waiting for them is a counted vmcnt
+  // (loaded inside process() they were the newest loads, and the wait for them drained the next
+  // row's prefetch every row)
+  double fA = 0.0, fB = 0.0, wA = 0.0, wB = 0.0;
   // buffer loads over the row (J elements): one lane offset, the 64 k steps as scalar offsets;
   // columns past J read 0 (their g slice is -1e300: no contribution) without a clamp per column
-  const uint32_t voff = (uint32_t)(c0 + lane) * sizeof(T);
-  auto load = [&](T (&kv)[NCM], int r) {
+  const uint32_t voff = (uint32_t)(c0 + lbase) * sizeof(T);
+  auto load = [&](T (&kv)[NCM], double& fv, double& wv, int r) {
+    fv = d.f[(int64_t)slot_fp * a.I + r];
+    wv = a.wa[r];
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(C + (int64_t)r * a.ldc), (short)0, a.J * (int)sizeof(T), 0x00020000);
+    if constexpr (PAIR) {
 #pragma unroll
-    for (int k = 0; k < NCM; ++k) {
-      if constexpr (sizeof(T) == 4)
-        kv[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, 256 * k, 0));
-      else
-        kv[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 512 * k, 0));
+      for (int p = 0; p < NCM / 2; ++p) {
+        const uint64_t v = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
+            rs, voff, 512 * p, 0));
+        kv[2 * p] = __builtin_bit_cast(T, (uint32_t)v);
+        kv[2 * p + 1] = __builtin_bit_cast(T, (uint32_t)(v >> 32));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NCM; ++k) {
+        if constexpr (sizeof(T) == 4)
+          kv[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, 256 * k, 0));
+        else
+          kv[k] = __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 512 * k, 0));
+      }
     }
   };
   // the first row's loads go out before the stop decision (round trips on the status block)
-  if (r0 < r1) load(kA, r0);
+  if (r0 < r1) load(kA, fA, wA, r0);
   if (!PH0 && knopp_stop(d, it)) return;
   double acc[NCM];
 #pragma unroll
   for (int k = 0; k < NCM; ++k) acc[k] = 0.0;
   const double neg_s = -a.inv_eps;
-  int nfb = 0;  // SH: rows listed for the exact update (k_lsk_fix)
-  auto process = [&](const T (&kv)[NCM], int r, int par) {
+  int nfb = 0;  // rows listed for the exact update (k_lsk_fix)
+  auto process = [&](const T (&kv)[NCM], const double fv, const double wv, int r, int par) {
     // x = (g_j + k_ij) in units of ln2 / 2048; masked terms -3e303 (exp2x -> 0).  The slice of g
     // is re-read from LDS per row (opaque to hoisting: held in registers it would cost 2 NCM)
     asm volatile("" ::: "memory");
     double e[NCM];
     if (PH0) {
-      const double f0 = d.f[(int64_t)slot_fp * a.I + r] * kFScale;
+      const double f0 = fv * kFScale;
 #pragma unroll
       for (int k = 0; k < NCM; ++k) {
         const double kn = (double)kv[k] * neg_s;
         const double kk = kn < kExpUnderflow ? -1e300 : kn;
-        e[k] = exp2x(__builtin_fma(kk, kFScale, gl[64 * k] + f0), tab);
+        e[k] = exp2x(__builtin_fma(kk, kFScale, gl[eo(k)] + f0), tab);
         acc[k] += e[k];
       }
       return;
     }
-    const bool exact = !SH;  // the running-maximum form (GNNEA_SK_FUSED=max)
-    if (SH) {
-      // shifted by f_prev: x + f_prev = log P(u_prev, v_it)_ij <= log b_j (v_it = b / K^T u_prev),
-      // so e_ij = P(u_prev, v_it)_ij needs no running maximum; s_i = u_prev (K v_it)_i
-      const double fp = d.f[(int64_t)slot_fp * a.I + r];
-      const double fps = fp * kFScale;
-      double rsum = 0.0;
-#pragma unroll
-      for (int k = 0; k < NCM; ++k) {
-        const double kn = (double)kv[k] * neg_s;
-        const double kk = kn < kExpUnderflow ? -1e300 : kn;
-        e[k] = exp2x(__builtin_fma(kk, kFScale, gl[64 * k] + fps), tab);
-        rsum += e[k];
-        if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);
-      }
-      rsum = wave_sum_f64(rsum);
-      if (lane == 0) reds[par][w] = rsum;
-      __syncthreads();  // double-buffered by row parity: one barrier per row
-      double sr = 0.0;
-#pragma unroll
-      for (int q = 0; q < kFW; ++q) sr += reds[par][q];  // every wave, the same order
-      // (NaN -- in C or a potential -- propagates through the fast path; the row update flags it)
-      if ((sr >= kFLo && sr <= kFHi) || sr != sr) {  // u_it / u_prev = a / s
-        const double wi = a.wa[r] / sr;
-        // f_it = f_prev + log a - log s, written by k_lsk_fix (no log in the streaming kernel)
-        if (w == 0 && lane == 0) d.rowbuf[r] = sr;
-#pragma unroll
-        for (int k = 0; k < NCM; ++k) acc[k] = __builtin_fma(e[k], wi, acc[k]);
-        return;
-      }
-      // out of range (uniform: every wave summed the same partials): the row is listed for
-      // k_lsk_fix, which writes its exact update and adds its column contributions to this
-      // workgroup's partial row after the sweep; nothing of it goes into acc
-      if (w == 0 && lane == 0) {
-        d.fbrows[(int64_t)blockIdx.x * rpw + nfb] = r;
-        d.rowbuf[r] = -1.0;  // (k_lsk_fix: listed, not a row sum)
-      }
-      ++nfb;
-      return;
-    }
-    if (!exact) return;
-    double mw = -1e308;
+    // shifted by f_prev: x + f_prev = log P(u_prev, v_it)_ij <= log b_j (v_it = b / K^T u_prev),
+    // so e_ij = P(u_prev, v_it)_ij needs no running maximum; s_i = u_prev (K v_it)_i
+    const double fps = fv * kFScale;
+    double rsum = 0.0;
 #pragma unroll
     for (int k = 0; k < NCM; ++k) {
       const double kn = (double)kv[k] * neg_s;
       const double kk = kn < kExpUnderflow ? -1e300 : kn;
-      e[k] = __builtin_fma(kk, kFScale, gl[64 * k]);
-      mw = fmax(mw, e[k]);
-      if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound the live temporaries
-    }
-    mw = wave_max(mw);
-    double sw = 0.0;
-#pragma unroll
-    for (int k = 0; k < NCM; ++k) {
-      e[k] = exp2x(e[k] - mw, tab);  // <= 1
-      sw += e[k];
+      e[k] = exp2x(__builtin_fma(kk, kFScale, gl[eo(k)] + fps), tab);
+      rsum += e[k];
       if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);
     }
-    sw = wave_sum_f64(sw);
-    if (lane == 0) {
-      redm[par][w] = mw;
-      reds[par][w] = sw;
-    }
-    __syncthreads();  // double-buffered by row parity: one barrier per row
-    // the row's LSE from the wave pairs, lane q holding wave q's (every wave the same sums):
-    // M = max_q M_q, s = sum_q s_q 2^((M_q - M) / 2048)
-    const double mq = lane < kFW ? redm[par][lane] : -1e308;
-    const double M = wave_max(mq);
-    const double sr = wave_sum_f64(lane < kFW ? reds[par][lane] * exp2x(mq - M, tab) : 0.0);
-    // f_new = log a - LSE_j(g_j + k_ij) (u = a / (K v)); P(u_new, v)_ij = e_ij 2^(M_w - M) a / s
-    const double wi = exp2x(mw - M, tab) * (a.wa[r] / sr);
-    if (w == 0 && lane == 0) {
-      const double fnew = a.la[r] - (M / kFScale + log(sr));
-      d.f[(int64_t)slot_fo * a.I + r] = fnew;
-      if (!(fnew <= kExpOverflow)) mark_done(d.st, it, 2, (it + 1) & 1);  // u inf / NaN
-    }
+    rsum = wave_sum_f64(rsum);
+    if (lane == 0) reds[par][w] = rsum;
+    row_barrier();  // double-buffered by row parity: one barrier per row
+    double sr = 0.0;
 #pragma unroll
-    for (int k = 0; k < NCM; ++k) acc[k] = __builtin_fma(e[k], wi, acc[k]);
+    for (int q = 0; q < kFW; ++q) sr += reds[par][q];  // every wave, the same order
+    // (NaN -- in C or a potential -- propagates through the fast path; the row update flags it)
+    if ((sr >= kFLo && sr <= kFHi) || sr != sr) {  // u_it / u_prev = a / s
+      const double wi = wv / sr;
+      // f_it = f_prev + log a - log s, written by k_lsk_fix (no log in the streaming kernel)
+      if (w == 0 && lane == 0) d.rowbuf[r] = sr;
+#pragma unroll
+      for (int k = 0; k < NCM; ++k) acc[k] = __builtin_fma(e[k], wi, acc[k]);
+      return;
+    }
+    // out of range (uniform: every wave summed the same partials): the row is listed for
+    // k_lsk_fix, which writes its exact update and adds its column contributions to this
+    // workgroup's partial row after the sweep; nothing of it goes into acc
+    if (w == 0 && lane == 0) {
+      d.fbrows[(int64_t)blockIdx.x * rpw + nfb] = r;
+      d.rowbuf[r] = -1.0;  // (k_lsk_fix: listed, not a row sum)
+    }
+    ++nfb;
+    return;
   };
+  // the next row's loads go out unconditionally (past the last row: the last row again), so
+  // every path into a row's processing has the same loads outstanding and its waits are counted
+  // vmcnt(NCM loads of the next row) -- a conditional load made the compiler wait for the
+  // count of the path without it, i.e. for most of the next row's loads
   int r = r0, par = 0;
   while (r < r1) {
-    if (r + 1 < r1) load(kB, r + 1);
-    process(kA, r, par);
+    load(kB, fB, wB, min(r + 1, r1 - 1));
+    process(kA, fA, wA, r, par);
     if (r + 1 >= r1) break;
-    if (r + 2 < r1) load(kA, r + 2);
-    process(kB, r + 1, par ^ 1);
+    load(kA, fA, wA, min(r + 2, r1 - 1));
+    process(kB, fB, wB, r + 1, par ^ 1);
     r += 2;
   }
-  double* __restrict__ part = d.fpart + (int64_t)blockIdx.x * a.J + c0 + lane;
+  double* __restrict__ part = d.fpart + (int64_t)blockIdx.x * a.J + c0 + lbase;
 #pragma unroll
   for (int k = 0; k < NCM; ++k)
-    if (64 * k < lim) part[64 * k] = acc[k];
-  if (SH && !PH0 && tid == 0) d.fbcnt[blockIdx.x] = nfb;
+    if (eo(k) < limv) part[eo(k)] = acc[k];
+  if (!PH0 && tid == 0) d.fbcnt[blockIdx.x] = nfb;
 }
 
 // The exact row update for the rows a fused sweep workgroup listed (k_lsk_sweep, SH): per row in
@@ -1177,10 +1185,10 @@ __global__ __launch_bounds__(1024) void k_lsk_colfin(const T* __restrict__ C, Sk
   }
 }
 
-// the fused sweep serves KNOPP for J <= kFMaxJ (GNNEA_SK_FUSED=0 keeps the two passes: A/B only)
+// the fused sweep serves KNOPP for J <= kFMaxJ (flag GNNEA_SK_TWO_PASS keeps the two passes: the
+// parity tests compare the two)
 static bool fused_applies(const gnnea_sinkhorn* p) {
-  const char* e = getenv("GNNEA_SK_FUSED");  // read per call: tests switch it between solves
-  const bool on = !(e && e[0] == '0');
+  const bool on = !(p->flags & GNNEA_SK_TWO_PASS);
   // fp64 C: the slice's loads double, J <= kFMaxJ / 2 keeps them in registers
   return on && p->mode == GNNEA_SK_KNOPP &&
          p->J <= (p->c_dtype == GNNEA_F64 ? kFMaxJ / 2 : kFMaxJ);
@@ -1188,35 +1196,33 @@ static bool fused_applies(const gnnea_sinkhorn* p) {
 
 bool fused_ok(const gnnea_sinkhorn* p) { return p && fused_applies(p); }
 
-template <typename T, bool PH0, bool SH>
-static void launch_fused_sweep_sh(const T* C, const SkArgs& a, const SkDev& d, int it, int sfp,
-                                  int sg, int sfo, hipStream_t s) {
+template <typename T, bool PH0, bool PAIR>
+static void launch_fused_sweep_p(const T* C, const SkArgs& a, const SkDev& d, int it, int sfp,
+                                 int sg, int sfo, hipStream_t s) {
   const int rpw = fused_rpw(a.I), ns = fused_wgs(a.I);
   const int nc = (((a.J + kFW - 1) / kFW + 63) & ~63) / 64;
   const dim3 g(ns), b(64 * kFW);
   if (nc <= 4)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 4, PH0, SH>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+    hipLaunchKernelGGL((k_lsk_sweep<T, 4, PH0, PAIR>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
   else if (nc <= 8)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 8, PH0, SH>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+    hipLaunchKernelGGL((k_lsk_sweep<T, 8, PH0, PAIR>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
   else if (sizeof(T) == 8 || nc <= 16)  // (fp64 C: fused_applies bounds nc by 16)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 16, PH0, SH>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+    hipLaunchKernelGGL((k_lsk_sweep<T, 16, PH0, PAIR>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
   else if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 32, PH0, SH>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+    hipLaunchKernelGGL((k_lsk_sweep<T, 32, PH0, PAIR>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
 }
 
-// GNNEA_SK_FUSED=max: the per-row running-maximum form of the row pass (A/B only)
-static bool fused_shift() {
-  const char* e = getenv("GNNEA_SK_FUSED");
-  return !(e && e[0] == 'm');
-}
-
+// fp32 C whose rows start on 8-B boundaries and hold whole column pairs: the PAIR layout
 template <typename T, bool PH0>
 static void launch_fused_sweep(const T* C, const SkArgs& a, const SkDev& d, int it, int sfp,
                                int sg, int sfo, hipStream_t s) {
-  if (PH0 || fused_shift())  // (PH0 has no row update: one instantiation)
-    launch_fused_sweep_sh<T, PH0, true>(C, a, d, it, sfp, sg, sfo, s);
-  else
-    launch_fused_sweep_sh<T, PH0, false>(C, a, d, it, sfp, sg, sfo, s);
+  if constexpr (sizeof(T) == 4) {
+    if (a.J % 2 == 0 && a.ldc % 2 == 0 && ((uintptr_t)C & 7) == 0) {
+      launch_fused_sweep_p<T, PH0, true>(C, a, d, it, sfp, sg, sfo, s);
+      return;
+    }
+  }
+  launch_fused_sweep_p<T, PH0, false>(C, a, d, it, sfp, sg, sfo, s);
 }
 
 // Launch configurations of the two passes (10*row + col); the path runs configuration 0, the
@@ -1280,12 +1286,7 @@ static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t 
   // default pass configuration: the fused column pass serialises I / 64 rows per thread, the
   // split pass (row splits + combine) fills the chip at large I: 1.065 -> 0.780 ms per KNOPP
   // iteration at B = 15000, equal within 5 % at B = 3000 (tools/dbg/sk_log_cfg.py)
-  int rv = 0, cv = p->I > 4096 ? 1 : 0;
-  if (const char* e = getenv("GNNEA_SK_LOG_CFG")) {  // tuning override only: 10*row + col
-    const int v = atoi(e);
-    rv = v / 10;
-    cv = v % 10;
-  }
+  const int rv = 0, cv = p->I > 4096 ? 1 : 0;
   const dim3 gabs(div_up(p->I, 4));
   const T* C = (const T*)p->C;
   const bool fused = fused_applies(p);
@@ -1297,8 +1298,7 @@ static int sk_iter_t(const gnnea_sinkhorn* p, int first, int count, hipStream_t 
       hipLaunchKernelGGL(k_lsk_colfin<T>, dim3(d.ncb), dim3(1024), 0, s, C, a, d,
                          fused_wgs(a.I), prev, prev, cur);
       launch_fused_sweep<T, false>(C, a, d, it, prev, cur, cur, s);
-      if (fused_shift())
-        hipLaunchKernelGGL(k_lsk_fix<T>, dim3(fused_wgs(a.I)), dim3(64 * kFW), 0, s, C, a, d, it,
+      hipLaunchKernelGGL(k_lsk_fix<T>, dim3(fused_wgs(a.I)), dim3(64 * kFW), 0, s, C, a, d, it,
                            prev, cur, cur, fused_rpw(a.I));
     } else if (p->mode == GNNEA_SK_KNOPP) {
       launch_col<T, true>(cv, C, a, d, it, prev, prev, cur, s);  // sets d.ncb for the row pass

@@ -39,6 +39,8 @@ GNNEA_SK_STATUS_BYTES = 256
 GNNEA_SK_PATH_SWEEP, GNNEA_SK_PATH_ONCHIP, GNNEA_SK_PATH_LOG = 0, 1, 2
 GNNEA_SK_ST_TIMEOUT = 16  # status word: an inter-workgroup wait of k_sk_res timed out
 GNNEA_SK_NO_ONCHIP = 1  # gnnea_sinkhorn.flags: never the on-chip persistent path
+GNNEA_SK_TWO_PASS = 2  # gnnea_sinkhorn.flags: KNOPP log domain as two passes (not the fused sweep)
+GNNEA_SK_DEBUG_SPIN = 4  # gnnea_sinkhorn.flags: zero wait budget on chip (timeout-path tests)
 GNNEA_SK_AUTO = 3  # gnnea_sinkhorn.variant: on chip / fused log-domain sweep / scaling form
 
 _p = ctypes.c_void_p
@@ -267,6 +269,8 @@ SIGNATURES = {
     "gnnea_ub_copy": (ctypes.c_int, [_p, _p, _i64, _i32, _i32, _p]),
     "gnnea_ub_gather": (ctypes.c_int, [_p, _i64, _p, _i64, _p, _i32, _p]),
     "gnnea_l1_rank_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _p, _p]),
+    "gnnea_l1_rank_range_f32": (ctypes.c_int, [_p, _i64, _i32, _p, _i64, _i32, _i32, _p, _i32, _p,
+                                               _p]),
     "gnnea_topk_rows_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _i64, _p, _i64, _i32,
                                            _i32, _p, _p, _i32, _p, _p]),
     "gnnea_margin_fwd_f32": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p, _p,

@@ -358,6 +358,17 @@ class DistAdj:
         r, c, v = shard_coo(triples, n, t, part)
         return cls(part, r, c, v, device, engine)
 
+    @classmethod
+    def from_shard(cls, shard):
+        """The layers' view of a bench KGShard (gnnea.dist, rows partition): its CSR and KG
+        group are shared, nothing is rebuilt."""
+        if shard.part.kind != "rows":
+            raise ValueError("gnnea.DistAdj: the layers need the row partition")
+        self = cls.__new__(cls)
+        self.part, self.device, self.engine = shard.part, shard.device, HipEngine()
+        self.nnz, self.csr, self.group = shard.nnz, shard.csr, shard.group
+        return self
+
     # ---- the drop-in layer hooks ------------------------------------------------------------
     def aggregate(self, hidden, act_fn):
         from .ops import act_code
@@ -742,6 +753,154 @@ class GatherRowsFn(torch.autograd.Function):
     def backward(ctx, dfull):
         r0 = ctx.rank * ctx.rows
         return dfull[r0:r0 + ctx.rows].contiguous(), None
+
+
+def _world_reduce(vals, op):
+    """All-reduce a few float64 scalars over the world (host tensors under gloo)."""
+    if dist.get_backend() == "gloo":
+        t = torch.tensor(vals, dtype=torch.float64)
+    else:
+        t = torch.tensor(vals, dtype=torch.float64,
+                         device=torch.device("cuda", torch.cuda.current_device()))
+    dist.all_reduce(t, op=op)
+    return t.cpu().tolist()
+
+
+def _world_sum(t):
+    """Sum of a tensor over every rank (the replicated parameters' gradients)."""
+    t = t.detach().contiguous()
+    if dist.get_backend() == "gloo" and t.device.type != "cpu":
+        h = t.cpu()
+        dist.all_reduce(h)
+        return h.to(t.device)
+    t = t.clone()
+    dist.all_reduce(t)
+    return t
+
+
+def validate_staged(dadj, D=300, heads=4, alpha=0.2, dtype=None, reps=3, tol=1e-6, seed=0,
+                    apply=True):
+    """Prove the per-slice halo pipeline on this job's own ranks before it is used (SURVEY.md §8e;
+    layers/layers.py:35,64, layers/att_layers.py:45-58): one HighWay layer tail
+    (HaloHighwayFn), one GCN aggregation (HaloAggregateFn) and one all-head GAT layer
+    (HaloGATFn), forward + backward on the same seeded inputs with exchange.STAGED off, then on.
+    Compared: outputs, input gradients and the world-summed `a` gradient, norm-relative
+    ‖staged − unstaged‖∞ / ‖unstaged‖∞, the max over tensors and ranks; `match` when it is
+    ≤ ``tol`` and finite on every rank (one all-reduce decides, so all ranks agree).  Each leg is
+    timed both ways (median of ``reps`` fwd + bwd after one warm-up, wall clock bracketed by
+    barriers and device syncs, max over ranks).  ``apply``: leave exchange.STAGED = match
+    (GNNEA_HALO_STAGED=0 keeps it off whatever the outcome).  Every rank must call this.
+    Returns the report (the same dict on every rank)."""
+    import time
+
+    import torch.nn.functional as F
+
+    from . import exchange
+    part = dadj.part
+    if part.g == 1:
+        return {"applies": False, "reason": "one KG per rank: nothing to exchange"}
+    dev = dadj.device
+    if dtype is None:
+        dtype = torch.float64 if dev.type == "cpu" else torch.float32
+    d_head = D // heads
+    n = part.n_rows
+    # the rows are the rank's own; the parameters (bias_gate, a) are replicated on every rank
+    rows_gen = torch.Generator(device=dev).manual_seed(seed * 1000 + 1 + part.rank)
+    par_gen = torch.Generator(device=dev).manual_seed(seed * 1000)
+
+    def rnd(*shape, scale=1.0, gen=rows_gen):
+        return (scale * torch.randn(*shape, generator=gen, device=dev, dtype=torch.float32)
+                ).to(dtype)
+    hidden, gate_pre, resid = rnd(n, D), rnd(n, D), rnd(n, D)
+    bias_gate = rnd(D, scale=0.1, gen=par_gen)
+    dY = rnd(n, D)
+    H = rnd(n, heads * d_head, scale=0.3)
+    a_all = rnd(heads, 2 * d_head, scale=0.3, gen=par_gen)
+    dYg = rnd(n, heads * d_head)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    def leg_highway():
+        xs = [t.clone().requires_grad_() for t in (hidden, gate_pre, resid)]
+        out = dadj.highway(xs[0], xs[1], xs[2], bias_gate, F.relu)
+        out.backward(dY)
+        return [out.detach()] + [x.grad for x in xs]
+
+    def leg_gcn():
+        x = hidden.clone().requires_grad_()
+        out = dadj.aggregate(x, F.relu)
+        out.backward(dY)
+        return [out.detach(), x.grad]
+
+    def leg_gat():
+        h = H.clone().requires_grad_()
+        a = a_all.clone().requires_grad_()
+        out = dadj.gat(h, a, heads, d_head, alpha, F.relu)
+        out.backward(dYg)
+        return [out.detach(), h.grad, _world_sum(a.grad)]
+    legs = {"highway": leg_highway, "gcn": leg_gcn}
+    if dadj.engine.gat_staged_ok(heads, d_head) if hasattr(dadj.engine, "gat_staged_ok") \
+            else False:
+        legs["gat"] = leg_gat
+
+    def timed(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            sync()
+            dist.barrier()
+            t0 = time.perf_counter()
+            fn()
+            sync()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e3
+
+    keep = exchange.STAGED
+    res, ms = {}, {}
+    try:
+        for mode in (False, True):
+            exchange.STAGED = mode
+            for name, fn in legs.items():
+                res[(name, mode)] = [t.detach().clone() for t in fn()]
+                ms[(name, mode)] = timed(fn)
+    finally:
+        exchange.STAGED = keep
+    errs = []
+    for name in legs:
+        e = 0.0
+        for s, u in zip(res[(name, True)], res[(name, False)]):
+            s, u = s.double(), u.double()
+            if not bool(torch.isfinite(s).all()) or s.shape != u.shape:
+                e = float("inf")
+                break
+            den = float(u.abs().max()) if u.numel() else 0.0
+            num = float((s - u).abs().max()) if u.numel() else 0.0
+            e = max(e, num / den if den > 0 else (0.0 if num == 0 else float("inf")))
+        errs.append(e)
+    # one all-reduce: every rank's errors (max) and its leg times (max over ranks)
+    times = [ms[(k, m)] for k in legs for m in (True, False)]
+    red = _world_reduce([min(e, 1e300) for e in errs] + times, dist.ReduceOp.MAX)
+    errs, times = red[:len(legs)], red[len(legs):]
+    err = max(errs)
+    match = err <= tol
+    report = {"applies": True, "match": bool(match), "tol": tol, "max_norm_rel_err": err,
+              "legs": {}, "dtype": str(dtype).replace("torch.", ""), "D": D, "heads": heads,
+              "reps": reps, "world": part.world, "group_ranks": part.g,
+              "method": "staged vs unstaged on the same inputs: outputs, input gradients and "
+                        "the world-summed attention-vector gradient, norm-relative, max over "
+                        "tensors and ranks; fwd + bwd wall ms, median of %d, max over ranks"
+                        % reps}
+    for i, k in enumerate(legs):
+        report["legs"][k] = {"err": errs[i], "staged_ms": round(times[2 * i], 4),
+                             "unstaged_ms": round(times[2 * i + 1], 4)}
+    report["staged_ms"] = round(sum(times[0::2]), 4)
+    report["unstaged_ms"] = round(sum(times[1::2]), 4)
+    if apply:
+        exchange.STAGED = bool(match) and exchange.STAGED_ENV != "0"
+    report["staged_in_use"] = bool(exchange.STAGED) if apply else bool(keep)
+    return report
 
 
 def allreduce_grads(params, group=None):

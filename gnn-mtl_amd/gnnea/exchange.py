@@ -36,13 +36,17 @@ import torch
 import torch.distributed as dist
 
 MODE = os.environ.get("GNNEA_HALO", "relay")
-# GNNEA_HALO_STAGED=1: the per-column-slice pipeline (all_gather_slices / reduce_scatter_start:
-# several RCCL group calls in flight, each slice aggregated as soon as it has landed).  Default
-# (0): the unstaged path -- the whole halo row-major, then one aggregation, and one blocking
-# reduce-scatter back.  Both are exercised with gloo at world 2 / 4 / 8 and rehearsed on one
-# MI355X (host-staged); RCCL refuses two ranks on one device ("Duplicate GPU detected"), so the
-# staged path's asynchronous RCCL behaviour has not run on hardware yet and stays opt-in.
-STAGED = os.environ.get("GNNEA_HALO_STAGED", "0") == "1"
+# The per-column-slice pipeline (all_gather_slices / reduce_scatter_start: several RCCL group
+# calls in flight, each slice aggregated as soon as it has landed) against the unstaged path (the
+# whole halo row-major, then one aggregation, and one blocking reduce-scatter back).  Both are
+# exercised with gloo at world 2 / 4 / 8 and rehearsed on one MI355X (host-staged); RCCL refuses
+# two ranks on one device ("Duplicate GPU detected"), so the staged path's asynchronous RCCL
+# behaviour is proven on the job's own ranks: gnnea.dist_graph.validate_staged runs a HighWay,
+# a GCN and a GAT layer both ways on the same inputs, and switches STAGED on only when every
+# rank saw the two agree.  GNNEA_HALO_STAGED: "auto" (default: unstaged until validated), "1"
+# (staged without validation), "0" (never staged, validate_staged reports but keeps it off).
+STAGED_ENV = os.environ.get("GNNEA_HALO_STAGED", "auto")
+STAGED = STAGED_ENV == "1"
 
 
 def _gloo(group):
@@ -238,7 +242,9 @@ def all_gather(h_loc, full, group, ranks, li, copy_own=False, async_op=False, ot
 class PendingSum:
     """An issued reduce-scatter: ``finish()`` waits for the receives (stream-ordered on the
     caller's stream for RCCL) and returns the owner's rows: its own partial plus the peers'
-    partials in peer order (deterministic, no RCCL reduction kernel)."""
+    partials in peer order (deterministic, no RCCL reduction kernel) for the relay and direct
+    schedules.  Under GNNEA_HALO=ring ``own`` is already RCCL's reduce_scatter result, whose
+    summation order is RCCL's (not order-deterministic across ring configurations)."""
 
     def __init__(self, own, recv, works, out=None):
         self.own, self.recv, self.works, self.out = own, recv, works, out

@@ -67,6 +67,25 @@ def ranks(Q, X, diag):
     return out
 
 
+def ranks_range(Q, X, diag, x_off):
+    """int32 count, per row q of Q, of the candidates X = [x_off, x_off + len(X)) of a larger
+    candidate list that come before candidate q in the stable distance order of row q (the
+    row-sharded get_hits sums these over the ranks)."""
+    Q = _rows(Q)
+    nq, D = Q.shape
+    X = _rows(X) if X.shape[0] else X
+    if X.shape[0] and X.shape[1] != D:
+        raise ValueError("gnnea.l1.ranks_range: dim mismatch")
+    diag = diag.to(device=Q.device, dtype=torch.float64).contiguous()
+    out = torch.empty(nq, dtype=torch.int32, device=Q.device)
+    with _lib.on_device(Q.device):
+        check(_lib.lib().gnnea_l1_rank_range_f32(
+            ptr(Q), Q.stride(0), nq, ptr(X) if X.shape[0] else None,
+            X.stride(0) if X.shape[0] else D, X.shape[0], D, ptr(diag), int(x_off), ptr(out),
+            stream_of(Q.device)))
+    return out
+
+
 def hits_ranks(L, R):
     """(rank_lr, rank_rl) of the aligned pairs (L[i], R[i]) in both search directions."""
     diag = pairs(L, R)

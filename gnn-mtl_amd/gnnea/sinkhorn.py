@@ -17,6 +17,9 @@ ST_DONE, ST_ITERS, ST_REASON, ST_SLOT = 0, 1, 2, 3
 # sweep), 3 = GNNEA_SK_AUTO: KNOPP on chip where it fits, else the fused log-domain sweep (one
 # pass over C per iteration), the STAB family as 0
 DEFAULT_VARIANT = _lib.GNNEA_SK_AUTO
+# gnnea_sinkhorn.flags of solve() calls that pass none (the drop-in ot_loss / sinkhorn_loss
+# functions): 0; tests select a path by setting it (GNNEA_SK_NO_ONCHIP: the resident-K sweep)
+DEFAULT_FLAGS = 0
 SD_ERR, SD_TPREV, SD_LOSS, SD_TNEW = 8, 9, 10, 12  # GNNEA_SK_SD_* (include/gnnea.h)
 MAX_BATCH = 100  # iterations enqueued between two host polls of the status block, at most
 
@@ -76,17 +79,27 @@ class _StatusPoll:
         return self.buf[:, ST_DONE].clone()
 
 
+def _retry_flags(flags):
+    """The re-solve after an on-chip timeout: never on chip (the debug bit is moot there)."""
+    return (flags | _lib.GNNEA_SK_NO_ONCHIP) & ~_lib.GNNEA_SK_DEBUG_SPIN
+
+
 def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
-          want_plan=True, batch=10, variant=None):
+          want_plan=True, batch=10, variant=None, flags=None):
     """Run one Sinkhorn solve; C is [I, J] fp32 / fp64 on a HIP device, a / b the weights.
-    An on-chip solve whose inter-workgroup wait timed out is solved again from the start on
-    the sweep path (same iterates: both paths run the reference's operations)."""
+    ``flags``: gnnea_sinkhorn.flags bits (GNNEA_SK_NO_ONCHIP, GNNEA_SK_TWO_PASS,
+    GNNEA_SK_DEBUG_SPIN).  An on-chip solve whose inter-workgroup wait timed out is solved again
+    from the start on the sweep path (same iterates: both paths run the reference's operations);
+    the result then carries ``onchip_timeout = True``."""
+    flags = DEFAULT_FLAGS if flags is None else flags
     try:
         return _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch,
-                      variant, 0)
+                      variant, flags)
     except SinkhornTimeout:
-        return _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch,
-                      variant, _lib.GNNEA_SK_NO_ONCHIP)
+        res = _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch,
+                     variant, _retry_flags(flags))
+        res.onchip_timeout = True
+        return res
 
 
 def _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch, variant, flags):
@@ -164,21 +177,27 @@ def _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch, v
                          float(dbl[SD_ERR]), float(dbl[SD_TNEW]), float(dbl[SD_TPREV]),
                          float(dbl[SD_LOSS]))
     res.path = ("sweep", "onchip", "logdomain")[path]  # gnnea_sinkhorn_path
+    res.onchip_timeout = False
     return res
 
 
 def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64, batch=10,
-                variant=None):
+                variant=None, flags=None):
     """Solve a batch of problems of one shape [bt, I, J] as ONE launch sequence: every problem's
     iterations are enqueued batch by batch on the same stream and ONE device->host copy of all
     status blocks per round decides which problems continue (solve() polls once per problem
     per round).  Cs [bt, I, J], As [bt, I], Bs [bt, J] on the device; returns SinkhornResults.
     A timed-out on-chip wait re-runs the batch on the sweep path, as solve() does."""
+    flags = DEFAULT_FLAGS if flags is None else flags
     try:
-        return _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, variant, 0)
-    except SinkhornTimeout:
         return _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, variant,
-                            _lib.GNNEA_SK_NO_ONCHIP)
+                            flags)
+    except SinkhornTimeout:
+        out = _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, variant,
+                           _retry_flags(flags))
+        for r in out:
+            r.onchip_timeout = True
+        return out
 
 
 def _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, variant, flags):
@@ -252,6 +271,7 @@ def _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, var
         out.append(SinkhornResult(plan, row_sum, col_sum, int(ints[ST_ITERS]),
                                   int(ints[ST_REASON]), float(dbl[SD_ERR]), float(dbl[SD_TNEW]),
                                   float(dbl[SD_TPREV]), float(dbl[SD_LOSS])))
+        out[-1].onchip_timeout = False
     return out
 
 

@@ -12,7 +12,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from gnnea import l1, margin
+from gnnea import dist_search, l1, margin
 from gnnea.dist_graph import DistAdj
 from gnnea.dist_loss import sharded_margin_loss
 from models.decoders import model2decoder
@@ -45,9 +45,22 @@ class BaseModel(nn.Module):
         self.n_nodes = args.n_nodes
         self.device = args.device
 
+    def _shard(self, output):
+        """The DistAdj of the last encode when ``output`` is this rank's rows of a row-sharded
+        output (several ranks), else None (a gathered or single-GPU output)."""
+        dadj = getattr(self, "_dadj", None)
+        if dadj is not None and dadj.part.world > 1 and output.shape[0] == dadj.part.n_rows:
+            return dadj
+        return None
+
     def get_neg(self, ILL, output, k):
         """The k L1-nearest entities of each ILL entity, nearest first, the entity itself (rank 0)
-        excluded; flattened to t*k (models/models_ea.py:19-30)."""
+        excluded; flattened to t*k (models/models_ea.py:19-30).  On a row-sharded output (the
+        rank's rows after a DistAdj encode): every rank searches its own rows, the per-rank lists
+        are merged (gnnea.dist_search; index-exact with the single-GPU search)."""
+        dadj = self._shard(output) if self is not None else None
+        if dadj is not None:
+            return dist_search.get_neg(ILL, output, dadj.part, k)
         out = output.detach()
         if not out.is_cuda and torch.cuda.is_available():
             out = out.to("cuda")
@@ -78,6 +91,9 @@ class BaseModel(nn.Module):
 
     def compute_metrics(self, outputs, data, split):
         pair = data["train"] if split == "train" else data["test"]
+        dadj = self._shard(outputs) if self is not None else None
+        if dadj is not None:  # row-sharded output: per-rank candidate blocks, counts summed
+            return dist_search.get_hits(outputs, dadj.part, pair, top_k=[1])
         return get_hits(outputs, pair, top_k=[1])
 
     def has_improved(self, m1, m2):

@@ -47,8 +47,18 @@ def _metrics(rank_lr, rank_rl, top_k, n):
     return metrics
 
 
-def get_hits(vec, test_pair, top_k=(1, 10, 50, 100)):
-    """utils/eval_utils.py:71-98: Hits@k of the aligned pairs under the L1 distance, both ways."""
+def _sharded(vec, adj):
+    from gnnea.dist_graph import DistAdj
+    return isinstance(adj, DistAdj) and adj.part.world > 1 and vec.shape[0] == adj.part.n_rows
+
+
+def get_hits(vec, test_pair, top_k=(1, 10, 50, 100), adj=None):
+    """utils/eval_utils.py:71-98: Hits@k of the aligned pairs under the L1 distance, both ways.
+    ``adj``: the DistAdj of a row-sharded ``vec`` (this rank's rows; every rank calls this):
+    the ranks are counted over per-rank candidate blocks and summed (gnnea.dist_search)."""
+    if _sharded(vec, adj):
+        from gnnea import dist_search
+        return dist_search.get_hits(vec, adj.part, test_pair, top_k)
     vec = _on_device(vec)
     li, ri = _pair_index(test_pair, vec.device)
     rank_lr, rank_rl = l1.hits_ranks(vec[li], vec[ri])
@@ -71,9 +81,12 @@ def eval_gw_matching_matrix(T, test_pair, index1_R, index2_R, top_k=(1, 10, 50, 
     return _metrics(rank_lr, rank_rl, top_k, len(test_pair))
 
 
-def eval_at_1(outputs, data):
+def eval_at_1(outputs, data, adj=None):
     """utils/eval_utils.py:161-167: % of test entities whose L1-nearest right entity is the match
-    (argmin of exact fp64 distances, first index on ties)."""
+    (argmin of exact fp64 distances, first index on ties).  ``adj``: as get_hits."""
+    if _sharded(outputs, adj):
+        from gnnea import dist_search
+        return dist_search.eval_at_1(outputs, adj.part, data["test"])
     outputs = _on_device(outputs)
     li, ri = _pair_index(data["test"], outputs.device)
     idx, _ = l1.nearest(outputs[li], outputs[ri])

@@ -561,12 +561,18 @@ typedef struct gnnea_sinkhorn {
                        GNNEA_SK_AUTO (3, the Python default): KNOPP on chip where it fits, else
                           the fused log-domain sweep, else variant 0 / 1 as above; the STAB
                           family as variant 0 (sharded KNOPP: as variant 0) */
-  int flags;        /* GNNEA_SK_NO_ONCHIP: never take the on-chip cooperative KNOPP path (the
-                       host's retry after an inter-workgroup wait timed out); 0 otherwise */
+  int flags;        /* bit set: GNNEA_SK_NO_ONCHIP: never take the on-chip KNOPP path (the host's
+                       retry after an inter-workgroup wait timed out; A/B measurements);
+                       GNNEA_SK_TWO_PASS: KNOPP log domain as the two-pass form instead of the
+                       fused sweep (the parity tests compare the two);
+                       GNNEA_SK_DEBUG_SPIN: the on-chip kernel's inter-workgroup waits get a
+                       zero time budget, so it times out (tests of the timeout path) */
   void* ws;         /* device workspace of gnnea_sinkhorn_ws_bytes(I, J) bytes */
 } gnnea_sinkhorn;
 
 #define GNNEA_SK_NO_ONCHIP 1
+#define GNNEA_SK_TWO_PASS 2
+#define GNNEA_SK_DEBUG_SPIN 4
 #define GNNEA_SK_AUTO 3
 
 int64_t gnnea_sinkhorn_ws_bytes(int I, int J);
@@ -659,6 +665,13 @@ int gnnea_l1_pairs_f32(const float* A, int64_t lda, const float* B, int64_t ldb,
  * x = q in a stable argsort of row q (get_hits' rank_index).  rank is zeroed by the call. */
 int gnnea_l1_rank_f32(const float* Q, int64_t ldq, int32_t nq, const float* X, int64_t ldx,
                       int32_t nx, int32_t D, const double* diag, int32_t* rank, void* stream);
+/* The same count over one block of the candidates, X = candidates [x_off, x_off + nx): rank[q]
+ * = #{x : d < diag[q] or (d == diag[q] and x_off + x < q)} (no nq <= nx requirement).  The
+ * row-sharded get_hits (gnnea/dist_search.py) sums the blocks' counts over the ranks; replaces the
+ * same utils/eval_utils.py:71-98 argsort position as gnnea_l1_rank_f32. */
+int gnnea_l1_rank_range_f32(const float* Q, int64_t ldq, int32_t nq, const float* X, int64_t ldx,
+                            int32_t nx, int32_t D, const double* diag, int32_t x_off, int32_t* rank,
+                            void* stream);
 /* Per row q of keys (from gnnea_l1_keys_f32 of the same Q, X): the K smallest exact distances
  * ordered by (distance, index), entries [skip, K) written to out_idx / out_dist (nullable) rows
  * of stride ldo.  get_neg: K = k+1, skip = 1.  K <= 512.  *overflow (nullable) counts rows where

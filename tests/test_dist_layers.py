@@ -538,6 +538,65 @@ def test_dist_layers_bf16_rehearsal_on_device(device, staged):
     _run(4, "gpu_bf16", staged)
 
 
+class BrokenStagedEngine(CpuEngine):
+    """A staged pipeline that is wrong in one slice (test stand-in): validate_staged must see
+    the mismatch and leave the halo unstaged."""
+
+    def spmm_slice(self, A, table, w, act, out):
+        super().spmm_slice(A, table, w, act, out)
+        out.mul_(1.0 + 1e-3)
+        return out
+
+
+def _ab_worker(rank, world, port, broken, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "gnn-mtl_amd"))
+    from gnnea import exchange, synth
+    from gnnea.dist_graph import DistAdj, validate_staged
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        exchange.STAGED = False
+        exchange.STAGED_ENV = "auto"
+        tr = synth.kg_pair_triples(N_KG, T_KG, 20)
+        eng = BrokenStagedEngine() if broken else CpuEngine()
+        dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, torch.device("cpu"), engine=eng)
+        rep = validate_staged(dadj, D=D, heads=3, reps=2, tol=1e-12)
+        q.put((rank, rep["match"], rep["max_norm_rel_err"], exchange.STAGED,
+               sorted(rep["legs"]), rep["staged_in_use"]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,broken", [(4, False), (4, True), (8, False)])
+def test_validate_staged_gloo_cpu(world, broken):
+    """gnnea.dist_graph.validate_staged (the N > 1 bench's halo_ab): staged and unstaged HighWay,
+    GCN and GAT layers on the same inputs; a correct pipeline matches (fp64 engine: 1e-12) and is
+    switched on, a pipeline wrong in one slice is caught on every rank and the halo stays
+    unstaged."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ab_worker, args=(r, world, port, broken, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [q.get(timeout=5) for _ in range(world)]
+    for rank, match, err, staged, legs, in_use in res:
+        assert legs == ["gat", "gcn", "highway"]
+        assert match is (not broken), (rank, err)
+        assert staged is (not broken) and in_use is (not broken)
+        if broken:
+            assert err > 1e-4
+        else:
+            assert err <= 1e-12
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_dist_margin_loss_gloo_cpu(world):
     """Column-sharded EA margin loss (gnnea.dist_loss: all-to-all to column blocks, one

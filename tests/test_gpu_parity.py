@@ -266,11 +266,11 @@ def sk_path(request, monkeypatch):
     """Run a Sinkhorn test through every device path."""
     import gnnea.sinkhorn
     # onchip: KNOPP with K held in registers + LDS by the persistent k_sk_res where it fits
-    # (STAB family and larger problems take the sweep); sweep: GNNEA_SK_RESIDENT=0, the
+    # (STAB family and larger problems take the sweep); sweep: flag GNNEA_SK_NO_ONCHIP, the
     # resident-K sweep for every mode; logdomain: variant 1
     monkeypatch.setattr(gnnea.sinkhorn, "DEFAULT_VARIANT", 1 if request.param == "logdomain" else 0)
     if request.param == "sweep":
-        monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
+        monkeypatch.setattr(gnnea.sinkhorn, "DEFAULT_FLAGS", gnnea.sinkhorn._lib.GNNEA_SK_NO_ONCHIP)
     return request.param
 
 
@@ -360,11 +360,10 @@ def test_sinkhorn_onchip_matches_sweep(device, monkeypatch, I, J, reg, tol):
     Mt, at, bt = (torch.from_numpy(x).to(device) for x in (M, a, b))
     res = {}
     for path in ("onchip", "sweep"):
-        if path == "sweep":
-            monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
-        # the scaling form (variant 0): with resident K off, GNNEA_SK_AUTO would take the fused
-        # log-domain sweep instead
-        res[path] = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, reg, tol, 400, variant=0)
+        # the scaling form (variant 0): with the on-chip path off, GNNEA_SK_AUTO would take the
+        # fused log-domain sweep instead
+        res[path] = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, reg, tol, 400, variant=0,
+                              flags=_lib.GNNEA_SK_NO_ONCHIP if path == "sweep" else 0)
     r0, r1 = res["onchip"], res["sweep"]
     assert (r0.path, r1.path) == ("onchip", "sweep")
     assert (r0.iters, r0.reason) == (r1.iters, r1.reason), ((r0.iters, r0.reason),
@@ -393,12 +392,9 @@ def test_sinkhorn_onchip_bad_u_break(device):
     a, b = np.ones(I), np.ones(J) * I / J
     Mt, at, bt = (torch.from_numpy(x).to(device) for x in (M, a, b))
     out = []
-    for env in ("1", "0"):
-        os.environ["GNNEA_SK_RESIDENT"] = env
-        try:
-            out.append(gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, 0.05, 1e-9, 50, variant=0))
-        finally:
-            os.environ.pop("GNNEA_SK_RESIDENT", None)
+    for fl in (0, _lib.GNNEA_SK_NO_ONCHIP):
+        out.append(gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, at, bt, 0.05, 1e-9, 50, variant=0,
+                             flags=fl))
     r0, r1 = out
     assert (r0.path, r1.path) == ("onchip", "sweep")
     assert (r0.iters, r0.reason) == (r1.iters, r1.reason) and r0.reason == 2, \
@@ -417,14 +413,14 @@ def test_sinkhorn_logdomain_nonfinite_cost(device, monkeypatch, bad):
     plan where it is finite."""
     from gnnea import sinkhorn as gsk
     from gnnea import _lib
-    monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
     rng = np.random.default_rng(8)
     M = rng.uniform(0, 1, (300, 200))
     M[7, 11] = bad
     w = torch.ones(300, dtype=torch.float64, device=device)
     wb = torch.full((200,), 1.5, dtype=torch.float64, device=device)
     Mt = torch.from_numpy(M).to(device)
-    r0 = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, w, wb, 0.05, 1e-9, 50, variant=0)
+    r0 = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, w, wb, 0.05, 1e-9, 50, variant=0,
+                   flags=_lib.GNNEA_SK_NO_ONCHIP)
     r1 = gsk.solve(_lib.GNNEA_SK_KNOPP, Mt, w, wb, 0.05, 1e-9, 50, variant=1)
     assert (r1.iters, r1.reason) == (r0.iters, r0.reason), ((r1.iters, r1.reason),
                                                             (r0.iters, r0.reason))

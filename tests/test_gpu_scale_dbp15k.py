@@ -138,11 +138,11 @@ def test_dbp15k_ea_step_vs_reference(golden, device, dbp, model):
 def sk_path(request, monkeypatch):
     import gnnea.sinkhorn
     # onchip: KNOPP with K held in registers + LDS by the persistent k_sk_res where it fits
-    # (STAB family and larger problems take the sweep); sweep: GNNEA_SK_RESIDENT=0, the
+    # (STAB family and larger problems take the sweep); sweep: flag GNNEA_SK_NO_ONCHIP, the
     # resident-K sweep for every mode; logdomain: variant 1
     monkeypatch.setattr(gnnea.sinkhorn, "DEFAULT_VARIANT", 1 if request.param == "logdomain" else 0)
     if request.param == "sweep":
-        monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
+        monkeypatch.setattr(gnnea.sinkhorn, "DEFAULT_FLAGS", gnnea.sinkhorn._lib.GNNEA_SK_NO_ONCHIP)
     return request.param
 
 

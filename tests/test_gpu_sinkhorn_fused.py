@@ -1,6 +1,6 @@
 """The fused log-domain KNOPP sweep (csrc/sinkhorn_log.hip k_lsk_sweep + k_lsk_colfin: one pass
 over C per iteration, one exponential per element) against the two-pass log-domain form
-(GNNEA_SK_FUSED=0), the scaling form and the fp64 oracle (utils/ot_loss.py:5-76 restated in
+(flag GNNEA_SK_TWO_PASS), the scaling form and the fp64 oracle (utils/ot_loss.py:5-76 restated in
 oracle/sinkhorn.py).  The fused path is what variant 1 runs for KNOPP at J <= 16384 (fp32 C;
 8192 for fp64 C); every variant-1 fixture test (test_gpu_parity.py, test_gpu_scale_dbp15k.py)
 runs through it as well.
@@ -20,14 +20,11 @@ pytestmark = pytest.mark.gpu
 TOL64 = 1e-9
 
 
-def _solve(mode_env, monkeypatch, M, a, b, reg, tol=1e-9, iters=300, variant=1):
+def _solve(two_pass, M, a, b, reg, tol=1e-9, iters=300, variant=1, flags=0):
     from gnnea import _lib
     from gnnea.sinkhorn import solve
-    if mode_env is None:
-        monkeypatch.delenv("GNNEA_SK_FUSED", raising=False)
-    else:
-        monkeypatch.setenv("GNNEA_SK_FUSED", mode_env)
-    return solve(_lib.GNNEA_SK_KNOPP, M, a, b, reg, tol, iters, variant=variant)
+    return solve(_lib.GNNEA_SK_KNOPP, M, a, b, reg, tol, iters, variant=variant,
+                 flags=flags | (_lib.GNNEA_SK_TWO_PASS if two_pass else 0))
 
 
 @pytest.mark.parametrize("I,J,reg,dtype", [(300, 200, 0.05, torch.float64),
@@ -45,8 +42,8 @@ def test_fused_matches_two_pass(device, monkeypatch, I, J, reg, dtype):
     b *= a.sum() / b.sum()
     Mt = torch.from_numpy(M).to(device=device, dtype=dtype)
     at, bt = torch.from_numpy(a).to(device), torch.from_numpy(b).to(device)
-    rf = _solve(None, monkeypatch, Mt, at, bt, reg)
-    r2 = _solve("0", monkeypatch, Mt, at, bt, reg)
+    rf = _solve(False, Mt, at, bt, reg)
+    r2 = _solve(True, Mt, at, bt, reg)
     assert rf.path == r2.path == "logdomain"
     assert (rf.iters, rf.reason) == (r2.iters, r2.reason), ((rf.iters, rf.reason),
                                                             (r2.iters, r2.reason))
@@ -68,9 +65,9 @@ def test_fused_matches_scaling_form(device, monkeypatch):
     M = torch.from_numpy(rng.uniform(0, 1, (I, J))).to(device=device, dtype=torch.float32)
     a = torch.ones(I, dtype=torch.float64, device=device)
     b = torch.full((J,), I / J, dtype=torch.float64, device=device)
-    monkeypatch.setenv("GNNEA_SK_RESIDENT", "0")
-    rf = _solve(None, monkeypatch, M, a, b, reg)
-    rs = _solve(None, monkeypatch, M, a, b, reg, variant=0)
+    from gnnea import _lib
+    rf = _solve(False, M, a, b, reg)
+    rs = _solve(False, M, a, b, reg, variant=0, flags=_lib.GNNEA_SK_NO_ONCHIP)
     assert (rf.path, rs.path) == ("logdomain", "sweep")
     assert (rf.iters, rf.reason) == (rs.iters, rs.reason)
     assert rel_err(rf.plan.cpu(), rs.plan.cpu()) < 1e-11
@@ -88,8 +85,8 @@ def test_fused_exact_column_recompute(device, monkeypatch):
     M[:, 230] = 7.2                                    # exp(-720) ~ 1e-313: subnormal K
     a, b = np.ones(I), np.ones(J) * I / J
     Mt, at, bt = (torch.from_numpy(x).to(device) for x in (M, a, b))
-    rf = _solve(None, monkeypatch, Mt, at, bt, reg, iters=200)
-    r2 = _solve("0", monkeypatch, Mt, at, bt, reg, iters=200)
+    rf = _solve(False, Mt, at, bt, reg, iters=200)
+    r2 = _solve(True, Mt, at, bt, reg, iters=200)
     assert (rf.iters, rf.reason) == (r2.iters, r2.reason), ((rf.iters, rf.reason),
                                                             (r2.iters, r2.reason))
     f = torch.isfinite(r2.plan)
@@ -115,8 +112,8 @@ def test_fused_breaks(device, monkeypatch, what):
         M[7, 11] = float("-inf")
     a, b = np.ones(I), np.ones(J) * I / J
     Mt, at, bt = (torch.from_numpy(x).to(device) for x in (M, a, b))
-    rf = _solve(None, monkeypatch, Mt, at, bt, reg, iters=50)
-    r2 = _solve("0", monkeypatch, Mt, at, bt, reg, iters=50)
+    rf = _solve(False, Mt, at, bt, reg, iters=50)
+    r2 = _solve(True, Mt, at, bt, reg, iters=50)
     assert (rf.iters, rf.reason) == (r2.iters, r2.reason), ((rf.iters, rf.reason),
                                                             (r2.iters, r2.reason))
     assert rf.reason == 2
@@ -131,8 +128,6 @@ def test_auto_routing(device, monkeypatch):
     (J > 8192) on the scaling form too.  The fused result equals the explicit variant 1's."""
     from gnnea import _lib
     from gnnea.sinkhorn import solve
-    monkeypatch.delenv("GNNEA_SK_FUSED", raising=False)
-    monkeypatch.delenv("GNNEA_SK_RESIDENT", raising=False)
     rng = np.random.default_rng(21)
 
     def run(I, J, mode, dtype, variant=None):

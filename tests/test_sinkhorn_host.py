@@ -1,34 +1,44 @@
 """Host logic of the Sinkhorn driver (no device): an on-chip solve whose inter-workgroup wait
 timed out is solved again from the start with the on-chip path disabled (gnnea_sinkhorn.flags =
-GNNEA_SK_NO_ONCHIP), once; a timeout on that path propagates."""
+GNNEA_SK_NO_ONCHIP), once, and the result says so (onchip_timeout); a timeout on that path
+propagates.  The device side of the same path: tests/test_gpu_sinkhorn_timeout.py."""
+import types
+
 import pytest
 
 from gnnea import _lib, sinkhorn
 
 
-def _fake(calls, fail_flags):
+def _fake(calls, fail_flags, batch=False):
     def f(*args):
         flags = args[-1]
         calls.append(flags)
         if flags in fail_flags:
             raise sinkhorn.SinkhornTimeout("timed out")
-        return ("solved", flags)
+        r = types.SimpleNamespace(flags=flags)
+        return [r, types.SimpleNamespace(flags=flags)] if batch else r
     return f
 
 
 def test_solve_retries_on_the_sweep_path(monkeypatch):
     calls = []
     monkeypatch.setattr(sinkhorn, "_solve", _fake(calls, {0}))
-    assert sinkhorn.solve(0, None, None, None, 0.01, 1e-9, 10) == ("solved",
-                                                                   _lib.GNNEA_SK_NO_ONCHIP)
+    r = sinkhorn.solve(0, None, None, None, 0.01, 1e-9, 10)
+    assert r.flags == _lib.GNNEA_SK_NO_ONCHIP and r.onchip_timeout is True
     assert calls == [0, _lib.GNNEA_SK_NO_ONCHIP]
+    # the debug bit (zero wait budget) is dropped on the retry
+    calls.clear()
+    monkeypatch.setattr(sinkhorn, "_solve", _fake(calls, {_lib.GNNEA_SK_DEBUG_SPIN}))
+    r = sinkhorn.solve(0, None, None, None, 0.01, 1e-9, 10, flags=_lib.GNNEA_SK_DEBUG_SPIN)
+    assert calls == [_lib.GNNEA_SK_DEBUG_SPIN, _lib.GNNEA_SK_NO_ONCHIP]
 
 
 def test_solve_batch_retries_and_second_timeout_propagates(monkeypatch):
     calls = []
-    monkeypatch.setattr(sinkhorn, "_solve_batch", _fake(calls, {0}))
-    assert sinkhorn.solve_batch(0, None, None, None, 0.01, 1e-9, 10)[1] == \
-        _lib.GNNEA_SK_NO_ONCHIP
+    monkeypatch.setattr(sinkhorn, "_solve_batch", _fake(calls, {0}, batch=True))
+    out = sinkhorn.solve_batch(0, None, None, None, 0.01, 1e-9, 10)
+    assert [r.flags for r in out] == [_lib.GNNEA_SK_NO_ONCHIP] * 2
+    assert all(r.onchip_timeout for r in out)
     calls.clear()
     monkeypatch.setattr(sinkhorn, "_solve", _fake(calls, {0, _lib.GNNEA_SK_NO_ONCHIP}))
     with pytest.raises(sinkhorn.SinkhornTimeout):

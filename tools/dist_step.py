@@ -62,7 +62,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        import datetime
+        dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(
+            seconds=float(os.environ.get("GNNEA_PG_TIMEOUT_S", "300"))))
     res = measure(args.model, args.entities, rank, world, dev, args.steps, args.warmup,
                   torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     if rank == 0:
