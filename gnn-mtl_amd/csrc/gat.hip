@@ -224,55 +224,9 @@ __global__ __launch_bounds__(256) void k_gat_fwd(const int32_t* __restrict__ row
 //        dH_i += ds1_i (x) a1
 // ---------------------------------------------------------------------------------------- //
 
-template <int ACT, int H, int NCH, typename T>
-__global__ __launch_bounds__(256) void k_gat_bwd_prep(int n_rows, int D, int dh,
-                                                      const typename Vec4<T>::raw* __restrict__ dY,
-                                                      const typename Vec4<T>::raw* __restrict__ Y,
-                                                      int64_t ld4,
-                                                      const float* __restrict__ s1,
-                                                      const float* __restrict__ mrow,
-                                                      const float* __restrict__ den,
-                                                      typename Vec4<T>::raw* __restrict__ G,
-                                                      float4* __restrict__ rec) {
-  const int row = blockIdx.x * 4 + wave_id();
-  if (row >= n_rows) return;
-  const int lane = lane_id();
-  // the record's row statistics, read up front (read in the epilogue they were one more serial
-  // round trip per row after the wave sums)
-  const int64_t ro = (int64_t)row * H + (lane < H ? lane : 0);
-  const float rs1 = s1[ro], rmx = mrow[ro], rdv = den[ro];
-  float cp[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) cp[h] = 0.f;
-#pragma unroll
-  for (int q = 0; q < NCH; ++q) {
-    const int c4 = lane + 64 * q;
-    if (4 * c4 >= D) continue;
-    const float4 dy = Vec4<T>::get(dY[(int64_t)row * ld4 + c4]);
-    const float4 y = Vec4<T>::get(Y[(int64_t)row * ld4 + c4]);
-    const float ys[4] = {y.x, y.y, y.z, y.w};
-    float gs[4] = {dy.x, dy.y, dy.z, dy.w};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int c = 4 * c4 + t;
-      gs[t] = c < D ? gs[t] * act_grad_from_out<ACT>(ys[t]) : 0.f;
-      const int hh = c < D ? c / dh : H;
-      // P = h' (pre-activation); for relu / identity G * Y == G * h' element-wise
-#pragma unroll
-      for (int h = 0; h < H; ++h) cp[h] += (hh == h) ? gs[t] * ys[t] : 0.f;
-    }
-    G[(int64_t)row * ld4 + c4] = Vec4<T>::put(make_float4(gs[0], gs[1], gs[2], gs[3]));
-  }
-#pragma unroll
-  for (int h = 0; h < H; ++h) cp[h] = wave_sum(cp[h]);
-  if (lane < H)
-    rec[(int64_t)row * H + lane] =
-        make_float4(rs1, rmx, rdv > 0.f ? 1.f / rdv : 0.f, hsel<H>(cp, lane));
-}
-
-// The same prep over FOUR rows per wave (the default): every dY / Y load of the four rows issued
-// before any is used (k_gat_bwd_prep keeps one row's loads in flight per wave); per row the same
-// element arithmetic and the same wave-sum order, so G and rec are bit-identical to it.
+// prep over FOUR rows per wave: every dY / Y load of the four rows issued before any is used (a
+// row per wave kept one row's loads in flight and measured slower, round 4; removed); per row the
+// element arithmetic and the wave sums in a fixed order.
 template <int ACT, int H, int NCH, typename T>
 __global__ __launch_bounds__(256) void k_gat_bwd_prep4(int n_rows, int D, int dh,
                                                        const typename Vec4<T>::raw* __restrict__ dY,
@@ -498,55 +452,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(
     if (hl.ok[t]) out[hl.c[t]] = from_f32<T>(acc[t] + d2me * a2l[t]);
 }
 
-template <int H, int NCH, typename T>
-__global__ __launch_bounds__(256) void k_gat_bwd_dst(const int32_t* __restrict__ rowptr,
-                                                     const int64_t* __restrict__ tpos, int n_rows,
-                                                     int D, int dh, const float* __restrict__ dzT,
-                                                     const float* __restrict__ a,
-                                                     typename Vec4<T>::raw* __restrict__ dH,
-                                                     int64_t lddh4,
-                                                     float* __restrict__ ds1) {
-  const int row = blockIdx.x * 4 + wave_id();
-  if (row >= n_rows) return;
-  const int lane = lane_id();
-  const int beg = rowptr[row], end = rowptr[row + 1];
-  float p[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) p[h] = 0.f;
-  for (int e = beg + lane; e < end; e += 64) {
-    const int64_t t = tpos[e];
-#pragma unroll
-    for (int h = 0; h < H; ++h) p[h] += dzT[t * H + h];
-  }
-#pragma unroll
-  for (int h = 0; h < H; ++h) p[h] = wave_sum(p[h]);
-#pragma unroll
-  for (int q = 0; q < NCH; ++q) {
-    const int c4 = lane + 64 * q;
-    if (4 * c4 >= D) continue;
-    float4 v = Vec4<T>::get(dH[(int64_t)row * lddh4 + c4]);
-    float o[4] = {v.x, v.y, v.z, v.w};
-    // the attention-vector terms read unconditionally (a clamped column) and together: read
-    // inside the per-element branch they were four serial L2 round trips per group
-    float av[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int c = min(4 * c4 + t, D - 1), h = c / dh;
-      av[t] = a[h * 2 * dh + (c - h * dh)];
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int c = 4 * c4 + t;
-      if (c < D) o[t] += hsel<H>(p, c / dh) * av[t];
-    }
-    dH[(int64_t)row * lddh4 + c4] = Vec4<T>::put(make_float4(o[0], o[1], o[2], o[3]));
-  }
-  if (lane < H) ds1[(int64_t)row * H + lane] = hsel<H>(p, lane);
-}
-
-// The same pass with FOUR destination rows per wave (the default): k_gat_bwd_dst is a chain of
-// dependent loads per row (rowptr -> tpos -> dzT -> the dH row's read-modify-write) with one row
-// in flight per wave.  Here lane group g (16 lanes) walks row r0 + g's edges (ds1 partials summed
+// dst with FOUR destination rows per wave: per row a chain of dependent loads (rowptr -> tpos ->
+// dzT -> the dH row's read-modify-write), so one row per wave kept one chain in flight (measured
+// slower, round 4; removed).  Here lane group g (16 lanes) walks row r0 + g's edges (ds1 partials summed
 // over the group in fixed order: lane-strided edges, then xor 1, 2, 4, 8), and the wave then
 // updates the four dH rows with all of their loads issued before any is used.
 template <int H, int NCH, typename T>
@@ -1003,14 +911,6 @@ __global__ __launch_bounds__(256) GNNEA_HG_ATTR_SRC void k_gat_bwd_src_hg(
     if (hl.ok[t]) out[hl.c[t]] = from_f32<T>(acc[t] + d2me * a2l[t]);
 }
 
-// the head-grouped passes: on unless GNNEA_GAT_HG=0 (A/B timing against k_gat_fwd / _bwd_src)
-static bool gat_hg_on() {
-  static const bool on = [] {
-    const char* e = getenv("GNNEA_GAT_HG");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 
 // every lane's window ends inside the row's ld (elements, T-sized) for this head layout
 template <typename T, int EPL>
@@ -1086,17 +986,8 @@ static int hg_epl(int heads, int dh) {
     if (e <= o) return o;
   return -1;
 }
-static int hg_group() {  // edges per pipelined group (tuning override GNNEA_GAT_HG_F = 2 / 4 / 8)
-  static const int f = [] {
-    const char* e = getenv("GNNEA_GAT_HG_F");
-    const int v = e ? atoi(e) : 4;
-    return v == 2 || v == 8 ? v : 4;
-  }();
-  return f;
-}
 template <typename T>
 static bool hg_applies(int heads, int dh, int64_t ld, const float* s2, const float* emask) {
-  if (!gat_hg_on()) return false;
   const int epl = hg_epl(heads, dh);
   bool fits = false;
   switch (epl) {
@@ -1161,7 +1052,6 @@ static int gat_fwd_t(const int32_t* rowptr, const int32_t* col, int32_t n_rows, 
 #define CALL(HH, EE)                                                                          \
   case HH * 32 + EE:                                                                          \
     if (edge_mask) GNNEA_HG_L(HH, EE, true, 4);                                               \
-    else if (HH == 4 && EE == 5 && hg_group() == 8) GNNEA_HG_L(HH, EE, false, 8);             \
     else GNNEA_HG_L(HH, EE, false, 4);                                                        \
     break;
     GNNEA_GAT_HG_DISPATCH(CALL);
@@ -1202,20 +1092,10 @@ static int gat_bwd_prep_t(int32_t n_rows, int heads, int d_head, const T* dY, co
   if (!ok_ld(ld, D) || !alv<T>(dY) || !alv<T>(Y) || !alv<T>(G) || !alv<float>(rec))
     return GNNEA_EALIGN;
   if (act != GNNEA_ACT_IDENTITY && act != GNNEA_ACT_RELU) return GNNEA_EINVAL;
-  static const bool four = [] {  // A/B comparison only (GNNEA_GAT_PREP4=0: a row per wave)
-    const char* e = getenv("GNNEA_GAT_PREP4");
-    return !(e && e[0] == '0');
-  }();
-  const int nb = four ? div_up(n_rows, 16) : div_up(n_rows, 4);
+  const int nb = div_up(n_rows, 16);
 #define CALL_A(A, HH, NN)                                                                      \
-  if (four)                                                                                    \
-    hipLaunchKernelGGL((k_gat_bwd_prep4<A, HH, NN, T>), dim3(nb), dim3(256), 0, s, n_rows, D, \
-                       d_head, (const R*)dY, (const R*)Y, ld / 4, s1, m, den, (R*)G,          \
-                       (float4*)rec);                                                          \
-  else                                                                                         \
-    hipLaunchKernelGGL((k_gat_bwd_prep<A, HH, NN, T>), dim3(nb), dim3(256), 0, s, n_rows, D,  \
-                       d_head, (const R*)dY, (const R*)Y, ld / 4, s1, m, den, (R*)G,          \
-                       (float4*)rec)
+  hipLaunchKernelGGL((k_gat_bwd_prep4<A, HH, NN, T>), dim3(nb), dim3(256), 0, s, n_rows, D,   \
+                     d_head, (const R*)dY, (const R*)Y, ld / 4, s1, m, den, (R*)G, (float4*)rec)
 #define CALL(HH, NN)                                                        \
   case HH * 8 + NN:                                                         \
     if (act == GNNEA_ACT_RELU) CALL_A(GNNEA_ACT_RELU, HH, NN);              \
@@ -1251,7 +1131,6 @@ static int gat_bwd_src_t(const int32_t* rowptrT, const int32_t* colT, const int6
 #define CALL(HH, EE)                                                                          \
   case HH * 32 + EE:                                                                          \
     if (edge_mask) GNNEA_HG_L(HH, EE, true, 4);                                               \
-    else if (HH == 4 && EE == 5 && hg_group() == 8) GNNEA_HG_L(HH, EE, false, 8);             \
     else GNNEA_HG_L(HH, EE, false, 4);                                                        \
     break;
     GNNEA_GAT_HG_DISPATCH(CALL);
@@ -1291,19 +1170,11 @@ static int gat_bwd_dst_t(const int32_t* rowptr, const int64_t* tpos, int32_t n_r
   const int D = heads * d_head, D4 = (D + 3) / 4;
   if (!rowptr || !tpos || !dzT || !a || !dH || !ds1) return GNNEA_EINVAL;
   if (!ok_ld(lddh, D) || !alv<T>(dH)) return GNNEA_EALIGN;
-  static const bool four = [] {  // A/B comparison only (GNNEA_GAT_DST4=0: a row per wave)
-    const char* e = getenv("GNNEA_GAT_DST4");
-    return !(e && e[0] == '0');
-  }();
-  const int nb = four ? div_up(n_rows, 16) : div_up(n_rows, 4);
+  const int nb = div_up(n_rows, 16);
 #define CALL(HH, NN)                                                                          \
   case HH * 8 + NN:                                                                           \
-    if (four)                                                                                 \
-      hipLaunchKernelGGL((k_gat_bwd_dst4<HH, NN, T>), dim3(nb), dim3(256), 0, s, rowptr,      \
-                         tpos, n_rows, D, d_head, dzT, a, (R*)dH, lddh / 4, ds1);             \
-    else                                                                                      \
-      hipLaunchKernelGGL((k_gat_bwd_dst<HH, NN, T>), dim3(nb), dim3(256), 0, s, rowptr, tpos, \
-                         n_rows, D, d_head, dzT, a, (R*)dH, lddh / 4, ds1);                   \
+    hipLaunchKernelGGL((k_gat_bwd_dst4<HH, NN, T>), dim3(nb), dim3(256), 0, s, rowptr, tpos,  \
+                       n_rows, D, d_head, dzT, a, (R*)dH, lddh / 4, ds1);                     \
     break;
   GNNEA_GAT_DISPATCH(CALL);
 #undef CALL

@@ -659,26 +659,8 @@ extern "C" int gnnea_slice_pack64_bf16(const void* X, int64_t ldx, int64_t n, in
   switch (heads) { CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) }
 
 // lanes per source row of the weight and edge passes: 32 (cfg-4, mean in-degree 21: edge pass
-// 1.70 / 1.45 / 2.02 ms and weights 0.68 / 0.60 / 0.84 ms at 16 / 32 / 8 lanes; GNNEA_GAT_LPR
-// = 8 / 16 / 64 overrides, tuning only)
-static int gat_lpr() {
-  static const int v = [] {
-    const char* e = getenv("GNNEA_GAT_LPR");
-    const int x = e ? atoi(e) : 32;
-    return x == 8 || x == 16 || x == 64 ? x : 32;
-  }();
-  return v;
-}
-
-// lanes per row of the destination pass: 32 (two rows per wave; 2.37 vs 3.13 ms per cfg-4
-// layer at 64) by default, 64 with GNNEA_GAT_DST_LANES=64 (tuning only)
-static int gat_dst_lanes() {
-  static const int v = [] {
-    const char* e = getenv("GNNEA_GAT_DST_LANES");
-    return e && atoi(e) == 64 ? 64 : 32;
-  }();
-  return v;
-}
+// 1.70 / 1.45 / 2.02 ms and weights 0.68 / 0.60 / 0.84 ms at 16 / 32 / 8 lanes); lanes per row
+// of the destination pass: 32 (two rows per wave; 2.37 vs 3.13 ms per cfg-4 layer at 64)
 
 static bool gat_sl_shape(int heads, int d_head, int64_t sstride) {
   const int D = heads * d_head;
@@ -757,10 +739,7 @@ int gat_bwd_src_sliced(const int32_t* rowptrT, const int32_t* colT, const int64_
                      rowptrT, colT, permT, n_rows, s2, alpha, emask, (const float4*)rec, wT)
 #define GNNEA_W(HH)                                              \
   case HH:                                                       \
-    if (gat_lpr() == 8) GNNEA_W1(HH, 8);                         \
-    else if (gat_lpr() == 16) GNNEA_W1(HH, 16);                  \
-    else if (gat_lpr() == 64) GNNEA_W1(HH, 64);                  \
-    else GNNEA_W1(HH, 32);                                       \
+    GNNEA_W1(HH, 32);                                            \
     break;
   GNNEA_HEADS_SWITCH(GNNEA_W)
 #undef GNNEA_W
@@ -798,10 +777,7 @@ int gat_bwd_edge_sliced(const int32_t* rowptrT, const int32_t* colT, const int64
                      (const float4*)rec, (const float2*)pd, nnzT, a, dH, lddh, dzT, ds2)
 #define GNNEA_E(HH)                                              \
   case HH:                                                       \
-    if (gat_lpr() == 8) GNNEA_E1(HH, 8);                         \
-    else if (gat_lpr() == 16) GNNEA_E1(HH, 16);                  \
-    else if (gat_lpr() == 64) GNNEA_E1(HH, 64);                  \
-    else GNNEA_E1(HH, 32);                                       \
+    GNNEA_E1(HH, 32);                                            \
     break;
   GNNEA_HEADS_SWITCH(GNNEA_E)
 #undef GNNEA_E
@@ -823,12 +799,8 @@ int gat_bwd_dst_sliced(const int32_t* rowptr, const int64_t* tpos, int32_t n_row
   const int nch = (D / 4 + 63) / 64;
   typedef typename Vec4<T>::raw R;
 #define GNNEA_D(HH, NC)                                                                            \
-  if (gat_dst_lanes() == 64)                                                                       \
-    hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC, 64, T>), dim3(div_up(n_rows, 4)), dim3(256), 0,    \
-                       st, rowptr, tpos, n_rows, D, d_head, dzT, a, ds2, (R*)dH, lddh / 4, ds1);   \
-  else                                                                                             \
-    hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC, 32, T>), dim3(div_up(n_rows, 8)), dim3(256), 0,    \
-                       st, rowptr, tpos, n_rows, D, d_head, dzT, a, ds2, (R*)dH, lddh / 4, ds1)
+  hipLaunchKernelGGL((k_gat_bwd_dst_s<HH, NC, 32, T>), dim3(div_up(n_rows, 8)), dim3(256), 0, st,  \
+                     rowptr, tpos, n_rows, D, d_head, dzT, a, ds2, (R*)dH, lddh / 4, ds1)
 #define GNNEA_D_H(HH)                        \
   case HH:                                   \
     switch (nch) {                           \

@@ -617,10 +617,7 @@ __device__ __forceinline__ void store_tile_v4(const f32x16& acc, uint32_t region
 // as ONE stream of k-steps, so the DMA ring runs across tile boundaries (the next tile's first
 // stages are in flight while the last ones of the current tile are multiplied) and a tile's
 // epilogue (16-B stores through LDS) is written while the next tile's stages land.
-template <int WT, int NW, int MODE = 0>  // MODE (timing experiments only): 1 = no MFMA,
-                            // 2 = no DMA, 3 = no DMA and no A split, 4 = no DMA and no epilogue
-                            // stores, 8 = every epilogue store to the 1-KB dummy (no C traffic), 9 = DMA on, no
-                            // epilogue stores
+template <int WT, int NW>
 __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const float* __restrict__ A,
                                                   int64_t lda, const bf16_t* __restrict__ Bp,
                                                   int64_t ldp, int64_t pstride,
@@ -683,12 +680,11 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
     for (int qq = 0; qq < 2; ++qq) {
       // a quad past K reads a valid address (k = 0 of the row) and is zeroed at use
       const float* ap = (k0 + 4 * a_slot[qq] < K) ? a_src[qq] + k0 : a_src[qq] - 4 * a_slot[qq];
-      // (MODE 5 timing experiment: the A stream re-reads the tile's first k-block)
-      glds16(MODE == 5 ? a_src[qq] : ap, st + (w + NW * qq) * 1024);
+      glds16(ap, st + (w + NW * qq) * 1024);
     }
 #pragma unroll
-    for (int qq = 0; qq < G::B_CHUNKS_PAD / NW; ++qq)  // (MODE 6: B stream re-reads k-block 0)
-      glds16(b_src[qq] + (MODE == 6 ? 0 : (int64_t)is * ldp), st + G::A_BYTES + (w + NW * qq) * 1024);
+    for (int qq = 0; qq < G::B_CHUNKS_PAD / NW; ++qq)
+      glds16(b_src[qq] + (int64_t)is * ldp, st + G::A_BYTES + (w + NW * qq) * 1024);
     if (++is == nsteps) { is = 0; ++iq; }
   };
 
@@ -709,24 +705,15 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
   auto epilogue = [&](int q, int buf) {
     int m0, n0;
     tile_of(q, m0, n0);
-    if (MODE == 4 || MODE == 9) {  // timing experiment: one store per wave keeps the accumulators live
-      float t = 0.f;
-#pragma unroll
-      for (int qq = 0; qq < WT; ++qq)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += acc[qq][r];
-      if (t == 12345.f) C[tid] = t;
-      return;
-    }
     const uint32_t region = smem_lds + buf * G::STAGE + w * 32 * G::EPI_LD * 4;
 #pragma unroll
     for (int t = 0; t < WT; ++t)
-      store_tile_v4<G::EPI_LD>(acc[t], region, MODE == 8 ? 0 : M, N, m0 + w * 32, n0 + 32 * t, kh, li, lane, beta, C, ldc,
+      store_tile_v4<G::EPI_LD>(acc[t], region, M, N, m0 + w * 32, n0 + 32 * t, kh, li, lane, beta, C, ldc,
                     cs, vec4 != 0, dummy, C2, cs2);
   };
   // vmcnt allowance for the first step after an epilogue: its 16-B stores (exactly 4 per tile
   // of 32 columns when vec4 and no beta loads) were issued after the DMA that step waits for
-  const bool count_stores = vec4 != 0 && beta == 0.f && MODE != 4 && MODE != 9 &&
+  const bool count_stores = vec4 != 0 && beta == 0.f &&
                             G::LOADS * (NS - 2) + (C2 ? 8 : 4) * WT <= 63;
 
 #pragma unroll
@@ -766,7 +753,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
     }
-    if ((MODE < 2 || MODE >= 8) && g + NS - 1 < total) issue_next(prev);
+    if (g + NS - 1 < total) issue_next(prev);
     const uint32_t st = smem_lds + cur * G::STAGE;
     const f32x4_t x0 = ds_read128f(st + a_off0);
     const f32x4_t x1 = ds_read128f(st + a_off1);
@@ -792,21 +779,15 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
       for (int j = 0; j < 8; ++j)
         if (j >= kval) xa[j] = (hb && j == kval) ? 1.f : 0.f;
     }
-    bf16x8_t ah, am, al;
-    if (MODE == 3) {
-      ah = __builtin_bit_cast(bf16x8_t, x0);
-      am = __builtin_bit_cast(bf16x8_t, x1);
-      al = ah;
-    } else {  // pairwise (common.h x3_split_pair: split3's values, half the instructions)
-      uint4 h4, m4, l4;
-      x3_split_pair(xa[0], xa[1], h4.x, m4.x, l4.x);
-      x3_split_pair(xa[2], xa[3], h4.y, m4.y, l4.y);
-      x3_split_pair(xa[4], xa[5], h4.z, m4.z, l4.z);
-      x3_split_pair(xa[6], xa[7], h4.w, m4.w, l4.w);
-      ah = __builtin_bit_cast(bf16x8_t, h4);
-      am = __builtin_bit_cast(bf16x8_t, m4);
-      al = __builtin_bit_cast(bf16x8_t, l4);
-    }
+    // pairwise (common.h x3_split_pair: split3's values, half the instructions)
+    uint4 h4, m4, l4;
+    x3_split_pair(xa[0], xa[1], h4.x, m4.x, l4.x);
+    x3_split_pair(xa[2], xa[3], h4.y, m4.y, l4.y);
+    x3_split_pair(xa[4], xa[5], h4.z, m4.z, l4.z);
+    x3_split_pair(xa[6], xa[7], h4.w, m4.w, l4.w);
+    const bf16x8_t ah = __builtin_bit_cast(bf16x8_t, h4);
+    const bf16x8_t am = __builtin_bit_cast(bf16x8_t, m4);
+    const bf16x8_t al = __builtin_bit_cast(bf16x8_t, l4);
     // the wave's column tiles in NH halves of TH (a 320-wide wave tile keeps 160 accumulator
     // registers; its B fragments are read half by half, the second half's reads in flight
     // under the first half's MFMAs)
@@ -830,11 +811,6 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
         bl[t] = __builtin_bit_cast(bf16x8_t, braw[3 * t + 2]);
       }
       f32x16* ac = acc + hf * TH;
-      if (MODE == 1) {  // timing experiment: keep the data live, skip the matrix cores
-#pragma unroll
-        for (int t = 0; t < TH; ++t)
-          ac[t][0] += (float)(ah[0] + am[1] + al[2] + bh[t][0] + bm_[t][1] + bl[t][2]);
-      } else {
 #pragma unroll
       for (int t = 0; t < TH; ++t) ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t], ac[t], 0, 0, 0);
 #pragma unroll
@@ -847,7 +823,6 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_x3p(int M, int N, int K, const
       for (int t = 0; t < TH; ++t) ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bm_[t], ac[t], 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < TH; ++t) ac[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t], ac[t], 0, 0, 0);
-      }
     }
     cur = cur == NS - 1 ? 0 : cur + 1;
     if (++s == nsteps) { s = 0; ++q; }
@@ -1041,14 +1016,6 @@ static int gemm_x3_ta(int64_t M, int64_t N, int64_t K, const float* A, int64_t l
                       const float* B, int64_t ldb, const float* bias, float beta, float* C,
                       int64_t ldc, int64_t cs, void* ws, int64_t ws_bytes, hipStream_t s);
 
-// k_gemm_x3p on (default) or off (GNNEA_X3_PIPE=0: the register-staged k_gemm_x3, A/B comparison)
-static bool x3_pipe_on() {
-  static const bool pipe = [] {
-    const char* e = getenv("GNNEA_X3_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return pipe;
-}
 
 static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
                    int64_t lda, const float* B, int64_t ldb, const float* bias, float beta,
@@ -1075,7 +1042,7 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
     const int64_t pb = x3_planes_bytes(N, K);
     // the same condition as k_gemm_x3p's launch below (pipe on, float4 A, no split-K): any other
     // kernel leaves C2 unwritten, so it is packed after
-    const bool fused = x3_pipe_on() && lda_ok && ws && ws_bytes >= pb &&
+    const bool fused = lda_ok && ws && ws_bytes >= pb &&
                        pick_splits(M, N, K, ws_bytes - pb) == 1;
     if (!fused) {
       const int rc = gemm_x3(trans_a, trans_b, M, N, K, A, lda, B, ldb, bias, beta, C, ldc, cs,
@@ -1104,8 +1071,7 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
   bf16_t* planes = (bf16_t*)ws;
   const bool vec = lda % 4 == 0 && K % 4 == 0 && al16(A);
   const int splits = pick_splits(M, N, K, ws_bytes - pbytes);
-  const bool pipe = x3_pipe_on();
-  if (!(pipe && vec && splits == 1)) {
+  if (!(vec && splits == 1)) {
     const int64_t tot = N * ldp;
     const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
     // B op-form [N][K]: trans_b = 1 means B is stored [N][K] (no transpose needed)
@@ -1113,17 +1079,9 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
                        (int)N, (int)K, ldp, planes, pstride);
     GNNEA_LAUNCH_CHECK();
   }
-  if (pipe && vec && splits == 1) {  // k_gemm_x3p: LDS-DMA pipeline, two workgroups per CU
+  if (vec && splits == 1) {  // k_gemm_x3p: LDS-DMA pipeline, two workgroups per CU
     // 32*WT-column tiles, WT <= 5 (N = 300: two 160-column tiles)
     int wtp = (int)((N + 31) / 32 < 5 ? (N + 31) / 32 : 5);
-    if (const char* e = getenv("GNNEA_X3_WT")) {  // tuning override only
-      // taken only when its padded plane rows fit the 320-row rounding x3_planes_bytes reserves
-      // (N = 300 with WT 3 / 4 would pad to 384 rows and overrun the planes)
-      const int v = atoi(e);
-      if (((v >= 1 && v <= 5) || v == 10) &&
-          (N + 32 * v - 1) / (32 * v) * (32 * v) <= (N + 319) / 320 * 320)
-        wtp = v;
-    }
     const int tn = (int)((N + 32 * wtp - 1) / (32 * wtp));
     const int np = tn * 32 * wtp;  // <= the 320-row rounding x3_planes_bytes reserves
     const int kp = (int)((K + (bias ? 1 : 0) + kPlaneAlign - 1) / kPlaneAlign * kPlaneAlign);
@@ -1136,12 +1094,7 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
       GNNEA_LAUNCH_CHECK();
     }
     // 8 waves (256-row tiles, one workgroup per CU) for tall operands, else 4 (128 rows, two)
-    int nw = M >= 65536 ? 8 : 4;
-    if (const char* e = getenv("GNNEA_X3P_NW")) {  // tuning override only
-      const int v = atoi(e);
-      if (v == 4 || v == 8) nw = v;
-    }
-    if (wtp == 10) nw = 8;  // the 320-wide wave tile: 8 waves, one workgroup per CU
+    const int nw = M >= 65536 ? 8 : 4;
     const int64_t tm = (M + 32 * nw - 1) / (32 * nw);
     if (tm * tn >= (1ll << 31)) return GNNEA_EINVAL;
     const int ntiles = (int)(tm * tn);
@@ -1155,40 +1108,20 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
     const int per_cu = nw == 8 ? 1 : 2;  // persistent: as many workgroups as fit at once
     const dim3 grid((unsigned)(ntiles < per_cu * ncu ? ntiles : per_cu * ncu));
     const int vec4 = N % 4 == 0 && ldc % 4 == 0 && cs % 4 == 0 && al16(C);
-    static const int mode = [] {  // timing experiments only (GNNEA_X3P_MODE=1..4, WT = 5)
-      const char* e = getenv("GNNEA_X3P_MODE");
-      return e ? atoi(e) : 0;
-    }();
-#define GNNEA_X3P_L(W, NWV, MD)                                                                  \
-  hipLaunchKernelGGL((k_gemm_x3p<W, NWV, MD>), grid, dim3(64 * NWV), 0, s, (int)M, (int)N,       \
-                     (int)K, A, lda, planes, (int64_t)np * GBK, (int64_t)np * kp, bias, beta, C, \
-                     ldc, cs, tn, ntiles, vec4, dummy, C2, cs2)
+#define GNNEA_X3P_L(W, NWV)                                                                      \
+  hipLaunchKernelGGL((k_gemm_x3p<W, NWV>), grid, dim3(64 * NWV), 0, s, (int)M, (int)N, (int)K, A, \
+                     lda, planes, (int64_t)np * GBK, (int64_t)np * kp, bias, beta, C, ldc, cs, tn, \
+                     ntiles, vec4, dummy, C2, cs2)
 #define GNNEA_X3P(W)                                                                             \
   case W:                                                                                        \
-    if (nw == 8) {                                                                               \
-      if (W == 5 && mode == 1) GNNEA_X3P_L(W, 8, 1);                                             \
-      else if (W == 5 && mode == 2) GNNEA_X3P_L(W, 8, 2);                                        \
-      else if (W == 5 && mode == 4) GNNEA_X3P_L(W, 8, 4);                                        \
-      else if (W == 5 && mode == 8) GNNEA_X3P_L(W, 8, 8);                                        \
-      else if (W == 5 && mode == 9) GNNEA_X3P_L(W, 8, 9);                                        \
-      else GNNEA_X3P_L(W, 8, 0);                                                                 \
-    } else {                                                                                     \
-      if (W == 5 && mode == 1) GNNEA_X3P_L(W, 4, 1);                                             \
-      else if (W == 5 && mode == 5) GNNEA_X3P_L(W, 4, 5);                                        \
-      else if (W == 5 && mode == 6) GNNEA_X3P_L(W, 4, 6);                                        \
-      else if (W == 5 && mode == 2) GNNEA_X3P_L(W, 4, 2);                                        \
-      else if (W == 5 && mode == 4) GNNEA_X3P_L(W, 4, 4);                                        \
-      else GNNEA_X3P_L(W, 4, 0);                                                                 \
-    }                                                                                            \
+    if (nw == 8) GNNEA_X3P_L(W, 8);                                                              \
+    else GNNEA_X3P_L(W, 4);                                                                      \
     break;
     switch (wtp) {
       GNNEA_X3P(1)
       GNNEA_X3P(2)
       GNNEA_X3P(3)
       GNNEA_X3P(4)
-      case 10:
-        GNNEA_X3P_L(10, 8, 0);
-        break;
       default:
       GNNEA_X3P(5)
     }
@@ -1199,11 +1132,7 @@ static int gemm_x3(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, co
   }
   // wider than one 320-column tile: 128-column tiles (WT = 2, the finer work split) measured
   // faster than 2 x 320 (2M x 600 x 300: 5.76 vs 6.05 ms; 30k rows: 0.109 vs 0.118 ms)
-  int wt = N > 320 ? 2 : pick_wt(N);
-  if (const char* e = getenv("GNNEA_X3_WT")) {  // tuning override only
-    const int v = atoi(e);
-    if (v >= 1 && v <= 5) wt = v;
-  }
+  const int wt = N > 320 ? 2 : pick_wt(N);
   const int64_t bn = 64 * wt;
   const int tiles_n = (int)((N + bn - 1) / bn);
   const int tiles = (int)(((M + XBM - 1) / XBM) * tiles_n);
@@ -1247,11 +1176,7 @@ static int64_t x3_ta_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
   const int64_t bn = 64 * pick_wt(N);
   const int64_t tiles = ((M + XBM - 1) / XBM) * ((N + bn - 1) / bn);
   if (tiles >= 256 || K < 16 * GBK) return 1;
-  static const int64_t target = [] {  // workgroups to aim for (GNNEA_X3TA_WGS: tuning only)
-    const char* e = getenv("GNNEA_X3TA_WGS");
-    const int v = e ? atoi(e) : 512;
-    return (int64_t)(v >= 64 && v <= 4096 ? v : 512);
-  }();
+  constexpr int64_t target = 512;  // workgroups to aim for
   int64_t s = target / tiles;
   const int64_t by_k = K / (8 * GBK);
   if (s > by_k) s = by_k;

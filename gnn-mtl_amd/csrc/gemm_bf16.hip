@@ -449,8 +449,7 @@ __device__ __forceinline__ void bfp_wait(int later, bool stores_after) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int WT, int AW, int NW_, typename TC, int MODE = 0>  // MODE (timing experiments
-                  // only): 1 = no MFMA, 2 = no DMA, 4 = no epilogue stores (accumulators live)
+template <int WT, int AW, int NW_, typename TC>
 __global__ __launch_bounds__(64 * NW_) void k_gemm_bf16p(int M, int N, int K,
                                                    const bf16_t* __restrict__ A, int64_t lda,
                                                    const bf16_t* __restrict__ Bp, int NP, int hb,
@@ -540,15 +539,6 @@ __global__ __launch_bounds__(64 * NW_) void k_gemm_bf16p(int M, int N, int K,
   auto epilogue = [&](int q, int buf) {
     int m0, n0;
     tile_of(q, m0, n0);
-    if (MODE == 4) {  // timing experiment: one store per wave keeps the accumulators live
-      float t = 0.f;
-#pragma unroll
-      for (int qq = 0; qq < WT; ++qq)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) t += acc[qq][r];
-      if (t == 12345.f) C[tid] = from_f32<TC>(t);
-      return;
-    }
     const uint32_t region = smem_lds + buf * G::STAGE + w * 32 * G::EPI_LD * 4;
     if constexpr (std::is_same<TC, bf16_t>::value) {
       if (vec != 0 && beta == 0.f) {  // tile pairs as 128-B row pieces
@@ -571,11 +561,11 @@ __global__ __launch_bounds__(64 * NW_) void k_gemm_bf16p(int M, int N, int K,
   // vec and no beta loads) were issued after the DMA those steps wait for
   // epilogue stores per lane: bf16 tile pairs 4 + a single tile 2 (= 2 per tile), fp32 4 per tile
   constexpr int ST = BfpEpi<TC>::STORES * WT;
-  const bool count_stores = vec != 0 && beta == 0.f && MODE != 4 && G::LOADS_HI * (NS - 2) + ST <= 63;
+  const bool count_stores = vec != 0 && beta == 0.f && G::LOADS_HI * (NS - 2) + ST <= 63;
 
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i)
-    if (MODE != 2 && i < total) issue_next(i);
+    if (i < total) issue_next(i);
   int cur = 0, s = 0, q = 0;
   for (int g = 0; g < total; ++g) {
     const bool epi = s == 0 && q > 0;
@@ -597,7 +587,7 @@ __global__ __launch_bounds__(64 * NW_) void k_gemm_bf16p(int M, int N, int K,
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
     }
-    if (MODE != 2 && g + NS - 1 < total) issue_next(prev);
+    if (g + NS - 1 < total) issue_next(prev);
     const uint32_t st = smem_lds + cur * G::STAGE;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -622,15 +612,10 @@ __global__ __launch_bounds__(64 * NW_) void k_gemm_bf16p(int M, int N, int K,
         araw = u32x4{d[0], d[1], d[2], d[3]};
       }
       const bf16x8 a = __builtin_bit_cast(bf16x8, araw);
-      if (MODE == 1) {  // timing experiment: keep the data live, skip the matrix cores
 #pragma unroll
-        for (int t = 0; t < WT; ++t) acc[t][0] += (float)(a[0] + __builtin_bit_cast(bf16x8, braw[t])[1]);
-      } else {
-#pragma unroll
-        for (int t = 0; t < WT; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, __builtin_bit_cast(bf16x8, braw[t]),
-                                                           acc[t], 0, 0, 0);
-      }
+      for (int t = 0; t < WT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, __builtin_bit_cast(bf16x8, braw[t]),
+                                                         acc[t], 0, 0, 0);
     }
     cur = cur == NS - 1 ? 0 : cur + 1;
     if (++s == nsteps) { s = 0; ++q; }
@@ -713,14 +698,6 @@ static int bf16_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
   return (int)(s < 1 ? 1 : s);
 }
 
-static bool bf16_lds_epilogue() {
-  static const bool on = [] {  // A/B comparison only (GNNEA_BF16_EPI=0: per-element stores)
-    const char* e = getenv("GNNEA_BF16_EPI");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 template <int TA, int TB, int WT, typename TC>
 static void launch_bf16_wt(dim3 grid, hipStream_t s, bool vec, int M, int N, int K,
                            const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
@@ -728,7 +705,7 @@ static void launch_bf16_wt(dim3 grid, hipStream_t s, bool vec, int M, int N, int
                            int kps, float* slab, int tiles_n) {
   if constexpr (std::is_same<TC, bf16_t>::value) {
     if (vec && !slab && beta == 0.f && (((uintptr_t)C) & 7) == 0 && ldc % 4 == 0 &&
-        cs % 4 == 0 && bf16_lds_epilogue()) {
+        cs % 4 == 0) {  // the LDS-staged epilogue: 128-B row pieces
       hipLaunchKernelGGL((k_gemm_bf16<TA, TB, WT, true, TC, 1, true>), grid, dim3(256), 0, s, M,
                          N, K, A, lda, B, ldb, bias, beta, C, ldc, cs, kps, slab, tiles_n);
       return;
@@ -767,16 +744,9 @@ static void launch_bf16_t(int wt, dim3 grid, hipStream_t s, bool vec, int M, int
 
 // k_gemm_bf16p applies to the tall projection form: A [M][K] K-contiguous (rows 4-B aligned, K
 // even), M >= 64K rows, the whole output 2 column tiles of 160 at most per 320 (N > 128)
-static bool bf16p_on() {
-  static const bool on = [] {  // A/B comparison only (GNNEA_BF16_PIPE=0: k_gemm_bf16)
-    const char* e = getenv("GNNEA_BF16_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 static bool bf16p_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda,
                           const void* A) {
-  return bf16p_on() && !trans_a && M >= 65536 && N > 128 && N <= 4096 && K > 0 && K % 2 == 0 &&
+  return !trans_a && M >= 65536 && N > 128 && N <= 4096 && K > 0 && K % 2 == 0 &&
          lda % 2 == 0 && (((uintptr_t)A) & 3) == 0;
 }
 // column tile of k_gemm_bf16p: 32 * 5 = 160 columns (a 320-wide tile that reads A once at
@@ -792,30 +762,13 @@ template <int WT, int AW, int NW, typename TC>
 static void launch_bf16p(hipStream_t s, int grid, int M, int N, int K, const bf16_t* A,
                          int64_t lda, const bf16_t* P, int NP, int hb, float beta, TC* C,
                          int64_t ldc, int64_t cs, int tiles_n, int ntiles, int vec, TC* dummy) {
-  static const int mode = [] {  // timing experiments only (GNNEA_BF16P_MODE = 1, 2, 4)
-    const char* e = getenv("GNNEA_BF16P_MODE");
-    return e ? atoi(e) : 0;
-  }();
-#define GNNEA_BFP(MD)                                                                           \
-  hipLaunchKernelGGL((k_gemm_bf16p<WT, AW, NW, TC, MD>), dim3(grid), dim3(64 * NW), 0, s, M, N, \
-                     K, A, lda, P, NP, hb, beta, C, ldc, cs, tiles_n, ntiles, vec, dummy)
-  constexpr bool modes = std::is_same<TC, bf16_t>::value && AW == 16;
-  if (modes && mode == 1) GNNEA_BFP(modes ? 1 : 0);
-  else if (modes && mode == 2) GNNEA_BFP(modes ? 2 : 0);
-  else if (modes && mode == 4) GNNEA_BFP(modes ? 4 : 0);
-  else GNNEA_BFP(0);
-#undef GNNEA_BFP
+  hipLaunchKernelGGL((k_gemm_bf16p<WT, AW, NW, TC>), dim3(grid), dim3(64 * NW), 0, s, M, N, K,
+                     A, lda, P, NP, hb, beta, C, ldc, cs, tiles_n, ntiles, vec, dummy);
 }
 
 // waves per workgroup: 8 (256-row tiles, one workgroup per CU) or 4 (128-row tiles, two per CU:
-// one's barriers and epilogue under the other's MFMAs); GNNEA_BF16P_NW overrides (tuning)
-static int bf16p_nw() {
-  static const int v = [] {
-    const char* e = getenv("GNNEA_BF16P_NW");
-    return e && atoi(e) == 4 ? 4 : 8;
-  }();
-  return v;
-}
+// one's barriers and epilogue under the other's MFMAs); 8 measured faster at the cfg-5 shapes
+static int bf16p_nw() { return 8; }
 
 template <typename TC>
 static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

@@ -493,14 +493,6 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
 
 // ---- host side ----
 
-static bool ta_x3d_on() {  // A/B comparison only (GNNEA_TA_X3D=0: k_gemm_ta<float>)
-  static const bool on = [] {
-    const char* e = getenv("GNNEA_TA_X3D");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 static int ta_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
   const int tiles_n = (int)((N + TA_NP - 1) / TA_NP);
   int64_t s = 256 / tiles_n;                 // one workgroup per CU
@@ -512,12 +504,8 @@ static int ta_splits(int64_t M, int64_t N, int64_t K, int64_t ws_bytes) {
 
 bool gemm_ta_applies(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* A,
                      const void* B, int es) {
-  static const bool on = [] {  // A/B comparison only (GNNEA_GEMM_TA=0: the tiled TA kernels)
-    const char* e = getenv("GNNEA_GEMM_TA");
-    return !(e && e[0] == '0');
-  }();
   // 4-element rows and row strides (8-B bf16 / 16-B fp32 granules), >= one chunk per row
-  return on && M >= 8 && N >= 8 && M <= TA_MP && N <= 2 * TA_NP && K >= 4 * TA_BK &&
+  return M >= 8 && N >= 8 && M <= TA_MP && N <= 2 * TA_NP && K >= 4 * TA_BK &&
          K < (1ll << 31) && M % 4 == 0 && N % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 &&
          lda >= M && ldb >= N && (((uintptr_t)A) % (4 * es)) == 0 &&
          (((uintptr_t)B) % (4 * es)) == 0;
@@ -538,7 +526,7 @@ int gemm_ta_launch(int64_t M, int64_t N, int64_t K, const T* A, int64_t lda, con
   // every split must own rows (kps rounding can leave the last ones empty): trim the grid
   const int used = (int)((K + kps - 1) / kps);
   float* slab = (float*)ws;
-  if (std::is_same<T, float>::value && ta_x3d_on())
+  if constexpr (std::is_same<T, float>::value)  // fp32: split at the fragment read
     hipLaunchKernelGGL(k_gemm_ta_x3d, dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M, (int)N,
                        (int)K, (const float*)A, lda, (const float*)B, ldb, kps, tiles_n, slab);
   else

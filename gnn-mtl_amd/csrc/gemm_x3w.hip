@@ -1,26 +1,26 @@
-// fp32 projection GEMM through the three-way bf16 split with the WEIGHT RESIDENT in LDS
-// (k_gemm_x3w): C[M][N] = A[M][K] · op(B) (+ bias) for the EA layers' projections (x·Wᵀ + b,
-// dX = dY·W, x·[Wᵀ|K_g]: layers/layers.py:32,61, att_layers.py:33 and their autograd), K in
-// (256, 320], M tall.
+// fp32 projection GEMMs with the WEIGHT RESIDENT in LDS: C[M][N] = A[M][K] · op(B) (+ bias)
+// (+ beta C) (relu) for the EA layers' tall projections (x·Wᵀ + b, dX = dY·W, x·[Wᵀ|K_g] and the
+// HighWay input gradient [dh | dg]·[W ; K_gᵀ]: layers/layers.py:32,61, att_layers.py:33 and their
+// autograd), K in (288, 320] (and (576, 608] for the f16x2 form).
 //
-// k_gemm_x3p streams both operands through an LDS-DMA ring (2.45 ms at 2M x 300 x 300): the B
-// tile is re-read from L2 for every 256-row tile, each k-step costs a barrier and DMA issue slots
-// beside the MFMAs, and timing modes put the DMA feed at ~0.7 ms of it.  Here (as gemm_bf16.hip's
-// k_gemm_bf16w for bf16) an 80-column tile of the weight, split h / m / l, stays in LDS for the
-// whole launch (3 planes x 320 k x 80 n bf16 = 150 KB, one 8-wave workgroup per CU) and the
-// activations go straight from HBM into registers: no barrier and no LDS traffic for A.  The
-// product is computed transposed, Dᵀ = W_tile · Aᵀ on v_mfma_f32_16x16x32_bf16: the weight tile is
-// the MFMA's A operand (ds_read_b128 of 8 k per lane, conflict-free), 16 activation rows per wave
-// its B operand, split in registers; a lane's accumulators come out as 4 consecutive output
-// columns of one row (16-B stores straight from registers, the bias added from LDS).  The k
-// dimension is permuted alike for both operands: at step s the lanes of k-quarter kq hold
-// k = 32 s + 4 kq + {0..3} and 32 s + 16 + 4 kq + {0..3}, so a wave-instruction's 64 lanes read
-// 16 rows x 64 contiguous bytes (an operand lane order that reads 16 B from 64 different lines
-// per instruction measured no faster than k_gemm_x3p).  Each wave holds its next row tile's
-// activations (20 x 16 B) in flight while it multiplies the current one.  Workgroup b owns column tile (b / 8) % ntn and the row stream
-// (b / (8 ntn)) * 8 + b % 8: the column tiles of the same rows are on one XCD (b mod 8), so A
-// is read from HBM once and from L2 by the other tiles.  Same six products, same pairing as
-// gemm.hip's x3 (small ones first); the bias joins in the epilogue (one fp32 rounding).
+// k_gemm_x3p (gemm.hip) streams both operands through an LDS-DMA ring: the B tile is re-read from
+// L2 for every row tile and each k-step costs a barrier and DMA issue slots.  Here (as
+// gemm_bf16.hip's k_gemm_bf16w for bf16) a column tile of the weight, split into planes, stays in
+// LDS for the whole launch (one 8-wave workgroup per CU) and the activations go straight from
+// HBM into registers: no barrier and no LDS traffic for A.  The product is computed transposed,
+// Dᵀ = W_tile · Aᵀ on the 16x16x32 MFMA: the weight tile is the MFMA's A operand (ds_read_b128 of
+// 8 k per lane, conflict-free), 16 activation rows per wave its B operand, split in registers; a
+// lane's accumulators come out as 4 consecutive output columns of one row (16-B stores straight
+// from registers, the bias added from LDS).  The k dimension is permuted alike for both
+// operands: at step s the lanes of k-quarter kq hold k = 32 s + 4 kq + {0..3} and
+// 32 s + 16 + 4 kq + {0..3}, so a wave-instruction's 64 lanes read 16 rows x 64 contiguous bytes.
+// Workgroup b owns column tile (b / 8) % ntn and the row stream (b / (8 ntn)) * 8 + b % 8: the
+// column tiles of the same rows are on one XCD (b mod 8), so A is read from HBM once and from L2
+// by the other tiles.  Two forms:
+//   k_gemm_x3w_ring    three bf16 pieces per operand, six products (gemm.hip's x3), 80-column
+//                      tiles (GNNEA_X3W=2: the higher-fidelity fallback)
+//   k_gemm_f16x2_ring  two fp16 pieces per operand with power-of-two row / column scaling, three
+//                      products, 112-column tiles (64 for K = 600) -- the default
 #include "common.h"
 #include "gemm_x3w.h"
 
@@ -31,9 +31,6 @@ typedef float w3_f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int W3_NC = 80;   // columns per tile
 constexpr int W3_KC = 10;   // k-steps of 32 (K <= 320)
-constexpr int W3_NW = 4;    // waves per workgroup (one per SIMD, 512 registers)
-constexpr int W3_MF = 1;    // 16-row fragments per wave (the compute loop assumes 1)
-constexpr int W3_BM = 16 * W3_MF * W3_NW;
 constexpr int W3_PLANE = W3_KC * 4 * W3_NC;  // 16-B units per plane of a tile
 constexpr int64_t W3_TILE_BYTES = 3ll * W3_PLANE * 16;
 
@@ -68,203 +65,9 @@ __global__ __launch_bounds__(256) void k_pack_x3w(const float* __restrict__ B, i
   }
 }
 
-struct W3Split {
-  w3_bf16x8 h, m, l;
-};
-
-__device__ __forceinline__ W3Split w3_split(const uint4& q0, const uint4& q1) {
-  const float x[8] = {__builtin_bit_cast(float, q0.x), __builtin_bit_cast(float, q0.y),
-                      __builtin_bit_cast(float, q0.z), __builtin_bit_cast(float, q0.w),
-                      __builtin_bit_cast(float, q1.x), __builtin_bit_cast(float, q1.y),
-                      __builtin_bit_cast(float, q1.z), __builtin_bit_cast(float, q1.w)};
-  W3Split t;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const __bf16 h = (__bf16)x[e];
-    const float r1 = x[e] - (float)h;
-    const __bf16 m = (__bf16)r1;
-    t.h[e] = h;
-    t.m[e] = m;
-    t.l[e] = (__bf16)(r1 - (float)m);
-  }
-  return t;
-}
-
-__global__ __launch_bounds__(64 * W3_NW, 1) void k_gemm_x3w(int M, int N, int K, int ntn,
-                                                            const float* __restrict__ A,
-                                                            int64_t lda,
-                                                            const bf16_t* __restrict__ P,
-                                                            const float* __restrict__ bias,
-                                                            float* __restrict__ C, int64_t ldc,
-                                                            int64_t cs, float* __restrict__ C2,
-                                                            int64_t cs2) {
-  __shared__ __attribute__((aligned(16))) uint4 wl[3 * W3_PLANE];
-  __shared__ __attribute__((aligned(16))) float bsh[W3_NC];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int b = blockIdx.x;
-  const int nt = (b / 8) % ntn;
-  const int rs = (b / (8 * ntn)) * 8 + b % 8, nrs = (int)gridDim.x / ntn;
-  const int n0 = nt * W3_NC;
-  {  // the resident weight tile
-    const uint4* src = (const uint4*)(P + (int64_t)nt * 3 * W3_PLANE * 8);
-    for (int i = tid; i < 3 * W3_PLANE; i += 64 * W3_NW) wl[i] = src[i];
-    if (tid < W3_NC) bsh[tid] = bias && n0 + tid < N ? bias[n0 + tid] : 0.f;
-  }
-  __syncthreads();
-  const int tm = (M + W3_BM - 1) / W3_BM;
-  const int kq = lane >> 4, ml = lane & 15;
-  // this lane's quads at step s: row m, k = 32 s + 16 j + 4 kq (j = 0, 1): the four k-quarter
-  // lanes of a row read 64 contiguous bytes per load (16 lines per wave-instruction) and the two
-  // loads of a step one whole 128-B line; a quad at or past K reads the row's first quad (finite,
-  // valid) and is zeroed at use (K % 4 == 0: quads are whole)
-  // first step holding a quad past K (the zeroing branch is uniform)
-  const int s_tail = K / 32;
-  auto issue = [&](uint4 (&f)[W3_MF][2 * W3_KC], int rt) {
-#pragma unroll
-    for (int mf = 0; mf < W3_MF; ++mf) {
-      const float* p = A + (int64_t)min(rt * W3_BM + w * 16 * W3_MF + 16 * mf + ml, M - 1) * lda;
-#pragma unroll
-      for (int s = 0; s < W3_KC; ++s)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int k = 32 * s + 16 * j + 4 * kq;
-          f[mf][2 * s + j] = *(const uint4*)(p + (k < K ? k : 0));
-        }
-    }
-  };
-  // weight fragment (plane p, step s, column block jn) of this lane: unit ((p*KC + s)*4 + kq)*80 +
-  // 16 jn + ml
-  const uint4* wlane = wl + kq * W3_NC + ml;
-  auto compute_store = [&](const uint4 (&f)[W3_MF][2 * W3_KC], int rt) {
-    w3_f32x4 acc[W3_MF][5];
-#pragma unroll
-    for (int mf = 0; mf < W3_MF; ++mf)
-#pragma unroll
-      for (int j = 0; j < 5; ++j) acc[mf][j] = w3_f32x4{0.f, 0.f, 0.f, 0.f};
-    // the raw activation fragment of step s (quads at or past K zeroed: uniform branch)
-    auto raw_step = [&](int s, float (&x)[8]) {
-      uint4 q0 = f[0][2 * s], q1 = f[0][2 * s + 1];
-      if (s >= s_tail) {
-        const int k = 32 * s + 4 * kq;
-        if (k >= K) q0 = make_uint4(0u, 0u, 0u, 0u);
-        if (k + 16 >= K) q1 = make_uint4(0u, 0u, 0u, 0u);
-      }
-      x[0] = __builtin_bit_cast(float, q0.x); x[1] = __builtin_bit_cast(float, q0.y);
-      x[2] = __builtin_bit_cast(float, q0.z); x[3] = __builtin_bit_cast(float, q0.w);
-      x[4] = __builtin_bit_cast(float, q1.x); x[5] = __builtin_bit_cast(float, q1.y);
-      x[6] = __builtin_bit_cast(float, q1.z); x[7] = __builtin_bit_cast(float, q1.w);
-    };
-    auto split_el = [&](const float (&x)[8], int e, W3Split& t) {
-      const __bf16 h = (__bf16)x[e];
-      const float r1 = x[e] - (float)h;
-      const __bf16 m = (__bf16)r1;
-      t.h[e] = h;
-      t.m[e] = m;
-      t.l[e] = (__bf16)(r1 - (float)m);
-    };
-    W3Split acur;
-    uint4 wc[3], wn[3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) wc[p] = wlane[p * W3_PLANE];
-    {
-      float x[8];
-      raw_step(0, x);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) split_el(x, e, acur);
-    }
-#pragma unroll
-    for (int s = 0; s < W3_KC; ++s) {
-      // one step's weight fragments live at a time (the scheduler would hoist them all); the
-      // next step's activation split rides between the column blocks' MFMAs, two elements per
-      // block (the MFMAs leave half the vector issue cycles free)
-      __builtin_amdgcn_sched_barrier(0);
-      float xn[8];
-      if (s + 1 < W3_KC) raw_step(s + 1, xn);
-      W3Split anx;
-      const uint4* wp = wlane + s * 4 * W3_NC;
-      // (the last block prefetches the next step's first: step 0's after the last step)
-      const uint4* wq = wlane + ((s + 1) % W3_KC) * 4 * W3_NC;
-#pragma unroll
-      for (int jn = 0; jn < 5; ++jn) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          wn[p] = jn + 1 < 5 ? wp[p * W3_PLANE + 16 * (jn + 1)] : wq[p * W3_PLANE];
-        __builtin_amdgcn_sched_barrier(0);
-        const w3_bf16x8 wh = __builtin_bit_cast(w3_bf16x8, wc[0]);
-        const w3_bf16x8 wm = __builtin_bit_cast(w3_bf16x8, wc[1]);
-        const w3_bf16x8 wlo = __builtin_bit_cast(w3_bf16x8, wc[2]);
-        // gemm.hip's x3 order: small products first (activation x weight)
-        w3_f32x4& c = acc[0][jn];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.l, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, acur.m, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, acur.h, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.m, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, acur.h, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, acur.h, c, 0, 0, 0);
-        if (s + 1 < W3_KC && jn < 4) {
-          split_el(xn, 2 * jn, anx);
-          split_el(xn, 2 * jn + 1, anx);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) wc[p] = wn[p];
-      }
-      if (s + 1 < W3_KC) acur = anx;
-    }
-    // Dᵀ tile: lane holds row m = l % 16 of the wave's 16, columns 16 jn + 4 (l / 16) + 0..3
-#pragma unroll
-    for (int mf = 0; mf < W3_MF; ++mf) {
-      const int m = rt * W3_BM + w * 16 * W3_MF + 16 * mf + ml;
-      if (m >= M) continue;
-#pragma unroll
-      for (int jn = 0; jn < 5; ++jn) {
-        const int c = 16 * jn + 4 * kq;
-        const int n = n0 + c;
-        if (n < N) {  // N % 4 == 0: a group is wholly in or out
-          const float4 bv = *(const float4*)(bsh + c);
-          const w3_f32x4 a4 = acc[mf][jn];
-          const float4 o = make_float4(a4[0] + bv.x, a4[1] + bv.y, a4[2] + bv.z, a4[3] + bv.w);
-          *(float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63))) = o;
-          if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
-        }
-      }
-    }
-  };
-  uint4 fa[W3_MF][2 * W3_KC], fb[W3_MF][2 * W3_KC];
-  int rt = rs;
-  if (rt < tm) issue(fa, rt);
-  while (rt < tm) {
-    const int r1 = rt + nrs;
-    if (r1 < tm) issue(fb, r1);
-    compute_store(fa, rt);
-    if (r1 >= tm) break;
-    const int r2 = r1 + nrs;
-    if (r2 < tm) issue(fa, r2);
-    compute_store(fb, r1);
-    rt = r2;
-  }
-}
-
 // The activation split of the ring kernel, two elements at a time into packed bf16 pairs
-// (dword q of a fragment = elements 2q, 2q + 1).  GNNEA_X3W_SPLIT (a tuning switch, default 0):
-//   0  round-to-nearest-even: h = bf16(x), m = bf16(x - h), l = bf16(x - h - m)  (gemm.hip's split)
-//   2  truncation: h = the top 16 bits of x, m = the top 16 bits of x - h, l = bf16(x - h - m);
-//      x = h + m + l exactly (each residual keeps at most 16, then 8 significant bits), the two
-//      residuals as packed fp32 subtractions and the h / m pairs as byte permutes (fewer vector
-//      instructions per element; the dropped products m*l, l*m, l*l stay below 2^-21 |a||w|)
-//   1  timing only: h = m = l = the top halves (NOT a split; measures the split's cost)
-#ifndef GNNEA_X3W_SPLIT
-#define GNNEA_X3W_SPLIT 0
-#endif
-#ifndef GNNEA_X3W_AHOT
-#define GNNEA_X3W_AHOT 0
-#endif
-#ifndef GNNEA_X3W_NOSTORE
-#define GNNEA_X3W_NOSTORE 0
-#endif
-#ifndef GNNEA_F2_NOMFMA
-#define GNNEA_F2_NOMFMA 0
-#endif
+// (dword q of a fragment = elements 2q, 2q + 1): round-to-nearest-even, h = bf16(x),
+// m = bf16(x - h), l = bf16(x - h - m) (gemm.hip's split, pairwise instructions).
 struct W3SplitP {
   uint32_t h[4], m[4], l[4];
   __device__ __forceinline__ w3_bf16x8 vh() const { return __builtin_bit_cast(w3_bf16x8, *(const uint4*)h); }
@@ -276,27 +79,9 @@ __device__ __forceinline__ uint32_t w3_pk(__bf16 a, __bf16 b) {
   return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
 }
 
-template <int MODE>
 __device__ __forceinline__ void w3_split_pair(float x0, float x1, uint32_t& h, uint32_t& m,
                                               uint32_t& l) {
-  if constexpr (MODE == 0) {  // the same values as per-element casts, pairwise instructions
-    x3_split_pair(x0, x1, h, m, l);
-  } else if constexpr (MODE == 2) {
-    const uint32_t u0 = __builtin_bit_cast(uint32_t, x0), u1 = __builtin_bit_cast(uint32_t, x1);
-    const x3_f32x2 hv = {__builtin_bit_cast(float, u0 & 0xffff0000u),
-                         __builtin_bit_cast(float, u1 & 0xffff0000u)};
-    const x3_f32x2 r = x3_f32x2{x0, x1} - hv;
-    const uint32_t v0 = __builtin_bit_cast(uint32_t, r.x), v1 = __builtin_bit_cast(uint32_t, r.y);
-    const x3_f32x2 mv = {__builtin_bit_cast(float, v0 & 0xffff0000u),
-                         __builtin_bit_cast(float, v1 & 0xffff0000u)};
-    const x3_f32x2 q = r - mv;
-    h = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
-    m = __builtin_amdgcn_perm(v1, v0, 0x07060302u);
-    l = x3_cvt2(q);
-  } else {
-    const uint32_t u0 = __builtin_bit_cast(uint32_t, x0), u1 = __builtin_bit_cast(uint32_t, x1);
-    h = m = l = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
-  }
+  x3_split_pair(x0, x1, h, m, l);  // the same values as per-element casts
 }
 
 // The same product with 8 waves (two per SIMD: each one's LDS-read latency and split under the
@@ -329,9 +114,6 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
   const uint4* wlane = wl + kq * W3_NC + ml;
   uint4 f[2 * W3_KC];
   auto row_ptr = [&](int rt) {
-#if GNNEA_X3W_AHOT  // timing experiment only: every tile re-reads the first 8 row tiles (L2-hot)
-    rt = rt % 8;
-#endif
     return A + (int64_t)min(rt * BM + w * 16 + ml, M - 1) * lda;
   };
   // K in (288, 320]: steps 0..8 are inside every row (immediate offsets from the lane's base);
@@ -360,7 +142,7 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
     x[6] = __builtin_bit_cast(float, q1.z); x[7] = __builtin_bit_cast(float, q1.w);
   };
   auto split_pair = [&](const float (&x)[8], int q, W3SplitP& t) {
-    w3_split_pair<GNNEA_X3W_SPLIT>(x[2 * q], x[2 * q + 1], t.h[q], t.m[q], t.l[q]);
+    w3_split_pair(x[2 * q], x[2 * q + 1], t.h[q], t.m[q], t.l[q]);
   };
   if (rs < tm) {
     const float* p = row_ptr(rs);
@@ -428,148 +210,6 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
           float4 o = make_float4(a4[0] + bv.x, a4[1] + bv.y, a4[2] + bv.z, a4[3] + bv.w);
           float4* cp = (float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63)));
           if (beta != 0.f) {  // C = A·B + bias + beta C (uniform branch)
-            const float4 cv = *cp;
-            o.x += beta * cv.x; o.y += beta * cv.y; o.z += beta * cv.z; o.w += beta * cv.w;
-          }
-          if (relu) o = f4_relu(o);  // the Linear's act (layers/layers.py:121-122), uniform
-#if GNNEA_X3W_NOSTORE  // timing experiment only: no C traffic (the accumulators kept live)
-          if (o.x == 1.2345e-30f) *cp = o;
-#else
-          *cp = o;
-#endif
-          if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
-        }
-      }
-    }
-  }
-}
-
-// Two 16-row fragments per wave (GNNEA_X3W=3, A/B): every weight fragment read from LDS feeds
-// 12 MFMAs (two independent accumulator chains, interleaved) instead of 6, halving the LDS reads
-// per MFMA; the activation ring holds 5 steps of both fragments (a prefetch distance of half a
-// tile: 80 registers, as the one-fragment ring), refilled with step s + 5 -- the next tile's
-// step s - 5 past the tile's end -- as soon as step s has been split.  256-row tiles.
-__global__ __launch_bounds__(512) void k_gemm_x3w_ring2(int M, int N, int K, int ntn,
-                                                        const float* __restrict__ A, int64_t lda,
-                                                        const bf16_t* __restrict__ P,
-                                                        const float* __restrict__ bias,
-                                                        float* __restrict__ C, int64_t ldc,
-                                                        int64_t cs, float* __restrict__ C2,
-                                                        int64_t cs2, float beta, int relu) {
-  constexpr int NW = 8, BM = 32 * NW, RS = 5;  // ring slots (steps in flight)
-  __shared__ __attribute__((aligned(16))) uint4 wl[3 * W3_PLANE];
-  __shared__ __attribute__((aligned(16))) float bsh[W3_NC];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int b = blockIdx.x;
-  const int nt = (b / 8) % ntn;
-  const int rs = (b / (8 * ntn)) * 8 + b % 8, nrs = (int)gridDim.x / ntn;
-  const int n0 = nt * W3_NC;
-  {
-    const uint4* src = (const uint4*)(P + (int64_t)nt * 3 * W3_PLANE * 8);
-    for (int i = tid; i < 3 * W3_PLANE; i += 64 * NW) wl[i] = src[i];
-    if (tid < W3_NC) bsh[tid] = bias && n0 + tid < N ? bias[n0 + tid] : 0.f;
-  }
-  __syncthreads();
-  const int tm = (M + BM - 1) / BM;
-  const int kq = lane >> 4, ml = lane & 15;
-  const uint4* wlane = wl + kq * W3_NC + ml;
-  uint4 f[RS][2][2];  // [slot][fragment][quad]
-  auto row_ptr = [&](int rt, int fr) {
-    return A + (int64_t)min(rt * BM + w * 32 + 16 * fr + ml, M - 1) * lda;
-  };
-  auto load_step = [&](const float* p0, const float* p1, int s, uint4 (&slot)[2][2]) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int k = 32 * s + 16 * j + 4 * kq;
-      const int ko = (s < W3_KC - 1 || k < K) ? k : 0;  // the last step's quads past K: clamped
-      slot[0][j] = *(const uint4*)(p0 + ko);
-      slot[1][j] = *(const uint4*)(p1 + ko);
-    }
-  };
-  auto split_step = [&](int s, const uint4 (&slot)[2][2], W3SplitP (&t)[2]) {
-#pragma unroll
-    for (int fr = 0; fr < 2; ++fr) {
-      uint4 q0 = slot[fr][0], q1 = slot[fr][1];
-      if (s == W3_KC - 1) {
-        const int k = 32 * s + 4 * kq;
-        if (k >= K) q0 = make_uint4(0u, 0u, 0u, 0u);
-        if (k + 16 >= K) q1 = make_uint4(0u, 0u, 0u, 0u);
-      }
-      const float x[8] = {__builtin_bit_cast(float, q0.x), __builtin_bit_cast(float, q0.y),
-                          __builtin_bit_cast(float, q0.z), __builtin_bit_cast(float, q0.w),
-                          __builtin_bit_cast(float, q1.x), __builtin_bit_cast(float, q1.y),
-                          __builtin_bit_cast(float, q1.z), __builtin_bit_cast(float, q1.w)};
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        w3_split_pair<GNNEA_X3W_SPLIT>(x[2 * q], x[2 * q + 1], t[fr].h[q], t[fr].m[q], t[fr].l[q]);
-    }
-  };
-  if (rs < tm) {
-    const float* p0 = row_ptr(rs, 0);
-    const float* p1 = row_ptr(rs, 1);
-#pragma unroll
-    for (int s = 0; s < RS; ++s) load_step(p0, p1, s, f[s]);
-  }
-  for (int rt = rs; rt < tm; rt += nrs) {
-    const float* c0p = row_ptr(rt, 0);
-    const float* c1p = row_ptr(rt, 1);
-    const int rn = rt + nrs < tm ? rt + nrs : rt;  // past the end: valid rows, never used
-    const float* n0p = row_ptr(rn, 0);
-    const float* n1p = row_ptr(rn, 1);
-    w3_f32x4 acc[2][5];
-#pragma unroll
-    for (int fr = 0; fr < 2; ++fr)
-#pragma unroll
-      for (int j = 0; j < 5; ++j) acc[fr][j] = w3_f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < W3_KC; ++s) {
-      __builtin_amdgcn_sched_barrier(0);
-      W3SplitP a[2];
-      split_step(s, f[s % RS], a);
-      // refill the slot with step s + RS (this tile's, or the next tile's step s + RS - KC)
-      if (s + RS < W3_KC) load_step(c0p, c1p, s + RS, f[s % RS]);
-      else load_step(n0p, n1p, s + RS - W3_KC, f[s % RS]);
-      const w3_bf16x8 a0h = a[0].vh(), a0m = a[0].vm(), a0l = a[0].vl();
-      const w3_bf16x8 a1h = a[1].vh(), a1m = a[1].vm(), a1l = a[1].vl();
-      const uint4* wp = wlane + s * 4 * W3_NC;
-#pragma unroll
-      for (int jn = 0; jn < 5; ++jn) {
-        __builtin_amdgcn_sched_barrier(0);
-        const w3_bf16x8 wh = __builtin_bit_cast(w3_bf16x8, wp[16 * jn]);
-        const w3_bf16x8 wm = __builtin_bit_cast(w3_bf16x8, wp[W3_PLANE + 16 * jn]);
-        const w3_bf16x8 wlo = __builtin_bit_cast(w3_bf16x8, wp[2 * W3_PLANE + 16 * jn]);
-        w3_f32x4& c0 = acc[0][jn];
-        w3_f32x4& c1 = acc[1][jn];
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a0l, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a1l, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, a0m, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, a1m, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, a0h, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wlo, a1h, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a0m, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a1m, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, a0h, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, a1h, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a0h, c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, a1h, c1, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-#pragma unroll
-    for (int fr = 0; fr < 2; ++fr) {
-      const int m = rt * BM + w * 32 + 16 * fr + ml;
-      if (m >= M) continue;
-#pragma unroll
-      for (int jn = 0; jn < 5; ++jn) {
-        const int c = 16 * jn + 4 * kq;
-        int n = n0 + c;
-        asm volatile("" : "+v"(n));  // (as the ring: keep the column offsets out of LICM)
-        if (n < N) {
-          const float4 bv = *(const float4*)(bsh + c);
-          const w3_f32x4 a4 = acc[fr][jn];
-          float4 o = make_float4(a4[0] + bv.x, a4[1] + bv.y, a4[2] + bv.z, a4[3] + bv.w);
-          float4* cp = (float4*)(C + ((int64_t)(n >> 6) * cs + (int64_t)m * ldc + (n & 63)));
-          if (beta != 0.f) {
             const float4 cv = *cp;
             o.x += beta * cv.x; o.y += beta * cv.y; o.z += beta * cv.z; o.w += beta * cv.w;
           }
@@ -722,9 +362,6 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
   const uint4* wlane = wl + kq * NC + ml;
   uint4 f[20];
   auto row_ptr = [&](int rt) {
-#if GNNEA_X3W_AHOT  // timing experiment only: every tile re-reads the first 8 row tiles (L2-hot)
-    rt = rt % 8;
-#endif
     return A + (int64_t)min(rt * BM + w * 16 + ml, M - 1) * lda;
   };
   // chunk c's quads: steps 10 c .. ; steps before the last are inside every row, the last one's
@@ -823,13 +460,9 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
           const f2_f16x8 wh = __builtin_bit_cast(f2_f16x8, wp[16 * jn]);
           const f2_f16x8 wlo = __builtin_bit_cast(f2_f16x8, wp[PL + 16 * jn]);
           w3_f32x4& cc = acc[jn];
-#if GNNEA_F2_NOMFMA  // timing experiment only: no MFMAs (operands kept live by one add)
-          cc[0] += (float)wh[0] * (float)xl[0] + (float)wlo[1] * (float)xh[1];
-#else
           cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, cc, 0, 0, 0);
           cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wlo, xh, cc, 0, 0, 0);
           cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, cc, 0, 0, 0);
-#endif
         }
       }
     }
@@ -855,11 +488,7 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
             o.x += beta * c4.x; o.y += beta * c4.y; o.z += beta * c4.z; o.w += beta * c4.w;
           }
           if (relu) o = f4_relu(o);
-#if GNNEA_X3W_NOSTORE  // timing experiment only: no C traffic (the accumulators kept live)
-          if (o.x == 1.2345e-30f) *cp = o;
-#else
           *cp = o;
-#endif
           if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
         }
       }
@@ -869,18 +498,19 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
 
 // ---- host side ----
 
-// GNNEA_X3W: 0 k_gemm_x3p, 1 k_gemm_x3w, 2 k_gemm_x3w_ring, 3 k_gemm_x3w_ring2, 4 (default)
-// k_gemm_f16x2_ring (two fp16 pieces, three products; measured against mode 2 on one box:
-// 2M x 300 x 300 1.89 vs 2.18 ms, x·[Wᵀ|K_g] 3.92 vs 4.25, the K = 600 input gradient with
-// +C 5.34 vs 6.16 on the chunked form instead of k_gemm_x3p; profiles/r04_gemm_ab_f16x2_v2.json)
+// The tall K <= 320 (and K = 600) fp32 projections: k_gemm_f16x2_ring (two fp16 pieces, three
+// products) by default; GNNEA_X3W=2 selects the x3 ring (three bf16 pieces, six products: ~24
+// significant bits against ~22, the higher-fidelity fallback; tests/test_gpu_gemm_range.py pins
+// both).  Measured on one box: 2M x 300 x 300 1.89 vs 2.18 ms, x·[Wᵀ|K_g] 3.92 vs 4.25, the
+// K = 600 input gradient with +C 5.34 vs 6.16 (profiles/r04_gemm_ab_f16x2_v2.json).  The other
+// round-3/4 forms (the 4-wave x3w, the two-fragment ring) measured slower and were removed.
 static int x3w_mode() {
   static const int mode = [] {
     const char* e = getenv("GNNEA_X3W");
-    return e ? atoi(e) : 4;
+    return e && atoi(e) == 2 ? 2 : 4;
   }();
   return mode;
 }
-static bool x3w_on() { return x3w_mode() != 0; }
 
 // the f16x2 forms: K in (288, 320] on 80-column tiles, K in (576, 608] (the HighWay input
 // gradient [dh | dg]·[W ; K_gᵀ], K = 600) on 64-column tiles (2 planes x 19 steps x 64 columns =
@@ -888,18 +518,12 @@ static bool x3w_on() { return x3w_mode() != 0; }
 constexpr int F2_NC_WIDE = 64, F2_KC_WIDE = 19;
 // K <= 320 tile width: 112 columns (143 KB of weight; the activations re-read by 3 column
 // tiles at N = 300 instead of 4, 6 at N = 600 instead of 8; 12 % of the MFMAs on padding at
-// N = 300): 2M x 300 x 300 1.79 vs 1.87 ms, x·[Wᵀ|K_g] 3.45 vs 3.81, HGCN-EA step 88.0 vs 89.3
-// (profiles/r04_gemm_ab_f16x2_nc112.json); GNNEA_F2_NC=80 the 80-column tile (A/B)
-static int f16x2_nc() {
-  static const int nc = [] {
-    const char* e = getenv("GNNEA_F2_NC");
-    return e && atoi(e) == 80 ? W3_NC : 112;
-  }();
-  return nc;
-}
+// N = 300): 2M x 300 x 300 1.79 vs 1.87 ms on 80-column tiles, x·[Wᵀ|K_g] 3.45 vs 3.81, HGCN-EA
+// step 88.0 vs 89.3 (profiles/r04_gemm_ab_f16x2_nc112.json)
+constexpr int F2_NC = 112;
 static bool f16x2_k(int64_t K, int* kc, int* nc) {
   if (K > 32 * (W3_KC - 1) && K <= 32 * W3_KC) {
-    *kc = W3_KC, *nc = f16x2_nc();
+    *kc = W3_KC, *nc = F2_NC;
     return true;
   }
   if (K > 32 * (F2_KC_WIDE - 1) && K <= 32 * F2_KC_WIDE) {
@@ -916,7 +540,7 @@ static int64_t f16x2_ws_bytes(int64_t N, int kc, int nc) {
 int64_t gemm_x3w_ws_bytes(int64_t N) {  // the largest of the forms
   const int64_t x3 = (N + W3_NC - 1) / W3_NC * W3_TILE_BYTES;
   const int64_t f2 = f16x2_ws_bytes(N, F2_KC_WIDE, F2_NC_WIDE);
-  const int64_t f3 = f16x2_ws_bytes(N, W3_KC, 112);
+  const int64_t f3 = f16x2_ws_bytes(N, W3_KC, F2_NC);
   const int64_t m = x3 > f2 ? x3 : f2;
   return m > f3 ? m : f3;
 }
@@ -928,7 +552,7 @@ bool gemm_x3w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda,
   int kc, nc;
   const bool kok = x3w_mode() == 4 ? f16x2_k(K, &kc, &nc)
                                    : (K > 32 * (W3_KC - 1) && K <= 32 * W3_KC);
-  return x3w_on() && !trans_a && ((beta == 0.f && act == GNNEA_ACT_IDENTITY) || x3w_mode() >= 2) &&
+  return !trans_a &&
          (act == GNNEA_ACT_IDENTITY || act == GNNEA_ACT_RELU) && A && C && M >= 65536 &&
          M < (1ll << 31) && N >= 64 && N <= 4096 && N % 4 == 0 && kok && K % 4 == 0 &&
          lda >= K && lda % 4 == 0 && (((uintptr_t)A) & 15) == 0 &&
@@ -977,12 +601,8 @@ static int f16x2_launch(int trans_b, int64_t M, int64_t N, int64_t K, const floa
                      (int)K, ntn, kc, nc, (const float*)tsc, (uint16_t*)ws);
   GNNEA_LAUNCH_CHECK();
   const int grid = ring_grid(ntn, M, 128);
-  if (kc == W3_KC && nc == 112)
-    hipLaunchKernelGGL((k_gemm_f16x2_ring<W3_KC, 112>), dim3(grid), dim3(512), 0, s, (int)M,
-                       (int)N, (int)K, ntn, A, lda, (const uint16_t*)ws, (const float*)tinv, bias,
-                       C, ldc, cs, C2, cs2, beta, relu);
-  else if (kc == W3_KC)
-    hipLaunchKernelGGL((k_gemm_f16x2_ring<W3_KC, W3_NC>), dim3(grid), dim3(512), 0, s, (int)M,
+  if (kc == W3_KC)
+    hipLaunchKernelGGL((k_gemm_f16x2_ring<W3_KC, F2_NC>), dim3(grid), dim3(512), 0, s, (int)M,
                        (int)N, (int)K, ntn, A, lda, (const uint16_t*)ws, (const float*)tinv, bias,
                        C, ldc, cs, C2, cs2, beta, relu);
   else
@@ -1012,17 +632,9 @@ int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A
                        (int)K, ntn, P);
     GNNEA_LAUNCH_CHECK();
   }
-  const bool ring = x3w_mode() == 2, ring2 = x3w_mode() == 3;
-  const int grid = ring_grid(ntn, M, ring2 ? 256 : ring ? 128 : W3_BM);
-  if (ring2)
-    hipLaunchKernelGGL(k_gemm_x3w_ring2, dim3(grid), dim3(512), 0, s, (int)M, (int)N, (int)K,
-                       ntn, A, lda, P, bias, C, ldc, cs, C2, cs2, beta, relu);
-  else if (ring)
-    hipLaunchKernelGGL(k_gemm_x3w_ring, dim3(grid), dim3(512), 0, s, (int)M, (int)N, (int)K, ntn,
-                       A, lda, P, bias, C, ldc, cs, C2, cs2, beta, relu);
-  else
-    hipLaunchKernelGGL(k_gemm_x3w, dim3(grid), dim3(64 * W3_NW), 0, s, (int)M, (int)N, (int)K,
-                       ntn, A, lda, P, bias, C, ldc, cs, C2, cs2);
+  const int grid = ring_grid(ntn, M, 128);
+  hipLaunchKernelGGL(k_gemm_x3w_ring, dim3(grid), dim3(512), 0, s, (int)M, (int)N, (int)K, ntn, A,
+                     lda, P, bias, C, ldc, cs, C2, cs2, beta, relu);
   GNNEA_LAUNCH_CHECK();
   return 0;
 }

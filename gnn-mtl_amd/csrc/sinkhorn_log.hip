@@ -762,25 +762,45 @@ __global__ __launch_bounds__(256) void k_sk_plan(const T* __restrict__ C, SkArgs
   }
 }
 
+// Column sums of the returned plan: kMaxSplits row ranges per 256-column block (one thread per
+// column, partial sums into the workspace's split rows), then the splits added in order by
+// k_sk_colsum_fin: deterministic.  (One thread per column over all I rows ran 59 workgroups for
+// 7.6 ms at B = 15000.)
 template <typename T>
 __global__ __launch_bounds__(256) void k_sk_colsum(const T* __restrict__ C, SkArgs a, SkDev d,
-                                                   int iters_run, double* __restrict__ col_sum) {
+                                                   int iters_run, double* __restrict__ part) {
   const int slot = sk_final_slot(d, iters_run);
   const int j = blockIdx.x * 256 + threadIdx.x;
+  const int ns = gridDim.y, sp = blockIdx.y;
+  const int i0 = (int)((int64_t)a.I * sp / ns), i1 = (int)((int64_t)a.I * (sp + 1) / ns);
   if (j >= a.J) return;
   const bool knopp = a.mode == GNNEA_SK_KNOPP;
   const double gj = knopp ? d.g[(int64_t)slot * a.J + j] : d.va[j];
   const double* f = knopp ? d.f + (int64_t)slot * a.I : d.ua;
-  double s = 0.0;
-  for (int i = 0; i < a.I; ++i) {
+  double s0 = 0.0, s1 = 0.0;
+  auto term = [&](int i) {
     const double c = ld_c(C, (int64_t)i * a.ldc + j);
     if (knopp) {
       const double k = -c * a.inv_eps;
-      s += k < kExpUnderflow ? 0.0 : exp_f64(f[i] + gj + k);
-    } else {
-      s += exp_f64(fmin(f[i] + gj - c * a.inv_eps, a.kclamp));
+      return k < kExpUnderflow ? 0.0 : exp_f64(f[i] + gj + k);
     }
+    return exp_f64(fmin(f[i] + gj - c * a.inv_eps, a.kclamp));
+  };
+  int i = i0;
+  for (; i + 1 < i1; i += 2) {  // two independent chains
+    s0 += term(i);
+    s1 += term(i + 1);
   }
+  if (i < i1) s0 += term(i);
+  part[(int64_t)sp * a.J + j] = s0 + s1;
+}
+
+__global__ __launch_bounds__(256) void k_sk_colsum_fin(const double* __restrict__ part, int ns,
+                                                       int J, double* __restrict__ col_sum) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= J) return;
+  double s = 0.0;
+  for (int q = 0; q < ns; ++q) s += part[(int64_t)q * J + j];
   col_sum[j] = s;
 }
 
@@ -905,24 +925,24 @@ __device__ __forceinline__ void row_barrier() {
 // PAIR (fp32 C, J and ldc even): lane l owns the column PAIRS c0 + 128 p + 2 l + {0, 1}, read as
 // one 8-B buffer load each (NCM / 2 loads per row instead of NCM: two rows in flight stay below
 // the 63 outstanding loads vmcnt can count), g as one 16-B LDS read per pair.
-template <typename T, int NCM, bool PH0, bool PAIR>
-__global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C, SkArgs a, SkDev d,
+template <typename T, int NCM, bool PH0, bool PAIR, int FW>
+__global__ __launch_bounds__(64 * FW) void k_lsk_sweep(const T* __restrict__ C, SkArgs a, SkDev d,
                                                         int it, int slot_fp, int slot_g,
                                                         int slot_fo, int rpw) {
   __shared__ double tab[kFTab];
-  __shared__ double gsh[kFW * NCM * 64];
-  __shared__ double reds[2][kFW];
+  __shared__ double gsh[FW * NCM * 64];
+  __shared__ double reds[2][FW];
   if (!PH0 && d.st[ST_DONE]) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   {
-    double tv[kFTab / (64 * kFW)];
+    double tv[kFTab / (64 * FW)];
 #pragma unroll
-    for (int q = 0; q < kFTab / (64 * kFW); ++q) tv[q] = d.ftab[tid + q * 64 * kFW];
+    for (int q = 0; q < kFTab / (64 * FW); ++q) tv[q] = d.ftab[tid + q * 64 * FW];
 #pragma unroll
-    for (int q = 0; q < kFTab / (64 * kFW); ++q) tab[tid + q * 64 * kFW] = tv[q];
+    for (int q = 0; q < kFTab / (64 * FW); ++q) tab[tid + q * 64 * FW] = tv[q];
   }
   const int r0 = blockIdx.x * rpw, r1 = min(a.I, r0 + rpw);
-  const int cw = ((a.J + kFW - 1) / kFW + 63) & ~63;
+  const int cw = ((a.J + FW - 1) / FW + 63) & ~63;
   const int c0 = w * cw;
   const int lim = min(c0 + cw, a.J) - c0 - lane;  // column c0 + 64 k + lane is valid iff 64 k < lim
   const double* __restrict__ g = d.g + (int64_t)slot_g * a.J;
@@ -941,12 +961,12 @@ __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C,
   const int lbase = PAIR ? 2 * lane : lane;
   const int limv = min(c0 + cw, a.J) - c0 - lbase;  // element k valid iff eo(k) < limv
   const double* __restrict__ gl = gsh + w * NCM * 64 + lbase;
-  T kA[NCM], kB[NCM];
+  T kA[NCM], kB[NCM], kC[NCM];
   // the row's two scalars (f_prev, a) ride with its C loads, issued FIRST: a row's scalars are
   // then older than the next row's C loads in flight, and waiting for them is a counted vmcnt
   // (loaded inside process() they were the newest loads, and the wait for them drained the next
   // row's prefetch every row)
-  double fA = 0.0, fB = 0.0, wA = 0.0, wB = 0.0;
+  double fA = 0.0, fB = 0.0, fC = 0.0, wA = 0.0, wB = 0.0, wC = 0.0;
   // buffer loads over the row (J elements): one lane offset, the 64 k steps as scalar offsets;
   // columns past J read 0 (their g slice is -1e300: no contribution) without a clamp per column
   const uint32_t voff = (uint32_t)(c0 + lbase) * sizeof(T);
@@ -973,13 +993,35 @@ __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C,
       }
     }
   };
-  // the first row's loads go out before the stop decision (round trips on the status block)
-  if (r0 < r1) load(kA, fA, wA, r0);
+  // the first rows' loads go out before the stop decision (round trips on the status block)
+  if (r0 < r1) {
+    load(kA, fA, wA, r0);
+    if (PAIR && FW == 8) load(kB, fB, wB, min(r0 + 1, r1 - 1));
+  }
   if (!PH0 && knopp_stop(d, it)) return;
   double acc[NCM];
 #pragma unroll
   for (int k = 0; k < NCM; ++k) acc[k] = 0.0;
   const double neg_s = -a.inv_eps;
+  // fp32 C: the term is masked (the reference's K entry underflows to 0: -C/reg below
+  // kExpUnderflow) exactly when C > cthr, the largest float that still gives a finite term --
+  // one f32 compare per element; the masked element's C is replaced by 1e30 (x -> -huge ->
+  // exp2x 0); the logit is one fma with the folded scale C * (-kFScale / reg)
+  const double ncs = neg_s * kFScale;
+  float cthr = (float)(kExpUnderflow / neg_s);
+  while (!((double)cthr * neg_s >= kExpUnderflow)) cthr = nextafterf(cthr, -INFINITY);
+  while ((double)nextafterf(cthr, INFINITY) * neg_s >= kExpUnderflow)
+    cthr = nextafterf(cthr, INFINITY);
+  auto logit = [&](T c, double gsum) {
+    if constexpr (sizeof(T) == 4) {
+      const float cm = c > cthr ? 1e30f : (float)c;
+      return __builtin_fma((double)cm, ncs, gsum);
+    } else {
+      const double kn = (double)c * neg_s;
+      const double kk = kn < kExpUnderflow ? -1e300 : kn;
+      return __builtin_fma(kk, kFScale, gsum);
+    }
+  };
   int nfb = 0;  // rows listed for the exact update (k_lsk_fix)
   auto process = [&](const T (&kv)[NCM], const double fv, const double wv, int r, int par) {
     // x = (g_j + k_ij) in units of ln2 / 2048; masked terms -3e303 (exp2x -> 0).  The slice of g
@@ -990,9 +1032,7 @@ __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C,
       const double f0 = fv * kFScale;
 #pragma unroll
       for (int k = 0; k < NCM; ++k) {
-        const double kn = (double)kv[k] * neg_s;
-        const double kk = kn < kExpUnderflow ? -1e300 : kn;
-        e[k] = exp2x(__builtin_fma(kk, kFScale, gl[eo(k)] + f0), tab);
+        e[k] = exp2x(logit(kv[k], gl[eo(k)] + f0), tab);
         acc[k] += e[k];
       }
       return;
@@ -1003,9 +1043,7 @@ __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C,
     double rsum = 0.0;
 #pragma unroll
     for (int k = 0; k < NCM; ++k) {
-      const double kn = (double)kv[k] * neg_s;
-      const double kk = kn < kExpUnderflow ? -1e300 : kn;
-      e[k] = exp2x(__builtin_fma(kk, kFScale, gl[eo(k)] + fps), tab);
+      e[k] = exp2x(logit(kv[k], gl[eo(k)] + fps), tab);
       rsum += e[k];
       if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);
     }
@@ -1014,7 +1052,7 @@ __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C,
     row_barrier();  // double-buffered by row parity: one barrier per row
     double sr = 0.0;
 #pragma unroll
-    for (int q = 0; q < kFW; ++q) sr += reds[par][q];  // every wave, the same order
+    for (int q = 0; q < FW; ++q) sr += reds[par][q];  // every wave, the same order
     // (NaN -- in C or a potential -- propagates through the fast path; the row update flags it)
     if ((sr >= kFLo && sr <= kFHi) || sr != sr) {  // u_it / u_prev = a / s
       const double wi = wv / sr;
@@ -1038,14 +1076,31 @@ __global__ __launch_bounds__(64 * kFW) void k_lsk_sweep(const T* __restrict__ C,
   // every path into a row's processing has the same loads outstanding and its waits are counted
   // vmcnt(NCM loads of the next row) -- a conditional load made the compiler wait for the
   // count of the path without it, i.e. for most of the next row's loads
+  // PAIR: NCM / 2 + 2 loads per row, two rows ahead in flight (three register buffers, the
+  // waits vmcnt(2 rows)); otherwise one row ahead
   int r = r0, par = 0;
-  while (r < r1) {
-    load(kB, fB, wB, min(r + 1, r1 - 1));
-    process(kA, fA, wA, r, par);
-    if (r + 1 >= r1) break;
-    load(kA, fA, wA, min(r + 2, r1 - 1));
-    process(kB, fB, wB, r + 1, par ^ 1);
-    r += 2;
+  if constexpr (PAIR && FW == 8) {
+    while (r < r1) {
+      load(kC, fC, wC, min(r + 2, r1 - 1));
+      process(kA, fA, wA, r, par);
+      if (r + 1 >= r1) break;
+      load(kA, fA, wA, min(r + 3, r1 - 1));
+      process(kB, fB, wB, r + 1, par ^ 1);
+      if (r + 2 >= r1) break;
+      load(kB, fB, wB, min(r + 4, r1 - 1));
+      process(kC, fC, wC, r + 2, par);
+      par ^= 1;
+      r += 3;
+    }
+  } else {
+    while (r < r1) {
+      load(kB, fB, wB, min(r + 1, r1 - 1));
+      process(kA, fA, wA, r, par);
+      if (r + 1 >= r1) break;
+      load(kA, fA, wA, min(r + 2, r1 - 1));
+      process(kB, fB, wB, r + 1, par ^ 1);
+      r += 2;
+    }
   }
   double* __restrict__ part = d.fpart + (int64_t)blockIdx.x * a.J + c0 + lbase;
 #pragma unroll
@@ -1196,20 +1251,24 @@ static bool fused_applies(const gnnea_sinkhorn* p) {
 
 bool fused_ok(const gnnea_sinkhorn* p) { return p && fused_applies(p); }
 
-template <typename T, bool PH0, bool PAIR>
+template <typename T, bool PH0, bool PAIR, int FW>
 static void launch_fused_sweep_p(const T* C, const SkArgs& a, const SkDev& d, int it, int sfp,
                                  int sg, int sfo, hipStream_t s) {
   const int rpw = fused_rpw(a.I), ns = fused_wgs(a.I);
-  const int nc = (((a.J + kFW - 1) / kFW + 63) & ~63) / 64;
-  const dim3 g(ns), b(64 * kFW);
+  const int nc = (((a.J + FW - 1) / FW + 63) & ~63) / 64;
+  const dim3 g(ns), b(64 * FW);
   if (nc <= 4)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 4, PH0, PAIR>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+    hipLaunchKernelGGL((k_lsk_sweep<T, 4, PH0, PAIR, FW>), g, b, 0, s, C, a, d, it, sfp, sg, sfo,
+                       rpw);
   else if (nc <= 8)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 8, PH0, PAIR>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
-  else if (sizeof(T) == 8 || nc <= 16)  // (fp64 C: fused_applies bounds nc by 16)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 16, PH0, PAIR>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
-  else if constexpr (sizeof(T) == 4)
-    hipLaunchKernelGGL((k_lsk_sweep<T, 32, PH0, PAIR>), g, b, 0, s, C, a, d, it, sfp, sg, sfo, rpw);
+    hipLaunchKernelGGL((k_lsk_sweep<T, 8, PH0, PAIR, FW>), g, b, 0, s, C, a, d, it, sfp, sg, sfo,
+                       rpw);
+  else if (sizeof(T) == 8 || FW == 16 || nc <= 16)  // (fp64 C: fused_applies bounds nc by 16)
+    hipLaunchKernelGGL((k_lsk_sweep<T, 16, PH0, PAIR, FW>), g, b, 0, s, C, a, d, it, sfp, sg, sfo,
+                       rpw);
+  else if constexpr (sizeof(T) == 4 && FW == 8)
+    hipLaunchKernelGGL((k_lsk_sweep<T, 32, PH0, PAIR, FW>), g, b, 0, s, C, a, d, it, sfp, sg, sfo,
+                       rpw);
 }
 
 // fp32 C whose rows start on 8-B boundaries and hold whole column pairs: the PAIR layout
@@ -1218,11 +1277,15 @@ static void launch_fused_sweep(const T* C, const SkArgs& a, const SkDev& d, int 
                                int sg, int sfo, hipStream_t s) {
   if constexpr (sizeof(T) == 4) {
     if (a.J % 2 == 0 && a.ldc % 2 == 0 && ((uintptr_t)C & 7) == 0) {
-      launch_fused_sweep_p<T, PH0, true>(C, a, d, it, sfp, sg, sfo, s);
+      // wide rows: 16 waves of 16 columns per lane (four waves per SIMD) instead of 8 of 32
+      if (a.J > 64 * 8 * 16)
+        launch_fused_sweep_p<T, PH0, true, 16>(C, a, d, it, sfp, sg, sfo, s);
+      else
+        launch_fused_sweep_p<T, PH0, true, 8>(C, a, d, it, sfp, sg, sfo, s);
       return;
     }
   }
-  launch_fused_sweep_p<T, PH0, false>(C, a, d, it, sfp, sg, sfo, s);
+  launch_fused_sweep_p<T, PH0, false, 8>(C, a, d, it, sfp, sg, sfo, s);
 }
 
 // Launch configurations of the two passes (10*row + col); the path runs configuration 0, the
@@ -1400,13 +1463,17 @@ int finish(const gnnea_sinkhorn* p, void* plan, int plan_dtype, int64_t ldp, dou
   hipLaunchKernelGGL(k_sk_loss, dim3(1), dim3(1024), 0, s, a, d, p->iters_run);
   GNNEA_LAUNCH_CHECK();
   if (col_sum) {
-    const dim3 gcs(div_up(p->J, 256));
+    const int ns = std::max(1, std::min(kMaxSplits, div_up(p->I, 256)));
+    const dim3 gcs(div_up(p->J, 256), ns);
     if (p->c_dtype == GNNEA_F32)
       hipLaunchKernelGGL(k_sk_colsum<float>, gcs, dim3(256), 0, s, (const float*)p->C, a, d,
-                         slot, col_sum);
+                         slot, d.pm);
     else
       hipLaunchKernelGGL(k_sk_colsum<double>, gcs, dim3(256), 0, s, (const double*)p->C, a, d,
-                         slot, col_sum);
+                         slot, d.pm);
+    GNNEA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_sk_colsum_fin, dim3(div_up(p->J, 256)), dim3(256), 0, s, d.pm, ns, p->J,
+                       col_sum);
     GNNEA_LAUNCH_CHECK();
   }
   return 0;

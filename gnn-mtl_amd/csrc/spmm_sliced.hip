@@ -48,13 +48,13 @@ struct SlicedHighway {
 
 __device__ __forceinline__ float sigm_f(float x) { return 1.f / (1.f + expf(-x)); }
 
-// PIPE (default): the gathers of a row are issued unconditionally (edges past the chunk re-read
-// its last edge's piece with weight 0; lanes past D read their group's first 16 B and discard
-// the sum), in batches of 4U edges with the next batch in flight while one is summed (register
-// double buffer), so no gathered piece is waited on inside a branch; !PIPE: one batch at a time
-// behind per-lane conditions (A/B timing, GNNEA_SPMM_PIPE=0).  The per-lane sum order is the
-// same either way (edge k + 4u + g, u ascending).
-template <int ACT, int U, bool HW, typename TX, typename TY, bool PIPE = true>
+// The gathers of a row are issued unconditionally (edges past the chunk re-read its last edge's
+// piece with weight 0; lanes past D read their group's first 16 B and discard the sum), in
+// batches of 4U edges with the next batch in flight while one is summed (register double buffer),
+// so no gathered piece is waited on inside a branch (behind per-lane conditions, one batch at a
+// time, the same kernel measured slower: round 3).  Per-lane sum order: edge k + 4u + g, u
+// ascending.
+template <int ACT, int U, bool HW, typename TX, typename TY>
 __global__ __launch_bounds__(256) void k_spmm_sliced(const int32_t* __restrict__ rowptr,
                                                      const int32_t* __restrict__ col,
                                                      const float* __restrict__ val, int n_rows,
@@ -70,77 +70,65 @@ __global__ __launch_bounds__(256) void k_spmm_sliced(const int32_t* __restrict__
   const int lane = lane_id(), g = lane >> 4, c = lane & 15;
   const int c0 = s * W + E * c;
   const bool own = c0 < D;
-  const uint4* X = Xs + (int64_t)s * sstride16 + c;
   const int beg = rowptr[row], end = rowptr[row + 1];
+  // HighWay epilogue operands (gate_pre, bias_gate, resid of this row piece) loaded by every
+  // lane from a clamped column BEFORE the gathers: the groups share group 0's addresses (no extra
+  // lines), and their latency hides under the row's gathers instead of following them (read in
+  // the epilogue they cost one serial round trip per row after the reduction)
+  float4 hgp[E / 4], hrr[E / 4];
+  if constexpr (HW) {
+#pragma unroll
+    for (int k = 0; k < E / 4; ++k) {
+      const int cc = min(c0 + 4 * k, D - 4);
+      const int gc = hw.goff + cc;
+      hgp[k] = hw.gate[(int64_t)(gc >> 6) * hw.gsstride4 + (int64_t)row * (kSliceW / 4) +
+                       ((gc & 63) >> 2)];
+      hrr[k] = *(const float4*)(hw.resid + (int64_t)row * hw.ldr + cc);
+      if (hw.bias) {
+        const float4 bv = *(const float4*)(hw.bias + cc);
+        hgp[k].x += bv.x; hgp[k].y += bv.y; hgp[k].z += bv.z; hgp[k].w += bv.w;
+      }
+    }
+  }
   float acc[E];
 #pragma unroll
   for (int k = 0; k < E; ++k) acc[k] = 0.f;
-  if constexpr (PIPE) {
-    const uint4* Xp = Xs + (int64_t)s * sstride16 + (own ? c : 0);
-    for (int base = beg; base < end; base += 64) {
-      const int cnt = min(64, end - base);
-      const int el = base + min(lane, cnt - 1);
-      const int mc = col[el];
-      const float mv = val[el] * (lane < cnt ? 1.f : 0.f);  // (a select would sink the load)
-      uint4 ra[U], rb[U];
-      auto issue = [&](uint4 (&r)[U], int k) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int j = __shfl(mc, min(k + 4 * u + g, cnt - 1), 64);
-          r[u] = Xp[(int64_t)j * 16];
-        }
-      };
-      auto consume = [&](const uint4 (&r)[U], int k) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int e = k + 4 * u + g;
-          // (the shuffle runs in every lane: a bpermute from a lane masked off by the
-          // condition would return its inactive value)
-          const float vs = __shfl(mv, e & 63, 64);
-          const float v = e < cnt ? vs : 0.f;
-          float f[E];
-          unpack16(r[u], f);
-#pragma unroll
-          for (int q = 0; q < E; ++q) acc[q] = fmaf(v, f[q], acc[q]);
-        }
-      };
-      issue(ra, 0);
-      for (int k = 0; k < cnt; k += 8 * U) {
-        issue(rb, k + 4 * U);
-        __builtin_amdgcn_sched_barrier(0);  // the next batch's gathers ahead of this batch's FMAs
-        consume(ra, k);
-        issue(ra, k + 8 * U);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(rb, k + 4 * U);
-      }
-    }
-  } else
+  const uint4* Xp = Xs + (int64_t)s * sstride16 + (own ? c : 0);
   for (int base = beg; base < end; base += 64) {
     const int cnt = min(64, end - base);
-    const int mc = lane < cnt ? col[base + lane] : 0;
-    const float mv = lane < cnt ? val[base + lane] : 0.f;
-    for (int k = 0; k < cnt; k += 4 * U) {
-      uint4 r[U];
-      float v[U];
+    const int el = base + min(lane, cnt - 1);
+    const int mc = col[el];
+    const float mv = val[el] * (lane < cnt ? 1.f : 0.f);  // (a select would sink the load)
+    uint4 ra[U], rb[U];
+    auto issue = [&](uint4 (&r)[U], int k) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int e = k + 4 * u + g;  // <= 63: k is a multiple of 4U that divides 64
-        const int j = __shfl(mc, e & 63, 64);
-        v[u] = __shfl(mv, e & 63, 64);
-        if (e < cnt && own) {
-          r[u] = X[(int64_t)j * 16];
-        } else {
-          r[u] = make_uint4(0u, 0u, 0u, 0u);
-          v[u] = 0.f;
-        }
+        const int j = __shfl(mc, min(k + 4 * u + g, cnt - 1), 64);
+        r[u] = Xp[(int64_t)j * 16];
       }
+    };
+    auto consume = [&](const uint4 (&r)[U], int k) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        const int e = k + 4 * u + g;
+        // (the shuffle runs in every lane: a bpermute from a lane masked off by the
+        // condition would return its inactive value)
+        const float vs = __shfl(mv, e & 63, 64);
+        const float v = e < cnt ? vs : 0.f;
         float f[E];
         unpack16(r[u], f);
 #pragma unroll
-        for (int q = 0; q < E; ++q) acc[q] = fmaf(v[u], f[q], acc[q]);
+        for (int q = 0; q < E; ++q) acc[q] = fmaf(v, f[q], acc[q]);
       }
+    };
+    issue(ra, 0);
+    for (int k = 0; k < cnt; k += 8 * U) {
+      issue(rb, k + 4 * U);
+      __builtin_amdgcn_sched_barrier(0);  // the next batch's gathers ahead of this batch's FMAs
+      consume(ra, k);
+      issue(ra, k + 8 * U);
+      __builtin_amdgcn_sched_barrier(0);
+      consume(rb, k + 4 * U);
     }
   }
 #pragma unroll
@@ -158,15 +146,9 @@ __global__ __launch_bounds__(256) void k_spmm_sliced(const int32_t* __restrict__
     if constexpr (!HW) {
       *(RY*)(Y + (int64_t)row * ldy + cc) = Vec4<TY>::put(sv);
     } else {
-      const int gc = hw.goff + cc;  // gate_pre column in its table (multiple of 4)
-      float4 gp = hw.gate[(int64_t)(gc >> 6) * hw.gsstride4 + (int64_t)row * (kSliceW / 4) +
-                          ((gc & 63) >> 2)];
-      if (hw.bias) {
-        const float4 bv = *(const float4*)(hw.bias + cc);
-        gp.x += bv.x; gp.y += bv.y; gp.z += bv.z; gp.w += bv.w;
-      }
+      const float4 gp = hgp[k];  // gate_pre + bias_gate (loaded before the gathers)
       const float4 gt = make_float4(sigm_f(gp.x), sigm_f(gp.y), sigm_f(gp.z), sigm_f(gp.w));
-      const float4 rr = *(const float4*)(hw.resid + (int64_t)row * hw.ldr + cc);
+      const float4 rr = hrr[k];
       // reference order: transform_gate * support + carry_gate * residual, carry = 1 - g
       float4 o;
       o.x = gt.x * sv.x + (1.f - gt.x) * rr.x;
@@ -263,17 +245,9 @@ static int spmm_sliced(const int32_t* rowptr, const int32_t* col, const float* v
   const int S = (D + W - 1) / W;
   if ((int64_t)nbs * S >= (1ll << 31)) return GNNEA_EINVAL;
   const int64_t ss16 = sstride * (int64_t)sizeof(TX) / 16;
-  static const bool pipe = [] {  // A/B timing only (GNNEA_SPMM_PIPE=0: one batch at a time)
-    const char* e = getenv("GNNEA_SPMM_PIPE");
-    return !(e && e[0] == '0');
-  }();
 #define GNNEA_SS(A)                                                                            \
-  if (pipe)                                                                                    \
-    hipLaunchKernelGGL((k_spmm_sliced<A, 2, HW, TX, TY, true>), dim3(nbs * S), dim3(256), 0, s, \
-                       rowptr, col, val, n_rows, nbs, D, (const uint4*)Xs, ss16, Y, ldy, hw);  \
-  else                                                                                         \
-    hipLaunchKernelGGL((k_spmm_sliced<A, 4, HW, TX, TY, false>), dim3(nbs * S), dim3(256), 0,  \
-                       s, rowptr, col, val, n_rows, nbs, D, (const uint4*)Xs, ss16, Y, ldy, hw)
+  hipLaunchKernelGGL((k_spmm_sliced<A, 2, HW, TX, TY>), dim3(nbs * S), dim3(256), 0, s, rowptr, \
+                     col, val, n_rows, nbs, D, (const uint4*)Xs, ss16, Y, ldy, hw)
   switch (act) {
     case GNNEA_ACT_IDENTITY: GNNEA_SS(GNNEA_ACT_IDENTITY); break;
     case GNNEA_ACT_RELU: GNNEA_SS(GNNEA_ACT_RELU); break;

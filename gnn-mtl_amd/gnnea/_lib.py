@@ -93,6 +93,9 @@ SIGNATURES = {
                                                      ctypes.c_int, _p]),
     "gnnea_highway_bwd_sliced_f32": (ctypes.c_int, [_p, _p, _p, _p, _i64, _i64, _i32, _p, _i64,
                                                     _p, _i64, _p, _i64, ctypes.c_int, _p]),
+    "gnnea_highway_bwd_sliced_zg_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _p, _p, _i64, _i64,
+                                                       _i32, _p, _i64, _p, _i64, _p, _i64,
+                                                       ctypes.c_int, _p]),
     "gnnea_spmm_sliced_bf16": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64,
                                               ctypes.c_int, ctypes.c_int, _p]),
     "gnnea_slice_pack_bf16": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, _p]),

@@ -830,10 +830,11 @@ class HighwayFn(torch.autograd.Function):
         return dh, dgate, dres, None, None, None
 
 
-def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act):
+def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act, save_g=True):
     """HighWay tail over the slice-major projection table Zs ([S, N, 64] holding x·[Wᵀ | K_g] +
     [b | 0]: hidden in columns [0, D), gate_pre in [D, 2D)), per diagonal block
-    (gnnea_spmm_highway_sliced_f32).  Returns (out, S, g), row-major."""
+    (gnnea_spmm_highway_sliced_f32).  Returns (out, S, g), row-major; g is None with
+    ``save_g=False`` (the backward recomputes it from Zs: highway_bwd_sliced_zg)."""
     resid = _rows(resid, torch.float32)
     N = csr.n_rows
     if Zs.dim() != 3 or Zs.shape[2] != SLICE_W or Zs.shape[1] < csr.n_cols or \
@@ -841,7 +842,7 @@ def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act):
         raise ValueError("gnnea.highway_sliced: shape mismatch")
     out = torch.empty((N, D), dtype=torch.float32, device=Zs.device)
     S = torch.empty_like(out)
-    G = torch.empty_like(out)
+    G = torch.empty_like(out) if save_g else None
     bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
     L = _lib.lib()
     with _lib.on_device(Zs.device):
@@ -850,8 +851,27 @@ def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act):
                 _off32(csr.rowptr, r0), ptr(csr.col), ptr(csr.val), r1 - r0, D, ptr(Zs),
                 Zs.stride(0), ctypes.c_void_p(Zs.data_ptr() + 4 * r0 * SLICE_W), Zs.stride(0),
                 D, ptr(bias), _off(resid, r0), resid.stride(0), _off(out, r0), out.stride(0),
-                _off(S, r0), _off(G, r0), S.stride(0), int(act), stream_of(Zs.device)))
+                _off(S, r0), _off(G, r0) if save_g else None, S.stride(0), int(act),
+                stream_of(Zs.device)))
     return out, S, G
+
+
+def highway_bwd_sliced_zg(dy, S, Zs, D, bias_gate, resid, act, want_dresid, dgate):
+    """highway_bwd_sliced with g = sigmoid(gate_pre + bias_gate) recomputed from the projection
+    table Zs (gate_pre at column D; gnnea_highway_bwd_sliced_zg_f32) instead of a saved G."""
+    S = _featc(S)
+    dy = _featc(dy, S.dtype)
+    resid = _featc(resid, S.dtype)
+    N = S.shape[0]
+    dSs = sliced_empty(N, D, S.device)
+    dres = torch.empty_like(S) if want_dresid else None
+    bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
+    with _lib.on_device(S.device):
+        check(_lib.lib().gnnea_highway_bwd_sliced_zg_f32(
+            ptr(dy), ptr(S), ptr(Zs), Zs.stride(0), D, ptr(bias), ptr(resid), S.stride(0), N, D,
+            ptr(dSs), dSs.stride(0), ptr(dgate), _ld(dgate), ptr(dres),
+            _ld(dres) if want_dresid else D, int(act), stream_of(S.device)))
+    return dSs, dres
 
 
 def highway_bwd_sliced(dy, S, G, resid, act, want_dresid, dgate):
@@ -929,9 +949,12 @@ class HighwayLayerFn(torch.autograd.Function):
         ctx.sliced = agg.sliced_ok(D, x.dtype)
         if ctx.sliced:
             # above the Infinity Cache: Z written slice-major by the GEMM, the HighWay SpMM
-            # gathers the hidden slices and reads gate_pre from the same table at offset D
+            # gathers the hidden slices and reads gate_pre from the same table at offset D; the
+            # gate itself is not stored: the backward recomputes it from Z (kept alive instead)
             Zs = gemm_sliced(x, wcat.t(), bcat)
-            out, S, G = agg.highway_fwd_sliced(Zs, D, x, bias_gate, act)
+            out, S, _ = agg.highway_fwd_sliced(Zs, D, x, bias_gate, act)
+            G = Zs
+            ctx.bias_gate = bias_gate
         else:
             Z = gemm(x, wcat, bias=bcat)
             out, S, G = agg.highway_fwd(Z[:, :D], Z[:, D:], x, bias_gate, act)
@@ -945,8 +968,9 @@ class HighwayLayerFn(torch.autograd.Function):
         N, D = S.shape
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         P = torch.empty((N, 2 * D), dtype=S.dtype, device=S.device)
-        if ctx.sliced:
-            dSs, dres = highway_bwd_sliced(dy, S, G, x, ctx.act, need_x, P[:, D:])
+        if ctx.sliced:  # (G is the projection table Zs here)
+            dSs, dres = highway_bwd_sliced_zg(dy, S, G, D, ctx.bias_gate, x, ctx.act, need_x,
+                                              P[:, D:])
             ctx.agg.aggregate_t_sliced(dSs, D, P[:, :D])
         else:
             dS, _, dres = highway_bwd(dy, S, G, x, ctx.act, want_dresid=need_x, dgate=P[:, D:])
@@ -981,7 +1005,7 @@ class LocalAgg:
         return dtype == torch.float32 and use_sliced(self.csr.n_cols, D, dtype)
 
     def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act):
-        return highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act)
+        return highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act, save_g=False)
 
     def aggregate_t_sliced(self, gs, D, out):
         return spmm_sliced(self.csr.transpose(), gs, D, out=out)
@@ -1043,14 +1067,14 @@ def _pad4(t, D, dtype=None):
     return out
 
 
-# tests switch it off to compare with the row-major edge pass (GNNEA_GAT_SLICED=0: A/B timing)
-GAT_SLICED = os.environ.get("GNNEA_GAT_SLICED", "1") != "0"
+# tests switch it off (monkeypatch) to compare with the row-major edge pass
+GAT_SLICED = True
 # bf16 storage (cfg-5): the sliced passes are built and parity-tested but not the default.  At
 # cfg-5 (2 x 2M rows, 84M edges) the passes are bound by per-edge work, not by gathered bytes:
 # five 128-B slice passes cost five times the per-edge overhead of one 600-B row-major pass
 # (per KG: forward 6.4 ms sliced + 1.3 ms row statistics vs 6.3 ms row-major; source pass 8.7
 # vs 10.8 ms but the side passes add ~6 ms per layer; GAT-EA step 145 vs 133 ms).
-GAT_SLICED_BF16 = os.environ.get("GNNEA_GAT_SLICED_BF16", "0") != "0"
+GAT_SLICED_BF16 = False
 
 
 def gat_two_heads_per_slice(heads, d_head):

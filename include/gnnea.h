@@ -124,6 +124,15 @@ int gnnea_highway_bwd_sliced_f32(const float* dY, const float* S, const float* G
                                  const float* resid, int64_t ld, int64_t n_rows, int32_t D,
                                  float* dS_s, int64_t sstride, float* dgate, int64_t ld_dg,
                                  float* dresid, int64_t ld_dr, int act, void* stream);
+/* gnnea_highway_bwd_sliced_f32 without a saved gate: g = sigmoid(gate_pre + bias_gate)
+ * recomputed from the slice-major projection table Zs (slice stride zs_stride, gate_pre at
+ * column goff: the forward's gate_s / goff), bit-identical to the forward's g, so the forward
+ * passes save_g = NULL (autograd of layers/layers.py:64-76; 16-B aligned operands, D % 4 == 0) */
+int gnnea_highway_bwd_sliced_zg_f32(const float* dY, const float* S, const float* Zs,
+                                    int64_t zs_stride, int32_t goff, const float* bias_gate,
+                                    const float* resid, int64_t ld, int64_t n_rows, int32_t D,
+                                    float* dS_s, int64_t sstride, float* dgate, int64_t ld_dg,
+                                    float* dresid, int64_t ld_dr, int act, void* stream);
 /* row-major [n, D] (row stride ldx) -> slice-major table (the drop-in path for a row-major
  * hidden that no gnnea GEMM produced) */
 int gnnea_slice_pack_f32(const float* X, int64_t ldx, int64_t n, int32_t D, float* Xs,

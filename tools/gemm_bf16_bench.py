@@ -3,7 +3,6 @@ gnnea.ops.gemm vs hipBLASLt (torch.nn.functional.linear); HIP events, median of 
 result checked against an fp32 product of the same bf16 operands.
 
     python tools/gemm_bf16_bench.py [--rows 4000000] [--reps 10]
-(GNNEA_BF16_EPI=0 selects the per-element epilogue stores, for comparison.)
 """
 import argparse
 import json
@@ -54,9 +53,7 @@ def main():
     io = 2 * (M * K + M * D + D * K)
     ms = timeit(lambda: ops.gemm(X, W, trans_b=True, bias=b), args.reps)
     if args.only_fwd:
-        print(json.dumps({"rows": M, "K": K, "pipe": os.environ.get("GNNEA_BF16_PIPE", "1"),
-                          "wres": os.environ.get("GNNEA_BF16_WRES", "1"),
-                          "mode": os.environ.get("GNNEA_BF16P_MODE", "0"),
+        print(json.dumps({"rows": M, "K": K, "wres": os.environ.get("GNNEA_BF16_WRES", "1"),
                           "gnnea_ms": round(ms, 4), "gnnea_GBps_io": round(io / ms / 1e6, 1),
                           "max_rel_err_vs_fp32": err}))
         return
@@ -72,7 +69,6 @@ def main():
     ms_x = timeit(lambda: ops.gemm(dY, W), args.reps)
     del dW
     print(json.dumps({"rows": M, "wres": os.environ.get("GNNEA_BF16_WRES", "1"),
-                      "pipe": os.environ.get("GNNEA_BF16_PIPE", "1"),
                       "dW_ms": round(ms_w, 4), "dW_hipblaslt_ms": round(ms_wt, 4),
                       "dW_max_rel_err_vs_fp32": errw, "dX_ms": round(ms_x, 4),
                       "gnnea_ms": round(ms, 4), "gnnea_GBps_io": round(io / ms / 1e6, 1),

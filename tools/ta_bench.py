@@ -1,6 +1,5 @@
 """Weight-gradient GEMM dW = Aᵀ·B at the EA-step shapes (gemm_ta.hip): fp32 2M x 300 x 300
 (cfg-4) and bf16 4M x 300 x 300 (cfg-5); HIP events, median of reps, error vs fp64.
-Run once per kernel choice (GNNEA_TA_X3D=0 selects k_gemm_ta<float> for fp32).
 
     python tools/ta_bench.py [--reps 21] [--out gpurun_out/ta_bench.json]
 """
@@ -41,7 +40,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
-    res = {"GNNEA_TA_X3D": os.environ.get("GNNEA_TA_X3D", "1")}
+    res = {}
     for name, K, dt in (("fp32 2M x 300 x 300", 2_000_000, torch.float32),
                         ("bf16 4M x 300 x 300", 4_000_000, torch.bfloat16)):
         a = torch.randn(K, 300, device=dev, generator=g).to(dt)
