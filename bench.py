@@ -294,9 +294,9 @@ def bf16_rate(device, steps):
         del Hs
         # the value is the faster layout's (both reported)
         if ms64 <= ms128:
-            ms, W, kernel = ms64, 64, "gnnea::k_spmm_sliced64_bf16<relu,2,bf16>"
+            ms, W, kernel = ms64, 64, "gnnea::k_spmm_sliced64_bf16<1, 2, unsigned short>"
         else:
-            ms, W, kernel = ms128, 128, "gnnea::k_spmm_sliced<relu,2,false,bf16,bf16,true>"
+            ms, W, kernel = ms128, 128, "gnnea::k_spmm_sliced<1, 2, false, unsigned short, unsigned short>"
     else:
         ms = ms_row
     traffic = gather_model_bytes(shard.n_rows, shard.nnz, D, elem=2)
@@ -777,7 +777,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_bytes, "traffic_source": pmc_src,
-                         "kernel": ("gnnea::k_spmm_sliced<relu,4>" if sliced else
+                         "kernel": ("gnnea::k_spmm_sliced<1, 2, false, float, float>" if sliced else
                                     "gnnea::k_spmm_v4<relu,act,2>"),
                          "launches_per_step": launches,
                          "kernel_ms": round(kernel_ms / launches, 4),

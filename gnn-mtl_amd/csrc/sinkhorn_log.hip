@@ -905,6 +905,28 @@ __device__ __forceinline__ double exp2x(double x, const double* __restrict__ tab
   return __builtin_ldexp(__builtin_fma(tj, p, tj), ti >> 11);
 }
 
+// exp2x in two halves, so that a group of elements issues its table reads together and the reads'
+// LDS latency runs under the group's polynomials (one element at a time, each read was waited
+// for three instructions after its issue)
+struct Exp2Part {
+  double r;  // x - rint(x)
+  int ti;    // rint(x) (saturated for a masked term)
+};
+__device__ __forceinline__ Exp2Part exp2x_split(double x) {
+  const double t = __builtin_rint(x);
+  return Exp2Part{x - t, (int)t};
+}
+__device__ __forceinline__ double exp2x_finish(const Exp2Part& q, double tj) {
+  constexpr double c1 = 0.0003384507717577858, c2 = 5.72744624517204e-08,
+                   c3 = 6.461528672932365e-12;  // (ln2/2048)^k / k!
+  double p = __builtin_fma(q.r, c3, c2);
+  p = __builtin_fma(p, q.r, c1);
+  p *= q.r;
+  return __builtin_ldexp(__builtin_fma(tj, p, tj), q.ti >> 11);
+}
+constexpr int kExpGroup = 4;  // B = 15000: 4305-4402 iters/s (8: 4266, 1: 4095;
+                              // profiles/r05_sinkhorn_egrp_ab.json)
+
 // natural-unit logit of K_ij (masked: -inf where exp_f64(-C/reg) underflows, as sk_term)
 __device__ __forceinline__ double lsk_k(double c, double inv_eps) {
   const double k = -c * inv_eps;
@@ -1041,11 +1063,23 @@ __global__ __launch_bounds__(64 * FW) void k_lsk_sweep(const T* __restrict__ C, 
     // so e_ij = P(u_prev, v_it)_ij needs no running maximum; s_i = u_prev (K v_it)_i
     const double fps = fv * kFScale;
     double rsum = 0.0;
+    // groups of EG elements: logits and table indices, the EG table reads, then the polynomials
+    constexpr int EG = kExpGroup < NCM ? kExpGroup : NCM;
+    static_assert(NCM % EG == 0, "group size");
 #pragma unroll
-    for (int k = 0; k < NCM; ++k) {
-      e[k] = exp2x(logit(kv[k], gl[eo(k)] + fps), tab);
-      rsum += e[k];
-      if (k % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+    for (int k0 = 0; k0 < NCM; k0 += EG) {
+      Exp2Part q[EG];
+      double tj[EG];
+#pragma unroll
+      for (int u = 0; u < EG; ++u) q[u] = exp2x_split(logit(kv[k0 + u], gl[eo(k0 + u)] + fps));
+#pragma unroll
+      for (int u = 0; u < EG; ++u) tj[u] = tab[q[u].ti & (kFTab - 1)];
+#pragma unroll
+      for (int u = 0; u < EG; ++u) {
+        e[k0 + u] = exp2x_finish(q[u], tj[u]);
+        rsum += e[k0 + u];
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     rsum = wave_sum_f64(rsum);
     if (lane == 0) reds[par][w] = rsum;

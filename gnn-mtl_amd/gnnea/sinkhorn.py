@@ -79,6 +79,16 @@ class _StatusPoll:
         return self.buf[:, ST_DONE].clone()
 
 
+def _default_flags():
+    """DEFAULT_FLAGS, plus GNNEA_SK_NO_ONCHIP inside a multi-rank process group: the on-chip
+    solver needs all its workgroups resident at once, which another stream's collective kernels
+    holding CUs can prevent (its bounded waits would then time out before the sweep re-solve)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return DEFAULT_FLAGS | _lib.GNNEA_SK_NO_ONCHIP
+    return DEFAULT_FLAGS
+
+
 def _retry_flags(flags):
     """The re-solve after an on-chip timeout: never on chip (the debug bit is moot there)."""
     return (flags | _lib.GNNEA_SK_NO_ONCHIP) & ~_lib.GNNEA_SK_DEBUG_SPIN
@@ -91,7 +101,7 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
     GNNEA_SK_DEBUG_SPIN).  An on-chip solve whose inter-workgroup wait timed out is solved again
     from the start on the sweep path (same iterates: both paths run the reference's operations);
     the result then carries ``onchip_timeout = True``."""
-    flags = DEFAULT_FLAGS if flags is None else flags
+    flags = _default_flags() if flags is None else flags
     try:
         return _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch,
                       variant, flags)
@@ -188,7 +198,7 @@ def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.fl
     status blocks per round decides which problems continue (solve() polls once per problem
     per round).  Cs [bt, I, J], As [bt, I], Bs [bt, J] on the device; returns SinkhornResults.
     A timed-out on-chip wait re-runs the batch on the sweep path, as solve() does."""
-    flags = DEFAULT_FLAGS if flags is None else flags
+    flags = _default_flags() if flags is None else flags
     try:
         return _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, variant,
                             flags)

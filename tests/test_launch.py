@@ -18,6 +18,12 @@ STUB = r'''
 import json, os, sys, time
 r, w = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 mode = sys.argv[1]
+if mode == "ignore_term":  # a rank that survives SIGTERM (stuck in a collective, say)
+    import signal
+    signal.signal(signal.SIGTERM, signal.SIG_IGN)
+    open(sys.argv[2] + ".%d" % r, "w").write(str(os.getpid()))
+    time.sleep(120)
+    sys.exit(0)
 if mode == "fail" and r == 1:
     sys.exit(7)
 if mode == "fail":
@@ -102,3 +108,47 @@ def test_launched_ranks_rendezvous_gloo(stub, capfd):
     out = capfd.readouterr().out
     line = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][0])
     assert line == {"n_gpus": 2, "sum": 1.0, "addr": "127.0.0.1"}
+
+
+def _alive(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    try:  # a zombie (exited, not yet reaped by its new parent) is not running
+        with open("/proc/%d/stat" % pid) as f:
+            return f.read().split(")")[-1].split()[0] != "Z"
+    except OSError:
+        return False
+
+
+def test_signal_to_parent_kills_ranks_that_ignore_sigterm(stub, tmp_path):
+    """An outer time limit's SIGTERM to the launching process is forwarded to the ranks; ranks
+    still running after the grace period (here: ignoring SIGTERM) are SIGKILLed before the
+    parent exits with 128 + SIGTERM."""
+    import signal
+    marker = str(tmp_path / "pid")
+    code = ("import sys; sys.path.insert(0, %r); from tools import launch; "
+            "sys.exit(launch.spawn(2, %r, ['ignore_term', %r], grace_s=2.0))"
+            % (ROOT, stub, marker))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    parent = subprocess.Popen([sys.executable, "-c", code], cwd=ROOT, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    try:
+        t0 = time.time()
+        while not all(os.path.exists(marker + ".%d" % r) for r in range(2)):
+            assert parent.poll() is None and time.time() - t0 < 60, parent.communicate()
+            time.sleep(0.1)
+        pids = [int(open(marker + ".%d" % r).read()) for r in range(2)]
+        t1 = time.time()
+        parent.send_signal(signal.SIGTERM)
+        rc = parent.wait(timeout=60)
+        assert rc == 128 + signal.SIGTERM, parent.communicate()
+        assert time.time() - t1 < 30  # the grace period, then SIGKILL: not the ranks' 120 s
+        t2 = time.time()
+        while any(_alive(p) for p in pids) and time.time() - t2 < 10:
+            time.sleep(0.1)
+        assert not any(_alive(p) for p in pids), pids
+    finally:
+        if parent.poll() is None:
+            parent.kill()

@@ -51,3 +51,19 @@ def test_problem_struct_carries_flags():
     assert p.flags == 1
     names = [f[0] for f in _lib.SinkhornProblem._fields_]
     assert names[-2:] == ["flags", "ws"]
+
+
+def test_default_flags_skip_onchip_in_a_process_group(monkeypatch):
+    """Inside a multi-rank process group the default flags skip the on-chip solver (its
+    workgroups must all be resident; collective kernels on another stream can hold CUs)."""
+    import torch.distributed as dist
+    assert sinkhorn._default_flags() == sinkhorn.DEFAULT_FLAGS
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_world_size", lambda group=None: 4)
+    assert sinkhorn._default_flags() & _lib.GNNEA_SK_NO_ONCHIP
+    calls = []
+    monkeypatch.setattr(sinkhorn, "_solve", _fake(calls, set()))
+    sinkhorn.solve(0, None, None, None, 0.01, 1e-9, 10)
+    assert calls == [_lib.GNNEA_SK_NO_ONCHIP]
+    monkeypatch.setattr(dist, "get_world_size", lambda group=None: 1)
+    assert sinkhorn._default_flags() == sinkhorn.DEFAULT_FLAGS

@@ -1,6 +1,6 @@
 """Where do the bf16 <-> fp32 casts of the cfg-5 GAT-EA step come from?  Runs a few steps of
-tools/dist_step.measure (GAT, bf16) on a small graph under a TorchFunctionMode that records every
-dtype conversion of a large tensor with the repo frames of its call stack.
+tools/dist_step.measure (GAT, bf16) on a small graph under a TorchDispatchMode that records every
+aten dtype conversion (and fill) of a large tensor with the repo frames of its call stack.
     python tools/dbg/cast_trace.py [entities]"""
 import collections
 import json
@@ -9,40 +9,35 @@ import sys
 import traceback
 
 import torch
+from torch.utils._python_dispatch import TorchDispatchMode
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "gnn-mtl_amd"))
 sys.path.insert(0, ROOT)
 
 SEEN = collections.Counter()
-
-
 ON = [False]
+_CASTS = {"aten._to_copy.default", "aten.copy_.default", "aten.to.dtype", "aten.fill_.Scalar",
+          "aten.zeros_like.default", "aten.zero_.default", "aten.zeros.default"}
 
 
-def _record(src, out):
-    if ON[0] and isinstance(src, torch.Tensor) and isinstance(out, torch.Tensor) and \
-            src.dtype != out.dtype and out.numel() >= 100000 and \
-            {src.dtype, out.dtype} <= {torch.float32, torch.bfloat16}:
-        frames = [f for f in traceback.extract_stack()[:-2] if ROOT in f.filename]
-        key = "%s -> %s %s | %s" % (src.dtype, out.dtype, tuple(out.shape), " < ".join(
-            "%s:%d" % (os.path.relpath(f.filename, ROOT), f.lineno)
-            for f in reversed(frames[-4:])))
-        SEEN[key] += 1
+class Trace(TorchDispatchMode):
+    """Every aten op that changes dtype (or fills) a large tensor, with the repo frames of the
+    Python stack (empty for ops the autograd engine issues from its own thread)."""
 
-
-def _wrap(name):
-    orig = getattr(torch.Tensor, name)
-
-    def f(self, *a, **k):
-        out = orig(self, *a, **k)
-        _record(self, out)
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        out = func(*args, **(kwargs or {}))
+        name = str(func)
+        if ON[0] and name in _CASTS and isinstance(out, torch.Tensor) and out.numel() >= 100000:
+            src = args[1] if name == "aten.copy_.default" else args[0]
+            sd = src.dtype if isinstance(src, torch.Tensor) else None
+            if name.startswith("aten.fill") or name.startswith("aten.zero") or sd != out.dtype:
+                frames = [f for f in traceback.extract_stack()[:-1] if ROOT in f.filename]
+                key = "%s %s -> %s %s | %s" % (name, sd, out.dtype, tuple(out.shape), " < ".join(
+                    "%s:%d" % (os.path.relpath(f.filename, ROOT), f.lineno)
+                    for f in reversed(frames[-4:])))
+                SEEN[key] += 1
         return out
-    setattr(torch.Tensor, name, f)
-
-
-for _n in ("to", "float", "bfloat16", "type", "type_as"):
-    _wrap(_n)
 
 
 def main():
@@ -53,7 +48,8 @@ def main():
     measure("GAT", n, 0, 1, dev, 1, 1, torch.bfloat16, attribute=0)  # warm (lazy setup)
     SEEN.clear()
     ON[0] = True
-    measure("GAT", n, 0, 1, dev, 1, 1, torch.bfloat16, attribute=0)
+    with Trace():
+        measure("GAT", n, 0, 1, dev, 1, 1, torch.bfloat16, attribute=0)
     ON[0] = False
     for k, v in SEEN.most_common():
         print(json.dumps({"calls": v, "cast": k}))

@@ -59,11 +59,29 @@ def _stop(procs, sig):
                 pass
 
 
-def spawn(nprocs, script, argv, environ=None, poll_s=0.2, log=None):
+def _stop_all(procs, sig, grace_s, poll_s=0.1):
+    """Send ``sig`` to the children still running, wait up to ``grace_s`` for them to exit, then
+    SIGKILL the rest and reap them (a child that ignores or handles SIGTERM cannot outlive it)."""
+    _stop(procs, sig)
+    deadline = time.monotonic() + grace_s
+    while any(p.poll() is None for p in procs) and time.monotonic() < deadline:
+        time.sleep(poll_s)
+    _stop(procs, signal.SIGKILL)
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            pass
+
+
+def spawn(nprocs, script, argv, environ=None, poll_s=0.2, log=None, grace_s=None):
     """Run ``python -u script argv`` as ranks 0..nprocs-1 and wait for all of them.
 
     Returns 0 when every rank exits 0, else the first failing rank's status (128 + signal for a
-    rank killed by a signal)."""
+    rank killed by a signal).  A SIGTERM / SIGINT to this process is forwarded to the ranks; the
+    ones still running ``grace_s`` (default GRACE_S) later are killed, then this process exits
+    with 128 + the signal."""
+    grace_s = GRACE_S if grace_s is None else grace_s
     base = dict(os.environ if environ is None else environ)
     base.setdefault("MASTER_ADDR", "127.0.0.1")
     base["MASTER_PORT"] = str(free_port())
@@ -76,9 +94,11 @@ def spawn(nprocs, script, argv, environ=None, poll_s=0.2, log=None):
     log("launch: %d ranks (pids %s), rendezvous 127.0.0.1:%s"
         % (nprocs, " ".join(str(p.pid) for p in procs), base["MASTER_PORT"]))
 
-    # a SIGTERM / SIGINT to the parent (an outer time limit) goes to the children first
+    # a SIGTERM / SIGINT to the parent (an outer time limit) goes to the children first; any
+    # still running after the grace period are killed before the parent exits
     def forward(signum, _frame):
-        _stop(procs, signum)
+        log("launch: signal %d; stopping the ranks" % signum)
+        _stop_all(procs, signum, grace_s)
         raise SystemExit(128 + signum)
     old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
     first_bad, deadline = None, None
@@ -91,7 +111,7 @@ def spawn(nprocs, script, argv, environ=None, poll_s=0.2, log=None):
                         first_bad = (r, st)
                         log("launch: rank %d exited with %d; stopping the other ranks" % (r, st))
                         _stop(procs, signal.SIGTERM)
-                        deadline = time.monotonic() + GRACE_S
+                        deadline = time.monotonic() + grace_s
                         break
             if all(st is not None for st in states):
                 break
