@@ -24,20 +24,23 @@ struct RowFrag {
   float v[NC][VEC];
 };
 
-template <int VEC, int NC>
-__device__ __forceinline__ void load_row(const float* __restrict__ p, int D, RowFrag<VEC, NC>& r) {
+// (T = bf16_t: the rows' bf16 values widened exactly, so every sum below is the one the fp32
+// kernels compute on the fp32 copy of the same rows)
+template <int VEC, int NC, typename T = float>
+__device__ __forceinline__ void load_row(const T* __restrict__ p, int D, RowFrag<VEC, NC>& r) {
   const int lane = lane_id();
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int d = (c * 64 + lane) * VEC;
     if constexpr (VEC == 4) {
-      const float4 x = d < D ? *(const float4*)(p + d) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 x = d < D ? Vec4<T>::get(*(const typename Vec4<T>::raw*)(p + d))
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
       r.v[c][0] = x.x;
       r.v[c][1] = x.y;
       r.v[c][2] = x.z;
       r.v[c][3] = x.w;
     } else {
-      r.v[c][0] = d < D ? p[d] : 0.f;
+      r.v[c][0] = d < D ? to_f32<T>(p[d]) : 0.f;
     }
   }
 }
@@ -62,13 +65,12 @@ __device__ __forceinline__ float sgn(float x) { return (float)((x > 0.f) - (x < 
 // 2 bits each, the 2-bit two's complement of sgn(x_a - x_b): 01 = +1, 11 = -1, 00 = equal.  The backward reads them instead of
 // re-gathering both rows: sgn(x_r - x_other) is +code at the a-end, -code at the b-end, the exact
 // values the row gather would give (same fp32 operands).
-template <int NC>
-__device__ __forceinline__ float l1_rows_code(const float* __restrict__ a,
-                                              const float* __restrict__ b, int D,
-                                              uint8_t* __restrict__ code) {
+template <int NC, typename T>
+__device__ __forceinline__ float l1_rows_code(const T* __restrict__ a, const T* __restrict__ b,
+                                              int D, uint8_t* __restrict__ code) {
   RowFrag<4, NC> x, y;
-  load_row<4, NC>(a, D, x);
-  load_row<4, NC>(b, D, y);
+  load_row<4, NC, T>(a, D, x);
+  load_row<4, NC, T>(b, D, y);
   const int lane = lane_id();
   float s = 0.f;
 #pragma unroll
@@ -110,8 +112,8 @@ __device__ __forceinline__ float l1_frag(const RowFrag<VEC, NC>& x, const RowFra
   return wave_sum(s);
 }
 
-template <int VEC, int NC, bool CODE = false>
-__global__ __launch_bounds__(256) void k_margin_fwd(const float* __restrict__ out, int64_t ld,
+template <int VEC, int NC, bool CODE = false, typename T = float>
+__global__ __launch_bounds__(256) void k_margin_fwd(const T* __restrict__ out, int64_t ld,
                                                     int D, int t, int k,
                                                     const int64_t* __restrict__ left,
                                                     const int64_t* __restrict__ right,
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(256) void k_margin_fwd(const float* __restrict__ ou
   const int64_t tk = (int64_t)t * k;
   auto l1 = [&](int64_t ra, int64_t rb, int64_t term) {
     if constexpr (CODE)
-      return l1_rows_code<NC>(out + ra * ld, out + rb * ld, D, codes + term * sb);
+      return l1_rows_code<NC, T>(out + ra * ld, out + rb * ld, D, codes + term * sb);
     else
       return l1_rows<VEC, NC>(out + ra * ld, out + rb * ld, D);
   };
@@ -154,8 +156,8 @@ __global__ __launch_bounds__(256) void k_margin_fwd(const float* __restrict__ ou
       const int s = q >= k, j = q - s * k;
       const int64_t e = (int64_t)i * k + j;
       term[u] = s * tk + e;
-      load_row<VEC, NC>(out + (s ? nl2[e] : nl1[e]) * ld, D, xa[u]);
-      load_row<VEC, NC>(out + (s ? nr2[e] : nr1[e]) * ld, D, xb[u]);
+      load_row<VEC, NC, T>(out + (s ? nl2[e] : nl1[e]) * ld, D, xa[u]);
+      load_row<VEC, NC, T>(out + (s ? nr2[e] : nr1[e]) * ld, D, xb[u]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -291,7 +293,7 @@ typedef short short2v __attribute__((ext_vector_type(2)));
 // 256-entry LDS table of its four signs as two packed int16 pairs and accumulated with packed
 // 16-bit multiply-adds (2 instructions per 4 columns instead of 8), flushed into the int32
 // accumulators after every 64-entry batch.  Exact like the int32 path.
-template <int NC, bool PK = false>
+template <int NC, bool PK = false, typename TG = float>
 __global__ __launch_bounds__(256) void k_margin_bwd_code(int D, int64_t M,
                                                          const float* __restrict__ m,
                                                          const uint8_t* __restrict__ codes,
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(256) void k_margin_bwd_code(int D, int64_t M,
                                                          const int4* __restrict__ items,
                                                          int n_items,
                                                          const float* __restrict__ gout,
-                                                         float inv, float* __restrict__ grad,
+                                                         float inv, TG* __restrict__ grad,
                                                          int64_t ldg,
                                                          float* __restrict__ scratch) {
   __shared__ uint2 lut[PK ? 256 : 1];
@@ -387,23 +389,35 @@ __global__ __launch_bounds__(256) void k_margin_bwd_code(int D, int64_t M,
     }
   }
   const float c0 = slot < 0 ? gout[0] * inv : 1.0f;
-  float* dst = slot < 0 ? grad + (int64_t)row * ldg : scratch + (int64_t)slot * D;
+  if (slot < 0) {  // the row's gradient (bf16: rounded once, as torch's cast of the fp32 value)
+    TG* dst = grad + (int64_t)row * ldg;
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    if (!own[c]) continue;
-    const int d = (c * 64 + lane) * 4;
+    for (int c = 0; c < NC; ++c) {
+      if (!own[c]) continue;
+      const int d = (c * 64 + lane) * 4;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) dst[d + e] = c0 * (float)acc[c][e];
+      for (int e = 0; e < 4; ++e) dst[d + e] = from_f32<TG>(c0 * (float)acc[c][e]);
+    }
+  } else {  // a long row's chunk partial (fp32, integer-valued)
+    float* dst = scratch + (int64_t)slot * D;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (!own[c]) continue;
+      const int d = (c * 64 + lane) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[d + e] = c0 * (float)acc[c][e];
+    }
   }
 }
 
 // long rows: grad[row] = c * sum of the row's chunk partials, in slot order (one wave per row)
+template <typename TG = float>
 __global__ __launch_bounds__(256) void k_margin_combine(const int32_t* __restrict__ long_rows,
                                                         const int32_t* __restrict__ long_ptr,
                                                         int n_long, int D,
                                                         const float* __restrict__ scratch,
                                                         const float* __restrict__ gout, float inv,
-                                                        float* __restrict__ grad, int64_t ldg) {
+                                                        TG* __restrict__ grad, int64_t ldg) {
   const int w = blockIdx.x * 4 + wave_id();
   if (w >= n_long) return;
   const int row = long_rows[w], s0 = long_ptr[w], s1 = long_ptr[w + 1];
@@ -411,7 +425,7 @@ __global__ __launch_bounds__(256) void k_margin_combine(const int32_t* __restric
   for (int d = lane_id(); d < D; d += 64) {
     float sum = 0.f;
     for (int sl = s0; sl < s1; ++sl) sum += scratch[(int64_t)sl * D + d];
-    grad[(int64_t)row * ldg + d] = c0 * sum;
+    grad[(int64_t)row * ldg + d] = from_f32<TG>(c0 * sum);
   }
 }
 
@@ -511,30 +525,35 @@ extern "C" int gnnea_margin_bwd_f32(const float* out, int64_t ld, int32_t D, int
   GNNEA_MARGIN_DISPATCH(launch_bwd, a, m, inc_ent, (const int4*)items, n_items, grad_loss, scale,
                         grad, ldg, scratch, s);
   if (n_long > 0)
-    hipLaunchKernelGGL(k_margin_combine, dim3(div_up(n_long, 4)), dim3(256), 0, s, long_rows,
+    hipLaunchKernelGGL(k_margin_combine<float>, dim3(div_up(n_long, 4)), dim3(256), 0, s, long_rows,
                        long_ptr, n_long, D, scratch, grad_loss, scale, grad, ldg);
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
 
 // ---- sign-code forward / backward (float4 rows: D % 4 == 0, ld % 4 == 0, 16-B aligned out) ----
-extern "C" int gnnea_margin_fwd_code_f32(const float* out, int64_t ld, int32_t D, int32_t t,
-                                         int32_t k, const int64_t* left, const int64_t* right,
-                                         const int64_t* neg_left, const int64_t* neg_right,
-                                         const int64_t* neg2_left, const int64_t* neg2_right,
-                                         float* A, float* h, float* m, void* codes, int64_t sb,
-                                         void* stream) {
-  const MarginArgs a{out, ld, D, t, k, left, right, neg_left, neg_right, neg2_left, neg2_right};
-  if (const int rc = margin_check(a)) return rc;
-  if (a.t == 0) return 0;
-  if (!A || !m || (a.k > 0 && !h) || !codes) return GNNEA_EINVAL;
-  if (D % 4 || ld % 4 || (((uintptr_t)out) & 15) || sb < (D + 3) / 4) return GNNEA_EINVAL;
+// T = bf16_t (cfg-5 storage): the rows read as bf16 and widened exactly, the gradient rounded to
+// bf16 once -- bit-identical to the fp32 kernels on the fp32 copy of the rows followed by a cast
+// of the gradient, without the copy, the cast and the fp32 gradient buffer.
+template <typename T>
+static int margin_fwd_code(const T* out, int64_t ld, int32_t D, int32_t t, int32_t k,
+                           const int64_t* left, const int64_t* right, const int64_t* neg_left,
+                           const int64_t* neg_right, const int64_t* neg2_left,
+                           const int64_t* neg2_right, float* A, float* h, float* m, void* codes,
+                           int64_t sb, void* stream) {
+  if (t < 0 || k < 0 || D < 0 || D > 1024 || ld < D || !out) return GNNEA_EINVAL;
+  if (t > 0 && (!left || !right)) return GNNEA_EINVAL;
+  if (t > 0 && k > 0 && (!neg_left || !neg_right || !neg2_left || !neg2_right)) return GNNEA_EINVAL;
+  if (t == 0) return 0;
+  if (!A || !m || (k > 0 && !h) || !codes) return GNNEA_EINVAL;
+  if (D % 4 || ld % 4 || (((uintptr_t)out) & (4 * sizeof(T) - 1)) || sb < (D + 3) / 4)
+    return GNNEA_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-#define GNNEA_FC(N)                                                                            \
-  case N:                                                                                      \
-    hipLaunchKernelGGL((k_margin_fwd<4, N, true>), dim3(t), dim3(256), 0, s, out, ld, D, t, k, \
-                       left, right, neg_left, neg_right, neg2_left, neg2_right, A, h, m,       \
-                       (uint8_t*)codes, sb);                                                   \
+#define GNNEA_FC(N)                                                                               \
+  case N:                                                                                         \
+    hipLaunchKernelGGL((k_margin_fwd<4, N, true, T>), dim3(t), dim3(256), 0, s, out, ld, D, t, k, \
+                       left, right, neg_left, neg_right, neg2_left, neg2_right, A, h, m,          \
+                       (uint8_t*)codes, sb);                                                      \
     break;
   switch (div_up(D, 256)) {
     GNNEA_FC(1)
@@ -548,12 +567,12 @@ extern "C" int gnnea_margin_fwd_code_f32(const float* out, int64_t ld, int32_t D
   return 0;
 }
 
-extern "C" int gnnea_margin_bwd_code_f32(int32_t D, int32_t t, int32_t k, const float* m,
-                                         const void* codes, int64_t sb, const int32_t* inc_ent,
-                                         const int32_t* items, int32_t n_items,
-                                         const int32_t* long_rows, const int32_t* long_ptr,
-                                         int32_t n_long, float* scratch, const float* grad_loss,
-                                         float scale, float* grad, int64_t ldg, void* stream) {
+template <typename TG>
+static int margin_bwd_code(int32_t D, int32_t t, int32_t k, const float* m, const void* codes,
+                           int64_t sb, const int32_t* inc_ent, const int32_t* items,
+                           int32_t n_items, const int32_t* long_rows, const int32_t* long_ptr,
+                           int32_t n_long, float* scratch, const float* grad_loss, float scale,
+                           TG* grad, int64_t ldg, void* stream) {
   if (n_items < 0 || n_long < 0 || D < 0 || D > 1024 || D % 4 || t < 0 || k < 0)
     return GNNEA_EINVAL;
   if (n_items == 0) return 0;
@@ -564,16 +583,16 @@ extern "C" int gnnea_margin_bwd_code_f32(int32_t D, int32_t t, int32_t k, const 
   const int64_t M = 2ll * t * k + t;
   // packed 16-bit accumulation needs 64 * max|m_j| = 64 * 2k < 2^15
   const bool pk = k <= 255;
-#define GNNEA_BC(N)                                                                             \
-  case N:                                                                                       \
-    if (pk)                                                                                     \
-      hipLaunchKernelGGL((k_margin_bwd_code<N, true>), dim3(div_up(n_items, 4)), dim3(256), 0,  \
-                         s, D, M, m, (const uint8_t*)codes, sb, inc_ent, (const int4*)items,    \
-                         n_items, grad_loss, scale, grad, ldg, scratch);                        \
-    else                                                                                        \
-      hipLaunchKernelGGL((k_margin_bwd_code<N, false>), dim3(div_up(n_items, 4)), dim3(256), 0, \
-                         s, D, M, m, (const uint8_t*)codes, sb, inc_ent, (const int4*)items,    \
-                         n_items, grad_loss, scale, grad, ldg, scratch);                        \
+#define GNNEA_BC(N)                                                                               \
+  case N:                                                                                         \
+    if (pk)                                                                                       \
+      hipLaunchKernelGGL((k_margin_bwd_code<N, true, TG>), dim3(div_up(n_items, 4)), dim3(256),   \
+                         0, s, D, M, m, (const uint8_t*)codes, sb, inc_ent, (const int4*)items,   \
+                         n_items, grad_loss, scale, grad, ldg, scratch);                          \
+    else                                                                                          \
+      hipLaunchKernelGGL((k_margin_bwd_code<N, false, TG>), dim3(div_up(n_items, 4)), dim3(256),  \
+                         0, s, D, M, m, (const uint8_t*)codes, sb, inc_ent, (const int4*)items,   \
+                         n_items, grad_loss, scale, grad, ldg, scratch);                          \
     break;
   switch (div_up(D, 256)) {
     GNNEA_BC(1)
@@ -584,8 +603,49 @@ extern "C" int gnnea_margin_bwd_code_f32(int32_t D, int32_t t, int32_t k, const 
   }
 #undef GNNEA_BC
   if (n_long > 0)
-    hipLaunchKernelGGL(k_margin_combine, dim3(div_up(n_long, 4)), dim3(256), 0, s, long_rows,
+    hipLaunchKernelGGL(k_margin_combine<TG>, dim3(div_up(n_long, 4)), dim3(256), 0, s, long_rows,
                        long_ptr, n_long, D, scratch, grad_loss, scale, grad, ldg);
   GNNEA_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int gnnea_margin_fwd_code_f32(const float* out, int64_t ld, int32_t D, int32_t t,
+                                         int32_t k, const int64_t* left, const int64_t* right,
+                                         const int64_t* neg_left, const int64_t* neg_right,
+                                         const int64_t* neg2_left, const int64_t* neg2_right,
+                                         float* A, float* h, float* m, void* codes, int64_t sb,
+                                         void* stream) {
+  return margin_fwd_code<float>(out, ld, D, t, k, left, right, neg_left, neg_right, neg2_left,
+                                neg2_right, A, h, m, codes, sb, stream);
+}
+
+extern "C" int gnnea_margin_fwd_code_bf16(const void* out, int64_t ld, int32_t D, int32_t t,
+                                          int32_t k, const int64_t* left, const int64_t* right,
+                                          const int64_t* neg_left, const int64_t* neg_right,
+                                          const int64_t* neg2_left, const int64_t* neg2_right,
+                                          float* A, float* h, float* m, void* codes, int64_t sb,
+                                          void* stream) {
+  return margin_fwd_code<bf16_t>((const bf16_t*)out, ld, D, t, k, left, right, neg_left,
+                                 neg_right, neg2_left, neg2_right, A, h, m, codes, sb, stream);
+}
+
+extern "C" int gnnea_margin_bwd_code_f32(int32_t D, int32_t t, int32_t k, const float* m,
+                                         const void* codes, int64_t sb, const int32_t* inc_ent,
+                                         const int32_t* items, int32_t n_items,
+                                         const int32_t* long_rows, const int32_t* long_ptr,
+                                         int32_t n_long, float* scratch, const float* grad_loss,
+                                         float scale, float* grad, int64_t ldg, void* stream) {
+  return margin_bwd_code<float>(D, t, k, m, codes, sb, inc_ent, items, n_items, long_rows,
+                                long_ptr, n_long, scratch, grad_loss, scale, grad, ldg, stream);
+}
+
+extern "C" int gnnea_margin_bwd_code_bf16(int32_t D, int32_t t, int32_t k, const float* m,
+                                          const void* codes, int64_t sb, const int32_t* inc_ent,
+                                          const int32_t* items, int32_t n_items,
+                                          const int32_t* long_rows, const int32_t* long_ptr,
+                                          int32_t n_long, float* scratch, const float* grad_loss,
+                                          float scale, void* grad, int64_t ldg, void* stream) {
+  return margin_bwd_code<bf16_t>(D, t, k, m, codes, sb, inc_ent, items, n_items, long_rows,
+                                 long_ptr, n_long, scratch, grad_loss, scale, (bf16_t*)grad, ldg,
+                                 stream);
 }

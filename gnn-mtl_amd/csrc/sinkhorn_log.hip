@@ -916,6 +916,13 @@ __device__ __forceinline__ Exp2Part exp2x_split(double x) {
   const double t = __builtin_rint(x);
   return Exp2Part{x - t, (int)t};
 }
+__device__ __forceinline__ double exp2x_poly(double r) {  // e^(r ln2/2048) - 1
+  constexpr double c1 = 0.0003384507717577858, c2 = 5.72744624517204e-08,
+                   c3 = 6.461528672932365e-12;
+  double p = __builtin_fma(r, c3, c2);
+  p = __builtin_fma(p, r, c1);
+  return p * r;
+}
 __device__ __forceinline__ double exp2x_finish(const Exp2Part& q, double tj) {
   constexpr double c1 = 0.0003384507717577858, c2 = 5.72744624517204e-08,
                    c3 = 6.461528672932365e-12;  // (ln2/2048)^k / k!
@@ -924,6 +931,9 @@ __device__ __forceinline__ double exp2x_finish(const Exp2Part& q, double tj) {
   p *= q.r;
   return __builtin_ldexp(__builtin_fma(tj, p, tj), q.ti >> 11);
 }
+#ifndef GNNEA_SK_PHASE
+#define GNNEA_SK_PHASE 1
+#endif
 constexpr int kExpGroup = 4;  // B = 15000: 4305-4402 iters/s (8: 4266, 1: 4095;
                               // profiles/r05_sinkhorn_egrp_ab.json)
 
@@ -1066,6 +1076,36 @@ __global__ __launch_bounds__(64 * FW) void k_lsk_sweep(const T* __restrict__ C, 
     // groups of EG elements: logits and table indices, the EG table reads, then the polynomials
     constexpr int EG = kExpGroup < NCM ? kExpGroup : NCM;
     static_assert(NCM % EG == 0, "group size");
+#if GNNEA_SK_PHASE
+    // phased: the group's table reads and the NEXT group's g reads are issued, then the group's
+    // polynomials run under them, then the reads are consumed
+    double gv[EG];
+#pragma unroll
+    for (int u = 0; u < EG; ++u) gv[u] = gl[eo(u)];
+#pragma unroll
+    for (int k0 = 0; k0 < NCM; k0 += EG) {
+      Exp2Part q[EG];
+      double tj[EG], pp[EG];
+#pragma unroll
+      for (int u = 0; u < EG; ++u) q[u] = exp2x_split(logit(kv[k0 + u], gv[u] + fps));
+#pragma unroll
+      for (int u = 0; u < EG; ++u) tj[u] = tab[q[u].ti & (kFTab - 1)];
+      if (k0 + EG < NCM) {
+#pragma unroll
+        for (int u = 0; u < EG; ++u) gv[u] = gl[eo(k0 + EG + u)];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < EG; ++u) pp[u] = exp2x_poly(q[u].r);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < EG; ++u) {
+        e[k0 + u] = __builtin_ldexp(__builtin_fma(tj[u], pp[u], tj[u]), q[u].ti >> 11);
+        rsum += e[k0 + u];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#else
 #pragma unroll
     for (int k0 = 0; k0 < NCM; k0 += EG) {
       Exp2Part q[EG];
@@ -1081,6 +1121,7 @@ __global__ __launch_bounds__(64 * FW) void k_lsk_sweep(const T* __restrict__ C, 
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+#endif
     rsum = wave_sum_f64(rsum);
     if (lane == 0) reds[par][w] = rsum;
     row_barrier();  // double-buffered by row parity: one barrier per row

@@ -285,6 +285,10 @@ SIGNATURES = {
                                                  _p, _p, _p, _p, _p, _i64, _p]),
     "gnnea_margin_bwd_code_f32": (ctypes.c_int, [_i32, _i32, _i32, _p, _p, _i64, _p, _p, _i32, _p,
                                                  _p, _i32, _p, _p, _f32, _p, _i64, _p]),
+    "gnnea_margin_fwd_code_bf16": (ctypes.c_int, [_p, _i64, _i32, _i32, _i32, _p, _p, _p, _p, _p,
+                                                  _p, _p, _p, _p, _p, _i64, _p]),
+    "gnnea_margin_bwd_code_bf16": (ctypes.c_int, [_i32, _i32, _i32, _p, _p, _i64, _p, _p, _i32,
+                                                  _p, _p, _i32, _p, _p, _f32, _p, _i64, _p]),
 }
 
 _LIB = None

@@ -113,8 +113,8 @@ class MarginLossFn(torch.autograd.Function):
     def forward(ctx, outputs, left, right, nl1, nr1, nl2, nr2, t, k):
         _lib.require_device(outputs)
         out = outputs if outputs.stride(-1) == 1 else outputs.contiguous()
-        if out.dtype != torch.float32:
-            raise TypeError("gnnea.margin: outputs must be fp32")
+        if out.dtype not in (torch.float32, torch.bfloat16):
+            raise TypeError("gnnea.margin: outputs must be fp32 or bf16")
         N, D = out.shape
         dev = out.device
         M = 2 * t * k + t
@@ -123,12 +123,16 @@ class MarginLossFn(torch.autograd.Function):
         m = torch.empty(M, dtype=torch.float32, device=dev)
         # float4 rows: the forward also stores 2-bit sign codes per column (D/4 bytes per term,
         # 90 MB at t=4500, k=125, D=300) so the backward reads them instead of both rows
-        use_codes = CODES and D % 4 == 0 and out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0
+        bf = out.dtype == torch.bfloat16
+        use_codes = bf or (CODES and D % 4 == 0 and out.stride(0) % 4 == 0 and
+                           out.data_ptr() % 16 == 0)
         with _lib.on_device(dev):
             if use_codes:
                 sb = D // 4
                 codes = torch.empty(M * sb, dtype=torch.uint8, device=dev)
-                check(_lib.lib().gnnea_margin_fwd_code_f32(
+                fn = _lib.lib().gnnea_margin_fwd_code_bf16 if bf else \
+                    _lib.lib().gnnea_margin_fwd_code_f32
+                check(fn(
                     ptr(out), out.stride(0), D, t, k, ptr(left), ptr(right), ptr(nl1), ptr(nr1),
                     ptr(nl2), ptr(nr2), ptr(A), ptr(h), ptr(m), ptr(codes), sb, stream_of(dev)))
             else:
@@ -146,12 +150,15 @@ class MarginLossFn(torch.autograd.Function):
         t, k = ctx.tk
         N, D = out.shape
         inc = incidence((left, right, nl1, nr1, nl2, nr2), N)
-        grad = torch.zeros((N, D), dtype=torch.float32, device=out.device)
+        # (bf16 rows: the gradient in bf16, each value rounded once from the fp32 sum)
+        grad = torch.zeros((N, D), dtype=out.dtype, device=out.device)
         scratch = torch.empty((max(inc.n_slots, 1), D), dtype=torch.float32, device=out.device)
         g = g.reshape(1).to(torch.float32).contiguous()
         with _lib.on_device(out.device):
             if codes is not None:
-                check(_lib.lib().gnnea_margin_bwd_code_f32(
+                fn = _lib.lib().gnnea_margin_bwd_code_bf16 if out.dtype == torch.bfloat16 else \
+                    _lib.lib().gnnea_margin_bwd_code_f32
+                check(fn(
                     D, t, k, ptr(m), ptr(codes), D // 4, ptr(inc.csr.col), ptr(inc.items),
                     inc.items.shape[0], ptr(inc.long_rows), ptr(inc.long_ptr),
                     inc.long_rows.numel(), ptr(scratch), ptr(g), 1.0 / (2.0 * t * k), ptr(grad),
@@ -203,6 +210,13 @@ def margin_loss(outputs, left, right, neg_left, neg_right, neg2_left, neg2_right
         idx = [_idx_cached(a, outputs.device, outputs.shape[0]) for a in arrays]
     if idx[0].numel() != t or any(a.numel() != t * k for a in idx[2:]):
         raise ValueError("gnnea.margin: index arrays must have t and t*k entries")
-    if outputs.dtype == torch.bfloat16:  # bf16 models (cfg-5): the loss is an fp32 reduction
-        outputs = outputs.float()
+    if outputs.dtype == torch.bfloat16:
+        # bf16 models (cfg-5): the sign-code kernels read the bf16 rows and write a bf16
+        # gradient (the same values as the fp32 kernels on outputs.float() and a cast back);
+        # rows they cannot take (D or the row stride not a multiple of 4, unaligned) go through
+        # that copy
+        o = outputs if outputs.stride(-1) == 1 else outputs.contiguous()
+        D = o.shape[1]
+        if not (D % 4 == 0 and o.stride(0) % 4 == 0 and o.data_ptr() % 8 == 0):
+            outputs = outputs.float()
     return MarginLossFn.apply(outputs, *idx, t, k)

@@ -739,6 +739,21 @@ int gnnea_margin_bwd_code_f32(int32_t D, int32_t t, int32_t k, const float* m, c
                               int32_t n_items, const int32_t* long_rows, const int32_t* long_ptr,
                               int32_t n_long, float* scratch, const float* grad_loss, float scale,
                               float* grad, int64_t ldg, void* stream);
+/* The same two calls over bf16 rows (cfg-5 storage; the reference model converted with
+ * .bfloat16()): out is bf16 [N][ld], the rows widened exactly to fp32, every sum as in the _f32
+ * calls on the fp32 copy of the rows; grad is bf16 [N][ldg], each value rounded once (nearest
+ * even) from the fp32 gradient -- bit-identical to the _f32 calls on out.float() followed by a
+ * cast of their gradient.  out 8-B aligned, ld % 4 == 0. */
+int gnnea_margin_fwd_code_bf16(const void* out, int64_t ld, int32_t D, int32_t t, int32_t k,
+                               const int64_t* left, const int64_t* right,
+                               const int64_t* neg_left, const int64_t* neg_right,
+                               const int64_t* neg2_left, const int64_t* neg2_right, float* A,
+                               float* h, float* m, void* codes, int64_t sb, void* stream);
+int gnnea_margin_bwd_code_bf16(int32_t D, int32_t t, int32_t k, const float* m, const void* codes,
+                               int64_t sb, const int32_t* inc_ent, const int32_t* items,
+                               int32_t n_items, const int32_t* long_rows, const int32_t* long_ptr,
+                               int32_t n_long, float* scratch, const float* grad_loss,
+                               float scale, void* grad, int64_t ldg, void* stream);
 
 #ifdef __cplusplus
 }

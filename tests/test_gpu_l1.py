@@ -218,3 +218,29 @@ def test_margin_sign_codes_match_row_gather(device, N, D, t, k):
     assert out[0][0] == out[1][0]
     assert (out[0][1] == out[1][1]).all()
     assert np.abs(out[0][1]).sum() > 0
+
+
+@pytest.mark.parametrize("N,D,t,k", [(3000, 300, 200, 40), (500, 1024, 30, 9), (60, 8, 50, 6),
+                                     (40, 64, 300, 30), (80, 300, 4, 300), (300, 37, 40, 5)])
+def test_margin_bf16_rows_match_fp32_copy(device, N, D, t, k):
+    """bf16 embeddings (cfg-5 storage): the sign-code kernels read the bf16 rows and write a bf16
+    gradient.  Loss and gradient are bit-identical to the fp32 kernels on out.float() with the
+    gradient cast back (the path without the bf16 kernels): hub rows (chunked items, k > 255 on
+    the int32 path), tied columns; D = 37 takes the fp32-copy fallback."""
+    from gnnea.margin import margin_loss
+    rng = np.random.default_rng(N + D + k)
+    vec = torch.from_numpy((0.05 * rng.standard_normal((N, D))).astype(np.float32))
+    vec[1] = vec[0]  # a tied pair: code 00 in every column
+    xb = vec.to(device).bfloat16()
+    idx = [rng.integers(0, N, t), rng.integers(0, N, t)] + \
+        [rng.integers(0, 20 if i % 2 == 0 else N, t * k) for i in range(4)]  # hub rows
+    idx[0][0], idx[1][0] = 0, 1
+    x1 = xb.clone().requires_grad_(True)
+    l1 = margin_loss(x1, *idx, t, k)
+    l1.backward()
+    x2 = xb.clone().requires_grad_(True)
+    l2 = margin_loss(x2.float(), *idx, t, k)
+    l2.backward()
+    assert x1.grad.dtype == torch.bfloat16
+    assert float(l1) == float(l2)
+    assert torch.equal(x1.grad, x2.grad)

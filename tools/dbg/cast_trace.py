@@ -18,7 +18,9 @@ sys.path.insert(0, ROOT)
 SEEN = collections.Counter()
 ON = [False]
 _CASTS = {"aten._to_copy.default", "aten.copy_.default", "aten.to.dtype", "aten.fill_.Scalar",
-          "aten.zeros_like.default", "aten.zero_.default", "aten.zeros.default"}
+          "aten.zeros_like.default", "aten.zero_.default", "aten.zeros.default",
+          "aten.add.Tensor", "aten.add_.Tensor", "aten.new_zeros.default",
+          "aten.empty_like.default", "aten.fill_.Tensor"}
 
 
 class Trace(TorchDispatchMode):
@@ -31,7 +33,8 @@ class Trace(TorchDispatchMode):
         if ON[0] and name in _CASTS and isinstance(out, torch.Tensor) and out.numel() >= 100000:
             src = args[1] if name == "aten.copy_.default" else args[0]
             sd = src.dtype if isinstance(src, torch.Tensor) else None
-            if name.startswith("aten.fill") or name.startswith("aten.zero") or sd != out.dtype:
+            if name.startswith("aten.fill") or name.startswith("aten.zero") or \
+                    name.startswith("aten.add") or name.startswith("aten.new_zeros") or sd != out.dtype:
                 frames = [f for f in traceback.extract_stack()[:-1] if ROOT in f.filename]
                 key = "%s %s -> %s %s | %s" % (name, sd, out.dtype, tuple(out.shape), " < ".join(
                     "%s:%d" % (os.path.relpath(f.filename, ROOT), f.lineno)
@@ -48,7 +51,8 @@ def main():
     measure("GAT", n, 0, 1, dev, 1, 1, torch.bfloat16, attribute=0)  # warm (lazy setup)
     SEEN.clear()
     ON[0] = True
-    with Trace():
+    # the backward on this thread (the autograd engine's device threads do not see the mode)
+    with torch.autograd.set_multithreading_enabled(False), Trace():
         measure("GAT", n, 0, 1, dev, 1, 1, torch.bfloat16, attribute=0)
     ON[0] = False
     for k, v in SEEN.most_common():

@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--entities", type=int, default=synth.CONFIGS["cfg4"]["n"])
     ap.add_argument("--dtype", default="f32", choices=("f32", "bf16"),
                     help="feature / weight storage (bf16: configs[4]'s dtype, fp32 arithmetic)")
+    ap.add_argument("--attribute", type=int, default=3,
+                    help="steps run after the timed ones with HIP events around every launch "
+                         "(the per-class kernel times); 0 for profiler runs")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -66,7 +69,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(
             seconds=float(os.environ.get("GNNEA_PG_TIMEOUT_S", "300"))))
     res = measure(args.model, args.entities, rank, world, dev, args.steps, args.warmup,
-                  torch.bfloat16 if args.dtype == "bf16" else torch.float32)
+                  torch.bfloat16 if args.dtype == "bf16" else torch.float32,
+                  attribute=args.attribute)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -112,7 +116,7 @@ def measure(model, n, rank, world, dev, steps, warmup, dtype=torch.float32, attr
         from gnnea.margin import margin_loss
 
         def loss_of(out):
-            return margin_loss(out.float() if out.dtype != torch.float32 else out, *idx, t_, k_)
+            return margin_loss(out, *idx, t_, k_)  # (bf16 rows read as bf16)
     ar = []
 
     def step(ar_events=False):
