@@ -859,9 +859,8 @@ def main():
     # deterministic teardown: the package's cached buffers and torch's cached device / pinned
     # blocks go back to the runtime now, not from the C-level exit handlers
     del shard, h_local, y
-    if os.environ.get("GNNEA_EXIT_CLEANUP", "1") != "0":
-        import gnnea
-        gnnea.release()
+    import gnnea
+    gnnea.release()
 
 
 def _dump_maps_at_exit(path):

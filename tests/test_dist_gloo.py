@@ -151,12 +151,13 @@ def test_partition_covers_every_row_once():
         Partition(1000, 0, 3)
 
 
-def _relay_worker(rank, world, port, rows, q):
+def _relay_worker(rank, world, port, rows, q, mode="relay"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "gnn-mtl_amd"))
     from gnnea import exchange
     from gnnea.dist import Partition, make_groups
+    exchange.MODE = mode
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -164,7 +165,7 @@ def _relay_worker(rank, world, port, rows, q):
         part = Partition(world // 2 * rows, rank, world, "rows", 3)
         group = make_groups(part)
         ranks = part.group_ranks(part.kg)
-        assert exchange.relay_applies(ranks, part.other_ranks())
+        assert exchange.relay_applies(ranks, part.other_ranks()) == (mode == "relay")
         h = torch.arange(rows * 3, dtype=torch.float64).reshape(rows, 3) + 1000 * rank
         full = torch.full((world // 2 * rows, 3), -1.0, dtype=torch.float64)
         exchange.all_gather(h, full, group, ranks, part.li, copy_own=True,
@@ -185,15 +186,18 @@ def _relay_worker(rank, world, port, rows, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("mode", ["relay", "p2p"])
 @pytest.mark.parametrize("world,rows", [(4, 1), (4, 7), (4, 100), (8, 5), (8, 77)])
-def test_relay_exchange(world, rows):
+def test_relay_exchange(world, rows, mode):
     """The two-phase relays (units direct and through the other group's GPUs) deliver exactly
     every group peer's block (all-gather) and the group sum of the owner's rows (reduce-scatter),
-    for row counts that do not split into equal units."""
+    for row counts that do not split into equal units; GNNEA_HALO=p2p (the direct schedule) the
+    same.  (GNNEA_HALO=ring, RCCL's all_gather_into_tensor / reduce_scatter_tensor, has no gloo
+    form: on gloo the p2p schedule runs.)"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_relay_worker, args=(r, world, port, rows, q))
+    procs = [ctx.Process(target=_relay_worker, args=(r, world, port, rows, q, mode))
              for r in range(world)]
     for p in procs:
         p.start()
