@@ -149,6 +149,15 @@ __device__ __forceinline__ float4 f4_fma(float a, float4 x, float4 acc) {
   return acc;
 }
 
+// The HighWay gate g = sigmoid(gate_pre + b) (layers/layers.py:71): the hardware exponential and
+// reciprocal (v_exp_f32 of x log2 e, v_rcp_f32; a few ulp, ~1e-6 relative at |x| ~ 10) instead of
+// the library expf and an IEEE division (about 25 instructions per element, which made the
+// backward that recomputes g slower than reading a stored one).  Every kernel that forms the
+// gate calls this one function, so a forward's and a backward's g are the same bits.
+__device__ __forceinline__ float gate_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
+
 // bf16 storage (cfg-5): 16-bit brain floats carried as uint16_t, arithmetic in fp32.
 // f32 -> bf16 rounds to nearest even with NaN -> 0x7fc0, bit-identical to c10::BFloat16.
 typedef uint16_t bf16_t;

@@ -40,7 +40,7 @@ __device__ __forceinline__ float4 act4(float4 v) {
   return make_float4(act_fwd<ACT>(v.x), act_fwd<ACT>(v.y), act_fwd<ACT>(v.z), act_fwd<ACT>(v.w));
 }
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float sigm(float x) { return gate_sigmoid(x); }
 
 template <int ACT, int EPI, int NCH, typename TX, typename TY>
 __global__ __launch_bounds__(256) void k_spmm_v4(const int32_t* __restrict__ rowptr,
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(256) void k_highway_bwd_zg(
       float ds[4], dg[4], dr[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float g = 1.f / (1.f + expf(-gp4[e]));  // as sigm_f in the forward epilogue
+        const float g = gate_sigmoid(gp4[e]);  // as sigm_f in the forward epilogue
         ds[e] = dyv[e] * g * act_grad_from_out<ACT>(s4[e]);
         dg[e] = dyv[e] * (s4[e] - x4[e]) * g * (1.f - g);
         dr[e] = dyv[e] * (1.f - g);

@@ -46,7 +46,7 @@ struct SlicedHighway {
   int64_t lds;
 };
 
-__device__ __forceinline__ float sigm_f(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float sigm_f(float x) { return gate_sigmoid(x); }
 
 // The gathers of a row are issued unconditionally (edges past the chunk re-read its last edge's
 // piece with weight 0; lanes past D read their group's first 16 B and discard the sum), in

@@ -523,9 +523,10 @@ class DistAdj:
         return (dtype == torch.float32 and self.local_csr() is not None
                 and use_sliced(self.csr.n_cols, D, dtype))
 
-    def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act):
+    def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act, goff=None):
         from . import ops
-        return ops.highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act, save_g=False)
+        return ops.highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act, save_g=False,
+                                      goff=goff)
 
     def aggregate_t_sliced(self, gs, D, out):
         from . import ops

@@ -830,15 +830,24 @@ class HighwayFn(torch.autograd.Function):
         return dh, dgate, dres, None, None, None
 
 
-def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act, save_g=True):
-    """HighWay tail over the slice-major projection table Zs ([S, N, 64] holding x·[Wᵀ | K_g] +
-    [b | 0]: hidden in columns [0, D), gate_pre in [D, 2D)), per diagonal block
-    (gnnea_spmm_highway_sliced_f32).  Returns (out, S, g), row-major; g is None with
-    ``save_g=False`` (the backward recomputes it from Zs: highway_bwd_sliced_zg)."""
+def gate_offset(D):
+    """First column of gate_pre in the fused HighWay projection table: D rounded up to a whole
+    64-column slice, so that output slice q's gate columns are exactly table slice goff/64 + q
+    (one 256-B piece per row for the aggregation's epilogue and the backward, not two partial
+    ones); the padding columns' weights are zero."""
+    return (D + SLICE_W - 1) // SLICE_W * SLICE_W
+
+
+def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act, save_g=True, goff=None):
+    """HighWay tail over the slice-major projection table Zs ([S, N, 64] holding x·[Wᵀ | 0 | K_g]
+    + [b | 0]: hidden in columns [0, D), gate_pre in [goff, goff + D), goff = D by default), per
+    diagonal block (gnnea_spmm_highway_sliced_f32).  Returns (out, S, g), row-major; g is None
+    with ``save_g=False`` (the backward recomputes it from Zs: highway_bwd_sliced_zg)."""
+    goff = D if goff is None else goff
     resid = _rows(resid, torch.float32)
     N = csr.n_rows
     if Zs.dim() != 3 or Zs.shape[2] != SLICE_W or Zs.shape[1] < csr.n_cols or \
-            Zs.shape[0] * SLICE_W < 2 * D or resid.shape != (N, D):
+            Zs.shape[0] * SLICE_W < goff + D or goff < D or resid.shape != (N, D):
         raise ValueError("gnnea.highway_sliced: shape mismatch")
     out = torch.empty((N, D), dtype=torch.float32, device=Zs.device)
     S = torch.empty_like(out)
@@ -850,15 +859,17 @@ def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act, save_g=True):
             check(L.gnnea_spmm_highway_sliced_f32(
                 _off32(csr.rowptr, r0), ptr(csr.col), ptr(csr.val), r1 - r0, D, ptr(Zs),
                 Zs.stride(0), ctypes.c_void_p(Zs.data_ptr() + 4 * r0 * SLICE_W), Zs.stride(0),
-                D, ptr(bias), _off(resid, r0), resid.stride(0), _off(out, r0), out.stride(0),
+                goff, ptr(bias), _off(resid, r0), resid.stride(0), _off(out, r0), out.stride(0),
                 _off(S, r0), _off(G, r0) if save_g else None, S.stride(0), int(act),
                 stream_of(Zs.device)))
     return out, S, G
 
 
-def highway_bwd_sliced_zg(dy, S, Zs, D, bias_gate, resid, act, want_dresid, dgate):
+def highway_bwd_sliced_zg(dy, S, Zs, D, bias_gate, resid, act, want_dresid, dgate, goff=None):
     """highway_bwd_sliced with g = sigmoid(gate_pre + bias_gate) recomputed from the projection
-    table Zs (gate_pre at column D; gnnea_highway_bwd_sliced_zg_f32) instead of a saved G."""
+    table Zs (gate_pre at column goff, D by default; gnnea_highway_bwd_sliced_zg_f32) instead of
+    a saved G."""
+    goff = D if goff is None else goff
     S = _featc(S)
     dy = _featc(dy, S.dtype)
     resid = _featc(resid, S.dtype)
@@ -868,7 +879,7 @@ def highway_bwd_sliced_zg(dy, S, Zs, D, bias_gate, resid, act, want_dresid, dgat
     bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
     with _lib.on_device(S.device):
         check(_lib.lib().gnnea_highway_bwd_sliced_zg_f32(
-            ptr(dy), ptr(S), ptr(Zs), Zs.stride(0), D, ptr(bias), ptr(resid), S.stride(0), N, D,
+            ptr(dy), ptr(S), ptr(Zs), Zs.stride(0), goff, ptr(bias), ptr(resid), S.stride(0), N, D,
             ptr(dSs), dSs.stride(0), ptr(dgate), _ld(dgate), ptr(dres),
             _ld(dres) if want_dresid else D, int(act), stream_of(S.device)))
     return dSs, dres
@@ -949,12 +960,20 @@ class HighwayLayerFn(torch.autograd.Function):
         ctx.sliced = agg.sliced_ok(D, x.dtype)
         if ctx.sliced:
             # above the Infinity Cache: Z written slice-major by the GEMM, the HighWay SpMM
-            # gathers the hidden slices and reads gate_pre from the same table at offset D; the
-            # gate itself is not stored: the backward recomputes it from Z (kept alive instead)
+            # gathers the hidden slices and reads gate_pre from the same table, starting at the
+            # first whole slice past the hidden columns (gate_offset: zero weight columns in
+            # between); the gate itself is not stored: the backward recomputes it from Z (kept
+            # alive instead)
+            goff = gate_offset(D)
+            if goff != D:
+                pad = torch.zeros((wcat.shape[0], goff - D), dtype=wcat.dtype, device=wcat.device)
+                wcat = torch.cat([wcat[:, :D], pad, wcat[:, D:]], dim=1)
+                if bcat is not None:
+                    bcat = torch.cat([bias, torch.zeros(goff, dtype=bias.dtype, device=bias.device)])
             Zs = gemm_sliced(x, wcat.t(), bcat)
-            out, S, _ = agg.highway_fwd_sliced(Zs, D, x, bias_gate, act)
+            out, S, _ = agg.highway_fwd_sliced(Zs, D, x, bias_gate, act, goff=goff)
             G = Zs
-            ctx.bias_gate = bias_gate
+            ctx.bias_gate, ctx.goff = bias_gate, goff
         else:
             Z = gemm(x, wcat, bias=bcat)
             out, S, G = agg.highway_fwd(Z[:, :D], Z[:, D:], x, bias_gate, act)
@@ -970,7 +989,7 @@ class HighwayLayerFn(torch.autograd.Function):
         P = torch.empty((N, 2 * D), dtype=S.dtype, device=S.device)
         if ctx.sliced:  # (G is the projection table Zs here)
             dSs, dres = highway_bwd_sliced_zg(dy, S, G, D, ctx.bias_gate, x, ctx.act, need_x,
-                                              P[:, D:])
+                                              P[:, D:], goff=ctx.goff)
             ctx.agg.aggregate_t_sliced(dSs, D, P[:, :D])
         else:
             dS, _, dres = highway_bwd(dy, S, G, x, ctx.act, want_dresid=need_x, dgate=P[:, D:])
@@ -1004,8 +1023,9 @@ class LocalAgg:
     def sliced_ok(self, D, dtype):
         return dtype == torch.float32 and use_sliced(self.csr.n_cols, D, dtype)
 
-    def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act):
-        return highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act, save_g=False)
+    def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act, goff=None):
+        return highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act, save_g=False,
+                                  goff=goff)
 
     def aggregate_t_sliced(self, gs, D, out):
         return spmm_sliced(self.csr.transpose(), gs, D, out=out)
