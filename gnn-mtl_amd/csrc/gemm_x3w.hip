@@ -222,6 +222,7 @@ __global__ __launch_bounds__(512) void k_gemm_x3w_ring(int M, int N, int K, int 
   }
 }
 
+
 // ---- k_gemm_f16x2_ring: the same projection through a TWO-way fp16 split, three products ----
 // The x3 forms above spend six bf16 MFMAs per fp32 product (h·l, m·m, l·h, h·m, m·h, h·h).  fp16
 // carries 11 significant bits to bf16's 8, so two fp16 pieces hold 22 bits of an fp32 operand:
@@ -323,12 +324,13 @@ __global__ __launch_bounds__(256) void k_pack_f16x2(const float* __restrict__ B,
   }
 }
 
+
 // KC k-steps of 32 (K in (32 (KC - 1), 32 KC]), NC-column weight tiles.  The k dimension runs in
 // CHUNKS of up to 10 steps, each with its own row scale and accumulators (K = 600: two): a
 // chunk's 20 raw quads are split whole once they have landed, and the next chunk's (this tile's
 // or the next tile's first) are issued into the freed registers, one chunk of MFMAs ahead.
-template <int KC, int NC>
-__global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, int ntn,
+template <int KC, int NC, int CH, int NW>
+__global__ __launch_bounds__(64 * NW) void k_gemm_f16x2_ring(int M, int N, int K, int ntn,
                                                          const float* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ P,
                                                          const float* __restrict__ tinv_g,
@@ -336,10 +338,10 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
                                                          float* __restrict__ C, int64_t ldc,
                                                          int64_t cs, float* __restrict__ C2,
                                                          int64_t cs2, float beta, int relu) {
-  constexpr int NW = 8, BM = 16 * NW, NJ = NC / 16;
-  constexpr int PL = KC * 4 * NC;      // 16-B units per plane of a tile
-  constexpr int NCH = (KC + 9) / 10;   // k-chunks
-  static_assert(NC % 16 == 0 && NCH <= 2, "tile shape");
+  constexpr int BM = 16 * NW, NJ = NC / 16;
+  constexpr int PL = KC * 4 * NC;           // 16-B units per plane of a tile
+  constexpr int NCH = (KC + CH - 1) / CH;   // k-chunks of CH steps
+  static_assert(NC % 16 == 0, "tile shape");
   __shared__ __attribute__((aligned(16))) uint4 wl[2 * PL];
   __shared__ __attribute__((aligned(16))) float bsh[NC];
   __shared__ __attribute__((aligned(16))) float tsh[NC];
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
   const int tm = (M + BM - 1) / BM;
   const int kq = lane >> 4, ml = lane & 15;
   const uint4* wlane = wl + kq * NC + ml;
-  uint4 f[20];
+  uint4 f[2 * CH];
   auto row_ptr = [&](int rt) {
     return A + (int64_t)min(rt * BM + w * 16 + ml, M - 1) * lda;
   };
@@ -368,8 +370,8 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
   // quads past K read the row's first quad (valid) and are zeroed at use
   auto load_chunk = [&](const float* p, const int c) {
 #pragma unroll
-    for (int i = 0; i < 20; ++i) {
-      const int st = 10 * c + i / 2, j = i & 1;
+    for (int i = 0; i < 2 * CH; ++i) {
+      const int st = CH * c + i / 2, j = i & 1;
       if (st < KC - 1) {
         f[i] = *(const uint4*)(p + 4 * kq + 32 * st + 16 * j);
       } else if (st == KC - 1) {
@@ -388,7 +390,7 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
     float4 cv[CAHEAD ? NJ : 1];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const int s0 = 10 * c, ns = KC - s0 < 10 ? KC - s0 : 10;
+      const int s0 = CH * c, ns = KC - s0 < CH ? KC - s0 : CH;
       __builtin_amdgcn_sched_barrier(0);
       if (s0 + ns == KC) {
         const int k = 32 * (KC - 1) + 4 * kq, i = 2 * (KC - 1 - s0);
@@ -419,7 +421,7 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
         er = ec;
       }
       const float sr = f2_pow2(14 - er);
-      uint32_t ah[20][2], al[20][2];
+      uint32_t ah[2 * CH][2], al[2 * CH][2];
 #pragma unroll
       for (int q = 0; q < 2 * ns; ++q) {
         ah[q][0] = f2_split_pair(__builtin_bit_cast(float, f[q].x),
@@ -445,25 +447,44 @@ __global__ __launch_bounds__(512) void k_gemm_f16x2_ring(int M, int N, int K, in
         load_chunk(row_ptr(rt), c + 1);
       else
         load_chunk(row_ptr(rt + nrs < tm ? rt + nrs : rt), 0);
+      // the chunk's (step, column block) blocks in order; with registers to spare (CH <= 5 at
+      // 8 waves) each block's two weight fragments are read two blocks ahead, under the MFMAs of
+      // the blocks before it (read per block, each block waited ~100 cycles for its reads)
+      constexpr bool WPF = CH <= 5 && NW <= 8;
+      uint4 bw[3][2];
+      auto rd = [&](int q, uint4 (&d)[2]) {
+        const uint4* wp = wlane + (s0 + q / NJ) * 4 * NC + 16 * (q % NJ);
+        d[0] = wp[0];
+        d[1] = wp[PL];
+      };
+      if constexpr (WPF) {
+        rd(0, bw[0]);
+        if (ns * NJ > 1) rd(1, bw[1]);
+      }
 #pragma unroll
-      for (int s = 0; s < ns; ++s) {
+      for (int q = 0; q < CH * NJ; ++q) {
+        const int s = q / NJ, jn = q % NJ;
+        if (s >= ns) break;
         const f2_f16x8 xh = __builtin_bit_cast(
             f2_f16x8, make_uint4(ah[2 * s][0], ah[2 * s][1], ah[2 * s + 1][0], ah[2 * s + 1][1]));
         const f2_f16x8 xl = __builtin_bit_cast(
             f2_f16x8, make_uint4(al[2 * s][0], al[2 * s][1], al[2 * s + 1][0], al[2 * s + 1][1]));
-        const uint4* wp = wlane + (s0 + s) * 4 * NC;
-#pragma unroll
-        for (int jn = 0; jn < NJ; ++jn) {
-          // (the weight fragments read per block: reading them one block ahead measured no
-          // faster, 1.89 vs 1.91 ms at 2M x 300 x 300, profiles/r04_gemm_ab_f16x2_v2.json)
-          __builtin_amdgcn_sched_barrier(0);
-          const f2_f16x8 wh = __builtin_bit_cast(f2_f16x8, wp[16 * jn]);
-          const f2_f16x8 wlo = __builtin_bit_cast(f2_f16x8, wp[PL + 16 * jn]);
-          w3_f32x4& cc = acc[jn];
-          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wlo, xh, cc, 0, 0, 0);
-          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, cc, 0, 0, 0);
+        uint4 cur[2];
+        if constexpr (WPF) {
+          if (q + 2 < ns * NJ) rd(q + 2, bw[(q + 2) % 3]);
+          cur[0] = bw[q % 3][0];
+          cur[1] = bw[q % 3][1];
+        } else {
+          rd(q, cur);
         }
+        __builtin_amdgcn_sched_barrier(0);
+        const f2_f16x8 wh = __builtin_bit_cast(f2_f16x8, cur[0]);
+        const f2_f16x8 wlo = __builtin_bit_cast(f2_f16x8, cur[1]);
+        w3_f32x4& cc = acc[jn];
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wlo, xh, cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, cc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -600,15 +621,22 @@ static int f16x2_launch(int trans_b, int64_t M, int64_t N, int64_t K, const floa
   hipLaunchKernelGGL(k_pack_f16x2, dim3(nb), dim3(256), 0, s, B, ldb, trans_b ? 1 : 0, (int)N,
                      (int)K, ntn, kc, nc, (const float*)tsc, (uint16_t*)ws);
   GNNEA_LAUNCH_CHECK();
-  const int grid = ring_grid(ntn, M, 128);
-  if (kc == W3_KC)
-    hipLaunchKernelGGL((k_gemm_f16x2_ring<W3_KC, F2_NC>), dim3(grid), dim3(512), 0, s, (int)M,
-                       (int)N, (int)K, ntn, A, lda, (const uint16_t*)ws, (const float*)tinv, bias,
-                       C, ldc, cs, C2, cs2, beta, relu);
-  else
-    hipLaunchKernelGGL((k_gemm_f16x2_ring<F2_KC_WIDE, F2_NC_WIDE>), dim3(grid), dim3(512), 0, s,
-                       (int)M, (int)N, (int)K, ntn, A, lda, (const uint16_t*)ws,
-                       (const float*)tinv, bias, C, ldc, cs, C2, cs2, beta, relu);
+  // k-chunk of CH steps and NW waves per workgroup (the register budget: 10 x 8 at 256
+  // registers, 5 x 8 with the weight fragments two blocks ahead, 3 x 16 at 128 = four waves per
+  // SIMD).  Measured on one box (profiles/r05_gemm_ring_occupancy_ab.json): x·[Wᵀ|K_g]
+  // (ntn = 6) 3.43 -> 3.26 ms with 3 x 16 (5 x 8: 3.45-3.49), the K = 600 input gradient
+  // 4.94 -> 4.52 with 5 x 8, 2M x 300 x 300 (ntn = 3) 1.74 -> 1.70 with 5 x 8 (3 x 16: 1.78)
+#define GNNEA_F2R(KC_, NC_, CH_, NW_)                                                          \
+  hipLaunchKernelGGL((k_gemm_f16x2_ring<KC_, NC_, CH_, NW_>), dim3(ring_grid(ntn, M, 16 * NW_)), \
+                     dim3(64 * NW_), 0, s, (int)M, (int)N, (int)K, ntn, A, lda,                \
+                     (const uint16_t*)ws, (const float*)tinv, bias, C, ldc, cs, C2, cs2, beta, relu)
+  if (kc == W3_KC) {
+    if (ntn >= 4) GNNEA_F2R(W3_KC, F2_NC, 3, 16);
+    else GNNEA_F2R(W3_KC, F2_NC, 5, 8);
+  } else {
+    GNNEA_F2R(F2_KC_WIDE, F2_NC_WIDE, 5, 8);
+  }
+#undef GNNEA_F2R
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
