@@ -612,23 +612,7 @@ __device__ __forceinline__ float head_w(const float (&wl)[H], int k, int hme) {
 }
 
 template <int H, int EPL, typename T, bool EM, int F>
-#ifndef GNNEA_HG_WPE_FWD  // A/B: waves per SIMD the register budget is set for (0 = compiler's)
-#define GNNEA_HG_WPE_FWD 0
-#endif
-#ifndef GNNEA_HG_WPE_SRC
-#define GNNEA_HG_WPE_SRC 0
-#endif
-#if GNNEA_HG_WPE_FWD
-#define GNNEA_HG_ATTR_FWD __attribute__((amdgpu_waves_per_eu(GNNEA_HG_WPE_FWD)))
-#else
-#define GNNEA_HG_ATTR_FWD
-#endif
-#if GNNEA_HG_WPE_SRC
-#define GNNEA_HG_ATTR_SRC __attribute__((amdgpu_waves_per_eu(GNNEA_HG_WPE_SRC)))
-#else
-#define GNNEA_HG_ATTR_SRC
-#endif
-__global__ __launch_bounds__(256) GNNEA_HG_ATTR_FWD void k_gat_fwd_hg(const int32_t* __restrict__ rowptr,
+__global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ rowptr,
                                                     const int32_t* __restrict__ col, int n_rows,
                                                     const T* __restrict__ Hm, int64_t ldh, int D,
                                                     int dh, const float* __restrict__ s1,
@@ -770,7 +754,7 @@ __global__ __launch_bounds__(256) GNNEA_HG_ATTR_FWD void k_gat_fwd_hg(const int3
 // F edges per group, two groups in flight; per group one grp_sum gives every edge's per-head
 // G_i . H_j; dz = -(alpha (mask da - c_i)) LeakyReLU'(z) lands in the edge's lane.
 template <int H, int EPL, typename T, bool EM, int F>
-__global__ __launch_bounds__(256) GNNEA_HG_ATTR_SRC void k_gat_bwd_src_hg(
+__global__ __launch_bounds__(256) void k_gat_bwd_src_hg(
     const int32_t* __restrict__ rowptrT, const int32_t* __restrict__ colT,
     const int64_t* __restrict__ permT, int n_rows, int dh, const T* __restrict__ Hm,
     int64_t ldh, const float* __restrict__ s2, float alpha, const float* __restrict__ emask,

@@ -27,10 +27,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16_b __attribute__((ext_vector_type(16)));
 
 constexpr int HBM = 64, HBK = 32, HLD = HBK + 8;
-#ifndef GNNEA_BF16_TRANS_QUADS
-#define GNNEA_BF16_TRANS_QUADS 1
-#endif
-constexpr bool TRANS_QUADS = GNNEA_BF16_TRANS_QUADS;  // 0: HLoader's 2-B transposing stores
+constexpr bool TRANS_QUADS = true;  // (false: HLoader's 2-B transposing stores, slower)
 
 __device__ __forceinline__ bf16_t u4_elem(const uint4& v, int e) {
   const uint32_t w = e < 2 ? v.x : e < 4 ? v.y : e < 6 ? v.z : v.w;
@@ -839,33 +836,11 @@ static int gemm_bf16p(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
 // while the current tile is multiplied.  Workgroup b owns column tile (b / 8) % ntn and the row
 // stream of the blocks b and b + 8 * (ntn - 1)... (so the column tiles of the same rows run on
 // one XCD, sharing its L2 for the activations).
-// GNNEA_BW_STAGE=1 (A/B builds only) stages a wave's bf16 output tile in LDS and stores 16-B
-// row pieces instead; measured 6-8% SLOWER on the 2M x 300 x 300 projection (0.939 vs 0.887 ms,
-// relu 0.907 vs 0.841 ms; profiles/r04_gemm_bf16_epilogue_ab.json), so the default stores the
-// 8-B pieces straight from the accumulators.
-#ifndef GNNEA_BW_STAGE
-#define GNNEA_BW_STAGE 0
-#endif
-// activation register sets in flight (A/B builds: 2 = one tile ahead, 3 = two tiles ahead;
-// measured equal, 0.887 vs 0.871-0.892 ms)
-#ifndef GNNEA_BW_DEPTH
-#define GNNEA_BW_DEPTH 2
-#endif
-// the k permutation of a lane's fragments (A and W alike): 0 = k-half kh holds k in
-// [kh Kh + 8 s, +8) (a wave-instruction reads 16 B from each of 64 rows' lines), 1 = k in
-// [16 s + 8 kh, +8) (the row's two lanes read 32 contiguous bytes: 32 lines per instruction)
-#ifndef GNNEA_BW_KPERM
-#define GNNEA_BW_KPERM 0
-#endif
-#ifndef GNNEA_BW_NOMFMA
-#define GNNEA_BW_NOMFMA 0
-#endif
-#ifndef GNNEA_BW_NOSTORE
-#define GNNEA_BW_NOSTORE 0
-#endif
+// (Staging a wave's bf16 output tile in LDS to store 16-B row pieces measured 6-8 % slower,
+// profiles/r04_gemm_bf16_epilogue_ab.json; two register sets of activations in flight measured
+// the same as three, and a k permutation reading 32 contiguous bytes per row the same as
+// 16 B from each of 64 rows: none kept.)
 constexpr int kBwCols = 160, kBwKC = 20;  // column tile, max k-steps (K <= 320)
-// a wave's staged bf16 output tile: 32 rows of 320 B, row stride padded by 16 B (bank spread)
-constexpr int kBwStageRS = 2 * kBwCols + 16, kBwStageBytes = 32 * kBwStageRS;
 
 __global__ __launch_bounds__(256) void k_pack_bf16w(const bf16_t* __restrict__ B, int64_t ldb,
                                                     int b_nk, int N, int K, int kc, int ntn,
@@ -882,7 +857,7 @@ __global__ __launch_bounds__(256) void k_pack_bf16w(const bf16_t* __restrict__ B
     r >>= 1;
     const int s = (int)(r % kc);
     const int nt = (int)(r / kc);
-    const int col = nt * kBwCols + n, k = (GNNEA_BW_KPERM ? 16 * s + 8 * kh : kh * 8 * kc + 8 * s) + e;
+    const int col = nt * kBwCols + n, k = kh * 8 * kc + 8 * s + e;
     bf16_t v = 0;
     if (col < N && k < K) v = b_nk ? B[(int64_t)col * ldb + k] : B[(int64_t)k * ldb + col];
     P[t] = v;
@@ -900,10 +875,6 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
   // the tile's bias in LDS: a global load in the epilogue would wait (vmcnt counts in order)
   // for the next tile's activation loads issued before it
   __shared__ __attribute__((aligned(16))) float bsh[kBwCols];
-  // bf16 C: each wave's 32 x 160 output tile staged here, then written as row-contiguous 16-B
-  // pieces (the accumulator layout puts a lane's 8 B in 32 different rows per store instruction)
-  constexpr bool kStage = std::is_same<TC, bf16_t>::value && GNNEA_BW_STAGE;
-  __shared__ __attribute__((aligned(16))) unsigned char stage[kStage ? 4 * kBwStageBytes : 16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int kh = lane >> 5, li = lane & 31;
   const int b = blockIdx.x;
@@ -918,19 +889,13 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
   }
   __syncthreads();
   const int tm = (M + 127) / 128;  // 128-row tiles: 4 waves x 32 rows
-  // one k-step fragment of the lane's row: 8 bf16 at k = kh Kh + 8 s (GNNEA_BW_KPERM: 16 s +
-  // 8 kh).  Only the last steps can reach K (K > 16 (KC - 1)); there a chunk holding K is read
+  // one k-step fragment of the lane's row: 8 bf16 at k = kh Kh + 8 s.  Only the last steps can reach K (K > 16 (KC - 1)); there a chunk holding K is read
   // as the 16 B ending at K (in bounds, K even) and a chunk past K reads the same 16 B; both
   // are fixed up when they are USED (tail_fix: shifted down by words / zeroed).  Fixing them
   // up here, as loads are issued, made the compiler wait vmcnt(0) right after the next tile's
   // loads — the whole tile's load latency exposed every tile (0.89 ms -> see DESIGN §9).
-#if GNNEA_BW_KPERM
-  constexpr int s_tail = KC - 1;
-  auto k0_of = [&](int s) { return 16 * s + 8 * kh; };
-#else
   constexpr int s_tail = KC - 2;
   auto k0_of = [&](int s) { return kh * Kh + 8 * s; };
-#endif
   auto issue = [&](uint4 (&f)[KC], int rt) {
     const bf16_t* row = A + (int64_t)min(rt * 128 + w * 32 + li, M - 1) * lda;
 #pragma unroll
@@ -968,55 +933,16 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
       }
       __builtin_amdgcn_sched_barrier(0);
       const bf16x8 x = __builtin_bit_cast(bf16x8, tail_fix(s, f[s]));
-#if GNNEA_BW_NOMFMA  // timing experiment only: no MFMAs (operands kept live by one add)
-    (void)x;
-#pragma unroll
-      for (int t = 0; t < 5; ++t)
-        acc[t][0] += __builtin_bit_cast(float, wc[t].x ^ wc[t].w ^ f[s].x ^ f[s].y ^ f[s].z ^ f[s].w);
-#else
 #pragma unroll
       for (int t = 0; t < 5; ++t)
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, wc[t]), x,
                                                          acc[t], 0, 0, 0);
-#endif
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < 5; ++t) wc[t] = wn[t];
     }
     // lane: output row m, columns n0 + 32 t + 8 g + 4 kh + (0..3) = acc[t][4 g .. 4 g + 3]
     const int m = rt * 128 + w * 32 + li;
-    if constexpr (kStage) {
-      unsigned char* sw = stage + w * kBwStageBytes;
-#pragma unroll
-      for (int t = 0; t < 5; ++t) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int c = 32 * t + 8 * g + 4 * kh;
-          float4 o = make_float4(acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2],
-                                 acc[t][4 * g + 3]);
-          const float4 bv = *(const float4*)(bsh + c);
-          o.x += bv.x; o.y += bv.y; o.z += bv.z; o.w += bv.w;
-          if (relu) o = f4_relu(o);
-          *(uint2*)(sw + li * kBwStageRS + 2 * c) =
-              make_uint2((uint32_t)f32_to_bf16(o.x) | ((uint32_t)f32_to_bf16(o.y) << 16),
-                         (uint32_t)f32_to_bf16(o.z) | ((uint32_t)f32_to_bf16(o.w) << 16));
-        }
-      }
-      // (the wave's own LDS writes are ordered before its reads; no other wave touches sw)
-      const int r0 = rt * 128 + w * 32;
-#pragma unroll
-      for (int i = 0; i < 10; ++i) {  // 32 rows x 20 pieces of 8 columns: 10 per lane
-        const int q = lane + 64 * i, row = q / 20, pc = q - 20 * row;
-        const int mr = r0 + row, n = n0 + 8 * pc;
-        if (mr < M && n < N) {
-          const uint4 v = *(const uint4*)(sw + row * kBwStageRS + 16 * pc);
-          bf16_t* c = (bf16_t*)C + c_index_bf(mr, n, ldc, cs);
-          if (n + 8 <= N) *(uint4*)c = v;  // (dword-aligned: ldc, cs even)
-          else *(uint2*)c = make_uint2(v.x, v.y);  // N % 4 == 0: the piece's first 4 columns
-        }
-      }
-      return;
-    }
     if (m >= M) return;
 #pragma unroll
     for (int t = 0; t < 5; ++t) {
@@ -1030,9 +956,6 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
           o.x += bv.x; o.y += bv.y; o.z += bv.z; o.w += bv.w;
           if (relu) o = f4_relu(o);  // the Linear's act (layers/layers.py:121-122), uniform
           TC* c = C + c_index_bf(m, n, ldc, cs);
-#if GNNEA_BW_NOSTORE  // timing experiment only: no C traffic
-          if (o.x != 1.2345e-30f) continue;
-#endif
           if constexpr (std::is_same<TC, bf16_t>::value) {
             *(uint2*)c = make_uint2((uint32_t)f32_to_bf16(o.x) | ((uint32_t)f32_to_bf16(o.y) << 16),
                                     (uint32_t)f32_to_bf16(o.z) | ((uint32_t)f32_to_bf16(o.w) << 16));
@@ -1043,28 +966,6 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
       }
     }
   };
-#if GNNEA_BW_DEPTH == 3
-  // three register sets: a tile's activations are issued two tiles ahead of their MFMAs
-  uint4 fa[KC], fb[KC], fc[KC];
-  int rt = rs, r1 = rs + nrs;
-  if (rt < tm) issue(fa, rt);
-  if (r1 < tm) issue(fb, r1);
-  while (rt < tm) {
-    const int r2 = r1 + nrs;
-    if (r2 < tm) issue(fc, r2);
-    compute_store(fa, rt);
-    if (r1 >= tm) break;
-    const int r3 = r2 + nrs;
-    if (r3 < tm) issue(fa, r3);
-    compute_store(fb, r1);
-    if (r2 >= tm) break;
-    const int r4 = r3 + nrs;
-    if (r4 < tm) issue(fb, r4);
-    compute_store(fc, r2);
-    rt = r3;
-    r1 = r4;
-  }
-#else
   // every iteration issues the next tile's loads unconditionally (past the last tile: the last
   // tile again, never used), so that the outstanding-load count at each use is the same on
   // every path through the loop and the compiler's waits cover only the tile being used
@@ -1083,7 +984,6 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
     if (r2 >= tm) break;
     rt = r2;
   }
-#endif
 }
 
 static bool bf16w_applies(int trans_a, int64_t M, int64_t N, int64_t K, int64_t lda,

@@ -931,9 +931,6 @@ __device__ __forceinline__ double exp2x_finish(const Exp2Part& q, double tj) {
   p *= q.r;
   return __builtin_ldexp(__builtin_fma(tj, p, tj), q.ti >> 11);
 }
-#ifndef GNNEA_SK_PHASE
-#define GNNEA_SK_PHASE 1
-#endif
 constexpr int kExpGroup = 4;  // B = 15000: 4305-4402 iters/s (8: 4266, 1: 4095;
                               // profiles/r05_sinkhorn_egrp_ab.json)
 
@@ -1076,7 +1073,6 @@ __global__ __launch_bounds__(64 * FW) void k_lsk_sweep(const T* __restrict__ C, 
     // groups of EG elements: logits and table indices, the EG table reads, then the polynomials
     constexpr int EG = kExpGroup < NCM ? kExpGroup : NCM;
     static_assert(NCM % EG == 0, "group size");
-#if GNNEA_SK_PHASE
     // phased: the group's table reads and the NEXT group's g reads are issued, then the group's
     // polynomials run under them, then the reads are consumed
     double gv[EG];
@@ -1105,23 +1101,6 @@ __global__ __launch_bounds__(64 * FW) void k_lsk_sweep(const T* __restrict__ C, 
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-#else
-#pragma unroll
-    for (int k0 = 0; k0 < NCM; k0 += EG) {
-      Exp2Part q[EG];
-      double tj[EG];
-#pragma unroll
-      for (int u = 0; u < EG; ++u) q[u] = exp2x_split(logit(kv[k0 + u], gl[eo(k0 + u)] + fps));
-#pragma unroll
-      for (int u = 0; u < EG; ++u) tj[u] = tab[q[u].ti & (kFTab - 1)];
-#pragma unroll
-      for (int u = 0; u < EG; ++u) {
-        e[k0 + u] = exp2x_finish(q[u], tj[u]);
-        rsum += e[k0 + u];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#endif
     rsum = wave_sum_f64(rsum);
     if (lane == 0) reds[par][w] = rsum;
     row_barrier();  // double-buffered by row parity: one barrier per row

@@ -272,9 +272,7 @@ constexpr SlicedHighway kNoHighway{nullptr, 0, 0, nullptr, nullptr, 0, nullptr, 
 // unconditionally in double-buffered batches of 8U edges (the PIPE scheme of k_spmm_sliced),
 // fp32 sums, the group partials summed in fixed order (xor 8, 16, 32), group 0 writes the row
 // piece with the activation fused (a last slice ending 4 columns into a lane's 8 stores 4).
-#ifndef GNNEA_S64_U  // edges per group and batch (A/B builds only)
-#define GNNEA_S64_U 2
-#endif
+constexpr int kS64U = 2;  // edges per group and batch
 template <int ACT, int U, typename TY>
 __global__ __launch_bounds__(256) void k_spmm_sliced64_bf16(const int32_t* __restrict__ rowptr,
                                                             const int32_t* __restrict__ col,
@@ -366,7 +364,7 @@ static int spmm_sliced64_bf16(const int32_t* rowptr, const int32_t* col, const f
   if ((int64_t)nbs * S >= (1ll << 31)) return GNNEA_EINVAL;
   const int64_t ss16 = sstride / 8;  // 16-B units
 #define GNNEA_S64(A)                                                                           \
-  hipLaunchKernelGGL((k_spmm_sliced64_bf16<A, GNNEA_S64_U, TY>), dim3(nbs * S), dim3(256), 0, s, rowptr, \
+  hipLaunchKernelGGL((k_spmm_sliced64_bf16<A, kS64U, TY>), dim3(nbs * S), dim3(256), 0, s, rowptr, \
                      col, val, n_rows, nbs, D, (const uint4*)Xs, ss16, Y, ldy)
   switch (act) {
     case GNNEA_ACT_IDENTITY: GNNEA_S64(GNNEA_ACT_IDENTITY); break;
