@@ -364,6 +364,49 @@ __global__ __launch_bounds__(256) void k_highway_bwd_zg(
   }
 }
 
+// The same backward without S: act' from the forward's relu sign mask (ACT relu; identity: 1)
+// and S - x from the output, g (S - x) = out - x, so
+//   dS_pre = dY g act',  dgate = dY (out - x)(1 - g),  dresid = dY (1 - g).
+template <int ACT>
+__global__ __launch_bounds__(256) void k_highway_bwd_zgm(
+    const float* __restrict__ dY, const float* __restrict__ O, const float4* __restrict__ Zs,
+    int64_t zs4, int goff, const float* __restrict__ bias, const float* __restrict__ R, int64_t ld,
+    int64_t n_rows, int D, const uint8_t* __restrict__ mask, int64_t ldm,
+    float* __restrict__ dS_s, int64_t cs_ds, float* __restrict__ dgate, int64_t ld_dg,
+    float* __restrict__ dresid, int64_t ld_dr) {
+  const int lane = lane_id();
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + wave_id(); r < n_rows; r += nw) {
+    for (int c = 4 * lane; c < D; c += 256) {
+      const int64_t i = r * ld + c;
+      const int gc = goff + c;
+      const float4 dy = *(const float4*)(dY + i), ov = *(const float4*)(O + i);
+      const float4 x = *(const float4*)(R + i);
+      float4 gp = Zs[(int64_t)(gc >> 6) * zs4 + r * 16 + ((gc & 63) >> 2)];
+      uint32_t mb = 15u;
+      if constexpr (ACT == GNNEA_ACT_RELU) mb = mask[r * ldm + 16 * (c >> 6) + ((c & 63) >> 2)];
+      if (bias) {
+        const float4 bv = *(const float4*)(bias + c);
+        gp.x += bv.x; gp.y += bv.y; gp.z += bv.z; gp.w += bv.w;
+      }
+      const float dyv[4] = {dy.x, dy.y, dy.z, dy.w}, o4[4] = {ov.x, ov.y, ov.z, ov.w};
+      const float gp4[4] = {gp.x, gp.y, gp.z, gp.w}, x4[4] = {x.x, x.y, x.z, x.w};
+      float ds[4], dg[4], dr[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g = gate_sigmoid(gp4[e]);  // as sigm_f in the forward epilogue
+        ds[e] = ((mb >> e) & 1u) ? dyv[e] * g : 0.f;
+        dg[e] = dyv[e] * (o4[e] - x4[e]) * (1.f - g);
+        dr[e] = dyv[e] * (1.f - g);
+      }
+      *(float4*)(dS_s + (c >> 6) * cs_ds + r * 64 + (c & 63)) = make_float4(ds[0], ds[1], ds[2], ds[3]);
+      *(float4*)(dgate + r * ld_dg + c) = make_float4(dg[0], dg[1], dg[2], dg[3]);
+      if (dresid)
+        *(float4*)(dresid + r * ld_dr + c) = make_float4(dr[0], dr[1], dr[2], dr[3]);
+    }
+  }
+}
+
 template <typename T>
 static int act_bwd_t(const T* dY, const T* Y, T* G, int64_t n, int act, hipStream_t s) {
   if (n < 0) return GNNEA_EINVAL;
@@ -497,6 +540,41 @@ extern "C" int gnnea_highway_bwd_sliced_f32(const float* dY, const float* S, con
   if (sstride == 64) return GNNEA_EINVAL;  // 64 is the row-major code of the kernel
   return highway_bwd_t<float>(dY, S, G, resid, ld, n_rows, D, dS_s, 64, dgate, ld_dg, dresid,
                               ld_dr, act, (hipStream_t)stream, sstride);
+}
+
+// as gnnea_highway_bwd_sliced_zg_f32 without S: the forward's output and (relu) its sign mask
+extern "C" int gnnea_highway_bwd_sliced_zgm_f32(const float* dY, const float* O, const float* Zs,
+                                                int64_t zs_stride, int32_t goff,
+                                                const float* bias_gate, const float* resid,
+                                                int64_t ld, int64_t n_rows, int32_t D,
+                                                const uint8_t* mask, int64_t ldm, float* dS_s,
+                                                int64_t sstride, float* dgate, int64_t ld_dg,
+                                                float* dresid, int64_t ld_dr, int act,
+                                                void* stream) {
+  if (n_rows < 0 || D < 0) return GNNEA_EINVAL;
+  if (n_rows == 0 || D == 0) return 0;
+  if (!dY || !O || !Zs || !resid || !dS_s || !dgate) return GNNEA_EINVAL;
+  if (act != GNNEA_ACT_RELU && act != GNNEA_ACT_IDENTITY) return GNNEA_EINVAL;
+  if (act == GNNEA_ACT_RELU && (!mask || ldm < 16 * ((D + 63) / 64))) return GNNEA_EINVAL;
+  const uintptr_t al = (uintptr_t)dY | (uintptr_t)O | (uintptr_t)Zs | (uintptr_t)resid |
+                       (uintptr_t)dS_s | (uintptr_t)dgate | (uintptr_t)dresid |
+                       (uintptr_t)bias_gate;
+  if (D % 4 || ld % 4 || ld < D || goff < 0 || goff % 4 || zs_stride % 64 ||
+      zs_stride < n_rows * 64 || sstride % 64 || sstride < n_rows * 64 || ld_dg % 4 ||
+      ld_dg < D || (dresid && (ld_dr % 4 || ld_dr < D)) || (al & 15))
+    return GNNEA_EINVAL;
+  const int nbv = (int)((n_rows + 3) / 4 < 16384 ? (n_rows + 3) / 4 : 16384);
+  hipStream_t s = (hipStream_t)stream;
+  if (act == GNNEA_ACT_RELU)
+    hipLaunchKernelGGL((k_highway_bwd_zgm<GNNEA_ACT_RELU>), dim3(nbv), dim3(256), 0, s, dY, O,
+                       (const float4*)Zs, zs_stride / 4, goff, bias_gate, resid, ld, n_rows, D,
+                       mask, ldm, dS_s, sstride, dgate, ld_dg, dresid, ld_dr);
+  else
+    hipLaunchKernelGGL((k_highway_bwd_zgm<GNNEA_ACT_IDENTITY>), dim3(nbv), dim3(256), 0, s, dY,
+                       O, (const float4*)Zs, zs_stride / 4, goff, bias_gate, resid, ld, n_rows, D,
+                       mask, ldm, dS_s, sstride, dgate, ld_dg, dresid, ld_dr);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
 }
 
 // as gnnea_highway_bwd_sliced_f32 with the gate recomputed from the projection table (above)

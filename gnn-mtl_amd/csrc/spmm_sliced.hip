@@ -44,6 +44,11 @@ struct SlicedHighway {
   float* save_s;
   float* save_g;
   int64_t lds;
+  // (relu only) instead of S, its sign: byte [row][16 slice + lane] holds bit q = S > 0 for the
+  // lane's column 4 lane + q of the slice; the backward takes act' from it and S - x from the
+  // output (out - x = g (S - x)), so S itself is never stored
+  uint8_t* save_m = nullptr;
+  int64_t ldm = 0;
 };
 
 __device__ __forceinline__ float sigm_f(float x) { return gate_sigmoid(x); }
@@ -157,6 +162,9 @@ __global__ __launch_bounds__(256) void k_spmm_sliced(const int32_t* __restrict__
       o.w = gt.w * sv.w + (1.f - gt.w) * rr.w;
       *(float4*)(Y + (int64_t)row * ldy + cc) = o;
       if (hw.save_s) *(float4*)(hw.save_s + (int64_t)row * hw.lds + cc) = sv;
+      if (hw.save_m)
+        hw.save_m[(int64_t)row * hw.ldm + 16 * s + c] =
+            (uint8_t)((sv.x > 0.f) | ((sv.y > 0.f) << 1) | ((sv.z > 0.f) << 2) | ((sv.w > 0.f) << 3));
       if (hw.save_g) *(float4*)(hw.save_g + (int64_t)row * hw.lds + cc) = gt;
     }
   }
@@ -402,6 +410,26 @@ extern "C" int gnnea_spmm_highway_sliced_f32(const int32_t* rowptr, const int32_
   if (gsstride % 4) return GNNEA_EINVAL;
   const SlicedHighway hw{(const float4*)gate_s, gsstride / 4, goff, bias_gate, resid, ldr,
                          save_s, save_g, lds};
+  return spmm_sliced<true, float, float>(rowptr, col, val, n_rows, D, Xs, sstride, Y, ldy, act,
+                                         hw, (hipStream_t)stream);
+}
+
+// the fused HighWay layer's forward with the relu sign mask in place of S (SlicedHighway::save_m:
+// [n_rows][ldm] bytes, ldm >= 16 * ceil(D / 64)); act must be relu
+extern "C" int gnnea_spmm_highway_sliced_m_f32(const int32_t* rowptr, const int32_t* col,
+                                               const float* val, int32_t n_rows, int32_t D,
+                                               const float* Xs, int64_t sstride,
+                                               const float* gate_s, int64_t gsstride,
+                                               int32_t goff, const float* bias_gate,
+                                               const float* resid, int64_t ldr, float* Y,
+                                               int64_t ldy, uint8_t* save_m, int64_t ldm, int act,
+                                               void* stream) {
+  if (gsstride % 4 || act != GNNEA_ACT_RELU || !save_m || ldm < 16 * ((D + 63) / 64))
+    return GNNEA_EINVAL;
+  SlicedHighway hw{(const float4*)gate_s, gsstride / 4, goff, bias_gate, resid, ldr,
+                   nullptr, nullptr, 0};
+  hw.save_m = save_m;
+  hw.ldm = ldm;
   return spmm_sliced<true, float, float>(rowptr, col, val, n_rows, D, Xs, sstride, Y, ldy, act,
                                          hw, (hipStream_t)stream);
 }

@@ -96,6 +96,12 @@ SIGNATURES = {
     "gnnea_highway_bwd_sliced_zg_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _p, _p, _i64, _i64,
                                                        _i32, _p, _i64, _p, _i64, _p, _i64,
                                                        ctypes.c_int, _p]),
+    "gnnea_spmm_highway_sliced_m_f32": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p,
+                                                       _i64, _i32, _p, _p, _i64, _p, _i64, _p,
+                                                       _i64, ctypes.c_int, _p]),
+    "gnnea_highway_bwd_sliced_zgm_f32": (ctypes.c_int, [_p, _p, _p, _i64, _i32, _p, _p, _i64,
+                                                        _i64, _i32, _p, _i64, _p, _i64, _p, _i64,
+                                                        _p, _i64, ctypes.c_int, _p]),
     "gnnea_spmm_sliced_bf16": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64,
                                               ctypes.c_int, ctypes.c_int, _p]),
     "gnnea_slice_pack_bf16": (ctypes.c_int, [_p, _i64, _i64, _i32, _p, _i64, _p]),

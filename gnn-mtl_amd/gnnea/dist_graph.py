@@ -523,10 +523,14 @@ class DistAdj:
         return (dtype == torch.float32 and self.local_csr() is not None
                 and use_sliced(self.csr.n_cols, D, dtype))
 
-    def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act, goff=None):
+    def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act, goff=None, save_s=True):
         from . import ops
         return ops.highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act, save_g=False,
-                                      goff=goff)
+                                      goff=goff, save_s=save_s)
+
+    def highway_fwd_sliced_m(self, Zs, D, resid, bias_gate, goff):
+        from . import ops
+        return ops.highway_fwd_sliced_m(self.csr, Zs, D, resid, bias_gate, goff)
 
     def aggregate_t_sliced(self, gs, D, out):
         from . import ops

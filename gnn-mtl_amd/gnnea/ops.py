@@ -838,7 +838,7 @@ def gate_offset(D):
     return (D + SLICE_W - 1) // SLICE_W * SLICE_W
 
 
-def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act, save_g=True, goff=None):
+def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act, save_g=True, goff=None, save_s=True):
     """HighWay tail over the slice-major projection table Zs ([S, N, 64] holding x·[Wᵀ | 0 | K_g]
     + [b | 0]: hidden in columns [0, D), gate_pre in [goff, goff + D), goff = D by default), per
     diagonal block (gnnea_spmm_highway_sliced_f32).  Returns (out, S, g), row-major; g is None
@@ -850,7 +850,7 @@ def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act, save_g=True, goff=None
             Zs.shape[0] * SLICE_W < goff + D or goff < D or resid.shape != (N, D):
         raise ValueError("gnnea.highway_sliced: shape mismatch")
     out = torch.empty((N, D), dtype=torch.float32, device=Zs.device)
-    S = torch.empty_like(out)
+    S = torch.empty_like(out) if save_s else None
     G = torch.empty_like(out) if save_g else None
     bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
     L = _lib.lib()
@@ -860,9 +860,52 @@ def highway_fwd_sliced(csr, Zs, D, resid, bias_gate, act, save_g=True, goff=None
                 _off32(csr.rowptr, r0), ptr(csr.col), ptr(csr.val), r1 - r0, D, ptr(Zs),
                 Zs.stride(0), ctypes.c_void_p(Zs.data_ptr() + 4 * r0 * SLICE_W), Zs.stride(0),
                 goff, ptr(bias), _off(resid, r0), resid.stride(0), _off(out, r0), out.stride(0),
-                _off(S, r0), _off(G, r0) if save_g else None, S.stride(0), int(act),
+                _off(S, r0) if save_s else None, _off(G, r0) if save_g else None, D, int(act),
                 stream_of(Zs.device)))
     return out, S, G
+
+
+def highway_fwd_sliced_m(csr, Zs, D, resid, bias_gate, goff):
+    """highway_fwd_sliced (relu) storing S's sign mask instead of S (gnnea_spmm_highway_sliced_m_f32):
+    returns (out, mask), mask uint8 [N, 16 * ceil(D / 64)]."""
+    resid = _rows(resid, torch.float32)
+    N = csr.n_rows
+    if Zs.dim() != 3 or Zs.shape[2] != SLICE_W or Zs.shape[1] < csr.n_cols or \
+            Zs.shape[0] * SLICE_W < goff + D or goff < D or resid.shape != (N, D):
+        raise ValueError("gnnea.highway_sliced_m: shape mismatch")
+    out = torch.empty((N, D), dtype=torch.float32, device=Zs.device)
+    ldm = 16 * ((D + SLICE_W - 1) // SLICE_W)
+    mask = torch.empty((N, ldm), dtype=torch.uint8, device=Zs.device)
+    bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
+    L = _lib.lib()
+    with _lib.on_device(Zs.device):
+        for r0, r1 in csr.row_blocks():
+            check(L.gnnea_spmm_highway_sliced_m_f32(
+                _off32(csr.rowptr, r0), ptr(csr.col), ptr(csr.val), r1 - r0, D, ptr(Zs),
+                Zs.stride(0), ctypes.c_void_p(Zs.data_ptr() + 4 * r0 * SLICE_W), Zs.stride(0),
+                goff, ptr(bias), _off(resid, r0), resid.stride(0), _off(out, r0), out.stride(0),
+                ctypes.c_void_p(mask.data_ptr() + r0 * ldm), ldm, _lib.GNNEA_ACT_RELU,
+                stream_of(Zs.device)))
+    return out, mask
+
+
+def highway_bwd_sliced_zgm(dy, out, mask, Zs, D, bias_gate, resid, act, want_dresid, dgate, goff):
+    """The fused HighWay layer's backward without S (gnnea_highway_bwd_sliced_zgm_f32): act'
+    from the forward's relu sign mask (None for identity), S - resid from its output."""
+    out = _featc(out)
+    dy = _featc(dy, out.dtype)
+    resid = _featc(resid, out.dtype)
+    N = out.shape[0]
+    dSs = sliced_empty(N, D, out.device)
+    dres = torch.empty_like(out) if want_dresid else None
+    bias = _featc(bias_gate, torch.float32) if bias_gate is not None else None
+    with _lib.on_device(out.device):
+        check(_lib.lib().gnnea_highway_bwd_sliced_zgm_f32(
+            ptr(dy), ptr(out), ptr(Zs), Zs.stride(0), goff, ptr(bias), ptr(resid), out.stride(0),
+            N, D, ptr(mask), mask.stride(0) if mask is not None else 0, ptr(dSs), dSs.stride(0),
+            ptr(dgate), _ld(dgate), ptr(dres), _ld(dres) if want_dresid else D, int(act),
+            stream_of(out.device)))
+    return dSs, dres
 
 
 def highway_bwd_sliced_zg(dy, S, Zs, D, bias_gate, resid, act, want_dresid, dgate, goff=None):
@@ -971,23 +1014,45 @@ class HighwayLayerFn(torch.autograd.Function):
                 if bcat is not None:
                     bcat = torch.cat([bias, torch.zeros(goff, dtype=bias.dtype, device=bias.device)])
             Zs = gemm_sliced(x, wcat.t(), bcat)
-            out, S, _ = agg.highway_fwd_sliced(Zs, D, x, bias_gate, act, goff=goff)
+            # relu / identity: S is not stored either -- the backward takes act' from a sign
+            # mask (relu) and S - x from the output (g (S - x) = out - x)
+            ctx.masked = int(act) in (_lib.GNNEA_ACT_RELU, _lib.GNNEA_ACT_IDENTITY) and \
+                hasattr(agg, "highway_fwd_sliced_m")
+            if ctx.masked and int(act) == _lib.GNNEA_ACT_RELU:
+                out, S = agg.highway_fwd_sliced_m(Zs, D, x, bias_gate, goff)  # S: the mask
+            elif ctx.masked:
+                out, S, _ = agg.highway_fwd_sliced(Zs, D, x, bias_gate, act, goff=goff,
+                                                   save_s=False)  # (S None)
+            else:
+                out, S, _ = agg.highway_fwd_sliced(Zs, D, x, bias_gate, act, goff=goff)
             G = Zs
             ctx.bias_gate, ctx.goff = bias_gate, goff
         else:
             Z = gemm(x, wcat, bias=bcat)
             out, S, G = agg.highway_fwd(Z[:, :D], Z[:, D:], x, bias_gate, act)
         ctx.agg, ctx.act = agg, act
-        ctx.save_for_backward(x, weight, kernel_gate, S, G)
+        if ctx.sliced and ctx.masked:
+            ctx.save_for_backward(x, weight, kernel_gate, S, G, out)
+        else:
+            ctx.save_for_backward(x, weight, kernel_gate, S, G)
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, Kg, S, G = ctx.saved_tensors
-        N, D = S.shape
+        if ctx.sliced and ctx.masked:
+            x, weight, Kg, S, G, out = ctx.saved_tensors  # (S: the relu mask or None)
+        else:
+            x, weight, Kg, S, G = ctx.saved_tensors
+            out = None
+        N, D = x.shape[0], weight.shape[0]
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
-        P = torch.empty((N, 2 * D), dtype=S.dtype, device=S.device)
-        if ctx.sliced:  # (G is the projection table Zs here)
+        pdt = torch.float32 if (ctx.sliced and ctx.masked) else S.dtype
+        P = torch.empty((N, 2 * D), dtype=pdt, device=x.device)
+        if ctx.sliced and ctx.masked:  # (G is the projection table Zs here)
+            dSs, dres = highway_bwd_sliced_zgm(dy, out, S, G, D, ctx.bias_gate, x, ctx.act,
+                                               need_x, P[:, D:], ctx.goff)
+            ctx.agg.aggregate_t_sliced(dSs, D, P[:, :D])
+        elif ctx.sliced:
             dSs, dres = highway_bwd_sliced_zg(dy, S, G, D, ctx.bias_gate, x, ctx.act, need_x,
                                               P[:, D:], goff=ctx.goff)
             ctx.agg.aggregate_t_sliced(dSs, D, P[:, :D])
@@ -1023,9 +1088,12 @@ class LocalAgg:
     def sliced_ok(self, D, dtype):
         return dtype == torch.float32 and use_sliced(self.csr.n_cols, D, dtype)
 
-    def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act, goff=None):
+    def highway_fwd_sliced(self, Zs, D, resid, bias_gate, act, goff=None, save_s=True):
         return highway_fwd_sliced(self.csr, Zs, D, resid, bias_gate, act, save_g=False,
-                                  goff=goff)
+                                  goff=goff, save_s=save_s)
+
+    def highway_fwd_sliced_m(self, Zs, D, resid, bias_gate, goff):
+        return highway_fwd_sliced_m(self.csr, Zs, D, resid, bias_gate, goff)
 
     def aggregate_t_sliced(self, gs, D, out):
         return spmm_sliced(self.csr.transpose(), gs, D, out=out)

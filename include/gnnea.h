@@ -133,6 +133,23 @@ int gnnea_highway_bwd_sliced_zg_f32(const float* dY, const float* S, const float
                                     const float* resid, int64_t ld, int64_t n_rows, int32_t D,
                                     float* dS_s, int64_t sstride, float* dgate, int64_t ld_dg,
                                     float* dresid, int64_t ld_dr, int act, void* stream);
+/* The fused HighWay layer without S (relu only): the forward stores S's sign instead of S
+ * (save_m: [n_rows][ldm] bytes, ldm >= 16 * ceil(D / 64); byte 16 q + l of a row holds bit e =
+ * S[row][64 q + 4 l + e] > 0), and the backward takes act' from that mask (act relu; identity
+ * needs none: mask may be NULL) and S - resid from the forward's output Y (g (S - resid) =
+ * Y - resid): dS_pre = dY g act', dgate = dY (Y - resid)(1 - g), dresid = dY (1 - g). */
+int gnnea_spmm_highway_sliced_m_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                                    int32_t n_rows, int32_t D, const float* Xs, int64_t sstride,
+                                    const float* gate_s, int64_t gsstride, int32_t goff,
+                                    const float* bias_gate, const float* resid, int64_t ldr,
+                                    float* Y, int64_t ldy, uint8_t* save_m, int64_t ldm, int act,
+                                    void* stream);
+int gnnea_highway_bwd_sliced_zgm_f32(const float* dY, const float* Y, const float* Zs,
+                                     int64_t zs_stride, int32_t goff, const float* bias_gate,
+                                     const float* resid, int64_t ld, int64_t n_rows, int32_t D,
+                                     const uint8_t* mask, int64_t ldm, float* dS_s,
+                                     int64_t sstride, float* dgate, int64_t ld_dg, float* dresid,
+                                     int64_t ld_dr, int act, void* stream);
 /* row-major [n, D] (row stride ldx) -> slice-major table (the drop-in path for a row-major
  * hidden that no gnnea GEMM produced) */
 int gnnea_slice_pack_f32(const float* X, int64_t ldx, int64_t n, int32_t D, float* Xs,

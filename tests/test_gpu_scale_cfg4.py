@@ -88,8 +88,14 @@ def test_cfg4_highway_layer_vs_oracle(device, cfg4, relu_band):
     xx = d["x"].clone().requires_grad_(True)
     out, _ = layer((xx, d["adj"]))
     assert type(out.grad_fn).__name__ == "HighwayLayerFnBackward"
-    S_gpu = out.grad_fn.saved_tensors[3]  # relu(A·hidden) as the layer computed it (branch band)
-    assert S_gpu.shape == out.shape
+    # relu's branch as the layer took it (for the rounding band): the forward keeps only the
+    # sign of S = relu(A·hidden), bit (c % 4) of byte [row][16 (c // 64) + (c % 64) // 4]
+    mask = out.grad_fn.saved_tensors[3]
+    assert mask.dtype == torch.uint8 and mask.shape == (out.shape[0], 16 * 5)
+    cols = torch.arange(out.shape[1], device=device)
+    S_gpu = ((mask[:, 16 * (cols // 64) + (cols % 64) // 4] >> (cols % 4).to(torch.uint8)) & 1)
+    S_gpu = S_gpu.to(torch.float32)
+    del mask
     (out * d["R"]).sum().backward()
     W = layer.linear.weight.detach().cpu().double()
     b = layer.linear.bias.detach().cpu().double()

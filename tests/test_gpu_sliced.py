@@ -219,12 +219,17 @@ def test_highway_layer_sliced_matches_rowmajor(device, monkeypatch, act):
         return [out.detach(), xx.grad, layer.linear.weight.grad.clone(),
                 layer.linear.bias.grad.clone()]
     calls = []
-    orig = ops.highway_fwd_sliced
+    orig, orig_m = ops.highway_fwd_sliced, ops.highway_fwd_sliced_m
 
     def spy(*a, **k):
         calls.append(1)
         return orig(*a, **k)
+
+    def spy_m(*a, **k):  # (relu: the sign-mask form, S not stored)
+        calls.append(2)
+        return orig_m(*a, **k)
     monkeypatch.setattr(ops, "highway_fwd_sliced", spy)
+    monkeypatch.setattr(ops, "highway_fwd_sliced_m", spy_m)
     monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 0)  # force the sliced path at test size
     got = run()
     assert calls, "the sliced HighWay layer was not used"
@@ -233,6 +238,44 @@ def test_highway_layer_sliced_matches_rowmajor(device, monkeypatch, act):
     assert len(calls) == 1
     for g, w in zip(got, ref):
         assert rel_err(g.cpu(), w.cpu()) < TOL32
+
+@pytest.mark.parametrize("act", [1, 0])
+def test_highway_layer_fn_sliced_without_s(device, monkeypatch, act):
+    """HighwayLayerFn on the sliced path with relu (code 1: sign mask saved, S not stored) and
+    identity (code 0: nothing but the output) against the torch fp32 formula
+    out = g S + (1 - g) x, S = act(A (x Wᵀ + b)), g = sigmoid(x K_g + b_g): output and the
+    gradients of x (through the gate too), W and b."""
+    from gnnea import _lib, ops
+    rng = np.random.default_rng(11)
+    n, D = 1300, 300
+    r, c, v, csr = _graph(rng, n, 10000, device)
+    A = torch.sparse_coo_tensor(torch.from_numpy(np.stack([r, c]).astype(np.int64)),
+                                torch.from_numpy(v), (n, n)).to(device).coalesce()
+    torch.manual_seed(3)
+    x0 = torch.randn(n, D, device=device) * 0.1
+    W0 = torch.randn(D, D, device=device) * 0.05
+    b0 = torch.randn(D, device=device) * 0.1
+    K0 = torch.randn(D, D, device=device) * 0.05
+    bg = torch.randn(D, device=device) * 0.1
+    R = torch.randn(n, D, device=device)
+    code = _lib.GNNEA_ACT_RELU if act else _lib.GNNEA_ACT_IDENTITY
+    monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 0)
+    agg = ops.LocalAgg(csr)
+    assert agg.sliced_ok(D, torch.float32)
+    leaves = [t.clone().requires_grad_(True) for t in (x0, W0, b0, K0)]
+    out = ops.HighwayLayerFn.apply(leaves[0], leaves[1], leaves[2], leaves[3], bg, agg, code)
+    (out * R).sum().backward()
+    ref_leaves = [t.clone().requires_grad_(True) for t in (x0, W0, b0, K0)]
+    x, W, b, K = ref_leaves
+    S = torch.sparse.mm(A, x @ W.t() + b)
+    S = torch.relu(S) if act else S
+    g = torch.sigmoid(x @ K + bg)
+    ref = g * S + (1.0 - g) * x
+    (ref * R).sum().backward()
+    assert rel_err(out.detach().cpu(), ref.detach().cpu()) < TOL32
+    for got, want in zip(leaves[:3], ref_leaves[:3]):  # (K_g is a constant, as in the reference)
+        assert rel_err(got.grad.cpu(), want.grad.cpu()) < TOL32
+
 
 
 def test_distadj_world1_takes_sliced_layers(device, monkeypatch):
@@ -254,7 +297,7 @@ def test_distadj_world1_takes_sliced_layers(device, monkeypatch):
     x = torch.from_numpy(synth.features(2 * n, 300, seed=4)).to(device)
     Rw = torch.randn(2 * n, 300, device=device)
     used = []
-    for name in ("gemm_sliced", "highway_fwd_sliced"):
+    for name in ("gemm_sliced", "highway_fwd_sliced", "highway_fwd_sliced_m"):
         orig = getattr(ops, name)
         monkeypatch.setattr(ops, name, (lambda f, nm: lambda *a, **k: (used.append(nm),
                                                                         f(*a, **k))[1])(orig, name))
@@ -269,7 +312,7 @@ def test_distadj_world1_takes_sliced_layers(device, monkeypatch):
                                           list(l1.parameters()) + list(l2.parameters())]
     monkeypatch.setattr(ops, "INFINITY_CACHE_BYTES", 0)
     got = run(dadj)
-    assert {"gemm_sliced", "highway_fwd_sliced"} <= set(used)
+    assert "gemm_sliced" in used and {"highway_fwd_sliced", "highway_fwd_sliced_m"} & set(used)
     monkeypatch.setattr(ops, "SLICED", False)
     ref = run(adj)
     for g, w in zip(got, ref):
