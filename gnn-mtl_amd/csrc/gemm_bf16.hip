@@ -864,13 +864,21 @@ __global__ __launch_bounds__(256) void k_pack_bf16w(const bf16_t* __restrict__ B
   }
 }
 
-template <typename TC, int KC>
+// DM (the backward of a relu Linear whose output y fed this product, bf16): the stored value is
+// g = bf16(acc) * relu'(y) at the same position (act_bwd_colsum's g on the product it would read,
+// bit for bit), y read for the tile before the next tile's activations are issued.  (Column sums
+// of g kept per lane across the tiles as well -- 80 more registers -- spilled: the bias gradient
+// is a separate streaming pass over g.)
+template <typename TC, int KC, bool DM = false>
 __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int ntn,
                                                       const bf16_t* __restrict__ A, int64_t lda,
                                                       const bf16_t* __restrict__ P,
                                                       const float* __restrict__ bias,
                                                       TC* __restrict__ C, int64_t ldc,
-                                                      int64_t cs, int relu) {
+                                                      int64_t cs, int relu,
+                                                      const bf16_t* __restrict__ Ym = nullptr,
+                                                      int64_t ldym = 0) {
+  static_assert(!DM || std::is_same<TC, bf16_t>::value, "the masked form stores bf16");
   __shared__ __attribute__((aligned(16))) uint4 wl[KC * 2 * kBwCols];  // [s][kh][n] x 16 B
   // the tile's bias in LDS: a global load in the epilogue would wait (vmcnt counts in order)
   // for the next tile's activation loads issued before it
@@ -916,6 +924,18 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
                       sh == 1 ? v.w : 0u, 0u);
   };
   const uint4* wlane = wl + kh * kBwCols + li;  // + (2 s) * 160 + 32 t
+  // DM: the tile's y pieces (the output positions, clamped in bounds: unconditional loads)
+  uint2 ym[DM ? 20 : 1];
+  auto load_y = [&](int rt) {
+    if constexpr (DM) {
+      const int64_t m = min(rt * 128 + w * 32 + li, M - 1);
+#pragma unroll
+      for (int q = 0; q < 20; ++q) {
+        const int n = min(n0 + 32 * (q >> 2) + 8 * (q & 3) + 4 * kh, N - 4);
+        ym[q] = *(const uint2*)(Ym + m * ldym + n);
+      }
+    }
+  };
   auto compute_store = [&](const uint4 (&f)[KC], int rt) {
     f32x16_b acc[5];
 #pragma unroll
@@ -956,7 +976,23 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
           o.x += bv.x; o.y += bv.y; o.z += bv.z; o.w += bv.w;
           if (relu) o = f4_relu(o);  // the Linear's act (layers/layers.py:121-122), uniform
           TC* c = C + c_index_bf(m, n, ldc, cs);
-          if constexpr (std::is_same<TC, bf16_t>::value) {
+          if constexpr (DM) {
+            // g = bf16(bf16(o) * relu'(y)): the product rounded as stored, then the derivative
+            const uint2 yv = ym[4 * t + g];
+            const float y4[4] = {bf16_to_f32((bf16_t)(yv.x & 0xffffu)),
+                                 bf16_to_f32((bf16_t)(yv.x >> 16)),
+                                 bf16_to_f32((bf16_t)(yv.y & 0xffffu)),
+                                 bf16_to_f32((bf16_t)(yv.y >> 16))};
+            const float o4[4] = {o.x, o.y, o.z, o.w};
+            bf16_t gb[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              gb[e] = f32_to_bf16(bf16_to_f32(f32_to_bf16(o4[e])) *
+                                  act_grad_from_out<GNNEA_ACT_RELU>(y4[e]));
+            }
+            *(uint2*)c = make_uint2((uint32_t)gb[0] | ((uint32_t)gb[1] << 16),
+                                    (uint32_t)gb[2] | ((uint32_t)gb[3] << 16));
+          } else if constexpr (std::is_same<TC, bf16_t>::value) {
             *(uint2*)c = make_uint2((uint32_t)f32_to_bf16(o.x) | ((uint32_t)f32_to_bf16(o.y) << 16),
                                     (uint32_t)f32_to_bf16(o.z) | ((uint32_t)f32_to_bf16(o.w) << 16));
           } else {
@@ -969,16 +1005,20 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
   // every iteration issues the next tile's loads unconditionally (past the last tile: the last
   // tile again, never used), so that the outstanding-load count at each use is the same on
   // every path through the loop and the compiler's waits cover only the tile being used
+  // (DM: the tile's y is loaded before the next tile's activations, so the epilogue's wait for it
+  // does not cover them)
   if (rs >= tm) return;
   uint4 fa[KC], fb[KC];
   int rt = rs;
   issue(fa, rt);
   while (true) {
     const int r1 = rt + nrs;
+    load_y(rt);
     issue(fb, min(r1, tm - 1));
     compute_store(fa, rt);
     if (r1 >= tm) break;
     const int r2 = r1 + nrs;
+    load_y(r1);
     issue(fa, min(r2, tm - 1));
     compute_store(fb, r1);
     if (r2 >= tm) break;
@@ -1035,6 +1075,30 @@ static int gemm_bf16w(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t
   GNNEA_LAUNCH_CHECK();
   return 0;
 }
+
+// the masked backward product (k_gemm_bf16w<bf16, KC, true>): G = bf16(A·op(B)) * relu'(Y);
+// workspace = the weight planes
+static int bf16w_grid(int64_t M, int ntn) {
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  const int unit = 8 * ntn;
+  const int64_t tm = (M + 127) / 128;
+  int grid = ncu / unit * unit;
+  if (grid < unit) grid = unit;
+  if ((int64_t)grid / ntn > tm) grid = (int)((tm + 7) / 8 * 8 * ntn);
+  return grid;
+}
+static bool dmask_applies(int64_t M, int64_t N, int64_t K, int64_t lda, const void* A,
+                          int64_t ldy, const void* Y, int64_t ldg, const void* G) {
+  return bf16w_applies(0, M, N, K, lda, A) && ldy >= N && ldy % 4 == 0 && ldg >= N &&
+         ldg % 4 == 0 && (((uintptr_t)Y | (uintptr_t)G) & 7) == 0;
+}
+static int64_t dmask_ws_bytes(int64_t N, int64_t K) { return bf16w_planes_bytes(N, K); }
 
 template <typename TC>
 static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
@@ -1159,6 +1223,55 @@ extern "C" int gnnea_gemm_bf16_act(int trans_a, int trans_b, int64_t M, int64_t 
                               (const bf16_t*)B, ldb, bias, 0.f, (float*)C, ldc, ws, ws_bytes, s,
                               128, act);
   return GNNEA_EINVAL;
+}
+
+extern "C" int gnnea_gemm_bf16_dmask_applies(int64_t M, int64_t N, int64_t K, int64_t lda,
+                                             int64_t ldy, int64_t ldg) {
+  return M > 0 && M < (1ll << 31) && N < (1ll << 31) && dmask_applies(M, N, K, lda, nullptr, ldy,
+                                                                      nullptr, ldg, nullptr)
+             ? 1 : 0;
+}
+
+extern "C" int64_t gnnea_gemm_bf16_dmask_ws_bytes(int64_t N, int64_t K) {
+  if (N < 0 || K < 0) return GNNEA_EINVAL;
+  return dmask_ws_bytes(N, K);
+}
+
+// The backward of y = relu(x Wᵀ + b) through the product that consumed y (MLPDecoder's relu
+// Linear layers, models/decoders.py; layers/layers.py:121-122): G = bf16(A·op(B)) * relu'(Y),
+// bit-identical to gnnea_gemm_bf16 followed by gnnea_act_bwd_colsum_bf16's G.  Only where the
+// weight-resident kernel applies (gnnea_gemm_bf16_dmask_applies), else GNNEA_EINVAL.
+extern "C" int gnnea_gemm_bf16_dmask(int trans_b, int64_t M, int64_t N, int64_t K, const void* A,
+                                     int64_t lda, const void* B, int64_t ldb, const void* Y,
+                                     int64_t ldy, void* G, int64_t ldg, void* ws,
+                                     int64_t ws_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  if (M == 0 || N == 0) return 0;
+  if (M >= (1ll << 31) || N >= (1ll << 31) || !A || !B || !Y || !G || !ws) return GNNEA_EINVAL;
+  if (trans_b ? ldb < K : ldb < N) return GNNEA_EINVAL;
+  if (!dmask_applies(M, N, K, lda, A, ldy, Y, ldg, G)) return GNNEA_EINVAL;
+  if (ws_bytes < dmask_ws_bytes(N, K)) return GNNEA_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  const int kc = bf16w_kc(K), ntn = (int)((N + kBwCols - 1) / kBwCols);
+  bf16_t* P = (bf16_t*)ws;
+  {
+    const int64_t tot = (int64_t)ntn * kc * 2 * kBwCols * 8;
+    const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
+    hipLaunchKernelGGL(k_pack_bf16w, dim3(nb), dim3(256), 0, s, (const bf16_t*)B, ldb,
+                       trans_b ? 1 : 0, (int)N, (int)K, kc, ntn, P);
+    GNNEA_LAUNCH_CHECK();
+  }
+  const int grid = bf16w_grid(M, ntn);
+  if (kc == 19)
+    hipLaunchKernelGGL((k_gemm_bf16w<bf16_t, 19, true>), dim3(grid), dim3(256), 0, s, (int)M,
+                       (int)N, (int)K, ntn, (const bf16_t*)A, lda, P, nullptr, (bf16_t*)G, ldg,
+                       (int64_t)128, 0, (const bf16_t*)Y, ldy);
+  else
+    hipLaunchKernelGGL((k_gemm_bf16w<bf16_t, 20, true>), dim3(grid), dim3(256), 0, s, (int)M,
+                       (int)N, (int)K, ntn, (const bf16_t*)A, lda, P, nullptr, (bf16_t*)G, ldg,
+                       (int64_t)128, 0, (const bf16_t*)Y, ldy);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
 }
 
 extern "C" int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

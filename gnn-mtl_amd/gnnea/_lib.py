@@ -173,6 +173,10 @@ SIGNATURES = {
                                                 _i64, _p, _p, _i64, _p]),
     "gnnea_act_bwd_colsum_bf16": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i32, ctypes.c_int, _p,
                                                  _i64, _p, _p, _i64, _p]),
+    "gnnea_gemm_bf16_dmask_applies": (ctypes.c_int, [_i64, _i64, _i64, _i64, _i64, _i64]),
+    "gnnea_gemm_bf16_dmask_ws_bytes": (_i64, [_i64, _i64]),
+    "gnnea_gemm_bf16_dmask": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p, _i64,
+                                             _p, _i64, _p, _i64, _p, _i64, _p]),
     "gnnea_gemm_bf16_act": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64,
                                            _p, _i64, _p, ctypes.c_int, _p, _i64, ctypes.c_int, _p,
                                            _i64, _p]),

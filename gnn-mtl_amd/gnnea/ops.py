@@ -435,6 +435,123 @@ def act_bwd_colsum(dy, y, act, want_db=True):
     return g, db
 
 
+def gemm_dmask(g, weight, y):
+    """bf16(g · weight) * relu'(y) in one pass (gnnea_gemm_bf16_dmask: the product that carries the
+    gradient into a relu Linear's output y, masked in its epilogue -- bit-identical to gemm
+    followed by act_bwd's G), or None where that kernel does not apply (then the caller runs the
+    two steps)."""
+    if g.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 or y.dtype != torch.bfloat16:
+        return None
+    g, weight, y = _rows(g), _rows(weight), _rows(y)
+    M, K = g.shape
+    N = weight.shape[1]
+    if weight.shape[0] != K or y.shape != (M, N):
+        raise ValueError("gnnea.gemm_dmask: shape mismatch")
+    L = _lib.lib()
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=g.device)
+    if not L.gnnea_gemm_bf16_dmask_applies(M, N, K, _ld(g), _ld(y), _ld(out)) or \
+            (g.data_ptr() | y.data_ptr() | weight.data_ptr()) % 8:
+        return None
+    ws_bytes = int(L.gnnea_gemm_bf16_dmask_ws_bytes(N, K))
+    ws = _gemm_ws(g.device, ws_bytes)
+    with _lib.on_device(g.device):
+        check(L.gnnea_gemm_bf16_dmask(0, M, N, K, ptr(g), _ld(g), ptr(weight), _ld(weight), ptr(y),
+                                      _ld(y), ptr(out), _ld(out), ptr(ws), ws_bytes,
+                                      stream_of(g.device)))
+    return out
+
+
+class MLPChainFn(torch.autograd.Function):
+    """A stack of Linear layers y_{k+1} = act_k(y_k W_kᵀ + b_k), act_k relu or identity, dropout
+    inactive (the MLPDecoder, models/decoders.py, each layer as layers/layers.py:121-122) as ONE
+    autograd node, so that the backward can fuse across layers: the product carrying the gradient
+    into a relu layer's output y_k masks it in its epilogue (gemm_dmask), which removes the
+    act_bwd pass over (dy_k, y_k) of the per-layer LinearActFn; db_k is a column sum of the
+    masked gradient.  Forward and every stored value as LinearFn / LinearActFn compute them
+    (same GEMM calls); the bias gradients sum the same values in another order."""
+
+    @staticmethod
+    def forward(ctx, x, acts, *params):
+        ys = [x]
+        for k, act in enumerate(acts):
+            w, b = params[2 * k], params[2 * k + 1]
+            a = act if act == _lib.GNNEA_ACT_RELU else None
+            ys.append(gemm(ys[-1], w, trans_b=True, bias=b, act=a))
+        ctx.acts = tuple(acts)
+        ctx.bias_dtypes = [params[2 * k + 1].dtype if params[2 * k + 1] is not None else None
+                           for k in range(len(acts))]
+        ws = [params[2 * k] for k in range(len(acts))]
+        ctx.save_for_backward(*ys[:-1], ys[-1], *ws)
+        return ys[-1]
+
+    @staticmethod
+    def backward(ctx, dy):
+        nl = len(ctx.acts)
+        saved = ctx.saved_tensors
+        ys, ws = list(saved[:nl + 1]), list(saved[nl + 1:])
+        need = ctx.needs_input_grad
+        grads = [None] * (2 * nl)
+        g = None     # the gradient at the current layer's pre-activation (masked), when known
+        d = dy       # else the gradient at its output
+        dx = None
+        for k in range(nl - 1, -1, -1):
+            x, w, y, act = ys[k], ws[k], ys[k + 1], ctx.acts[k]
+            bf = x.dtype == torch.bfloat16 or w.dtype == torch.bfloat16
+            want_db = ctx.bias_dtypes[k] is not None and need[3 + 2 * k]
+            db = None
+            if g is None:
+                if act == _lib.GNNEA_ACT_RELU:
+                    d = _featc(d, y.dtype)
+                    g, db = act_bwd_colsum(d, y, act, want_db)
+                else:
+                    g = _featc(d, torch.bfloat16 if bf else torch.float32)
+                    if want_db:
+                        db = colsum(g, ctx.bias_dtypes[k])
+            elif want_db:
+                db = colsum(g, ctx.bias_dtypes[k])
+            g = _featc(g, torch.bfloat16 if bf else torch.float32)
+            if need[2 + 2 * k]:
+                grads[2 * k] = gemm(g, x, trans_a=True, out_dtype=w.dtype if bf else None)
+            if db is not None and db.dtype != ctx.bias_dtypes[k]:
+                db = db.to(ctx.bias_dtypes[k])
+            grads[2 * k + 1] = db
+            if k == 0 and not need[0]:
+                break
+            # the gradient into x = y_{k-1}: masked here when that layer is a relu layer
+            gn = None
+            if k > 0 and ctx.acts[k - 1] == _lib.GNNEA_ACT_RELU:
+                gn = gemm_dmask(g, w, x)
+            if gn is not None:
+                g, d = gn, None
+            else:
+                d = gemm(g, w, out_dtype=x.dtype if bf else None)
+                g = None
+            if k == 0:
+                dx = d
+        return (dx, None, *grads)
+
+
+def mlp_chain(x, layers):
+    """The fused MLPChainFn over an nn.Sequential of layers.layers.Linear, or None when a layer
+    is not fusable (an act other than relu / identity, active dropout, no weight) or carries
+    forward hooks (they see the per-layer modules' calls, which the chain does not make)."""
+    acts, params = [], []
+    for m in [layers] + list(layers):
+        if m._forward_hooks or m._forward_pre_hooks:
+            return None
+    for m in layers:
+        code = act_code(getattr(m, "act", None))
+        lin = getattr(m, "linear", None)
+        if code not in (_lib.GNNEA_ACT_RELU, _lib.GNNEA_ACT_IDENTITY) or lin is None or \
+                (m.training and m.dropout > 0):
+            return None
+        acts.append(int(code))
+        params += [lin.weight, lin.bias]
+    if not acts:
+        return None
+    return MLPChainFn.apply(x, tuple(acts), *params)
+
+
 def matmul(x, w, sliced=False):
     return MatmulFn.apply(x, w, sliced)
 

@@ -9,7 +9,7 @@ import torch.nn.functional as F
 from gnnea import _lib, ops
 
 from layers.att_layers import GraphAttentionLayer
-from layers.layers import GraphConvolution, HighWayGraphConvolution, Linear
+from layers.layers import GraphConvolution, HighWayGraphConvolution, Linear, dense_of
 
 
 def _identity(x):
@@ -62,6 +62,12 @@ class MLPDecoder(Decoder):
         self.cls = nn.Sequential(*[Linear(widths[k], widths[k + 1], args.dropout, acts[k],
                                           args.bias) for k in range(3)])
         self.decode_adj = False
+
+    def decode(self, x, adj):
+        # the three layers as one autograd node (ops.MLPChainFn: the backward masks each relu
+        # layer's gradient in the epilogue of the product that produces it); per layer otherwise
+        out = ops.mlp_chain(dense_of(x), self.cls)
+        return out if out is not None else self.cls.forward(x)
 
 
 class LinearDecoder(Decoder):

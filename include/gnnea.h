@@ -525,6 +525,20 @@ int gnnea_gemm_bf16_act(int trans_a, int trans_b, int64_t M, int64_t N, int64_t 
                         int64_t lda, const void* B, int64_t ldb, const float* bias, int act,
                         void* C, int64_t ldc, int c_dtype, void* ws, int64_t ws_bytes,
                         void* stream);
+/* The backward of a relu Linear through the product that consumed its output Y (MLPDecoder,
+ * models/decoders.py; replaces torch's dY·W then threshold_backward(·, Y, 0) and the bias
+ * gradient's sum(0) of layers/layers.py:121-122 under autograd): G = bf16(A·op(B)) * relu'(Y),
+ * bit-identical to gnnea_gemm_bf16 + gnnea_act_bwd_colsum_bf16's G (the bias gradient: a
+ * gnnea_colsum_bf16 pass over G).  A, B, Y, G bf16 row-major.  Only where the weight-resident
+ * kernel runs (gnnea_gemm_bf16_dmask_applies: K in (288, 320], M >= 65536, 128 < N <= 4096,
+ * N % 4 == 0, 8-B aligned Y / G with ld % 4 == 0), else GNNEA_EINVAL.  Workspace:
+ * gnnea_gemm_bf16_dmask_ws_bytes. */
+int gnnea_gemm_bf16_dmask_applies(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldy,
+                                  int64_t ldg);
+int64_t gnnea_gemm_bf16_dmask_ws_bytes(int64_t N, int64_t K);
+int gnnea_gemm_bf16_dmask(int trans_b, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                          const void* B, int64_t ldb, const void* Y, int64_t ldy, void* G,
+                          int64_t ldg, void* ws, int64_t ws_bytes, void* stream);
 /* the bf16 GEMM writing C slice-major (bf16, 128-column slices):
  * element (r, c) at Cs[(c/128)*sstride + r*128 + c%128], sstride % 128 == 0, >= M*128 */
 int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

@@ -127,3 +127,55 @@ def test_act_bwd_colsum_vs_fp64(device, n, D, ld, dtype):
         assert rel_err(db.cpu(), G.double().sum(0).cpu()) < 1e-6
         G2, db2 = ops.act_bwd_colsum(dy, y, act)
         assert torch.equal(G, G2) and torch.equal(db, db2)  # deterministic
+
+
+@pytest.mark.parametrize("dtype,M", [(torch.bfloat16, 70000),   # masked backward products
+                                     (torch.bfloat16, 1000),    # small: the two-step fallback
+                                     (torch.float32, 70000)])   # fp32: the two-step fallback
+def test_mlp_chain_vs_per_layer(device, dtype, M):
+    """MLPDecoder's three Linear layers (relu, relu, identity; models/decoders.py) as one
+    MLPChainFn against the per-layer LinearActFn / LinearFn path: output, dx and every dW bit
+    for bit (gemm_dmask's masked product = the product then act_bwd's G), db to 1e-6 (the same
+    values summed in another order; bf16 biases round each sum) -- and the fused path is the one
+    that ran (bf16, tall)."""
+    import torch.nn as nn
+    from gnnea import ops
+    from layers.layers import Linear
+    from models.decoders import _identity
+    torch.manual_seed(5)
+    layers = nn.Sequential(Linear(300, 300, 0.0, F.relu, True), Linear(300, 300, 0.0, F.relu, True),
+                           Linear(300, 300, 0.0, _identity, True)).to(device).to(dtype)
+    g = torch.Generator(device=device).manual_seed(6)
+    x0 = torch.randn(M, 300, device=device, generator=g).to(dtype)
+    R = torch.randn(M, 300, device=device, generator=g).to(dtype)
+    calls = []
+    orig = ops.gemm_dmask
+
+    def spy(*a):
+        out = orig(*a)
+        calls.append(out is not None)
+        return out
+
+    def run(fused):
+        layers.zero_grad()
+        x = x0.clone().requires_grad_(True)
+        y = ops.mlp_chain(x, layers) if fused else layers(x)
+        assert y is not None
+        (y.float() * R.float()).sum().backward()
+        return [y.detach(), x.grad] + [p.grad.clone() for p in layers.parameters()]
+    import pytest as _pt
+    mp = _pt.MonkeyPatch()
+    mp.setattr(ops, "gemm_dmask", spy)
+    try:
+        got = run(True)
+    finally:
+        mp.undo()
+    ref = run(False)
+    assert calls == [dtype == torch.bfloat16 and M >= 65536] * 2
+    names = ["y", "dx", "dW0", "db0", "dW1", "db1", "dW2", "db2"]
+    for nm, a, b in zip(names, got, ref):
+        if nm.startswith("db"):  # (bf16 biases: each sum rounded to bf16, a 2^-8 step apart)
+            tol = 1e-6 if dtype == torch.float32 else 8e-3
+            assert rel_err(a.float().cpu(), b.float().cpu()) < tol, nm
+        else:
+            assert torch.equal(a, b), nm

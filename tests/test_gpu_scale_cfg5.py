@@ -143,11 +143,15 @@ def test_cfg5_gat_ea_step_vs_fp64(device, cfg5, monkeypatch, relu_band, record_p
     m = EAModel(a).to(device).bfloat16()
     m.train()
     acts = []  # every relu'd activation, in forward order (tested signs for the band)
-    for L in list(m.encoder.layers) + list(m.decoder.cls)[:2]:
+    for L in list(m.encoder.layers):
         L.register_forward_hook(lambda mod, i, o: acts.append(
             (o[0] if isinstance(o, tuple) else o).detach()))
     outputs = m.decode(m.encode(d["xb"], d["adj"]), d["adj"])
     assert outputs.dtype == torch.bfloat16
+    # the decoder ran as one node (ops.MLPChainFn): its saved (x, y1, y2, y3, W...) hold the two
+    # relu layers' outputs
+    assert type(outputs.grad_fn).__name__ == "MLPChainFnBackward"
+    acts += [t.detach() for t in outputs.grad_fn.saved_tensors[1:3]]
     m.neg_right = si.negatives(N, t, k, 31)
     m.neg2_left = si.negatives(N, t, k, 32)
     loss = m.get_loss(outputs, {"train": train}, "train")
