@@ -864,21 +864,28 @@ __global__ __launch_bounds__(256) void k_pack_bf16w(const bf16_t* __restrict__ B
   }
 }
 
-// DM (the backward of a relu Linear whose output y fed this product, bf16): the stored value is
-// g = bf16(acc) * relu'(y) at the same position (act_bwd_colsum's g on the product it would read,
-// bit for bit), y read for the tile before the next tile's activations are issued.  (Column sums
-// of g kept per lane across the tiles as well -- 80 more registers -- spilled: the bias gradient
-// is a separate streaming pass over g.)
-template <typename TC, int KC, bool DM = false>
+// Epilogue modes EP (bf16 out):
+//  1 (the backward of a relu Linear whose output y fed this product): the stored value is
+//    g = bf16(acc) * relu'(y) at the same position (act_bwd_colsum's g on the product it would
+//    read, bit for bit), y read for the tile before the next tile's activations are issued;
+//  2 the same with relu'(y) from the sign bits mode 3 wrote (Ym: 1 bit per element instead of
+//    16: 20 bytes per row and column tile, byte 4 t + g of a tile holds columns 32 t + 8 g + 0..7);
+//  3 (the forward of that relu Linear) relu as mode 0, and the sign bits of the stored y -> Mo.
+// (Column sums of g kept per lane across the tiles as well -- 80 more registers -- spilled: the
+// bias gradient is a separate streaming pass over g.)
+template <typename TC, int KC, int EP = 0>
 __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int ntn,
                                                       const bf16_t* __restrict__ A, int64_t lda,
                                                       const bf16_t* __restrict__ P,
                                                       const float* __restrict__ bias,
                                                       TC* __restrict__ C, int64_t ldc,
                                                       int64_t cs, int relu,
-                                                      const bf16_t* __restrict__ Ym = nullptr,
-                                                      int64_t ldym = 0) {
-  static_assert(!DM || std::is_same<TC, bf16_t>::value, "the masked form stores bf16");
+                                                      const void* __restrict__ Ym = nullptr,
+                                                      int64_t ldym = 0,
+                                                      uint8_t* __restrict__ Mo = nullptr,
+                                                      int64_t ldmo = 0) {
+  static_assert(EP == 0 || std::is_same<TC, bf16_t>::value, "the masked forms store bf16");
+  constexpr bool DM = EP == 1 || EP == 2;
   __shared__ __attribute__((aligned(16))) uint4 wl[KC * 2 * kBwCols];  // [s][kh][n] x 16 B
   // the tile's bias in LDS: a global load in the epilogue would wait (vmcnt counts in order)
   // for the next tile's activation loads issued before it
@@ -924,16 +931,22 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
                       sh == 1 ? v.w : 0u, 0u);
   };
   const uint4* wlane = wl + kh * kBwCols + li;  // + (2 s) * 160 + 32 t
-  // DM: the tile's y pieces (the output positions, clamped in bounds: unconditional loads)
-  uint2 ym[DM ? 20 : 1];
+  // EP 1: the tile's y pieces (the output positions, clamped in bounds: unconditional loads);
+  // EP 2: the row's 20 sign bytes of this column tile
+  uint2 ym[EP == 1 ? 20 : 1];
+  uint32_t mb[EP == 2 ? 5 : 1];
   auto load_y = [&](int rt) {
-    if constexpr (DM) {
-      const int64_t m = min(rt * 128 + w * 32 + li, M - 1);
+    const int64_t m = min(rt * 128 + w * 32 + li, M - 1);
+    if constexpr (EP == 1) {
 #pragma unroll
       for (int q = 0; q < 20; ++q) {
         const int n = min(n0 + 32 * (q >> 2) + 8 * (q & 3) + 4 * kh, N - 4);
-        ym[q] = *(const uint2*)(Ym + m * ldym + n);
+        ym[q] = *(const uint2*)((const bf16_t*)Ym + m * ldym + n);
       }
+    } else if constexpr (EP == 2) {
+      const uint32_t* mp = (const uint32_t*)((const uint8_t*)Ym + m * ldym + nt * 20);
+#pragma unroll
+      for (int t = 0; t < 5; ++t) mb[t] = mp[t];
     }
   };
   auto compute_store = [&](const uint4 (&f)[KC], int rt) {
@@ -964,6 +977,7 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
     // lane: output row m, columns n0 + 32 t + 8 g + 4 kh + (0..3) = acc[t][4 g .. 4 g + 3]
     const int m = rt * 128 + w * 32 + li;
     if (m >= M) return;
+    uint32_t nb[3] = {0u, 0u, 0u};  // EP 3: the sign nibbles, (t, g) = q at bits 4 (q % 8)
 #pragma unroll
     for (int t = 0; t < 5; ++t) {
 #pragma unroll
@@ -978,20 +992,33 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
           TC* c = C + c_index_bf(m, n, ldc, cs);
           if constexpr (DM) {
             // g = bf16(bf16(o) * relu'(y)): the product rounded as stored, then the derivative
-            const uint2 yv = ym[4 * t + g];
-            const float y4[4] = {bf16_to_f32((bf16_t)(yv.x & 0xffffu)),
-                                 bf16_to_f32((bf16_t)(yv.x >> 16)),
-                                 bf16_to_f32((bf16_t)(yv.y & 0xffffu)),
-                                 bf16_to_f32((bf16_t)(yv.y >> 16))};
+            float d4[4];
+            if constexpr (EP == 1) {
+              const uint2 yv = ym[4 * t + g];
+              d4[0] = act_grad_from_out<GNNEA_ACT_RELU>(bf16_to_f32((bf16_t)(yv.x & 0xffffu)));
+              d4[1] = act_grad_from_out<GNNEA_ACT_RELU>(bf16_to_f32((bf16_t)(yv.x >> 16)));
+              d4[2] = act_grad_from_out<GNNEA_ACT_RELU>(bf16_to_f32((bf16_t)(yv.y & 0xffffu)));
+              d4[3] = act_grad_from_out<GNNEA_ACT_RELU>(bf16_to_f32((bf16_t)(yv.y >> 16)));
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) d4[e] = (mb[t] >> (8 * g + 4 * kh + e)) & 1u ? 1.f : 0.f;
+            }
             const float o4[4] = {o.x, o.y, o.z, o.w};
             bf16_t gb[4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              gb[e] = f32_to_bf16(bf16_to_f32(f32_to_bf16(o4[e])) *
-                                  act_grad_from_out<GNNEA_ACT_RELU>(y4[e]));
-            }
+            for (int e = 0; e < 4; ++e) gb[e] = f32_to_bf16(bf16_to_f32(f32_to_bf16(o4[e])) * d4[e]);
             *(uint2*)c = make_uint2((uint32_t)gb[0] | ((uint32_t)gb[1] << 16),
                                     (uint32_t)gb[2] | ((uint32_t)gb[3] << 16));
+          } else if constexpr (EP == 3) {
+            const bf16_t y0 = f32_to_bf16(o.x), y1 = f32_to_bf16(o.y), y2 = f32_to_bf16(o.z),
+                         y3 = f32_to_bf16(o.w);
+            *(uint2*)c = make_uint2((uint32_t)y0 | ((uint32_t)y1 << 16),
+                                    (uint32_t)y2 | ((uint32_t)y3 << 16));
+            // relu'(y) = y > 0 on the stored value (y >= 0: its bits nonzero)
+            const uint32_t nib = (y0 != 0 ? 1u : 0u) | (y1 != 0 ? 2u : 0u) | (y2 != 0 ? 4u : 0u) |
+                                 (y3 != 0 ? 8u : 0u);
+            const int q = 4 * t + g;
+            nb[q >> 3] |= nib << (4 * (q & 7));
           } else if constexpr (std::is_same<TC, bf16_t>::value) {
             *(uint2*)c = make_uint2((uint32_t)f32_to_bf16(o.x) | ((uint32_t)f32_to_bf16(o.y) << 16),
                                     (uint32_t)f32_to_bf16(o.z) | ((uint32_t)f32_to_bf16(o.w) << 16));
@@ -999,6 +1026,26 @@ __global__ __launch_bounds__(256, 1) void k_gemm_bf16w(int M, int N, int K, int 
             *(float4*)c = o;
           }
         }
+      }
+    }
+    if constexpr (EP == 3) {
+      // the row's bytes: columns 8 g .. 8 g + 3 from the kh = 0 lane, + 4 .. + 7 from its kh = 1
+      // partner (the same row); kh = 0 lanes store dwords t = 0..2, kh = 1 lanes t = 3, 4
+      uint32_t ot[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) ot[i] = __shfl_xor(nb[i], 32);
+      uint32_t* mp = (uint32_t*)(Mo + (int64_t)m * ldmo + nt * 20);
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        uint32_t d = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int q = 4 * t + g;
+          const uint32_t a0 = (nb[q >> 3] >> (4 * (q & 7))) & 15u;
+          const uint32_t a1 = (ot[q >> 3] >> (4 * (q & 7))) & 15u;
+          d |= (kh ? (a1 | (a0 << 4)) : (a0 | (a1 << 4))) << (8 * g);
+        }
+        if (kh ? t >= 3 : t < 3) mp[t] = d;
       }
     }
   };
@@ -1099,6 +1146,35 @@ static bool dmask_applies(int64_t M, int64_t N, int64_t K, int64_t lda, const vo
          ldg % 4 == 0 && (((uintptr_t)Y | (uintptr_t)G) & 7) == 0;
 }
 static int64_t dmask_ws_bytes(int64_t N, int64_t K) { return bf16w_planes_bytes(N, K); }
+static int64_t mask_ld(int64_t N) { return 20 * ((N + kBwCols - 1) / kBwCols); }
+
+// the weight-resident kernel with epilogue mode EP (bf16 out, row-major, no split)
+template <int EP>
+static int bf16w_ep_launch(int trans_b, int64_t M, int64_t N, int64_t K, const bf16_t* A,
+                           int64_t lda, const bf16_t* B, int64_t ldb, const float* bias,
+                           bf16_t* C, int64_t ldc, int relu, const void* Ym, int64_t ldym,
+                           uint8_t* Mo, int64_t ldmo, void* ws, hipStream_t s) {
+  const int kc = bf16w_kc(K), ntn = (int)((N + kBwCols - 1) / kBwCols);
+  bf16_t* P = (bf16_t*)ws;
+  {
+    const int64_t tot = (int64_t)ntn * kc * 2 * kBwCols * 8;
+    const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
+    hipLaunchKernelGGL(k_pack_bf16w, dim3(nb), dim3(256), 0, s, B, ldb, trans_b ? 1 : 0, (int)N,
+                       (int)K, kc, ntn, P);
+    GNNEA_LAUNCH_CHECK();
+  }
+  const int grid = bf16w_grid(M, ntn);
+  if (kc == 19)
+    hipLaunchKernelGGL((k_gemm_bf16w<bf16_t, 19, EP>), dim3(grid), dim3(256), 0, s, (int)M,
+                       (int)N, (int)K, ntn, A, lda, P, bias, C, ldc, (int64_t)128, relu, Ym, ldym,
+                       Mo, ldmo);
+  else
+    hipLaunchKernelGGL((k_gemm_bf16w<bf16_t, 20, EP>), dim3(grid), dim3(256), 0, s, (int)M,
+                       (int)N, (int)K, ntn, A, lda, P, bias, C, ldc, (int64_t)128, relu, Ym, ldym,
+                       Mo, ldmo);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
+}
 
 template <typename TC>
 static int gemm_bf16_t(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
@@ -1251,27 +1327,53 @@ extern "C" int gnnea_gemm_bf16_dmask(int trans_b, int64_t M, int64_t N, int64_t 
   if (trans_b ? ldb < K : ldb < N) return GNNEA_EINVAL;
   if (!dmask_applies(M, N, K, lda, A, ldy, Y, ldg, G)) return GNNEA_EINVAL;
   if (ws_bytes < dmask_ws_bytes(N, K)) return GNNEA_EWORKSPACE;
-  hipStream_t s = (hipStream_t)stream;
-  const int kc = bf16w_kc(K), ntn = (int)((N + kBwCols - 1) / kBwCols);
-  bf16_t* P = (bf16_t*)ws;
-  {
-    const int64_t tot = (int64_t)ntn * kc * 2 * kBwCols * 8;
-    const int nb = (int)((tot + 255) / 256 < 2048 ? (tot + 255) / 256 : 2048);
-    hipLaunchKernelGGL(k_pack_bf16w, dim3(nb), dim3(256), 0, s, (const bf16_t*)B, ldb,
-                       trans_b ? 1 : 0, (int)N, (int)K, kc, ntn, P);
-    GNNEA_LAUNCH_CHECK();
-  }
-  const int grid = bf16w_grid(M, ntn);
-  if (kc == 19)
-    hipLaunchKernelGGL((k_gemm_bf16w<bf16_t, 19, true>), dim3(grid), dim3(256), 0, s, (int)M,
-                       (int)N, (int)K, ntn, (const bf16_t*)A, lda, P, nullptr, (bf16_t*)G, ldg,
-                       (int64_t)128, 0, (const bf16_t*)Y, ldy);
-  else
-    hipLaunchKernelGGL((k_gemm_bf16w<bf16_t, 20, true>), dim3(grid), dim3(256), 0, s, (int)M,
-                       (int)N, (int)K, ntn, (const bf16_t*)A, lda, P, nullptr, (bf16_t*)G, ldg,
-                       (int64_t)128, 0, (const bf16_t*)Y, ldy);
-  GNNEA_LAUNCH_CHECK();
-  return 0;
+  return bf16w_ep_launch<1>(trans_b, M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb,
+                            nullptr, (bf16_t*)G, ldg, 0, Y, ldy, nullptr, 0, ws,
+                            (hipStream_t)stream);
+}
+
+extern "C" int64_t gnnea_gemm_bf16_mask_ld(int64_t N) {
+  if (N < 0) return GNNEA_EINVAL;
+  return mask_ld(N);
+}
+
+// C = relu(A·op(B) + bias) (bf16, as gnnea_gemm_bf16_act with relu on the weight-resident kernel,
+// bit for bit) and its sign bits M[row][...] (gnnea_gemm_bf16_mask_ld(N) bytes per row at least:
+// byte 20 t + 4 u + g of a row holds columns 160 t + 32 u + 8 g + 0..7, bit e = column + e > 0)
+// for gnnea_gemm_bf16_dmask_bits.  Where gnnea_gemm_bf16_dmask_applies (with ldy = ldc).
+extern "C" int gnnea_gemm_bf16_relu_mask(int trans_b, int64_t M, int64_t N, int64_t K,
+                                         const void* A, int64_t lda, const void* B, int64_t ldb,
+                                         const float* bias, void* C, int64_t ldc, void* Mo,
+                                         int64_t ldm, void* ws, int64_t ws_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  if (M == 0 || N == 0) return 0;
+  if (M >= (1ll << 31) || N >= (1ll << 31) || !A || !B || !C || !Mo || !ws) return GNNEA_EINVAL;
+  if (trans_b ? ldb < K : ldb < N) return GNNEA_EINVAL;
+  if (!dmask_applies(M, N, K, lda, A, ldc, C, ldc, C) || ldm < mask_ld(N) || ldm % 4 ||
+      ((uintptr_t)Mo & 3))
+    return GNNEA_EINVAL;
+  if (ws_bytes < dmask_ws_bytes(N, K)) return GNNEA_EWORKSPACE;
+  return bf16w_ep_launch<3>(trans_b, M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, bias,
+                            (bf16_t*)C, ldc, 1, nullptr, 0, (uint8_t*)Mo, ldm, ws,
+                            (hipStream_t)stream);
+}
+
+// gnnea_gemm_bf16_dmask with relu'(y) from the sign bits gnnea_gemm_bf16_relu_mask wrote
+extern "C" int gnnea_gemm_bf16_dmask_bits(int trans_b, int64_t M, int64_t N, int64_t K,
+                                          const void* A, int64_t lda, const void* B, int64_t ldb,
+                                          const void* Mi, int64_t ldm, void* G, int64_t ldg,
+                                          void* ws, int64_t ws_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  if (M == 0 || N == 0) return 0;
+  if (M >= (1ll << 31) || N >= (1ll << 31) || !A || !B || !Mi || !G || !ws) return GNNEA_EINVAL;
+  if (trans_b ? ldb < K : ldb < N) return GNNEA_EINVAL;
+  if (!dmask_applies(M, N, K, lda, A, ldg, G, ldg, G) || ldm < mask_ld(N) || ldm % 4 ||
+      ((uintptr_t)Mi & 3))
+    return GNNEA_EINVAL;
+  if (ws_bytes < dmask_ws_bytes(N, K)) return GNNEA_EWORKSPACE;
+  return bf16w_ep_launch<2>(trans_b, M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb,
+                            nullptr, (bf16_t*)G, ldg, 0, Mi, ldm, nullptr, 0, ws,
+                            (hipStream_t)stream);
 }
 
 extern "C" int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

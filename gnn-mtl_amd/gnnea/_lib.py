@@ -177,6 +177,11 @@ SIGNATURES = {
     "gnnea_gemm_bf16_dmask_ws_bytes": (_i64, [_i64, _i64]),
     "gnnea_gemm_bf16_dmask": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p, _i64,
                                              _p, _i64, _p, _i64, _p, _i64, _p]),
+    "gnnea_gemm_bf16_mask_ld": (_i64, [_i64]),
+    "gnnea_gemm_bf16_relu_mask": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
+                                                 _i64, _p, _p, _i64, _p, _i64, _p, _i64, _p]),
+    "gnnea_gemm_bf16_dmask_bits": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
+                                                  _i64, _p, _i64, _p, _i64, _p, _i64, _p]),
     "gnnea_gemm_bf16_act": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64,
                                            _p, _i64, _p, ctypes.c_int, _p, _i64, ctypes.c_int, _p,
                                            _i64, _p]),

@@ -435,11 +435,40 @@ def act_bwd_colsum(dy, y, act, want_db=True):
     return g, db
 
 
-def gemm_dmask(g, weight, y):
+def gemm_relu_mask(x, weight, bias):
+    """(relu(x Wᵀ + b), sign bits) in one pass (gnnea_gemm_bf16_relu_mask: the output bit-identical
+    to gemm(..., act=relu), plus 1 bit per element for gemm_dmask), or None where the bf16
+    weight-resident kernel does not apply."""
+    if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
+        return None
+    x, weight = _rows(x), _rows(weight)
+    M, K = x.shape
+    N = weight.shape[0]
+    if weight.shape[1] != K:
+        raise ValueError("gnnea.gemm_relu_mask: shape mismatch")
+    L = _lib.lib()
+    if not L.gnnea_gemm_bf16_dmask_applies(M, N, K, _ld(x), N, N) or \
+            (x.data_ptr() | weight.data_ptr()) % 8:
+        return None
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    ldm = int(L.gnnea_gemm_bf16_mask_ld(N))
+    mask = torch.empty((M, ldm), dtype=torch.uint8, device=x.device)
+    b = _featc(bias, torch.float32) if bias is not None else None
+    ws_bytes = int(L.gnnea_gemm_bf16_dmask_ws_bytes(N, K))
+    ws = _gemm_ws(x.device, ws_bytes)
+    with _lib.on_device(x.device):
+        check(L.gnnea_gemm_bf16_relu_mask(1, M, N, K, ptr(x), _ld(x), ptr(weight), _ld(weight),
+                                          ptr(b), ptr(y), N, ptr(mask), ldm, ptr(ws), ws_bytes,
+                                          stream_of(x.device)))
+    return y, mask
+
+
+def gemm_dmask(g, weight, y, mask=None):
     """bf16(g · weight) * relu'(y) in one pass (gnnea_gemm_bf16_dmask: the product that carries the
     gradient into a relu Linear's output y, masked in its epilogue -- bit-identical to gemm
-    followed by act_bwd's G), or None where that kernel does not apply (then the caller runs the
-    two steps)."""
+    followed by act_bwd's G; with ``mask``, gemm_relu_mask's sign bits of y, read instead of y:
+    gnnea_gemm_bf16_dmask_bits), or None where that kernel does not apply (then the caller runs
+    the two steps)."""
     if g.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 or y.dtype != torch.bfloat16:
         return None
     g, weight, y = _rows(g), _rows(weight), _rows(y)
@@ -455,9 +484,14 @@ def gemm_dmask(g, weight, y):
     ws_bytes = int(L.gnnea_gemm_bf16_dmask_ws_bytes(N, K))
     ws = _gemm_ws(g.device, ws_bytes)
     with _lib.on_device(g.device):
-        check(L.gnnea_gemm_bf16_dmask(0, M, N, K, ptr(g), _ld(g), ptr(weight), _ld(weight), ptr(y),
-                                      _ld(y), ptr(out), _ld(out), ptr(ws), ws_bytes,
-                                      stream_of(g.device)))
+        if mask is not None:
+            check(L.gnnea_gemm_bf16_dmask_bits(0, M, N, K, ptr(g), _ld(g), ptr(weight),
+                                               _ld(weight), ptr(mask), mask.stride(0), ptr(out),
+                                               _ld(out), ptr(ws), ws_bytes, stream_of(g.device)))
+        else:
+            check(L.gnnea_gemm_bf16_dmask(0, M, N, K, ptr(g), _ld(g), ptr(weight), _ld(weight),
+                                          ptr(y), _ld(y), ptr(out), _ld(out), ptr(ws), ws_bytes,
+                                          stream_of(g.device)))
     return out
 
 
@@ -465,30 +499,32 @@ class MLPChainFn(torch.autograd.Function):
     """A stack of Linear layers y_{k+1} = act_k(y_k W_kᵀ + b_k), act_k relu or identity, dropout
     inactive (the MLPDecoder, models/decoders.py, each layer as layers/layers.py:121-122) as ONE
     autograd node, so that the backward can fuse across layers: the product carrying the gradient
-    into a relu layer's output y_k masks it in its epilogue (gemm_dmask), which removes the
-    act_bwd pass over (dy_k, y_k) of the per-layer LinearActFn; db_k is a column sum of the
-    masked gradient.  Forward and every stored value as LinearFn / LinearActFn compute them
+    into a relu layer's output y_k masks it in its epilogue (gemm_dmask, reading the sign bits
+    the forward product wrote with y_k, gemm_relu_mask), which removes the act_bwd pass over
+    (dy_k, y_k) of the per-layer LinearActFn; db_k is a column sum of the masked gradient.  Forward and every stored value as LinearFn / LinearActFn compute them
     (same GEMM calls); the bias gradients sum the same values in another order."""
 
     @staticmethod
     def forward(ctx, x, acts, *params):
-        ys = [x]
+        ys, masks = [x], []
         for k, act in enumerate(acts):
             w, b = params[2 * k], params[2 * k + 1]
             a = act if act == _lib.GNNEA_ACT_RELU else None
-            ys.append(gemm(ys[-1], w, trans_b=True, bias=b, act=a))
+            ym = gemm_relu_mask(ys[-1], w, b) if a is not None and k + 1 < len(acts) else None
+            ys.append(ym[0] if ym is not None else gemm(ys[-1], w, trans_b=True, bias=b, act=a))
+            masks.append(ym[1] if ym is not None else None)
         ctx.acts = tuple(acts)
         ctx.bias_dtypes = [params[2 * k + 1].dtype if params[2 * k + 1] is not None else None
                            for k in range(len(acts))]
         ws = [params[2 * k] for k in range(len(acts))]
-        ctx.save_for_backward(*ys[:-1], ys[-1], *ws)
+        ctx.save_for_backward(*ys[:-1], ys[-1], *ws, *masks)
         return ys[-1]
 
     @staticmethod
     def backward(ctx, dy):
         nl = len(ctx.acts)
         saved = ctx.saved_tensors
-        ys, ws = list(saved[:nl + 1]), list(saved[nl + 1:])
+        ys, ws, masks = list(saved[:nl + 1]), list(saved[nl + 1:2 * nl + 1]), saved[2 * nl + 1:]
         need = ctx.needs_input_grad
         grads = [None] * (2 * nl)
         g = None     # the gradient at the current layer's pre-activation (masked), when known
@@ -520,7 +556,7 @@ class MLPChainFn(torch.autograd.Function):
             # the gradient into x = y_{k-1}: masked here when that layer is a relu layer
             gn = None
             if k > 0 and ctx.acts[k - 1] == _lib.GNNEA_ACT_RELU:
-                gn = gemm_dmask(g, w, x)
+                gn = gemm_dmask(g, w, x, masks[k - 1])
             if gn is not None:
                 g, d = gn, None
             else:

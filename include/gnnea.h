@@ -539,6 +539,20 @@ int64_t gnnea_gemm_bf16_dmask_ws_bytes(int64_t N, int64_t K);
 int gnnea_gemm_bf16_dmask(int trans_b, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                           const void* B, int64_t ldb, const void* Y, int64_t ldy, void* G,
                           int64_t ldg, void* ws, int64_t ws_bytes, void* stream);
+/* The forward of that relu Linear keeping 1 bit per element for the backward: C = relu(A·op(B) +
+ * bias) bf16 (bit-identical to gnnea_gemm_bf16_act's relu) and its sign bits Mo (byte
+ * 20 t + 4 u + g of a row: columns 160 t + 32 u + 8 g + 0..7, bit e set where that column's
+ * stored value > 0; ldm >= gnnea_gemm_bf16_mask_ld(N), % 4 == 0); gnnea_gemm_bf16_dmask_bits is
+ * gnnea_gemm_bf16_dmask reading them instead of Y.  Same applicability and workspace as
+ * gnnea_gemm_bf16_dmask. */
+int64_t gnnea_gemm_bf16_mask_ld(int64_t N);
+int gnnea_gemm_bf16_relu_mask(int trans_b, int64_t M, int64_t N, int64_t K, const void* A,
+                              int64_t lda, const void* B, int64_t ldb, const float* bias, void* C,
+                              int64_t ldc, void* Mo, int64_t ldm, void* ws, int64_t ws_bytes,
+                              void* stream);
+int gnnea_gemm_bf16_dmask_bits(int trans_b, int64_t M, int64_t N, int64_t K, const void* A,
+                               int64_t lda, const void* B, int64_t ldb, const void* Mi, int64_t ldm,
+                               void* G, int64_t ldg, void* ws, int64_t ws_bytes, void* stream);
 /* the bf16 GEMM writing C slice-major (bf16, 128-column slices):
  * element (r, c) at Cs[(c/128)*sstride + r*128 + c%128], sstride % 128 == 0, >= M*128 */
 int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

@@ -153,7 +153,7 @@ def test_mlp_chain_vs_per_layer(device, dtype, M):
 
     def spy(*a):
         out = orig(*a)
-        calls.append(out is not None)
+        calls.append(out is not None and a[3] is not None)  # (from the forward's sign bits)
         return out
 
     def run(fused):
@@ -179,3 +179,26 @@ def test_mlp_chain_vs_per_layer(device, dtype, M):
             assert rel_err(a.float().cpu(), b.float().cpu()) < tol, nm
         else:
             assert torch.equal(a, b), nm
+
+
+def test_relu_mask_bits_and_dmask_forms(device):
+    """gemm_relu_mask: y bit-identical to the relu GEMM, the sign bits = (y > 0) in the documented
+    layout (byte 20 t + 4 u + g of a row: columns 160 t + 32 u + 8 g + 0..7); gemm_dmask from the
+    bits = from y = the product then act_bwd, bit for bit (ragged rows, N = 300 in two tiles)."""
+    from gnnea import _lib, ops
+    g0 = torch.Generator(device=device).manual_seed(9)
+    M = 70001
+    x = torch.randn(M, 300, device=device, generator=g0).bfloat16()
+    W = (torch.randn(300, 300, device=device, generator=g0) / 17).bfloat16()
+    b = (0.1 * torch.randn(300, device=device, generator=g0)).bfloat16()
+    y, mask = ops.gemm_relu_mask(x, W, b)
+    assert torch.equal(y, ops.gemm(x, W, trans_b=True, bias=b, act=_lib.GNNEA_ACT_RELU))
+    cols = torch.arange(300, device=device)
+    byte = 20 * (cols // 160) + (cols % 160) // 8
+    bits = (mask[:, byte] >> (cols % 8).to(torch.uint8)) & 1
+    assert torch.equal(bits.bool(), y > 0)
+    dy = torch.randn(M, 300, device=device, generator=g0).bfloat16()
+    W2 = (torch.randn(300, 300, device=device, generator=g0) / 17).bfloat16()
+    ref = ops.act_bwd(ops.gemm(dy, W2), y, _lib.GNNEA_ACT_RELU)
+    assert torch.equal(ops.gemm_dmask(dy, W2, y), ref)
+    assert torch.equal(ops.gemm_dmask(dy, W2, y, mask), ref)
