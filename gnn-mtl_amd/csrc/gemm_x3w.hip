@@ -329,7 +329,12 @@ __global__ __launch_bounds__(256) void k_pack_f16x2(const float* __restrict__ B,
 // CHUNKS of up to 10 steps, each with its own row scale and accumulators (K = 600: two): a
 // chunk's 20 raw quads are split whole once they have landed, and the next chunk's (this tile's
 // or the next tile's first) are issued into the freed registers, one chunk of MFMAs ahead.
-template <int KC, int NC, int CH, int NW>
+// Epilogue modes EP (the relu Linear's masked backward, as gemm_bf16.hip's k_gemm_bf16w):
+//  3 relu as mode 0, and the sign bits of the stored output -> Mo: per row and column tile 16 bytes,
+//    byte 2 jn + h holding columns 16 jn + 8 h + 0..7 of the tile (bit e: column + e > 0);
+//  2 the stored value is acc * relu'(y) with relu'(y) from those bits (Mi), read with the tile's
+//    last chunk, before the next tile's activations are issued.
+template <int KC, int NC, int CH, int NW, int EP = 0>
 __global__ __launch_bounds__(64 * NW) void k_gemm_f16x2_ring(int M, int N, int K, int ntn,
                                                          const float* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ P,
@@ -337,8 +342,12 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_f16x2_ring(int M, int N, int K
                                                          const float* __restrict__ bias,
                                                          float* __restrict__ C, int64_t ldc,
                                                          int64_t cs, float* __restrict__ C2,
-                                                         int64_t cs2, float beta, int relu) {
+                                                         int64_t cs2, float beta, int relu,
+                                                         const uint8_t* __restrict__ Mi = nullptr,
+                                                         uint8_t* __restrict__ Mo = nullptr,
+                                                         int64_t ldm = 0) {
   constexpr int BM = 16 * NW, NJ = NC / 16;
+  static_assert(EP == 0 || NJ <= 8, "sign bits: 16 bytes per row and tile");
   constexpr int PL = KC * 4 * NC;           // 16-B units per plane of a tile
   constexpr int NCH = (KC + CH - 1) / CH;   // k-chunks of CH steps
   static_assert(NC % 16 == 0, "tile shape");
@@ -388,6 +397,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_f16x2_ring(int M, int N, int K
     // activations (the 80 / 112-column forms have no registers to spare: C read in the epilogue)
     constexpr bool CAHEAD = KC > 10;
     float4 cv[CAHEAD ? NJ : 1];
+    uint4 mk;  // EP 2: the row's sign bytes of this column tile
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int s0 = CH * c, ns = KC - s0 < CH ? KC - s0 : CH;
@@ -440,6 +450,10 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_f16x2_ring(int M, int N, int K
           cv[jn] = *(const float4*)(C + ((int64_t)(nn >> 6) * cs + (int64_t)mm * ldc + (nn & 63)));
         }
       }
+      if constexpr (EP == 2) {
+        if (c == NCH - 1)
+          mk = *(const uint4*)(Mi + (int64_t)min(rt * BM + w * 16 + ml, M - 1) * ldm + nt * 16);
+      }
       // the next chunk's activations, a chunk of MFMAs ahead (past the last tile: none)
       // (unconditional, past the last tile the last tile again: the same outstanding-load
       // count on every path, so the compiler's waits never cover the loads in flight)
@@ -491,6 +505,7 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_f16x2_ring(int M, int N, int K
     const float rinv = f2_pow2(er - 14);
     const int m = rt * BM + w * 16 + ml;
     if (m < M) {
+      uint32_t nb = 0;  // EP 3: the sign nibbles, column block jn at bits 4 jn
 #pragma unroll
       for (int jn = 0; jn < NJ; ++jn) {
         const int c = 16 * jn + 4 * kq;
@@ -508,9 +523,45 @@ __global__ __launch_bounds__(64 * NW) void k_gemm_f16x2_ring(int M, int N, int K
             const float4 c4 = CAHEAD ? cv[CAHEAD ? jn : 0] : *cp;
             o.x += beta * c4.x; o.y += beta * c4.y; o.z += beta * c4.z; o.w += beta * c4.w;
           }
+          if constexpr (EP == 2) {  // o * relu'(y): act_bwd's G on the stored product
+            const uint32_t wd = jn >> 1 == 0 ? mk.x : (jn >> 1 == 1 ? mk.y : (jn >> 1 == 2 ? mk.z : mk.w));
+            const uint32_t bits = wd >> (8 * (2 * (jn & 1) + (kq >> 1)) + 4 * (kq & 1));
+            o.x *= (bits & 1u) ? 1.f : 0.f;
+            o.y *= (bits & 2u) ? 1.f : 0.f;
+            o.z *= (bits & 4u) ? 1.f : 0.f;
+            o.w *= (bits & 8u) ? 1.f : 0.f;
+          }
           if (relu) o = f4_relu(o);
           *cp = o;
           if (C2) *(float4*)(C2 + ((int64_t)(n >> 6) * cs2 + (int64_t)m * 64 + (n & 63))) = o;
+          if constexpr (EP == 3)
+            nb |= ((o.x > 0.f ? 1u : 0u) | (o.y > 0.f ? 2u : 0u) | (o.z > 0.f ? 4u : 0u) |
+                   (o.w > 0.f ? 8u : 0u)) << (4 * jn);
+        }
+      }
+      if constexpr (EP == 3) {
+        // byte 2 jn + h = the nibbles of kq = 2 h (low) and 2 h + 1 (high): partners lane ^ 16,
+        // then the two h halves (lane ^ 32) meet in the kq = 0 lane, which stores the 16 bytes
+        const uint32_t p1 = __shfl_xor(nb, 16);
+        const uint32_t lo = (kq & 1) ? p1 : nb, hi = (kq & 1) ? nb : p1;
+        uint32_t bl = 0, bh = 0;  // this h's bytes, jn 0..3 and 4..7
+#pragma unroll
+        for (int jn = 0; jn < NJ; ++jn) {
+          const uint32_t by = ((lo >> (4 * jn)) & 15u) | (((hi >> (4 * jn)) & 15u) << 4);
+          if (jn < 4) bl |= by << (8 * jn);
+          else bh |= by << (8 * (jn - 4));
+        }
+        const uint32_t ql = __shfl_xor(bl, 32), qh = __shfl_xor(bh, 32);
+        if (kq == 0) {  // (h = 0: own bytes B0, the partner's B1)
+          uint32_t d[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t s0 = q < 2 ? bl : bh, s1 = q < 2 ? ql : qh;
+            const int sh = 16 * (q & 1);
+            d[q] = ((s0 >> sh) & 255u) | (((s1 >> sh) & 255u) << 8) |
+                   (((s0 >> (sh + 8)) & 255u) << 16) | (((s1 >> (sh + 8)) & 255u) << 24);
+          }
+          *(uint4*)(Mo + (int64_t)m * ldm + nt * 16) = make_uint4(d[0], d[1], d[2], d[3]);
         }
       }
     }
@@ -605,7 +656,8 @@ static int ring_grid(int ntn, int64_t M, int bm) {
 static int f16x2_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                         const float* B, int64_t ldb, const float* bias, float* C, int64_t ldc,
                         int64_t cs, float* C2, int64_t cs2, void* ws, int64_t ws_bytes,
-                        hipStream_t s, float beta, int relu) {
+                        hipStream_t s, float beta, int relu, int ep = 0,
+                        const uint8_t* Mi = nullptr, uint8_t* Mo = nullptr, int64_t ldm = 0) {
   int kc, nc;
   if (!f16x2_k(K, &kc, &nc)) return GNNEA_EINVAL;
   if (ws_bytes < f16x2_ws_bytes(N, kc, nc)) return GNNEA_EWORKSPACE;
@@ -630,7 +682,17 @@ static int f16x2_launch(int trans_b, int64_t M, int64_t N, int64_t K, const floa
   hipLaunchKernelGGL((k_gemm_f16x2_ring<KC_, NC_, CH_, NW_>), dim3(ring_grid(ntn, M, 16 * NW_)), \
                      dim3(64 * NW_), 0, s, (int)M, (int)N, (int)K, ntn, A, lda,                \
                      (const uint16_t*)ws, (const float*)tinv, bias, C, ldc, cs, C2, cs2, beta, relu)
-  if (kc == W3_KC) {
+  if (ep != 0) {  // (f16x2_mask_applies: kc == W3_KC, ntn < 4)
+    const dim3 g(ring_grid(ntn, M, 16 * 8)), bl(64 * 8);
+    if (ep == 2)
+      hipLaunchKernelGGL((k_gemm_f16x2_ring<W3_KC, F2_NC, 5, 8, 2>), g, bl, 0, s, (int)M, (int)N,
+                         (int)K, ntn, A, lda, (const uint16_t*)ws, (const float*)tinv, bias, C, ldc,
+                         cs, C2, cs2, beta, relu, Mi, nullptr, ldm);
+    else
+      hipLaunchKernelGGL((k_gemm_f16x2_ring<W3_KC, F2_NC, 5, 8, 3>), g, bl, 0, s, (int)M, (int)N,
+                         (int)K, ntn, A, lda, (const uint16_t*)ws, (const float*)tinv, bias, C, ldc,
+                         cs, C2, cs2, beta, relu, nullptr, Mo, ldm);
+  } else if (kc == W3_KC) {
     if (ntn >= 4) GNNEA_F2R(W3_KC, F2_NC, 3, 16);
     else GNNEA_F2R(W3_KC, F2_NC, 5, 8);
   } else {
@@ -639,6 +701,27 @@ static int f16x2_launch(int trans_b, int64_t M, int64_t N, int64_t K, const floa
 #undef GNNEA_F2R
   GNNEA_LAUNCH_CHECK();
   return 0;
+}
+
+int64_t f16x2_mask_ld(int64_t N) { return 16 * ((N + F2_NC - 1) / F2_NC); }
+
+bool f16x2_mask_applies(int64_t M, int64_t N, int64_t K, int64_t lda, const void* A, int64_t ldc,
+                        const void* C) {
+  int kc, nc;
+  return x3w_mode() == 4 && f16x2_k(K, &kc, &nc) && kc == W3_KC && (N + F2_NC - 1) / F2_NC < 4 &&
+         gemm_x3w_applies(0, M, N, K, lda, A, 0.f, ldc, 64, C, nullptr, 0, GNNEA_ACT_RELU);
+}
+
+int f16x2_mask_launch(int ep, int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                      int64_t lda, const float* B, int64_t ldb, const float* bias, float* C,
+                      int64_t ldc, const uint8_t* Mi, uint8_t* Mo, int64_t ldm, void* ws,
+                      int64_t ws_bytes, hipStream_t s) {
+  if ((ep != 2 && ep != 3) || !f16x2_mask_applies(M, N, K, lda, A, ldc, C) ||
+      ldm < f16x2_mask_ld(N) || ldm % 16 || ((uintptr_t)(ep == 2 ? (const void*)Mi : Mo) & 15))
+    return GNNEA_EINVAL;
+  if (!ws || ws_bytes < gemm_x3w_ws_bytes(N)) return GNNEA_EWORKSPACE;
+  return f16x2_launch(trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, 64, nullptr, 0, ws, ws_bytes,
+                      s, 0.f, ep == 3 ? 1 : 0, ep, Mi, Mo, ldm);
 }
 
 int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
@@ -668,3 +751,49 @@ int gemm_x3w_launch(int trans_b, int64_t M, int64_t N, int64_t K, const float* A
 }
 
 }  // namespace gnnea
+
+// ---- C-ABI: the fp32 relu Linear's sign bits (gnnea.h) ----
+using namespace gnnea;
+
+extern "C" int gnnea_gemm_f32_mask_applies(int64_t M, int64_t N, int64_t K, int64_t lda,
+                                           int64_t ldc) {
+  const void* dummy = (const void*)(uintptr_t)256;  // (alignment is checked on the real call)
+  return M > 0 && f16x2_mask_applies(M, N, K, lda, dummy, ldc, dummy) ? 1 : 0;
+}
+
+extern "C" int64_t gnnea_gemm_f32_mask_ld(int64_t N) {
+  if (N < 0) return GNNEA_EINVAL;
+  return f16x2_mask_ld(N);
+}
+
+extern "C" int64_t gnnea_gemm_f32_mask_ws_bytes(int64_t N) {
+  if (N < 0) return GNNEA_EINVAL;
+  return gemm_x3w_ws_bytes(N);
+}
+
+// C = relu(A·op(B) + bias) (bit-identical to gnnea_gemm_x3_act_f32's relu on this kernel) and the
+// sign bits of C (16 bytes per row and 112-column tile: byte 16 t + 2 j + h holds columns
+// 112 t + 16 j + 8 h + 0..7, bit e set where that column's value > 0)
+extern "C" int gnnea_gemm_f32_relu_mask(int trans_b, int64_t M, int64_t N, int64_t K,
+                                        const float* A, int64_t lda, const float* B, int64_t ldb,
+                                        const float* bias, float* C, int64_t ldc, void* Mo,
+                                        int64_t ldm, void* ws, int64_t ws_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  if (M == 0 || N == 0) return 0;
+  if (!A || !B || !C || !Mo || (trans_b ? ldb < K : ldb < N)) return GNNEA_EINVAL;
+  return f16x2_mask_launch(3, trans_b, M, N, K, A, lda, B, ldb, bias, C, ldc, nullptr,
+                           (uint8_t*)Mo, ldm, ws, ws_bytes, (hipStream_t)stream);
+}
+
+// G = (A·op(B)) * relu'(y), relu'(y) from gnnea_gemm_f32_relu_mask's bits of y: bit-identical to
+// gnnea_gemm_x3_f32 followed by gnnea_act_bwd_colsum_f32's G
+extern "C" int gnnea_gemm_f32_dmask_bits(int trans_b, int64_t M, int64_t N, int64_t K,
+                                         const float* A, int64_t lda, const float* B, int64_t ldb,
+                                         const void* Mi, int64_t ldm, float* G, int64_t ldg,
+                                         void* ws, int64_t ws_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  if (M == 0 || N == 0) return 0;
+  if (!A || !B || !G || !Mi || (trans_b ? ldb < K : ldb < N)) return GNNEA_EINVAL;
+  return f16x2_mask_launch(2, trans_b, M, N, K, A, lda, B, ldb, nullptr, G, ldg,
+                           (const uint8_t*)Mi, nullptr, ldm, ws, ws_bytes, (hipStream_t)stream);
+}

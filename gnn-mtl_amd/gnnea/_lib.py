@@ -182,6 +182,13 @@ SIGNATURES = {
                                                  _i64, _p, _p, _i64, _p, _i64, _p, _i64, _p]),
     "gnnea_gemm_bf16_dmask_bits": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
                                                   _i64, _p, _i64, _p, _i64, _p, _i64, _p]),
+    "gnnea_gemm_f32_mask_applies": (ctypes.c_int, [_i64, _i64, _i64, _i64, _i64]),
+    "gnnea_gemm_f32_mask_ld": (_i64, [_i64]),
+    "gnnea_gemm_f32_mask_ws_bytes": (_i64, [_i64]),
+    "gnnea_gemm_f32_relu_mask": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
+                                                _i64, _p, _p, _i64, _p, _i64, _p, _i64, _p]),
+    "gnnea_gemm_f32_dmask_bits": (ctypes.c_int, [ctypes.c_int, _i64, _i64, _i64, _p, _i64, _p,
+                                                 _i64, _p, _i64, _p, _i64, _p, _i64, _p]),
     "gnnea_gemm_bf16_act": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64,
                                            _p, _i64, _p, ctypes.c_int, _p, _i64, ctypes.c_int, _p,
                                            _i64, _p]),

@@ -435,10 +435,35 @@ def act_bwd_colsum(dy, y, act, want_db=True):
     return g, db
 
 
+def _f32_mask_ok(M, N, K, lda, ldc, *ts):
+    return (_use_x3(M, N, K, None) and all(t.data_ptr() % 16 == 0 for t in ts)
+            and bool(_lib.lib().gnnea_gemm_f32_mask_applies(M, N, K, lda, ldc)))
+
+
 def gemm_relu_mask(x, weight, bias):
-    """(relu(x Wᵀ + b), sign bits) in one pass (gnnea_gemm_bf16_relu_mask: the output bit-identical
-    to gemm(..., act=relu), plus 1 bit per element for gemm_dmask), or None where the bf16
-    weight-resident kernel does not apply."""
+    """(relu(x Wᵀ + b), sign bits) in one pass (gnnea_gemm_{bf16,f32}_relu_mask: the output
+    bit-identical to gemm(..., act=relu), plus 1 bit per element for gemm_dmask), or None where
+    the weight-resident kernel that gemm would run does not apply."""
+    if x.dtype == torch.float32 and weight.dtype == torch.float32:
+        x, weight = _rows(x), _rows(weight)
+        M, K = x.shape
+        N = weight.shape[0]
+        if weight.shape[1] != K:
+            raise ValueError("gnnea.gemm_relu_mask: shape mismatch")
+        if not _f32_mask_ok(M, N, K, _ld(x), N, x):
+            return None
+        L = _lib.lib()
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        ldm = int(L.gnnea_gemm_f32_mask_ld(N))
+        mask = torch.empty((M, ldm), dtype=torch.uint8, device=x.device)
+        b = _featc(bias, torch.float32) if bias is not None else None
+        ws_bytes = int(L.gnnea_gemm_f32_mask_ws_bytes(N))
+        ws = _gemm_ws(x.device, ws_bytes)
+        with _lib.on_device(x.device):
+            check(L.gnnea_gemm_f32_relu_mask(1, M, N, K, ptr(x), _ld(x), ptr(weight), _ld(weight),
+                                             ptr(b), ptr(y), N, ptr(mask), ldm, ptr(ws), ws_bytes,
+                                             stream_of(x.device)))
+        return y, mask
     if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
         return None
     x, weight = _rows(x), _rows(weight)
@@ -468,7 +493,26 @@ def gemm_dmask(g, weight, y, mask=None):
     gradient into a relu Linear's output y, masked in its epilogue -- bit-identical to gemm
     followed by act_bwd's G; with ``mask``, gemm_relu_mask's sign bits of y, read instead of y:
     gnnea_gemm_bf16_dmask_bits), or None where that kernel does not apply (then the caller runs
-    the two steps)."""
+    the two steps).  fp32: from the sign bits only (gnnea_gemm_f32_dmask_bits)."""
+    if g.dtype == torch.float32 and weight.dtype == torch.float32 and y.dtype == torch.float32:
+        if mask is None:
+            return None
+        g, weight = _rows(g), _rows(weight)
+        M, K = g.shape
+        N = weight.shape[1]
+        if weight.shape[0] != K or y.shape != (M, N):
+            raise ValueError("gnnea.gemm_dmask: shape mismatch")
+        if not _f32_mask_ok(M, N, K, _ld(g), N, g, mask):
+            return None
+        L = _lib.lib()
+        out = torch.empty((M, N), dtype=torch.float32, device=g.device)
+        ws_bytes = int(L.gnnea_gemm_f32_mask_ws_bytes(N))
+        ws = _gemm_ws(g.device, ws_bytes)
+        with _lib.on_device(g.device):
+            check(L.gnnea_gemm_f32_dmask_bits(0, M, N, K, ptr(g), _ld(g), ptr(weight), _ld(weight),
+                                              ptr(mask), mask.stride(0), ptr(out), N, ptr(ws),
+                                              ws_bytes, stream_of(g.device)))
+        return out
     if g.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 or y.dtype != torch.bfloat16:
         return None
     g, weight, y = _rows(g), _rows(weight), _rows(y)

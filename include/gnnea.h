@@ -553,6 +553,23 @@ int gnnea_gemm_bf16_relu_mask(int trans_b, int64_t M, int64_t N, int64_t K, cons
 int gnnea_gemm_bf16_dmask_bits(int trans_b, int64_t M, int64_t N, int64_t K, const void* A,
                                int64_t lda, const void* B, int64_t ldb, const void* Mi, int64_t ldm,
                                void* G, int64_t ldg, void* ws, int64_t ws_bytes, void* stream);
+/* The fp32 forms of the relu Linear's sign bits (the f16x2 weight-resident ring, K in (288, 320],
+ * N <= 336, tall M: gnnea_gemm_f32_mask_applies; workspace gnnea_gemm_f32_mask_ws_bytes):
+ * gnnea_gemm_f32_relu_mask = gnnea_gemm_x3_act_f32 with relu, bit for bit, plus the bits (byte
+ * 16 t + 2 j + h of a row: columns 112 t + 16 j + 8 h + 0..7; ldm >= gnnea_gemm_f32_mask_ld(N),
+ * % 16 == 0, 16-B aligned); gnnea_gemm_f32_dmask_bits = the product times relu'(y) from them
+ * (= gnnea_gemm_x3_f32 then gnnea_act_bwd_colsum_f32's G, bit for bit). */
+int gnnea_gemm_f32_mask_applies(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldc);
+int64_t gnnea_gemm_f32_mask_ld(int64_t N);
+int64_t gnnea_gemm_f32_mask_ws_bytes(int64_t N);
+int gnnea_gemm_f32_relu_mask(int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                             int64_t lda, const float* B, int64_t ldb, const float* bias, float* C,
+                             int64_t ldc, void* Mo, int64_t ldm, void* ws, int64_t ws_bytes,
+                             void* stream);
+int gnnea_gemm_f32_dmask_bits(int trans_b, int64_t M, int64_t N, int64_t K, const float* A,
+                              int64_t lda, const float* B, int64_t ldb, const void* Mi,
+                              int64_t ldm, float* G, int64_t ldg, void* ws, int64_t ws_bytes,
+                              void* stream);
 /* the bf16 GEMM writing C slice-major (bf16, 128-column slices):
  * element (r, c) at Cs[(c/128)*sstride + r*128 + c%128], sstride % 128 == 0, >= M*128 */
 int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

@@ -131,13 +131,14 @@ def test_act_bwd_colsum_vs_fp64(device, n, D, ld, dtype):
 
 @pytest.mark.parametrize("dtype,M", [(torch.bfloat16, 70000),   # masked backward products
                                      (torch.bfloat16, 1000),    # small: the two-step fallback
-                                     (torch.float32, 70000)])   # fp32: the two-step fallback
+                                     (torch.float32, 70000),    # fp32: the ring's sign bits
+                                     (torch.float32, 1000)])    # fp32 small: two steps
 def test_mlp_chain_vs_per_layer(device, dtype, M):
     """MLPDecoder's three Linear layers (relu, relu, identity; models/decoders.py) as one
     MLPChainFn against the per-layer LinearActFn / LinearFn path: output, dx and every dW bit
     for bit (gemm_dmask's masked product = the product then act_bwd's G), db to 1e-6 (the same
     values summed in another order; bf16 biases round each sum) -- and the fused path is the one
-    that ran (bf16, tall)."""
+    that ran (tall)."""
     import torch.nn as nn
     from gnnea import ops
     from layers.layers import Linear
@@ -171,7 +172,7 @@ def test_mlp_chain_vs_per_layer(device, dtype, M):
     finally:
         mp.undo()
     ref = run(False)
-    assert calls == [dtype == torch.bfloat16 and M >= 65536] * 2
+    assert calls == [M >= 65536] * 2
     names = ["y", "dx", "dW0", "db0", "dW1", "db1", "dW2", "db2"]
     for nm, a, b in zip(names, got, ref):
         if nm.startswith("db"):  # (bf16 biases: each sum rounded to bf16, a 2^-8 step apart)
@@ -201,4 +202,27 @@ def test_relu_mask_bits_and_dmask_forms(device):
     W2 = (torch.randn(300, 300, device=device, generator=g0) / 17).bfloat16()
     ref = ops.act_bwd(ops.gemm(dy, W2), y, _lib.GNNEA_ACT_RELU)
     assert torch.equal(ops.gemm_dmask(dy, W2, y), ref)
+    assert torch.equal(ops.gemm_dmask(dy, W2, y, mask), ref)
+
+
+def test_relu_mask_bits_f32(device):
+    """The fp32 forms (the f16x2 ring's epilogue): y bit-identical to the relu GEMM, the bits =
+    (y > 0) in the documented layout (byte 16 t + 2 j + h: columns 112 t + 16 j + 8 h + 0..7),
+    gemm_dmask from them = the product then act_bwd, bit for bit (ragged rows, three tiles)."""
+    from gnnea import _lib, ops
+    g0 = torch.Generator(device=device).manual_seed(10)
+    M = 70001
+    x = torch.randn(M, 300, device=device, generator=g0)
+    W = torch.randn(300, 300, device=device, generator=g0) / 17
+    b = 0.1 * torch.randn(300, device=device, generator=g0)
+    y, mask = ops.gemm_relu_mask(x, W, b)
+    assert torch.equal(y, ops.gemm(x, W, trans_b=True, bias=b, act=_lib.GNNEA_ACT_RELU))
+    cols = torch.arange(300, device=device)
+    byte = 16 * (cols // 112) + (cols % 112) // 8
+    bits = (mask[:, byte] >> (cols % 8).to(torch.uint8)) & 1
+    assert torch.equal(bits.bool(), y > 0)
+    dy = torch.randn(M, 300, device=device, generator=g0)
+    W2 = torch.randn(300, 300, device=device, generator=g0) / 17
+    ref = ops.act_bwd(ops.gemm(dy, W2), y, _lib.GNNEA_ACT_RELU)
+    assert ops.gemm_dmask(dy, W2, y) is None  # (fp32: from the bits only)
     assert torch.equal(ops.gemm_dmask(dy, W2, y, mask), ref)
