@@ -554,7 +554,8 @@ class MLPChainFn(torch.autograd.Function):
         for k, act in enumerate(acts):
             w, b = params[2 * k], params[2 * k + 1]
             a = act if act == _lib.GNNEA_ACT_RELU else None
-            ym = gemm_relu_mask(ys[-1], w, b) if a is not None and k + 1 < len(acts) else None
+            ym = gemm_relu_mask(ys[-1], w, b) if a is not None and k + 1 < len(acts) and \
+                any(ctx.needs_input_grad) else None  # (the sign bits only for a backward)
             ys.append(ym[0] if ym is not None else gemm(ys[-1], w, trans_b=True, bias=b, act=a))
             masks.append(ym[1] if ym is not None else None)
         ctx.acts = tuple(acts)

@@ -1,12 +1,12 @@
 #!/bin/bash
-# MLP decoder as one autograd node (masked backward products): tests, cfg-5 GAT-EA step, kernel stats
+# MLP decoder: forward sign bits for the masked backward products: tests, cfg-5 GAT-EA step, kernel stats
 set -u
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
-O=$R/gpurun_out/s33
+O=$R/gpurun_out/s34
 mkdir -p "$O"
 cd "$R"
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_act.py tests/test_gpu_bf16.py tests/test_gpu_scale_cfg5.py tests/test_gpu_parity.py tests/test_gpu_dist_ea.py tests/test_gpu_scale_dbp15k.py tests/test_gpu_scale_cfg4.py > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
+  tests/test_gpu_act.py tests/test_gpu_bf16.py tests/test_gpu_scale_cfg5.py tests/test_gpu_dist_ea.py > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
 tail -1 "$O/tests.log"
 timeout -k 10 400 python -u tools/dist_step.py --model GAT --dtype bf16 --entities 2000000 --steps 21 --warmup 3 > "$O/gat5.log" 2>&1 || { tail -5 "$O/gat5.log"; exit 1; }
 grep -o '"ms_per_step": [0-9.]*' "$O/gat5.log" | head -1
