@@ -982,6 +982,16 @@ static int gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, c
   return 0;
 }
 
+// db[m] = sum over the splits' partial column sums, in split order
+__global__ void k_db_reduce(int M, int splits, const float* __restrict__ part,
+                            float* __restrict__ db) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  float a = 0.f;
+  for (int q = 0; q < splits; ++q) a += part[(int64_t)q * M + m];
+  db[m] = a;
+}
+
 extern "C" int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                               const float* A, int64_t lda, const float* B, int64_t ldb,
                               const float* bias, float beta, float* C, int64_t ldc, void* ws,
@@ -1258,6 +1268,46 @@ extern "C" int64_t gnnea_gemm_x3t_ws_bytes(int64_t M, int64_t N, int64_t K) {
 extern "C" int64_t gnnea_gemm_x3_ws_bytes(int64_t M, int64_t N, int64_t K) {
   if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
   return x3_planes_bytes(N, K) + pick_splits(M, N, K, INT64_MAX / 2) * M * N * 4;
+}
+
+extern "C" int gnnea_gemm_x3_ta_db_applies(int64_t M, int64_t N, int64_t K, int64_t lda,
+                                           int64_t ldb) {
+  const void* dummy = (const void*)(uintptr_t)256;  // (alignment is checked on the real call)
+  return gemm_ta_db_applies(M, N, K, lda, ldb, dummy, dummy) ? 1 : 0;
+}
+
+extern "C" int64_t gnnea_gemm_x3_ta_db_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  if (M < 0 || N < 0 || K < 0) return GNNEA_EINVAL;
+  return gemm_ta_db_ws_bytes(M, N, K);
+}
+
+// The weight and bias gradients of one Linear-like layer in one pass over its output gradient:
+// C = Aᵀ·B (A [K][M] = dh, B [K][N] = x; gnnea_gemm_x3_f32's trans_a product, the same kernel and
+// values) and db = column sums of A (fp32 [M]), from the kernel's ones column in B's tile padding
+// (N % 160 != 0; gnnea_gemm_x3_ta_db_applies).  Replaces gnnea_colsum_f32's separate pass over A.
+extern "C" int gnnea_gemm_x3_ta_db_f32(int64_t M, int64_t N, int64_t K, const float* A,
+                                       int64_t lda, const float* B, int64_t ldb, float* C,
+                                       int64_t ldc, float* db, void* ws, int64_t ws_bytes,
+                                       void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C || !db || ldc < N) return GNNEA_EINVAL;
+  if (M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return GNNEA_EINVAL;
+  if (!gemm_ta_db_applies(M, N, K, lda, ldb, A, B)) return GNNEA_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  float* slab = nullptr;
+  float* dbslab = nullptr;
+  int used = 0;
+  const int rc = gemm_ta_launch<float>(M, N, K, A, lda, B, ldb, ws, ws ? ws_bytes : 0, s, &slab,
+                                       &used, &dbslab);
+  if (rc) return rc;
+  const int64_t n = M * N;
+  const int nb = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  hipLaunchKernelGGL(k_gemm_reduce, dim3(nb), dim3(256), 0, s, (int)M, (int)N, used, slab,
+                     nullptr, 0.f, C, ldc, (int64_t)64);
+  GNNEA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_db_reduce, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, (int)M, used,
+                     dbslab, db);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
 }
 
 // fp32 GEMM through three-way bf16 splits on the bf16 MFMA (k_gemm_x3); workspace from

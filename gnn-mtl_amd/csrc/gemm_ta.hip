@@ -296,6 +296,9 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta(int M, int N, int K,
 // LDS reads are inline asm (hipcc would wait vmcnt(0) for the in-flight DMA before plain ones)
 // with explicit lgkmcnt waits.  Rows past a split's end are DMA'd from its last row and zeroed in
 // registers (one uniform branch, last step only).
+// dbslab != null (the bias gradient of the same layer, db = column sums of A): B's padding column
+// N (N < the tile width) is read as ones, so output column N is sum_k A[k][m] (the x3 split of 1
+// is exact: h = 1, m = l = 0) -> dbslab[split][m]; one wave's one column block, a uniform branch.
 constexpr int TD_RSA = 1280, TD_RSB = 640;                   // image row strides (bytes)
 constexpr int TD_IMG_A = TA_BK * TD_RSA, TD_IMG_B = TA_BK * TD_RSB;
 constexpr int TD_STAGE = TD_IMG_A + TD_IMG_B;                // 61,440 B
@@ -347,7 +350,8 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
                                                           int64_t lda,
                                                           const float* __restrict__ B,
                                                           int64_t ldb, int kps, int tiles_n,
-                                                          float* __restrict__ slab) {
+                                                          float* __restrict__ slab,
+                                                          float* __restrict__ dbslab) {
   __shared__ __attribute__((aligned(1024))) unsigned char smem[2 * TD_STAGE];
   const int t_id = xcd_remap(blockIdx.x, gridDim.x);
   const int tn = t_id % tiles_n, split = t_id / tiles_n;
@@ -403,6 +407,10 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
   // fragment read addresses (stage 0): lane l -> column l % 16 of a 16-wide tile, rows
   // 8 (l / 16) + e; chunk (col / 4) ^ (4 * ((l / 16) & 1)), dword col % 4
   const int g = lane >> 4, cl = lane & 15;
+  // the ones column: this wave's column block jdb (uniform, -1: none) and its lane
+  const int nrel = N - n0 - wn * 80;
+  const int jdb = dbslab && nrel >= 0 && nrel < 80 ? nrel / 16 : -1;
+  const bool ones_lane = jdb >= 0 && cl == nrel % 16;
   const uint32_t base = lds_addr(smem);
   uint32_t a_ad[5], b_ad[5];
 #pragma unroll
@@ -450,6 +458,10 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
 #pragma unroll
         for (int e = 0; e < 8; ++e) xb[e] = e < kval ? xb[e] : 0.f;
       }
+      if (j == jdb) {  // (uniform)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xb[e] = ones_lane ? (tail && e >= kval ? 0.f : 1.f) : xb[e];
+      }
       const TdTriple bt = td_split(xb);
       if (j + 1 < 5) td_read8<TD_RSB>(b_ad[j + 1] + so, xb);  // in flight under the MFMAs
       // product-major: five independent accumulators between two dependent MFMAs (each
@@ -481,7 +493,16 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta_x3d(int M, int N, int K,
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       const int n = n0 + wn * 80 + 16 * j + (lane & 15);
-      if (n >= N) continue;
+      if (n >= N) {
+        if (j == jdb && ones_lane) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = wm * 80 + 16 * i + 4 * (lane >> 4) + r;
+            if (m < M) dbslab[(int64_t)split * M + m] = acc[i][j][r];
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = wm * 80 + 16 * i + 4 * (lane >> 4) + r;
@@ -515,23 +536,39 @@ int64_t gemm_ta_ws_bytes(int64_t M, int64_t N, int64_t K) {
   return (int64_t)ta_splits(M, N, K, INT64_MAX / 4) * M * N * 4;
 }
 
+bool gemm_ta_db_applies(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* A,
+                        const void* B) {
+  return gemm_ta_applies(M, N, K, lda, ldb, A, B, 4) && N % TA_NP != 0;
+}
+
+int64_t gemm_ta_db_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  return (int64_t)ta_splits(M, N + 1, K, INT64_MAX / 4) * M * (N + 1) * 4;
+}
+
 template <typename T>
 int gemm_ta_launch(int64_t M, int64_t N, int64_t K, const T* A, int64_t lda, const T* B,
                    int64_t ldb, void* ws, int64_t ws_bytes, hipStream_t s, float** slab_out,
-                   int* splits_out) {
-  const int splits = ta_splits(M, N, K, ws ? ws_bytes : 0);
-  if (!ws || ws_bytes < (int64_t)splits * M * N * 4) return GNNEA_EWORKSPACE;
+                   int* splits_out, float** dbslab_out) {
+  // (with the bias column: the slabs, then splits x M partial column sums)
+  const int splits = ta_splits(M, dbslab_out ? N + 1 : N, K, ws ? ws_bytes : 0);
+  if (!ws || ws_bytes < (int64_t)splits * M * (dbslab_out ? N + 1 : N) * 4)
+    return GNNEA_EWORKSPACE;
   const int tiles_n = (int)((N + TA_NP - 1) / TA_NP);
   const int kps = (int)(((K + splits - 1) / splits + TA_BK - 1) / TA_BK * TA_BK);
   // every split must own rows (kps rounding can leave the last ones empty): trim the grid
   const int used = (int)((K + kps - 1) / kps);
   float* slab = (float*)ws;
-  if constexpr (std::is_same<T, float>::value)  // fp32: split at the fragment read
+  float* dbslab = dbslab_out ? slab + (int64_t)splits * M * N : nullptr;
+  if constexpr (std::is_same<T, float>::value) {  // fp32: split at the fragment read
     hipLaunchKernelGGL(k_gemm_ta_x3d, dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M, (int)N,
-                       (int)K, (const float*)A, lda, (const float*)B, ldb, kps, tiles_n, slab);
-  else
+                       (int)K, (const float*)A, lda, (const float*)B, ldb, kps, tiles_n, slab,
+                       dbslab);
+  } else {
+    if (dbslab_out) return GNNEA_EINVAL;  // (the bias column is the fp32 kernel's)
     hipLaunchKernelGGL((k_gemm_ta<T>), dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M, (int)N,
                        (int)K, A, lda, B, ldb, kps, tiles_n, slab);
+  }
+  if (dbslab_out) *dbslab_out = dbslab;
   GNNEA_LAUNCH_CHECK();
   *slab_out = slab;
   *splits_out = used;
@@ -540,8 +577,8 @@ int gemm_ta_launch(int64_t M, int64_t N, int64_t K, const T* A, int64_t lda, con
 
 template int gemm_ta_launch<bf16_t>(int64_t, int64_t, int64_t, const bf16_t*, int64_t,
                                     const bf16_t*, int64_t, void*, int64_t, hipStream_t, float**,
-                                    int*);
+                                    int*, float**);
 template int gemm_ta_launch<float>(int64_t, int64_t, int64_t, const float*, int64_t, const float*,
-                                   int64_t, void*, int64_t, hipStream_t, float**, int*);
+                                   int64_t, void*, int64_t, hipStream_t, float**, int*, float**);
 
 }  // namespace gnnea

@@ -281,9 +281,15 @@ class LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = gemm(dy, weight, out_dtype=x.dtype if bf else None)  # [N,out]·[out,in]
-        if ctx.needs_input_grad[1]:
+        want_w, want_b = ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2]
+        if want_w and want_b and not bf:  # (fp32: dW and db from one pass over dY)
+            r = gemm_ta_db(dy, x)
+            if r is not None:
+                dw, db = r[0], r[1].to(ctx.bias_dtype)
+                want_w = want_b = False
+        if want_w:
             dw = gemm(dy, x, trans_a=True, out_dtype=weight.dtype if bf else None)  # [out,N]·[N,in]
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if want_b:
             db = colsum(dy, ctx.bias_dtype)
         return dx, dw, db
 
@@ -435,6 +441,41 @@ def act_bwd_colsum(dy, y, act, want_db=True):
     return g, db
 
 
+def gemm_ta_db(a, b):
+    """(aᵀ·b, column sums of a) in one pass over a (gnnea_gemm_x3_ta_db_f32: a layer's dW = dhᵀ·x
+    and db = colsum(dh); dW bit-identical to gemm(a, b, trans_a=True)), or None where that
+    kernel is not the one gemm would run (then: gemm + colsum)."""
+    if a.dtype != torch.float32 or b.dtype != torch.float32:
+        return None
+    a, b = _rows(a), _rows(b)
+    K, M = a.shape
+    N = b.shape[1]
+    if b.shape[0] != K:
+        raise ValueError("gnnea.gemm_ta_db: shape mismatch")
+    L = _lib.lib()
+    if not (_use_x3(M, N, K, None, trans_a=True) and
+            L.gnnea_gemm_x3_ta_db_applies(M, N, K, _ld(a), _ld(b)) and
+            a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0):
+        return None
+    out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    db = torch.empty(M, dtype=torch.float32, device=a.device)
+    ws_bytes = int(L.gnnea_gemm_x3_ta_db_ws_bytes(M, N, K))
+    ws = _gemm_ws(a.device, ws_bytes)
+    with _lib.on_device(a.device):
+        check(L.gnnea_gemm_x3_ta_db_f32(M, N, K, ptr(a), _ld(a), ptr(b), _ld(b), ptr(out), N,
+                                        ptr(db), ptr(ws), ws_bytes, stream_of(a.device)))
+    return out, db
+
+
+def _wgrads(dh, x, need_w, need_b):
+    """(dW, db) of a layer h = x Wᵀ + b from dh: one pass when both are wanted (gemm_ta_db)."""
+    if need_w and need_b:
+        r = gemm_ta_db(dh, x)
+        if r is not None:
+            return r
+    return (gemm(dh, x, trans_a=True) if need_w else None), (colsum(dh) if need_b else None)
+
+
 def _f32_mask_ok(M, N, K, lda, ldc, *ts):
     return (_use_x3(M, N, K, None) and all(t.data_ptr() % 16 == 0 for t in ts)
             and bool(_lib.lib().gnnea_gemm_f32_mask_applies(M, N, K, lda, ldc)))
@@ -545,8 +586,10 @@ class MLPChainFn(torch.autograd.Function):
     autograd node, so that the backward can fuse across layers: the product carrying the gradient
     into a relu layer's output y_k masks it in its epilogue (gemm_dmask, reading the sign bits
     the forward product wrote with y_k, gemm_relu_mask), which removes the act_bwd pass over
-    (dy_k, y_k) of the per-layer LinearActFn; db_k is a column sum of the masked gradient.  Forward and every stored value as LinearFn / LinearActFn compute them
-    (same GEMM calls); the bias gradients sum the same values in another order."""
+    (dy_k, y_k) of the per-layer LinearActFn; db_k is a column sum of the masked gradient (fp32:
+    from the weight-gradient product itself, gemm_ta_db).  Forward and every stored value as
+    LinearFn / LinearActFn compute them (same GEMM calls); the bias gradients sum the same values
+    in another order."""
 
     @staticmethod
     def forward(ctx, x, acts, *params):
@@ -579,20 +622,24 @@ class MLPChainFn(torch.autograd.Function):
             x, w, y, act = ys[k], ws[k], ys[k + 1], ctx.acts[k]
             bf = x.dtype == torch.bfloat16 or w.dtype == torch.bfloat16
             want_db = ctx.bias_dtypes[k] is not None and need[3 + 2 * k]
-            db = None
+            db, pend = None, want_db  # (pend: db still to form from g)
             if g is None:
                 if act == _lib.GNNEA_ACT_RELU:
                     d = _featc(d, y.dtype)
                     g, db = act_bwd_colsum(d, y, act, want_db)
+                    pend = False
                 else:
                     g = _featc(d, torch.bfloat16 if bf else torch.float32)
-                    if want_db:
-                        db = colsum(g, ctx.bias_dtypes[k])
-            elif want_db:
-                db = colsum(g, ctx.bias_dtypes[k])
             g = _featc(g, torch.bfloat16 if bf else torch.float32)
-            if need[2 + 2 * k]:
+            need_w = need[2 + 2 * k]
+            if pend and need_w and not bf:
+                r = gemm_ta_db(g, x)
+                if r is not None:
+                    (grads[2 * k], db), need_w, pend = r, False, False
+            if need_w:
                 grads[2 * k] = gemm(g, x, trans_a=True, out_dtype=w.dtype if bf else None)
+            if pend:
+                db = colsum(g, ctx.bias_dtypes[k])
             if db is not None and db.dtype != ctx.bias_dtypes[k]:
                 db = db.to(ctx.bias_dtypes[k])
             grads[2 * k + 1] = db
@@ -919,8 +966,7 @@ class GCNLayerFn(torch.autograd.Function):
         dh = aggregate_t_into(ctx.csr, dy, out, ctx.act)
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         dx = gemm(dh, weight) if need_x else None
-        dw = gemm(dh, x, trans_a=True) if need_w else None
-        db = colsum(dh) if need_b else None
+        dw, db = _wgrads(dh, x, need_w, need_b)
         return dx, dw, db, None, None
 
 
@@ -1262,10 +1308,7 @@ class HighwayLayerFn(torch.autograd.Function):
         if need_x:
             w2 = torch.cat([weight, Kg.t().to(weight.dtype)], dim=0)  # [2D, Din]
             dx = gemm(P, w2, out=dres, beta=1.0)
-        if need_w:
-            dw = gemm(dh, x, trans_a=True)
-        if need_b:
-            db = colsum(dh)
+        dw, db = _wgrads(dh, x, need_w, need_b)
         return dx, dw, db, None, None, None, None
 
 

@@ -570,6 +570,17 @@ int gnnea_gemm_f32_dmask_bits(int trans_b, int64_t M, int64_t N, int64_t K, cons
                               int64_t lda, const float* B, int64_t ldb, const void* Mi,
                               int64_t ldm, float* G, int64_t ldg, void* ws, int64_t ws_bytes,
                               void* stream);
+/* A layer's weight AND bias gradients in one pass over its output gradient: C = Aᵀ·B (A [K][M]
+ * = dh row-major, B [K][N] = x; the gnnea_gemm_x3_f32 trans_a product, same kernel, same values)
+ * and db = column sums of A (fp32 [M]) from a ones column in the kernel's B-tile padding
+ * (N % 160 != 0, M, N <= 320, K >= 128: gnnea_gemm_x3_ta_db_applies; workspace
+ * gnnea_gemm_x3_ta_db_ws_bytes).  Replaces the separate gnnea_colsum_f32 pass (the bias
+ * gradient of layers/layers.py:32,61 under autograd). */
+int gnnea_gemm_x3_ta_db_applies(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
+int64_t gnnea_gemm_x3_ta_db_ws_bytes(int64_t M, int64_t N, int64_t K);
+int gnnea_gemm_x3_ta_db_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                            const float* B, int64_t ldb, float* C, int64_t ldc, float* db,
+                            void* ws, int64_t ws_bytes, void* stream);
 /* the bf16 GEMM writing C slice-major (bf16, 128-column slices):
  * element (r, c) at Cs[(c/128)*sstride + r*128 + c%128], sstride % 128 == 0, >= M*128 */
 int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

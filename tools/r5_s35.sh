@@ -8,11 +8,11 @@ cd "$R"
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
   tests/test_gpu_act.py tests/test_gpu_parity.py tests/test_gpu_scale_cfg4.py tests/test_gpu_scale_dbp15k.py tests/test_gpu_dist_ea.py > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
 tail -1 "$O/tests.log"
-timeout -k 10 300 python -u tools/dbg/no_chain.py --model GAT --steps 15 --warmup 3 > "$O/gat4_nochain.log" 2>&1 || { tail -5 "$O/gat4_nochain.log"; exit 1; }
+timeout -k 10 300 python -u tools/dbg/ab_step.py --off chain --model GAT --steps 15 --warmup 3 > "$O/gat4_nochain.log" 2>&1 || { tail -5 "$O/gat4_nochain.log"; exit 1; }
 grep -o '"ms_per_step": [0-9.]*' "$O/gat4_nochain.log" | head -1
 timeout -k 10 300 python -u tools/dist_step.py --model GAT --steps 15 --warmup 3 > "$O/gat4.log" 2>&1 || { tail -5 "$O/gat4.log"; exit 1; }
 grep -o '"ms_per_step": [0-9.]*' "$O/gat4.log" | head -1
-timeout -k 10 300 python -u tools/dbg/no_chain.py --model GCN --steps 15 --warmup 3 > "$O/gcn4_nochain.log" 2>&1 || { tail -5 "$O/gcn4_nochain.log"; exit 1; }
+timeout -k 10 300 python -u tools/dbg/ab_step.py --off chain --model GCN --steps 15 --warmup 3 > "$O/gcn4_nochain.log" 2>&1 || { tail -5 "$O/gcn4_nochain.log"; exit 1; }
 grep -o '"ms_per_step": [0-9.]*' "$O/gcn4_nochain.log" | head -1
 timeout -k 10 300 python -u tools/dist_step.py --model GCN --steps 15 --warmup 3 > "$O/gcn4.log" 2>&1 || { tail -5 "$O/gcn4.log"; exit 1; }
 grep -o '"ms_per_step": [0-9.]*' "$O/gcn4.log" | head -1
