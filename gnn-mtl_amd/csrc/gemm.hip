@@ -982,16 +982,6 @@ static int gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, c
   return 0;
 }
 
-// db[m] = sum over the splits' partial column sums, in split order
-__global__ void k_db_reduce(int M, int splits, const float* __restrict__ part,
-                            float* __restrict__ db) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  float a = 0.f;
-  for (int q = 0; q < splits; ++q) a += part[(int64_t)q * M + m];
-  db[m] = a;
-}
-
 extern "C" int gnnea_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                               const float* A, int64_t lda, const float* B, int64_t ldb,
                               const float* bias, float beta, float* C, int64_t ldc, void* ws,
@@ -1273,7 +1263,7 @@ extern "C" int64_t gnnea_gemm_x3_ws_bytes(int64_t M, int64_t N, int64_t K) {
 extern "C" int gnnea_gemm_x3_ta_db_applies(int64_t M, int64_t N, int64_t K, int64_t lda,
                                            int64_t ldb) {
   const void* dummy = (const void*)(uintptr_t)256;  // (alignment is checked on the real call)
-  return gemm_ta_db_applies(M, N, K, lda, ldb, dummy, dummy) ? 1 : 0;
+  return gemm_ta_db_applies(M, N, K, lda, ldb, dummy, dummy, 4) ? 1 : 0;
 }
 
 extern "C" int64_t gnnea_gemm_x3_ta_db_ws_bytes(int64_t M, int64_t N, int64_t K) {
@@ -1291,7 +1281,7 @@ extern "C" int gnnea_gemm_x3_ta_db_f32(int64_t M, int64_t N, int64_t K, const fl
                                        void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C || !db || ldc < N) return GNNEA_EINVAL;
   if (M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return GNNEA_EINVAL;
-  if (!gemm_ta_db_applies(M, N, K, lda, ldb, A, B)) return GNNEA_EINVAL;
+  if (!gemm_ta_db_applies(M, N, K, lda, ldb, A, B, 4)) return GNNEA_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   float* slab = nullptr;
   float* dbslab = nullptr;
@@ -1304,10 +1294,7 @@ extern "C" int gnnea_gemm_x3_ta_db_f32(int64_t M, int64_t N, int64_t K, const fl
   hipLaunchKernelGGL(k_gemm_reduce, dim3(nb), dim3(256), 0, s, (int)M, (int)N, used, slab,
                      nullptr, 0.f, C, ldc, (int64_t)64);
   GNNEA_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_db_reduce, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, (int)M, used,
-                     dbslab, db);
-  GNNEA_LAUNCH_CHECK();
-  return 0;
+  return ta_db_reduce(M, used, dbslab, db, s);
 }
 
 // fp32 GEMM through three-way bf16 splits on the bf16 MFMA (k_gemm_x3); workspace from

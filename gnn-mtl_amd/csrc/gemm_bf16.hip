@@ -1376,6 +1376,41 @@ extern "C" int gnnea_gemm_bf16_dmask_bits(int trans_b, int64_t M, int64_t N, int
                             (hipStream_t)stream);
 }
 
+extern "C" int gnnea_gemm_bf16_ta_db_applies(int64_t M, int64_t N, int64_t K, int64_t lda,
+                                             int64_t ldb) {
+  const void* dummy = (const void*)(uintptr_t)256;  // (alignment is checked on the real call)
+  return gemm_ta_db_applies(M, N, K, lda, ldb, dummy, dummy, 2) ? 1 : 0;
+}
+
+// gnnea_gemm_x3_ta_db_f32 for bf16 operands: C = Aᵀ·B (gnnea_gemm_bf16's trans_a product, the
+// same kernel and values; C bf16 or fp32 by c_dtype) and db = column sums of A (fp32 [M]) from
+// the ones column in B's tile padding.  Workspace: gnnea_gemm_x3_ta_db_ws_bytes.
+extern "C" int gnnea_gemm_bf16_ta_db(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                                     const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype,
+                                     float* db, void* ws, int64_t ws_bytes, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C || !db || ldc < N) return GNNEA_EINVAL;
+  if (M >= (1ll << 31) || N >= (1ll << 31) || K >= (1ll << 31)) return GNNEA_EINVAL;
+  if (c_dtype != GNNEA_BF16 && c_dtype != GNNEA_F32) return GNNEA_EINVAL;
+  if (!gemm_ta_db_applies(M, N, K, lda, ldb, A, B, 2)) return GNNEA_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  float* slab = nullptr;
+  float* dbslab = nullptr;
+  int used = 0;
+  const int rc = gemm_ta_launch<bf16_t>(M, N, K, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, ws,
+                                        ws ? ws_bytes : 0, s, &slab, &used, &dbslab);
+  if (rc) return rc;
+  const int64_t nn = M * N;
+  const int nb = (int)((nn + 255) / 256 < 4096 ? (nn + 255) / 256 : 4096);
+  if (c_dtype == GNNEA_BF16)
+    hipLaunchKernelGGL((k_gemm_bf16_reduce<bf16_t>), dim3(nb), dim3(256), 0, s, (int)M, (int)N,
+                       used, slab, nullptr, 0.f, (bf16_t*)C, ldc, (int64_t)128);
+  else
+    hipLaunchKernelGGL((k_gemm_bf16_reduce<float>), dim3(nb), dim3(256), 0, s, (int)M, (int)N,
+                       used, slab, nullptr, 0.f, (float*)C, ldc, (int64_t)128);
+  GNNEA_LAUNCH_CHECK();
+  return ta_db_reduce(M, used, dbslab, db, s);
+}
+
 extern "C" int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
                                       const void* A, int64_t lda, const void* B, int64_t ldb,
                                       const float* bias, float beta, void* Cs, int64_t sstride,

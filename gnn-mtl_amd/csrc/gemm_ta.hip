@@ -109,9 +109,10 @@ __device__ __forceinline__ void ta_load(TaRegs<T>& R, const T* __restrict__ A, i
   }
 }
 
+// dbn >= 0 (bf16, the bias column): B's element dbn (in the tile's padding) is written as 1.0
 template <typename T>
 __device__ __forceinline__ void ta_write(const TaRegs<T>& R, char* lds, int M, int N, int n0,
-                                         int K, int k0, int ke, int tid) {
+                                         int K, int k0, int ke, int tid, int dbn = -1) {
   using Ti = TaTile<T>;
 #pragma unroll
   for (int q = 0; q < Ti::NCH; ++q) {
@@ -126,6 +127,16 @@ __device__ __forceinline__ void ta_write(const TaRegs<T>& R, char* lds, int M, i
     if (gk == K - 1 && col < lim && (col + Ti::CE) * (int)sizeof(T) > lim * (int)sizeof(T))
       u = make_uint4(u.z, u.w, 0u, 0u);  // read 8 B early: shift down
     if (gk >= ke) u = make_uint4(0u, 0u, 0u, 0u);  // past the split's K range
+    if constexpr (sizeof(T) == 2) {
+      if (!isa && dbn >= col && dbn < col + Ti::CE && gk < ke) {
+        const int e = dbn - col;
+        const uint32_t mk = 0xffffu << (16 * (e & 1)), one = 0x3F80u << (16 * (e & 1));
+        u.x = (e >> 1) == 0 ? (u.x & ~mk) | one : u.x;
+        u.y = (e >> 1) == 1 ? (u.y & ~mk) | one : u.y;
+        u.z = (e >> 1) == 2 ? (u.z & ~mk) | one : u.z;
+        u.w = (e >> 1) == 3 ? (u.w & ~mk) | one : u.w;
+      }
+    }
     const uint32_t swz = ((row >> 3) & 1) << 5;
     char* img = lds + (isa ? 0 : TaTraits<T>::PL * TA_IMG_A);
     const int rs = isa ? TA_RSA : TA_RSB;
@@ -159,7 +170,8 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta(int M, int N, int K,
                                                       const T* __restrict__ A, int64_t lda,
                                                       const T* __restrict__ B, int64_t ldb,
                                                       int kps, int tiles_n,
-                                                      float* __restrict__ slab) {
+                                                      float* __restrict__ slab,
+                                                      float* __restrict__ dbslab) {
   constexpr int PL = TaTraits<T>::PL;
   __shared__ __attribute__((aligned(16))) char lds[PL * (TA_IMG_A + TA_IMG_B)];
   const int t_id = xcd_remap(blockIdx.x, gridDim.x);
@@ -171,6 +183,10 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta(int M, int N, int K,
   const int nsteps = (ke - kb + TA_BK - 1) / TA_BK;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w & 3, wn = w >> 2;  // 80-row x 80-column wave tile
+  const int dbn = dbslab ? N : -1;  // the ones column (bias gradient), see k_gemm_ta_x3d
+  const int nrel = N - n0 - wn * 80;
+  const int jdb = dbslab && nrel >= 0 && nrel < 80 ? nrel / 16 : -1;
+  const bool ones_lane = jdb >= 0 && (lane & 15) == nrel % 16;
 
   ta_f32x4 acc[5][5];
 #pragma unroll
@@ -232,33 +248,33 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta(int M, int N, int K,
     TaRegs<T> R0, R1;
     ta_load<T>(R0, A, lda, B, ldb, M, N, n0, K, kstep(0), ke, tid);
     ta_load<T>(R1, A, lda, B, ldb, M, N, n0, K, kstep(1), ke, tid);
-    ta_write<T>(R0, lds, M, N, n0, K, kstep(0), ke, tid);
+    ta_write<T>(R0, lds, M, N, n0, K, kstep(0), ke, tid, dbn);
     __syncthreads();
     for (int s = 0; s < nsteps; s += 2) {
       ta_load<T>(R0, A, lda, B, ldb, M, N, n0, K, kstep(s + 2), ke, tid);
       __builtin_amdgcn_sched_barrier(0);  // the loads stay ahead of the MFMAs
       compute();  // step s
       __syncthreads();
-      ta_write<T>(R1, lds, M, N, n0, K, kstep(s + 1), ke, tid);
+      ta_write<T>(R1, lds, M, N, n0, K, kstep(s + 1), ke, tid, dbn);
       __syncthreads();
       ta_load<T>(R1, A, lda, B, ldb, M, N, n0, K, kstep(s + 3), ke, tid);
       __builtin_amdgcn_sched_barrier(0);
       if (s + 1 < nsteps) compute();  // step s + 1
       __syncthreads();
-      ta_write<T>(R0, lds, M, N, n0, K, kstep(s + 2), ke, tid);
+      ta_write<T>(R0, lds, M, N, n0, K, kstep(s + 2), ke, tid, dbn);
       __syncthreads();
     }
   } else {
     TaRegs<T> R;
     ta_load<T>(R, A, lda, B, ldb, M, N, n0, K, kstep(0), ke, tid);
-    ta_write<T>(R, lds, M, N, n0, K, kstep(0), ke, tid);
+    ta_write<T>(R, lds, M, N, n0, K, kstep(0), ke, tid, dbn);
     __syncthreads();
     for (int s = 0; s < nsteps; ++s) {
       ta_load<T>(R, A, lda, B, ldb, M, N, n0, K, kstep(s + 1), ke, tid);
       __builtin_amdgcn_sched_barrier(0);
       compute();
       __syncthreads();
-      ta_write<T>(R, lds, M, N, n0, K, kstep(s + 1), ke, tid);
+      ta_write<T>(R, lds, M, N, n0, K, kstep(s + 1), ke, tid, dbn);
       __syncthreads();
     }
   }
@@ -270,7 +286,16 @@ __global__ __launch_bounds__(TA_NT, 1) void k_gemm_ta(int M, int N, int K,
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       const int n = n0 + wn * 80 + 16 * j + (lane & 15);
-      if (n >= N) continue;
+      if (n >= N) {
+        if (j == jdb && ones_lane) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = wm * 80 + 16 * i + 4 * (lane >> 4) + r;
+            if (m < M) dbslab[(int64_t)split * M + m] = acc[i][j][r];
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = wm * 80 + 16 * i + 4 * (lane >> 4) + r;
@@ -537,8 +562,25 @@ int64_t gemm_ta_ws_bytes(int64_t M, int64_t N, int64_t K) {
 }
 
 bool gemm_ta_db_applies(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* A,
-                        const void* B) {
-  return gemm_ta_applies(M, N, K, lda, ldb, A, B, 4) && N % TA_NP != 0;
+                        const void* B, int es) {
+  return gemm_ta_applies(M, N, K, lda, ldb, A, B, es) && N % TA_NP != 0;
+}
+
+// db[m] = sum over the splits' partial column sums, in split order
+__global__ void k_db_reduce(int M, int splits, const float* __restrict__ part,
+                            float* __restrict__ db) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  float a = 0.f;
+  for (int q = 0; q < splits; ++q) a += part[(int64_t)q * M + m];
+  db[m] = a;
+}
+
+int ta_db_reduce(int64_t M, int splits, const float* part, float* db, hipStream_t s) {
+  hipLaunchKernelGGL(k_db_reduce, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, (int)M,
+                     splits, part, db);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
 }
 
 int64_t gemm_ta_db_ws_bytes(int64_t M, int64_t N, int64_t K) {
@@ -564,9 +606,8 @@ int gemm_ta_launch(int64_t M, int64_t N, int64_t K, const T* A, int64_t lda, con
                        (int)K, (const float*)A, lda, (const float*)B, ldb, kps, tiles_n, slab,
                        dbslab);
   } else {
-    if (dbslab_out) return GNNEA_EINVAL;  // (the bias column is the fp32 kernel's)
     hipLaunchKernelGGL((k_gemm_ta<T>), dim3(used * tiles_n), dim3(TA_NT), 0, s, (int)M, (int)N,
-                       (int)K, A, lda, B, ldb, kps, tiles_n, slab);
+                       (int)K, A, lda, B, ldb, kps, tiles_n, slab, dbslab);
   }
   if (dbslab_out) *dbslab_out = dbslab;
   GNNEA_LAUNCH_CHECK();

@@ -282,8 +282,8 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = gemm(dy, weight, out_dtype=x.dtype if bf else None)  # [N,out]·[out,in]
         want_w, want_b = ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2]
-        if want_w and want_b and not bf:  # (fp32: dW and db from one pass over dY)
-            r = gemm_ta_db(dy, x)
+        if want_w and want_b:  # dW and db from one pass over dY
+            r = gemm_ta_db(dy, x, weight.dtype if bf else None)
             if r is not None:
                 dw, db = r[0], r[1].to(ctx.bias_dtype)
                 want_w = want_b = False
@@ -441,11 +441,13 @@ def act_bwd_colsum(dy, y, act, want_db=True):
     return g, db
 
 
-def gemm_ta_db(a, b):
-    """(aᵀ·b, column sums of a) in one pass over a (gnnea_gemm_x3_ta_db_f32: a layer's dW = dhᵀ·x
-    and db = colsum(dh); dW bit-identical to gemm(a, b, trans_a=True)), or None where that
-    kernel is not the one gemm would run (then: gemm + colsum)."""
-    if a.dtype != torch.float32 or b.dtype != torch.float32:
+def gemm_ta_db(a, b, out_dtype=None):
+    """(aᵀ·b, column sums of a) in one pass over a (gnnea_gemm_x3_ta_db_f32 / gnnea_gemm_bf16_ta_db:
+    a layer's dW = dhᵀ·x and db = colsum(dh), db fp32; dW bit-identical to gemm(a, b,
+    trans_a=True, out_dtype=out_dtype)), or None where that kernel is not the one gemm would run
+    (then: gemm + colsum)."""
+    bf = a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+    if not bf and (a.dtype != torch.float32 or b.dtype != torch.float32):
         return None
     a, b = _rows(a), _rows(b)
     K, M = a.shape
@@ -453,17 +455,27 @@ def gemm_ta_db(a, b):
     if b.shape[0] != K:
         raise ValueError("gnnea.gemm_ta_db: shape mismatch")
     L = _lib.lib()
-    if not (_use_x3(M, N, K, None, trans_a=True) and
-            L.gnnea_gemm_x3_ta_db_applies(M, N, K, _ld(a), _ld(b)) and
-            a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0):
+    al = 8 if bf else 16
+    if bf:
+        ok = L.gnnea_gemm_bf16_ta_db_applies(M, N, K, _ld(a), _ld(b))
+    else:
+        ok = _use_x3(M, N, K, None, trans_a=True) and \
+            L.gnnea_gemm_x3_ta_db_applies(M, N, K, _ld(a), _ld(b))
+    if not ok or a.data_ptr() % al or b.data_ptr() % al:
         return None
-    out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    odt = (out_dtype or torch.bfloat16) if bf else torch.float32
+    out = torch.empty((M, N), dtype=odt, device=a.device)
     db = torch.empty(M, dtype=torch.float32, device=a.device)
     ws_bytes = int(L.gnnea_gemm_x3_ta_db_ws_bytes(M, N, K))
     ws = _gemm_ws(a.device, ws_bytes)
     with _lib.on_device(a.device):
-        check(L.gnnea_gemm_x3_ta_db_f32(M, N, K, ptr(a), _ld(a), ptr(b), _ld(b), ptr(out), N,
-                                        ptr(db), ptr(ws), ws_bytes, stream_of(a.device)))
+        if bf:
+            cd = _lib.GNNEA_BF16 if odt == torch.bfloat16 else _lib.GNNEA_F32
+            check(L.gnnea_gemm_bf16_ta_db(M, N, K, ptr(a), _ld(a), ptr(b), _ld(b), ptr(out), N, cd,
+                                          ptr(db), ptr(ws), ws_bytes, stream_of(a.device)))
+        else:
+            check(L.gnnea_gemm_x3_ta_db_f32(M, N, K, ptr(a), _ld(a), ptr(b), _ld(b), ptr(out), N,
+                                            ptr(db), ptr(ws), ws_bytes, stream_of(a.device)))
     return out, db
 
 
@@ -632,8 +644,8 @@ class MLPChainFn(torch.autograd.Function):
                     g = _featc(d, torch.bfloat16 if bf else torch.float32)
             g = _featc(g, torch.bfloat16 if bf else torch.float32)
             need_w = need[2 + 2 * k]
-            if pend and need_w and not bf:
-                r = gemm_ta_db(g, x)
+            if pend and need_w:
+                r = gemm_ta_db(g, x, w.dtype if bf else None)
                 if r is not None:
                     (grads[2 * k], db), need_w, pend = r, False, False
             if need_w:

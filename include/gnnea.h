@@ -581,6 +581,12 @@ int64_t gnnea_gemm_x3_ta_db_ws_bytes(int64_t M, int64_t N, int64_t K);
 int gnnea_gemm_x3_ta_db_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                             const float* B, int64_t ldb, float* C, int64_t ldc, float* db,
                             void* ws, int64_t ws_bytes, void* stream);
+/* The same for bf16 operands (gnnea_gemm_bf16's trans_a product; C bf16 or fp32 by c_dtype; the
+ * workspace of gnnea_gemm_x3_ta_db_ws_bytes). */
+int gnnea_gemm_bf16_ta_db_applies(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
+int gnnea_gemm_bf16_ta_db(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                          const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype, float* db,
+                          void* ws, int64_t ws_bytes, void* stream);
 /* the bf16 GEMM writing C slice-major (bf16, 128-column slices):
  * element (r, c) at Cs[(c/128)*sstride + r*128 + c%128], sstride % 128 == 0, >= M*128 */
 int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

@@ -228,25 +228,29 @@ def test_relu_mask_bits_f32(device):
     assert torch.equal(ops.gemm_dmask(dy, W2, y, mask), ref)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("K,M,N,block", [(200003, 300, 300, False),   # K tail, 2 column tiles
                                          (70000, 300, 300, True),     # dh a column block (ld 2M)
                                          (70000, 128, 100, False),    # one tile, M < 160
+                                         (70000, 300, 296, False),    # N % 8 == 0 (bf16 chunk)
                                          (70000, 300, 320, False)])   # no padding column: None
-def test_gemm_ta_db_vs_separate(device, K, M, N, block):
+def test_gemm_ta_db_vs_separate(device, K, M, N, block, dtype):
     """gemm_ta_db: a layer's dW = dhᵀ·x bit-identical to gemm(dh, x, trans_a=True) (the same
-    kernel) and db = column sums of dh from the kernel's ones column, against fp64 (fp32 sums of
-    K = 2e5 terms: 1e-6 norm-relative) and against colsum."""
+    kernel; bf16: bf16 out as the Linear's bf16 weight) and db = column sums of dh from the
+    kernel's ones column, against fp64 of the same (stored) values (fp32 sums of K = 2e5 terms:
+    1e-6 norm-relative) and against colsum."""
     from gnnea import ops
     g0 = torch.Generator(device=device).manual_seed(11)
-    big = torch.randn(K, 2 * M if block else M, device=device, generator=g0)
+    big = torch.randn(K, 2 * M if block else M, device=device, generator=g0).to(dtype)
     dh = big[:, :M]
-    x = torch.randn(K, N, device=device, generator=g0)
-    r = ops.gemm_ta_db(dh, x)
+    x = torch.randn(K, N, device=device, generator=g0).to(dtype)
+    od = torch.bfloat16 if dtype == torch.bfloat16 else None
+    r = ops.gemm_ta_db(dh, x, od)
     if N % 160 == 0:
         assert r is None
         return
     dw, db = r
-    assert torch.equal(dw, ops.gemm(dh, x, trans_a=True))
+    assert torch.equal(dw, ops.gemm(dh, x, trans_a=True, out_dtype=od))
     ref = dh.double().sum(0)
     assert rel_err(db.cpu(), ref.cpu()) < 1e-6
-    assert rel_err(db.cpu(), ops.colsum(dh).cpu()) < 1e-6
+    assert rel_err(db.cpu(), ops.colsum(dh, torch.float32).cpu()) < 1e-6

@@ -19,7 +19,7 @@ if "--off" in sys.argv:
 if "chain" in off:
     ops.mlp_chain = lambda x, layers: None
 if "tadb" in off:
-    ops.gemm_ta_db = lambda a, b: None
+    ops.gemm_ta_db = lambda a, b, out_dtype=None: None
 
 from tools import dist_step  # noqa: E402
 
