@@ -42,6 +42,11 @@ struct HeadLanes {
 
 // s1[i,h] = sum_d H[i, h*dh+d] * a[h, d];  s2[i,h] = sum_d H[i, h*dh+d] * a[h, dh+d]
 // A wave walks rows (grid-stride) with the lane's slice of a preloaded.
+// A lane's EPL consecutive elements are read as whole 16-B windows: bf16 (EPL <= 6) ONE load of
+// the 4-B aligned window holding them (as k_gat_bwd_src's WIN), fp32 (EPL <= 8) the 16 or 32 B
+// from its first element -- one or two load instructions per row instead of EPL element loads,
+// which left the pass at 2.5 (bf16) / 3.6 (fp32) TB/s; a window may run into the next row, so the
+// last row takes the element loads, in a pass of its own (every main-loop load unconditional).
 template <int H, int EPL, typename T>
 __global__ __launch_bounds__(256) void k_gat_scores(const T* __restrict__ Hm, int64_t ldh,
                                                     int n_rows, int dh,
@@ -49,6 +54,7 @@ __global__ __launch_bounds__(256) void k_gat_scores(const T* __restrict__ Hm, in
                                                     float* __restrict__ s1,
                                                     float* __restrict__ s2) {
   using L = HeadLanes<H, EPL>;
+  constexpr bool WIN = sizeof(T) == 2 ? EPL <= 6 : EPL <= 8;
   const int lane = lane_id();
   const L hl(lane, dh);
   float a1[EPL], a2[EPL];
@@ -59,35 +65,66 @@ __global__ __launch_bounds__(256) void k_gat_scores(const T* __restrict__ Hm, in
     a1[t] = hl.ok[t] ? a[hh * 2 * dh + d] : 0.f;
     a2[t] = hl.ok[t] ? a[hh * 2 * dh + dh + d] : 0.f;
   }
-  // four rows per round, every element load of the four issued before any is used (one row's
-  // loads in flight per wave left the pass latency-bound); the per-row arithmetic is unchanged
+  const int wbyte = (2 * hl.c[0]) & ~3;  // WIN: the lane's window, halfword shift
+  const bool wsh = (hl.c[0] & 1) != 0;
+  auto score = [&](const float (&xv)[EPL], int row) {
+    float p[2] = {0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) {
+      const float v = hl.ok[t] ? xv[t] : 0.f;
+      p[0] = fmaf(v, a1[t], p[0]);
+      p[1] = fmaf(v, a2[t], p[1]);
+    }
+    const float r = grp_sum<2, L::LPH>(p, lane);
+    const int o = lane % L::LPH;
+    if (hl.h < H) {
+      if (o == grp_lane<2, L::LPH>(0)) s1[(int64_t)row * H + hl.h] = r;
+      if (o == grp_lane<2, L::LPH>(1)) s2[(int64_t)row * H + hl.h] = r;
+    }
+  };
+  // RR rows per round, every load of the round issued before any is used (one row's loads in
+  // flight per wave left the pass latency-bound); the per-row arithmetic is unchanged
+  constexpr int RR = WIN ? 8 : 4;
+  const int nmain = WIN ? n_rows - 1 : n_rows;  // (WIN: rows whose window stays in the table)
   const int nw = gridDim.x * 4;
-  for (int base = blockIdx.x * 4 + wave_id(); base < n_rows; base += 4 * nw) {
-    float xv[4][EPL];
+  for (int base = blockIdx.x * 4 + wave_id(); base < nmain; base += RR * nw) {
+    float xv[RR][EPL];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const T* x = Hm + (int64_t)min(base + k * nw, n_rows - 1) * ldh;
+    for (int k = 0; k < RR; ++k) {
+      const T* x = Hm + (int64_t)min(base + k * nw, nmain - 1) * ldh;
+      if constexpr (WIN && sizeof(T) == 4) {
+        const uint4 v0 = *(const uint4*)(x + hl.c[0]);
+        const uint4 v1 = EPL > 4 ? *(const uint4*)(x + hl.c[0] + 4) : v0;
+        const uint32_t dw[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
 #pragma unroll
-      for (int t = 0; t < EPL; ++t) xv[k][t] = to_f32<T>(x[hl.c[t]]);
+        for (int t = 0; t < EPL; ++t) xv[k][t] = __uint_as_float(dw[t]);
+      } else if constexpr (WIN) {
+        const uint4 v = *(const uint4*)((const char*)x + wbyte);
+        const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int t = 0; t < EPL; ++t) {  // halfword t + wsh of the window, widened to f32
+          const uint32_t lo = (t & 1) ? (dw[t >> 1] & 0xffff0000u) : (dw[t >> 1] << 16);
+          const uint32_t hi = (t & 1) ? (dw[(t + 1) >> 1] << 16) : (dw[t >> 1] & 0xffff0000u);
+          xv[k][t] = __uint_as_float(wsh ? hi : lo);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < EPL; ++t) xv[k][t] = to_f32<T>(x[hl.c[t]]);
+      }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < RR; ++k) {
       const int row = base + k * nw;
-      if (row >= n_rows) break;  // uniform
-      float p[2] = {0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < EPL; ++t) {
-        const float v = hl.ok[t] ? xv[k][t] : 0.f;
-        p[0] = fmaf(v, a1[t], p[0]);
-        p[1] = fmaf(v, a2[t], p[1]);
-      }
-      const float r = grp_sum<2, L::LPH>(p, lane);
-      const int o = lane % L::LPH;
-      if (hl.h < H) {
-        if (o == grp_lane<2, L::LPH>(0)) s1[(int64_t)row * H + hl.h] = r;
-        if (o == grp_lane<2, L::LPH>(1)) s2[(int64_t)row * H + hl.h] = r;
-      }
+      if (row >= nmain) break;  // uniform
+      score(xv[k], row);
     }
+  }
+  if (WIN && blockIdx.x == 0 && wave_id() == 0) {  // the last row, element loads
+    const T* x = Hm + (int64_t)(n_rows - 1) * ldh;
+    float xv[EPL];
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) xv[t] = to_f32<T>(x[hl.c[t]]);
+    score(xv, n_rows - 1);
   }
 }
 
