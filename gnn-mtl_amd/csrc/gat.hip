@@ -275,15 +275,27 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep4(int n_rows, int D, int dh
                                                        typename Vec4<T>::raw* __restrict__ G,
                                                        float4* __restrict__ rec) {
   typedef typename Vec4<T>::raw R;
+  constexpr int HP = Pow2<H>::v;  // the per-head sums reduce-scattered over the wave (grp_sum)
   const int r0 = (blockIdx.x * 4 + wave_id()) * 4;
   if (r0 >= n_rows) return;
   const int lane = lane_id();
+  // the lane that ends with head h's sum: grp_lane<HP, 64>(h) = h * (16 / HP); its record loads
+  const int hw = lane % (16 / HP) == 0 && lane < 16 ? lane / (16 / HP) : 0;
+  // per chunk: the head of the lane's first element and how many of its four are in that head
+  // (a chunk of four spans at most two heads: dh >= 4), the rest in the next
+  int hq[NCH], es[NCH];
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    const int c = 4 * (lane + 64 * q);
+    hq[q] = c < D ? c / dh : HP;
+    es[q] = c < D ? (hq[q] + 1) * dh - c : 4;
+  }
   R vd[4][NCH], vy[4][NCH];
   float rs1[4], rmx[4], rdv[4];  // the records' row statistics, read with the rows
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     const int64_t rw = min(r0 + rr, n_rows - 1);
-    const int64_t ro = rw * H + (lane < H ? lane : 0);
+    const int64_t ro = rw * H + (hw < H ? hw : 0);
     rs1[rr] = s1[ro];
     rmx[rr] = mrow[ro];
     rdv[rr] = den[ro];
@@ -298,9 +310,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep4(int n_rows, int D, int dh
   for (int rr = 0; rr < 4; ++rr) {
     const int row = r0 + rr;
     if (row >= n_rows) break;  // uniform
-    float cp[H];
+    float cp[HP];
 #pragma unroll
-    for (int h = 0; h < H; ++h) cp[h] = 0.f;
+    for (int h = 0; h < HP; ++h) cp[h] = 0.f;
 #pragma unroll
     for (int q = 0; q < NCH; ++q) {
       const int c4 = lane + 64 * q;
@@ -309,22 +321,28 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep4(int n_rows, int D, int dh
       const float4 y = Vec4<T>::get(vy[rr][q]);
       const float ys[4] = {y.x, y.y, y.z, y.w};
       float gs[4] = {dy.x, dy.y, dy.z, dy.w};
+      float pa = 0.f, pb = 0.f;  // G.Y over the elements in head hq and in the next
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        const int c = 4 * c4 + t;
-        gs[t] = c < D ? gs[t] * act_grad_from_out<ACT>(ys[t]) : 0.f;
-        const int hh = c < D ? c / dh : H;
+        gs[t] = 4 * c4 + t < D ? gs[t] * act_grad_from_out<ACT>(ys[t]) : 0.f;
+        const float v = gs[t] * ys[t];
+        if (dh >= 4) {  // (uniform) at most two heads per chunk
+          pa += t < es[q] ? v : 0.f;
+          pb += t < es[q] ? 0.f : v;
+        } else {
+          const int hh = (4 * c4 + t) / dh;
 #pragma unroll
-        for (int h = 0; h < H; ++h) cp[h] += (hh == h) ? gs[t] * ys[t] : 0.f;
+          for (int h = 0; h < HP; ++h) cp[h] += hh == h ? v : 0.f;
+        }
       }
+#pragma unroll
+      for (int h = 0; h < HP; ++h) cp[h] += (h == hq[q] ? pa : 0.f) + (h == hq[q] + 1 ? pb : 0.f);
       G[(int64_t)row * ld4 + c4] = Vec4<T>::put(make_float4(gs[0], gs[1], gs[2], gs[3]));
     }
-#pragma unroll
-    for (int h = 0; h < H; ++h) cp[h] = wave_sum(cp[h]);
-    if (lane < H)
-      rec[(int64_t)row * H + lane] = make_float4(rs1[rr], rmx[rr],
-                                                 rdv[rr] > 0.f ? 1.f / rdv[rr] : 0.f,
-                                                 hsel<H>(cp, lane));
+    const float cs = grp_sum<HP, 64>(cp, lane);
+    if (lane % (16 / HP) == 0 && lane < 16 && hw < H)
+      rec[(int64_t)row * H + hw] = make_float4(rs1[rr], rmx[rr],
+                                               rdv[rr] > 0.f ? 1.f / rdv[rr] : 0.f, cs);
   }
 }
 
