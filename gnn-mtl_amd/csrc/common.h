@@ -323,4 +323,47 @@ __device__ __forceinline__ float grp_sum(float (&p)[NV], int lane) {
 template <int NV, int LPH>
 __device__ __forceinline__ constexpr int grp_lane(int v) { return v * ((LPH >= 16 ? 16 : 8) / NV); }
 
+// The same reduce-scatter over the whole wave with max (order-free, so exact), and the all-reduce
+// forms: every lane ends with all NV values (reduce-scatter, then one scalar read per value) --
+// NV values for the price of about one wave_sum instead of NV of them.
+template <int CTRL, int CNT, int NV>
+__device__ __forceinline__ void rs_step_max(float (&p)[NV], bool up) {
+  if constexpr (CNT > 1) {
+    constexpr int half = CNT / 2;
+#pragma unroll
+    for (int t = 0; t < half; ++t) {
+      const float keep = up ? p[t + half] : p[t];
+      const float o = mov_dpp_f32<CTRL>(up ? p[t] : p[t + half]);
+      p[t] = o > keep ? o : keep;
+    }
+  } else {
+    const float o = mov_dpp_f32<CTRL>(p[0]);
+    p[0] = o > p[0] ? o : p[0];
+  }
+}
+template <int NV>
+__device__ __forceinline__ float grp_max64(float (&p)[NV], int lane) {
+  static_assert((NV & (NV - 1)) == 0 && NV <= 16, "grp_max64 shape");
+  rs_step_max<0x140, NV, NV>(p, lane & 8);
+  rs_step_max<0x141, NV / 2, NV>(p, lane & 4);
+  rs_step_max<0x1B, NV / 4, NV>(p, lane & 2);
+  rs_step_max<0xB1, NV / 8, NV>(p, lane & 1);
+  float v = p[0], w = __shfl_xor(v, 16, 64);
+  v = w > v ? w : v;
+  w = __shfl_xor(v, 32, 64);
+  return w > v ? w : v;
+}
+template <int NV>
+__device__ __forceinline__ void wave_allsum(float (&p)[NV], int lane) {
+  const float r = grp_sum<NV, 64>(p, lane);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) p[v] = readlane_f(r, grp_lane<NV, 64>(v));
+}
+template <int NV>
+__device__ __forceinline__ void wave_allmax(float (&p)[NV], int lane) {
+  const float r = grp_max64<NV>(p, lane);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) p[v] = readlane_f(r, grp_lane<NV, 64>(v));
+}
+
 }  // namespace gnnea

@@ -676,6 +676,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ 
                                                     T* __restrict__ Y, int64_t ldy,
                                                     float* __restrict__ m_out,
                                                     float* __restrict__ den_out) {
+  constexpr int HPW = Pow2<H>::v;  // heads padded to a power of two (the all-reduces)
   using L = HeadLanes<H, EPL>;
   using WN = RowWin<T, EPL>;
   constexpr int W = WN::W;
@@ -723,12 +724,20 @@ __global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ 
 #pragma unroll
         for (int h = 0; h < H; ++h) m2[h] = fmaxf(m2[h], sc[h]);
       }
+      float mp[HPW];  // (all heads in one all-reduce, exact)
 #pragma unroll
-      for (int h = 0; h < H; ++h) mx[h] = wave_max(m2[h]);
+      for (int h = 0; h < HPW; ++h) mp[h] = h < H ? m2[h] : 0.f;
+      wave_allmax<HPW>(mp, lane);
+#pragma unroll
+      for (int h = 0; h < H; ++h) mx[h] = mp[h];
       chunk(beg, min(64, end - beg));
     } else {
+      float mp[HPW];
 #pragma unroll
-      for (int h = 0; h < H; ++h) mx[h] = wave_max(sc[h]);
+      for (int h = 0; h < HPW; ++h) mp[h] = h < H ? sc[h] : 0.f;
+      wave_allmax<HPW>(mp, lane);
+#pragma unroll
+      for (int h = 0; h < H; ++h) mx[h] = mp[h];
     }
     for (int base = beg; base < end; base += 64) {
       const int cnt = min(64, end - base);
@@ -783,10 +792,16 @@ __global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ 
     for (int h = 0; h < H; ++h) mx[h] = -INFINITY;
   }
   float rinv[H];
+  {
+    float dp[HPW];  // every head's row sum in one all-reduce
 #pragma unroll
-  for (int h = 0; h < H; ++h) {
-    den[h] = wave_sum(den[h]);
-    rinv[h] = den[h] > 0.f ? 1.f / den[h] : 0.f;
+    for (int h = 0; h < HPW; ++h) dp[h] = h < H ? den[h] : 0.f;
+    wave_allsum<HPW>(dp, lane);
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      den[h] = dp[h];
+      rinv[h] = den[h] > 0.f ? 1.f / den[h] : 0.f;
+    }
   }
   const float ri = hsel<H>(rinv, hme);
   T* y = Y + (int64_t)row * ldy;
@@ -816,6 +831,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hg(
     const float4* __restrict__ rec, const T* __restrict__ G, int64_t ldg,
     const float* __restrict__ a, T* __restrict__ dH, int64_t lddh, float* __restrict__ dzT,
     float* __restrict__ ds2) {
+  constexpr int HPW = Pow2<H>::v;  // heads padded to a power of two (the all-reduces)
   using L = HeadLanes<H, EPL>;
   using WN = RowWin<T, EPL>;
   constexpr int W = WN::W;
@@ -938,9 +954,13 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hg(
     }
   }
   float d2me = 0.f;
+  float dp[HPW];  // every head's sum in one all-reduce
+#pragma unroll
+  for (int h = 0; h < HPW; ++h) dp[h] = h < H ? ds2p[h] : 0.f;
+  wave_allsum<HPW>(dp, lane);
 #pragma unroll
   for (int h = 0; h < H; ++h) {
-    const float d2 = wave_sum(ds2p[h]);
+    const float d2 = dp[h];
     d2me = hme == h ? d2 : d2me;
     if (lane == 0) ds2[(int64_t)row * H + h] = d2;
   }
