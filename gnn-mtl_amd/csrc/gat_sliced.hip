@@ -248,13 +248,16 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_s(int n_rows, int D, int d
   const int row = xcd_remap(blockIdx.x, gridDim.x) * 4 + wave_id();
   if (row >= n_rows) return;
   const int lane = lane_id();
-  // the record's row statistics, read up front (read in the epilogue they were one more serial
-  // round trip per row after the wave sums)
-  const int64_t ro = (int64_t)row * H + (lane < H ? lane : 0);
+  // the per-head sums reduce-scattered over the wave (grp_sum, as k_gat_bwd_prep4): the lane that
+  // ends with head hw's sum writes its record; the record's row statistics, read up front (read in
+  // the epilogue they were one more serial round trip per row after the sums)
+  constexpr int HP = H <= 1 ? 1 : H <= 2 ? 2 : H <= 4 ? 4 : 8;
+  const int hw = lane % (16 / HP) == 0 && lane < 16 ? lane / (16 / HP) : 0;
+  const int64_t ro = (int64_t)row * H + (hw < H ? hw : 0);
   const float rs1 = s1[ro], rmx = mrow[ro], rdv = den[ro];
-  float cp[H];
+  float cp[HP];
 #pragma unroll
-  for (int h = 0; h < H; ++h) cp[h] = 0.f;
+  for (int h = 0; h < HP; ++h) cp[h] = 0.f;
 #pragma unroll
   for (int q = 0; q < NCH; ++q) {
     const int c4 = lane + 64 * q;
@@ -272,21 +275,32 @@ __global__ __launch_bounds__(256) void k_gat_bwd_prep_s(int n_rows, int D, int d
     const typename Vec4<T>::raw gr = Vec4<T>::put(make_float4(gs[0], gs[1], gs[2], gs[3]));
     const float4 gq = Vec4<T>::get(gr);
     const float gv[4] = {gq.x, gq.y, gq.z, gq.w};
+    if (dh >= 4) {  // (uniform) four elements span at most two heads: hq and the next
+      const int hq = (4 * c4) / dh, es = (hq + 1) * dh - 4 * c4;
+      float pa = 0.f, pb = 0.f;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int c = 4 * c4 + t;
-      const int hh = c < D ? c / dh : H;
+      for (int t = 0; t < 4; ++t) {
+        const float v = 4 * c4 + t < D ? gv[t] * ys[t] : 0.f;
+        pa += t < es ? v : 0.f;
+        pb += t < es ? 0.f : v;
+      }
 #pragma unroll
-      for (int h = 0; h < H; ++h) cp[h] += (hh == h) ? gv[t] * ys[t] : 0.f;
+      for (int h = 0; h < HP; ++h) cp[h] += (h == hq ? pa : 0.f) + (h == hq + 1 ? pb : 0.f);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int c = 4 * c4 + t;
+        const int hh = c < D ? c / dh : HP;
+#pragma unroll
+        for (int h = 0; h < HP; ++h) cp[h] += (hh == h) ? gv[t] * ys[t] : 0.f;
+      }
     }
     // column 4*c4 -> slice c4 / 16, offset 4 * (c4 % 16)
     Gs[(int64_t)(c4 >> 4) * sstride4 + (int64_t)row * 16 + (c4 & 15)] = gr;
   }
-#pragma unroll
-  for (int h = 0; h < H; ++h) cp[h] = wave_sum(cp[h]);
-  if (lane < H)
-    rec[(int64_t)row * H + lane] =
-        make_float4(rs1, rmx, rdv > 0.f ? 1.f / rdv : 0.f, hsel<H>(cp, lane));
+  const float cs = grp_sum<HP, 64>(cp, lane);
+  if (lane % (16 / HP) == 0 && lane < 16 && hw < H)
+    rec[(int64_t)row * H + hw] = make_float4(rs1, rmx, rdv > 0.f ? 1.f / rdv : 0.f, cs);
 }
 
 template <int H, int LPR>  // LPR lanes per source row
