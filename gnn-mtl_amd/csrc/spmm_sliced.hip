@@ -150,6 +150,11 @@ __global__ __launch_bounds__(256) void k_spmm_sliced(const int32_t* __restrict__
     typedef typename Vec4<TY>::raw RY;
     if constexpr (!HW) {
       *(RY*)(Y + (int64_t)row * ldy + cc) = Vec4<TY>::put(sv);
+      if constexpr (E == 4) {  // (the GCN layer's relu: its sign bits for the backward, as HW)
+        if (hw.save_m)
+          hw.save_m[(int64_t)row * hw.ldm + 16 * s + c] = (uint8_t)(
+              (sv.x > 0.f) | ((sv.y > 0.f) << 1) | ((sv.z > 0.f) << 2) | ((sv.w > 0.f) << 3));
+      }
     } else {
       const float4 gp = hgp[k];  // gate_pre + bias_gate (loaded before the gathers)
       const float4 gt = make_float4(sigm_f(gp.x), sigm_f(gp.y), sigm_f(gp.z), sigm_f(gp.w));
@@ -232,6 +237,27 @@ static int slice_fill(const T* dY, int64_t ld, const T* Y, int64_t ldo, int64_t 
 #undef GNNEA_SF
   GNNEA_LAUNCH_CHECK();
   return 0;
+}
+
+// G = dY * relu'(Y) written slice-major with relu' from the forward's sign bits (mask byte q of a
+// row = its 4-element chunk q, bit e = element 4 q + e > 0): fp32 (16 chunks per slice row)
+__global__ __launch_bounds__(256) void k_slice_fill_bits(const float4* __restrict__ dY,
+                                                         int64_t ld4,
+                                                         const uint8_t* __restrict__ M,
+                                                         int64_t ldm, int64_t n, int D4,
+                                                         float4* __restrict__ Gs,
+                                                         int64_t sstride4) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave_id();
+  if (r >= n) return;
+  for (int q = lane_id(); q < D4; q += 64) {
+    float4 d = dY[r * ld4 + q];
+    const uint32_t b = M[r * ldm + q];
+    d.x *= (b & 1u) ? 1.f : 0.f;  // (act_grad_from_out<relu>: y > 0 ? 1 : 0, multiplied)
+    d.y *= (b & 2u) ? 1.f : 0.f;
+    d.z *= (b & 4u) ? 1.f : 0.f;
+    d.w *= (b & 8u) ? 1.f : 0.f;
+    Gs[(int64_t)(q >> 4) * sstride4 + r * 16 + (q & 15)] = d;
+  }
 }
 
 template <bool HW, typename TX, typename TY>
@@ -432,6 +458,36 @@ extern "C" int gnnea_spmm_highway_sliced_m_f32(const int32_t* rowptr, const int3
   hw.ldm = ldm;
   return spmm_sliced<true, float, float>(rowptr, col, val, n_rows, D, Xs, sstride, Y, ldy, act,
                                          hw, (hipStream_t)stream);
+}
+
+// gnnea_spmm_sliced_f32 with relu, also writing the output's sign bits (save_m [n_rows][ldm]
+// bytes, ldm >= D / 4: byte q = the 4-element chunk q, bit e = element 4 q + e > 0)
+extern "C" int gnnea_spmm_sliced_m_f32(const int32_t* rowptr, const int32_t* col,
+                                       const float* val, int32_t n_rows, int32_t D,
+                                       const float* Xs, int64_t sstride, float* Y, int64_t ldy,
+                                       uint8_t* save_m, int64_t ldm, void* stream) {
+  if (!save_m || ldm < (D + 3) / 4) return GNNEA_EINVAL;
+  SlicedHighway hw = kNoHighway;
+  hw.save_m = save_m;
+  hw.ldm = ldm;
+  return spmm_sliced<false, float, float>(rowptr, col, val, n_rows, D, Xs, sstride, Y, ldy,
+                                          GNNEA_ACT_RELU, hw, (hipStream_t)stream);
+}
+
+// gnnea_act_bwd_sliced_f32 (relu) with relu'(Y) from gnnea_spmm_sliced_m_f32's sign bits
+extern "C" int gnnea_act_bwd_sliced_bits_f32(const float* dY, int64_t lddy, const uint8_t* M,
+                                             int64_t ldm, int64_t n, int32_t D, float* Gs,
+                                             int64_t sstride, void* stream) {
+  if (n < 0 || D < 0) return GNNEA_EINVAL;
+  if (n == 0 || D == 0) return 0;
+  if (!dY || !M || !Gs || D % 4 || lddy % 4 || lddy < D || ldm < D / 4 || sstride % 4 ||
+      sstride < n * kSliceW || !al16(dY) || !al16(Gs) || (n + 3) / 4 >= (1ll << 31))
+    return GNNEA_EINVAL;
+  hipLaunchKernelGGL(k_slice_fill_bits, dim3((unsigned)((n + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, (const float4*)dY, lddy / 4, M, ldm, n, D / 4,
+                     (float4*)Gs, sstride / 4);
+  GNNEA_LAUNCH_CHECK();
+  return 0;
 }
 
 extern "C" int gnnea_slice_pack_f32(const float* X, int64_t ldx, int64_t n, int32_t D,

@@ -196,6 +196,10 @@ SIGNATURES = {
     "gnnea_gemm_bf16_ta_db_applies": (ctypes.c_int, [_i64, _i64, _i64, _i64, _i64]),
     "gnnea_gemm_bf16_ta_db": (ctypes.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, _i64,
                                              ctypes.c_int, _p, _p, _i64, _p]),
+    "gnnea_spmm_sliced_m_f32": (ctypes.c_int, [_p, _p, _p, _i32, _i32, _p, _i64, _p, _i64, _p,
+                                               _i64, _p]),
+    "gnnea_act_bwd_sliced_bits_f32": (ctypes.c_int, [_p, _i64, _p, _i64, _i64, _i32, _p, _i64,
+                                                     _p]),
     "gnnea_gemm_bf16_act": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _i64, _i64, _i64, _p, _i64,
                                            _p, _i64, _p, ctypes.c_int, _p, _i64, ctypes.c_int, _p,
                                            _i64, _p]),

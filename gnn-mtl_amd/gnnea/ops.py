@@ -867,6 +867,37 @@ def spmm_sliced(csr, xs, D, act=_lib.GNNEA_ACT_IDENTITY, out=None, out_dtype=Non
     return out
 
 
+def spmm_sliced_m(csr, xs, D):
+    """(relu(A @ X), sign bits of it) for an fp32 slice-major X (gnnea_spmm_sliced_m_f32): the
+    bits [n_rows, D / 4] bytes replace the output in the backward (act_bwd_sliced_bits)."""
+    out = torch.empty((csr.n_rows, D), dtype=torch.float32, device=xs.device)
+    ldm = (D + 3) // 4
+    mask = torch.empty((csr.n_rows, ldm), dtype=torch.uint8, device=xs.device)
+    if xs.dtype != torch.float32 or xs.dim() != 3 or xs.shape[2] != slice_w(xs.dtype) or \
+            xs.shape[1] < csr.n_cols or not xs.is_contiguous():
+        raise ValueError("gnnea.spmm_sliced_m: a contiguous fp32 slice table required")
+    L = _lib.lib()
+    with _lib.on_device(xs.device):
+        for r0, r1 in csr.row_blocks():
+            check(L.gnnea_spmm_sliced_m_f32(_off32(csr.rowptr, r0), ptr(csr.col), ptr(csr.val),
+                                            r1 - r0, D, ptr(xs), xs.stride(0), _off(out, r0),
+                                            _ld(out), ctypes.c_void_p(mask.data_ptr() + r0 * ldm),
+                                            ldm, stream_of(xs.device)))
+    return out, mask
+
+
+def act_bwd_sliced_bits(dy, mask, D):
+    """Gs = dy * relu'(y) slice-major with relu' from spmm_sliced_m's sign bits."""
+    dy = _rows(dy, torch.float32)
+    n = dy.shape[0]
+    gs = sliced_empty(n, D, dy.device, torch.float32)
+    with _lib.on_device(dy.device):
+        check(_lib.lib().gnnea_act_bwd_sliced_bits_f32(ptr(dy), _ld(dy), ptr(mask), mask.stride(0),
+                                                       n, D, ptr(gs), gs.stride(0),
+                                                       stream_of(dy.device)))
+    return gs
+
+
 def spmm_sliced64(csr, xs, D, act=_lib.GNNEA_ACT_IDENTITY, out=None, out_dtype=None):
     """out = act(A @ X) for a bf16 X held in 64-column slices ([S, n_src, 64]: 128 B per row
     piece, one cfg-5 KG slice = 256 MB; slice_pack64's layout), per diagonal (KG) block."""
@@ -962,20 +993,33 @@ class GCNLayerFn(torch.autograd.Function):
     """A whole graph convolution act(A · (x Wᵀ + b)) (layers/layers.py:30-39, dropout inactive)
     with the hidden kept slice-major: the projection GEMM writes it as the sliced aggregation
     reads it (never row-major in HBM); backward dY ⊙ act'(Y) is written slice-major by one
-    elementwise pass, Aᵀ·G gives d hidden row-major for dx = dh·W, dW = dhᵀ·x, db = colsum(dh)."""
+    elementwise pass (fp32 relu: act' from the sign bits the forward wrote instead of Y),
+    Aᵀ·G gives d hidden row-major for dx = dh·W, dW = dhᵀ·x, db = colsum(dh)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, csr, act):
         hs = gemm_sliced(x, weight, bias)
-        out = spmm_sliced(csr, hs, weight.shape[0], act)
+        D = weight.shape[0]
+        # fp32 relu with a sliced backward: the output's sign bits are what the backward keeps
+        ctx.bits = int(act) == _lib.GNNEA_ACT_RELU and hs.dtype == torch.float32 and \
+            D % 4 == 0 and use_sliced(csr.n_rows, D, torch.float32)
+        if ctx.bits:
+            out, keep = spmm_sliced_m(csr, hs, D)
+        else:
+            out = spmm_sliced(csr, hs, D, act)
+            keep = out
         ctx.csr, ctx.act = csr, act
-        ctx.save_for_backward(x, weight, out)
+        ctx.save_for_backward(x, weight, keep)
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, out = ctx.saved_tensors
-        dh = aggregate_t_into(ctx.csr, dy, out, ctx.act)
+        x, weight, keep = ctx.saved_tensors
+        if ctx.bits:
+            dh = spmm_sliced(ctx.csr.transpose(), act_bwd_sliced_bits(dy, keep, weight.shape[0]),
+                             weight.shape[0])
+        else:
+            dh = aggregate_t_into(ctx.csr, dy, keep, ctx.act)
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         dx = gemm(dh, weight) if need_x else None
         dw, db = _wgrads(dh, x, need_w, need_b)

@@ -587,6 +587,16 @@ int gnnea_gemm_bf16_ta_db_applies(int64_t M, int64_t N, int64_t K, int64_t lda, 
 int gnnea_gemm_bf16_ta_db(int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                           const void* B, int64_t ldb, void* C, int64_t ldc, int c_dtype, float* db,
                           void* ws, int64_t ws_bytes, void* stream);
+/* The GCN layer's relu with 1 bit per element kept for the backward (fp32, the slice-major
+ * path): gnnea_spmm_sliced_m_f32 = gnnea_spmm_sliced_f32 with act relu, also writing the sign
+ * bits of Y (save_m [n_rows][ldm] bytes, ldm >= D / 4: byte q holds elements 4 q .. 4 q + 3, bit
+ * e set where Y > 0); gnnea_act_bwd_sliced_bits_f32 = gnnea_act_bwd_sliced_f32 (relu) reading
+ * them instead of Y (the same G, bit for bit). */
+int gnnea_spmm_sliced_m_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                            int32_t n_rows, int32_t D, const float* Xs, int64_t sstride, float* Y,
+                            int64_t ldy, uint8_t* save_m, int64_t ldm, void* stream);
+int gnnea_act_bwd_sliced_bits_f32(const float* dY, int64_t lddy, const uint8_t* M, int64_t ldm,
+                                  int64_t n, int32_t D, float* Gs, int64_t sstride, void* stream);
 /* the bf16 GEMM writing C slice-major (bf16, 128-column slices):
  * element (r, c) at Cs[(c/128)*sstride + r*128 + c%128], sstride % 128 == 0, >= M*128 */
 int gnnea_gemm_sliced_bf16(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,

@@ -127,6 +127,26 @@ def test_act_bwd_sliced(device, act, fn):
     assert torch.equal(_unslice(gs, 132), ops.act_bwd(dy, y, act))
 
 
+@pytest.mark.parametrize("D", [4, 68, 300])
+def test_relu_sign_bits_sliced(device, D):
+    """spmm_sliced_m: the relu aggregation bit-identical to spmm_sliced, its sign bits = (y > 0)
+    (byte q: elements 4 q .. 4 q + 3); act_bwd_sliced_bits from them = act_bwd_sliced from y,
+    bit for bit (the GCN layer's fp32 relu backward keeps only the bits)."""
+    from gnnea import _lib, ops
+    rng = np.random.default_rng(12)
+    n = 1500
+    _, _, _, csr = _graph(rng, n, 12000, device)
+    xs = ops.slice_pack(torch.randn(n, D, device=device))
+    y, m = ops.spmm_sliced_m(csr, xs, D)
+    assert torch.equal(y, ops.spmm_sliced(csr, xs, D, _lib.GNNEA_ACT_RELU))
+    cols = torch.arange(D, device=device)
+    bits = (m[:, cols // 4] >> (cols % 4).to(torch.uint8)) & 1
+    assert torch.equal(bits.bool(), y > 0)
+    dy = torch.randn(n, D, device=device)
+    assert torch.equal(_unslice(ops.act_bwd_sliced_bits(dy, m, D), D),
+                       _unslice(ops.act_bwd_sliced(dy, y, _lib.GNNEA_ACT_RELU), D))
+
+
 def test_gcn_layer_sliced_vs_oracle(device, monkeypatch):
     """GraphConvolution through GCNLayerFn (hidden written slice-major by the GEMM, sliced
     aggregation, sliced backward) vs the fp64 oracle: output, dx, dW, db."""
