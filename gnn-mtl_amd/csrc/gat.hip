@@ -540,12 +540,15 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst4(const int32_t* __restrict_
       for (int h = 0; h < H; ++h) p[h] += dzT[t * H + h];
     }
   }
+  // the group's head sums reduce-scattered inside its 16-lane row (DPP, no LDS): lane
+  // grp_lane<HP, 16>(h) of the group ends with head h's sum
+  constexpr int HP = Pow2<H>::v;
+  float pp[HP];
 #pragma unroll
-  for (int h = 0; h < H; ++h) {
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) p[h] += __shfl_xor(p[h], o, 64);
-  }
-  if (live && l16 < H) ds1[(int64_t)row * H + l16] = hsel<H>(p, l16);
+  for (int h = 0; h < HP; ++h) pp[h] = h < H ? p[h] : 0.f;
+  const float gsum = grp_sum<HP, 16>(pp, lane);
+  const int hw = l16 % (16 / HP) == 0 ? l16 / (16 / HP) : H;
+  if (live && hw < H) ds1[(int64_t)row * H + hw] = gsum;
   // the four rows' dH pieces: every load first
   typedef typename Vec4<T>::raw R;
   R v[4][NCH];
@@ -558,28 +561,34 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst4(const int32_t* __restrict_
       v[rr][q] = dH[(int64_t)rw * lddh4 + c4];
     }
   }
+  // a1 of the lane's columns and their heads: the same for the four rows, read once
+  float av[NCH][4];
+  int hc[NCH][4];
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int c = min(4 * (lane + 64 * q) + t, D - 1), h = c / dh;
+      hc[q][t] = h;
+      av[q][t] = a[h * 2 * dh + (c - h * dh)];
+    }
+  }
 #pragma unroll
   for (int rr = 0; rr < 4; ++rr) {
     if (r0 + rr >= n_rows) break;  // uniform
-    float ph[H];
+    float ph[H];  // row r0 + rr's head sums: scalar reads from its group's lanes
 #pragma unroll
-    for (int h = 0; h < H; ++h) ph[h] = __shfl(p[h], 16 * rr, 64);
+    for (int h = 0; h < H; ++h) ph[h] = readlane_f(gsum, 16 * rr + grp_lane<HP, 16>(h));
 #pragma unroll
     for (int q = 0; q < NCH; ++q) {
       const int c4 = lane + 64 * q;
       if (4 * c4 >= D) continue;
       const float4 x = Vec4<T>::get(v[rr][q]);
       float o[4] = {x.x, x.y, x.z, x.w};
-      float av[4];  // (read together, as in k_gat_bwd_dst)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int c = min(4 * c4 + t, D - 1), h = c / dh;
-        av[t] = a[h * 2 * dh + (c - h * dh)];
-      }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int c = 4 * c4 + t;
-        if (c < D) o[t] += hsel<H>(ph, c / dh) * av[t];
+        if (c < D) o[t] += hsel<H>(ph, hc[q][t]) * av[q][t];
       }
       dH[(int64_t)(r0 + rr) * lddh4 + c4] = Vec4<T>::put(make_float4(o[0], o[1], o[2], o[3]));
     }
