@@ -523,6 +523,20 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_s(const int32_t* __restrict
     const int c4 = l + L * k;
     v[k] = 4 * c4 < D ? Vec4<T>::get(dH[(int64_t)row * lddh4 + c4]) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // the lane's columns' heads and a1 / a2 values, likewise before the chain (read after it they
+  // were one more dependent round trip per row, with an integer division per element)
+  int hc[NC][4];
+  float a1v[NC][4], a2v[NC][4];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int c = min(4 * (l + L * k) + t, D - 1), h = c / dh, d = c - h * dh;
+      hc[k][t] = h;
+      a1v[k][t] = a[h * 2 * dh + d];
+      a2v[k][t] = ds2 ? a[h * 2 * dh + dh + d] : 0.f;
+    }
+  }
   float p[H], q[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) p[h] = 0.f;
@@ -544,9 +558,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_s(const int32_t* __restrict
     float o[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int c = 4 * c4 + t, h = c / dh, d = c - h * dh;
-      o[t] += hsel<H>(p, h) * a[h * 2 * dh + d];
-      if (ds2) o[t] += hsel<H>(q, h) * a[h * 2 * dh + dh + d];
+      const int h = hc[k][t];
+      o[t] += hsel<H>(p, h) * a1v[k][t];
+      if (ds2) o[t] += hsel<H>(q, h) * a2v[k][t];
     }
     dH[(int64_t)row * lddh4 + c4] = Vec4<T>::put(make_float4(o[0], o[1], o[2], o[3]));
   }
