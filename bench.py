@@ -11,8 +11,11 @@ aggregation over the owned rows (default --partition rows).  The exchange-free p
 (tiles / features: every rank aggregates a column slice from the whole KG, which a layer can
 only do after an all-gather of its input) are reported as a labelled side number.
 
-Side measurement (`train_step`): the row-sharded HGCN-EA training step of configs[3] through
-the drop-in Encoder/Decoder modules with the RCCL halo exchange (tools/dist_step.py).
+Side measurements (`train_step`, `train_step_gat`, `train_step_gat_cfg5_bf16`): the row-sharded
+EA training steps through the drop-in Encoder/Decoder modules with the RCCL halo exchange
+(tools/dist_step.py) -- HGCN-EA on the cfg-4 graph (configs[3]), GAT-EA fp32 on the same graph
+(configs[2]'s model), GAT-EA bf16 on the cfg-5 graph (configs[4]) -- at N = 1 and row-sharded
+at N > 1, each with per-kernel-class GPU time.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]   (N > 1: starts its own N ranks)
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
@@ -474,6 +477,14 @@ def cpu_baseline(shard, H, budget_s=12.0):
     return out
 
 
+# EA training-step legs (tools/dist_step.measure): line key -> (encoder, graph, storage dtype).
+# HGCN-EA on cfg-4 is BASELINE configs[3]; GAT-EA on cfg-4 in fp32 is configs[2]'s model at
+# configs[3]'s size; GAT-EA on the cfg-5 graph (2 x 2M entities, ~84M nnz) in bf16 is configs[4]
+TRAIN_LEGS = {"train_step": ("HGCN", "cfg4", "f32"),
+              "train_step_gat": ("GAT", "cfg4", "f32"),
+              "train_step_gat_cfg5_bf16": ("GAT", "cfg5", "bf16")}
+
+
 def shard_t(n):
     return synth.CONFIGS["cfg4"]["t"] if n == synth.CONFIGS["cfg4"]["n"] else 10 * n
 
@@ -495,8 +506,11 @@ def main():
     ap.add_argument("--no-side", action="store_true",
                     help="N > 1: skip the labelled exchange-free side number (tiles)")
     ap.add_argument("--no-train", action="store_true",
-                    help="skip the side measurement of the row-sharded HGCN-EA training step")
+                    help="skip the side measurements of the row-sharded EA training steps")
     ap.add_argument("--train-steps", type=int, default=21)
+    ap.add_argument("--train-models", default=",".join(TRAIN_LEGS),
+                    help="comma-separated EA training-step legs (default all: %s)"
+                         % ", ".join(TRAIN_LEGS))
     ap.add_argument("--layout", choices=("sliced", "rowmajor"), default="sliced",
                     help="feature table layout of the aggregation input (sliced: 64-column "
                          "slices, each one Infinity-Cache-sized table at 1M rows)")
@@ -551,18 +565,26 @@ def main():
     from gnnea import exchange as _ex
     # N > 1, row shards: prove the per-slice staged halo on THESE ranks (RCCL) before using it --
     # one HighWay, one GCN and one GAT layer fwd + bwd staged and unstaged on the same inputs
-    # (gnnea.dist_graph.validate_staged); the step and train_step take the staged path only when
-    # every rank saw them agree (GNNEA_HALO_STAGED=0 / 1 forces it off / on)
+    # (gnnea.dist_graph.validate_staged); the step and the train legs take the staged path only
+    # for the dtypes whose legs every rank saw agree (GNNEA_HALO_STAGED=0: always off; =1: on
+    # without validation, the report still says what matched)
+    # the legs run in fp32 and in bf16 (configs[4]'s storage, whose GAT stages move bf16
+    # 64-column tables); each dtype takes the staged path only if its own legs matched
     halo_ab = None
     if shard.g > 1 and part.kind == "rows":
         from gnnea.dist_graph import DistAdj, validate_staged
         t_ab = time.time()
-        halo_ab = validate_staged(DistAdj.from_shard(shard), D=D)
-        log("rank %d: halo_ab match=%s err=%.3g staged %.2f ms / unstaged %.2f ms (%.1fs)"
-            % (rank, halo_ab["match"], halo_ab["max_norm_rel_err"], halo_ab["staged_ms"],
-               halo_ab["unstaged_ms"], time.time() - t_ab))
+        halo_ab = validate_staged(DistAdj.from_shard(shard), D=D,
+                                  dtypes=(torch.float32, torch.bfloat16))
+        for dn, rep in halo_ab["dtypes"].items():
+            log("rank %d: halo_ab %s match=%s err=%.3g (tol %.0e)" % (
+                rank, dn, rep["match"], rep["max_norm_rel_err"], rep["tol"]))
+        log("rank %d: halo_ab staged %.2f ms / unstaged %.2f ms, in use %s (%.1fs)"
+            % (rank, halo_ab["staged_ms"], halo_ab["unstaged_ms"], halo_ab["staged_in_use"],
+               time.time() - t_ab))
         torch.cuda.empty_cache()
-    n_slices = (len(shard.slices(Dl)) if _ex.STAGED else 1) \
+    staged32 = _ex.staged_for(torch.float32)
+    n_slices = (len(shard.slices(Dl)) if staged32 else 1) \
         if shard.g > 1 and part.kind == "rows" else 0
 
     def step(ev=None):
@@ -613,10 +635,10 @@ def main():
         other = {}
         keep = _ex.STAGED
         for mode in (True, False):
-            if mode == keep:
+            if mode == staged32:
                 other[mode] = ms_per_step
                 continue
-            if mode and not halo_ab["match"]:
+            if mode and not halo_ab["dtypes"]["float32"]["match"]:
                 continue  # never time a pipeline that did not validate
             _ex.STAGED = mode
             try:
@@ -642,7 +664,7 @@ def main():
         from gnnea import exchange as ex
         ranks = part.group_ranks(part.kg)
 
-        if ex.STAGED:
+        if staged32:
             tables = shard.halo_tables(Dl)
 
             def xchg():  # the same per-slice exchanges as the step, without the aggregation
@@ -682,7 +704,7 @@ def main():
                     # slices, slice q aggregated while slices > q move; the hidden fraction of
                     # the exchange = (exchange alone + aggregation - step) / exchange alone
                     "pipeline": ("%d column slices (64 fp32 columns; slice-major KG tables)"
-                                 % n_slices) if ex.STAGED else
+                                 % n_slices) if staged32 else
                                 "none (GNNEA_HALO_STAGED=0: the whole halo, then the "
                                 "aggregation)",
                     "step_ms": round(ms_per_step, 4),
@@ -717,20 +739,38 @@ def main():
                 "edges_per_s": round(total_nnz / (s_ms * 1e-3), 1), "ms_per_step": round(s_ms, 4)}
         del sh2, h2, y2, hs2
 
-    # side measurement (every rank, same collective sequence): the row-sharded HGCN-EA training
-    # step of BASELINE.json configs[3] through the drop-in modules with the RCCL halo exchange
-    # these legs run collectives at N > 1: an exception there propagates (the run exits non-zero)
-    # instead of being recorded on one rank while the others wait in the next collective
-    train = None
-    if not args.no_train and not args.rehearse:
+    # side measurements (every rank, same collective sequence): the row-sharded EA training
+    # steps through the drop-in modules with the RCCL halo exchange -- HGCN-EA (configs[3]),
+    # GAT-EA fp32 on the same graph, GAT-EA bf16 on the cfg-5 graph (configs[4]); each with
+    # per-kernel-class attribution.  These legs run collectives at N > 1: an exception there
+    # propagates (the run exits non-zero) instead of being recorded on one rank while the others
+    # wait in the next collective.  --rehearse (one device, gloo): 1 warm-up + --train-steps
+    # steps, no attribution -- the code path, not a rate.
+    train = {}
+    if not args.no_train:
         from tools.dist_step import measure
-        if world == 1:
-            try:
-                train = measure("HGCN", n, rank, world, device, args.train_steps, 3)
-            except Exception as e:  # report, never hide
-                train = {"error": repr(e)}
-        else:
-            train = measure("HGCN", n, rank, world, device, args.train_steps, 3)
+        want = [k.strip() for k in args.train_models.split(",") if k.strip()]
+        for key in want:
+            model, gname, dn = TRAIN_LEGS[key]
+            n_leg = n if gname == "cfg4" else (synth.CONFIGS["cfg5"]["n"]
+                                               if n == synth.CONFIGS["cfg4"]["n"] else 2 * n)
+            dt = torch.bfloat16 if dn == "bf16" else torch.float32
+            kw = dict(min_steps=1, min_warmup=1, attribute=0) if args.rehearse else {}
+
+            def leg():
+                r = measure(model, n_leg, rank, world, device, args.train_steps,
+                            1 if args.rehearse else 3, dt, **kw)
+                r["config"] = {"graph_config": gname, "entities_per_kg": n_leg,
+                               "storage": dn}
+                return r
+            if world == 1:
+                try:
+                    train[key] = leg()
+                except Exception as e:  # report, never hide
+                    train[key] = {"error": repr(e)}
+            else:
+                train[key] = leg()
+            torch.cuda.empty_cache()
     sk_shard = None
     if world > 1 and not args.no_sinkhorn:
         # (--rehearse: the code path only; the rate means nothing there)
@@ -770,7 +810,7 @@ def main():
                               else ("2 KG groups of %d GPUs, row blocks + per-column-slice halo "
                                     "exchange (relayed peer transfers) pipelined with the "
                                     "per-slice aggregation, inside the timed step" % shard.g)
-                              if _ex.STAGED else
+                              if staged32 else
                               ("2 KG groups of %d GPUs, row blocks + the whole halo exchange "
                                "(relayed peer transfers), then the aggregation, inside the "
                                "timed step" % shard.g)))},
@@ -818,8 +858,8 @@ def main():
                 line["layouts"] = layout_rates(shard, h_local, y, args.steps)
             except Exception as e:  # report, never hide
                 line["layouts"] = {"error": repr(e)}
-        if train is not None:
-            line["train_step"] = train
+        for key, val in train.items():
+            line[key] = val
         if sk_shard is not None:
             line["sinkhorn_B15000_row_sharded"] = sk_shard
         if world == 1 and not args.no_sinkhorn:

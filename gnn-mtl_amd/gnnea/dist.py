@@ -207,7 +207,7 @@ class KGShard:
             rec(1)
             return out
         D = h_local.shape[1]
-        if not exchange.STAGED:  # the whole halo row-major, then one aggregation
+        if not exchange.staged_for(h_local.dtype):  # the whole halo row-major, then aggregate
             rec(0)
             full = self._full
             if full is None or full.shape != (self.n_cols, D) or full.dtype != h_local.dtype:

@@ -414,8 +414,8 @@ class DistAdj:
         4-column chunks (the HighWay tail too: the fp32 sliced kernel, or for bf16 the
         row-major kernel over each 128-column slice table)."""
         from . import exchange
-        if (self.part.g == 1 or not exchange.STAGED or not hasattr(self.engine, "slice_w")
-                or t.shape[1] % 4):
+        if (self.part.g == 1 or not exchange.staged_for(t.dtype)
+                or not hasattr(self.engine, "slice_w") or t.shape[1] % 4):
             return False
         if isinstance(self.engine, HipEngine):
             return t.dtype in (torch.float32, torch.bfloat16)
@@ -429,11 +429,12 @@ class DistAdj:
     def _peers(self):
         return self.part.group_ranks(self.part.kg), self.part.li, self.part.other_ranks()
 
-    def staged_gat(self, heads, d_head):
+    def staged_gat(self, heads, d_head, dtype):
         """The GAT halo moves slice by slice (64-column tables), overlapped with the per-slice
         aggregation: row shards (g > 1) whose engine has the staged GAT operations."""
         from . import exchange
-        return (self.part.g > 1 and exchange.STAGED and hasattr(self.engine, "gat_fwd_slice")
+        return (self.part.g > 1 and exchange.staged_for(dtype)
+                and hasattr(self.engine, "gat_fwd_slice")
                 and self.engine.gat_staged_ok(heads, d_head))
 
     def halo_slices(self, h_loc, gat=False):
@@ -716,7 +717,7 @@ class HaloGATFn(torch.autograd.Function):
     def forward(ctx, H, a_all, dadj, heads, d_head, alpha, act):
         ctx.dadj = dadj
         ctx.meta = (heads, d_head, float(alpha), int(act))
-        ctx.staged = dadj.staged_gat(heads, d_head) and H.shape[1] == heads * d_head
+        ctx.staged = dadj.staged_gat(heads, d_head, H.dtype) and H.shape[1] == heads * d_head
         if ctx.staged:  # per-slice exchange / aggregation (§8e overlap)
             Y, ctx.saved = dadj.gat_staged_forward(H.contiguous(), a_all, heads, d_head, alpha,
                                                    act)
@@ -783,23 +784,28 @@ def _world_sum(t):
     return t
 
 
-def validate_staged(dadj, D=300, heads=4, alpha=0.2, dtype=None, reps=3, tol=1e-6, seed=0,
-                    apply=True):
+def validate_staged(dadj, D=300, heads=4, alpha=0.2, dtypes=None, reps=3, tol=1e-6,
+                    tol_bf16=1e-2, seed=0, apply=True):
     """Prove the per-slice halo pipeline on this job's own ranks before it is used (SURVEY.md §8e;
     layers/layers.py:35,64, layers/att_layers.py:45-58): one HighWay layer tail
     (HaloHighwayFn), one GCN aggregation (HaloAggregateFn) and one all-head GAT layer
-    (HaloGATFn), forward + backward on the same seeded inputs with exchange.STAGED off, then on.
+    (HaloGATFn), forward + backward on the same seeded inputs with exchange.STAGED off, then on,
+    once per storage dtype in ``dtypes`` (default fp32 on the device, fp64 on the CPU; the bench
+    passes fp32 and bf16, configs[4]'s dtype, whose staged GAT runs the bf16 64-column tables).
     The legs run with smooth activations (tanh; GAT: none): with relu, an output within rounding
     of 0 can take the other branch of relu' on one side, and the input gradient then differs by
     a whole adjacency weight at that row (the staged and unstaged forwards sum in different
     orders) — a branch decision, not an exchange error.
     Compared: outputs, input gradients and the world-summed `a` gradient, norm-relative
-    ‖staged − unstaged‖∞ / ‖unstaged‖∞, the max over tensors and ranks; `match` when it is
-    ≤ ``tol`` and finite on every rank (one all-reduce decides, so all ranks agree).  Each leg is
-    timed both ways (median of ``reps`` fwd + bwd after one warm-up, wall clock bracketed by
-    barriers and device syncs, max over ranks).  ``apply``: leave exchange.STAGED = match
-    (GNNEA_HALO_STAGED=0 keeps it off whatever the outcome).  Every rank must call this.
-    Returns the report (the same dict on every rank)."""
+    ‖staged − unstaged‖∞ / ‖unstaged‖∞, the max over tensors and ranks; a dtype matches when it
+    is ≤ ``tol`` (bf16: ``tol_bf16``, the bf16 storage tolerance of tests/test_gpu_scale_cfg5.py:
+    the two paths round differently ordered fp32 sums to bf16) and finite on every rank (one
+    all-reduce decides, so all ranks agree).  Each leg is timed both ways (median of ``reps``
+    fwd + bwd after one warm-up, wall clock bracketed by barriers and device syncs, max over
+    ranks).  ``apply`` (GNNEA_HALO_STAGED unset / "auto"): exchange.STAGED is left on for
+    exactly the dtypes that matched (exchange.STAGED_DTYPES), off when none did; "0" keeps it
+    off and "1" keeps it on for every dtype whatever the outcome (the report still says what
+    matched).  Every rank must call this.  Returns the report (the same dict on every rank)."""
     import time
 
     from . import exchange
@@ -807,50 +813,53 @@ def validate_staged(dadj, D=300, heads=4, alpha=0.2, dtype=None, reps=3, tol=1e-
     if part.g == 1:
         return {"applies": False, "reason": "one KG per rank: nothing to exchange"}
     dev = dadj.device
-    if dtype is None:
-        dtype = torch.float64 if dev.type == "cpu" else torch.float32
+    if dtypes is None:
+        dtypes = (torch.float64 if dev.type == "cpu" else torch.float32,)
     d_head = D // heads
     n = part.n_rows
-    # the rows are the rank's own; the parameters (bias_gate, a) are replicated on every rank
-    rows_gen = torch.Generator(device=dev).manual_seed(seed * 1000 + 1 + part.rank)
-    par_gen = torch.Generator(device=dev).manual_seed(seed * 1000)
-
-    def rnd(*shape, scale=1.0, gen=rows_gen):
-        return (scale * torch.randn(*shape, generator=gen, device=dev, dtype=torch.float32)
-                ).to(dtype)
-    hidden, gate_pre, resid = rnd(n, D), rnd(n, D), rnd(n, D)
-    bias_gate = rnd(D, scale=0.1, gen=par_gen)
-    dY = rnd(n, D)
-    H = rnd(n, heads * d_head, scale=0.3)
-    a_all = rnd(heads, 2 * d_head, scale=0.3, gen=par_gen)
-    dYg = rnd(n, heads * d_head)
 
     def sync():
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
-    def leg_highway():
-        xs = [t.clone().requires_grad_() for t in (hidden, gate_pre, resid)]
-        out = dadj.highway(xs[0], xs[1], xs[2], bias_gate, torch.tanh)
-        out.backward(dY)
-        return [out.detach()] + [x.grad for x in xs]
+    def make_legs(dtype):
+        # the rows are the rank's own; the parameters (bias_gate, a) are replicated on every rank
+        rows_gen = torch.Generator(device=dev).manual_seed(seed * 1000 + 1 + part.rank)
+        par_gen = torch.Generator(device=dev).manual_seed(seed * 1000)
 
-    def leg_gcn():
-        x = hidden.clone().requires_grad_()
-        out = dadj.aggregate(x, torch.tanh)
-        out.backward(dY)
-        return [out.detach(), x.grad]
+        def rnd(*shape, scale=1.0, gen=rows_gen):
+            return (scale * torch.randn(*shape, generator=gen, device=dev, dtype=torch.float32)
+                    ).to(dtype)
+        hidden, gate_pre, resid = rnd(n, D), rnd(n, D), rnd(n, D)
+        bias_gate = rnd(D, scale=0.1, gen=par_gen)
+        dY = rnd(n, D)
+        H = rnd(n, heads * d_head, scale=0.3)
+        a_all = rnd(heads, 2 * d_head, scale=0.3, gen=par_gen)
+        dYg = rnd(n, heads * d_head)
 
-    def leg_gat():
-        h = H.clone().requires_grad_()
-        a = a_all.clone().requires_grad_()
-        out = dadj.gat(h, a, heads, d_head, alpha, None)
-        out.backward(dYg)
-        return [out.detach(), h.grad, _world_sum(a.grad)]
-    legs = {"highway": leg_highway, "gcn": leg_gcn}
-    if dadj.engine.gat_staged_ok(heads, d_head) if hasattr(dadj.engine, "gat_staged_ok") \
-            else False:
-        legs["gat"] = leg_gat
+        def leg_highway():
+            xs = [t.clone().requires_grad_() for t in (hidden, gate_pre, resid)]
+            out = dadj.highway(xs[0], xs[1], xs[2], bias_gate, torch.tanh)
+            out.backward(dY)
+            return [out.detach()] + [x.grad for x in xs]
+
+        def leg_gcn():
+            x = hidden.clone().requires_grad_()
+            out = dadj.aggregate(x, torch.tanh)
+            out.backward(dY)
+            return [out.detach(), x.grad]
+
+        def leg_gat():
+            h = H.clone().requires_grad_()
+            a = a_all.clone().requires_grad_()
+            out = dadj.gat(h, a, heads, d_head, alpha, None)
+            out.backward(dYg)
+            return [out.detach(), h.grad, _world_sum(a.grad)]
+        legs = {"highway": leg_highway, "gcn": leg_gcn}
+        if dadj.engine.gat_staged_ok(heads, d_head) if hasattr(dadj.engine, "gat_staged_ok") \
+                else False:
+            legs["gat"] = leg_gat
+        return legs
 
     def timed(fn):
         fn()
@@ -864,20 +873,26 @@ def validate_staged(dadj, D=300, heads=4, alpha=0.2, dtype=None, reps=3, tol=1e-
             ts.append(time.perf_counter() - t0)
         return float(np.median(ts)) * 1e3
 
-    keep = exchange.STAGED
-    res, ms = {}, {}
+    keep, keep_dt = exchange.STAGED, exchange.STAGED_DTYPES
+    res, ms, names = {}, {}, {}
     try:
-        for mode in (False, True):
-            exchange.STAGED = mode
-            for name, fn in legs.items():
-                res[(name, mode)] = [t.detach().clone() for t in fn()]
-                ms[(name, mode)] = timed(fn)
+        exchange.STAGED_DTYPES = None  # the legs run each mode for their own dtype
+        for dtype in dtypes:
+            legs = make_legs(dtype)
+            names[dtype] = list(legs)
+            for mode in (False, True):
+                exchange.STAGED = mode
+                for name, fn in legs.items():
+                    res[(dtype, name, mode)] = [t.detach().clone() for t in fn()]
+                    ms[(dtype, name, mode)] = timed(fn)
+            del legs
     finally:
-        exchange.STAGED = keep
+        exchange.STAGED, exchange.STAGED_DTYPES = keep, keep_dt
+    keys = [(dt, k) for dt in dtypes for k in names[dt]]
     errs = []
-    for name in legs:
+    for dt, name in keys:
         e = 0.0
-        for s, u in zip(res[(name, True)], res[(name, False)]):
+        for s, u in zip(res[(dt, name, True)], res[(dt, name, False)]):
             s, u = s.double(), u.double()
             if not bool(torch.isfinite(s).all()) or s.shape != u.shape:
                 e = float("inf")
@@ -886,27 +901,46 @@ def validate_staged(dadj, D=300, heads=4, alpha=0.2, dtype=None, reps=3, tol=1e-
             num = float((s - u).abs().max()) if u.numel() else 0.0
             e = max(e, num / den if den > 0 else (0.0 if num == 0 else float("inf")))
         errs.append(e)
+    res = None
     # one all-reduce: every rank's errors (max) and its leg times (max over ranks)
-    times = [ms[(k, m)] for k in legs for m in (True, False)]
+    times = [ms[(dt, k, m)] for dt, k in keys for m in (True, False)]
     red = _world_reduce([min(e, 1e300) for e in errs] + times, dist.ReduceOp.MAX)
-    errs, times = red[:len(legs)], red[len(legs):]
-    err = max(errs)
-    match = err <= tol
-    report = {"applies": True, "match": bool(match), "tol": tol, "max_norm_rel_err": err,
-              "legs": {}, "dtype": str(dtype).replace("torch.", ""), "D": D, "heads": heads,
-              "reps": reps, "world": part.world, "group_ranks": part.g,
-              "method": "staged vs unstaged on the same inputs: outputs, input gradients and "
-                        "the world-summed attention-vector gradient, norm-relative, max over "
-                        "tensors and ranks; fwd + bwd wall ms, median of %d, max over ranks"
-                        % reps}
-    for i, k in enumerate(legs):
-        report["legs"][k] = {"err": errs[i], "staged_ms": round(times[2 * i], 4),
-                             "unstaged_ms": round(times[2 * i + 1], 4)}
+    errs, times = red[:len(keys)], red[len(keys):]
+    report = {"applies": True, "reps": reps, "world": part.world, "group_ranks": part.g,
+              "D": D, "heads": heads, "dtypes": {},
+              "method": "staged vs unstaged on the same inputs, per storage dtype: outputs, input "
+                        "gradients and the world-summed attention-vector gradient, "
+                        "norm-relative, max over tensors and ranks; fwd + bwd wall ms, median "
+                        "of %d, max over ranks" % reps}
+    matched = []
+    for dt in dtypes:
+        name = str(dt).replace("torch.", "")
+        t_ = tol_bf16 if dt == torch.bfloat16 else tol
+        rep = {"tol": t_, "legs": {}}
+        e_dt = 0.0
+        for i, (d2, k) in enumerate(keys):
+            if d2 != dt:
+                continue
+            e_dt = max(e_dt, errs[i])
+            rep["legs"][k] = {"err": errs[i], "staged_ms": round(times[2 * i], 4),
+                              "unstaged_ms": round(times[2 * i + 1], 4)}
+        rep["max_norm_rel_err"] = e_dt
+        rep["match"] = bool(e_dt <= t_)
+        if rep["match"]:
+            matched.append(dt)
+        report["dtypes"][name] = rep
+    report["match"] = len(matched) == len(dtypes)
     report["staged_ms"] = round(sum(times[0::2]), 4)
     report["unstaged_ms"] = round(sum(times[1::2]), 4)
     if apply:
-        exchange.STAGED = bool(match) and exchange.STAGED_ENV != "0"
-    report["staged_in_use"] = bool(exchange.STAGED) if apply else bool(keep)
+        if exchange.STAGED_ENV == "0":
+            exchange.STAGED, exchange.STAGED_DTYPES = False, None
+        elif exchange.STAGED_ENV != "1":
+            exchange.STAGED = bool(matched)
+            exchange.STAGED_DTYPES = set(matched) if matched else None
+    report["staged_env"] = exchange.STAGED_ENV
+    report["staged_in_use"] = {str(dt).replace("torch.", ""): bool(exchange.staged_for(dt))
+                               for dt in dtypes}
     return report
 
 
@@ -916,7 +950,12 @@ def allreduce_grads(params, group=None):
     ps = [p for p in params if p.grad is not None]
     if not ps or dist.get_world_size(group) == 1:
         return
-    flat = torch.cat([p.grad.reshape(-1) for p in ps])
+    # summed in at least fp32: bf16 gradients (configs[4]) are rounded once, after the sum,
+    # instead of at every step of the reduction
+    acc = torch.float32
+    for p in ps:
+        acc = torch.promote_types(acc, p.grad.dtype)
+    flat = torch.cat([p.grad.reshape(-1).to(acc) for p in ps])
     if dist.get_backend(group) == "gloo" and flat.device.type != "cpu":
         h = flat.cpu()
         dist.all_reduce(h, group=group)

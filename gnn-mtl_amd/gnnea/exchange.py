@@ -43,10 +43,20 @@ MODE = os.environ.get("GNNEA_HALO", "relay")
 # two ranks on one device ("Duplicate GPU detected"), so the staged path's asynchronous RCCL
 # behaviour is proven on the job's own ranks: gnnea.dist_graph.validate_staged runs a HighWay,
 # a GCN and a GAT layer both ways on the same inputs, and switches STAGED on only when every
-# rank saw the two agree.  GNNEA_HALO_STAGED: "auto" (default: unstaged until validated), "1"
-# (staged without validation), "0" (never staged, validate_staged reports but keeps it off).
+# rank saw the two agree.  GNNEA_HALO_STAGED: "auto" (default: unstaged until validated; then
+# staged for exactly the storage dtypes whose legs matched), "1" (staged for every dtype without
+# validation: validate_staged reports but changes nothing), "0" (never staged, validate_staged
+# reports but keeps it off).
 STAGED_ENV = os.environ.get("GNNEA_HALO_STAGED", "auto")
 STAGED = STAGED_ENV == "1"
+# None: STAGED applies to every storage dtype (GNNEA_HALO_STAGED=1, tests); else the set of
+# dtypes validate_staged saw match on this job's ranks
+STAGED_DTYPES = None
+
+
+def staged_for(dtype):
+    """Whether the per-slice pipeline carries a halo of this storage dtype."""
+    return STAGED and (STAGED_DTYPES is None or dtype in STAGED_DTYPES)
 
 
 def _gloo(group):
@@ -252,15 +262,29 @@ class PendingSum:
     def finish(self):
         for w in self.works:
             w.wait()
-        out = self.out
-        if out is None:
-            out = self.own.clone()
-        else:
-            out.copy_(self.own)
-        for r in self.recv:
-            out += r.to(out.device) if r.device != out.device else r
+        out = _owner_sum(self.own, self.recv, self.out)
         self.own = self.recv = self.works = None
         return out
+
+
+def _owner_sum(own, recv, out=None):
+    """own + recv[0] + recv[1] + ... in that order.  Low-precision partials (bf16 storage) are
+    summed in fp32 and rounded once into ``out`` (a bf16 running sum would round at every peer)."""
+    if own.dtype in (torch.bfloat16, torch.float16) and recv:
+        acc = own.float()
+        for r in recv:
+            acc += r.to(device=acc.device, dtype=torch.float32)
+        if out is None:
+            return acc.to(own.dtype)
+        out.copy_(acc)
+        return out
+    if out is None:
+        out = own.clone()
+    else:
+        out.copy_(own)
+    for r in recv:
+        out += r.to(out.device) if r.device != out.device else r
+    return out
 
 
 def reduce_scatter_start(partial, group, ranks, li, other=None, out=None):
@@ -322,11 +346,8 @@ def reduce_scatter(partial, group, ranks, li, other=None):
         send = [b.detach().cpu() if stage else b for b in blocks]
         recv = {p: torch.empty_like(send[li]) for p in ranks if p != ranks[li]}
         _relay_rs(send, recv, ranks, li, other, sync=True)
-        out = blocks[li].clone()
-        for p in ranks:  # peer order, as the direct schedule sums
-            if p != ranks[li]:
-                out += recv[p].to(out.device) if stage else recv[p]
-        return out
+        # peer order, as the direct schedule sums
+        return _owner_sum(blocks[li], [recv[p] for p in ranks if p != ranks[li]])
     if not _gloo(group) and MODE == "ring":
         out = torch.empty_like(blocks[li])
         dist.reduce_scatter_tensor(out, partial, group=group)
@@ -341,8 +362,4 @@ def reduce_scatter(partial, group, ranks, li, other=None):
             ops.append(dist.P2POp(dist.irecv, recv[p], ranks[p], group=group))
     for w in dist.batch_isend_irecv(ops):
         w.wait()
-    out = blocks[li].clone()
-    for p in range(g):
-        if p != li:
-            out += recv[p].to(out.device) if stage else recv[p]
-    return out
+    return _owner_sum(blocks[li], [recv[p] for p in range(g) if p != li])

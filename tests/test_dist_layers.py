@@ -29,6 +29,11 @@ def _free_port():
     return port
 
 
+def _mm(A, x):
+    """A·x in x's dtype (the fp64 adjacency cast for bf16 storage: torch's CPU bf16 sparse mm)."""
+    return torch.sparse.mm(A if A.dtype == x.dtype else A.to(x.dtype), x)
+
+
 class CpuEngine:
     """fp64 torch double of gnnea.dist_graph.HipEngine (test stand-in, never shipped)."""
 
@@ -42,7 +47,7 @@ class CpuEngine:
         return torch.relu(y) if act == 1 else y
 
     def spmm(self, A, x, act, out=None, beta=0.0):
-        y = torch.sparse.mm(A, x)
+        y = _mm(A, x)
         if out is not None:
             y = y + beta * out
             out.copy_(self._act(y, act))
@@ -50,7 +55,7 @@ class CpuEngine:
         return self._act(y, act)
 
     def spmm_t(self, A, x, out=None):
-        y = torch.sparse.mm(A.t().coalesce(), x)
+        y = _mm(A.t().coalesce(), x)
         if out is not None:
             out.copy_(y)
             return out
@@ -63,7 +68,7 @@ class CpuEngine:
         return self.spmm_t(A, self.act_bwd(dy, y, act))
 
     def highway_fwd(self, A, h, gate_pre, resid, bias, act):
-        S = self._act(torch.sparse.mm(A, h), act)
+        S = self._act(_mm(A, h), act)
         g = torch.sigmoid(gate_pre + bias if bias is not None else gate_pre)
         return g * S + (1 - g) * resid, S, g
 
@@ -85,11 +90,11 @@ class CpuEngine:
         return tables
 
     def spmm_slice(self, A, table, w, act, out):
-        out.copy_(self._act(torch.sparse.mm(A, table[:, :w].contiguous()), act))
+        out.copy_(self._act(_mm(A, table[:, :w].contiguous()), act))
         return out
 
     def spmm_t_slice(self, A, table, w):
-        return torch.sparse.mm(A.t().coalesce(), table[:, :w].contiguous())
+        return _mm(A.t().coalesce(), table[:, :w].contiguous())
 
     def _slices(self, x):
         S = (x.shape[1] + self.W - 1) // self.W
@@ -99,7 +104,7 @@ class CpuEngine:
         return self._slices(self.act_bwd(dy, y, act))
 
     def highway_slice(self, A, table, w, gates, c0, bias, resid, out, S, G, act):
-        sv = self._act(torch.sparse.mm(A, table[:, :w].contiguous()), act)
+        sv = self._act(_mm(A, table[:, :w].contiguous()), act)
         gp = gates[c0 // self.W][:, :w]
         g = torch.sigmoid(gp + bias[c0:c0 + w] if bias is not None else gp)
         out[:, c0:c0 + w] = g * sv + (1 - g) * resid[:, c0:c0 + w]
@@ -309,13 +314,18 @@ def _worker(rank, world, port, mode, q, staged=True):
         X = torch.from_numpy(synth.features(2 * N_KG, D, seed=5)).double()
         Rw = torch.from_numpy(np.random.default_rng(9).standard_normal((2 * N_KG, D)))
         HEADS, DH = 3, D // 3
-        if mode == "gat_cpu":
+        if mode in ("gat_cpu", "gat_cpu_bf16"):
+            # gat_cpu_bf16: every tensor the DistAdj moves (H halo, slice tables, dH partials,
+            # parameter gradients) in bf16 through gloo; the engine double computes in torch's
+            # CPU bf16 arithmetic, so the bar is the bf16 one
+            dt = torch.bfloat16 if mode == "gat_cpu_bf16" else torch.float64
             dev = torch.device("cpu")
             dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev, engine=CpuEngine())
             torch.manual_seed(0)
-            Wg = torch.randn(D, D, dtype=torch.float64) * 0.3
-            a_all = torch.randn(HEADS, 2 * DH, dtype=torch.float64) * 0.3
-            W2 = torch.randn(D, D, dtype=torch.float64)
+            X, Rw = X.to(dt), Rw.to(dt)
+            Wg = (torch.randn(D, D, dtype=torch.float64) * 0.3).to(dt)
+            a_all = (torch.randn(HEADS, 2 * DH, dtype=torch.float64) * 0.3).to(dt)
+            W2 = (torch.randn(D, D, dtype=torch.float64) / D ** 0.5).to(dt)
             params = [p.requires_grad_() for p in (Wg, a_all, W2)]
 
             def model(x, adj):
@@ -325,16 +335,20 @@ def _worker(rank, world, port, mode, q, staged=True):
                     return CpuEngine.gat_dense(A, y @ W2, a_all, HEADS, DH, 0.2, 0, 0)
                 y = adj.gat(x @ Wg, a_all, HEADS, DH, 0.2, F.relu)
                 return adj.gather_rows(adj.gat(y @ W2, a_all, HEADS, DH, 0.2, None))
-            tol = 1e-12
-        elif mode == "gat_gpu":
+            tol = 5e-2 if dt == torch.bfloat16 else 1e-12
+        elif mode in ("gat_gpu", "gat_gpu_bf16"):
+            # gat_gpu_bf16: configs[4]'s storage dtype -- the bf16 projection, the bf16 halo and
+            # (staged) the bf16 64-column GAT slice tables / dH partials, against the same bf16
+            # layers on the whole adjacency in one process (the row-major bf16 passes)
             from layers.att_layers import GraphAttentionLayer
+            dt = torch.bfloat16 if mode == "gat_gpu_bf16" else torch.float32
             dev = torch.device("cuda:0")
             torch.cuda.set_device(dev)
-            X, Rw = X.float().to(dev), Rw.float().to(dev)
+            X, Rw = X.to(device=dev, dtype=dt), Rw.float().to(dev)
             dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev)
             torch.manual_seed(0)
-            g1 = GraphAttentionLayer(D, DH, 0.0, F.relu, 0.2, HEADS, True).to(dev)
-            g2 = GraphAttentionLayer(D, DH, 0.0, F.elu, 0.2, HEADS, True).to(dev)  # torch act
+            g1 = GraphAttentionLayer(D, DH, 0.0, F.relu, 0.2, HEADS, True).to(dev, dt)
+            g2 = GraphAttentionLayer(D, DH, 0.0, F.elu, 0.2, HEADS, True).to(dev, dt)  # torch act
             params = list(g1.parameters()) + list(g2.parameters())
             adj_full = torch.sparse_coo_tensor(torch.from_numpy(np.stack([R, C])).long(),
                                                torch.from_numpy(V), (2 * N_KG, 2 * N_KG)).to(dev)
@@ -343,7 +357,8 @@ def _worker(rank, world, port, mode, q, staged=True):
                 if adj is None:
                     return g2(g1((x, adj_full)))[0]
                 return adj.gather_rows(g2(g1((x, adj)))[0])
-            tol = 1e-4
+            # bf16: the storage tolerance of tests/test_gpu_scale_cfg5.py on gradients (2e-2)
+            tol = 2e-2 if dt == torch.bfloat16 else 1e-4
         elif mode == "loss_cpu":
             # the column-sharded EA margin loss (gnnea.dist_loss) on a GCN + HighWay shard
             # against the reference loss on the whole graph's output
@@ -544,11 +559,11 @@ class BrokenStagedEngine(CpuEngine):
 
     def spmm_slice(self, A, table, w, act, out):
         super().spmm_slice(A, table, w, act, out)
-        out.mul_(1.0 + 1e-3)
+        out.mul_(1.25)  # (wrong by more than the bf16 bar too)
         return out
 
 
-def _ab_worker(rank, world, port, broken, q):
+def _ab_worker(rank, world, port, broken, q, env="auto"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "gnn-mtl_amd"))
@@ -558,28 +573,38 @@ def _ab_worker(rank, world, port, broken, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        exchange.STAGED = False
-        exchange.STAGED_ENV = "auto"
+        exchange.STAGED_ENV = env
+        exchange.STAGED = env == "1"
+        exchange.STAGED_DTYPES = None
         tr = synth.kg_pair_triples(N_KG, T_KG, 20)
         eng = BrokenStagedEngine() if broken else CpuEngine()
         dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, torch.device("cpu"), engine=eng)
-        rep = validate_staged(dadj, D=D, heads=3, reps=2, tol=1e-12)
-        q.put((rank, rep["match"], rep["max_norm_rel_err"], exchange.STAGED,
-               sorted(rep["legs"]), rep["staged_in_use"]))
+        # fp64 (the engine double's exact arithmetic) and bf16 (configs[4]'s storage; the
+        # double computes in CPU bf16 arithmetic, hence the looser bar)
+        rep = validate_staged(dadj, D=D, heads=3, reps=2, tol=1e-12, tol_bf16=5e-2,
+                              dtypes=(torch.float64, torch.bfloat16))
+        q.put((rank, {k: (v["match"], v["max_norm_rel_err"], sorted(v["legs"]))
+                      for k, v in rep["dtypes"].items()}, rep["match"],
+               [exchange.staged_for(t) for t in (torch.float64, torch.bfloat16, torch.float32)],
+               rep["staged_in_use"]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,broken", [(4, False), (4, True), (8, False)])
-def test_validate_staged_gloo_cpu(world, broken):
+@pytest.mark.parametrize("world,broken,env", [(4, False, "auto"), (4, True, "auto"),
+                                              (8, False, "auto"), (4, True, "1"),
+                                              (4, False, "0")])
+def test_validate_staged_gloo_cpu(world, broken, env):
     """gnnea.dist_graph.validate_staged (the N > 1 bench's halo_ab): staged and unstaged HighWay,
-    GCN and GAT layers on the same inputs; a correct pipeline matches (fp64 engine: 1e-12) and is
-    switched on, a pipeline wrong in one slice is caught on every rank and the halo stays
-    unstaged."""
+    GCN and GAT layers on the same inputs, in fp64 and in bf16; a correct pipeline matches in
+    both and is switched on for exactly those dtypes (fp32, never validated here, stays
+    unstaged), a pipeline wrong in one slice is caught on every rank and the halo stays
+    unstaged.  GNNEA_HALO_STAGED=1 keeps the staged path on whatever validation says (the report
+    still records the mismatch); =0 keeps it off."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ab_worker, args=(r, world, port, broken, q))
+    procs = [ctx.Process(target=_ab_worker, args=(r, world, port, broken, q, env))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -587,14 +612,24 @@ def test_validate_staged_gloo_cpu(world, broken):
         p.join(180)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     res = [q.get(timeout=5) for _ in range(world)]
-    for rank, match, err, staged, legs, in_use in res:
-        assert legs == ["gat", "gcn", "highway"]
-        assert match is (not broken), (rank, err)
-        assert staged is (not broken) and in_use is (not broken)
-        if broken:
-            assert err > 1e-4
+    for rank, per, match, staged_for, in_use in res:
+        assert sorted(per) == ["bfloat16", "float64"]
+        for name, (m, err, legs) in per.items():
+            assert legs == ["gat", "gcn", "highway"]
+            assert m is (not broken), (rank, name, err)
+            if broken:
+                assert err > 1e-4
+            else:
+                assert err <= (1e-12 if name == "float64" else 5e-2), (name, err)
+        assert match is (not broken)
+        if env == "1":
+            want = [True, True, True]
+        elif env == "0" or broken:
+            want = [False, False, False]
         else:
-            assert err <= 1e-12
+            want = [True, True, False]
+        assert staged_for == want, (rank, staged_for)
+        assert in_use == {"float64": want[0], "bfloat16": want[1]}
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
@@ -625,6 +660,24 @@ def test_dist_gat_gloo_cpu(world):
 def test_dist_gat_gloo_cpu_unstaged(world):
     """GNNEA_HALO_STAGED=0: the whole H halo, one aggregation, one blocking reduce-scatter."""
     _run(world, "gat_cpu", staged=False)
+
+
+@pytest.mark.parametrize("world,staged", [(2, True), (4, True), (4, False), (8, True)])
+def test_dist_gat_bf16_gloo_cpu(world, staged):
+    """configs[4]'s storage dtype through the row-sharded GAT: the bf16 H halo, slice tables,
+    dH partials and ds2 sums move through the same exchange schedule (gloo), the bf16 parameter
+    gradients through allreduce_grads; against the single-process bf16 computation."""
+    _run(world, "gat_cpu_bf16", staged)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,staged", [(2, True), (4, True), (4, False)])
+def test_dist_gat_bf16_rehearsal_on_device(device, world, staged):
+    """The drop-in GraphAttentionLayer in bf16 (configs[4]) handed a DistAdj on the HIP kernels:
+    world 4 staged runs gnnea_gat_fwd_sliced_range_bf16 / gnnea_gat_bwd_src_sliced_range_bf16
+    over the exchanged bf16 64-column tables, unstaged the row-major bf16 passes over the whole
+    halo; against the same bf16 layers on the whole adjacency (2e-2 norm-relative)."""
+    _run(world, "gat_gpu_bf16", staged)
 
 
 @pytest.mark.gpu

@@ -34,7 +34,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, model_name, q):
+def _worker(rank, world, port, model_name, q, dtype="f32"):
     import sys
     import types
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -62,10 +62,12 @@ def _worker(rank, world, port, model_name, q):
                                      n_classes=D, cuda=0, device=dev, n_nodes=2 * N_KG,
                                      neg_num=k, data={"train": pairs, "test": pairs})
         data = {"train": pairs, "test": pairs}
+        dt = torch.bfloat16 if dtype == "bf16" else torch.float32
+        X = X.to(dt)
         torch.manual_seed(10086)
-        ref = EAModel(args).to(dev)
+        ref = EAModel(args).to(dev, dt)
         torch.manual_seed(10086)
-        mdl = EAModel(args).to(dev)
+        mdl = EAModel(args).to(dev, dt)
         dadj = DistAdj.from_triples(tr, N_KG, T_KG, rank, world, dev)
         p0, nr = dadj.part.global_row0, dadj.part.n_rows
         # sharded forward; the search on the rank's rows vs the one-GPU search on the gathered rows
@@ -85,6 +87,15 @@ def _worker(rank, world, port, model_name, q):
         # the sharded loss and gradients vs the one-process model on the whole graph
         loss = mdl.get_loss(out, data, "train")
         loss.backward()
+        # each rank's partial of every parameter gradient, rounded to the parameter dtype: for a
+        # gradient that is analytically zero (the last Linear's bias: the L1 loss is translation
+        # invariant) the partials cancel across ranks and what is left is their rounding, at
+        # most half an ulp of each -- the bound that gradient is held to
+        ulp = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -24
+        bounds = {n: (p.grad.detach().float().abs() * ulp).cpu() for n, p in mdl.named_parameters()
+                  if p.grad is not None}
+        for b_ in bounds.values():
+            dist.all_reduce(b_)
         allreduce_grads(list(mdl.parameters()))
         enc_r = ref.encode(X, adj_full)
         enc_r.retain_grad()
@@ -101,9 +112,16 @@ def _worker(rank, world, port, model_name, q):
         # Linear's bias gradient is a sum of +-c sign(x_a - x_b) pairs that cancels exactly (L1
         # distances are translation invariant), so its own scale is rounding noise
         gmax = max(float(pr.grad.abs().max()) for pr in ref.parameters() if pr.grad is not None)
-        res["grad_errs"] = {n: float((p.grad.double() - pr.grad.double()).abs().max()) / gmax
-                            for (n, p), pr in zip(mdl.named_parameters(), ref.parameters())
-                            if pr.grad is not None}
+        res["grad_errs"], res["zero_grads"] = {}, {}
+        for (n, p), pr in zip(mdl.named_parameters(), ref.parameters()):
+            if pr.grad is None:
+                continue
+            diff = (p.grad.double() - pr.grad.double()).abs().cpu()
+            if float(pr.grad.abs().max()) < 1e-3 * gmax:  # analytically zero: the rounding bound
+                res["zero_grads"][n] = float((diff - bounds[n].double()
+                                              - pr.grad.double().abs().cpu()).max()) / gmax
+            else:
+                res["grad_errs"][n] = float(diff.max()) / gmax
         res["grads"] = max(res["grad_errs"].values())
         res["enc_grad"] = rel(enc.grad, enc_r.grad[p0:p0 + nr])
         q.put((rank, res))
@@ -112,14 +130,19 @@ def _worker(rank, world, port, model_name, q):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("model_name", ["GCN", "HGCN"])
-def test_eamodel_sharded_rehearsal(device, world, model_name):
+@pytest.mark.parametrize("model_name,dtype", [("GCN", "f32"), ("HGCN", "f32"), ("GAT", "f32"),
+                                              ("GAT", "bf16")])
+def test_eamodel_sharded_rehearsal(device, world, model_name, dtype):
+    """GAT / bf16: configs[4]'s model and storage dtype (two 4-head GAT layers, the MLP decoder,
+    bf16 projections, halo and -- world 4, staged -- the bf16 GAT slice tables); bf16 judged at
+    the storage tolerances of tests/test_gpu_scale_cfg5.py (outputs 1e-2, gradients 2e-2 of the
+    largest, loss 1e-2), the searches index-exact as in fp32 (both run on the same output)."""
     import queue
     import time
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, model_name, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, model_name, q, dtype))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -136,6 +159,11 @@ def test_eamodel_sharded_rehearsal(device, world, model_name):
         p.join(60)
     for rank, r in out:
         assert r["neg_right"] and r["neg2_left"] and r["hits"], (rank, r)
-        bad = {k: v for k, v in r["grad_errs"].items() if v >= 1e-4}
-        assert r["out"] < 1e-4 and r["loss"] < 1e-5 and r["grads"] < 1e-4, \
+        t_out, t_loss, t_grad = (1e-2, 1e-2, 2e-2) if dtype == "bf16" else (1e-4, 1e-5, 1e-4)
+        bad = {k: v for k, v in r["grad_errs"].items() if v >= t_grad}
+        print(model_name, dtype, world, rank, "out %.2e loss %.2e grads %.2e enc_grad %.2e"
+              % (r["out"], r["loss"], r["grads"], r["enc_grad"]), "zero-gradient excess over "
+              "the partials' rounding bound:", r["zero_grads"])
+        assert all(v <= 1e-6 for v in r["zero_grads"].values()), (rank, r["zero_grads"])
+        assert r["out"] < t_out and r["loss"] < t_loss and r["grads"] < t_grad, \
             (rank, r["out"], r["loss"], r["enc_grad"], bad)

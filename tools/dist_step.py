@@ -92,9 +92,12 @@ def loss_indices(n, t=4500, k=125, seed=7):
              rng.integers(0, 2 * n, t * k), np.repeat(right, k)], t, k)
 
 
-def measure(model, n, rank, world, dev, steps, warmup, dtype=torch.float32, attribute=3):
+def measure(model, n, rank, world, dev, steps, warmup, dtype=torch.float32, attribute=3,
+            min_steps=21, min_warmup=3):
     """Time `steps` sharded training steps (after `warmup`), max over ranks; returns the summary
-    (the same dict on every rank).  Every rank runs the same collective sequence."""
+    (the same dict on every rank).  Every rank runs the same collective sequence.  SURVEY.md §8d
+    timing asks for >= 3 warm-ups and >= 21 timed steps (min_warmup / min_steps; lower only for
+    the one-device rehearsal, where the rate means nothing)."""
     from gnnea.profile import ClockSampler, KernelClassTimer
     t0 = time.time()
     enc, dec, dadj = build(model, n, rank, world, dev, dtype=dtype)
@@ -136,7 +139,7 @@ def measure(model, n, rank, world, dev, steps, warmup, dtype=torch.float32, attr
 
     # SURVEY.md §8d timing: >= 3 warm-ups, then per-step HIP events on the launching stream,
     # median of >= 21 steps (max over ranks step by step); the wall-clock mean is kept beside it
-    warmup, steps = max(3, warmup), max(21, steps)
+    warmup, steps = max(min_warmup, warmup), max(min_steps, steps)
     wev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(warmup)]
     for a, b in wev:  # timed too: first-use costs (allocator growth, lazy transposes) show here
@@ -158,8 +161,10 @@ def measure(model, n, rank, world, dev, steps, warmup, dtype=torch.float32, attr
         torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    # (host tensors under gloo: the one-device rehearsal)
+    red_dev = "cpu" if world > 1 and dist.get_backend() == "gloo" else dev
     per = torch.tensor([a.elapsed_time(b) for a, b in evs] + [(time.perf_counter() - t1) * 1e3],
-                       dtype=torch.float64, device=dev)
+                       dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(per, op=dist.ReduceOp.MAX)
     per = per.cpu()
@@ -191,7 +196,7 @@ def measure(model, n, rank, world, dev, steps, warmup, dtype=torch.float32, attr
         attrib["note"] = ("HIP events around every libgnnea launch of %d steps after the timed "
                           "ones (rank 0); other = torch elementwise kernels, copies, the loss's "
                           "and the halo's collectives, gaps" % attribute)
-    nnz = torch.tensor([float(dadj.nnz)], dtype=torch.float64, device=dev)
+    nnz = torch.tensor([float(dadj.nnz)], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(nnz)  # row shards: every edge of the graph once
     layers = {"HGCN": "3 HighWay graph convolutions",
