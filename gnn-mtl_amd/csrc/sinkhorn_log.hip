@@ -110,6 +110,9 @@ enum { ST_DONE = 0, ST_ITERS = 1, ST_REASON = 2, ST_SLOT = 3, ST_BIG = 4, ST_FAI
 // set by init when C holds a non-finite value: the KNOPP passes then keep the NaN-propagating
 // natural-unit terms instead of the scaled fast path (whose clamp would hide a NaN)
 enum { ST_CNAN = 17 };
+// set by init when some K entry underflows (-C / reg < kExpUnderflow: the reference's exp gives
+// 0 there): only then does the fused sweep carry the per-element mask (a compare and a select)
+enum { ST_CMASK = 18 };
 enum { SD_ERR = GNNEA_SK_SD_ERR, SD_TPREV = GNNEA_SK_SD_TPREV, SD_LOSS = GNNEA_SK_SD_LOSS,
        SD_TOL = GNNEA_SK_SD_TOL, SD_TNEW = GNNEA_SK_SD_TNEW };
 
@@ -677,17 +680,21 @@ __global__ __launch_bounds__(1024) void k_sk_absorb_final(SkArgs a, SkDev d, int
   if (it == max_iter - 1) mark_done(d.st, max_iter, 0, slot);
 }
 
-// ST_CNAN: does C hold a NaN or an infinity (KNOPP: the passes then take the exact terms)
+// ST_CNAN: does C hold a NaN or an infinity (KNOPP: the passes then take the exact terms);
+// ST_CMASK: does any term underflow (-C / reg < kExpUnderflow, the fused sweep's mask predicate)
 template <typename T>
 __global__ __launch_bounds__(256) void k_sk_cscan(const T* __restrict__ C, int I, int J,
-                                                  int64_t ldc, int64_t* st) {
-  bool bad = false;
+                                                  int64_t ldc, double neg_s, int64_t* st) {
+  bool bad = false, msk = false;
   const int64_t n = (int64_t)I * J;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
     const int64_t i = e / J, j = e - i * J;
-    bad |= !isfinite((double)C[i * ldc + j]);
+    const double c = (double)C[i * ldc + j];
+    bad |= !isfinite(c);
+    msk |= c * neg_s < kExpUnderflow;
   }
   if (__any(bad) && lane_id() == 0) atomicOr((unsigned long long*)&st[ST_CNAN], 1ull);
+  if (__any(msk) && lane_id() == 0) atomicOr((unsigned long long*)&st[ST_CMASK], 1ull);
 }
 
 __global__ void k_sk_logw(const double* __restrict__ wa, const double* __restrict__ wb, int I,
@@ -1041,18 +1048,26 @@ __global__ __launch_bounds__(64 * FW) void k_lsk_sweep(const T* __restrict__ C, 
   while (!((double)cthr * neg_s >= kExpUnderflow)) cthr = nextafterf(cthr, -INFINITY);
   while ((double)nextafterf(cthr, INFINITY) * neg_s >= kExpUnderflow)
     cthr = nextafterf(cthr, INFINITY);
-  auto logit = [&](T c, double gsum) {
+  // MT: the mask (std::true_type when init found an underflowing term, ST_CMASK; a uniform
+  // choice for the whole launch): without it no element needs the compare and select
+  auto logit = [&](T c, double gsum, auto mt) {
     if constexpr (sizeof(T) == 4) {
-      const float cm = c > cthr ? 1e30f : (float)c;
+      float cm = (float)c;
+      if constexpr (decltype(mt)::value) cm = c > cthr ? 1e30f : cm;
       return __builtin_fma((double)cm, ncs, gsum);
     } else {
-      const double kn = (double)c * neg_s;
-      const double kk = kn < kExpUnderflow ? -1e300 : kn;
-      return __builtin_fma(kk, kFScale, gsum);
+      if constexpr (decltype(mt)::value) {
+        const double kn = (double)c * neg_s;
+        const double kk = kn < kExpUnderflow ? -1e300 : kn;
+        return __builtin_fma(kk, kFScale, gsum);
+      } else {
+        return __builtin_fma((double)c, ncs, gsum);
+      }
     }
   };
   int nfb = 0;  // rows listed for the exact update (k_lsk_fix)
-  auto process = [&](const T (&kv)[NCM], const double fv, const double wv, int r, int par) {
+  auto process = [&](const T (&kv)[NCM], const double fv, const double wv, int r, int par,
+                     auto mt) {
     // x = (g_j + k_ij) in units of ln2 / 2048; masked terms -3e303 (exp2x -> 0).  The slice of g
     // is re-read from LDS per row (opaque to hoisting: held in registers it would cost 2 NCM)
     asm volatile("" ::: "memory");
@@ -1061,7 +1076,7 @@ __global__ __launch_bounds__(64 * FW) void k_lsk_sweep(const T* __restrict__ C, 
       const double f0 = fv * kFScale;
 #pragma unroll
       for (int k = 0; k < NCM; ++k) {
-        e[k] = exp2x(logit(kv[k], gl[eo(k)] + f0), tab);
+        e[k] = exp2x(logit(kv[k], gl[eo(k)] + f0, mt), tab);
         acc[k] += e[k];
       }
       return;
@@ -1083,7 +1098,7 @@ __global__ __launch_bounds__(64 * FW) void k_lsk_sweep(const T* __restrict__ C, 
       Exp2Part q[EG];
       double tj[EG], pp[EG];
 #pragma unroll
-      for (int u = 0; u < EG; ++u) q[u] = exp2x_split(logit(kv[k0 + u], gv[u] + fps));
+      for (int u = 0; u < EG; ++u) q[u] = exp2x_split(logit(kv[k0 + u], gv[u] + fps, mt));
 #pragma unroll
       for (int u = 0; u < EG; ++u) tj[u] = tab[q[u].ti & (kFTab - 1)];
       if (k0 + EG < NCM) {
@@ -1132,30 +1147,36 @@ __global__ __launch_bounds__(64 * FW) void k_lsk_sweep(const T* __restrict__ C, 
   // count of the path without it, i.e. for most of the next row's loads
   // PAIR: NCM / 2 + 2 loads per row, two rows ahead in flight (three register buffers, the
   // waits vmcnt(2 rows)); otherwise one row ahead
-  int r = r0, par = 0;
-  if constexpr (PAIR && FW == 8) {
-    while (r < r1) {
-      load(kC, fC, wC, min(r + 2, r1 - 1));
-      process(kA, fA, wA, r, par);
-      if (r + 1 >= r1) break;
-      load(kA, fA, wA, min(r + 3, r1 - 1));
-      process(kB, fB, wB, r + 1, par ^ 1);
-      if (r + 2 >= r1) break;
-      load(kB, fB, wB, min(r + 4, r1 - 1));
-      process(kC, fC, wC, r + 2, par);
-      par ^= 1;
-      r += 3;
+  auto rows = [&](auto mt) {
+    int r = r0, par = 0;
+    if constexpr (PAIR && FW == 8) {
+      while (r < r1) {
+        load(kC, fC, wC, min(r + 2, r1 - 1));
+        process(kA, fA, wA, r, par, mt);
+        if (r + 1 >= r1) break;
+        load(kA, fA, wA, min(r + 3, r1 - 1));
+        process(kB, fB, wB, r + 1, par ^ 1, mt);
+        if (r + 2 >= r1) break;
+        load(kB, fB, wB, min(r + 4, r1 - 1));
+        process(kC, fC, wC, r + 2, par, mt);
+        par ^= 1;
+        r += 3;
+      }
+    } else {
+      while (r < r1) {
+        load(kB, fB, wB, min(r + 1, r1 - 1));
+        process(kA, fA, wA, r, par, mt);
+        if (r + 1 >= r1) break;
+        load(kA, fA, wA, min(r + 2, r1 - 1));
+        process(kB, fB, wB, r + 1, par ^ 1, mt);
+        r += 2;
+      }
     }
-  } else {
-    while (r < r1) {
-      load(kB, fB, wB, min(r + 1, r1 - 1));
-      process(kA, fA, wA, r, par);
-      if (r + 1 >= r1) break;
-      load(kA, fA, wA, min(r + 2, r1 - 1));
-      process(kB, fB, wB, r + 1, par ^ 1);
-      r += 2;
-    }
-  }
+  };
+  if (d.st[ST_CMASK])
+    rows(std::true_type{});
+  else
+    rows(std::false_type{});
   double* __restrict__ part = d.fpart + (int64_t)blockIdx.x * a.J + c0 + lbase;
 #pragma unroll
   for (int k = 0; k < NCM; ++k)
@@ -1455,10 +1476,10 @@ int init(const gnnea_sinkhorn* p, void* stream) {
                                                              : 2048;
     if (p->c_dtype == GNNEA_F32)
       hipLaunchKernelGGL(k_sk_cscan<float>, dim3(nb), dim3(256), 0, s, (const float*)p->C, p->I,
-                         p->J, p->ldc, d.st);
+                         p->J, p->ldc, -a.inv_eps, d.st);
     else
       hipLaunchKernelGGL(k_sk_cscan<double>, dim3(nb), dim3(256), 0, s, (const double*)p->C,
-                         p->I, p->J, p->ldc, d.st);
+                         p->I, p->J, p->ldc, -a.inv_eps, d.st);
     GNNEA_LAUNCH_CHECK();
     if (fused_applies(p)) {  // the table, then the partials of v_0 K^T u_0 (slot 1: u_0, v_0)
       hipLaunchKernelGGL(k_lsk_tab, dim3(div_up(kFTab, 256)), dim3(256), 0, s, d.ftab);

@@ -102,6 +102,24 @@ def bf16_store(t):
     return BF16Store.apply(t)
 
 
+class F32Store(torch.autograd.Function):
+    """The fp32 path's storage points (a projection / layer output written as fp32, its gradient
+    as fp32), as BF16Store for bf16: an fp64 restatement with these inserted differs from the fp32
+    kernels by their arithmetic only, not by the roundings of what they store."""
+
+    @staticmethod
+    def forward(ctx, t):
+        return t.to(torch.float32).to(t.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.float32).to(g.dtype)
+
+
+def f32_store(t):
+    return F32Store.apply(t)
+
+
 def gat_layer(x, Ws, As, r, c, alpha=0.2, relu=True, tested=None, tau=TAU, store=None):
     """GraphAttentionLayer forward (concat of the heads) in the precision of x: Ws [H, in, d],
     As [H, 1, 2d]; edges (r, c) coalesced (unique pairs); exp(-LeakyReLU(z)) without a shift,
@@ -168,3 +186,88 @@ def margin_loss(out, left, right, neg_left, neg_right, neg2_left, neg2_right, t,
     L2 = torch.relu(-B2.reshape(t, k) + D.reshape(t, 1))
     return (L1.sum() + L2.sum()) / (2.0 * t * k)
 
+
+
+def highway_s_sign(out):
+    """relu(S)'s sign as the fused HighWay layer took it (its saved mask, bit (c % 4) of byte
+    [row][16 (c // 64) + (c % 64) // 4]), or None where the layer kept no mask."""
+    fn = out.grad_fn
+    if fn is None or type(fn).__name__ != "HighwayLayerFnBackward":
+        return None
+    mask = fn.saved_tensors[3]
+    if mask is None or mask.dtype != torch.uint8:
+        return None
+    cols = torch.arange(out.shape[1], device=out.device)
+    return ((mask[:, 16 * (cols // 64) + (cols % 64) // 4] >> (cols % 4).to(torch.uint8)) & 1
+            ).to(torch.float32)
+
+
+def ea_step_grads(m, model, x, r, c, v, ix, t, k, outputs, enc_acts, dec_acts, er=None, ec=None,
+                  tau=TAU, store=None, dtype=torch.float64):
+    """Every parameter gradient of one EA step (run/train_ea.py:55-66) through the fp64
+    restatement of ``m`` (EAModel with the weights it holds; encoders models/encoders.py, decoders
+    models/decoders.py), differentiated with the cotangent of the reference loss formula
+    (models/models_ea.py:103-123) at OUR ``outputs``: the margin loss's sign pattern is chaotic
+    under rounding (which sign(x_a - x_b) flip depends on the last bits of the outputs), so the
+    cotangent is taken where our step took it and what is compared is the backward itself.
+    ReLU branches inside the rounding band follow our activations (``enc_acts``: each encoder
+    layer's output -- HGCN: relu(S)'s sign as the fused layer saved it, or None -- and
+    ``dec_acts``: the MLP decoder's two relu outputs).  ``store``: bf16 storage
+    emulation (bf16_store) after every projection / layer output.  ``dtype``: torch.float32
+    evaluates the same restatement in fp32 (the accuracy any fp32 evaluation of these sums has,
+    reported beside ours).  Returns ({name: grad} in m.named_parameters() names, outputs)."""
+    p64 = {}
+
+    def P(name, t_):
+        q = t_.detach().to(dtype).requires_grad_(True)
+        p64[name] = q
+        return q
+    st = store if store is not None else (lambda z: z)
+    N = x.shape[0]
+    h = x.to(dtype)
+    v = v.to(dtype)
+    for i, L in enumerate(m.encoder.layers):
+        pre_n = "encoder.layers.%d." % i
+        tst = enc_acts[i].to(dtype) if enc_acts[i] is not None else None
+        if model == "GCN":
+            W, b = P(pre_n + "linear.weight", L.linear.weight), P(pre_n + "linear.bias", L.linear.bias)
+            pre = Agg.apply(st(h @ W.t() + b), r, c, v, N)
+            with torch.no_grad():
+                mk = relu_mask(pre, tst, tau)
+            h = st(pre * mk)
+        elif model == "HGCN":
+            W, b = P(pre_n + "linear.weight", L.linear.weight), P(pre_n + "linear.bias", L.linear.bias)
+            s = Agg.apply(h @ W.t() + b, r, c, v, N)
+            with torch.no_grad():
+                mk = relu_mask(s, tst, tau)
+            g = torch.sigmoid(h @ L.kernel_gate.to(dtype) + L.bias_gate.to(dtype))
+            h = g * (s * mk) + (1.0 - g) * h
+        else:
+            Ws = torch.stack([P(pre_n + "attention_%d.W" % j, a.W)
+                              for j, a in enumerate(L.attentions)])
+            As = torch.stack([P(pre_n + "attention_%d.a" % j, a.a)
+                              for j, a in enumerate(L.attentions)])
+            h = gat_layer(h, Ws, As, er, ec, 0.2, True, tested=tst, tau=tau, store=store)
+    if model == "HGCN":
+        L = m.decoder.cls
+        W, b = P("decoder.cls.linear.weight", L.linear.weight), P("decoder.cls.linear.bias",
+                                                                   L.linear.bias)
+        s = Agg.apply(h @ W.t() + b, r, c, v, N)
+        g = torch.sigmoid(h @ L.kernel_gate.to(dtype) + L.bias_gate.to(dtype))
+        h = g * s + (1.0 - g) * h
+    else:
+        for i, L in enumerate(m.decoder.cls):
+            pre_n = "decoder.cls.%d." % i
+            W, b = P(pre_n + "linear.weight", L.linear.weight), P(pre_n + "linear.bias", L.linear.bias)
+            h = st(h @ W.t() + b)
+            if i < 2:
+                with torch.no_grad():
+                    mk = relu_mask(h, dec_acts[i].to(dtype), tau)
+                h = h * mk
+    o64 = outputs.detach().double().requires_grad_(True)
+    margin_loss(o64, *ix, t, k).backward()
+    cot = o64.grad
+    if store is not None:
+        cot = cot.to(torch.bfloat16).double()  # as the bf16 outputs receive it
+    h.backward(cot.to(dtype))
+    return {n: q.grad for n, q in p64.items()}, h.detach()

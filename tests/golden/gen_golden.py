@@ -254,6 +254,42 @@ def gen_l1():
     print("l1 fixtures written to", HERE)
 
 
+def gen_ties():
+    """Tie-heavy fixture for get_neg / get_hits: duplicated rows, an all-equal
+    block and rows on a coarse grid, so many L1 distances are exactly equal.  The reference ranks
+    with numpy's default argsort (models/models_ea.py:26, utils/eval_utils.py:78,85), whose order
+    among equal keys is unspecified (introsort; SIMD-dispatched on some CPUs); the engine orders
+    ties by index.  The fixture records what the reference returned here, with the numpy
+    version, so the test can pin everything that does not depend on the tie order."""
+    _synth()
+    _placeholders()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import models.models_ea as RM
+    import utils.eval_utils as REV
+    rng = np.random.default_rng(17)
+    n, D = 400, 64
+    base = np.round(rng.standard_normal((n, D)) * 2) / 4  # coarse grid: exact, many equal sums
+    base[40:80] = base[40]                                 # an all-equal block
+    dup = rng.choice(n, 60, replace=False)
+    base[dup[30:]] = base[dup[:30]]                         # 30 duplicated pairs
+    vec = np.concatenate([base, base + (rng.random((n, D)) < 0.05) / 4]).astype(np.float32)
+    perm = rng.permutation(n)
+    train = np.stack([perm[:100], perm[:100] + n], 1).astype(np.int64)
+    test = np.stack([perm[100:300], perm[100:300] + n], 1).astype(np.int64)
+    tv = torch.from_numpy(vec)
+    out = {"vec": vec, "train": train, "test": test, "numpy_version": np.array(np.__version__)}
+    k = 25
+    out["neg_right"] = RM.BaseModel.get_neg(None, train[:, 0], tv, k)
+    out["neg2_left"] = RM.BaseModel.get_neg(None, train[:, 1], tv, k)
+    for split, pairs in (("train", train), ("test", test)):
+        m = REV.get_hits(tv, pairs)
+        out["hits_%s_keys" % split] = np.array(list(m.keys()))
+        out["hits_%s_vals" % split] = np.array(list(m.values()), dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "l1_ties.npz"), **out)
+    print("tie fixtures written to", HERE)
+
+
 def gen_train_trace():
     """run/train_ea.py:53-67 loop (3 epochs) of the reference EAModel on the cfg-1 graph."""
     _synth()
@@ -534,7 +570,7 @@ def gen_sinkhorn_scale():
 
 
 if __name__ == "__main__":
-    sections = {"l1": gen_l1, "train": gen_train_trace, "gw": gen_gw, "ingest": gen_ingest,
+    sections = {"l1": gen_l1, "ties": gen_ties, "train": gen_train_trace, "gw": gen_gw, "ingest": gen_ingest,
                 "dbp15k": gen_dbp15k, "sinkhorn_scale": gen_sinkhorn_scale}
     if sys.argv[1:]:
         for name in sys.argv[1:]:
@@ -542,6 +578,7 @@ if __name__ == "__main__":
     else:
         main()
         gen_l1()
+        gen_ties()
         gen_train_trace()
         gen_gw()
         gen_ingest()

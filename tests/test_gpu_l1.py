@@ -244,3 +244,25 @@ def test_margin_bf16_rows_match_fp32_copy(device, N, D, t, k):
     assert x1.grad.dtype == torch.bfloat16
     assert float(l1) == float(l2)
     assert torch.equal(x1.grad, x2.grad)
+
+
+def test_l1_ties_vs_reference(golden, device):
+    """The drop-in get_neg / get_hits on the tie-heavy fixture the reference produced: equal to
+    the reference up to the order among exactly equal distances (tests/tie_rules.py), and index
+    for index equal to the stable-order oracle (ties by index, the documented rule)."""
+    import tie_rules
+    from models.models_ea import BaseModel
+    from oracle import l1 as l1o
+    from utils.eval_utils import get_hits
+    f = golden("l1_ties")
+    vec, train, test = f["vec"], f["train"], f["test"]
+    out = torch.from_numpy(vec).to(device)
+    for col, key in ((0, "neg_right"), (1, "neg2_left")):
+        got = BaseModel.get_neg(None, train[:, col], out, 25)
+        tie_rules.check_neg(vec, train[:, col], got, f[key], 25)
+        assert np.array_equal(got, l1o.get_neg(train[:, col], vec, 25))
+    for split, pairs in (("train", train), ("test", test)):
+        got = get_hits(out, pairs)
+        tie_rules.check_hits(vec, pairs, got, f["hits_%s_keys" % split],
+                             f["hits_%s_vals" % split])
+        assert got == l1o.get_hits(vec, pairs)

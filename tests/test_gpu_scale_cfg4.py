@@ -116,8 +116,11 @@ def test_cfg4_highway_layer_vs_oracle(device, cfg4, relu_band):
 
 def test_cfg4_hgcn_ea_step_vs_fp64(device, cfg4, relu_band, record_property):
     """One HGCN-EA training step (run/train_ea.py:55-66) on the full configs[3] graph, with the
-    default projection GEMMs (the f16x2 form, GNNEA_X3W unset = 4): the step's loss and every
-    parameter gradient against the fp64 restatement (recorded for -rA)."""
+    default projection GEMMs (the f16x2 form, GNNEA_X3W unset = 4): the loss against the fp64
+    restatement's (1e-5), and EVERY parameter gradient against the fp64 restatement
+    differentiated with the reference loss's cotangent at OUR outputs (1e-4; the margin loss's
+    sign pattern is chaotic under rounding, so the fp64 step's own cotangent, whose gradients
+    are recorded beside it, is not the bar)."""
     from models.models_ea import EAModel
     from test_dropin_cpu import make_args
     d = cfg4
@@ -130,43 +133,56 @@ def test_cfg4_hgcn_ea_step_vs_fp64(device, cfg4, relu_band, record_property):
     torch.manual_seed(10086)
     m = EAModel(a).to(device)
     m.train()
+    enc_acts = []  # relu(S)'s sign of each encoder layer, as the layer took it (rounding band)
+    for L in m.encoder.layers:
+        L.register_forward_hook(lambda mod, i, o: enc_acts.append(
+            fp64_ref.highway_s_sign(o[0] if isinstance(o, tuple) else o)))
     outputs = m.decode(m.encode(d["x"], d["adj"]), d["adj"])
+    assert all(a_ is not None for a_ in enc_acts)
     m.neg_right = si.negatives(N, t, k, 31)
     m.neg2_left = si.negatives(N, t, k, 32)
     loss = m.get_loss(outputs, {"train": train}, "train")
     loss.backward()
-    # fp64 restatement with the same weights (encoder: 2 HighWay layers, relu; decoder: 1, identity)
-    layers = list(m.encoder.layers) + [m.decoder.cls]
-    ps = [(L.linear.weight.detach().double().requires_grad_(True),
-           L.linear.bias.detach().double().requires_grad_(True),
-           L.kernel_gate.detach().double()) for L in layers]
-    v64 = d["v"].double()
-    h = d["x"].double()
-    for i, (W, b, Kg) in enumerate(ps):
-        h = fp64_ref.highway_layer(h, W, b, Kg, d["r"], d["c"], v64, relu=i < 2)
     ix = [torch.from_numpy(np.asarray(z, dtype=np.int64)).to(device) for z in
           (train[:, 0], train[:, 1], m.neg_left, m.neg_right, m.neg2_left, m.neg2_right)]
-    loss64 = fp64_ref.margin_loss(h, *ix, t, k)
-    loss64.backward()
+    v64 = d["v"].double()
+    # the same restatement in fp32 first (what any fp32 evaluation of these sums gets), then fp64
+    g32, _ = fp64_ref.ea_step_grads(m, "HGCN", d["x"], d["r"], d["c"], v64, ix, t, k, outputs,
+                                    enc_acts, [], dtype=torch.float32)
+    g32 = {nm: g_.double() for nm, g_ in g32.items()}
+    g64, h64 = fp64_ref.ea_step_grads(m, "HGCN", d["x"], d["r"], d["c"], v64, ix, t, k, outputs,
+                                      enc_acts, [])
+    with torch.no_grad():
+        loss64 = fp64_ref.margin_loss(h64, *ix, t, k)
     loss_err = abs(float(loss) - float(loss64)) / abs(float(loss64))
-    got = [(L.linear.weight.grad, L.linear.bias.grad) for L in layers]
-    gmax = max(float(p.grad.abs().max()) for trip in ps for p in trip[:2])
-    errs = {"loss": loss_err}
-    for i, ((gW, gb), (W, b, _)) in enumerate(zip(got, ps)):
-        errs["W%d" % i] = rel_err(gW.cpu(), W.grad.cpu())
-        errs["b%d" % i] = rel_err(gb.cpu(), b.grad.cpu()) if float(b.grad.abs().max()) >= 1e-3 * gmax \
-            else float(gb.abs().max()) / gmax
-    record_property("cfg4_hgcn_step_errs", errs)
-    print("cfg4 HGCN-EA step vs fp64 (loss rel, grads norm-rel; analytically-zero bias: "
-          "max / largest gradient):", errs)
+    params = [(nm, p) for nm, p in m.named_parameters()]
+    assert sorted(g64) == sorted(nm for nm, _ in params)
+    gmax = max(float(g64[nm].abs().max()) for nm, _ in params)
+    errs, errs32 = {"loss": loss_err}, {}
+    for nm, p in params:
+        ref = g64[nm]
+        zero = float(ref.abs().max()) < 1e-3 * gmax
+        for dst, got in ((errs, p.grad.double()), (errs32, g32[nm])):
+            dst[nm] = float((got - ref).abs().max()) / gmax if zero else \
+                rel_err(got.cpu(), ref.cpu())
+    # reported: the fp64 step's own gradients (its cotangent at the fp64 outputs)
+    h64r = h64.clone().requires_grad_(True)
+    fp64_ref.margin_loss(h64r, *ix, t, k).backward()
+    o64 = outputs.detach().double().requires_grad_(True)
+    fp64_ref.margin_loss(o64, *ix, t, k).backward()
+    cot_diff = rel_err(o64.grad.cpu(), h64r.grad.cpu())
+    record_property("cfg4_hgcn_step_errs", {"vs_fp64_at_our_outputs": errs,
+                                            "fp32_restatement_vs_fp64": errs32,
+                                            "loss_cotangent_ours_vs_fp64_outputs": cot_diff})
+    print("cfg4 HGCN-EA step vs the fp64 restatement at our outputs (loss rel; grads norm-rel; "
+          "analytically-zero bias: max / largest gradient):", errs,
+          "; the same restatement evaluated in fp32:", errs32,
+          "; the loss cotangent at our outputs vs at the fp64 outputs: %.2e" % cot_diff)
     assert loss_err <= 1e-5
-    for (gW, gb), (W, b, _) in zip(got, ps):
-        for g_, p in ((gW, W), (gb, b)):
-            ref = p.grad
-            if float(ref.abs().max()) < 1e-3 * gmax:  # analytically zero (last bias)
-                assert float(g_.abs().max()) < 1e-3 * gmax
-            else:
-                assert rel_err(g_.cpu(), ref.cpu()) < 3e-3
+    # every parameter at 1e-4 (relu's branch in the rounding band follows the layers' own
+    # signs: without that, a few near-zero S entries taking the other branch moved W1 to 1.3e-4)
+    for nm, _ in params:
+        assert errs[nm] < TOL32, (nm, errs[nm], errs32[nm])
 
 
 def _coalesced(r, c, N):
@@ -205,28 +221,38 @@ def test_cfg4_gat_layer_vs_oracle(device, cfg4, monkeypatch, relu_band, record_p
     assert rel_err(_rows_of(xx.grad)(T), dx_ref) < TOL32
     r, c = _coalesced(d["r"], d["c"], d["N"])
     grads = {}
-    for dt in (torch.float64, torch.float32):
+    for dt, store in ((torch.float64, None), (torch.float32, None),
+                      ("f64_store32", fp64_ref.f32_store)):
         # the reference's op sequence (tests/fp64_ref.gat_layer: gathers, exp, index_add) in
-        # fp64, and in fp32 for the accumulation error any fp32 evaluation of these sums has
-        Wd = Ws.to(device, dt).requires_grad_(True)
-        Ad = As.to(device, dt).requires_grad_(True)
-        yd = fp64_ref.gat_layer(d["x"].to(dt), Wd, Ad, r, c, 0.2, True,
-                                tested=out.detach().to(dt))
-        (yd * d["R"].to(dt)).sum().backward()
+        # fp64, in fp32 for the accumulation error any fp32 evaluation of these sums has, and in
+        # fp64 with this path's fp32 storage points emulated (each head's projection H and the
+        # output rounded to fp32, value and gradient): what is left there is our arithmetic
+        cdt = torch.float64 if store is not None else dt
+        Wd = Ws.to(device, cdt).requires_grad_(True)
+        Ad = As.to(device, cdt).requires_grad_(True)
+        yd = fp64_ref.gat_layer(d["x"].to(cdt), Wd, Ad, r, c, 0.2, True,
+                                tested=out.detach().to(cdt), store=store)
+        (yd * d["R"].to(cdt)).sum().backward()
         grads[dt] = (Wd.grad.double().cpu(), Ad.grad.double().cpu())
         del yd
     W64, A64 = grads[torch.float64]
     W32, A32 = grads[torch.float32]
+    Ws32, As32 = grads["f64_store32"]
     # dW sums x_i (x) dH_i over 2M rows; da sums ds (x) H over every row, ds = sum of dz over the
     # row's 21 edges with dz = alpha (mask g.h_j - c_i) LeakyReLU', differences of nearby
     # products: far more cancellation, so fp32 accumulation alone lands further from fp64 there.
     # Each gradient must be within 1e-4 of fp64, or within twice the torch-fp32 evaluation's own
     # error, whichever is larger (the DBP15K tests' rule for the reference's fp32 step).
+    # (The fp64 leg with this path's fp32 storage points emulated is reported: it does not close
+    # the gap -- the a gradients' error is the fp32 arithmetic of the softmax backward's
+    # differences G.H_j - c_i, which the torch fp32 evaluation shares.)
     errs = []
     for h, att in enumerate(layer.attentions):
-        for ours, r64, r32 in ((att.W.grad, W64[h], W32[h]), (att.a.grad, A64[h], A32[h])):
-            e, e32 = rel_err(ours.cpu(), r64), rel_err(r32, r64)
-            errs.append((e, e32))
+        for ours, r64, r32, rst in ((att.W.grad, W64[h], W32[h], Ws32[h]),
+                                    (att.a.grad, A64[h], A32[h], As32[h])):
+            e, e32, est = rel_err(ours.cpu(), r64), rel_err(r32, r64), rel_err(ours.cpu(), rst)
+            errs.append((e, e32, est))
             assert e < max(TOL32, 2.0 * e32), (h, e, e32)
     record_property("cfg4_gat_grad_errs", errs)
-    print("cfg4 GAT layer grads (ours vs fp64, torch-fp32 vs fp64):", errs)
+    print("cfg4 GAT layer grads (ours vs fp64, torch-fp32 vs fp64, ours vs fp64 with the fp32 "
+          "storage points):", errs)

@@ -132,3 +132,22 @@ def test_margin_oracle(golden):
                                          f["neg2_left"], nr2, t, k)
     assert abs(loss - float(f["margin_loss"])) <= 1e-5 * abs(loss)
     assert rel_err(grad, f["margin_grad"]) < 1e-5
+
+
+def test_l1_ties_oracle_vs_reference(golden):
+    """Tie-heavy fixture (gen_golden.py gen_ties: duplicated rows, an all-equal block, a coarse
+    grid): the stable-order oracle agrees with the reference's numpy-argsort results up to the
+    order among exactly equal distances (tests/tie_rules.py), and does differ in that order on
+    this input -- the documented deviation ("Ties")."""
+    import tie_rules
+    from oracle import l1
+    f = golden("l1_ties")
+    vec, train, test = f["vec"], f["train"], f["test"]
+    differ = 0
+    for col, key in ((0, "neg_right"), (1, "neg2_left")):
+        got = l1.get_neg(train[:, col], vec, 25)
+        differ += tie_rules.check_neg(vec, train[:, col], got, f[key], 25)
+    assert differ > 0  # the fixture does exercise tie order
+    for split, pairs in (("train", train), ("test", test)):
+        tie_rules.check_hits(vec, pairs, l1.get_hits(vec, pairs), f["hits_%s_keys" % split],
+                             f["hits_%s_vals" % split])
