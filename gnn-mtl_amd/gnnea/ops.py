@@ -1326,34 +1326,37 @@ class HighwayLayerFn(torch.autograd.Function):
             else:
                 out, S, _ = agg.highway_fwd_sliced(Zs, D, x, bias_gate, act, goff=goff)
             G = Zs
-            ctx.bias_gate, ctx.goff = bias_gate, goff
+            ctx.goff = goff
         else:
             Z = gemm(x, wcat, bias=bcat)
             out, S, G = agg.highway_fwd(Z[:, :D], Z[:, D:], x, bias_gate, act)
         ctx.agg, ctx.act = agg, act
+        # bias_gate goes through save_for_backward too (the sliced backward recomputes the gate
+        # from it): an in-place update between forward and backward raises autograd's version
+        # error instead of silently using the new value
         if ctx.sliced and ctx.masked:
-            ctx.save_for_backward(x, weight, kernel_gate, S, G, out)
+            ctx.save_for_backward(x, weight, kernel_gate, S, G, bias_gate, out)
         else:
-            ctx.save_for_backward(x, weight, kernel_gate, S, G)
+            ctx.save_for_backward(x, weight, kernel_gate, S, G, bias_gate)
         return out
 
     @staticmethod
     def backward(ctx, dy):
         if ctx.sliced and ctx.masked:
-            x, weight, Kg, S, G, out = ctx.saved_tensors  # (S: the relu mask or None)
+            x, weight, Kg, S, G, bias_gate, out = ctx.saved_tensors  # (S: the relu mask or None)
         else:
-            x, weight, Kg, S, G = ctx.saved_tensors
+            x, weight, Kg, S, G, bias_gate = ctx.saved_tensors
             out = None
         N, D = x.shape[0], weight.shape[0]
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         pdt = torch.float32 if (ctx.sliced and ctx.masked) else S.dtype
         P = torch.empty((N, 2 * D), dtype=pdt, device=x.device)
         if ctx.sliced and ctx.masked:  # (G is the projection table Zs here)
-            dSs, dres = highway_bwd_sliced_zgm(dy, out, S, G, D, ctx.bias_gate, x, ctx.act,
+            dSs, dres = highway_bwd_sliced_zgm(dy, out, S, G, D, bias_gate, x, ctx.act,
                                                need_x, P[:, D:], ctx.goff)
             ctx.agg.aggregate_t_sliced(dSs, D, P[:, :D])
         elif ctx.sliced:
-            dSs, dres = highway_bwd_sliced_zg(dy, S, G, D, ctx.bias_gate, x, ctx.act, need_x,
+            dSs, dres = highway_bwd_sliced_zg(dy, S, G, D, bias_gate, x, ctx.act, need_x,
                                               P[:, D:], goff=ctx.goff)
             ctx.agg.aggregate_t_sliced(dSs, D, P[:, :D])
         else:

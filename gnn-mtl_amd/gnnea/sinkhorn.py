@@ -79,14 +79,26 @@ class _StatusPoll:
         return self.buf[:, ST_DONE].clone()
 
 
+# Set once an on-chip solve of this process timed out for real (not under GNNEA_SK_DEBUG_SPIN):
+# the on-chip solver needs all its workgroups resident at once, which another stream's kernels
+# holding CUs (an RCCL collective still in flight) can prevent; after one such timeout -- whose
+# problem is re-solved on the sweep path -- later default solves start on the sweep.
+_ONCHIP_TIMED_OUT = False
+
+
 def _default_flags():
-    """DEFAULT_FLAGS, plus GNNEA_SK_NO_ONCHIP inside a multi-rank process group: the on-chip
-    solver needs all its workgroups resident at once, which another stream's collective kernels
-    holding CUs can prevent (its bounded waits would then time out before the sweep re-solve)."""
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    """DEFAULT_FLAGS, plus GNNEA_SK_NO_ONCHIP once an on-chip solve has timed out in this
+    process.  Rank-local solves of a multi-rank job (evaluation, per-rank OT losses) keep the
+    on-chip path: a collective in flight costs at most one bounded wait and a re-solve."""
+    if _ONCHIP_TIMED_OUT:
         return DEFAULT_FLAGS | _lib.GNNEA_SK_NO_ONCHIP
     return DEFAULT_FLAGS
+
+
+def _note_timeout(flags):
+    global _ONCHIP_TIMED_OUT
+    if not flags & _lib.GNNEA_SK_DEBUG_SPIN:
+        _ONCHIP_TIMED_OUT = True
 
 
 def _retry_flags(flags):
@@ -106,6 +118,7 @@ def solve(mode, C, a, b, eps, tol, max_iter, p=1.0, plan_dtype=torch.float64,
         return _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch,
                       variant, flags)
     except SinkhornTimeout:
+        _note_timeout(flags)
         res = _solve(mode, C, a, b, eps, tol, max_iter, p, plan_dtype, want_plan, batch,
                      variant, _retry_flags(flags))
         res.onchip_timeout = True
@@ -203,6 +216,7 @@ def solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p=1.0, plan_dtype=torch.fl
         return _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, variant,
                             flags)
     except SinkhornTimeout:
+        _note_timeout(flags)
         out = _solve_batch(mode, Cs, As, Bs, eps, tol, max_iter, p, plan_dtype, batch, variant,
                            _retry_flags(flags))
         for r in out:

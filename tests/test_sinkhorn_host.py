@@ -9,6 +9,11 @@ import pytest
 from gnnea import _lib, sinkhorn
 
 
+@pytest.fixture(autouse=True)
+def _fresh_timeout_state(monkeypatch):
+    monkeypatch.setattr(sinkhorn, "_ONCHIP_TIMED_OUT", False)
+
+
 def _fake(calls, fail_flags, batch=False):
     def f(*args):
         flags = args[-1]
@@ -40,6 +45,7 @@ def test_solve_batch_retries_and_second_timeout_propagates(monkeypatch):
     assert [r.flags for r in out] == [_lib.GNNEA_SK_NO_ONCHIP] * 2
     assert all(r.onchip_timeout for r in out)
     calls.clear()
+    monkeypatch.setattr(sinkhorn, "_ONCHIP_TIMED_OUT", False)  # (the timeout above is sticky)
     monkeypatch.setattr(sinkhorn, "_solve", _fake(calls, {0, _lib.GNNEA_SK_NO_ONCHIP}))
     with pytest.raises(sinkhorn.SinkhornTimeout):
         sinkhorn.solve(0, None, None, None, 0.01, 1e-9, 10)
@@ -53,17 +59,25 @@ def test_problem_struct_carries_flags():
     assert names[-2:] == ["flags", "ws"]
 
 
-def test_default_flags_skip_onchip_in_a_process_group(monkeypatch):
-    """Inside a multi-rank process group the default flags skip the on-chip solver (its
-    workgroups must all be resident; collective kernels on another stream can hold CUs)."""
+def test_default_flags_after_a_real_timeout(monkeypatch):
+    """The on-chip solver stays the default in a multi-rank process group (rank-local solves);
+    after one real timeout in this process -- re-solved on the sweep path -- later default solves
+    start on the sweep; a timeout under GNNEA_SK_DEBUG_SPIN (the tests' forced one) changes
+    nothing."""
     import torch.distributed as dist
-    assert sinkhorn._default_flags() == sinkhorn.DEFAULT_FLAGS
+    monkeypatch.setattr(sinkhorn, "_ONCHIP_TIMED_OUT", False)
     monkeypatch.setattr(dist, "is_initialized", lambda: True)
     monkeypatch.setattr(dist, "get_world_size", lambda group=None: 4)
-    assert sinkhorn._default_flags() & _lib.GNNEA_SK_NO_ONCHIP
+    assert sinkhorn._default_flags() == sinkhorn.DEFAULT_FLAGS
     calls = []
-    monkeypatch.setattr(sinkhorn, "_solve", _fake(calls, set()))
+    monkeypatch.setattr(sinkhorn, "_solve", _fake(calls, {_lib.GNNEA_SK_DEBUG_SPIN}))
+    sinkhorn.solve(0, None, None, None, 0.01, 1e-9, 10, flags=_lib.GNNEA_SK_DEBUG_SPIN)
+    assert sinkhorn._default_flags() == sinkhorn.DEFAULT_FLAGS
+    calls.clear()
+    monkeypatch.setattr(sinkhorn, "_solve", _fake(calls, {0}))
+    sinkhorn.solve(0, None, None, None, 0.01, 1e-9, 10)
+    assert calls == [0, _lib.GNNEA_SK_NO_ONCHIP]
+    assert sinkhorn._default_flags() & _lib.GNNEA_SK_NO_ONCHIP
+    calls.clear()
     sinkhorn.solve(0, None, None, None, 0.01, 1e-9, 10)
     assert calls == [_lib.GNNEA_SK_NO_ONCHIP]
-    monkeypatch.setattr(dist, "get_world_size", lambda group=None: 1)
-    assert sinkhorn._default_flags() == sinkhorn.DEFAULT_FLAGS
