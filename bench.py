@@ -11,11 +11,11 @@ aggregation over the owned rows (default --partition rows).  The exchange-free p
 (tiles / features: every rank aggregates a column slice from the whole KG, which a layer can
 only do after an all-gather of its input) are reported as a labelled side number.
 
-Side measurements (`train_step`, `train_step_gat`, `train_step_gat_cfg5_bf16`): the row-sharded
-EA training steps through the drop-in Encoder/Decoder modules with the RCCL halo exchange
-(tools/dist_step.py) -- HGCN-EA on the cfg-4 graph (configs[3]), GAT-EA fp32 on the same graph
-(configs[2]'s model), GAT-EA bf16 on the cfg-5 graph (configs[4]) -- at N = 1 and row-sharded
-at N > 1, each with per-kernel-class GPU time.
+Side measurements (`train_step`, `train_step_gat`, `train_step_gcn`, `train_step_gat_cfg5_bf16`):
+the row-sharded EA training steps through the drop-in Encoder/Decoder modules with the RCCL halo
+exchange (tools/dist_step.py) -- HGCN-EA on the cfg-4 graph (configs[3]), GAT-EA and GCN-EA fp32
+on the same graph (configs[2]'s and configs[1]'s models), GAT-EA bf16 on the cfg-5 graph
+(configs[4]) -- at N = 1 and row-sharded at N > 1, each with per-kernel-class GPU time.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]   (N > 1: starts its own N ranks)
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
@@ -479,9 +479,11 @@ def cpu_baseline(shard, H, budget_s=12.0):
 
 # EA training-step legs (tools/dist_step.measure): line key -> (encoder, graph, storage dtype).
 # HGCN-EA on cfg-4 is BASELINE configs[3]; GAT-EA on cfg-4 in fp32 is configs[2]'s model at
-# configs[3]'s size; GAT-EA on the cfg-5 graph (2 x 2M entities, ~84M nnz) in bf16 is configs[4]
+# configs[3]'s size, GCN-EA configs[1]'s; GAT-EA on the cfg-5 graph (2 x 2M entities, ~84M nnz)
+# in bf16 is configs[4]
 TRAIN_LEGS = {"train_step": ("HGCN", "cfg4", "f32"),
               "train_step_gat": ("GAT", "cfg4", "f32"),
+              "train_step_gcn": ("GCN", "cfg4", "f32"),
               "train_step_gat_cfg5_bf16": ("GAT", "cfg5", "bf16")}
 
 
