@@ -800,13 +800,17 @@ __global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ 
 #pragma unroll
     for (int h = 0; h < H; ++h) mx[h] = -INFINITY;
   }
-  // (the row sums keep wave_sum's order: the forward's outputs, and with them which of the EA
-  // loss's sign terms flip under rounding, stay those of the validated build)
   float rinv[H];
+  {
+    float dp[HPW];  // every head's row sum in one all-reduce
 #pragma unroll
-  for (int h = 0; h < H; ++h) {
-    den[h] = wave_sum(den[h]);
-    rinv[h] = den[h] > 0.f ? 1.f / den[h] : 0.f;
+    for (int h = 0; h < HPW; ++h) dp[h] = h < H ? den[h] : 0.f;
+    wave_allsum<HPW>(dp, lane);
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      den[h] = dp[h];
+      rinv[h] = den[h] > 0.f ? 1.f / den[h] : 0.f;
+    }
   }
   const float ri = hsel<H>(rinv, hme);
   T* y = Y + (int64_t)row * ldy;
