@@ -630,11 +630,39 @@ __device__ __forceinline__ void load_dw(const char* p, uint32_t* d) {
   }
 }
 
+// the same window through a buffer resource on the (wave-uniform) row base: the row address is
+// scalar arithmetic, the lane's window offset the 32-bit voffset -- no 64-bit vector address
+// per edge (a global pointer formed as base + row * ld + lane offset is re-associated by the
+// compiler into a per-lane 64-bit multiply-add)
+template <int W>
+__device__ __forceinline__ void load_dw_row(const char* row, uint32_t off, uint32_t* d) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)row, (short)0, 0x7fffffff, 0x00020000);
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  typedef unsigned int u3 __attribute__((ext_vector_type(3)));
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  int q = 0;
+#pragma unroll
+  for (; q + 4 <= W; q += 4) {
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 4 * q, 0, 0);
+    d[q] = v.x; d[q + 1] = v.y; d[q + 2] = v.z; d[q + 3] = v.w;
+  }
+  if constexpr (W % 4 == 3) {
+    const u3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, off + 4 * q, 0, 0);
+    d[q] = v.x; d[q + 1] = v.y; d[q + 2] = v.z;
+  } else if constexpr (W % 4 == 2) {
+    const u2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 4 * q, 0, 0);
+    d[q] = v.x; d[q + 1] = v.y;
+  } else if constexpr (W % 4 == 1) {
+    d[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * q, 0, 0);
+  }
+}
+
 template <typename T, int EPL> struct RowWin;
 template <int EPL> struct RowWin<float, EPL> {
   static constexpr int W = EPL;
   static __host__ __device__ int64_t byte_off(int c) { return 4 * (int64_t)c; }
-  static __device__ __forceinline__ void unpack(const uint32_t (&d)[W], bool, float (&f)[EPL]) {
+  static __device__ __forceinline__ void unpack(const uint32_t (&d)[W], uint32_t, float (&f)[EPL]) {
 #pragma unroll
     for (int t = 0; t < EPL; ++t) f[t] = __builtin_bit_cast(float, d[t]);
   }
@@ -642,12 +670,15 @@ template <int EPL> struct RowWin<float, EPL> {
 template <int EPL> struct RowWin<bf16_t, EPL> {
   static constexpr int W = (EPL + 2) / 2;  // EPL halfwords + a possible leading one
   static __host__ __device__ int64_t byte_off(int c) { return (2 * (int64_t)c) & ~(int64_t)3; }
-  static __device__ __forceinline__ void unpack(const uint32_t (&d)[W], bool sh, float (&f)[EPL]) {
+  // shb: the window's byte shift (2 when the first element is odd): one v_alignbyte per element
+  // pair brings halfwords (2p, 2p + 1) into a dword, then a shift / a mask widens each to f32
+  static __device__ __forceinline__ void unpack(const uint32_t (&d)[W], uint32_t shb,
+                                                float (&f)[EPL]) {
 #pragma unroll
-    for (int t = 0; t < EPL; ++t) {  // halfword t + sh of the window, widened to f32
-      const uint32_t lo = (t & 1) ? (d[t >> 1] & 0xffff0000u) : (d[t >> 1] << 16);
-      const uint32_t hi = (t & 1) ? (d[(t + 1) >> 1] << 16) : (d[t >> 1] & 0xffff0000u);
-      f[t] = __builtin_bit_cast(float, sh ? hi : lo);
+    for (int p = 0; 2 * p < EPL; ++p) {
+      const uint32_t v = __builtin_amdgcn_alignbyte(d[p + 1 < W ? p + 1 : W - 1], d[p], shb);
+      f[2 * p] = __builtin_bit_cast(float, v << 16);
+      if (2 * p + 1 < EPL) f[2 * p + 1] = __builtin_bit_cast(float, v & 0xffff0000u);
     }
   }
 };
@@ -696,9 +727,11 @@ __global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ 
   const int beg = rowptr[row], end = rowptr[row + 1];
   const L hl(lane, dh);
   const int hme = hl.h < H ? hl.h : 0;
-  const int64_t woff = WN::byte_off(hl.c[0]);
-  const bool wsh = (hl.c[0] & 1) != 0;
-  const char* Hb = (const char*)Hm + woff;
+  // the gathered row's address: a wave-uniform (scalar) row base plus the lane's 32-bit window
+  // offset (load_dw_row)
+  const uint32_t woff = (uint32_t)WN::byte_off(hl.c[0]);
+  const uint32_t wsh = (hl.c[0] & 1) ? 2u : 0u;
+  const char* Hb = (const char*)Hm;
   const int64_t ldb = ldh * (int64_t)sizeof(T);
 
   float si[H];
@@ -756,7 +789,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ 
 #pragma unroll
         for (int e = 0; e < F; ++e) {
           const int j = readlane_i(mj, min(k + e, cnt - 1));
-          load_dw<W>(Hb + (int64_t)j * ldb, g[e]);
+          load_dw_row<W>(Hb + (int64_t)j * ldb, woff, g[e]);
         }
       };
       issue(ga, 0);  // depends on the neighbour ids only: out before the weights are known
@@ -769,21 +802,18 @@ __global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ 
         den[h] += w;  // the row sum uses the un-dropped weights (att_layers.py:45-51)
         wl[h] = EM ? w * em[h] : w;
       }
-      // no early exits between a group's issue and its use: every edge of a group is consumed
-      // (edges past the chunk leave acc unchanged through a uniform select), so the compiler's
-      // wait counts stay exact across the loop's back edge
+      // no early exits between a group's issue and its use: every edge of a group is consumed,
+      // so the compiler's wait counts stay exact across the loop's back edge.  Edges past the
+      // chunk have weight 0 (sc = -inf there) and re-read a live edge's finite row: their fma
+      // adds +-0, no select needed
       auto consume = [&](const uint32_t (&g)[F][W], int k) {
 #pragma unroll
         for (int e = 0; e < F; ++e) {
-          const bool live = k + e < cnt;  // uniform
           const float we = head_w<H>(wl, min(k + e, 63), hme);
           float x[EPL];
           WN::unpack(g[e], wsh, x);
 #pragma unroll
-          for (int t = 0; t < EPL; ++t) {
-            const float v = fmaf(we, x[t], acc[t]);
-            acc[t] = live ? v : acc[t];
-          }
+          for (int t = 0; t < EPL; ++t) acc[t] = fmaf(we, x[t], acc[t]);
         }
       };
       // (sched_barrier: keep each group's loads ahead of the previous group's arithmetic)
@@ -865,8 +895,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hg(
   const int beg = rowptrT[row], end = rowptrT[row + 1];
   const L hl(lane, dh);
   const int hme = hl.h < H ? hl.h : 0;
-  const char* Gb = (const char*)G + WN::byte_off(hl.c[0]);
-  const bool wsh = (hl.c[0] & 1) != 0;
+  const uint32_t woff = (uint32_t)WN::byte_off(hl.c[0]);  // (load_dw_row's lane offset)
+  const uint32_t wsh = (hl.c[0] & 1) ? 2u : 0u;
+  const char* Gb = (const char*)G;
   const int64_t ldb = ldg * (int64_t)sizeof(T);
 
   float hj[EPL], acc[EPL], a2l[EPL];
@@ -895,7 +926,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hg(
 #pragma unroll
       for (int e = 0; e < F; ++e) {
         const int r = readlane_i(mi, min(k + e, cnt - 1));
-        load_dw<W>(Gb + (int64_t)r * ldb, g[e]);
+        load_dw_row<W>(Gb + (int64_t)r * ldb, woff, g[e]);
       }
     };
     issue(ga, 0);  // depends on the neighbour ids only
@@ -922,18 +953,18 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hg(
       float pd[F], we[F];
 #pragma unroll
       for (int e = 0; e < F; ++e) we[e] = shw[min(k + e, 63) * H + hme];
+      // edges past the chunk: weight 0 (shw), a live edge's finite row re-read, so their fma
+      // adds +-0; elements past the head (hl.ok false) meet hj = 0 in the dot product and are
+      // never stored from acc -- no selects
 #pragma unroll
       for (int e = 0; e < F; ++e) {
         float x[EPL];
         WN::unpack(g[e], wsh, x);
-        const bool live = k + e < cnt;  // uniform; no branch between issue and use
         float q = 0.f;
 #pragma unroll
         for (int t = 0; t < EPL; ++t) {
-          const float gv = hl.ok[t] ? x[t] : 0.f;
-          const float u = fmaf(we[e], gv, acc[t]);
-          acc[t] = live ? u : acc[t];
-          q = fmaf(gv, hj[t], q);
+          acc[t] = fmaf(we[e], x[t], acc[t]);
+          q = fmaf(x[t], hj[t], q);
         }
         pd[e] = q;
       }
