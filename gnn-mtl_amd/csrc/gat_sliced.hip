@@ -118,6 +118,22 @@ __device__ __forceinline__ void store_cols(T* row, int c0, int D, const float (&
           Vec4<T>::put(make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]));
 }
 
+// one lane's piece of a gathered slice row through a buffer resource on the slice base (wave-
+// uniform, scalar): the 32-bit offset row * (64 sizeof(T)) + lane piece is one vector multiply-
+// add, where a 64-bit per-lane address took three; host-checked: a slice spans < 4 GB
+template <typename R>
+__device__ __forceinline__ R load_piece(const __amdgpu_buffer_rsrc_t& rs, uint32_t off) {
+  if constexpr (sizeof(R) == 16) {
+    return __builtin_bit_cast(R, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+  } else {
+    static_assert(sizeof(R) == 8, "piece size");
+    return __builtin_bit_cast(R, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+  }
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slice_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)0xffffffffu, 0x00020000);
+}
+
 template <int ACT, int U, typename TX, typename TY>
 __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
     const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, int n_rows, int nbs,
@@ -141,7 +157,10 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
   bool second[E];
 #pragma unroll
   for (int t = 0; t < E; ++t) second[t] = (c0 + t) / dh != h0;
-  const RX* X = Hs + (int64_t)s * sstrideR + c;
+  // every lane loads unconditionally: edges past the chunk take row 0 with weight 0, lanes past D
+  // re-read the row's first piece (finite; never stored)
+  const __amdgpu_buffer_rsrc_t xs = slice_rsrc(Hs + (int64_t)s * sstrideR);
+  const uint32_t loff = (uint32_t)(own ? c : 0) * (uint32_t)sizeof(RX);
   const int beg = rowptr[row], end = rowptr[row + 1];
   float acc[E];
 #pragma unroll
@@ -164,12 +183,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sliced(
         const int j = __shfl(mj, e & 63, 64);
         v0[u] = __shfl(w0, e & 63, 64);
         v1[u] = __shfl(w1, e & 63, 64);
-        if (e < cnt && own) {
-          r[u] = X[(int64_t)j * LPG];
-        } else {
-          r[u] = Vec4<TX>::zero();
-          v0[u] = v1[u] = 0.f;
-        }
+        r[u] = load_piece<RX>(xs, (uint32_t)j * (uint32_t)(LPG * sizeof(RX)) + loff);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -360,11 +374,16 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
 #pragma unroll
     for (int t = 0; t < E; ++t) {
       second[t] = (c0 + t) / dh != h0;
-      hj0[t] = second[t] ? 0.f : v[t];
-      hj1[t] = second[t] ? v[t] : 0.f;
+      const float vt = c0 + t < D ? v[t] : 0.f;
+      hj0[t] = second[t] ? 0.f : vt;
+      hj1[t] = second[t] ? vt : 0.f;
     }
   }
-  const RX* X = Gs + (int64_t)s * sstrideR + c;
+  // unconditional loads as k_gat_fwd_sliced: edges past the chunk take row 0 with weight 0 (their
+  // products are never stored), lanes past D re-read the row's first piece (finite; hj = 0 there,
+  // acc never stored); columns in [D, 4 ceil(D/4)) hold zeros (k_gat_bwd_prep_s writes them)
+  const __amdgpu_buffer_rsrc_t xs = slice_rsrc(Gs + (int64_t)s * sstrideR);
+  const uint32_t loff = (uint32_t)(own ? c : 0) * (uint32_t)sizeof(RX);
   float* pds = pd + (int64_t)s * pstride;
   const int beg = rowptrT[row], end = rowptrT[row + 1];
   float acc[E];
@@ -388,22 +407,16 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_sl(
         const int j = __shfl(mj, e & 63, 64);
         v0[u] = __shfl(w0, e & 63, 64);
         v1[u] = __shfl(w1, e & 63, 64);
-        if (e < cnt && own) {
-          r[u] = X[(int64_t)j * LPG];
-        } else {
-          r[u] = Vec4<T>::zero();
-          v0[u] = v1[u] = 0.f;
-        }
+        r[u] = load_piece<RX>(xs, (uint32_t)j * (uint32_t)(LPG * sizeof(RX)) + loff);
       }
       float q[2 * U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const float4 fv = Vec4<T>::get(r[u]);
-        float f[E] = {fv.x, fv.y, fv.z, fv.w};
+        const float f[E] = {fv.x, fv.y, fv.z, fv.w};
         float qa = 0.f, qb = 0.f;
 #pragma unroll
         for (int t = 0; t < E; ++t) {
-          f[t] = c0 + t < D ? f[t] : 0.f;  // G's padding columns are never written
           acc[t] = fmaf(second[t] ? v1[u] : v0[u], f[t], acc[t]);
           qa = fmaf(f[t], hj0[t], qa);
           qb = fmaf(f[t], hj1[t], qb);
@@ -601,6 +614,7 @@ int gat_fwd_sliced(const int32_t* rowptr, const int32_t* col, int32_t n_rows, co
   if (!rowptr || !col || !s1 || !s2 || !m_out || !den_out || !wgt) return GNNEA_EINVAL;
   if (s_end > s_begin && (!Hs || !Y)) return GNNEA_EINVAL;
   if (!alv<T>(Hs) || !alv<T>(Y)) return GNNEA_EALIGN;
+  if ((uint64_t)sstride * sizeof(T) > 0xffffffffull) return GNNEA_EINVAL;  // (load_piece)
   const int nbs = div_up(n_rows, 4);
   if (stats) switch (heads) {
 #define GNNEA_RS(HH)                                                                             \
@@ -761,6 +775,7 @@ int gat_bwd_src_sliced(const int32_t* rowptrT, const int32_t* colT, const int64_
   if (!rowptrT || !colT || !s2 || !rec || !wT || !pd || (emask && !permT)) return GNNEA_EINVAL;
   if (s_end > s_begin && (!Hm || !Gs || !dH)) return GNNEA_EINVAL;
   if (!alv<T>(Hm) || !alv<T>(Gs) || !alv<T>(dH)) return GNNEA_EALIGN;
+  if ((uint64_t)sstride * sizeof(T) > 0xffffffffull) return GNNEA_EINVAL;  // (load_piece)
   if (weights) {
 #define GNNEA_W1(HH, LP)                                                                        \
   hipLaunchKernelGGL((k_gat_bwd_w<HH, LP>), dim3(div_up(n_rows, 256 / LP)), dim3(256), 0, st,   \
