@@ -694,18 +694,6 @@ __device__ __forceinline__ void load_heads(const float* p, float (&v)[H]) {
   }
 }
 
-// the lane's head weight of edge k (lane k holds every head's weight of its edge)
-template <int H>
-__device__ __forceinline__ float head_w(const float (&wl)[H], int k, int hme) {
-  float we = 0.f;
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    const float v = readlane_f(wl[h], k);
-    we = hme == h ? v : we;
-  }
-  return we;
-}
-
 template <int H, int EPL, typename T, bool EM, int F>
 __global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ rowptr,
                                                     const int32_t* __restrict__ col, int n_rows,
@@ -720,10 +708,14 @@ __global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ 
   using L = HeadLanes<H, EPL>;
   using WN = RowWin<T, EPL>;
   constexpr int W = WN::W;
+  // per wave: the chunk's edge weights [edge][head]; each lane reads its head's weight of an edge
+  // as one broadcast ds_read (H readlanes + selects per edge before)
+  __shared__ float sh_w[4][64 * H];
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   const int row = blk * 4 + wave_id();
   if (row >= n_rows) return;
   const int lane = lane_id();
+  float* shw = sh_w[wave_id()];
   const int beg = rowptr[row], end = rowptr[row + 1];
   const L hl(lane, dh);
   const int hme = hl.h < H ? hl.h : 0;
@@ -801,19 +793,22 @@ __global__ __launch_bounds__(256) void k_gat_fwd_hg(const int32_t* __restrict__ 
         const float w = __expf(sc[h] - mx[h]);  // 0 past the chunk (sc = -inf there)
         den[h] += w;  // the row sum uses the un-dropped weights (att_layers.py:45-51)
         wl[h] = EM ? w * em[h] : w;
+        shw[lane * H + h] = wl[h];  // lanes past the chunk: 0
       }
       // no early exits between a group's issue and its use: every edge of a group is consumed,
       // so the compiler's wait counts stay exact across the loop's back edge.  Edges past the
       // chunk have weight 0 (sc = -inf there) and re-read a live edge's finite row: their fma
       // adds +-0, no select needed
       auto consume = [&](const uint32_t (&g)[F][W], int k) {
+        float we[F];
+#pragma unroll
+        for (int e = 0; e < F; ++e) we[e] = shw[min(k + e, 63) * H + hme];
 #pragma unroll
         for (int e = 0; e < F; ++e) {
-          const float we = head_w<H>(wl, min(k + e, 63), hme);
           float x[EPL];
           WN::unpack(g[e], wsh, x);
 #pragma unroll
-          for (int t = 0; t < EPL; ++t) acc[t] = fmaf(we, x[t], acc[t]);
+          for (int t = 0; t < EPL; ++t) acc[t] = fmaf(we[e], x[t], acc[t]);
         }
       };
       // (sched_barrier: keep each group's loads ahead of the previous group's arithmetic)
