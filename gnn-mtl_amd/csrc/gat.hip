@@ -40,6 +40,79 @@ struct HeadLanes {
   }
 };
 
+struct __attribute__((aligned(4))) U3 { uint32_t x, y, z; };
+
+template <int W>
+__device__ __forceinline__ void load_dw(const char* p, uint32_t* d) {
+  if constexpr (W >= 4) {
+    const uint4 v = *(const uint4*)p;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    if constexpr (W > 4) load_dw<W - 4>(p + 16, d + 4);
+  } else if constexpr (W == 3) {
+    const U3 v = *(const U3*)p;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z;
+  } else if constexpr (W == 2) {
+    const uint2 v = *(const uint2*)p;
+    d[0] = v.x; d[1] = v.y;
+  } else {
+    d[0] = *(const uint32_t*)p;
+  }
+}
+
+// the same window through a buffer resource on the (wave-uniform) row base: the row address is
+// scalar arithmetic, the lane's window offset the 32-bit voffset -- no 64-bit vector address
+// per edge (a global pointer formed as base + row * ld + lane offset is re-associated by the
+// compiler into a per-lane 64-bit multiply-add)
+template <int W>
+__device__ __forceinline__ void load_dw_row(const char* row, uint32_t off, uint32_t* d) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)row, (short)0, 0x7fffffff, 0x00020000);
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  typedef unsigned int u3 __attribute__((ext_vector_type(3)));
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  int q = 0;
+#pragma unroll
+  for (; q + 4 <= W; q += 4) {
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 4 * q, 0, 0);
+    d[q] = v.x; d[q + 1] = v.y; d[q + 2] = v.z; d[q + 3] = v.w;
+  }
+  if constexpr (W % 4 == 3) {
+    const u3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, off + 4 * q, 0, 0);
+    d[q] = v.x; d[q + 1] = v.y; d[q + 2] = v.z;
+  } else if constexpr (W % 4 == 2) {
+    const u2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 4 * q, 0, 0);
+    d[q] = v.x; d[q + 1] = v.y;
+  } else if constexpr (W % 4 == 1) {
+    d[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * q, 0, 0);
+  }
+}
+
+template <typename T, int EPL> struct RowWin;
+template <int EPL> struct RowWin<float, EPL> {
+  static constexpr int W = EPL;
+  static __host__ __device__ int64_t byte_off(int c) { return 4 * (int64_t)c; }
+  static __device__ __forceinline__ void unpack(const uint32_t (&d)[W], uint32_t, float (&f)[EPL]) {
+#pragma unroll
+    for (int t = 0; t < EPL; ++t) f[t] = __builtin_bit_cast(float, d[t]);
+  }
+};
+template <int EPL> struct RowWin<bf16_t, EPL> {
+  static constexpr int W = (EPL + 2) / 2;  // EPL halfwords + a possible leading one
+  static __host__ __device__ int64_t byte_off(int c) { return (2 * (int64_t)c) & ~(int64_t)3; }
+  // shb: the window's byte shift (2 when the first element is odd): one v_alignbyte per element
+  // pair brings halfwords (2p, 2p + 1) into a dword, then a shift / a mask widens each to f32
+  static __device__ __forceinline__ void unpack(const uint32_t (&d)[W], uint32_t shb,
+                                                float (&f)[EPL]) {
+#pragma unroll
+    for (int p = 0; 2 * p < EPL; ++p) {
+      const uint32_t v = __builtin_amdgcn_alignbyte(d[p + 1 < W ? p + 1 : W - 1], d[p], shb);
+      f[2 * p] = __builtin_bit_cast(float, v << 16);
+      if (2 * p + 1 < EPL) f[2 * p + 1] = __builtin_bit_cast(float, v & 0xffff0000u);
+    }
+  }
+};
+
+
 // s1[i,h] = sum_d H[i, h*dh+d] * a[h, d];  s2[i,h] = sum_d H[i, h*dh+d] * a[h, dh+d]
 // A wave walks rows (grid-stride) with the lane's slice of a preloaded.
 // A lane's EPL consecutive elements are read as whole 16-B windows: bf16 (EPL <= 6) ONE load of
@@ -65,8 +138,7 @@ __global__ __launch_bounds__(256) void k_gat_scores(const T* __restrict__ Hm, in
     a1[t] = hl.ok[t] ? a[hh * 2 * dh + d] : 0.f;
     a2[t] = hl.ok[t] ? a[hh * 2 * dh + dh + d] : 0.f;
   }
-  const int wbyte = (2 * hl.c[0]) & ~3;  // WIN: the lane's window, halfword shift
-  const bool wsh = (hl.c[0] & 1) != 0;
+  const bool wsh = (hl.c[0] & 1) != 0;  // WIN (bf16): the window's halfword shift
   auto score = [&](const float (&xv)[EPL], int row) {
     float p[2] = {0.f, 0.f};
 #pragma unroll
@@ -92,21 +164,10 @@ __global__ __launch_bounds__(256) void k_gat_scores(const T* __restrict__ Hm, in
 #pragma unroll
     for (int k = 0; k < RR; ++k) {
       const T* x = Hm + (int64_t)min(base + k * nw, nmain - 1) * ldh;
-      if constexpr (WIN && sizeof(T) == 4) {
-        const uint4 v0 = *(const uint4*)(x + hl.c[0]);
-        const uint4 v1 = EPL > 4 ? *(const uint4*)(x + hl.c[0] + 4) : v0;
-        const uint32_t dw[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-        for (int t = 0; t < EPL; ++t) xv[k][t] = __uint_as_float(dw[t]);
-      } else if constexpr (WIN) {
-        const uint4 v = *(const uint4*)((const char*)x + wbyte);
-        const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int t = 0; t < EPL; ++t) {  // halfword t + wsh of the window, widened to f32
-          const uint32_t lo = (t & 1) ? (dw[t >> 1] & 0xffff0000u) : (dw[t >> 1] << 16);
-          const uint32_t hi = (t & 1) ? (dw[(t + 1) >> 1] << 16) : (dw[t >> 1] & 0xffff0000u);
-          xv[k][t] = __uint_as_float(wsh ? hi : lo);
-        }
+      if constexpr (WIN) {  // the exact window (RowWin: EPL dwords / the 4-B aligned halfwords)
+        uint32_t dw[RowWin<T, EPL>::W];
+        load_dw<RowWin<T, EPL>::W>((const char*)x + RowWin<T, EPL>::byte_off(hl.c[0]), dw);
+        RowWin<T, EPL>::unpack(dw, wsh ? 2u : 0u, xv[k]);
       } else {
 #pragma unroll
         for (int t = 0; t < EPL; ++t) xv[k][t] = to_f32<T>(x[hl.c[t]]);
@@ -611,78 +672,6 @@ static bool ok_ld(int64_t ld, int D) { return ld % 4 == 0 && ld >= ((D + 3) / 4)
 // every per-element sum runs in edge order: the forward's outputs equal k_gat_fwd's.           //
 // Host-checked: every lane's window ends inside the row's ld (no read past the table).        //
 // ---------------------------------------------------------------------------------------- //
-struct __attribute__((aligned(4))) U3 { uint32_t x, y, z; };
-
-template <int W>
-__device__ __forceinline__ void load_dw(const char* p, uint32_t* d) {
-  if constexpr (W >= 4) {
-    const uint4 v = *(const uint4*)p;
-    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-    if constexpr (W > 4) load_dw<W - 4>(p + 16, d + 4);
-  } else if constexpr (W == 3) {
-    const U3 v = *(const U3*)p;
-    d[0] = v.x; d[1] = v.y; d[2] = v.z;
-  } else if constexpr (W == 2) {
-    const uint2 v = *(const uint2*)p;
-    d[0] = v.x; d[1] = v.y;
-  } else {
-    d[0] = *(const uint32_t*)p;
-  }
-}
-
-// the same window through a buffer resource on the (wave-uniform) row base: the row address is
-// scalar arithmetic, the lane's window offset the 32-bit voffset -- no 64-bit vector address
-// per edge (a global pointer formed as base + row * ld + lane offset is re-associated by the
-// compiler into a per-lane 64-bit multiply-add)
-template <int W>
-__device__ __forceinline__ void load_dw_row(const char* row, uint32_t off, uint32_t* d) {
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)row, (short)0, 0x7fffffff, 0x00020000);
-  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
-  typedef unsigned int u3 __attribute__((ext_vector_type(3)));
-  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-  int q = 0;
-#pragma unroll
-  for (; q + 4 <= W; q += 4) {
-    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 4 * q, 0, 0);
-    d[q] = v.x; d[q + 1] = v.y; d[q + 2] = v.z; d[q + 3] = v.w;
-  }
-  if constexpr (W % 4 == 3) {
-    const u3 v = __builtin_amdgcn_raw_buffer_load_b96(rs, off + 4 * q, 0, 0);
-    d[q] = v.x; d[q + 1] = v.y; d[q + 2] = v.z;
-  } else if constexpr (W % 4 == 2) {
-    const u2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 4 * q, 0, 0);
-    d[q] = v.x; d[q + 1] = v.y;
-  } else if constexpr (W % 4 == 1) {
-    d[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4 * q, 0, 0);
-  }
-}
-
-template <typename T, int EPL> struct RowWin;
-template <int EPL> struct RowWin<float, EPL> {
-  static constexpr int W = EPL;
-  static __host__ __device__ int64_t byte_off(int c) { return 4 * (int64_t)c; }
-  static __device__ __forceinline__ void unpack(const uint32_t (&d)[W], uint32_t, float (&f)[EPL]) {
-#pragma unroll
-    for (int t = 0; t < EPL; ++t) f[t] = __builtin_bit_cast(float, d[t]);
-  }
-};
-template <int EPL> struct RowWin<bf16_t, EPL> {
-  static constexpr int W = (EPL + 2) / 2;  // EPL halfwords + a possible leading one
-  static __host__ __device__ int64_t byte_off(int c) { return (2 * (int64_t)c) & ~(int64_t)3; }
-  // shb: the window's byte shift (2 when the first element is odd): one v_alignbyte per element
-  // pair brings halfwords (2p, 2p + 1) into a dword, then a shift / a mask widens each to f32
-  static __device__ __forceinline__ void unpack(const uint32_t (&d)[W], uint32_t shb,
-                                                float (&f)[EPL]) {
-#pragma unroll
-    for (int p = 0; 2 * p < EPL; ++p) {
-      const uint32_t v = __builtin_amdgcn_alignbyte(d[p + 1 < W ? p + 1 : W - 1], d[p], shb);
-      f[2 * p] = __builtin_bit_cast(float, v << 16);
-      if (2 * p + 1 < EPL) f[2 * p + 1] = __builtin_bit_cast(float, v & 0xffff0000u);
-    }
-  }
-};
-
 template <int H>
 __device__ __forceinline__ void load_heads(const float* p, float (&v)[H]) {
   if constexpr (H == 4) {  // 16-B aligned rows (host-checked)
