@@ -1488,7 +1488,10 @@ def gat_sliced_wanted(n_rows, heads, d_head, dtype):
                             (dtype == torch.bfloat16 and GAT_SLICED_BF16))
             and gat_two_heads_per_slice(heads, d_head)
             and D % 4 == 0 and heads <= 8 and 128 <= D <= 1024
-            and n_rows * D * es > INFINITY_CACHE_BYTES)
+            and n_rows * D * es > INFINITY_CACHE_BYTES
+            # (the sliced passes address a slice with 32-bit offsets: one slice < 4 GB; larger
+            # tables take the row-major head-grouped passes)
+            and n_rows * 64 * es < (1 << 32) - (1 << 24))
 
 
 def _gat_sliced_applies(H, heads, d_head, Y):
