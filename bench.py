@@ -11,6 +11,8 @@ aggregation over the owned rows (default --partition rows).  The exchange-free p
 (tiles / features: every rank aggregates a column slice from the whole KG, which a layer can
 only do after an all-gather of its input) are reported as a labelled side number.
 
+Side measurement `dbp15k_step_graph` (N = 1): the DBP15K-scale GCN-EA and GAT-EA iteration with
+Adam (configs[1] / [2]), eager against one captured HIP graph replay (tools/graph_step.py).
 Side measurements (`train_step`, `train_step_gat`, `train_step_gcn`, `train_step_gat_cfg5_bf16`):
 the row-sharded EA training steps through the drop-in Encoder/Decoder modules with the RCCL halo
 exchange (tools/dist_step.py) -- HGCN-EA on the cfg-4 graph (configs[3]), GAT-EA and GCN-EA fp32
@@ -881,6 +883,16 @@ def main():
                 line["fgw_outer"] = fgw_rate(device)
             except Exception as e:  # report, never hide
                 line["fgw_outer"] = {"error": repr(e)}
+        if world == 1 and not args.no_train:
+            # configs[1] / [2]'s DBP15K-scale EA iteration (with Adam) eager and as one captured
+            # HIP graph (tools/graph_step.py; replay checked bit-identical to the eager step)
+            try:
+                from tools.graph_step import run as graph_run
+                line["dbp15k_step_graph"] = {m: graph_run(m, synth.CONFIGS["dbp15k"]["n"],
+                                                          synth.CONFIGS["dbp15k"]["t"], 30,
+                                                          device) for m in ("GCN", "GAT")}
+            except Exception as e:  # report, never hide
+                line["dbp15k_step_graph"] = {"error": repr(e)}
         if world == 1 and not args.headline_only:
             try:
                 line["hbm_anchors"] = anchors(device)
