@@ -127,8 +127,10 @@ def test_cfg5_gat_ea_step_vs_fp64(device, cfg5, monkeypatch, relu_band, record_p
     pinned without that chaos: the fp64 restatement, with the bf16 path's storage roundings
     inserted (fp64_ref.bf16_store after every projection / layer output, value and gradient),
     is differentiated with the cotangent of the reference loss formula at OUR outputs, relu
-    masks inside the bf16 band following our activations; every parameter gradient within
-    2e-2 norm-relative."""
+    masks inside the bf16 band following our activations, and every layer's input taking our
+    stored activation's value (gradients still flowing through the restatement); every parameter
+    gradient within 1e-2 norm-relative (measured <= 3.7e-3; 1.6e-2 before the inputs followed
+    ours)."""
     from models.models_ea import EAModel
     from test_dropin_cpu import make_args
     d = cfg5
@@ -170,10 +172,19 @@ def test_cfg5_gat_ea_step_vs_fp64(device, cfg5, monkeypatch, relu_band, record_p
               L.linear.bias.detach().double().requires_grad_(True)) for L in m.decoder.cls]
     h = d["xb"].double()
     st = fp64_ref.bf16_store
-    for (W, A), tst in zip(gat_p, acts[:2]):
+
+    def ours_value(h, a):
+        # every layer's input takes OUR stored activation's value, the gradient still flows
+        # through the restatement (straight-through): a weight gradient X^T dY then sums our X,
+        # not an fp64 X whose bf16 roundings differ from ours by an ulp here and there
+        return h + (a.double() - h).detach()
+    for li, ((W, A), tst) in enumerate(zip(gat_p, acts[:2])):
+        if li:
+            h = ours_value(h, acts[li - 1])
         h = fp64_ref.gat_layer(h, W, A, d["er"], d["ec"], 0.2, True, tested=tst.double(),
                                tau=TAU_BF16, store=st)
     for i, (W, b) in enumerate(lin_p):
+        h = ours_value(h, acts[1 + i])
         h = st(h @ W.t() + b)  # the bf16 GEMM's output (and its bf16 gradient)
         if i < 2:
             with torch.no_grad():
@@ -205,4 +216,4 @@ def test_cfg5_gat_ea_step_vs_fp64(device, cfg5, monkeypatch, relu_band, record_p
     assert e_out < 2 * TOL_BF16
     for name, e in zip(["enc0.W", "enc0.a", "enc1.W", "enc1.a", "dec0.W", "dec0.b", "dec1.W",
                         "dec1.b", "dec2.W", "dec2.b"], errs):
-        assert e < 2 * TOL_BF16, (name, e)
+        assert e < TOL_BF16, (name, e)
