@@ -320,7 +320,18 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d
         p = wave_sum_f64(p);
         if (lane == 0) red[par][w][r] = p;
       }
-      __syncthreads();  // the only barrier of the group: red[par] is double-buffered
+      // the only barrier of the group (red[par] is double-buffered).  STAB / GEN / RELAX: the
+      // wave partials in LDS are complete (lgkmcnt(0)), then a raw s_barrier -- __syncthreads()
+      // is a workgroup fence too, whose vmcnt(0) drained the next group's K loads (the prefetch)
+      // at every group: sinkhorn_iteration at B = 15000 2,164 -> 2,385 iters/s.  KNOPP keeps
+      // the fence (its row loads of 1/a sit behind the prefetch: 2,770 -> 2,628 without it)
+      if constexpr (KNOPP) {
+        __syncthreads();
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
       // every wave reduces the 8 wave partials of each row itself (same order -> same y)
 #pragma unroll
       for (int r = 0; r < G; ++r) {
@@ -365,13 +376,17 @@ __global__ __launch_bounds__(64 * kSweepWaves) void k_sk_sweep(SkArgs a, SkDev d
   if (g0 < r1) load(kA, g0);
   if (gate && d.st[ST_DONE]) return;
   if (PH1 && KNOPP && knopp_stop<KNOPP>(a, d, it)) return;
+  // STAB / GEN / RELAX: the next group's loads go out unconditionally (past the last group: the
+  // last rows again, never used), so every path into a group's processing has the same loads
+  // outstanding and the compiler's waits there cover only the group being processed (KNOPP: as
+  // before, loads only for groups that exist)
   while (g0 < r1) {
     const int g1 = g0 + G;
-    if (g1 < r1) load(kB, g1);
+    if (!KNOPP || g1 < r1) load(kB, g1);
     process(kA, g0, 0);
     if (g1 >= r1) break;
     const int g2 = g1 + G;
-    if (g2 < r1) load(kA, g2);
+    if (!KNOPP || g2 < r1) load(kA, g2);
     process(kB, g1, 1);
     g0 = g2;
   }
