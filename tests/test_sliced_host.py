@@ -49,3 +49,14 @@ def test_sliced_table_shape_and_map():
             assert flat[(c // 64) * sstride + r * 64 + c % 64] == x[r, c]
     # the test-side inverse used by the GPU tests
     assert torch.equal(xs.permute(1, 0, 2).reshape(7, -1)[:, :132], x)
+
+
+def test_gat_sliced_wanted_slice_size_limit(monkeypatch):
+    # the sliced GAT passes address a 64-column slice with 32-bit offsets (gat_sliced.hip
+    # load_piece): below 4 GB per slice they apply above the Infinity Cache, beyond it the
+    # head-grouped row-major passes take the table
+    monkeypatch.setattr(ops, "GAT_SLICED", True)
+    assert ops.gat_sliced_wanted(2_000_000, 4, 75, torch.float32)        # cfg-4: 512 MB slices
+    assert not ops.gat_sliced_wanted(30_000, 4, 75, torch.float32)       # cache resident
+    assert ops.gat_sliced_wanted(16_000_000, 4, 75, torch.float32)       # 4.1e9 B < 2^32 - 2^24
+    assert not ops.gat_sliced_wanted(17_000_000, 4, 75, torch.float32)   # 4.35e9 B
