@@ -1213,9 +1213,11 @@ static int gat_bwd_src_t(const int32_t* rowptrT, const int32_t* colT, const int6
                      (const float4*)rec, G, ldg, a, dH, lddh, dzT, ds2)
 #define CALL(HH, EE)                                                                          \
   case HH * 32 + EE:                                                                          \
-    if (edge_mask) GNNEA_HG_L(HH, EE, true, 4);                                               \
-    else GNNEA_HG_L(HH, EE, false, 4);                                                        \
+    if (edge_mask) GNNEA_HG_L(HH, EE, true, 1);                                               \
+    else GNNEA_HG_L(HH, EE, false, 1);                                                        \
     break;
+    // (one edge per gather group, F = 1: the source pass's per-group reduce-scatter then runs
+    // per edge; cfg-5 6.32 -> 6.11 ms per launch against F = 4, F = 2 6.18)
     GNNEA_GAT_HG_DISPATCH(CALL);
 #undef CALL
 #undef GNNEA_HG_L
