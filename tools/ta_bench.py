@@ -37,21 +37,27 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=21)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--wide", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     res = {}
-    for name, K, dt in (("fp32 2M x 300 x 300", 2_000_000, torch.float32),
-                        ("bf16 4M x 300 x 300", 4_000_000, torch.bfloat16)):
+    shapes = [("fp32 2M x 300 x 300", 2_000_000, 300, torch.float32),
+              ("bf16 4M x 300 x 300", 4_000_000, 300, torch.bfloat16)]
+    if args.wide:  # the 300- against the 600-wide dW on the same kernel, per-flop rate
+        shapes += [("fp32 2M x 300 x 600", 2_000_000, 600, torch.float32),
+                   ("fp32 4M x 300 x 300", 4_000_000, 300, torch.float32)]
+    for name, K, N, dt in shapes:
         a = torch.randn(K, 300, device=dev, generator=g).to(dt)
-        b = torch.randn(K, 300, device=dev, generator=g).to(dt)
+        b = torch.randn(K, N, device=dev, generator=g).to(dt)
         ref = a.double().t() @ b.double()
         y = ops.gemm(a, b, trans_a=True, out_dtype=torch.float32)
         err = float((y.double() - ref).norm() / ref.norm())
         ms = timeit(lambda: ops.gemm(a, b, trans_a=True, out_dtype=torch.float32), args.reps)
-        byts = 2 * K * 300 * a.element_size()
+        byts = K * (300 + N) * a.element_size()
         res[name] = {"ms": round(ms, 4), "rel_err_vs_fp64": err,
-                     "TBps_compulsory": round(byts / (ms * 1e-3) / 1e12, 3)}
+                     "TBps_compulsory": round(byts / (ms * 1e-3) / 1e12, 3),
+                     "TFLOPs_product": round(2.0 * K * 300 * N / (ms * 1e-3) / 1e12, 1)}
         del a, b, ref, y
         torch.cuda.empty_cache()
     print(json.dumps(res), flush=True)
